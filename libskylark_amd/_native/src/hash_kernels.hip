@@ -1,0 +1,256 @@
+// CountSketch-family kernels (CWT / MMT / WZT): hash_transform_t.
+//
+// Reference: sketch/hash_transform_Elemental.hpp:83-130 (dense),
+// :201-260 (CSC -> dense), sketch/hash_transform_local_sparse.hpp:88-223.
+// Columnwise:  SA[h[r], :] += v[r] * A[r, :]     (A: N x m)
+// Rowwise:     SA[:, h[c]] += v[c] * A[:, c]     (A: m x N)
+//
+// gfx950 design.  The sketch data (h, v) is static, so the host builds ONCE
+// per sketch a bucket permutation (rows sorted by h; `perm`, `bptr`) and the
+// kernels become gathers + segmented reductions instead of scattered float
+// atomics into HBM (which run at ~1.3 TB/s at best and ~0.08 TB/s with one
+// lane per row, MI355X_MICROARCH.md "Global float atomics"):
+//   * dense columnwise: one workgroup per (bucket, 256*VEC column slice);
+//     every thread owns VEC output columns in registers and streams the
+//     bucket's rows (coalesced 16-B loads) -> deterministic, no atomics;
+//   * dense rowwise: the input row is staged in LDS by coalesced loads, each
+//     thread produces whole output buckets by gathering from LDS;
+//   * CSR columnwise: one workgroup per (bucket, column chunk), the chunk
+//     accumulated in LDS with ds_add_f32, then one coalesced store.
+#include "sl_common.hpp"
+
+template <typename T, typename OT, int VEC>
+__global__ void __launch_bounds__(256)
+k_hash_dense_col(const T* __restrict__ A, int64_t lda, int64_t m, const int64_t* __restrict__ perm,
+                 const int64_t* __restrict__ bptr, const double* __restrict__ val,
+                 OT* __restrict__ out, int64_t ldo, int64_t row_offset, int accumulate) {
+  const int64_t b = blockIdx.y;
+  const int64_t c0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  const int64_t p0 = bptr[b], p1 = bptr[b + 1];
+  if (c0 < m) {
+    const bool full = c0 + VEC <= m;
+    for (int64_t p = p0; p < p1; ++p) {
+      const int64_t r = perm[p];  // wave-uniform
+      const float w = (float)val[r];
+      const T* row = A + (r - row_offset) * lda + c0;
+      if (full) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += w * Cvt<T>::to_f(row[j]);
+      } else {
+        for (int j = 0; j < VEC && c0 + j < m; ++j) acc[j] += w * Cvt<T>::to_f(row[j]);
+      }
+    }
+    OT* o = out + b * ldo + c0;
+    for (int j = 0; j < VEC && c0 + j < m; ++j)
+      o[j] = accumulate ? Cvt<OT>::from_f(Cvt<OT>::to_f(o[j]) + acc[j]) : Cvt<OT>::from_f(acc[j]);
+  }
+}
+
+// double-precision variant: exact fp64 accumulation
+template <int VEC>
+__global__ void __launch_bounds__(256)
+k_hash_dense_col_f64(const double* __restrict__ A, int64_t lda, int64_t m,
+                     const int64_t* __restrict__ perm, const int64_t* __restrict__ bptr,
+                     const double* __restrict__ val, double* __restrict__ out, int64_t ldo,
+                     int64_t row_offset, int accumulate) {
+  const int64_t b = blockIdx.y;
+  const int64_t c0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
+  double acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
+  const int64_t p0 = bptr[b], p1 = bptr[b + 1];
+  if (c0 < m) {
+    for (int64_t p = p0; p < p1; ++p) {
+      const int64_t r = perm[p];
+      const double w = val[r];
+      const double* row = A + (r - row_offset) * lda + c0;
+      for (int j = 0; j < VEC && c0 + j < m; ++j) acc[j] += w * row[j];
+    }
+    double* o = out + b * ldo + c0;
+    for (int j = 0; j < VEC && c0 + j < m; ++j) o[j] = accumulate ? o[j] + acc[j] : acc[j];
+  }
+}
+
+SL_API int sl_hash_dense_colwise(const void* A, int dtype, int64_t lda, int64_t m,
+                                 const int64_t* perm, const int64_t* bptr, const double* val,
+                                 int64_t S, void* out, int out_dtype, int64_t ldo,
+                                 int64_t row_offset, int accumulate, void* stream) {
+  if (S <= 0 || m <= 0) return SL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SL_F64) {
+    if (out_dtype != SL_F64) { sl_set_last_error("f64 input needs f64 output"); return SL_ERR_UNSUPPORTED; }
+    constexpr int VEC = 2;
+    dim3 grid((unsigned)((m + 256 * VEC - 1) / (256 * VEC)), (unsigned)S);
+    k_hash_dense_col_f64<VEC><<<grid, 256, 0, s>>>((const double*)A, lda, m, perm, bptr, val,
+                                                    (double*)out, ldo, row_offset, accumulate);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  }
+  constexpr int VEC = 4;
+  dim3 grid((unsigned)((m + 256 * VEC - 1) / (256 * VEC)), (unsigned)S);
+#define SL_HC(TI, TO) k_hash_dense_col<TI, TO, VEC><<<grid, 256, 0, s>>>((const TI*)A, lda, m, perm, bptr, val, (TO*)out, ldo, row_offset, accumulate)
+  if (dtype == SL_F32 && out_dtype == SL_F32) SL_HC(float, float);
+  else if (dtype == SL_BF16 && out_dtype == SL_F32) SL_HC(bf16_t, float);
+  else if (dtype == SL_BF16 && out_dtype == SL_BF16) SL_HC(bf16_t, bf16_t);
+  else if (dtype == SL_F32 && out_dtype == SL_BF16) SL_HC(float, bf16_t);
+  else { sl_set_last_error("hash colwise: dtype combination"); return SL_ERR_UNSUPPORTED; }
+#undef SL_HC
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ---------------------------------------------------------------- rowwise
+// One workgroup per input row: row -> LDS (coalesced), then thread t produces
+// buckets t, t+256, ... by gathering the bucket members from LDS.
+template <typename T, typename AT, typename OT>
+__global__ void __launch_bounds__(256)
+k_hash_dense_row(const T* __restrict__ A, int64_t lda, int64_t ncols, const int64_t* __restrict__ perm,
+                 const int64_t* __restrict__ bptr, const double* __restrict__ val, int64_t S,
+                 OT* __restrict__ out, int64_t ldo, int64_t col_offset, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  AT* row = (AT*)smem;
+  const int64_t r = blockIdx.x;
+  const T* a = A + r * lda;
+  for (int64_t c = threadIdx.x; c < ncols; c += 256) row[c] = (AT)Cvt<T>::to_d(a[c]);
+  __syncthreads();
+  for (int64_t b = threadIdx.x; b < S; b += 256) {
+    AT acc = 0;
+    for (int64_t p = bptr[b]; p < bptr[b + 1]; ++p) {
+      const int64_t c = perm[p];
+      acc += (AT)val[c] * row[c - col_offset];
+    }
+    OT* o = out + r * ldo + b;
+    if (accumulate) *o = Cvt<OT>::from_d(Cvt<OT>::to_d(*o) + (double)acc);
+    else *o = Cvt<OT>::from_d((double)acc);
+  }
+}
+
+SL_API int sl_hash_dense_rowwise(const void* A, int dtype, int64_t lda, int64_t rows,
+                                 int64_t ncols, const int64_t* perm, const int64_t* bptr,
+                                 const double* val, int64_t S, void* out, int out_dtype,
+                                 int64_t ldo, int64_t col_offset, int accumulate, void* stream) {
+  if (rows <= 0 || S <= 0) return SL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  size_t esz = dtype == SL_F64 ? 8 : 4;
+  size_t lds = (size_t)ncols * esz;
+  if (lds > 160 * 1024) { sl_set_last_error("hash rowwise: row too long for LDS"); return SL_ERR_UNSUPPORTED; }
+  if (dtype == SL_F64 && out_dtype == SL_F64)
+    k_hash_dense_row<double, double, double><<<(unsigned)rows, 256, lds, s>>>((const double*)A, lda, ncols, perm, bptr, val, S, (double*)out, ldo, col_offset, accumulate);
+  else if (dtype == SL_F32 && out_dtype == SL_F32)
+    k_hash_dense_row<float, float, float><<<(unsigned)rows, 256, lds, s>>>((const float*)A, lda, ncols, perm, bptr, val, S, (float*)out, ldo, col_offset, accumulate);
+  else if (dtype == SL_BF16 && out_dtype == SL_F32)
+    k_hash_dense_row<bf16_t, float, float><<<(unsigned)rows, 256, lds, s>>>((const bf16_t*)A, lda, ncols, perm, bptr, val, S, (float*)out, ldo, col_offset, accumulate);
+  else if (dtype == SL_BF16 && out_dtype == SL_BF16)
+    k_hash_dense_row<bf16_t, float, bf16_t><<<(unsigned)rows, 256, lds, s>>>((const bf16_t*)A, lda, ncols, perm, bptr, val, S, (bf16_t*)out, ldo, col_offset, accumulate);
+  else { sl_set_last_error("hash rowwise: dtype combination"); return SL_ERR_UNSUPPORTED; }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ------------------------------------------------------------ CSR columnwise
+// A: CSR (rowptr, col, vals) holding global rows [row_offset, row_offset+nrows).
+// Workgroup = (bucket b, column chunk [c0, c0+CW)); lanes are split in groups
+// of G lanes per CSR row (G ~ average row length, a power of two).
+template <typename IT, typename VT, int G>
+__global__ void __launch_bounds__(512)
+k_hash_csr_col(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
+               const VT* __restrict__ vals, const int64_t* __restrict__ perm,
+               const int64_t* __restrict__ bptr, const double* __restrict__ hval,
+               float* __restrict__ out, int64_t ldo, int64_t m, int64_t CW,
+               int64_t row_offset) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* acc = (float*)smem;
+  const int64_t b = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * CW;
+  const int64_t cw = (c0 + CW <= m) ? CW : (m - c0);
+  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) acc[c] = 0.f;
+  __syncthreads();
+  const int groups = blockDim.x / G;
+  const int gid = threadIdx.x / G, gl = threadIdx.x % G;
+  const bool chunked = cw != m;
+  for (int64_t p = bptr[b] + gid; p < bptr[b + 1]; p += groups) {
+    const int64_t r = perm[p];
+    const float w = (float)hval[r];
+    const int64_t lr = r - row_offset;
+    for (int64_t q = rowptr[lr] + gl; q < rowptr[lr + 1]; q += G) {
+      const int64_t c = (int64_t)col[q] - c0;
+      if (!chunked || (c >= 0 && c < cw)) atomicAdd(&acc[c], w * (float)vals[q]);
+    }
+  }
+  __syncthreads();
+  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) out[b * ldo + c0 + c] += acc[c];
+}
+
+SL_API int sl_hash_csr_colwise(const int64_t* rowptr, const void* col, int idx32, const void* vals,
+                               int vdtype, const int64_t* perm, const int64_t* bptr,
+                               const double* hval, int64_t S, int64_t m, float* out, int64_t ldo,
+                               int64_t row_offset, int group, void* stream) {
+  if (S <= 0 || m <= 0) return SL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int64_t CW = m < 32768 ? m : 32768;  // 128 KB of LDS at most
+  dim3 grid((unsigned)((m + CW - 1) / CW), (unsigned)S);
+  size_t lds = (size_t)CW * 4;
+#define SL_CSR(IT, VT, G) k_hash_csr_col<IT, VT, G><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, hval, out, ldo, m, CW, row_offset)
+#define SL_CSR_G(IT, VT)                                   \
+  switch (group) {                                         \
+    case 1: SL_CSR(IT, VT, 1); break;                      \
+    case 4: SL_CSR(IT, VT, 4); break;                      \
+    case 16: SL_CSR(IT, VT, 16); break;                    \
+    default: SL_CSR(IT, VT, 64); break;                    \
+  }
+  if (vdtype == SL_F32) {
+    if (idx32) { SL_CSR_G(int32_t, float) } else { SL_CSR_G(int64_t, float) }
+  } else if (vdtype == SL_F64) {
+    if (idx32) { SL_CSR_G(int32_t, double) } else { SL_CSR_G(int64_t, double) }
+  } else { sl_set_last_error("hash csr: value dtype"); return SL_ERR_UNSUPPORTED; }
+#undef SL_CSR_G
+#undef SL_CSR
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ------------------------------------------------------------- CSR rowwise
+// out[r, h[c]] += v[c] * A[r, c]: G lanes per CSR row, float atomics into the
+// row of `out` (rows are disjoint between groups, so contention is per row).
+template <typename IT, typename VT, int G>
+__global__ void __launch_bounds__(256)
+k_hash_csr_row(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
+               const VT* __restrict__ vals, int64_t rows, const int64_t* __restrict__ h,
+               const double* __restrict__ hval, float* __restrict__ out, int64_t ldo,
+               int64_t col_offset) {
+  const int64_t gid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int gl = threadIdx.x % G;
+  if (gid >= rows) return;
+  for (int64_t q = rowptr[gid] + gl; q < rowptr[gid + 1]; q += G) {
+    const int64_t c = (int64_t)col[q] + col_offset;
+    atomicAdd(&out[gid * ldo + h[c]], (float)hval[c] * (float)vals[q]);
+  }
+}
+
+SL_API int sl_hash_csr_rowwise(const int64_t* rowptr, const void* col, int idx32, const void* vals,
+                               int vdtype, int64_t rows, const int64_t* h, const double* hval,
+                               float* out, int64_t ldo, int64_t col_offset, int group,
+                               void* stream) {
+  if (rows <= 0) return SL_OK;
+  hipStream_t s = (hipStream_t)stream;
+#define SL_CR(IT, VT, G) k_hash_csr_row<IT, VT, G><<<(unsigned)((rows * G + 255) / 256), 256, 0, s>>>(rowptr, (const IT*)col, (const VT*)vals, rows, h, hval, out, ldo, col_offset)
+#define SL_CR_G(IT, VT)                                   \
+  switch (group) {                                        \
+    case 1: SL_CR(IT, VT, 1); break;                      \
+    case 4: SL_CR(IT, VT, 4); break;                      \
+    case 16: SL_CR(IT, VT, 16); break;                    \
+    default: SL_CR(IT, VT, 64); break;                    \
+  }
+  if (vdtype == SL_F32) {
+    if (idx32) { SL_CR_G(int32_t, float) } else { SL_CR_G(int64_t, float) }
+  } else if (vdtype == SL_F64) {
+    if (idx32) { SL_CR_G(int32_t, double) } else { SL_CR_G(int64_t, double) }
+  } else { sl_set_last_error("hash csr rowwise: value dtype"); return SL_ERR_UNSUPPORTED; }
+#undef SL_CR_G
+#undef SL_CR
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

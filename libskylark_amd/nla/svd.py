@@ -1,0 +1,244 @@
+"""Randomized SVD (Halko-Martinsson-Tropp) and power iteration.
+
+Reference: ``nla/svd.hpp`` — ``approximate_svd_params_t`` (ratio 2, additive 0,
+iterations 0, skip_qr false, ``:22-48``), ``PowerIteration`` (``:71-149``),
+``ApproximateSVD`` (``:222-318``: ``k = max(r, min(n, ratio*r + add))``, JLT
+rowwise sketch, power iteration, ``El::SVD`` of the n x k iterate,
+``U = Q B_1``), ``ApproximateSymmetricSVD`` (``:321-392``).
+
+MI355X formulation (tall case m >= n, A row-distributed one shard per GPU):
+a subspace iteration pass needs ``Q = orth(A Z)`` and ``A^T Q``.  With
+``Y = A Z``, ``R = chol(Y^T Y)``: ``Q = Y R^{-1}`` and ``A^T Q = (A^T Y)
+R^{-1}`` — so ONE streaming read of A (``ops.tallskinny.fused_pass``)
+yields both, where the textbook loop reads A twice.  The reference itself
+uses this identity in its ``skip_qr, num_iterations == 0`` branch
+(``nla/svd.hpp:263-269``).  Per pass the only collective is one all-reduce of
+``[A^T Y | Y^T Y]`` ((n + k) x k floats).  Robustness: the n x k iterate is
+re-orthonormalised exactly (Householder, fp64) between passes; the final
+basis is CholeskyQR2-refined from the stored ``Y`` (m x k, a fraction of A's
+bytes); if a Gram factorisation fails the code falls back to TSQR.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ..base import linalg as L
+from ..base.context import Context
+from ..base.exceptions import InvalidParametersError
+from ..parallel.comm import Comm
+from ..parallel.distmatrix import DistMatrix
+
+
+@dataclass
+class ApproximateSVDParams:
+    oversampling_ratio: int = 2
+    oversampling_additive: int = 0
+    num_iterations: int = 0
+    skip_qr: bool = False
+    sketch: str = "JLT"          # "JLT" (reference) | "FJLT" | "CWT"
+    am_i_printing: bool = False
+    log_level: int = 0
+    prefix: str = ""
+    debug_level: int = 0
+
+    @classmethod
+    def from_dict(cls, d: dict):
+        keys = cls.__dataclass_fields__.keys()
+        return cls(**{k: v for k, v in d.items() if k in keys})
+
+    def to_dict(self):
+        return dict(self.__dict__)
+
+
+approximate_svd_params_t = ApproximateSVDParams
+
+
+def _sketch_operator(kind: str, n: int, k: int, ctx: Context, device, dtype) -> torch.Tensor:
+    """Z0 = Omega^T (n x k) for the rowwise sketch A Omega^T."""
+    from .. import sketch as S
+    cls = {"JLT": S.JLT, "FJLT": S.FJLT, "CWT": S.CWT, "CT": S.CT}.get(kind.upper())
+    if cls is None:
+        raise InvalidParametersError(f"unsupported sketch {kind} for approximate_svd")
+    sk = cls(n, k, context=ctx)
+    if kind.upper() == "FJLT":
+        return sk.realize(dtype=torch.float64, device=device).t().to(dtype).contiguous()
+    if kind.upper() == "CWT":
+        return sk.realize(dtype=torch.float64).t().to(device=device, dtype=dtype).contiguous()
+    return sk.realize(dtype=torch.float64, device=device).t().to(dtype).contiguous()
+
+
+def _as_rowdist(A):
+    """(local row shard tensor, comm, m_global, reassemble-info)."""
+    if isinstance(A, DistMatrix):
+        if A.layout not in ("VC_STAR", "VR_STAR"):
+            A = A.redistribute("VC_STAR")
+        return A.local, A.comm, A.shape[0], A
+    return A, Comm(None) if False else _LocalComm(), A.shape[0], None
+
+
+class _LocalComm(Comm):
+    def __init__(self):
+        self.group, self.rank, self.size, self.backend, self._active = None, 0, 1, None, False
+
+
+def _small_chol_inv(G: torch.Tensor):
+    """R^{-1} for R = chol(G)^T (upper), fp64; None when G is not numerically SPD."""
+    L_, info = torch.linalg.cholesky_ex(G)
+    if int(info) != 0:
+        return None, None
+    R = L_.t()
+    I = torch.eye(R.shape[0], dtype=R.dtype, device=R.device)
+    Rinv = torch.linalg.solve_triangular(R, I, upper=True)
+    return R, Rinv
+
+
+def approximate_svd(A, rank: int, context: Context | None = None,
+                    params: ApproximateSVDParams | None = None):
+    """Rank-``rank`` approximate SVD ``A ~ U diag(s) V^T``.
+
+    ``A``: dense ``torch.Tensor`` (any device/dtype) or a DistMatrix.  Returns
+    ``(U, s, V)``; U is row-distributed like A (a DistMatrix ``[VC,*]`` when A
+    is distributed), s and V replicated.
+    """
+    from .. import default_context
+    ctx = context if context is not None else default_context()
+    params = params or ApproximateSVDParams()
+    m, n = (A.shape if not isinstance(A, DistMatrix) else A.shape)
+    if rank > min(m, n):
+        raise InvalidParametersError(f"Incompatible matrix dimensions ({min(m, n)}) and target rank ({rank})")
+    if m < n:
+        # wide: work on A^T (tall) and swap the factors
+        At = _transpose(A)
+        U, s, V = approximate_svd(At, rank, ctx, params)
+        if isinstance(A, DistMatrix):
+            return _dist_like_cols(V, A), s, (U.to_global() if isinstance(U, DistMatrix) else U)
+        return V, s, U
+    k = max(rank, min(n, params.oversampling_ratio * rank + params.oversampling_additive))
+    A_loc, comm, _, Ad = _as_rowdist(A)
+    dev = A_loc.device
+    work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
+    from ..ops import tallskinny as T
+
+    Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float64)
+    q = max(0, int(params.num_iterations))
+    for it in range(q + 1):
+        last = it == q
+        W, G, Y = T.fused_pass(A_loc, Z.to(work), keep_y=last)
+        WG = torch.cat([W.double(), G.double()], 0)
+        comm.all_reduce(WG)
+        W, G = WG[:n], WG[n:]
+        R, Rinv = _small_chol_inv(G)
+        if R is None:
+            # Gram not SPD in working precision: explicit TSQR of Y (rare)
+            Yx = Y if Y is not None else T.matmul(A_loc, Z, out_dtype=work)
+            Qx, R = L.tsqr(Yx, comm)
+            Rinv = torch.linalg.solve_triangular(R.double(), torch.eye(k, dtype=torch.float64, device=dev), upper=True)
+            W = L.gemm_tn(A_loc.to(work) if A_loc.dtype != work else A_loc, Qx.to(work), comm).double()
+            Y, Rfix = Qx, True
+        else:
+            Rfix = False
+            W = W @ Rinv  # = A^T Q
+        if not last:
+            if params.skip_qr:
+                Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-300)
+            else:
+                Z, _ = torch.linalg.qr(W, mode="reduced")
+            continue
+        # --- final: Q = Y R^{-1}; refine with one more CholeskyQR on Q (CholQR2)
+        if Rfix:
+            Q = Y.to(work)
+            Vt = W  # A^T Q
+        else:
+            Q = Y.to(work) @ Rinv.to(work)
+            G2 = L.gram(Q, comm)
+            R2, R2inv = _small_chol_inv(G2)
+            if R2 is None:
+                Q, R2 = L.tsqr(Q, comm)
+                R2inv = torch.linalg.solve_triangular(R2.double(), torch.eye(k, dtype=torch.float64, device=dev), upper=True)
+            else:
+                Q = Q @ R2inv.to(work)
+            Vt = W @ R2inv  # A^T Q_refined
+    # SVD of the n x k matrix A^T Q = V S Ub^T  =>  B = Q^T A = Ub S V^T
+    Vv, s, Ubt = torch.linalg.svd(Vt, full_matrices=False)
+    Ub = Ubt.t()
+    U_loc = (Q @ Ub[:, :rank].to(work))
+    s = s[:rank]
+    V = Vv[:, :rank]
+    if Ad is not None:
+        U = DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm)
+        return U, s, V
+    return U_loc, s, V.to(work) if A_loc.dtype != torch.float64 else V
+
+
+def _transpose(A):
+    if isinstance(A, DistMatrix):
+        g = A.redistribute("STAR_VC")
+        return DistMatrix(g.local.t().contiguous(), (A.shape[1], A.shape[0]), "VC_STAR", A.comm)
+    return A.t()
+
+
+def _dist_like_cols(V, A):
+    return V
+
+
+# ------------------------------------------------------------ power iteration
+def power_iteration(A, V: torch.Tensor, iternum: int, ortho: bool = True, comm: Comm | None = None):
+    """``V <- (A^T A)^iternum V`` with optional re-orthonormalisation
+    (reference ``PowerIteration(ADJOINT, NORMAL, NORMAL, ...)``).  Returns (U = A V, V)."""
+    A_loc, c, _, _ = _as_rowdist(A)
+    c = comm or c
+    work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
+    from ..ops import tallskinny as T
+    U = T.matmul(A_loc, V, out_dtype=work)
+    for _ in range(iternum):
+        if ortho:
+            U = L.orthonormalize(U, c)
+        V = L.gemm_tn(A_loc.to(work), U, c)
+        if ortho:
+            V, _ = torch.linalg.qr(V, mode="reduced")
+        U = T.matmul(A_loc, V, out_dtype=work)
+    return U, V
+
+
+def approximate_symmetric_svd(A: torch.Tensor, rank: int, context: Context | None = None,
+                              params: ApproximateSVDParams | None = None, uplo: str = "L"):
+    """Approximate eigendecomposition of a symmetric matrix (reference ``:321-392``):
+    Gaussian Omega, power iterations, Rayleigh-Ritz with a symmetric eigensolver
+    (descending).  Returns ``(V, s)``.  ``A`` may be dense or sparse (CSR)."""
+    from .. import default_context
+    from ..base import distributions as D
+    from ..ops import rng
+    ctx = context if context is not None else default_context()
+    params = params or ApproximateSVDParams()
+    n = A.shape[0]
+    k = max(rank, min(n, params.oversampling_ratio * rank + params.oversampling_additive))
+    dev = A.device
+    work = torch.float64 if (A.dtype == torch.float64 or (A.is_sparse_csr and A.values().dtype == torch.float64)) else torch.float32
+    arr = ctx.allocate_random_samples_array(n * k, D.Normal())
+    V = torch.empty(n, k, dtype=work, device=dev)
+    rng.fill_random(V, D.Normal(), arr.seed, arr.base, ir=1, ic=n)
+
+    def mv(X):
+        if A.layout != torch.strided:
+            return torch.sparse.mm(A.to(work) if A.values().dtype != work else A, X)
+        return A.to(work) @ X
+
+    U = mv(V)
+    for _ in range(params.num_iterations):
+        if not params.skip_qr:
+            U, _ = torch.linalg.qr(U, mode="reduced")
+        U = mv(U)
+    Q, _ = torch.linalg.qr(U, mode="reduced")
+    B = Q.t() @ mv(Q)
+    B = 0.5 * (B + B.t())
+    w, E = torch.linalg.eigh(B.double())
+    order = torch.argsort(w.abs(), descending=True)[:rank]
+    return (Q.double() @ E[:, order]).to(work), w[order].to(work)
+
+
+ApproximateSVD = approximate_svd
+ApproximateSymmetricSVD = approximate_symmetric_svd
+PowerIteration = power_iteration

@@ -1,0 +1,105 @@
+"""Fast unitary transforms: DCT-II/III, DHT, WHT along a matrix dimension.
+
+Reference: ``utility/fft/fftw_futs.h:3-126`` (FFTW ``REDFT10``/``REDFT01``
+with scale ``1/sqrt(2N)``; ``DHT`` with ``1/sqrt(N)``), SpiralWHT ``WHT_t``.
+
+We implement the *orthonormal* DCT-II (``norm='ortho'``, the semantics of the
+reference's pure-Python fallback ``scipy.fftpack.dct(..., norm='ortho')``,
+``python-skylark/skylark/sketch.py:FJLT._ppyapply``); the C++ reference's
+REDFT10 scaling leaves its k = 0 row sqrt(2) too large, i.e. not unitary.
+
+The transforms run through rocFFT (``torch.fft``, hipFFT) with the
+Makhoul even/odd reordering and the post-twiddle; on GPU the twiddle +
+scaling is done in the same pass that extracts the real part.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def _move(x, dim):
+    return x if dim == 0 else x.transpose(0, 1)
+
+
+def _cplx(dt):
+    return torch.complex128 if dt == torch.float64 else torch.complex64
+
+
+def _work_dtype(dt):
+    return torch.float64 if dt == torch.float64 else torch.float32
+
+
+def dct2(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
+    """Orthonormal DCT-II along ``dim`` of a 2-D tensor (returns a new tensor)."""
+    xt = _move(x, dim).to(_work_dtype(x.dtype))
+    N = xt.shape[0]
+    v = torch.cat([xt[0::2], xt[1::2].flip(0)], dim=0)
+    V = torch.fft.fft(v, dim=0)
+    k = torch.arange(N, device=x.device, dtype=xt.dtype)
+    w = torch.exp(torch.complex(torch.zeros_like(k), -math.pi * k / (2 * N)))
+    X = (V * w[:, None]).real
+    scale = torch.full((N,), math.sqrt(2.0 / N), dtype=xt.dtype, device=x.device)
+    scale[0] = math.sqrt(1.0 / N)
+    X = X * scale[:, None]
+    return _move(X, dim).contiguous()
+
+
+def dct3(X: torch.Tensor, dim: int = 0) -> torch.Tensor:
+    """Orthonormal DCT-III along ``dim`` (inverse of :func:`dct2`)."""
+    Xt = _move(X, dim).to(_work_dtype(X.dtype))
+    N = Xt.shape[0]
+    scale = torch.full((N,), math.sqrt(2.0 / N), dtype=Xt.dtype, device=X.device)
+    scale[0] = math.sqrt(1.0 / N)
+    Y = Xt / scale[:, None]  # undo ortho scaling -> un-normalised DCT-II coefficients Z_k
+    k = torch.arange(N, device=X.device, dtype=Xt.dtype)
+    # Makhoul inverse: V_k = (Z_k - i Z_{N-k}) e^{i pi k / 2N}, Z_N = 0; v = IDFT(V)
+    Yr = torch.zeros_like(Y)
+    Yr[1:] = Y.flip(0)[:-1]
+    w = torch.exp(torch.complex(torch.zeros_like(k), math.pi * k / (2 * N)))
+    V = torch.complex(Y, -Yr) * w[:, None]
+    v = torch.fft.ifft(V, dim=0).real
+    x = torch.empty_like(v)
+    h = (N + 1) // 2
+    x[0::2] = v[:h]
+    x[1::2] = v[h:].flip(0)
+    return _move(x, dim).contiguous()
+
+
+def dht(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
+    """Unitary discrete Hartley transform (self-inverse), scale 1/sqrt(N)."""
+    xt = _move(x, dim).to(_work_dtype(x.dtype))
+    F = torch.fft.fft(xt, dim=0)
+    H = (F.real - F.imag) / math.sqrt(xt.shape[0])
+    return _move(H, dim).contiguous()
+
+
+def wht(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
+    """Orthonormal Walsh-Hadamard transform (N must be a power of two)."""
+    xt = _move(x, dim).to(_work_dtype(x.dtype)).contiguous()
+    N = xt.shape[0]
+    if N & (N - 1):
+        raise ValueError("WHT length must be a power of two")
+    m = xt.shape[1]
+    y = xt.clone()
+    h = 1
+    while h < N:
+        y = y.view(N // (2 * h), 2, h, m)
+        a, b = y[:, 0], y[:, 1]
+        y = torch.stack([a + b, a - b], dim=1).reshape(N, m)
+        h *= 2
+    y = y / math.sqrt(N)
+    return _move(y, dim).contiguous()
+
+
+FUTS = {"DCT": (dct2, dct3), "DHT": (dht, dht), "WHT": (wht, wht)}
+
+
+def dct2_rows_matrix(N: int, rows: torch.Tensor, dtype=torch.float64, device=None) -> torch.Tensor:
+    """Explicit rows ``rows`` of the orthonormal DCT-II matrix (len(rows) x N)."""
+    k = rows.to(device=device, dtype=dtype)[:, None]
+    n = torch.arange(N, device=device, dtype=dtype)[None, :]
+    F = torch.cos(math.pi * k * (2 * n + 1) / (2 * N)) * math.sqrt(2.0 / N)
+    F[rows.to(device) == 0] *= math.sqrt(0.5)
+    return F

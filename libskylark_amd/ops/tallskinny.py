@@ -1,0 +1,128 @@
+"""Streaming tall-skinny products over a row shard of A (the randSVD / LSQR hot path).
+
+For ``A`` (m x n, m >> n) and a skinny ``Z`` (n x k) the randomized SVD needs,
+per power iteration, ``Y = A Z`` and ``A^T Y`` (and ``Y^T Y`` to
+orthonormalise).  Those are bandwidth-bound (k ~ 40: ~40 flop per A element)
+so the only thing that matters is how many times A streams through HBM.
+
+``fused_pass`` reads A ONCE and returns ``W = A^T (A Z)``, ``G = (A Z)^T (A Z)``
+(and optionally ``Y = A Z``): the row block's ``y = A_blk Z`` never leaves
+the chip.  This halves the HBM traffic of subspace iteration.  On gfx950 it
+is the hand-written MFMA kernel ``sl_tsk_fused_pass`` (bf16 A, bf16-hi/lo
+split operands, f32 accumulation); elsewhere a chunked torch composition
+with the same semantics.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+_lib.register("sl_tsk_fused_pass", [vp, i64, i64, i64, vp, i32, vp, vp, vp, i64, vp, vp])
+_lib.register("sl_tsk_fused_workspace", [i64, i64, i32], C.c_int64)
+_lib.register("sl_tsk_matmul", [vp, i64, i64, i64, vp, i32, vp, i64, i32, vp])
+
+# rows per chunk in the torch fallback (bounds the y temporary)
+CHUNK_ROWS = 1 << 18
+USE_NATIVE = True
+
+
+def _native_ok(A: torch.Tensor, k: int) -> bool:
+    if not (USE_NATIVE and A.is_cuda and A.dtype == torch.bfloat16 and k <= 64):
+        return False
+    if A.stride(1) != 1 or A.shape[1] % 8 or A.stride(0) % 8:
+        return False
+    if A.shape[1] > 2048:
+        return False
+    lib = _lib.load()
+    return lib is not None and hasattr(lib, "sl_tsk_fused_pass")
+
+
+def _split_bf16(X: torch.Tensor):
+    hi = X.to(torch.bfloat16)
+    lo = (X - hi.to(X.dtype)).to(torch.bfloat16)
+    return hi, lo
+
+
+class FusedWorkspace:
+    """Per-device scratch for the native fused pass (partial slabs)."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, device, nbytes):
+        key = str(device)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+
+_WS = FusedWorkspace()
+
+
+def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False):
+    """Return ``(W, G, Y)`` with ``Y = A Z``, ``W = A^T Y`` (n x k), ``G = Y^T Y`` (k x k).
+
+    W and G are float32 (A bf16/fp32) or float64 (A fp64); Y is float32/64 or
+    None.  Partial over this shard only — the caller all-reduces W and G.
+    """
+    m, n = A.shape
+    k = Z.shape[1]
+    if _native_ok(A, k):
+        return _fused_native(A, Z, keep_y)
+    wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
+    Zc = Z.to(A.dtype) if A.dtype in (torch.bfloat16, torch.float16) else Z.to(wdt)
+    W = torch.zeros(n, k, dtype=wdt, device=A.device)
+    G = torch.zeros(k, k, dtype=torch.float64, device=A.device)
+    Ys = [] if keep_y else None
+    for r0 in range(0, m, CHUNK_ROWS):
+        Ab = A[r0:r0 + CHUNK_ROWS]
+        y = torch.matmul(Ab, Zc).to(wdt)
+        if A.dtype in (torch.bfloat16, torch.float16):
+            yh, yl = _split_bf16(y)
+            W += (torch.matmul(Ab.t(), yh).to(wdt) + torch.matmul(Ab.t(), yl).to(wdt))
+        else:
+            W += torch.matmul(Ab.t().to(wdt), y)
+        G += (y.t() @ y).double()
+        if keep_y:
+            Ys.append(y)
+    Y = torch.cat(Ys, 0) if keep_y and Ys else (torch.zeros(0, k, dtype=wdt, device=A.device) if keep_y else None)
+    return W, G, Y
+
+
+def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool):
+    m, n = A.shape
+    k = Z.shape[1]
+    dev = A.device
+    Zb = Z.to(torch.bfloat16).contiguous()
+    W = torch.empty(n, k, dtype=torch.float32, device=dev)
+    G = torch.empty(k, k, dtype=torch.float32, device=dev)
+    Y = torch.empty(m, k, dtype=torch.float32, device=dev) if keep_y else None
+    nbytes = int(_lib.require().sl_tsk_fused_workspace(m, n, k))
+    ws = _WS.get(dev, max(nbytes, 16))
+    _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zb), k, _lib.ptr(W), _lib.ptr(G),
+              _lib.ptr(Y) if Y is not None else None, 0 if Y is None else Y.stride(0), _lib.ptr(ws),
+              vp(_lib.stream_of(A)))
+    return W, G.double(), Y
+
+
+def matmul(A: torch.Tensor, Z: torch.Tensor, out_dtype=torch.float32) -> torch.Tensor:
+    """``Y = A Z`` streaming (A bf16 m x n, Z n x k small) with f32 output."""
+    if _native_ok(A, Z.shape[1]) and hasattr(_lib.require(), "sl_tsk_matmul"):
+        m, n = A.shape
+        k = Z.shape[1]
+        hi, lo = _split_bf16(Z.float())
+        Zs = torch.cat([hi, lo], 1).contiguous()
+        Y = torch.empty(m, k, dtype=torch.float32, device=A.device)
+        _lib.call("sl_tsk_matmul", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zs), k, _lib.ptr(Y), Y.stride(0), 1,
+                  vp(_lib.stream_of(A)))
+        return Y.to(out_dtype)
+    if A.dtype in (torch.bfloat16, torch.float16):
+        hi, lo = _split_bf16(Z.float())
+        return (torch.matmul(A, hi).float() + torch.matmul(A, lo).float()).to(out_dtype)
+    return torch.matmul(A, Z.to(A.dtype)).to(out_dtype)

@@ -1,0 +1,20 @@
+"""Sketching transforms (reference ``sketch/``, ``python-skylark/skylark/sketch.py``)."""
+from .base import (COLUMNWISE, ROWWISE, SketchTransform, deserialize_sketch, from_json, from_ptree,
+                   parse_dim, sketch_class, supported_sketch_transforms)
+from .dense import CT, JLT
+from .fjlt import FJLT, RFUT, UST, URST, FastJLT
+from .frft import PPT, FastGaussianRFT, FastMaternRFT, Fastfood
+from .hash import CWT, MMT, WZT, CountSketch
+from .rft import (ExpSemigroupQRLT, ExpSemigroupRLT, GaussianQRFT, GaussianRFT, LaplacianQRFT,
+                  LaplacianRFT, MaternRFT)
+
+columnwise, rowwise = COLUMNWISE, ROWWISE
+TensorSketch = PPT
+
+__all__ = [
+    "COLUMNWISE", "ROWWISE", "SketchTransform", "deserialize_sketch", "from_json", "from_ptree",
+    "JLT", "CT", "FJLT", "FastJLT", "RFUT", "UST", "URST", "CWT", "CountSketch", "MMT", "WZT",
+    "PPT", "TensorSketch", "GaussianRFT", "LaplacianRFT", "MaternRFT", "GaussianQRFT",
+    "LaplacianQRFT", "FastGaussianRFT", "Fastfood", "FastMaternRFT", "ExpSemigroupRLT",
+    "ExpSemigroupQRLT", "supported_sketch_transforms", "sketch_class", "parse_dim",
+]

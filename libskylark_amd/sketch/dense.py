@@ -1,0 +1,90 @@
+"""Dense sketches: JLT (Gaussian) and CT (Cauchy).
+
+Reference: ``sketch/JLT_data.hpp:17-78`` (scale ``sqrt(1/S)``, ``N*S`` normals
+allocated lazily), ``sketch/CT_data.hpp:20-91`` (scale ``C/S``, ``N*S``
+Cauchy samples), engine ``sketch/dense_transform_*``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..base import distributions as D
+from ..ops import dense_sketch as _ds
+from .base import COLUMNWISE, SketchTransform, register
+
+
+class DenseSketch(SketchTransform):
+    """S x N matrix with iid entries ``scale * dist`` realised from the stream."""
+
+    dist = D.Normal()
+
+    def _scale(self) -> float:
+        raise NotImplementedError
+
+    def _build(self, ctx):
+        self.scale = self._scale()
+        self.entries = ctx.allocate_random_samples_array(self._N * self._S, self.dist)
+
+    # global realisation helpers (used by tests, nla and the distributed layer)
+    def realize(self, dtype=torch.float64, device=None, rows=None, cols=None) -> torch.Tensor:
+        r = rows or (0, self._S)
+        c = cols or (0, self._N)
+        return _ds.realize_panel(self.dist, self.entries.seed, self.entries.base, self._S, r, c,
+                                 scale=self.scale, dtype=dtype, device=device,
+                                 precise=dtype == torch.float64)
+
+    def _apply_dense(self, A, dim, in_offset: int = 0, out_rows=None):
+        return _ds.apply_dense(A, dim, dist=self.dist, seed=self.entries.seed, base=self.entries.base,
+                               S=self._S, N=self._N, scale=self.scale, in_offset=in_offset,
+                               out_rows=out_rows)
+
+    def _apply_sparse(self, A, dim, sparse_out):
+        return _ds.apply_sparse(A, dim, dist=self.dist, seed=self.entries.seed, base=self.entries.base,
+                                S=self._S, N=self._N, scale=self.scale)
+
+    # distributed hook: partial product of a shard along the sketched dim
+    def apply_local_shard(self, A_local, dim, in_offset, out_rows=None):
+        if A_local.layout == torch.sparse_csr:
+            if in_offset != 0 or out_rows is not None:
+                A_local = A_local.to_dense()
+            else:
+                return self._apply_sparse(A_local, dim, False)
+        return self._apply_dense(A_local, dim, in_offset=in_offset, out_rows=out_rows)
+
+
+@register
+class JLT(DenseSketch):
+    """Johnson-Lindenstrauss transform: Gaussian S with scale sqrt(1/S)."""
+
+    sketch_type = "JLT"
+    dist = D.Normal()
+
+    def _scale(self):
+        return math.sqrt(1.0 / self._S)
+
+
+@register
+class CT(DenseSketch):
+    """Cauchy transform (l1 embedding): Cauchy S with scale C/S."""
+
+    sketch_type = "CT"
+    dist = D.Cauchy()
+
+    def __init__(self, n, s, C=1.0, context=None):
+        self._C = float(C)
+        super().__init__(n, s, context)
+
+    def _scale(self):
+        return self._C / self._S
+
+    def _extra_params(self):
+        return {"C": self._C}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        return {"C": float(d["C"])}
+
+
+__all__ = ["JLT", "CT", "DenseSketch", "COLUMNWISE"]

@@ -1,0 +1,165 @@
+"""FJLT (fast JL / SRHT-style), RFUT and UST.
+
+Reference: ``sketch/FJLT_data.hpp:19-94`` (RFUT data: ``N`` Rademacher for D,
+then ``S`` uniform ints in [0, N) with replacement), apply
+``sketch/FJLT_Elemental.hpp:144-171``: ``SA = sqrt(N/S) * P * F * D * A``;
+``sketch/RFUT_data.hpp:20-51``; ``sketch/UST_data.hpp:75-100`` (with
+replacement: ``S`` ints; without: inside-out Fisher-Yates with one
+``uniform_int(0, i)`` draw per i, N draws), UST applies without scaling.
+
+MI355X design: when the number of samples is small (``S <= 256``) the
+sampled rows of ``F*D`` are realised explicitly (``S x N``) and applied as an
+MFMA GEMM — one streaming pass over A; otherwise the rocFFT DCT pipeline
+(D-scale, FFT, twiddle, gather) is used.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..base import distributions as D
+from ..ops import fut as _fut
+from ..ops import rng as _rng
+from .base import COLUMNWISE, SketchTransform, register
+
+DIRECT_MAX_S = 256
+
+
+class RFUT:
+    """Random fast unitary transform ``F * D`` (not a registered sketch type;
+    used by FJLT and Blendenpik).  ``fut`` in {"DCT", "DHT", "WHT"}."""
+
+    def __init__(self, N: int, context, fut: str = "DCT"):
+        self.N = N
+        self.fut = fut
+        self.D = context.generate_random_samples_array(N, D.Rademacher())
+
+    def apply(self, A: torch.Tensor, dim: int = COLUMNWISE) -> torch.Tensor:
+        d = self.D.to(device=A.device, dtype=torch.float64 if A.dtype == torch.float64 else torch.float32)
+        X = A * (d[:, None] if dim == COLUMNWISE else d[None, :])
+        return _fut.FUTS[self.fut][0](X, dim)
+
+    def apply_inverse(self, A: torch.Tensor, dim: int = COLUMNWISE) -> torch.Tensor:
+        d = self.D.to(device=A.device, dtype=torch.float64 if A.dtype == torch.float64 else torch.float32)
+        X = _fut.FUTS[self.fut][1](A, dim)
+        return X * (d[:, None] if dim == COLUMNWISE else d[None, :])
+
+
+@register
+class FJLT(SketchTransform):
+    sketch_type = "FJLT"
+
+    def _build(self, ctx):
+        self.rfut = RFUT(self._N, ctx, "DCT")
+        self.samples = ctx.generate_random_samples_array(self._S, D.UniformInt(0, self._N - 1),
+                                                         dtype=torch.int64)
+        self.scale = math.sqrt(self._N / self._S)
+        self._W = {}
+
+    def realize(self, dtype=torch.float64, device=None) -> torch.Tensor:
+        """Explicit ``S x N`` operator ``sqrt(N/S) P F D``."""
+        F = _fut.dct2_rows_matrix(self._N, self.samples, dtype=torch.float64, device=device)
+        W = self.scale * F * self.rfut.D.to(device=device, dtype=torch.float64)[None, :]
+        return W.to(dtype)
+
+    def _operator(self, device, dtype):
+        key = (str(device), dtype)
+        if key not in self._W:
+            self._W[key] = self.realize(dtype=dtype, device=device)
+        return self._W[key]
+
+    def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
+        cdt = A.dtype if A.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.float16) else torch.float32
+        if self._S <= DIRECT_MAX_S:
+            W = self._operator(A.device, cdt)
+            k = A.shape[dim]
+            Wl = W[:, in_offset:in_offset + k]
+            if dim == COLUMNWISE:
+                out = torch.matmul(Wl, A.to(cdt))
+            else:
+                out = torch.matmul(A.to(cdt), Wl.t())
+            return out.float() if cdt in (torch.bfloat16, torch.float16) else out
+        if in_offset != 0:
+            raise ValueError("FFT-based FJLT needs the full sketched dimension on one device")
+        FA = self.rfut.apply(A, dim)
+        idx = self.samples.to(A.device)
+        out = FA.index_select(dim, idx) * self.scale
+        return out
+
+    def apply_local_shard(self, A_local, dim, in_offset, out_rows=None):
+        if A_local.layout == torch.sparse_csr:
+            A_local = A_local.to_dense()
+        if in_offset == 0 and A_local.shape[dim] == self._N:
+            return self._apply_dense(A_local, dim)
+        return self._apply_dense(A_local, dim, in_offset=in_offset)
+
+
+def _fisher_yates_prefix(ctx, N: int, S: int):
+    seed, base = ctx.seed, ctx.counter
+    ctx.counter += N
+    import numpy as np
+    work = np.empty(N, dtype=np.int64)
+    # draws: slot base+i gives uniform_int(0, i)
+    blocks = torch.empty(2 * N, dtype=torch.int64)
+    from ..ops import _lib
+    import ctypes as C
+    _lib.call("sl_uniform_prefix_host", _lib.ptr(blocks), C.c_uint64(seed), C.c_uint64(base), N)
+    j_all = blocks[:N].numpy()
+    for i in range(N):
+        j = int(j_all[i])
+        work[i] = work[j]
+        work[j] = i
+    return torch.from_numpy(work[:S].copy())
+
+
+@register
+class UST(SketchTransform):
+    """Uniform sampling transform (row/column selection, unscaled)."""
+
+    sketch_type = "UST"
+
+    def __init__(self, n, s, replace=True, context=None):
+        self._replace = bool(replace)
+        super().__init__(n, s, context)
+
+    def _build(self, ctx):
+        if self._replace:
+            self.samples = ctx.generate_random_samples_array(self._S, D.UniformInt(0, self._N - 1),
+                                                             dtype=torch.int64)
+        else:
+            if self._S > self._N:
+                from ..base.exceptions import InvalidParametersError
+                raise InvalidParametersError("UST without replacement needs S <= N")
+            self.samples = _fisher_yates_prefix(ctx, self._N, self._S)
+
+    def realize(self, dtype=torch.float64):
+        P = torch.zeros(self._S, self._N, dtype=dtype)
+        P[torch.arange(self._S), self.samples] = 1
+        return P
+
+    def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
+        idx = self.samples.to(A.device)
+        return A.index_select(dim, idx)
+
+    def _apply_sparse(self, A, dim, sparse_out):
+        idx = self.samples.to(A.device)
+        coo = A.to_sparse_coo().coalesce()
+        out = coo.index_select(dim, idx).coalesce()
+        return out.to_sparse_csr() if sparse_out else out.to_dense()
+
+    supports_sparse_output = True
+
+    def _extra_params(self):
+        return {"replace": self._replace}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        r = d.get("replace", True)
+        if isinstance(r, str):
+            r = r.lower() == "true"
+        return {"replace": bool(r)}
+
+
+URST = UST
+FastJLT = FJLT

@@ -1,0 +1,178 @@
+"""Fastfood random features (FastGaussianRFT, FastMaternRFT) and the
+Pham-Pagh TensorSketch (PPT).
+
+Fastfood (reference ``sketch/FRFT_data.hpp:26-291``,
+``sketch/FRFT_Elemental.hpp:72-250``): block size NB = N, ``numblks =
+ceil(S/NB)``; draws in order: S shifts U(0, 2pi), numblks*NB Rademacher (B),
+numblks*NB normals (G), numblks*(NB-1) Fisher-Yates swap indices (P); per
+block ``x = Sm * F G Pi F (B * a)`` with unitary DCT F, features
+``sqrt(2/S) cos(x + shift)``.  ``Sm = sqrt(N)/sigma`` (Gaussian: the
+reference's ``1/(sigma sqrt N)`` times the N of its two un-normalised
+transforms) or ``sqrt(2 nu / chi2_{2 nu}) sqrt(N) / l`` (Matérn, S chi-squared
+draws).
+
+PPT (``sketch/PPT_data.hpp:24-122``, ``sketch/PPT_Elemental.hpp:140-185``):
+q CountSketches, then q hash indices and q ±1 values for the homogeneous
+term; per column ``P = prod_i FFT(sqrt(gamma) CWT_i(a) + sqrt(c) h_i e_idx_i)``,
+``SA = IFFT(P)`` (scaled by 1/S).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from ..base import distributions as D
+from ..ops import fut as _fut
+from ..ops import hash_sketch as _hs
+from .base import COLUMNWISE, SketchTransform, register
+from .rft import EPI_COS, _FeatureMap
+
+
+class _Fastfood(_FeatureMap):
+    mode = EPI_COS
+
+    def _build(self, ctx):
+        N, S = self._N, self._S
+        self.NB = N
+        self.numblks = (S + N - 1) // N
+        nb, NB = self.numblks, self.NB
+        self.outscale = math.sqrt(2.0 / S)
+        self.shifts = ctx.generate_random_samples_array(S, D.Uniform(0.0, 2 * math.pi))
+        self.B = ctx.generate_random_samples_array(nb * NB, D.Rademacher()).view(nb, NB)
+        self.G = ctx.generate_random_samples_array(nb * NB, D.Normal()).view(nb, NB)
+        raw = ctx.generate_random_samples_array(nb * (NB - 1), D.UniformInt(0, 2**62), dtype=torch.int64)
+        raw = raw.view(nb, NB - 1).numpy() if NB > 1 else np.zeros((nb, 0), dtype=np.int64)
+        perms = np.empty((nb, NB), dtype=np.int64)
+        for i in range(nb):
+            w = np.arange(NB)
+            for l in range(NB - 1):  # noqa: E741
+                j = NB - 1 - l
+                k = int(raw[i, l] % (j + 1))
+                w[j], w[k] = w[k], w[j]
+            perms[i] = w
+        self.perms = torch.from_numpy(perms)
+        self.scales = None
+        self._Sm = self._make_Sm(ctx)
+
+    def _make_Sm(self, ctx) -> torch.Tensor:
+        raise NotImplementedError
+
+    def _features_pre(self, A, dim, in_offset=0, out_rows=None):
+        if in_offset != 0 or A.shape[dim] != self._N:
+            raise ValueError("Fastfood needs the whole input dimension on one device")
+        X = A if dim == COLUMNWISE else A.t()
+        wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
+        X = X.to(wdt)
+        outs = []
+        dev = A.device
+        for i in range(self.numblks):
+            s, e = i * self.NB, min((i + 1) * self.NB, self._S)
+            W = X * self.B[i].to(dev, wdt)[:, None]
+            W = _fut.dct2(W, 0)
+            W = W.index_select(0, self.perms[i].to(dev))
+            W = W * self.G[i].to(dev, wdt)[:, None]
+            W = _fut.dct2(W, 0)
+            W = W[: e - s] * self._Sm[s:e].to(dev, wdt)[:, None]
+            outs.append(W)
+        Z = torch.cat(outs, 0)
+        if out_rows is not None:
+            Z = Z[out_rows[0]:out_rows[1]]
+        return Z if dim == COLUMNWISE else Z.t().contiguous()
+
+
+@register
+class FastGaussianRFT(_Fastfood):
+    sketch_type = "FastGaussianRFT"
+
+    def __init__(self, n, s, sigma=1.0, context=None):
+        self._sigma = float(sigma)
+        super().__init__(n, s, context)
+
+    def _make_Sm(self, ctx):
+        return torch.full((self._S,), math.sqrt(self._N) / self._sigma, dtype=torch.float64)
+
+    def _extra_params(self):
+        return {"sigma": self._sigma}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        return {"sigma": float(d["sigma"])}
+
+
+@register
+class FastMaternRFT(_Fastfood):
+    sketch_type = "FastMaternRFT"
+
+    def __init__(self, n, s, nu=1.5, l=1.0, context=None):  # noqa: E741
+        self._nu, self._l = float(nu), float(l)
+        super().__init__(n, s, context)
+
+    def _make_Sm(self, ctx):
+        chi = ctx.generate_random_samples_array(self._S, D.ChiSquared(2 * self._nu))
+        return torch.sqrt(2.0 * self._nu / chi) * math.sqrt(self._N) / self._l
+
+    def _extra_params(self):
+        return {"nu": self._nu, "l": self._l}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        return {"nu": float(d["nu"]), "l": float(d["l"])}
+
+
+Fastfood = FastGaussianRFT
+
+
+@register
+class PPT(SketchTransform):
+    """TensorSketch for the polynomial kernel (gamma <x,y> + c)^q."""
+
+    sketch_type = "PPT"
+
+    def __init__(self, n, s, q=3, c=1.0, gamma=1.0, context=None):
+        self._q, self._c, self._gamma = int(q), float(c), float(gamma)
+        super().__init__(n, s, context)
+
+    def _build(self, ctx):
+        from .hash import CWT
+        self.cwts = []
+        for _ in range(self._q):
+            cw = CWT.__new__(CWT)
+            cw._N, cw._S = self._N, self._S
+            cw._creation_context = ctx.copy()
+            cw._params = {}
+            cw._build(ctx)
+            self.cwts.append(cw)
+        self.hash_idx = ctx.generate_random_samples_array(self._q, D.UniformInt(0, self._S - 1), dtype=torch.int64)
+        self.hash_val = ctx.generate_random_samples_array(self._q, D.Rademacher())
+
+    def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
+        X = A if dim == COLUMNWISE else A.t()
+        wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
+        X = X.to(wdt).contiguous()
+        m = X.shape[1]
+        P = None
+        sg, sc = math.sqrt(self._gamma), math.sqrt(self._c)
+        for i, cw in enumerate(self.cwts):
+            W = _hs.apply_dense(cw._hd, X, 0) * sg
+            W[int(self.hash_idx[i])] += sc * float(self.hash_val[i])
+            FW = torch.fft.rfft(W, dim=0)
+            P = FW if P is None else P * FW
+        out = torch.fft.irfft(P, n=self._S, dim=0) if P is not None else torch.zeros(self._S, m, dtype=wdt, device=A.device)
+        return out if dim == COLUMNWISE else out.t().contiguous()
+
+    def _apply_sparse(self, A, dim, sparse_out):
+        return self._apply_dense(A.to_dense(), dim)
+
+    def apply_local_shard(self, A_local, dim, in_offset, out_rows=None):
+        if A_local.layout == torch.sparse_csr:
+            A_local = A_local.to_dense()
+        return self._apply_dense(A_local, dim, in_offset)
+
+    def _extra_params(self):
+        return {"q": self._q, "c": self._c, "gamma": self._gamma}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        return {"q": int(d["q"]), "c": float(d["c"]), "gamma": float(d["gamma"])}

@@ -1,0 +1,83 @@
+"""HIP kernel numerics on the MI355X vs plain PyTorch fp32/fp64 references."""
+import pytest
+import torch
+
+import libskylark_amd as sk
+from libskylark_amd.ops import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_library_is_loaded():
+    lib = _lib.require()
+    assert lib.sl_version() >= 1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+@pytest.mark.parametrize("dim", [0, 1])
+def test_cwt_dense_gpu_vs_explicit(dev, dtype, dim):
+    N, S, M = 3000, 257, 333
+    T = sk.sketch.CWT(N, S, context=sk.Context(7))
+    P = T.realize(torch.float64)
+    A = torch.randn(N, M, dtype=torch.float64) if dim == 0 else torch.randn(M, N, dtype=torch.float64)
+    Ad = A.to(dev, dtype)
+    out = T.apply(Ad, dim=dim).double().cpu()
+    Aq = Ad.double().cpu()
+    ref = P @ Aq if dim == 0 else Aq @ P.t()
+    tol = 1e-10 if dtype == torch.float64 else 1e-4 * float(ref.abs().max())
+    torch.testing.assert_close(out, ref, atol=tol, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dim", [0, 1])
+@pytest.mark.parametrize("vdt", [torch.float32, torch.float64])
+def test_cwt_csr_gpu_vs_explicit(dev, dim, vdt):
+    N, S, M = 5000, 300, 700
+    T = sk.sketch.MMT(N, S, context=sk.Context(3))
+    P = T.realize(torch.float64)
+    A = torch.randn(N, M, dtype=torch.float64)
+    A[torch.rand(N, M) > 0.05] = 0
+    if dim == 1:
+        A = A.t().contiguous()
+    As = A.to(vdt).to_sparse_csr().to(dev)
+    out = T.apply(As, dim=dim, sparse_output=False).double().cpu()
+    Aq = A.to(vdt).double()
+    ref = P @ Aq if dim == 0 else Aq @ P.t()
+    torch.testing.assert_close(out, ref, atol=1e-4 * float(ref.abs().max()), rtol=1e-4)
+
+
+@pytest.mark.parametrize("dim", [0, 1])
+def test_jlt_gpu_vs_cpu(dev, dim):
+    N, S, M = 2048, 128, 96
+    T = sk.sketch.JLT(N, S, context=sk.Context(11))
+    A = torch.randn(N, M, dtype=torch.float64) if dim == 0 else torch.randn(M, N, dtype=torch.float64)
+    cpu = T.apply(A, dim=dim)
+    gpu64 = T.apply(A.to(dev), dim=dim).cpu()
+    torch.testing.assert_close(gpu64, cpu, rtol=1e-10, atol=1e-10)
+    gpu32 = T.apply(A.float().to(dev), dim=dim).double().cpu()
+    torch.testing.assert_close(gpu32, cpu, rtol=1e-3, atol=1e-3 * float(cpu.abs().max()))
+
+
+def test_rft_epilogue_gpu(dev):
+    d, s = 64, 512
+    T = sk.sketch.GaussianRFT(d, s, sigma=2.0, context=sk.Context(1))
+    X = torch.randn(d, 200, dtype=torch.float64)
+    torch.testing.assert_close((T * X.to(dev)).cpu(), T * X, rtol=1e-9, atol=1e-9)
+    Tm = sk.sketch.MaternRFT(d, s, nu=1.5, l=2.0, context=sk.Context(1))
+    torch.testing.assert_close((Tm / X.t().contiguous().to(dev)).cpu(), Tm / X.t().contiguous(), rtol=1e-9, atol=1e-9)
+    Tr = sk.sketch.ExpSemigroupRLT(d, s, beta=0.5, context=sk.Context(2))
+    Xp = X.abs()
+    torch.testing.assert_close((Tr * Xp.to(dev)).cpu(), Tr * Xp, rtol=1e-8, atol=1e-10)
+
+
+def test_fjlt_gpu(dev):
+    for s in (40, 400):
+        T = sk.sketch.FJLT(1000, s, context=sk.Context(5))
+        A = torch.randn(1000, 64, dtype=torch.float64)
+        torch.testing.assert_close((T * A.to(dev)).cpu(), T.realize() @ A, rtol=1e-8, atol=1e-8)
+
+
+def test_fastfood_and_ppt_gpu(dev):
+    X = torch.randn(32, 50, dtype=torch.float64)
+    for T in (sk.sketch.FastGaussianRFT(32, 100, sigma=1.0, context=sk.Context(3)),
+              sk.sketch.PPT(32, 128, q=3, context=sk.Context(3))):
+        torch.testing.assert_close((T * X.to(dev)).cpu(), T * X, rtol=1e-8, atol=1e-8)

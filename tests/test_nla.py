@@ -1,0 +1,91 @@
+"""Randomized SVD / power iteration / fused pass: reconstruction and accuracy."""
+import pytest
+import torch
+
+import libskylark_amd as sk
+from libskylark_amd.ops import tallskinny
+
+
+def _lowrank(m, n, r, decay=0.5, noise=1e-3, seed=0, dtype=torch.float64):
+    g = torch.Generator().manual_seed(seed)
+    U, _ = torch.linalg.qr(torch.randn(m, n, generator=g, dtype=torch.float64))
+    V, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    s = torch.tensor([decay ** i for i in range(n)], dtype=torch.float64) * 10
+    s[r:] *= noise
+    return ((U * s) @ V.t()).to(dtype), s
+
+
+@pytest.mark.parametrize("sketch", ["JLT", "FJLT", "CWT"])
+@pytest.mark.parametrize("iters", [0, 2])
+def test_approximate_svd_tall(sketch, iters):
+    A, s0 = _lowrank(2000, 120, 10, decay=0.7)
+    U, s, V = sk.nla.approximate_svd(A, 10, context=sk.Context(1),
+                                     params=sk.nla.ApproximateSVDParams(num_iterations=iters, sketch=sketch))
+    assert U.shape == (2000, 10) and V.shape == (120, 10)
+    torch.testing.assert_close(s, s0[:10], rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(U.t() @ U, torch.eye(10, dtype=U.dtype), atol=1e-8, rtol=0)
+    R = (U * s) @ V.t()
+    assert float((A - R).norm() / A.norm()) < 1e-2
+
+
+def test_approximate_svd_wide():
+    A, s0 = _lowrank(1500, 100, 8, decay=0.6)
+    At = A.t().contiguous()
+    U, s, V = sk.nla.approximate_svd(At, 8, params=sk.nla.ApproximateSVDParams(num_iterations=1))
+    assert U.shape == (100, 8) and V.shape == (1500, 8)
+    torch.testing.assert_close(s, s0[:8], rtol=1e-2, atol=1e-2)
+
+
+def test_rank_check():
+    with pytest.raises(sk.base.exceptions.InvalidParametersError):
+        sk.nla.approximate_svd(torch.randn(10, 5, dtype=torch.float64), 6)
+
+
+def test_fused_pass_torch_path():
+    A = torch.randn(5000, 64, dtype=torch.float64)
+    Z = torch.randn(64, 12, dtype=torch.float64)
+    W, G, Y = tallskinny.fused_pass(A, Z, keep_y=True)
+    Yr = A @ Z
+    torch.testing.assert_close(Y, Yr)
+    torch.testing.assert_close(W, A.t() @ Yr)
+    torch.testing.assert_close(G, Yr.t() @ Yr)
+
+
+def test_symmetric_svd():
+    A, s0 = _lowrank(300, 300, 6, decay=0.5)
+    Asym = A @ A.t()
+    V, w = sk.nla.approximate_symmetric_svd(Asym, 6, params=sk.nla.ApproximateSVDParams(num_iterations=2))
+    torch.testing.assert_close(w, (s0[:6] ** 2), rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_approximate_svd_gpu_bf16(dev):
+    A, s0 = _lowrank(20000, 256, 12, decay=0.7)
+    Ab = A.to(dev, torch.bfloat16)
+    ref_s = torch.linalg.svdvals(Ab.double())[:12].cpu()
+    U, s, V = sk.nla.approximate_svd(Ab, 12, context=sk.Context(2),
+                                     params=sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT"))
+    torch.testing.assert_close(s.double().cpu(), ref_s, rtol=2e-3, atol=2e-3)
+    I = torch.eye(12, device=dev)
+    torch.testing.assert_close(U.t().float() @ U.float(), I, atol=1e-4, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("native", [False, True])
+def test_fused_pass_gpu_bf16(dev, native):
+    old = tallskinny.USE_NATIVE
+    tallskinny.USE_NATIVE = native
+    try:
+        m, n, k = 70001, 1000, 40
+        A = torch.randn(m, n, device=dev).to(torch.bfloat16)
+        Z = torch.randn(n, k, device=dev) / 30
+        W, G, Y = tallskinny.fused_pass(A, Z, keep_y=True)
+        Ad = A.double()
+        Yr = Ad @ Z.to(torch.bfloat16).double()
+        torch.testing.assert_close(Y.double(), Yr, rtol=1e-4, atol=1e-4 * float(Yr.abs().max()))
+        Wr = Ad.t() @ Yr
+        torch.testing.assert_close(W.double(), Wr, rtol=1e-3, atol=1e-4 * float(Wr.abs().max()))
+        Gr = Yr.t() @ Yr
+        torch.testing.assert_close(G.double(), Gr, rtol=1e-3, atol=1e-5 * float(Gr.abs().max()))
+    finally:
+        tallskinny.USE_NATIVE = old

@@ -1,0 +1,213 @@
+"""Sketch transforms: explicit-operator oracles, serialization round trips, dims.
+
+Oracle pattern of the reference tests (tests/unit/test_utils.hpp:14-35,
+SparseSketchApplyElementalTest.cpp:63-140): build the explicit S and compare
+apply() with S @ A (columnwise) and A @ S^T (rowwise).
+"""
+import json
+import math
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+import libskylark_amd as sk
+from libskylark_amd.sketch import COLUMNWISE, ROWWISE, deserialize_sketch
+
+N, S, M = 120, 24, 17
+
+
+def _A(rows, cols, seed=0, dtype=torch.float64):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(rows, cols, generator=g, dtype=dtype)
+
+
+def _explicit(T):
+    return T.realize(dtype=torch.float64)
+
+
+LINEAR = [
+    lambda c: sk.sketch.JLT(N, S, context=c),
+    lambda c: sk.sketch.CT(N, S, C=2.0, context=c),
+    lambda c: sk.sketch.CWT(N, S, context=c),
+    lambda c: sk.sketch.MMT(N, S, context=c),
+    lambda c: sk.sketch.WZT(N, S, p=1.5, context=c),
+    lambda c: sk.sketch.FJLT(N, S, context=c),
+    lambda c: sk.sketch.UST(N, S, replace=True, context=c),
+    lambda c: sk.sketch.UST(N, S, replace=False, context=c),
+]
+
+
+@pytest.mark.parametrize("mk", LINEAR)
+def test_linear_sketch_matches_explicit(mk):
+    T = mk(sk.Context(7))
+    P = _explicit(T)
+    A = _A(N, M)
+    torch.testing.assert_close(T.apply(A, dim=COLUMNWISE).double(), P @ A, rtol=1e-9, atol=1e-9)
+    B = _A(M, N, 1)
+    torch.testing.assert_close(T.apply(B, dim=ROWWISE).double(), B @ P.t(), rtol=1e-9, atol=1e-9)
+    # operators
+    torch.testing.assert_close((T * A).double(), P @ A, rtol=1e-9, atol=1e-9)
+    torch.testing.assert_close((T / B).double(), B @ P.t(), rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("mk", LINEAR)
+def test_serialization_roundtrip(mk):
+    T = mk(sk.Context(13))
+    d = T.serialize()
+    assert d["skylark_object_type"] == "sketch" and d["N"] == N and d["S"] == S
+    assert d["creation_context"]["skylark_object_type"] == "context"
+    T2 = deserialize_sketch(json.loads(json.dumps(d)))
+    A = _A(N, M)
+    torch.testing.assert_close(T2 * A, T * A)
+    T3 = pickle.loads(pickle.dumps(T))
+    torch.testing.assert_close(T3 * A, T * A)
+
+
+def test_context_advances_like_reference():
+    c = sk.Context(1)
+    sk.sketch.JLT(10, 3, context=c)
+    assert c.counter == 30
+    sk.sketch.CWT(10, 3, context=c)
+    assert c.counter == 50
+    sk.sketch.FJLT(10, 3, context=c)
+    assert c.counter == 63
+    sk.sketch.WZT(10, 3, p=1.2, context=c)
+    assert c.counter == 93
+
+
+def test_sparse_input_matches_dense():
+    A = _A(N, M)
+    A[A.abs() < 1.0] = 0
+    As = A.to_sparse_csr()
+    for T in (sk.sketch.JLT(N, S, context=sk.Context(1)), sk.sketch.CWT(N, S, context=sk.Context(2))):
+        dense_out = T.apply(A, dim=COLUMNWISE)
+        sp_out = T.apply(As, dim=COLUMNWISE)
+        sp_out = sp_out.to_dense() if sp_out.layout != torch.strided else sp_out
+        torch.testing.assert_close(sp_out.double(), dense_out.double(), rtol=1e-9, atol=1e-9)
+        B = A.t().contiguous()
+        ro = T.apply(B.to_sparse_csr(), dim=ROWWISE)
+        ro = ro.to_dense() if ro.layout != torch.strided else ro
+        torch.testing.assert_close(ro.double(), T.apply(B, dim=ROWWISE).double(), rtol=1e-9, atol=1e-9)
+
+
+def test_numpy_and_scipy_operands():
+    import scipy.sparse as sp
+    T = sk.sketch.CWT(N, S, context=sk.Context(3))
+    A = np.random.default_rng(0).standard_normal((N, M))
+    out = T * A
+    assert isinstance(out, np.ndarray) and out.shape == (S, M)
+    As = sp.random(N, M, density=0.2, format="csr", random_state=1)
+    out2 = T * As
+    assert sp.issparse(out2) and out2.shape == (S, M)
+    np.testing.assert_allclose(out2.toarray(), T.realize().numpy() @ As.toarray(), atol=1e-12)
+
+
+def test_dimension_checks():
+    T = sk.sketch.JLT(N, S)
+    with pytest.raises(sk.base.exceptions.DimensionMismatchError):
+        T * _A(N + 1, 3)
+
+
+def test_jlt_preserves_norms_statistically():
+    T = sk.sketch.JLT(2000, 400, context=sk.Context(5))
+    A = _A(2000, 50)
+    r = (T * A).norm(dim=0) / A.norm(dim=0)
+    assert 0.8 < float(r.min()) and float(r.max()) < 1.2
+
+
+def test_rft_gaussian_kernel_approximation():
+    """E[z(x)^T z(y)] = exp(-|x-y|^2 / (2 sigma^2))."""
+    d, s, sigma = 6, 20000, 1.5
+    T = sk.sketch.GaussianRFT(d, s, sigma=sigma, context=sk.Context(3))
+    X = _A(d, 5, 2) * 0.5
+    Z = T * X
+    K = Z.t() @ Z
+    D2 = torch.cdist(X.t(), X.t()) ** 2
+    torch.testing.assert_close(K, torch.exp(-D2 / (2 * sigma ** 2)), atol=0.03, rtol=0)
+
+
+def test_laplacian_rft_kernel_approximation():
+    d, s, sigma = 4, 20000, 2.0
+    T = sk.sketch.LaplacianRFT(d, s, sigma=sigma, context=sk.Context(3))
+    X = _A(d, 5, 2) * 0.5
+    Z = T * X
+    D1 = torch.cdist(X.t(), X.t(), p=1)
+    torch.testing.assert_close(Z.t() @ Z, torch.exp(-D1 / sigma), atol=0.04, rtol=0)
+
+
+def test_fastfood_gaussian_kernel_approximation():
+    d, s, sigma = 16, 16 * 800, 2.0
+    T = sk.sketch.FastGaussianRFT(d, s, sigma=sigma, context=sk.Context(3))
+    X = _A(d, 4, 2) * 0.4
+    Z = T * X
+    D2 = torch.cdist(X.t(), X.t()) ** 2
+    torch.testing.assert_close(Z.t() @ Z, torch.exp(-D2 / (2 * sigma ** 2)), atol=0.05, rtol=0)
+
+
+def test_qrft_kernel_approximation():
+    d, s, sigma = 3, 4000, 1.0
+    T = sk.sketch.GaussianQRFT(d, s, sigma=sigma, skip=10, context=sk.Context(0))
+    X = _A(d, 4, 2) * 0.3
+    Z = T * X
+    D2 = torch.cdist(X.t(), X.t()) ** 2
+    torch.testing.assert_close(Z.t() @ Z, torch.exp(-D2 / (2 * sigma ** 2)), atol=0.03, rtol=0)
+    T2 = deserialize_sketch(T.serialize())
+    torch.testing.assert_close(T2 * X, Z)
+
+
+def test_rlt_expsemigroup_kernel():
+    d, s, beta = 3, 40000, 0.5
+    T = sk.sketch.ExpSemigroupRLT(d, s, beta=beta, context=sk.Context(9))
+    X = torch.rand(d, 4, dtype=torch.float64, generator=torch.Generator().manual_seed(1))
+    Z = T * X
+    K = torch.exp(-beta * torch.sqrt(X[:, :, None] + X[:, None, :]).sum(0))
+    torch.testing.assert_close(Z.t() @ Z, K, atol=0.03, rtol=0)
+
+
+def test_ppt_polynomial_kernel():
+    d, s = 5, 8192
+    T = sk.sketch.PPT(d, s, q=2, c=1.0, gamma=1.0, context=sk.Context(2))
+    X = _A(d, 3, 4) * 0.5
+    Z = T * X
+    K = (X.t() @ X + 1.0) ** 2
+    torch.testing.assert_close(Z.t() @ Z, K, atol=0.25 * float(K.abs().max()), rtol=0)
+
+
+@pytest.mark.parametrize("name,kw", [("GaussianRFT", {"sigma": 2.0}), ("LaplacianRFT", {"sigma": 2.0}),
+                                     ("MaternRFT", {"nu": 1.5, "l": 1.0}), ("FastGaussianRFT", {"sigma": 1.0}),
+                                     ("FastMaternRFT", {"nu": 2.5, "l": 1.0}), ("PPT", {"q": 2, "c": 1.0, "gamma": 1.0}),
+                                     ("ExpSemigroupRLT", {"beta": 1.0}), ("ExpSemigroupQRLT", {"beta": 1.0, "skip": 3}),
+                                     ("LaplacianQRFT", {"sigma": 1.0, "skip": 2}), ("GaussianQRFT", {"sigma": 1.0, "skip": 0})])
+def test_feature_maps_serialize(name, kw):
+    T = sk.sketch.sketch_class(name)(12, 30, context=sk.Context(4), **kw)
+    X = torch.rand(12, 5, dtype=torch.float64)
+    T2 = deserialize_sketch(json.dumps(T.serialize()))
+    torch.testing.assert_close(T2 * X, T * X)
+    torch.testing.assert_close(T2 / X.t().contiguous(), (T * X).t())
+
+
+def test_typo_alias_and_registry():
+    T = sk.sketch.FastMaternRFT(8, 8, context=sk.Context(1))
+    d = T.serialize()
+    d["sketch_type"] = "FastMaternnRFT"
+    assert deserialize_sketch(d).sketch_type == "FastMaternRFT"
+    combos = sk.sketch.supported_sketch_transforms()
+    assert ("JLT", "Matrix", "Matrix") in combos and ("CWT", "SparseMatrix", "SparseMatrix") in combos
+
+
+def test_fut_transforms():
+    from scipy.fft import dct
+    from libskylark_amd.ops import fut
+    X = _A(37, 5)
+    torch.testing.assert_close(fut.dct2(X, 0), torch.from_numpy(dct(X.numpy(), type=2, axis=0, norm="ortho")))
+    torch.testing.assert_close(fut.dct3(fut.dct2(X, 0), 0), X)
+    torch.testing.assert_close(fut.dct2(X.t().contiguous(), 1), fut.dct2(X, 0).t())
+    torch.testing.assert_close(fut.dht(fut.dht(X, 0), 0), X)
+    Y = _A(32, 3)
+    torch.testing.assert_close(fut.wht(fut.wht(Y, 0), 0), Y)
+    # FJLT large-S FFT path vs explicit operator
+    T = sk.sketch.FJLT(300, 280, context=sk.Context(1))
+    A = _A(300, 4)
+    torch.testing.assert_close(T * A, T.realize() @ A)
