@@ -1,0 +1,407 @@
+// Tall-skinny streaming kernels for the randomized SVD / power iteration.
+//
+//   sl_tsk_fused_pass:  ONE read of A (m x n bf16, row-major) produces
+//        Y = A Z            (m x k, optional store, f32)
+//        W = A^T Y          (n x k, f32)
+//        G = Y^T Y          (k x k, f32)
+//   sl_tsk_matmul:      Y = A Z  (Z given as bf16 hi + lo split, f32 out)
+//
+// Reference hot loops these replace: the two El::Gemm calls per power
+// iteration plus the QR Gram (nla/svd.hpp:71-149, base/Gemm.hpp:84-103).
+//
+// gfx950 design (one workgroup of 8 waves per CU, persistent):
+//   * the n columns are split over the 8 waves (NW = 64 or 128 columns
+//     each); a wave keeps its slice of Z (bf16 MFMA B-fragments) and its
+//     slice of W (f32 accumulators) in registers for the whole kernel;
+//   * row blocks of BM = 16 rows stream HBM -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4, 1 KiB per wave-instruction), triple
+//     buffered, each wave fetching only its own columns; the LDS image is
+//     XOR-swizzled through the SOURCE address (chunk ^ row) so both reads
+//     below are (nearly) conflict-free:
+//       - step 1  y_w = A_w Z_w  : ds_read_b128 row fragments,
+//                                  v_mfma_f32_16x16x32_bf16
+//       - step 2  y = sum_w y_w  : partials through LDS (2 barriers)
+//       - step 3  W_w += A_w^T y : ds_read_b64_tr_b16 transposed fragments
+//                                  of the SAME LDS image, y as bf16 hi+lo,
+//                                  v_mfma_f32_16x16x16_bf16 (2 per tile)
+//       - step 4  G += y^T y     : hi*hi + hi*lo + lo*hi, tiles spread
+//                                  over the waves;
+//   * raw s_barrier + counted vmcnt (no __syncthreads, which would drain
+//     the DMA queue), all LDS in one dynamic array;
+//   * per-workgroup W/G partial slabs, summed in f64 by a second kernel.
+#include "sl_common.hpp"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int WAVES = 8;
+constexpr int THREADS = WAVES * 64;
+constexpr int BM = 16;
+constexpr int NBUF = 3;
+
+// hardware round-to-nearest-even (v_cvt_pk_bf16_f32), NaN-preserving, branch-free
+__device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
+__device__ __forceinline__ float bf16_val(short h) { return (float)__builtin_bit_cast(__bf16, h); }
+
+// LDS-DMA of 16 B per lane into LDS[lds_base + lane*16], issued as inline asm
+// so hipcc does not insert its own (draining) vmcnt(0) before later LDS
+// reads; completion is tracked by the hand-counted s_waitcnt vmcnt(N).
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+template <int NW, int KT>
+struct Geo {
+  static constexpr int ROWB = NW * 2;                 // bytes per LDS row of a wave region
+  static constexpr int NCH = NW / 8;                  // 16-B chunks per row
+  static constexpr int REGION = BM * ROWB;            // bytes per wave per buffer
+  static constexpr int LPB = REGION / 1024;           // glds instructions per block per wave
+  static constexpr int KP = KT * 16;
+  static constexpr int ABYTES = NBUF * WAVES * REGION;
+  static constexpr int YP_BYTES = WAVES * BM * KP * 4;
+  static constexpr int YF_BYTES = BM * KP * 4;
+  static constexpr int LDS = ABYTES + YP_BYTES + YF_BYTES;
+  static constexpr int GTILES = KT * KT;
+  static constexpr int GS = (GTILES + WAVES - 1) / WAVES;  // G tiles per wave
+};
+
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT>
+__global__ void __launch_bounds__(THREADS, 1)
+k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
+           const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
+           float* __restrict__ Wslab, float* __restrict__ Gslab,
+           float* __restrict__ Y, int64_t ldy) {
+  using GG = Geo<NW, KT>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* abuf = smem;
+  float* yp = (float*)(smem + GG::ABYTES);
+  float* yf = (float*)(smem + GG::ABYTES + GG::YP_BYTES);
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0w = w * NW;
+  const int64_t nblocks = (m + BM - 1) / BM;
+  const int64_t b0 = blockIdx.x;
+  const int64_t bstep = gridDim.x;
+
+  // ---- Z fragments (B operand of step 1): lane holds Z[c0w+32ks+8(l>>4)+j][16t+(l&15)]
+  bf16x8 zh[NW / 32][KT];
+  bf16x8 zl[ZSPLIT ? NW / 32 : 1][ZSPLIT ? KT : 1];
+#pragma unroll
+  for (int ks = 0; ks < NW / 32; ++ks)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int col = 16 * t + (lane & 15);
+      const int kk = c0w + 32 * ks + 8 * (lane >> 4);
+      bf16x8 v = {};
+      if (col < k && kk + 8 <= n) v = *(const bf16x8*)(Zt + (int64_t)col * n + kk);
+      zh[ks][t] = v;
+      if constexpr (ZSPLIT) {
+        bf16x8 u = {};
+        if (col < k && kk + 8 <= n) u = *(const bf16x8*)(Zt + (int64_t)(col + k) * n + kk);
+        zl[ks][t] = u;
+      }
+    }
+
+  // Consume the Z registers here so hipcc's vmcnt wait for these loads sits
+  // before the loop (otherwise it lands on the first MFMA of every
+  // iteration and drains the LDS-DMA prefetch queue).
+#pragma unroll
+  for (int ks = 0; ks < NW / 32; ++ks)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      asm volatile("" ::"v"(zh[ks][t]));
+      if constexpr (ZSPLIT) asm volatile("" ::"v"(zl[ks][t]));
+    }
+
+  f32x4 accW[DO_W ? NW / 16 : 1][DO_W ? KT : 1];
+  if constexpr (DO_W) {
+#pragma unroll
+    for (int a = 0; a < NW / 16; ++a)
+#pragma unroll
+      for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 accG[GG::GS];
+#pragma unroll
+  for (int s = 0; s < GG::GS; ++s) accG[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- LDS-DMA of one row block (this wave's columns) into buffer `buf`
+  auto issue = [&](int64_t blk, int buf) {
+    char* region = abuf + (buf * WAVES + w) * GG::REGION;
+    const int64_t r0 = blk * BM;
+#pragma unroll
+    for (int i = 0; i < GG::LPB; ++i) {
+      const int byte = i * 1024 + lane * 16;
+      const int row = byte / GG::ROWB;
+      const int slot = (byte % GG::ROWB) / 16;
+      const int chunk = slot ^ (row & (GG::NCH - 1));
+      int64_t grow = r0 + row;
+      grow = grow < m ? grow : m - 1;
+      int col = c0w + chunk * 8;
+      col = col + 8 <= n ? col : n - 8;
+      const bf16_t* src = A + grow * lda + col;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(
+          (unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
+      glds16((const void*)src, dst);
+    }
+  };
+
+  int64_t my = 0;  // local iteration index
+  if (b0 < nblocks) issue(b0, 0);
+  if (b0 + bstep < nblocks) issue(b0 + bstep, 1);
+
+  for (int64_t blk = b0; blk < nblocks; blk += bstep, ++my) {
+    const int buf = (int)(my % NBUF);
+    const bool more = blk + bstep < nblocks;
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const char* region = abuf + (buf * WAVES + w) * GG::REGION;
+
+    // ---- step 1: partial y over this wave's columns
+    f32x4 accY[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) accY[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NW / 32; ++ks) {
+      const int row = lane & 15;
+      const int chunk = (lane >> 4) + 4 * ks;
+      const int slot = chunk ^ (row & (GG::NCH - 1));
+      const bf16x8 af = *(const bf16x8*)(region + row * GG::ROWB + slot * 16);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        accY[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zh[ks][t], accY[t], 0, 0, 0);
+        if constexpr (ZSPLIT) accY[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zl[ks][t], accY[t], 0, 0, 0);
+      }
+    }
+    // ---- step 2: cross-wave reduction of y through LDS
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        yp[(w * BM + (lane >> 4) * 4 + j) * GG::KP + 16 * t + (lane & 15)] = accY[t][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+      const int64_t r0 = blk * BM;
+      for (int idx = lane; idx < 2 * GG::KP; idx += 64) {
+        const int row = 2 * w + idx / GG::KP;
+        const int col = idx % GG::KP;
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < WAVES; ++v) s += yp[(v * BM + row) * GG::KP + col];
+        if (r0 + row >= m) s = 0.f;
+        yf[row * GG::KP + col] = s;
+        if constexpr (STORE_Y) {
+          if (r0 + row < m && col < k) Y[(r0 + row) * ldy + col] = s;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // prefetch two blocks ahead into the buffer consumed two iterations ago
+    if (blk + 2 * bstep < nblocks) issue(blk + 2 * bstep, (int)((my + 2) % NBUF));
+
+    if constexpr (DO_W || DO_G) {
+      // ---- y fragments (rows 4(l>>4)+j, col 16t+(l&15)), bf16 hi/lo
+      s16x4 yh[KT], yl[KT];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = yf[((lane >> 4) * 4 + j) * GG::KP + 16 * t + (lane & 15)];
+          const short h = bf16_bits(v);
+          yh[t][j] = h;
+          yl[t][j] = bf16_bits(v - bf16_val(h));
+        }
+      }
+      if constexpr (DO_W) {
+        // ---- step 3: W_w += A_w^T y   (transposed LDS reads of the same image)
+        const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+        const int row = 4 * g + q;
+#pragma unroll
+        for (int ct = 0; ct < NW / 16; ++ct) {
+          const int chunk = 2 * ct + (p >> 1);
+          const int slot = chunk ^ (row & (GG::NCH - 1));
+          const char* addr = region + row * GG::ROWB + slot * 16 + (p & 1) * 8;
+          const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
+#pragma unroll
+          for (int t = 0; t < KT; ++t) {
+            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);
+            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0);
+          }
+        }
+      }
+      if constexpr (DO_G) {
+        // ---- step 4: G tiles tau = w + 8 s  (t1 = tau / KT, t2 = tau % KT)
+#pragma unroll
+        for (int s = 0; s < GG::GS; ++s) {
+          const int tau = w + WAVES * s;
+          if (tau < GG::GTILES) {
+            const int t1 = tau / KT, t2 = tau % KT;
+            s16x4 ah = yh[0], al = yl[0], bh = yh[0], bl = yl[0];
+#pragma unroll
+            for (int t = 1; t < KT; ++t) {
+              if (t1 == t) { ah = yh[t]; al = yl[t]; }
+              if (t2 == t) { bh = yh[t]; bl = yl[t]; }
+            }
+            accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, accG[s], 0, 0, 0);
+            accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, accG[s], 0, 0, 0);
+            accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, accG[s], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- partial slabs: W rows = A columns, layout [WAVES*NW][KP]
+  if constexpr (DO_W) {
+    float* ws = Wslab + (int64_t)blockIdx.x * (WAVES * NW) * GG::KP;
+#pragma unroll
+    for (int ct = 0; ct < NW / 16; ++ct)
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          ws[(c0w + 16 * ct + (lane >> 4) * 4 + j) * GG::KP + 16 * t + (lane & 15)] = accW[ct][t][j];
+  }
+  if constexpr (DO_G) {
+    float* gs = Gslab + (int64_t)blockIdx.x * GG::KP * GG::KP;
+#pragma unroll
+    for (int s = 0; s < GG::GS; ++s) {
+      const int tau = w + WAVES * s;
+      if (tau < GG::GTILES) {
+        const int t1 = tau / KT, t2 = tau % KT;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          gs[(16 * t1 + (lane >> 4) * 4 + j) * GG::KP + 16 * t2 + (lane & 15)] = accG[s][j];
+      }
+    }
+  }
+}
+
+// out[i][j] = sum_s slab[s][i][j]  (i < rows, j < cols) accumulated in f64
+__global__ void __launch_bounds__(256)
+k_slab_reduce(const float* __restrict__ slab, int nslab, int64_t slab_stride, int ld_in,
+              int rows, int cols, float* __restrict__ out, int ld_out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)rows * cols) return;
+  const int i = (int)(t / cols), j = (int)(t % cols);
+  double s = 0.0;
+  for (int b = 0; b < nslab; ++b) s += slab[b * slab_stride + (int64_t)i * ld_in + j];
+  out[(int64_t)i * ld_out + j] = (float)s;
+}
+
+int grid_for(int64_t m) {
+  static int ncu = -1;
+  if (ncu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  int64_t nb = (m + BM - 1) / BM;
+  return (int)(nb < ncu ? nb : ncu);
+}
+
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT>
+int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
+           float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
+  using GG = Geo<NW, KT>;
+  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT>;
+  static bool attr = false;
+  if (!attr) {
+    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
+    attr = true;
+  }
+  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+}  // namespace
+
+// workspace bytes needed by sl_tsk_fused_pass
+SL_API int64_t sl_tsk_fused_workspace(int64_t m, int64_t n, int k) {
+  const int KP = ((k + 15) / 16) * 16;
+  const int NWP = n <= 512 ? 512 : 1024;
+  const int64_t g = 256;  // upper bound on the grid
+  return g * (int64_t)NWP * KP * 4 + g * (int64_t)KP * KP * 4 + 256;
+}
+
+SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k,
+                             float* W, float* G, float* Y, int64_t ldy, void* ws, void* stream) {
+  if (m <= 0) return SL_OK;
+  if (n % 8 || lda % 8 || n > 1024 || k > 64 || k < 1 || n < 8) {
+    sl_set_last_error("tsk_fused_pass: needs n%8==0, lda%8==0, 8<=n<=1024, 1<=k<=64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int KT = (k + 15) / 16;
+  const int KP = KT * 16;
+  const bool small = n <= 512;
+  const int NWT = small ? 512 : 1024;
+  const int g = grid_for(m);
+  float* Wslab = (float*)ws;
+  float* Gslab = Wslab + (int64_t)g * NWT * KP;
+  int rc = SL_ERR_UNSUPPORTED;
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* z = (const bf16_t*)Zt;
+#define SL_TSK(NW, KTT)                                                                              \
+  rc = Y ? launch<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+         : launch<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
+  if (small) {
+    switch (KT) { case 1: SL_TSK(64, 1); break; case 2: SL_TSK(64, 2); break; case 3: SL_TSK(64, 3); break; default: SL_TSK(64, 4); }
+  } else {
+    switch (KT) { case 1: SL_TSK(128, 1); break; case 2: SL_TSK(128, 2); break; case 3: SL_TSK(128, 3); break; default: SL_TSK(128, 4); }
+  }
+#undef SL_TSK
+  if (rc != SL_OK) return rc;
+  {
+    int64_t tot = n * (int64_t)k;
+    k_slab_reduce<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k);
+    SL_LAUNCH_CHECK();
+    tot = (int64_t)k * k;
+    k_slab_reduce<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(Gslab, g, (int64_t)KP * KP, KP, k, k, G, k);
+    SL_LAUNCH_CHECK();
+  }
+  return SL_OK;
+}
+
+// Y = A Z with Z given as [Z_hi; Z_lo] (2k x n, bf16, "Zt" layout), f32 out.
+SL_API int sl_tsk_matmul(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k,
+                         float* Y, int64_t ldy, int zsplit, void* stream) {
+  if (m <= 0) return SL_OK;
+  if (n % 8 || lda % 8 || n > 1024 || k > 64 || k < 1 || n < 8) {
+    sl_set_last_error("tsk_matmul: needs n%8==0, lda%8==0, 8<=n<=1024, 1<=k<=64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int KT = (k + 15) / 16;
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* z = (const bf16_t*)Zt;
+  int rc = SL_ERR_UNSUPPORTED;
+#define SL_MM(NW, KTT)                                                                                      \
+  rc = zsplit ? launch<NW, KTT, false, false, true, true>(a, m, (int)n, lda, z, k, nullptr, nullptr, Y, ldy, s) \
+              : launch<NW, KTT, false, false, true, false>(a, m, (int)n, lda, z, k, nullptr, nullptr, Y, ldy, s)
+  if (n <= 512) {
+    switch (KT) { case 1: SL_MM(64, 1); break; case 2: SL_MM(64, 2); break; case 3: SL_MM(64, 3); break; default: SL_MM(64, 4); }
+  } else {
+    switch (KT) { case 1: SL_MM(128, 1); break; case 2: SL_MM(128, 2); break; case 3: SL_MM(128, 3); break; default: SL_MM(128, 4); }
+  }
+#undef SL_MM
+  return rc;
+}

@@ -22,10 +22,23 @@ def _c(comm):
 
 
 # ------------------------------------------------------------- products
+GRAM_CHUNK = 1 << 16
+
+
 def gram(Y_local: torch.Tensor, comm: Comm | None = None, dtype=torch.float64) -> torch.Tensor:
-    """``Y^T Y`` for a row-distributed Y (all-reduced, replicated k x k)."""
-    Yd = Y_local.to(dtype) if Y_local.dtype != dtype and Y_local.dtype != torch.float64 else Y_local
-    G = Yd.t() @ Yd
+    """``Y^T Y`` for a row-distributed Y (all-reduced, replicated k x k, float64).
+
+    f32 inputs are multiplied in f32 on the matrix cores in row chunks whose
+    partial Grams are accumulated in f64 (an f64 GEMM over a million rows
+    is ~50x slower on MI355X and buys nothing here)."""
+    if Y_local.dtype == torch.float64:
+        G = Y_local.t() @ Y_local
+    else:
+        Yf = Y_local if Y_local.dtype == torch.float32 else Y_local.float()
+        G = torch.zeros(Yf.shape[1], Yf.shape[1], dtype=torch.float64, device=Yf.device)
+        for r0 in range(0, Yf.shape[0], GRAM_CHUNK):
+            Yc = Yf[r0:r0 + GRAM_CHUNK]
+            G += (Yc.t() @ Yc).double()
     return _c(comm).all_reduce(G.contiguous())
 
 

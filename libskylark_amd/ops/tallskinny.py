@@ -26,16 +26,17 @@ _lib.register("sl_tsk_fused_workspace", [i64, i64, i32], C.c_int64)
 _lib.register("sl_tsk_matmul", [vp, i64, i64, i64, vp, i32, vp, i64, i32, vp])
 
 # rows per chunk in the torch fallback (bounds the y temporary)
-CHUNK_ROWS = 1 << 18
+CHUNK_ROWS = 1 << 16
 USE_NATIVE = True
 
 
 def _native_ok(A: torch.Tensor, k: int) -> bool:
     if not (USE_NATIVE and A.is_cuda and A.dtype == torch.bfloat16 and k <= 64):
         return False
-    if A.stride(1) != 1 or A.shape[1] % 8 or A.stride(0) % 8:
+    if A.stride(1) != 1 or A.shape[1] % 8 or A.stride(0) % 8 or A.shape[1] < 8:
         return False
-    if A.shape[1] > 2048:
+    n = A.shape[1]
+    if n > 1024 or (n > 512 and k > 48):
         return False
     lib = _lib.load()
     return lib is not None and hasattr(lib, "sl_tsk_fused_pass")
@@ -76,13 +77,15 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False):
     if _native_ok(A, k):
         return _fused_native(A, Z, keep_y)
     wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
-    Zc = Z.to(A.dtype) if A.dtype in (torch.bfloat16, torch.float16) else Z.to(wdt)
+    # low-precision A: Z is rounded to A's dtype (as the MFMA kernel does) and
+    # the products are formed in f32
+    Zc = Z.to(A.dtype).to(wdt) if A.dtype in (torch.bfloat16, torch.float16) else Z.to(wdt)
     W = torch.zeros(n, k, dtype=wdt, device=A.device)
     G = torch.zeros(k, k, dtype=torch.float64, device=A.device)
     Ys = [] if keep_y else None
     for r0 in range(0, m, CHUNK_ROWS):
         Ab = A[r0:r0 + CHUNK_ROWS]
-        y = torch.matmul(Ab, Zc).to(wdt)
+        y = torch.matmul(Ab.to(wdt), Zc)
         if A.dtype in (torch.bfloat16, torch.float16):
             yh, yl = _split_bf16(y)
             W += (torch.matmul(Ab.t(), yh).to(wdt) + torch.matmul(Ab.t(), yl).to(wdt))
@@ -99,7 +102,7 @@ def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool):
     m, n = A.shape
     k = Z.shape[1]
     dev = A.device
-    Zb = Z.to(torch.bfloat16).contiguous()
+    Zb = Z.t().to(torch.bfloat16).contiguous()  # Zt layout (k x n)
     W = torch.empty(n, k, dtype=torch.float32, device=dev)
     G = torch.empty(k, k, dtype=torch.float32, device=dev)
     Y = torch.empty(m, k, dtype=torch.float32, device=dev) if keep_y else None
@@ -117,7 +120,7 @@ def matmul(A: torch.Tensor, Z: torch.Tensor, out_dtype=torch.float32) -> torch.T
         m, n = A.shape
         k = Z.shape[1]
         hi, lo = _split_bf16(Z.float())
-        Zs = torch.cat([hi, lo], 1).contiguous()
+        Zs = torch.cat([hi.t(), lo.t()], 0).contiguous()  # [Z_hi^T; Z_lo^T] (2k x n)
         Y = torch.empty(m, k, dtype=torch.float32, device=A.device)
         _lib.call("sl_tsk_matmul", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zs), k, _lib.ptr(Y), Y.stride(0), 1,
                   vp(_lib.stream_of(A)))

@@ -71,6 +71,37 @@ def test_approximate_svd_gpu_bf16(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(70001, 1000, 40), (5000, 512, 64), (3000, 136, 9), (33, 64, 16)])
+def test_tsk_matmul_native(dev, m, n, k):
+    A = torch.randn(m, n, device=dev).to(torch.bfloat16)
+    Z = torch.randn(n, k, device=dev, dtype=torch.float64)
+    assert tallskinny._native_ok(A, k)
+    Y = tallskinny.matmul(A, Z)
+    Yr = A.double() @ Z
+    torch.testing.assert_close(Y.double(), Yr, rtol=1e-4, atol=1e-4 * float(Yr.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(70001, 1000, 40), (4099, 512, 64), (1000, 72, 3), (17, 1024, 48)])
+def test_fused_pass_native_shapes(dev, shape):
+    m, n, k = shape
+    A = torch.randn(m, n, device=dev).to(torch.bfloat16)
+    Z = torch.randn(n, k, device=dev) / 30
+    assert tallskinny._native_ok(A, k)
+    W, G, Y = tallskinny.fused_pass(A, Z, keep_y=True)
+    Ad = A.double()
+    Yr = Ad @ Z.to(torch.bfloat16).double()
+    torch.testing.assert_close(Y.double(), Yr, rtol=1e-4, atol=1e-4 * float(Yr.abs().max()))
+    Wr = Ad.t() @ Yr
+    torch.testing.assert_close(W.double(), Wr, rtol=1e-3, atol=1e-4 * float(Wr.abs().max()))
+    Gr = Yr.t() @ Yr
+    torch.testing.assert_close(G.double(), Gr, rtol=1e-3, atol=1e-5 * float(Gr.abs().max()))
+    W2, G2, Y2 = tallskinny.fused_pass(A, Z, keep_y=False)
+    assert Y2 is None
+    torch.testing.assert_close(W2, W)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("native", [False, True])
 def test_fused_pass_gpu_bf16(dev, native):
     old = tallskinny.USE_NATIVE
