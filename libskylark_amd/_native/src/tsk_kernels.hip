@@ -294,17 +294,44 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
   }
 }
 
-// out[i][j] = sum_s slab[s][i][j]  (i < rows, j < cols) accumulated in f64
+}  // namespace
+
+// out[i][j] = sum_s slab[s][i][j]  (i < rows, j < cols <= 64) accumulated in f64.
+// One workgroup per output row; 4 slab groups x 64 columns, coalesced rows.
+template <typename OT>
 __global__ void __launch_bounds__(256)
-k_slab_reduce(const float* __restrict__ slab, int nslab, int64_t slab_stride, int ld_in,
-              int rows, int cols, float* __restrict__ out, int ld_out) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)rows * cols) return;
-  const int i = (int)(t / cols), j = (int)(t % cols);
+k_slab_reduce_rows(const float* __restrict__ slab, int nslab, int64_t slab_stride, int ld_in,
+                   int cols, OT* __restrict__ out, int ld_out) {
+  __shared__ double part[4][64];
+  const int i = blockIdx.x;
+  const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
   double s = 0.0;
-  for (int b = 0; b < nslab; ++b) s += slab[b * slab_stride + (int64_t)i * ld_in + j];
-  out[(int64_t)i * ld_out + j] = (float)s;
+  if (j < cols)
+    for (int b = g; b < nslab; b += 4) s += slab[b * slab_stride + (int64_t)i * ld_in + j];
+  part[g][j] = s;
+  __syncthreads();
+  if (g == 0 && j < cols) out[(int64_t)i * ld_out + j] = (OT)(part[0][j] + part[1][j] + part[2][j] + part[3][j]);
 }
+
+int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
+                          int cols, float* out, int ld_out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return SL_OK;
+  if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
+  k_slab_reduce_rows<float><<<rows, 256, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
+                              int cols, double* out, int ld_out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return SL_OK;
+  if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
+  k_slab_reduce_rows<double><<<rows, 256, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+namespace {
 
 int grid_for(int64_t m) {
   static int ncu = -1;
@@ -370,15 +397,9 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   }
 #undef SL_TSK
   if (rc != SL_OK) return rc;
-  {
-    int64_t tot = n * (int64_t)k;
-    k_slab_reduce<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k);
-    SL_LAUNCH_CHECK();
-    tot = (int64_t)k * k;
-    k_slab_reduce<<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(Gslab, g, (int64_t)KP * KP, KP, k, k, G, k);
-    SL_LAUNCH_CHECK();
-  }
-  return SL_OK;
+  rc = sl_slab_reduce_launch(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k, s);
+  if (rc != SL_OK) return rc;
+  return sl_slab_reduce_launch(Gslab, g, (int64_t)KP * KP, KP, k, k, G, k, s);
 }
 
 // Y = A Z with Z given as [Z_hi; Z_lo] (2k x n, bf16, "Zt" layout), f32 out.

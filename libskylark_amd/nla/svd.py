@@ -23,7 +23,9 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
+import numpy as np
 import torch
+from scipy.linalg import solve_triangular
 
 from ..base import linalg as L
 from ..base.context import Context
@@ -122,55 +124,104 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
     from ..ops import tallskinny as T
 
-    Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float64)
+    Zh = _sketch_operator(params.sketch, n, k, ctx, "cpu", torch.float64).numpy()
     q = max(0, int(params.num_iterations))
+    Y = W = None
     for it in range(q + 1):
         last = it == q
-        W, G, Y = T.fused_pass(A_loc, Z.to(work), keep_y=last)
-        WG = torch.cat([W.double(), G.double()], 0)
-        comm.all_reduce(WG)
-        W, G = WG[:n], WG[n:]
-        R, Rinv = _small_chol_inv(G)
-        if R is None:
-            # Gram not SPD in working precision: explicit TSQR of Y (rare)
-            Yx = Y if Y is not None else T.matmul(A_loc, Z, out_dtype=work)
-            Qx, R = L.tsqr(Yx, comm)
-            Rinv = torch.linalg.solve_triangular(R.double(), torch.eye(k, dtype=torch.float64, device=dev), upper=True)
-            W = L.gemm_tn(A_loc.to(work) if A_loc.dtype != work else A_loc, Qx.to(work), comm).double()
-            Y, Rfix = Qx, True
-        else:
-            Rfix = False
-            W = W @ Rinv  # = A^T Q
+        Wd, Gd, Y = T.fused_pass(A_loc, torch.from_numpy(Zh).to(dev, work), keep_y=last)
         if not last:
-            if params.skip_qr:
-                Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-300)
-            else:
-                Z, _ = torch.linalg.qr(W, mode="reduced")
+            # orth(A^T Q) = orth(A^T A Z): the column space of W = A^T (A Z)
+            # (R^{-1} only re-mixes columns), so only W crosses the network.
+            Wd = Wd.double().contiguous()
+            comm.all_reduce(Wd)
+            Wh = Wd.cpu().numpy()
+            R = _chol_upper(Gd.double().cpu().numpy()) if comm.size == 1 else None
+            if R is not None:  # better conditioned: orth(W R^{-1})
+                Wh = _rsolve(Wh, R)
+            Zh = _normalize_cols(Wh) if params.skip_qr else _cholqr2_host(Wh)[0]
             continue
-        # --- final: Q = Y R^{-1}; refine with one more CholeskyQR on Q (CholQR2)
-        if Rfix:
-            Q = Y.to(work)
-            Vt = W  # A^T Q
+        Wd = Wd.double().contiguous()
+        comm.all_reduce(Wd)
+        W = Wd.cpu().numpy()  # A^T Y  (n x k)
+    # ---- final basis Q = Y R^{-1}, R from CholeskyQR2 of the stored Y (f32)
+    _, G1 = T.f32_xm(Y, None, store=False, gram=True) if work == torch.float32 else (None, L.gram(Y, None))
+    comm.all_reduce(G1)
+    R1 = _chol_upper(G1.cpu().numpy())
+    if R1 is None:
+        # rank-deficient / ill-conditioned sample (e.g. repeated FJLT samples):
+        # Householder TSQR gives an orthonormal Q regardless; one extra pass
+        # over A forms A^T Q explicitly.
+        Qx, _ = L.tsqr(Y, comm)
+        Qx = Qx.to(work)
+        Vt = L.gemm_tn(A_loc.to(work) if A_loc.dtype != work else A_loc, Qx, comm).double().cpu().numpy()
+        Qv, Rv = _cholqr2_host(Vt)
+        Ur, s, Vrt = np.linalg.svd(Rv)
+        Ub = torch.from_numpy(np.ascontiguousarray(Vrt.T[:, :rank])).to(dev, work)
+        U_loc = Qx @ Ub
+        s = torch.from_numpy(s[:rank].copy()).to(dev, work)
+        V = torch.from_numpy(np.ascontiguousarray((Qv @ Ur)[:, :rank])).to(dev, work)
+        if Ad is not None:
+            return DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm), s, V
+        return U_loc, s, V
+    else:
+        R1inv = _rsolve(np.eye(k), R1)
+        if work == torch.float32:
+            _, G2 = T.f32_xm(Y, torch.from_numpy(R1inv).float().to(dev), store=False, gram=True)
         else:
-            Q = Y.to(work) @ Rinv.to(work)
-            G2 = L.gram(Q, comm)
-            R2, R2inv = _small_chol_inv(G2)
-            if R2 is None:
-                Q, R2 = L.tsqr(Q, comm)
-                R2inv = torch.linalg.solve_triangular(R2.double(), torch.eye(k, dtype=torch.float64, device=dev), upper=True)
-            else:
-                Q = Q @ R2inv.to(work)
-            Vt = W @ R2inv  # A^T Q_refined
-    # SVD of the n x k matrix A^T Q = V S Ub^T  =>  B = Q^T A = Ub S V^T
-    Vv, s, Ubt = torch.linalg.svd(Vt, full_matrices=False)
-    Ub = Ubt.t()
-    U_loc = (Q @ Ub[:, :rank].to(work))
-    s = s[:rank]
-    V = Vv[:, :rank]
+            G2 = L.gram(Y @ torch.from_numpy(R1inv).to(dev, work), None)
+        comm.all_reduce(G2)
+        R2 = _chol_upper(G2.cpu().numpy())
+        Rt = R1 if R2 is None else R2 @ R1
+    Vt = _rsolve(W, Rt)  # = A^T Q  (n x k), Q = Y Rt^{-1} orthonormal
+    # SVD of A^T Q = V S Ub^T  =>  B = Q^T A = Ub S V^T   (QR first: n x k -> k x k)
+    Qv, Rv = _cholqr2_host(Vt)
+    Ur, s, Vrt = np.linalg.svd(Rv)
+    Vv = Qv @ Ur
+    Ub = Vrt.T
+    M = _rsolve(np.eye(k), Rt) @ Ub[:, :rank]  # U = Y Rt^{-1} Ub_r
+    Mt = torch.from_numpy(np.ascontiguousarray(M)).to(dev, work)
+    U_loc = T.f32_xm(Y, Mt, store=True)[0] if work == torch.float32 else Y @ Mt
+    s = torch.from_numpy(s[:rank].copy()).to(dev, work)
+    V = torch.from_numpy(np.ascontiguousarray(Vv[:, :rank])).to(dev, work)
     if Ad is not None:
         U = DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm)
         return U, s, V
-    return U_loc, s, V.to(work) if A_loc.dtype != torch.float64 else V
+    return U_loc, s, V
+
+
+# ------------------------------------------------------- host small LA (fp64)
+def _chol_upper(G: np.ndarray):
+    """Upper Cholesky factor R (G = R^T R) or None if G is not numerically SPD."""
+    try:
+        R = np.linalg.cholesky(0.5 * (G + G.T)).T
+    except np.linalg.LinAlgError:
+        return None
+    d = np.abs(np.diag(R))
+    if d.min() <= 1e-13 * d.max():
+        return None
+    return R
+
+
+def _rsolve(X: np.ndarray, R: np.ndarray) -> np.ndarray:
+    """X R^{-1} for upper-triangular R."""
+    return solve_triangular(R, X.T, trans="T", lower=False).T
+
+
+def _cholqr2_host(W: np.ndarray):
+    """CholeskyQR2 of a small n x k fp64 matrix; Householder QR if it breaks down."""
+    R1 = _chol_upper(W.T @ W)
+    if R1 is not None:
+        Q1 = _rsolve(W, R1)
+        R2 = _chol_upper(Q1.T @ Q1)
+        if R2 is not None:
+            return _rsolve(Q1, R2), R2 @ R1
+    Q, R = np.linalg.qr(W)
+    return Q, R
+
+
+def _normalize_cols(W: np.ndarray) -> np.ndarray:
+    return W / np.maximum(np.linalg.norm(W, axis=0, keepdims=True), 1e-300)
 
 
 def _transpose(A):

@@ -88,7 +88,10 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False):
         y = torch.matmul(Ab.to(wdt), Zc)
         if A.dtype in (torch.bfloat16, torch.float16):
             yh, yl = _split_bf16(y)
-            W += (torch.matmul(Ab.t(), yh).to(wdt) + torch.matmul(Ab.t(), yl).to(wdt))
+            if A.is_cuda:
+                W += torch.mm(Ab.t(), yh, out_dtype=torch.float32) + torch.mm(Ab.t(), yl, out_dtype=torch.float32)
+            else:
+                W += Ab.t().float() @ (yh.float() + yl.float())
         else:
             W += torch.matmul(Ab.t().to(wdt), y)
         G += (y.t() @ y).double()
@@ -112,6 +115,37 @@ def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool):
               _lib.ptr(Y) if Y is not None else None, 0 if Y is None else Y.stride(0), _lib.ptr(ws),
               vp(_lib.stream_of(A)))
     return W, G.double(), Y
+
+
+_lib.register("sl_tsk_f32_xm", [vp, i64, i32, i64, vp, i32, vp, i64, vp, vp, vp])
+_lib.register("sl_tsk_f32_workspace", [i64], C.c_int64)
+_WS32 = FusedWorkspace()
+
+
+def f32_xm(Y: torch.Tensor, M: torch.Tensor | None = None, store: bool = True, gram: bool = False):
+    """``Q = Y M`` (``M=None``: ``Q = Y``) for tall f32 ``Y`` (k, k2 <= 64).
+
+    Returns ``(Q or None, G or None)`` with ``G = Q^T Q`` in float64 (partial
+    over this shard).  Native streaming kernel on GPU, torch on CPU.
+    """
+    m, k = Y.shape
+    k2 = k if M is None else M.shape[1]
+    if Y.is_cuda and Y.dtype == torch.float32 and k <= 64 and k2 <= 64 and Y.stride(1) == 1 and _lib.available():
+        Mc = None if M is None else M.to(device=Y.device, dtype=torch.float32).contiguous()
+        out = torch.empty(m, k2, dtype=torch.float32, device=Y.device) if (store and M is not None) else None
+        G = torch.empty(k2, k2, dtype=torch.float64, device=Y.device) if gram else None
+        ws = _WS32.get(Y.device, int(_lib.require().sl_tsk_f32_workspace(m))) if gram else None
+        _lib.call("sl_tsk_f32_xm", _lib.ptr(Y), m, k, Y.stride(0), _lib.ptr(Mc) if Mc is not None else None, k2,
+                  _lib.ptr(out) if out is not None else None, out.stride(0) if out is not None else 0,
+                  _lib.ptr(G) if G is not None else None, _lib.ptr(ws) if ws is not None else None,
+                  vp(_lib.stream_of(Y)))
+        return (out if M is not None else (Y if store else None)), G
+    Q = Y if M is None else Y @ M.to(Y.dtype)
+    G = None
+    if gram:
+        from ..base.linalg import gram as _g
+        G = _g(Q, None)
+    return (Q if store else None), G
 
 
 def matmul(A: torch.Tensor, Z: torch.Tensor, out_dtype=torch.float32) -> torch.Tensor:

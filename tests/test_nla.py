@@ -120,3 +120,16 @@ def test_fused_pass_gpu_bf16(dev, native):
         torch.testing.assert_close(G.double(), Gr, rtol=1e-3, atol=1e-5 * float(Gr.abs().max()))
     finally:
         tallskinny.USE_NATIVE = old
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,k2", [(1000003, 40, 20), (5000, 64, 64), (77, 5, 3)])
+def test_f32_xm_native(dev, m, k, k2):
+    Y = torch.randn(m, k, device=dev)
+    M = torch.randn(k, k2, device=dev)
+    Q, G = tallskinny.f32_xm(Y, M, store=True, gram=True)
+    Qr = Y.double() @ M.double()
+    torch.testing.assert_close(Q.double(), Qr, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(G, Qr.t() @ Qr, rtol=1e-4, atol=1e-3)
+    _, G1 = tallskinny.f32_xm(Y, None, store=False, gram=True)
+    torch.testing.assert_close(G1, Y.double().t() @ Y.double(), rtol=1e-4, atol=1e-3)
