@@ -4,12 +4,17 @@
 //                   optionally stores Q and/or accumulates G = Q^T Q (f64 out)
 //                   with M == NULL meaning Q = Y (a plain Gram pass).
 //
-// Y is only m x k floats (a few % of A's bytes) so these passes are cheap as
-// long as they stream: one workgroup of 256 threads per 64-row chunk,
-// persistent grid, Y chunk transposed into LDS, 4x4 register blocks for both
-// the small GEMM and the Gram (16 FMAs per two ds_read_b128), per-workgroup
-// Gram slabs summed by k_slab_reduce_rows in f64.  hipBLASLt's choice for
-// these (k x 1e6) x (1e6 x k) shapes was ~40x slower (profiles/).
+// Exact-f32 products on the matrix cores (v_mfma_f32_32x32x2_f32 is a k-ordered
+// fmaf chain, no reduced-precision shortcut).  One wave owns 32 rows at a time:
+//   * Q tile (32 rows x 32 cols) = sum over k-pairs of mfma(Y[r, 2s+h], M[2s+h, c])
+//     with M kept in registers for the whole kernel;
+//   * the Q tile's ACCUMULATOR registers are directly the K = 2 operands of
+//     the Gram MFMA: register `reg` of lane (h, c) holds row 4h + (reg&3) +
+//     8(reg>>2), col c — both operands of mfma(Qa[reg], Qb[reg]) pair the same
+//     two rows, so 16 MFMAs add the 32 rows' outer products with no LDS and
+//     no shuffles;
+//   * per-workgroup Gram slabs (waves summed through LDS), reduced in f64.
+// hipBLASLt's choice for these (k x 1e6) x (1e6 x k) shapes was ~40x slower.
 #include "sl_common.hpp"
 
 int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
@@ -17,97 +22,125 @@ int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride,
 
 namespace {
 
-constexpr int CH = 64;  // rows per chunk
+typedef __attribute__((ext_vector_type(16))) float f16v;
 constexpr int KMAX = 64;
+constexpr int WPB = 4;  // waves per block
 
-typedef __attribute__((ext_vector_type(4))) float f4;
+__device__ __forceinline__ int crow(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
+template <int KT2, bool IDENT, bool STORE, bool GRAM>
 __global__ void __launch_bounds__(256)
-k_f32_xm(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, const float* __restrict__ M,
-         int k2, float* __restrict__ out, int64_t ldo, float* __restrict__ Gslab) {
-  __shared__ __attribute__((aligned(16))) float Yt[KMAX][CH];      // transposed chunk
-  __shared__ __attribute__((aligned(16))) float Ms[KMAX][KMAX];
-  __shared__ __attribute__((aligned(16))) float Qs[CH][KMAX + 4];  // +4: b128-aligned, fewer conflicts
-  const int t = threadIdx.x;
-  const int rg = t >> 4, cg = t & 15;  // 4x4 block coordinates
-  const bool ident = (M == nullptr);
-  const int kq = ident ? k : k2;
-  if (!ident) {
-    for (int e = t; e < KMAX * KMAX; e += 256) {
-      const int i = e / KMAX, j = e % KMAX;
-      Ms[i][j] = (i < k && j < k2) ? M[i * k2 + j] : 0.f;
-    }
+k_f32_mfma(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, const float* __restrict__ M,
+           int k2, float* __restrict__ out, int64_t ldo, float* __restrict__ Gslab) {
+  __shared__ float gred[1][KT2 * 32][KT2 * 32 + 1];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const int kq = IDENT ? k : k2;
+
+  // M fragments: B operand of step s: M[2s + h][32 ct + c]
+  float mreg[IDENT ? 1 : KMAX / 2][KT2];
+  if constexpr (!IDENT) {
+#pragma unroll
+    for (int s = 0; s < KMAX / 2; ++s)
+#pragma unroll
+      for (int ct = 0; ct < KT2; ++ct) {
+        const int r = 2 * s + h, col = 32 * ct + c;
+        mreg[s][ct] = (r < k && col < k2) ? M[r * k2 + col] : 0.f;
+      }
   }
-  float g[4][4] = {};
-  const int64_t nchunks = (m + CH - 1) / CH;
-  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int64_t r0 = c * CH;
-    __syncthreads();
-    for (int e = t; e < CH * KMAX; e += 256) {
-      const int row = e / KMAX, col = e % KMAX;
-      float v = 0.f;
-      if (col < k && r0 + row < m) v = Y[(r0 + row) * ldy + col];
-      Yt[col][row] = v;
-    }
-    __syncthreads();
-    // ---- Q block (rows 4rg.., cols 4cg..)
-    float q[4][4] = {};
-    if (ident) {
+  f16v g[KT2][KT2];
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < KT2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) q[a][b] = Yt[4 * cg + b][4 * rg + a];
+    for (int b = 0; b < KT2; ++b) g[a][b] = f16v{};
+
+  const int64_t ngroups = (m + 31) / 32;
+  for (int64_t gi = (int64_t)blockIdx.x * WPB + w; gi < ngroups; gi += (int64_t)gridDim.x * WPB) {
+    const int64_t r0 = gi * 32;
+    f16v q[KT2];
+    if constexpr (IDENT) {
+#pragma unroll
+      for (int ct = 0; ct < KT2; ++ct)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int64_t r = r0 + crow(reg, h);
+          const int col = 32 * ct + c;
+          q[ct][reg] = (r < m && col < k) ? Y[r * ldy + col] : 0.f;
+        }
     } else {
-      for (int i = 0; i < k; ++i) {
-        const f4 y = *(const f4*)&Yt[i][4 * rg];
-        const f4 mm = *(const f4*)&Ms[i][4 * cg];
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+      for (int ct = 0; ct < KT2; ++ct) q[ct] = f16v{};
+      const int64_t r = r0 + c;
+      const float* yr = Y + (r < m ? r : 0) * ldy;
+      const bool rv = r < m;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) q[a][b] += y[a] * mm[b];
+      for (int s = 0; s < KMAX / 2; ++s) {
+        if (2 * s >= k) break;
+        const int col = 2 * s + h;
+        const float a = (rv && col < k) ? yr[col] : 0.f;
+#pragma unroll
+        for (int ct = 0; ct < KT2; ++ct)
+          q[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, mreg[s][ct], q[ct], 0, 0, 0);
       }
     }
+    if constexpr (STORE) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a) *(f4*)&Qs[4 * rg + a][4 * cg] = f4{q[a][0], q[a][1], q[a][2], q[a][3]};
-    if (out) {
+      for (int ct = 0; ct < KT2; ++ct)
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int64_t r = r0 + 4 * rg + a;
-        if (r < m)
-#pragma unroll
-          for (int b = 0; b < 4; ++b)
-            if (4 * cg + b < kq) out[r * ldo + 4 * cg + b] = q[a][b];
-      }
+        for (int reg = 0; reg < 16; ++reg) {
+          const int64_t r = r0 + crow(reg, h);
+          const int col = 32 * ct + c;
+          if (r < m && col < kq) out[r * ldo + col] = q[ct][reg];
+        }
     }
-    if (Gslab) {
+    if constexpr (GRAM) {
+#pragma unroll
+      for (int a = 0; a < KT2; ++a)
+#pragma unroll
+        for (int b = a; b < KT2; ++b)
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg)
+            g[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(q[a][reg], q[b][reg], g[a][b], 0, 0, 0);
+    }
+  }
+  if constexpr (GRAM) {
+    // wave 0..3 partial tiles -> LDS -> one slab per workgroup (KMAX x KMAX)
+    for (int v = 0; v < WPB; ++v) {
+      if (w == v) {
+#pragma unroll
+        for (int a = 0; a < KT2; ++a)
+#pragma unroll
+          for (int b = 0; b < KT2; ++b)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+              const int i = 32 * a + crow(reg, h), j = 32 * b + c;
+              const float val = (b >= a) ? g[a][b][reg] : 0.f;
+              if (v == 0) gred[0][i][j] = val;
+              else gred[0][i][j] += val;
+            }
+      }
       __syncthreads();
-      // ---- G block (rows 4rg.. of Q^T, cols 4cg..) over the chunk's rows
-      for (int r = 0; r < CH; ++r) {
-        const f4 x = *(const f4*)&Qs[r][4 * rg];
-        const f4 z = *(const f4*)&Qs[r][4 * cg];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) g[a][b] += x[a] * z[b];
-      }
+    }
+    float* gs = Gslab + (int64_t)blockIdx.x * KMAX * KMAX;
+    for (int e = threadIdx.x; e < KT2 * 32 * KT2 * 32; e += 256) {
+      const int i = e / (KT2 * 32), j = e % (KT2 * 32);
+      // symmetrise: upper tiles were accumulated, mirror into the lower part
+      const float val = (j / 32 >= i / 32) ? gred[0][i][j] : gred[0][j][i];
+      gs[i * KMAX + j] = val;
     }
   }
-  if (Gslab) {
-    float* gs = Gslab + (int64_t)blockIdx.x * KMAX * KMAX;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) gs[(4 * rg + a) * KMAX + 4 * cg + b] = g[a][b];
-  }
+}
+
+int grid_for(int64_t m) {
+  const int64_t ng = (m + 31) / 32;
+  int64_t g = (ng + WPB - 1) / WPB;
+  return (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
 }
 
 }  // namespace
 
-SL_API int64_t sl_tsk_f32_workspace(int64_t m) {
-  int64_t nch = (m + CH - 1) / CH;
-  int64_t g = nch < 1024 ? nch : 1024;
-  return g * KMAX * KMAX * 4 + 256;
-}
+SL_API int64_t sl_tsk_f32_workspace(int64_t m) { return (int64_t)grid_for(m) * KMAX * KMAX * 4 + 256; }
 
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2,
                          float* out, int64_t ldo, double* G, void* ws, void* stream) {
@@ -117,14 +150,23 @@ SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const fl
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int64_t nch = (m + CH - 1) / CH;
-  const int g = (int)(nch < 1024 ? nch : 1024);
+  const int g = grid_for(m);
   float* slab = G ? (float*)ws : nullptr;
-  k_f32_xm<<<g, 256, 0, s>>>(Y, m, k, ldy, M, k2, out, ldo, slab);
+  const int kq = M ? k2 : k;
+  const bool two = kq > 32;
+  const bool store = out != nullptr && M != nullptr;
+#define SL_F(KT2, ID, ST, GR) k_f32_mfma<KT2, ID, ST, GR><<<g, 256, 0, s>>>(Y, m, k, ldy, M, k2, out, ldo, slab)
+#define SL_F2(ID, ST, GR) { if (two) SL_F(2, ID, ST, GR); else SL_F(1, ID, ST, GR); }
+  if (!M) {
+    if (!G) return SL_OK;
+    SL_F2(true, false, true);
+  } else if (store && G) SL_F2(false, true, true)
+  else if (store) SL_F2(false, true, false)
+  else if (G) SL_F2(false, false, true)
+  else return SL_OK;
+#undef SL_F2
+#undef SL_F
   SL_LAUNCH_CHECK();
-  if (G) {
-    const int kq = M ? k2 : k;
-    return sl_slab_reduce_launch_f64(slab, g, (int64_t)KMAX * KMAX, KMAX, kq, kq, G, kq, s);
-  }
+  if (G) return sl_slab_reduce_launch_f64(slab, g, (int64_t)KMAX * KMAX, KMAX, kq, kq, G, kq, s);
   return SL_OK;
 }

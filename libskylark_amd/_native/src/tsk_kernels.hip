@@ -30,18 +30,20 @@
 //     the DMA queue), all LDS in one dynamic array;
 //   * per-workgroup W/G partial slabs, summed in f64 by a second kernel.
 #include "sl_common.hpp"
+#include <stdlib.h>
 
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int WAVES = 8;
 constexpr int THREADS = WAVES * 64;
 constexpr int BM = 16;
-constexpr int NBUF = 3;
+constexpr int NBUF_DEFAULT = 4;
 
 // hardware round-to-nearest-even (v_cvt_pk_bf16_f32), NaN-preserving, branch-free
 __device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
@@ -63,7 +65,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
       : "memory");
 }
 
-template <int NW, int KT>
+template <int NW, int KT, int NBUF>
 struct Geo {
   static constexpr int ROWB = NW * 2;                 // bytes per LDS row of a wave region
   static constexpr int NCH = NW / 8;                  // 16-B chunks per row
@@ -78,13 +80,13 @@ struct Geo {
   static constexpr int GS = (GTILES + WAVES - 1) / WAVES;  // G tiles per wave
 };
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
            float* __restrict__ Wslab, float* __restrict__ Gslab,
            float* __restrict__ Y, int64_t ldy) {
-  using GG = Geo<NW, KT>;
+  using GG = Geo<NW, KT, NBUF>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* abuf = smem;
   float* yp = (float*)(smem + GG::ABYTES);
@@ -159,14 +161,21 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     }
   };
 
+  // prefetch depth PD = NBUF - 1 blocks ahead of the one being consumed
+  constexpr int PD = NBUF - 1;
   int64_t my = 0;  // local iteration index
-  if (b0 < nblocks) issue(b0, 0);
-  if (b0 + bstep < nblocks) issue(b0 + bstep, 1);
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (b0 + p * bstep < nblocks) issue(b0 + p * bstep, p);
 
   for (int64_t blk = b0; blk < nblocks; blk += bstep, ++my) {
     const int buf = (int)(my % NBUF);
-    const bool more = blk + bstep < nblocks;
-    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
+    // blocks issued after this one and still possibly in flight: min(PD-1, remaining)
+    const int64_t rem = (nblocks - 1 - blk) / bstep;
+    const int younger = (int)(rem < PD - 1 ? rem : PD - 1);
+    if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GG::LPB) : "memory");
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GG::LPB) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const char* region = abuf + (buf * WAVES + w) * GG::REGION;
 
@@ -186,82 +195,104 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         if constexpr (ZSPLIT) accY[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zl[ks][t], accY[t], 0, 0, 0);
       }
     }
-    // ---- step 2: cross-wave reduction of y through LDS
+    // ---- step 2: cross-wave reduction of y through LDS.  Partials are stored
+    //      column-major ([wave][col][16 rows]) so that every access is b128:
+    //      a lane's C fragment is 4 consecutive rows of one column.
+    const int g4 = lane >> 4, i16 = lane & 15;
 #pragma unroll
     for (int t = 0; t < KT; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        yp[(w * BM + (lane >> 4) * 4 + j) * GG::KP + 16 * t + (lane & 15)] = accY[t][j];
+      *(f32x4*)&yp[((w * GG::KP) + 16 * t + i16) * BM + 4 * g4] = accY[t];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     {
+      constexpr int CPW = GG::KP / WAVES;  // columns reduced per wave
       const int64_t r0 = blk * BM;
-      for (int idx = lane; idx < 2 * GG::KP; idx += 64) {
-        const int row = 2 * w + idx / GG::KP;
-        const int col = idx % GG::KP;
-        float s = 0.f;
+      if (lane < CPW * 4) {
+        const int col = w * CPW + (lane >> 2), rg = lane & 3;
+        f32x4 sum = *(const f32x4*)&yp[col * BM + 4 * rg];
 #pragma unroll
-        for (int v = 0; v < WAVES; ++v) s += yp[(v * BM + row) * GG::KP + col];
-        if (r0 + row >= m) s = 0.f;
-        yf[row * GG::KP + col] = s;
+        for (int v = 1; v < WAVES; ++v) sum += *(const f32x4*)&yp[(v * GG::KP + col) * BM + 4 * rg];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (r0 + 4 * rg + j >= m) sum[j] = 0.f;
+        *(f32x4*)&yf[col * BM + 4 * rg] = sum;
         if constexpr (STORE_Y) {
-          if (r0 + row < m && col < k) Y[(r0 + row) * ldy + col] = s;
+          if (col < k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (r0 + 4 * rg + j < m) Y[(r0 + 4 * rg + j) * ldy + col] = sum[j];
         }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
 
-    // prefetch two blocks ahead into the buffer consumed two iterations ago
-    if (blk + 2 * bstep < nblocks) issue(blk + 2 * bstep, (int)((my + 2) % NBUF));
+    // prefetch PD blocks ahead into the buffer this wave consumed last iteration
+    if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
 
-    if constexpr (DO_W || DO_G) {
-      // ---- y fragments (rows 4(l>>4)+j, col 16t+(l&15)), bf16 hi/lo
+    if constexpr (DO_W) {
+      // ---- step 3: W_w += A_w^T (y_hi + y_lo) with ONE K=32 MFMA per tile:
+      //      k = 0..15 -> A rows 0..15 against y_hi, k = 16..31 -> the same A
+      //      rows against y_lo.  A^T fragments = two transposed LDS reads
+      //      (ds_read_b64_tr_b16) of the same swizzled image.
+      bf16x8 yk[KT];
+      const int rb = 8 * (g4 & 1);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const f32x4 v0 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb];
+        const f32x4 v1 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb + 4];
+        s16x8 e;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const short h0 = bf16_bits(v0[j]), h1 = bf16_bits(v1[j]);
+          e[j] = g4 < 2 ? h0 : bf16_bits(v0[j] - bf16_val(h0));
+          e[4 + j] = g4 < 2 ? h1 : bf16_bits(v1[j] - bf16_val(h1));
+        }
+        yk[t] = __builtin_bit_cast(bf16x8, e);
+      }
+      const int q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+      for (int ct = 0; ct < NW / 16; ++ct) {
+        const int chunk = 2 * ct + (p >> 1);
+        const int ra = rb + q, rc = rb + 4 + q;
+        const char* a0 = region + ra * GG::ROWB + (chunk ^ (ra & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+        const char* a1 = region + rc * GG::ROWB + (chunk ^ (rc & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+        const s16x4 f0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a0);
+        const s16x4 f1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a1);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(f0, f1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+          accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, yk[t], accW[ct][t], 0, 0, 0);
+      }
+    }
+    if constexpr (DO_G) {
+      // ---- step 4: G tiles tau = w + 8 s (t1 = tau / KT, t2 = tau % KT),
+      //      hi*hi + hi*lo + lo*hi with K=16 fragments (rows 4(l>>4)+j)
       s16x4 yh[KT], yl[KT];
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
+        const f32x4 v = *(const f32x4*)&yf[(16 * t + i16) * BM + 4 * g4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float v = yf[((lane >> 4) * 4 + j) * GG::KP + 16 * t + (lane & 15)];
-          const short h = bf16_bits(v);
+          const short h = bf16_bits(v[j]);
           yh[t][j] = h;
-          yl[t][j] = bf16_bits(v - bf16_val(h));
+          yl[t][j] = bf16_bits(v[j] - bf16_val(h));
         }
       }
-      if constexpr (DO_W) {
-        // ---- step 3: W_w += A_w^T y   (transposed LDS reads of the same image)
-        const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-        const int row = 4 * g + q;
 #pragma unroll
-        for (int ct = 0; ct < NW / 16; ++ct) {
-          const int chunk = 2 * ct + (p >> 1);
-          const int slot = chunk ^ (row & (GG::NCH - 1));
-          const char* addr = region + row * GG::ROWB + slot * 16 + (p & 1) * 8;
-          const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
+      for (int s = 0; s < GG::GS; ++s) {
+        const int tau = w + WAVES * s;
+        if (tau < GG::GTILES) {
+          const int t1 = tau / KT, t2 = tau % KT;
+          s16x4 ah = yh[0], al = yl[0], bh = yh[0], bl = yl[0];
 #pragma unroll
-          for (int t = 0; t < KT; ++t) {
-            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);
-            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0);
+          for (int t = 1; t < KT; ++t) {
+            if (t1 == t) { ah = yh[t]; al = yl[t]; }
+            if (t2 == t) { bh = yh[t]; bl = yl[t]; }
           }
-        }
-      }
-      if constexpr (DO_G) {
-        // ---- step 4: G tiles tau = w + 8 s  (t1 = tau / KT, t2 = tau % KT)
-#pragma unroll
-        for (int s = 0; s < GG::GS; ++s) {
-          const int tau = w + WAVES * s;
-          if (tau < GG::GTILES) {
-            const int t1 = tau / KT, t2 = tau % KT;
-            s16x4 ah = yh[0], al = yl[0], bh = yh[0], bl = yl[0];
-#pragma unroll
-            for (int t = 1; t < KT; ++t) {
-              if (t1 == t) { ah = yh[t]; al = yl[t]; }
-              if (t2 == t) { bh = yh[t]; bl = yl[t]; }
-            }
-            accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, accG[s], 0, 0, 0);
-            accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, accG[s], 0, 0, 0);
-            accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, accG[s], 0, 0, 0);
-          }
+          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, accG[s], 0, 0, 0);
+          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, accG[s], 0, 0, 0);
+          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, accG[s], 0, 0, 0);
         }
       }
     }
@@ -344,11 +375,11 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF>
 int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
-  using GG = Geo<NW, KT>;
-  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT>;
+  using GG = Geo<NW, KT, NBUF>;
+  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF>;
   static bool attr = false;
   if (!attr) {
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
@@ -359,7 +390,40 @@ int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int
   return SL_OK;
 }
 
+// buffer depth: SL_TSK_NBUF env (A/B tuning), default NBUF_DEFAULT, clamped to the LDS budget
+int g_nbuf = -1;
+int nbuf_request() {
+  int& nb = g_nbuf;
+  if (nb < 0) {
+    const char* e = getenv("SL_TSK_NBUF");
+    nb = e ? atoi(e) : NBUF_DEFAULT;
+    if (nb < 2) nb = 2;
+    if (nb > 5) nb = 5;
+  }
+  return nb;
+}
+
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT>
+int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
+              float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
+  int nb = nbuf_request();
+  constexpr int LIM = 160 * 1024;
+  if (nb >= 5 && Geo<NW, KT, 5>::LDS <= LIM)
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 5>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  if (nb >= 4 && Geo<NW, KT, 4>::LDS <= LIM)
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 4>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  if (nb >= 3)
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 3>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 2>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+}
+
 }  // namespace
+
+// tuning hook: LDS-DMA ring depth (2..5) for subsequent launches
+SL_API int sl_tsk_set_nbuf(int nb) {
+  g_nbuf = nb < 2 ? 2 : (nb > 5 ? 5 : nb);
+  return SL_OK;
+}
 
 // workspace bytes needed by sl_tsk_fused_pass
 SL_API int64_t sl_tsk_fused_workspace(int64_t m, int64_t n, int k) {
@@ -388,8 +452,8 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
 #define SL_TSK(NW, KTT)                                                                              \
-  rc = Y ? launch<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
-         : launch<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
+  rc = Y ? launch_nb<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+         : launch_nb<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
   if (small) {
     switch (KT) { case 1: SL_TSK(64, 1); break; case 2: SL_TSK(64, 2); break; case 3: SL_TSK(64, 3); break; default: SL_TSK(64, 4); }
   } else {
@@ -416,8 +480,8 @@ SL_API int sl_tsk_matmul(const void* A, int64_t m, int64_t n, int64_t lda, const
   const bf16_t* z = (const bf16_t*)Zt;
   int rc = SL_ERR_UNSUPPORTED;
 #define SL_MM(NW, KTT)                                                                                      \
-  rc = zsplit ? launch<NW, KTT, false, false, true, true>(a, m, (int)n, lda, z, k, nullptr, nullptr, Y, ldy, s) \
-              : launch<NW, KTT, false, false, true, false>(a, m, (int)n, lda, z, k, nullptr, nullptr, Y, ldy, s)
+  rc = zsplit ? launch_nb<NW, KTT, false, false, true, true>(a, m, (int)n, lda, z, k, nullptr, nullptr, Y, ldy, s) \
+              : launch_nb<NW, KTT, false, false, true, false>(a, m, (int)n, lda, z, k, nullptr, nullptr, Y, ldy, s)
   if (n <= 512) {
     switch (KT) { case 1: SL_MM(64, 1); break; case 2: SL_MM(64, 2); break; case 3: SL_MM(64, 3); break; default: SL_MM(64, 4); }
   } else {

@@ -32,6 +32,7 @@ from ..base.context import Context
 from ..base.exceptions import InvalidParametersError
 from ..parallel.comm import Comm
 from ..parallel.distmatrix import DistMatrix
+from ..utils.timer import PROFILER
 
 
 @dataclass
@@ -124,30 +125,36 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
     from ..ops import tallskinny as T
 
-    Zh = _sketch_operator(params.sketch, n, k, ctx, "cpu", torch.float64).numpy()
+    prof = PROFILER
+    with prof.phase("svd.sketch"):
+        Zh = _sketch_operator(params.sketch, n, k, ctx, "cpu", torch.float64).numpy()
     q = max(0, int(params.num_iterations))
-    Y = W = None
+    Y = W = G = None
     for it in range(q + 1):
         last = it == q
-        Wd, Gd, Y = T.fused_pass(A_loc, torch.from_numpy(Zh).to(dev, work), keep_y=last)
-        if not last:
-            # orth(A^T Q) = orth(A^T A Z): the column space of W = A^T (A Z)
-            # (R^{-1} only re-mixes columns), so only W crosses the network.
-            Wd = Wd.double().contiguous()
-            comm.all_reduce(Wd)
-            Wh = Wd.cpu().numpy()
-            R = _chol_upper(Gd.double().cpu().numpy()) if comm.size == 1 else None
-            if R is not None:  # better conditioned: orth(W R^{-1})
-                Wh = _rsolve(Wh, R)
+        with prof.phase("svd.fused_pass"):
+            Wd, Gd, Y = T.fused_pass(A_loc, torch.from_numpy(Zh).to(dev, work), keep_y=last)
+        with prof.phase("svd.allreduce_small"):
+            WG = torch.cat([Wd.double(), Gd.double()], 0)
+            comm.all_reduce(WG)
+            WGh = WG.cpu().numpy()
+        W, G = WGh[:n], WGh[n:]
+        if last:
+            break
+        with prof.phase("svd.host_orth"):
+            # orth(A^T Q) = orth(W R^{-1}) = orth(W): R^{-1} only re-mixes columns;
+            # applying it first just improves the conditioning of the QR.
+            R = _chol_upper(G)
+            Wh = _rsolve(W, R) if R is not None else W
             Zh = _normalize_cols(Wh) if params.skip_qr else _cholqr2_host(Wh)[0]
-            continue
-        Wd = Wd.double().contiguous()
-        comm.all_reduce(Wd)
-        W = Wd.cpu().numpy()  # A^T Y  (n x k)
-    # ---- final basis Q = Y R^{-1}, R from CholeskyQR2 of the stored Y (f32)
-    _, G1 = T.f32_xm(Y, None, store=False, gram=True) if work == torch.float32 else (None, L.gram(Y, None))
-    comm.all_reduce(G1)
-    R1 = _chol_upper(G1.cpu().numpy())
+    # ---- final basis Q = Y Rt^{-1}: CholeskyQR2 on the stored Y, first factor
+    #      from the pass's own Gram (no extra read), refinement Gram(s) exact f32.
+    with prof.phase("svd.final_qr"):
+        R1 = _chol_upper(G)
+        if R1 is None:
+            _, G1 = T.f32_xm(Y, None, store=False, gram=True) if work == torch.float32 else (None, L.gram(Y, None))
+            comm.all_reduce(G1)
+            R1 = _chol_upper(G1.cpu().numpy())
     if R1 is None:
         # rank-deficient / ill-conditioned sample (e.g. repeated FJLT samples):
         # Householder TSQR gives an orthonormal Q regardless; one extra pass
@@ -164,24 +171,32 @@ def approximate_svd(A, rank: int, context: Context | None = None,
         if Ad is not None:
             return DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm), s, V
         return U_loc, s, V
-    else:
-        R1inv = _rsolve(np.eye(k), R1)
-        if work == torch.float32:
-            _, G2 = T.f32_xm(Y, torch.from_numpy(R1inv).float().to(dev), store=False, gram=True)
-        else:
-            G2 = L.gram(Y @ torch.from_numpy(R1inv).to(dev, work), None)
-        comm.all_reduce(G2)
-        R2 = _chol_upper(G2.cpu().numpy())
-        Rt = R1 if R2 is None else R2 @ R1
-    Vt = _rsolve(W, Rt)  # = A^T Q  (n x k), Q = Y Rt^{-1} orthonormal
-    # SVD of A^T Q = V S Ub^T  =>  B = Q^T A = Ub S V^T   (QR first: n x k -> k x k)
-    Qv, Rv = _cholqr2_host(Vt)
-    Ur, s, Vrt = np.linalg.svd(Rv)
-    Vv = Qv @ Ur
-    Ub = Vrt.T
-    M = _rsolve(np.eye(k), Rt) @ Ub[:, :rank]  # U = Y Rt^{-1} Ub_r
-    Mt = torch.from_numpy(np.ascontiguousarray(M)).to(dev, work)
-    U_loc = T.f32_xm(Y, Mt, store=True)[0] if work == torch.float32 else Y @ Mt
+    Rt = R1
+    with prof.phase("svd.final_qr"):
+        for _ in range(2):  # CholeskyQR2, a third step only if still far from orthonormal
+            Rinv = _rsolve(np.eye(k), Rt)
+            if work == torch.float32:
+                _, G2 = T.f32_xm(Y, torch.from_numpy(Rinv).float().to(dev), store=False, gram=True)
+            else:
+                G2 = L.gram(Y @ torch.from_numpy(Rinv).to(dev, work), None)
+            comm.all_reduce(G2)
+            R2 = _chol_upper(G2.cpu().numpy())
+            if R2 is None:
+                break
+            Rt = R2 @ Rt
+            if np.abs(R2 - np.eye(k)).max() < 1e-3:
+                break
+    with prof.phase("svd.small_svd"):
+        Vt = _rsolve(W, Rt)  # = A^T Q  (n x k), Q = Y Rt^{-1} orthonormal
+        # SVD of A^T Q = V S Ub^T  =>  B = Q^T A = Ub S V^T   (QR first: n x k -> k x k)
+        Qv, Rv = _cholqr2_host(Vt)
+        Ur, s, Vrt = np.linalg.svd(Rv)
+        Vv = Qv @ Ur
+        Ub = Vrt.T
+        M = _rsolve(np.eye(k), Rt) @ Ub[:, :rank]  # U = Y Rt^{-1} Ub_r
+        Mt = torch.from_numpy(np.ascontiguousarray(M)).to(dev, work)
+    with prof.phase("svd.form_U"):
+        U_loc = T.f32_xm(Y, Mt, store=True)[0] if work == torch.float32 else Y @ Mt
     s = torch.from_numpy(s[:rank].copy()).to(dev, work)
     V = torch.from_numpy(np.ascontiguousarray(Vv[:, :rank])).to(dev, work)
     if Ad is not None:
