@@ -44,6 +44,8 @@ constexpr int WAVES = 8;
 constexpr int THREADS = WAVES * 64;
 constexpr int BM = 16;
 constexpr int NBUF_DEFAULT = 4;
+int g_flags = 0;   // per-call mode bits (8: no Gram, 32: y_hi only)
+int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, bit3 step 4
 
 // hardware round-to-nearest-even (v_cvt_pk_bf16_f32), NaN-preserving, branch-free
 __device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
@@ -85,7 +87,7 @@ __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
            float* __restrict__ Wslab, float* __restrict__ Gslab,
-           float* __restrict__ Y, int64_t ldy) {
+           float* __restrict__ Y, int64_t ldy, int ab) {
   using GG = Geo<NW, KT, NBUF>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* abuf = smem;
@@ -185,6 +187,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     for (int t = 0; t < KT; ++t) accY[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NW / 32; ++ks) {
+      if (ab & 1) break;  // ablation (tuning only)
       const int row = lane & 15;
       const int chunk = (lane >> 4) + 4 * ks;
       const int slot = chunk ^ (row & (GG::NCH - 1));
@@ -199,6 +202,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     //      column-major ([wave][col][16 rows]) so that every access is b128:
     //      a lane's C fragment is 4 consecutive rows of one column.
     const int g4 = lane >> 4, i16 = lane & 15;
+    if (!(ab & 2)) {
 #pragma unroll
     for (int t = 0; t < KT; ++t)
       *(f32x4*)&yp[((w * GG::KP) + 16 * t + i16) * BM + 4 * g4] = accY[t];
@@ -226,59 +230,78 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    }
 
     // prefetch PD blocks ahead into the buffer this wave consumed last iteration
     if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
 
-    if constexpr (DO_W) {
-      // ---- step 3: W_w += A_w^T (y_hi + y_lo) with ONE K=32 MFMA per tile:
-      //      k = 0..15 -> A rows 0..15 against y_hi, k = 16..31 -> the same A
-      //      rows against y_lo.  A^T fragments = two transposed LDS reads
-      //      (ds_read_b64_tr_b16) of the same swizzled image.
-      bf16x8 yk[KT];
-      const int rb = 8 * (g4 & 1);
+    // y fragments with rows 4(l>>4)+j of column 16t+(l&15) (K=16 MFMA layout), hi/lo
+    const bool hi_only = (ab & 32) != 0;
+    const bool need_g = DO_G && !(ab & 8);
+    s16x4 yh[KT], yl[KT];
 #pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const f32x4 v0 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb];
-        const f32x4 v1 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb + 4];
-        s16x8 e;
+    for (int t = 0; t < KT; ++t) {
+      const f32x4 v = *(const f32x4*)&yf[(16 * t + i16) * BM + 4 * g4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const short h0 = bf16_bits(v0[j]), h1 = bf16_bits(v1[j]);
-          e[j] = g4 < 2 ? h0 : bf16_bits(v0[j] - bf16_val(h0));
-          e[4 + j] = g4 < 2 ? h1 : bf16_bits(v1[j] - bf16_val(h1));
-        }
-        yk[t] = __builtin_bit_cast(bf16x8, e);
-      }
-      const int q = i16 >> 2, p = i16 & 3;
-#pragma unroll
-      for (int ct = 0; ct < NW / 16; ++ct) {
-        const int chunk = 2 * ct + (p >> 1);
-        const int ra = rb + q, rc = rb + 4 + q;
-        const char* a0 = region + ra * GG::ROWB + (chunk ^ (ra & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-        const char* a1 = region + rc * GG::ROWB + (chunk ^ (rc & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-        const s16x4 f0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a0);
-        const s16x4 f1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a1);
-        const bf16x8 af = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(f0, f1, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-        for (int t = 0; t < KT; ++t)
-          accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, yk[t], accW[ct][t], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        const short h = bf16_bits(v[j]);
+        yh[t][j] = h;
+        yl[t][j] = bf16_bits(v[j] - bf16_val(h));
       }
     }
-    if constexpr (DO_G) {
-      // ---- step 4: G tiles tau = w + 8 s (t1 = tau / KT, t2 = tau % KT),
-      //      hi*hi + hi*lo + lo*hi with K=16 fragments (rows 4(l>>4)+j)
-      s16x4 yh[KT], yl[KT];
+    if (DO_W && !(ab & 4)) {
+      const int q = i16 >> 2, p = i16 & 3;
+      if (!(ab & 16) || hi_only) {
+        // ---- step 3 (K=16 form): one transposed read per 16-column tile,
+        //      W += A^T y_hi (+ A^T y_lo)
+        const int row = 4 * g4 + q;
 #pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const f32x4 v = *(const f32x4*)&yf[(16 * t + i16) * BM + 4 * g4];
+        for (int ct = 0; ct < NW / 16; ++ct) {
+          const int chunk = 2 * ct + (p >> 1);
+          const char* addr = region + row * GG::ROWB + (chunk ^ (row & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const short h = bf16_bits(v[j]);
-          yh[t][j] = h;
-          yl[t][j] = bf16_bits(v[j] - bf16_val(h));
+          for (int t = 0; t < KT; ++t) {
+            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);
+            if (!hi_only) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0);
+          }
+        }
+      } else {
+        // ---- step 3 (K=32 form): ONE MFMA per tile over [y_hi; y_lo]:
+        //      k = 0..15 -> A rows 0..15 x y_hi, k = 16..31 -> same rows x y_lo
+        bf16x8 yk[KT];
+        const int rb = 8 * (g4 & 1);
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const f32x4 v0 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb];
+          const f32x4 v1 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb + 4];
+          s16x8 e;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const short h0 = bf16_bits(v0[j]), h1 = bf16_bits(v1[j]);
+            e[j] = g4 < 2 ? h0 : bf16_bits(v0[j] - bf16_val(h0));
+            e[4 + j] = g4 < 2 ? h1 : bf16_bits(v1[j] - bf16_val(h1));
+          }
+          yk[t] = __builtin_bit_cast(bf16x8, e);
+        }
+#pragma unroll
+        for (int ct = 0; ct < NW / 16; ++ct) {
+          const int chunk = 2 * ct + (p >> 1);
+          const int ra = rb + q, rc = rb + 4 + q;
+          const char* a0 = region + ra * GG::ROWB + (chunk ^ (ra & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const char* a1 = region + rc * GG::ROWB + (chunk ^ (rc & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const s16x4 f0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a0);
+          const s16x4 f1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a1);
+          const bf16x8 af = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(f0, f1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int t = 0; t < KT; ++t)
+            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, yk[t], accW[ct][t], 0, 0, 0);
         }
       }
+    }
+    if (need_g) {
+      // ---- step 4: G tiles tau = w + 8 s (t1 = tau / KT, t2 = tau % KT):
+      //      hi*hi + hi*lo + lo*hi
 #pragma unroll
       for (int s = 0; s < GG::GS; ++s) {
         const int tau = w + WAVES * s;
@@ -385,13 +408,14 @@ int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
     attr = true;
   }
-  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy);
+  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, g_ablate | g_flags);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
 // buffer depth: SL_TSK_NBUF env (A/B tuning), default NBUF_DEFAULT, clamped to the LDS budget
 int g_nbuf = -1;
+
 int nbuf_request() {
   int& nb = g_nbuf;
   if (nb < 0) {
@@ -419,6 +443,11 @@ int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, 
 
 }  // namespace
 
+SL_API int sl_tsk_set_ablate(int ab) {
+  g_ablate = ab;
+  return SL_OK;
+}
+
 // tuning hook: LDS-DMA ring depth (2..5) for subsequent launches
 SL_API int sl_tsk_set_nbuf(int nb) {
   g_nbuf = nb < 2 ? 2 : (nb > 5 ? 5 : nb);
@@ -433,8 +462,11 @@ SL_API int64_t sl_tsk_fused_workspace(int64_t m, int64_t n, int k) {
   return g * (int64_t)NWP * KP * 4 + g * (int64_t)KP * KP * 4 + 256;
 }
 
+// flags: bit0 (1) skip the Gram G (G left untouched), bit1 (2) W from y_hi only
+// (bf16-rounded y: for intermediate power iterations, whose W is only
+// orthonormalised).  Default 0 = exact-f32-equivalent W and G.
 SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k,
-                             float* W, float* G, float* Y, int64_t ldy, void* ws, void* stream) {
+                             float* W, float* G, float* Y, int64_t ldy, void* ws, int flags, void* stream) {
   if (m <= 0) return SL_OK;
   if (n % 8 || lda % 8 || n > 1024 || k > 64 || k < 1 || n < 8) {
     sl_set_last_error("tsk_fused_pass: needs n%8==0, lda%8==0, 8<=n<=1024, 1<=k<=64");
@@ -451,6 +483,7 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   int rc = SL_ERR_UNSUPPORTED;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
+  g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0);
 #define SL_TSK(NW, KTT)                                                                              \
   rc = Y ? launch_nb<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
          : launch_nb<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
@@ -460,9 +493,10 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
     switch (KT) { case 1: SL_TSK(128, 1); break; case 2: SL_TSK(128, 2); break; case 3: SL_TSK(128, 3); break; default: SL_TSK(128, 4); }
   }
 #undef SL_TSK
+  g_flags = 0;
   if (rc != SL_OK) return rc;
   rc = sl_slab_reduce_launch(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k, s);
-  if (rc != SL_OK) return rc;
+  if (rc != SL_OK || (flags & 1)) return rc;
   return sl_slab_reduce_launch(Gslab, g, (int64_t)KP * KP, KP, k, k, G, k, s);
 }
 

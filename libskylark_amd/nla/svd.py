@@ -133,20 +133,19 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     for it in range(q + 1):
         last = it == q
         with prof.phase("svd.fused_pass"):
-            Wd, Gd, Y = T.fused_pass(A_loc, torch.from_numpy(Zh).to(dev, work), keep_y=last)
+            # intermediate passes only need orth(A^T A Z): no Gram, bf16 y for W
+            Wd, Gd, Y = T.fused_pass(A_loc, torch.from_numpy(Zh).to(dev, work), keep_y=last,
+                                     gram=last, exact=last)
         with prof.phase("svd.allreduce_small"):
-            WG = torch.cat([Wd.double(), Gd.double()], 0)
+            WG = torch.cat([Wd.double(), Gd.double()], 0) if last else Wd.double().contiguous()
             comm.all_reduce(WG)
             WGh = WG.cpu().numpy()
-        W, G = WGh[:n], WGh[n:]
+        W, G = WGh[:n], (WGh[n:] if last else None)
         if last:
             break
         with prof.phase("svd.host_orth"):
-            # orth(A^T Q) = orth(W R^{-1}) = orth(W): R^{-1} only re-mixes columns;
-            # applying it first just improves the conditioning of the QR.
-            R = _chol_upper(G)
-            Wh = _rsolve(W, R) if R is not None else W
-            Zh = _normalize_cols(Wh) if params.skip_qr else _cholqr2_host(Wh)[0]
+            # orth(A^T Q) = orth(W R^{-1}) = orth(W): R^{-1} only re-mixes columns
+            Zh = _normalize_cols(W) if params.skip_qr else _cholqr2_host(W)[0]
     # ---- final basis Q = Y Rt^{-1}: CholeskyQR2 on the stored Y, first factor
     #      from the pass's own Gram (no extra read), refinement Gram(s) exact f32.
     with prof.phase("svd.final_qr"):

@@ -21,7 +21,7 @@ import torch
 from . import _lib
 
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
-_lib.register("sl_tsk_fused_pass", [vp, i64, i64, i64, vp, i32, vp, vp, vp, i64, vp, vp])
+_lib.register("sl_tsk_fused_pass", [vp, i64, i64, i64, vp, i32, vp, vp, vp, i64, vp, i32, vp])
 _lib.register("sl_tsk_fused_workspace", [i64, i64, i32], C.c_int64)
 _lib.register("sl_tsk_matmul", [vp, i64, i64, i64, vp, i32, vp, i64, i32, vp])
 
@@ -66,16 +66,20 @@ class FusedWorkspace:
 _WS = FusedWorkspace()
 
 
-def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False):
+def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: bool = True,
+               exact: bool = True):
     """Return ``(W, G, Y)`` with ``Y = A Z``, ``W = A^T Y`` (n x k), ``G = Y^T Y`` (k x k).
 
     W and G are float32 (A bf16/fp32) or float64 (A fp64); Y is float32/64 or
     None.  Partial over this shard only — the caller all-reduces W and G.
+    ``gram=False`` skips G (returns None); ``exact=False`` lets the native
+    kernel form W from bf16-rounded y (intermediate power iterations only
+    orthonormalise W, so a 2^-9 relative perturbation is harmless there).
     """
     m, n = A.shape
     k = Z.shape[1]
     if _native_ok(A, k):
-        return _fused_native(A, Z, keep_y)
+        return _fused_native(A, Z, keep_y, gram, exact)
     wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
     # low-precision A: Z is rounded to A's dtype (as the MFMA kernel does) and
     # the products are formed in f32
@@ -101,7 +105,7 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False):
     return W, G, Y
 
 
-def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool):
+def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool, gram: bool = True, exact: bool = True):
     m, n = A.shape
     k = Z.shape[1]
     dev = A.device
@@ -113,8 +117,8 @@ def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool):
     ws = _WS.get(dev, max(nbytes, 16))
     _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zb), k, _lib.ptr(W), _lib.ptr(G),
               _lib.ptr(Y) if Y is not None else None, 0 if Y is None else Y.stride(0), _lib.ptr(ws),
-              vp(_lib.stream_of(A)))
-    return W, G.double(), Y
+              (0 if gram else 1) | (0 if exact else 2), vp(_lib.stream_of(A)))
+    return W, (G.double() if gram else None), Y
 
 
 _lib.register("sl_tsk_f32_xm", [vp, i64, i32, i64, vp, i32, vp, i64, vp, vp, vp])
