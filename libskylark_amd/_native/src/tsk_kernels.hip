@@ -251,51 +251,19 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     }
     if (DO_W && !(ab & 4)) {
       const int q = i16 >> 2, p = i16 & 3;
-      if (!(ab & 16) || hi_only) {
-        // ---- step 3 (K=16 form): one transposed read per 16-column tile,
-        //      W += A^T y_hi (+ A^T y_lo)
-        const int row = 4 * g4 + q;
+      // ---- step 3: one transposed LDS read per 16-column tile of A,
+      //      W += A^T y_hi (+ A^T y_lo).  (A single K=32 MFMA over [y_hi; y_lo]
+      //      needs two transposed reads per tile and measured 15% slower.)
+      const int row = 4 * g4 + q;
 #pragma unroll
-        for (int ct = 0; ct < NW / 16; ++ct) {
-          const int chunk = 2 * ct + (p >> 1);
-          const char* addr = region + row * GG::ROWB + (chunk ^ (row & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-          const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
-#pragma unroll
-          for (int t = 0; t < KT; ++t) {
-            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);
-            if (!hi_only) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0);
-          }
-        }
-      } else {
-        // ---- step 3 (K=32 form): ONE MFMA per tile over [y_hi; y_lo]:
-        //      k = 0..15 -> A rows 0..15 x y_hi, k = 16..31 -> same rows x y_lo
-        bf16x8 yk[KT];
-        const int rb = 8 * (g4 & 1);
+      for (int ct = 0; ct < NW / 16; ++ct) {
+        const int chunk = 2 * ct + (p >> 1);
+        const char* addr = region + row * GG::ROWB + (chunk ^ (row & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+        const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
 #pragma unroll
         for (int t = 0; t < KT; ++t) {
-          const f32x4 v0 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb];
-          const f32x4 v1 = *(const f32x4*)&yf[(16 * t + i16) * BM + rb + 4];
-          s16x8 e;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const short h0 = bf16_bits(v0[j]), h1 = bf16_bits(v1[j]);
-            e[j] = g4 < 2 ? h0 : bf16_bits(v0[j] - bf16_val(h0));
-            e[4 + j] = g4 < 2 ? h1 : bf16_bits(v1[j] - bf16_val(h1));
-          }
-          yk[t] = __builtin_bit_cast(bf16x8, e);
-        }
-#pragma unroll
-        for (int ct = 0; ct < NW / 16; ++ct) {
-          const int chunk = 2 * ct + (p >> 1);
-          const int ra = rb + q, rc = rb + 4 + q;
-          const char* a0 = region + ra * GG::ROWB + (chunk ^ (ra & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-          const char* a1 = region + rc * GG::ROWB + (chunk ^ (rc & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-          const s16x4 f0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a0);
-          const s16x4 f1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)a1);
-          const bf16x8 af = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(f0, f1, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-          for (int t = 0; t < KT; ++t)
-            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, yk[t], accW[ct][t], 0, 0, 0);
+          accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);
+          if (!hi_only) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0);
         }
       }
     }
