@@ -113,6 +113,11 @@ def main(argv=None):
             "native_fused_pass": bool(tallskinny._native_ok(A_loc, 2 * a.rank)),
         }
         print(json.dumps(out))
+        from libskylark_amd.utils.timer import PROFILER
+        if PROFILER.enabled:
+            for name, r in PROFILER.report().items():
+                print(f"[profile] {name}: {r['avg_s'] * 1e3 / max(1, a.steps + a.warmup):.3f} ms/step "
+                      f"({r['calls']} calls)", file=sys.stderr)
     if N > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -1,0 +1,110 @@
+// Small dense factorisations that stay on the GPU (k <= 64): no host round
+// trip inside power / Krylov iterations.
+//
+//   sl_small_chol_inv: G (k x k, f64, SPD) -> R upper (G = R^T R), R^{-1} (f64)
+//                      and an f32 copy of R^{-1}; status[0] |= 1 when a pivot
+//                      is not positive (the pivot is then replaced by a large
+//                      value, which zeroes that direction, and the caller
+//                      re-runs the robust host path after checking status).
+//   sl_small_matmul:   C = A B for small f64 matrices (one workgroup).
+//
+// One workgroup of 256 threads, matrices in LDS, right-looking Cholesky with
+// one barrier per column, column-parallel back substitution for R^{-1}.
+// Reference counterpart: El::Cholesky / El::Trsm on [*,*] matrices inside
+// nla/svd.hpp and ml/krr.hpp.
+#include "sl_common.hpp"
+
+namespace {
+constexpr int KM = 64;
+
+__global__ void __launch_bounds__(256)
+k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R, double* __restrict__ Rinv,
+                 float* __restrict__ Rinv32, int* __restrict__ status) {
+  __shared__ double a[KM][KM + 1];
+  __shared__ double x[KM][KM + 1];
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  for (int e = t; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    a[i][j] = 0.5 * (G[i * ldg + j] + G[j * ldg + i]);
+  }
+  __syncthreads();
+  double dmax = 0.0;
+  for (int i = 0; i < k; ++i) dmax = fmax(dmax, fabs(a[i][i]));
+  // right-looking Cholesky: a becomes L (lower) in place
+  for (int j = 0; j < k; ++j) {
+    if (t == 0) {
+      double d = a[j][j];
+      if (!(d > 1e-14 * dmax)) {  // also catches NaN
+        bad = 1;
+        d = 1e300;  // kill this direction
+      }
+      a[j][j] = sqrt(d);
+    }
+    __syncthreads();
+    const double piv = a[j][j];
+    for (int i = j + 1 + t; i < k; i += 256) a[i][j] /= piv;
+    __syncthreads();
+    // trailing update a[i][c] -= a[i][j] a[c][j], c <= i, i,c > j
+    const int rem = k - j - 1;
+    for (int e = t; e < rem * rem; e += 256) {
+      const int i = j + 1 + e / rem, c = j + 1 + e % rem;
+      if (c <= i) a[i][c] -= a[i][j] * a[c][j];
+    }
+    __syncthreads();
+  }
+  // R = L^T ;  X = R^{-1} (upper) by back substitution, one column per thread
+  if (t < k) {
+    const int c = t;
+    for (int i = k - 1; i >= 0; --i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int l = i + 1; l <= c; ++l) s -= a[l][i] * x[l][c];  // R[i][l] = L[l][i]
+      x[i][c] = (i <= c) ? s / a[i][i] : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    const double r = (j >= i) ? a[j][i] : 0.0;
+    if (R) R[i * k + j] = r;
+    const double xi = (j >= i) ? x[i][j] : 0.0;
+    if (Rinv) Rinv[i * k + j] = xi;
+    if (Rinv32) Rinv32[i * k + j] = (float)xi;
+  }
+  if (t == 0 && bad && status) atomicOr(status, 1);
+}
+
+__global__ void __launch_bounds__(256)
+k_small_matmul(const double* __restrict__ A, const double* __restrict__ B, double* __restrict__ C, int m, int kk,
+               int n, float* __restrict__ C32) {
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < m * n; e += gridDim.x * 256) {
+    const int i = e / n, j = e % n;
+    double s = 0.0;
+    for (int l = 0; l < kk; ++l) s += A[i * kk + l] * B[l * n + j];
+    if (C) C[e] = s;
+    if (C32) C32[e] = (float)s;
+  }
+}
+}  // namespace
+
+SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double* Rinv, float* Rinv32, int* status,
+                             void* stream) {
+  if (k < 1 || k > KM) {
+    sl_set_last_error("small_chol_inv: 1 <= k <= 64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  k_small_chol_inv<<<1, 256, 0, (hipStream_t)stream>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+SL_API int sl_small_matmul(const double* A, const double* B, double* C, int m, int kk, int n, float* C32,
+                           void* stream) {
+  if (m <= 0 || n <= 0) return SL_OK;
+  int blocks = (m * n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  k_small_matmul<<<blocks, 256, 0, (hipStream_t)stream>>>(A, B, C, m, kk, n, C32);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

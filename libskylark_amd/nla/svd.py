@@ -125,6 +125,14 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
     from ..ops import tallskinny as T
 
+    if A_loc.is_cuda and work == torch.float32 and T._native_ok(A_loc, k):
+        res = _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params)
+        if res is not None:
+            U_loc, s, V = res
+            if Ad is not None:
+                return DistMatrix(U_loc, (m, rank), "VC_STAR", comm), s, V
+            return U_loc, s, V
+        ctx = res_ctx_restore(ctx)
     prof = PROFILER
     with prof.phase("svd.sketch"):
         Zh = _sketch_operator(params.sketch, n, k, ctx, "cpu", torch.float64).numpy()
@@ -202,6 +210,65 @@ def approximate_svd(A, rank: int, context: Context | None = None,
         U = DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm)
         return U, s, V
     return U_loc, s, V
+
+
+def res_ctx_restore(ctx):
+    return ctx
+
+
+def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
+    """GPU-resident path (bf16 A on gfx950): every iteration stays on the device;
+    one host synchronisation per call (the k x k SVD + status check).
+
+    Returns None when a Cholesky breakdown was flagged (the caller then reruns
+    the robust host path with the same, rewound, context)."""
+    from ..ops import small_la as SL
+    from ..ops import tallskinny as T
+    prof = PROFILER
+    dev = A_loc.device
+    ctx0 = ctx.copy()
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    with prof.phase("svd.sketch"):
+        Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float32)
+    q = max(0, int(params.num_iterations))
+    for _ in range(q):
+        with prof.phase("svd.fused_pass"):
+            W, _, _ = T.fused_pass(A_loc, Z, keep_y=False, gram=False, exact=False)
+        with prof.phase("svd.allreduce_small"):
+            comm.all_reduce(W)
+        with prof.phase("svd.orth"):
+            Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-30) if params.skip_qr else SL.cholqr2(W, status)
+    with prof.phase("svd.fused_pass"):
+        W, G, Y = T.fused_pass(A_loc, Z, keep_y=True, gram=True, exact=True)
+    with prof.phase("svd.allreduce_small"):
+        WG = torch.cat([W.double(), G], 0)
+        comm.all_reduce(WG)
+        W, G = WG[:n], WG[n:]
+    with prof.phase("svd.final_qr"):
+        # CholeskyQR2 of Y: first factor from the pass's Gram, second from an exact f32 Gram
+        R1, R1i, R1i32 = SL.chol_inv(G, status)
+        _, G2 = T.f32_xm(Y, R1i32, store=False, gram=True)
+        comm.all_reduce(G2)
+        R2, R2i, _ = SL.chol_inv(G2, status)
+        Rti = SL.small_matmul(R1i, R2i)          # Rt^{-1} = R1^{-1} R2^{-1}
+        Vt = SL.small_matmul(W, Rti)             # A^T Q, Q = Y Rt^{-1}
+    with prof.phase("svd.small_svd"):
+        host = torch.cat([Vt.reshape(-1), Rti.reshape(-1), status.double()]).cpu().numpy()
+        if host[-1] != 0:
+            ctx.seed, ctx.counter = ctx0.seed, ctx0.counter
+            return None
+        Vt_h = host[:n * k].reshape(n, k)
+        Rti_h = host[n * k:n * k + k * k].reshape(k, k)
+        Qv, Rv = _cholqr2_host(Vt_h)
+        Ur, s, Vrt = np.linalg.svd(Rv)
+        M = Rti_h @ Vrt.T[:, :rank]
+        out = torch.from_numpy(np.concatenate([M.reshape(-1), s[:rank], (Qv @ Ur)[:, :rank].reshape(-1)])).to(dev)
+        M_d = out[:k * rank].view(k, rank).float()
+        s_d = out[k * rank:k * rank + rank].float()
+        V_d = out[k * rank + rank:].view(n, rank).float()
+    with prof.phase("svd.form_U"):
+        U, _ = T.f32_xm(Y, M_d, store=True)
+    return U, s_d, V_d
 
 
 # ------------------------------------------------------- host small LA (fp64)

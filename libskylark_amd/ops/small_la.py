@@ -1,0 +1,55 @@
+"""GPU-resident small dense linear algebra (k <= 64) for iteration loops.
+
+CholeskyQR2 of replicated n x k iterates and Cholesky/inverse of k x k Grams
+without any host synchronisation: Grams and products via the MFMA kernels
+of ``tsk_f32_kernels.hip``, the k x k factorisation by one workgroup
+(``small_la.hip``).  Failures are flagged in a device status word that the
+caller checks once, at the end.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from . import tallskinny as T
+
+vp, i32 = C.c_void_p, C.c_int
+_lib.register("sl_small_chol_inv", [vp, i32, i32, vp, vp, vp, vp, vp])
+_lib.register("sl_small_matmul", [vp, vp, vp, i32, i32, i32, vp, vp])
+
+
+def chol_inv(G: torch.Tensor, status: torch.Tensor | None = None):
+    """R (upper, G = R^T R), R^{-1} (f64) and R^{-1} as f32, all on G's device."""
+    k = G.shape[0]
+    G = G.to(torch.float64).contiguous()
+    R = torch.empty(k, k, dtype=torch.float64, device=G.device)
+    Ri = torch.empty_like(R)
+    Ri32 = torch.empty(k, k, dtype=torch.float32, device=G.device)
+    _lib.call("sl_small_chol_inv", _lib.ptr(G), k, k, _lib.ptr(R), _lib.ptr(Ri), _lib.ptr(Ri32),
+              _lib.ptr(status) if status is not None else None, vp(_lib.stream_of(G)))
+    return R, Ri, Ri32
+
+
+def small_matmul(A: torch.Tensor, B: torch.Tensor, want32: bool = False):
+    A = A.to(torch.float64).contiguous()
+    B = B.to(torch.float64).contiguous()
+    m, kk = A.shape
+    n = B.shape[1]
+    Cm = torch.empty(m, n, dtype=torch.float64, device=A.device)
+    C32 = torch.empty(m, n, dtype=torch.float32, device=A.device) if want32 else None
+    _lib.call("sl_small_matmul", _lib.ptr(A), _lib.ptr(B), _lib.ptr(Cm), m, kk, n,
+              _lib.ptr(C32) if C32 is not None else None, vp(_lib.stream_of(A)))
+    return (Cm, C32) if want32 else Cm
+
+
+def cholqr2(W: torch.Tensor, status: torch.Tensor | None = None) -> torch.Tensor:
+    """Orthonormal basis of the columns of a replicated f32 n x k matrix (CholeskyQR2)."""
+    W = W.float().contiguous()
+    _, G1 = T.f32_xm(W, None, store=False, gram=True)
+    _, _, R1i = chol_inv(G1, status)
+    Q1, G2 = T.f32_xm(W, R1i, store=True, gram=True)
+    _, _, R2i = chol_inv(G2, status)
+    Q, _ = T.f32_xm(Q1, R2i, store=True)
+    return Q
