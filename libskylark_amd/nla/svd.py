@@ -253,19 +253,20 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
         Rti = SL.small_matmul(R1i, R2i)          # Rt^{-1} = R1^{-1} R2^{-1}
         Vt = SL.small_matmul(W, Rti)             # A^T Q, Q = Y Rt^{-1}
     with prof.phase("svd.small_svd"):
-        host = torch.cat([Vt.reshape(-1), Rti.reshape(-1), status.double()]).cpu().numpy()
+        # A^T Q = Qv Rv (device CholeskyQR2), then only the k x k SVD on the host
+        Qv, Rv = SL.cholqr2(Vt, status, want_r=True)
+        host = torch.cat([Rv.reshape(-1), status.double()]).cpu().numpy()
         if host[-1] != 0:
             ctx.seed, ctx.counter = ctx0.seed, ctx0.counter
             return None
-        Vt_h = host[:n * k].reshape(n, k)
-        Rti_h = host[n * k:n * k + k * k].reshape(k, k)
-        Qv, Rv = _cholqr2_host(Vt_h)
-        Ur, s, Vrt = np.linalg.svd(Rv)
-        M = Rti_h @ Vrt.T[:, :rank]
-        out = torch.from_numpy(np.concatenate([M.reshape(-1), s[:rank], (Qv @ Ur)[:, :rank].reshape(-1)])).to(dev)
-        M_d = out[:k * rank].view(k, rank).float()
-        s_d = out[k * rank:k * rank + rank].float()
-        V_d = out[k * rank + rank:].view(n, rank).float()
+        Ur, s, Vrt = np.linalg.svd(host[:k * k].reshape(k, k))
+        small = torch.from_numpy(np.concatenate([Ur[:, :rank].reshape(-1), Vrt.T[:, :rank].reshape(-1),
+                                                 s[:rank]])).to(dev)
+        Ur_d = small[:k * rank].view(k, rank)
+        Vr_d = small[k * rank:2 * k * rank].view(k, rank)
+        s_d = small[2 * k * rank:].float()
+        V_d = SL.small_matmul(Qv.double(), Ur_d).float()    # V = Qv Ur_r
+        M_d = SL.small_matmul(Rti, Vr_d).float()            # U = Y Rt^{-1} Vr_r
     with prof.phase("svd.form_U"):
         U, _ = T.f32_xm(Y, M_d, store=True)
     return U, s_d, V_d

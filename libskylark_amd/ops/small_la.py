@@ -44,12 +44,17 @@ def small_matmul(A: torch.Tensor, B: torch.Tensor, want32: bool = False):
     return (Cm, C32) if want32 else Cm
 
 
-def cholqr2(W: torch.Tensor, status: torch.Tensor | None = None) -> torch.Tensor:
-    """Orthonormal basis of the columns of a replicated f32 n x k matrix (CholeskyQR2)."""
+def cholqr2(W: torch.Tensor, status: torch.Tensor | None = None, want_r: bool = False):
+    """Orthonormal basis of the columns of a replicated f32 n x k matrix (CholeskyQR2).
+
+    With ``want_r`` also returns the f64 triangular factor ``R = R2 R1``
+    (``W = Q R``)."""
     W = W.float().contiguous()
     _, G1 = T.f32_xm(W, None, store=False, gram=True)
-    _, _, R1i = chol_inv(G1, status)
+    R1, _, R1i = chol_inv(G1, status)
     Q1, G2 = T.f32_xm(W, R1i, store=True, gram=True)
-    _, _, R2i = chol_inv(G2, status)
+    R2, _, R2i = chol_inv(G2, status)
     Q, _ = T.f32_xm(Q1, R2i, store=True)
+    if want_r:
+        return Q, small_matmul(R2, R1)
     return Q
