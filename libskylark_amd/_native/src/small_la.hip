@@ -54,21 +54,27 @@ k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restric
     }
     __syncthreads();
   }
-  // R = L^T ;  X = R^{-1} (upper) by back substitution, one column per thread
-  if (t < k) {
-    const int c = t;
-    for (int i = k - 1; i >= 0; --i) {
-      double s = (i == c) ? 1.0 : 0.0;
-      for (int l = i + 1; l <= c; ++l) s -= a[l][i] * x[l][c];  // R[i][l] = L[l][i]
-      x[i][c] = (i <= c) ? s / a[i][i] : 0.0;
-    }
-  }
+  // X = L^{-1} by right-looking elimination (every step updates all remaining
+  // entries in parallel: no serial dependency chain per thread); then
+  // R^{-1} = (L^T)^{-1} = X^T.
+  for (int e = t; e < k * k; e += 256) x[e / k][e % k] = (e / k == e % k) ? 1.0 : 0.0;
   __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    const double inv = 1.0 / a[j][j];
+    for (int c = t; c <= j; c += 256) x[j][c] *= inv;
+    __syncthreads();
+    const int rows = k - j - 1, cols = j + 1;
+    for (int e = t; e < rows * cols; e += 256) {
+      const int i = j + 1 + e / cols, c = e % cols;
+      x[i][c] -= a[i][j] * x[j][c];
+    }
+    __syncthreads();
+  }
   for (int e = t; e < k * k; e += 256) {
     const int i = e / k, j = e % k;
     const double r = (j >= i) ? a[j][i] : 0.0;
     if (R) R[i * k + j] = r;
-    const double xi = (j >= i) ? x[i][j] : 0.0;
+    const double xi = (j >= i) ? x[j][i] : 0.0;  // R^{-1}[i][j] = (L^{-1})[j][i]
     if (Rinv) Rinv[i * k + j] = xi;
     if (Rinv32) Rinv32[i * k + j] = (float)xi;
   }
