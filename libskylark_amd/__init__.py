@@ -39,4 +39,8 @@ def set_default_context(ctx: Context):
     _default_context = ctx
 
 
-from . import base, nla, parallel, sketch  # noqa: E402,F401
+import warnings as _w  # noqa: E402
+
+_w.filterwarnings("ignore", message="Sparse CSR tensor support is in beta state")
+
+from . import algorithms, base, nla, parallel, sketch  # noqa: E402,F401

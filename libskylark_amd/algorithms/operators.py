@@ -1,0 +1,170 @@
+"""Linear-operator adapters for the iterative solvers.
+
+The reference's solvers are templated on Elemental / sparse matrix types and
+call ``base::Gemm`` / ``base::Symm`` / ``base::ColumnNrm2`` (which contain the
+all-reduces, ``base/Gemm.hpp:84-103``, ``base/inner.hpp``).  Here an
+:class:`Operator` hides the layout:
+
+* "long" vectors live on the row side of A (m x k); for a row-distributed A
+  ([VC,*]) they are row-distributed too and inner products all-reduce k
+  scalars;
+* "short" vectors live on the column side (n x k) and are replicated on every
+  GPU; ``A^T U`` is a local GEMM plus ONE all-reduce of n x k.
+
+Dense (torch, any device), sparse CSR (torch) and DistMatrix [VC,*] inputs
+are supported; anything with ``matmul``/``rmatmul`` methods passes through.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..parallel.comm import Comm
+from ..parallel.distmatrix import DistMatrix
+
+
+class Operator:
+    distributed = False
+
+    def __init__(self, shape, dtype, device, comm: Comm | None = None):
+        self.shape = tuple(shape)
+        self.dtype = dtype
+        self.device = device
+        self.comm = comm or Comm(None)
+
+    # y = A x (x short/replicated, y long/distributed)
+    def matmul(self, X):
+        raise NotImplementedError
+
+    # x = A^T y (y long/distributed, x short/replicated)
+    def rmatmul(self, Y):
+        raise NotImplementedError
+
+    # column 2-norms / dots of LONG vectors (all-reduce when distributed)
+    def long_colnorm(self, U):
+        s = (U * U).sum(0)
+        if self.distributed:
+            self.comm.all_reduce(s)
+        return s.sqrt()
+
+    def long_coldot(self, U, V):
+        s = (U * V).sum(0)
+        if self.distributed:
+            self.comm.all_reduce(s)
+        return s
+
+    @staticmethod
+    def short_colnorm(X):
+        return (X * X).sum(0).sqrt()
+
+    def long_like(self, B):
+        return B
+
+    def local_rows(self):
+        return self.shape[0]
+
+
+class DenseOp(Operator):
+    def __init__(self, A: torch.Tensor, compute_dtype=None):
+        cdt = compute_dtype or (A.dtype if A.dtype in (torch.float32, torch.float64) else torch.float32)
+        super().__init__(A.shape, cdt, A.device)
+        self.A = A
+
+    def matmul(self, X):
+        if self.A.dtype in (torch.bfloat16, torch.float16):
+            from ..ops import tallskinny as T
+            return T.matmul(self.A, X, out_dtype=self.dtype)
+        return self.A @ X.to(self.A.dtype)
+
+    def rmatmul(self, Y):
+        if self.A.dtype in (torch.bfloat16, torch.float16):
+            hi = Y.to(self.A.dtype)
+            lo = (Y - hi.to(Y.dtype)).to(self.A.dtype)
+            if self.A.is_cuda:
+                return (torch.mm(self.A.t(), hi, out_dtype=torch.float32) +
+                        torch.mm(self.A.t(), lo, out_dtype=torch.float32)).to(self.dtype)
+            return (self.A.t().float() @ (hi.float() + lo.float())).to(self.dtype)
+        return self.A.t() @ Y.to(self.A.dtype)
+
+
+class SparseOp(Operator):
+    def __init__(self, A: torch.Tensor):
+        vdt = A.values().dtype
+        super().__init__(A.shape, vdt if vdt in (torch.float32, torch.float64) else torch.float32, A.device)
+        self.A = A
+        self._At = None
+
+    def matmul(self, X):
+        return torch.sparse.mm(self.A, X.to(self.dtype))
+
+    def rmatmul(self, Y):
+        if self._At is None:
+            self._At = self.A.to_sparse_coo().t().coalesce().to_sparse_csr()
+        return torch.sparse.mm(self._At, Y.to(self.dtype))
+
+
+class DistRowOp(Operator):
+    """A distributed as [VC,*] row blocks (local shard m_loc x n)."""
+
+    distributed = True
+
+    def __init__(self, D: DistMatrix):
+        if D.layout not in ("VC_STAR", "VR_STAR"):
+            D = D.redistribute("VC_STAR")
+        loc = D.local
+        inner = SparseOp(loc) if loc.layout == torch.sparse_csr else DenseOp(loc)
+        super().__init__(D.shape, inner.dtype, loc.device, D.comm)
+        self.D = D
+        self.inner = inner
+        self.distributed = D.comm.size > 1
+
+    def matmul(self, X):
+        return self.inner.matmul(X)
+
+    def rmatmul(self, Y):
+        out = self.inner.rmatmul(Y).contiguous()
+        if self.distributed:
+            self.comm.all_reduce(out)
+        return out
+
+    def local_rows(self):
+        return self.D.local.shape[0]
+
+    def long_like(self, B):
+        # B may be given globally (replicated m x k) or already as the local shard
+        if isinstance(B, DistMatrix):
+            return B.redistribute("VC_STAR").local
+        if B.shape[0] == self.shape[0] and self.D.local.shape[0] != self.shape[0]:
+            s, e = self.D.row_range()
+            return B[s:e]
+        return B
+
+
+class CallableOp(Operator):
+    def __init__(self, obj):
+        super().__init__(obj.shape, getattr(obj, "dtype", torch.float64), getattr(obj, "device", None),
+                         getattr(obj, "comm", None))
+        self.obj = obj
+        self.distributed = getattr(obj, "distributed", False)
+
+    def matmul(self, X):
+        return self.obj.matmul(X)
+
+    def rmatmul(self, Y):
+        return self.obj.rmatmul(Y)
+
+
+def as_operator(A) -> Operator:
+    if isinstance(A, Operator):
+        return A
+    if isinstance(A, DistMatrix):
+        return DistRowOp(A)
+    if isinstance(A, torch.Tensor):
+        if A.layout != torch.strided:
+            return SparseOp(A.to_sparse_csr() if A.layout != torch.sparse_csr else A)
+        return DenseOp(A)
+    if hasattr(A, "matmul") and hasattr(A, "rmatmul"):
+        return CallableOp(A)
+    import numpy as np
+    if isinstance(A, np.ndarray):
+        return DenseOp(torch.from_numpy(A))
+    raise TypeError(f"cannot build an operator from {type(A)}")
