@@ -252,10 +252,9 @@ def cg(A, B, X=None, params: KrylovIterParams | None = None, M: Precond | None =
     if Bv.dim() == 1:
         Bv = Bv[:, None]
     k = Bv.shape[1]
-    n = op.shape[0]
-    dev = Bv.device
     tol = _clamp_tol(params.tolerance, dt)
-    X = torch.zeros(n, k, dtype=dt, device=dev) if X is None else X.to(dt).clone()
+    # X lives where B does (row-distributed for a DistSymOp)
+    X = torch.zeros_like(Bv) if X is None else op.long_like(X).to(dt).clone()
     Rr = Bv - op.matmul(X).to(dt)
     nrmb = op.long_colnorm(Bv)
     ressqr = op.long_coldot(Rr, Rr)

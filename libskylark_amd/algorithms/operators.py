@@ -139,6 +139,21 @@ class DistRowOp(Operator):
         return B
 
 
+class DistSymOp(DistRowOp):
+    """Square symmetric A held as [VC,*] row blocks, for CG-type solvers where
+    every vector is "long" (row-distributed like A): ``A P`` all-gathers the
+    n x k direction block (one collective per iteration) and multiplies the
+    local row block; ``A^T`` is ``A``."""
+
+    def matmul(self, X):
+        if self.distributed:
+            counts = [e - s for s, e in self.D.row_blocks()]
+            X = self.comm.all_gather_v(X.contiguous(), counts, dim=0)
+        return self.inner.matmul(X)
+
+    rmatmul = matmul
+
+
 class CallableOp(Operator):
     def __init__(self, obj):
         super().__init__(obj.shape, getattr(obj, "dtype", torch.float64), getattr(obj, "device", None),

@@ -1,0 +1,140 @@
+"""Data IO (reference ``utility/io/*``, ``ml/io.hpp``).
+
+* LIBSVM: native multi-threaded parser, byte-range distributed reader,
+  writer (:mod:`.libsvm`).
+* Arc lists (edge lists): byte-range parallel read into a sparse adjacency
+  (:func:`read_arc_list`), reference ``utility/io/arc_list.hpp``.
+* HDF5: the reference's ``ReadHDF5``/``write_hdf5`` need h5py here, which is
+  not installed in this image — the functions exist and raise a clear
+  :class:`~libskylark_amd.base.exceptions.IOError_` unless h5py is importable.
+* :func:`read` — ``ml/io.hpp:869`` dispatch on fileformat code
+  (0 libsvm-dense, 1 libsvm-sparse, 2 hdf5-dense, 3 hdf5-sparse).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..base.exceptions import IOError_
+from .libsvm import ReadLIBSVM, WriteLIBSVM, read_libsvm, read_libsvm_dist, write_libsvm  # noqa: F401
+
+LIBSVM_DENSE, LIBSVM_SPARSE, HDF5_DENSE, HDF5_SPARSE = range(4)
+
+
+def _h5py():
+    try:
+        import h5py  # noqa: F401
+        return h5py
+    except ImportError as e:  # pragma: no cover - depends on image
+        raise IOError_("HDF5 IO requires h5py, which is not installed") from e
+
+
+def read_hdf5(fname: str, max_n: int = -1, sparse: bool = False, dtype=torch.float64):
+    """Reference layout: datasets ``X`` (d x n, examples as columns) and ``Y``;
+    sparse files hold ``dimensions``, ``indptr``, ``indices``, ``values``.
+    Returns ``(X, Y)`` with examples as ROWS."""
+    h5py = _h5py()
+    with h5py.File(fname, "r") as f:
+        if "indptr" in f:
+            dims = np.asarray(f["dimensions"])
+            d, n = int(dims[0]), int(dims[1])
+            indptr = np.asarray(f["indptr"], dtype=np.int64)
+            n = n if max_n < 0 else min(n, max_n)
+            nnz = int(indptr[n])
+            X = torch.sparse_csr_tensor(torch.from_numpy(indptr[:n + 1]),
+                                        torch.from_numpy(np.asarray(f["indices"][:nnz], dtype=np.int64)),
+                                        torch.from_numpy(np.asarray(f["values"][:nnz], dtype=np.float64)).to(dtype),
+                                        (n, d))
+            if not sparse:
+                X = X.to_dense()
+        else:
+            Xd = np.asarray(f["X"])
+            n = Xd.shape[1] if max_n < 0 else min(Xd.shape[1], max_n)
+            X = torch.from_numpy(np.ascontiguousarray(Xd[:, :n].T)).to(dtype)
+            if sparse:
+                X = X.to_sparse_csr()
+        Y = torch.from_numpy(np.asarray(f["Y"]).reshape(-1)[:X.shape[0]].astype(np.float64))
+    return X, Y
+
+
+def write_hdf5(fname: str, X, Y):
+    h5py = _h5py()
+    with h5py.File(fname, "w") as f:
+        if X.layout != torch.strided:
+            Xc = X.to_sparse_csr().cpu()
+            f["dimensions"] = np.array([X.shape[1], X.shape[0], Xc.values().numel()], dtype=np.int64)
+            f["indptr"] = Xc.crow_indices().numpy()
+            f["indices"] = Xc.col_indices().numpy()
+            f["values"] = Xc.values().numpy()
+        else:
+            f["X"] = X.detach().cpu().t().contiguous().numpy()
+        f["Y"] = torch.as_tensor(Y).reshape(-1).cpu().numpy()
+
+
+def read(fileformat: int, fname: str, min_d: int = 0, comm=None, dtype=torch.float64, device=None):
+    """Dispatch on the reference's fileformat codes; distributed when ``comm`` has >1 rank."""
+    if fileformat in (LIBSVM_DENSE, LIBSVM_SPARSE):
+        if comm is not None and comm.size > 1:
+            return read_libsvm_dist(fname, comm, min_d, fileformat == LIBSVM_SPARSE, dtype, device)
+        return read_libsvm(fname, min_d, sparse=(fileformat == LIBSVM_SPARSE), dtype=dtype, device=device)
+    if fileformat in (HDF5_DENSE, HDF5_SPARSE):
+        return read_hdf5(fname, sparse=(fileformat == HDF5_SPARSE), dtype=dtype)
+    raise IOError_(f"unknown file format code {fileformat}")
+
+
+def read_arc_list(fname: str, symmetrize: bool = False, comm=None, dtype=torch.float64):
+    """Edge list ``u v [w]`` (0-based vertex ids, ``#`` comments) -> sparse CSR
+    adjacency n x n (n = max id + 1).  With a multi-rank ``comm`` each rank
+    parses its byte range (line-aligned) and the result is a [VC,*]
+    DistMatrix of adjacency rows (reference MPI-IO reader,
+    ``utility/io/arc_list.hpp:151-325``)."""
+    import os
+    size = os.path.getsize(fname)
+    rank, P = (comm.rank, comm.size) if comm is not None else (0, 1)
+    with open(fname, "rb") as f:
+        lo, hi = size * rank // P, size * (rank + 1) // P
+
+        def align(pos):
+            if pos <= 0 or pos >= size:
+                return min(max(pos, 0), size)
+            f.seek(pos - 1)
+            if f.read(1) == b"\n":
+                return pos
+            f.seek(pos)
+            f.readline()
+            return f.tell()
+        lo, hi = align(lo), align(hi)
+        f.seek(lo)
+        data = f.read(hi - lo).decode()
+    rows = []
+    for line in data.splitlines():
+        if not line.strip() or line.lstrip().startswith("#"):
+            continue
+        t = line.split()
+        rows.append((int(t[0]), int(t[1]), float(t[2]) if len(t) > 2 else 1.0))
+    e = np.array(rows, dtype=np.float64).reshape(-1, 3)
+    if symmetrize:
+        e = np.concatenate([e, e[:, [1, 0, 2]]], axis=0)
+    n_loc = int(e[:, :2].max()) + 1 if len(e) else 0
+    if comm is None or P == 1:
+        return _csr(e, 0, n_loc, n_loc, dtype)
+    # route every edge to the rank owning its source row ([VC,*] blocks): one all-to-all
+    from ..parallel.comm import balanced_offsets
+    from ..parallel.distmatrix import DistMatrix
+    n = max(comm.all_gather_object(n_loc))
+    offs = np.asarray(balanced_offsets(n, P))
+    owner = np.searchsorted(offs, e[:, 0], side="right") - 1
+    sends = [torch.from_numpy(np.ascontiguousarray(e[owner == r])) for r in range(P)]
+    mine = torch.cat(comm.all_to_all_v(sends), dim=0).numpy()
+    return DistMatrix(_csr(mine, int(offs[rank]), int(offs[rank + 1] - offs[rank]), n, dtype), (n, n), "VC_STAR",
+                      comm)
+
+
+def _csr(e, row0, nrows, ncols, dtype):
+    src, dst, w = e[:, 0].astype(np.int64) - row0, e[:, 1].astype(np.int64), e[:, 2]
+    return torch.sparse_coo_tensor(torch.from_numpy(np.stack([src, dst])), torch.from_numpy(w).to(dtype),
+                                   (nrows, ncols)).coalesce().to_sparse_csr()
+
+
+ReadArcList = read_arc_list
+ReadHDF5 = read_hdf5

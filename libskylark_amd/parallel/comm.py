@@ -127,6 +127,7 @@ class Comm:
         dev = sends[0].device
         sz = torch.tensor([s.shape[0] for s in sends], dtype=torch.int64, device=dev)
         rsz = torch.empty_like(sz)
+        allsz = None
         if self.backend == "gloo":
             allsz = self.all_gather(sz.view(1, -1), 0)
             rsz = allsz[:, self.rank].contiguous()
@@ -137,13 +138,11 @@ class Comm:
         recvs = [torch.empty((n,) + tail, dtype=sends[0].dtype, device=dev) for n in rs]
         if self.backend == "gloo":
             # gloo lacks all_to_all: emulate with an all-gather of padded buffers
-            mx = max(max(s.shape[0] for s in sends), 1)
+            mx = max(int(allsz.max()), 1)  # same padded size on every rank
             buf = torch.zeros((self.size, mx) + tail, dtype=sends[0].dtype, device=dev)
             for i, s in enumerate(sends):
                 buf[i, : s.shape[0]] = s
             allb = self.all_gather(buf.view((1,) + tuple(buf.shape)), 0)
-            mxs = [int(x) for x in self.all_gather(torch.tensor([[mx]], device=dev), 0).view(-1).tolist()]
-            del mxs
             for src in range(self.size):
                 recvs[src].copy_(allb[src, self.rank, : rs[src]])
             return recvs

@@ -1,0 +1,76 @@
+"""GPU numerics for the ML / solver native kernels vs fp64 torch references."""
+import math
+
+import pytest
+import torch
+
+import libskylark_amd as sk
+from libskylark_amd import ml
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("m,n,d", [(1, 1, 1), (70, 130, 33), (257, 64, 100)])
+def test_pairwise_kernels(dev, dt, m, n, d):
+    g = torch.Generator().manual_seed(m + n + d)
+    X = torch.rand(m, d, generator=g, dtype=torch.float64)
+    Y = torch.rand(n, d, generator=g, dtype=torch.float64)
+    for k, ref in [(ml.Laplacian(d, 3.0), torch.exp(-(X[:, None] - Y[None]).abs().sum(-1) / 3.0)),
+                   (ml.ExpSemigroup(d, 0.1), torch.exp(-0.1 * torch.sqrt(X[:, None] + Y[None]).sum(-1)))]:
+        K = k.gram(X.to(dev, dt), Y=Y.to(dev, dt))
+        tol = 1e-4 if dt == torch.float32 else 1e-10
+        torch.testing.assert_close(K.double().cpu(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_gemm_kernels(dev, dt):
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(300, 20, generator=g, dtype=torch.float64)
+    Y = torch.randn(200, 20, generator=g, dtype=torch.float64)
+    tol = 2e-4 if dt == torch.float32 else 1e-10
+    kg = ml.Gaussian(20, 3.0)
+    ref = torch.exp(-torch.cdist(X, Y) ** 2 / 18.0)
+    torch.testing.assert_close(kg.gram(X.to(dev, dt), Y=Y.to(dev, dt)).double().cpu(), ref, rtol=tol, atol=tol)
+    kp = ml.Polynomial(20, 2, 1.0, 0.1)
+    ref = (0.1 * X @ Y.t() + 1.0) ** 2
+    torch.testing.assert_close(kp.gram(X.to(dev, dt), Y=Y.to(dev, dt)).double().cpu(), ref, rtol=tol, atol=tol)
+
+
+def test_asyrgs_native(dev):
+    n = 2000
+    T = torch.diag(torch.full((n,), 4.0, dtype=torch.float64))
+    T -= torch.diag(torch.ones(n - 1, dtype=torch.float64), 1) + torch.diag(torch.ones(n - 1, dtype=torch.float64), -1)
+    b = torch.randn(n, 3, dtype=torch.float64)
+    X, code = sk.algorithms.asy_rgs(T.to_sparse_csr().to(dev), b.to(dev), context=sk.Context(3),
+                                    params=sk.algorithms.AsyIterParams(tolerance=1e-9, sweeps_lim=300))
+    assert code == -1
+    assert float((T @ X.cpu() - b).norm() / b.norm()) < 1e-8
+
+
+def test_krr_and_admm_on_gpu(dev):
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(2000, 8, generator=g, dtype=torch.float64)
+    Y = torch.sin(X[:, :1])
+    k = ml.Gaussian(8, 2.0)
+    A = ml.faster_kernel_ridge(k, X.to(dev), Y.to(dev), 0.1, 256, sk.Context(2),
+                               params=ml.KrrParams(tolerance=1e-10, iter_lim=300))
+    Ar = ml.kernel_ridge(k, X, Y, 0.1)
+    torch.testing.assert_close(A.cpu(), Ar, rtol=1e-5, atol=1e-6)
+    lab = (X[:, 0] > 0).to(torch.float64) * 2 - 1
+    s = ml.BlockADMMSolver("hinge", "l2", 0.01, 512, kernel=k, context=sk.Context(3))
+    s.set_maxiter(20)
+    model = s.train(X.to(dev).float(), lab.to(dev), regression=False, log=None)
+    pred, _ = model.predict(X.to(dev).float())
+    assert float((pred.cpu() == lab).double().mean()) > 0.95
+
+
+def test_lsqr_on_gpu(dev):
+    g = torch.Generator().manual_seed(0)
+    A = torch.randn(5000, 50, generator=g, dtype=torch.float64)
+    B = torch.randn(5000, 2, generator=g, dtype=torch.float64)
+    X, code = sk.algorithms.lsqr(A.to(dev), B.to(dev),
+                                 params=sk.algorithms.KrylovIterParams(tolerance=1e-13, iter_lim=300))
+    torch.testing.assert_close(X.cpu(), torch.linalg.lstsq(A, B).solution, rtol=1e-8, atol=1e-8)
+    Xf = sk.nla.faster_least_squares(A.to(dev), B.to(dev), sk.Context(1))
+    torch.testing.assert_close(Xf.cpu(), torch.linalg.lstsq(A, B).solution, rtol=1e-7, atol=1e-7)
