@@ -22,6 +22,8 @@ SRC = os.path.join(HERE, "src")
 INC = os.path.join(HERE, "include")
 OBJ = os.path.join(HERE, "build")
 LIB = os.path.join(HERE, "libskylark_hip.so")
+CAPI_SRC = os.path.join(HERE, "capi", "skylark_capi.cpp")
+CAPI_LIB = os.path.join(HERE, "libskylark_capi.so")
 ARCH = os.environ.get("SKH_GFX_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -93,6 +95,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         os.replace(tmp, LIB)
         if verbose:
             print("linked", LIB)
+    build_capi(force)
     # drop stale objects of older source versions
     keep = set(objs)
     for f in os.listdir(OBJ):
@@ -103,6 +106,24 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             except OSError:
                 pass
     return LIB
+
+
+def build_capi(force: bool = False) -> str:
+    """C API library (host C++, embeds/joins CPython; no device code)."""
+    if not force and os.path.exists(CAPI_LIB) and os.path.getmtime(CAPI_LIB) >= os.path.getmtime(CAPI_SRC):
+        return CAPI_LIB
+    import sysconfig
+    inc = sysconfig.get_paths()["include"]
+    libdir = sysconfig.get_config_var("LIBDIR")
+    ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    tmp = CAPI_LIB + f".{os.getpid()}.tmp"
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden",
+           "-I", inc, CAPI_SRC, "-o", tmp, f"-L{libdir}", f"-lpython{ver}", "-ldl", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"C API build failed:\n{r.stderr[-6000:]}")
+    os.replace(tmp, CAPI_LIB)
+    return CAPI_LIB
 
 
 def main(argv=None):

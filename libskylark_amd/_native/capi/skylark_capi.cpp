@@ -1,0 +1,534 @@
+// C API of the framework: the reference's sl_* ABI (capi/basec.hpp,
+// sketchc.hpp, nlac.hpp, kernelc.hpp, ioc.hpp) over the MI355X runtime.
+//
+// The compute path lives in the Python/HIP runtime (libskylark_amd +
+// libskylark_hip.so); this library is a thin C++ marshalling layer.  It
+// embeds CPython when called from a plain C/C++ program (first call
+// initialises the interpreter, adds this library's package root to
+// sys.path, and imports libskylark_amd.capi), or joins the running
+// interpreter when loaded from Python.  Every entry point:
+//   - takes the GIL (PyGILState_Ensure),
+//   - converts handles / raw matrix wraps / varargs to Python objects,
+//   - calls libskylark_amd.capi.<fn>,
+//   - maps a Python exception to the reference's integer error code and
+//     keeps the formatted traceback for sl_get_exception_info().
+#include <Python.h>
+#include <dlfcn.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#define SL_CAPI extern "C" __attribute__((visibility("default")))
+
+struct sl_context_t {
+  PyObject* obj;
+};
+struct sl_sketch_transform_t {
+  PyObject* obj;
+};
+struct sl_kernel_t {
+  PyObject* obj;
+};
+struct sl_raw_matrix_t {
+  double* data;
+  int m, n;
+};
+struct sl_raw_sp_matrix_t {
+  int* indptr;
+  int* ind;
+  double* data;
+  int nnz, m, n;
+  PyObject* out;  // library-owned result (capi.SparseOut) when used as output
+};
+
+namespace {
+
+std::once_flag g_init;
+PyObject* g_mod = nullptr;
+std::string g_last_error;
+std::string g_supported;
+
+void init_python() {
+  if (!Py_IsInitialized()) {
+    Py_InitializeEx(0);
+    // hand the GIL back; every entry point re-acquires it
+    PyEval_SaveThread();
+  }
+  PyGILState_STATE st = PyGILState_Ensure();
+  Dl_info info;
+  if (dladdr((void*)&init_python, &info) && info.dli_fname) {
+    // <root>/libskylark_amd/_native/libskylark_capi.so -> <root>
+    std::string p(info.dli_fname);
+    for (int i = 0; i < 3; ++i) {
+      auto k = p.find_last_of('/');
+      if (k == std::string::npos) break;
+      p = p.substr(0, k);
+    }
+    PyObject* sys_path = PySys_GetObject("path");
+    PyObject* s = PyUnicode_FromString(p.c_str());
+    if (sys_path && s && !PySequence_Contains(sys_path, s)) PyList_Append(sys_path, s);
+    Py_XDECREF(s);
+  }
+  g_mod = PyImport_ImportModule("libskylark_amd.capi");
+  if (!g_mod) {
+    PyErr_Print();
+  }
+  PyGILState_Release(st);
+}
+
+struct Gil {
+  PyGILState_STATE st;
+  Gil() {
+    std::call_once(g_init, init_python);
+    st = PyGILState_Ensure();
+  }
+  ~Gil() { PyGILState_Release(st); }
+};
+
+// Convert the pending Python exception to an error code (and keep the text).
+int fail() {
+  PyObject *t, *v, *tb;
+  PyErr_Fetch(&t, &v, &tb);
+  PyErr_NormalizeException(&t, &v, &tb);
+  int code = 100;
+  g_last_error = "unknown error";
+  if (v) {
+    PyObject* tbm = PyImport_ImportModule("traceback");
+    if (tbm) {
+      PyObject* lines = PyObject_CallMethod(tbm, "format_exception", "OOO", t ? t : Py_None, v, tb ? tb : Py_None);
+      if (lines) {
+        PyObject* sep = PyUnicode_FromString("");
+        PyObject* joined = PyUnicode_Join(sep, lines);
+        if (joined) g_last_error = PyUnicode_AsUTF8(joined);
+        Py_XDECREF(joined);
+        Py_XDECREF(sep);
+        Py_DECREF(lines);
+      }
+      Py_DECREF(tbm);
+    }
+    if (g_mod) {
+      PyObject* c = PyObject_CallMethod(g_mod, "error_code", "O", v);
+      if (c) {
+        code = (int)PyLong_AsLong(c);
+        Py_DECREF(c);
+      }
+    }
+  }
+  PyErr_Clear();
+  Py_XDECREF(t);
+  Py_XDECREF(v);
+  Py_XDECREF(tb);
+  return code;
+}
+
+PyObject* call(const char* fn, PyObject* args) {
+  if (!g_mod) {
+    PyErr_SetString(PyExc_RuntimeError, "libskylark_amd.capi could not be imported");
+    Py_XDECREF(args);
+    return nullptr;
+  }
+  PyObject* f = PyObject_GetAttrString(g_mod, fn);
+  if (!f) {
+    Py_XDECREF(args);
+    return nullptr;
+  }
+  PyObject* r = PyObject_CallObject(f, args);
+  Py_DECREF(f);
+  Py_XDECREF(args);
+  return r;
+}
+
+PyObject* dense_desc(void* A) {
+  auto* M = (sl_raw_matrix_t*)A;
+  return Py_BuildValue("(Kii)", (unsigned long long)(uintptr_t)M->data, M->m, M->n);
+}
+
+PyObject* sparse_in_desc(void* A) {
+  auto* M = (sl_raw_sp_matrix_t*)A;
+  return Py_BuildValue("(KKKiii)", (unsigned long long)(uintptr_t)M->indptr,
+                       (unsigned long long)(uintptr_t)M->ind, (unsigned long long)(uintptr_t)M->data, M->nnz, M->m,
+                       M->n);
+}
+
+PyObject* in_desc(const char* type, void* A) {
+  if (!strcmp(type, "Matrix")) return dense_desc(A);
+  if (!strcmp(type, "SparseMatrix")) return sparse_in_desc(A);
+  PyErr_Format(PyExc_ValueError, "unsupported matrix type %s (host C API takes Matrix / SparseMatrix)", type);
+  return nullptr;
+}
+
+PyObject* out_desc(const char* type, void* A) {
+  if (!strcmp(type, "Matrix")) return dense_desc(A);
+  if (!strcmp(type, "SparseMatrix")) {
+    auto* M = (sl_raw_sp_matrix_t*)A;
+    if (!M->out) {
+      M->out = call("SparseOut", PyTuple_New(0));
+      if (!M->out) return nullptr;
+    }
+    Py_INCREF(M->out);
+    return M->out;
+  }
+  PyErr_Format(PyExc_ValueError, "unsupported output matrix type %s", type);
+  return nullptr;
+}
+
+// Build a tuple of varargs from a spec string ('d' double, 'i' int).
+PyObject* varargs_tuple(const std::string& spec, va_list ap) {
+  PyObject* t = PyTuple_New((Py_ssize_t)spec.size());
+  for (size_t i = 0; i < spec.size(); ++i) {
+    PyObject* o = spec[i] == 'i' ? PyLong_FromLong(va_arg(ap, int)) : PyFloat_FromDouble(va_arg(ap, double));
+    PyTuple_SET_ITEM(t, (Py_ssize_t)i, o);
+  }
+  return t;
+}
+
+std::string spec_of(const char* fn, const char* type) {
+  PyObject* r = call(fn, Py_BuildValue("(s)", type));
+  std::string s;
+  if (r) {
+    s = PyUnicode_AsUTF8(r);
+    Py_DECREF(r);
+  } else {
+    PyErr_Clear();
+  }
+  return s;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- base
+SL_CAPI const char* sl_strerror(const int code) {
+  switch (code) {
+    case 0: return "No error";
+    case 100: return "Skylark failure";
+    case 101: return "Failed to allocate memory";
+    case 102: return "Unsupported matrix distribution";
+    case 103: return "Unsupported operation";
+    case 104: return "Dimension mismatch";
+    case 105: return "CombBLAS failure";
+    case 106: return "Native (HIP) library failure";
+    case 107: return "IO failure";
+    case 108: return "NLA failure";
+    case 109: return "Invalid parameters";
+    case 110: return "Unsupported base operation";
+    case 111: return "Unknown transform type";
+    default: return "Unknown error code";
+  }
+}
+
+SL_CAPI bool sl_has_elemental() { return false; }
+SL_CAPI bool sl_has_combblas() { return false; }
+
+SL_CAPI char* sl_supported_sketch_transforms() {
+  Gil g;
+  PyObject* r = call("supported_sketch_transforms", PyTuple_New(0));
+  if (!r) {
+    fail();
+    return nullptr;
+  }
+  g_supported = PyUnicode_AsUTF8(r);
+  Py_DECREF(r);
+  return (char*)g_supported.c_str();
+}
+
+SL_CAPI void sl_get_exception_info(char** info) { *info = strdup(g_last_error.c_str()); }
+SL_CAPI void sl_print_exception_trace() { fprintf(stderr, "%s\n", g_last_error.c_str()); }
+
+SL_CAPI int sl_create_default_context(int seed, sl_context_t** ctxt) {
+  Gil g;
+  PyObject* r = call("create_context", Py_BuildValue("(i)", seed));
+  if (!r) return fail();
+  *ctxt = new sl_context_t{r};
+  return 0;
+}
+
+// The communicator argument is accepted for ABI shape only: the process group
+// is torch.distributed's (RCCL) world, set up by the launcher.
+SL_CAPI int sl_create_context(int seed, void* /*comm*/, sl_context_t** ctxt) {
+  return sl_create_default_context(seed, ctxt);
+}
+
+SL_CAPI int sl_free_context(sl_context_t* ctxt) {
+  if (!ctxt) return 0;
+  Gil g;
+  Py_XDECREF(ctxt->obj);
+  delete ctxt;
+  return 0;
+}
+
+SL_CAPI int sl_wrap_raw_matrix(double* data, int m, int n, void** A) {
+  *A = new sl_raw_matrix_t{data, m, n};
+  return 0;
+}
+
+SL_CAPI int sl_free_raw_matrix_wrap(void* A) {
+  delete (sl_raw_matrix_t*)A;
+  return 0;
+}
+
+SL_CAPI int sl_wrap_raw_sp_matrix(int* indptr, int* ind, double* data, int nnz, int n_rows, int n_cols, void** A) {
+  *A = new sl_raw_sp_matrix_t{indptr, ind, data, nnz, n_rows, n_cols, nullptr};
+  return 0;
+}
+
+SL_CAPI int sl_free_raw_sp_matrix_wrap(void* A) {
+  auto* M = (sl_raw_sp_matrix_t*)A;
+  if (M->out) {
+    Gil g;
+    Py_DECREF(M->out);
+  }
+  delete M;
+  return 0;
+}
+
+namespace {
+template <typename F>
+int sp_query(void* A, F&& f) {
+  auto* M = (sl_raw_sp_matrix_t*)A;
+  if (!M->out) return 109;
+  Gil g;
+  return f(M->out);
+}
+long attr_long(PyObject* o, const char* name, int idx = -1) {
+  PyObject* a = PyObject_GetAttrString(o, name);
+  if (!a) return -1;
+  long v;
+  if (idx >= 0) {
+    PyObject* it = PySequence_GetItem(a, idx);
+    v = PyLong_AsLong(it);
+    Py_XDECREF(it);
+  } else {
+    v = PyObject_IsTrue(a);
+  }
+  Py_DECREF(a);
+  return v;
+}
+long array_len(PyObject* o, const char* name) {
+  PyObject* a = PyObject_GetAttrString(o, name);
+  if (!a) return -1;
+  long v = (long)PyObject_Length(a);
+  Py_DECREF(a);
+  return v;
+}
+void copy_array(PyObject* o, const char* name, void* dst, size_t elem) {
+  PyObject* a = PyObject_GetAttrString(o, name);
+  if (!a) return;
+  PyObject* b = PyObject_CallMethod(a, "tobytes", nullptr);
+  if (b) {
+    char* p;
+    Py_ssize_t n;
+    PyBytes_AsStringAndSize(b, &p, &n);
+    memcpy(dst, p, (size_t)n);
+    Py_DECREF(b);
+  }
+  (void)elem;
+  Py_DECREF(a);
+}
+}  // namespace
+
+SL_CAPI int sl_raw_sp_matrix_struct_updated(void* A, bool* updated) {
+  return sp_query(A, [&](PyObject* o) {
+    *updated = attr_long(o, "updated") != 0;
+    return 0;
+  });
+}
+
+SL_CAPI int sl_raw_sp_matrix_reset_update_flag(void* A) {
+  return sp_query(A, [&](PyObject* o) {
+    PyObject_SetAttrString(o, "updated", Py_False);
+    return 0;
+  });
+}
+
+SL_CAPI int sl_raw_sp_matrix_nnz(void* A, int* nnz) {
+  return sp_query(A, [&](PyObject* o) {
+    *nnz = (int)array_len(o, "values");
+    return 0;
+  });
+}
+
+SL_CAPI int sl_raw_sp_matrix_height(void* A, int* h) {
+  return sp_query(A, [&](PyObject* o) {
+    *h = (int)attr_long(o, "shape", 0);
+    return 0;
+  });
+}
+
+SL_CAPI int sl_raw_sp_matrix_width(void* A, int* w) {
+  return sp_query(A, [&](PyObject* o) {
+    *w = (int)attr_long(o, "shape", 1);
+    return 0;
+  });
+}
+
+SL_CAPI int sl_raw_sp_matrix_data(void* A, int32_t* indptr, int32_t* indices, double* values) {
+  return sp_query(A, [&](PyObject* o) {
+    copy_array(o, "indptr", indptr, 4);
+    copy_array(o, "indices", indices, 4);
+    copy_array(o, "values", values, 8);
+    return 0;
+  });
+}
+
+// ---------------------------------------------------------------- sketches
+SL_CAPI int sl_create_sketch_transform(sl_context_t* ctxt, char* type, int n, int s, sl_sketch_transform_t** sketch,
+                                       ...) {
+  Gil g;
+  std::string spec = spec_of("sketch_param_spec", type);
+  va_list ap;
+  va_start(ap, sketch);
+  PyObject* params = varargs_tuple(spec, ap);
+  va_end(ap);
+  PyObject* r = call("create_sketch", Py_BuildValue("(OsiiN)", ctxt->obj, type, n, s, params));
+  if (!r) {
+    int c = fail();
+    return c == 100 || c == 109 ? 111 : c;
+  }
+  *sketch = new sl_sketch_transform_t{r};
+  return 0;
+}
+
+SL_CAPI int sl_deserialize_sketch_transform(const char* data, sl_sketch_transform_t** sketch) {
+  Gil g;
+  PyObject* r = call("deserialize_sketch", Py_BuildValue("(s)", data));
+  if (!r) return fail();
+  *sketch = new sl_sketch_transform_t{r};
+  return 0;
+}
+
+SL_CAPI int sl_serialize_sketch_transform(const sl_sketch_transform_t* sketch, char** data) {
+  Gil g;
+  PyObject* r = call("serialize_sketch", Py_BuildValue("(O)", sketch->obj));
+  if (!r) return fail();
+  *data = strdup(PyUnicode_AsUTF8(r));
+  Py_DECREF(r);
+  return 0;
+}
+
+SL_CAPI int sl_free_sketch_transform(sl_sketch_transform_t* S) {
+  if (!S) return 0;
+  Gil g;
+  Py_XDECREF(S->obj);
+  delete S;
+  return 0;
+}
+
+SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type, void* A, char* output_type,
+                                      void* SA, int dim) {
+  Gil g;
+  PyObject* a = in_desc(input_type, A);
+  if (!a) return fail();
+  PyObject* o = out_desc(output_type, SA);
+  if (!o) {
+    Py_DECREF(a);
+    return fail();
+  }
+  PyObject* r = call("apply_sketch", Py_BuildValue("(OsNsNi)", S->obj, input_type, a, output_type, o, dim));
+  if (!r) return fail();
+  Py_DECREF(r);
+  return 0;
+}
+
+// --------------------------------------------------------------------- NLA
+SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, char* S_type, void* Sv, char* V_type,
+                               void* V, uint16_t k, char* params, sl_context_t* ctxt) {
+  Gil g;
+  (void)U_type;
+  (void)S_type;
+  (void)V_type;
+  PyObject* a = in_desc(A_type, A);
+  if (!a) return fail();
+  PyObject* r = call("approximate_svd", Py_BuildValue("(sNNNNisO)", A_type, a, dense_desc(U), dense_desc(Sv),
+                                                      dense_desc(V), (int)k, params ? params : "", ctxt->obj));
+  if (!r) return fail();
+  Py_DECREF(r);
+  return 0;
+}
+
+SL_CAPI int sl_approximate_symmetric_svd(char* A_type, void* A, char* S_type, void* Sv, char* V_type, void* V,
+                                         uint16_t k, char* params, sl_context_t* ctxt) {
+  Gil g;
+  (void)S_type;
+  (void)V_type;
+  PyObject* a = in_desc(A_type, A);
+  if (!a) return fail();
+  PyObject* r = call("approximate_symmetric_svd", Py_BuildValue("(sNNNisO)", A_type, a, dense_desc(Sv),
+                                                                dense_desc(V), (int)k, params ? params : "",
+                                                                ctxt->obj));
+  if (!r) return fail();
+  Py_DECREF(r);
+  return 0;
+}
+
+SL_CAPI int sl_faster_least_squares(int orientation, char* A_type, void* A, char* B_type, void* B, char* X_type,
+                                    void* X, char* params, sl_context_t* ctxt) {
+  Gil g;
+  (void)B_type;
+  (void)X_type;
+  PyObject* a = in_desc(A_type, A);
+  if (!a) return fail();
+  PyObject* r = call("faster_least_squares", Py_BuildValue("(isNNNsO)", orientation, A_type, a, dense_desc(B),
+                                                           dense_desc(X), params ? params : "", ctxt->obj));
+  if (!r) return fail();
+  Py_DECREF(r);
+  return 0;
+}
+
+// ----------------------------------------------------------------- kernels
+SL_CAPI int sl_create_kernel(char* type, int N, sl_kernel_t** kernel, ...) {
+  Gil g;
+  std::string spec = spec_of("kernel_param_spec", type);
+  va_list ap;
+  va_start(ap, kernel);
+  PyObject* params = varargs_tuple(spec, ap);
+  va_end(ap);
+  PyObject* r = call("create_kernel", Py_BuildValue("(siN)", type, N, params));
+  if (!r) return fail();
+  *kernel = new sl_kernel_t{r};
+  return 0;
+}
+
+SL_CAPI int sl_free_kernel(sl_kernel_t* k) {
+  if (!k) return 0;
+  Gil g;
+  Py_XDECREF(k->obj);
+  delete k;
+  return 0;
+}
+
+SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, void* X, char* Y_type, void* Y,
+                           char* K_type, void* K) {
+  Gil g;
+  (void)K_type;
+  PyObject* x = in_desc(X_type, X);
+  if (!x) return fail();
+  PyObject* y = in_desc(Y_type, Y);
+  if (!y) {
+    Py_DECREF(x);
+    return fail();
+  }
+  PyObject* r = call("kernel_gram", Py_BuildValue("(iiOsNsNN)", dirX, dirY, k->obj, X_type, x, Y_type, y,
+                                                  dense_desc(K)));
+  if (!r) return fail();
+  Py_DECREF(r);
+  return 0;
+}
+
+// ---------------------------------------------------------------------- IO
+SL_CAPI int sl_readlibsvm(char* fname, char* X_type, void* X, char* Y_type, void* Y, int direction, int min_d,
+                          int max_n) {
+  Gil g;
+  (void)Y_type;
+  PyObject* xo = out_desc(X_type, X);
+  if (!xo) return fail();
+  PyObject* yo = Y ? dense_desc(Y) : (Py_INCREF(Py_None), Py_None);
+  PyObject* r = call("readlibsvm", Py_BuildValue("(ssNNiii)", fname, X_type, xo, yo, direction, min_d, max_n));
+  if (!r) return fail();
+  Py_DECREF(r);
+  return 0;
+}

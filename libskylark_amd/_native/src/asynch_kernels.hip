@@ -63,8 +63,15 @@ SL_API int sl_asyrgs(const int64_t* rowptr, const void* col, int idx32, const vo
                      const double* B, double* X, int k, uint64_t seed, uint64_t base, int64_t nsteps, void* stream) {
   if (nsteps <= 0 || n <= 0) return SL_OK;
   hipStream_t s = (hipStream_t)stream;
-  // 4 waves per block; enough waves in flight to fill the chip, capped by work
-  int64_t waves = nsteps < 8192 ? nsteps : 8192;
+  // Concurrency bounds the staleness (delay) of the asynchronous updates: the
+  // IPDPS'14 analysis needs the number of in-flight updates to stay well
+  // below n, and two waves hitting the same coordinate double-apply its
+  // correction.  Allow ~n/64 concurrent waves (4 per block), at most 8192
+  // (enough to fill 256 CUs for large systems).
+  int64_t waves = n / 64;
+  if (waves < 1) waves = 1;
+  if (waves > 8192) waves = 8192;
+  if (waves > nsteps) waves = nsteps;
   unsigned grid = (unsigned)((waves + 3) / 4);
 #define SL_A(IT, VT) k_asyrgs<IT, VT><<<grid, 256, 0, s>>>(rowptr, (const IT*)col, (const VT*)val, n, B, X, k, seed, base, nsteps)
   if (vdtype == SL_F64) {

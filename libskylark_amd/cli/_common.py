@@ -1,0 +1,62 @@
+"""Shared plumbing for the command-line tools.
+
+Launch one process per GPU with ``torchrun`` (``--master-addr 127.0.0.1``);
+each rank binds ``cuda:LOCAL_RANK`` and joins the RCCL process group.  A plain
+``python -m libskylark_amd.cli.<tool>`` runs single-process (GPU 0 if present).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+
+from ..parallel.comm import init_distributed
+
+
+def setup(cpu: bool = False):
+    """Returns ``(comm, device)``."""
+    use_gpu = torch.cuda.is_available() and not cpu
+    comm = init_distributed(device="cuda" if use_gpu else "cpu")
+    if use_gpu:
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(lr)
+        dev = torch.device("cuda", lr)
+    else:
+        dev = torch.device("cpu")
+    return comm, dev
+
+
+class Timer:
+    def __init__(self, comm, verbose=True):
+        self.comm, self.verbose, self.t = comm, verbose, time.time()
+
+    def start(self, msg: str):
+        if self.verbose and self.comm.rank == 0:
+            print(msg, end="", flush=True)
+        self.t = time.time()
+
+    def done(self):
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if self.verbose and self.comm.rank == 0:
+            print(f"took {time.time() - self.t:.2e} sec", flush=True)
+
+
+def write_ascii(M: torch.Tensor, path: str):
+    """Elemental ``El::Write(..., ASCII)`` style: one matrix row per line."""
+    M = M.detach().to(torch.float64).cpu()
+    if M.dim() == 1:
+        M = M[:, None]
+    with open(path, "w") as f:
+        for row in M.tolist():
+            f.write(" ".join(f"{v:.17g}" for v in row) + "\n")
+
+
+def read_ascii(path: str) -> torch.Tensor:
+    rows = []
+    with open(path) as f:
+        for line in f:
+            if line.strip():
+                rows.append([float(x) for x in line.split()])
+    return torch.tensor(rows, dtype=torch.float64)
