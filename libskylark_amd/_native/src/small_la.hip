@@ -16,6 +16,7 @@
 
 namespace {
 constexpr int KM = 64;
+int g_chol_impl = 0;
 
 __global__ void __launch_bounds__(256)
 k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R, double* __restrict__ Rinv,
@@ -81,6 +82,80 @@ k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restric
   if (t == 0 && bad && status) atomicOr(status, 1);
 }
 
+// Single-wave variant (k <= K <= 64): lane i keeps row i of the matrix in
+// registers, every column broadcast is a pair of v_readlane_b32 (no LDS, no
+// barriers), loops fully unrolled over the compile-time K.  Right-looking
+// Cholesky, then X = L^{-1} by right-looking elimination, R = L^T, R^{-1} = X^T.
+__device__ __forceinline__ double bcast(double v, int src) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, src);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), src);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_wave_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R, double* __restrict__ Rinv,
+                float* __restrict__ Rinv32, int* __restrict__ status) {
+  const int i = threadIdx.x;
+  double a[K], x[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    double v = 0.0;
+    if (i < k && c < k) v = 0.5 * (G[i * ldg + c] + G[c * ldg + i]);
+    else if (i == c) v = 1.0;  // identity padding keeps the factorisation regular
+    a[c] = v;
+    x[c] = (i == c) ? 1.0 : 0.0;
+  }
+  double dmax = 0.0;
+#pragma unroll
+  for (int c = 0; c < K; ++c) dmax = fmax(dmax, fabs(bcast(a[c], c)));
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double d = bcast(a[j], j);
+    if (!(d > 1e-14 * dmax)) {
+      bad |= (j < k);
+      d = 1e300;
+    }
+    const double piv = sqrt(d);
+    const double inv = 1.0 / piv;
+    if (i == j) a[j] = piv;
+    if (i > j) a[j] *= inv;
+#pragma unroll
+    for (int c = j + 1; c < K; ++c) {
+      const double lcj = bcast(a[j], c);
+      if (i > j) a[c] -= a[j] * lcj;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double ljj = bcast(a[j], j);
+    if (i == j) {
+#pragma unroll
+      for (int c = 0; c <= j; ++c) x[c] /= ljj;
+    }
+#pragma unroll
+    for (int c = 0; c <= j; ++c) {
+      const double xjc = bcast(x[c], j);
+      if (i > j) x[c] -= a[j] * xjc;
+    }
+  }
+  if (i < k) {
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      if (c < k) {
+        const double l = (c <= i) ? a[c] : 0.0;   // L[i][c] = R[c][i]
+        const double xi = (c <= i) ? x[c] : 0.0;  // X[i][c] = R^{-1}[c][i]
+        if (R) R[c * k + i] = l;
+        if (Rinv) Rinv[c * k + i] = xi;
+        if (Rinv32) Rinv32[c * k + i] = (float)xi;
+      }
+    }
+  }
+  if (i == 0 && bad && status) atomicOr(status, 1);
+}
+
 __global__ void __launch_bounds__(256)
 k_small_matmul(const double* __restrict__ A, const double* __restrict__ B, double* __restrict__ C, int m, int kk,
                int n, float* __restrict__ C32) {
@@ -100,8 +175,24 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
     sl_set_last_error("small_chol_inv: 1 <= k <= 64");
     return SL_ERR_UNSUPPORTED;
   }
-  k_small_chol_inv<<<1, 256, 0, (hipStream_t)stream>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  hipStream_t s = (hipStream_t)stream;
+  if (g_chol_impl == 1)
+    k_small_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  else if (k <= 16)
+    k_wave_chol_inv<16><<<1, 64, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  else if (k <= 32)
+    k_wave_chol_inv<32><<<1, 64, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  else if (k <= 48)
+    k_wave_chol_inv<48><<<1, 64, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  else
+    k_wave_chol_inv<64><<<1, 64, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
   SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// tuning/testing hook: 0 = single-wave register kernel (default), 1 = LDS workgroup kernel
+SL_API int sl_small_chol_impl(int impl) {
+  g_chol_impl = impl;
   return SL_OK;
 }
 

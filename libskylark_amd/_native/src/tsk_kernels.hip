@@ -45,7 +45,7 @@ constexpr int THREADS = WAVES * 64;
 constexpr int BM = 16;
 constexpr int NBUF_DEFAULT = 4;
 int g_flags = 0;   // per-call mode bits (8: no Gram, 32: y_hi only)
-int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, bit3 step 4
+int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, bit3 step 4; bit6 nt loads
 
 // hardware round-to-nearest-even (v_cvt_pk_bf16_f32), NaN-preserving, branch-free
 __device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
@@ -61,6 +61,20 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+// same with the non-temporal policy (A is read exactly once per pass)
+__device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
@@ -159,7 +173,8 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       const bf16_t* src = A + grow * lda + col;
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           (unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-      glds16((const void*)src, dst);
+      if (ab & 64) glds16_nt((const void*)src, dst);
+      else glds16((const void*)src, dst);
     }
   };
 

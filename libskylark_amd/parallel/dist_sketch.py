@@ -30,11 +30,11 @@ COLUMNWISE, ROWWISE = 0, 1
 
 
 def _kind(sk):
-    if hasattr(sk, "linear_local_shard"):
-        return "feature"
     name = sk.sketch_type
     if name in ("PPT", "FastGaussianRFT", "FastMaternRFT"):
         return "local_only"
+    if hasattr(sk, "linear_local_shard"):
+        return "feature"
     if name == "FJLT":
         from ..sketch.fjlt import DIRECT_MAX_S
         return "linear" if sk.getsketchdim() <= DIRECT_MAX_S else "local_only"
@@ -116,8 +116,9 @@ def _partial_and_reduce(sk, A: DistMatrix, dim, kind, out_layout, out_shape):
 
     if A.layout == "MC_MR":
         g = A.grid
-        # partial covers S x (my column tiles): reduce over the grid column
-        g.col_comm.all_reduce(part)
+        # the sketched dimension is spread over grid rows (columnwise: sum over
+        # the grid-column communicator) or grid columns (rowwise: grid-row comm)
+        (g.col_comm if dim == COLUMNWISE else g.row_comm).all_reduce(part)
         if finish is not None:
             part = finish(part)
         if dim == COLUMNWISE:

@@ -7,8 +7,19 @@ from libskylark_amd.ops import small_la as SL
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("k", [1, 7, 40, 64])
-def test_chol_inv(dev, k):
+@pytest.fixture(params=[0, 1], ids=["wave", "lds"])
+def impl(request):
+    import ctypes
+    from libskylark_amd.ops import _lib
+    lib = _lib.require()
+    lib.sl_small_chol_impl.argtypes = [ctypes.c_int]
+    lib.sl_small_chol_impl(request.param)
+    yield request.param
+    lib.sl_small_chol_impl(0)
+
+
+@pytest.mark.parametrize("k", [1, 7, 16, 17, 33, 40, 48, 64])
+def test_chol_inv(dev, k, impl):
     X = torch.randn(3 * k + 5, k, dtype=torch.float64)
     G = X.t() @ X
     st = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -20,7 +31,7 @@ def test_chol_inv(dev, k):
     torch.testing.assert_close(Ri32.cpu().double(), Ri.cpu(), rtol=1e-6, atol=1e-6)
 
 
-def test_chol_inv_flags_breakdown(dev):
+def test_chol_inv_flags_breakdown(dev, impl):
     G = torch.zeros(5, 5, dtype=torch.float64, device=dev)
     G[0, 0] = 1
     st = torch.zeros(1, dtype=torch.int32, device=dev)
