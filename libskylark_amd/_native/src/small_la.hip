@@ -13,10 +13,11 @@
 // Reference counterpart: El::Cholesky / El::Trsm on [*,*] matrices inside
 // nla/svd.hpp and ml/krr.hpp.
 #include "sl_common.hpp"
+#include <stdlib.h>
 
 namespace {
 constexpr int KM = 64;
-int g_chol_impl = 0;
+int g_chol_impl = -1;  // -1: read SL_CHOL_IMPL once (default 0)
 
 __global__ void __launch_bounds__(256)
 k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R, double* __restrict__ Rinv,
@@ -82,74 +83,79 @@ k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restric
   if (t == 0 && bad && status) atomicOr(status, 1);
 }
 
-// Single-wave variant (k <= K <= 64): lane i keeps row i of the matrix in
-// registers, every column broadcast is a pair of v_readlane_b32 (no LDS, no
-// barriers), loops fully unrolled over the compile-time K.  Right-looking
-// Cholesky, then X = L^{-1} by right-looking elimination, R = L^T, R^{-1} = X^T.
-__device__ __forceinline__ double bcast(double v, int src) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, src);
-  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), src);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
+// Single-wave variant (k <= K <= 64), no barriers:
+//   Cholesky: lane i keeps row i of the matrix in registers; per column j the
+//   pivot column is published through a 64-double LDS vector and read back as
+//   wave-uniform (broadcast) LDS reads, so the k dependent steps cost a few
+//   LDS round trips each instead of long v_readlane chains.
+//   Inverse:  L is written to LDS once; lane c then forward-substitutes
+//   column c of X = L^{-1} (all columns in parallel) with broadcast reads of
+//   L.  R = L^T, R^{-1} = X^T.  Loops are unrolled over the compile-time K so
+//   the per-lane rows stay in registers.
 template <int K>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_wave_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R, double* __restrict__ Rinv,
                 float* __restrict__ Rinv32, int* __restrict__ status) {
+  __shared__ double colv[64];
+  __shared__ double L[K][K + 1];
   const int i = threadIdx.x;
-  double a[K], x[K];
+  double a[K];
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     double v = 0.0;
     if (i < k && c < k) v = 0.5 * (G[i * ldg + c] + G[c * ldg + i]);
     else if (i == c) v = 1.0;  // identity padding keeps the factorisation regular
     a[c] = v;
-    x[c] = (i == c) ? 1.0 : 0.0;
   }
+  // max diagonal (for the relative pivot test)
+  double diag = 0.0;
+#pragma unroll
+  for (int c = 0; c < K; ++c)
+    if (i == c) diag = a[c];
+  colv[i] = fabs(diag);
   double dmax = 0.0;
 #pragma unroll
-  for (int c = 0; c < K; ++c) dmax = fmax(dmax, fabs(bcast(a[c], c)));
+  for (int c = 0; c < K; ++c) dmax = fmax(dmax, colv[c]);
   int bad = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    double d = bcast(a[j], j);
+    colv[i] = a[j];
+    double d = colv[j];
     if (!(d > 1e-14 * dmax)) {
       bad |= (j < k);
       d = 1e300;
     }
     const double piv = sqrt(d);
-    const double inv = 1.0 / piv;
-    if (i == j) a[j] = piv;
-    if (i > j) a[j] *= inv;
+    const double lij = (i == j) ? piv : a[j] / piv;
+    a[j] = (i >= j) ? lij : a[j];
+    colv[i] = lij;
 #pragma unroll
     for (int c = j + 1; c < K; ++c) {
-      const double lcj = bcast(a[j], c);
-      if (i > j) a[c] -= a[j] * lcj;
+      const double lcj = colv[c];
+      if (i > j) a[c] -= lij * lcj;
     }
   }
+  if (i < K) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const double ljj = bcast(a[j], j);
-    if (i == j) {
+    for (int c = 0; c < K; ++c) L[i][c] = (c <= i) ? a[c] : 0.0;
+  }
+  // column c = i of X = L^{-1}: x_r = (delta_rc - sum_{c<=s<r} L[r][s] x_s) / L[r][r]
+  double x[K];
 #pragma unroll
-      for (int c = 0; c <= j; ++c) x[c] /= ljj;
-    }
+  for (int r = 0; r < K; ++r) {
+    double acc = (r == i) ? 1.0 : 0.0;
 #pragma unroll
-    for (int c = 0; c <= j; ++c) {
-      const double xjc = bcast(x[c], j);
-      if (i > j) x[c] -= a[j] * xjc;
-    }
+    for (int s2 = 0; s2 < r; ++s2) acc -= L[r][s2] * x[s2];
+    x[r] = (r >= i) ? acc / L[r][r] : 0.0;
   }
   if (i < k) {
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       if (c < k) {
-        const double l = (c <= i) ? a[c] : 0.0;   // L[i][c] = R[c][i]
-        const double xi = (c <= i) ? x[c] : 0.0;  // X[i][c] = R^{-1}[c][i]
+        const double l = (c <= i) ? a[c] : 0.0;  // L[i][c] = R[c][i]
         if (R) R[c * k + i] = l;
-        if (Rinv) Rinv[c * k + i] = xi;
-        if (Rinv32) Rinv32[c * k + i] = (float)xi;
+        if (Rinv) Rinv[i * k + c] = x[c];      // X[c][i] = R^{-1}[i][c]
+        if (Rinv32) Rinv32[i * k + c] = (float)x[c];
       }
     }
   }
@@ -176,6 +182,10 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (g_chol_impl < 0) {
+    const char* e = getenv("SL_CHOL_IMPL");
+    g_chol_impl = e ? atoi(e) : 0;
+  }
   if (g_chol_impl == 1)
     k_small_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
   else if (k <= 16)

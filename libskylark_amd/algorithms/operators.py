@@ -147,7 +147,7 @@ class DistSymOp(DistRowOp):
 
     def matmul(self, X):
         if self.distributed:
-            counts = [e - s for s, e in self.D.row_blocks()]
+            counts = self.D.row_counts()
             X = self.comm.all_gather_v(X.contiguous(), counts, dim=0)
         return self.inner.matmul(X)
 

@@ -72,7 +72,7 @@ class _Data:
                                D.comm).redistribute("VC_STAR")
             self.local, self.comm, self.n, self.D = D.local, D.comm, D.shape[0], D
         else:
-            self.local, self.comm, self.D = _points(X, direction), Comm(None), None
+            self.local, self.comm, self.D = _points(X, direction), Comm.single(), None
             self.n = self.local.shape[0]
         self.distributed = self.comm.size > 1
 
@@ -125,7 +125,7 @@ def kernel_ridge(k: Kernel, X, Y, lam: float, direction="rows", params: KrrParam
     if data.distributed:
         Kd = k.gram(data.D)
         K = Kd.to_global()
-        Yg = data.comm.all_gather_v(data.rows_of(Y).contiguous(), [e - s for s, e in data.D.row_blocks()])
+        Yg = data.comm.all_gather_v(data.rows_of(Y).contiguous(), data.D.row_counts())
     else:
         K = k.symmetric_gram(data.local)
         Yg = data.rows_of(Y)

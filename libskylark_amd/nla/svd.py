@@ -237,7 +237,8 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
         with prof.phase("svd.allreduce_small"):
             comm.all_reduce(W)
         with prof.phase("svd.orth"):
-            Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-30) if params.skip_qr else SL.cholqr2(W, status)
+            # only the subspace matters between passes: one CholeskyQR step
+            Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-30) if params.skip_qr else SL.cholqr(W, status)
     with prof.phase("svd.fused_pass"):
         W, G, Y = T.fused_pass(A_loc, Z, keep_y=True, gram=True, exact=True)
     with prof.phase("svd.allreduce_small"):

@@ -47,6 +47,13 @@ class Comm:
         else:
             self.rank, self.size, self.backend, self._active = 0, 1, None, False
 
+    @classmethod
+    def single(cls) -> "Comm":
+        """A one-rank communicator that never communicates (process-local data)."""
+        c = cls.__new__(cls)
+        c.group, c.rank, c.size, c.backend, c._active = None, 0, 1, None, False
+        return c
+
     @property
     def is_root(self):
         return self.rank == 0

@@ -30,7 +30,7 @@ import math
 
 import torch
 
-from .comm import Comm, balanced_offsets, world
+from .comm import balanced_counts, Comm, balanced_offsets, world
 
 LAYOUTS = ("STAR_STAR", "CIRC_CIRC", "VC_STAR", "VR_STAR", "STAR_VC", "STAR_VR", "MC_MR")
 ALIASES = {"SharedMatrix": "STAR_STAR", "RootMatrix": "CIRC_CIRC", "DistMatrix": "MC_MR",
@@ -136,6 +136,10 @@ class DistMatrix:
         rank = self.comm.rank if rank is None else rank
         off = balanced_offsets(self.shape[1], self.comm.size)
         return off[rank], off[rank + 1]
+
+    def row_counts(self):
+        """Rows held by every rank, for the 1-D row layouts ([VC,*]/[VR,*])."""
+        return balanced_counts(self.shape[0], self.comm.size)
 
     def row_blocks(self):
         """Global row ranges held locally (in local order)."""
