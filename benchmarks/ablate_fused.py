@@ -3,6 +3,11 @@
 Results are wrong in ablated runs by design; only the timing matters."""
 from __future__ import annotations
 
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
 import ctypes as C
 import statistics
 import sys

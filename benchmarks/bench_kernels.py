@@ -6,6 +6,11 @@ bytes the kernel must move.
 """
 from __future__ import annotations
 
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
 import argparse
 import ctypes as C
 import json

@@ -2,6 +2,11 @@
 (k x k Cholesky/inverse implementations, CholeskyQR2 of an n x k iterate)."""
 from __future__ import annotations
 
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
 import ctypes as C
 import statistics
 
@@ -35,7 +40,7 @@ def main():
     for k in (16, 40, 64):
         X = torch.randn(4 * k, k, dtype=torch.float64, device=dev)
         G = X.t() @ X
-        for impl, name in ((0, "wave"), (1, "lds")):
+        for impl, name in ((0, "wave"), (1, "lds"), (2, "roll")):
             lib.sl_small_chol_impl(impl)
             us = timeit(lambda: SL.chol_inv(G, st))
             print(f"chol_inv k={k:2d} {name:4s} {us:8.1f} us", flush=True)

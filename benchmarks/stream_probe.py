@@ -3,6 +3,11 @@
 compute steps ablated or not.  Timing only (ablated results are wrong)."""
 from __future__ import annotations
 
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
 import ctypes as C
 import statistics
 import time
