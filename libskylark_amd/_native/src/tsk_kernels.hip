@@ -185,10 +185,12 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
   for (int p = 0; p < PD; ++p)
     if (b0 + p * bstep < nblocks) issue(b0 + p * bstep, p);
 
+  // blocks this workgroup owns (one 64-bit division, outside the loop)
+  const int64_t nloc = b0 < nblocks ? (nblocks - 1 - b0) / bstep + 1 : 0;
   for (int64_t blk = b0; blk < nblocks; blk += bstep, ++my) {
     const int buf = (int)(my % NBUF);
     // blocks issued after this one and still possibly in flight: min(PD-1, remaining)
-    const int64_t rem = (nblocks - 1 - blk) / bstep;
+    const int64_t rem = nloc - 1 - my;
     const int younger = (int)(rem < PD - 1 ? rem : PD - 1);
     if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GG::LPB) : "memory");
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GG::LPB) : "memory");
@@ -226,20 +228,30 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     {
       constexpr int CPW = GG::KP / WAVES;  // columns reduced per wave
       const int64_t r0 = blk * BM;
+      const bool full = r0 + BM <= m;        // wave-uniform: only the last block is ragged
       if (lane < CPW * 4) {
         const int col = w * CPW + (lane >> 2), rg = lane & 3;
         f32x4 sum = *(const f32x4*)&yp[col * BM + 4 * rg];
 #pragma unroll
         for (int v = 1; v < WAVES; ++v) sum += *(const f32x4*)&yp[(v * GG::KP + col) * BM + 4 * rg];
+        if (!full) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (r0 + 4 * rg + j >= m) sum[j] = 0.f;
+          for (int j = 0; j < 4; ++j)
+            if (r0 + 4 * rg + j >= m) sum[j] = 0.f;
+        }
         *(f32x4*)&yf[col * BM + 4 * rg] = sum;
         if constexpr (STORE_Y) {
-          if (col < k)
+          if (col < k) {
+            float* yrow = Y + (r0 + 4 * rg) * ldy + col;
+            if (full) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (r0 + 4 * rg + j < m) Y[(r0 + 4 * rg + j) * ldy + col] = sum[j];
+              for (int j = 0; j < 4; ++j) yrow[j * ldy] = sum[j];
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (r0 + 4 * rg + j < m) yrow[j * ldy] = sum[j];
+            }
+          }
         }
       }
     }
@@ -285,20 +297,14 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     if (need_g) {
       // ---- step 4: G tiles tau = w + 8 s (t1 = tau / KT, t2 = tau % KT):
       //      hi*hi + hi*lo + lo*hi
+      // tile indices are compile-time; only the owner test (wave-uniform) is runtime
 #pragma unroll
-      for (int s = 0; s < GG::GS; ++s) {
-        const int tau = w + WAVES * s;
-        if (tau < GG::GTILES) {
-          const int t1 = tau / KT, t2 = tau % KT;
-          s16x4 ah = yh[0], al = yl[0], bh = yh[0], bl = yl[0];
-#pragma unroll
-          for (int t = 1; t < KT; ++t) {
-            if (t1 == t) { ah = yh[t]; al = yl[t]; }
-            if (t2 == t) { bh = yh[t]; bl = yl[t]; }
-          }
-          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, accG[s], 0, 0, 0);
-          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, accG[s], 0, 0, 0);
-          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, accG[s], 0, 0, 0);
+      for (int tau = 0; tau < GG::GTILES; ++tau) {
+        if ((tau % WAVES) == w) {
+          const int s = tau / WAVES, t1 = tau / KT, t2 = tau % KT;
+          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(yh[t1], yh[t2], accG[s], 0, 0, 0);
+          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(yh[t1], yl[t2], accG[s], 0, 0, 0);
+          accG[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(yl[t1], yh[t2], accG[s], 0, 0, 0);
         }
       }
     }
