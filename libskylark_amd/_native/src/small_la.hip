@@ -83,6 +83,83 @@ k_small_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restric
   if (t == 0 && bad && status) atomicOr(status, 1);
 }
 
+// Workgroup variant with ONE barrier per elimination step.  Cholesky: step j
+// reads the (already updated) pivot a[j][j], updates the trailing matrix
+// from the UNSCALED column j (a[i][c] -= a[i][j] a[c][j] / d), and scales
+// column j of the previous step (never read again) in the same phase.
+// Inverse X = L^{-1}: step j subtracts L[i][j] * (x[j][c] / L[j][j]) from the
+// rows below using the unscaled row j, and scales row j-1 meanwhile.
+__global__ void __launch_bounds__(256)
+k_small_chol_inv1b(const double* __restrict__ G, int k, int ldg, double* __restrict__ R, double* __restrict__ Rinv,
+                   float* __restrict__ Rinv32, int* __restrict__ status) {
+  __shared__ double a[KM][KM + 1];
+  __shared__ double x[KM][KM + 1];
+  const int t = threadIdx.x;
+  for (int e = t; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    a[i][j] = 0.5 * (G[i * ldg + j] + G[j * ldg + i]);
+    x[i][j] = (i == j) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  double dmax = 0.0;
+  for (int i = 0; i < k; ++i) dmax = fmax(dmax, fabs(a[i][i]));
+  int bad = 0;
+  double pinv_prev = 0.0;  // 1/sqrt(d_{j-1}) for the deferred column scaling
+  for (int j = 0; j <= k; ++j) {
+    double d = 1.0, dinv = 0.0, pinv = 0.0;
+    if (j < k) {
+      d = a[j][j];
+      if (!(d > 1e-14 * dmax)) {
+        bad = 1;
+        d = 1e300;
+      }
+      dinv = 1.0 / d;
+      pinv = sqrt(dinv);
+    }
+    // deferred scaling of column j-1 (rows > j-1) and its pivot
+    if (j > 0) {
+      const int jp = j - 1;
+      for (int i = jp + 1 + t; i < k; i += 256) a[i][jp] *= pinv_prev;
+      if (t == 0) a[jp][jp] = 1.0 / pinv_prev;  // sqrt(d) (or 1e150 for a killed pivot)
+    }
+    if (j < k) {
+      const int rem = k - j - 1;
+      for (int e = t; e < rem * rem; e += 256) {
+        const int i = j + 1 + e / rem, c = j + 1 + e % rem;
+        if (c <= i) a[i][c] -= a[i][j] * a[c][j] * dinv;
+      }
+    }
+    pinv_prev = pinv;
+    __syncthreads();
+  }
+  // a now holds L (lower, diagonal sqrt(d_j)).
+  for (int j = 0; j <= k; ++j) {
+    if (j > 0) {  // scale row j-1 of X by 1 / L[j-1][j-1]
+      const int jp = j - 1;
+      const double inv = 1.0 / a[jp][jp];
+      for (int c = t; c <= jp; c += 256) x[jp][c] *= inv;
+    }
+    if (j < k) {
+      const double inv = 1.0 / a[j][j];
+      const int rows = k - j - 1, cols = j + 1;
+      for (int e = t; e < rows * cols; e += 256) {
+        const int i = j + 1 + e / cols, c = e % cols;
+        x[i][c] -= a[i][j] * (x[j][c] * inv);
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    const double r = (j >= i) ? a[j][i] : 0.0;
+    if (R) R[i * k + j] = r;
+    const double xi = (j >= i) ? x[j][i] : 0.0;  // R^{-1}[i][j] = (L^{-1})[j][i]
+    if (Rinv) Rinv[i * k + j] = xi;
+    if (Rinv32) Rinv32[i * k + j] = (float)xi;
+  }
+  if (t == 0 && bad && status) atomicOr(status, 1);
+}
+
 // Single-wave variant (k <= K <= 64), no barriers:
 //   Cholesky: lane i keeps row i of the matrix in registers; per column j the
 //   pivot column is published through a 64-double LDS vector and read back as
@@ -245,9 +322,11 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
   // measured on MI355X (rocprof, k x k f64): k<=16 single wave 10 us; k=40:
   // workgroup 61 us vs wave 57; k=64: wave 95 vs workgroup 121 -> pick per size
   int impl = g_chol_impl;
-  if (impl == 0) impl = (k <= 16 || k > 48) ? 3 : 1;
+  if (impl == 0) impl = (k <= 16 || k > 48) ? 3 : 4;
   if (impl == 1)
     k_small_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  else if (impl == 4)
+    k_small_chol_inv1b<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
   else if (impl == 2)
     k_wave_chol_inv_rolled<<<1, 64, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
   else if (k <= 16)
@@ -263,7 +342,7 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
 }
 
 // tuning/testing hook: 0 = auto (default), 1 = LDS workgroup kernel, 2 = single-wave rolled LDS
-// kernel, 3 = single-wave register kernel
+// kernel, 3 = single-wave register kernel, 4 = one-barrier-per-step workgroup kernel
 SL_API int sl_small_chol_impl(int impl) {
   g_chol_impl = impl;
   return SL_OK;

@@ -251,23 +251,30 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
         _, G2 = T.f32_xm(Y, R1i32, store=False, gram=True)
         comm.all_reduce(G2)
         R2, R2i, _ = SL.chol_inv(G2, status)
-        Rti = SL.small_matmul(R1i, R2i)          # Rt^{-1} = R1^{-1} R2^{-1}
-        Vt = SL.small_matmul(W, Rti)             # A^T Q, Q = Y Rt^{-1}
+        Rti = R1i @ R2i                          # Rt^{-1} = R1^{-1} R2^{-1}  (k x k, f64)
     with prof.phase("svd.small_svd"):
-        # A^T Q = Qv Rv (device CholeskyQR2), then only the k x k SVD on the host
-        Qv, Rv = SL.cholqr2(Vt, status, want_r=True)
-        host = torch.cat([Rv.reshape(-1), status.double()]).cpu().numpy()
+        # B^T = A^T Q = W Rt^{-1} (n x k).  Its right singular pairs come from the
+        # k x k f64 Gram  C = Rt^{-T} (W^T W) Rt^{-1} = Ub S^2 Ub^T: one host
+        # eigensolve, no further factorisation on the device.  (sigma_i keeps
+        # relative accuracy ~eps64 (sigma_1/sigma_i)^2: far below the bf16 data
+        # error for every rank the sketch can resolve.)
+        Vt = W @ Rti
+        C = Vt.t() @ Vt
+        host = torch.cat([C.reshape(-1), status.double()]).cpu().numpy()
         if host[-1] != 0:
             ctx.seed, ctx.counter = ctx0.seed, ctx0.counter
             return None
-        Ur, s, Vrt = np.linalg.svd(host[:k * k].reshape(k, k))
-        small = torch.from_numpy(np.concatenate([Ur[:, :rank].reshape(-1), Vrt.T[:, :rank].reshape(-1),
-                                                 s[:rank]])).to(dev)
-        Ur_d = small[:k * rank].view(k, rank)
-        Vr_d = small[k * rank:2 * k * rank].view(k, rank)
-        s_d = small[2 * k * rank:].float()
-        V_d = SL.small_matmul(Qv.double(), Ur_d).float()    # V = Qv Ur_r
-        M_d = SL.small_matmul(Rti, Vr_d).float()            # U = Y Rt^{-1} Vr_r
+        Cm = host[:k * k].reshape(k, k)
+        evals, evecs = np.linalg.eigh(0.5 * (Cm + Cm.T))
+        order = np.argsort(evals)[::-1][:rank]
+        s = np.sqrt(np.clip(evals[order], 0.0, None))
+        Ub = evecs[:, order]
+        small = torch.from_numpy(np.concatenate([Ub.reshape(-1), s])).to(dev)
+        Ub_d = small[:k * rank].view(k, rank)
+        s64 = small[k * rank:]
+        V_d = ((Vt @ Ub_d) / s64.clamp_min(1e-300)).float()   # V = A^T Q Ub S^{-1}
+        M_d = (Rti @ Ub_d).float()                            # U = Y Rt^{-1} Ub
+        s_d = s64.float()
     with prof.phase("svd.form_U"):
         U, _ = T.f32_xm(Y, M_d, store=True)
     return U, s_d, V_d
