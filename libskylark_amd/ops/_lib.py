@@ -41,6 +41,7 @@ SIGNATURES = {
     "sl_halton": [vp, vp, i64, i64, i64, i64, vp],
     "sl_halton_host": [vp, vp, i64, i64, i64, i64],
     "sl_uniform_prefix_host": [vp, u64, u64, i64],
+    "sl_dct2_rows": [vp, i64, i64, vp, f64, vp, i32, i64, i32, vp],
 }
 _RESTYPE = {"sl_last_error": cp}
 

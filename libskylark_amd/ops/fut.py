@@ -96,10 +96,28 @@ def wht(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
 FUTS = {"DCT": (dct2, dct3), "DHT": (dht, dht), "WHT": (wht, wht)}
 
 
-def dct2_rows_matrix(N: int, rows: torch.Tensor, dtype=torch.float64, device=None) -> torch.Tensor:
-    """Explicit rows ``rows`` of the orthonormal DCT-II matrix (len(rows) x N)."""
-    k = rows.to(device=device, dtype=dtype)[:, None]
-    n = torch.arange(N, device=device, dtype=dtype)[None, :]
-    F = torch.cos(math.pi * k * (2 * n + 1) / (2 * N)) * math.sqrt(2.0 / N)
-    F[rows.to(device) == 0] *= math.sqrt(0.5)
-    return F
+def dct2_rows_matrix(N: int, rows: torch.Tensor, dtype=torch.float64, device=None, d: torch.Tensor | None = None,
+                     scale: float = 1.0, transpose: bool = False) -> torch.Tensor:
+    """Explicit rows ``rows`` of the orthonormal DCT-II matrix (len(rows) x N),
+    optionally times ``scale * diag(d)`` on the right; ``transpose`` returns the
+    N x len(rows) layout.  On the GPU one native launch (``sl_dct2_rows``)."""
+    dev = torch.device(device) if device is not None else rows.device
+    S = rows.numel()
+    if dev.type == "cuda" and dtype in (torch.float32, torch.float64, torch.bfloat16):
+        from . import _lib
+        _lib.require()
+        r = rows.to(device=dev, dtype=torch.int64).contiguous()
+        dd = d.to(device=dev, dtype=torch.float64).contiguous() if d is not None else None
+        out = torch.empty((N, S) if transpose else (S, N), dtype=dtype, device=dev)
+        _lib.call("sl_dct2_rows", _lib.ptr(r), S, N, _lib.ptr(dd) if dd is not None else None, float(scale),
+                  _lib.ptr(out), _lib.dtype_code(dtype), out.stride(0), int(transpose), _lib.stream_of(out))
+        return out
+    k = rows.to(device=dev, dtype=torch.float64)[:, None]
+    n = torch.arange(N, device=dev, dtype=torch.float64)[None, :]
+    ang = torch.remainder(k * (2 * n + 1), 4 * N) * (math.pi / (2 * N))
+    F = torch.cos(ang) * torch.where(k == 0, math.sqrt(1.0 / N), math.sqrt(2.0 / N))
+    if d is not None:
+        F = F * d.to(device=dev, dtype=torch.float64)[None, :]
+    F = F * scale
+    F = F.t() if transpose else F
+    return F.to(dtype).contiguous()

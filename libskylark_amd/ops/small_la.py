@@ -44,11 +44,11 @@ def small_matmul(A: torch.Tensor, B: torch.Tensor, want32: bool = False):
     return (Cm, C32) if want32 else Cm
 
 
-def cholqr(W: torch.Tensor, status: torch.Tensor | None = None):
+def cholqr(W: torch.Tensor, status: torch.Tensor | None = None, ws: torch.Tensor | None = None):
     """One CholeskyQR step (basis of the column space, orthonormal to ~eps*cond(W)):
     enough to re-condition an intermediate power-iteration block."""
     W = W.float().contiguous()
-    _, G1 = T.f32_xm(W, None, store=False, gram=True)
+    _, G1 = T.f32_xm(W, None, store=False, gram=True, ws=ws)
     _, _, R1i = chol_inv(G1, status)
     Q, _ = T.f32_xm(W, R1i, store=True)
     return Q

@@ -67,7 +67,7 @@ _WS = FusedWorkspace()
 
 
 def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: bool = True,
-               exact: bool = True):
+               exact: bool = True, ws: torch.Tensor | None = None):
     """Return ``(W, G, Y)`` with ``Y = A Z``, ``W = A^T Y`` (n x k), ``G = Y^T Y`` (k x k).
 
     W and G are float32 (A bf16/fp32) or float64 (A fp64); Y is float32/64 or
@@ -79,7 +79,7 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
     m, n = A.shape
     k = Z.shape[1]
     if _native_ok(A, k):
-        return _fused_native(A, Z, keep_y, gram, exact)
+        return _fused_native(A, Z, keep_y, gram, exact, ws)
     wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
     # low-precision A: Z is rounded to A's dtype (as the MFMA kernel does) and
     # the products are formed in f32
@@ -105,7 +105,16 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
     return W, G, Y
 
 
-def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool, gram: bool = True, exact: bool = True):
+def fused_workspace_bytes(m: int, n: int, k: int) -> int:
+    return max(int(_lib.require().sl_tsk_fused_workspace(m, n, k)), 16)
+
+
+def f32_workspace_bytes(m: int) -> int:
+    return int(_lib.require().sl_tsk_f32_workspace(m))
+
+
+def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool, gram: bool = True, exact: bool = True,
+                  ws: torch.Tensor | None = None):
     m, n = A.shape
     k = Z.shape[1]
     dev = A.device
@@ -113,8 +122,8 @@ def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool, gram: bool = T
     W = torch.empty(n, k, dtype=torch.float32, device=dev)
     G = torch.empty(k, k, dtype=torch.float32, device=dev)
     Y = torch.empty(m, k, dtype=torch.float32, device=dev) if keep_y else None
-    nbytes = int(_lib.require().sl_tsk_fused_workspace(m, n, k))
-    ws = _WS.get(dev, max(nbytes, 16))
+    if ws is None:
+        ws = _WS.get(dev, fused_workspace_bytes(m, n, k))
     _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zb), k, _lib.ptr(W), _lib.ptr(G),
               _lib.ptr(Y) if Y is not None else None, 0 if Y is None else Y.stride(0), _lib.ptr(ws),
               (0 if gram else 1) | (0 if exact else 2), vp(_lib.stream_of(A)))
@@ -126,7 +135,8 @@ _lib.register("sl_tsk_f32_workspace", [i64], C.c_int64)
 _WS32 = FusedWorkspace()
 
 
-def f32_xm(Y: torch.Tensor, M: torch.Tensor | None = None, store: bool = True, gram: bool = False):
+def f32_xm(Y: torch.Tensor, M: torch.Tensor | None = None, store: bool = True, gram: bool = False,
+           ws: torch.Tensor | None = None):
     """``Q = Y M`` (``M=None``: ``Q = Y``) for tall f32 ``Y`` (k, k2 <= 64).
 
     Returns ``(Q or None, G or None)`` with ``G = Q^T Q`` in float64 (partial
@@ -138,7 +148,8 @@ def f32_xm(Y: torch.Tensor, M: torch.Tensor | None = None, store: bool = True, g
         Mc = None if M is None else M.to(device=Y.device, dtype=torch.float32).contiguous()
         out = torch.empty(m, k2, dtype=torch.float32, device=Y.device) if (store and M is not None) else None
         G = torch.empty(k2, k2, dtype=torch.float64, device=Y.device) if gram else None
-        ws = _WS32.get(Y.device, int(_lib.require().sl_tsk_f32_workspace(m))) if gram else None
+        if gram and ws is None:
+            ws = _WS32.get(Y.device, f32_workspace_bytes(m))
         _lib.call("sl_tsk_f32_xm", _lib.ptr(Y), m, k, Y.stride(0), _lib.ptr(Mc) if Mc is not None else None, k2,
                   _lib.ptr(out) if out is not None else None, out.stride(0) if out is not None else 0,
                   _lib.ptr(G) if G is not None else None, _lib.ptr(ws) if ws is not None else None,

@@ -57,11 +57,10 @@ class FJLT(SketchTransform):
         self.scale = math.sqrt(self._N / self._S)
         self._W = {}
 
-    def realize(self, dtype=torch.float64, device=None) -> torch.Tensor:
-        """Explicit ``S x N`` operator ``sqrt(N/S) P F D``."""
-        F = _fut.dct2_rows_matrix(self._N, self.samples, dtype=torch.float64, device=device)
-        W = self.scale * F * self.rfut.D.to(device=device, dtype=torch.float64)[None, :]
-        return W.to(dtype)
+    def realize(self, dtype=torch.float64, device=None, transpose: bool = False) -> torch.Tensor:
+        """Explicit ``S x N`` operator ``sqrt(N/S) P F D`` (``transpose``: its N x S transpose)."""
+        return _fut.dct2_rows_matrix(self._N, self.samples, dtype=dtype, device=device, d=self.rfut.D,
+                                     scale=self.scale, transpose=transpose)
 
     def _operator(self, device, dtype):
         key = (str(device), dtype)

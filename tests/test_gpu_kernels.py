@@ -81,3 +81,18 @@ def test_fastfood_and_ppt_gpu(dev):
     for T in (sk.sketch.FastGaussianRFT(32, 100, sigma=1.0, context=sk.Context(3)),
               sk.sketch.PPT(32, 128, q=3, context=sk.Context(3))):
         torch.testing.assert_close((T * X.to(dev)).cpu(), T * X, rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,S", [(1, 1), (1000, 40), (4099, 17)])
+def test_dct2_rows_native(dev, N, S):
+    from libskylark_amd.ops import fut
+    rows = torch.randint(0, N, (S,))
+    rows[0] = 0
+    d = torch.randint(0, 2, (N,)).double() * 2 - 1
+    ref = fut.dct2_rows_matrix(N, rows, dtype=torch.float64, d=d, scale=1.7)
+    for tr in (False, True):
+        got = fut.dct2_rows_matrix(N, rows, dtype=torch.float64, device=dev, d=d, scale=1.7, transpose=tr)
+        torch.testing.assert_close(got.cpu(), ref.t() if tr else ref, rtol=1e-12, atol=1e-12)
+    got32 = fut.dct2_rows_matrix(N, rows, dtype=torch.float32, device=dev, d=d, scale=1.7, transpose=True)
+    torch.testing.assert_close(got32.cpu().double(), ref.t(), rtol=1e-6, atol=1e-6)

@@ -133,3 +133,26 @@ def test_f32_xm_native(dev, m, k, k2):
     torch.testing.assert_close(G, Qr.t() @ Qr, rtol=1e-4, atol=1e-3)
     _, G1 = tallskinny.f32_xm(Y, None, store=False, gram=True)
     torch.testing.assert_close(G1, Y.double().t() @ Y.double(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_approximate_svd_graph_replay_matches_eager(dev):
+    """The hipGraph-replayed device plan gives the eager result (same context)."""
+    g = torch.Generator().manual_seed(4)
+    U0, _ = torch.linalg.qr(torch.randn(20000, 12, generator=g))
+    V0, _ = torch.linalg.qr(torch.randn(256, 12, generator=g))
+    s0 = torch.linspace(50, 5, 12)
+    A = ((U0 * s0) @ V0.t()).to(dev, torch.bfloat16)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT")
+    outs = []
+    for _ in range(4):  # call 1 eager, call 2 captures, calls 3-4 replay
+        U, s, V = sk.nla.approximate_svd(A, 8, context=sk.Context(9), params=p)
+        outs.append((U.cpu(), s.cpu(), V.cpu()))
+    for U, s, V in outs[1:]:
+        torch.testing.assert_close(s, outs[0][1], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(U.abs(), outs[0][0].abs(), rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(V.abs(), outs[0][2].abs(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(outs[0][1], s0[:8], rtol=2e-2, atol=2e-2)
+    # a different sketch (fresh context) still gives the same top spectrum
+    _, s2, _ = sk.nla.approximate_svd(A, 8, context=sk.Context(10), params=p)
+    torch.testing.assert_close(s2.cpu(), s0[:8], rtol=2e-2, atol=2e-2)
