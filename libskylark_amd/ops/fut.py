@@ -115,7 +115,9 @@ def dct2_rows_matrix(N: int, rows: torch.Tensor, dtype=torch.float64, device=Non
     k = rows.to(device=dev, dtype=torch.float64)[:, None]
     n = torch.arange(N, device=dev, dtype=torch.float64)[None, :]
     ang = torch.remainder(k * (2 * n + 1), 4 * N) * (math.pi / (2 * N))
-    F = torch.cos(ang) * torch.where(k == 0, math.sqrt(1.0 / N), math.sqrt(2.0 / N))
+    c0 = torch.tensor(math.sqrt(1.0 / N), dtype=torch.float64, device=dev)
+    c1 = torch.tensor(math.sqrt(2.0 / N), dtype=torch.float64, device=dev)
+    F = torch.cos(ang) * torch.where(k == 0, c0, c1)
     if d is not None:
         F = F * d.to(device=dev, dtype=torch.float64)[None, :]
     F = F * scale
