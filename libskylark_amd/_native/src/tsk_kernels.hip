@@ -340,27 +340,51 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
 }  // namespace
 
 // out[i][j] = sum_s slab[s][i][j]  (i < rows, j < cols <= 64) accumulated in f64.
-// One workgroup per output row; 4 slab groups x 64 columns, coalesced rows.
+// A 1024-thread workgroup owns 64 consecutive output elements; its 16 waves
+// split the slabs (wave g sums slabs g, g+16, ...), each lane of a wave on
+// consecutive elements of a slab row (coalesced), 4 slabs in flight per lane;
+// the 16 partials are combined through LDS.  Enough parallelism both for
+// the n x k W slabs and for the k x k Gram slabs.
 template <typename OT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 k_slab_reduce_rows(const float* __restrict__ slab, int nslab, int64_t slab_stride, int ld_in,
-                   int cols, OT* __restrict__ out, int ld_out) {
-  __shared__ double part[4][64];
-  const int i = blockIdx.x;
-  const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
-  double s = 0.0;
-  if (j < cols)
-    for (int b = g; b < nslab; b += 4) s += slab[b * slab_stride + (int64_t)i * ld_in + j];
-  part[g][j] = s;
+                   int cols, OT* __restrict__ out, int ld_out, int rows) {
+  __shared__ double part[16][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  const bool ok = t < (int64_t)rows * cols;
+  double acc = 0.0;
+  if (ok) {
+    const int64_t i = t / cols, j = t - i * cols;
+    const float* p = slab + i * ld_in + j;
+    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    int b = g;
+    for (; b + 48 < nslab; b += 64) {
+      a0 += p[(int64_t)b * slab_stride];
+      a1 += p[(int64_t)(b + 16) * slab_stride];
+      a2 += p[(int64_t)(b + 32) * slab_stride];
+      a3 += p[(int64_t)(b + 48) * slab_stride];
+    }
+    for (; b < nslab; b += 16) a0 += p[(int64_t)b * slab_stride];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  part[g][lane] = acc;
   __syncthreads();
-  if (g == 0 && j < cols) out[(int64_t)i * ld_out + j] = (OT)(part[0][j] + part[1][j] + part[2][j] + part[3][j]);
+  if (g == 0 && ok) {
+    double s = 0.0;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) s += part[v][lane];
+    const int64_t i = t / cols, j = t - i * cols;
+    out[i * ld_out + j] = (OT)s;
+  }
 }
 
 int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
                           int cols, float* out, int ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return SL_OK;
   if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
-  k_slab_reduce_rows<float><<<rows, 256, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out);
+  const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
+  k_slab_reduce_rows<float><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -369,7 +393,8 @@ int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride,
                               int cols, double* out, int ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return SL_OK;
   if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
-  k_slab_reduce_rows<double><<<rows, 256, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out);
+  const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
+  k_slab_reduce_rows<double><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

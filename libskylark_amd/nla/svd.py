@@ -20,6 +20,7 @@ bytes); if a Gram factorisation fails the code falls back to TSQR.
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import math
@@ -229,8 +230,9 @@ class _DevicePlan:
     the short kernels between the streaming passes no longer wait on host
     launch latency.  Graph inputs are static buffers (the sketch Z and the
     eigenpairs); A is read in place, so replays always see A's current
-    contents.  Outputs are cloned before they are returned.  Collectives
-    (RCCL) are captured too; if capture fails the plan stays eager.
+    contents.  Outputs are cloned before they are returned.  With more than
+    one rank the collectives stay eager unless SKH_GRAPH_COLLECTIVES=1
+    (RCCL capture); if a capture fails the plan stays eager.
     """
 
     def __init__(self, A_loc, comm, n, rank, k, q, skip_qr, use_graph):
@@ -367,7 +369,11 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     if plan is None:
         if len(_PLANS) >= 4:
             _PLANS.pop(next(iter(_PLANS)))
-        plan = _DevicePlan(A_loc, comm, n, rank, k, q, params.skip_qr, bool(params.graph) and dev.type == "cuda")
+        # multi-rank: capture collectives only on request — a capture that fails on
+        # one rank but not another would desynchronise the collectives
+        use_graph = bool(params.graph) and dev.type == "cuda" and (
+            comm.size == 1 or os.environ.get("SKH_GRAPH_COLLECTIVES", "0") == "1")
+        plan = _DevicePlan(A_loc, comm, n, rank, k, q, params.skip_qr, use_graph)
         _PLANS[key] = plan
     res = plan(Z)
     if res is None:
