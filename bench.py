@@ -53,7 +53,7 @@ def main(argv=None):
         return 2
     comm = init_distributed()
     if comm.size == 1:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     dev = torch.device("cuda", torch.cuda.current_device())
     N = comm.size
     m_loc, n = a.rows, a.cols

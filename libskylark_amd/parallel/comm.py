@@ -26,10 +26,13 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         if backend is None:
-            backend = "nccl" if (device != "cpu" and torch.cuda.is_available()) else "gloo"
-        if backend == "nccl":
+            backend = os.environ.get("SKH_DIST_BACKEND") or (
+                "nccl" if (device != "cpu" and torch.cuda.is_available()) else "gloo")
+        if torch.cuda.is_available() and device != "cpu":
+            # one process per GPU; modulo only matters for rehearsals with more
+            # ranks than GPUs (gloo backend)
             lr = int(os.environ.get("LOCAL_RANK", "0"))
-            torch.cuda.set_device(lr)
+            torch.cuda.set_device(lr % max(1, torch.cuda.device_count()))
         dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     return Comm()
 
