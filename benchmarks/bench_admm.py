@@ -1,0 +1,85 @@
+"""BASELINE config 4: Gaussian random Fourier features + kernel ridge
+regression / classification with BlockADMM, 1e6 x 512 synthetic examples per
+GPU (weak scaling), one process per GPU (torchrun for N > 1).
+
+Reports seconds per ADMM iteration and feature throughput (examples x random
+features per second), plus the one-off feature-map + factorisation time of
+the first iteration.  Data: synthetic Gaussian blobs (3 classes), random-init
+feature maps.
+
+usage: python benchmarks/bench_admm.py [--rows 1e6] [--dim 512] [--features 4096] [--partitions 4] [--iters 5]
+       torchrun --nproc-per-node N --master-addr 127.0.0.1 benchmarks/bench_admm.py ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=float, default=1e6)
+    ap.add_argument("--dim", type=int, default=512)
+    ap.add_argument("--features", type=int, default=4096)
+    ap.add_argument("--partitions", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--loss", default="hinge")
+    ap.add_argument("--cache", type=int, default=1, help="cache the feature blocks (HBM is 288 GB)")
+    a = ap.parse_args(argv)
+    import libskylark_amd as sk
+    from libskylark_amd import ml
+    from libskylark_amd.parallel import init_distributed
+    comm = init_distributed()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    m, d = int(a.rows), a.dim
+    g = torch.Generator(device=dev).manual_seed(1 + comm.rank)
+    lab = torch.randint(0, 3, (m,), generator=g, device=dev)
+    centers = torch.randn(3, d, generator=torch.Generator(device=dev).manual_seed(99), device=dev) * 0.5
+    X = centers[lab] + 0.5 * torch.randn(m, d, generator=g, device=dev)
+    k = ml.Gaussian(d, sigma=float(d) ** 0.5)
+    solver = ml.BlockADMMSolver(a.loss, "l2", 1e-3, a.features, kernel=k, NumFeaturePartitions=a.partitions,
+                                context=sk.Context(5))
+    solver.set_cache_transform(bool(a.cache))
+    times = []
+
+    def log(msg):
+        torch.cuda.synchronize()
+        times.append(time.perf_counter())
+
+    solver.set_maxiter(a.iters)
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    model = solver.train(X, lab.double(), regression=False, comm=comm, log=log)
+    torch.cuda.synchronize()
+    comm.barrier()
+    total = time.perf_counter() - t0
+    first = times[0] - t0
+    rest = (times[-1] - times[0]) / max(1, len(times) - 1)
+    t = torch.tensor([first, rest, total], dtype=torch.float64, device=dev)
+    comm.all_reduce_max(t)
+    first, rest, total = (float(v) for v in t.tolist())
+    pred, _ = model.predict(X[:100000])
+    acc = float((pred.to(lab.device) == lab[:100000].double()).double().mean())
+    if comm.rank == 0:
+        print(json.dumps({"metric": "BlockADMM seconds per iteration (Gaussian RFT features)",
+                          "value": round(rest, 5), "unit": "s/iter", "higher_is_better": False,
+                          "n_gpus": comm.size, "scaling": "weak",
+                          "first_iteration_s": round(first, 4), "total_s": round(total, 4),
+                          "feature_throughput_per_s": round(m * comm.size * a.features / rest, 1),
+                          "train_accuracy_sample": round(acc, 4),
+                          "config": {"rows_per_gpu": m, "dim": d, "features": a.features,
+                                     "partitions": a.partitions, "loss": a.loss, "iters": a.iters,
+                                     "cache_transforms": bool(a.cache)}}))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
