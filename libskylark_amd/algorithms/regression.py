@@ -173,6 +173,11 @@ def _utcondest(R: torch.Tensor) -> float:
     return float("inf") if rc == 0 else 1.0 / rc
 
 
+def _on_gpu(A) -> bool:
+    loc = A.local if isinstance(A, DistMatrix) else A
+    return isinstance(loc, torch.Tensor) and loc.is_cuda and loc.dtype == torch.float32
+
+
 def _build_precond(SA: torch.Tensor, kind: str):
     SA = SA.to(torch.float64)
     if kind == "qr":
@@ -194,7 +199,7 @@ class AcceleratedRegressionSolver:
 
     def __init__(self, problem: RegressionProblem, context: Context | None = None, method: str = "blendenpik",
                  precond: str = "qr", transform: str = "FJLT", sketch_size: int | None = None,
-                 params: KrylovIterParams | None = None, oversample: int = 4):
+                 params: KrylovIterParams | None = None, oversample: int = 4, lowp_sketch: bool = True):
         from .. import default_context
         ctx = context if context is not None else default_context()
         self.problem = problem
@@ -222,8 +227,13 @@ class AcceleratedRegressionSolver:
         elif self.method == "lsrn":
             delta = 1e-6
             sk = _sketch_rows("JLT", m, t, ctx)
+            if _on_gpu(A) and lowp_sketch:
+                sk.set_precision("bf16x2")  # S rounded to bf16: still a Gaussian-like sketch
             SA = _apply_columnwise(sk, A)
-            self.precond, _ = _build_precond(SA, "svd" if precond == "qr" else precond)
+            # LSRN's N = V S^{-1} (precond="svd") and R^{-1} from SA = QR ("qr") give
+            # preconditioned operators with identical singular values, so the
+            # Chebyshev bounds below hold for both; QR is far cheaper for large n.
+            self.precond, _ = _build_precond(SA, precond)
             alpha = math.sqrt(2 * math.log(2.0 / delta) / t)
             if alpha >= 1 - math.sqrt(n / t):
                 self.use_lsqr = True

@@ -74,9 +74,14 @@ def faster_least_squares(A, B, context: Context | None = None, orientation: str 
 
 
 def lsrn_least_squares(A, B, context: Context | None = None, params: KrylovIterParams | None = None,
-                       oversample: int = 4):
-    """LSRN: JLT sketch (t = oversample * n), SVD preconditioner, Chebyshev or LSQR."""
-    solver = AcceleratedRegressionSolver(RegressionProblem(A), context, method="lsrn", precond="svd",
+                       oversample: int = 4, precond: str = "auto"):
+    """LSRN: JLT sketch (t = oversample * n), SVD (or equivalent-spectrum QR)
+    preconditioner, Chebyshev or LSQR.  ``precond="auto"``: SVD for n <= 2000,
+    QR (same preconditioned singular values, much cheaper) above."""
+    n = A.shape[1]
+    if precond == "auto":
+        precond = "svd" if n <= 2000 else "qr"
+    solver = AcceleratedRegressionSolver(RegressionProblem(A), context, method="lsrn", precond=precond,
                                          params=params or KrylovIterParams(tolerance=1e-10, iter_lim=200),
                                          oversample=oversample)
     X, _ = solver.solve(B)

@@ -23,9 +23,16 @@ class DenseSketch(SketchTransform):
     def _scale(self) -> float:
         raise NotImplementedError
 
+    precision = "exact"   # "bf16x2": bf16-rounded S on MFMA (see ops.dense_sketch.apply_dense)
+
     def _build(self, ctx):
         self.scale = self._scale()
         self.entries = ctx.allocate_random_samples_array(self._N * self._S, self.dist)
+
+    def set_precision(self, precision: str):
+        """"exact" (default) or "bf16x2" (fast internal sketches; GPU fp32 inputs)."""
+        self.precision = precision
+        return self
 
     # global realisation helpers (used by tests, nla and the distributed layer)
     def realize(self, dtype=torch.float64, device=None, rows=None, cols=None) -> torch.Tensor:
@@ -38,7 +45,7 @@ class DenseSketch(SketchTransform):
     def _apply_dense(self, A, dim, in_offset: int = 0, out_rows=None):
         return _ds.apply_dense(A, dim, dist=self.dist, seed=self.entries.seed, base=self.entries.base,
                                S=self._S, N=self._N, scale=self.scale, in_offset=in_offset,
-                               out_rows=out_rows)
+                               out_rows=out_rows, precision=self.precision)
 
     def _apply_sparse(self, A, dim, sparse_out):
         return _ds.apply_sparse(A, dim, dist=self.dist, seed=self.entries.seed, base=self.entries.base,
