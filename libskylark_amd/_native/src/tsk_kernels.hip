@@ -31,6 +31,7 @@
 //   * per-workgroup W/G partial slabs, summed in f64 by a second kernel.
 #include "sl_common.hpp"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -96,7 +97,7 @@ struct Geo {
   static constexpr int GS = (GTILES + WAVES - 1) / WAVES;  // G tiles per wave
 };
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
@@ -157,7 +158,8 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
   for (int s = 0; s < GG::GS; ++s) accG[s] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ---- LDS-DMA of one row block (this wave's columns) into buffer `buf`
-  auto issue = [&](int64_t blk, int buf) {
+  auto issue_impl = [&](int64_t blk, int buf, auto nt_c) {
+    constexpr bool NT = decltype(nt_c)::value;
     char* region = abuf + (buf * WAVES + w) * GG::REGION;
     const int64_t r0 = blk * BM;
 #pragma unroll
@@ -173,9 +175,13 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       const bf16_t* src = A + grow * lda + col;
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           (unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-      if (ab & 64) glds16_nt((const void*)src, dst);
+      if constexpr (NT) glds16_nt((const void*)src, dst);
       else glds16((const void*)src, dst);
     }
+  };
+  auto issue = [&](int64_t blk, int buf) {
+    if (ab & 64) issue_impl(blk, buf, std::true_type{});
+    else issue_impl(blk, buf, std::false_type{});
   };
 
   // prefetch depth PD = NBUF - 1 blocks ahead of the one being consumed
@@ -282,17 +288,25 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       //      W += A^T y_hi (+ A^T y_lo).  (A single K=32 MFMA over [y_hi; y_lo]
       //      needs two transposed reads per tile and measured 15% slower.)
       const int row = 4 * g4 + q;
-#pragma unroll
-      for (int ct = 0; ct < NW / 16; ++ct) {
-        const int chunk = 2 * ct + (p >> 1);
-        const char* addr = region + row * GG::ROWB + (chunk ^ (row & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-        const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
-#pragma unroll
-        for (int t = 0; t < KT; ++t) {
-          accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);
-          if (!hi_only) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0);
-        }
+      // hi_only is wave-uniform: one branch selects a whole unrolled copy
+      // (a macro, not a lambda: capturing the accumulator arrays by reference
+      // makes hipcc demote them to scratch)
+#define SL_STEP3(HI)                                                                                  \
+  _Pragma("unroll") for (int ct = 0; ct < NW / 16; ++ct) {                                           \
+    const int chunk = 2 * ct + (p >> 1);                                                             \
+    const char* addr = region + row * GG::ROWB + (chunk ^ (row & (GG::NCH - 1))) * 16 + (p & 1) * 8;  \
+    const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr); \
+    _Pragma("unroll") for (int t = 0; t < KT; ++t) {                                                 \
+      accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);     \
+      if (!(HI)) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0); \
+    }                                                                                                \
+  }
+      if constexpr (HI_T) {
+        SL_STEP3(true)
+      } else {
+        SL_STEP3(hi_only)
       }
+#undef SL_STEP3
     }
     if (need_g) {
       // ---- step 4: G tiles tau = w + 8 s (t1 = tau / KT, t2 = tau % KT):
@@ -412,11 +426,11 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false>
 int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   using GG = Geo<NW, KT, NBUF>;
-  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF>;
+  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T>;
   static bool attr = false;
   if (!attr) {
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
@@ -441,18 +455,18 @@ int nbuf_request() {
   return nb;
 }
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, bool HI_T = false>
 int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
               float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   int nb = nbuf_request();
   constexpr int LIM = 160 * 1024;
   if (nb >= 5 && Geo<NW, KT, 5>::LDS <= LIM)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 5>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 5, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
   if (nb >= 4 && Geo<NW, KT, 4>::LDS <= LIM)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 4>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 4, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
   if (nb >= 3)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 3>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-  return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 2>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 3, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 2, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
 }
 
 }  // namespace
@@ -498,8 +512,11 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
   g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0);
+  // intermediate power-iteration passes (no Gram, bf16 y): compile-time specialisation
+  const bool inter = (flags & 3) == 3 && !Y;
 #define SL_TSK(NW, KTT)                                                                              \
   rc = Y ? launch_nb<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+     : inter ? launch_nb<NW, KTT, true, false, false, false, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
          : launch_nb<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
   if (small) {
     switch (KT) { case 1: SL_TSK(64, 1); break; case 2: SL_TSK(64, 2); break; case 3: SL_TSK(64, 3); break; default: SL_TSK(64, 4); }
