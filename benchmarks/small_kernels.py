@@ -40,7 +40,7 @@ def main():
     for k in (16, 40, 64):
         X = torch.randn(4 * k, k, dtype=torch.float64, device=dev)
         G = X.t() @ X
-        for impl, name in ((0, "auto"), (1, "lds"), (3, "wave"), (4, "lds1b")):
+        for impl, name in ((0, "auto"), (1, "lds"), (3, "wave"), (4, "lds1b"), (5, "aug")):
             lib.sl_small_chol_impl(impl)
             us = timeit(lambda: SL.chol_inv(G, st))
             print(f"chol_inv k={k:2d} {name:4s} {us:8.1f} us", flush=True)

@@ -295,6 +295,94 @@ k_wave_chol_inv_rolled(const double* __restrict__ G, int k, int ldg, double* __r
   if (i == 0 && bad && status) atomicOr(status, 1);
 }
 
+// Register-resident elimination of the augmented matrix [G | I] (impl 5):
+// Gaussian elimination without pivoting turns [G | I] into [D L_u^T | L_u^{-1}]
+// (G = L_u D L_u^T), so R = D^{-1/2} (left part) and R^{-1} = (right part)^T
+// D^{-1/2} come out of ONE k-step elimination instead of a factorisation
+// followed by a triangular inversion.  The 64 x 128 augmented matrix lives in
+// registers, 2-D cyclic over a 16 x 16 thread grid (32 doubles per thread).
+// The trailing block stays symmetric, so the multipliers of step j are the
+// pivot row itself: step j publishes row j (final from then on) into its own
+// LDS slot, one barrier, and every thread reads the 13 values it needs.  No
+// slot is ever rewritten, so one barrier per step is race free, and the slots
+// hold the whole eliminated matrix for the final output pass.
+__global__ void __launch_bounds__(256)
+k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R,
+                    double* __restrict__ Rinv, float* __restrict__ Rinv32, int* __restrict__ status) {
+  __shared__ double rows[KM][2 * KM];
+  __shared__ double dsh[KM];
+  const int t = threadIdx.x, tr = t >> 4, tc = t & 15;
+  double m[4][8];
+  double dmax = 0.0;
+  for (int c = 0; c < k; ++c) dmax = fmax(dmax, fabs(G[c * ldg + c]));
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = tr + 16 * a;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int c = tc + 16 * b;
+      double v = (i == c) ? 1.0 : 0.0;
+      if (i < k && c < k) v = 0.5 * (G[i * ldg + c] + G[c * ldg + i]);
+      m[a][b] = v;
+      m[a][4 + b] = (i == c) ? 1.0 : 0.0;
+    }
+  }
+  int bad = 0;
+  for (int j = 0; j < k; ++j) {
+    const int ja = j >> 4;
+    if (tr == (j & 15)) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        if (a == ja) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            rows[j][tc + 16 * b] = m[a][b];
+            rows[j][KM + tc + 16 * b] = m[a][4 + b];
+          }
+        }
+    }
+    __syncthreads();
+    double d = rows[j][j];
+    if (!(d > 1e-14 * dmax)) {  // also catches NaN: kill this direction
+      bad = 1;
+      d = 1e300;
+    }
+    const double dinv = 1.0 / d;
+    double mult[4], rv[8];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int i = tr + 16 * a;
+      mult[a] = (i > j) ? rows[j][i] * dinv : 0.0;
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      rv[b] = rows[j][tc + 16 * b];
+      rv[4 + b] = rows[j][KM + tc + 16 * b];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) m[a][b] = fma(-mult[a], rv[b], m[a][b]);
+    if (t == j) dsh[j] = d;
+  }
+  __syncthreads();
+  // R[i][c] = U[i][c] / sqrt(d_i) (c >= i; the diagonal is sqrt(d_i) itself, which also
+  // gives 1e150 for a killed pivot); R^{-1}[i][c] = X[c][i] / sqrt(d_c) (c >= i).
+  for (int e = t; e < k * k; e += 256) {
+    const int i = e / k, c = e % k;
+    double r = 0.0, ri = 0.0;
+    if (c >= i) {
+      const double si = sqrt(dsh[i]);
+      r = (c == i) ? si : rows[i][c] / si;
+      ri = rows[c][KM + i] / sqrt(dsh[c]);
+    }
+    if (R) R[e] = r;
+    if (Rinv) Rinv[e] = ri;
+    if (Rinv32) Rinv32[e] = (float)ri;
+  }
+  if (t == 0 && bad && status) atomicOr(status, 1);
+}
+
 __global__ void __launch_bounds__(256)
 k_small_matmul(const double* __restrict__ A, const double* __restrict__ B, double* __restrict__ C, int m, int kk,
                int n, float* __restrict__ C32) {
@@ -322,8 +410,10 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
   // measured on MI355X (rocprof, k x k f64): k<=16 single wave 10 us; k=40:
   // workgroup 61 us vs wave 57; k=64: wave 95 vs workgroup 121 -> pick per size
   int impl = g_chol_impl;
-  if (impl == 0) impl = (k <= 16 || k > 48) ? 3 : 4;
-  if (impl == 1)
+  if (impl == 0) impl = 5;
+  if (impl == 5)
+    k_aug_elim_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  else if (impl == 1)
     k_small_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
   else if (impl == 4)
     k_small_chol_inv1b<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
@@ -342,7 +432,8 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
 }
 
 // tuning/testing hook: 0 = auto (default), 1 = LDS workgroup kernel, 2 = single-wave rolled LDS
-// kernel, 3 = single-wave register kernel, 4 = one-barrier-per-step workgroup kernel
+// kernel, 3 = single-wave register kernel, 4 = one-barrier-per-step workgroup kernel,
+// 5 = register-resident augmented elimination
 SL_API int sl_small_chol_impl(int impl) {
   g_chol_impl = impl;
   return SL_OK;

@@ -19,6 +19,8 @@
 
 int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
                               int cols, double* out, int ld_out, hipStream_t s);
+int sl_slab_reduce_launch_d2d(const double* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
+                              int cols, double* out, int ld_out, hipStream_t s);
 
 namespace {
 
@@ -132,6 +134,168 @@ k_f32_mfma(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, const flo
   }
 }
 
+// G = Y^T Y in fp64 from f32 Y (k <= 64) on the f64 matrix cores
+// (v_mfma_f64_16x16x4f64).  Lane l of a wave loads Y[r + (l>>4)][16 t + (l&15)]:
+// that register is at once the A operand (G rows of tile t) and the B operand
+// (G columns of tile t) of the 16x16x4 MFMA, so the upper-triangle tile pairs
+// (a <= b) accumulate G with no data movement; 8 four-row chunks per wave
+// iteration keep 8*KT loads in flight.  Products and sums are fp64 (f32 -> f64
+// is exact), so G carries fp64 accuracy and one fp64 CholeskyQR of Y is as
+// orthogonal as CholeskyQR2 with an f32 second Gram, at a third of the work.
+// Per-workgroup k x k f64 slabs (the 4 waves summed through LDS), then a
+// deterministic slab reduction.
+typedef __attribute__((ext_vector_type(4))) double d4v;
+constexpr int G64_UNR = 8;
+constexpr int G64_GRID_MAX = 512;
+
+template <int KT>
+__global__ void __launch_bounds__(256)
+k_gram64(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, double* __restrict__ slab) {
+  constexpr int KP = 16 * KT, NT = KT * (KT + 1) / 2;
+  __shared__ double red[KP][KP + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  d4v acc[NT];
+#pragma unroll
+  for (int p = 0; p < NT; ++p) acc[p] = d4v{0.0, 0.0, 0.0, 0.0};
+  const int64_t step = (int64_t)gridDim.x * WPB * 4 * G64_UNR;
+  for (int64_t r0 = ((int64_t)blockIdx.x * WPB + w) * 4 * G64_UNR; r0 < m; r0 += step) {
+    float v[G64_UNR][KT];
+#pragma unroll
+    for (int u = 0; u < G64_UNR; ++u) {
+      const int64_t r = r0 + 4 * u + q;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int col = 16 * t + c;
+        v[u][t] = (r < m && col < k) ? Y[r * ldy + col] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G64_UNR; ++u) {
+      int p = 0;
+#pragma unroll
+      for (int a = 0; a < KT; ++a)
+#pragma unroll
+        for (int b = a; b < KT; ++b, ++p)
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)v[u][a], (double)v[u][b], acc[p], 0, 0, 0);
+    }
+  }
+  // C/D layout of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 reg
+  for (int vw = 0; vw < WPB; ++vw) {
+    if (w == vw) {
+      int p = 0;
+#pragma unroll
+      for (int a = 0; a < KT; ++a)
+#pragma unroll
+        for (int b = a; b < KT; ++b, ++p)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int i = 16 * a + q + 4 * reg, j = 16 * b + c;
+            if (vw == 0) red[i][j] = acc[p][reg];
+            else red[i][j] += acc[p][reg];
+          }
+    }
+    __syncthreads();
+  }
+  double* gs = slab + (int64_t)blockIdx.x * k * k;
+  for (int e = threadIdx.x; e < k * k; e += 256) {
+    const int i = e / k, j = e - (e / k) * k;
+    gs[e] = ((i >> 4) <= (j >> 4)) ? red[i][j] : red[j][i];  // mirror the lower tiles
+  }
+}
+
+// Contiguous fast path (ldy == k, k % 8 == 0): each wave streams 32-row chunks
+// (32 k contiguous floats) with float4 loads; chunk i+1 is in flight while
+// chunk i goes registers -> a wave-private LDS tile (row pitch LD = 16 mod 32,
+// so the MFMA-layout ds_read_b32 are bank-conflict free) -> f64 MFMAs.  The
+// strided kernel above serialises its 4-byte loads with the MFMAs (loads
+// 50 us + MFMA 51 us -> 118 us at m = 1e6, k = 40); this one overlaps them
+// (60 us; benchmarks/native/gram64_probe.hip).
+template <int KT>
+__global__ void __launch_bounds__(256)
+k_gram64_pipe(const float* __restrict__ Y, int64_t m, int k, double* __restrict__ slab) {
+  constexpr int KP = 16 * KT, NT = KT * (KT + 1) / 2;
+  constexpr int LD = (KT & 1) ? 16 * KT : 16 * KT + 16;
+  constexpr int NLMAX = 2 * KT;  // k / 8 float4 per lane per chunk
+  __shared__ float tile[WPB][32 * LD];
+  __shared__ double red[KP][KP + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  float* T = tile[w];
+  const int nl = k >> 3;
+  int loff[NLMAX], lrow[NLMAX];
+#pragma unroll
+  for (int j = 0; j < NLMAX; ++j) {
+    const int e = 4 * (64 * j + lane);
+    lrow[j] = e / k;
+    loff[j] = lrow[j] * LD + (e - lrow[j] * k);
+  }
+  d4v acc[NT];
+#pragma unroll
+  for (int p = 0; p < NT; ++p) acc[p] = d4v{0.0, 0.0, 0.0, 0.0};
+  const int64_t step = (int64_t)gridDim.x * WPB * 32;
+  int64_t r0 = ((int64_t)blockIdx.x * WPB + w) * 32;
+  float4 nx[NLMAX];
+  auto load = [&](int64_t rb) {
+#pragma unroll
+    for (int j = 0; j < NLMAX; ++j)
+      if (j < nl)
+        nx[j] = (rb + lrow[j] < m) ? *(const float4*)(Y + rb * k + 4 * (64 * j + lane)) : float4{0.f, 0.f, 0.f, 0.f};
+  };
+  if (r0 < m) load(r0);
+  for (; r0 < m; r0 += step) {
+#pragma unroll
+    for (int j = 0; j < NLMAX; ++j)
+      if (j < nl) *(float4*)(T + loff[j]) = nx[j];
+    if (r0 + step < m) load(r0 + step);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      double v[KT];
+#pragma unroll
+      for (int t = 0; t < KT; ++t) v[t] = (16 * t + c < k) ? (double)T[(4 * u + q) * LD + 16 * t + c] : 0.0;
+      int p = 0;
+#pragma unroll
+      for (int a = 0; a < KT; ++a)
+#pragma unroll
+        for (int b = a; b < KT; ++b, ++p) acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[a], v[b], acc[p], 0, 0, 0);
+    }
+  }
+  for (int vw = 0; vw < WPB; ++vw) {
+    if (w == vw) {
+      int p = 0;
+#pragma unroll
+      for (int a = 0; a < KT; ++a)
+#pragma unroll
+        for (int b = a; b < KT; ++b, ++p)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int i = 16 * a + q + 4 * reg, j = 16 * b + c;
+            if (vw == 0) red[i][j] = acc[p][reg];
+            else red[i][j] += acc[p][reg];
+          }
+    }
+    __syncthreads();
+  }
+  double* gs = slab + (int64_t)blockIdx.x * k * k;
+  for (int e = threadIdx.x; e < k * k; e += 256) {
+    const int i = e / k, j = e - (e / k) * k;
+    gs[e] = ((i >> 4) <= (j >> 4)) ? red[i][j] : red[j][i];
+  }
+}
+
+constexpr int G64_PIPE_GRID_MAX = 1024;
+
+int gram64_pipe_grid(int64_t m) {
+  const int64_t g = (m + WPB * 32 - 1) / (WPB * 32);
+  return (int)(g < G64_PIPE_GRID_MAX ? (g < 1 ? 1 : g) : G64_PIPE_GRID_MAX);
+}
+
+int gram64_grid(int64_t m) {
+  const int64_t rows_per_block = (int64_t)WPB * 4 * G64_UNR;
+  const int64_t g = (m + rows_per_block - 1) / rows_per_block;
+  return (int)(g < G64_GRID_MAX ? (g < 1 ? 1 : g) : G64_GRID_MAX);
+}
+
 int grid_for(int64_t m) {
   const int64_t ng = (m + 31) / 32;
   int64_t g = (ng + WPB - 1) / WPB;
@@ -141,6 +305,42 @@ int grid_for(int64_t m) {
 }  // namespace
 
 SL_API int64_t sl_tsk_f32_workspace(int64_t m) { return (int64_t)grid_for(m) * KMAX * KMAX * 4 + 256; }
+
+SL_API int64_t sl_tsk_gram64_workspace(int64_t m, int k) {
+  const int g = gram64_grid(m) > gram64_pipe_grid(m) ? gram64_grid(m) : gram64_pipe_grid(m);
+  return (int64_t)g * k * k * 8 + 256;
+}
+
+// G (k x k, f64) = Y^T Y with Y m x k f32 (row stride ldy); ws >= sl_tsk_gram64_workspace bytes.
+SL_API int sl_tsk_gram64(const float* Y, int64_t m, int k, int64_t ldy, double* G, void* ws, void* stream) {
+  if (k < 1 || k > KMAX) {
+    sl_set_last_error("tsk_gram64: needs 1 <= k <= 64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (m <= 0) return hipMemsetAsync(G, 0, (size_t)k * k * 8, s) == hipSuccess ? SL_OK : SL_ERR_HIP;
+  double* slab = (double*)ws;
+  if (ldy == k && k % 8 == 0) {
+    const int g = gram64_pipe_grid(m);
+    switch ((k + 15) / 16) {
+      case 1: k_gram64_pipe<1><<<g, 256, 0, s>>>(Y, m, k, slab); break;
+      case 2: k_gram64_pipe<2><<<g, 256, 0, s>>>(Y, m, k, slab); break;
+      case 3: k_gram64_pipe<3><<<g, 256, 0, s>>>(Y, m, k, slab); break;
+      default: k_gram64_pipe<4><<<g, 256, 0, s>>>(Y, m, k, slab); break;
+    }
+    SL_LAUNCH_CHECK();
+    return sl_slab_reduce_launch_d2d(slab, g, (int64_t)k * k, k, k, k, G, k, s);
+  }
+  const int g = gram64_grid(m);
+  switch ((k + 15) / 16) {
+    case 1: k_gram64<1><<<g, 256, 0, s>>>(Y, m, k, ldy, slab); break;
+    case 2: k_gram64<2><<<g, 256, 0, s>>>(Y, m, k, ldy, slab); break;
+    case 3: k_gram64<3><<<g, 256, 0, s>>>(Y, m, k, ldy, slab); break;
+    default: k_gram64<4><<<g, 256, 0, s>>>(Y, m, k, ldy, slab); break;
+  }
+  SL_LAUNCH_CHECK();
+  return sl_slab_reduce_launch_d2d(slab, g, (int64_t)k * k, k, k, k, G, k, s);
+}
 
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2,
                          float* out, int64_t ldo, double* G, void* ws, void* stream) {

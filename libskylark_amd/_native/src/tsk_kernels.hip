@@ -359,9 +359,9 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
 // consecutive elements of a slab row (coalesced), 4 slabs in flight per lane;
 // the 16 partials are combined through LDS.  Enough parallelism both for
 // the n x k W slabs and for the k x k Gram slabs.
-template <typename OT>
+template <typename IT, typename OT>
 __global__ void __launch_bounds__(1024)
-k_slab_reduce_rows(const float* __restrict__ slab, int nslab, int64_t slab_stride, int ld_in,
+k_slab_reduce_rows(const IT* __restrict__ slab, int nslab, int64_t slab_stride, int ld_in,
                    int cols, OT* __restrict__ out, int ld_out, int rows) {
   __shared__ double part[16][64];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -370,7 +370,7 @@ k_slab_reduce_rows(const float* __restrict__ slab, int nslab, int64_t slab_strid
   double acc = 0.0;
   if (ok) {
     const int64_t i = t / cols, j = t - i * cols;
-    const float* p = slab + i * ld_in + j;
+    const IT* p = slab + i * ld_in + j;
     double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     int b = g;
     for (; b + 48 < nslab; b += 64) {
@@ -398,7 +398,7 @@ int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int
   if (rows <= 0 || cols <= 0) return SL_OK;
   if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
   const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
-  k_slab_reduce_rows<float><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
+  k_slab_reduce_rows<float, float><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -408,7 +408,17 @@ int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride,
   if (rows <= 0 || cols <= 0) return SL_OK;
   if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
   const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
-  k_slab_reduce_rows<double><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
+  k_slab_reduce_rows<float, double><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+int sl_slab_reduce_launch_d2d(const double* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
+                              int cols, double* out, int ld_out, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return SL_OK;
+  if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
+  const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
+  k_slab_reduce_rows<double, double><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -514,8 +524,11 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0);
   // intermediate power-iteration passes (no Gram, bf16 y): compile-time specialisation
   const bool inter = (flags & 3) == 3 && !Y;
+  // final pass whose Gram is taken separately (fp64 Gram of the stored Y)
+  const bool nog = (flags & 3) == 1;
 #define SL_TSK(NW, KTT)                                                                              \
-  rc = Y ? launch_nb<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+  rc = (Y && nog) ? launch_nb<NW, KTT, true, false, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+     : Y ? launch_nb<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
      : inter ? launch_nb<NW, KTT, true, false, false, false, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
          : launch_nb<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
   if (small) {

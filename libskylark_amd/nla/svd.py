@@ -16,7 +16,10 @@ uses this identity in its ``skip_qr, num_iterations == 0`` branch
 ``[A^T Y | Y^T Y]`` ((n + k) x k floats).  Robustness: the n x k iterate is
 re-orthonormalised exactly (Householder, fp64) between passes; the final
 basis is CholeskyQR2-refined from the stored ``Y`` (m x k, a fraction of A's
-bytes); if a Gram factorisation fails the code falls back to TSQR.
+bytes); if a Gram factorisation fails the code falls back to TSQR.  The
+GPU-resident plan (``_DevicePlan``) instead takes an fp64 Gram of the stored
+f32 ``Y`` on the f64 matrix cores (``ops.tallskinny.gram64``) and needs one
+fp64 CholeskyQR only.
 """
 from __future__ import annotations
 
@@ -249,6 +252,7 @@ class _DevicePlan:
         self.ws = torch.empty(T.fused_workspace_bytes(m, n, k), dtype=torch.uint8, device=dev)
         self.ws32 = torch.empty(max(T.f32_workspace_bytes(m), T.f32_workspace_bytes(n)), dtype=torch.uint8,
                                 device=dev)
+        self.ws64 = torch.empty(T.gram64_workspace_bytes(m, k), dtype=torch.uint8, device=dev)
         self.use_graph = use_graph
         self.g1 = self.g2 = None
         self.calls = 0
@@ -270,18 +274,18 @@ class _DevicePlan:
                 Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-30) if self.skip_qr else \
                     SL.cholqr(W, st, ws=self.ws32)
         with prof.phase("svd.fused_pass"):
-            W, G, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws)
+            W, _, Y = T.fused_pass(A, Z, keep_y=True, gram=False, exact=True, ws=self.ws)
+        with prof.phase("svd.final_qr"):
+            # fp64 Gram of the stored f32 Y (f64 matrix cores): one fp64 CholeskyQR
+            # then leaves Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2
+            # with an f32 second Gram only reached ~eps32, at three times the work)
+            G = T.gram64(Y, ws=self.ws64)
         with prof.phase("svd.allreduce_small"):
             WG = torch.cat([W.double(), G], 0)
             comm.all_reduce(WG)
             W, G = WG[:n], WG[n:]
         with prof.phase("svd.final_qr"):
-            # CholeskyQR2 of Y: first factor from the pass's Gram, second from an exact f32 Gram
-            R1, R1i, R1i32 = SL.chol_inv(G, st)
-            _, G2 = T.f32_xm(Y, R1i32, store=False, gram=True, ws=self.ws32)
-            comm.all_reduce(G2)
-            R2, R2i, _ = SL.chol_inv(G2, st)
-            Rti = R1i @ R2i                      # Rt^{-1} = R1^{-1} R2^{-1}  (k x k, f64)
+            _, Rti, _ = SL.chol_inv(G, st)
             # B^T = A^T Q = W Rt^{-1} (n x k); its right singular pairs come from the
             # k x k f64 Gram C = Rt^{-T} (W^T W) Rt^{-1} = Ub S^2 Ub^T (host eigensolve).
             # sigma_i keeps relative accuracy ~eps64 (sigma_1/sigma_i)^2, far below

@@ -163,6 +163,30 @@ def f32_xm(Y: torch.Tensor, M: torch.Tensor | None = None, store: bool = True, g
     return (Q if store else None), G
 
 
+_lib.register("sl_tsk_gram64", [vp, i64, i32, i64, vp, vp, vp])
+_lib.register("sl_tsk_gram64_workspace", [i64, i32], C.c_int64)
+
+
+def gram64_workspace_bytes(m: int, k: int) -> int:
+    return int(_lib.require().sl_tsk_gram64_workspace(m, k))
+
+
+def gram64(Y: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
+    """``G = Y^T Y`` in float64 for tall f32 ``Y`` (k <= 64), partial over this
+    shard: fp64 products and sums on the f64 matrix cores, so one fp64
+    CholeskyQR of ``Y`` from this ``G`` is as orthogonal as CholeskyQR2 with an
+    f32 second Gram.  Torch (fp64) on CPU."""
+    m, k = Y.shape
+    if Y.is_cuda and Y.dtype == torch.float32 and k <= 64 and Y.stride(1) == 1 and _lib.available():
+        G = torch.empty(k, k, dtype=torch.float64, device=Y.device)
+        if ws is None:
+            ws = _WS32.get(Y.device, gram64_workspace_bytes(m, k))
+        _lib.call("sl_tsk_gram64", _lib.ptr(Y), m, k, Y.stride(0), _lib.ptr(G), _lib.ptr(ws), vp(_lib.stream_of(Y)))
+        return G
+    Yd = Y.double()
+    return Yd.t() @ Yd
+
+
 def matmul(A: torch.Tensor, Z: torch.Tensor, out_dtype=torch.float32) -> torch.Tensor:
     """``Y = A Z`` streaming (A bf16 m x n, Z n x k small) with f32 output."""
     if _native_ok(A, Z.shape[1]) and hasattr(_lib.require(), "sl_tsk_matmul"):

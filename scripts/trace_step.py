@@ -5,10 +5,12 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "k_tsk_pass<128, 3, true, true, true" in r["Kernel_Name"]]
+FINAL = ("k_tsk_pass<128, 3, true, true, true", "k_tsk_pass<128, 3, true, false, true")
+idx = [i for i, r in enumerate(rows) if any(p in r["Kernel_Name"] for p in FINAL)]
 a, b = idx[-2], idx[-1]
 # step = from the first pass of step i to the first pass of step i+1
-starts = [i for i, r in enumerate(rows) if "k_tsk_pass<128, 3, true, true, false" in r["Kernel_Name"] and i < b]
+starts = [i for i, r in enumerate(rows) if i < b and any(
+    p in r["Kernel_Name"] for p in ("k_tsk_pass<128, 3, true, true, false", "k_tsk_pass<128, 3, true, false, false"))]
 first = [i for i in starts if i < a]
 a0 = first[-2] if len(first) >= 2 else first[-1]
 b0 = [i for i in starts if i > a][0] if any(i > a for i in starts) else b

@@ -125,14 +125,33 @@ def test_fused_pass_gpu_bf16(dev, native):
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k,k2", [(1000003, 40, 20), (5000, 64, 64), (77, 5, 3)])
 def test_f32_xm_native(dev, m, k, k2):
-    Y = torch.randn(m, k, device=dev)
-    M = torch.randn(k, k2, device=dev)
+    g = torch.Generator(device=dev).manual_seed(m + k)
+    Y = torch.randn(m, k, device=dev, generator=g)
+    M = torch.randn(k, k2, device=dev, generator=g)
     Q, G = tallskinny.f32_xm(Y, M, store=True, gram=True)
     Qr = Y.double() @ M.double()
     torch.testing.assert_close(Q.double(), Qr, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(G, Qr.t() @ Qr, rtol=1e-4, atol=1e-3)
+
+    def rel(a, b):  # f32 accumulation: error ~ eps * sum |terms|, so compare in norm
+        return float((a.double() - b).norm() / b.norm())
+    assert rel(G, Qr.t() @ Qr) < 1e-5
     _, G1 = tallskinny.f32_xm(Y, None, store=False, gram=True)
-    torch.testing.assert_close(G1, Y.double().t() @ Y.double(), rtol=1e-4, atol=1e-3)
+    assert rel(G1, Y.double().t() @ Y.double()) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,ld", [(1000003, 40, 40), (5000, 64, 64), (77, 5, 5), (4099, 17, 24), (3, 33, 33)])
+def test_gram64_native(dev, m, k, ld):
+    """fp64 Gram of f32 Y on the f64 matrix cores == fp64 torch (to ~eps64)."""
+    g = torch.Generator(device=dev).manual_seed(m + k)
+    Yf = torch.randn(m, ld, device=dev, generator=g)
+    Y = Yf[:, :k]
+    G = tallskinny.gram64(Y)
+    Yd = Y.double()
+    Gr = sum(Yd[i:i + 8192].t() @ Yd[i:i + 8192] for i in range(0, m, 8192))  # short fp64 chains
+    assert G.dtype == torch.float64 and G.shape == (k, k)
+    assert float((G - Gr).norm() / Gr.norm()) < 1e-12
+    assert float((G - G.t()).abs().max()) <= 1e-14 * float(Gr.abs().max())
 
 
 @pytest.mark.gpu

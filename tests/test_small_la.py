@@ -7,7 +7,7 @@ from libskylark_amd.ops import small_la as SL
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "lds", "rolled", "wave", "lds1b"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["auto", "lds", "rolled", "wave", "lds1b", "aug"])
 def impl(request):
     import ctypes
     from libskylark_amd.ops import _lib
