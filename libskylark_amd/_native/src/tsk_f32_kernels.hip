@@ -283,6 +283,92 @@ k_gram64_pipe(const float* __restrict__ Y, int64_t m, int k, double* __restrict_
   }
 }
 
+// Q = Y M, stored (no Gram), contiguous fast path (ldy == k, k % 8 == 0,
+// ldo == k2): the U = Y (R^{-1} U_B) pass of randSVD.  Each wave streams 32-row
+// chunks with float4 loads (next chunk in flight), stages them in a
+// wave-private LDS tile of odd pitch k + 1 (row-per-lane A reads of the
+// 32x32x2 f32 MFMA are then bank-conflict free), multiplies with M held in
+// registers, and writes the 32 x k2 result back through LDS as coalesced
+// float4 rows — the strided kernel above reads and writes one float per lane
+// per instruction.
+template <int KT2>
+__global__ void __launch_bounds__(256)
+k_xm_pipe(const float* __restrict__ Y, int64_t m, int k, const float* __restrict__ M, int k2,
+          float* __restrict__ out) {
+  __shared__ float tin[WPB][32 * (KMAX + 1)];
+  __shared__ float tout[WPB][32 * 32 * KT2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  float* Ti = tin[w];
+  float* To = tout[w];
+  const int lda = k + 1;
+  float mreg[KMAX / 2][KT2];
+#pragma unroll
+  for (int s = 0; s < KMAX / 2; ++s)
+#pragma unroll
+    for (int ct = 0; ct < KT2; ++ct) {
+      const int r = 2 * s + h, col = 32 * ct + c;
+      mreg[s][ct] = (r < k && col < k2) ? M[r * k2 + col] : 0.f;
+    }
+  constexpr int NLMAX = KMAX / 8;
+  const int nl = k >> 3;
+  int loff[NLMAX], lrow[NLMAX];
+#pragma unroll
+  for (int j = 0; j < NLMAX; ++j) {
+    const int e = 4 * (64 * j + lane);
+    lrow[j] = e / k;
+    loff[j] = lrow[j] * lda + (e - lrow[j] * k);
+  }
+  const int64_t step = (int64_t)gridDim.x * WPB * 32;
+  int64_t r0 = ((int64_t)blockIdx.x * WPB + w) * 32;
+  float4 nx[NLMAX];
+  auto load = [&](int64_t rb) {
+#pragma unroll
+    for (int j = 0; j < NLMAX; ++j)
+      if (j < nl)
+        nx[j] = (rb + lrow[j] < m) ? *(const float4*)(Y + rb * k + 4 * (64 * j + lane)) : float4{0.f, 0.f, 0.f, 0.f};
+  };
+  if (r0 < m) load(r0);
+  for (; r0 < m; r0 += step) {
+#pragma unroll
+    for (int j = 0; j < NLMAX; ++j)
+      if (j < nl) {
+        float* d = Ti + loff[j];
+        d[0] = nx[j].x;
+        d[1] = nx[j].y;
+        d[2] = nx[j].z;
+        d[3] = nx[j].w;
+      }
+    if (r0 + step < m) load(r0 + step);
+    f16v q[KT2];
+#pragma unroll
+    for (int ct = 0; ct < KT2; ++ct) q[ct] = f16v{};
+#pragma unroll
+    for (int s = 0; s < KMAX / 2; ++s) {
+      if (2 * s >= k) break;
+      const float a = Ti[c * lda + 2 * s + h];
+#pragma unroll
+      for (int ct = 0; ct < KT2; ++ct) q[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, mreg[s][ct], q[ct], 0, 0, 0);
+    }
+#pragma unroll
+    for (int ct = 0; ct < KT2; ++ct)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int col = 32 * ct + c;
+        if (col < k2) To[crow(reg, h) * k2 + col] = q[ct][reg];
+      }
+    const int64_t left = m - r0;
+    float* o = out + r0 * k2;
+    if (left >= 32) {
+      for (int e4 = lane; e4 < 8 * k2; e4 += 64) *(float4*)(o + 4 * e4) = *(const float4*)(To + 4 * e4);
+    } else {
+      for (int e = lane; e < (int)left * k2; e += 64) o[e] = To[e];
+    }
+  }
+}
+
+constexpr int XM_PIPE_GRID_MAX = 2048;
+
 constexpr int G64_PIPE_GRID_MAX = 1024;
 
 int gram64_pipe_grid(int64_t m) {
@@ -357,6 +443,15 @@ SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const fl
   const bool store = out != nullptr && M != nullptr;
 #define SL_F(KT2, ID, ST, GR) k_f32_mfma<KT2, ID, ST, GR><<<g, 256, 0, s>>>(Y, m, k, ldy, M, k2, out, ldo, slab)
 #define SL_F2(ID, ST, GR) { if (two) SL_F(2, ID, ST, GR); else SL_F(1, ID, ST, GR); }
+  if (M && store && !G && ldy == k && k % 8 == 0 && ldo == k2 && ((uintptr_t)Y & 15) == 0 &&
+      ((uintptr_t)out & 15) == 0) {
+    int64_t gx = (m + WPB * 32 - 1) / (WPB * 32);
+    if (gx > XM_PIPE_GRID_MAX) gx = XM_PIPE_GRID_MAX;
+    if (two) k_xm_pipe<2><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out);
+    else k_xm_pipe<1><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  }
   if (!M) {
     if (!G) return SL_OK;
     SL_F2(true, false, true);

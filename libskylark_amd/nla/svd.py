@@ -227,13 +227,15 @@ class _DevicePlan:
     """Device randSVD for one (A, k, rank, q) configuration, replayed as two
     hipGraphs once warm (``ApproximateSVDParams.graph``).
 
-    Segment 1 (sketch Z -> power passes -> final pass -> CholeskyQR2 of Y ->
-    k x k Gram of A^T Q) and segment 2 (V, U from the host eigensolve) are
-    each one graph: the ~30 launches per call collapse into two replays, so
-    the short kernels between the streaming passes no longer wait on host
-    launch latency.  Graph inputs are static buffers (the sketch Z and the
-    eigenpairs); A is read in place, so replays always see A's current
-    contents.  Outputs are cloned before they are returned.  With more than
+    Segment 1 (sketch Z -> power passes -> final pass -> fp64 Gram and
+    CholeskyQR of Y -> k x k Gram of A^T Q) and segment 2 (V and the k x r
+    map of U from the host eigensolve) are each one graph: the ~30 launches
+    per call collapse into two replays, so the short kernels between the
+    streaming passes no longer wait on host launch latency.  Graph inputs are
+    static buffers (the sketch Z and the eigenpairs); A is read in place, so
+    replays always see A's current contents.  The small outputs (s, V) are
+    cloned out of graph memory; U = Y M is one eager launch into a fresh
+    tensor (no m x r copy).  With more than
     one rank the collectives stay eager unless SKH_GRAPH_COLLECTIVES=1
     (RCCL capture); if a capture fails the plan stays eager.
     """
@@ -296,14 +298,12 @@ class _DevicePlan:
         self.Y, self.Rti, self.Vt = Y, Rti, Vt
 
     def seg2(self):
-        from ..ops import tallskinny as T
         k, r = self.k, self.rank
         Ub = self.small[:k * r].view(k, r)
         s64 = self.small[k * r:]
         with PROFILER.phase("svd.form_U"):
             self.V = ((self.Vt @ Ub) / s64.clamp_min(1e-300)).float()   # V = A^T Q Ub S^{-1}
-            M = (self.Rti @ Ub).float()                                   # U = Y Rt^{-1} Ub
-            self.U, _ = T.f32_xm(self.Y, M, store=True)
+            self.M = (self.Rti @ Ub).float()                              # U = Y Rt^{-1} Ub
             self.s = s64.float()
 
     def _capture(self, fn):
@@ -348,7 +348,12 @@ class _DevicePlan:
         self.small.copy_(torch.from_numpy(np.concatenate([evecs[:, order].reshape(-1), s])))
         self._run(2)
         self.calls += 1
-        return self.U.clone(), self.s.clone(), self.V.clone()
+        from ..ops import tallskinny as T
+        with PROFILER.phase("svd.form_U"):
+            # outside the graph: U lands in a fresh allocation, so the m x r
+            # result needs no copy out of the graph's static memory
+            U, _ = T.f32_xm(self.Y, self.M, store=True)
+        return U, self.s.clone(), self.V.clone()
 
 
 _PLANS: dict = {}

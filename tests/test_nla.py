@@ -140,6 +140,19 @@ def test_f32_xm_native(dev, m, k, k2):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m,k,k2", [(1000003, 40, 20), (5001, 64, 64), (31, 8, 3), (70000, 16, 40), (100, 24, 33)])
+def test_f32_xm_store_native(dev, m, k, k2):
+    """Store-only Q = Y M (the contiguous pipelined kernel) == fp64 torch."""
+    g = torch.Generator(device=dev).manual_seed(m + k2)
+    Y = torch.randn(m, k, device=dev, generator=g)
+    M = torch.randn(k, k2, device=dev, generator=g)
+    Q, G = tallskinny.f32_xm(Y, M, store=True, gram=False)
+    assert G is None and Q.shape == (m, k2)
+    Qr = Y.double() @ M.double()
+    torch.testing.assert_close(Q.double(), Qr, rtol=1e-5, atol=1e-5 * float(Qr.abs().max()))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("m,k,ld", [(1000003, 40, 40), (5000, 64, 64), (77, 5, 5), (4099, 17, 24), (3, 33, 33)])
 def test_gram64_native(dev, m, k, ld):
     """fp64 Gram of f32 Y on the f64 matrix cores == fp64 torch (to ~eps64)."""
