@@ -86,6 +86,7 @@ enum Dist : int {
   DIST_CHISQ = 6,       // chi-squared, p0 = degrees of freedom
   DIST_UNIFORM_INT = 7, // integer in [p0, p1]
   DIST_WZT = 8,         // +-(1/E)^(1/p), p0 = p  (Woodruff-Zhang value)
+  DIST_SPARSE_SIGN = 9, // +-1/sqrt(d) w.p. d/2 each, else 0; p0 = d (sparse JL, Achlioptas / Li et al.)
 };
 
 // Normal: Box-Muller on the two 64-bit words of element idx's first block.
@@ -165,6 +166,12 @@ SL_HD double sample_d(int dist, uint64_t seed, uint64_t idx, double p0, double p
       double v = pow(1.0 / e, 1.0 / p0);
       return (b.y >> 63) ? v : -v;
     }
+    case DIST_SPARSE_SIGN: {
+      u64x2 b = stream_block(seed, idx);
+      double u = u01_d(b.x);
+      if (u >= p0) return 0.0;
+      return (u < 0.5 * p0 ? -1.0 : 1.0) / sqrt(p0);
+    }
   }
   return 0.0;
 }
@@ -191,6 +198,12 @@ SL_HD float sample_f(int dist, uint64_t seed, uint64_t idx, float p0, float p1) 
     case DIST_UNIFORM: {
       u64x2 b = stream_block(seed, idx);
       return p0 + (p1 - p0) * u01_f(b.x);
+    }
+    case DIST_SPARSE_SIGN: {
+      u64x2 b = stream_block(seed, idx);
+      float u = u01_f(b.x);
+      if (u >= p0) return 0.0f;
+      return (u < 0.5f * p0 ? -1.0f : 1.0f) * __builtin_sqrtf(1.0f / p0);
     }
     default: return (float)sample_d(dist, seed, idx, p0, p1);
   }

@@ -93,3 +93,14 @@ class WZTValue(Distribution):
     @property
     def p0(self):
         return self.p
+
+
+@dataclass
+class SparseSign(Distribution):
+    """±1/sqrt(d) with probability d/2 each, 0 otherwise (sparse JL entries)."""
+    density: float = 1.0 / 3.0
+    code = 9
+
+    @property
+    def p0(self):
+        return self.density

@@ -1,8 +1,8 @@
 """Sketching transforms (reference ``sketch/``, ``python-skylark/skylark/sketch.py``)."""
 from .base import (COLUMNWISE, ROWWISE, SketchTransform, deserialize_sketch, from_json, from_ptree,
                    parse_dim, sketch_class, supported_sketch_transforms)
-from .dense import CT, JLT
-from .fjlt import FJLT, RFUT, UST, URST, FastJLT
+from .dense import CT, JLT, SJLT, SparseJLT
+from .fjlt import FJLT, NURST, RFUT, UST, URST, FastJLT, NonUniformSampler, UniformSampler
 from .frft import PPT, FastGaussianRFT, FastMaternRFT, Fastfood
 from .hash import CWT, MMT, WZT, CountSketch
 from .rft import (ExpSemigroupQRLT, ExpSemigroupRLT, GaussianQRFT, GaussianRFT, LaplacianQRFT,
@@ -10,11 +10,13 @@ from .rft import (ExpSemigroupQRLT, ExpSemigroupRLT, GaussianQRFT, GaussianRFT, 
 
 columnwise, rowwise = COLUMNWISE, ROWWISE
 TensorSketch = PPT
+RRT = GaussianRFT
+MaternFastfood = FastMaternRFT
 
 __all__ = [
     "COLUMNWISE", "ROWWISE", "SketchTransform", "deserialize_sketch", "from_json", "from_ptree",
-    "JLT", "CT", "FJLT", "FastJLT", "RFUT", "UST", "URST", "CWT", "CountSketch", "MMT", "WZT",
-    "PPT", "TensorSketch", "GaussianRFT", "LaplacianRFT", "MaternRFT", "GaussianQRFT",
+    "JLT", "CT", "SJLT", "SparseJLT", "NURST", "NonUniformSampler", "UniformSampler", "FJLT", "FastJLT", "RFUT", "UST", "URST", "CWT", "CountSketch", "MMT", "WZT",
+    "PPT", "TensorSketch", "RRT", "MaternFastfood", "GaussianRFT", "LaplacianRFT", "MaternRFT", "GaussianQRFT",
     "LaplacianQRFT", "FastGaussianRFT", "Fastfood", "FastMaternRFT", "ExpSemigroupRLT",
     "ExpSemigroupQRLT", "supported_sketch_transforms", "sketch_class", "parse_dim",
 ]

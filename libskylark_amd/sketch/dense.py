@@ -94,4 +94,40 @@ class CT(DenseSketch):
         return {"C": float(d["C"])}
 
 
-__all__ = ["JLT", "CT", "DenseSketch", "COLUMNWISE"]
+@register
+class SJLT(DenseSketch):
+    """Sparse Johnson-Lindenstrauss transform (Achlioptas 2003; Li, Hastie,
+    Church 2006): entries ``±sqrt(1/(density*S))`` with probability
+    ``density/2`` each, zero otherwise, so ``E[S^T S] = I``.
+
+    Reference: ``python-skylark/skylark/sketch.py:303-338`` (pure-Python
+    only there; its ``_S`` construction refers to undefined names and omits
+    the ``1/sqrt(S)`` scale its JLT uses — here entries follow the same
+    counter layout as JLT, ``base + j*S + i``, so the operator is realisable
+    lazily and shard-locally like every dense sketch).
+    """
+
+    sketch_type = "SJLT"
+
+    def __init__(self, n, s, density=1.0 / 3.0, context=None):
+        self._density = float(density)
+        if not 0.0 < self._density <= 1.0:
+            from ..base.exceptions import InvalidParametersError
+            raise InvalidParametersError("SJLT density must be in (0, 1]")
+        self.dist = D.SparseSign(self._density)
+        super().__init__(n, s, context)
+
+    def _scale(self):
+        return math.sqrt(1.0 / self._S)
+
+    def _extra_params(self):
+        return {"density": self._density}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        return {"density": float(d.get("density", 1.0 / 3.0))}
+
+
+SparseJLT = SJLT
+
+__all__ = ["JLT", "CT", "SJLT", "SparseJLT", "DenseSketch", "COLUMNWISE"]

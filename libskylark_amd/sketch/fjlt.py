@@ -160,5 +160,56 @@ class UST(SketchTransform):
         return {"replace": bool(r)}
 
 
+@register
+class NURST(SketchTransform):
+    """Non-uniform random sampling transform: ``S`` indices drawn with
+    replacement from the probability vector ``p`` over ``[0, N)``
+    (reference pure-Python ``NURST``, ``python-skylark/skylark/sketch.py:906-933``).
+
+    Draws: ``S`` uniform(0,1) slots of the context stream, mapped through the
+    inverse CDF of ``p`` (so the indices are reproducible from the context,
+    unlike the reference's scipy draw).  ``p`` is normalised; it is stored in
+    the serialised form.
+    """
+
+    sketch_type = "NURST"
+    supports_sparse_output = True
+
+    def __init__(self, n, s, p=None, context=None):
+        import numpy as np
+        if p is None:
+            raise ValueError("NURST needs a probability vector p")
+        p = np.asarray(p.cpu().numpy() if isinstance(p, torch.Tensor) else p, dtype=np.float64).reshape(-1)
+        if p.shape[0] != int(n):
+            from ..base.exceptions import InvalidParametersError
+            raise InvalidParametersError("size of probability array should be exactly n")
+        if (p < 0).any() or p.sum() <= 0:
+            from ..base.exceptions import InvalidParametersError
+            raise InvalidParametersError("p must be a non-negative, non-zero vector")
+        self._p = p / p.sum()
+        super().__init__(n, s, context)
+
+    def _build(self, ctx):
+        import numpy as np
+        u = ctx.generate_random_samples_array(self._S, D.Uniform(0.0, 1.0)).cpu().numpy()
+        cdf = np.cumsum(self._p)
+        cdf[-1] = 1.0
+        idx = np.searchsorted(cdf, u, side="right")
+        self.samples = torch.from_numpy(np.minimum(idx, self._N - 1).astype(np.int64))
+
+    realize = UST.realize
+    _apply_dense = UST._apply_dense
+    _apply_sparse = UST._apply_sparse
+
+    def _extra_params(self):
+        return {"p": [float(x) for x in self._p]}
+
+    @classmethod
+    def _params_from_dict(cls, d):
+        return {"p": d["p"]}
+
+
 URST = UST
+UniformSampler = UST
+NonUniformSampler = NURST
 FastJLT = FJLT

@@ -36,6 +36,8 @@ LINEAR = [
     lambda c: sk.sketch.FJLT(N, S, context=c),
     lambda c: sk.sketch.UST(N, S, replace=True, context=c),
     lambda c: sk.sketch.UST(N, S, replace=False, context=c),
+    lambda c: sk.sketch.SJLT(N, S, density=0.25, context=c),
+    lambda c: sk.sketch.NURST(N, S, p=np.linspace(1.0, 2.0, N), context=c),
 ]
 
 
@@ -211,3 +213,27 @@ def test_fut_transforms():
     T = sk.sketch.FJLT(300, 280, context=sk.Context(1))
     A = _A(300, 4)
     torch.testing.assert_close(T * A, T.realize() @ A)
+
+
+def test_sjlt_density_and_scale():
+    T = sk.sketch.SJLT(4000, 50, density=0.1, context=sk.Context(5))
+    W = T.realize()
+    nz = (W != 0).double().mean().item()
+    assert abs(nz - 0.1) < 0.01
+    vals = W[W != 0].abs().unique()
+    assert torch.allclose(vals, torch.tensor([math.sqrt(1 / (0.1 * 50))], dtype=torch.float64))
+    # E[S^T S] = I  ->  norms preserved on average
+    x = _A(4000, 1, seed=3)
+    r = ((T * x).norm() / x.norm()).item()
+    assert 0.6 < r < 1.4
+
+
+def test_nurst_follows_probabilities():
+    p = np.zeros(10)
+    p[[2, 7]] = [1.0, 3.0]
+    T = sk.sketch.NURST(10, 4000, p=p, context=sk.Context(9))
+    idx = T.samples.numpy()
+    assert set(np.unique(idx)) == {2, 7}
+    assert abs((idx == 7).mean() - 0.75) < 0.03
+    A = _A(10, 3)
+    assert torch.equal(T * A, A[torch.from_numpy(idx)])
