@@ -1,10 +1,125 @@
-"""Fused RNG-GEMM and streaming tall-skinny MFMA kernels (see _native/src/*)."""
+"""Fused dense-sketch / random-feature GEMM (``_native/src/feature_gemm.hip``).
+
+``Z = outscale * epi(scale_f * (A W^T)[r, f] + shift_f)`` in one launch on
+bf16 MFMA: f32 inputs are split into bf16 hi + lo in-kernel and the realised
+sketching matrix W is held as a bf16 hi + lo pair, so the 3-term product is
+f32-class accurate (|err| ~ 2^-16 of sum |a w|) at 3/16 of the bf16 MFMA cost.
+
+Used by the dense transforms (JLT / CT / SJLT, ``epi = none``) and the
+feature maps (RFT / QRFT ``cos``, RLT / QRLT ``exp(-x)``) whenever the
+sketched dimension is small enough for W (``S x N``) to be realised once and
+cached on the device (``MAX_W_ELEMS``); tall sketched dimensions stream W
+panels through ``ops.dense_sketch`` instead.
+"""
 from __future__ import annotations
 
+import ctypes as C
+import os
 
+import torch
+
+from . import _lib
+
+EPI_NONE, EPI_COS, EPI_EXPNEG = 0, 1, 2
+BN, BK = 128, 32
+MAX_W_ELEMS = 1 << 26          # W (S x N) realised whole up to 64 M entries (256 MB as hi+lo)
+
+_lib.register("sl_feature_gemm", [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64,
+                                  C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                  C.c_void_p, C.c_void_p, C.c_float, C.c_int,
+                                  C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p])
+
+
+def enabled() -> bool:
+    return os.environ.get("SKH_FUSED_SKETCH", "1") != "0"
+
+
+def fused_ok(A: torch.Tensor, dim: int, k: int, nf: int) -> bool:
+    """Can (and should) ``A`` (dense, on a GPU) take the fused kernel?"""
+    if not (enabled() and isinstance(A, torch.Tensor) and A.is_cuda and A.dim() == 2
+            and A.layout == torch.strided and A.dtype in (torch.float32, torch.bfloat16)):
+        return False
+    if k <= 0 or nf <= 0 or nf * k > MAX_W_ELEMS or not _lib.available():
+        return False
+    if dim == 1:
+        return True
+    # columnwise needs A^T row-major: free if A is a transposed view, else a copy
+    # that only pays off when the product is wide enough to be compute bound
+    return A.t().is_contiguous() or nf >= 256
+
+
+class SplitW:
+    """A realised S x N block of W as zero-padded bf16 hi/lo planes."""
+
+    __slots__ = ("hi", "lo", "nf", "k", "ldw")
+
+    def __init__(self, W: torch.Tensor):
+        nf, k = W.shape
+        npad = -(-nf // BN) * BN
+        ldw = -(-k // BK) * BK
+        Wf = torch.zeros(npad, ldw, dtype=torch.float32, device=W.device)
+        Wf[:nf, :k] = W
+        self.hi = Wf.to(torch.bfloat16)
+        self.lo = (Wf - self.hi.float()).to(torch.bfloat16)
+        self.nf, self.k, self.ldw = nf, k, ldw
+
+
+def _align_rows(X: torch.Tensor) -> torch.Tensor:
+    """Row-major with 16-B aligned rows (what the kernel's vector loads need)."""
+    align = 4 if X.dtype == torch.float32 else 8
+    if X.stride(1) == 1 and X.stride(0) % align == 0 and X.data_ptr() % 16 == 0 and X.stride(0) >= X.shape[1]:
+        return X
+    m, k = X.shape
+    ld = -(-k // align) * align
+    buf = torch.empty(m, ld, dtype=X.dtype, device=X.device)
+    buf[:, :k] = X
+    return buf[:, :k]
+
+
+def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=None,
+                 outscale: float = 1.0, epi: int = EPI_NONE, out_dtype=torch.float32,
+                 use_lo: bool = True) -> torch.Tensor:
+    """Columnwise (dim 0: A is K x m -> Z is nf x m) or rowwise (dim 1: A is
+    m x K -> Z is m x nf) fused product with W^T and the epilogue."""
+    X = A if dim == 1 else A.t()
+    m, k = X.shape
+    if k != W.k:
+        raise ValueError(f"feature_gemm: inner dimension {k} != {W.k}")
+    X = _align_rows(X)
+    dev = A.device
+    if dim == 1:
+        out = torch.empty(m, W.nf, dtype=out_dtype, device=dev)
+        ldo, out_t = W.nf, 0
+    else:
+        out = torch.empty(W.nf, m, dtype=out_dtype, device=dev)
+        ldo, out_t = m, 1
+    sc = scales.to(device=dev, dtype=torch.float32).contiguous() if scales is not None else None
+    sh = shifts.to(device=dev, dtype=torch.float32).contiguous() if shifts is not None else None
+    _lib.call("sl_feature_gemm", _lib.ptr(X), _lib.dtype_code(X.dtype), m, k, X.stride(0),
+              _lib.ptr(W.hi), _lib.ptr(W.lo) if use_lo else None, W.nf, W.ldw,
+              _lib.ptr(sc) if sc is not None else None, _lib.ptr(sh) if sh is not None else None,
+              float(outscale), int(epi), _lib.ptr(out), _lib.dtype_code(out_dtype), ldo, out_t,
+              C.c_void_p(_lib.stream_of(out)))
+    return out
+
+
+class WCache:
+    """Per-sketch cache of realised, split W blocks keyed by device and window."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, key, make):
+        w = self._d.get(key)
+        if w is None:
+            w = SplitW(make())
+            self._d[key] = w
+        return w
+
+    def clear(self):
+        self._d.clear()
+
+
+# kept for the dense_sketch hook
 def dense_sketch_fused_ok(A, dim, s, k, m) -> bool:
     return False
-
-
-def dense_sketch_fused(*a, **k):
-    raise NotImplementedError

@@ -12,6 +12,7 @@ import torch
 
 from ..base import distributions as D
 from ..ops import dense_sketch as _ds
+from ..ops import fused as _fused
 from .base import COLUMNWISE, SketchTransform, register
 
 
@@ -43,6 +44,16 @@ class DenseSketch(SketchTransform):
                                  precise=dtype == torch.float64)
 
     def _apply_dense(self, A, dim, in_offset: int = 0, out_rows=None):
+        k = A.shape[dim]
+        i0, i1 = out_rows if out_rows is not None else (0, self._S)
+        if _fused.fused_ok(A, dim, k, i1 - i0):
+            # W block realised once (f64 sampler -> f32 -> bf16 hi/lo) and cached
+            # on the device; one MFMA launch per apply (ops/fused.py)
+            if getattr(self, "_wcache", None) is None:
+                self._wcache = _fused.WCache()
+            W = self._wcache.get((str(A.device), i0, i1, in_offset, k), lambda: self.realize(
+                torch.float64, A.device, rows=(i0, i1), cols=(in_offset, in_offset + k)).float())
+            return _fused.feature_gemm(A, W, dim, use_lo=self.precision != "bf16x2")
         return _ds.apply_dense(A, dim, dist=self.dist, seed=self.entries.seed, base=self.entries.base,
                                S=self._S, N=self._N, scale=self.scale, in_offset=in_offset,
                                out_rows=out_rows, precision=self.precision)

@@ -27,6 +27,7 @@ from ..base import distributions as D
 from ..base import quasirand as Q
 from ..ops import _lib
 from ..ops import dense_sketch as _ds
+from ..ops import fused as _fused
 from .base import COLUMNWISE, SketchTransform, register
 
 _lib.register("sl_feature_epilogue", [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
@@ -71,6 +72,18 @@ class _FeatureMap(SketchTransform):
         return feature_epilogue(X, sc, sh, self.outscale, 0 if dim == COLUMNWISE else 1, self.mode)
 
     def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
+        k = A.shape[dim]
+        i0, i1 = out_rows if out_rows is not None else (0, self._S)
+        if hasattr(self, "realize_W") and in_offset == 0 and k == self._N and _fused.fused_ok(A, dim, k, i1 - i0):
+            # GEMM + cos/exp epilogue in one MFMA launch (ops/fused.py)
+            if getattr(self, "_wcache", None) is None:
+                self._wcache = _fused.WCache()
+            W = self._wcache.get((str(A.device), i0, i1),
+                                 lambda: self.realize_W(torch.float64, A.device)[i0:i1].float())
+            sc = self.scales[i0:i1] if getattr(self, "scales", None) is not None else None
+            sh = self.shifts[i0:i1] if getattr(self, "shifts", None) is not None else None
+            epi = _fused.EPI_COS if self.mode == EPI_COS else _fused.EPI_EXPNEG
+            return _fused.feature_gemm(A, W, dim, scales=sc, shifts=sh, outscale=self.outscale, epi=epi)
         return self._post(self._features_pre(A, dim, in_offset, out_rows), dim, out_rows)
 
     def _apply_sparse(self, A, dim, sparse_out):
