@@ -342,7 +342,7 @@ class _DevicePlan:
         if host[-1] != 0:
             return None
         Cm = host[:k * k].reshape(k, k)
-        evals, evecs = np.linalg.eigh(0.5 * (Cm + Cm.T))
+        evals, evecs = _host_eigh(0.5 * (Cm + Cm.T))
         order = np.argsort(evals)[::-1][:r]
         s = np.sqrt(np.clip(evals[order], 0.0, None))
         self.small.copy_(torch.from_numpy(np.concatenate([evecs[:, order].reshape(-1), s])))
@@ -354,6 +354,24 @@ class _DevicePlan:
             # result needs no copy out of the graph's static memory
             U, _ = T.f32_xm(self.Y, self.M, store=True)
         return U, self.s.clone(), self.V.clone()
+
+
+def _host_eigh(C: np.ndarray):
+    """LAPACK eigh of the k x k core on ONE host thread: for k ~ 40 the
+    threaded BLAS costs 2-4x more than it saves (measured 177 us single
+    threaded vs 290-700 us threaded on the build host).  A device Jacobi
+    (ops.small_la.sym_eig_topr) was measured at ~500 us for k = 40, so the
+    host solve stays on the randSVD critical path."""
+    n = torch.get_num_threads()
+    if n == 1:
+        w, v = torch.linalg.eigh(torch.from_numpy(C))
+        return w.numpy(), v.numpy()
+    torch.set_num_threads(1)
+    try:
+        w, v = torch.linalg.eigh(torch.from_numpy(C))
+    finally:
+        torch.set_num_threads(n)
+    return w.numpy(), v.numpy()
 
 
 _PLANS: dict = {}

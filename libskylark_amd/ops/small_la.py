@@ -18,6 +18,21 @@ from . import tallskinny as T
 vp, i32 = C.c_void_p, C.c_int
 _lib.register("sl_small_chol_inv", [vp, i32, i32, vp, vp, vp, vp, vp])
 _lib.register("sl_small_matmul", [vp, vp, vp, i32, i32, i32, vp, vp])
+_lib.register("sl_sym_eig_topr", [vp, i32, i32, i32, vp, i32, i32, vp, vp])
+
+
+def sym_eig_topr(C: torch.Tensor, r: int, out: torch.Tensor | None = None, sqrt: bool = False,
+                 max_sweeps: int = 30, sweeps: torch.Tensor | None = None):
+    """Top-``r`` eigenpairs (descending) of a symmetric k x k (k <= 64) matrix
+    by device Jacobi: returns ``out`` (f64, k*r + r) = [V_r row-major, lambda_r]
+    (``sqrt(max(lambda, 0))`` with ``sqrt``), all on C's device, no host sync."""
+    k = C.shape[0]
+    C = C.to(torch.float64).contiguous()
+    if out is None:
+        out = torch.empty(k * r + r, dtype=torch.float64, device=C.device)
+    _lib.call("sl_sym_eig_topr", _lib.ptr(C), k, k, r, _lib.ptr(out), int(bool(sqrt)), int(max_sweeps),
+              _lib.ptr(sweeps) if sweeps is not None else None, vp(_lib.stream_of(C)))
+    return out
 
 
 def chol_inv(G: torch.Tensor, status: torch.Tensor | None = None):

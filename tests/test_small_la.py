@@ -1,4 +1,5 @@
 """GPU-resident small linear algebra (k <= 64) vs fp64 torch references."""
+import math
 import pytest
 import torch
 
@@ -56,3 +57,44 @@ def test_small_matmul(dev):
     C, C32 = SL.small_matmul(A, B, want32=True)
     torch.testing.assert_close(C, A @ B)
     torch.testing.assert_close(C32, (A @ B).float())
+
+
+@pytest.mark.parametrize("k,r", [(40, 20), (7, 3), (64, 64), (48, 10)])
+@pytest.mark.parametrize("spread", [1.0, 1e-12])
+def test_sym_eig_topr_vs_lapack(dev, k, r, spread):
+    g = torch.Generator().manual_seed(k)
+    Q, _ = torch.linalg.qr(torch.randn(k, k, generator=g, dtype=torch.float64))
+    lam = torch.logspace(0, math.log10(spread), k, dtype=torch.float64) if spread != 1.0 else \
+        torch.rand(k, generator=g, dtype=torch.float64) + 0.1
+    C = (Q * lam) @ Q.t()
+    out = SL.sym_eig_topr(C.to(dev), r, sqrt=True).cpu()
+    V, s = out[:k * r].view(k, r), out[k * r:]
+    ref = torch.sort(torch.linalg.eigvalsh(C), descending=True).values[:r]
+    # backward stable: |lambda - lambda_lapack| ~ eps * ||C||
+    assert ((s * s - ref).abs().max() / lam.max()) < 1e-13, (s * s - ref).abs().max()
+    # eigenvector residuals
+    res = (C @ V - V * (s * s)).norm(dim=0) / lam.max()
+    assert res.max() < 1e-10
+    assert torch.allclose(V.t() @ V, torch.eye(r, dtype=torch.float64), atol=1e-10)
+
+
+def test_sym_eig_repeated_eigenvalues(dev):
+    k = 32
+    C = torch.diag(torch.tensor([2.0] * 16 + [1.0] * 16, dtype=torch.float64))
+    g = torch.Generator().manual_seed(0)
+    Q, _ = torch.linalg.qr(torch.randn(k, k, generator=g, dtype=torch.float64))
+    C = Q @ C @ Q.t()
+    out = SL.sym_eig_topr(C.to(dev), 20).cpu()
+    lam = out[k * 20:]
+    assert torch.allclose(lam[:16], torch.full((16,), 2.0, dtype=torch.float64), atol=1e-12)
+    assert torch.allclose(lam[16:], torch.full((4,), 1.0, dtype=torch.float64), atol=1e-12)
+
+
+def test_sym_eig_converges_in_few_sweeps(dev):
+    k = 40
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(1000, k, generator=g, dtype=torch.float64)
+    C = X.t() @ X
+    sweeps = torch.zeros(1, dtype=torch.int32, device=dev)
+    SL.sym_eig_topr(C.to(dev), 20, sweeps=sweeps)
+    assert 2 <= int(sweeps.item()) <= 12
