@@ -236,8 +236,9 @@ class _DevicePlan:
     replays always see A's current contents.  The small outputs (s, V) are
     cloned out of graph memory; U = Y M is one eager launch into a fresh
     tensor (no m x r copy).  With more than
-    one rank the collectives stay eager unless SKH_GRAPH_COLLECTIVES=1
-    (RCCL capture); if a capture fails the plan stays eager.
+    one rank segment 1 is split at its all-reduces: each piece is its own
+    graph and the collectives run eagerly between the replays (no RCCL
+    capture); if a capture fails the plan stays eager.
     """
 
     def __init__(self, A_loc, comm, n, rank, k, q, skip_qr, use_graph):
@@ -257,24 +258,34 @@ class _DevicePlan:
         self.ws64 = torch.empty(T.gram64_workspace_bytes(m, k), dtype=torch.uint8, device=dev)
         self.use_graph = use_graph
         self.g1 = self.g2 = None
+        self.piece_graphs = None   # multi-rank: per-piece graphs (False: capture failed)
+        self._Wout = [None] * (q + 1)
         self.calls = 0
 
-    def seg1(self):
+    # ---- segment 1 as pieces separated by the collectives: with one rank the
+    # pieces are captured into one graph; with several, each piece is its own
+    # graph and the all-reduces run eagerly between replays, so multi-GPU
+    # steps replay ~5 graphs instead of launching ~35 kernels from Python.
+    def _piece_pass(self, i):
         from ..ops import small_la as SL
         from ..ops import tallskinny as T
-        st, A, comm, n = self.status, self.Aref(), self.comm, self.n
-        st.zero_()
-        Z = self.Zs
         prof = PROFILER
-        for _ in range(self.q):
-            with prof.phase("svd.fused_pass"):
-                W, _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws)
-            with prof.phase("svd.allreduce_small"):
-                comm.all_reduce(W)
+        A = self.Aref()
+        if i == 0:
+            self.status.zero_()
+            Z = self.Zs
+        else:
             with prof.phase("svd.orth"):
                 # only the subspace matters between passes: one CholeskyQR step
+                W = self._Wout[i - 1]
                 Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-30) if self.skip_qr else \
-                    SL.cholqr(W, st, ws=self.ws32)
+                    SL.cholqr(W, self.status, ws=self.ws32)
+        if i < self.q:
+            with prof.phase("svd.fused_pass"):
+                # every piece writes its own output slot: a piece's capture then
+                # reads its predecessor's graph-owned result, never its own warm-up's
+                self._Wout[i], _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws)
+            return self._Wout[i]
         with prof.phase("svd.fused_pass"):
             W, _, Y = T.fused_pass(A, Z, keep_y=True, gram=False, exact=True, ws=self.ws)
         with prof.phase("svd.final_qr"):
@@ -282,20 +293,39 @@ class _DevicePlan:
             # then leaves Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2
             # with an f32 second Gram only reached ~eps32, at three times the work)
             G = T.gram64(Y, ws=self.ws64)
-        with prof.phase("svd.allreduce_small"):
-            WG = torch.cat([W.double(), G], 0)
-            comm.all_reduce(WG)
-            W, G = WG[:n], WG[n:]
-        with prof.phase("svd.final_qr"):
-            _, Rti, _ = SL.chol_inv(G, st)
+            self._WG = torch.cat([W.double(), G], 0)
+        self.Y = Y
+        return self._WG
+
+    def _piece_core(self):
+        from ..ops import small_la as SL
+        n = self.n
+        W, G = self._WG[:n], self._WG[n:]
+        with PROFILER.phase("svd.final_qr"):
+            _, Rti, _ = SL.chol_inv(G, self.status)
             # B^T = A^T Q = W Rt^{-1} (n x k); its right singular pairs come from the
             # k x k f64 Gram C = Rt^{-T} (W^T W) Rt^{-1} = Ub S^2 Ub^T (host eigensolve).
             # sigma_i keeps relative accuracy ~eps64 (sigma_1/sigma_i)^2, far below
             # the bf16 data error for every rank the sketch resolves.
             Vt = W @ Rti
             C = Vt.t() @ Vt
-            self.host_src = torch.cat([C.reshape(-1), st.double()])
-        self.Y, self.Rti, self.Vt = Y, Rti, Vt
+            self.host_src = torch.cat([C.reshape(-1), self.status.double()])
+        self.Rti, self.Vt = Rti, Vt
+
+    def pieces(self):
+        """[(graph-able piece, tensor to all-reduce after it or None)]"""
+        out = [(lambda i=i: self._piece_pass(i), True) for i in range(self.q + 1)]
+        out.append((self._piece_core, False))
+        return out
+
+    def seg1(self):
+        with PROFILER.phase("svd.allreduce_small"):
+            pass
+        for fn, reduce_after in self.pieces():
+            t = fn()
+            if reduce_after:
+                with PROFILER.phase("svd.allreduce_small"):
+                    self.comm.all_reduce(t)
 
     def seg2(self):
         k, r = self.k, self.rank
@@ -306,7 +336,7 @@ class _DevicePlan:
             self.M = (self.Rti @ Ub).float()                              # U = Y Rt^{-1} Ub
             self.s = s64.float()
 
-    def _capture(self, fn):
+    def _capture(self, fn, want_out=False):
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
@@ -314,13 +344,30 @@ class _DevicePlan:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            fn()
-        return g
+            out = fn()
+        return (g, out) if want_out else g
 
     def _run(self, which):
         fn = self.seg1 if which == 1 else self.seg2
         g = self.g1 if which == 1 else self.g2
-        if g is None and self.use_graph and self.calls >= 1 and not PROFILER.enabled:
+        warm = self.use_graph and self.calls >= 1 and not PROFILER.enabled
+        if which == 1 and self.comm.size > 1 and self.piece_graphs is not False:
+            # multi-rank: one graph per piece, eager collectives in between
+            if self.piece_graphs is None and warm:
+                try:
+                    self.piece_graphs = [(*self._capture(f, want_out=True), r) for f, r in self.pieces()]
+                except Exception:  # noqa: BLE001 - capture unsupported here: stay eager
+                    self.piece_graphs = False
+            if self.piece_graphs:
+                for gp, out, reduce_after in self.piece_graphs:
+                    gp.replay()
+                    if reduce_after:
+                        with PROFILER.phase("svd.allreduce_small"):
+                            self.comm.all_reduce(out)
+                return
+            fn()
+            return
+        if g is None and warm:
             try:
                 g = self._capture(fn)
             except Exception:  # noqa: BLE001 - capture unsupported here: stay eager
@@ -398,8 +445,7 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
             _PLANS.pop(next(iter(_PLANS)))
         # multi-rank: capture collectives only on request — a capture that fails on
         # one rank but not another would desynchronise the collectives
-        use_graph = bool(params.graph) and dev.type == "cuda" and (
-            comm.size == 1 or os.environ.get("SKH_GRAPH_COLLECTIVES", "0") == "1")
+        use_graph = bool(params.graph) and dev.type == "cuda"
         plan = _DevicePlan(A_loc, comm, n, rank, k, q, params.skip_qr, use_graph)
         _PLANS[key] = plan
     res = plan(Z)
