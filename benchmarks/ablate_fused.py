@@ -22,7 +22,8 @@ from libskylark_amd.ops import _lib, rng
 def main():
     m, n, k = 1_000_000, 1000, int(sys.argv[1]) if len(sys.argv) > 1 else 40
     dev = torch.device("cuda")
-    A = torch.empty(m, n, dtype=torch.bfloat16, device=dev)
+    lda = int(os.environ.get("LDA", n))   # padded leading dimension (elements)
+    A = torch.empty(m, lda, dtype=torch.bfloat16, device=dev)[:, :n]
     rng.fill_random(A, D.Normal(), 1, 0, ir=n, ic=1)
     Zt = (torch.randn(k, n, device=dev) / 30).to(torch.bfloat16)
     W = torch.empty(n, k, device=dev)
@@ -39,7 +40,8 @@ def main():
 
     flags = [0]
     variants = {"full": 0, "k32_step3": 16, "hi_only": 32, "hi_only_nog": 40, "no_step1": 1, "no_step2": 2,
-                "no_step3": 4, "no_step4": 8, "no_3_4": 12, "loads_only": 15}
+                "no_step3": 4, "no_step4": 8, "no_3_4": 12, "loads_only": 15,
+                "loads_only_nt": 79, "full_nt": 64, "hi_only_nog_nt": 104}
     res = {v: [] for v in variants}
     for nb in (3, 4, 5):
         lib.sl_tsk_set_nbuf(nb)
