@@ -23,10 +23,12 @@ fp64 CholeskyQR only.
 """
 from __future__ import annotations
 
+import math
 import os
+import sys
+import time
 import weakref
 
-import math
 from dataclasses import dataclass
 
 import numpy as np
@@ -250,8 +252,13 @@ class _DevicePlan:
         self.dev = dev
         self.comm, self.n, self.rank, self.k, self.q, self.skip_qr = comm, n, rank, k, q, skip_qr
         self.Zs = torch.empty(n, k, dtype=torch.float32, device=dev)
+        # FJLT sketches are realised inside segment 1 from device-held stream
+        # coordinates {seed, base_D, base_samples} (ops.fut.fjlt_operator)
+        self.prm = torch.zeros(3, dtype=torch.int64, device=dev)
+        self.fjlt_scale = None
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.small = torch.zeros(k * rank + rank, dtype=torch.float64, device=dev)
+        self.small_host = torch.zeros(k * rank + rank, dtype=torch.float64).pin_memory()
         self.ws = torch.empty(T.fused_workspace_bytes(m, n, k), dtype=torch.uint8, device=dev)
         self.ws32 = torch.empty(max(T.f32_workspace_bytes(m), T.f32_workspace_bytes(n)), dtype=torch.uint8,
                                 device=dev)
@@ -273,6 +280,10 @@ class _DevicePlan:
         A = self.Aref()
         if i == 0:
             self.status.zero_()
+            if self.fjlt_scale is not None:
+                from ..ops import fut as F
+                with prof.phase("svd.sketch"):
+                    F.fjlt_operator(self.prm, self.k, self.n, self.fjlt_scale, self.Zs, transpose=True)
             Z = self.Zs
         else:
             with prof.phase("svd.orth"):
@@ -309,6 +320,7 @@ class _DevicePlan:
             # the bf16 data error for every rank the sketch resolves.
             Vt = W @ Rti
             C = Vt.t() @ Vt
+            C = 0.5 * (C + C.t())
             self.host_src = torch.cat([C.reshape(-1), self.status.double()])
         self.Rti, self.Vt = Rti, Vt
 
@@ -335,6 +347,14 @@ class _DevicePlan:
             self.V = ((self.Vt @ Ub) / s64.clamp_min(1e-300)).float()   # V = A^T Q Ub S^{-1}
             self.M = (self.Rti @ Ub).float()                              # U = Y Rt^{-1} Ub
             self.s = s64.float()
+
+    def graph_built(self):
+        return self.g1 is not None or bool(self.piece_graphs)
+
+    def reset_graphs(self):
+        self.g1 = self.g2 = None
+        self.piece_graphs = None
+        self.calls = 0
 
     def _capture(self, fn, want_out=False):
         s = torch.cuda.Stream(device=self.dev)
@@ -381,29 +401,56 @@ class _DevicePlan:
         else:
             fn()
 
-    def __call__(self, Z):
-        self.Zs.copy_(Z)
+    def __call__(self, Z=None, fjlt=None):
+        """``Z``: realised sketch operator (n x k), or ``fjlt`` = (seed, base_D,
+        base_samples, scale) to realise an FJLT inside the graph."""
+        if fjlt is not None:
+            if self.fjlt_scale is None and self.graph_built():
+                self.reset_graphs()
+            self.fjlt_scale = float(fjlt[3])
+            self.prm.copy_(torch.tensor(fjlt[:3], dtype=torch.int64))
+        else:
+            if self.fjlt_scale is not None:
+                self.fjlt_scale = None
+                self.reset_graphs()
+            self.Zs.copy_(Z)
+        tr = _TRACE and [time.perf_counter()]
         self._run(1)
-        host = self.host_src.cpu().numpy()
+        tr and tr.append(time.perf_counter())
+        host = self.host_src.cpu()
+        tr and tr.append(time.perf_counter())
         k, r = self.k, self.rank
-        if host[-1] != 0:
+        if float(host[-1]) != 0.0:
             return None
-        Cm = host[:k * k].reshape(k, k)
-        evals, evecs = _host_eigh(0.5 * (Cm + Cm.T))
-        order = np.argsort(evals)[::-1][:r]
-        s = np.sqrt(np.clip(evals[order], 0.0, None))
-        self.small.copy_(torch.from_numpy(np.concatenate([evecs[:, order].reshape(-1), s])))
+        # C was symmetrised on the device; eigh returns ascending eigenpairs
+        evals, evecs = _host_eigh(host[:k * k].view(k, k))
+        pin = self.small_host
+        pin[:k * r].view(k, r).copy_(evecs[:, k - r:].flip(1))
+        torch.sqrt(evals[k - r:].flip(0).clamp_min(0.0), out=pin[k * r:])
+        tr and tr.append(time.perf_counter())
+        # pinned + non_blocking: the copy is ordered on the stream, the host
+        # does not wait (the buffer is rewritten only after the next call's
+        # synchronising D2H, which follows this copy in stream order)
+        self.small.copy_(pin, non_blocking=True)
+        tr and tr.append(time.perf_counter())
         self._run(2)
+        tr and tr.append(time.perf_counter())
         self.calls += 1
         from ..ops import tallskinny as T
         with PROFILER.phase("svd.form_U"):
             # outside the graph: U lands in a fresh allocation, so the m x r
             # result needs no copy out of the graph's static memory
             U, _ = T.f32_xm(self.Y, self.M, store=True)
-        return U, self.s.clone(), self.V.clone()
+        out = U, self.s.clone(), self.V.clone()
+        if tr:
+            tr.append(time.perf_counter())
+            names = ["replay1", "d2h_sync", "eigh", "h2d", "replay2", "form_U"]
+            print("[svd.trace] " + " ".join(f"{n}={(b - a) * 1e6:.0f}us" for n, a, b in zip(names, tr, tr[1:])),
+                  file=sys.stderr)
+        return out
 
 
-def _host_eigh(C: np.ndarray):
+def _host_eigh(C: torch.Tensor):
     """LAPACK eigh of the k x k core on ONE host thread: for k ~ 40 the
     threaded BLAS costs 2-4x more than it saves (measured 177 us single
     threaded vs 290-700 us threaded on the build host).  A device Jacobi
@@ -411,17 +458,16 @@ def _host_eigh(C: np.ndarray):
     host solve stays on the randSVD critical path."""
     n = torch.get_num_threads()
     if n == 1:
-        w, v = torch.linalg.eigh(torch.from_numpy(C))
-        return w.numpy(), v.numpy()
+        return torch.linalg.eigh(C)
     torch.set_num_threads(1)
     try:
-        w, v = torch.linalg.eigh(torch.from_numpy(C))
+        return torch.linalg.eigh(C)
     finally:
         torch.set_num_threads(n)
-    return w.numpy(), v.numpy()
 
 
 _PLANS: dict = {}
+_TRACE = os.environ.get("SKH_TRACE_SVD", "0") == "1"   # host-side phase timestamps
 
 
 def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
@@ -432,8 +478,18 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     the robust host path with the same, rewound, context)."""
     ctx0 = ctx.copy()
     dev = A_loc.device
-    with PROFILER.phase("svd.sketch"):
-        Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float32)
+    fjlt = None
+    if params.sketch.upper() == "FJLT":
+        # FJLT_data draw layout: N Rademacher signs, then S sample rows; the
+        # operator itself is realised on the device inside the plan's graph
+        base_d = ctx.counter
+        base_s = base_d + n
+        ctx.counter = base_s + k
+        fjlt = (ctx.seed, base_d, base_s, math.sqrt(n / k))
+        Z = None
+    else:
+        with PROFILER.phase("svd.sketch"):
+            Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float32)
     q = max(0, int(params.num_iterations))
     key = (A_loc.data_ptr(), tuple(A_loc.shape), tuple(A_loc.stride()), A_loc.dtype, str(dev), rank, k, q,
            bool(params.skip_qr), comm.size, id(getattr(comm, "group", None)))
@@ -448,7 +504,7 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
         use_graph = bool(params.graph) and dev.type == "cuda"
         plan = _DevicePlan(A_loc, comm, n, rank, k, q, params.skip_qr, use_graph)
         _PLANS[key] = plan
-    res = plan(Z)
+    res = plan(Z, fjlt=fjlt)
     if res is None:
         ctx.seed, ctx.counter = ctx0.seed, ctx0.counter
     return res

@@ -123,3 +123,29 @@ def dct2_rows_matrix(N: int, rows: torch.Tensor, dtype=torch.float64, device=Non
     F = F * scale
     F = F.t() if transpose else F
     return F.to(dtype).contiguous()
+
+
+def _register_fjlt():
+    import ctypes as C
+    from . import _lib
+    _lib.register("sl_fjlt_operator", [C.c_void_p, C.c_int64, C.c_int64, C.c_double, C.c_void_p, C.c_int,
+                                       C.c_int64, C.c_int, C.c_void_p])
+
+
+_register_fjlt()
+
+
+def fjlt_operator(prm: torch.Tensor, S: int, N: int, scale: float, out: torch.Tensor,
+                  transpose: bool = True) -> torch.Tensor:
+    """FJLT operator ``scale * P F D`` realised from stream coordinates held on
+    the device (``prm`` = int64 {seed, base_D, base_samples}); graph-capturable
+    (``sl_fjlt_operator``).  ``out``: N x S (transpose) or S x N, row-major."""
+    import ctypes as C
+    from . import _lib
+    _lib.require()
+    exp = (N, S) if transpose else (S, N)
+    if tuple(out.shape) != exp or out.stride(1) != 1 or prm.dtype != torch.int64 or not prm.is_cuda:
+        raise ValueError("fjlt_operator: bad operand layout")
+    _lib.call("sl_fjlt_operator", _lib.ptr(prm), S, N, float(scale), _lib.ptr(out), _lib.dtype_code(out.dtype),
+              out.stride(0), int(transpose), C.c_void_p(_lib.stream_of(out)))
+    return out

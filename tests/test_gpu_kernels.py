@@ -96,3 +96,15 @@ def test_dct2_rows_native(dev, N, S):
         torch.testing.assert_close(got.cpu(), ref.t() if tr else ref, rtol=1e-12, atol=1e-12)
     got32 = fut.dct2_rows_matrix(N, rows, dtype=torch.float32, device=dev, d=d, scale=1.7, transpose=True)
     torch.testing.assert_close(got32.cpu().double(), ref.t(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,S", [(1000, 40), (257, 13)])
+def test_fjlt_operator_from_device_params_matches_sketch(dev, N, S):
+    from libskylark_amd.ops import fut as F
+    ctx = sk.Context(38734, counter=77)
+    T = sk.sketch.FJLT(N, S, context=ctx.copy())
+    ref = T.realize(torch.float64, transpose=True)
+    prm = torch.tensor([ctx.seed, ctx.counter, ctx.counter + N], dtype=torch.int64, device=dev)
+    out = torch.empty(N, S, dtype=torch.float64, device=dev)
+    F.fjlt_operator(prm, S, N, (N / S) ** 0.5, out, transpose=True)
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-12, rtol=1e-12)
