@@ -61,6 +61,13 @@ class Comm:
     def is_root(self):
         return self.rank == 0
 
+    def collective_device(self) -> torch.device:
+        """Where tensors must live for this backend's collectives (RCCL: the
+        current GPU; gloo / single rank: host)."""
+        if self.backend == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
     def _ready(self, t):
         return t
 
