@@ -1,6 +1,6 @@
 """``skylark_convert2hdf5``: LIBSVM -> HDF5 conversion (reference
-``ml/skylark_convert2hdf5.cpp``).  Requires h5py (absent from this image: the
-tool then exits with a clear error)."""
+``ml/skylark_convert2hdf5.cpp``).  Writes through h5py when installed,
+otherwise through the built-in HDF5 writer (``io/h5.py``)."""
 from __future__ import annotations
 
 import argparse

@@ -4,9 +4,8 @@
   writer (:mod:`.libsvm`).
 * Arc lists (edge lists): byte-range parallel read into a sparse adjacency
   (:func:`read_arc_list`), reference ``utility/io/arc_list.hpp``.
-* HDF5: the reference's ``ReadHDF5``/``write_hdf5`` need h5py here, which is
-  not installed in this image — the functions exist and raise a clear
-  :class:`~libskylark_amd.base.exceptions.IOError_` unless h5py is importable.
+* HDF5: ``ReadHDF5``/``write_hdf5`` use h5py when present, otherwise the
+  built-in reader/writer of ``io/h5.py`` (no libhdf5 needed).
 * :func:`read` — ``ml/io.hpp:869`` dispatch on fileformat code
   (0 libsvm-dense, 1 libsvm-sparse, 2 hdf5-dense, 3 hdf5-sparse).
 """
@@ -25,16 +24,29 @@ def _h5py():
     try:
         import h5py  # noqa: F401
         return h5py
-    except ImportError as e:  # pragma: no cover - depends on image
-        raise IOError_("HDF5 IO requires h5py, which is not installed") from e
+    except ImportError:
+        return None
+
+
+class _H5Native:
+    """Adapter giving the built-in reader/writer (io/h5.py) h5py's File shape."""
+
+    @staticmethod
+    def File(fname, mode="r"):
+        from .h5 import H5File
+        if mode != "r":
+            raise ValueError("the built-in HDF5 module reads via H5File and writes via write_h5")
+        return H5File(fname)
 
 
 def read_hdf5(fname: str, max_n: int = -1, sparse: bool = False, dtype=torch.float64):
-    """Reference layout: datasets ``X`` (d x n, examples as columns) and ``Y``;
-    sparse files hold ``dimensions``, ``indptr``, ``indices``, ``values``.
-    Returns ``(X, Y)`` with examples as ROWS."""
-    h5py = _h5py()
-    with h5py.File(fname, "r") as f:
+    """Reference layout: datasets ``X`` (d x n, examples as columns) and ``Y``
+    (also the python-skylark dataset names ``Features`` / ``Labels``); sparse
+    files hold ``dimensions``, ``indptr``, ``indices``, ``values``.  Returns
+    ``(X, Y)`` with examples as ROWS.  Uses h5py when importable, else the
+    built-in reader (``io/h5.py``)."""
+    h5 = _h5py() or _H5Native
+    with h5.File(fname, "r") as f:
         if "indptr" in f:
             dims = np.asarray(f["dimensions"])
             d, n = int(dims[0]), int(dims[1])
@@ -47,28 +59,37 @@ def read_hdf5(fname: str, max_n: int = -1, sparse: bool = False, dtype=torch.flo
                                         (n, d))
             if not sparse:
                 X = X.to_dense()
+            yname = "Y"
         else:
-            Xd = np.asarray(f["X"])
+            xname, yname = ("X", "Y") if "X" in f else ("Features", "Labels")
+            Xd = np.asarray(f[xname])
             n = Xd.shape[1] if max_n < 0 else min(Xd.shape[1], max_n)
             X = torch.from_numpy(np.ascontiguousarray(Xd[:, :n].T)).to(dtype)
             if sparse:
                 X = X.to_sparse_csr()
-        Y = torch.from_numpy(np.asarray(f["Y"]).reshape(-1)[:X.shape[0]].astype(np.float64))
+        Y = torch.from_numpy(np.asarray(f[yname]).reshape(-1)[:X.shape[0]].astype(np.float64))
     return X, Y
 
 
 def write_hdf5(fname: str, X, Y):
+    """Write the reference layout (dense: ``X`` d x n + ``Y``; sparse:
+    ``dimensions``/``indptr``/``indices``/``values`` + ``Y``)."""
+    if X.layout != torch.strided:
+        Xc = X.to_sparse_csr().cpu()
+        data = {"dimensions": np.array([X.shape[1], X.shape[0], Xc.values().numel()], dtype=np.int64),
+                "indptr": Xc.crow_indices().numpy(), "indices": Xc.col_indices().numpy(),
+                "values": Xc.values().double().numpy()}
+    else:
+        data = {"X": X.detach().cpu().t().contiguous().double().numpy()}
+    data["Y"] = torch.as_tensor(Y).reshape(-1).cpu().double().numpy()
     h5py = _h5py()
+    if h5py is None:
+        from .h5 import write_h5
+        write_h5(fname, data)
+        return
     with h5py.File(fname, "w") as f:
-        if X.layout != torch.strided:
-            Xc = X.to_sparse_csr().cpu()
-            f["dimensions"] = np.array([X.shape[1], X.shape[0], Xc.values().numel()], dtype=np.int64)
-            f["indptr"] = Xc.crow_indices().numpy()
-            f["indices"] = Xc.col_indices().numpy()
-            f["values"] = Xc.values().numpy()
-        else:
-            f["X"] = X.detach().cpu().t().contiguous().numpy()
-        f["Y"] = torch.as_tensor(Y).reshape(-1).cpu().numpy()
+        for k, v in data.items():
+            f[k] = v
 
 
 def read(fileformat: int, fname: str, min_d: int = 0, comm=None, dtype=torch.float64, device=None):

@@ -88,3 +88,15 @@ def test_community_and_graph_se(tmp_path, capsys):
     assert graph_se.main(["-g", str(f), "-k", "2", "--prefix", pre, "--cpu"]) == 0
     X = read_ascii(pre + ".vec.txt")
     assert X.shape == (16, 2)
+
+
+def test_convert2hdf5_cli_roundtrip(tmp_path):
+    import libskylark_amd as sk
+    from libskylark_amd.cli import convert2hdf5
+    src = tmp_path / "a.libsvm"
+    src.write_text("1 1:0.5 3:2.0\n-1 2:1.5\n1 1:-1.0 2:0.25 3:1.0\n")
+    out = tmp_path / "a.h5"
+    convert2hdf5.main([str(src), str(out)])
+    X, Y = sk.io.read_hdf5(str(out))
+    assert X.shape == (3, 3) and Y.tolist() == [1.0, -1.0, 1.0]
+    assert float(X[0, 2]) == 2.0 and float(X[1, 1]) == 1.5
