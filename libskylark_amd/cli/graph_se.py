@@ -9,12 +9,13 @@ import sys
 from .. import nla
 from ..base.context import Context
 from ..ml.graph import SimpleGraph, approximate_ase
-from ._common import Timer, setup, write_ascii
+from ._common import Timer, host_if_small, setup, write_ascii
 
 
 def build_parser():
     p = argparse.ArgumentParser(prog="skylark_graph_se")
-    p.add_argument("-g", "--graphfile", required=True)
+    p.add_argument("graphfile_pos", nargs="?", default="", metavar="graphfile")
+    p.add_argument("-g", "--graphfile", default="")
     p.add_argument("-s", "--seed", type=int, default=38734)
     p.add_argument("--hdfs", default="")
     p.add_argument("--port", type=int, default=0)
@@ -26,11 +27,15 @@ def build_parser():
     p.add_argument("-n", "--numeric", action="store_true")
     p.add_argument("--prefix", default="out")
     p.add_argument("--cpu", action="store_true")
+    p.add_argument("--gpu", action="store_true", help="use the GPU even for small graphs")
     return p
 
 
 def main(argv=None):
     a = build_parser().parse_args(argv)
+    a.graphfile = a.graphfile or a.graphfile_pos
+    if not a.graphfile:
+        raise SystemExit("skylark_graph_se: a graph file is required (positional or -g)")
     if a.hdfs:
         raise SystemExit("HDFS input is not supported in this build")
     comm, dev = setup(a.cpu)
@@ -41,7 +46,8 @@ def main(argv=None):
     T.start("Computing embeddings... ")
     p = nla.ApproximateSVDParams(oversampling_ratio=a.ratio, oversampling_additive=a.additive,
                                  num_iterations=a.powerits, skip_qr=a.skipqr)
-    X, indexmap = approximate_ase(G, a.rank, Context(a.seed), p, device=dev)
+    n = G.num_vertices()
+    X, indexmap = approximate_ase(G, a.rank, Context(a.seed), p, device=host_if_small(dev, n * n, comm, a.gpu))
     T.done()
     T.start("Writing results... ")
     if comm.rank == 0:

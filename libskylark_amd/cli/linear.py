@@ -13,7 +13,7 @@ from .. import io as IO
 from .. import nla
 from ..base.context import Context
 from ..parallel.distmatrix import DistMatrix
-from ._common import Timer, setup, write_ascii
+from ._common import Timer, host_if_small, setup, write_ascii
 
 
 def build_parser():
@@ -27,6 +27,7 @@ def build_parser():
     p.add_argument("-p", "--highprecision", action="store_true", help="Solve to high precision.")
     p.add_argument("-f", "--single", action="store_true", help="Single precision instead of double.")
     p.add_argument("--cpu", action="store_true")
+    p.add_argument("--gpu", action="store_true", help="use the GPU even for small problems")
     return p
 
 
@@ -42,11 +43,17 @@ def main(argv=None):
     dt = torch.float32 if a.single else torch.float64
     T = Timer(comm)
     T.start("Reading the matrix... ")
-    if comm.size > 1:
+    if a.directory:
+        A, b = IO.read_dir_libsvm(a.inputfile, dtype=dt, device=dev, comm=comm if comm.size > 1 else None)
+        if comm.size == 1:
+            b = b[:, None]
+    elif comm.size > 1:
         A, b = IO.read_libsvm_dist(a.inputfile, comm, dtype=dt, device=dev)
     else:
         A, b = IO.read_libsvm(a.inputfile, dtype=dt, device=dev)
         b = b[:, None]
+        sdev = host_if_small(dev, A.shape[0] * A.shape[1], comm, a.gpu)
+        A, b = A.to(sdev), b.to(sdev)
     T.done()
     T.start("Solving the least squares problem... ")
     if a.highprecision:

@@ -61,13 +61,10 @@ def _read_inputs(a, comm, dev, dtype):
         if comm.size > 1:
             return IO.read_libsvm_dist(files[0], comm, sparse=a.sparse, dtype=dtype, device=dev)[0]
         return IO.read_libsvm(files[0], sparse=a.sparse, dtype=dtype, device=dev)[0]
-    # directory: the concatenation of all files (each rank keeps its [VC,*] rows)
-    mats = [IO.read_libsvm(f, dtype=dtype)[0] for f in files]
-    d = max(m.shape[1] for m in mats)
-    cat = torch.cat([torch.nn.functional.pad(m, (0, d - m.shape[1])) for m in mats], 0)
+    # directory: the concatenation of all files (ReadDirLIBSVM; [VC,*] rows with several ranks)
     if comm.size > 1:
-        return DistMatrix.from_global(cat.to(dev), "VC_STAR", comm)
-    return cat.to_sparse_csr().to(dev) if a.sparse else cat.to(dev)
+        return IO.read_dir_libsvm(a.inputfile, sparse=a.sparse, dtype=dtype, device=dev, comm=comm)[0]
+    return IO.read_dir_libsvm(a.inputfile, sparse=a.sparse, dtype=dtype, device=dev)[0]
 
 
 def main(argv=None):

@@ -15,7 +15,8 @@ import numpy as np
 import torch
 
 from ..base.exceptions import IOError_
-from .libsvm import ReadLIBSVM, WriteLIBSVM, read_libsvm, read_libsvm_dist, write_libsvm  # noqa: F401
+from .libsvm import (ReadDirLIBSVM, ReadLIBSVM, WriteLIBSVM, read_dir_libsvm, read_libsvm,  # noqa: F401
+                     read_libsvm_dist, write_libsvm)
 
 LIBSVM_DENSE, LIBSVM_SPARSE, HDF5_DENSE, HDF5_SPARSE = range(4)
 

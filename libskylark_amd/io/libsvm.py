@@ -97,6 +97,70 @@ def read_libsvm(fname: str, min_d: int = 0, max_n: int = -1, sparse: bool = Fals
     return _to_tensor(labels, rowptr, cols, vals, max(maxidx, min_d), sparse, dtype, device)
 
 
+def read_dir_libsvm(dirname: str, min_d: int = 0, max_n: int = -1, sparse: bool = False, dtype=torch.float64,
+                    device=None, comm: Comm | None = None):
+    """Read every file of a directory (sorted by name) as one LIBSVM dataset
+    (reference ``ReadDirLIBSVM``, ``utility/io/libsvm_io.hpp:926-1483``): the
+    rows are concatenated in file order and ``d`` is the largest index over
+    all files.  With ``comm`` (several ranks) the files are split over the
+    ranks in contiguous runs and the result is a ``[VC,*]`` DistMatrix pair."""
+    import os
+    files = sorted(os.path.join(dirname, f) for f in os.listdir(dirname)
+                   if os.path.isfile(os.path.join(dirname, f)) and not f.startswith("."))
+    if not files:
+        raise FileNotFoundError(f"no files in {dirname}")
+    dist = comm is not None and comm.size > 1
+    mine = files
+    if dist:
+        from ..parallel.comm import balanced_offsets
+        off = balanced_offsets(len(files), comm.size)
+        mine = files[off[comm.rank]:off[comm.rank + 1]]
+    parts, labels, d = [], [], min_d
+    for f in mine:
+        m = _Mapped(f)
+        try:
+            lab, rowptr, cols, vals, maxidx = _parse(m.addr, 0, m.size, -1)
+        finally:
+            m.close()
+        parts.append((lab, rowptr, cols, vals))
+        d = max(d, maxidx)
+    if dist:
+        dt = torch.tensor([d], dtype=torch.int64, device=comm.collective_device())
+        comm.all_reduce_max(dt)
+        d = int(dt.item())
+    Xs, Ys = [], []
+    for lab, rowptr, cols, vals in parts:
+        X, Y = _to_tensor(lab, rowptr, cols, vals, d, True, dtype, None)
+        Xs.append(X)
+        Ys.append(Y)
+    if Xs:
+        X = torch.cat([x.to_sparse_coo() for x in Xs], 0).coalesce().to_sparse_csr()
+        Y = torch.cat(Ys)
+    else:
+        X = torch.sparse_csr_tensor(torch.zeros(1, dtype=torch.int64), torch.zeros(0, dtype=torch.int64),
+                                    torch.zeros(0, dtype=dtype), (0, d))
+        Y = torch.zeros(0, dtype=torch.float64)
+    if max_n >= 0 and not dist:
+        X, Y = X.to_dense()[:max_n].to_sparse_csr(), Y[:max_n]
+    if not sparse:
+        X = X.to_dense()
+    X, Y = X.to(device) if device is not None else X, Y.to(device) if device is not None else Y
+    if not dist:
+        return X, Y
+    from ..parallel.comm import balanced_counts
+    cnt = torch.tensor([X.shape[0]], dtype=torch.int64, device=comm.collective_device())
+    have = [int(c) for c in comm.all_gather(cnt, 0).tolist()]
+    n = sum(have)
+    # the file split need not match the balanced row blocks: rebalance
+    Xl, Yl = _rebalance(comm, X.to_dense() if X.layout != torch.strided else X, Y, have, balanced_counts(n, comm.size))
+    if sparse:
+        Xl = Xl.to_sparse_csr()
+    return (DistMatrix(Xl, (n, d), "VC_STAR", comm), DistMatrix(Yl[:, None].contiguous(), (n, 1), "VC_STAR", comm))
+
+
+ReadDirLIBSVM = read_dir_libsvm
+
+
 def read_libsvm_dist(fname: str, comm: Comm | None = None, min_d: int = 0, sparse: bool = False,
                      dtype=torch.float64, device=None):
     """Distributed read: returns ``(X, Y)`` as [VC,*] DistMatrices (rows balanced)."""

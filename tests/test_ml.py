@@ -321,3 +321,30 @@ def test_approximate_ase():
     a = col[[idx.index(i) for i in range(8)]]
     b = col[[idx.index(i) for i in range(10, 18)]]
     assert (a.sign() == a[0].sign()).all() and (b.sign() == b[0].sign()).all() and a[0].sign() != b[0].sign()
+
+
+def test_read_dir_libsvm(tmp_path):
+    import libskylark_amd as sk
+    (tmp_path / "a").write_text("1 1:1.0 2:2.0\n2 3:3.0\n")
+    (tmp_path / "b").write_text("3 5:5.0\n")
+    X, Y = sk.io.read_dir_libsvm(str(tmp_path))
+    assert X.shape == (3, 5) and Y.tolist() == [1.0, 2.0, 3.0]
+    assert float(X[2, 4]) == 5.0 and float(X[1, 2]) == 3.0
+    Xs, _ = sk.io.ReadDirLIBSVM(str(tmp_path), sparse=True, min_d=7)
+    assert Xs.layout == torch.sparse_csr and Xs.shape == (3, 7)
+
+
+def _dir_worker(rank, world, d):
+    import libskylark_amd as sk
+    from libskylark_amd.parallel.comm import world as W
+    X, Y = sk.io.read_dir_libsvm(d, comm=W())
+    Xg, Yg = X.to_global(), Y.to_global()
+    ref, refy = sk.io.read_dir_libsvm(d)
+    assert torch.equal(Xg, ref.to(Xg.dtype)) and torch.equal(Yg[:, 0], refy)
+
+
+def test_read_dir_libsvm_distributed(tmp_path):
+    from mp_utils import run_distributed
+    for i in range(3):
+        (tmp_path / f"f{i}").write_text("".join(f"{i + j} {j + 1}:{float(i * 10 + j)}\n" for j in range(1 + i)))
+    run_distributed(_dir_worker, 2, str(tmp_path))
