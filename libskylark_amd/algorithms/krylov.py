@@ -72,16 +72,32 @@ class MatPrecond(Precond):
 
 
 class TriInversePrecond(Precond):
-    """``P X = R^{-1} X`` for triangular R (reference tri_inverse_precond_t)."""
+    """``P X = R^{-1} X`` for triangular R (reference tri_inverse_precond_t).
 
-    def __init__(self, R: torch.Tensor, upper: bool = True):
+    With ``Rinv`` given (the explicit inverse, formed once) every application
+    is a GEMV/GEMM instead of a triangular solve: on the MI355X a 5000 x 5000
+    ``trsv`` is latency bound at ~1.9 ms per call, the GEMV streams R^{-1} in
+    ~40 us, and a Krylov loop applies the preconditioner twice per iteration."""
+
+    def __init__(self, R: torch.Tensor, upper: bool = True, Rinv: torch.Tensor | None = None):
         self.R = R
         self.upper = upper
+        self.Rinv = Rinv
+        self._cast = {}
+
+    def _inv(self, dtype):
+        if dtype not in self._cast:
+            self._cast[dtype] = self.Rinv.to(dtype)
+        return self._cast[dtype]
 
     def apply(self, X):
+        if self.Rinv is not None:
+            return self._inv(X.dtype) @ X
         return torch.linalg.solve_triangular(self.R.to(X.dtype), X, upper=self.upper)
 
     def apply_adjoint(self, X):
+        if self.Rinv is not None:
+            return self._inv(X.dtype).t() @ X
         return torch.linalg.solve_triangular(self.R.to(X.dtype).t(), X, upper=not self.upper)
 
 

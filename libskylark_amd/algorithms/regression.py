@@ -178,11 +178,61 @@ def _on_gpu(A) -> bool:
     return isinstance(loc, torch.Tensor) and loc.is_cuda and loc.dtype == torch.float32
 
 
+CHOLQR_MAX_COND = 1e7     # fp64 Gram squares the condition number: keep kappa(R)^2 eps64 << 1
+
+
+def _tri_inv_upper(R: torch.Tensor, block: int = 1024) -> torch.Tensor:
+    """R^{-1} of an upper-triangular R, one column block at a time (column
+    block j of R^{-1} only involves the leading j1 x j1 block of R; blocking
+    also bounds the BLAS trsm workspace, which failed to allocate for a single
+    5000-column right-hand side on the MI355X)."""
+    n = R.shape[0]
+    Rinv = torch.zeros_like(R)
+    for j0 in range(0, n, block):
+        j1 = min(n, j0 + block)
+        E = torch.zeros(j1, j1 - j0, dtype=R.dtype, device=R.device)
+        E[j0:j1] = torch.eye(j1 - j0, dtype=R.dtype, device=R.device)
+        Rinv[:j1, j0:j1] = torch.linalg.solve_triangular(R[:j1, :j1], E, upper=True)
+    return Rinv
+
+
+def _cholqr_r(SA: torch.Tensor):
+    """(R, R^{-1}) of the sketch SA = Q R by fp64 Cholesky of the Gram on the
+    GPU (one f64 GEMM of t x n^2 flops + an n^3/3 Cholesky + a triangular
+    inverse, all on the matrix cores), or None when the Gram is not safely
+    SPD: then the caller falls back to Householder QR.  The guard is the exact
+    1-norm condition number of R computed from R^{-1} (which the explicit
+    preconditioner needs anyway)."""
+    X = SA.to(torch.float64)
+    G = X.t() @ X
+    L, info = torch.linalg.cholesky_ex(G)
+    if int(info) != 0:
+        return None
+    R = L.t().contiguous()
+    Rinv = _tri_inv_upper(R)
+    kappa = float(torch.linalg.matrix_norm(R, 1) * torch.linalg.matrix_norm(Rinv, 1))
+    if not (kappa < CHOLQR_MAX_COND):
+        return None
+    return R, Rinv
+
+
 def _build_precond(SA: torch.Tensor, kind: str):
-    SA = SA.to(torch.float64)
     if kind == "qr":
-        _, R = torch.linalg.qr(SA, mode="r")
-        return TriInversePrecond(R, upper=True), R
+        if SA.is_cuda and SA.shape[1] >= 256:
+            rr = _cholqr_r(SA)
+            if rr is not None:
+                return TriInversePrecond(rr[0], upper=True, Rinv=rr[1]), rr[0]
+        _, R = torch.linalg.qr(SA.to(torch.float64), mode="r")
+        Rinv = None
+        if SA.is_cuda and SA.shape[1] >= 256:
+            # explicit inverse only while it stays accurate (its error grows like
+            # kappa(R) eps); ill-conditioned R keeps the backward-stable solves
+            Rinv = _tri_inv_upper(R)
+            kappa = float(torch.linalg.matrix_norm(R, 1) * torch.linalg.matrix_norm(Rinv, 1))
+            if not (kappa < CHOLQR_MAX_COND):
+                Rinv = None
+        return TriInversePrecond(R, upper=True, Rinv=Rinv), R
+    SA = SA.to(torch.float64)
     U, s, Vh = torch.linalg.svd(SA, full_matrices=False)
     tol = s.max() * max(SA.shape) * torch.finfo(torch.float64).eps
     sinv = torch.where(s > tol, 1.0 / s, torch.zeros_like(s))

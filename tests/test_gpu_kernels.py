@@ -108,3 +108,23 @@ def test_fjlt_operator_from_device_params_matches_sketch(dev, N, S):
     out = torch.empty(N, S, dtype=torch.float64, device=dev)
     F.fjlt_operator(prm, S, N, (N / S) ** 0.5, out, transpose=True)
     torch.testing.assert_close(out.cpu(), ref, atol=1e-12, rtol=1e-12)
+
+
+@pytest.mark.parametrize("cond,dt", [(1e3, torch.float32), (1e10, torch.float64)])
+def test_lsrn_gpu_preconditioner_paths(dev, cond, dt):
+    """Cholesky-QR + explicit R^-1 for well-conditioned sketches, Householder +
+    triangular solves for ill-conditioned ones: both solve the problem."""
+    import libskylark_amd as sk
+    from libskylark_amd.algorithms import AcceleratedRegressionSolver, KrylovIterParams, RegressionProblem
+    torch.manual_seed(0)
+    m, n = 20000, 300
+    U, _ = torch.linalg.qr(torch.randn(m, n, dtype=torch.float64, device=dev))
+    s = torch.logspace(0, -torch.log10(torch.tensor(cond)).item(), n, dtype=torch.float64, device=dev)
+    A = ((U * s) @ torch.linalg.qr(torch.randn(n, n, dtype=torch.float64, device=dev))[0]).to(dt)
+    x = torch.randn(n, 1, device=dev, dtype=dt)
+    b = A @ x
+    solver = AcceleratedRegressionSolver(RegressionProblem(A), sk.Context(3), method="lsrn", precond="qr",
+                                         params=KrylovIterParams(tolerance=1e-6, iter_lim=400))
+    X, code = solver.solve(b)
+    res = float((A @ X.to(A.dtype) - b).norm() / b.norm())
+    assert res < 1e-4, (res, code)
