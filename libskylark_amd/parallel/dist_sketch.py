@@ -108,12 +108,54 @@ def _partial(sk, A: DistMatrix, dim, kind):
     return out.contiguous()
 
 
+def _use_outer_panel(sk, A: DistMatrix, dim, kind) -> bool:
+    """Outer-panel vs panel-matrix for a columnwise dense sketch of an [MC,MR]
+    matrix (reference selector ``dense_transform_Elemental_mc_mr.hpp:617-656``):
+    gathering the input panel (N x m/pc per grid column) beats reducing the
+    output panel (S x m/pc) when S exceeds factor * N / 20 (equal collective
+    volumes at the default factor)."""
+    from ..sketch import params
+    from ..sketch.dense import DenseSketch
+    if kind != "linear" or dim != COLUMNWISE or not isinstance(sk, DenseSketch):
+        return False
+    if A.local.layout != torch.strided or A.grid.pr == 1:
+        return False
+    N, S = sk.getindim(), sk.getsketchdim()
+    return S * 20 > N * params.get_factor()
+
+
+def _outer_panel(sk, A: DistMatrix, out_shape):
+    """All-gather A's rows inside the grid column, then every rank realises
+    only ITS output rows of S over the full N: no reduction of the output."""
+    from .distmatrix import _cyclic_blocks
+    g = A.grid
+    N, S = sk.getindim(), sk.getsketchdim()
+    counts, order = [], []
+    for r in range(g.pr):
+        blk = _cyclic_blocks(N, A.block[0], g.pr, r)
+        counts.append(sum(e - s for s, e in blk))
+        order.extend(i for s, e in blk for i in range(s, e))
+    G = g.col_comm.all_gather_v(A.local.contiguous(), counts, 0)
+    full = torch.empty_like(G)
+    full[torch.tensor(order, device=G.device)] = G
+    R = DistMatrix(torch.empty(0), out_shape, "MC_MR", A.comm, g, (max(1, -(-S // g.pr)), A.block[1]))
+    parts = [sk.apply_local_shard(full, COLUMNWISE, 0, out_rows=(s, e)) for s, e in R.row_blocks()]
+    if parts:
+        R.local = torch.cat(parts, 0).contiguous()
+    else:
+        dt = torch.float64 if A.local.dtype == torch.float64 else torch.float32
+        R.local = torch.zeros(0, full.shape[1], dtype=dt, device=full.device)
+    return R
+
+
 def _partial_and_reduce(sk, A: DistMatrix, dim, kind, out_layout, out_shape):
     c = A.comm
     part = _partial(sk, A, dim, kind)
     finish = (lambda X, rows=None: sk.finish_features(X, dim, rows)) if kind == "feature" else None
     S = sk.getsketchdim()
 
+    if A.layout == "MC_MR" and _use_outer_panel(sk, A, dim, kind):
+        return _outer_panel(sk, A, out_shape)
     if A.layout == "MC_MR":
         g = A.grid
         # the sketched dimension is spread over grid rows (columnwise: sum over

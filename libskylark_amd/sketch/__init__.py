@@ -1,4 +1,5 @@
 """Sketching transforms (reference ``sketch/``, ``python-skylark/skylark/sketch.py``)."""
+from . import params  # noqa: F401
 from .base import (COLUMNWISE, ROWWISE, SketchTransform, deserialize_sketch, from_json, from_ptree,
                    parse_dim, sketch_class, supported_sketch_transforms)
 from .dense import CT, JLT, SJLT, SparseJLT

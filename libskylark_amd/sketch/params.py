@@ -1,0 +1,41 @@
+"""Global sketch-application knobs (reference ``sketch/sketch_params.hpp:13-34``:
+``sketch::params::blocksize`` = panel width of the lazily realised S,
+``factor`` = threshold of the ``[MC,MR]`` panel-algorithm selection).
+
+* ``blocksize``: columns of S realised per panel by the dense transforms;
+  0 (default) sizes panels by memory instead (``ops.dense_sketch.PANEL_ELEMS``
+  entries, ~128-512 MB on the MI355X's 288 GB HBM, which keeps each GEMM long).
+* ``factor``: selects the ``[MC,MR]`` columnwise dense-sketch algorithm.
+  *Outer panel* (all-gather A's sketched dimension inside each grid column,
+  every rank realises only its own output rows, no reduction) is used when
+  ``S * 20 > N * factor``; otherwise *panel matrix* (local partial product +
+  one reduction in the grid-column communicator).  At the default factor 20
+  the rule compares the two collective volumes (N vs S rows per grid column)
+  directly; a larger factor favours reductions, as in the reference.
+"""
+from __future__ import annotations
+
+_BLOCKSIZE = 0
+_FACTOR = 20
+
+
+def get_blocksize() -> int:
+    return _BLOCKSIZE
+
+
+def set_blocksize(b: int):
+    global _BLOCKSIZE
+    if b < 0:
+        raise ValueError("blocksize must be >= 0")
+    _BLOCKSIZE = int(b)
+
+
+def get_factor() -> int:
+    return _FACTOR
+
+
+def set_factor(f: int):
+    global _FACTOR
+    if f <= 0:
+        raise ValueError("factor must be positive")
+    _FACTOR = int(f)
