@@ -21,9 +21,11 @@
 //   * 128 x 128 output tile per 256-thread workgroup (2 x 2 waves, each a
 //     64 x 64 block = 4 x 4 v_mfma_f32_16x16x32_bf16 tiles), 64 KB of LDS so
 //     two workgroups share a CU and hide each other's load latency;
-//   * f32 A is split in-kernel into bf16 hi + lo while staging to LDS, and
-//     the product is the 3-term sum  Ah*Wh + Al*Wh + Ah*Wl  (f32-class
-//     accuracy at 3/16 of the bf16 MFMA cost instead of f32 MFMA's 1/16 rate);
+//   * f32 A is split once into bf16 hi + lo planes by k_split_bf16 (doing
+//     it while staging cost ~5 VALU instructions per MFMA and made the kernel
+//     VALU bound: A is re-read by every feature tile), and the product is the
+//     3-term sum  Ah*Wh + Al*Wh + Ah*Wl  (f32-class accuracy at 3/16 of the
+//     bf16 MFMA cost instead of f32 MFMA's 1/16 rate);
 //   * K slices of 32 are double-buffered in LDS (64-B rows: ds_read_b128 of
 //     a 16-row x 32-k fragment touches 1 KB contiguous, conflict free) and
 //     the global loads run two slices ahead in two register sets;
@@ -77,32 +79,31 @@ __device__ __forceinline__ float epilogue(float x, float sc, float sh, float out
   }
 }
 
-template <bool AF32, bool WLO, int EPI, bool OUT_T, typename OutT>
+template <bool ALO, bool WLO, int EPI, bool OUT_T, typename OutT>
 __global__ void __launch_bounds__(NT, 2)
-k_feat_gemm(const void* __restrict__ Av, int64_t M, int64_t K, int64_t lda,
+k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int64_t M, int64_t K, int64_t lda,
             const bf16_t* __restrict__ Whi, const bf16_t* __restrict__ Wlo, int64_t Nf, int64_t ldw,
             const float* __restrict__ scales, const float* __restrict__ shifts, float outscale,
             OutT* __restrict__ out, int64_t ldo, int ntm, int ntn, int per) {
   __shared__ __attribute__((aligned(16))) bf16_t sAh[2][BM * BK];
-  __shared__ __attribute__((aligned(16))) bf16_t sAl[2][AF32 ? BM * BK : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t sAl[2][ALO ? BM * BK : 8];
   __shared__ __attribute__((aligned(16))) bf16_t sWh[2][BN * BK];
   __shared__ __attribute__((aligned(16))) bf16_t sWl[2][WLO ? BN * BK : 8];
 
   // XCD-aware tile order (block b runs on XCD b % 8).  When the feature tiles
-  // split evenly over the 8 XCDs, XCD x owns feature tiles
-  // [x * ntn/8, (x+1) * ntn/8) for every row block, so its slice of W stays
-  // resident in its own L2 and only A streams (once per XCD, via the MALL).
-  // The XCD's feature tiles are strided (x, x+8, ...): a contiguous slice per
-  // XCD made row-major output 5x slower (measured), strided spreads the writes.
-  // Otherwise XCD x takes a contiguous run of tiles with the feature tile
-  // fastest, so the workgroups sharing an A row block share that L2.
+  // split evenly over the 8 XCDs, XCD x owns ntn/8 of them for every row block,
+  // so its slice of W stays resident in its own L2 and only A streams (once
+  // per XCD, via the MALL).  The XCD's feature tiles are strided (x, x+8, ...)
+  // so its output columns spread over the row.  Otherwise XCD x takes a
+  // contiguous run of tiles with the feature tile fastest, so the workgroups
+  // sharing an A row block share that L2.
   const int b = blockIdx.x, xcd = b & 7, li = b >> 3;
   int tm, tn;
   if ((ntn & 7) == 0) {
     const int nx = ntn >> 3;
     if (li >= ntm * nx) return;
     tm = li / nx;
-    tn = xcd + 8 * (li - tm * nx);     // strided: an XCD's output columns spread over the row
+    tn = xcd + 8 * (li - tm * nx);
   } else {
     const int tile = xcd * per + li;
     if (tile >= ntm * ntn) return;
@@ -116,81 +117,60 @@ k_feat_gemm(const void* __restrict__ Av, int64_t M, int64_t K, int64_t lda,
   const int wr = wave >> 1, wc = wave & 1;          // 2 x 2 waves, 64 x 64 each
   const int nk = (int)((K + BK - 1) / BK);
 
-  // ---- global -> register staging (two register sets: k-steps of each parity)
-  // A f32: 128 rows x 32 k = 1024 float4 chunks, 4 per thread (row = c>>3, k = (c&7)*4)
-  // A bf16: 512 chunks of 8 bf16, 2 per thread (row = c>>2, k = (c&3)*8)
-  // W: 128 rows x 32 k bf16 = 512 chunks per plane, 2 per thread
-  constexpr int ACH = AF32 ? 4 : 2;
-  struct Regs { uint4 a[ACH]; uint4 wh[2]; uint4 wl[2]; };
-  Regs R0, R1;
-
-  auto load_global = [&](Regs& R, int kt) {
-    const int64_t k0 = (int64_t)kt * BK;
+  // ---- global -> register staging, two register sets (k-steps of each parity).
+  // Every operand tile is 128 rows x 32 k bf16 = 512 chunks of 16 B, two per
+  // thread (row = c >> 2, k = (c & 3) * 8).  The planes are zero padded to a
+  // multiple of 32 columns by the host and rows past M are clamped (their
+  // results are never stored), so the loop has no bounds checks and each
+  // chunk is one 16-B load from a pointer fixed for the whole K loop.
+  const bf16_t* pa[2];
+  const bf16_t* pw[2];
+  int soff[2];
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int c = tid + NT * i;
-      int r, kk;
-      if (AF32) { r = c >> 3; kk = (c & 7) * 4; } else { r = c >> 2; kk = (c & 3) * 8; }
-      const int64_t gr = row0 + r, gk = k0 + kk;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (gr < M) {
-        constexpr int W = AF32 ? 4 : 8;
-        if (gk + W <= K) {
-          if (AF32) v = *(const uint4*)((const float*)Av + gr * lda + gk);
-          else v = *(const uint4*)((const bf16_t*)Av + gr * lda + gk);
-        } else if (gk < K) {
-          if (AF32) {
-            const float* p = (const float*)Av + gr * lda;
-            float t[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) t[e] = (gk + e < K) ? p[gk + e] : 0.f;
-            v = make_uint4(__float_as_uint(t[0]), __float_as_uint(t[1]), __float_as_uint(t[2]), __float_as_uint(t[3]));
-          } else {
-            const bf16_t* p = (const bf16_t*)Av + gr * lda;
-            uint32_t t[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) t[e] = (gk + e < K) ? p[gk + e] : 0u;
-            v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
-          }
-        }
-      }
-      R.a[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + NT * i;
-      const int r = c >> 2, kk = (c & 3) * 8;
-      const int64_t off = (col0 + r) * ldw + k0 + kk;
-      R.wh[i] = *(const uint4*)(Whi + off);
-      if (WLO) R.wl[i] = *(const uint4*)(Wlo + off);
-    }
-  };
-
-  auto store_lds = [&](const Regs& R, int s) {
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const int c = tid + NT * i;
-      if (AF32) {
-        const int r = c >> 3, kk = (c & 7) * 4;
-        uint2 hi, lo;
-        float4 f = make_float4(__uint_as_float(R.a[i].x), __uint_as_float(R.a[i].y),
-                               __uint_as_float(R.a[i].z), __uint_as_float(R.a[i].w));
-        split4(f, hi, lo);
-        *(uint2*)&sAh[s][r * BK + kk] = hi;
-        *(uint2*)&sAl[s][r * BK + kk] = lo;
-      } else {
-        const int r = c >> 2, kk = (c & 3) * 8;
-        *(uint4*)&sAh[s][r * BK + kk] = R.a[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + NT * i;
-      const int r = c >> 2, kk = (c & 3) * 8;
-      *(uint4*)&sWh[s][r * BK + kk] = R.wh[i];
-      if (WLO) *(uint4*)&sWl[s][r * BK + kk] = R.wl[i];
-    }
-  };
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + NT * i;
+    const int r = c >> 2, kk = (c & 3) * 8;
+    int64_t gr = row0 + r;
+    gr = gr < M ? gr : M - 1;
+    pa[i] = Ahi + gr * lda + kk;
+    pw[i] = Whi + (col0 + r) * ldw + kk;
+    soff[i] = r * BK + kk;
+  }
+  const int64_t alo_off = ALO ? (Alo - Ahi) : 0;     // planes addressed from the hi pointers
+  const int64_t wlo_off = WLO ? (Wlo - Whi) : 0;
+  // register staging sets as plain local arrays driven by macros: passing a
+  // struct of arrays by reference into lambdas made hipcc keep them in
+  // scratch memory (every prefetch went through scratch_store / load)
+  // (named scalars, not arrays: hipcc's alloca promotion gave up on the
+  // 2 x 8 x uint4 staging arrays and kept them in scratch)
+  uint4 r0ah0, r0ah1, r0al0, r0al1, r0wh0, r0wh1, r0wl0, r0wl1;
+  uint4 r1ah0, r1ah1, r1al0, r1al1, r1wh0, r1wh1, r1wl0, r1wl1;
+  const bf16_t* const pa0 = pa[0];
+  const bf16_t* const pa1 = pa[1];
+  const bf16_t* const pw0 = pw[0];
+  const bf16_t* const pw1 = pw[1];
+  const int so0 = soff[0], so1 = soff[1];
+#define SL_FG_LOAD(P, KT)                                                     \
+  {                                                                           \
+    const int k0_ = (KT) * BK;                                                \
+    P##ah0 = *(const uint4*)(pa0 + k0_);                                      \
+    P##ah1 = *(const uint4*)(pa1 + k0_);                                      \
+    if (ALO) { P##al0 = *(const uint4*)(pa0 + alo_off + k0_);                 \
+               P##al1 = *(const uint4*)(pa1 + alo_off + k0_); }               \
+    P##wh0 = *(const uint4*)(pw0 + k0_);                                      \
+    P##wh1 = *(const uint4*)(pw1 + k0_);                                      \
+    if (WLO) { P##wl0 = *(const uint4*)(pw0 + wlo_off + k0_);                 \
+               P##wl1 = *(const uint4*)(pw1 + wlo_off + k0_); }               \
+  }
+#define SL_FG_STORE(P, S)                                                     \
+  {                                                                           \
+    *(uint4*)&sAh[S][so0] = P##ah0;                                           \
+    *(uint4*)&sAh[S][so1] = P##ah1;                                           \
+    if (ALO) { *(uint4*)&sAl[S][so0] = P##al0; *(uint4*)&sAl[S][so1] = P##al1; } \
+    *(uint4*)&sWh[S][so0] = P##wh0;                                           \
+    *(uint4*)&sWh[S][so1] = P##wh1;                                           \
+    if (WLO) { *(uint4*)&sWl[S][so0] = P##wl0; *(uint4*)&sWl[S][so1] = P##wl1; } \
+  }
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -199,62 +179,59 @@ k_feat_gemm(const void* __restrict__ Av, int64_t M, int64_t K, int64_t lda,
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frag_off = (lane & 15) * BK + (lane >> 4) * 8;
-  auto compute = [&](int s) {
-    bf16x8 ah[4], al[4], wh[4], wl[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int o = (wc * 64 + cb * 16) * BK + frag_off;
-      wh[cb] = *(const bf16x8*)&sWh[s][o];
-      if (WLO) wl[cb] = *(const bf16x8*)&sWl[s][o];
-    }
-#pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-      const int o = (wr * 64 + rb * 16) * BK + frag_off;
-      ah[rb] = *(const bf16x8*)&sAh[s][o];
-      if (AF32) al[rb] = *(const bf16x8*)&sAl[s][o];
-    }
-    // term-major order: 16 independent MFMAs between dependent ones
-#pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rb], wh[cb], acc[rb][cb], 0, 0, 0);
-    if (AF32) {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rb], wh[cb], acc[rb][cb], 0, 0, 0);
-    }
-    if (WLO) {
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rb], wl[cb], acc[rb][cb], 0, 0, 0);
-    }
-  };
+  // (a macro, not a lambda: a lambda capturing acc by reference demotes it to scratch)
+#define SL_FG_COMPUTE(S)                                                                      \
+  {                                                                                           \
+    bf16x8 ah[4], al[4], wh[4], wl[4];                                                        \
+    _Pragma("unroll") for (int cb = 0; cb < 4; ++cb) {                                       \
+      const int o = (wc * 64 + cb * 16) * BK + frag_off;                                      \
+      wh[cb] = *(const bf16x8*)&sWh[S][o];                                                    \
+      if (WLO) wl[cb] = *(const bf16x8*)&sWl[S][o];                                           \
+    }                                                                                         \
+    _Pragma("unroll") for (int rb = 0; rb < 4; ++rb) {                                       \
+      const int o = (wr * 64 + rb * 16) * BK + frag_off;                                      \
+      ah[rb] = *(const bf16x8*)&sAh[S][o];                                                    \
+      if (ALO) al[rb] = *(const bf16x8*)&sAl[S][o];                                           \
+    }                                                                                         \
+    /* term-major order: 16 independent MFMAs between dependent ones */                      \
+    _Pragma("unroll") for (int rb = 0; rb < 4; ++rb)                                         \
+      _Pragma("unroll") for (int cb = 0; cb < 4; ++cb)                                       \
+        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rb], wh[cb], acc[rb][cb], 0, 0, 0); \
+    if (ALO) {                                                                                \
+      _Pragma("unroll") for (int rb = 0; rb < 4; ++rb)                                       \
+        _Pragma("unroll") for (int cb = 0; cb < 4; ++cb)                                     \
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rb], wh[cb], acc[rb][cb], 0, 0, 0); \
+    }                                                                                         \
+    if (WLO) {                                                                                \
+      _Pragma("unroll") for (int rb = 0; rb < 4; ++rb)                                       \
+        _Pragma("unroll") for (int cb = 0; cb < 4; ++cb)                                     \
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rb], wl[cb], acc[rb][cb], 0, 0, 0); \
+    }                                                                                         \
+  }
 
-  // prologue: step 0 staged in LDS, step 1 in flight in R1
-  load_global(R0, 0);
-  if (nk > 1) load_global(R1, 1);
-  store_lds(R0, 0);
+  // prologue: step 0 staged in LDS, step 1 in flight in set r1
+  SL_FG_LOAD(r0, 0)
+  if (nk > 1) SL_FG_LOAD(r1, 1)
+  SL_FG_STORE(r0, 0)
   __syncthreads();
 
   // steady state, unrolled by two so the register set of each parity is static:
   //   issue loads of kt+2, compute kt, land kt+1 in LDS, barrier
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-    if (kt + 2 < nk) load_global(R0, kt + 2);
-    compute(0);
-    store_lds(R1, 1);
+    if (kt + 2 < nk) SL_FG_LOAD(r0, kt + 2)
+    SL_FG_COMPUTE(0)
+    SL_FG_STORE(r1, 1)
     __syncthreads();
-    if (kt + 3 < nk) load_global(R1, kt + 3);
-    compute(1);
-    if (kt + 2 < nk) store_lds(R0, 0);
+    if (kt + 3 < nk) SL_FG_LOAD(r1, kt + 3)
+    SL_FG_COMPUTE(1)
+    if (kt + 2 < nk) SL_FG_STORE(r0, 0)
     __syncthreads();
   }
-  if (kt < nk) compute(0);
+  if (kt < nk) SL_FG_COMPUTE(0)
+#undef SL_FG_COMPUTE
+#undef SL_FG_LOAD
+#undef SL_FG_STORE
 
   // ---- epilogue: C[row][col], col = lane & 15, row = 4 * (lane >> 4) + reg
 #pragma unroll
@@ -288,15 +265,15 @@ k_feat_gemm(const void* __restrict__ Av, int64_t M, int64_t K, int64_t lda,
   }
 }
 
-template <bool AF32, bool WLO, int EPI>
-int launch_out(const void* A, int64_t M, int64_t K, int64_t lda, const bf16_t* Whi, const bf16_t* Wlo,
-               int64_t Nf, int64_t ldw, const float* sc, const float* sh, float outscale, void* out,
-               int out_dtype, int64_t ldo, int out_t, hipStream_t s) {
+template <bool ALO, bool WLO, int EPI>
+int launch_out(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda, const bf16_t* Whi,
+               const bf16_t* Wlo, int64_t Nf, int64_t ldw, const float* sc, const float* sh, float outscale,
+               void* out, int out_dtype, int64_t ldo, int out_t, hipStream_t s) {
   const int ntm = (int)((M + BM - 1) / BM), ntn = (int)((Nf + BN - 1) / BN);
   const int T = ntm * ntn, per = (T + 7) / 8;
   const unsigned grid = (unsigned)(8 * per);
 #define SL_FG_L(OT, TRANS) \
-  k_feat_gemm<AF32, WLO, EPI, TRANS, OT><<<grid, NT, 0, s>>>(A, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale, (OT*)out, ldo, ntm, ntn, per)
+  k_feat_gemm<ALO, WLO, EPI, TRANS, OT><<<grid, NT, 0, s>>>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale, (OT*)out, ldo, ntm, ntn, per)
   if (out_dtype == SL_F32) { if (out_t) SL_FG_L(float, true); else SL_FG_L(float, false); }
   else if (out_dtype == SL_BF16) { if (out_t) SL_FG_L(bf16_t, true); else SL_FG_L(bf16_t, false); }
   else return SL_ERR_UNSUPPORTED;
@@ -305,35 +282,76 @@ int launch_out(const void* A, int64_t M, int64_t K, int64_t lda, const bf16_t* W
   return SL_OK;
 }
 
+// f32 rows -> bf16 hi + lo planes (hi = rne(x), lo = rne(x - hi)), zero padded
+// to ldp columns: one streaming pass, so the GEMM's K loop carries no
+// conversion VALU work (A is re-read once per feature tile).
+__global__ void __launch_bounds__(256)
+k_split_bf16(const float* __restrict__ A, int64_t M, int64_t K, int64_t lda, bf16_t* __restrict__ hi,
+             bf16_t* __restrict__ lo, int64_t ldp) {
+  const int64_t per_row = ldp / 4;
+  const int64_t total = M * per_row;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / per_row, k = (t - r * per_row) * 4;
+    float x[4];
+    if (k + 4 <= K && (lda & 3) == 0) {
+      const float4 v = *(const float4*)(A + r * lda + k);
+      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = (k + e < K) ? A[r * lda + k + e] : 0.f;
+    }
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      h[e] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x[e]);
+      const float res = x[e] - __uint_as_float(h[e] << 16);
+      l[e] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)res);
+    }
+    *(uint2*)(hi + r * ldp + k) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    *(uint2*)(lo + r * ldp + k) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+  }
+}
+
 }  // namespace
 
-// Host contract (checked here; the Python wrapper pads W):
-//   * A: M x K row-major, row stride lda elements, 16-B aligned rows
-//     (lda % 4 == 0 for f32, % 8 == 0 for bf16);
+// Host contract (checked here; the Python wrapper pads the planes):
+//   * A: M x K as bf16 planes Ahi (+ optional Alo), row stride lda elements,
+//     lda % 32 == 0, zero in columns [K, lda) (sl_split_bf16 produces them);
 //   * Whi / Wlo: ceil(Nf/128)*128 rows x ldw bf16, ldw % 32 == 0, ldw >= K,
-//     zero in the padding (Wlo may be null: 2-term / 1-term products);
+//     zero in the padding (Wlo may be null);
 //   * out: f32 or bf16, Z[r*ldo + f] (out_t = 0) or Z[f*ldo + r] (out_t = 1).
-SL_API int sl_feature_gemm(const void* A, int a_dtype, int64_t M, int64_t K, int64_t lda,
+SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda,
                            const bf16_t* Whi, const bf16_t* Wlo, int64_t Nf, int64_t ldw,
                            const float* scales, const float* shifts, float outscale, int epi,
                            void* out, int out_dtype, int64_t ldo, int out_t, void* stream) {
   if (M <= 0 || Nf <= 0) return SL_OK;
-  if (K <= 0 || ldw % BK != 0 || ldw < K) return SL_ERR_DIMENSION;
-  const int align = a_dtype == SL_F32 ? 4 : 8;
-  if (lda % align != 0 || ((uintptr_t)A & 15) != 0 || ((uintptr_t)Whi & 15) != 0) return SL_ERR_INVALID;
+  if (K <= 0 || ldw % BK != 0 || ldw < K || lda % BK != 0 || lda < K) return SL_ERR_DIMENSION;
+  if (((uintptr_t)Ahi & 15) || ((uintptr_t)Whi & 15) || (Alo && ((uintptr_t)Alo & 15)) ||
+      (Wlo && ((uintptr_t)Wlo & 15)))
+    return SL_ERR_INVALID;
   if ((M + BM - 1) / BM * ((Nf + BN - 1) / BN) > (int64_t)0x7fffffff) return SL_ERR_DIMENSION;
   if (epi == EPI_COS && shifts == nullptr) return SL_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
-  const bool wlo = Wlo != nullptr;
-#define SL_FG_E(AF, WL)                                                                              \
+  const bool alo = Alo != nullptr, wlo = Wlo != nullptr;
+#define SL_FG_E(AL, WL)                                                                              \
   switch (epi) {                                                                                     \
-    case EPI_NONE: return launch_out<AF, WL, EPI_NONE>(A, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
-    case EPI_COS: return launch_out<AF, WL, EPI_COS>(A, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
-    case EPI_EXPNEG: return launch_out<AF, WL, EPI_EXPNEG>(A, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
+    case EPI_NONE: return launch_out<AL, WL, EPI_NONE>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
+    case EPI_COS: return launch_out<AL, WL, EPI_COS>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
+    case EPI_EXPNEG: return launch_out<AL, WL, EPI_EXPNEG>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
     default: return SL_ERR_INVALID;                                                                  \
   }
-  if (a_dtype == SL_F32) { if (wlo) { SL_FG_E(true, true) } else { SL_FG_E(true, false) } }
-  else if (a_dtype == SL_BF16) { if (wlo) { SL_FG_E(false, true) } else { SL_FG_E(false, false) } }
+  if (alo) { if (wlo) { SL_FG_E(true, true) } else { SL_FG_E(true, false) } }
+  else { if (wlo) { SL_FG_E(false, true) } else { SL_FG_E(false, false) } }
 #undef SL_FG_E
   return SL_ERR_UNSUPPORTED;
+}
+
+SL_API int sl_split_bf16(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t ldp,
+                         void* stream) {
+  if (M <= 0) return SL_OK;
+  if (ldp % 4 != 0 || ldp < K || ((uintptr_t)hi & 7) || ((uintptr_t)lo & 7)) return SL_ERR_INVALID;
+  const unsigned grid = sl_grid_for((size_t)(M * (ldp / 4)), 256, 8192);
+  k_split_bf16<<<grid, 256, 0, (hipStream_t)stream>>>(A, M, K, lda, hi, lo, ldp);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
 }

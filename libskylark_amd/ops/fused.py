@@ -1,9 +1,10 @@
 """Fused dense-sketch / random-feature GEMM (``_native/src/feature_gemm.hip``).
 
 ``Z = outscale * epi(scale_f * (A W^T)[r, f] + shift_f)`` in one launch on
-bf16 MFMA: f32 inputs are split into bf16 hi + lo in-kernel and the realised
-sketching matrix W is held as a bf16 hi + lo pair, so the 3-term product is
-f32-class accurate (|err| ~ 2^-16 of sum |a w|) at 3/16 of the bf16 MFMA cost.
+bf16 MFMA: f32 inputs are split once into bf16 hi + lo planes (one streaming
+pass, ``sl_split_bf16``) and the realised sketching matrix W is held as a
+bf16 hi + lo pair, so the 3-term product is f32-class accurate
+(|err| ~ 2^-16 of sum |a w|) at 3/16 of the bf16 MFMA cost.
 
 Used by the dense transforms (JLT / CT / SJLT, ``epi = none``) and the
 feature maps (RFT / QRFT ``cos``, RLT / QRLT ``exp(-x)``) whenever the
@@ -24,10 +25,12 @@ EPI_NONE, EPI_COS, EPI_EXPNEG = 0, 1, 2
 BN, BK = 128, 32
 MAX_W_ELEMS = 1 << 26          # W (S x N) realised whole up to 64 M entries (256 MB as hi+lo)
 
-_lib.register("sl_feature_gemm", [C.c_void_p, C.c_int, C.c_int64, C.c_int64, C.c_int64,
+_lib.register("sl_feature_gemm", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
                                   C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                                   C.c_void_p, C.c_void_p, C.c_float, C.c_int,
                                   C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p])
+_lib.register("sl_split_bf16", [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                C.c_void_p])
 
 
 def enabled() -> bool:
@@ -64,16 +67,27 @@ class SplitW:
         self.nf, self.k, self.ldw = nf, k, ldw
 
 
-def _align_rows(X: torch.Tensor) -> torch.Tensor:
-    """Row-major with 16-B aligned rows (what the kernel's vector loads need)."""
-    align = 4 if X.dtype == torch.float32 else 8
-    if X.stride(1) == 1 and X.stride(0) % align == 0 and X.data_ptr() % 16 == 0 and X.stride(0) >= X.shape[1]:
-        return X
+def split_planes(X: torch.Tensor):
+    """Row-major bf16 operand planes for the kernel: ``(hi, lo, ld)`` with
+    ``ld`` a multiple of 32 and zero padding.  f32 input -> hi + lo (one
+    ``sl_split_bf16`` streaming pass; x = hi + lo to ~2^-17); bf16 input ->
+    the data itself (lo = None), copied only when its rows are not padded."""
     m, k = X.shape
-    ld = -(-k // align) * align
-    buf = torch.empty(m, ld, dtype=X.dtype, device=X.device)
-    buf[:, :k] = X
-    return buf[:, :k]
+    ld = -(-k // BK) * BK
+    dev = X.device
+    if X.dtype == torch.bfloat16:
+        if X.stride(1) == 1 and X.stride(0) == ld and X.data_ptr() % 16 == 0 and ld == k:
+            return X, None, ld
+        buf = torch.zeros(m, ld, dtype=torch.bfloat16, device=dev)
+        buf[:, :k] = X
+        return buf, None, ld
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    hi = torch.empty(m, ld, dtype=torch.bfloat16, device=dev)
+    lo = torch.empty(m, ld, dtype=torch.bfloat16, device=dev)
+    _lib.call("sl_split_bf16", _lib.ptr(X), m, k, X.stride(0), _lib.ptr(hi), _lib.ptr(lo), ld,
+              C.c_void_p(_lib.stream_of(X)))
+    return hi, lo, ld
 
 
 def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=None,
@@ -85,7 +99,7 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
     m, k = X.shape
     if k != W.k:
         raise ValueError(f"feature_gemm: inner dimension {k} != {W.k}")
-    X = _align_rows(X)
+    hi, lo, ld = split_planes(X)
     dev = A.device
     if dim == 1:
         out = torch.empty(m, W.nf, dtype=out_dtype, device=dev)
@@ -95,7 +109,9 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
         ldo, out_t = m, 1
     sc = scales.to(device=dev, dtype=torch.float32).contiguous() if scales is not None else None
     sh = shifts.to(device=dev, dtype=torch.float32).contiguous() if shifts is not None else None
-    _lib.call("sl_feature_gemm", _lib.ptr(X), _lib.dtype_code(X.dtype), m, k, X.stride(0),
+    if W.ldw != ld:
+        raise ValueError("feature_gemm: W and A planes must share the padded inner dimension")
+    _lib.call("sl_feature_gemm", _lib.ptr(hi), _lib.ptr(lo) if lo is not None else None, m, k, ld,
               _lib.ptr(W.hi), _lib.ptr(W.lo) if use_lo else None, W.nf, W.ldw,
               _lib.ptr(sc) if sc is not None else None, _lib.ptr(sh) if sh is not None else None,
               float(outscale), int(epi), _lib.ptr(out), _lib.dtype_code(out_dtype), ldo, out_t,
