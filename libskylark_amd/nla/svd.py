@@ -115,6 +115,8 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     ``(U, s, V)``; U is row-distributed like A (a DistMatrix ``[VC,*]`` when A
     is distributed), s and V replicated.
     """
+    if _TRACE:
+        _T0[0] = time.perf_counter()
     from .. import default_context
     ctx = context if context is not None else default_context()
     params = params or ApproximateSVDParams()
@@ -255,6 +257,7 @@ class _DevicePlan:
         # FJLT sketches are realised inside segment 1 from device-held stream
         # coordinates {seed, base_D, base_samples} (ops.fut.fjlt_operator)
         self.prm = torch.zeros(3, dtype=torch.int64, device=dev)
+        self.prm_host = torch.zeros(3, dtype=torch.int64).pin_memory()
         self.fjlt_scale = None
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.small = torch.zeros(k * rank + rank, dtype=torch.float64, device=dev)
@@ -408,7 +411,10 @@ class _DevicePlan:
             if self.fjlt_scale is None and self.graph_built():
                 self.reset_graphs()
             self.fjlt_scale = float(fjlt[3])
-            self.prm.copy_(torch.tensor(fjlt[:3], dtype=torch.int64))
+            # pinned + non_blocking (no host wait): the previous call's copy of
+            # this buffer finished before that call's synchronising D2H
+            self.prm_host[0], self.prm_host[1], self.prm_host[2] = int(fjlt[0]), int(fjlt[1]), int(fjlt[2])
+            self.prm.copy_(self.prm_host, non_blocking=True)
         else:
             if self.fjlt_scale is not None:
                 self.fjlt_scale = None
@@ -468,6 +474,7 @@ def _host_eigh(C: torch.Tensor):
 
 _PLANS: dict = {}
 _TRACE = os.environ.get("SKH_TRACE_SVD", "0") == "1"   # host-side phase timestamps
+_T0 = [0.0]
 
 
 def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
@@ -476,6 +483,8 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
 
     Returns None when a Cholesky breakdown was flagged (the caller then reruns
     the robust host path with the same, rewound, context)."""
+    if _TRACE:
+        print(f"[svd.trace] python_prep={(time.perf_counter() - _T0[0]) * 1e6:.0f}us", file=sys.stderr)
     ctx0 = ctx.copy()
     dev = A_loc.device
     fjlt = None
