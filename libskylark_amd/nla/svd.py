@@ -366,7 +366,9 @@ class _DevicePlan:
             fn()
         torch.cuda.current_stream(self.dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread-local capture: with RCCL the process group's watchdog thread
+        # polls events concurrently, which a global-mode capture would reject
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             out = fn()
         return (g, out) if want_out else g
 
