@@ -59,6 +59,21 @@ class _Fastfood(_FeatureMap):
     def _make_Sm(self, ctx) -> torch.Tensor:
         raise NotImplementedError
 
+    # Largest input dimension realised as a dense W for the fused MFMA path.
+    DENSE_MAX_N = 4096
+
+    def realize_W(self, dtype=torch.float64, device=None) -> torch.Tensor:
+        """The Fastfood operator as an explicit S x N matrix: every block
+        ``Sm * F G Pi F B`` applied to the identity (same draws, exact same
+        linear map).  On the MI355X the fused feature GEMM with this W (one
+        MFMA launch with the cos epilogue) beats the FFT chain (two DCTs, a
+        gather and three scalings per block, each a pass over HBM) for
+        N <= DENSE_MAX_N; larger N keep the O(S log N) transform."""
+        if self._N > self.DENSE_MAX_N:
+            raise ValueError("Fastfood dense realisation is limited to N <= DENSE_MAX_N")
+        eye = torch.eye(self._N, dtype=torch.float64, device=device)
+        return self._features_pre(eye, COLUMNWISE).to(dtype)
+
     def _features_pre(self, A, dim, in_offset=0, out_rows=None):
         if in_offset != 0 or A.shape[dim] != self._N:
             raise ValueError("Fastfood needs the whole input dimension on one device")

@@ -74,7 +74,8 @@ class _FeatureMap(SketchTransform):
     def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
         k = A.shape[dim]
         i0, i1 = out_rows if out_rows is not None else (0, self._S)
-        if hasattr(self, "realize_W") and in_offset == 0 and k == self._N and _fused.fused_ok(A, dim, k, i1 - i0):
+        dense_ok = hasattr(self, "realize_W") and self._N <= getattr(self, "DENSE_MAX_N", self._N)
+        if dense_ok and in_offset == 0 and k == self._N and _fused.fused_ok(A, dim, k, i1 - i0):
             # GEMM + cos/exp epilogue in one MFMA launch (ops/fused.py)
             if getattr(self, "_wcache", None) is None:
                 self._wcache = _fused.WCache()

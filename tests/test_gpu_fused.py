@@ -85,7 +85,8 @@ def test_dense_sketch_fused_vs_explicit(dev, name, dim):
 
 @pytest.mark.parametrize("name,kw", [("GaussianRFT", {"sigma": 3.0}), ("LaplacianRFT", {"sigma": 3.0}),
                                      ("MaternRFT", {"nu": 1.5, "l": 3.0}), ("GaussianQRFT", {"sigma": 3.0}),
-                                     ("ExpSemigroupRLT", {"beta": 0.5}), ("ExpSemigroupQRLT", {"beta": 0.5})])
+                                     ("ExpSemigroupRLT", {"beta": 0.5}), ("ExpSemigroupQRLT", {"beta": 0.5}),
+                                     ("FastGaussianRFT", {"sigma": 3.0}), ("FastMaternRFT", {"nu": 1.5, "l": 3.0})])
 @pytest.mark.parametrize("dim", [0, 1])
 def test_feature_maps_fused_vs_cpu(dev, name, kw, dim):
     N, S, M = 64, 384, 1000
