@@ -71,6 +71,15 @@ class FJLT(SketchTransform):
     def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
         cdt = A.dtype if A.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.float16) else torch.float32
         if self._S <= DIRECT_MAX_S:
+            from ..ops import fused as _fused
+            k = A.shape[dim]
+            if _fused.fused_ok(A, dim, k, self._S):
+                # explicit sqrt(N/S) P F D on the fused bf16x3 MFMA GEMM
+                if getattr(self, "_wcache", None) is None:
+                    self._wcache = _fused.WCache()
+                Wf = self._wcache.get((str(A.device), in_offset, k), lambda: self.realize(
+                    torch.float64, A.device)[:, in_offset:in_offset + k].float())
+                return _fused.feature_gemm(A, Wf, dim)
             W = self._operator(A.device, cdt)
             k = A.shape[dim]
             Wl = W[:, in_offset:in_offset + k]

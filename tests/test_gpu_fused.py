@@ -109,3 +109,15 @@ def test_feature_maps_fused_vs_cpu(dev, name, kw, dim):
     err = (out - ref).abs()
     err = err.max(dim=1 - dim).values
     assert bool((err <= tol).all()), float((err - tol).max())
+
+
+@pytest.mark.parametrize("dim", [0, 1])
+def test_fjlt_direct_fused_vs_explicit(dev, dim):
+    N, S, M = 700, 120, 300
+    T = sk.sketch.FJLT(N, S, context=sk.Context(9))
+    P = T.realize(torch.float64)
+    A = torch.randn(N, M, dtype=torch.float64) if dim == 0 else torch.randn(M, N, dtype=torch.float64)
+    Ad = A.to(dev, torch.float32)
+    out = T.apply(Ad, dim=dim).double().cpu()
+    ref = P @ Ad.double().cpu() if dim == 0 else Ad.double().cpu() @ P.t()
+    assert (out - ref).abs().max().item() < 3e-5 * float(ref.abs().max())
