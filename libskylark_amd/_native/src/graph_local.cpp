@@ -58,8 +58,16 @@ struct PPR {
   }
   double* at(int64_t s) { return ry.data() + s * (N + NX); }
 
+  // Push budget: the reference loops until no residual violates its bound; a
+  // malformed operator D (or a tolerance below roundoff) would then never
+  // stop, so the native loop gives up after max_pops queue pops and reports
+  // it (converged = false) instead of spinning.
+  int64_t max_pops = 20000000;
+  bool converged = true;
+
   void run(const int64_t* seeds, const double* vals, int64_t ns) {
     std::deque<int64_t> q;
+    int64_t pops = 0;
     const int NR = N / NX;
     for (int64_t i = 0; i < ns; ++i) {
       const int64_t s = get(seeds[i]);
@@ -92,6 +100,10 @@ struct PPR {
     }
     std::vector<double> dyp(N);
     while (!q.empty()) {
+      if (++pops > max_pops) {
+        converged = false;
+        break;
+      }
       const int64_t node = q.front();
       q.pop_front();
       const int64_t s = slot[node];
@@ -169,6 +181,10 @@ SL_API int sl_td_ppr(int64_t n, const int64_t* rowptr, const int64_t* col, const
   Graph G{n, rowptr, col};
   PPR p(G, D, N, NX, alpha, C);
   p.run(seeds, seedvals, nseeds);
+  if (!p.converged) {
+    sl_set_last_error("td_ppr: push loop did not converge (check the collocation operator / tolerance)");
+    return SL_ERR_GENERIC;
+  }
   int64_t k = 0;
   for (size_t s = 0; s < p.verts.size(); ++s) {
     const double* r = p.at((int64_t)s);
@@ -190,10 +206,15 @@ SL_API int sl_local_cluster(int64_t n, const int64_t* rowptr, const int64_t* col
   std::vector<int64_t> cluster(seeds, seeds + nseeds);
   double currentcond = -1;
   bool improve;
+  int rounds = 0;   // the conductance strictly decreases, but bound the rounds anyway
   do {
     std::vector<double> sv(cluster.size(), 1.0 / (double)cluster.size());
     PPR p(G, D, N, NX, alpha, C);
     p.run(cluster.data(), sv.data(), (int64_t)cluster.size());
+    if (!p.converged) {
+      sl_set_last_error("local_cluster: push loop did not converge (check the collocation operator / tolerance)");
+      return SL_ERR_GENERIC;
+    }
     std::vector<int64_t> nz;
     for (size_t s = 0; s < p.verts.size(); ++s)
       if (p.at((int64_t)s)[N] != 0) nz.push_back((int64_t)s);
@@ -205,14 +226,14 @@ SL_API int sl_local_cluster(int64_t n, const int64_t* rowptr, const int64_t* col
         vals[i] = {-p.at(nz[i])[N + t] / (double)G.deg(v), v};
       }
       auto [best, prefix] = sweep(G, num_edges, vals);
-      if (currentcond == -1 || best < 0.999999 * currentcond) {
+      if (currentcond == -1 || (best >= 0 && best < currentcond - 1e-6 * std::fabs(currentcond))) {
         improve = true;
         cluster.clear();
         for (int64_t i = 0; i <= prefix && i < (int64_t)vals.size(); ++i) cluster.push_back(vals[i].second);
         currentcond = best;
       }
     }
-  } while (recursive && improve);
+  } while (recursive && improve && ++rounds < 1000);
   std::copy(cluster.begin(), cluster.end(), cluster_out);
   *ncluster = (int64_t)cluster.size();
   *cond = currentcond;
