@@ -38,10 +38,16 @@ def _warm_up(dev):
         a = torch.ones(8, 8, device=dev)
         (a @ a).sum().item()
         torch.linalg.qr(a.double())[0].sum().item()
-    else:
-        a = torch.ones(8, 8, dtype=torch.float64)
-        torch.linalg.qr(a)
-        torch.linalg.eigh(a)
+    # Small problems stay on the host (host_if_small) even when a GPU is
+    # present, so the host LAPACK / sparse paths are initialised as well.
+    a = torch.eye(8, dtype=torch.float64) + 0.5
+    torch.linalg.qr(a)
+    torch.linalg.eigh(a)
+    torch.linalg.svd(a)
+    torch.sparse.mm(a.to_sparse_csr(), a)
+    from ..ops.rng import fill_random
+    from ..base.distributions import Normal
+    fill_random(torch.empty(8, dtype=torch.float64), Normal(), 0, 0)
 
 
 # Below this many matrix entries a single-process solve is latency bound:
@@ -53,7 +59,11 @@ SMALL_PROBLEM = 1 << 20
 
 
 def host_if_small(dev, n_entries: int, comm, force_gpu: bool = False):
-    if dev.type == "cuda" and comm.size == 1 and not force_gpu and n_entries < SMALL_PROBLEM:
+    if comm.size == 1 and not force_gpu and n_entries < SMALL_PROBLEM:
+        # A problem this small runs in well under a millisecond on one core;
+        # waking the intra-op thread pool costs more than it saves (and its
+        # spin-up jitter was 10-25 ms in measurements of skylark_graph_se).
+        torch.set_num_threads(1)
         return torch.device("cpu")
     return dev
 

@@ -27,3 +27,14 @@ def pytest_collection_modifyitems(config, items):
 def dev():
     import torch
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _restore_threads():
+    """CLI mains run in-process here; a tiny problem sets the intra-op pool to
+    one thread for that (short-lived) tool process -- undo it per test."""
+    import torch
+    n = torch.get_num_threads()
+    yield
+    if torch.get_num_threads() != n:
+        torch.set_num_threads(n)
