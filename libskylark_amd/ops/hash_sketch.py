@@ -17,6 +17,12 @@ _lib.register("sl_hash_dense_colwise", [vp, i32, i64, i64, vp, vp, vp, i64, vp, 
 _lib.register("sl_hash_dense_rowwise", [vp, i32, i64, i64, i64, vp, vp, vp, i64, vp, i32, i64, i64, i32, vp])
 _lib.register("sl_hash_csr_colwise", [vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, i64, i64, i32, vp])
 _lib.register("sl_hash_csr_rowwise", [vp, vp, i32, vp, i32, i64, vp, vp, vp, i64, i64, i32, vp])
+_lib.register("sl_cwt_csr_rowwise_sparse", [vp, vp, i32, vp, i32, i64, i32, vp, vp, i64, i32, vp, vp, vp, vp])
+_lib.register("sl_cwt_csr_colwise_mark", [vp, vp, i32, i64, vp, i64, vp, i64, vp])
+_lib.register("sl_dense_occ_compact", [vp, i32, i64, vp, i64, i64, i32, vp, vp, vp, i32, vp])
+
+# dense staging limit of the columnwise CSR -> CSR path (S x ncols cells)
+SPARSE_OUT_DENSE_CELLS = 1 << 28
 
 
 class HashData:
@@ -166,7 +172,71 @@ def apply_csr_dense_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int 
 
 def apply_csr_sparse_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int = 0):
     """CountSketch CSR -> CSR (reference sketch/hash_transform_local_sparse.hpp:88-223):
-    duplicate (row, col) pairs produced by the hashing are merged."""
+    duplicate (row, col) pairs produced by the hashing are merged.  GPU inputs
+    run the sort-free kernels of ``hash_sparse_out.hip``; shapes they do not
+    cover (rowwise rows longer than 32 entries, a columnwise result beyond
+    ``SPARSE_OUT_DENSE_CELLS``, f64 columnwise) take the generic coalesce."""
+    if A.is_cuda:
+        out = _csr_sparse_out_native(hd, A, dim, in_offset)
+        if out is not None:
+            return out
+    return _csr_sparse_out_generic(hd, A, dim, in_offset)
+
+
+def _finish_csr(cnt, nr, nc, fill, vdt, device):
+    crow = torch.zeros(nr + 1, dtype=torch.int64, device=device)
+    torch.cumsum(cnt, 0, out=crow[1:])
+    nnz = int(crow[-1].item())
+    ocol = torch.empty(nnz, dtype=torch.int64, device=device)
+    oval = torch.empty(nnz, dtype=vdt, device=device)
+    if nnz:
+        fill(crow, ocol, oval)
+    return torch.sparse_csr_tensor(crow, ocol, oval, size=(nr, nc))
+
+
+def _csr_sparse_out_native(hd: HashData, A: torch.Tensor, dim: int, in_offset: int):
+    S = hd.S
+    idx, val, perm, bptr = hd.on(A.device)
+    nrows, ncols = A.shape
+    rp, ci, vals = _csr_parts(A)
+    idx32 = 1 if ci.dtype == torch.int32 else 0
+    if ci.dtype not in (torch.int32, torch.int64):
+        ci, idx32 = ci.to(torch.int64), 0
+    vdt = vals.dtype
+    st = vp(_lib.stream_of(A))
+    dev = A.device
+    if dim == 1:
+        maxlen = int((rp[1:] - rp[:-1]).max().item()) if nrows else 0
+        if maxlen > 32:
+            return None
+        cnt = torch.empty(nrows, dtype=torch.int64, device=dev)
+        args = (_lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals), _lib.dtype_code(vdt), nrows, maxlen,
+                _lib.ptr(idx), _lib.ptr(val), in_offset)
+        _lib.call("sl_cwt_csr_rowwise_sparse", *args, 0, _lib.ptr(cnt), None, None, st)
+        return _finish_csr(cnt, nrows, S, lambda crow, oc, ov: _lib.call(
+            "sl_cwt_csr_rowwise_sparse", *args, 1, _lib.ptr(crow), _lib.ptr(oc), _lib.ptr(ov), st), vdt, dev)
+    if vdt != torch.float32 or S * ncols > SPARSE_OUT_DENSE_CELLS:
+        return None
+    if in_offset != 0 or nrows != idx.numel():
+        perm, bptr = _restrict(idx, in_offset, nrows, S)
+    dense = torch.zeros(S, ncols, dtype=torch.float32, device=dev)
+    avg = vals.numel() / max(1, nrows)
+    _lib.call("sl_hash_csr_colwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals), _lib.dtype_code(vdt),
+              _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(val), S, ncols, _lib.ptr(dense), dense.stride(0),
+              in_offset, _group_for(avg), st)
+    occ = torch.zeros(S, ncols, dtype=torch.uint8, device=dev)
+    _lib.call("sl_cwt_csr_colwise_mark", _lib.ptr(rp), _lib.ptr(ci), idx32, nrows, _lib.ptr(idx), in_offset,
+              _lib.ptr(occ), ncols, st)
+    cnt = torch.empty(S, dtype=torch.int64, device=dev)
+    f32 = _lib.dtype_code(torch.float32)
+    _lib.call("sl_dense_occ_compact", _lib.ptr(dense), f32, dense.stride(0), _lib.ptr(occ), S, ncols, 0,
+              _lib.ptr(cnt), None, None, f32, st)
+    return _finish_csr(cnt, S, ncols, lambda crow, oc, ov: _lib.call(
+        "sl_dense_occ_compact", _lib.ptr(dense), f32, dense.stride(0), _lib.ptr(occ), S, ncols, 1,
+        _lib.ptr(crow), _lib.ptr(oc), _lib.ptr(ov), f32, st), vdt, dev)
+
+
+def _csr_sparse_out_generic(hd: HashData, A: torch.Tensor, dim: int, in_offset: int = 0):
     S = hd.S
     idx, val, _, _ = hd.on(A.device)
     coo = A.to_sparse_coo().coalesce()

@@ -46,6 +46,32 @@ def test_cwt_csr_gpu_vs_explicit(dev, dim, vdt):
 
 
 @pytest.mark.parametrize("dim", [0, 1])
+@pytest.mark.parametrize("vdt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("density", [0.002, 0.005, 0.05])
+def test_cwt_csr_sparse_out_native(dev, dim, vdt, density):
+    """hash_sparse_out.hip (sort-free CSR -> CSR) vs the generic coalesce
+    route: same sparsity pattern and values; rowwise row lengths ~8 / ~20 / ~200
+    exercise the 8/16/32 sorting networks and the generic fallback beyond 32."""
+    from libskylark_amd.ops import hash_sketch as H
+    N, S, M = 4000, 64, 700
+    T = sk.sketch.CWT(N, S, context=sk.Context(5))
+    A = torch.randn(N, M, dtype=torch.float64)
+    A[torch.rand(N, M) > density] = 0
+    if dim == 1:
+        A = A.t().contiguous()
+    As = A.to(vdt).to_sparse_csr().to(dev)
+    As = torch.sparse_csr_tensor(As.crow_indices(), As.col_indices(), As.values(), As.shape)
+    out = T.apply(As, dim=dim, sparse_output=True)
+    ref = H._csr_sparse_out_generic(T._hd, As, dim)
+    assert out.layout == torch.sparse_csr and out.shape == ref.shape
+    assert torch.equal(out.crow_indices().cpu(), ref.crow_indices().cpu().to(torch.int64))
+    assert torch.equal(out.col_indices().cpu(), ref.col_indices().cpu().to(torch.int64))
+    tol = 1e-12 if vdt == torch.float64 else 1e-4
+    torch.testing.assert_close(out.values().cpu(), ref.values().cpu(), rtol=tol, atol=tol)
+    assert out.values().dtype == vdt
+
+
+@pytest.mark.parametrize("dim", [0, 1])
 def test_jlt_gpu_vs_cpu(dev, dim):
     N, S, M = 2048, 128, 96
     T = sk.sketch.JLT(N, S, context=sk.Context(11))
