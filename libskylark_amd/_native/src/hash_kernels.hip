@@ -16,7 +16,8 @@
 //   * dense rowwise: the input row is staged in LDS by coalesced loads, each
 //     thread produces whole output buckets by gathering from LDS;
 //   * CSR columnwise: one workgroup per (bucket, column chunk), the chunk
-//     accumulated in LDS with ds_add_f32, then one coalesced store.
+//     accumulated in LDS with ds_add_f32 / ds_add_f64 (value dtype), then one
+//     coalesced store.
 #include "sl_common.hpp"
 
 template <typename T, typename OT, int VEC>
@@ -159,25 +160,26 @@ __global__ void __launch_bounds__(512)
 k_hash_csr_col(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
                const VT* __restrict__ vals, const int64_t* __restrict__ perm,
                const int64_t* __restrict__ bptr, const double* __restrict__ hval,
-               float* __restrict__ out, int64_t ldo, int64_t m, int64_t CW,
+               VT* __restrict__ out, int64_t ldo, int64_t m, int64_t CW,
                int64_t row_offset) {
+  // accumulation in the value type (f64 values: ds_add_f64, exact fp64 sums)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* acc = (float*)smem;
+  VT* acc = (VT*)smem;
   const int64_t b = blockIdx.y;
   const int64_t c0 = (int64_t)blockIdx.x * CW;
   const int64_t cw = (c0 + CW <= m) ? CW : (m - c0);
-  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) acc[c] = 0.f;
+  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) acc[c] = (VT)0;
   __syncthreads();
   const int groups = blockDim.x / G;
   const int gid = threadIdx.x / G, gl = threadIdx.x % G;
   const bool chunked = cw != m;
   for (int64_t p = bptr[b] + gid; p < bptr[b + 1]; p += groups) {
     const int64_t r = perm[p];
-    const float w = (float)hval[r];
+    const VT w = (VT)hval[r];
     const int64_t lr = r - row_offset;
     for (int64_t q = rowptr[lr] + gl; q < rowptr[lr + 1]; q += G) {
       const int64_t c = (int64_t)col[q] - c0;
-      if (!chunked || (c >= 0 && c < cw)) atomicAdd(&acc[c], w * (float)vals[q]);
+      if (!chunked || (c >= 0 && c < cw)) atomicAdd(&acc[c], w * vals[q]);
     }
   }
   __syncthreads();
@@ -186,14 +188,16 @@ k_hash_csr_col(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
 
 SL_API int sl_hash_csr_colwise(const int64_t* rowptr, const void* col, int idx32, const void* vals,
                                int vdtype, const int64_t* perm, const int64_t* bptr,
-                               const double* hval, int64_t S, int64_t m, float* out, int64_t ldo,
+                               const double* hval, int64_t S, int64_t m, void* out, int64_t ldo,
                                int64_t row_offset, int group, void* stream) {
   if (S <= 0 || m <= 0) return SL_OK;
   hipStream_t s = (hipStream_t)stream;
-  int64_t CW = m < 32768 ? m : 32768;  // 128 KB of LDS at most
+  const int64_t esz = vdtype == SL_F64 ? 8 : 4;
+  const int64_t cwmax = (128 * 1024) / esz;  // 128 KB of LDS at most
+  int64_t CW = m < cwmax ? m : cwmax;
   dim3 grid((unsigned)((m + CW - 1) / CW), (unsigned)S);
-  size_t lds = (size_t)CW * 4;
-#define SL_CSR(IT, VT, G) k_hash_csr_col<IT, VT, G><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, hval, out, ldo, m, CW, row_offset)
+  size_t lds = (size_t)CW * esz;
+#define SL_CSR(IT, VT, G) k_hash_csr_col<IT, VT, G><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, hval, (VT*)out, ldo, m, CW, row_offset)
 #define SL_CSR_G(IT, VT)                                   \
   switch (group) {                                         \
     case 1: SL_CSR(IT, VT, 1); break;                      \
@@ -213,30 +217,30 @@ SL_API int sl_hash_csr_colwise(const int64_t* rowptr, const void* col, int idx32
 }
 
 // ------------------------------------------------------------- CSR rowwise
-// out[r, h[c]] += v[c] * A[r, c]: G lanes per CSR row, float atomics into the
+// out[r, h[c]] += v[c] * A[r, c]: G lanes per CSR row, f32/f64 atomics into the
 // row of `out` (rows are disjoint between groups, so contention is per row).
 template <typename IT, typename VT, int G>
 __global__ void __launch_bounds__(256)
 k_hash_csr_row(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
                const VT* __restrict__ vals, int64_t rows, const int64_t* __restrict__ h,
-               const double* __restrict__ hval, float* __restrict__ out, int64_t ldo,
+               const double* __restrict__ hval, VT* __restrict__ out, int64_t ldo,
                int64_t col_offset) {
   const int64_t gid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
   const int gl = threadIdx.x % G;
   if (gid >= rows) return;
   for (int64_t q = rowptr[gid] + gl; q < rowptr[gid + 1]; q += G) {
     const int64_t c = (int64_t)col[q] + col_offset;
-    atomicAdd(&out[gid * ldo + h[c]], (float)hval[c] * (float)vals[q]);
+    atomicAdd(&out[gid * ldo + h[c]], (VT)hval[c] * vals[q]);
   }
 }
 
 SL_API int sl_hash_csr_rowwise(const int64_t* rowptr, const void* col, int idx32, const void* vals,
                                int vdtype, int64_t rows, const int64_t* h, const double* hval,
-                               float* out, int64_t ldo, int64_t col_offset, int group,
+                               void* out, int64_t ldo, int64_t col_offset, int group,
                                void* stream) {
   if (rows <= 0) return SL_OK;
   hipStream_t s = (hipStream_t)stream;
-#define SL_CR(IT, VT, G) k_hash_csr_row<IT, VT, G><<<(unsigned)((rows * G + 255) / 256), 256, 0, s>>>(rowptr, (const IT*)col, (const VT*)vals, rows, h, hval, out, ldo, col_offset)
+#define SL_CR(IT, VT, G) k_hash_csr_row<IT, VT, G><<<(unsigned)((rows * G + 255) / 256), 256, 0, s>>>(rowptr, (const IT*)col, (const VT*)vals, rows, h, hval, (VT*)out, ldo, col_offset)
 #define SL_CR_G(IT, VT)                                   \
   switch (group) {                                        \
     case 1: SL_CR(IT, VT, 1); break;                      \

@@ -156,18 +156,18 @@ def apply_csr_dense_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int 
     avg = vals.numel() / max(1, nrows)
     st = vp(_lib.stream_of(A))
     if dim == 0:
-        res = torch.zeros(S, ncols, dtype=torch.float32, device=A.device)
+        res = torch.zeros(S, ncols, dtype=odt, device=A.device)
         if in_offset != 0 or nrows != idx.numel():
             perm, bptr = _restrict(idx, in_offset, nrows, S)
         _lib.call("sl_hash_csr_colwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals),
                   _lib.dtype_code(vals.dtype), _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(val), S, ncols,
                   _lib.ptr(res), res.stride(0), in_offset, _group_for(avg), st)
     else:
-        res = torch.zeros(nrows, S, dtype=torch.float32, device=A.device)
+        res = torch.zeros(nrows, S, dtype=odt, device=A.device)
         _lib.call("sl_hash_csr_rowwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals),
                   _lib.dtype_code(vals.dtype), nrows, _lib.ptr(idx), _lib.ptr(val), _lib.ptr(res),
                   res.stride(0), in_offset, _group_for(avg), st)
-    return res.to(odt)
+    return res
 
 
 def apply_csr_sparse_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int = 0):
@@ -175,7 +175,7 @@ def apply_csr_sparse_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int
     duplicate (row, col) pairs produced by the hashing are merged.  GPU inputs
     run the sort-free kernels of ``hash_sparse_out.hip``; shapes they do not
     cover (rowwise rows longer than 32 entries, a columnwise result beyond
-    ``SPARSE_OUT_DENSE_CELLS``, f64 columnwise) take the generic coalesce."""
+    ``SPARSE_OUT_DENSE_CELLS``) take the generic coalesce."""
     if A.is_cuda:
         out = _csr_sparse_out_native(hd, A, dim, in_offset)
         if out is not None:
@@ -215,11 +215,11 @@ def _csr_sparse_out_native(hd: HashData, A: torch.Tensor, dim: int, in_offset: i
         _lib.call("sl_cwt_csr_rowwise_sparse", *args, 0, _lib.ptr(cnt), None, None, st)
         return _finish_csr(cnt, nrows, S, lambda crow, oc, ov: _lib.call(
             "sl_cwt_csr_rowwise_sparse", *args, 1, _lib.ptr(crow), _lib.ptr(oc), _lib.ptr(ov), st), vdt, dev)
-    if vdt != torch.float32 or S * ncols > SPARSE_OUT_DENSE_CELLS:
+    if S * ncols > SPARSE_OUT_DENSE_CELLS:
         return None
     if in_offset != 0 or nrows != idx.numel():
         perm, bptr = _restrict(idx, in_offset, nrows, S)
-    dense = torch.zeros(S, ncols, dtype=torch.float32, device=dev)
+    dense = torch.zeros(S, ncols, dtype=vdt, device=dev)
     avg = vals.numel() / max(1, nrows)
     _lib.call("sl_hash_csr_colwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals), _lib.dtype_code(vdt),
               _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(val), S, ncols, _lib.ptr(dense), dense.stride(0),
@@ -228,12 +228,12 @@ def _csr_sparse_out_native(hd: HashData, A: torch.Tensor, dim: int, in_offset: i
     _lib.call("sl_cwt_csr_colwise_mark", _lib.ptr(rp), _lib.ptr(ci), idx32, nrows, _lib.ptr(idx), in_offset,
               _lib.ptr(occ), ncols, st)
     cnt = torch.empty(S, dtype=torch.int64, device=dev)
-    f32 = _lib.dtype_code(torch.float32)
-    _lib.call("sl_dense_occ_compact", _lib.ptr(dense), f32, dense.stride(0), _lib.ptr(occ), S, ncols, 0,
-              _lib.ptr(cnt), None, None, f32, st)
+    dc = _lib.dtype_code(vdt)
+    _lib.call("sl_dense_occ_compact", _lib.ptr(dense), dc, dense.stride(0), _lib.ptr(occ), S, ncols, 0,
+              _lib.ptr(cnt), None, None, dc, st)
     return _finish_csr(cnt, S, ncols, lambda crow, oc, ov: _lib.call(
-        "sl_dense_occ_compact", _lib.ptr(dense), f32, dense.stride(0), _lib.ptr(occ), S, ncols, 1,
-        _lib.ptr(crow), _lib.ptr(oc), _lib.ptr(ov), f32, st), vdt, dev)
+        "sl_dense_occ_compact", _lib.ptr(dense), dc, dense.stride(0), _lib.ptr(occ), S, ncols, 1,
+        _lib.ptr(crow), _lib.ptr(oc), _lib.ptr(ov), dc, st), vdt, dev)
 
 
 def _csr_sparse_out_generic(hd: HashData, A: torch.Tensor, dim: int, in_offset: int = 0):

@@ -39,10 +39,13 @@ def test_cwt_csr_gpu_vs_explicit(dev, dim, vdt):
     if dim == 1:
         A = A.t().contiguous()
     As = A.to(vdt).to_sparse_csr().to(dev)
-    out = T.apply(As, dim=dim, sparse_output=False).double().cpu()
+    out = T.apply(As, dim=dim, sparse_output=False)
+    assert out.dtype == vdt                      # f64 values accumulate in f64 (ds_add_f64)
+    out = out.double().cpu()
     Aq = A.to(vdt).double()
     ref = P @ Aq if dim == 0 else Aq @ P.t()
-    torch.testing.assert_close(out, ref, atol=1e-4 * float(ref.abs().max()), rtol=1e-4)
+    rel = 1e-12 if vdt == torch.float64 else 1e-4
+    torch.testing.assert_close(out, ref, atol=rel * float(ref.abs().max()), rtol=rel)
 
 
 @pytest.mark.parametrize("dim", [0, 1])
