@@ -31,6 +31,7 @@ def main(argv=None):
     ap.add_argument("--cond", type=float, default=1e4)
     ap.add_argument("--oversample", type=int, default=4)
     ap.add_argument("--tol", type=float, default=1e-6)
+    ap.add_argument("--warmup", type=int, default=1, help="untimed full solves first (library init, kernel loads)")
     a = ap.parse_args(argv)
     import libskylark_amd as sk
     from libskylark_amd.algorithms import AcceleratedRegressionSolver, KrylovIterParams, RegressionProblem
@@ -51,17 +52,26 @@ def main(argv=None):
     rng.fill_random(noise, D.Normal(), seed=4, base=0, r0=comm.rank * m_loc, c0=0, ir=1, ic=1)
     b_loc += 1e-3 * noise
     A = DistMatrix(A_loc, (m, n), "VC_STAR", comm) if comm.size > 1 else A_loc
-    torch.cuda.synchronize()
-    comm.barrier()
-    t0 = time.perf_counter()
-    solver = AcceleratedRegressionSolver(RegressionProblem(A), sk.Context(7), method="lsrn", precond="qr",
-                                         oversample=a.oversample,
-                                         params=KrylovIterParams(tolerance=a.tol, iter_lim=300))
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    X, code = solver.solve(b_loc)
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
+    from libskylark_amd.utils.timer import PROFILER
+    cold = None
+    for rep in range(a.warmup + 1):
+        if rep == a.warmup:
+            PROFILER.reset()
+        torch.cuda.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        solver = AcceleratedRegressionSolver(RegressionProblem(A), sk.Context(7), method="lsrn", precond="qr",
+                                             oversample=a.oversample,
+                                             params=KrylovIterParams(tolerance=a.tol, iter_lim=300))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        X, code = solver.solve(b_loc)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        if rep == 0 and a.warmup:
+            cold = round(t2 - t0, 4)
+        use_lsqr = solver.use_lsqr
+        del solver
     r = (A_loc @ X.to(A_loc.dtype) - b_loc)
     st = torch.stack([(r * r).sum(), (b_loc * b_loc).sum()]).double()
     comm.all_reduce(st)
@@ -73,11 +83,15 @@ def main(argv=None):
                           "value": round(float(tt.sum()), 4), "unit": "s", "higher_is_better": False,
                           "n_gpus": comm.size, "scaling": "weak",
                           "setup_s": round(float(tt[0]), 4), "solve_s": round(float(tt[1]), 4),
-                          "method": "chebyshev" if not solver.use_lsqr else "lsqr", "code": int(code),
+                          "warmup_runs": a.warmup, "cold_first_run_s": cold,
+                          "method": "chebyshev" if not use_lsqr else "lsqr", "code": int(code),
                           "rel_residual": float((st[0] / st[1]).sqrt()), "rel_x_error": xerr,
                           "config": {"rows_per_gpu": m_loc, "cols": n, "cond": a.cond,
                                      "sketch": f"JLT t={a.oversample}n (bf16x2)", "precond": "QR of sketch",
                                      "dtype": "fp32"}}))
+        if PROFILER.enabled:
+            for name, r in PROFILER.report().items():
+                print(f"[profile] {name}: {r['avg_s'] * 1e3:.2f} ms total ({r['calls']} calls)", file=sys.stderr)
     return 0
 
 

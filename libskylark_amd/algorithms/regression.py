@@ -32,6 +32,7 @@ import torch
 from ..base.context import Context
 from ..base.exceptions import InvalidParametersError
 from ..parallel.distmatrix import DistMatrix
+from ..utils.timer import PROFILER
 from .krylov import IdPrecond, KrylovIterParams, MatPrecond, TriInversePrecond, chebyshev_ls, lsqr
 from .operators import as_operator
 
@@ -276,14 +277,16 @@ class AcceleratedRegressionSolver:
             self.precond, _ = _build_precond(_apply_columnwise(sk, A), precond)
         elif self.method == "lsrn":
             delta = 1e-6
-            sk = _sketch_rows("JLT", m, t, ctx)
-            if _on_gpu(A) and lowp_sketch:
-                sk.set_precision("bf16x2")  # S rounded to bf16: still a Gaussian-like sketch
-            SA = _apply_columnwise(sk, A)
+            with PROFILER.phase("lsrn.sketch"):
+                sk = _sketch_rows("JLT", m, t, ctx)
+                if _on_gpu(A) and lowp_sketch:
+                    sk.set_precision("bf16x2")  # S rounded to bf16: still a Gaussian-like sketch
+                SA = _apply_columnwise(sk, A)
             # LSRN's N = V S^{-1} (precond="svd") and R^{-1} from SA = QR ("qr") give
             # preconditioned operators with identical singular values, so the
             # Chebyshev bounds below hold for both; QR is far cheaper for large n.
-            self.precond, _ = _build_precond(SA, precond)
+            with PROFILER.phase("lsrn.precond"):
+                self.precond, _ = _build_precond(SA, precond)
             alpha = math.sqrt(2 * math.log(2.0 / delta) / t)
             if alpha >= 1 - math.sqrt(n / t):
                 self.use_lsqr = True
@@ -299,11 +302,12 @@ class AcceleratedRegressionSolver:
             return self.fallback.solve(b), -1
         vec = (b.dim() == 1) if isinstance(b, torch.Tensor) else False
         bb = b[:, None] if vec else b
-        if self.use_lsqr:
-            X, code = lsqr(self.problem.A, bb, params=self.params, R=self.precond)
-        else:
-            X = chebyshev_ls(self.problem.A, bb, self.sigma_L, self.sigma_U, self.params, self.precond)
-            code = -6
+        with PROFILER.phase("regression.krylov"):
+            if self.use_lsqr:
+                X, code = lsqr(self.problem.A, bb, params=self.params, R=self.precond)
+            else:
+                X = chebyshev_ls(self.problem.A, bb, self.sigma_L, self.sigma_U, self.params, self.precond)
+                code = -6
         return (X[:, 0] if vec else X), code
 
 
