@@ -321,10 +321,9 @@ class _DevicePlan:
             # k x k f64 Gram C = Rt^{-T} (W^T W) Rt^{-1} = Ub S^2 Ub^T (host eigensolve).
             # sigma_i keeps relative accuracy ~eps64 (sigma_1/sigma_i)^2, far below
             # the bf16 data error for every rank the sketch resolves.
-            Vt = W @ Rti
-            C = Vt.t() @ Vt
-            C = 0.5 * (C + C.t())
-            self.host_src = torch.cat([C.reshape(-1), self.status.double()])
+            # svd_core.hip: Vt = W Rt^{-1} and the symmetric C, staged with the
+            # breakdown status as [C | status] (2 launches)
+            Vt, self.host_src = SL.svd_core(W, Rti, self.status)
         self.Rti, self.Vt = Rti, Vt
 
     def pieces(self):
@@ -343,13 +342,11 @@ class _DevicePlan:
                     self.comm.all_reduce(t)
 
     def seg2(self):
-        k, r = self.k, self.rank
-        Ub = self.small[:k * r].view(k, r)
-        s64 = self.small[k * r:]
+        from ..ops import small_la as SL
+        r = self.rank
         with PROFILER.phase("svd.form_U"):
-            self.V = ((self.Vt @ Ub) / s64.clamp_min(1e-300)).float()   # V = A^T Q Ub S^{-1}
-            self.M = (self.Rti @ Ub).float()                              # U = Y Rt^{-1} Ub
-            self.s = s64.float()
+            # V = A^T Q Ub S^{-1} = Vt Ub S^{-1};  U = Y M with M = Rt^{-1} Ub (one launch)
+            self.V, self.M, self.s = SL.svd_finish(self.Vt, self.Rti, self.small, r)
 
     def graph_built(self):
         return self.g1 is not None or bool(self.piece_graphs)
@@ -428,10 +425,18 @@ class _DevicePlan:
         host = self.host_src.cpu()
         tr and tr.append(time.perf_counter())
         k, r = self.k, self.rank
-        if float(host[-1]) != 0.0:
+        # host[-1] != 0: a CholeskyQR pivot was dropped (rank-deficient block --
+        # e.g. an FJLT that sampled the same row twice, or a low-rank A); the
+        # dropped direction is an exactly-zero column from then on, harmless
+        # while at least r directions survive.  Non-finite data or fewer than
+        # r surviving directions send the call to the robust host path.
+        Cm = host[:k * k].view(k, k)
+        if not bool(torch.isfinite(Cm).all()):
             return None
-        # C was symmetrised on the device; eigh returns ascending eigenpairs
-        evals, evecs = _host_eigh(host[:k * k].view(k, k))
+        # C is exactly symmetric (svd_core.hip); eigh returns ascending eigenpairs
+        evals, evecs = _host_eigh(Cm)
+        if not float(evals[k - r]) > 1e-30 * max(float(evals[-1]), 1e-300):
+            return None
         pin = self.small_host
         pin[:k * r].view(k, r).copy_(evecs[:, k - r:].flip(1))
         torch.sqrt(evals[k - r:].flip(0).clamp_min(0.0), out=pin[k * r:])

@@ -167,6 +167,44 @@ def test_gram64_native(dev, m, k, ld):
     assert float((G - G.t()).abs().max()) <= 1e-14 * float(Gr.abs().max())
 
 
+def _fullrank_decaying(m, n, decay, seed):
+    g = torch.Generator().manual_seed(seed)
+    U0, _ = torch.linalg.qr(torch.randn(m, n, generator=g))
+    V0, _ = torch.linalg.qr(torch.randn(n, n, generator=g))
+    s0 = 100.0 * decay ** torch.arange(n, dtype=torch.float32)
+    return (U0 * s0) @ V0.t()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sketch", ["FJLT", "JLT"])
+def test_approximate_svd_device_plan_full_path(dev, sketch):
+    """Full-rank input (no CholeskyQR breakdown): the device plan runs end to
+    end -- fused passes, fp64 Gram, chol_inv, svd_core / svd_finish, graph
+    capture and replay -- and is not replaced by the host fallback."""
+    from libskylark_amd.nla import svd as SV
+    A = _fullrank_decaying(20000, 256, 0.9, 5).to(dev, torch.bfloat16)
+    ref = torch.linalg.svd(A.double(), full_matrices=False)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch=sketch)
+    SV._PLANS.clear()
+    outs = []
+    for _ in range(3):                       # eager, capture, replay
+        U, s, V = sk.nla.approximate_svd(A, 10, context=sk.Context(3), params=p)
+        outs.append((U, s, V))
+    plans = list(SV._PLANS.values())
+    assert len(plans) == 1 and plans[0].calls == 3 and plans[0].graph_built()
+    for U, s, V in outs:
+        torch.testing.assert_close(s.double(), ref.S[:10], rtol=1e-2, atol=0)
+        torch.testing.assert_close(s[:3].double(), ref.S[:3], rtol=1e-4, atol=0)
+        I = torch.eye(10, device=dev, dtype=torch.float64)
+        torch.testing.assert_close(U.double().t() @ U.double(), I, atol=1e-5, rtol=0)
+        torch.testing.assert_close(V.double().t() @ V.double(), I, atol=1e-4, rtol=0)
+        # leading singular vectors match the exact ones (up to sign)
+        cu = (U[:, :3].double() * ref.U[:, :3]).sum(0).abs()
+        cv = (V[:, :3].double() * ref.Vh[:3].t()).sum(0).abs()
+        assert float(cu.min()) > 0.999 and float(cv.min()) > 0.999
+    torch.testing.assert_close(outs[2][1], outs[1][1], rtol=1e-6, atol=0)
+
+
 @pytest.mark.gpu
 def test_approximate_svd_graph_replay_matches_eager(dev):
     """The hipGraph-replayed device plan gives the eager result (same context)."""
