@@ -312,9 +312,11 @@ k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __rest
   __shared__ double rows[KM][2 * KM];
   __shared__ double dsh[KM];
   const int t = threadIdx.x, tr = t >> 4, tc = t & 15;
+  __shared__ double diag[KM];
   double m[4][8];
-  double dmax = 0.0;
-  for (int c = 0; c < k; ++c) dmax = fmax(dmax, fabs(G[c * ldg + c]));
+  // diagonal staged through LDS: a rolled loop of k global loads here waited
+  // on one load at a time (~0.7 us each -> most of the kernel's 37 us)
+  if (t < k) diag[t] = fabs(G[t * ldg + t]);
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int i = tr + 16 * a;
@@ -327,6 +329,9 @@ k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __rest
       m[a][4 + b] = (i == c) ? 1.0 : 0.0;
     }
   }
+  __syncthreads();
+  double dmax = 0.0;
+  for (int c = 0; c < k; ++c) dmax = fmax(dmax, diag[c]);
   int bad = 0;
   for (int j = 0; j < k; ++j) {
     const int ja = j >> 4;
