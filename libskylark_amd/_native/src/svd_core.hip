@@ -10,7 +10,7 @@
 //   sl_svd_core:   Vt = W Rt^{-1} (n x k, f64) and C = Vt^T Vt, symmetric by
 //                  construction (only a <= c is summed, mirrored), written
 //                  with the breakdown status into the host staging vector
-//                  [C (k*k) | status].  Row blocks of 32: Rt^{-1} and the W
+//                  [C (k*k) | status].  Row blocks of 16: Rt^{-1} and the W
 //                  block in LDS, per-block C partials in a slab, reduced in a
 //                  fixed slab order by a second kernel (one thread per entry)
 //                  (deterministic, no float atomics).
@@ -20,8 +20,25 @@
 
 namespace {
 
-constexpr int RB = 32;     // rows per block
+constexpr int RB = 16;     // rows per block (more blocks: these kernels are latency bound)
 constexpr int KMAX = 64;
+
+// global -> LDS staging of n <= 256 * U doubles with every load issued before
+// the first LDS store (a rolled copy loop waits on one global load at a time)
+template <int U>
+__device__ __forceinline__ void stage(double* __restrict__ dst, const double* __restrict__ src, int n, int t) {
+  double v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = t + 256 * u;
+    v[u] = e < n ? src[e] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = t + 256 * u;
+    if (e < n) dst[e] = v[u];
+  }
+}
 
 // All dot products read LDS in unrolled loops (loads issued ahead of the
 // dependent FMA chain) -- the first version, with rolled loops, spent ~30 us
@@ -35,10 +52,19 @@ k_svd_core_block(const double* __restrict__ W, int n, int k, int ldw, const doub
   const int t = threadIdx.x;
   const int r0 = blockIdx.x * RB;
   const int rows = min(RB, n - r0);
-  for (int e = t; e < k * k; e += 256) sR[e] = Rti[e];
-  for (int e = t; e < RB * k; e += 256) {
-    const int i = e / k, j = e - i * k;
-    sW[e] = i < rows ? W[(int64_t)(r0 + i) * ldw + j] : 0.0;
+  stage<KMAX * KMAX / 256>(sR, Rti, k * k, t);
+  {
+    double v[RB * KMAX / 256];
+#pragma unroll
+    for (int u = 0; u < RB * KMAX / 256; ++u) {
+      const int e = t + 256 * u, i = e / k, j = e - i * k;
+      v[u] = (e < RB * k && i < rows) ? W[(int64_t)(r0 + i) * ldw + j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < RB * KMAX / 256; ++u) {
+      const int e = t + 256 * u;
+      if (e < RB * k) sW[e] = v[u];
+    }
   }
   __syncthreads();
   for (int e = t; e < RB * k; e += 256) {
@@ -106,14 +132,14 @@ k_svd_finish(const double* __restrict__ Vt, int n, int k, const double* __restri
   const int t = threadIdx.x;
   const double* Ub = small;          // k x r, row-major
   const double* s = small + k * r;   // r singular values
-  for (int e = t; e < k * r; e += 256) sU[e] = Ub[e];
-  for (int j = t; j < r; j += 256) sinv[j] = 1.0 / fmax(s[j], 1e-300);
+  stage<KMAX * KMAX / 256>(sU, Ub, k * r, t);
+  if (t < r) sinv[t] = 1.0 / fmax(s[t], 1e-300);
   const int nb = (n + RB - 1) / RB;
   const bool last = (int)blockIdx.x == nb;
   const int r0 = blockIdx.x * RB;
   const int rows = last ? k : min(RB, n - r0);
   const double* src = last ? Rti : Vt + (int64_t)r0 * k;
-  for (int e = t; e < rows * k; e += 256) sA[e] = src[e];
+  stage<KMAX * KMAX / 256>(sA, src, rows * k, t);
   __syncthreads();
   for (int e = t; e < rows * r; e += 256) {
     const int i = e / r, j = e - i * r;
@@ -136,7 +162,7 @@ k_svd_finish(const double* __restrict__ Vt, int n, int k, const double* __restri
 
 }  // namespace
 
-// slabs: ceil(n / 32) * k * k doubles of workspace.
+// slabs: ceil(n / 16) * k * k doubles of workspace.
 SL_API int sl_svd_core(const double* W, int n, int k, int ldw, const double* Rti, double* Vt, double* slabs,
                        double* host_src, const int* status, void* stream) {
   if (k < 1 || k > KMAX || n < 1) {

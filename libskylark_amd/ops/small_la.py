@@ -105,7 +105,7 @@ def svd_core(W: torch.Tensor, Rti: torch.Tensor, status: torch.Tensor | None = N
         W = W.contiguous()
     Rti = Rti.to(torch.float64).contiguous()
     Vt = torch.empty(n, k, dtype=torch.float64, device=W.device)
-    slabs = torch.empty(-(-n // 32) * k * k, dtype=torch.float64, device=W.device)
+    slabs = torch.empty(-(-n // 16) * k * k, dtype=torch.float64, device=W.device)
     host_src = torch.empty(k * k + 1, dtype=torch.float64, device=W.device)
     _lib.call("sl_svd_core", _lib.ptr(W), n, k, W.stride(0), _lib.ptr(Rti), _lib.ptr(Vt), _lib.ptr(slabs),
               _lib.ptr(host_src), _lib.ptr(status) if status is not None else None, vp(_lib.stream_of(W)))
