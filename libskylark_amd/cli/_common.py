@@ -35,9 +35,13 @@ def _warm_up(dev):
     from ..ops import _lib
     _lib.load()
     if dev.type == "cuda":
-        a = torch.ones(8, 8, device=dev)
-        (a @ a).sum().item()
-        torch.linalg.qr(a.double())[0].sum().item()
+        # BLAS kernels are loaded per (dtype, transpose) variant on first use:
+        # touch the f32 / f64 NN, TN and NT GEMMs and the solver paths once
+        for dt in (torch.float32, torch.float64):
+            a = torch.ones(64, 64, dtype=dt, device=dev)
+            ((a @ a) + (a.t() @ a) + (a @ a.t())).sum().item()
+        torch.linalg.qr(a)[0].sum().item()
+        torch.linalg.cholesky_ex(a + 64 * torch.eye(64, dtype=a.dtype, device=dev))[0].sum().item()
     # Small problems stay on the host (host_if_small) even when a GPU is
     # present, so the host LAPACK / sparse paths are initialised as well.
     a = torch.eye(8, dtype=torch.float64) + 0.5
