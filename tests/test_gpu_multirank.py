@@ -1,0 +1,54 @@
+"""Two ranks on ONE MI355X over gloo (CUDA tensors, host-staged collectives):
+rehearses the multi-rank device randSVD plan -- per-piece hipGraphs with the
+all-reduces between replays -- that bench.py runs over RCCL on 8 GPUs.  (RCCL
+itself needs one GPU per rank; the 8-GPU run is the driver's.)"""
+import pytest
+import torch
+
+from mp_utils import run_distributed
+
+pytestmark = pytest.mark.gpu
+
+
+def _matrix(m, n, seed=11):
+    g = torch.Generator().manual_seed(seed)
+    U0, _ = torch.linalg.qr(torch.randn(m, n, generator=g))
+    V0, _ = torch.linalg.qr(torch.randn(n, n, generator=g))
+    s0 = 100.0 * 0.9 ** torch.arange(n, dtype=torch.float32)
+    return ((U0 * s0) @ V0.t()).to(torch.bfloat16)
+
+
+def _rank_svd(rank, world, m, n):
+    import libskylark_amd as sk
+    from libskylark_amd.nla import svd as SV
+    from libskylark_amd.parallel import Comm, DistMatrix
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    A = _matrix(m, n)
+    ml = m // world
+    A_loc = A[rank * ml:(rank + 1) * ml].contiguous().to(dev)
+    comm = Comm()
+    D = DistMatrix(A_loc, (m, n), "VC_STAR", comm)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT")
+    outs = [sk.nla.approximate_svd(D, 10, context=sk.Context(3), params=p) for _ in range(3)]
+    plans = list(SV._PLANS.values())
+    s_all = [o[1].cpu() for o in outs]
+    U = outs[-1][0]
+    U_loc = (U.local if hasattr(U, "local") else U).cpu()
+    return {"s": s_all, "U": U_loc, "calls": plans[0].calls if plans else -1,
+            "pieces": bool(plans and plans[0].piece_graphs)}
+
+
+def test_two_rank_device_randsvd_matches_single(dev):
+    import libskylark_amd as sk
+    m, n = 40000, 256
+    res = run_distributed(_rank_svd, 2, m, n, timeout=300)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT")
+    U1, s1, V1 = sk.nla.approximate_svd(_matrix(m, n).to(dev), 10, context=sk.Context(3), params=p)
+    for r in (0, 1):
+        assert res[r]["calls"] == 3 and res[r]["pieces"], res[r]
+        for s in res[r]["s"]:
+            torch.testing.assert_close(s, s1.cpu(), rtol=1e-5, atol=0)
+    # the row blocks of U on the two ranks are the single-process U's blocks
+    Ucat = torch.cat([res[0]["U"], res[1]["U"]], 0)
+    torch.testing.assert_close(Ucat.abs(), U1.cpu().abs(), rtol=1e-3, atol=1e-4)
