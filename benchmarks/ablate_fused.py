@@ -16,7 +16,7 @@ import time
 import torch
 
 from libskylark_amd.base import distributions as D
-from libskylark_amd.ops import _lib, rng
+from libskylark_amd.ops import _lib, rng, tallskinny  # noqa: F401  (registers the sl_tsk_* signatures)
 
 
 def main():
@@ -29,7 +29,7 @@ def main():
     W = torch.empty(n, k, device=dev)
     G = torch.empty(k, k, device=dev)
     lib = _lib.require()
-    ws = torch.empty(int(lib.sl_tsk_fused_workspace(m, n, k)), dtype=torch.uint8, device=dev)
+    ws = torch.empty(tallskinny.fused_workspace_bytes(m, n, k), dtype=torch.uint8, device=dev)
     lib.sl_tsk_set_ablate.argtypes = [C.c_int]
     lib.sl_tsk_set_nbuf.argtypes = [C.c_int]
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)

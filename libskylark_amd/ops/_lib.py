@@ -107,7 +107,11 @@ def call(name: str, *args):
     fn = getattr(lib, name, None)
     if fn is None:
         raise NativeLibraryError(f"native symbol {name} missing from {LIB_PATH} (stale build?)")
-    if fn.argtypes is None and name in SIGNATURES:
+    if fn.argtypes is None:
+        if name not in SIGNATURES:
+            # never call with ctypes' default int conversion: a 64-bit size or
+            # stride would be passed as a 32-bit int with undefined upper bits
+            raise NativeLibraryError(f"{name}: no registered signature (import the ops module that declares it)")
         fn.argtypes = SIGNATURES[name]
         fn.restype = _RESTYPE.get(name, C.c_int)
     rc = fn(*args)
