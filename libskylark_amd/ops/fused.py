@@ -120,16 +120,30 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
 
 
 class WCache:
-    """Per-sketch cache of realised, split W blocks keyed by device and window."""
+    """Per-sketch LRU cache of realised, split W blocks keyed by device and
+    window.  Bounded (``MAX_ENTRIES`` blocks, ``MAX_BYTES`` of planes): a
+    streamed or sharded apply touches one window per panel, and keeping them
+    all would grow to the whole realised S."""
+
+    MAX_ENTRIES = 8
+    MAX_BYTES = 1 << 30
 
     def __init__(self):
         self._d = {}
 
+    @staticmethod
+    def _bytes(w):
+        return w.hi.numel() * w.hi.element_size() * 2
+
     def get(self, key, make):
-        w = self._d.get(key)
+        w = self._d.pop(key, None)
         if w is None:
             w = SplitW(make())
-            self._d[key] = w
+        self._d[key] = w                      # most recently used last
+        total = sum(self._bytes(v) for v in self._d.values())
+        while len(self._d) > 1 and (len(self._d) > self.MAX_ENTRIES or total > self.MAX_BYTES):
+            old = self._d.pop(next(iter(self._d)))
+            total -= self._bytes(old)
         return w
 
     def clear(self):

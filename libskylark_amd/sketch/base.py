@@ -199,6 +199,12 @@ class SketchTransform:
                 return SA
         return op.to_back(res)
 
+    def apply_streamed(self, A, dim=COLUMNWISE, **kw):
+        """Sketch a host-resident dense matrix through the GPU panel by panel
+        (pinned double-buffered H2D on a copy stream; see ``sketch.streaming``)."""
+        from .streaming import apply_streamed
+        return apply_streamed(self, A, dim, **kw)
+
     def __mul__(self, A):
         return self.apply(A, None, COLUMNWISE)
 

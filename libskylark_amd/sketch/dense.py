@@ -20,6 +20,7 @@ class DenseSketch(SketchTransform):
     """S x N matrix with iid entries ``scale * dist`` realised from the stream."""
 
     dist = D.Normal()
+    linear_shards = True   # S A = sum over row blocks of A of S[:, blk] A[blk] (streaming, distribution)
 
     def _scale(self) -> float:
         raise NotImplementedError

@@ -18,6 +18,7 @@ from .base import SketchTransform, register
 
 class HashSketch(SketchTransform):
     supports_sparse_output = True  # sparse in -> sparse out by default (reference: output ctor = input's)
+    linear_shards = True           # S A = sum over row blocks (streaming, distribution)
     value_dist = D.Rademacher()
 
     def _draw_values(self, ctx) -> torch.Tensor:
