@@ -98,9 +98,16 @@ def _ridge(Z: torch.Tensor, Y: torch.Tensor, lam: float, data: _Data | None = No
     """W = argmin |Z W - Y|^2 + lam |W|^2 via the s x s normal equations in
     fp64 (reference ``El::Ridge``); distributed Z: all-reduce [Z^T Z | Z^T Y]."""
     s = Z.shape[1]
-    Zd = Z.to(torch.float64)
-    Yd = Y.to(torch.float64)
-    G = torch.cat([Zd.t() @ Zd, Zd.t() @ Yd], dim=1).contiguous()
+    t = Y.shape[1] if Y.dim() > 1 else 1
+    Y2 = Y if Y.dim() > 1 else Y[:, None]
+    # [Z^T Z | Z^T Y] accumulated in fp64 over row chunks: no n x s fp64 copy
+    # of Z (32 GB for 1e6 x 4096 features), same fp64 products and sums
+    G = torch.zeros(s, s + t, dtype=torch.float64, device=Z.device)
+    chunk = max(1, (1 << 27) // max(1, s + t))
+    for r0 in range(0, Z.shape[0], chunk):
+        Zc = Z[r0:r0 + chunk].to(torch.float64)
+        G[:, :s].addmm_(Zc.t(), Zc)
+        G[:, s:].addmm_(Zc.t(), Y2[r0:r0 + chunk].to(torch.float64))
     if data is not None:
         data.allreduce(G)
     C = G[:, :s]
