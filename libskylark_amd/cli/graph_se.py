@@ -37,7 +37,8 @@ def main(argv=None):
     if not a.graphfile:
         raise SystemExit("skylark_graph_se: a graph file is required (positional or -g)")
     if a.hdfs:
-        raise SystemExit("HDFS input is not supported in this build")
+        from ..io.remote import hdfs_url
+        a.graphfile = hdfs_url(a.hdfs if not a.port else f"{a.hdfs}:{a.port}", a.graphfile)
     comm, dev = setup(a.cpu)
     T = Timer(comm)
     T.start("Reading the graph... ")

@@ -36,14 +36,18 @@ def main(argv=None):
     if not a.inputfile:
         print("Input file is required.")
         return -1
-    if a.hdfs:
-        raise SystemExit("HDFS input is not supported in this build")
     comm, dev = setup(a.cpu)
     ctx = Context(a.seed)
     dt = torch.float32 if a.single else torch.float64
     T = Timer(comm)
     T.start("Reading the matrix... ")
-    if a.directory:
+    if a.hdfs:
+        # file or directory on HDFS (or any fsspec URL), streamed block by block
+        url = IO.hdfs_url(a.hdfs if not a.port else f"{a.hdfs}:{a.port}", a.inputfile)
+        A, b = IO.read_libsvm_stream(url, dtype=dt, device=dev, comm=comm if comm.size > 1 else None)
+        if comm.size == 1:
+            b = b[:, None]
+    elif a.directory:
         A, b = IO.read_dir_libsvm(a.inputfile, dtype=dt, device=dev, comm=comm if comm.size > 1 else None)
         if comm.size == 1:
             b = b[:, None]

@@ -28,7 +28,7 @@ def build_parser():
     p.add_argument("--filetype", default="LIBSVM", help="Input file type (LIBSVM or ARC_LIST).")
     p.add_argument("-d", "--directory", action="store_true", help="inputfile is a directory of files.")
     p.add_argument("-s", "--seed", type=int, default=38734)
-    p.add_argument("--hdfs", default="", help="HDFS filesystem name (not supported in this build).")
+    p.add_argument("--hdfs", default="", help="HDFS namenode (or any fsspec URL prefix); input is streamed.")
     p.add_argument("--port", type=int, default=0)
     p.add_argument("-k", "--rank", type=int, default=6, help="Target rank.")
     p.add_argument("-i", "--powerits", type=int, default=2, help="Number of power iterations.")
@@ -50,7 +50,12 @@ def _read_inputs(a, comm, dev, dtype):
     import os
     from .. import io as IO
     if a.hdfs:
-        raise SystemExit("HDFS input is not supported in this build")
+        url = IO.hdfs_url(a.hdfs if not getattr(a, "port", 0) else f"{a.hdfs}:{a.port}", a.inputfile)
+        if a.filetype.upper() == "ARC_LIST":
+            raise SystemExit("ARC_LIST input from HDFS is not supported; use LIBSVM")
+        A = IO.read_libsvm_stream(url, sparse=a.sparse, dtype=dtype, device=dev,
+                                  comm=comm if comm.size > 1 else None)[0]
+        return A
     files = [a.inputfile]
     if a.directory:
         files = sorted(os.path.join(a.inputfile, f) for f in os.listdir(a.inputfile))

@@ -6,6 +6,8 @@
   (:func:`read_arc_list`), reference ``utility/io/arc_list.hpp``.
 * HDF5: ``ReadHDF5``/``write_hdf5`` use h5py when present, otherwise the
   built-in reader/writer of ``io/h5.py`` (no libhdf5 needed).
+* Remote / HDFS: :class:`LineStreamer`, :class:`LineStreamerIterator`,
+  :func:`read_libsvm_stream` over fsspec URLs (:mod:`.remote`).
 * :func:`read` — ``ml/io.hpp:869`` dispatch on fileformat code
   (0 libsvm-dense, 1 libsvm-sparse, 2 hdf5-dense, 3 hdf5-sparse).
 """
@@ -17,6 +19,8 @@ import torch
 from ..base.exceptions import IOError_
 from .libsvm import (ReadDirLIBSVM, ReadLIBSVM, WriteLIBSVM, read_dir_libsvm, read_libsvm,  # noqa: F401
                      read_libsvm_dist, write_libsvm)
+from .remote import (LineStreamer, LineStreamerIterator, ReadLIBSVMStream, hdfs_url,  # noqa: F401
+                     read_libsvm_stream)
 
 LIBSVM_DENSE, LIBSVM_SPARSE, HDF5_DENSE, HDF5_SPARSE = range(4)
 

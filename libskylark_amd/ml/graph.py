@@ -57,9 +57,15 @@ class SimpleGraph:
 
     @classmethod
     def from_file(cls, fname: str):
-        """Arc-list text: one ``u v`` per line, ``#`` comments."""
+        """Arc-list text: one ``u v`` per line, ``#`` comments.  ``fname`` may
+        be an fsspec URL (``hdfs://namenode/path``, ...), streamed line by line."""
         rows = []
-        with open(fname) as f:
+        if "://" in fname:
+            from ..io.remote import LineStreamer
+            f = LineStreamer(fname)
+        else:
+            f = open(fname)
+        with f:
             for line in f:
                 if not line.strip() or line.startswith("#"):
                     continue
