@@ -1,6 +1,6 @@
 """Machine learning on sketches (reference ``ml/``): kernels, KRR/RLSC,
 BlockADMM, models, graph analytics."""
-from . import admm, coding, graph, hilbert, kernels, krr, model, rlsc  # noqa: F401
+from . import admm, coding, graph, hilbert, kernels, krr, model, nonlinear, rlsc  # noqa: F401
 from .admm import BlockADMM, BlockADMMSolver  # noqa: F401
 from .coding import DummyCoding, DummyDecode, dummy_coding, dummy_decode  # noqa: F401
 from .graph import (ApproximateASE, FindLocalCluster, SimpleGraph, TimeDependentPPR, approximate_ase,  # noqa: F401
@@ -16,3 +16,6 @@ from .model import FeatureExpansionModel, HilbertModel, KernelModel, load_model,
 from .rlsc import (ApproximateKernelRLSC, FasterKernelRLSC, KernelRLSC, LargeScaleKernelRLSC,  # noqa: F401
                    SketchedApproximateKernelRLSC, approximate_kernel_rlsc, faster_kernel_rlsc, kernel_rlsc,
                    large_scale_kernel_rlsc, sketched_approximate_kernel_rlsc)
+from .nonlinear import (RLS, NystromRLS, SketchPCR, SketchRLS, approximate_domsubspace_basis,  # noqa: F401
+                        euclidean, nystromrls, rls, sketchpcr, sketchrls)
+from . import nonlinear as distances  # noqa: F401  (python-skylark ml.distances.euclidean)

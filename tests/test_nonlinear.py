@@ -1,0 +1,97 @@
+"""python-skylark kernel RLS estimators (reference
+``python-skylark/skylark/ml/nonlinear.py``; its docstrings quote ~87-93 %
+accuracy on USPS digits — parity unpinned, those runs need the full USPS
+train file; here a 3-blob problem with a known Bayes rate)."""
+import numpy as np
+import pytest
+import torch
+
+import libskylark_amd as sk
+from libskylark_amd.ml import nonlinear as NL
+
+
+def _blobs(n=600, seed=0, dtype=torch.float64):
+    g = torch.Generator().manual_seed(seed)
+    lab = torch.randint(0, 3, (n,), generator=g)
+    c = torch.tensor([[2.0, 0, 0, 0], [0, 2.0, 0, 0], [0, 0, 2.0, 0]], dtype=torch.float64)
+    X = c[lab] + 0.5 * torch.randn(n, 4, generator=g, dtype=torch.float64)
+    return X.to(dtype), (lab + 1).double()   # 1-based labels: decoded back to the same values
+
+
+ESTIMATORS = [
+    ("rls", lambda k: NL.RLS(k), dict(regularization=1e-2)),
+    ("sketchrls", lambda k: NL.SketchRLS(k, sk.Context(1)), dict(random_features=200, regularization=1e-2)),
+    ("nystrom", lambda k: NL.NystromRLS(k, sk.Context(2)), dict(random_features=80, regularization=1e-2)),
+    ("nystrom_lev", lambda k: NL.NystromRLS(k, sk.Context(2)),
+     dict(random_features=80, regularization=1e-2, probdist="leverages")),
+    ("pcr", lambda k: NL.SketchPCR(k, sk.Context(3)), dict(rank=30)),
+    ("pcr_sampled", lambda k: NL.SketchPCR(k, sk.Context(3)), dict(rank=30, samplesize=300)),
+]
+
+
+@pytest.mark.parametrize("name,make,kw", ESTIMATORS, ids=[e[0] for e in ESTIMATORS])
+def test_estimators_classify_blobs(name, make, kw):
+    X, Y = _blobs()
+    M = make(sk.ml.Gaussian(4, 1.5)).train(X[:400], Y[:400], **kw)
+    pred = np.array(M.predict(X[400:]))
+    assert set(pred.tolist()) <= {1, 2, 3}
+    assert (pred == Y[400:].numpy()).mean() >= 0.97
+
+
+def test_rls_matches_closed_form_and_regression():
+    X, _ = _blobs(200)
+    y = torch.sin(X[:, 0]) + X[:, 1]
+    k = sk.ml.Gaussian(4, 2.0)
+    M = NL.rls(k).train(X[:150], y[:150], regularization=1e-3, multiclass=False)
+    K = torch.exp(-torch.cdist(X[:150], X[:150]) ** 2 / (2 * 4.0))
+    alpha = torch.linalg.solve(K + 1e-3 * torch.eye(150, dtype=torch.float64), y[:150, None])
+    torch.testing.assert_close(M.model["alpha"], alpha, rtol=1e-6, atol=1e-8)
+    Kt = torch.exp(-torch.cdist(X[150:], X[:150]) ** 2 / (2 * 4.0))
+    torch.testing.assert_close(M.predict(X[150:]), (Kt @ alpha)[:, 0], rtol=1e-6, atol=1e-8)
+
+
+def test_sketchrls_is_ridge_on_features():
+    X, Y = _blobs(300)
+    k = sk.ml.Gaussian(4, 1.5)
+    M = NL.sketchrls(k, sk.Context(7)).train(X, Y, random_features=64, regularization=0.1)
+    Z = M.model["rft"] / X
+    T, _, _ = sk.ml.dummy_coding(Y)
+    W = torch.linalg.solve(Z.t() @ Z + 0.1 * torch.eye(64, dtype=torch.float64), Z.t() @ T)
+    torch.testing.assert_close(M.model["weights"], W, rtol=1e-8, atol=1e-10)
+
+
+def test_domsubspace_basis_is_orthonormal_dominant():
+    X, _ = _blobs(500)
+    k = sk.ml.Gaussian(4, 1.5)
+    Q, S, R, V = NL.approximate_domsubspace_basis(X, 10, 40, 400, k, context=sk.Context(5))
+    assert Q.shape == (500, 10) and R.shape == (40, 40) and V.shape == (40, 10)
+    # orthonormal up to the CountSketch's subspace distortion
+    G = Q.t() @ Q
+    assert float((G - torch.eye(10, dtype=G.dtype)).abs().max()) < 0.6
+    # spans (nearly) the top-10 left singular subspace of Z
+    Z = S / X
+    U = torch.linalg.svd(Z, full_matrices=False)[0][:, :10]
+    Qo = torch.linalg.qr(Q)[0]
+    s = torch.linalg.svdvals(U.t() @ Qo)
+    assert float(s.min()) > 0.9
+    with pytest.raises(sk.base.exceptions.InvalidParametersError):
+        NL.approximate_domsubspace_basis(X, 10, 40, 20, k)
+
+
+def test_euclidean_and_distances_alias():
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(7, 5, generator=g, dtype=torch.float64)
+    Y = torch.randn(3, 5, generator=g, dtype=torch.float64)
+    D = sk.ml.distances.euclidean(X, Y)
+    torch.testing.assert_close(D, torch.cdist(Y, X) ** 2, rtol=1e-10, atol=1e-10)
+    torch.testing.assert_close(NL.euclidean(X.to_sparse_csr(), Y), D)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,make,kw", ESTIMATORS[:3] + ESTIMATORS[4:5], ids=["rls", "sketchrls", "nystrom", "pcr"])
+def test_estimators_on_gpu(dev, name, make, kw):
+    X, Y = _blobs(dtype=torch.float32)
+    Xd = X.to(dev)
+    M = make(sk.ml.Gaussian(4, 1.5)).train(Xd[:400], Y[:400], **kw)
+    pred = np.array(M.predict(Xd[400:]))
+    assert (pred == Y[400:].numpy()).mean() >= 0.97
