@@ -44,4 +44,4 @@ import warnings as _w  # noqa: E402
 _w.filterwarnings("ignore", message="Sparse CSR tensor support is in beta state")
 _w.filterwarnings("ignore", message="Sparse CSC tensor support is in beta state")
 
-from . import algorithms, base, io, ml, nla, parallel, sketch  # noqa: E402,F401
+from . import algorithms, base, io, metrics, ml, nla, parallel, sketch  # noqa: E402,F401

@@ -58,6 +58,9 @@ class InvalidParametersError(SkylarkError, ValueError):
 
 
 InvalidObjectError = InvalidParametersError
+# python-skylark errors.py spellings
+InvalidParamterError = InvalidParametersError
+ParameterMistmatchError = DimensionMismatchError
 
 
 class UnsupportedBaseOperation(SkylarkError):

@@ -95,3 +95,12 @@ def test_estimators_on_gpu(dev, name, make, kw):
     M = make(sk.ml.Gaussian(4, 1.5)).train(Xd[:400], Y[:400], **kw)
     pred = np.array(M.predict(Xd[400:]))
     assert (pred == Y[400:].numpy()).mean() >= 0.97
+
+
+def test_metrics():
+    assert sk.metrics.classification_accuracy([1, 2, 3, 3], torch.tensor([1, 2, 3, 1])) == 75.0
+    assert sk.metrics.rmse(torch.tensor([1.0, 3.0]), [1.0, 1.0]) == pytest.approx(np.sqrt(2.0))
+    assert sk.metrics.relative_error([3.0, 4.0], [3.0, 4.0]) == 0.0
+    with pytest.raises(ValueError):
+        sk.metrics.classification_accuracy([1], [1, 2])
+    assert sk.base.exceptions.InvalidParamterError is sk.base.exceptions.InvalidParametersError
