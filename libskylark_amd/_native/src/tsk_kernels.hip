@@ -25,7 +25,11 @@
 //                                  of the SAME LDS image, y as bf16 hi+lo,
 //                                  v_mfma_f32_16x16x16_bf16 (2 per tile)
 //       - step 4  G += y^T y     : hi*hi + hi*lo + lo*hi, tiles spread
-//                                  over the waves;
+//                                  over the waves; or (G64) the upper
+//                                  16x16 tiles in f64 from the reduced f32
+//                                  y with v_mfma_f64_16x16x4_f64 — the fp64
+//                                  Gram CholeskyQR needs, hidden in the
+//                                  pass instead of a second read of Y;
 //   * raw s_barrier + counted vmcnt (no __syncthreads, which would drain
 //     the DMA queue), all LDS in one dynamic array;
 //   * per-workgroup W/G partial slabs, summed in f64 by a second kernel.
@@ -39,6 +43,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) double f64x4;
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int WAVES = 8;
@@ -95,9 +100,12 @@ struct Geo {
   static constexpr int LDS = ABYTES + YP_BYTES + YF_BYTES;
   static constexpr int GTILES = KT * KT;
   static constexpr int GS = (GTILES + WAVES - 1) / WAVES;  // G tiles per wave
+  static constexpr int GT64 = KT * (KT + 1) / 2;            // upper tiles (f64 Gram)
+  static constexpr int GS64 = (GT64 + WAVES - 1) / WAVES;
 };
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
+          bool G64 = false>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
@@ -153,9 +161,15 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
 #pragma unroll
       for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  f32x4 accG[GG::GS];
+  f32x4 accG[G64 ? 1 : GG::GS];
+  f64x4 accG64[G64 ? GG::GS64 : 1];
+  if constexpr (G64) {
 #pragma unroll
-  for (int s = 0; s < GG::GS; ++s) accG[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < GG::GS64; ++s) accG64[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+  } else {
+#pragma unroll
+    for (int s = 0; s < GG::GS; ++s) accG[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   // ---- LDS-DMA of one row block (this wave's columns) into buffer `buf`
   auto issue_impl = [&](int64_t blk, int buf, auto nt_c) {
@@ -308,7 +322,28 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       }
 #undef SL_STEP3
     }
-    if (need_g) {
+    if constexpr (G64) {
+      // ---- step 4 (f64): upper tile tau = w + 8 s is (t1, t2), t1 <= t2;
+      //      A[i][kk] = y[4u+kk][16 t1 + i], B[kk][j] = y[4u+kk][16 t2 + j]
+      //      (lane: i = j = l & 15, kk = l >> 4), four K=4 steps per block
+      if (need_g) {
+        int tau = 0;
+#pragma unroll
+        for (int t1 = 0; t1 < KT; ++t1)
+#pragma unroll
+          for (int t2 = t1; t2 < KT; ++t2, ++tau) {
+            if ((tau % WAVES) == w) {
+              const int s = tau / WAVES;
+#pragma unroll
+              for (int u = 0; u < BM / 4; ++u) {
+                const double va = (double)yf[(16 * t1 + i16) * BM + 4 * u + g4];
+                const double vb = (double)yf[(16 * t2 + i16) * BM + 4 * u + g4];
+                accG64[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, accG64[s], 0, 0, 0);
+              }
+            }
+          }
+      }
+    } else if (need_g) {
       // ---- step 4: G tiles tau = w + 8 s (t1 = tau / KT, t2 = tau % KT):
       //      hi*hi + hi*lo + lo*hi
       // tile indices are compile-time; only the owner test (wave-uniform) is runtime
@@ -336,7 +371,25 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         for (int j = 0; j < 4; ++j)
           ws[(c0w + 16 * ct + (lane >> 4) * 4 + j) * GG::KP + 16 * t + (lane & 15)] = accW[ct][t][j];
   }
-  if constexpr (DO_G) {
+  if constexpr (DO_G && G64) {
+    // f64 slab [KP][KP]: each upper tile and its mirror (D row = l>>4 + 4 r, col = l & 15)
+    double* gs = (double*)Gslab + (int64_t)blockIdx.x * GG::KP * GG::KP;
+    int tau = 0;
+#pragma unroll
+    for (int t1 = 0; t1 < KT; ++t1)
+#pragma unroll
+      for (int t2 = t1; t2 < KT; ++t2, ++tau) {
+        if ((tau % WAVES) == w) {
+          const int s = tau / WAVES;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * t1 + (lane >> 4) + 4 * r, j = 16 * t2 + (lane & 15);
+            gs[i * GG::KP + j] = accG64[s][r];
+            if (t1 != t2) gs[j * GG::KP + i] = accG64[s][r];
+          }
+        }
+      }
+  } else if constexpr (DO_G) {
     float* gs = Gslab + (int64_t)blockIdx.x * GG::KP * GG::KP;
 #pragma unroll
     for (int s = 0; s < GG::GS; ++s) {
@@ -393,6 +446,8 @@ k_slab_reduce_rows(const IT* __restrict__ slab, int nslab, int64_t slab_stride, 
   }
 }
 
+int sl_slab_reduce_launch_d2d(const double* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
+                              int cols, double* out, int ld_out, hipStream_t s);
 int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
                           int cols, float* out, int ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return SL_OK;
@@ -436,11 +491,12 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
+          bool G64 = false>
 int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   using GG = Geo<NW, KT, NBUF>;
-  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T>;
+  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64>;
   static bool attr = false;
   if (!attr) {
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
@@ -465,18 +521,18 @@ int nbuf_request() {
   return nb;
 }
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, bool HI_T = false>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, bool HI_T = false, bool G64 = false>
 int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
               float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   int nb = nbuf_request();
   constexpr int LIM = 160 * 1024;
   if (nb >= 5 && Geo<NW, KT, 5>::LDS <= LIM)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 5, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 5, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
   if (nb >= 4 && Geo<NW, KT, 4>::LDS <= LIM)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 4, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 4, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
   if (nb >= 3)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 3, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-  return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 2, HI_T>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 3, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 2, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
 }
 
 }  // namespace
@@ -497,12 +553,14 @@ SL_API int64_t sl_tsk_fused_workspace(int64_t m, int64_t n, int k) {
   const int KP = ((k + 15) / 16) * 16;
   const int NWP = n <= 512 ? 512 : 1024;
   const int64_t g = 256;  // upper bound on the grid
-  return g * (int64_t)NWP * KP * 4 + g * (int64_t)KP * KP * 4 + 256;
+  return g * (int64_t)NWP * KP * 4 + g * (int64_t)KP * KP * 8 + 256;  // G slab sized for f64
 }
 
 // flags: bit0 (1) skip the Gram G (G left untouched), bit1 (2) W from y_hi only
 // (bf16-rounded y: for intermediate power iterations, whose W is only
-// orthonormalised).  Default 0 = exact-f32-equivalent W and G.
+// orthonormalised), bit2 (4) G in f64 (G is a double*; exact products of the
+// f32 y accumulated in f64 — needs Y stored, i.e. the final pass).
+// Default 0 = exact-f32-equivalent W and G.
 SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k,
                              float* W, float* G, float* Y, int64_t ldy, void* ws, int flags, void* stream) {
   if (m <= 0) return SL_OK;
@@ -526,8 +584,14 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   const bool inter = (flags & 3) == 3 && !Y;
   // final pass whose Gram is taken separately (fp64 Gram of the stored Y)
   const bool nog = (flags & 3) == 1;
+  const bool g64 = (flags & 4) && !(flags & 3) && Y;
+  if ((flags & 4) && !g64) {
+    sl_set_last_error("tsk_fused_pass: the f64 Gram (flag 4) needs Y and flags & 3 == 0");
+    return SL_ERR_UNSUPPORTED;
+  }
 #define SL_TSK(NW, KTT)                                                                              \
-  rc = (Y && nog) ? launch_nb<NW, KTT, true, false, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+  rc = g64 ? launch_nb<NW, KTT, true, true, true, false, false, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
+     : (Y && nog) ? launch_nb<NW, KTT, true, false, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
      : Y ? launch_nb<NW, KTT, true, true, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
      : inter ? launch_nb<NW, KTT, true, false, false, false, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s) \
          : launch_nb<NW, KTT, true, true, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, s)
@@ -541,6 +605,7 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   if (rc != SL_OK) return rc;
   rc = sl_slab_reduce_launch(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k, s);
   if (rc != SL_OK || (flags & 1)) return rc;
+  if (g64) return sl_slab_reduce_launch_d2d((const double*)Gslab, g, (int64_t)KP * KP, KP, k, k, (double*)G, k, s);
   return sl_slab_reduce_launch(Gslab, g, (int64_t)KP * KP, KP, k, k, G, k, s);
 }
 

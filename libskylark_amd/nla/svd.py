@@ -265,7 +265,6 @@ class _DevicePlan:
         self.ws = torch.empty(T.fused_workspace_bytes(m, n, k), dtype=torch.uint8, device=dev)
         self.ws32 = torch.empty(max(T.f32_workspace_bytes(m), T.f32_workspace_bytes(n)), dtype=torch.uint8,
                                 device=dev)
-        self.ws64 = torch.empty(T.gram64_workspace_bytes(m, k), dtype=torch.uint8, device=dev)
         self.use_graph = use_graph
         self.g1 = self.g2 = None
         self.piece_graphs = None   # multi-rank: per-piece graphs (False: capture failed)
@@ -301,12 +300,12 @@ class _DevicePlan:
                 self._Wout[i], _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws)
             return self._Wout[i]
         with prof.phase("svd.fused_pass"):
-            W, _, Y = T.fused_pass(A, Z, keep_y=True, gram=False, exact=True, ws=self.ws)
+            # fp64 Gram of the f32 Y on the f64 matrix cores, formed inside the
+            # same pass (no second read of Y): one fp64 CholeskyQR then leaves
+            # Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2 with an
+            # f32 second Gram only reached ~eps32, at three times the work)
+            W, G, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True)
         with prof.phase("svd.final_qr"):
-            # fp64 Gram of the stored f32 Y (f64 matrix cores): one fp64 CholeskyQR
-            # then leaves Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2
-            # with an f32 second Gram only reached ~eps32, at three times the work)
-            G = T.gram64(Y, ws=self.ws64)
             self._WG = torch.cat([W.double(), G], 0)
         self.Y = Y
         return self._WG

@@ -67,7 +67,7 @@ _WS = FusedWorkspace()
 
 
 def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: bool = True,
-               exact: bool = True, ws: torch.Tensor | None = None):
+               exact: bool = True, ws: torch.Tensor | None = None, gram64: bool = False):
     """Return ``(W, G, Y)`` with ``Y = A Z``, ``W = A^T Y`` (n x k), ``G = Y^T Y`` (k x k).
 
     W and G are float32 (A bf16/fp32) or float64 (A fp64); Y is float32/64 or
@@ -75,11 +75,15 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
     ``gram=False`` skips G (returns None); ``exact=False`` lets the native
     kernel form W from bf16-rounded y (intermediate power iterations only
     orthonormalise W, so a 2^-9 relative perturbation is harmless there).
+    ``gram64=True`` (with ``keep_y`` and ``exact``) forms G from the f32 ``Y``
+    with f64 products and f64 accumulation inside the same pass (the fp64
+    Gram a CholeskyQR of an ill-conditioned ``Y`` needs; same numbers as
+    :func:`gram64` of the returned ``Y`` up to summation order).
     """
     m, n = A.shape
     k = Z.shape[1]
     if _native_ok(A, k):
-        return _fused_native(A, Z, keep_y, gram, exact, ws)
+        return _fused_native(A, Z, keep_y, gram, exact, ws, gram64)
     wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
     # low-precision A: Z is rounded to A's dtype (as the MFMA kernel does) and
     # the products are formed in f32
@@ -98,7 +102,7 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
                 W += Ab.t().float() @ (yh.float() + yl.float())
         else:
             W += torch.matmul(Ab.t().to(wdt), y)
-        G += (y.t() @ y).double()
+        G += (y.double().t() @ y.double()) if gram64 else (y.t() @ y).double()
         if keep_y:
             Ys.append(y)
     Y = torch.cat(Ys, 0) if keep_y and Ys else (torch.zeros(0, k, dtype=wdt, device=A.device) if keep_y else None)
@@ -114,19 +118,20 @@ def f32_workspace_bytes(m: int) -> int:
 
 
 def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool, gram: bool = True, exact: bool = True,
-                  ws: torch.Tensor | None = None):
+                  ws: torch.Tensor | None = None, gram64: bool = False):
     m, n = A.shape
     k = Z.shape[1]
     dev = A.device
     Zb = Z.t().to(torch.bfloat16).contiguous()  # Zt layout (k x n)
     W = torch.empty(n, k, dtype=torch.float32, device=dev)
-    G = torch.empty(k, k, dtype=torch.float32, device=dev)
+    g64 = bool(gram64 and gram and keep_y and exact)
+    G = torch.empty(k, k, dtype=torch.float64 if g64 else torch.float32, device=dev)
     Y = torch.empty(m, k, dtype=torch.float32, device=dev) if keep_y else None
     if ws is None:
         ws = _WS.get(dev, fused_workspace_bytes(m, n, k))
     _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zb), k, _lib.ptr(W), _lib.ptr(G),
               _lib.ptr(Y) if Y is not None else None, 0 if Y is None else Y.stride(0), _lib.ptr(ws),
-              (0 if gram else 1) | (0 if exact else 2), vp(_lib.stream_of(A)))
+              (0 if gram else 1) | (0 if exact else 2) | (4 if g64 else 0), vp(_lib.stream_of(A)))
     return W, (G.double() if gram else None), Y
 
 

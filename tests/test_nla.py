@@ -102,6 +102,25 @@ def test_fused_pass_native_shapes(dev, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(70001, 1000, 40), (4099, 512, 64), (1000, 72, 3), (17, 1024, 48), (33, 64, 16)])
+def test_fused_pass_native_gram64(dev, shape):
+    """In-pass f64 Gram of the stored f32 Y equals the f64 Gram of that Y
+    (exact f32 products, f64 sums) — the numbers the separate gram64 pass gave."""
+    m, n, k = shape
+    A = torch.randn(m, n, device=dev).to(torch.bfloat16)
+    Z = torch.randn(n, k, device=dev) / 30
+    W, G, Y = tallskinny.fused_pass(A, Z, keep_y=True, gram64=True)
+    assert G.dtype == torch.float64 and G.shape == (k, k)
+    Yd = Y.double()
+    Gr = Yd.t() @ Yd
+    torch.testing.assert_close(G, Gr, rtol=1e-12, atol=1e-12 * float(Gr.abs().max()))
+    torch.testing.assert_close(G, tallskinny.gram64(Y), rtol=1e-12, atol=1e-12 * float(Gr.abs().max()))
+    W0, _, Y0 = tallskinny.fused_pass(A, Z, keep_y=True, gram=False)
+    torch.testing.assert_close(W, W0, rtol=0, atol=0)
+    torch.testing.assert_close(Y, Y0, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("native", [False, True])
 def test_fused_pass_gpu_bf16(dev, native):
     old = tallskinny.USE_NATIVE
