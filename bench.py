@@ -1,16 +1,26 @@
 #!/usr/bin/env python
-"""Headline benchmark: FJLT-sketched randomized rank-20 SVD of a dense bf16
-1e6 x 1e3 matrix per GPU (BASELINE.json config 3: "FJLT + randomized rank-20
-SVD of 1e6x1e3 dense bf16"), one process per GPU, A row-distributed
-([VC,*]) over the N GPUs, RCCL all-reduces of the (n+k) x k pass results.
+"""Headline benchmark (BASELINE.json config 3): FJLT-sketched randomized
+rank-20 SVD (q = 2 power iterations) of a dense bf16 1e6 x 1e3 matrix held
+2-D block-cyclic ([MC,MR]) over the N GPUs of one node, one process per GPU,
+RCCL over xGMI.
 
-Scaling is WEAK: every GPU holds a 1e6 x 1e3 bf16 shard (2 GB), the global
-matrix is (N*1e6) x 1e3.  One "step" = one complete ``approximate_svd``
-(sketch + q=2 power iterations + final basis + small SVD), nothing cached
-between steps except the input matrix.
+Scaling is STRONG by default: the GLOBAL matrix is 1e6 x 1e3 for every N
+(1 GPU: a 1 x 1 grid; 8 GPUs: a 2 x 4 grid of 4096 x 128 tiles).  One
+"step" = one complete ``approximate_svd`` call on the [MC,MR] operand: the
+one all-to-all that brings it to row shards, the FJLT sketch, q = 2 fused
+power passes, the final basis pass, the small SVD and U returned in A's
+[MC,MR] layout.  Nothing is cached between steps except the input matrix
+and reusable workspaces.  ``--scaling weak`` times 1e6 rows PER GPU in
+[VC,*] instead; for N > 1 a short weak run is appended as a secondary key.
 
-metric value = aggregate sketch+apply throughput in GB/s = (bytes of the
-global A) / (randSVD wall-clock);  ms_per_step = randSVD wall-clock.
+The matrix is synthetic, planted low rank plus noise,
+    A = U0 diag(sigma) V0^T + eps E,  sigma_i = 1000 * 0.9^i (i < 20),
+every entry realised from its GLOBAL index by the Threefry kernel (so the
+matrix is the same for every N and layout).  After the timed loop the run
+checks the answer: orthogonality of U and ||A V - U S||_F / ||S||_F.
+
+metric value = (bytes of the global bf16 A) / (randSVD wall-clock)  [GB/s];
+ms_per_step  = randSVD wall-clock (max over ranks).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N > 1: torchrun --nproc-per-node N bench.py --gpus N ...)
@@ -19,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -26,6 +37,102 @@ import time
 import torch
 
 METRIC = "sketch+apply GB/s and randSVD wall-clock on 1e6×1e3 dense, 1/2/4/8 MI355X"
+PLANT_RANK = 20
+
+
+def planted_matrix(shape, layout, comm, dev, grid=None, block=None, seed=1234, eps=0.05):
+    """bf16 DistMatrix A = U0 diag(sigma) V0^T + eps E from global indices."""
+    from libskylark_amd.base import distributions as D
+    from libskylark_amd.ops import rng
+    from libskylark_amd.parallel.distmatrix import DistMatrix, _merge
+    m, n = shape
+    p = PLANT_RANK
+    A = DistMatrix.empty(shape, layout, comm, dtype=torch.bfloat16, device=dev, grid=grid, block=block)
+    sig = 1000.0 * 0.9 ** torch.arange(p, dtype=torch.float32, device=dev)
+    rows, cols = _merge(A.row_blocks()), _merge(A.col_blocks())
+    V0 = torch.empty(n, p, dtype=torch.float32, device=dev)
+    rng.fill_random(V0, D.Normal(), seed + 2, 0, ir=p, ic=1, scale=1.0 / math.sqrt(n))
+    ro = 0
+    for rs, re in rows:
+        for c0 in range(rs, re, 1 << 16):
+            c1 = min(re, c0 + (1 << 16))
+            U0 = torch.empty(c1 - c0, p, dtype=torch.float32, device=dev)
+            rng.fill_random(U0, D.Normal(), seed + 1, 0, r0=c0, ir=p, ic=1, scale=1.0 / math.sqrt(m))
+            co = 0
+            for cs, ce in cols:
+                T = torch.empty(c1 - c0, ce - cs, dtype=torch.float32, device=dev)
+                rng.fill_random(T, D.Normal(), seed, 0, r0=c0, c0=cs, ir=n, ic=1, scale=eps)
+                T.addmm_(U0 * sig, V0[cs:ce].t())
+                A.local[ro + c0 - rs: ro + c1 - rs, co: co + ce - cs].copy_(T)
+                co += ce - cs
+        ro += re - rs
+    return A
+
+
+def check_answer(A, U, s, V, comm):
+    """(max |U^T U - I|, ||A V - U S||_F / ||S||_F, sigma_1..3) with A, U distributed."""
+    Avc = A.redistribute("VC_STAR")
+    Uvc = U.redistribute("VC_STAR").local.double()
+    G = Uvc.t() @ Uvc
+    comm.all_reduce(G)
+    orth = float((G - torch.eye(G.shape[0], dtype=G.dtype, device=G.device)).abs().max())
+    R = Avc.local.float() @ V.float() - (Uvc * s.double()).float()
+    r2 = torch.tensor([float((R.double() ** 2).sum())], dtype=torch.float64, device=R.device)
+    comm.all_reduce(r2)
+    resid = math.sqrt(float(r2)) / float(s.double().norm())
+    return orth, resid
+
+
+def run(a, comm, dev, scaling):
+    import libskylark_amd as sk
+    from libskylark_amd.ops import tallskinny
+    from libskylark_amd.parallel.distmatrix import Grid
+    N = comm.size
+    n = a.cols
+    if scaling == "strong":
+        m = a.rows
+        layout = a.layout
+    else:
+        m = a.rows * N
+        layout = "VC_STAR"
+    grid = Grid.default(comm) if layout == "MC_MR" else None
+    block = (a.tile_rows, a.tile_cols) if layout == "MC_MR" else None
+    A = planted_matrix((m, n), layout, comm, dev, grid, block)
+    torch.cuda.synchronize()
+    params = sk.nla.ApproximateSVDParams(num_iterations=a.iters, sketch=a.sketch)
+
+    def step():
+        return sk.nla.approximate_svd(A, a.rank, context=sk.Context(seed=38734), params=params)
+
+    steps, warmup = (a.steps, a.warmup) if scaling == a.scaling else (max(3, a.steps // 2), 2)
+    for _ in range(warmup):
+        U, s, V = step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        U, s, V = step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    comm.all_reduce_max(t)
+    ms = float(t.item()) / steps * 1e3
+    orth, resid = check_answer(A, U, s, V, comm)
+    if grid is not None:
+        par = f"2-D block-cyclic [MC,MR] {grid.pr}x{grid.pc} grid, tile {block[0]}x{block[1]}, " \
+              f"one all-to-all to [VC,*] + RCCL all-reduces"
+    else:
+        par = f"dp{N} ([VC,*] row blocks, RCCL all-reduce)"
+    return {
+        "m": m, "n": n, "ms": ms, "gbs": m * n * 2 / (ms / 1e3) / 1e9, "steps": steps, "warmup": warmup,
+        "parallelism": par, "orth_err": orth, "resid_rel": resid,
+        "top_singular_values": [round(float(x), 3) for x in s[:3].tolist()],
+        "native_fused_pass": bool(tallskinny._native_ok(torch.empty(8, 8, dtype=torch.bfloat16, device=dev),
+                                                        2 * a.rank)),
+    }
 
 
 def main(argv=None):
@@ -33,19 +140,21 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
+    ap.add_argument("--rows", type=int, default=1_000_000, help="global rows (strong) / rows per GPU (weak)")
     ap.add_argument("--cols", type=int, default=1000)
     ap.add_argument("--rank", type=int, default=20)
     ap.add_argument("--iters", type=int, default=2, help="power iterations")
     ap.add_argument("--sketch", default="FJLT")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
+    ap.add_argument("--layout", default="MC_MR", help="layout of A for strong scaling")
+    ap.add_argument("--tile-rows", type=int, default=4096)
+    ap.add_argument("--tile-cols", type=int, default=128)
+    ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling run (N > 1)")
     ap.add_argument("--native", type=int, default=1, help="use the fused HIP pass kernel")
-    ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
-    import libskylark_amd as sk
-    from libskylark_amd.base import distributions as D
-    from libskylark_amd.ops import rng, tallskinny
-    from libskylark_amd.parallel import DistMatrix, init_distributed
+    from libskylark_amd.ops import tallskinny
+    from libskylark_amd.parallel import init_distributed
 
     tallskinny.USE_NATIVE = bool(a.native)
     if not torch.cuda.is_available():
@@ -56,62 +165,41 @@ def main(argv=None):
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     dev = torch.device("cuda", torch.cuda.current_device())
     N = comm.size
-    m_loc, n = a.rows, a.cols
-    m = m_loc * N
-
-    # synthetic input: Gaussian entries realised from GLOBAL indices (each GPU
-    # produces its own rows; identical to the single-GPU matrix for N = 1)
-    A_loc = torch.empty(m_loc, n, dtype=torch.bfloat16, device=dev)
-    rng.fill_random(A_loc, D.Normal(), seed=1234, base=0, r0=comm.rank * m_loc, c0=0, ir=n, ic=1)
-    A = DistMatrix(A_loc, (m, n), "VC_STAR", comm)
-    params = sk.nla.ApproximateSVDParams(num_iterations=a.iters, sketch=a.sketch)
-
-    def step():
-        ctx = sk.Context(seed=38734)
-        return sk.nla.approximate_svd(A, a.rank, context=ctx, params=params)
-
-    for _ in range(a.warmup):
-        U, s, V = step()
-    torch.cuda.synchronize()
-    comm.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        U, s, V = step()
-    torch.cuda.synchronize()
-    comm.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    comm.all_reduce_max(t)
-    dt = float(t.item())
-    ms = dt / a.steps * 1e3
-    a_bytes = m * n * 2
-    gbs = a_bytes / (ms / 1e3) / 1e9
+    res = run(a, comm, dev, a.scaling)
+    weak = None
+    if N > 1 and a.scaling == "strong" and not a.no_weak:
+        weak = run(a, comm, dev, "weak")
+    ok = res["orth_err"] < 1e-3 and res["resid_rel"] < 5e-2
     if comm.rank == 0:
         out = {
             "metric": METRIC,
-            "value": round(gbs, 2),
+            "value": round(res["gbs"], 2),
             "unit": "GB/s",
             "n_gpus": N,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms, 4),
+            "steps": res["steps"],
+            "warmup": res["warmup"],
+            "ms_per_step": round(res["ms"], 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (Gaussian bf16 matrix realised by the Threefry kernel; random-init sketch)",
+            "data": "synthetic planted rank-20 + Gaussian noise bf16 matrix (Threefry, global indices); "
+                    "random-init FJLT sketch",
             "config": {
-                "model": f"FJLT + randomized rank-{a.rank} SVD (q={a.iters}) of dense bf16 {m_loc}x{n} per GPU",
-                "global_batch": m,
-                "seq_len": n,
-                "parallelism": f"dp{N} ([VC,*] row blocks, RCCL all-reduce)",
+                "model": f"FJLT + randomized rank-{a.rank} SVD (q={a.iters}) of dense bf16 {res['m']}x{res['n']}",
+                "global_batch": res["m"],
+                "seq_len": res["n"],
+                "parallelism": res["parallelism"],
             },
-            "randsvd_ms": round(ms, 4),
-            "top_singular_values": [round(float(x), 3) for x in s[:3].tolist()],
-            "native_fused_pass": bool(tallskinny._native_ok(A_loc, 2 * a.rank)),
+            "randsvd_ms": round(res["ms"], 4),
+            "check": {"orth_err": res["orth_err"], "resid_rel": res["resid_rel"], "ok": ok},
+            "top_singular_values": res["top_singular_values"],
+            "native_fused_pass": res["native_fused_pass"],
         }
+        if weak is not None:
+            out["weak"] = {"value": round(weak["gbs"], 2), "ms_per_step": round(weak["ms"], 4),
+                           "global_rows": weak["m"], "steps": weak["steps"], "parallelism": weak["parallelism"],
+                           "check": {"orth_err": weak["orth_err"], "resid_rel": weak["resid_rel"]}}
         print(json.dumps(out))
         from libskylark_amd.utils.timer import PROFILER
         if PROFILER.enabled:
@@ -121,7 +209,7 @@ def main(argv=None):
     if N > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
-    return 0
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":

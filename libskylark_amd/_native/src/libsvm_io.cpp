@@ -21,7 +21,7 @@
 namespace {
 
 struct ChunkStats {
-  int64_t rows = 0, nnz = 0, maxidx = 0;
+  int64_t rows = 0, nnz = 0, maxidx = 0, bad = 0;  // bad: 1 + byte offset of a malformed line
 };
 
 inline const char* skip_ws(const char* p, const char* e) {
@@ -34,28 +34,63 @@ inline const char* line_end(const char* p, const char* e) {
   return q ? (const char*)q : e;
 }
 
-// Returns true if the line holds a data row.  Calls f(idx, val) per entry.
-template <typename F>
-inline bool parse_line(const char* p, const char* e, double* label, F&& f) {
-  p = skip_ws(p, e);
-  if (p >= e || *p == '#') return false;
+// Number parsing bounded by the line end: the mapped file is not
+// NUL-terminated, so strtod/strtoll run on a NUL-terminated copy of the token
+// (at most 63 chars) and can neither read past the mapping nor skip the
+// newline into the next line.
+inline const char* token_end(const char* p, const char* e, char stop) {
+  while (p < e && *p != ' ' && *p != '\t' && *p != '\r' && *p != '\n' && *p != stop) ++p;
+  return p;
+}
+
+inline bool parse_double(const char* p, const char* te, double* out) {
+  char tmp[64];
+  const size_t n = (size_t)(te - p);
+  if (n == 0 || n >= sizeof(tmp)) return false;
+  memcpy(tmp, p, n);
+  tmp[n] = 0;
   char* q;
-  const double lab = strtod(p, &q);
-  if (q == p) return false;
+  *out = strtod(tmp, &q);
+  return q == tmp + n;
+}
+
+inline bool parse_int(const char* p, const char* te, long long* out) {
+  char tmp[32];
+  const size_t n = (size_t)(te - p);
+  if (n == 0 || n >= sizeof(tmp)) return false;
+  memcpy(tmp, p, n);
+  tmp[n] = 0;
+  char* q;
+  *out = strtoll(tmp, &q, 10);
+  return q == tmp + n;
+}
+
+// Returns 1 if the line holds a data row, 0 if it is blank / a comment, and
+// -1 for a malformed entry (bad number, a missing value, index < 1).  Calls
+// f(idx, val) per entry.
+template <typename F>
+inline int parse_line(const char* p, const char* e, double* label, F&& f) {
+  p = skip_ws(p, e);
+  if (p >= e || *p == '#') return 0;
+  const char* te = token_end(p, e, 0);
+  double lab;
+  if (!parse_double(p, te, &lab)) return -1;
   if (label) *label = lab;
-  p = q;
+  p = te;
   while (true) {
     p = skip_ws(p, e);
     if (p >= e || *p == '#') break;
-    const long long idx = strtoll(p, &q, 10);
-    if (q == p || q >= e || *q != ':') break;
-    p = q + 1;
-    const double v = strtod(p, &q);
-    if (q == p) break;
-    p = q;
+    const char* ie = token_end(p, e, ':');
+    long long idx;
+    if (ie >= e || *ie != ':' || !parse_int(p, ie, &idx) || idx < 1) return -1;
+    p = ie + 1;
+    const char* ve = token_end(p, e, 0);
+    double v;
+    if (!parse_double(p, ve, &v)) return -1;
+    p = ve;
     f((int64_t)idx, v);
   }
-  return true;
+  return 1;
 }
 
 void split(const char* buf, int64_t len, int nthreads, std::vector<std::pair<int64_t, int64_t>>& ranges) {
@@ -106,17 +141,30 @@ SL_API int sl_libsvm_scan(const char* buf, int64_t len, int nthreads, int64_t* s
       ChunkStats s;
       while (p < e) {
         const char* le = line_end(p, e);
-        if (parse_line(p, le, nullptr, [&](int64_t idx, double) {
-              ++s.nnz;
-              if (idx > s.maxidx) s.maxidx = idx;
-            }))
-          ++s.rows;
+        const int r = parse_line(p, le, nullptr, [&](int64_t idx, double) {
+          ++s.nnz;
+          if (idx > s.maxidx) s.maxidx = idx;
+        });
+        if (r < 0) {
+          s.bad = (int64_t)(p - buf) + 1;
+          break;
+        }
+        s.rows += r;
         p = le + 1;
       }
       cs[c] = s;
     });
   }
   for (auto& t : th) t.join();
+  for (size_t c = 0; c < cs.size(); ++c) {
+    if (cs[c].bad) {
+      sl_set_last_error("LIBSVM: malformed entry (bad number, missing value or index < 1)");
+      stats[0] = stats[1] = stats[2] = 0;
+      stats[3] = cs[c].bad - 1;
+      *nchunks = 0;
+      return SL_ERR_INVALID;
+    }
+  }
   ChunkStats tot;
   for (size_t c = 0; c < cs.size(); ++c) {
     tot.rows += cs[c].rows;
@@ -159,7 +207,7 @@ SL_API int sl_libsvm_fill(const char* buf, const int64_t* ranges, const int64_t*
               cols[k] = idx - 1;
               vals[k] = v;
               ++k;
-            })) {
+            }) > 0) {
           labels[r] = lab;
           rowptr[r + 1] = k;
           ++r;

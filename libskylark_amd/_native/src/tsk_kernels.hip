@@ -105,7 +105,7 @@ struct Geo {
 };
 
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false>
+          bool G64 = false, bool X = false>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
@@ -209,9 +209,15 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
   const int64_t nloc = b0 < nblocks ? (nblocks - 1 - b0) / bstep + 1 : 0;
   for (int64_t blk = b0; blk < nblocks; blk += bstep, ++my) {
     const int buf = (int)(my % NBUF);
-    // blocks issued after this one and still possibly in flight: min(PD-1, remaining)
+    // X: the ring slots are private to the wave, so the next prefetch goes out
+    // at the top of the iteration (into the slot this wave finished with in the
+    // previous one) and PD blocks stay in flight throughout
+    if constexpr (X) {
+      if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
+    }
+    // blocks issued after this one and still possibly in flight
     const int64_t rem = nloc - 1 - my;
-    const int younger = (int)(rem < PD - 1 ? rem : PD - 1);
+    const int younger = X ? (int)(rem < PD ? rem : PD) : (int)(rem < PD - 1 ? rem : PD - 1);
     if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GG::LPB) : "memory");
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GG::LPB) : "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
@@ -280,7 +286,9 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     }
 
     // prefetch PD blocks ahead into the buffer this wave consumed last iteration
-    if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
+    if constexpr (!X) {
+      if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
+    }
 
     // y fragments with rows 4(l>>4)+j of column 16t+(l&15) (K=16 MFMA layout), hi/lo
     const bool hi_only = (ab & 32) != 0;
@@ -315,7 +323,62 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       if (!(HI)) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0); \
     }                                                                                                \
   }
-      if constexpr (HI_T) {
+      if constexpr (X) {
+        // one v_mfma_f32_16x16x32_bf16 per tile over K = [16 rows of y_hi ; the
+        // same 16 rows of y_lo] (the K = 16 form runs at half rate on gfx950):
+        // a lane reads 4 rows rb..rb+3 of the transposed A tile and of y, its
+        // partner lane (l ^ 32) supplies the other 4 (v_permlane32_swap);
+        // lanes 0-31 carry y_hi, lanes 32-63 y_lo.  Exact W at hi-only cost.
+        const bool low = lane < 32;
+        const int rb = 8 * (g4 & 1) + 4 * (g4 >> 1);
+        bf16x8 yb[KT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const f32x4 v = *(const f32x4*)&yf[(16 * t + i16) * BM + rb];
+          f32x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v[j]),
+                                                            __builtin_bit_cast(unsigned, v[j]), false, false);
+            o[j] = __builtin_bit_cast(float, low ? r[1] : r[0]);
+          }
+          s16x8 e;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float r03 = low ? v[j] : o[j], r47 = low ? o[j] : v[j];
+            const short h0 = bf16_bits(r03), h1 = bf16_bits(r47);
+            e[j] = low ? h0 : bf16_bits(r03 - bf16_val(h0));
+            e[4 + j] = low ? h1 : bf16_bits(r47 - bf16_val(h1));
+          }
+          yb[t] = __builtin_bit_cast(bf16x8, e);
+        }
+        const int trow = rb + q;
+#pragma unroll
+        for (int ct = 0; ct < NW / 16; ++ct) {
+          const int chunk = 2 * ct + (p >> 1);
+          const char* addr = region + trow * GG::ROWB + (chunk ^ (trow & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
+          typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+          const u32x2 u = __builtin_bit_cast(u32x2, a4);
+          u32x2 uo;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const auto r = __builtin_amdgcn_permlane32_swap(u[j], u[j], false, false);
+            uo[j] = low ? r[1] : r[0];
+          }
+          const s16x4 b4 = __builtin_bit_cast(s16x4, uo);
+          s16x8 a8;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a8[j] = low ? a4[j] : b4[j];
+            a8[4 + j] = low ? b4[j] : a4[j];
+          }
+          const bf16x8 af8 = __builtin_bit_cast(bf16x8, a8);
+#pragma unroll
+          for (int t = 0; t < KT; ++t)
+            accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yb[t], accW[ct][t], 0, 0, 0);
+        }
+      } else if constexpr (HI_T) {
         SL_STEP3(true)
       } else {
         SL_STEP3(hi_only)
@@ -491,12 +554,14 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
+int g_x = -1;  // 1: top-of-loop prefetch + K = 32 hi/lo step 3 (SL_TSK_X), 0: original
+
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false>
-int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
+          bool G64 = false, bool X = false>
+int launch_x(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   using GG = Geo<NW, KT, NBUF>;
-  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64>;
+  auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, X>;
   static bool attr = false;
   if (!attr) {
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
@@ -505,6 +570,22 @@ int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int
   kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, g_ablate | g_flags);
   SL_LAUNCH_CHECK();
   return SL_OK;
+}
+
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
+          bool G64 = false>
+int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
+           float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
+  if (g_x < 0) {
+    const char* e = getenv("SL_TSK_X");
+    g_x = e ? atoi(e) : 0;
+  }
+  // the K = 32 step 3 needs the W update (DO_W) and a non-split Z
+  if constexpr (DO_W && !ZSPLIT && KT <= 3) {
+    if (g_x == 1)
+      return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, true>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  }
+  return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, false>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
 }
 
 // buffer depth: SL_TSK_NBUF env (A/B tuning), default NBUF_DEFAULT, clamped to the LDS budget
@@ -536,6 +617,11 @@ int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, 
 }
 
 }  // namespace
+
+SL_API int sl_tsk_set_x(int x) {
+  g_x = x;
+  return SL_OK;
+}
 
 SL_API int sl_tsk_set_ablate(int ab) {
   g_ablate = ab;

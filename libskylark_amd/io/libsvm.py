@@ -56,7 +56,7 @@ def _parse(addr: int, start: int, end: int, max_n: int = -1):
     if end <= start:
         z = np.zeros(0, dtype=np.int64)
         return np.zeros(0), np.zeros(1, dtype=np.int64), z, np.zeros(0), 0
-    stats = np.zeros(3, dtype=np.int64)
+    stats = np.zeros(4, dtype=np.int64)
     ranges = np.zeros(2 * _NTHREADS, dtype=np.int64)
     counts = np.zeros(2 * _NTHREADS, dtype=np.int64)
     nch = np.zeros(1, dtype=np.int32)
@@ -77,7 +77,7 @@ def _parse(addr: int, start: int, end: int, max_n: int = -1):
 def _to_tensor(labels, rowptr, cols, vals, d, sparse, dtype, device):
     n = len(labels)
     X = torch.sparse_csr_tensor(torch.from_numpy(rowptr), torch.from_numpy(cols), torch.from_numpy(vals).to(dtype),
-                                (n, d))
+                                (n, d), check_invariants=True)
     if not sparse:
         X = X.to_dense()
     if device is not None:

@@ -89,10 +89,16 @@ class LineStreamer:
         if len(self._buf) <= target:
             cut = len(self._buf)
             if self._buf[-1:] != b"\n":
-                # keep reading until the current line ends (or the file does)
-                while self._buf[-1:] != b"\n" and self._fill():
-                    pass
-                cut = len(self._buf)
+                # keep reading until the current line ends (or the file does):
+                # search each newly read piece for the first newline and cut
+                # there, so block_bytes keeps bounding memory
+                i = -1
+                while i < 0:
+                    old = len(self._buf)
+                    if not self._fill():
+                        break
+                    i = self._buf.find(b"\n", old)
+                cut = len(self._buf) if i < 0 else i + 1
         else:
             cut = self._buf.rfind(b"\n", 0, target) + 1
             if cut == 0:

@@ -82,13 +82,41 @@ def _sketch_operator(kind: str, n: int, k: int, ctx: Context, device, dtype) -> 
     return sk.realize(dtype=torch.float64, device=device).t().to(dtype).contiguous()
 
 
+_ROWBUF: dict = {}
+
+
 def _as_rowdist(A):
-    """(local row shard tensor, comm, m_global, reassemble-info)."""
+    """(local row shard tensor, comm, m_global, DistMatrix or None).
+
+    A non-row-distributed DistMatrix (e.g. ``[MC,MR]``) is redistributed to
+    ``[VC,*]`` by one all-to-all into a persistent per-geometry buffer, so
+    repeated calls on the same operand keep a stable shard address (the
+    device plan and its graphs stay valid) and allocate nothing."""
     if isinstance(A, DistMatrix):
         if A.layout not in ("VC_STAR", "VR_STAR"):
-            A = A.redistribute("VC_STAR")
+            key = (A.layout, A.shape, A.block, None if A.grid is None else (A.grid.pr, A.grid.pc),
+                   A.comm.rank, A.comm.size, id(A.comm.group), A.local.dtype, str(A.local.device))
+            buf = _ROWBUF.get(key)
+            with PROFILER.phase("svd.redistribute"):
+                R = A.redistribute("VC_STAR", out=buf)
+            if buf is None:
+                if len(_ROWBUF) >= 2:
+                    _ROWBUF.pop(next(iter(_ROWBUF)))
+                _ROWBUF[key] = R.local
+            A = R
         return A.local, A.comm, A.shape[0], A
-    return A, Comm(None) if False else _LocalComm(), A.shape[0], None
+    return A, _LocalComm(), A.shape[0], None
+
+
+def _u_like(U_loc, m, rank, comm, Ad, A):
+    """U as a DistMatrix in A's layout (the reference's UType follows A's
+    type, nla/svd.hpp:222); computed row-distributed, moved by one
+    all-to-all of the m x rank factor when A is 2-D."""
+    U = DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm)
+    if isinstance(A, DistMatrix) and A.layout not in ("VC_STAR", "VR_STAR"):
+        with PROFILER.phase("svd.redistribute"):
+            U = U.redistribute(A.layout, A.grid, A.block if A.layout == "MC_MR" else None)
+    return U
 
 
 class _LocalComm(Comm):
@@ -124,13 +152,19 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     if rank > min(m, n):
         raise InvalidParametersError(f"Incompatible matrix dimensions ({min(m, n)}) and target rank ({rank})")
     if m < n:
-        # wide: work on A^T (tall) and swap the factors
+        # wide (reference's m < n branch, nla/svd.hpp:287-317): work on the
+        # tall A^T and swap the factors.  For a DistMatrix, U (m x rank, from
+        # the replicated right factor of A^T) is sliced into A's layout with no
+        # communication and V (n x rank) is gathered to every rank like the
+        # tall case's V.
         At = _transpose(A)
-        U, s, V = approximate_svd(At, rank, ctx, params)
+        Ut, s, Vt = approximate_svd(At, rank, ctx, params)
         if isinstance(A, DistMatrix):
-            return _dist_like_cols(V, A), s, (U.to_global() if isinstance(U, DistMatrix) else U)
-        return V, s, U
+            U = DistMatrix.from_global(Vt, A.layout, A.comm, A.grid, A.block if A.layout == "MC_MR" else None)
+            return U, s, Ut.to_global()
+        return Vt, s, Ut
     k = max(rank, min(n, params.oversampling_ratio * rank + params.oversampling_additive))
+    A_in = A
     A_loc, comm, _, Ad = _as_rowdist(A)
     dev = A_loc.device
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
@@ -141,9 +175,8 @@ def approximate_svd(A, rank: int, context: Context | None = None,
         if res is not None:
             U_loc, s, V = res
             if Ad is not None:
-                return DistMatrix(U_loc, (m, rank), "VC_STAR", comm), s, V
+                return _u_like(U_loc, m, rank, comm, Ad, A_in), s, V
             return U_loc, s, V
-        ctx = res_ctx_restore(ctx)
     prof = PROFILER
     with prof.phase("svd.sketch"):
         Zh = _sketch_operator(params.sketch, n, k, ctx, "cpu", torch.float64).numpy()
@@ -187,7 +220,7 @@ def approximate_svd(A, rank: int, context: Context | None = None,
         s = torch.from_numpy(s[:rank].copy()).to(dev, work)
         V = torch.from_numpy(np.ascontiguousarray((Qv @ Ur)[:, :rank])).to(dev, work)
         if Ad is not None:
-            return DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm), s, V
+            return _u_like(U_loc, m, rank, comm, Ad, A_in), s, V
         return U_loc, s, V
     Rt = R1
     with prof.phase("svd.final_qr"):
@@ -218,13 +251,8 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     s = torch.from_numpy(s[:rank].copy()).to(dev, work)
     V = torch.from_numpy(np.ascontiguousarray(Vv[:, :rank])).to(dev, work)
     if Ad is not None:
-        U = DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm)
-        return U, s, V
+        return _u_like(U_loc, m, rank, comm, Ad, A_in), s, V
     return U_loc, s, V
-
-
-def res_ctx_restore(ctx):
-    return ctx
 
 
 class _DevicePlan:
@@ -566,10 +594,6 @@ def _transpose(A):
     return A.t()
 
 
-def _dist_like_cols(V, A):
-    return V
-
-
 # ------------------------------------------------------------ power iteration
 def power_iteration(A, V: torch.Tensor, iternum: int, ortho: bool = True, comm: Comm | None = None):
     """``V <- (A^T A)^iternum V`` with optional re-orthonormalisation
@@ -589,40 +613,115 @@ def power_iteration(A, V: torch.Tensor, iternum: int, ortho: bool = True, comm: 
     return U, V
 
 
-def approximate_symmetric_svd(A: torch.Tensor, rank: int, context: Context | None = None,
+def _symm_operator(A, uplo: str, work, comm):
+    """``X -> A X`` for a symmetric A of which only the ``uplo`` triangle is
+    read (reference ``base::Symm(El::LEFT, uplo, ...)``, base/Symm.hpp; the
+    other triangle may hold anything).
+
+    * dense local: the full symmetric matrix is formed once from the triangle;
+    * sparse CSR local: entries outside the triangle are dropped, the rest
+      mirrored (diagonal once);
+    * row-distributed DistMatrix (any layout, redistributed to ``[VC,*]``):
+      ``A X = T X + T^T X - D X`` with T the local rows of the triangle; the
+      ``T^T X`` part is a partial n x k product on every rank combined by ONE
+      reduce-scatter onto the row distribution.  X and the result are
+      row-distributed (local rows)."""
+    lower = str(uplo).upper().startswith("L")
+    if isinstance(A, DistMatrix):
+        D = A if A.layout in ("VC_STAR", "VR_STAR") else A.redistribute("VC_STAR")
+        r0, r1 = D.row_range()
+        n = D.shape[1]
+        loc = D.local.to(work)
+        rows = torch.arange(r0, r1, device=loc.device)[:, None]
+        cols = torch.arange(n, device=loc.device)[None, :]
+        T = torch.where((cols <= rows) if lower else (cols >= rows), loc, torch.zeros((), dtype=work, device=loc.device))
+        diag = loc[torch.arange(r1 - r0, device=loc.device), torch.arange(r0, r1, device=loc.device)] if r1 > r0 else \
+            torch.zeros(0, dtype=work, device=loc.device)
+        counts = D.row_counts()
+
+        def mv(Xloc):
+            Xfull = D.comm.all_gather_v(Xloc.contiguous(), counts, 0)     # n x k replicated
+            part = T.t() @ Xloc                                             # n x k partial
+            Tt = D.comm.reduce_scatter_v(part, counts, 0)                   # my rows of T^T X
+            return T @ Xfull + Tt - diag[:, None] * Xloc
+        return mv, (r0, r1), D
+    if A.layout != torch.strided:
+        Acoo = A.to_sparse_coo().coalesce() if A.layout != torch.sparse_coo else A.coalesce()
+        i, j = Acoo.indices()
+        v = Acoo.values().to(work)
+        keep = (i >= j) if lower else (i <= j)
+        i, j, v = i[keep], j[keep], v[keep]
+        off = i != j
+        I = torch.cat([i, j[off]])
+        J = torch.cat([j, i[off]])
+        V = torch.cat([v, v[off]])
+        S = torch.sparse_coo_tensor(torch.stack([I, J]), V, A.shape).coalesce().to_sparse_csr()
+        return (lambda X: torch.sparse.mm(S, X)), None, None
+    Aw = A.to(work)
+    T = torch.tril(Aw) if lower else torch.triu(Aw)
+    S = T + T.t() - torch.diag(torch.diagonal(Aw))
+    return (lambda X: S @ X), None, None
+
+
+def approximate_symmetric_svd(A, rank: int, context: Context | None = None,
                               params: ApproximateSVDParams | None = None, uplo: str = "L"):
-    """Approximate eigendecomposition of a symmetric matrix (reference ``:321-392``):
-    Gaussian Omega, power iterations, Rayleigh-Ritz with a symmetric eigensolver
-    (descending).  Returns ``(V, s)``.  ``A`` may be dense or sparse (CSR)."""
+    """Approximate eigendecomposition of a symmetric matrix (reference
+    ``ApproximateSymmetricSVD``, ``nla/svd.hpp:321-392``): Gaussian Omega
+    (``base::GaussianMatrix``), ``Symm`` power iterations, Rayleigh-Ritz with a
+    symmetric eigensolver sorted by SIGNED value, descending (El::DESCENDING).
+    Only the ``uplo`` ("L"/"U") triangle of A is read.
+
+    ``A``: dense tensor, sparse CSR/COO tensor, or a DistMatrix (row-sharded
+    work, replicated k x k Rayleigh-Ritz).  Returns ``(V, s)``; V is a
+    ``[VC,*]`` DistMatrix when A is distributed."""
     from .. import default_context
     from ..base import distributions as D
     from ..ops import rng
     ctx = context if context is not None else default_context()
     params = params or ApproximateSVDParams()
+    if A.shape[0] != A.shape[1]:
+        raise InvalidParametersError(f"Matrix is not square ({A.shape[0]} x {A.shape[1]}) -- symmetric matrix required")
     n = A.shape[0]
+    if rank > n:
+        raise InvalidParametersError(f"Incompatible matrix dimensions ({n}) and target rank ({rank}).")
     k = max(rank, min(n, params.oversampling_ratio * rank + params.oversampling_additive))
-    dev = A.device
-    work = torch.float64 if (A.dtype == torch.float64 or (A.is_sparse_csr and A.values().dtype == torch.float64)) else torch.float32
+    if isinstance(A, DistMatrix):
+        dtype, dev = A.local.dtype, A.local.device
+    else:
+        dtype = A.values().dtype if A.layout != torch.strided else A.dtype
+        dev = A.device
+    work = torch.float64 if dtype == torch.float64 else torch.float32
+    comm = A.comm if isinstance(A, DistMatrix) else _LocalComm()
+    mv, rr, Dm = _symm_operator(A, uplo, work, comm)
+    r0, r1 = rr if rr is not None else (0, n)
+    # Omega: global-index Gaussian (identical for every layout / rank count)
     arr = ctx.allocate_random_samples_array(n * k, D.Normal())
-    V = torch.empty(n, k, dtype=work, device=dev)
-    rng.fill_random(V, D.Normal(), arr.seed, arr.base, ir=1, ic=n)
+    Om = torch.empty(r1 - r0, k, dtype=work, device=dev)
+    rng.fill_random(Om, D.Normal(), arr.seed, arr.base, r0=r0, c0=0, ir=1, ic=n)
 
-    def mv(X):
-        if A.layout != torch.strided:
-            return torch.sparse.mm(A.to(work) if A.values().dtype != work else A, X)
-        return A.to(work) @ X
+    def orth(X):
+        if Dm is None:
+            return torch.linalg.qr(X, mode="reduced")[0]
+        return L.orthonormalize(X, comm, method="tsqr")
 
-    U = mv(V)
+    V = mv(Om)
     for _ in range(params.num_iterations):
         if not params.skip_qr:
-            U, _ = torch.linalg.qr(U, mode="reduced")
-        U = mv(U)
-    Q, _ = torch.linalg.qr(U, mode="reduced")
-    B = Q.t() @ mv(Q)
+            V = orth(V)
+        V = mv(V)
+    Q = orth(V)
+    U = mv(Q)
+    B = Q.t() @ U
+    if Dm is not None:
+        comm.all_reduce(B)
     B = 0.5 * (B + B.t())
     w, E = torch.linalg.eigh(B.double())
-    order = torch.argsort(w.abs(), descending=True)[:rank]
-    return (Q.double() @ E[:, order]).to(work), w[order].to(work)
+    order = torch.argsort(w, descending=True)[:rank]
+    Vr = (Q.double() @ E[:, order].to(Q.device)).to(work)
+    s = w[order].to(device=dev, dtype=work)
+    if Dm is not None:
+        return DistMatrix(Vr.contiguous(), (n, rank), "VC_STAR", comm), s
+    return Vr, s
 
 
 ApproximateSVD = approximate_svd

@@ -49,12 +49,14 @@ class Comm:
             self._active = self.size > 1
         else:
             self.rank, self.size, self.backend, self._active = 0, 1, None, False
+        self.bytes_sent = 0   # payload bytes this rank put on the wire (diagnostics, tests)
 
     @classmethod
     def single(cls) -> "Comm":
         """A one-rank communicator that never communicates (process-local data)."""
         c = cls.__new__(cls)
         c.group, c.rank, c.size, c.backend, c._active = None, 0, 1, None, False
+        c.bytes_sent = 0
         return c
 
     @property
@@ -68,12 +70,24 @@ class Comm:
             return torch.device("cuda", torch.cuda.current_device())
         return torch.device("cpu")
 
-    def _ready(self, t):
-        return t
+    # Every collective stages its operands onto collective_device() and hands
+    # results back on the caller's device, so host tensors may be passed on
+    # an RCCL communicator (IO paths build their buffers on the host) and GPU
+    # tensors on a gloo one (multi-rank rehearsals on one GPU).
+    def _stage(self, t: torch.Tensor) -> torch.Tensor:
+        dev = self.collective_device()
+        return t if t.device == dev else t.to(dev)
+
+    def _count(self, nbytes: int):
+        self.bytes_sent = getattr(self, "bytes_sent", 0) + int(nbytes)
 
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM if dist.is_available() else None):
         if self._active:
-            dist.all_reduce(t, op=op, group=self.group)
+            st = self._stage(t)
+            dist.all_reduce(st, op=op, group=self.group)
+            if st is not t:
+                t.copy_(st)
+            self._count(2 * t.numel() * t.element_size() * (self.size - 1) // self.size)
         return t
 
     def all_reduce_max(self, t):
@@ -84,87 +98,108 @@ class Comm:
 
     def reduce(self, t: torch.Tensor, root: int = 0):
         if self._active:
-            dist.reduce(t, dst=self.global_rank(root), group=self.group)
+            st = self._stage(t)
+            dist.reduce(st, dst=self.global_rank(root), group=self.group)
+            if st is not t and self.rank == root:
+                t.copy_(st)
         return t
 
     def broadcast(self, t: torch.Tensor, root: int = 0):
         if self._active:
-            dist.broadcast(t, src=self.global_rank(root), group=self.group)
+            st = self._stage(t)
+            dist.broadcast(st, src=self.global_rank(root), group=self.group)
+            if st is not t:
+                t.copy_(st)
+            if self.rank == root:
+                self._count(t.numel() * t.element_size())
         return t
 
     def all_gather(self, t: torch.Tensor, dim: int = 0) -> torch.Tensor:
         """Concatenate equal-shaped shards along ``dim``."""
         if not self._active:
             return t
-        t = t.contiguous()
-        if dim == 0:
-            out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-            dist.all_gather_into_tensor(out, t, group=self.group)
-            return out
-        parts = [torch.empty_like(t) for _ in range(self.size)]
-        dist.all_gather(parts, t, group=self.group)
-        return torch.cat(parts, dim)
+        src_dev = t.device
+        t = self._stage(t).contiguous()
+        if dim != 0:
+            t = t.movedim(dim, 0).contiguous()
+        out = torch.empty((self.size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        self._count(t.numel() * t.element_size() * (self.size - 1))
+        if dim != 0:
+            out = out.view((self.size, t.shape[0]) + tuple(t.shape[1:]))
+            out = torch.cat(list(out.unbind(0)), 0).movedim(0, dim)
+        return out.to(src_dev)
 
     def all_gather_v(self, t: torch.Tensor, counts, dim: int = 0) -> torch.Tensor:
         """All-gather shards of unequal size along ``dim`` (counts per rank)."""
         if not self._active:
             return t
         mx = max(counts)
-        pad = list(t.shape)
-        pad[dim] = mx
-        buf = torch.zeros(pad, dtype=t.dtype, device=t.device)
-        buf.narrow(dim, 0, t.shape[dim]).copy_(t)
-        g = self.all_gather(buf.movedim(dim, 0).contiguous(), 0)
+        tt = t.movedim(dim, 0)
+        if all(c == mx for c in counts):
+            return self.all_gather(tt.contiguous(), 0).movedim(0, dim)
+        buf = torch.zeros((mx,) + tuple(tt.shape[1:]), dtype=t.dtype, device=t.device)
+        buf[: tt.shape[0]].copy_(tt)
+        g = self.all_gather(buf, 0)
         g = g.view((self.size, mx) + tuple(g.shape[1:]))
         parts = [g[r, :counts[r]] for r in range(self.size)]
         return torch.cat(parts, 0).movedim(0, dim)
 
     def reduce_scatter_v(self, t: torch.Tensor, counts, dim: int = 0) -> torch.Tensor:
-        """Sum ``t`` over ranks and keep this rank's slice (counts along dim)."""
+        """Sum ``t`` over ranks and keep this rank's slice (counts along dim).
+
+        Unequal counts are padded to the largest one and reduced with ONE
+        reduce-scatter (never an all-reduce of the whole operand)."""
         if not self._active:
             return t
         if dim != 0:
             return self.reduce_scatter_v(t.movedim(dim, 0).contiguous(), counts, 0).movedim(0, dim)
+        src_dev = t.device
+        t = self._stage(t)
         mx = max(counts)
-        if all(c == mx for c in counts) and self.backend == "nccl":
-            out = torch.empty((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-            dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
-            return out
-        # general path: all-reduce and slice (gloo has no reduce_scatter)
-        tt = t.contiguous().clone()
-        self.all_reduce(tt)
-        off = sum(counts[: self.rank])
-        return tt[off: off + counts[self.rank]].contiguous()
-
-    def all_to_all_v(self, sends: list[torch.Tensor]) -> list[torch.Tensor]:
-        """Exchange a list of per-destination tensors (any shapes with equal trailing dims)."""
-        if not self._active:
-            return sends
-        # exchange sizes first
-        dev = sends[0].device
-        sz = torch.tensor([s.shape[0] for s in sends], dtype=torch.int64, device=dev)
-        rsz = torch.empty_like(sz)
-        allsz = None
-        if self.backend == "gloo":
-            allsz = self.all_gather(sz.view(1, -1), 0)
-            rsz = allsz[:, self.rank].contiguous()
+        tail = tuple(t.shape[1:])
+        if all(c == mx for c in counts):
+            buf = t.contiguous()
         else:
-            dist.all_to_all_single(rsz, sz, group=self.group)
-        rs = [int(x) for x in rsz.tolist()]
+            buf = torch.zeros((self.size * mx,) + tail, dtype=t.dtype, device=t.device)
+            off = 0
+            for r, c in enumerate(counts):
+                buf[r * mx: r * mx + c].copy_(t[off: off + c])
+                off += c
+        out = torch.empty((mx,) + tail, dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, buf, group=self.group)
+        self._count(buf.numel() * buf.element_size() * (self.size - 1) // self.size)
+        return out[: counts[self.rank]].to(src_dev)
+
+    def all_to_all_v(self, sends: list[torch.Tensor], recv_counts=None) -> list[torch.Tensor]:
+        """Exchange per-destination tensors (equal trailing dims): ``sends[d]``
+        goes to rank d; returns the list of pieces received from each rank.
+
+        One ``all_to_all_single`` with split sizes (RCCL and gloo alike);
+        ``recv_counts`` (rows from every source) skips the size exchange when
+        the caller already knows the geometry."""
+        if not self._active:
+            return list(sends)
+        src_dev = sends[0].device
+        dt = sends[0].dtype
         tail = tuple(sends[0].shape[1:])
-        recvs = [torch.empty((n,) + tail, dtype=sends[0].dtype, device=dev) for n in rs]
-        if self.backend == "gloo":
-            # gloo lacks all_to_all: emulate with an all-gather of padded buffers
-            mx = max(int(allsz.max()), 1)  # same padded size on every rank
-            buf = torch.zeros((self.size, mx) + tail, dtype=sends[0].dtype, device=dev)
-            for i, s in enumerate(sends):
-                buf[i, : s.shape[0]] = s
-            allb = self.all_gather(buf.view((1,) + tuple(buf.shape)), 0)
-            for src in range(self.size):
-                recvs[src].copy_(allb[src, self.rank, : rs[src]])
-            return recvs
-        dist.all_to_all([r.contiguous() for r in recvs], [s.contiguous() for s in sends], group=self.group)
-        return recvs
+        row = 1
+        for x in tail:
+            row *= int(x)
+        dev = self.collective_device()
+        send_counts = [int(s.shape[0]) for s in sends]
+        if recv_counts is None:
+            sz = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+            rsz = torch.empty_like(sz)
+            dist.all_to_all_single(rsz, sz, group=self.group)
+            recv_counts = [int(x) for x in rsz.tolist()]
+        flat = torch.cat([s.reshape(-1).to(dev) for s in sends]) if sends else torch.empty(0, dtype=dt, device=dev)
+        out = torch.empty(sum(recv_counts) * row, dtype=dt, device=dev)
+        dist.all_to_all_single(out, flat, [c * row for c in recv_counts], [c * row for c in send_counts],
+                               group=self.group)
+        self._count((flat.numel() - send_counts[self.rank] * row) * flat.element_size())
+        pieces = torch.split(out, [c * row for c in recv_counts])
+        return [p.view((c,) + tail).to(src_dev) for p, c in zip(pieces, recv_counts)]
 
     def barrier(self):
         if self._active:

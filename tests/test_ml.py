@@ -348,3 +348,21 @@ def test_read_dir_libsvm_distributed(tmp_path):
     for i in range(3):
         (tmp_path / f"f{i}").write_text("".join(f"{i + j} {j + 1}:{float(i * 10 + j)}\n" for j in range(1 + i)))
     run_distributed(_dir_worker, 2, str(tmp_path))
+
+
+def test_libsvm_parser_bounds(tmp_path):
+    """The parser stays inside each line and the mapping: no trailing newline
+    at EOF, an empty value must not swallow the next line's label, and a
+    0 (or negative) feature index is rejected instead of becoming column -1."""
+    from libskylark_amd.io import read_libsvm
+    from libskylark_amd.ops._lib import NativeLibraryError
+    p = tmp_path / "noeol.svm"
+    p.write_bytes(b"1 1:0.5 3:2\n-1 2:1.25")   # last line has no newline
+    X, Y = read_libsvm(str(p))
+    assert Y.tolist() == [1.0, -1.0]
+    assert X.tolist() == [[0.5, 0.0, 2.0], [0.0, 1.25, 0.0]]
+    for bad in (b"1 0:1.0\n", b"1 2:\n-1 1:1\n", b"1 -3:1\n", b"1 x:1\n"):
+        q = tmp_path / "bad.svm"
+        q.write_bytes(bad)
+        with pytest.raises((NativeLibraryError, RuntimeError, ValueError)):
+            read_libsvm(str(q))

@@ -58,6 +58,35 @@ def test_symmetric_svd():
     torch.testing.assert_close(w, (s0[:6] ** 2), rtol=1e-3, atol=1e-6)
 
 
+def _indefinite(n, spec):
+    g = torch.Generator().manual_seed(11)
+    Q, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    return (Q * torch.tensor(spec, dtype=torch.float64)) @ Q.t()
+
+
+@pytest.mark.parametrize("uplo", ["L", "U"])
+def test_symmetric_svd_reads_one_triangle(uplo):
+    """Only the uplo triangle is read (the other holds garbage); eigenvalues are
+    ordered by signed value, descending (reference El::DESCENDING)."""
+    n = 120
+    spec = [50.0, -45.0, 30.0, -20.0, 10.0] + [1e-3] * (n - 5)
+    S = _indefinite(n, spec)
+    junk = torch.randn(n, n, dtype=torch.float64) * 100
+    A = torch.tril(S) + torch.triu(junk, 1) if uplo == "L" else torch.triu(S) + torch.tril(junk, -1)
+    V, w = sk.nla.approximate_symmetric_svd(A, 5, context=sk.Context(4),
+                                            params=sk.nla.ApproximateSVDParams(num_iterations=3), uplo=uplo)
+    # the 2 r = 10 Ritz values hold the 5 dominant |lambda|; sorted by signed
+    # value the top 5 are 50, 30, 10 and two from the 1e-3 cluster
+    torch.testing.assert_close(w[:3], torch.tensor([50.0, 30.0, 10.0], dtype=torch.float64), rtol=1e-6, atol=1e-6)
+    assert (w[3:] - 1e-3).abs().max() < 1e-4
+    # eigenvectors of the full symmetric matrix
+    torch.testing.assert_close(S @ V[:, :3], V[:, :3] * w[:3], rtol=1e-6, atol=1e-5)
+    # sparse input, same triangle semantics
+    Vs, ws = sk.nla.approximate_symmetric_svd(A.to_sparse_csr(), 5, context=sk.Context(4),
+                                              params=sk.nla.ApproximateSVDParams(num_iterations=3), uplo=uplo)
+    torch.testing.assert_close(ws, w, rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.gpu
 def test_approximate_svd_gpu_bf16(dev):
     A, s0 = _lowrank(20000, 256, 12, decay=0.7)
