@@ -85,15 +85,24 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 #undef SL_VMW
 
-// value of x held by lane (l ^ 32)
+// value of x held by lane (l ^ 32).  Inline asm on purpose: hipcc (ROCm 7.2)
+// merged several __builtin_amdgcn_permlane32_swap(x, x) calls on DIFFERENT x
+// into one swap (tsk3 .s: one v_permlane32_swap feeding four selects) -- the real
+// cause was the element bit_cast below, the asm form is kept anyway.  The s_nop covers the VALU-write -> permlane hazard.
 __device__ __forceinline__ unsigned partner32(unsigned x, bool low) {
-  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  return low ? r[1] : r[0];
+  unsigned a = x, b = x;
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return low ? b : a;
 }
 __device__ __forceinline__ f32x4 partner32(f32x4 v, bool low) {
   f32x4 o;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = __builtin_bit_cast(float, partner32(__builtin_bit_cast(unsigned, v[j]), low));
+  for (int j = 0; j < 4; ++j) {
+            // scalar copy first: clang's __builtin_bit_cast of an ext_vector ELEMENT
+            // lvalue reads element 0 (ROCm 7.2), which silently broke this swap
+            const float e = v[j];
+            o[j] = __builtin_bit_cast(float, partner32(__builtin_bit_cast(unsigned, e), low));
+          }
   return o;
 }
 __device__ __forceinline__ s16x4 partner32(s16x4 v, bool low) {

@@ -57,6 +57,14 @@ int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, 
 __device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
 __device__ __forceinline__ float bf16_val(short h) { return (float)__builtin_bit_cast(__bf16, h); }
 
+// value of x held by lane (l ^ 32) (inline asm: hipcc merged distinct
+// __builtin_amdgcn_permlane32_swap(x, x) calls into one; see tsk3_kernels.hip)
+__device__ __forceinline__ unsigned partner32(unsigned x, bool low) {
+  unsigned a = x, b = x;
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return low ? b : a;
+}
+
 // LDS-DMA of 16 B per lane into LDS[lds_base + lane*16], issued as inline asm
 // so hipcc does not insert its own (draining) vmcnt(0) before later LDS
 // reads; completion is tracked by the hand-counted s_waitcnt vmcnt(N).
@@ -105,7 +113,7 @@ struct Geo {
 };
 
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false, bool X = false>
+          bool G64 = false, int X = 0>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
@@ -212,12 +220,12 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     // X: the ring slots are private to the wave, so the next prefetch goes out
     // at the top of the iteration (into the slot this wave finished with in the
     // previous one) and PD blocks stay in flight throughout
-    if constexpr (X) {
+    if constexpr ((X & 1) != 0) {
       if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
     }
     // blocks issued after this one and still possibly in flight
     const int64_t rem = nloc - 1 - my;
-    const int younger = X ? (int)(rem < PD ? rem : PD) : (int)(rem < PD - 1 ? rem : PD - 1);
+    const int younger = (X & 1) ? (int)(rem < PD ? rem : PD) : (int)(rem < PD - 1 ? rem : PD - 1);
     if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GG::LPB) : "memory");
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GG::LPB) : "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
@@ -286,7 +294,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     }
 
     // prefetch PD blocks ahead into the buffer this wave consumed last iteration
-    if constexpr (!X) {
+    if constexpr ((X & 1) == 0) {
       if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
     }
 
@@ -323,55 +331,41 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       if (!(HI)) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yl[t], accW[ct][t], 0, 0, 0); \
     }                                                                                                \
   }
-      if constexpr (X) {
+      if constexpr ((X & 2) != 0) {
         // one v_mfma_f32_16x16x32_bf16 per tile over K = [16 rows of y_hi ; the
         // same 16 rows of y_lo] (the K = 16 form runs at half rate on gfx950):
-        // a lane reads 4 rows rb..rb+3 of the transposed A tile and of y, its
-        // partner lane (l ^ 32) supplies the other 4 (v_permlane32_swap);
-        // lanes 0-31 carry y_hi, lanes 32-63 y_lo.  Exact W at hi-only cost.
+        // lane group g holds rows 8 (g & 1) .. +7 -- of y_hi for g < 2, of y_lo
+        // for g >= 2 -- read directly (two transposed A reads and two y reads
+        // per lane; lane swaps measured far slower).  Exact W at hi-only cost.
         const bool low = lane < 32;
-        const int rb = 8 * (g4 & 1) + 4 * (g4 >> 1);
+        const int r8 = 8 * (g4 & 1);
         bf16x8 yb[KT];
 #pragma unroll
         for (int t = 0; t < KT; ++t) {
-          const f32x4 v = *(const f32x4*)&yf[(16 * t + i16) * BM + rb];
-          f32x4 o;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v[j]),
-                                                            __builtin_bit_cast(unsigned, v[j]), false, false);
-            o[j] = __builtin_bit_cast(float, low ? r[1] : r[0]);
-          }
+          const f32x4 va = *(const f32x4*)&yf[(16 * t + i16) * BM + r8];
+          const f32x4 vb = *(const f32x4*)&yf[(16 * t + i16) * BM + r8 + 4];
           s16x8 e;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const float r03 = low ? v[j] : o[j], r47 = low ? o[j] : v[j];
-            const short h0 = bf16_bits(r03), h1 = bf16_bits(r47);
-            e[j] = low ? h0 : bf16_bits(r03 - bf16_val(h0));
-            e[4 + j] = low ? h1 : bf16_bits(r47 - bf16_val(h1));
+            const short ha = bf16_bits(va[j]), hb = bf16_bits(vb[j]);
+            e[j] = low ? ha : bf16_bits(va[j] - bf16_val(ha));
+            e[4 + j] = low ? hb : bf16_bits(vb[j] - bf16_val(hb));
           }
           yb[t] = __builtin_bit_cast(bf16x8, e);
         }
-        const int trow = rb + q;
 #pragma unroll
         for (int ct = 0; ct < NW / 16; ++ct) {
           const int chunk = 2 * ct + (p >> 1);
-          const char* addr = region + trow * GG::ROWB + (chunk ^ (trow & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-          const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr);
-          typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-          const u32x2 u = __builtin_bit_cast(u32x2, a4);
-          u32x2 uo;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const auto r = __builtin_amdgcn_permlane32_swap(u[j], u[j], false, false);
-            uo[j] = low ? r[1] : r[0];
-          }
-          const s16x4 b4 = __builtin_bit_cast(s16x4, uo);
+          const int ra = r8 + q, rbb = r8 + 4 + q;
+          const char* aa = region + ra * GG::ROWB + (chunk ^ (ra & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const char* ab2 = region + rbb * GG::ROWB + (chunk ^ (rbb & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)aa);
+          const s16x4 b4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)ab2);
           s16x8 a8;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            a8[j] = low ? a4[j] : b4[j];
-            a8[4 + j] = low ? b4[j] : a4[j];
+            a8[j] = a4[j];
+            a8[4 + j] = b4[j];
           }
           const bf16x8 af8 = __builtin_bit_cast(bf16x8, a8);
 #pragma unroll
@@ -554,10 +548,10 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
-int g_x = -1;  // 1: top-of-loop prefetch + K = 32 hi/lo step 3 (SL_TSK_X), 0: original
+int g_x = -1;  // SL_TSK_X bits: 1 top-of-loop prefetch, 2 K = 32 hi/lo step 3 (default 3)
 
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false, bool X = false>
+          bool G64 = false, int X = 0>
 int launch_x(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   using GG = Geo<NW, KT, NBUF>;
@@ -578,14 +572,21 @@ int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   if (g_x < 0) {
     const char* e = getenv("SL_TSK_X");
-    g_x = e ? atoi(e) : 0;
+    g_x = e ? atoi(e) : 3;
   }
   // the K = 32 step 3 needs the W update (DO_W) and a non-split Z
+  // bit 0: top-of-loop prefetch; bit 1: K = 32 hi/lo step 3 (exact passes only:
+  // the hi-only intermediate form costs the same on K = 16)
   if constexpr (DO_W && !ZSPLIT && KT <= 3) {
-    if (g_x == 1)
-      return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, true>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    switch (g_x & 3) {
+      case 1: return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 1>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+      case 2: if constexpr (!HI_T) return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 2>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s); break;
+      case 3: if constexpr (!HI_T) return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 3>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+              return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 1>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+      default: break;
+    }
   }
-  return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, false>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 0>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
 }
 
 // buffer depth: SL_TSK_NBUF env (A/B tuning), default NBUF_DEFAULT, clamped to the LDS budget

@@ -57,9 +57,7 @@ regression_problem_t = RegressionProblem
 
 
 def _local_dense(A):
-    """A as a dense replicated tensor (small/medium problems and exact solvers)."""
-    if isinstance(A, DistMatrix):
-        return A.to_global()
+    """A local (non-distributed) operand as a dense tensor."""
     if A.layout != torch.strided:
         return A.to_dense()
     return A
@@ -71,7 +69,15 @@ def _wdt(A):
 
 
 class RegressionSolver:
-    """Exact solvers: ``method`` in {"qr", "sne", "ne", "svd", "lsqr"}."""
+    """Exact solvers: ``method`` in {"qr", "sne", "ne", "svd", "lsqr"}.
+
+    A row-distributed DistMatrix (any layout; non-row layouts are brought to
+    ``[VC,*]`` by one all-to-all) is never gathered: "qr", "sne" and "svd"
+    factor it by TSQR (reference ``El::qr::ExplicitTS`` for ``[VC,*]``,
+    ``base/QR.hpp:11-36``) -- a local Householder QR per GPU plus one
+    all-gather of the n x n R factors -- "ne" by the all-reduced Gram, and the
+    right-hand side enters only through ``Q^T b`` / ``A^T b`` (one all-reduce
+    of n x k).  The n x n factorisations are redundant on every rank."""
 
     def __init__(self, problem: RegressionProblem, method: str = "qr", params: KrylovIterParams | None = None):
         self.problem = problem
@@ -80,45 +86,75 @@ class RegressionSolver:
         A = problem.A
         if self.method == "lsqr":
             return
-        Ad = _local_dense(A).to(torch.float64)
-        if self.method == "qr":
-            self.Q, self.R = torch.linalg.qr(Ad, mode="reduced")
-        elif self.method == "sne":
-            _, self.R = torch.linalg.qr(Ad, mode="r")
-            self.Ad = Ad
-        elif self.method == "ne":
-            self.Ad = Ad
-            self.L = torch.linalg.cholesky(Ad.t() @ Ad)
-        elif self.method == "svd":
-            self.U, self.s, self.Vh = torch.linalg.svd(Ad, full_matrices=False)
-        else:
+        if self.method not in ("qr", "sne", "ne", "svd"):
             raise InvalidParametersError(f"unknown exact solver {method}")
+        self.dist = isinstance(A, DistMatrix)
+        if self.dist:
+            D = A if A.layout in ("VC_STAR", "VR_STAR") else A.redistribute("VC_STAR")
+            self.D, self.comm = D, D.comm
+            Ad = D.local.to(torch.float64)
+        else:
+            self.comm = None
+            Ad = _local_dense(A).to(torch.float64)
+        from ..base import linalg as L
+        if self.method in ("qr", "sne", "svd"):
+            if self.dist:
+                self.Q, self.R = L.tsqr(Ad, self.comm)
+            else:
+                self.Q, self.R = torch.linalg.qr(Ad, mode="reduced")
+            if self.method == "sne":
+                self.Ad, self.Q = Ad, None
+            elif self.method == "svd":
+                Ur, self.s, self.Vh = torch.linalg.svd(self.R, full_matrices=False)
+                self.Ur = Ur
+        else:
+            self.Ad = Ad
+            G = Ad.t() @ Ad
+            if self.dist:
+                self.comm.all_reduce(G)
+            self.L = torch.linalg.cholesky(G)
+
+    def _rhs_local(self, b):
+        """Rows of b matching this rank's rows of A (fp64, 2-D)."""
+        if isinstance(b, DistMatrix):
+            if self.dist:
+                bb = b if b.layout in ("VC_STAR", "VR_STAR") else b.redistribute("VC_STAR")
+                return bb.local
+            return b.to_global()
+        if self.dist:
+            r0, r1 = self.D.row_range()
+            return b[r0:r1]
+        return b
+
+    def _reduce(self, X):
+        if self.dist:
+            self.comm.all_reduce(X)
+        return X
 
     def solve(self, b):
         A = self.problem.A
-        B = b.to_global() if isinstance(b, DistMatrix) else b
-        vec = B.dim() == 1
-        B2 = (B[:, None] if vec else B)
+        vec = (b.dim() == 1) if isinstance(b, torch.Tensor) else False
         if self.method == "lsqr":
-            X, _ = lsqr(A, b if not vec else b[:, None], params=self.params)
+            X, _ = lsqr(A, b[:, None] if vec else b, params=self.params)
+            return X[:, 0] if vec else X
+        B = self._rhs_local(b)
+        B2 = (B[:, None] if B.dim() == 1 else B).to(torch.float64).to(self._dev())
+        if self.method == "qr":
+            X = torch.linalg.solve_triangular(self.R, self._reduce(self.Q.t() @ B2), upper=True)
+        elif self.method == "sne":
+            # semi-normal equations R^T R x = A^T b
+            y = torch.linalg.solve_triangular(self.R.t(), self._reduce(self.Ad.t() @ B2), upper=False)
+            X = torch.linalg.solve_triangular(self.R, y, upper=True)
+        elif self.method == "ne":
+            X = torch.cholesky_solve(self._reduce(self.Ad.t() @ B2), self.L)
         else:
-            Bd = B2.to(torch.float64).to(self._dev())
-            if self.method == "qr":
-                X = torch.linalg.solve_triangular(self.R, self.Q.t() @ Bd, upper=True)
-            elif self.method == "sne":
-                # semi-normal equations R^T R x = A^T b
-                y = torch.linalg.solve_triangular(self.R.t(), self.Ad.t() @ Bd, upper=False)
-                X = torch.linalg.solve_triangular(self.R, y, upper=True)
-            elif self.method == "ne":
-                X = torch.cholesky_solve(self.Ad.t() @ Bd, self.L)
-            else:
-                tol = self.s.max() * max(self.U.shape) * torch.finfo(torch.float64).eps
-                sinv = torch.where(self.s > tol, 1.0 / self.s, torch.zeros_like(self.s))
-                X = self.Vh.t() @ (sinv[:, None] * (self.U.t() @ Bd))
+            tol = self.s.max() * max(self.problem.m, self.problem.n) * torch.finfo(torch.float64).eps
+            sinv = torch.where(self.s > tol, 1.0 / self.s, torch.zeros_like(self.s))
+            X = self.Vh.t() @ (sinv[:, None] * (self.Ur.t() @ self._reduce(self.Q.t() @ B2)))
         return X[:, 0] if vec else X
 
     def _dev(self):
-        for name in ("Q", "R", "U", "Ad"):
+        for name in ("Q", "R", "Ad"):
             t = getattr(self, name, None)
             if isinstance(t, torch.Tensor):
                 return t.device
