@@ -44,36 +44,74 @@ class _H5Native:
         return H5File(fname)
 
 
-def read_hdf5(fname: str, max_n: int = -1, sparse: bool = False, dtype=torch.float64):
+def _h5_slice(f, name, axis, s0, s1):
+    if hasattr(f, "read_slice"):                 # built-in reader (mmap hyperslab)
+        return f.read_slice(name, axis, s0, s1)
+    ds = f[name]                                 # h5py: hyperslab selection
+    return np.asarray(ds[:, s0:s1] if axis == 1 else ds[s0:s1])
+
+
+def read_hdf5(fname: str, max_n: int = -1, sparse: bool = False, dtype=torch.float64, comm=None):
     """Reference layout: datasets ``X`` (d x n, examples as columns) and ``Y``
     (also the python-skylark dataset names ``Features`` / ``Labels``); sparse
     files hold ``dimensions``, ``indptr``, ``indices``, ``values``.  Returns
     ``(X, Y)`` with examples as ROWS.  Uses h5py when importable, else the
-    built-in reader (``io/h5.py``)."""
+    built-in reader (``io/h5.py``).
+
+    With a multi-rank ``comm`` every rank reads only ITS balanced block of
+    examples (a column hyperslab of ``X``, the matching ``indptr`` range and
+    ``indices``/``values`` slices) and the result is a pair of ``[VC,*]``
+    DistMatrices -- where the reference reads on rank 0 and ships chunks by
+    send/recv (``ml/io.hpp:256-526``, ``utility/io/hdf5_io.hpp:148-262``)."""
     h5 = _h5py() or _H5Native
+    dist = comm is not None and comm.size > 1
     with h5.File(fname, "r") as f:
         if "indptr" in f:
             dims = np.asarray(f["dimensions"])
             d, n = int(dims[0]), int(dims[1])
-            indptr = np.asarray(f["indptr"], dtype=np.int64)
             n = n if max_n < 0 else min(n, max_n)
-            nnz = int(indptr[n])
-            X = torch.sparse_csr_tensor(torch.from_numpy(indptr[:n + 1]),
-                                        torch.from_numpy(np.asarray(f["indices"][:nnz], dtype=np.int64)),
-                                        torch.from_numpy(np.asarray(f["values"][:nnz], dtype=np.float64)).to(dtype),
-                                        (n, d))
+            r0, r1 = _my_rows(n, comm) if dist else (0, n)
+            ip = np.asarray(_h5_slice(f, "indptr", 0, r0, r1 + 1), dtype=np.int64)
+            a, b = int(ip[0]), int(ip[-1])
+            X = torch.sparse_csr_tensor(torch.from_numpy(ip - a),
+                                        torch.from_numpy(np.asarray(_h5_slice(f, "indices", 0, a, b), dtype=np.int64)),
+                                        torch.from_numpy(np.asarray(_h5_slice(f, "values", 0, a, b),
+                                                                    dtype=np.float64)).to(dtype),
+                                        (r1 - r0, d))
             if not sparse:
                 X = X.to_dense()
             yname = "Y"
         else:
             xname, yname = ("X", "Y") if "X" in f else ("Features", "Labels")
-            Xd = np.asarray(f[xname])
-            n = Xd.shape[1] if max_n < 0 else min(Xd.shape[1], max_n)
-            X = torch.from_numpy(np.ascontiguousarray(Xd[:, :n].T)).to(dtype)
+            d, n = _h5_shape(f, xname)
+            n = n if max_n < 0 else min(n, max_n)
+            r0, r1 = _my_rows(n, comm) if dist else (0, n)
+            Xd = _h5_slice(f, xname, 1, r0, r1)
+            X = torch.from_numpy(np.ascontiguousarray(Xd.T)).to(dtype)
             if sparse:
                 X = X.to_sparse_csr()
-        Y = torch.from_numpy(np.asarray(f[yname]).reshape(-1)[:X.shape[0]].astype(np.float64))
+        yshape = _h5_shape(f, yname)
+        if len(yshape) == 1:
+            Yall = _h5_slice(f, yname, 0, r0, r1)
+        else:   # 1 x n or n x 1 label arrays
+            Yall = np.asarray(f[yname]).reshape(-1)[r0:r1]
+        Y = torch.from_numpy(np.asarray(Yall).reshape(-1)[: r1 - r0].astype(np.float64))
+    if dist:
+        from ..parallel.distmatrix import DistMatrix
+        return (DistMatrix(X, (n, d), "VC_STAR", comm), DistMatrix(Y[:, None].contiguous(), (n, 1), "VC_STAR", comm))
     return X, Y
+
+
+def _h5_shape(f, name):
+    if hasattr(f, "read_slice"):
+        return tuple(int(x) for x in f.shape(name))
+    return tuple(int(x) for x in f[name].shape)
+
+
+def _my_rows(n, comm):
+    from ..parallel.comm import balanced_offsets
+    off = balanced_offsets(n, comm.size)
+    return off[comm.rank], off[comm.rank + 1]
 
 
 def write_hdf5(fname: str, X, Y):
@@ -104,7 +142,8 @@ def read(fileformat: int, fname: str, min_d: int = 0, comm=None, dtype=torch.flo
             return read_libsvm_dist(fname, comm, min_d, fileformat == LIBSVM_SPARSE, dtype, device)
         return read_libsvm(fname, min_d, sparse=(fileformat == LIBSVM_SPARSE), dtype=dtype, device=device)
     if fileformat in (HDF5_DENSE, HDF5_SPARSE):
-        return read_hdf5(fname, sparse=(fileformat == HDF5_SPARSE), dtype=dtype)
+        return read_hdf5(fname, sparse=(fileformat == HDF5_SPARSE), dtype=dtype,
+                         comm=comm if (comm is not None and comm.size > 1) else None)
     raise IOError_(f"unknown file format code {fileformat}")
 
 

@@ -174,7 +174,7 @@ class _Reader:
         hdata = self.off(heap + 8 + 2 * self.sl)
 
         def name_at(o):
-            e = d.index(b"\x00", hdata + o)
+            e = d.find(b"\x00", hdata + o)
             return d[hdata + o:e].decode()
 
         def walk(node):
@@ -348,8 +348,14 @@ class H5File:
     nested paths ``"group/name"``."""
 
     def __init__(self, path):
-        with open(path, "rb") as fh:
-            self._r = _Reader(fh.read())
+        # memory-mapped: a rank that reads a hyperslab touches only its pages
+        import mmap
+        self._fh = open(path, "rb")
+        try:
+            self._mm = mmap.mmap(self._fh.fileno(), 0, access=mmap.ACCESS_READ)
+        except ValueError:            # empty file
+            self._mm = b""
+        self._r = _Reader(self._mm)
         r = self._r
         self._root = r.group_links(r.root, r.root_scratch if r.root_cache == 1 else None, r.root_cache)
 
@@ -381,10 +387,43 @@ class H5File:
     def shape(self, name):
         return self._r.dataset(self._resolve(name))[0]
 
+    def read_slice(self, name, axis: int, s0: int, s1: int) -> np.ndarray:
+        """``f[name]`` restricted to [s0, s1) along ``axis``.  Contiguous
+        datasets are sliced from a zero-copy view of the mapping (only the
+        slab's pages are read); chunked / compact ones are read whole."""
+        r = self._r
+        addr = self._resolve(name)
+        shape, dt, lay, _ = r.dataset(addr)
+        a = None
+        if lay[0] in (3, 4) and lay[1] == 1:
+            a = r.off_b(lay, 2)
+        elif lay[0] in (1, 2) and lay[2] == 1:
+            a = r.off_b(lay, 8)
+        if a is None or a == UNDEF:
+            full = r.read_dataset(addr)
+        else:
+            n = int(np.prod(shape)) if shape else 1
+            full = np.frombuffer(r.d, dt, n, a).reshape(shape)
+        sl = [slice(None)] * len(shape)
+        sl[axis] = slice(s0, s1)
+        out = np.array(full[tuple(sl)], copy=True, order="C")   # never a view of the mapping
+        del full
+        return out
+
+    def close(self):
+        self._r = None
+        if hasattr(self._mm, "close"):
+            try:
+                self._mm.close()
+            except BufferError:   # a caller still holds a view: the GC unmaps later
+                pass
+        self._fh.close()
+
     def __enter__(self):
         return self
 
     def __exit__(self, *a):
+        self.close()
         return False
 
 

@@ -31,6 +31,8 @@ i32, i64, u64, f64, vp, cp = C.c_int, C.c_int64, C.c_uint64, C.c_double, C.c_voi
 # name -> argtypes (restype is always c_int error code unless listed in _RESTYPE)
 SIGNATURES = {
     "sl_version": [],
+    "sl_ust_noreplace_host": [vp, u64, u64, i64, i64],
+    "sl_fastfood_perms_host": [vp, u64, u64, i64, i64],
     "sl_last_error": [],
     "sl_fill_random": [vp, i32, i32, u64, u64, i64, i64, i64, i64, i64, i64, i64, i64, f64, f64, f64, i32, vp],
     "sl_fill_random_host": [vp, i32, i32, u64, u64, i64, i64, i64, i64, i64, i64, i64, i64, f64, f64, f64, i32],

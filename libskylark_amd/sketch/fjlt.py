@@ -104,21 +104,16 @@ class FJLT(SketchTransform):
 
 
 def _fisher_yates_prefix(ctx, N: int, S: int):
+    """S distinct indices of [0, N): S steps of the backward Fisher-Yates
+    shuffle in native code (``sl_ust_noreplace_host``, O(S) time and memory);
+    reserves N counter slots like the reference (``sketch/UST_data.hpp:81-100``)."""
+    import ctypes as C
+    from ..ops import _lib
     seed, base = ctx.seed, ctx.counter
     ctx.counter += N
-    import numpy as np
-    work = np.empty(N, dtype=np.int64)
-    # draws: slot base+i gives uniform_int(0, i)
-    blocks = torch.empty(2 * N, dtype=torch.int64)
-    from ..ops import _lib
-    import ctypes as C
-    _lib.call("sl_uniform_prefix_host", _lib.ptr(blocks), C.c_uint64(seed), C.c_uint64(base), N)
-    j_all = blocks[:N].numpy()
-    for i in range(N):
-        j = int(j_all[i])
-        work[i] = work[j]
-        work[j] = i
-    return torch.from_numpy(work[:S].copy())
+    out = torch.empty(S, dtype=torch.int64)
+    _lib.call("sl_ust_noreplace_host", _lib.ptr(out), C.c_uint64(seed), C.c_uint64(base), N, S)
+    return out
 
 
 @register

@@ -42,17 +42,14 @@ class _Fastfood(_FeatureMap):
         self.shifts = ctx.generate_random_samples_array(S, D.Uniform(0.0, 2 * math.pi))
         self.B = ctx.generate_random_samples_array(nb * NB, D.Rademacher()).view(nb, NB)
         self.G = ctx.generate_random_samples_array(nb * NB, D.Normal()).view(nb, NB)
-        raw = ctx.generate_random_samples_array(nb * (NB - 1), D.UniformInt(0, 2**62), dtype=torch.int64)
-        raw = raw.view(nb, NB - 1).numpy() if NB > 1 else np.zeros((nb, 0), dtype=np.int64)
-        perms = np.empty((nb, NB), dtype=np.int64)
-        for i in range(nb):
-            w = np.arange(NB)
-            for l in range(NB - 1):  # noqa: E741
-                j = NB - 1 - l
-                k = int(raw[i, l] % (j + 1))
-                w[j], w[k] = w[k], w[j]
-            perms[i] = w
-        self.perms = torch.from_numpy(perms)
+        # nb Fisher-Yates permutations of length NB (reference FRFT_data.hpp:91-116:
+        # nb (NB - 1) draws); native, unbiased bounded integers
+        import ctypes as C
+        from ..ops import _lib
+        perms = torch.empty(nb, NB, dtype=torch.int64)
+        _lib.call("sl_fastfood_perms_host", _lib.ptr(perms), C.c_uint64(ctx.seed), C.c_uint64(ctx.counter), nb, NB)
+        ctx.counter += nb * (NB - 1)
+        self.perms = perms
         self.scales = None
         self._Sm = self._make_Sm(ctx)
 

@@ -76,3 +76,33 @@ def test_chunked_deflate_dataset_reader():
     r = _Reader(bytes(blob[:8]) + bytes([0, 0, 0, 0, 0, 8, 8]) + bytes(blob[15:]))
     out = r._read_chunked(btree, (6, 5), (4, 5), np.dtype("<f8"), [(1, (6,))])
     assert np.array_equal(out, A)
+
+
+def _dist_h5_worker(rank, world, dense_path, sparse_path):
+    from libskylark_amd.parallel.comm import world as W
+    comm = W()
+    Xl, Yl = sk.io.read_hdf5(dense_path)
+    Xd, Yd = sk.io.read_hdf5(dense_path, comm=comm)
+    assert Xd.layout == "VC_STAR" and Xd.shape == tuple(Xl.shape)
+    torch.testing.assert_close(Xd.to_global(), Xl)
+    torch.testing.assert_close(Yd.to_global()[:, 0], Yl)
+    Xs, Ys = sk.io.read_hdf5(sparse_path, sparse=True, comm=comm)
+    Xsl, _ = sk.io.read_hdf5(sparse_path, sparse=True)
+    r0, r1 = Xs.row_range()
+    torch.testing.assert_close(Xs.local.to_dense(), Xsl.to_dense()[r0:r1])
+    return True
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_hdf5_hyperslabs(tmp_path, world):
+    """Each rank reads only its example block (reference rank-0 read +
+    send/recv, ml/io.hpp:256-526)."""
+    from mp_utils import run_distributed
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(37, 6, generator=g, dtype=torch.float64)
+    X[X.abs() < 0.7] = 0
+    Y = torch.arange(37, dtype=torch.float64)
+    p, ps = tmp_path / "d.h5", tmp_path / "s.h5"
+    sk.io.write_hdf5(str(p), X, Y)
+    sk.io.write_hdf5(str(ps), X.to_sparse_csr(), Y)
+    run_distributed(_dist_h5_worker, world, str(p), str(ps))

@@ -237,3 +237,30 @@ def test_nurst_follows_probabilities():
     assert abs((idx == 7).mean() - 0.75) < 0.03
     A = _A(10, 3)
     assert torch.equal(T * A, A[torch.from_numpy(idx)])
+
+
+def test_ust_noreplace_native_fast_and_uniform():
+    """UST without replacement at N = 1e7 builds natively in O(S) (the
+    reference runs an N-step Fisher-Yates, sketch/UST_data.hpp:81-100) and
+    reserves N counter slots; small-N sampling is uniform over positions."""
+    import time
+    ctx = sk.Context(3)
+    t0 = time.perf_counter()
+    U = sk.sketch.UST(10_000_000, 200_000, replace=False, context=ctx)
+    assert time.perf_counter() - t0 < 1.0
+    s = U.samples
+    assert len(torch.unique(s)) == len(s) and int(s.min()) >= 0 and int(s.max()) < 10_000_000
+    assert ctx.counter == 10_000_000
+    counts = torch.zeros(10)
+    for seed in range(400):
+        counts[sk.sketch.UST(10, 3, replace=False, context=sk.Context(seed)).samples] += 1
+    # each of 10 positions is chosen 3/10 of the time: 120 +- 3 sigma (~ 28)
+    assert (counts - 120).abs().max() < 40, counts
+
+
+def test_fastfood_perms_are_permutations():
+    F = sk.sketch.FastGaussianRFT(512, 2048, sigma=2.0, context=sk.Context(4))
+    for p in F.perms:
+        assert sorted(p.tolist()) == list(range(512))
+    G = sk.sketch.FastGaussianRFT(512, 2048, sigma=2.0, context=sk.Context(4))
+    assert torch.equal(F.perms, G.perms)
