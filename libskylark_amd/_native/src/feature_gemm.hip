@@ -69,8 +69,8 @@ template <int EPI>
 __device__ __forceinline__ float epilogue(float x, float sc, float sh, float outscale) {
   if constexpr (EPI == EPI_COS) {
     // cos via v_cos_f32, which takes revolutions: reduce to [0, 1) first
-    float rev = (x * sc + sh) * 0.15915494309189535f;
-    rev = rev - floorf(rev);
+    // v_fract_f32: one instruction for the reduction to [0, 1)
+    const float rev = __builtin_amdgcn_fractf((x * sc + sh) * 0.15915494309189535f);
     return outscale * __builtin_amdgcn_cosf(rev);
   } else if constexpr (EPI == EPI_EXPNEG) {
     return outscale * __expf(-x);
@@ -85,10 +85,19 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
             const bf16_t* __restrict__ Whi, const bf16_t* __restrict__ Wlo, int64_t Nf, int64_t ldw,
             const float* __restrict__ scales, const float* __restrict__ shifts, float outscale,
             OutT* __restrict__ out, int64_t ldo, int ntm, int ntn, int per) {
-  __shared__ __attribute__((aligned(16))) bf16_t sAh[2][BM * BK];
-  __shared__ __attribute__((aligned(16))) bf16_t sAl[2][ALO ? BM * BK : 8];
-  __shared__ __attribute__((aligned(16))) bf16_t sWh[2][BN * BK];
-  __shared__ __attribute__((aligned(16))) bf16_t sWl[2][WLO ? BN * BK : 8];
+  // one LDS array: the K-loop staging planes, reused by the epilogue to turn
+  // the MFMA C fragments (4 rows x 1 column per lane) into row-contiguous
+  // 16-B stores (the store tail is issue-bound: cdna_hip_programming.md T21)
+  constexpr int PLANE = 2 * BM * BK;                           // bf16 elements, 2 stages
+  constexpr int STAGE_ELEMS = PLANE * (2 + (ALO ? 1 : 0) + (WLO ? 1 : 0));
+  constexpr int EPI_LD = 64 + 4;                               // f32 row stride of a wave's 64 x 64 block
+  constexpr int EPI_ELEMS = 4 * 64 * EPI_LD * 2;               // as bf16 elements (4 waves, f32)
+  constexpr int LDS_ELEMS = (OUT_T ? STAGE_ELEMS : (STAGE_ELEMS > EPI_ELEMS ? STAGE_ELEMS : EPI_ELEMS));
+  __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS];
+  bf16_t (*sAh)[BM * BK] = (bf16_t (*)[BM * BK])(lds_all);
+  bf16_t (*sWh)[BN * BK] = (bf16_t (*)[BN * BK])(lds_all + PLANE);
+  bf16_t (*sAl)[BM * BK] = (bf16_t (*)[BM * BK])(lds_all + 2 * PLANE);
+  bf16_t (*sWl)[BN * BK] = (bf16_t (*)[BN * BK])(lds_all + (ALO ? 3 : 2) * PLANE);
 
   // XCD-aware tile order (block b runs on XCD b % 8).  When the feature tiles
   // split evenly over the 8 XCDs, XCD x owns ntn/8 of them for every row block,
@@ -234,19 +243,60 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
 #undef SL_FG_STORE
 
   // ---- epilogue: C[row][col], col = lane & 15, row = 4 * (lane >> 4) + reg
+  if constexpr (!OUT_T) {
+    // stage the wave's 64 x 64 block (after the epilogue map) in LDS, then
+    // store whole 16-B row pieces: 16 dwordx4 (f32) per lane instead of 64 dwords
+    __syncthreads();                                   // every wave is done with the staging planes
+    float* blk = (float*)lds_all + wave * 64 * EPI_LD;
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    const int64_t f = col0 + wc * 64 + cb * 16 + (lane & 15);
-    if (f >= Nf) continue;
-    const float sc = scales ? scales[f] : 1.f;
-    const float sh = shifts ? shifts[f] : 0.f;
+    for (int cb = 0; cb < 4; ++cb) {
+      const int64_t f = col0 + wc * 64 + cb * 16 + (lane & 15);
+      const float sc = (scales && f < Nf) ? scales[f] : 1.f;
+      const float sh = (shifts && f < Nf) ? shifts[f] : 0.f;
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
-      const int64_t r = row0 + wr * 64 + rb * 16 + 4 * (lane >> 4);
-      float v[4];
+      for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale);
-      if (OUT_T) {
+        for (int e = 0; e < 4; ++e)
+          blk[(rb * 16 + 4 * (lane >> 4) + e) * EPI_LD + cb * 16 + (lane & 15)] =
+              epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale);
+    }
+    __syncthreads();
+    const int64_t rbase = row0 + wr * 64;
+    const int64_t fbase = col0 + wc * 64;
+    const bool fullc = fbase + 64 <= Nf && ((ldo & 3) == 0);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int idx = it * 64 + lane;
+      const int rr = idx >> 4, c4 = (idx & 15) * 4;
+      const int64_t r = rbase + rr;
+      if (r >= M) continue;
+      const f32x4 v = *(const f32x4*)&blk[rr * EPI_LD + c4];
+      OutT* p = out + r * ldo + fbase + c4;
+      if (fullc) {
+        if constexpr (sizeof(OutT) == 4) {
+          *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          *(uint2*)p = make_uint2(f2bf_bits(v[0]) | (f2bf_bits(v[1]) << 16), f2bf_bits(v[2]) | (f2bf_bits(v[3]) << 16));
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (fbase + c4 + e < Nf) p[e] = cvt_out<OutT>(v[e]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int64_t f = col0 + wc * 64 + cb * 16 + (lane & 15);
+      if (f >= Nf) continue;
+      const float sc = scales ? scales[f] : 1.f;
+      const float sh = shifts ? shifts[f] : 0.f;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int64_t r = row0 + wr * 64 + rb * 16 + 4 * (lane >> 4);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale);
         OutT* p = out + f * ldo + r;
         if (r + 3 < M) {
           if constexpr (sizeof(OutT) == 4) {
@@ -256,10 +306,6 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (r + e < M) p[e] = cvt_out<OutT>(v[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (r + e < M) out[(r + e) * ldo + f] = cvt_out<OutT>(v[e]);
       }
     }
   }

@@ -83,3 +83,160 @@ SL_API int sl_fjlt_operator(const uint64_t* prm, int64_t S, int64_t N, double sc
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
+
+// ---------------------------------------------------------------------------
+// FJLT / RFUT DCT-II pipeline for large S (reference sketch/FJLT_Elemental.hpp
+// :144-171, RFUT_Elemental.hpp:66-85, utility/fft/fftw_futs.h:50-108).
+//   pre:  v = Makhoul reorder of (D x) along the transform axis, in one pass
+//         (v[n] = d[2n] x[2n] for n < ceil(N/2), v[N-1-n] = d[2n+1] x[2n+1]),
+//         written as f32 for rocFFT's real-to-complex transform;
+//   post: only the S sampled frequencies k_s of the orthonormal DCT-II,
+//         X_k = c_k Re(e^{-i pi k / 2N} V_k) with V_k = conj(V_{N-k}) past N/2,
+//         times the sketch scale -- one gather of S rows/columns of the
+//         half spectrum instead of the full transform + index_select.
+// Layout: the transform runs along dim 0 (N x m, row-major) or dim 1 (m x N).
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_fjlt_pre(const T* __restrict__ x, int64_t N, int64_t m, int64_t ldx, int dim, const double* __restrict__ d,
+           float* __restrict__ v, int64_t ldv) {
+  const int64_t total = N * m;
+  const int64_t half = (N + 1) / 2;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t n, c;
+    if (dim == 0) { n = t / m; c = t - n * m; }   // consecutive threads along the row (coalesced)
+    else { c = t / N; n = t - c * N; }
+    const int64_t src = n < half ? 2 * n : 2 * (N - 1 - n) + 1;
+    const float sgn = (float)d[src];
+    if (dim == 0) v[n * ldv + c] = sgn * Cvt<T>::to_f(x[src * ldx + c]);
+    else v[c * ldv + n] = sgn * Cvt<T>::to_f(x[c * ldx + src]);
+  }
+}
+
+// dim 0 input (N x m) written TRANSPOSED (m x N) so that rocFFT runs
+// contiguous transforms (a strided N = 1e6 transform over 1000 columns ran
+// ~10x below the contiguous one): 64 x 64 tiles through LDS, coalesced on
+// both sides.
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_fjlt_pre_t(const T* __restrict__ x, int64_t N, int64_t m, int64_t ldx, const double* __restrict__ d,
+             float* __restrict__ vt, int64_t ldv) {
+  __shared__ float tile[64][65];
+  const int64_t half = (N + 1) / 2;
+  const int64_t n0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t n = n0 + i, c = c0 + tx;
+    float val = 0.f;
+    if (n < N && c < m) {
+      const int64_t src = n < half ? 2 * n : 2 * (N - 1 - n) + 1;
+      val = (float)d[src] * Cvt<T>::to_f(x[src * ldx + c]);
+    }
+    tile[i][tx] = val;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, n = n0 + tx;
+    if (c < m && n < N) vt[c * ldv + n] = tile[tx][i];
+  }
+}
+
+// V: complex half spectrum (interleaved f32 pairs), (N/2+1) x m (vt = 0) or
+// m x (N/2+1) (vt = 1), leading dimension ldV in complex elements; the output
+// is S x m (ot = 0) or m x S (ot = 1).
+__global__ void __launch_bounds__(256)
+k_fjlt_post(const float2* __restrict__ V, int64_t N, int64_t m, int64_t ldV, int vt, int ot,
+            const int64_t* __restrict__ samples, int64_t S, double scale, float* __restrict__ out, int64_t ldo) {
+  const int64_t total = S * m;
+  const double c0 = sqrt(1.0 / (double)N), c1 = sqrt(2.0 / (double)N);
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t s, c;
+    if (ot == 0) { s = t / m; c = t - s * m; }
+    else { c = t / S; s = t - c * S; }
+    const int64_t k = samples[s];
+    const bool mirror = 2 * k > N;
+    const int64_t kk = mirror ? N - k : k;
+    const float2 z = vt == 0 ? V[kk * ldV + c] : V[c * ldV + kk];
+    const double re = z.x, im = mirror ? -(double)z.y : (double)z.y;
+    // angle -pi k / 2N reduced exactly in integers (k < N)
+    double sn, cs;
+    sincospi(-(double)k / (2.0 * (double)N), &sn, &cs);
+    const double val = (re * cs - im * sn) * (k == 0 ? c0 : c1) * scale;
+    if (ot == 0) out[s * ldo + c] = (float)val;
+    else out[c * ldo + s] = (float)val;
+  }
+}
+
+// dim = 2: dim-0 input (N x m) written transposed (m x N, row stride ldv)
+SL_API int sl_fjlt_pre(const void* x, int dtype, int64_t N, int64_t m, int64_t ldx, int dim, const double* d,
+                       float* v, int64_t ldv, void* stream) {
+  if (N <= 0 || m <= 0) return SL_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dim == 2) {
+    dim3 grid((unsigned)((N + 63) / 64), (unsigned)((m + 63) / 64));
+    if (dtype == SL_F32) k_fjlt_pre_t<float><<<grid, 256, 0, s>>>((const float*)x, N, m, ldx, d, v, ldv);
+    else if (dtype == SL_BF16) k_fjlt_pre_t<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, N, m, ldx, d, v, ldv);
+    else { sl_set_last_error("fjlt_pre: f32 or bf16 input"); return SL_ERR_UNSUPPORTED; }
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  }
+  const unsigned grid = sl_grid_for((size_t)(N * m), 256, 8192);
+  if (dtype == SL_F32) k_fjlt_pre<float><<<grid, 256, 0, s>>>((const float*)x, N, m, ldx, dim, d, v, ldv);
+  else if (dtype == SL_BF16) k_fjlt_pre<bf16_t><<<grid, 256, 0, s>>>((const bf16_t*)x, N, m, ldx, dim, d, v, ldv);
+  else { sl_set_last_error("fjlt_pre: f32 or bf16 input"); return SL_ERR_UNSUPPORTED; }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// layout = vt + 2 * ot (see k_fjlt_post)
+SL_API int sl_fjlt_post(const void* V, int64_t N, int64_t m, int64_t ldV, int layout, const int64_t* samples, int64_t S,
+                        double scale, float* out, int64_t ldo, void* stream) {
+  if (S <= 0 || m <= 0) return SL_OK;
+  const unsigned grid = sl_grid_for((size_t)(S * m), 256, 8192);
+  k_fjlt_post<<<grid, 256, 0, (hipStream_t)stream>>>((const float2*)V, N, m, ldV, layout & 1, (layout >> 1) & 1,
+                                                       samples, S, scale, out, ldo);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// PPT / TensorSketch spectral product (reference sketch/PPT_Elemental.hpp
+// :140-185).  F holds the q half spectra (q x (S/2+1) x m, complex f32) of the
+// UNSCALED CountSketches C_i A; the reference adds sqrt(c) h_i e_{idx_i} to
+// sqrt(gamma) C_i A before its FFT, which is folded in analytically here:
+//     P[k][c] = prod_i ( sqrt(gamma) F_i[k][c] + sqrt(c) h_i w^(k idx_i) ),
+//     w = exp(-2 pi i / S)
+// -- one pass over the q spectra, no per-sketch scale / add / multiply passes.
+__global__ void __launch_bounds__(256)
+k_ppt_product(const float2* __restrict__ F, int q, int64_t K, int64_t m, int64_t S, const int64_t* __restrict__ idx,
+              const double* __restrict__ hv, double sg, double sc, float2* __restrict__ P) {
+  const int64_t total = K * m;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = t / m;
+    float pr = 1.f, pi = 0.f;
+    for (int i = 0; i < q; ++i) {
+      const float2 z = F[(int64_t)i * total + t];
+      // w^(k idx) with the exponent reduced mod S in integers (exact angle)
+      const int64_t e = (k * idx[i]) % S;
+      double sn, cs;
+      sincospi(-2.0 * (double)e / (double)S, &sn, &cs);
+      const float ar = (float)(sg * z.x + sc * hv[i] * cs), ai = (float)(sg * z.y + sc * hv[i] * sn);
+      const float nr = pr * ar - pi * ai, ni = pr * ai + pi * ar;
+      pr = nr;
+      pi = ni;
+    }
+    P[t] = make_float2(pr, pi);
+  }
+}
+
+SL_API int sl_ppt_product(const void* F, int q, int64_t K, int64_t m, int64_t S, const int64_t* idx, const double* hv,
+                          double sg, double sc, void* P, void* stream) {
+  if (K <= 0 || m <= 0) return SL_OK;
+  const unsigned grid = sl_grid_for((size_t)(K * m), 256, 8192);
+  k_ppt_product<<<grid, 256, 0, (hipStream_t)stream>>>((const float2*)F, q, K, m, S, idx, hv, sg, sc, (float2*)P);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

@@ -130,6 +130,10 @@ def _register_fjlt():
     from . import _lib
     _lib.register("sl_fjlt_operator", [C.c_void_p, C.c_int64, C.c_int64, C.c_double, C.c_void_p, C.c_int,
                                        C.c_int64, C.c_int, C.c_void_p])
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int
+    _lib.register("sl_fjlt_pre", [vp, i32, i64, i64, i64, i32, vp, vp, i64, vp])
+    _lib.register("sl_fjlt_post", [vp, i64, i64, i64, i32, vp, i64, C.c_double, vp, i64, vp])
+    _lib.register("sl_ppt_product", [vp, i32, i64, i64, i64, vp, vp, C.c_double, C.c_double, vp, vp])
 
 
 _register_fjlt()
@@ -149,3 +153,42 @@ def fjlt_operator(prm: torch.Tensor, S: int, N: int, scale: float, out: torch.Te
     _lib.call("sl_fjlt_operator", _lib.ptr(prm), S, N, float(scale), _lib.ptr(out), _lib.dtype_code(out.dtype),
               out.stride(0), int(transpose), C.c_void_p(_lib.stream_of(out)))
     return out
+
+
+def fjlt_sampled(A: torch.Tensor, dim: int, d: torch.Tensor, samples: torch.Tensor, scale: float) -> torch.Tensor:
+    """``scale * P F D A`` along ``dim`` with F the orthonormal DCT-II and P the
+    rows ``samples`` (FJLT with many samples, Blendenpik's t = 4n sketch).
+
+    GPU (f32 / bf16 A): one fused pass for D-scaling + Makhoul reordering
+    (``sl_fjlt_pre``), rocFFT real-to-complex along ``dim`` (``torch.fft.rfft``),
+    and one gather of the S sampled frequencies with the post-twiddle and
+    scales (``sl_fjlt_post``) -- the full DCT is never formed.  Elsewhere the
+    torch DCT + index_select composition (same numbers up to rounding)."""
+    N = A.shape[dim]
+    m = A.shape[1 - dim]
+    if A.is_cuda and A.dtype in (torch.float32, torch.bfloat16) and A.stride(1) == 1 and N >= 2:
+        import ctypes as C
+        from . import _lib
+        _lib.require()
+        st = C.c_void_p(_lib.stream_of(A))
+        dd = d.to(device=A.device, dtype=torch.float64).contiguous()
+        # always transform along contiguous rows of an m x N buffer (dim 0 input
+        # is transposed by the pre-pass itself)
+        v = torch.empty(m, N, dtype=torch.float32, device=A.device)
+        _lib.call("sl_fjlt_pre", _lib.ptr(A), _lib.dtype_code(A.dtype), N, m, A.stride(0), 2 if dim == 0 else 1,
+                  _lib.ptr(dd), _lib.ptr(v), v.stride(0), st)
+        V = torch.fft.rfft(v, dim=1)
+        del v
+        if V.stride(1) != 1:
+            V = V.contiguous()
+        smp = samples.to(device=A.device, dtype=torch.int64).contiguous()
+        S = smp.numel()
+        out = torch.empty((S, m) if dim == 0 else (m, S), dtype=torch.float32, device=A.device)
+        _lib.call("sl_fjlt_post", _lib.ptr(V), N, m, V.stride(0), 1 + 2 * (1 if dim == 1 else 0), _lib.ptr(smp), S,
+                  float(scale), _lib.ptr(out), out.stride(0), st)
+        return out
+    wd = _work_dtype(A.dtype)
+    dv = d.to(device=A.device, dtype=wd)
+    X = A.to(wd) * (dv[:, None] if dim == 0 else dv[None, :])
+    FA = dct2(X, dim)
+    return FA.index_select(dim, samples.to(A.device)) * scale

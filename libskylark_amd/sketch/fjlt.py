@@ -90,10 +90,8 @@ class FJLT(SketchTransform):
             return out.float() if cdt in (torch.bfloat16, torch.float16) else out
         if in_offset != 0:
             raise ValueError("FFT-based FJLT needs the full sketched dimension on one device")
-        FA = self.rfut.apply(A, dim)
-        idx = self.samples.to(A.device)
-        out = FA.index_select(dim, idx) * self.scale
-        return out
+        out = _fut.fjlt_sampled(A, dim, self.rfut.D, self.samples, self.scale)
+        return out.to(torch.float64) if A.dtype == torch.float64 else out
 
     def apply_local_shard(self, A_local, dim, in_offset, out_rows=None):
         if A_local.layout == torch.sparse_csr:

@@ -160,26 +160,59 @@ class PPT(SketchTransform):
         self.hash_val = ctx.generate_random_samples_array(self._q, D.Rademacher())
 
     def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
-        X = A if dim == COLUMNWISE else A.t()
-        wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
-        X = X.to(wdt).contiguous()
+        """Reference loop (PPT_Elemental.hpp:140-185): per column,
+        ``P = prod_i FFT(sqrt(gamma) C_i a + sqrt(c) h_i e_{idx_i})``,
+        ``SA = IFFT(P)`` (1/S normalised).  Here: the q CountSketches of the
+        whole block (dense or CSR input -- sparse input is never densified),
+        ONE batched real FFT over the q x S x m stack, ONE fused q-way
+        complex product with the scale and the constant term folded into the
+        spectrum (``sl_ppt_product`` on GPU), one inverse real FFT."""
+        sparse = A.layout == torch.sparse_csr
+        if dim == COLUMNWISE:
+            X = A
+        else:
+            X = A.to_sparse_coo().t().coalesce().to_sparse_csr() if sparse else A.t()
+        vdt = X.values().dtype if sparse else X.dtype
+        wdt = torch.float64 if vdt == torch.float64 else torch.float32
+        if not sparse:
+            X = X.to(wdt).contiguous()
         m = X.shape[1]
-        P = None
+        S, q = self._S, self._q
         sg, sc = math.sqrt(self._gamma), math.sqrt(self._c)
+        if q == 0:
+            out = torch.zeros(S, m, dtype=wdt, device=A.device)
+            return out if dim == COLUMNWISE else out.t().contiguous()
+        W = torch.empty(q, S, m, dtype=wdt, device=A.device)
         for i, cw in enumerate(self.cwts):
-            W = _hs.apply_dense(cw._hd, X, 0) * sg
-            W[int(self.hash_idx[i])] += sc * float(self.hash_val[i])
-            FW = torch.fft.rfft(W, dim=0)
-            P = FW if P is None else P * FW
-        out = torch.fft.irfft(P, n=self._S, dim=0) if P is not None else torch.zeros(self._S, m, dtype=wdt, device=A.device)
+            W[i] = (_hs.apply_csr_dense_out(cw._hd, X, 0) if sparse else _hs.apply_dense(cw._hd, X, 0)).to(wdt)
+        F = torch.fft.rfft(W, dim=1)                      # q x (S/2+1) x m
+        del W
+        K = F.shape[1]
+        if F.is_cuda and F.dtype == torch.complex64:
+            import ctypes as C
+            from ..ops import _lib
+            _lib.require()
+            F = F.contiguous()
+            P = torch.empty(K, m, dtype=torch.complex64, device=A.device)
+            idx = self.hash_idx.to(device=A.device, dtype=torch.int64).contiguous()
+            hv = self.hash_val.to(device=A.device, dtype=torch.float64).contiguous()
+            _lib.call("sl_ppt_product", _lib.ptr(F), q, K, m, S, _lib.ptr(idx), _lib.ptr(hv), sg, sc, _lib.ptr(P),
+                      C.c_void_p(_lib.stream_of(F)))
+        else:
+            kk = torch.arange(K, dtype=torch.float64, device=A.device)
+            P = None
+            for i in range(q):
+                e = torch.remainder(kk * int(self.hash_idx[i]), S)
+                delta = sc * float(self.hash_val[i]) * torch.exp(torch.complex(torch.zeros_like(e), -2 * math.pi * e / S))
+                Fi = sg * F[i] + delta.to(F.dtype)[:, None]
+                P = Fi if P is None else P * Fi
+        out = torch.fft.irfft(P, n=S, dim=0).to(wdt)
         return out if dim == COLUMNWISE else out.t().contiguous()
 
     def _apply_sparse(self, A, dim, sparse_out):
-        return self._apply_dense(A.to_dense(), dim)
+        return self._apply_dense(A, dim)
 
     def apply_local_shard(self, A_local, dim, in_offset, out_rows=None):
-        if A_local.layout == torch.sparse_csr:
-            A_local = A_local.to_dense()
         return self._apply_dense(A_local, dim, in_offset)
 
     def _extra_params(self):

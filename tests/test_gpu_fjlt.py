@@ -1,0 +1,52 @@
+"""GPU FJLT with many samples (fused D-scale/reorder -> rocFFT rfft -> sampled
+post-twiddle gather) against the fp64 explicit operator sqrt(N/S) P F D."""
+import pytest
+import torch
+
+import libskylark_amd as sk
+from libskylark_amd.ops import fut
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,m,S,dim,dt", [(4096, 64, 600, 0, torch.float32), (3001, 40, 700, 0, torch.float32),
+                                          (2048, 33, 512, 1, torch.float32), (1999, 20, 300, 1, torch.bfloat16),
+                                          (1000, 16, 999, 0, torch.bfloat16)])
+def test_fjlt_sampled_gpu_vs_operator(dev, N, m, S, dim, dt):
+    g = torch.Generator().manual_seed(N)
+    A = torch.randn(N, m, generator=g, dtype=torch.float64) if dim == 0 else \
+        torch.randn(m, N, generator=g, dtype=torch.float64)
+    d = torch.where(torch.rand(N, generator=g) < 0.5, -1.0, 1.0).double()
+    samples = torch.randint(0, N, (S,), generator=g)
+    scale = (N / S) ** 0.5
+    W = fut.dct2_rows_matrix(N, samples, dtype=torch.float64, d=d, scale=scale)   # S x N, fp64, host
+    Ad = A.to(dt).double()
+    ref = W @ Ad if dim == 0 else Ad @ W.t()
+    got = fut.fjlt_sampled(A.to(dev, dt), dim, d, samples, scale).double().cpu()
+    err = float((got - ref).norm() / ref.norm())
+    assert err < 2e-6, err
+
+
+@pytest.mark.gpu
+def test_fjlt_sketch_large_s_gpu(dev):
+    """The FJLT sketch class routes S > 256 through the sampled pipeline."""
+    A = torch.randn(5000, 12, dtype=torch.float64)
+    S = sk.sketch.FJLT(5000, 800, context=sk.Context(7))
+    ref = S.realize(torch.float64) @ A
+    got = S.apply(A.float().to(dev), dim=sk.sketch.COLUMNWISE).double().cpu()
+    assert float((got - ref).norm() / ref.norm()) < 2e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,S", [(3, 256), (2, 1000)])
+def test_ppt_gpu_fused_product(dev, q, S):
+    g = torch.Generator().manual_seed(S)
+    A = torch.randn(300, 40, generator=g, dtype=torch.float64)
+    P = sk.sketch.PPT(300, S, q=q, c=1.0, gamma=0.5, context=sk.Context(3))
+    ref = P.apply(A, dim=sk.sketch.COLUMNWISE)                 # fp64 CPU (folded-spectrum torch path)
+    got = P.apply(A.float().to(dev), dim=sk.sketch.COLUMNWISE).double().cpu()
+    assert float((got - ref).norm() / ref.norm()) < 1e-4
+    As = A.clone()
+    As[As.abs() < 1.0] = 0
+    got_s = P.apply(As.float().to(dev).to_sparse_csr(), dim=sk.sketch.COLUMNWISE).double().cpu()
+    ref_s = P.apply(As, dim=sk.sketch.COLUMNWISE)
+    assert float((got_s - ref_s).norm() / ref_s.norm()) < 1e-4

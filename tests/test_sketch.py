@@ -264,3 +264,32 @@ def test_fastfood_perms_are_permutations():
         assert sorted(p.tolist()) == list(range(512))
     G = sk.sketch.FastGaussianRFT(512, 2048, sigma=2.0, context=sk.Context(4))
     assert torch.equal(F.perms, G.perms)
+
+
+def _ppt_reference(P, A):
+    """Reference loop (sketch/PPT_Elemental.hpp:140-185), fp64."""
+    import math
+    from libskylark_amd.ops import hash_sketch as hs
+    X = A.double()
+    Pr = None
+    for i, cw in enumerate(P.cwts):
+        W = hs.apply_dense(cw._hd, X, 0).double() * math.sqrt(P._gamma)
+        W[int(P.hash_idx[i])] += math.sqrt(P._c) * float(P.hash_val[i])
+        F = torch.fft.rfft(W, dim=0)
+        Pr = F if Pr is None else Pr * F
+    return torch.fft.irfft(Pr, n=P._S, dim=0)
+
+
+@pytest.mark.parametrize("q,S", [(3, 64), (2, 33), (1, 16)])
+def test_ppt_folded_spectrum_matches_reference_loop(q, S):
+    g = torch.Generator().manual_seed(q * 100 + S)
+    A = torch.randn(50, 7, generator=g, dtype=torch.float64)
+    P = sk.sketch.PPT(50, S, q=q, c=0.7, gamma=0.3, context=sk.Context(11))
+    ref = _ppt_reference(P, A)
+    torch.testing.assert_close(P.apply(A, dim=sk.sketch.COLUMNWISE), ref, rtol=1e-10, atol=1e-10)
+    torch.testing.assert_close(P.apply(A.t().contiguous(), dim=sk.sketch.ROWWISE), ref.t(), rtol=1e-10, atol=1e-10)
+    # sparse input is sketched without densifying and gives the same result
+    As = A.clone()
+    As[As.abs() < 0.8] = 0
+    torch.testing.assert_close(P.apply(As.to_sparse_csr(), dim=sk.sketch.COLUMNWISE), _ppt_reference(P, As),
+                               rtol=1e-10, atol=1e-10)
