@@ -31,6 +31,7 @@ def main(argv=None):
     ap.add_argument("--cond", type=float, default=1e4)
     ap.add_argument("--oversample", type=int, default=4)
     ap.add_argument("--tol", type=float, default=1e-6)
+    ap.add_argument("--classic", action="store_true", help="two products per Krylov iteration (no fused A^T A pass)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed full solves first (library init, kernel loads)")
     a = ap.parse_args(argv)
     import libskylark_amd as sk
@@ -62,7 +63,8 @@ def main(argv=None):
         t0 = time.perf_counter()
         solver = AcceleratedRegressionSolver(RegressionProblem(A), sk.Context(7), method="lsrn", precond="qr",
                                              oversample=a.oversample,
-                                             params=KrylovIterParams(tolerance=a.tol, iter_lim=300))
+                                             params=KrylovIterParams(tolerance=a.tol, iter_lim=300,
+                                                                             fused_normal=False if a.classic else None))
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         X, code = solver.solve(b_loc)
@@ -85,6 +87,7 @@ def main(argv=None):
                           "setup_s": round(float(tt[0]), 4), "solve_s": round(float(tt[1]), 4),
                           "warmup_runs": a.warmup, "cold_first_run_s": cold,
                           "method": "chebyshev" if not use_lsqr else "lsqr", "code": int(code),
+                          "krylov_form": "classic" if a.classic else "normal (fused A^T A pass)",
                           "rel_residual": float((st[0] / st[1]).sqrt()), "rel_x_error": xerr,
                           "config": {"rows_per_gpu": m_loc, "cols": n, "cond": a.cond,
                                      "sketch": f"JLT t={a.oversample}n (bf16x2)", "precond": "QR of sketch",

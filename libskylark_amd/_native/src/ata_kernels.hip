@@ -1,0 +1,160 @@
+// One-pass normal-equations product for tall f32 operators: W = A^T (A Y)
+// (and optionally Y_out = A Y), A m x n row-major with n up to 6144, Y n x K
+// with K in {1, 2, 4}.
+//
+// Reference hot loops: LSQR's A Z then A^T U (algorithms/Krylov/LSQR.hpp
+// :113-248) and the Chebyshev semi-iteration's A^T R / A V pair
+// (algorithms/Krylov/Chebyshev.hpp:18-85) each read A twice per iteration;
+// both only need A^T A applied to a short block (the residual recurrences
+// move to n-space, see algorithms/krylov.py), so one streaming read of A
+// per iteration suffices -- half the HBM traffic of the Krylov phase of
+// LSRN (1.25e6 x 5e3 f32 = 25 GB per GPU per read).
+//
+// gfx950 design: 256-thread workgroups, thread t owns the columns
+// t, t + 256, ... (J per thread) and keeps its slice of Y and of the W
+// accumulators in registers for the whole kernel; rows stream in blocks of
+// BM = 4 (coalesced 4-B loads, 1 KB per wave-instruction), the BM x K dots
+// are reduced across the workgroup (DPP/shuffle inside a wave, LDS across the
+// 4 waves, one barrier), then every thread updates its W slice.  Several
+// workgroups per CU hide the load latency; per-workgroup W partial slabs are
+// summed by the shared slab-reduce kernel.
+#include "sl_common.hpp"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int BM = 4;
+
+template <int J, int K, bool STORE_Y>
+__global__ void __launch_bounds__(NT, 2)
+k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Y,
+           float* __restrict__ Wslab, float* __restrict__ Yout, int64_t ldyo) {
+  __shared__ float red[NT / 64][BM * K];
+  __shared__ float yrow[BM * K];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float yv[J][K], wacc[J][K];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = tid + NT * j;
+#pragma unroll
+    for (int kk = 0; kk < K; ++kk) {
+      yv[j][kk] = c < n ? Y[(int64_t)c * K + kk] : 0.f;
+      wacc[j][kk] = 0.f;
+    }
+  }
+  const int64_t nblk = (m + BM - 1) / BM;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t r0 = blk * BM;
+    float a[BM][J];
+#pragma unroll
+    for (int b = 0; b < BM; ++b) {
+      const int64_t r = r0 + b < m ? r0 + b : m - 1;
+      const float* row = A + r * lda;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int c = tid + NT * j;
+        a[b][j] = (c < n && r0 + b < m) ? row[c] : 0.f;
+      }
+    }
+    float p[BM][K];
+#pragma unroll
+    for (int b = 0; b < BM; ++b)
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < J; ++j) s = fmaf(a[b][j], yv[j][kk], s);
+        // wave reduction
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+        p[b][kk] = s;
+      }
+    if (lane == 0) {
+#pragma unroll
+      for (int b = 0; b < BM; ++b)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) red[wave][b * K + kk] = p[b][kk];
+    }
+    __syncthreads();
+    if (tid < BM * K) {
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < NT / 64; ++v) s += red[v][tid];
+      yrow[tid] = s;
+      if (STORE_Y) {
+        const int b = tid / K, kk = tid - (tid / K) * K;
+        if (r0 + b < m) Yout[(r0 + b) * ldyo + kk] = s;
+      }
+    }
+    __syncthreads();
+    float yr[BM][K];
+#pragma unroll
+    for (int b = 0; b < BM; ++b)
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) yr[b][kk] = yrow[b * K + kk];
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) {
+        float w = wacc[j][kk];
+#pragma unroll
+        for (int b = 0; b < BM; ++b) w = fmaf(a[b][j], yr[b][kk], w);
+        wacc[j][kk] = w;
+      }
+  }
+  float* ws = Wslab + (int64_t)blockIdx.x * n * K;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int c = tid + NT * j;
+    if (c < n) {
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) ws[(int64_t)c * K + kk] = wacc[j][kk];
+    }
+  }
+}
+
+int ata_grid() {
+  static int ncu = -1;
+  if (ncu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  return 2 * ncu;
+}
+
+}  // namespace
+
+int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows, int cols,
+                          float* out, int ld_out, hipStream_t s);
+
+SL_API int64_t sl_ata_workspace(int64_t n, int k) { return (int64_t)ata_grid() * n * k * 4 + 256; }
+
+// W (n x k, row-major) = A^T (A Y); Yout (m x k, ld ldyo) = A Y when non-null.
+SL_API int sl_ata_pass(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
+                       float* Yout, int64_t ldyo, void* ws, void* stream) {
+  if (m <= 0 || n <= 0) return SL_OK;
+  const int64_t Jn = (n + NT - 1) / NT;
+  // register budget (no spills): J <= 8 any k, J <= 16 k <= 2, J <= 24 k == 1
+  if (n > 6144 || !(k == 1 || k == 2 || k == 4) || (Jn > 8 && k == 4) || (Jn > 16 && k > 1)) {
+    sl_set_last_error("ata_pass: needs n <= 6144, k in {1, 2, 4} (k <= 2 past n = 2048, k = 1 past 4096)");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int g = (int)std::min<int64_t>((int64_t)ata_grid(), (m + BM - 1) / BM);
+  float* slab = (float*)ws;
+  const int J = (int)((n + NT - 1) / NT);
+#define SL_ATA(JJ, KK)                                                                                   \
+  if (Yout) k_ata_pass<JJ, KK, true><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo);           \
+  else k_ata_pass<JJ, KK, false><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo);
+#define SL_ATA_K(JJ) \
+  if (k == 1) { SL_ATA(JJ, 1) } else if (k == 2) { SL_ATA(JJ, 2) } else { SL_ATA(JJ, 4) }
+  if (J <= 4) { SL_ATA_K(4) }
+  else if (J <= 8) { SL_ATA_K(8) }
+  else if (J <= 16) { if (k == 1) { SL_ATA(16, 1) } else { SL_ATA(16, 2) } }
+  else { SL_ATA(24, 1) }
+#undef SL_ATA_K
+#undef SL_ATA
+  SL_LAUNCH_CHECK();
+  return sl_slab_reduce_launch(slab, g, n * k, k, (int)n, k, W, k, s);
+}

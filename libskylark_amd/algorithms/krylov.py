@@ -9,7 +9,22 @@ convergence, -6 limit), ``FlexibleCG.hpp``, ``Chebyshev.hpp:18-85``,
 All k right-hand sides advance together; every per-column scalar lives in a
 length-k device tensor, so an iteration is a handful of fused element-wise
 ops, one ``A Z`` and one ``A^T U`` (+ one all-reduce of n x k when A is
-row-distributed) and ONE host synchronisation (the convergence test).
+row-distributed) and a host synchronisation only every ``check_every``
+iterations (the convergence test).
+
+Normal form (LSQR and Chebyshev, ``KrylovIterParams.fused_normal``): both
+methods only ever need ``A^T`` of the NEW long vector, which is a linear
+combination of ``A Z`` and vectors whose ``A^T`` image is already known, so the
+recurrences are carried in n-space:
+
+* LSQR: ``U' = (A Z - alpha U) / beta``  =>  ``A^T U' = (A^T A Z - alpha A^T U) / beta``;
+* Chebyshev: ``R' = R - alpha A PV``     =>  ``A^T R' = A^T R - alpha A^T A PV``;
+
+and ``(A^T A Z, A Z)`` comes from ONE streaming read of A (``ops/normal_eq.py``,
+``ata_kernels.hip``), halving the HBM traffic of an iteration (A is read
+twice per iteration in the reference, ``LSQR.hpp:113-248``,
+``Chebyshev.hpp:18-85``).  The carried ``A^T U`` is replaced by the exact
+product every ``refresh_every`` iterations to bound the drift.
 """
 from __future__ import annotations
 
@@ -30,6 +45,13 @@ class KrylovIterParams:
     log_level: int = 0
     prefix: str = ""
     check_every: int = 1     # convergence test every N iterations (host sync)
+    # normal-form iteration: one fused ``A^T (A Z)`` pass per iteration instead
+    # of ``A Z`` then ``A^T U`` (None = when the operator has the kernel); the
+    # n-space recurrence for A^T U is recomputed exactly every ``refresh_every``
+    # iterations (0 = never; None = 16 for LSQR, whose recurrence divides by
+    # beta, and never for Chebyshev, where a refresh costs two passes)
+    fused_normal: bool | None = None
+    refresh_every: int | None = None
 
 
 krylov_iter_params_t = KrylovIterParams
@@ -152,9 +174,14 @@ def lsqr(A, B, X=None, params: KrylovIterParams | None = None, R: Precond | None
     iter_lim = params.iter_lim if params.iter_lim >= 0 else max(20, 2 * min(m, n))
     X = torch.zeros(n, k, dtype=dt, device=dev) if X is None else X.to(dt)
 
+    fused = params.fused_normal
+    if fused is None:
+        fused = op.has_fused_normal(k)
+    refresh = 16 if params.refresh_every is None else max(0, int(params.refresh_every))
     beta = op.long_colnorm(U)
     U = U / beta.clamp_min(torch.finfo(dt).tiny)
-    V = R.apply_adjoint(op.rmatmul(U))
+    T = op.rmatmul(U).to(dt)       # A^T U (carried in n-space in normal form)
+    V = R.apply_adjoint(T)
     alpha = op.short_colnorm(V)
     V = V / alpha.clamp_min(torch.finfo(dt).tiny)
     Z = R.apply(V.clone())
@@ -178,13 +205,21 @@ def lsqr(A, B, X=None, params: KrylovIterParams | None = None, R: Precond | None
     code = -6
     for itn in range(iter_lim):
         # 1. U = A Z - alpha U, beta = |U|
-        U = op.matmul(Z).to(dt) - alpha * U
+        if fused:
+            G, AZ = op.normal(Z, want_y=True)
+            U = AZ.to(dt) - alpha * U
+        else:
+            U = op.matmul(Z).to(dt) - alpha * U
         beta = op.long_colnorm(U)
         U = U / beta
         # 2. norm(A) estimate
         nrm_a = torch.sqrt(nrm_a * nrm_a + alpha * alpha + beta * beta)
         # 3. V = P^T A^T U - beta V
-        V = R.apply_adjoint(op.rmatmul(U).to(dt)) - beta * V
+        if not fused or (refresh and (itn + 1) % refresh == 0):
+            T = op.rmatmul(U).to(dt)
+        else:
+            T = (G.to(dt) - alpha * T) / beta
+        V = R.apply_adjoint(T) - beta * V
         alpha = op.short_colnorm(V)
         V = V / alpha
         Z = R.apply(V.clone())
@@ -357,7 +392,9 @@ def chebyshev_ls(A, B, sigma_L: float, sigma_U: float, params: KrylovIterParams 
                  P: Precond | None = None):
     """Chebyshev semi-iteration for least squares given singular value bounds of
     ``A P`` (LSRN).  Reference ``algorithms/Krylov/Chebyshev.hpp:18-85``.
-    No inner products: one ``A^T R`` and one ``A V`` per iteration."""
+    No inner products: one ``A^T R`` and one ``A V`` per iteration, or one
+    fused ``A^T A PV`` in normal form (the exact ``A^T (B - A X)`` is re-formed
+    every ``params.refresh_every`` iterations, two passes)."""
     op = as_operator(A)
     params = params or KrylovIterParams()
     P = P or IdPrecond()
@@ -373,6 +410,12 @@ def chebyshev_ls(A, B, sigma_L: float, sigma_U: float, params: KrylovIterParams 
     c = (sigma_U * sigma_U - sigma_L * sigma_L) / 2
     X = torch.zeros(n, k, dtype=dt, device=Rr.device)
     V = None  # search direction in the preconditioned (y = P^{-1} x) space
+    fused = params.fused_normal
+    if fused is None:
+        fused = op.has_fused_normal(k)
+    refresh = 0 if params.refresh_every is None else max(0, int(params.refresh_every))
+    T = op.rmatmul(Rr).to(dt) if fused else None     # A^T R carried in n-space
+    B0 = Rr if fused and refresh else None
     alpha = beta = 0.0
     i = 0
     while i < its:
@@ -384,11 +427,19 @@ def chebyshev_ls(A, B, sigma_L: float, sigma_U: float, params: KrylovIterParams 
         else:
             beta = alpha * alpha * c * c / 4.0
             alpha = 1 / (d - alpha * c * c / 4.0)
-        AR = P.apply_adjoint(op.rmatmul(Rr).to(dt))
+        if fused:
+            if refresh and i > 0 and i % refresh == 0:
+                T = op.rmatmul(B0 - op.matmul(X).to(dt)).to(dt)
+            AR = P.apply_adjoint(T)
+        else:
+            AR = P.apply_adjoint(op.rmatmul(Rr).to(dt))
         V = AR if V is None else beta * V + AR
         PV = P.apply(V)
         X = X + alpha * PV
-        Rr = Rr - alpha * op.matmul(PV).to(dt)
+        if fused:
+            T = T - alpha * op.normal(PV)[0].to(dt)
+        else:
+            Rr = Rr - alpha * op.matmul(PV).to(dt)
         i += 1
     return X
 

@@ -62,6 +62,14 @@ class Operator:
     def local_rows(self):
         return self.shape[0]
 
+    # (A^T A X, A X or None); operators with a one-pass kernel override this
+    def normal(self, X, want_y: bool = False):
+        Y = self.matmul(X)
+        return self.rmatmul(Y), (Y if want_y else None)
+
+    def has_fused_normal(self, k: int) -> bool:
+        return False
+
 
 class DenseOp(Operator):
     def __init__(self, A: torch.Tensor, compute_dtype=None):
@@ -84,6 +92,17 @@ class DenseOp(Operator):
                         torch.mm(self.A.t(), lo, out_dtype=torch.float32)).to(self.dtype)
             return (self.A.t().float() @ (hi.float() + lo.float())).to(self.dtype)
         return self.A.t() @ Y.to(self.A.dtype)
+
+    def has_fused_normal(self, k: int) -> bool:
+        from ..ops import normal_eq
+        return normal_eq.native_ok(self.A, k)
+
+    def normal(self, X, want_y: bool = False):
+        if self.has_fused_normal(X.shape[1]):
+            from ..ops import normal_eq
+            W, Y = normal_eq.ata(self.A, X, want_y)
+            return W.to(self.dtype), (Y.to(self.dtype) if Y is not None else None)
+        return super().normal(X, want_y)
 
 
 class SparseOp(Operator):
@@ -128,6 +147,17 @@ class DistRowOp(Operator):
 
     def local_rows(self):
         return self.D.local.shape[0]
+
+    def has_fused_normal(self, k: int) -> bool:
+        return self.inner.has_fused_normal(k)
+
+    def normal(self, X, want_y: bool = False):
+        """Local one-pass A_loc^T (A_loc X) + ONE all-reduce of n x k."""
+        W, Y = self.inner.normal(X, want_y)
+        W = W.contiguous()
+        if self.distributed:
+            self.comm.all_reduce(W)
+        return W, Y
 
     def long_like(self, B):
         # B may be given globally (replicated m x k) or already as the local shard

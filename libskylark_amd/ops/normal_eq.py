@@ -1,0 +1,52 @@
+"""One-pass ``A^T (A Y)`` for tall f32 operators (``ata_kernels.hip``).
+
+Used by the Krylov solvers (LSQR, Chebyshev) so that an iteration reads A
+once instead of twice (reference loops ``algorithms/Krylov/LSQR.hpp:113-248``,
+``Chebyshev.hpp:18-85``).  Falls back to two products where the kernel does
+not apply (CPU, f64, sparse, wide n, k > 4).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+_lib.register("sl_ata_pass", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, vp])
+_lib.register("sl_ata_workspace", [i64, i32], C.c_int64)
+
+_WS: dict = {}
+
+
+def native_ok(A: torch.Tensor, k: int) -> bool:
+    if not (isinstance(A, torch.Tensor) and A.is_cuda and A.dtype == torch.float32 and A.dim() == 2
+            and A.layout == torch.strided and A.stride(1) == 1 and _lib.available()):
+        return False
+    n = A.shape[1]
+    J = -(-n // 256)
+    if n > 6144 or k not in (1, 2, 4) or (J > 8 and k == 4) or (J > 16 and k > 1):
+        return False
+    return True
+
+
+def ata(A: torch.Tensor, Y: torch.Tensor, want_y: bool = False):
+    """``(A^T (A Y), A Y or None)`` for the local block A (m x n) and Y (n x k).
+    Partial over a row shard: the caller all-reduces the first result."""
+    k = Y.shape[1]
+    if native_ok(A, k):
+        m, n = A.shape
+        Yc = Y.to(torch.float32).contiguous()
+        W = torch.empty(n, k, dtype=torch.float32, device=A.device)
+        Yo = torch.empty(m, k, dtype=torch.float32, device=A.device) if want_y else None
+        nb = int(_lib.require().sl_ata_workspace(n, k))
+        key = str(A.device)
+        ws = _WS.get(key)
+        if ws is None or ws.numel() < nb:
+            ws = _WS[key] = torch.empty(nb, dtype=torch.uint8, device=A.device)
+        _lib.call("sl_ata_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Yc), k, _lib.ptr(W),
+                  _lib.ptr(Yo) if Yo is not None else None, k, _lib.ptr(ws), vp(_lib.stream_of(A)))
+        return W, Yo
+    AY = A @ Y.to(A.dtype)
+    return A.t() @ AY, (AY if want_y else None)

@@ -1,0 +1,71 @@
+"""One-pass ``A^T (A Y)`` kernel (ata_kernels.hip) against an fp64 torch
+reference, and the normal-form LSQR / Chebyshev iterations built on it
+against the classic two-product iterations."""
+import math
+
+import pytest
+import torch
+
+from libskylark_amd.algorithms import krylov as K
+from libskylark_amd.ops import normal_eq
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(10007, 100, 1), (10007, 1000, 4), (4099, 2048, 4), (20001, 3000, 2),
+                                   (7, 5000, 1), (30011, 5000, 1), (513, 6144, 1), (1, 257, 2)])
+def test_ata_pass_vs_fp64(dev, m, n, k):
+    g = torch.Generator().manual_seed(m + n + k)
+    A = torch.randn(m, n, generator=g)
+    Y = torch.randn(n, k, generator=g)
+    Ag = A.to(dev)
+    assert normal_eq.native_ok(Ag, k)
+    W, AY = normal_eq.ata(Ag, Y.to(dev), want_y=True)
+    torch.cuda.synchronize()
+    Yr = A.double() @ Y.double()
+    Wr = A.double().t() @ Yr
+    ew = float((W.double().cpu() - Wr).norm() / Wr.norm())
+    ey = float((AY.double().cpu() - Yr).norm() / Yr.norm())
+    assert ew < 1e-5 and ey < 1e-5, (ew, ey)
+    W2, none = normal_eq.ata(Ag, Y.to(dev), want_y=False)
+    assert none is None
+    assert torch.equal(W2, W)   # deterministic: fixed slab order
+
+
+@pytest.mark.gpu
+def test_ata_strided_rows(dev):
+    """lda > n (a column slice of a wider matrix)."""
+    g = torch.Generator().manual_seed(3)
+    big = torch.randn(5000, 1200, generator=g)
+    A = big.to(dev)[:, :1000]
+    Y = torch.randn(1000, 2, generator=g)
+    W, _ = normal_eq.ata(A, Y.to(dev))
+    Wr = big[:, :1000].double().t() @ (big[:, :1000].double() @ Y.double())
+    assert float((W.double().cpu() - Wr).norm() / Wr.norm()) < 1e-5
+
+
+@pytest.mark.gpu
+def test_normal_form_krylov_matches_classic(dev):
+    from libskylark_amd.algorithms.regression import _build_precond
+    g = torch.Generator().manual_seed(0)
+    m, n = 40000, 300
+    A = (torch.randn(m, n, generator=g) * torch.logspace(0, -4, n)).to(dev)
+    x = torch.randn(n, 1, generator=g).to(dev)
+    b = A @ x + 1e-3 * torch.randn(m, 1, generator=g).to(dev)
+    S = torch.randn(4 * n, m, generator=g).to(dev) / math.sqrt(4 * n)
+    P, _ = _build_precond(S @ A, "qr")
+    t = 4 * n
+    al = math.sqrt(2 * math.log(2e6) / t)
+    sU = math.sqrt(t) / ((1 - al) * math.sqrt(t) - math.sqrt(n))
+    sL = math.sqrt(t) / ((1 + al) * math.sqrt(t) + math.sqrt(n))
+    out = {}
+    for fused in (False, True):
+        p = K.KrylovIterParams(tolerance=1e-6, iter_lim=200, fused_normal=fused, check_every=5)
+        Xc = K.chebyshev_ls(A, b, sL, sU, p, P)
+        Xl, code = K.lsqr(A, b, params=p, R=P)
+        out[fused] = (Xc, Xl, code)
+    assert out[True][2] in (-2, -3)
+    for i in (0, 1):
+        d = float((out[True][i] - out[False][i]).norm() / out[False][i].norm())
+        assert d < 1e-3, (i, d)
+    r = float((A @ out[True][0] - b).norm() / (A @ out[False][0] - b).norm())
+    assert abs(r - 1) < 1e-4
