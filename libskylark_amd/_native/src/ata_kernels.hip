@@ -25,10 +25,13 @@ namespace {
 constexpr int NT = 256;
 constexpr int BM = 4;
 
-template <int J, int K, bool STORE_Y>
+// DUAL: the W update uses a GIVEN long block D (W = A^T D) instead of A Y;
+// with STORE_Y the pass still emits A Y (the BlockADMM pair {Z Wbar, Z^T d}).
+template <int J, int K, bool STORE_Y, bool DUAL>
 __global__ void __launch_bounds__(NT, 2)
 k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Y,
-           float* __restrict__ Wslab, float* __restrict__ Yout, int64_t ldyo) {
+           float* __restrict__ Wslab, float* __restrict__ Yout, int64_t ldyo,
+           const float* __restrict__ Dm, int64_t ldd_r, int64_t ldd_c) {
   __shared__ float red[NT / 64][BM * K];
   __shared__ float yrow[BM * K];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -38,7 +41,7 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
     const int c = tid + NT * j;
 #pragma unroll
     for (int kk = 0; kk < K; ++kk) {
-      yv[j][kk] = c < n ? Y[(int64_t)c * K + kk] : 0.f;
+      yv[j][kk] = (c < n && !(DUAL && !STORE_Y)) ? Y[(int64_t)c * K + kk] : 0.f;
       wacc[j][kk] = 0.f;
     }
   }
@@ -56,6 +59,13 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
         a[b][j] = (c < n && r0 + b < m) ? row[c] : 0.f;
       }
     }
+    float yr[BM][K];
+    if (DUAL && !STORE_Y) {
+#pragma unroll
+      for (int b = 0; b < BM; ++b)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) yr[b][kk] = r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f;
+    } else {
     float p[BM][K];
 #pragma unroll
     for (int b = 0; b < BM; ++b)
@@ -87,11 +97,12 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
       }
     }
     __syncthreads();
-    float yr[BM][K];
 #pragma unroll
     for (int b = 0; b < BM; ++b)
 #pragma unroll
-      for (int kk = 0; kk < K; ++kk) yr[b][kk] = yrow[b * K + kk];
+      for (int kk = 0; kk < K; ++kk)
+        yr[b][kk] = DUAL ? (r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f) : yrow[b * K + kk];
+    }
 #pragma unroll
     for (int j = 0; j < J; ++j)
 #pragma unroll
@@ -130,9 +141,11 @@ int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int
 
 SL_API int64_t sl_ata_workspace(int64_t n, int k) { return (int64_t)ata_grid() * n * k * 4 + 256; }
 
-// W (n x k, row-major) = A^T (A Y); Yout (m x k, ld ldyo) = A Y when non-null.
-SL_API int sl_ata_pass(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
-                       float* Yout, int64_t ldyo, void* ws, void* stream) {
+// W (n x k, row-major) = A^T (A Y) -- or A^T D when D is non-null (D(r, c) at
+// D[r * ldd_r + c * ldd_c]); Yout (m x k, ld ldyo) = A Y when non-null.
+SL_API int sl_ata_pass2(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
+                        float* Yout, int64_t ldyo, const float* D, int64_t ldd_r, int64_t ldd_c, void* ws,
+                        void* stream) {
   if (m <= 0 || n <= 0) return SL_OK;
   const int64_t Jn = (n + NT - 1) / NT;
   // register budget (no spills): J <= 8 any k, J <= 16 k <= 2, J <= 24 k == 1
@@ -144,9 +157,14 @@ SL_API int sl_ata_pass(const float* A, int64_t m, int64_t n, int64_t lda, const 
   const int g = (int)std::min<int64_t>((int64_t)ata_grid(), (m + BM - 1) / BM);
   float* slab = (float*)ws;
   const int J = (int)((n + NT - 1) / NT);
-#define SL_ATA(JJ, KK)                                                                                   \
-  if (Yout) k_ata_pass<JJ, KK, true><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo);           \
-  else k_ata_pass<JJ, KK, false><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo);
+#define SL_ATA_GO(JJ, KK, SY, DU) \
+  k_ata_pass<JJ, KK, SY, DU><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo, D, ldd_r, ldd_c);
+#define SL_ATA(JJ, KK)                                                      \
+  if (D) {                                                                  \
+    if (Yout) { SL_ATA_GO(JJ, KK, true, true) } else { SL_ATA_GO(JJ, KK, false, true) } \
+  } else {                                                                  \
+    if (Yout) { SL_ATA_GO(JJ, KK, true, false) } else { SL_ATA_GO(JJ, KK, false, false) } \
+  }
 #define SL_ATA_K(JJ) \
   if (k == 1) { SL_ATA(JJ, 1) } else if (k == 2) { SL_ATA(JJ, 2) } else { SL_ATA(JJ, 4) }
   if (J <= 4) { SL_ATA_K(4) }
@@ -155,6 +173,12 @@ SL_API int sl_ata_pass(const float* A, int64_t m, int64_t n, int64_t lda, const 
   else { SL_ATA(24, 1) }
 #undef SL_ATA_K
 #undef SL_ATA
+#undef SL_ATA_GO
   SL_LAUNCH_CHECK();
   return sl_slab_reduce_launch(slab, g, n * k, k, (int)n, k, W, k, s);
+}
+
+SL_API int sl_ata_pass(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
+                       float* Yout, int64_t ldyo, void* ws, void* stream) {
+  return sl_ata_pass2(A, m, n, lda, Y, k, W, Yout, ldyo, nullptr, 0, 0, ws, stream);
 }

@@ -46,6 +46,51 @@ __global__ void __launch_bounds__(256) k_fill_random(T* __restrict__ out, FillAr
   }
 }
 
+// Fast N(0,1) realisation for views whose fast dimension is contiguous (the
+// dense-sketch panels: LSRN's 2e4 x 1.3e4 bf16 panels, 2.5e10 normals per
+// 1.25e6-row sketch).  Same samples bit for bit as k_fill_random<T, true>;
+// what changes is the index arithmetic: each thread owns 8 consecutive
+// elements of one line (one 32-bit divide per 8 samples instead of a 64-bit
+// divide + multiplies per sample), the stream index advances by an add, and
+// the 8 results leave as one 16-B (bf16) or two 16-B (f32) stores.
+template <typename T>
+__global__ void __launch_bounds__(256) k_fill_normal_lines(T* __restrict__ out, uint64_t seed, uint64_t base0,
+                                                           uint32_t nlines, uint32_t ngrp, int64_t nfast, int64_t ld,
+                                                           int64_t s_line, int64_t s_fast, float scale) {
+  const uint32_t total = nlines * ngrp;
+  for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+    const uint32_t l = t / ngrp, g = t - l * ngrp;
+    const int64_t f = (int64_t)g * 8;
+    uint64_t idx = base0 + (uint64_t)((int64_t)l * s_line + f * s_fast);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = scale * sl::normal_f(seed, idx);
+      idx += (uint64_t)s_fast;
+    }
+    T* p = out + (int64_t)l * ld + f;
+    if (f + 8 <= nfast && (((uintptr_t)p) & 15) == 0) {
+      if constexpr (sizeof(T) == 2) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w[j] = (uint32_t)Cvt<T>::from_f(v[2 * j]) | ((uint32_t)Cvt<T>::from_f(v[2 * j + 1]) << 16);
+        *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (f + j < nfast) p[j] = Cvt<T>::from_f(v[j]);
+    }
+  }
+}
+
+static int g_fast_lines = 1;   // 0: always the generic kernel (A/B tests)
+SL_API void sl_rng_set_fast_lines(int on) { g_fast_lines = on; }
+
 // precise != 0 forces the double-precision sampler for fp32/bf16 outputs.
 SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_t base,
                           int64_t rows, int64_t cols, int64_t sr, int64_t sc, int64_t r0,
@@ -55,6 +100,25 @@ SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_
   FillArgs a{dist, seed, base, rows, cols, sr, sc, r0, c0, ir, ic, p0, p1, scale};
   unsigned grid = sl_grid_for((size_t)(rows * cols), 256, 4096);
   hipStream_t s = (hipStream_t)stream;
+  if (g_fast_lines && dist == sl::DIST_NORMAL && !precise && (dtype == SL_F32 || dtype == SL_BF16) && (sc == 1 || sr == 1)) {
+    // lines = the slow dimension, fast = the contiguous one
+    const bool rowmajor = sc == 1 && (sr != 1 || cols >= rows);
+    const int64_t nlines = rowmajor ? rows : cols, nfast = rowmajor ? cols : rows;
+    const int64_t ld = rowmajor ? sr : sc, s_line = rowmajor ? ir : ic, s_fast = rowmajor ? ic : ir;
+    const int64_t ngrp = (nfast + 7) / 8;
+    if (nlines * ngrp < (int64_t)0x7fffffff) {
+      const uint64_t base0 = base + (uint64_t)(r0 * ir + c0 * ic);
+      const unsigned g2 = sl_grid_for((size_t)(nlines * ngrp), 256, 8192);
+      if (dtype == SL_F32)
+        k_fill_normal_lines<float><<<g2, 256, 0, s>>>((float*)out, seed, base0, (uint32_t)nlines, (uint32_t)ngrp, nfast,
+                                                      ld, s_line, s_fast, (float)scale);
+      else
+        k_fill_normal_lines<bf16_t><<<g2, 256, 0, s>>>((bf16_t*)out, seed, base0, (uint32_t)nlines, (uint32_t)ngrp,
+                                                       nfast, ld, s_line, s_fast, (float)scale);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    }
+  }
   SL_DISPATCH_FLOAT(dtype, T, {
     if (dtype == SL_F64 || precise)
       k_fill_random<T, false><<<grid, 256, 0, s>>>((T*)out, a);

@@ -8,7 +8,11 @@ class Regularizer:
     name = "none"
 
     def evaluate(self, W: torch.Tensor) -> float:
-        return 0.0
+        return float(self.evaluate_t(W))
+
+    def evaluate_t(self, W: torch.Tensor) -> torch.Tensor:
+        """The penalty as a 0-d device tensor (no host synchronisation)."""
+        return torch.zeros((), dtype=W.dtype, device=W.device)
 
     def proxoperator(self, W: torch.Tensor, lam: float) -> torch.Tensor:
         return W
@@ -22,8 +26,8 @@ class L2Regularizer(Regularizer):
     """0.5 ||W||_F^2 ; prox = shrinkage W / (1 + lambda)."""
     name = "l2"
 
-    def evaluate(self, W):
-        return float(0.5 * (W * W).sum())
+    def evaluate_t(self, W):
+        return 0.5 * (W * W).sum()
 
     def proxoperator(self, W, lam):
         return W / (1.0 + lam)
@@ -33,8 +37,8 @@ class L1Regularizer(Regularizer):
     """||W||_1 ; prox = soft thresholding."""
     name = "l1"
 
-    def evaluate(self, W):
-        return float(W.abs().sum())
+    def evaluate_t(self, W):
+        return W.abs().sum()
 
     def proxoperator(self, W, lam):
         return torch.sign(W) * torch.clamp(W.abs() - lam, min=0)

@@ -20,6 +20,12 @@ consensus update are computed redundantly on every GPU, so Wbar is already
 replicated — no broadcast, no root bottleneck.  The loss is reduced with the
 same all-reduce (appended scalar).  Validation accuracy likewise.
 
+Per feature block and iteration Z_j is read TWICE, not four times: the pairs
+{Z Wbar_j, Z^T dsum} and {o = Z Wi_j, Z^T o} each come from one streaming
+pass (``ops/normal_eq.py``: ``dual`` and ``ata``; f32 on the GPU, k <= 4
+targets), and the loss / regulariser / validation statistics stay on the
+device until they are logged (one host transfer per logged iteration).
+
 Layout: examples as ROWS (X n_i x d); outputs O are k x n_i as in the
 reference's losses.  Feature blocks run back-to-back on the GPU (each is a
 fused RNG-GEMM + cos feature map and three GEMMs; the reference's OpenMP
@@ -36,10 +42,20 @@ from ..algorithms.loss import Loss, make_loss
 from ..algorithms.regularizers import Regularizer, make_regularizer
 from ..base import quasirand as Q
 from ..base.context import Context
+from ..ops import normal_eq
 from ..parallel.comm import Comm
 from ..parallel.distmatrix import DistMatrix
 from ..sketch import ROWWISE
 from .model import HilbertModel
+
+
+def _pad_cols(W: torch.Tensor, kp: int) -> torch.Tensor:
+    """W (n x k) zero-padded to kp columns, contiguous (one-pass kernel operand)."""
+    if W.shape[1] == kp:
+        return W.contiguous()
+    out = torch.zeros(W.shape[0], kp, dtype=W.dtype, device=W.device)
+    out[:, :W.shape[1]] = W
+    return out
 
 
 def _partition(D: int, P: int):
@@ -81,6 +97,7 @@ class BlockADMMSolver:
         self.rho, self.maxiter, self.tol = 1.0, 1000, 0.1
         self.cache_transforms = False
         self.num_threads = 1
+        self.one_pass = True      # fused Z-pair passes where the kernel applies
         if feature_maps is not None:
             self.maps = list(feature_maps)
             self.sizes = [S.get_S() for S in self.maps]
@@ -165,8 +182,13 @@ class BlockADMMSolver:
         del_o = torch.zeros(k, ni, dtype=dt, device=dev)
         cache, zcache = [None] * P, [None] * P
         Yt = Y if regression or Y.dim() == 1 else Y
+        # one-pass kernels for the two Z pairs per block (f32 on the GPU, k <= 4)
+        kp = 1 if k == 1 else (2 if k == 2 else 4)
+        fused = self.one_pass and dev.type == "cuda" and dt == torch.float32 and k <= 4
+        Dp = torch.zeros(kp, ni, dtype=dt, device=dev) if fused else None
         t0 = time.time()
         self.history = []
+        pending = []
         for it in range(1, self.maxiter + 1):
             mu_ij -= Wbar
             Obar -= nu
@@ -175,6 +197,8 @@ class BlockADMMSolver:
             sum_o = torch.zeros(k, ni, dtype=dt, device=dev)
             wbar_out = torch.zeros(k, ni, dtype=dt, device=dev)
             dsum = del_o + (P + 1.0) * nu  # k x ni
+            if fused:
+                Dp[:k] = dsum
             for j in range(P):
                 st, sj = self.starts[j], self.sizes[j]
                 if self.cache_transforms and zcache[j] is not None:
@@ -188,54 +212,79 @@ class BlockADMMSolver:
                     C.diagonal().add_(1.0)
                     cache[j] = torch.cholesky_inverse(torch.linalg.cholesky(C)).to(dt)
                 Wb = Wbar[st:st + sj]
-                wbar_out += (Z @ Wb).t()
-                rhs = Wb - mu_ij[st:st + sj] + ZtObar[st:st + sj] + (Z.t() @ dsum.t()) / (P + 1.0)
+                one_pass = fused and normal_eq.native_ok(Z, kp)
+                if one_pass:
+                    # pass 1: {Z Wbar_j, Z^T dsum^T} from one read of Z
+                    ztd, zw = normal_eq.dual(Z, Dp.t(), _pad_cols(Wb, kp))
+                    wbar_out += zw[:, :k].t()
+                    ztd = ztd[:, :k]
+                else:
+                    wbar_out += (Z @ Wb).t()
+                    ztd = Z.t() @ dsum.t()
+                rhs = Wb - mu_ij[st:st + sj] + ZtObar[st:st + sj] + ztd / (P + 1.0)
                 Wi_j = cache[j] @ rhs
                 Wi[st:st + sj] = Wi_j
-                o = (Z @ Wi_j).t()  # k x ni
+                if one_pass:
+                    # pass 2: {o = Z Wi_j, Z^T o} from one read of Z
+                    zto, zo = normal_eq.ata(Z, _pad_cols(Wi_j, kp), want_y=True)
+                    o = zo[:, :k].t()
+                    ZtObar[st:st + sj] = zto[:, :k]
+                else:
+                    o = (Z @ Wi_j).t()  # k x ni
+                    ZtObar[st:st + sj] = Z.t() @ o.t()
                 mu_ij[st:st + sj] += Wi_j
-                ZtObar[st:st + sj] = Z.t() @ o.t()
                 sum_o += o
             sum_o = O - sum_o
             del_o = sum_o.clone()
-            # ---- one all-reduce: [Wi | loss | validation stats]
-            local_loss = float(self.loss.evaluate(wbar_out, Yt))
-            acc_stats = self._validate(model, Wbar, Xv, Yv, regression) if Xv is not None else (0.0, 0.0)
-            buf = torch.cat([Wi.reshape(-1).to(torch.float64),
-                             torch.tensor([local_loss, acc_stats[0], acc_stats[1]], dtype=torch.float64,
-                                          device=dev)])
+            # ---- one all-reduce: [Wi | loss | validation stats]; all on the device
+            stats = [self.loss.evaluate_t(wbar_out, Yt).to(torch.float64)]
+            if Xv is not None:
+                stats += list(self._validate_t(model, Wbar, Xv, Yv, regression))
+            else:
+                stats += [torch.zeros((), dtype=torch.float64, device=dev)] * 2
+            buf = torch.cat([Wi.reshape(-1).to(torch.float64), torch.stack(stats)])
             if rank_count > 1:
                 comm.all_reduce(buf)
             Wsum = buf[:D * k].reshape(D, k).to(dt)
-            totalloss, s0, s1 = (float(v) for v in buf[D * k:].cpu())
-            obj = totalloss + self.lam * self.regularizer.evaluate(Wbar)
-            rec = {"iteration": it, "objective": obj, "time": time.time() - t0}
-            if Xv is not None:
-                rec["accuracy"] = math.sqrt(s0 / s1) if regression else 100.0 * s0 / max(s1, 1)
-            self.history.append(rec)
-            if log is not None and comm.rank == 0:
-                msg = f"iteration {it} objective {obj:g}"
-                if "accuracy" in rec:
-                    msg += f" accuracy {rec['accuracy']:.2f}"
-                log(msg + f" time {rec['time']:.3f} seconds")
+            tail = torch.cat([buf[D * k:], (self.lam * self.regularizer.evaluate_t(Wbar)).to(torch.float64)[None]])
+            pending.append((it, tail, time.time() - t0))
+            if log is not None:
+                rec = self._record(*pending.pop(), Xv is not None, regression)
+                if comm.rank == 0:
+                    msg = f"iteration {it} objective {rec['objective']:g}"
+                    if "accuracy" in rec:
+                        msg += f" accuracy {rec['accuracy']:.2f}"
+                    log(msg + f" time {rec['time']:.3f} seconds")
             Obar = O - sum_o / (P + 1.0)
             nu = nu + O - Obar
             Wbar = (Wsum + W) / (rank_count + 1.0)
             mu = mu + W - Wbar
             model.coef = Wbar
+        for p_ in pending:   # iterations not logged: one host transfer at the end
+            self._record(*p_, Xv is not None, regression)
+        self.history.sort(key=lambda r: r["iteration"])
         model.coef = Wbar.to(torch.float64).cpu() if not Wbar.is_cuda else Wbar.to(torch.float64)
         return model
 
+    def _record(self, it, tail, elapsed, has_val, regression):
+        totalloss, s0, s1, reg = (float(v) for v in tail.cpu())
+        rec = {"iteration": it, "objective": totalloss + reg, "time": elapsed}
+        if has_val:
+            rec["accuracy"] = math.sqrt(s0 / s1) if regression else 100.0 * s0 / max(s1, 1)
+        self.history.append(rec)
+        return rec
+
     @staticmethod
-    def _validate(model, Wbar, Xv, Yv, regression):
+    def _validate_t(model, Wbar, Xv, Yv, regression):
+        """(s0, s1) validation statistics as device scalars."""
         model.coef = Wbar
         labels, DV = model.predict(Xv.to(Wbar.device))
         Yv = Yv.to(DV.device)
         if regression:
             Yr = Yv if Yv.dim() == 2 else Yv[:, None]
-            return float(((DV - Yr) ** 2).sum()), float((Yr ** 2).sum())
-        correct = int((labels.to(torch.float64) == Yv.reshape(-1).to(torch.float64)).sum())
-        return float(correct), float(Yv.numel())
+            return ((DV - Yr) ** 2).sum().double(), (Yr ** 2).sum().double()
+        correct = (labels.to(torch.float64) == Yv.reshape(-1).to(torch.float64)).sum().double()
+        return correct, torch.tensor(float(Yv.numel()), dtype=torch.float64, device=DV.device)
 
 
 BlockADMM = BlockADMMSolver

@@ -68,7 +68,16 @@ def _gauss(n, ctx, dtype, device):
     return out
 
 
-def condest(A, context: Context | None = None, params: CondEstParams | None = None) -> CondEstResult:
+def condest(A, context: Context | None = None, params: CondEstParams | None = None,
+            check_every: int = 8) -> CondEstResult:
+    """Device-resident: every scalar of the recurrences is a 0-d device tensor
+    and the stopping tests are read back once per ``check_every`` iterations
+    (the state of the iteration the reference would stop at is restored from a
+    short per-iteration history, so the result does not depend on
+    ``check_every``).  With a one-pass normal kernel for A (f32 dense,
+    ``ops/normal_eq.py``) the power iterations read A once each and the Lanczos
+    step does ``(A^T A v, A v)`` in one pass plus the ``A d`` certificate
+    product: two reads of A per iteration instead of three."""
     from .. import default_context
     ctx = context if context is not None else default_context()
     p = params or CondEstParams()
@@ -76,6 +85,7 @@ def condest(A, context: Context | None = None, params: CondEstParams | None = No
     m, n = op.shape
     dt = torch.float64
     dev = op.device
+    fused = op.has_fused_normal(1)
 
     def Av(x):
         return op.matmul(x.to(op.dtype)).to(dt)
@@ -84,20 +94,18 @@ def condest(A, context: Context | None = None, params: CondEstParams | None = No
         return op.rmatmul(u.to(op.dtype)).to(dt)
 
     def lnorm(u):
-        return float(op.long_colnorm(u)[0])
+        return op.long_colnorm(u)[0]
 
-    # --- sigma_max by power iteration (normalised every step)
+    # --- sigma_max by power iteration (normalised every step, no host sync)
     v_max = _gauss(n, ctx, dt, dev)
     v_max = v_max / v_max.norm()
     for _ in range(p.powerits):
-        u = Av(v_max)
-        v_max = Atv(u)
+        v_max = op.normal(v_max.to(op.dtype))[0].to(dt) if fused else Atv(Av(v_max))
         v_max = v_max / v_max.norm()
     u_max = Av(v_max)
-    sigma_max = lnorm(u_max)
-    u_max = u_max / sigma_max
-    sigma_min = sigma_max
-    u_min, v_min = u_max.clone(), v_max.clone()
+    sigma_max_t = lnorm(u_max)
+    u_max = u_max / sigma_max_t
+    sigma_max = float(sigma_max_t)
 
     xhat = _gauss(n, ctx, dt, dev)
     nrm_xhat = float(xhat.norm())
@@ -105,30 +113,42 @@ def condest(A, context: Context | None = None, params: CondEstParams | None = No
     xhat = xhat / nrm_xhat
     b = Av(xhat)
     nrm_b = lnorm(b)
-    u = b.clone()
-    beta = lnorm(u)
-    u = u / beta
-    v = Atv(u)
-    alpha = float(v.norm())
-    v = v / alpha
+    beta = nrm_b
+    u = b / beta
+    Atu = Atv(u)
+    alpha = Atu.norm()
+    v = Atu / alpha
     x = torch.zeros(n, 1, dtype=dt, device=dev)
     w = v.clone()
     phibar, rhobar = beta, alpha
     T = p.iter_lim if p.iter_lim >= 0 else max(20, 2 * min(m, n))
     Tlim = T
     Rdiag, Rsub = [], []
-    c1 = p.c1
+    c1 = torch.tensor(p.c1, dtype=dt, device=dev)
+    c1t = torch.tensor(p.c1t, dtype=dt, device=dev)
+    sig_min = sigma_max_t.clone()
+    u_min, v_min = u_max.clone(), v_max.clone()
     retval = -6
-    theta = 0.0
+    theta = None
     itn = 0
+    hist, flags = [], []          # per-iteration (sig_min, v_min, u_min) / stopping flags since the last check
+    refresh = 16
     while itn < T:
-        u = Av(v) - alpha * u
-        beta = lnorm(u)
-        u = u / beta
-        v = Atv(u) - beta * v
-        alpha = float(v.norm())
+        if fused:
+            G, AvV = op.normal(v.to(op.dtype), want_y=True)
+            u = AvV.to(dt) - alpha * u
+            beta = lnorm(u)
+            u = u / beta
+            Atu = Atv(u) if (itn + 1) % refresh == 0 else (G.to(dt) - alpha * Atu) / beta
+        else:
+            u = Av(v) - alpha * u
+            beta = lnorm(u)
+            u = u / beta
+            Atu = Atv(u)
+        v = Atu - beta * v
+        alpha = v.norm()
         v = v / alpha
-        rho = math.sqrt(rhobar * rhobar + beta * beta)
+        rho = torch.sqrt(rhobar * rhobar + beta * beta)
         Rdiag.append(rho)
         if itn > 0:
             Rsub.append(theta)
@@ -140,35 +160,52 @@ def condest(A, context: Context | None = None, params: CondEstParams | None = No
         x = x + (phi / rho) * w
         w = v - (theta / rho) * w
         d = xhat - x
-        nrm_d = float(d.norm())
-        if nrm_d == 0.0:
-            return CondEstResult(1.0, sigma_max, v_max, u_max, sigma_max, sigma_max, v_max, u_max, -1)
+        nrm_d = d.norm()
         Ad = Av(d)
         nrm_ad = lnorm(Ad)
-        if nrm_ad <= sigma_min * nrm_d:
-            sigma_min = nrm_ad / nrm_d
-            v_min = d.clone()
-            u_min = Ad / nrm_ad
-        if c1 != p.c1t and sigma_min / sigma_max <= p.c4:
-            c1 = p.c1t
-        nrm_x = float(x.norm())
-        if T == Tlim and nrm_ad <= c1 * (sigma_max * nrm_x + nrm_b):
-            T, retval = int(1.25 * itn + 1), -2
-        if T == Tlim and nrm_d <= tau:
-            T, retval = int(1.25 * itn + 1), -3
-        if T == Tlim and sigma_max / sigma_min >= p.c3:
-            T, retval = int(1.25 * itn + 1), -4
+        better = nrm_ad <= sig_min * nrm_d
+        sig_min = torch.where(better, nrm_ad / nrm_d, sig_min)
+        v_min = torch.where(better, d, v_min)
+        u_min = torch.where(better, Ad / nrm_ad, u_min)
+        c1 = torch.where((c1 != c1t) & (sig_min / sigma_max <= p.c4), c1t, c1)
+        nrm_x = x.norm()
+        flags.append(torch.stack([nrm_d == 0, nrm_ad <= c1 * (sigma_max * nrm_x + nrm_b), nrm_d <= tau,
+                                  sigma_max / sig_min >= p.c3]))
+        hist.append((sig_min, v_min, u_min))
         if p.am_i_printing and p.log_level >= 2:
-            print(f"{p.prefix}CondEst: Iteration {itn} sigma_min = {sigma_min} cond = {sigma_max / sigma_min}")
+            print(f"{p.prefix}CondEst: Iteration {itn} sigma_min = {float(sig_min)} "
+                  f"cond = {sigma_max / float(sig_min)}")
         itn += 1
+        if itn % check_every == 0 or itn >= T:
+            F = torch.stack(flags).cpu().tolist()      # one host sync per check
+            first = itn - len(F)
+            for i, (zero_d, f1, f2, f3) in enumerate(F):
+                it_i = first + i
+                if it_i >= T:
+                    break
+                if zero_d:
+                    return CondEstResult(1.0, sigma_max, v_max, u_max, sigma_max, sigma_max, v_max, u_max, -1)
+                if T == Tlim and f1:
+                    T, retval = int(1.25 * it_i + 1), -2
+                if T == Tlim and f2:
+                    T, retval = int(1.25 * it_i + 1), -3
+                if T == Tlim and f3:
+                    T, retval = int(1.25 * it_i + 1), -4
+            if itn > T:      # overshoot past the stop iteration: restore its state
+                sig_min, v_min, u_min = hist[T - 1 - first]
+                del Rdiag[T:]
+                del Rsub[max(0, T - 1):]
+                itn = T
+            flags, hist = [], []
     # sigma_min of the Lanczos bidiagonal R
     from scipy.linalg import svdvals
     N = len(Rdiag)
-    Rm = np.diag(np.array(Rdiag)) + (np.diag(np.array(Rsub), 1) if N > 1 else 0)
-    sigma_min_R = float(svdvals(Rm)[-1]) if N else sigma_min
-    sigma_min_c = sigma_min
-    if sigma_min_R < sigma_min:
-        sigma_min = sigma_min_R
+    Rd = torch.stack(Rdiag).cpu().numpy() if N else np.zeros(0)
+    Rs = torch.stack(Rsub).cpu().numpy() if len(Rsub) else np.zeros(0)
+    Rm = np.diag(Rd) + (np.diag(Rs, 1) if N > 1 else 0)
+    sigma_min_c = float(sig_min)
+    sigma_min_R = float(svdvals(Rm)[-1]) if N else sigma_min_c
+    sigma_min = min(sigma_min_c, sigma_min_R)
     return CondEstResult(sigma_max / sigma_min, sigma_max, v_max, u_max, sigma_min, sigma_min_c, v_min, u_min,
                          retval)
 

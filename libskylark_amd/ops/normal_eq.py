@@ -16,6 +16,7 @@ from . import _lib
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_ata_pass", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, vp])
 _lib.register("sl_ata_workspace", [i64, i32], C.c_int64)
+_lib.register("sl_ata_pass2", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp])
 
 _WS: dict = {}
 
@@ -31,6 +32,34 @@ def native_ok(A: torch.Tensor, k: int) -> bool:
     return True
 
 
+def _ws(A, n, k):
+    nb = int(_lib.require().sl_ata_workspace(n, k))
+    key = str(A.device)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nb:
+        ws = _WS[key] = torch.empty(nb, dtype=torch.uint8, device=A.device)
+    return ws
+
+
+def dual(A: torch.Tensor, D: torch.Tensor, X: torch.Tensor | None = None):
+    """``(A^T D, A X or None)`` from ONE read of A (m x n): D is m x k (any
+    strides, e.g. the transpose of a k x m block), X n x k.  The BlockADMM pair
+    ``{Z Wbar, Z^T d}`` (``ml/BlockADMM.hpp:400-498``)."""
+    k = D.shape[1]
+    if X is not None and X.shape[1] != k:
+        raise ValueError("dual: X and D need the same number of columns")
+    if native_ok(A, k) and D.dtype == torch.float32 and D.is_cuda:
+        m, n = A.shape
+        W = torch.empty(n, k, dtype=torch.float32, device=A.device)
+        Xc = X.to(torch.float32).contiguous() if X is not None else None
+        Yo = torch.empty(m, k, dtype=torch.float32, device=A.device) if X is not None else None
+        _lib.call("sl_ata_pass2", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Xc) if Xc is not None else None, k,
+                  _lib.ptr(W), _lib.ptr(Yo) if Yo is not None else None, k, _lib.ptr(D), D.stride(0), D.stride(1),
+                  _lib.ptr(_ws(A, n, k)), vp(_lib.stream_of(A)))
+        return W, Yo
+    return A.t() @ D.to(A.dtype), (A @ X.to(A.dtype) if X is not None else None)
+
+
 def ata(A: torch.Tensor, Y: torch.Tensor, want_y: bool = False):
     """``(A^T (A Y), A Y or None)`` for the local block A (m x n) and Y (n x k).
     Partial over a row shard: the caller all-reduces the first result."""
@@ -40,13 +69,8 @@ def ata(A: torch.Tensor, Y: torch.Tensor, want_y: bool = False):
         Yc = Y.to(torch.float32).contiguous()
         W = torch.empty(n, k, dtype=torch.float32, device=A.device)
         Yo = torch.empty(m, k, dtype=torch.float32, device=A.device) if want_y else None
-        nb = int(_lib.require().sl_ata_workspace(n, k))
-        key = str(A.device)
-        ws = _WS.get(key)
-        if ws is None or ws.numel() < nb:
-            ws = _WS[key] = torch.empty(nb, dtype=torch.uint8, device=A.device)
         _lib.call("sl_ata_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Yc), k, _lib.ptr(W),
-                  _lib.ptr(Yo) if Yo is not None else None, k, _lib.ptr(ws), vp(_lib.stream_of(A)))
+                  _lib.ptr(Yo) if Yo is not None else None, k, _lib.ptr(_ws(A, n, k)), vp(_lib.stream_of(A)))
         return W, Yo
     AY = A @ Y.to(A.dtype)
     return A.t() @ AY, (AY if want_y else None)

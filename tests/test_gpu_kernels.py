@@ -182,3 +182,31 @@ def test_dense_sketch_bf16x2_panels(dev, dim, block):
                           dtype=torch.bfloat16, device=dev).double()
     ref = Sb @ A.double() if dim == 0 else A.double() @ Sb.t()
     torch.testing.assert_close(out.double(), ref, rtol=0, atol=2e-5 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,view,dt", [((20000, 1000), "row", torch.bfloat16), ((333, 1001), "row", torch.float32),
+                                           ((1000, 77), "col", torch.bfloat16), ((513, 1200), "slice", torch.bfloat16),
+                                           ((4097, 1), "row", torch.float32), ((1, 4097), "row", torch.bfloat16)])
+def test_fill_normal_fast_lines_bitwise(dev, shape, view, dt):
+    """The vectorised N(0,1) line kernel reproduces the generic fill bit for bit."""
+    from libskylark_amd.base import distributions as D
+    from libskylark_amd.ops import _lib, rng
+    lib = _lib.require()
+
+    def make():
+        if view == "col":
+            return torch.empty(shape[1], shape[0], dtype=dt, device=dev).t()
+        if view == "slice":
+            return torch.empty(shape[0], shape[1] + 40, dtype=dt, device=dev)[:, 3:3 + shape[1]]
+        return torch.empty(shape, dtype=dt, device=dev)
+    outs = []
+    for fast in (1, 0):
+        lib.sl_rng_set_fast_lines(fast)
+        o = make()
+        rng.fill_random(o, D.Normal(), 1234, 77, r0=5, c0=11, ir=1, ic=50021, scale=0.3)
+        outs.append(o)
+    lib.sl_rng_set_fast_lines(1)
+    torch.cuda.synchronize()
+    it = torch.int16 if dt == torch.bfloat16 else torch.int32
+    assert torch.equal(outs[0].contiguous().view(it), outs[1].contiguous().view(it))

@@ -69,3 +69,53 @@ def test_normal_form_krylov_matches_classic(dev):
         assert d < 1e-3, (i, d)
     r = float((A @ out[True][0] - b).norm() / (A @ out[False][0] - b).norm())
     assert abs(r - 1) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k,with_x", [(10007, 1024, 4, True), (5003, 1024, 4, False), (20001, 3000, 2, True),
+                                          (999, 5000, 1, False), (3, 300, 2, True)])
+def test_dual_pass_vs_fp64(dev, m, n, k, with_x):
+    g = torch.Generator().manual_seed(m * 7 + k)
+    A = torch.randn(m, n, generator=g)
+    Dt = torch.randn(k, m, generator=g)           # given as k x m: the kernel reads its transpose
+    X = torch.randn(n, k, generator=g) if with_x else None
+    W, Y = normal_eq.dual(A.to(dev), Dt.to(dev).t(), X.to(dev) if with_x else None)
+    torch.cuda.synchronize()
+    Wr = A.double().t() @ Dt.double().t()
+    assert float((W.double().cpu() - Wr).norm() / Wr.norm()) < 1e-5
+    if with_x:
+        Yr = A.double() @ X.double()
+        assert float((Y.double().cpu() - Yr).norm() / Yr.norm()) < 1e-5
+    else:
+        assert Y is None
+
+
+@pytest.mark.gpu
+def test_admm_one_pass_matches_four_products(dev):
+    """BlockADMM with the two fused Z passes per block is as accurate as the
+    four-product iteration: both f32 runs against an f64 run of the same
+    iteration (ADMM's (Z^T Z + I)^-1 step amplifies f32 rounding, so the two
+    f32 paths differ from each other at about the level they differ from f64)."""
+    import libskylark_amd as sk
+    from libskylark_amd import ml
+    g = torch.Generator(device=dev).manual_seed(1)
+    m, d = 20000, 32
+    lab = torch.randint(0, 3, (m,), generator=g, device=dev)
+    centers = torch.randn(3, d, generator=torch.Generator(device=dev).manual_seed(9), device=dev)
+    X = centers[lab] + 0.5 * torch.randn(m, d, generator=g, device=dev)
+    res = {}
+    for name, one_pass, dt in (("f64", False, torch.float64), ("f32_4", False, torch.float32),
+                               ("f32_fused", True, torch.float32)):
+        kern = ml.Gaussian(d, sigma=float(d) ** 0.5)
+        s = ml.BlockADMMSolver("squared", "l2", 1e-3, 512, kernel=kern, NumFeaturePartitions=2, context=sk.Context(5))
+        s.set_cache_transform(True)
+        s.set_maxiter(6)
+        s.one_pass = one_pass
+        model = s.train(X.to(dt), lab.double(), regression=False, log=None, dtype=dt)
+        res[name] = (model.coef.clone(), [h["objective"] for h in s.history])
+    ref = res["f64"][0]
+    e4 = float((res["f32_4"][0] - ref).norm() / ref.norm())
+    ef = float((res["f32_fused"][0] - ref).norm() / ref.norm())
+    assert ef <= 3 * e4 + 1e-6, (ef, e4)
+    for a, b in zip(res["f64"][1], res["f32_fused"][1]):
+        assert abs(a - b) <= 1e-3 * abs(a)
