@@ -39,7 +39,11 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     dev = torch.device("cuda")
-    m, n = int(a.rows), a.cols
+    for m, n in ((int(a.rows), a.cols), (1_000_000, 1024), (1_000_000, 2048)):
+        run(m, n, dev, a.reps)
+
+
+def run(m, n, dev, reps):
     A = torch.empty(m, n, device=dev)
     rng.fill_random(A, D.Normal(), 1, 0, ir=n, ic=1)
     gb = m * n * 4 / 1e9
@@ -51,10 +55,13 @@ def main():
         Yr = A @ y
         Wr = A.t() @ Yr
         err = float((W - Wr).norm() / Wr.norm())
+        Dt = torch.randn(k, m, device=dev)
         for name, fn in (("fused_ata", lambda: normal_eq.ata(A, y)),
+                         ("dual_AtD", lambda: normal_eq.dual(A, Dt.t())),
+                         ("dual_AtD_AX", lambda: normal_eq.dual(A, Dt.t(), y)),
                          ("fused_ata_storeY", lambda: normal_eq.ata(A, y, want_y=True)),
                          ("torch_two_gemv", lambda: A.t() @ (A @ y))):
-            t = timeit(fn, a.reps)
+            t = timeit(fn, reps)
             print(json.dumps({"bench": "normal_eq", "variant": name, "m": m, "n": n, "k": k,
                               "ms": round(t * 1e3, 3), "GBps_of_A": round(gb / t, 1),
                               "rel_err_vs_torch": err}), flush=True)

@@ -13,9 +13,10 @@
 // gfx950 design: 256-thread workgroups, thread t owns the columns
 // t, t + 256, ... (J per thread) and keeps its slice of Y and of the W
 // accumulators in registers for the whole kernel; rows stream in blocks of
-// BM = 4 (coalesced 4-B loads, 1 KB per wave-instruction), the BM x K dots
-// are reduced across the workgroup (DPP/shuffle inside a wave, LDS across the
-// 4 waves, one barrier), then every thread updates its W slice.  Several
+// BM = 4..16 (BM * n * 4 B >= ~64 KB in flight per workgroup; coalesced 4-B
+// loads, 1 KB per wave-instruction), the BM x K dots are reduced across the
+// workgroup (recursive-halving shuffles inside a wave, V - 1 shuffles for V
+// values; LDS across the 4 waves), then every thread updates its W slice.  Several
 // workgroups per CU hide the load latency; per-workgroup W partial slabs are
 // summed by the shared slab-reduce kernel.
 #include "sl_common.hpp"
@@ -23,25 +24,62 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int BM = 4;
+
+// Sum of vals[0..V) over the 64 lanes of a wave by recursive halving: at each
+// xor step a lane keeps half of its values (the lower or the upper half,
+// chosen by its lane bit) and adds the partner's copy of that half, so the
+// whole reduction costs V - 1 shuffles instead of 6 V.  On return vals[0] of
+// lane l holds the wave total of value index l >> (6 - log2 V).
+template <int CNT, int OFF, int V>
+__device__ __forceinline__ void wave_rs_step(float (&vals)[V], int lane) {
+  if constexpr (OFF >= 1) {
+    if constexpr (CNT > 1) {
+      constexpr int HALF = CNT / 2;
+      const bool upper = (lane & OFF) != 0;
+#pragma unroll
+      for (int i = 0; i < HALF; ++i) {
+        const float send = upper ? vals[i] : vals[i + HALF];
+        const float keep = upper ? vals[i + HALF] : vals[i];
+        vals[i] = keep + __shfl_xor(send, OFF, 64);
+      }
+      wave_rs_step<HALF, OFF / 2, V>(vals, lane);
+    } else {
+      vals[0] += __shfl_xor(vals[0], OFF, 64);
+      wave_rs_step<1, OFF / 2, V>(vals, lane);
+    }
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void wave_reduce_scatter(float (&vals)[V], int lane) {
+  wave_rs_step<V, 32, V>(vals, lane);
+}
+
+template <int V>
+constexpr int log2c() { return V <= 1 ? 0 : 1 + log2c<V / 2>(); }
 
 // DUAL: the W update uses a GIVEN long block D (W = A^T D) instead of A Y;
 // with STORE_Y the pass still emits A Y (the BlockADMM pair {Z Wbar, Z^T d}).
-template <int J, int K, bool STORE_Y, bool DUAL>
+// BM rows per iteration: enough bytes in flight per workgroup (BM * n * 4 >= ~64 KB).
+template <int J, int K, int BM, bool STORE_Y, bool DUAL>
 __global__ void __launch_bounds__(NT, 2)
 k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Y,
            float* __restrict__ Wslab, float* __restrict__ Yout, int64_t ldyo,
            const float* __restrict__ Dm, int64_t ldd_r, int64_t ldd_c) {
-  __shared__ float red[NT / 64][BM * K];
-  __shared__ float yrow[BM * K];
+  constexpr int V = BM * K;
+  static_assert(V <= 64 && (V & (V - 1)) == 0, "BM * K must be a power of two <= 64");
+  constexpr int SH = 6 - log2c<V>();
+  __shared__ float red[NT / 64][V];
+  __shared__ __attribute__((aligned(16))) float yrow[V];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr bool NEED_DOT = !(DUAL && !STORE_Y);
   float yv[J][K], wacc[J][K];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int c = tid + NT * j;
 #pragma unroll
     for (int kk = 0; kk < K; ++kk) {
-      yv[j][kk] = (c < n && !(DUAL && !STORE_Y)) ? Y[(int64_t)c * K + kk] : 0.f;
+      yv[j][kk] = (c < n && NEED_DOT) ? Y[(int64_t)c * K + kk] : 0.f;
       wacc[j][kk] = 0.f;
     }
   }
@@ -59,59 +97,50 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
         a[b][j] = (c < n && r0 + b < m) ? row[c] : 0.f;
       }
     }
-    float yr[BM][K];
-    if (DUAL && !STORE_Y) {
+    if (!NEED_DOT) {
+      // W = A^T D: the D rows of this block straight from memory (tiny, cached)
+      if (tid < V) {
+        const int b = tid / K, kk = tid - (tid / K) * K;
+        yrow[tid] = r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f;
+      }
+      __syncthreads();
+    } else {
+      float p[V];
 #pragma unroll
       for (int b = 0; b < BM; ++b)
 #pragma unroll
-        for (int kk = 0; kk < K; ++kk) yr[b][kk] = r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f;
-    } else {
-    float p[BM][K];
+        for (int kk = 0; kk < K; ++kk) {
+          float s = 0.f;
 #pragma unroll
-    for (int b = 0; b < BM; ++b)
-#pragma unroll
-      for (int kk = 0; kk < K; ++kk) {
+          for (int j = 0; j < J; ++j) s = fmaf(a[b][j], yv[j][kk], s);
+          p[b * K + kk] = s;
+        }
+      wave_reduce_scatter<V>(p, lane);
+      if ((lane & ((1 << SH) - 1)) == 0) red[wave][lane >> SH] = p[0];
+      __syncthreads();
+      if (tid < V) {
         float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < J; ++j) s = fmaf(a[b][j], yv[j][kk], s);
-        // wave reduction
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-        p[b][kk] = s;
-      }
-    if (lane == 0) {
-#pragma unroll
-      for (int b = 0; b < BM; ++b)
-#pragma unroll
-        for (int kk = 0; kk < K; ++kk) red[wave][b * K + kk] = p[b][kk];
-    }
-    __syncthreads();
-    if (tid < BM * K) {
-      float s = 0.f;
-#pragma unroll
-      for (int v = 0; v < NT / 64; ++v) s += red[v][tid];
-      yrow[tid] = s;
-      if (STORE_Y) {
+        for (int v = 0; v < NT / 64; ++v) s += red[v][tid];
         const int b = tid / K, kk = tid - (tid / K) * K;
-        if (r0 + b < m) Yout[(r0 + b) * ldyo + kk] = s;
+        if (STORE_Y && r0 + b < m) Yout[(r0 + b) * ldyo + kk] = s;
+        yrow[tid] = DUAL ? (r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f) : s;
       }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < BM; ++b)
-#pragma unroll
-      for (int kk = 0; kk < K; ++kk)
-        yr[b][kk] = DUAL ? (r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f) : yrow[b * K + kk];
+      __syncthreads();
     }
 #pragma unroll
-    for (int j = 0; j < J; ++j)
+    for (int b = 0; b < BM; ++b) {
+      float yr[K];
 #pragma unroll
-      for (int kk = 0; kk < K; ++kk) {
-        float w = wacc[j][kk];
+      for (int kk = 0; kk < K; ++kk) yr[kk] = yrow[b * K + kk];   // LDS broadcast
 #pragma unroll
-        for (int b = 0; b < BM; ++b) w = fmaf(a[b][j], yr[b][kk], w);
-        wacc[j][kk] = w;
-      }
+      for (int j = 0; j < J; ++j)
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) wacc[j][kk] = fmaf(a[b][j], yr[kk], wacc[j][kk]);
+    }
+    // with the dot path, the two barriers above already order this block's
+    // yrow / red reads before the next block's writes; the D path needs one
+    if (!NEED_DOT) __syncthreads();
   }
   float* ws = Wslab + (int64_t)blockIdx.x * n * K;
 #pragma unroll
@@ -154,11 +183,13 @@ SL_API int sl_ata_pass2(const float* A, int64_t m, int64_t n, int64_t lda, const
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int g = (int)std::min<int64_t>((int64_t)ata_grid(), (m + BM - 1) / BM);
-  float* slab = (float*)ws;
   const int J = (int)((n + NT - 1) / NT);
+  // rows per iteration: J = 4 -> 16, J = 8 -> 8, else 4 (>= 64 KB of A in flight per workgroup)
+  const int bm = J <= 4 ? 16 : (J <= 8 ? 8 : 4);
+  const int g = (int)std::min<int64_t>((int64_t)ata_grid(), (m + bm - 1) / bm);
+  float* slab = (float*)ws;
 #define SL_ATA_GO(JJ, KK, SY, DU) \
-  k_ata_pass<JJ, KK, SY, DU><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo, D, ldd_r, ldd_c);
+  k_ata_pass<JJ, KK, (JJ <= 4 ? 16 : (JJ <= 8 ? 8 : 4)), SY, DU><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo, D, ldd_r, ldd_c);
 #define SL_ATA(JJ, KK)                                                      \
   if (D) {                                                                  \
     if (Yout) { SL_ATA_GO(JJ, KK, true, true) } else { SL_ATA_GO(JJ, KK, false, true) } \

@@ -19,11 +19,16 @@
 //     accumulated in LDS with ds_add_f32 / ds_add_f64 (value dtype), then one
 //     coalesced store.
 #include "sl_common.hpp"
+#include <type_traits>
 
-template <typename T, typename OT, int VEC>
+// pval[p] = val[perm[p]] (bucket-ordered signs, built once per sketch): the
+// bucket's row indices and weights are read coalesced, and the row loads of
+// U rows are issued before any of them is consumed (U x fewer dependent
+// latency rounds than one row at a time).
+template <typename T, typename OT, int VEC, int U>
 __global__ void __launch_bounds__(256)
 k_hash_dense_col(const T* __restrict__ A, int64_t lda, int64_t m, const int64_t* __restrict__ perm,
-                 const int64_t* __restrict__ bptr, const double* __restrict__ val,
+                 const int64_t* __restrict__ bptr, const double* __restrict__ pval,
                  OT* __restrict__ out, int64_t ldo, int64_t row_offset, int accumulate) {
   const int64_t b = blockIdx.y;
   const int64_t c0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
@@ -33,16 +38,27 @@ k_hash_dense_col(const T* __restrict__ A, int64_t lda, int64_t m, const int64_t*
   const int64_t p0 = bptr[b], p1 = bptr[b + 1];
   if (c0 < m) {
     const bool full = c0 + VEC <= m;
-    for (int64_t p = p0; p < p1; ++p) {
-      const int64_t r = perm[p];  // wave-uniform
-      const float w = (float)val[r];
-      const T* row = A + (r - row_offset) * lda + c0;
-      if (full) {
+    int64_t p = p0;
+    if (full) {
+      for (; p + U <= p1; p += U) {
+        float x[U][VEC], w[U];
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] += w * Cvt<T>::to_f(row[j]);
-      } else {
-        for (int j = 0; j < VEC && c0 + j < m; ++j) acc[j] += w * Cvt<T>::to_f(row[j]);
+        for (int u = 0; u < U; ++u) {
+          const T* row = A + (perm[p + u] - row_offset) * lda + c0;   // wave-uniform row
+          w[u] = (float)pval[p + u];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) x[u][j] = Cvt<T>::to_f(row[j]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] += w[u] * x[u][j];
       }
+    }
+    for (; p < p1; ++p) {
+      const T* row = A + (perm[p] - row_offset) * lda + c0;
+      const float w = (float)pval[p];
+      for (int j = 0; j < VEC && c0 + j < m; ++j) acc[j] += w * Cvt<T>::to_f(row[j]);
     }
     OT* o = out + b * ldo + c0;
     for (int j = 0; j < VEC && c0 + j < m; ++j)
@@ -66,7 +82,7 @@ k_hash_dense_col_f64(const double* __restrict__ A, int64_t lda, int64_t m,
   if (c0 < m) {
     for (int64_t p = p0; p < p1; ++p) {
       const int64_t r = perm[p];
-      const double w = val[r];
+      const double w = val[p];
       const double* row = A + (r - row_offset) * lda + c0;
       for (int j = 0; j < VEC && c0 + j < m; ++j) acc[j] += w * row[j];
     }
@@ -92,7 +108,7 @@ SL_API int sl_hash_dense_colwise(const void* A, int dtype, int64_t lda, int64_t 
   }
   constexpr int VEC = 4;
   dim3 grid((unsigned)((m + 256 * VEC - 1) / (256 * VEC)), (unsigned)S);
-#define SL_HC(TI, TO) k_hash_dense_col<TI, TO, VEC><<<grid, 256, 0, s>>>((const TI*)A, lda, m, perm, bptr, val, (TO*)out, ldo, row_offset, accumulate)
+#define SL_HC(TI, TO) k_hash_dense_col<TI, TO, VEC, 4><<<grid, 256, 0, s>>>((const TI*)A, lda, m, perm, bptr, val, (TO*)out, ldo, row_offset, accumulate)
   if (dtype == SL_F32 && out_dtype == SL_F32) SL_HC(float, float);
   else if (dtype == SL_BF16 && out_dtype == SL_F32) SL_HC(bf16_t, float);
   else if (dtype == SL_BF16 && out_dtype == SL_BF16) SL_HC(bf16_t, bf16_t);
@@ -154,62 +170,100 @@ SL_API int sl_hash_dense_rowwise(const void* A, int dtype, int64_t lda, int64_t 
 // ------------------------------------------------------------ CSR columnwise
 // A: CSR (rowptr, col, vals) holding global rows [row_offset, row_offset+nrows).
 // Workgroup = (bucket b, column chunk [c0, c0+CW)); lanes are split in groups
-// of G lanes per CSR row (G ~ average row length, a power of two).
-template <typename IT, typename VT, int G>
+// of G lanes per CSR row (G ~ average row length, a power of two), and each
+// group keeps U rows in flight (their perm / rowptr loads issued together).
+// The workgroup owns its output cells: plain stores, no zero-fill.
+//
+// DET (deterministic mode): the chunk is accumulated in int64 fixed point
+// (ds_add_u64 is associative, so the result does not depend on the order the
+// lanes arrive in) with the per-bucket scale 2^62 / (R_b * max|v| * max|w|):
+// one row contributes at most one entry to a column, so no cell can overflow,
+// and the quantum is 2^-62 of that bound (~2^-50 relative for 4k-row
+// buckets, finer than f32 and close to f64 rounding).
+template <typename IT, typename VT, int G, int U, bool DET>
 __global__ void __launch_bounds__(512)
 k_hash_csr_col(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
                const VT* __restrict__ vals, const int64_t* __restrict__ perm,
-               const int64_t* __restrict__ bptr, const double* __restrict__ hval,
+               const int64_t* __restrict__ bptr, const VT* __restrict__ pval,
                VT* __restrict__ out, int64_t ldo, int64_t m, int64_t CW,
-               int64_t row_offset) {
-  // accumulation in the value type (f64 values: ds_add_f64, exact fp64 sums)
+               int64_t row_offset, const double* __restrict__ vmax, double wmax) {
+  typedef typename std::conditional<DET, unsigned long long, VT>::type AT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  VT* acc = (VT*)smem;
+  AT* acc = (AT*)smem;
   const int64_t b = blockIdx.y;
   const int64_t c0 = (int64_t)blockIdx.x * CW;
   const int64_t cw = (c0 + CW <= m) ? CW : (m - c0);
-  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) acc[c] = (VT)0;
+  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) acc[c] = (AT)0;
   __syncthreads();
   const int groups = blockDim.x / G;
   const int gid = threadIdx.x / G, gl = threadIdx.x % G;
   const bool chunked = cw != m;
-  for (int64_t p = bptr[b] + gid; p < bptr[b + 1]; p += groups) {
-    const int64_t r = perm[p];
-    const VT w = (VT)hval[r];
-    const int64_t lr = r - row_offset;
-    for (int64_t q = rowptr[lr] + gl; q < rowptr[lr + 1]; q += G) {
-      const int64_t c = (int64_t)col[q] - c0;
-      if (!chunked || (c >= 0 && c < cw)) atomicAdd(&acc[c], w * vals[q]);
+  const int64_t p0 = bptr[b], p1 = bptr[b + 1];
+  double sc = 0.0;
+  if (DET) {
+    const double bound = (double)(p1 - p0) * vmax[0] * wmax;
+    sc = bound > 0.0 ? 0x1p62 / bound : 0.0;
+  }
+  for (int64_t p = p0 + gid; p < p1; p += (int64_t)groups * U) {
+    int64_t rs[U], re[U];
+    VT w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t pp = p + (int64_t)u * groups;
+      rs[u] = re[u] = 0;
+      w[u] = (VT)0;
+      if (pp < p1) {
+        const int64_t lr = perm[pp] - row_offset;
+        w[u] = pval[pp];
+        rs[u] = rowptr[lr];
+        re[u] = rowptr[lr + 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      for (int64_t q = rs[u] + gl; q < re[u]; q += G) {
+        const int64_t c = (int64_t)col[q] - c0;
+        if (!chunked || (c >= 0 && c < cw)) {
+          if (DET) atomicAdd(&acc[c], (unsigned long long)__double2ll_rn((double)(w[u] * vals[q]) * sc));
+          else atomicAdd(&acc[c], w[u] * vals[q]);
+        }
+      }
     }
   }
   __syncthreads();
-  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) out[b * ldo + c0 + c] += acc[c];
+  for (int64_t c = threadIdx.x; c < cw; c += blockDim.x) {
+    if (DET) out[b * ldo + c0 + c] = sc > 0.0 ? (VT)((double)(long long)acc[c] / sc) : (VT)0;
+    else out[b * ldo + c0 + c] = (VT)acc[c];
+  }
 }
 
-SL_API int sl_hash_csr_colwise(const int64_t* rowptr, const void* col, int idx32, const void* vals,
-                               int vdtype, const int64_t* perm, const int64_t* bptr,
-                               const double* hval, int64_t S, int64_t m, void* out, int64_t ldo,
-                               int64_t row_offset, int group, void* stream) {
+SL_API int sl_hash_csr_colwise2(const int64_t* rowptr, const void* col, int idx32, const void* vals,
+                                int vdtype, const int64_t* perm, const int64_t* bptr,
+                                const void* pval, int64_t S, int64_t m, void* out, int64_t ldo,
+                                int64_t row_offset, int group, int deterministic, const double* vmax,
+                                double wmax, void* stream) {
   if (S <= 0 || m <= 0) return SL_OK;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t esz = vdtype == SL_F64 ? 8 : 4;
+  const int64_t esz = (vdtype == SL_F64 || deterministic) ? 8 : 4;
   const int64_t cwmax = (128 * 1024) / esz;  // 128 KB of LDS at most
   int64_t CW = m < cwmax ? m : cwmax;
   dim3 grid((unsigned)((m + CW - 1) / CW), (unsigned)S);
   size_t lds = (size_t)CW * esz;
-#define SL_CSR(IT, VT, G) k_hash_csr_col<IT, VT, G><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, hval, (VT*)out, ldo, m, CW, row_offset)
-#define SL_CSR_G(IT, VT)                                   \
+#define SL_CSR(IT, VT, G, DET) k_hash_csr_col<IT, VT, G, 4, DET><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, (const VT*)pval, (VT*)out, ldo, m, CW, row_offset, vmax, wmax)
+#define SL_CSR_G(IT, VT, DET)                              \
   switch (group) {                                         \
-    case 1: SL_CSR(IT, VT, 1); break;                      \
-    case 4: SL_CSR(IT, VT, 4); break;                      \
-    case 16: SL_CSR(IT, VT, 16); break;                    \
-    default: SL_CSR(IT, VT, 64); break;                    \
+    case 1: SL_CSR(IT, VT, 1, DET); break;                 \
+    case 4: SL_CSR(IT, VT, 4, DET); break;                 \
+    case 16: SL_CSR(IT, VT, 16, DET); break;               \
+    default: SL_CSR(IT, VT, 64, DET); break;               \
   }
+#define SL_CSR_D(IT, VT) if (deterministic) { SL_CSR_G(IT, VT, true) } else { SL_CSR_G(IT, VT, false) }
   if (vdtype == SL_F32) {
-    if (idx32) { SL_CSR_G(int32_t, float) } else { SL_CSR_G(int64_t, float) }
+    if (idx32) { SL_CSR_D(int32_t, float) } else { SL_CSR_D(int64_t, float) }
   } else if (vdtype == SL_F64) {
-    if (idx32) { SL_CSR_G(int32_t, double) } else { SL_CSR_G(int64_t, double) }
+    if (idx32) { SL_CSR_D(int32_t, double) } else { SL_CSR_D(int64_t, double) }
   } else { sl_set_last_error("hash csr: value dtype"); return SL_ERR_UNSUPPORTED; }
+#undef SL_CSR_D
 #undef SL_CSR_G
 #undef SL_CSR
   SL_LAUNCH_CHECK();
@@ -219,6 +273,9 @@ SL_API int sl_hash_csr_colwise(const int64_t* rowptr, const void* col, int idx32
 // ------------------------------------------------------------- CSR rowwise
 // out[r, h[c]] += v[c] * A[r, c]: G lanes per CSR row, f32/f64 atomics into the
 // row of `out` (rows are disjoint between groups, so contention is per row).
+// G = 1: the lane owns its output row and adds in CSR order with plain
+// read-modify-writes -- no atomics, deterministic (short rows, and the
+// deterministic mode).
 template <typename IT, typename VT, int G>
 __global__ void __launch_bounds__(256)
 k_hash_csr_row(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
@@ -230,7 +287,8 @@ k_hash_csr_row(const int64_t* __restrict__ rowptr, const IT* __restrict__ col,
   if (gid >= rows) return;
   for (int64_t q = rowptr[gid] + gl; q < rowptr[gid + 1]; q += G) {
     const int64_t c = (int64_t)col[q] + col_offset;
-    atomicAdd(&out[gid * ldo + h[c]], (VT)hval[c] * vals[q]);
+    if (G == 1) out[gid * ldo + h[c]] += (VT)hval[c] * vals[q];
+    else atomicAdd(&out[gid * ldo + h[c]], (VT)hval[c] * vals[q]);
   }
 }
 

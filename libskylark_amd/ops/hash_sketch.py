@@ -1,8 +1,11 @@
 """CountSketch-family application (hash_transform_t), native on gfx950.
 
-GPU tensors go through the bucketed HIP kernels of ``hash_kernels.hip``
-(deterministic for dense inputs); CPU tensors (plumbing path) use torch
-``index_add_``.  See the kernel file for the design.
+GPU tensors go through the bucketed HIP kernels of ``hash_kernels.hip``; CPU
+tensors (plumbing path) use torch ``index_add_``.  See the kernel file for the
+design.  Determinism: dense inputs and rowwise CSR with short rows are always
+bit-reproducible (no atomics); columnwise CSR accumulates with LDS float
+atomics unless ``sketch.params.set_deterministic(True)``, which switches it to
+int64 fixed-point accumulation (and rowwise CSR to one lane per row).
 """
 from __future__ import annotations
 
@@ -15,7 +18,8 @@ from . import _lib
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_hash_dense_colwise", [vp, i32, i64, i64, vp, vp, vp, i64, vp, i32, i64, i64, i32, vp])
 _lib.register("sl_hash_dense_rowwise", [vp, i32, i64, i64, i64, vp, vp, vp, i64, vp, i32, i64, i64, i32, vp])
-_lib.register("sl_hash_csr_colwise", [vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, i64, i64, i32, vp])
+_lib.register("sl_hash_csr_colwise2", [vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, i64, i64, i32, i32, vp,
+                                       C.c_double, vp])
 _lib.register("sl_hash_csr_rowwise", [vp, vp, i32, vp, i32, i64, vp, vp, vp, i64, i64, i32, vp])
 _lib.register("sl_cwt_csr_rowwise_sparse", [vp, vp, i32, vp, i32, i64, i32, vp, vp, i64, i32, vp, vp, vp, vp])
 _lib.register("sl_cwt_csr_colwise_mark", [vp, vp, i32, i64, vp, i64, vp, i64, vp])
@@ -33,6 +37,7 @@ class HashData:
         self._host_idx = idx.to(torch.int64).cpu()
         self._host_val = val.to(torch.float64).cpu()
         self._cache = {}
+        self.wmax = float(self._host_val.abs().max()) if self._host_val.numel() else 0.0
 
     def on(self, device):
         key = str(device)
@@ -46,7 +51,24 @@ class HashData:
             bptr[1:] = torch.cumsum(counts, 0)
             d = (idx, val, perm, bptr)
             self._cache[key] = d
+            self._cache[key + "/pval"] = _PVal(val[perm])
         return d
+
+    def pval(self, device, perm=None) -> "_PVal":
+        """Bucket-ordered weights ``val[perm]`` (f64 and f32), built once."""
+        if perm is not None:
+            return _PVal(self.on(device)[1][perm])
+        self.on(device)
+        return self._cache[str(device) + "/pval"]
+
+
+class _PVal:
+    def __init__(self, v64: torch.Tensor):
+        self.f64 = v64.contiguous()
+        self.f32 = v64.to(torch.float32).contiguous()
+
+    def of(self, dt):
+        return self.f64 if dt == torch.float64 else self.f32
 
 
 def _group_for(avg: float) -> int:
@@ -82,11 +104,13 @@ def apply_dense(hd: HashData, A: torch.Tensor, dim: int, in_offset: int = 0, out
             return res
         if A.stride(1) != 1:
             A = A.contiguous()
+        pv = hd.pval(A.device)
         if in_offset != 0 or k != idx.numel():
             # restrict the bucket permutation to this shard's rows
             perm, bptr = _restrict(idx, in_offset, k, S)
+            pv = hd.pval(A.device, perm)
         _lib.call("sl_hash_dense_colwise", _lib.ptr(A), _lib.dtype_code(A.dtype), A.stride(0), m,
-                  _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(val), S, _lib.ptr(res), _lib.dtype_code(odt),
+                  _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(pv.f64), S, _lib.ptr(res), _lib.dtype_code(odt),
                   res.stride(0), in_offset, 1, vp(_lib.stream_of(A)))
         return res
     m, k = A.shape
@@ -156,18 +180,38 @@ def apply_csr_dense_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int 
     avg = vals.numel() / max(1, nrows)
     st = vp(_lib.stream_of(A))
     if dim == 0:
-        res = torch.zeros(S, ncols, dtype=odt, device=A.device)
-        if in_offset != 0 or nrows != idx.numel():
-            perm, bptr = _restrict(idx, in_offset, nrows, S)
-        _lib.call("sl_hash_csr_colwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals),
-                  _lib.dtype_code(vals.dtype), _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(val), S, ncols,
-                  _lib.ptr(res), res.stride(0), in_offset, _group_for(avg), st)
+        res = torch.empty(S, ncols, dtype=odt, device=A.device)   # every cell is stored by its workgroup
+        _csr_colwise(hd, A.device, rp, ci, idx32, vals, S, ncols, res, in_offset, avg, st)
     else:
         res = torch.zeros(nrows, S, dtype=odt, device=A.device)
+        # one lane per row (atomic-free, deterministic) unless rows are long
+        g = 1 if (_det() or avg < 12) else _group_for(avg)
         _lib.call("sl_hash_csr_rowwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals),
                   _lib.dtype_code(vals.dtype), nrows, _lib.ptr(idx), _lib.ptr(val), _lib.ptr(res),
-                  res.stride(0), in_offset, _group_for(avg), st)
+                  res.stride(0), in_offset, g, st)
     return res
+
+
+def _det() -> bool:
+    from ..sketch import params
+    return params.get_deterministic()
+
+
+def _csr_colwise(hd, device, rp, ci, idx32, vals, S, ncols, res, in_offset, avg, st):
+    """res (S x ncols, fully overwritten) = columnwise CountSketch of CSR rows
+    [in_offset, in_offset + nrows)."""
+    idx, val, perm, bptr = hd.on(device)
+    nrows = rp.numel() - 1
+    pv = hd.pval(device)
+    if in_offset != 0 or nrows != idx.numel():
+        perm, bptr = _restrict(idx, in_offset, nrows, S)
+        pv = hd.pval(device, perm)
+    det = _det()
+    vmax = vals.abs().max().to(torch.float64).reshape(1) if (det and vals.numel()) else \
+        torch.zeros(1, dtype=torch.float64, device=device)
+    _lib.call("sl_hash_csr_colwise2", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals),
+              _lib.dtype_code(vals.dtype), _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(pv.of(vals.dtype)), S, ncols,
+              _lib.ptr(res), res.stride(0), in_offset, _group_for(avg), int(det), _lib.ptr(vmax), hd.wmax, st)
 
 
 def apply_csr_sparse_out(hd: HashData, A: torch.Tensor, dim: int, in_offset: int = 0):
@@ -217,13 +261,9 @@ def _csr_sparse_out_native(hd: HashData, A: torch.Tensor, dim: int, in_offset: i
             "sl_cwt_csr_rowwise_sparse", *args, 1, _lib.ptr(crow), _lib.ptr(oc), _lib.ptr(ov), st), vdt, dev)
     if S * ncols > SPARSE_OUT_DENSE_CELLS:
         return None
-    if in_offset != 0 or nrows != idx.numel():
-        perm, bptr = _restrict(idx, in_offset, nrows, S)
-    dense = torch.zeros(S, ncols, dtype=vdt, device=dev)
+    dense = torch.empty(S, ncols, dtype=vdt, device=dev)
     avg = vals.numel() / max(1, nrows)
-    _lib.call("sl_hash_csr_colwise", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals), _lib.dtype_code(vdt),
-              _lib.ptr(perm), _lib.ptr(bptr), _lib.ptr(val), S, ncols, _lib.ptr(dense), dense.stride(0),
-              in_offset, _group_for(avg), st)
+    _csr_colwise(hd, dev, rp, ci, idx32, vals, S, ncols, dense, in_offset, avg, st)
     occ = torch.zeros(S, ncols, dtype=torch.uint8, device=dev)
     _lib.call("sl_cwt_csr_colwise_mark", _lib.ptr(rp), _lib.ptr(ci), idx32, nrows, _lib.ptr(idx), in_offset,
               _lib.ptr(occ), ncols, st)

@@ -5,6 +5,8 @@
 * ``blocksize``: columns of S realised per panel by the dense transforms;
   0 (default) sizes panels by memory instead (``ops.dense_sketch.PANEL_ELEMS``
   entries, ~128-512 MB on the MI355X's 288 GB HBM, which keeps each GEMM long).
+* ``deterministic``: bit-reproducible GPU results where a kernel would
+  otherwise accumulate with atomics (CountSketch of CSR input).
 * ``factor``: selects the ``[MC,MR]`` columnwise dense-sketch algorithm.
   *Outer panel* (all-gather A's sketched dimension inside each grid column,
   every rank realises only its own output rows, no reduction) is used when
@@ -17,6 +19,20 @@ from __future__ import annotations
 
 _BLOCKSIZE = 0
 _FACTOR = 20
+_DETERMINISTIC = False
+
+
+def get_deterministic() -> bool:
+    return _DETERMINISTIC
+
+
+def set_deterministic(flag: bool):
+    """Bit-reproducible sketch application on the GPU: CountSketch of CSR
+    input accumulates in int64 fixed point instead of LDS float atomics (about
+    the same speed; see ``hash_kernels.hip``).  Everything else is already
+    deterministic."""
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(flag)
 
 
 def get_blocksize() -> int:

@@ -210,3 +210,52 @@ def test_fill_normal_fast_lines_bitwise(dev, shape, view, dt):
     torch.cuda.synchronize()
     it = torch.int16 if dt == torch.bfloat16 else torch.int32
     assert torch.equal(outs[0].contiguous().view(it), outs[1].contiguous().view(it))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vdt", [torch.float32, torch.float64])
+def test_cwt_csr_deterministic_mode(dev, vdt):
+    """Deterministic mode: int64 fixed-point accumulation gives bit-identical
+    results across runs, within f32/f64 rounding of the fp64 reference."""
+    from libskylark_amd.sketch import params
+    g = torch.Generator().manual_seed(5)
+    N, m, S = 20000, 3000, 256
+    nnz = N * 12
+    rows = torch.randint(0, N, (nnz,), generator=g)
+    cols = torch.randint(0, m, (nnz,), generator=g)
+    v = torch.randn(nnz, generator=g, dtype=torch.float64) * torch.exp(2 * torch.randn(nnz, generator=g,
+                                                                                      dtype=torch.float64))
+    A = torch.sparse_coo_tensor(torch.stack([rows, cols]), v, (N, m)).coalesce().to_sparse_csr()
+    sk_ = sk.sketch.CWT(N, S, context=sk.Context(3))
+    Ad = A.to(vdt).to(dev)
+    ref = sk_.apply(A.to_dense(), dim=sk.sketch.COLUMNWISE)     # CPU fp64 index_add reference
+    try:
+        params.set_deterministic(True)
+        outs = [sk_.apply(Ad, dim=sk.sketch.COLUMNWISE, sparse_output=False).cpu() for _ in range(3)]
+    finally:
+        params.set_deterministic(False)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    err = float((outs[0].double() - ref).norm() / ref.norm())
+    assert err < (1e-6 if vdt == torch.float32 else 1e-12), err
+    fast = sk_.apply(Ad, dim=sk.sketch.COLUMNWISE, sparse_output=False).cpu()
+    assert float((fast.double() - ref).norm() / ref.norm()) < (1e-6 if vdt == torch.float32 else 1e-12)
+
+
+@pytest.mark.gpu
+def test_cwt_csr_rowwise_atomic_free(dev):
+    """Rowwise CSR with short rows runs one lane per row (no atomics): repeated
+    runs are bitwise identical and match the fp64 reference."""
+    g = torch.Generator().manual_seed(6)
+    m, N, S = 5000, 20000, 512
+    nnz = m * 8
+    rows = torch.randint(0, m, (nnz,), generator=g)
+    cols = torch.randint(0, N, (nnz,), generator=g)
+    A = torch.sparse_coo_tensor(torch.stack([rows, cols]), torch.randn(nnz, generator=g), (m, N)).coalesce()
+    A = A.to_sparse_csr()
+    sk_ = sk.sketch.CWT(N, S, context=sk.Context(4))
+    ref = sk_.apply(A.to_dense().double(), dim=sk.sketch.ROWWISE)
+    o1 = sk_.apply(A.to(dev), dim=sk.sketch.ROWWISE, sparse_output=False).cpu()
+    o2 = sk_.apply(A.to(dev), dim=sk.sketch.ROWWISE, sparse_output=False).cpu()
+    assert torch.equal(o1, o2)
+    assert float((o1.double() - ref).norm() / ref.norm()) < 1e-6
