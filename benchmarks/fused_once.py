@@ -1,5 +1,6 @@
 """Run the fused tall-skinny pass N times (for rocprofv3 --pmc counter runs).
-usage: fused_once.py [flags=0|3] [reps=20] [lda=1000]"""
+usage: fused_once.py [flags=0|3] [reps=20] [lda=1000] [gram=1|0]
+(gram=0 with flags=3 is the randSVD inter-pass variant)"""
 from __future__ import annotations
 
 import os
@@ -12,13 +13,14 @@ import ctypes as C  # noqa: E402
 import torch  # noqa: E402
 
 from libskylark_amd.base import distributions as D  # noqa: E402
-from libskylark_amd.ops import _lib, rng  # noqa: E402
+from libskylark_amd.ops import _lib, rng, tallskinny  # noqa: E402,F401
 
 
 def main():
     flags = int(sys.argv[1]) if len(sys.argv) > 1 else 0
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     ld = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
+    gram = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     m, n, k = 1_000_000, 1000, 40
     dev = torch.device("cuda")
     lib = _lib.require()
@@ -31,7 +33,7 @@ def main():
     ws = torch.empty(int(lib.sl_tsk_fused_workspace(m, n, k)), dtype=torch.uint8, device=dev)
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     for _ in range(reps):
-        _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zt), k, _lib.ptr(W), _lib.ptr(G),
+        _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zt), k, _lib.ptr(W), _lib.ptr(G) if gram else None,
                   None, 0, _lib.ptr(ws), flags, st)
     torch.cuda.synchronize()
     print("ok", flags, reps, ld)

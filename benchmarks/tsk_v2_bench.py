@@ -28,13 +28,13 @@ def call(ver, A, Zt, k, W, G, Y, ws, flags):
     m, n = A.shape
     st = vp(torch.cuda.current_stream().cuda_stream)
     lib = _lib.require()
-    if ver in (1, 11, 12, 13):
+    if ver in (1, 11, 12, 13, 15, 17):
         lib.sl_tsk_set_x(0 if ver == 1 else ver - 10)
     if ver == 3:
         _lib.call("sl_tsk3_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zt), k, _lib.ptr(W),
                   _lib.ptr(G) if G is not None else None, _lib.ptr(Y) if Y is not None else None,
                   0 if Y is None else Y.stride(0), _lib.ptr(ws), ws.numel(), flags, st)
-    elif ver in (1, 11, 12, 13):
+    elif ver in (1, 11, 12, 13, 15, 17):
         _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zt), k, _lib.ptr(W),
                   _lib.ptr(G) if G is not None else None, _lib.ptr(Y) if Y is not None else None,
                   0 if Y is None else Y.stride(0), _lib.ptr(ws), flags, st)
@@ -57,7 +57,7 @@ def check(m, n, k, dev, out):
     res = {}
     for name, flags, keep_y, g64 in (("inter", 3, False, False), ("final_g64", 4, True, True),
                                      ("exact", 0, False, False), ("exact_y", 0, True, False)):
-        for ver in ((1, 11, 12, 13, 2, 3) if k <= 32 else (1, 11, 12, 13, 2)):
+        for ver in (1, 11, 13, 15, 17):
             if ver == 3 and name in ("exact", "exact_y"):
                 continue   # v3 forms every Gram in f64 (final_g64 covers it)
             W = torch.zeros(n, k, device=dev)
@@ -74,7 +74,7 @@ def check(m, n, k, dev, out):
             print(json.dumps(rec), flush=True)
     ok = True
     for (name, ver), e2 in res.items():
-        tolw = 2e-2 if (name == "inter" and ver in (1, 2, 11, 12, 13)) else 1e-4
+        tolw = 2e-2 if (name == "inter" and ver in (1, 2, 11, 12, 13, 15, 17)) else 1e-4
         if not (e2[0] < tolw and e2[1] < 1e-4 and e2[2] < 1e-5):
             ok = False
             print(f"MISMATCH {name} ver={ver} m={m} n={n} k={k}: {e2}", flush=True)
@@ -122,9 +122,9 @@ def main():
         G = torch.empty(k, k, device=dev, dtype=torch.float64)
         Y = torch.empty(m, k, device=dev)
         for name, flags, Yc in (("inter", 3, None), ("final_g64", 4, Y)):
-            vers = [(1, 0), (11, 0), (12, 0), (13, 0), (13, 64)]
+            vers = [(11, 0), (13, 0), (15, 0), (17, 0), (15, 64), (17, 64)]
             for ver, ab in vers:
-                if ver in (1, 11, 12, 13):
+                if ver in (1, 11, 12, 13, 15, 17):
                     lib.sl_tsk_set_ablate(ab)
                 elif ver == 2:
                     lib.sl_tsk2_set_tuning(1, ab)

@@ -49,7 +49,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int WAVES = 8;
 constexpr int THREADS = WAVES * 64;
 constexpr int BM = 16;
-constexpr int NBUF_DEFAULT = 4;
+constexpr int NBUF_DEFAULT = 3;   // 2..4 measured equal; 3 fits the padded y buffers
 int g_flags = 0;   // per-call mode bits (8: no Gram, 32: y_hi only)
 int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, bit3 step 4; bit6 nt loads
 
@@ -95,7 +95,7 @@ __device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_base) {
       : "memory");
 }
 
-template <int NW, int KT, int NBUF>
+template <int NW, int KT, int NBUF, int YFB = 1>
 struct Geo {
   static constexpr int ROWB = NW * 2;                 // bytes per LDS row of a wave region
   static constexpr int NCH = NW / 8;                  // 16-B chunks per row
@@ -103,8 +103,13 @@ struct Geo {
   static constexpr int LPB = REGION / 1024;           // glds instructions per block per wave
   static constexpr int KP = KT * 16;
   static constexpr int ABYTES = NBUF * WAVES * REGION;
-  static constexpr int YP_BYTES = WAVES * BM * KP * 4;
-  static constexpr int YF_BYTES = BM * KP * 4;
+  // column strides of the y partials / reduced y (f32): 16 rows + 4 pad, so
+  // the b128 partial stores (8 lanes = 8 consecutive columns per LDS cycle)
+  // and the f64 Gram's b32 reads hit distinct banks (stride 16: 4-way / 8-way)
+  static constexpr int YPS = BM + 4;
+  static constexpr int YFS = BM + 4;
+  static constexpr int YP_BYTES = WAVES * YPS * KP * 4;
+  static constexpr int YF_BYTES = YFB * YFS * KP * 4;   // YFB = 2: double-buffered (PIPE)
   static constexpr int LDS = ABYTES + YP_BYTES + YF_BYTES;
   static constexpr int GTILES = KT * KT;
   static constexpr int GS = (GTILES + WAVES - 1) / WAVES;  // G tiles per wave
@@ -112,14 +117,35 @@ struct Geo {
   static constexpr int GS64 = (GT64 + WAVES - 1) / WAVES;
 };
 
+// LDS chunk swizzle of A row `row` (16-B chunks; slot = chunk ^ swz(row)).
+// For 16 chunks per row the linear map row -> [0,2,4,..,14, 9,11,..,7]
+// (found by exhaustive search over GF(2) maps) keeps every read of the pass
+// conflict-free: the step-1 ds_read_b128 fragments, and the step-3
+// ds_read_b64_tr_b16 tiles of both the K = 16 (rows 0-7 / 8-15 per half-wave)
+// and the K = 32 (rows {0-3, 8-11} / {4-7, 12-15}) forms -- with plain
+// row & 15 the transposed reads were 2-way conflicted.
+template <int NCH>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (NCH == 16) return ((row << 1) & 15) ^ (((row >> 3) & 1) * 9);
+  else return row & (NCH - 1);
+}
+
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false, int X = 0>
+          bool G64 = false, int X = 0, bool ST = false>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
            float* __restrict__ Wslab, float* __restrict__ Gslab,
-           float* __restrict__ Y, int64_t ldy, int ab) {
-  using GG = Geo<NW, KT, NBUF>;
+           float* __restrict__ Y, int64_t ldy, int ab, unsigned long long* __restrict__ dbg = nullptr) {
+  using GG = Geo<NW, KT, NBUF, (X & 4) ? 2 : 1>;
+  // diagnostic build only (ST): per-phase s_memtime sums per wave -> dbg
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+#define SL_STAMP(I)                                                      \
+  if constexpr (ST) {                                                    \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+    if constexpr ((I) > 0) { if (my > 1) st_acc[(I) > 0 ? (I) - 1 : 0] += t_ - st_prev; } \
+    st_prev = t_;                                                        \
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* abuf = smem;
   float* yp = (float*)(smem + GG::ABYTES);
@@ -189,7 +215,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       const int byte = i * 1024 + lane * 16;
       const int row = byte / GG::ROWB;
       const int slot = (byte % GG::ROWB) / 16;
-      const int chunk = slot ^ (row & (GG::NCH - 1));
+      const int chunk = slot ^ swz<GG::NCH>(row);
       int64_t grow = r0 + row;
       grow = grow < m ? grow : m - 1;
       int col = c0w + chunk * 8;
@@ -206,31 +232,47 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     else issue_impl(blk, buf, std::false_type{});
   };
 
-  // prefetch depth PD = NBUF - 1 blocks ahead of the one being consumed
-  constexpr int PD = NBUF - 1;
-  int64_t my = 0;  // local iteration index
+  // PIPE (X & 4): step 3/4 of block j-1 runs between the two barriers of
+  // block j, beside the cross-wave reduction of block j (which only 24 lanes
+  // of each wave work on), instead of after the second barrier: the
+  // reduction's LDS latency and the barrier waits overlap MFMA work.  Needs
+  // the A tile of block j-1 resident while block j is consumed (prefetch
+  // depth NBUF - 2) and the reduced y double-buffered.
+  constexpr bool PIPE = (X & 4) != 0;
+  constexpr int PD = PIPE ? NBUF - 2 : NBUF - 1;
+  static_assert(PD >= 1, "ring too shallow");
+  constexpr int YFSZ = GG::YFS * GG::KP;   // floats per reduced-y buffer
 #pragma unroll
   for (int p = 0; p < PD; ++p)
     if (b0 + p * bstep < nblocks) issue(b0 + p * bstep, p);
 
   // blocks this workgroup owns (one 64-bit division, outside the loop)
   const int64_t nloc = b0 < nblocks ? (nblocks - 1 - b0) / bstep + 1 : 0;
-  for (int64_t blk = b0; blk < nblocks; blk += bstep, ++my) {
+  const int64_t niter = nloc + (PIPE && nloc > 0 ? 1 : 0);
+  int64_t my = 0;  // local iteration index
+  for (; my < niter; ++my) {
+    SL_STAMP(0)
+    const int64_t blk = b0 + my * bstep;
+    const bool have = my < nloc;   // false only on PIPE's drain iteration
     const int buf = (int)(my % NBUF);
     // X: the ring slots are private to the wave, so the next prefetch goes out
     // at the top of the iteration (into the slot this wave finished with in the
     // previous one) and PD blocks stay in flight throughout
-    if constexpr ((X & 1) != 0) {
-      if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
+    if constexpr ((X & 1) != 0 || PIPE) {
+      if (have && blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
     }
+    const char* region = abuf + (buf * WAVES + w) * GG::REGION;
+    float* yfc = PIPE ? yf + (my & 1) * YFSZ : yf;
+    const int g4 = lane >> 4, i16 = lane & 15;
+    if (have) {
     // blocks issued after this one and still possibly in flight
     const int64_t rem = nloc - 1 - my;
-    const int younger = (X & 1) ? (int)(rem < PD ? rem : PD) : (int)(rem < PD - 1 ? rem : PD - 1);
+    const int younger = ((X & 1) || PIPE) ? (int)(rem < PD ? rem : PD) : (int)(rem < PD - 1 ? rem : PD - 1);
     if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GG::LPB) : "memory");
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GG::LPB) : "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const char* region = abuf + (buf * WAVES + w) * GG::REGION;
+    SL_STAMP(1)
 
     // ---- step 1: partial y over this wave's columns
     f32x4 accY[KT];
@@ -241,7 +283,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       if (ab & 1) break;  // ablation (tuning only)
       const int row = lane & 15;
       const int chunk = (lane >> 4) + 4 * ks;
-      const int slot = chunk ^ (row & (GG::NCH - 1));
+      const int slot = chunk ^ swz<GG::NCH>(row);
       const bf16x8 af = *(const bf16x8*)(region + row * GG::ROWB + slot * 16);
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
@@ -252,28 +294,29 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     // ---- step 2: cross-wave reduction of y through LDS.  Partials are stored
     //      column-major ([wave][col][16 rows]) so that every access is b128:
     //      a lane's C fragment is 4 consecutive rows of one column.
-    const int g4 = lane >> 4, i16 = lane & 15;
+    SL_STAMP(2)
     if (!(ab & 2)) {
 #pragma unroll
     for (int t = 0; t < KT; ++t)
-      *(f32x4*)&yp[((w * GG::KP) + 16 * t + i16) * BM + 4 * g4] = accY[t];
+      *(f32x4*)&yp[((w * GG::KP) + 16 * t + i16) * GG::YPS + 4 * g4] = accY[t];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    SL_STAMP(3)
     {
       constexpr int CPW = GG::KP / WAVES;  // columns reduced per wave
       const int64_t r0 = blk * BM;
       const bool full = r0 + BM <= m;        // wave-uniform: only the last block is ragged
       if (lane < CPW * 4) {
         const int col = w * CPW + (lane >> 2), rg = lane & 3;
-        f32x4 sum = *(const f32x4*)&yp[col * BM + 4 * rg];
+        f32x4 sum = *(const f32x4*)&yp[col * GG::YPS + 4 * rg];
 #pragma unroll
-        for (int v = 1; v < WAVES; ++v) sum += *(const f32x4*)&yp[(v * GG::KP + col) * BM + 4 * rg];
+        for (int v = 1; v < WAVES; ++v) sum += *(const f32x4*)&yp[(v * GG::KP + col) * GG::YPS + 4 * rg];
         if (!full) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (r0 + 4 * rg + j >= m) sum[j] = 0.f;
         }
-        *(f32x4*)&yf[col * BM + 4 * rg] = sum;
+        *(f32x4*)&yfc[col * GG::YFS + 4 * rg] = sum;
         if constexpr (STORE_Y) {
           if (col < k) {
             float* yrow = Y + (r0 + 4 * rg) * ldy + col;
@@ -289,22 +332,30 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         }
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!PIPE) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
+    }
+    SL_STAMP(4)
+    }  // have
 
     // prefetch PD blocks ahead into the buffer this wave consumed last iteration
-    if constexpr ((X & 1) == 0) {
+    if constexpr ((X & 1) == 0 && !PIPE) {
       if (blk + PD * bstep < nblocks) issue(blk + PD * bstep, (int)((my + PD) % NBUF));
     }
 
+    // ---- steps 3/4 on block `my` (or, PIPE, on block my - 1)
+    if (!PIPE || my > 0) {
+    const char* s3region = PIPE ? abuf + ((int)((my - 1) % NBUF) * WAVES + w) * GG::REGION : region;
+    const float* s3yf = PIPE ? yf + ((my - 1) & 1) * YFSZ : yf;
     // y fragments with rows 4(l>>4)+j of column 16t+(l&15) (K=16 MFMA layout), hi/lo
     const bool hi_only = (ab & 32) != 0;
     const bool need_g = DO_G && !(ab & 8);
     s16x4 yh[KT], yl[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      const f32x4 v = *(const f32x4*)&yf[(16 * t + i16) * BM + 4 * g4];
+      const f32x4 v = *(const f32x4*)&s3yf[(16 * t + i16) * GG::YFS + 4 * g4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const short h = bf16_bits(v[j]);
@@ -312,11 +363,11 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         yl[t][j] = bf16_bits(v[j] - bf16_val(h));
       }
     }
+    SL_STAMP(5)
     if (DO_W && !(ab & 4)) {
       const int q = i16 >> 2, p = i16 & 3;
       // ---- step 3: one transposed LDS read per 16-column tile of A,
-      //      W += A^T y_hi (+ A^T y_lo).  (A single K=32 MFMA over [y_hi; y_lo]
-      //      needs two transposed reads per tile and measured 15% slower.)
+      //      W += A^T y_hi (+ A^T y_lo).
       const int row = 4 * g4 + q;
       // hi_only is wave-uniform: one branch selects a whole unrolled copy
       // (a macro, not a lambda: capturing the accumulator arrays by reference
@@ -324,7 +375,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
 #define SL_STEP3(HI)                                                                                  \
   _Pragma("unroll") for (int ct = 0; ct < NW / 16; ++ct) {                                           \
     const int chunk = 2 * ct + (p >> 1);                                                             \
-    const char* addr = region + row * GG::ROWB + (chunk ^ (row & (GG::NCH - 1))) * 16 + (p & 1) * 8;  \
+    const char* addr = s3region + row * GG::ROWB + (chunk ^ swz<GG::NCH>(row)) * 16 + (p & 1) * 8;    \
     const s16x4 af = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)addr); \
     _Pragma("unroll") for (int t = 0; t < KT; ++t) {                                                 \
       accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, yh[t], accW[ct][t], 0, 0, 0);     \
@@ -342,8 +393,8 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         bf16x8 yb[KT];
 #pragma unroll
         for (int t = 0; t < KT; ++t) {
-          const f32x4 va = *(const f32x4*)&yf[(16 * t + i16) * BM + r8];
-          const f32x4 vb = *(const f32x4*)&yf[(16 * t + i16) * BM + r8 + 4];
+          const f32x4 va = *(const f32x4*)&s3yf[(16 * t + i16) * GG::YFS + r8];
+          const f32x4 vb = *(const f32x4*)&s3yf[(16 * t + i16) * GG::YFS + r8 + 4];
           s16x8 e;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -357,8 +408,8 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         for (int ct = 0; ct < NW / 16; ++ct) {
           const int chunk = 2 * ct + (p >> 1);
           const int ra = r8 + q, rbb = r8 + 4 + q;
-          const char* aa = region + ra * GG::ROWB + (chunk ^ (ra & (GG::NCH - 1))) * 16 + (p & 1) * 8;
-          const char* ab2 = region + rbb * GG::ROWB + (chunk ^ (rbb & (GG::NCH - 1))) * 16 + (p & 1) * 8;
+          const char* aa = s3region + ra * GG::ROWB + (chunk ^ swz<GG::NCH>(ra)) * 16 + (p & 1) * 8;
+          const char* ab2 = s3region + rbb * GG::ROWB + (chunk ^ swz<GG::NCH>(rbb)) * 16 + (p & 1) * 8;
           const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)aa);
           const s16x4 b4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((s16x4 __attribute__((address_space(3)))*)ab2);
           s16x8 a8;
@@ -393,8 +444,8 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
               const int s = tau / WAVES;
 #pragma unroll
               for (int u = 0; u < BM / 4; ++u) {
-                const double va = (double)yf[(16 * t1 + i16) * BM + 4 * u + g4];
-                const double vb = (double)yf[(16 * t2 + i16) * BM + 4 * u + g4];
+                const double va = (double)s3yf[(16 * t1 + i16) * GG::YFS + 4 * u + g4];
+                const double vb = (double)s3yf[(16 * t2 + i16) * GG::YFS + 4 * u + g4];
                 accG64[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, accG64[s], 0, 0, 0);
               }
             }
@@ -414,8 +465,28 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         }
       }
     }
+    }  // steps 3/4
+    if constexpr (PIPE) {
+      if (have && !(ab & 2)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    if constexpr (ST) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      SL_STAMP(6)
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ST) {
+    if (lane == 0) {
+      unsigned long long* d = dbg + ((int64_t)blockIdx.x * WAVES + w) * 8;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) d[i] = st_acc[i];
+      d[6] = (unsigned long long)my;
+    }
+  }
+#undef SL_STAMP
 
   // ---- partial slabs: W rows = A columns, layout [WAVES*NW][KP]
   if constexpr (DO_W) {
@@ -548,20 +619,21 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
-int g_x = -1;  // SL_TSK_X bits: 1 top-of-loop prefetch, 2 K = 32 hi/lo step 3 (default 3)
+int g_x = -1;  // SL_TSK_X bits: 1 top-of-loop prefetch, 2 K = 32 hi/lo step 3, 4 PIPE, 8 nt loads (default 3)
 
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
           bool G64 = false, int X = 0>
 int launch_x(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
-  using GG = Geo<NW, KT, NBUF>;
+  using GG = Geo<NW, KT, NBUF, (X & 4) ? 2 : 1>;
   auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, X>;
   static bool attr = false;
   if (!attr) {
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
     attr = true;
   }
-  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, g_ablate | g_flags);
+  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy,
+                                             g_ablate | g_flags | ((g_x & 8) ? 64 : 0), nullptr);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -578,13 +650,22 @@ int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int
   // bit 0: top-of-loop prefetch; bit 1: K = 32 hi/lo step 3 (exact passes only:
   // the hi-only intermediate form costs the same on K = 16)
   if constexpr (DO_W && !ZSPLIT && KT <= 3) {
-    switch (g_x & 3) {
-      case 1: return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 1>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-      case 2: if constexpr (!HI_T) return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 2>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s); break;
-      case 3: if constexpr (!HI_T) return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 3>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-              return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 1>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+    // bit 2: PIPE (step 3/4 of the previous block between the barriers of the
+    // current one); needs a 3-deep ring and room for the second y buffer
+    constexpr bool PIPE_OK = NBUF >= 3 && Geo<NW, KT, NBUF, 2>::LDS <= 160 * 1024;
+    const int x = (g_x & 3) | ((PIPE_OK && (g_x & 4)) ? 4 : 0);
+#define SL_LX(XX) return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, XX>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s)
+    switch (x) {
+      case 1: SL_LX(1);
+      case 2: if constexpr (!HI_T) { SL_LX(2); } break;
+      case 3: if constexpr (!HI_T) { SL_LX(3); } SL_LX(1);
+      case 4: if constexpr (PIPE_OK) { SL_LX(4); } break;
+      case 5: if constexpr (PIPE_OK) { SL_LX(5); } break;
+      case 6: if constexpr (PIPE_OK && !HI_T) { SL_LX(6); } break;
+      case 7: if constexpr (PIPE_OK) { if constexpr (!HI_T) { SL_LX(7); } SL_LX(5); } break;
       default: break;
     }
+#undef SL_LX
   }
   return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 0>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
 }
@@ -618,6 +699,33 @@ int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, 
 }
 
 }  // namespace
+
+// Diagnostic: the headline-shape intermediate (flags 3, no Gram) or final
+// (G64 + Y) pass with per-phase s_memtime sums per wave:
+// dbg[(wg * 8 + wave) * 8 + i], i < 6 = (dma wait, step 1, partial write +
+// barrier 1, reduce + barrier 2, y fragments, step 3/4), 6 = blocks.
+SL_API int sl_tsk_stamp_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
+                             float* Y, unsigned long long* dbg, int final_pass, void* stream) {
+  if (n > 1024 || n <= 512 || k > 48 || k <= 32) return SL_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* z = (const bf16_t*)Zt;
+  float* Wslab = (float*)ws;
+  const int g = grid_for(m);
+  float* Gslab = Wslab + (int64_t)g * 1024 * 48;
+  using GG = Geo<128, 3, 3>;
+  if (final_pass) {
+    auto kern = k_tsk_pass<128, 3, true, true, true, false, 3, false, true, 3, true>;
+    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
+    kern<<<g, THREADS, GG::LDS, s>>>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, k, 0, dbg);
+  } else {
+    auto kern = k_tsk_pass<128, 3, true, false, false, false, 3, true, false, 1, true>;
+    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
+    kern<<<g, THREADS, GG::LDS, s>>>(a, m, (int)n, lda, z, k, Wslab, nullptr, nullptr, 0, 0, dbg);
+  }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
 
 SL_API int sl_tsk_set_x(int x) {
   g_x = x;
