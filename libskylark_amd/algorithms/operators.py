@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import torch
 
+from ..ops import krylov_native as _kn
 from ..parallel.comm import Comm
 from ..parallel.distmatrix import DistMatrix
 
@@ -39,14 +40,25 @@ class Operator:
     def rmatmul(self, Y):
         raise NotImplementedError
 
-    # column 2-norms / dots of LONG vectors (all-reduce when distributed)
+    # column 2-norms / dots of LONG vectors (all-reduce when distributed); on
+    # the GPU one native streaming pass each (ops/krylov_native.py, f64 sums)
     def long_colnorm(self, U):
+        if _kn.ok(U):
+            s = _kn.colsumsq(U)
+            if self.distributed:
+                self.comm.all_reduce(s)
+            return s.sqrt().to(U.dtype)
         s = (U * U).sum(0)
         if self.distributed:
             self.comm.all_reduce(s)
         return s.sqrt()
 
     def long_coldot(self, U, V):
+        if _kn.ok(U) and isinstance(V, torch.Tensor) and V.shape == U.shape and V.is_cuda:
+            s = _kn.coldot(U, V)
+            if self.distributed:
+                self.comm.all_reduce(s)
+            return s.to(U.dtype)
         s = (U * V).sum(0)
         if self.distributed:
             self.comm.all_reduce(s)
@@ -54,6 +66,8 @@ class Operator:
 
     @staticmethod
     def short_colnorm(X):
+        if _kn.ok(X):
+            return _kn.colsumsq(X).sqrt().to(X.dtype)
         return (X * X).sum(0).sqrt()
 
     def long_like(self, B):
@@ -81,9 +95,20 @@ class DenseOp(Operator):
         if self.A.dtype in (torch.bfloat16, torch.float16):
             from ..ops import tallskinny as T
             return T.matmul(self.A, X, out_dtype=self.dtype)
+        if X.dim() == 2 and self.has_fused_normal(X.shape[1]):
+            # A X from the one-pass kernel (its A^T A X byproduct is discarded):
+            # ~6 TB/s against ~2.4 TB/s for the library GEMV on tall f32 A
+            from ..ops import normal_eq
+            return normal_eq.ata(self.A, X, want_y=True)[1]
         return self.A @ X.to(self.A.dtype)
 
     def rmatmul(self, Y):
+        if Y.dim() == 2 and self.A.dtype == torch.float32 and self.has_fused_normal(Y.shape[1]) \
+                and Y.shape[0] == self.A.shape[0]:
+            # A^T Y as the dual pass with D = Y (one read of A; the transposed
+            # library GEMV ran at ~1 TB/s)
+            from ..ops import normal_eq
+            return normal_eq.dual(self.A, Y.to(torch.float32))[0]
         if self.A.dtype in (torch.bfloat16, torch.float16):
             hi = Y.to(self.A.dtype)
             lo = (Y - hi.to(Y.dtype)).to(self.A.dtype)

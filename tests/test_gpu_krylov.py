@@ -1,0 +1,87 @@
+"""Native Krylov vector kernels (krylov_kernels.hip) vs torch fp64 references,
+and the device-scalar LSQR against the torch-op LSQR on the same problem."""
+import math
+
+import pytest
+import torch
+
+from libskylark_amd.algorithms import krylov as K
+from libskylark_amd.ops import krylov_native as kn
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,dt", [(100003, 1, torch.float32), (5000, 3, torch.float64), (777, 40, torch.float32),
+                                    (1, 64, torch.float64), (65536, 17, torch.float32)])
+def test_colsumsq_coldot_axpby(dev, m, k, dt):
+    g = torch.Generator().manual_seed(m + k)
+    X = torch.randn(m, k, generator=g, dtype=torch.float64)
+    Y = torch.randn(m, k, generator=g, dtype=torch.float64)
+    Xd, Yd = X.to(dev, dt), Y.to(dev, dt)
+    tol = 1e-5 if dt == torch.float32 else 1e-12
+    ref = (Xd.double() ** 2).sum(0)
+    assert torch.allclose(kn.colsumsq(Xd), ref, rtol=tol)
+    assert torch.allclose(kn.coldot(Xd, Yd), (Xd.double() * Yd.double()).sum(0), rtol=tol, atol=tol * m)
+    a = torch.randn(k, generator=g, dtype=torch.float64).to(dev)
+    b = torch.randn(k, generator=g, dtype=torch.float64).to(dev)
+    want = (a * Xd.double() + b * Yd.double())
+    s2 = kn.axpby_colsumsq(Xd, Yd, a, b)
+    assert torch.allclose(Yd.double(), want, rtol=tol, atol=tol)
+    assert torch.allclose(s2, (Yd.double() ** 2).sum(0), rtol=tol)
+    kn.colscale(Yd, s2.sqrt(), inv=True)
+    assert torch.allclose(Yd.double().norm(dim=0), torch.ones(k, dtype=torch.float64, device=dev), rtol=1e-4)
+    # strided view (column slice of a wider matrix)
+    Wd = torch.randn(m, k + 5, device=dev, dtype=dt)[:, 2:2 + k]
+    assert torch.allclose(kn.colsumsq(Wd), (Wd.double() ** 2).sum(0), rtol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
+def test_native_lsqr_matches_torch_lsqr(dev, fused):
+    from libskylark_amd.algorithms.regression import _build_precond
+    g = torch.Generator().manual_seed(11)
+    m, n, k = 30000, 200, 2
+    A = (torch.randn(m, n, generator=g) * torch.logspace(0, -3, n)).to(dev)
+    B = torch.randn(m, k, generator=g).to(dev)
+    S = torch.randn(4 * n, m, generator=g).to(dev) / math.sqrt(4 * n)
+    P, _ = _build_precond(S @ A, "qr")
+    p = K.KrylovIterParams(tolerance=1e-6, iter_lim=100, fused_normal=fused, check_every=4)
+    Xn, cn = K.lsqr(A, B, params=p, R=P)
+    kn.ENABLED = False
+    try:
+        Xt, ct = K.lsqr(A, B, params=p, R=P)
+    finally:
+        kn.ENABLED = True
+    assert cn in (-2, -3) and ct in (-2, -3)
+    rn = (A @ Xn - B).norm() / B.norm()
+    rt = (A @ Xt - B).norm() / B.norm()
+    assert abs(float(rn / rt) - 1) < 1e-4
+    assert float((Xn - Xt).norm() / Xt.norm()) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nr,nc,k,dt", [(1000, 1000, 1, torch.float32), (5000, 5000, 2, torch.float32),
+                                        (333, 777, 5, torch.float64), (64, 3, 8, torch.float32)])
+def test_thin_gemm(dev, nr, nc, k, dt):
+    g = torch.Generator().manual_seed(nr + k)
+    M = torch.randn(nr, nc, generator=g, dtype=torch.float64)
+    X = torch.randn(nc, k, generator=g, dtype=torch.float64)
+    Md, Xd = M.to(dev, dt), X.to(dev, dt)
+    assert kn.thin_gemm_ok(Md, Xd)
+    Y = kn.thin_gemm(Md, Xd)
+    ref = Md.double() @ Xd.double()
+    tol = 1e-6 if dt == torch.float32 else 1e-13
+    assert float((Y.double() - ref).norm() / ref.norm()) < tol
+
+
+@pytest.mark.gpu
+def test_dense_operator_native_products(dev):
+    from libskylark_amd.algorithms.operators import DenseOp
+    g = torch.Generator().manual_seed(2)
+    A = torch.randn(50001, 700, generator=g)
+    X = torch.randn(700, 3, generator=g)
+    Yv = torch.randn(50001, 3, generator=g)
+    op = DenseOp(A.to(dev))
+    AX = op.matmul(X.to(dev)).double().cpu()
+    AtY = op.rmatmul(Yv.to(dev)).double().cpu()
+    assert float((AX - A.double() @ X.double()).norm() / AX.norm()) < 1e-5
+    assert float((AtY - A.double().t() @ Yv.double()).norm() / AtY.norm()) < 1e-5
