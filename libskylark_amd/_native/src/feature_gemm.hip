@@ -42,7 +42,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
 
-enum { EPI_NONE = 0, EPI_COS = 1, EPI_EXPNEG = 2 };
+enum { EPI_NONE = 0, EPI_COS = 1, EPI_EXPNEG = 2, EPI_GAUSS = 3, EPI_POLY = 4 };
 
 __device__ __forceinline__ uint32_t f2bf_bits(float f) {
   uint32_t u = __float_as_uint(f);
@@ -65,9 +65,18 @@ template <typename OutT> __device__ __forceinline__ OutT cvt_out(float v);
 template <> __device__ __forceinline__ float cvt_out<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16_t cvt_out<bf16_t>(float v) { return (bf16_t)f2bf_bits(v); }
 
+// EPI_GAUSS: kernel Gram exp(-a |x_i - y_j|^2) = exp(2a x.y - a|y|^2 - a|x|^2)
+// with sc = 2a, sh = -a|y_j|^2, rt = -a|x_i|^2 (exponent clamped at 0: the
+// distance can round below zero); EPI_POLY: (a x.y + c)^q with sc = a, sh = c,
+// p0 = q.  (Reference kernels: ml/kernels.hpp gram().)
 template <int EPI>
-__device__ __forceinline__ float epilogue(float x, float sc, float sh, float outscale) {
-  if constexpr (EPI == EPI_COS) {
+__device__ __forceinline__ float epilogue(float x, float sc, float sh, float outscale, float rt = 0.f,
+                                          float p0 = 0.f) {
+  if constexpr (EPI == EPI_GAUSS) {
+    return outscale * __expf(fminf(x * sc + sh + rt, 0.f));
+  } else if constexpr (EPI == EPI_POLY) {
+    return outscale * powf(x * sc + sh, p0);
+  } else if constexpr (EPI == EPI_COS) {
     // cos via v_cos_f32, which takes revolutions: reduce to [0, 1) first
     // v_fract_f32: one instruction for the reduction to [0, 1)
     const float rev = __builtin_amdgcn_fractf((x * sc + sh) * 0.15915494309189535f);
@@ -84,7 +93,8 @@ __global__ void __launch_bounds__(NT, 2)
 k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int64_t M, int64_t K, int64_t lda,
             const bf16_t* __restrict__ Whi, const bf16_t* __restrict__ Wlo, int64_t Nf, int64_t ldw,
             const float* __restrict__ scales, const float* __restrict__ shifts, float outscale,
-            OutT* __restrict__ out, int64_t ldo, int ntm, int ntn, int per) {
+            OutT* __restrict__ out, int64_t ldo, int ntm, int ntn, int per,
+            const float* __restrict__ rowterm, float p0) {
   // one LDS array: the K-loop staging planes, reused by the epilogue to turn
   // the MFMA C fragments (4 rows x 1 column per lane) into row-contiguous
   // 16-B stores (the store tail is issue-bound: cdna_hip_programming.md T21)
@@ -256,9 +266,15 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e) {
+          float rt = 0.f;
+          if constexpr (EPI == EPI_GAUSS) {
+            const int64_t r = row0 + wr * 64 + rb * 16 + 4 * (lane >> 4) + e;
+            rt = (rowterm && r < M) ? rowterm[r] : 0.f;
+          }
           blk[(rb * 16 + 4 * (lane >> 4) + e) * EPI_LD + cb * 16 + (lane & 15)] =
-              epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale);
+              epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale, rt, p0);
+        }
     }
     __syncthreads();
     const int64_t rbase = row0 + wr * 64;
@@ -296,7 +312,11 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
         const int64_t r = row0 + wr * 64 + rb * 16 + 4 * (lane >> 4);
         float v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale);
+        for (int e = 0; e < 4; ++e) {
+          float rt = 0.f;
+          if constexpr (EPI == EPI_GAUSS) rt = (rowterm && r + e < M) ? rowterm[r + e] : 0.f;
+          v[e] = epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale, rt, p0);
+        }
         OutT* p = out + f * ldo + r;
         if (r + 3 < M) {
           if constexpr (sizeof(OutT) == 4) {
@@ -314,12 +334,12 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
 template <bool ALO, bool WLO, int EPI>
 int launch_out(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda, const bf16_t* Whi,
                const bf16_t* Wlo, int64_t Nf, int64_t ldw, const float* sc, const float* sh, float outscale,
-               void* out, int out_dtype, int64_t ldo, int out_t, hipStream_t s) {
+               void* out, int out_dtype, int64_t ldo, int out_t, hipStream_t s, const float* rt, float p0) {
   const int ntm = (int)((M + BM - 1) / BM), ntn = (int)((Nf + BN - 1) / BN);
   const int T = ntm * ntn, per = (T + 7) / 8;
   const unsigned grid = (unsigned)(8 * per);
 #define SL_FG_L(OT, TRANS) \
-  k_feat_gemm<ALO, WLO, EPI, TRANS, OT><<<grid, NT, 0, s>>>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale, (OT*)out, ldo, ntm, ntn, per)
+  k_feat_gemm<ALO, WLO, EPI, TRANS, OT><<<grid, NT, 0, s>>>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale, (OT*)out, ldo, ntm, ntn, per, rt, p0)
   if (out_dtype == SL_F32) { if (out_t) SL_FG_L(float, true); else SL_FG_L(float, false); }
   else if (out_dtype == SL_BF16) { if (out_t) SL_FG_L(bf16_t, true); else SL_FG_L(bf16_t, false); }
   else return SL_ERR_UNSUPPORTED;
@@ -366,10 +386,11 @@ k_split_bf16(const float* __restrict__ A, int64_t M, int64_t K, int64_t lda, bf1
 //   * Whi / Wlo: ceil(Nf/128)*128 rows x ldw bf16, ldw % 32 == 0, ldw >= K,
 //     zero in the padding (Wlo may be null);
 //   * out: f32 or bf16, Z[r*ldo + f] (out_t = 0) or Z[f*ldo + r] (out_t = 1).
-SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda,
-                           const bf16_t* Whi, const bf16_t* Wlo, int64_t Nf, int64_t ldw,
-                           const float* scales, const float* shifts, float outscale, int epi,
-                           void* out, int out_dtype, int64_t ldo, int out_t, void* stream) {
+SL_API int sl_feature_gemm2(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda,
+                            const bf16_t* Whi, const bf16_t* Wlo, int64_t Nf, int64_t ldw,
+                            const float* scales, const float* shifts, float outscale, int epi,
+                            void* out, int out_dtype, int64_t ldo, int out_t, const float* rowterm, float p0,
+                            void* stream) {
   if (M <= 0 || Nf <= 0) return SL_OK;
   if (K <= 0 || ldw % BK != 0 || ldw < K || lda % BK != 0 || lda < K) return SL_ERR_DIMENSION;
   if (((uintptr_t)Ahi & 15) || ((uintptr_t)Whi & 15) || (Alo && ((uintptr_t)Alo & 15)) ||
@@ -379,17 +400,30 @@ SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int6
   if (epi == EPI_COS && shifts == nullptr) return SL_ERR_INVALID;
   hipStream_t s = (hipStream_t)stream;
   const bool alo = Alo != nullptr, wlo = Wlo != nullptr;
-#define SL_FG_E(AL, WL)                                                                              \
-  switch (epi) {                                                                                     \
-    case EPI_NONE: return launch_out<AL, WL, EPI_NONE>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
-    case EPI_COS: return launch_out<AL, WL, EPI_COS>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
-    case EPI_EXPNEG: return launch_out<AL, WL, EPI_EXPNEG>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s); \
-    default: return SL_ERR_INVALID;                                                                  \
+#define SL_FG_C(AL, WL, E) \
+  return launch_out<AL, WL, E>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, out, out_dtype, ldo, out_t, s, rowterm, p0)
+#define SL_FG_E(AL, WL)                                  \
+  switch (epi) {                                         \
+    case EPI_NONE: SL_FG_C(AL, WL, EPI_NONE);            \
+    case EPI_COS: SL_FG_C(AL, WL, EPI_COS);              \
+    case EPI_EXPNEG: SL_FG_C(AL, WL, EPI_EXPNEG);        \
+    case EPI_GAUSS: SL_FG_C(AL, WL, EPI_GAUSS);          \
+    case EPI_POLY: SL_FG_C(AL, WL, EPI_POLY);            \
+    default: return SL_ERR_INVALID;                      \
   }
   if (alo) { if (wlo) { SL_FG_E(true, true) } else { SL_FG_E(true, false) } }
   else { if (wlo) { SL_FG_E(false, true) } else { SL_FG_E(false, false) } }
 #undef SL_FG_E
+#undef SL_FG_C
   return SL_ERR_UNSUPPORTED;
+}
+
+SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda,
+                           const bf16_t* Whi, const bf16_t* Wlo, int64_t Nf, int64_t ldw,
+                           const float* scales, const float* shifts, float outscale, int epi,
+                           void* out, int out_dtype, int64_t ldo, int out_t, void* stream) {
+  return sl_feature_gemm2(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, epi, out, out_dtype, ldo,
+                          out_t, nullptr, 0.f, stream);
 }
 
 SL_API int sl_split_bf16(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t ldp,

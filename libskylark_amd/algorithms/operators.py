@@ -138,11 +138,19 @@ class SparseOp(Operator):
         self._At = None
 
     def matmul(self, X):
+        from ..ops import spmm
+        if X.dim() == 2 and spmm.ok(self.A, X):
+            return spmm.csr_mm(self.A, X)
         return torch.sparse.mm(self.A, X.to(self.dtype))
 
     def rmatmul(self, Y):
+        # the CSR of A^T is built once per operator (deterministic sums; an
+        # atomic scatter A^T Y would not be)
         if self._At is None:
             self._At = self.A.to_sparse_coo().t().coalesce().to_sparse_csr()
+        from ..ops import spmm
+        if Y.dim() == 2 and spmm.ok(self._At, Y):
+            return spmm.csr_mm(self._At, Y)
         return torch.sparse.mm(self._At, Y.to(self.dtype))
 
 

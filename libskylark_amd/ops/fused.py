@@ -21,7 +21,7 @@ import torch
 
 from . import _lib
 
-EPI_NONE, EPI_COS, EPI_EXPNEG = 0, 1, 2
+EPI_NONE, EPI_COS, EPI_EXPNEG, EPI_GAUSS, EPI_POLY = 0, 1, 2, 3, 4
 BN, BK = 128, 32
 MAX_W_ELEMS = 1 << 26          # W (S x N) realised whole up to 64 M entries (256 MB as hi+lo)
 
@@ -29,6 +29,10 @@ _lib.register("sl_feature_gemm", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, 
                                   C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                                   C.c_void_p, C.c_void_p, C.c_float, C.c_int,
                                   C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p])
+_lib.register("sl_feature_gemm2", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
+                                   C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                   C.c_void_p, C.c_void_p, C.c_float, C.c_int,
+                                   C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p, C.c_float, C.c_void_p])
 _lib.register("sl_split_bf16", [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                 C.c_void_p])
 
@@ -92,7 +96,7 @@ def split_planes(X: torch.Tensor):
 
 def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=None,
                  outscale: float = 1.0, epi: int = EPI_NONE, out_dtype=torch.float32,
-                 use_lo: bool = True) -> torch.Tensor:
+                 use_lo: bool = True, rowterm=None, p0: float = 0.0) -> torch.Tensor:
     """Columnwise (dim 0: A is K x m -> Z is nf x m) or rowwise (dim 1: A is
     m x K -> Z is m x nf) fused product with W^T and the epilogue."""
     X = A if dim == 1 else A.t()
@@ -111,11 +115,12 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
     sh = shifts.to(device=dev, dtype=torch.float32).contiguous() if shifts is not None else None
     if W.ldw != ld:
         raise ValueError("feature_gemm: W and A planes must share the padded inner dimension")
-    _lib.call("sl_feature_gemm", _lib.ptr(hi), _lib.ptr(lo) if lo is not None else None, m, k, ld,
+    rt = rowterm.to(device=dev, dtype=torch.float32).contiguous() if rowterm is not None else None
+    _lib.call("sl_feature_gemm2", _lib.ptr(hi), _lib.ptr(lo) if lo is not None else None, m, k, ld,
               _lib.ptr(W.hi), _lib.ptr(W.lo) if use_lo else None, W.nf, W.ldw,
               _lib.ptr(sc) if sc is not None else None, _lib.ptr(sh) if sh is not None else None,
               float(outscale), int(epi), _lib.ptr(out), _lib.dtype_code(out_dtype), ldo, out_t,
-              C.c_void_p(_lib.stream_of(out)))
+              _lib.ptr(rt) if rt is not None else None, float(p0), C.c_void_p(_lib.stream_of(out)))
     return out
 
 

@@ -85,3 +85,25 @@ def test_dense_operator_native_products(dev):
     AtY = op.rmatmul(Yv.to(dev)).double().cpu()
     assert float((AX - A.double() @ X.double()).norm() / AX.norm()) < 1e-5
     assert float((AtY - A.double().t() @ Yv.double()).norm() / AtY.norm()) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,density,k,vdt", [(20000, 3000, 5e-4, 1, torch.float32), (5000, 8000, 0.01, 3, torch.float64),
+                                               (1000, 500, 0.2, 20, torch.float32), (77, 33, 0.3, 40, torch.float64)])
+def test_csr_spmm_and_sparse_operator(dev, m, n, density, k, vdt):
+    from libskylark_amd.algorithms.operators import SparseOp
+    from libskylark_amd.ops import spmm
+    g = torch.Generator().manual_seed(m + k)
+    nnz = max(1, int(m * n * density))
+    idx = torch.stack([torch.randint(0, m, (nnz,), generator=g), torch.randint(0, n, (nnz,), generator=g)])
+    A = torch.sparse_coo_tensor(idx, torch.randn(nnz, generator=g, dtype=torch.float64), (m, n)).coalesce()
+    Ad = A.to_dense()
+    Acsr = A.to(vdt).to_sparse_csr().to(dev)
+    X = torch.randn(n, k, generator=g, dtype=torch.float64)
+    Yv = torch.randn(m, k, generator=g, dtype=torch.float64)
+    tol = 1e-5 if vdt == torch.float32 else 1e-12
+    got = spmm.csr_mm(Acsr, X.to(dev)).double().cpu()
+    assert float((got - Ad @ X).norm() / (Ad @ X).norm()) < tol
+    op = SparseOp(Acsr)
+    got_t = op.rmatmul(Yv.to(dev)).double().cpu()
+    assert float((got_t - Ad.t() @ Yv).norm() / (Ad.t() @ Yv).norm()) < tol

@@ -74,3 +74,25 @@ def test_lsqr_on_gpu(dev):
     torch.testing.assert_close(X.cpu(), torch.linalg.lstsq(A, B).solution, rtol=1e-8, atol=1e-8)
     Xf = sk.nla.faster_least_squares(A.to(dev), B.to(dev), sk.Context(1))
     torch.testing.assert_close(Xf.cpu(), torch.linalg.lstsq(A, B).solution, rtol=1e-7, atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["gaussian", "polynomial"])
+def test_fused_gram_epilogue(dev, kind):
+    """Large Gram matrices take the fused MFMA + epilogue kernel (EPI_GAUSS /
+    EPI_POLY): compare with the fp64 definition."""
+    from libskylark_amd.ml import kernels as KM
+    g = torch.Generator().manual_seed(4)
+    m, n, d = 3000, 2000, 64
+    X = torch.randn(m, d, generator=g, dtype=torch.float64) / d ** 0.5
+    Y = torch.randn(n, d, generator=g, dtype=torch.float64) / d ** 0.5
+    if kind == "gaussian":
+        k = ml.Gaussian(d, sigma=0.8)
+        ref = torch.exp(-torch.cdist(X, Y) ** 2 / (2 * 0.8 ** 2))
+    elif kind == "polynomial":
+        k = ml.Polynomial(d, q=3, c=1.0, gamma=0.5)
+        ref = (0.5 * X @ Y.t() + 1.0) ** 3
+    assert m * n >= KM.FUSED_GRAM_MIN
+    K = k.gram(X.float().to(dev), Y=Y.float().to(dev)).double().cpu()
+    err = float((K - ref).abs().max() / ref.abs().max())
+    assert err < 1e-4, err
