@@ -196,43 +196,74 @@ def _gemm_dist(oA, oB, alpha, A, B, beta, C):
 
 
 def _summa(A, B):
-    """``[MC,MR] x [MC,MR] -> [MC,MR]`` on the pr x pc grid (Elemental's SUMMA
-    ``Gemm``; reference call sites e.g. ``ml/krr.hpp:423``).
+    """``[MC,MR] x [MC,MR] -> [MC,MR]`` on the pr x pc grid: SUMMA (Elemental's
+    ``Gemm`` for this layout; reference call sites e.g. ``ml/krr.hpp:423``).
 
-    Rank (r, c) needs A's block row r (spread over its process ROW) and B's
-    block column c (spread over its process COLUMN): one all-gather in the
-    row communicator and one in the column communicator, then a single local
-    GEMM into C's tiles.  Nothing else moves, and the two gathers are the
-    only collectives (their volume is m K / pr + K n / pc per rank)."""
+    The inner dimension K is walked in super-panels of ``L = lcm(pr, pc)``
+    consecutive K-blocks: every process column owns L / pc blocks of A's
+    super-panel and every process row L / pr blocks of B's, so one
+    all-gather in the row communicator (A: m/pr x L bK) and one in the
+    column communicator (B: L bK x n/pc) bring rank (r, c) exactly the
+    operands of its local update ``C_rc += A[R_r, panel] B[panel, C_c]``.
+    Memory per rank is one super-panel of each operand (O(m/pr L bK)), not
+    whole block rows; the collective volume is SUMMA's m K / pr + K n / pc."""
+    import math as _m
     from ..parallel.distmatrix import DistMatrix, _cyclic_blocks
     m, K = A.shape
     K2, n = B.shape
     if K != K2:
         raise DimensionMismatchError("Gemm: inner dimensions differ")
     g = A.grid
-    if B.grid is not g:
-        B = B.redistribute("MC_MR", grid=g)
+    bK = A.block[1]
+    if B.grid is not g or B.layout != "MC_MR" or B.block[0] != bK:
+        B = B.redistribute("MC_MR", grid=g, block=(bK, B.block[1]))
     dev = A.local.device
     dt = torch.promote_types(A.dtype, B.dtype)
-
-    def cols_of(c):
-        return [i for s, e in _cyclic_blocks(K, A.block[1], g.pc, c) for i in range(s, e)]
-
-    def rows_of(r):
-        return [i for s, e in _cyclic_blocks(K, B.block[0], g.pr, r) for i in range(s, e)]
-
-    # A[R_r, :]: gather the column pieces across the process row (ordered by column coordinate)
-    ccounts = [len(cols_of(c)) for c in range(g.pc)]
-    Ag = g.row_comm.all_gather_v(A.local.to(dt).contiguous(), ccounts, 1) if g.pc > 1 else A.local.to(dt)
-    Apanel = torch.empty(Ag.shape[0], K, dtype=dt, device=dev)
-    Apanel[:, torch.tensor([i for c in range(g.pc) for i in cols_of(c)], device=dev)] = Ag
-    # B[:, C_c]: gather the row pieces across the process column (ordered by row coordinate)
-    rcounts = [len(rows_of(r)) for r in range(g.pr)]
-    Bg = g.col_comm.all_gather_v(B.local.to(dt).contiguous(), rcounts, 0) if g.pr > 1 else B.local.to(dt)
-    Bpanel = torch.empty(K, Bg.shape[1], dtype=dt, device=dev)
-    Bpanel[torch.tensor([i for r in range(g.pr) for i in rows_of(r)], device=dev)] = Bg
-    Cloc = Apanel @ Bpanel
-    return DistMatrix(Cloc, (m, n), "MC_MR", A.comm, grid=g, block=(A.block[0], B.block[1]))
+    Aloc = A.local.to(dt)
+    Bloc = B.local.to(dt)
+    C = torch.zeros(Aloc.shape[0], Bloc.shape[1], dtype=dt, device=dev)
+    L = g.pr * g.pc // _m.gcd(g.pr, g.pc)
+    nblk = (K + bK - 1) // bK
+    # local column offsets of A's K-blocks (this process column) / row offsets of B's
+    a_off, off = {}, 0
+    for s0, e0 in _cyclic_blocks(K, bK, g.pc, g.mycol):
+        a_off[s0 // bK] = (off, e0 - s0)
+        off += e0 - s0
+    b_off, off = {}, 0
+    for s0, e0 in _cyclic_blocks(K, bK, g.pr, g.myrow):
+        b_off[s0 // bK] = (off, e0 - s0)
+        off += e0 - s0
+    for j0 in range(0, nblk, L):
+        blocks = list(range(j0, min(nblk, j0 + L)))
+        # A super-panel: process column c contributes its blocks j (j % pc == c), in order
+        mineA = [a_off[j] for j in blocks if j % g.pc == g.mycol]
+        pieceA = torch.cat([Aloc[:, o:o + w] for o, w in mineA], 1) if mineA else Aloc[:, :0]
+        cntA = [sum(min(K, (j + 1) * bK) - j * bK for j in blocks if j % g.pc == c) for c in range(g.pc)]
+        GA = g.row_comm.all_gather_v(pieceA.contiguous(), cntA, 1) if g.pc > 1 else pieceA
+        # B super-panel: process row r contributes its blocks j (j % pr == r)
+        mineB = [b_off[j] for j in blocks if j % g.pr == g.myrow]
+        pieceB = torch.cat([Bloc[o:o + w] for o, w in mineB], 0) if mineB else Bloc[:0]
+        cntB = [sum(min(K, (j + 1) * bK) - j * bK for j in blocks if j % g.pr == r) for r in range(g.pr)]
+        GB = g.col_comm.all_gather_v(pieceB.contiguous(), cntB, 0) if g.pr > 1 else pieceB
+        # gathered order is owner-major; put both operands in K order
+        posA, o = {}, 0
+        for c in range(g.pc):
+            for j in blocks:
+                if j % g.pc == c:
+                    w = min(K, (j + 1) * bK) - j * bK
+                    posA[j] = (o, w)
+                    o += w
+        posB, o = {}, 0
+        for r in range(g.pr):
+            for j in blocks:
+                if j % g.pr == r:
+                    w = min(K, (j + 1) * bK) - j * bK
+                    posB[j] = (o, w)
+                    o += w
+        Ap = torch.cat([GA[:, posA[j][0]:posA[j][0] + posA[j][1]] for j in blocks], 1)
+        Bp = torch.cat([GB[posB[j][0]:posB[j][0] + posB[j][1]] for j in blocks], 0)
+        C += Ap @ Bp
+    return DistMatrix(C, (m, n), "MC_MR", A.comm, grid=g, block=(A.block[0], B.block[1]))
 
 
 def Gemv(oA: str, alpha, A, x, beta=0.0, y=None):

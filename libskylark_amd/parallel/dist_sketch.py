@@ -24,7 +24,7 @@ from __future__ import annotations
 import torch
 
 from ..base.exceptions import DimensionMismatchError
-from .distmatrix import DistMatrix, canon, is_col_dist, is_row_dist
+from .distmatrix import DistMatrix, _cyclic_blocks, canon, is_col_dist, is_row_dist
 
 COLUMNWISE, ROWWISE = 0, 1
 
@@ -148,32 +148,141 @@ def _outer_panel(sk, A: DistMatrix, out_shape):
     return R
 
 
+def _mc_mr_algorithm(sk, A: DistMatrix, dim, kind) -> str:
+    """Panel algorithm for a sketch of an [MC,MR] matrix: ``params.mc_mr_algorithm``
+    forces one ("inner" / "outer" / "panel"); "auto" takes the reference's
+    inner-panel regime (both output dimensions below 1/factor of the sketched
+    one, ``dense_transform_Elemental_mc_mr.hpp:640-656``) and otherwise the
+    collective-volume rule of :func:`_use_outer_panel`."""
+    from ..sketch import params
+    forced = params.get_mc_mr_algorithm()
+    if kind != "linear" or A.local.layout != torch.strided:
+        return "panel"
+    if forced != "auto":
+        if forced == "outer" and not (dim == COLUMNWISE and A.grid.pr > 1):
+            return "panel"
+        return forced
+    N = A.shape[0] if dim == COLUMNWISE else A.shape[1]
+    width = A.shape[1] if dim == COLUMNWISE else A.shape[0]
+    S, f = sk.getsketchdim(), params.get_factor()
+    if S * f <= N and width * f <= N:
+        return "inner"
+    return "outer" if _use_outer_panel(sk, A, dim, kind) else "panel"
+
+
+def _owner_order(n, b, p):
+    """(counts per coordinate, global indices in coordinate-major order) of a
+    block-cyclic distribution of n entries in blocks of b over p coordinates."""
+    counts, order = [], []
+    for r in range(p):
+        blk = _cyclic_blocks(n, b, p, r)
+        counts.append(sum(e - s for s, e in blk))
+        order.extend(i for s, e in blk for i in range(s, e))
+    return counts, order
+
+
+def _panel_matrix(part, sk, A: DistMatrix, dim, out_shape, finish):
+    """Panel-matrix algorithm: this rank's partial product over its tiles of
+    the sketched dimension, then ONE reduce-scatter inside the grid-column
+    (columnwise) or grid-row (rowwise) communicator straight into the output's
+    block-cyclic rows / columns (reference ``panel_matrix_gemm`` with
+    ``AxpyContract``, ``dense_transform_Elemental_mc_mr.hpp:545-615``)."""
+    g = A.grid
+    c = A.comm
+    S = sk.getsketchdim()
+    if dim == COLUMNWISE:
+        comm, p, me = g.col_comm, g.pr, g.myrow
+        bS = max(1, -(-S // g.pr))
+        block = (bS, A.block[1])
+    else:
+        comm, p, me = g.row_comm, g.pc, g.mycol
+        bS = max(1, -(-S // g.pc))
+        block = (A.block[0], bS)
+    counts, order = _owner_order(S, bS, p)
+    sdim = 0 if dim == COLUMNWISE else 1
+    if order != list(range(S)):
+        part = part.index_select(sdim, torch.tensor(order, device=part.device))
+    loc = comm.reduce_scatter_v(part.contiguous(), counts, sdim) if p > 1 else part
+    if finish is not None:
+        pieces, off = [], 0
+        for s0, e0 in _cyclic_blocks(S, bS, p, me):
+            blk = loc[off:off + e0 - s0] if dim == COLUMNWISE else loc[:, off:off + e0 - s0]
+            pieces.append(finish(blk, (s0, e0)))
+            off += e0 - s0
+        if pieces:
+            loc = torch.cat(pieces, sdim)
+    return DistMatrix(loc.contiguous(), out_shape, "MC_MR", c, g, block)
+
+
+def _inner_panel(sk, A: DistMatrix, dim, out_shape):
+    """Inner-panel algorithm (reference ``inner_panel_gemm``,
+    ``dense_transform_Elemental_mc_mr.hpp:211-326``): the input is
+    redistributed once to a 1-D layout over the WHOLE grid along the sketched
+    dimension (one all-to-all), every rank contracts its slice for a panel of
+    b sketch rows, and the small panel x width partial is reduce-scattered over
+    the whole grid straight into the output's [MC,MR] tiles.  Memory per rank:
+    one b x N_loc panel of S."""
+    from ..sketch import params
+    g = A.grid
+    c = A.comm
+    S = sk.getsketchdim()
+    if dim == COLUMNWISE:
+        A1 = A.redistribute("VC_STAR")
+        width = A.shape[1]
+    else:
+        A1 = A.redistribute("STAR_VC")
+        width = A.shape[0]
+    (s_in, e_in), = A1.row_blocks() if dim == COLUMNWISE else A1.col_blocks()
+    block = (max(1, -(-S // g.pr)), A.block[1]) if dim == COLUMNWISE else (A.block[0], max(1, -(-S // g.pc)))
+    R = DistMatrix(torch.empty(0), out_shape, "MC_MR", c, g, block)
+    b = params.get_blocksize() or S
+    # destination tiles of every rank of the grid: (its sketch rows, its width cols)
+    dest = []
+    for rk in range(c.size):
+        dest.append((R.row_blocks(rk) if dim == COLUMNWISE else R.col_blocks(rk),
+                     R.col_blocks(rk) if dim == COLUMNWISE else R.row_blocks(rk)))
+    pieces = []
+    for p0 in range(0, S, b):
+        p1 = min(S, p0 + b)
+        part = sk.apply_local_shard(A1.local, dim, s_in, out_rows=(p0, p1))   # (p1-p0) x width (col) / width x .. (row)
+        if dim == ROWWISE:
+            part = part.t()
+        part = part.contiguous()
+        sends, counts = [], []
+        for srows, wcols in dest:
+            ri = [i - p0 for s0, e0 in srows for i in range(max(s0, p0), min(e0, p1))]
+            ci = [j for s0, e0 in wcols for j in range(s0, e0)]
+            if ri and ci:
+                t = part.index_select(0, torch.tensor(ri, device=part.device)).index_select(
+                    1, torch.tensor(ci, device=part.device))
+            else:
+                t = part.new_zeros(0)
+            sends.append(t.reshape(-1))
+            counts.append(t.numel())
+        flat = torch.cat(sends) if sends else part.new_zeros(0)
+        mine = c.reduce_scatter_v(flat, counts, 0) if c.size > 1 else flat
+        myrows = [i for s0, e0 in dest[c.rank][0] for i in range(max(s0, p0), min(e0, p1))]
+        mycols = sum(e0 - s0 for s0, e0 in dest[c.rank][1])
+        pieces.append(mine.view(len(myrows), mycols))
+    loc = torch.cat(pieces, 0) if pieces else torch.zeros(0, 0)
+    R.local = (loc if dim == COLUMNWISE else loc.t()).contiguous()
+    return R
+
+
 def _partial_and_reduce(sk, A: DistMatrix, dim, kind, out_layout, out_shape):
     c = A.comm
+    if A.layout == "MC_MR":
+        algo = _mc_mr_algorithm(sk, A, dim, kind)
+        if algo == "inner":
+            return _inner_panel(sk, A, dim, out_shape)
+        if algo == "outer" and dim == COLUMNWISE:
+            return _outer_panel(sk, A, out_shape)
     part = _partial(sk, A, dim, kind)
     finish = (lambda X, rows=None: sk.finish_features(X, dim, rows)) if kind == "feature" else None
     S = sk.getsketchdim()
 
-    if A.layout == "MC_MR" and _use_outer_panel(sk, A, dim, kind):
-        return _outer_panel(sk, A, out_shape)
     if A.layout == "MC_MR":
-        g = A.grid
-        # the sketched dimension is spread over grid rows (columnwise: sum over
-        # the grid-column communicator) or grid columns (rowwise: grid-row comm)
-        (g.col_comm if dim == COLUMNWISE else g.row_comm).all_reduce(part)
-        if finish is not None:
-            part = finish(part)
-        if dim == COLUMNWISE:
-            R = DistMatrix(torch.empty(0), out_shape, "MC_MR", c, g, (A.block[0] if A.block else None, A.block[1]))
-            R.block = (max(1, -(-S // g.pr)), A.block[1])
-            rows = R.row_blocks()
-            R.local = torch.cat([part[s:e] for s, e in rows], 0) if rows else part[:0]
-        else:
-            R = DistMatrix(torch.empty(0), out_shape, "MC_MR", c, g, (A.block[0], max(1, -(-S // g.pc))))
-            cols = R.col_blocks()
-            R.local = torch.cat([part[:, s:e] for s, e in cols], 1) if cols else part[:, :0]
-        R.local = R.local.contiguous()
-        return R
+        return _panel_matrix(part, sk, A, dim, out_shape, finish)
 
     if out_layout == "CIRC_CIRC":
         c.reduce(part, 0)

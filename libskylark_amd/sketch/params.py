@@ -20,6 +20,19 @@ from __future__ import annotations
 _BLOCKSIZE = 0
 _FACTOR = 20
 _DETERMINISTIC = False
+_MC_MR_ALGO = "auto"
+
+
+def get_mc_mr_algorithm() -> str:
+    return _MC_MR_ALGO
+
+
+def set_mc_mr_algorithm(name: str):
+    """Force the [MC,MR] sketch algorithm: "inner", "outer", "panel" or "auto"."""
+    global _MC_MR_ALGO
+    if name not in ("auto", "inner", "outer", "panel"):
+        raise ValueError("mc_mr algorithm: auto | inner | outer | panel")
+    _MC_MR_ALGO = name
 
 
 def get_deterministic() -> bool:
