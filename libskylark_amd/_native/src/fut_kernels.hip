@@ -240,3 +240,73 @@ SL_API int sl_ppt_product(const void* F, int q, int64_t K, int64_t m, int64_t S,
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
+
+// ------------------------------------------------------------------ WHT
+// Orthonormal Walsh-Hadamard transform of V vectors of length N (power of
+// two, N * V * 4 B <= 64 KB) per workgroup, entirely in LDS: one coalesced
+// load of the tile, log2 N butterfly stages (each a pass of 256 threads over
+// the N/2 pairs of every vector, one barrier per stage), the 1/sqrt(N) scale
+// folded into the store.  Element e of vector v is x[v * vs + e * es]: dim 0
+// of a row-major N x m matrix has es = ld, vs = 1 (V consecutive columns per
+// workgroup -> 4V-byte contiguous row pieces), dim 1 has es = 1, vs = ld.
+// Reference: the Spiral WHT of utility/fft/fftw_futs.h (WHT_t).
+namespace {
+template <typename T>
+__global__ void __launch_bounds__(256) k_wht_lds(const T* __restrict__ x, T* __restrict__ y, int64_t nvec, int N,
+                                                 int V, int64_t es, int64_t vs, int logn, float scale) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];   // [N][V], vector index fastest
+  const int64_t v0 = (int64_t)blockIdx.x * V;
+  const int vcount = (int)((nvec - v0) < V ? (nvec - v0) : V);
+  const int tot = N * V;
+  for (int t = threadIdx.x; t < tot; t += 256) {
+    const int e = t / V, v = t - e * V;
+    tile[t] = v < vcount ? (float)Cvt<T>::to_f(x[(v0 + v) * vs + (int64_t)e * es]) : 0.f;
+  }
+  __syncthreads();
+  const int pairs = (N >> 1) * V;
+  for (int s = 0; s < logn; ++s) {
+    const int h = 1 << s;
+    for (int t = threadIdx.x; t < pairs; t += 256) {
+      const int pv = t / V, v = t - pv * V;                 // pair index within the vector
+      const int i = ((pv >> s) << (s + 1)) + (pv & (h - 1));
+      const float a = tile[i * V + v], b = tile[(i + h) * V + v];
+      tile[i * V + v] = a + b;
+      tile[(i + h) * V + v] = a - b;
+    }
+    __syncthreads();
+  }
+  for (int t = threadIdx.x; t < tot; t += 256) {
+    const int e = t / V, v = t - e * V;
+    if (v < vcount) y[(v0 + v) * vs + (int64_t)e * es] = Cvt<T>::from_f(tile[t] * scale);
+  }
+}
+}  // namespace
+
+// y = WHT(x) / sqrt(N) on nvec vectors (element stride es, vector stride vs);
+// x and y may alias.  N a power of two, N <= 16384.
+SL_API int sl_wht(const void* x, void* y, int dtype, int64_t nvec, int N, int64_t es, int64_t vs, void* stream) {
+  if (nvec <= 0) return SL_OK;
+  if (N < 1 || (N & (N - 1)) || N > 16384) {
+    sl_set_last_error("wht: N must be a power of two <= 16384");
+    return SL_ERR_UNSUPPORTED;
+  }
+  if (dtype != SL_F32 && dtype != SL_BF16) {
+    sl_set_last_error("wht: f32 / bf16 (f64 stays on the host path)");
+    return SL_ERR_UNSUPPORTED;
+  }
+  int logn = 0;
+  while ((1 << logn) < N) ++logn;
+  // vectors per workgroup: up to 16 (64-B row pieces for dim 0), LDS <= 64 KB
+  int V = es == 1 ? 1 : 16;
+  while (V > 1 && (int64_t)N * V * 4 > 65536) V >>= 1;
+  const size_t lds = (size_t)N * V * 4;
+  const unsigned grid = (unsigned)((nvec + V - 1) / V);
+  const float scale = 1.0f / sqrtf((float)N);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SL_F32)
+    k_wht_lds<float><<<grid, 256, lds, s>>>((const float*)x, (float*)y, nvec, N, V, es, vs, logn, scale);
+  else
+    k_wht_lds<bf16_t><<<grid, 256, lds, s>>>((const bf16_t*)x, (bf16_t*)y, nvec, N, V, es, vs, logn, scale);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

@@ -76,7 +76,29 @@ def dht(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
 
 
 def wht(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
-    """Orthonormal Walsh-Hadamard transform (N must be a power of two)."""
+    """Orthonormal Walsh-Hadamard transform (N must be a power of two).  On the
+    GPU (f32 / bf16, N <= 16384) one LDS kernel per call (``sl_wht``: tile
+    load, log2 N in-LDS butterfly stages, scaled store); else the butterfly
+    over torch ops."""
+    N = x.shape[dim]
+    if (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.dim() == 2 and N >= 1
+            and not (N & (N - 1)) and N <= 16384):
+        import ctypes as C
+        from . import _lib
+        _lib.require()
+        xc = x if x.stride(1) == 1 else x.contiguous()
+        y = torch.empty_like(xc, dtype=torch.float32)
+        es, vs = (xc.stride(0), 1) if dim == 0 else (1, xc.stride(0))
+        yes, yvs = (y.stride(0), 1) if dim == 0 else (1, y.stride(0))
+        nvec = x.shape[1 - dim]
+        if (es, vs) != (yes, yvs) or xc.dtype != torch.float32:
+            xf = xc.to(torch.float32).contiguous()
+            y = xf
+            es, vs = (xf.stride(0), 1) if dim == 0 else (1, xf.stride(0))
+            xc = xf
+        _lib.call("sl_wht", _lib.ptr(xc), _lib.ptr(y), _lib.dtype_code(torch.float32), nvec, N, es, vs,
+                  C.c_void_p(_lib.stream_of(x)))
+        return y
     xt = _move(x, dim).to(_work_dtype(x.dtype)).contiguous()
     N = xt.shape[0]
     if N & (N - 1):
@@ -134,6 +156,7 @@ def _register_fjlt():
     _lib.register("sl_fjlt_pre", [vp, i32, i64, i64, i64, i32, vp, vp, i64, vp])
     _lib.register("sl_fjlt_post", [vp, i64, i64, i64, i32, vp, i64, C.c_double, vp, i64, vp])
     _lib.register("sl_ppt_product", [vp, i32, i64, i64, i64, vp, vp, C.c_double, C.c_double, vp, vp])
+    _lib.register("sl_wht", [vp, vp, i32, i64, i32, i64, i64, vp])
 
 
 _register_fjlt()

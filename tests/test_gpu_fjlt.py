@@ -50,3 +50,19 @@ def test_ppt_gpu_fused_product(dev, q, S):
     got_s = P.apply(As.float().to(dev).to_sparse_csr(), dim=sk.sketch.COLUMNWISE).double().cpu()
     ref_s = P.apply(As, dim=sk.sketch.COLUMNWISE)
     assert float((got_s - ref_s).norm() / ref_s.norm()) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,m,dim", [(1024, 40, 0), (4096, 7, 0), (16384, 3, 0), (512, 100, 1), (8, 5, 1), (2048, 33, 1)])
+def test_wht_native_vs_hadamard(dev, N, m, dim):
+    g = torch.Generator().manual_seed(N + m)
+    X = torch.randn(N, m, generator=g, dtype=torch.float64) if dim == 0 else \
+        torch.randn(m, N, generator=g, dtype=torch.float64)
+    if N <= 2048:
+        from scipy.linalg import hadamard
+        H = torch.from_numpy(hadamard(N).astype("float64")) / N ** 0.5
+        ref = H @ X if dim == 0 else X @ H.t()
+    else:
+        ref = fut.wht(X, dim)          # host butterfly in f64
+    got = fut.wht(X.float().to(dev), dim).double().cpu()
+    assert float((got - ref).norm() / ref.norm()) < 1e-6
