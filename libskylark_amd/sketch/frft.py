@@ -74,6 +74,8 @@ class _Fastfood(_FeatureMap):
     def _features_pre(self, A, dim, in_offset=0, out_rows=None):
         if in_offset != 0 or A.shape[dim] != self._N:
             raise ValueError("Fastfood needs the whole input dimension on one device")
+        if A.is_cuda and A.dtype in (torch.float32, torch.bfloat16) and A.layout == torch.strided and self._N >= 2:
+            return self._features_pre_gpu(A, dim, out_rows)
         X = A if dim == COLUMNWISE else A.t()
         wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
         X = X.to(wdt)
@@ -92,6 +94,32 @@ class _Fastfood(_FeatureMap):
         if out_rows is not None:
             Z = Z[out_rows[0]:out_rows[1]]
         return Z if dim == COLUMNWISE else Z.t().contiguous()
+
+    def _features_pre_gpu(self, A, dim, out_rows=None):
+        """Per block ``Sm F G Pi F B`` as two native FJLT pipelines
+        (``ops.fut.fjlt_sampled``: fused diagonal scale + Makhoul reorder,
+        rocFFT R2C, fused post-twiddle gather): the permutation Pi is the
+        first pipeline's sample set, G the second's diagonal, the first
+        e - s frequencies its samples; no DCT is ever materialised beyond the
+        two spectra and no torch elementwise pass runs in between (reference
+        ``sketch/FRFT_Elemental.hpp:72-250``)."""
+        dev = A.device
+        X = A if A.stride(-1) == 1 else A.contiguous()
+        outs = []
+        r0, r1 = out_rows if out_rows is not None else (0, self._S)
+        for i in range(self.numblks):
+            s, e = i * self.NB, min((i + 1) * self.NB, self._S)
+            if e <= r0 or s >= r1:
+                continue
+            lo, hi = max(s, r0), min(e, r1)
+            Wb = _fut.fjlt_sampled(X, dim, self.B[i], self.perms[i], 1.0)
+            Wb = _fut.fjlt_sampled(Wb, dim, self.G[i], torch.arange(lo - s, hi - s), 1.0)
+            sm = self._Sm[lo:hi].to(dev, torch.float32)
+            outs.append(Wb * (sm[:, None] if dim == COLUMNWISE else sm[None, :]))
+        if not outs:
+            shape = (0, A.shape[1]) if dim == COLUMNWISE else (A.shape[0], 0)
+            return torch.zeros(shape, dtype=torch.float32, device=dev)
+        return torch.cat(outs, 0 if dim == COLUMNWISE else 1).contiguous()
 
 
 @register

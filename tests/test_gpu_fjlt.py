@@ -66,3 +66,19 @@ def test_wht_native_vs_hadamard(dev, N, m, dim):
         ref = fut.wht(X, dim)          # host butterfly in f64
     got = fut.wht(X.float().to(dev), dim).double().cpu()
     assert float((got - ref).norm() / ref.norm()) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,S,dim", [(8192, 10000, 0), (5000, 6000, 1), (6000, 3000, 0)])
+def test_fastfood_large_n_native_pipeline(dev, N, S, dim):
+    """Fastfood beyond the dense-W limit runs two native FJLT pipelines per
+    block; compare with the host f64 DCT chain of the same sketch."""
+    T = sk.sketch.FastGaussianRFT(N, S, sigma=40.0, context=sk.Context(9))
+    assert N > T.DENSE_MAX_N
+    g = torch.Generator().manual_seed(N)
+    A = torch.randn(N, 24, generator=g, dtype=torch.float64) if dim == 0 else \
+        torch.randn(24, N, generator=g, dtype=torch.float64)
+    ref = T.apply(A, dim=dim)
+    got = T.apply(A.float().to(dev), dim=dim).double().cpu()
+    err = float((got - ref).norm() / ref.norm())
+    assert err < 2e-4, err
