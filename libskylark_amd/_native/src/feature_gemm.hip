@@ -353,8 +353,8 @@ int launch_out(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64
 // conversion VALU work (A is re-read once per feature tile).
 __global__ void __launch_bounds__(256)
 k_split_bf16(const float* __restrict__ A, int64_t M, int64_t K, int64_t lda, bf16_t* __restrict__ hi,
-             bf16_t* __restrict__ lo, int64_t ldp) {
-  const int64_t per_row = ldp / 4;
+             bf16_t* __restrict__ lo, int64_t ldp, int64_t wpad) {
+  const int64_t per_row = wpad / 4;
   const int64_t total = M * per_row;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = t / per_row, k = (t - r * per_row) * 4;
@@ -426,12 +426,19 @@ SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int6
                           out_t, nullptr, 0.f, stream);
 }
 
-SL_API int sl_split_bf16(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t ldp,
-                         void* stream) {
+// hi / lo planes of width wpad (zero padded past K) with row stride ldp >= wpad
+SL_API int sl_split_bf16_2(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t wpad,
+                           int64_t ldp, void* stream) {
   if (M <= 0) return SL_OK;
-  if (ldp % 4 != 0 || ldp < K || ((uintptr_t)hi & 7) || ((uintptr_t)lo & 7)) return SL_ERR_INVALID;
-  const unsigned grid = sl_grid_for((size_t)(M * (ldp / 4)), 256, 8192);
-  k_split_bf16<<<grid, 256, 0, (hipStream_t)stream>>>(A, M, K, lda, hi, lo, ldp);
+  if (wpad % 4 != 0 || wpad < K || ldp < wpad || ldp % 4 != 0 || ((uintptr_t)hi & 7) || ((uintptr_t)lo & 7))
+    return SL_ERR_INVALID;
+  const unsigned grid = sl_grid_for((size_t)(M * (wpad / 4)), 256, 8192);
+  k_split_bf16<<<grid, 256, 0, (hipStream_t)stream>>>(A, M, K, lda, hi, lo, ldp, wpad);
   SL_LAUNCH_CHECK();
   return SL_OK;
+}
+
+SL_API int sl_split_bf16(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t ldp,
+                         void* stream) {
+  return sl_split_bf16_2(A, M, K, lda, hi, lo, ldp, ldp, stream);
 }

@@ -35,6 +35,8 @@ _lib.register("sl_feature_gemm2", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                                    C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p, C.c_float, C.c_void_p])
 _lib.register("sl_split_bf16", [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                 C.c_void_p])
+_lib.register("sl_split_bf16_2", [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                  C.c_int64, C.c_void_p])
 
 
 def enabled() -> bool:
