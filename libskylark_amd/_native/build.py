@@ -110,15 +110,16 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
 def build_capi(force: bool = False) -> str:
     """C API library (host C++, embeds/joins CPython; no device code)."""
-    if not force and os.path.exists(CAPI_LIB) and os.path.getmtime(CAPI_LIB) >= os.path.getmtime(CAPI_SRC):
+    srcs = [CAPI_SRC, os.path.join(HERE, "capi", "native_sketch.hpp"), os.path.join(INC, "sl_rng.hpp")]
+    if not force and os.path.exists(CAPI_LIB) and all(os.path.getmtime(CAPI_LIB) >= os.path.getmtime(f) for f in srcs):
         return CAPI_LIB
     import sysconfig
     inc = sysconfig.get_paths()["include"]
     libdir = sysconfig.get_config_var("LIBDIR")
     ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
     tmp = CAPI_LIB + f".{os.getpid()}.tmp"
-    cmd = [os.environ.get("CXX", "g++"), "-O2", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden",
-           "-I", inc, CAPI_SRC, "-o", tmp, f"-L{libdir}", f"-lpython{ver}", "-ldl", "-lpthread"]
+    cmd = [os.environ.get("CXX", "g++"), "-O3", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden",
+           "-I", inc, "-I", INC, CAPI_SRC, "-o", tmp, f"-L{libdir}", f"-lpython{ver}", "-ldl", "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"C API build failed:\n{r.stderr[-6000:]}")

@@ -1,8 +1,14 @@
 // C API of the framework: the reference's sl_* ABI (capi/basec.hpp,
 // sketchc.hpp, nlac.hpp, kernelc.hpp, ioc.hpp) over the MI355X runtime.
 //
-// The compute path lives in the Python/HIP runtime (libskylark_amd +
-// libskylark_hip.so); this library is a thin C++ marshalling layer.  It
+// Native path (no interpreter): contexts, and the core sketches JLT / CT /
+// CWT / MMT / WZT on host "Matrix" operands -- creation, application and
+// JSON (de)serialisation -- run in C++ (native_sketch.hpp, the same
+// counter-based streams as the runtime).  Everything else (other sketch
+// types, sparse operands, NLA, kernels, IO) goes through the Python/HIP
+// runtime (libskylark_amd + libskylark_hip.so); a natively created sketch
+// or context is handed to it lazily (via its JSON / seed + counter), so the
+// two paths see the same objects and the same random streams.  This library
 // embeds CPython when called from a plain C/C++ program (first call
 // initialises the interpreter, adds this library's package root to
 // sys.path, and imports libskylark_amd.capi), or joins the running
@@ -23,13 +29,20 @@
 #include <mutex>
 #include <string>
 
+#include "native_sketch.hpp"
+
 #define SL_CAPI extern "C" __attribute__((visibility("default")))
 
+// seed + counter are the context's state; obj (the runtime's Context) is
+// created on first use by a Python-path call and kept in sync around it
 struct sl_context_t {
   PyObject* obj;
+  uint64_t seed;
+  uint64_t counter;
 };
 struct sl_sketch_transform_t {
-  PyObject* obj;
+  PyObject* obj;          // runtime object (created lazily for native sketches)
+  slnat::Sketch* nat;     // native operator, or null
 };
 struct sl_kernel_t {
   PyObject* obj;
@@ -143,6 +156,38 @@ PyObject* call(const char* fn, PyObject* args) {
   return r;
 }
 
+// runtime Context for a C context, its counter set from the native state
+PyObject* py_ctx(sl_context_t* c) {
+  if (!c->obj) {
+    c->obj = call("create_context", Py_BuildValue("(K)", (unsigned long long)c->seed));
+    if (!c->obj) return nullptr;
+  }
+  PyObject* v = PyLong_FromUnsignedLongLong(c->counter);
+  PyObject_SetAttrString(c->obj, "counter", v);
+  Py_XDECREF(v);
+  return c->obj;
+}
+
+// after a runtime call: the runtime may have advanced the counter
+void ctx_sync_back(sl_context_t* c) {
+  if (!c->obj) return;
+  PyObject *t, *v0, *tb;
+  PyErr_Fetch(&t, &v0, &tb);      // keep a pending error for fail()
+  PyObject* v = PyObject_GetAttrString(c->obj, "counter");
+  if (v) {
+    c->counter = PyLong_AsUnsignedLongLong(v);
+    Py_DECREF(v);
+  }
+  PyErr_Clear();
+  PyErr_Restore(t, v0, tb);
+}
+
+// runtime object of a sketch (a native one is rebuilt from its JSON)
+PyObject* py_sketch(sl_sketch_transform_t* S) {
+  if (!S->obj && S->nat) S->obj = call("deserialize_sketch", Py_BuildValue("(s)", slnat::to_json(*S->nat).c_str()));
+  return S->obj;
+}
+
 PyObject* dense_desc(void* A) {
   auto* M = (sl_raw_matrix_t*)A;
   return Py_BuildValue("(Kii)", (unsigned long long)(uintptr_t)M->data, M->m, M->n);
@@ -240,10 +285,7 @@ SL_CAPI void sl_get_exception_info(char** info) { *info = strdup(g_last_error.c_
 SL_CAPI void sl_print_exception_trace() { fprintf(stderr, "%s\n", g_last_error.c_str()); }
 
 SL_CAPI int sl_create_default_context(int seed, sl_context_t** ctxt) {
-  Gil g;
-  PyObject* r = call("create_context", Py_BuildValue("(i)", seed));
-  if (!r) return fail();
-  *ctxt = new sl_context_t{r};
+  *ctxt = new sl_context_t{nullptr, (uint64_t)(int64_t)seed, 0};
   return 0;
 }
 
@@ -255,11 +297,16 @@ SL_CAPI int sl_create_context(int seed, void* /*comm*/, sl_context_t** ctxt) {
 
 SL_CAPI int sl_free_context(sl_context_t* ctxt) {
   if (!ctxt) return 0;
-  Gil g;
-  Py_XDECREF(ctxt->obj);
+  if (ctxt->obj) {
+    Gil g;
+    Py_XDECREF(ctxt->obj);
+  }
   delete ctxt;
   return 0;
 }
+
+// 1 once a call has needed the embedded runtime (tests: the native path stays interpreter-free)
+SL_CAPI int sl_runtime_started() { return Py_IsInitialized() && g_mod ? 1 : 0; }
 
 SL_CAPI int sl_wrap_raw_matrix(double* data, int m, int n, void** A) {
   *A = new sl_raw_matrix_t{data, m, n};
@@ -378,30 +425,63 @@ SL_CAPI int sl_raw_sp_matrix_data(void* A, int32_t* indptr, int32_t* indices, do
 // ---------------------------------------------------------------- sketches
 SL_CAPI int sl_create_sketch_transform(sl_context_t* ctxt, char* type, int n, int s, sl_sketch_transform_t** sketch,
                                        ...) {
+  if (slnat::supported(type) && n > 0 && s > 0) {
+    auto* ns = new slnat::Sketch();
+    ns->type = type;
+    ns->N = n;
+    ns->S = s;
+    ns->seed = ctxt->seed;
+    ns->ctr0 = ctxt->counter;
+    ns->param = 1.0;
+    if (slnat::takes_param(ns->type)) {
+      va_list ap;
+      va_start(ap, sketch);
+      ns->param = va_arg(ap, double);
+      va_end(ap);
+    }
+    ctxt->counter = slnat::build(*ns);
+    *sketch = new sl_sketch_transform_t{nullptr, ns};
+    return 0;
+  }
   Gil g;
   std::string spec = spec_of("sketch_param_spec", type);
   va_list ap;
   va_start(ap, sketch);
   PyObject* params = varargs_tuple(spec, ap);
   va_end(ap);
-  PyObject* r = call("create_sketch", Py_BuildValue("(OsiiN)", ctxt->obj, type, n, s, params));
-  if (!r) {
-    int c = fail();
-    return c == 100 || c == 109 ? 111 : c;
+  PyObject* c = py_ctx(ctxt);
+  if (!c) {
+    Py_XDECREF(params);
+    return fail();
   }
-  *sketch = new sl_sketch_transform_t{r};
+  PyObject* r = call("create_sketch", Py_BuildValue("(OsiiN)", c, type, n, s, params));
+  ctx_sync_back(ctxt);
+  if (!r) {
+    int code = fail();
+    return code == 100 || code == 109 ? 111 : code;
+  }
+  *sketch = new sl_sketch_transform_t{r, nullptr};
   return 0;
 }
 
 SL_CAPI int sl_deserialize_sketch_transform(const char* data, sl_sketch_transform_t** sketch) {
+  slnat::Sketch tmp;
+  if (slnat::from_json(data, tmp)) {
+    *sketch = new sl_sketch_transform_t{nullptr, new slnat::Sketch(std::move(tmp))};
+    return 0;
+  }
   Gil g;
   PyObject* r = call("deserialize_sketch", Py_BuildValue("(s)", data));
   if (!r) return fail();
-  *sketch = new sl_sketch_transform_t{r};
+  *sketch = new sl_sketch_transform_t{r, nullptr};
   return 0;
 }
 
 SL_CAPI int sl_serialize_sketch_transform(const sl_sketch_transform_t* sketch, char** data) {
+  if (sketch->nat) {
+    *data = strdup(slnat::to_json(*sketch->nat).c_str());
+    return 0;
+  }
   Gil g;
   PyObject* r = call("serialize_sketch", Py_BuildValue("(O)", sketch->obj));
   if (!r) return fail();
@@ -412,15 +492,27 @@ SL_CAPI int sl_serialize_sketch_transform(const sl_sketch_transform_t* sketch, c
 
 SL_CAPI int sl_free_sketch_transform(sl_sketch_transform_t* S) {
   if (!S) return 0;
-  Gil g;
-  Py_XDECREF(S->obj);
+  if (S->obj) {
+    Gil g;
+    Py_XDECREF(S->obj);
+  }
+  delete S->nat;
   delete S;
   return 0;
 }
 
 SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type, void* A, char* output_type,
                                       void* SA, int dim) {
+  if (S->nat && !strcmp(input_type, "Matrix") && !strcmp(output_type, "Matrix")) {
+    auto* a = (sl_raw_matrix_t*)A;
+    auto* o = (sl_raw_matrix_t*)SA;
+    const int rc = slnat::apply(*S->nat, a->data, a->m, a->n, o->data, o->m, o->n, dim);
+    if (rc) g_last_error = "sl_apply_sketch_transform: dimension mismatch";
+    return rc;
+  }
   Gil g;
+  PyObject* so = py_sketch(S);
+  if (!so) return fail();
   PyObject* a = in_desc(input_type, A);
   if (!a) return fail();
   PyObject* o = out_desc(output_type, SA);
@@ -428,7 +520,7 @@ SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type
     Py_DECREF(a);
     return fail();
   }
-  PyObject* r = call("apply_sketch", Py_BuildValue("(OsNsNi)", S->obj, input_type, a, output_type, o, dim));
+  PyObject* r = call("apply_sketch", Py_BuildValue("(OsNsNi)", so, input_type, a, output_type, o, dim));
   if (!r) return fail();
   Py_DECREF(r);
   return 0;
@@ -444,7 +536,8 @@ SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, cha
   PyObject* a = in_desc(A_type, A);
   if (!a) return fail();
   PyObject* r = call("approximate_svd", Py_BuildValue("(sNNNNisO)", A_type, a, dense_desc(U), dense_desc(Sv),
-                                                      dense_desc(V), (int)k, params ? params : "", ctxt->obj));
+                                                      dense_desc(V), (int)k, params ? params : "", py_ctx(ctxt)));
+  ctx_sync_back(ctxt);
   if (!r) return fail();
   Py_DECREF(r);
   return 0;
@@ -459,7 +552,8 @@ SL_CAPI int sl_approximate_symmetric_svd(char* A_type, void* A, char* S_type, vo
   if (!a) return fail();
   PyObject* r = call("approximate_symmetric_svd", Py_BuildValue("(sNNNisO)", A_type, a, dense_desc(Sv),
                                                                 dense_desc(V), (int)k, params ? params : "",
-                                                                ctxt->obj));
+                                                                py_ctx(ctxt)));
+  ctx_sync_back(ctxt);
   if (!r) return fail();
   Py_DECREF(r);
   return 0;
@@ -473,7 +567,8 @@ SL_CAPI int sl_faster_least_squares(int orientation, char* A_type, void* A, char
   PyObject* a = in_desc(A_type, A);
   if (!a) return fail();
   PyObject* r = call("faster_least_squares", Py_BuildValue("(isNNNsO)", orientation, A_type, a, dense_desc(B),
-                                                           dense_desc(X), params ? params : "", ctxt->obj));
+                                                           dense_desc(X), params ? params : "", py_ctx(ctxt)));
+  ctx_sync_back(ctxt);
   if (!r) return fail();
   Py_DECREF(r);
   return 0;

@@ -189,3 +189,110 @@ def test_standalone_c_program(capi, tmp_path):
     a = np.array([(i % 7) - 3.0 for i in range(60)]).reshape(3, 20).T
     ref = sk.sketch.FJLT(20, 4, context=sk.Context(11)).apply(torch.from_numpy(a)).numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("typ,param", [("JLT", None), ("CT", 2.5), ("CWT", None), ("MMT", None), ("WZT", 1.5)])
+def test_native_sketch_parity(capi, typ, param):
+    """The interpreter-free C path (native_sketch.hpp) builds the same operator
+    as the runtime from the same context stream: apply both ways, JSON both
+    ways, and a second sketch from the same context (counter advanced alike)."""
+    N, S, n = 37, 9, 5
+    ctx = C.c_void_p()
+    assert capi.sl_create_default_context(13, C.byref(ctx)) == 0
+    pctx = sk.Context(13)
+    cls = getattr(sk.sketch, typ)
+    hs, pys = [], []
+    for _ in range(2):     # the second draw checks the counter bookkeeping
+        h = C.c_void_p()
+        args = [C.c_double(param)] if param is not None else []
+        assert capi.sl_create_sketch_transform(ctx, typ.encode(), N, S, C.byref(h), *args) == 0
+        hs.append(h)
+        pys.append(cls(N, S, param, context=pctx) if param is not None else cls(N, S, context=pctx))
+    rng = np.random.default_rng(1)
+    A = rng.standard_normal((N, n))
+    B = rng.standard_normal((n, N))
+    for h, T in zip(hs, pys):
+        Aw, hA = _wrap(capi, A)
+        SA, hSA = _wrap(capi, np.zeros((S, n)))
+        assert capi.sl_apply_sketch_transform(h, b"Matrix", hA, b"Matrix", hSA, 0) == 0
+        np.testing.assert_allclose(SA, T.apply(torch.from_numpy(A.copy()), dim=0).numpy(), rtol=1e-11, atol=1e-11)
+        Bw, hB = _wrap(capi, B)
+        SB, hSB = _wrap(capi, np.zeros((n, S)))
+        assert capi.sl_apply_sketch_transform(h, b"Matrix", hB, b"Matrix", hSB, 1) == 0
+        np.testing.assert_allclose(SB, T.apply(torch.from_numpy(B.copy()), dim=1).numpy(), rtol=1e-11, atol=1e-11)
+        # C JSON -> runtime, runtime JSON -> C
+        data = C.c_char_p()
+        assert capi.sl_serialize_sketch_transform(h, C.byref(data)) == 0
+        T2 = sk.sketch.deserialize_sketch(json.loads(data.value.decode()))
+        np.testing.assert_allclose(T2.apply(torch.from_numpy(A.copy()), dim=0).numpy(), SA, rtol=1e-11, atol=1e-11)
+        h2 = C.c_void_p()
+        assert capi.sl_deserialize_sketch_transform(T.to_json().encode(), C.byref(h2)) == 0
+        SA2, hSA2 = _wrap(capi, np.zeros((S, n)))
+        assert capi.sl_apply_sketch_transform(h2, b"Matrix", hA, b"Matrix", hSA2, 0) == 0
+        np.testing.assert_allclose(SA2, SA, rtol=0, atol=0)
+        # dimension mismatch is the reference's code 104
+        bad, hbad = _wrap(capi, np.zeros((S + 1, n)))
+        assert capi.sl_apply_sketch_transform(h, b"Matrix", hA, b"Matrix", hbad, 0) == 104
+        capi.sl_free_sketch_transform(h2)
+    for h in hs:
+        capi.sl_free_sketch_transform(h)
+    capi.sl_free_context(ctx)
+
+
+C_NATIVE_PROGRAM = textwrap.dedent(r"""
+    #include <stdio.h>
+    #include <stdlib.h>
+    typedef struct sl_context_t sl_context_t;
+    typedef struct sl_sketch_transform_t sl_sketch_transform_t;
+    int sl_create_default_context(int, sl_context_t**);
+    int sl_create_sketch_transform(sl_context_t*, char*, int, int, sl_sketch_transform_t**, ...);
+    int sl_apply_sketch_transform(sl_sketch_transform_t*, char*, void*, char*, void*, int);
+    int sl_serialize_sketch_transform(const sl_sketch_transform_t*, char**);
+    int sl_wrap_raw_matrix(double*, int, int, void**);
+    int sl_free_sketch_transform(sl_sketch_transform_t*);
+    int sl_free_context(sl_context_t*);
+    int sl_runtime_started(void);
+    int main(void) {
+        sl_context_t* ctx; sl_sketch_transform_t *J, *W;
+        if (sl_create_default_context(21, &ctx)) return 1;
+        if (sl_create_sketch_transform(ctx, "JLT", 30, 6, &J)) return 2;
+        if (sl_create_sketch_transform(ctx, "WZT", 30, 6, &W, 1.5)) return 3;
+        double a[30 * 2], sa[6 * 2], sw[6 * 2];
+        for (int i = 0; i < 60; ++i) a[i] = (i % 5) - 2.0;
+        void *hA, *hS, *hW;
+        sl_wrap_raw_matrix(a, 30, 2, &hA); sl_wrap_raw_matrix(sa, 6, 2, &hS); sl_wrap_raw_matrix(sw, 6, 2, &hW);
+        if (sl_apply_sketch_transform(J, "Matrix", hA, "Matrix", hS, 0)) return 4;
+        if (sl_apply_sketch_transform(W, "Matrix", hA, "Matrix", hW, 0)) return 5;
+        char* js; if (sl_serialize_sketch_transform(W, &js)) return 6;
+        for (int i = 0; i < 12; ++i) printf("%.17g ", sa[i]);
+        for (int i = 0; i < 12; ++i) printf("%.17g ", sw[i]);
+        printf("\n%s\n%d\n", js, sl_runtime_started());
+        free(js); sl_free_sketch_transform(J); sl_free_sketch_transform(W); sl_free_context(ctx);
+        return 0;
+    }
+""")
+
+
+def test_native_c_program_is_interpreter_free(capi, tmp_path):
+    """A C program using only contexts and the native sketches never starts
+    the embedded runtime, and computes the runtime's operator."""
+    import sysconfig
+    src = tmp_path / "nat.c"
+    src.write_text(C_NATIVE_PROGRAM)
+    exe = tmp_path / "nat"
+    libdir = os.path.dirname(B.CAPI_LIB)
+    r = subprocess.run(["gcc", str(src), "-o", str(exe), f"-L{libdir}", "-lskylark_capi", f"-Wl,-rpath,{libdir}",
+                        f"-Wl,-rpath,{sysconfig.get_config_var('LIBDIR')}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.strip().split("\n")
+    vals = np.array([float(x) for x in lines[0].split()])
+    assert lines[2].strip() == "0"                      # runtime never started
+    a = np.array([(i % 5) - 2.0 for i in range(60)]).reshape(2, 30).T
+    ctx = sk.Context(21)
+    J = sk.sketch.JLT(30, 6, context=ctx)
+    W = sk.sketch.WZT(30, 6, 1.5, context=ctx)
+    np.testing.assert_allclose(vals[:12].reshape(2, 6).T, J.apply(torch.from_numpy(a)).numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(vals[12:].reshape(2, 6).T, W.apply(torch.from_numpy(a)).numpy(), rtol=1e-12, atol=1e-12)
+    assert json.loads(lines[1])["sketch_type"] == "WZT"
