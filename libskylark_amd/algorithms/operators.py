@@ -217,6 +217,48 @@ class DistSymOp(DistRowOp):
     rmatmul = matmul
 
 
+class Sparse2DOp(Operator):
+    """A held as 2-D block-sparse tiles (:class:`~..parallel.dist_sparse2d.DistSparse2D`,
+    the CombBLAS SpParMat analogue; reference ``base/detail/combblas_mixed_gemm.hpp``).
+
+    Long vectors are the row block ``R_r`` of the grid row (replicated along
+    it), short vectors are replicated: ``A X`` = tile SpMM + one all-reduce in
+    the grid row; ``A^T Y`` = tile SpMM placed at the tile's columns + ONE
+    world all-reduce (every tile contributes exactly once).  Long-vector
+    norms/dots reduce over the grid column (the ranks that partition the
+    rows)."""
+
+    def __init__(self, M):
+        vdt = M.local.values().dtype
+        super().__init__(M.shape, vdt if vdt in (torch.float32, torch.float64) else torch.float32,
+                         M.local.device, M.grid.col_comm)
+        self.M = M
+        self.distributed = M.comm.size > 1
+        self._cols = None
+
+    def matmul(self, X):
+        return self.M.matmul(X)
+
+    def rmatmul(self, Y):
+        M = self.M
+        part = M._spmm(M._transposed(), Y.contiguous())
+        if self._cols is None:
+            self._cols = M.cols.to(part.device)
+        out = torch.zeros(M.shape[1], part.shape[1], dtype=part.dtype, device=part.device)
+        out.index_copy_(0, self._cols, part)
+        if self.distributed:
+            M.comm.all_reduce(out)
+        return out
+
+    def local_rows(self):
+        return self.M.rows.numel()
+
+    def long_like(self, B):
+        if B.shape[0] == self.shape[0] and self.M.rows.numel() != self.shape[0]:
+            return B.index_select(0, self.M.rows.to(B.device))
+        return B
+
+
 class CallableOp(Operator):
     def __init__(self, obj):
         super().__init__(obj.shape, getattr(obj, "dtype", torch.float64), getattr(obj, "device", None),
@@ -236,6 +278,8 @@ def as_operator(A) -> Operator:
         return A
     if isinstance(A, DistMatrix):
         return DistRowOp(A)
+    if type(A).__name__ == "DistSparse2D":
+        return Sparse2DOp(A)
     if isinstance(A, torch.Tensor):
         if A.layout != torch.strided:
             return SparseOp(A.to_sparse_csr() if A.layout != torch.sparse_csr else A)

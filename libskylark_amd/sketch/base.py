@@ -169,6 +169,12 @@ class SketchTransform:
     def apply(self, A, SA=None, dim=COLUMNWISE, out_dtype=None, sparse_output: bool | None = None):
         """Apply the transform along ``dim``; returns SA (also written into SA if given)."""
         dim = parse_dim(dim)
+        if type(A).__name__ == "DistSparse2D":
+            # 2-D block-sparse distribution (CombBLAS analogue): local tile + one reduction
+            if A.shape[dim] != self._N:
+                raise DimensionMismatchError(
+                    f"Sketched dimension is incorrect (input): got {A.shape[dim]}, expected {self._N}")
+            return A.sketch(self, dim)
         op = Operand(A)
         if op.kind == "dist":
             from ..parallel.dist_sketch import dist_apply
