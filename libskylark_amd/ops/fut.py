@@ -70,8 +70,18 @@ def dct3(X: torch.Tensor, dim: int = 0) -> torch.Tensor:
 def dht(x: torch.Tensor, dim: int = 0) -> torch.Tensor:
     """Unitary discrete Hartley transform (self-inverse), scale 1/sqrt(N)."""
     xt = _move(x, dim).to(_work_dtype(x.dtype))
+    N = xt.shape[0]
+    if x.is_cuda and N >= 2:
+        # real input: half-spectrum R2C (F_{N-k} = conj F_k), H_k = Re F_k - Im F_k
+        # for k <= N/2 and Re F_{N-k} + Im F_{N-k} above
+        F = torch.fft.rfft(xt, dim=0)
+        lo = F.real - F.imag
+        h = N - F.shape[0]                      # rows N/2+1 .. N-1 (count N - (N//2+1))
+        hi = (F.real[1:1 + h] + F.imag[1:1 + h]).flip(0)
+        H = torch.cat([lo, hi], 0) / math.sqrt(N)
+        return _move(H, dim).contiguous()
     F = torch.fft.fft(xt, dim=0)
-    H = (F.real - F.imag) / math.sqrt(xt.shape[0])
+    H = (F.real - F.imag) / math.sqrt(N)
     return _move(H, dim).contiguous()
 
 

@@ -82,3 +82,20 @@ def test_fastfood_large_n_native_pipeline(dev, N, S, dim):
     got = T.apply(A.float().to(dev), dim=dim).double().cpu()
     err = float((got - ref).norm() / ref.norm())
     assert err < 2e-4, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fut_name", ["DCT", "DHT"])
+@pytest.mark.parametrize("N,m,dim", [(1000, 24, 0), (777, 10, 1), (4096, 8, 0)])
+def test_rfut_gpu_vs_f64(dev, fut_name, N, m, dim):
+    """RFUT F D A on the GPU (DCT: native pre-pass + rocFFT R2C + full post
+    pass; DHT: half-spectrum R2C) against the fp64 host transform."""
+    from libskylark_amd.sketch.fjlt import RFUT
+    g = torch.Generator().manual_seed(N + m)
+    A = torch.randn(N, m, generator=g, dtype=torch.float64) if dim == 0 else \
+        torch.randn(m, N, generator=g, dtype=torch.float64)
+    R = RFUT(N, sk.Context(3), fut_name)
+    ref = R.apply(A, dim)
+    got = R.apply(A.float().to(dev), dim).double().cpu()
+    err = float((got - ref).norm() / ref.norm())
+    assert err < 2e-6, err
