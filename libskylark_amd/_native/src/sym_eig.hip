@@ -127,7 +127,393 @@ k_sym_eig_jacobi(const double* __restrict__ Cin, int k, int ldc, int r, double* 
   if (tid == 0 && sweeps_out) *sweeps_out = sweep;
 }
 
+// ---------------------------------------------------------------------------
+// Tridiagonal path (the randSVD default, k <= 64, r <= 32): the k x k core's
+// top-r eigenpairs in one launch of one workgroup, ~20x fewer dependent
+// steps than Jacobi sweeps, so the randomized SVD runs start to finish on
+// the device (no host LAPACK round trip between its two halves).
+//   1. Householder tridiagonalisation T = Q^T C Q (wave 0, lane = row; the
+//      reflectors stay in C's lower triangle), one wave => no barriers.
+//   2. Eigenvalues of T by multisection on Sturm counts: the 256 threads are
+//      split over the r + 1 largest eigenvalues, G points per interval per
+//      round, to absolute accuracy ~eps ||T|| (LAPACK dstebz's default).
+//   3. Eigenvectors of T by the twisted factorisation at each eigenvalue
+//      (one lane per vector): backward UDU^T and forward LDL^T pivots, twist
+//      at min |gamma|, then two recurrences out from the twist.  Vectors in a
+//      close cluster (relative gap < 1e-3) are re-orthogonalised by MGS; a gap
+//      under 1e-14 ||T||, a tridiagonal residual above 1e-11 ||T||,
+//      non-finite data or a vanishing r-th eigenvalue set status bit 1 and the caller re-runs that call through host LAPACK.
+//   4. Back-transform Q x (4 lanes per vector, shuffles only).
+// Output as k_sym_eig_jacobi: out[i * r + c] = V[i][c] descending, then
+// sqrt(max(lambda, 0)) (or lambda) in out[k * r + c].
+constexpr int TRK = 64, TRV = 32;
+
+// DPP lane permutations of a double (two 32-bit moves); CTRL is a dpp_ctrl code
+template <int CTRL>
+__device__ __forceinline__ double dppd(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double lane_d(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+
+// all-lanes reductions of a full wave: quad butterflies, half-row and row
+// mirrors by DPP (no LDS round trips), then the four row results by readlane
+__device__ __forceinline__ double wave_sum_d(double x) {
+  x += dppd<0xB1>(x);
+  x += dppd<0x4E>(x);
+  x += dppd<0x141>(x);
+  x += dppd<0x140>(x);
+  return (lane_d(x, 0) + lane_d(x, 16)) + (lane_d(x, 32) + lane_d(x, 48));
+}
+
+__device__ __forceinline__ double wave_min_d(double x) {
+  x = fmin(x, dppd<0xB1>(x));
+  x = fmin(x, dppd<0x4E>(x));
+  x = fmin(x, dppd<0x141>(x));
+  x = fmin(x, dppd<0x140>(x));
+  return fmin(fmin(lane_d(x, 0), lane_d(x, 16)), fmin(lane_d(x, 32), lane_d(x, 48)));
+}
+
+__device__ __forceinline__ double wave_max_d(double x) {
+  x = fmax(x, dppd<0xB1>(x));
+  x = fmax(x, dppd<0x4E>(x));
+  x = fmax(x, dppd<0x141>(x));
+  x = fmax(x, dppd<0x140>(x));
+  return fmax(fmax(lane_d(x, 0), lane_d(x, 16)), fmax(lane_d(x, 32), lane_d(x, 48)));
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int K, bool ST>
+__global__ void __launch_bounds__(NT)
+k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double* __restrict__ out, int want_sqrt,
+                  int* __restrict__ status, long long* __restrict__ stamps) {
+  __shared__ double refl[K][K + 1];     // Householder vectors (column j = step j)
+  __shared__ __attribute__((aligned(16))) double vsh[K], wsh[K];
+  __shared__ double dd[K], ee[K], e2[K];
+  __shared__ double lo_s[K], hi_s[K], lam[K];
+  __shared__ double T1[K][TRV + 1];     // per-vector pivots, then the vector itself
+  __shared__ int cnt_s[NT];
+  __shared__ double bnd[2];
+  __shared__ int bad_s, clus_s;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const double eps = 2.220446049250313e-16, safmin = 2.2250738585072014e-308;
+  if constexpr (ST) { if (tid == 0) stamps[0] = clock64(); }
+  if (tid == 0) { bad_s = 0; clus_s = 0; }
+  __syncthreads();
+
+  // ---- 1. tridiagonalisation (wave 0, lane i keeps row i in registers) -----
+  if (wid == 0) {
+    const int i = lane;
+    double arow[K];
+    int nf = 0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      double v = 0.0;
+      if (i < k && c < k) v = 0.5 * (Cin[i * ldc + c] + Cin[c * ldc + i]);
+      nf |= !isfinite(v);
+      arow[c] = v;
+    }
+    if (nf) bad_s = 1;
+    for (int j = 0; j + 2 < k; ++j) {
+      double xi = 0.0;
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+        if (c == j) { xi = arow[c]; }
+      const double ajj = xi;                      // lane j: its diagonal (final now)
+      xi = (i > j) ? xi : 0.0;
+      const double s2 = wave_sum_d(xi * xi);
+      const double x0 = lane_d(xi, j + 1);
+      double vi = 0.0, alpha = x0;
+      if (s2 - x0 * x0 > safmin * 4.0) {
+        alpha = x0 >= 0.0 ? -sqrt(s2) : sqrt(s2);
+        const double vn = sqrt(2.0 * (s2 - alpha * x0));
+        vi = (xi - (i == j + 1 ? alpha : 0.0)) / vn;
+        vi = (i > j) ? vi : 0.0;
+      }
+      if (i == j) { dd[j] = ajj; ee[j] = alpha; }
+      if (i < K) {
+        vsh[i] = vi;
+        refl[i][j] = vi;
+      }
+      wave_lds_sync();
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+      for (int c = 0; c < K; c += 4) {
+        const double2 va = *(const double2*)(vsh + c);
+        const double2 vb = *(const double2*)(vsh + c + 2);
+        p0 = fma(arow[c], va.x, p0);
+        p1 = fma(arow[c + 1], va.y, p1);
+        p2 = fma(arow[c + 2], vb.x, p2);
+        p3 = fma(arow[c + 3], vb.y, p3);
+      }
+      double p = (i > j) ? (p0 + p1) + (p2 + p3) : 0.0;
+      const double Kd = wave_sum_d(vi * p);
+      const double wi = (i > j) ? p - Kd * vi : 0.0;
+      if (i < K) wsh[i] = wi;
+      wave_lds_sync();
+#pragma unroll
+      for (int c = 0; c < K; c += 2) {
+        const double2 vv = *(const double2*)(vsh + c);
+        const double2 ww = *(const double2*)(wsh + c);
+        arow[c] -= 2.0 * (vi * ww.x + wi * vv.x);
+        arow[c + 1] -= 2.0 * (vi * ww.y + wi * vv.y);
+      }
+      wave_lds_sync();   // vsh / wsh are rewritten next step
+    }
+    // the last two diagonal entries and the last off-diagonal one
+    double dl = 0.0, el = 0.0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      if (c == i) dl = arow[c];
+      if (c == k - 2) el = arow[c];
+    }
+    if (k >= 2 && i == k - 2) dd[k - 2] = dl;
+    if (i == k - 1) { dd[k - 1] = dl; ee[k - 1] = 0.0; if (k >= 2) ee[k - 2] = el; }
+    if (k == 1 && i == 0) dd[0] = dl;
+    wave_lds_sync();
+    if (i < k) e2[i] = ee[i] * ee[i];
+    double glo = dd[0], ghi = dd[0];
+    if (i < k) {
+      const double rad = fabs(ee[i]) + (i > 0 ? fabs(ee[i - 1]) : 0.0);
+      glo = dd[i] - rad;
+      ghi = dd[i] + rad;
+    }
+    glo = wave_min_d(glo);
+    ghi = wave_max_d(ghi);
+    if (i == 0) {
+      const double tn = fmax(fabs(glo), fabs(ghi));
+      bnd[0] = glo - 2.0 * eps * tn - 4.0 * safmin;
+      bnd[1] = ghi + 2.0 * eps * tn + 4.0 * safmin;
+    }
+  }
+  __syncthreads();
+  if constexpr (ST) { if (tid == 0) stamps[1] = clock64(); }
+
+  // ---- 2. multisection for the nt largest eigenvalues ----------------------
+  const int nt = r < k ? r + 1 : k;
+  const int G = NT / nt;
+  double pivmin = 1.0;
+  for (int i = 0; i + 1 < k; ++i) pivmin = fmax(pivmin, e2[i]);
+  pivmin *= safmin;
+  const double tnorm = fmax(fabs(bnd[0]), fabs(bnd[1]));
+  const double atol = 2.0 * eps * tnorm + 2.0 * pivmin;
+  if (tid < nt) { lo_s[tid] = bnd[0]; hi_s[tid] = bnd[1]; }
+  __syncthreads();
+  const int tg = tid / G, g = tid - tg * G;
+  for (int round = 0; round < 80; ++round) {
+    if (tg < nt) {
+      const double lo = lo_s[tg], hi = hi_s[tg];
+      const double x = lo + (hi - lo) * (double)(g + 1) / (double)(G + 1);
+      double q = dd[0] - x;
+      if (fabs(q) < pivmin) q = -pivmin;
+      int c = q < 0.0;
+#pragma unroll
+      for (int i = 1; i < K; ++i) {
+        if (i < k) {
+          q = (dd[i] - x) - e2[i - 1] / q;
+          if (fabs(q) < pivmin) q = -pivmin;
+          c += q < 0.0;
+        }
+      }
+      cnt_s[tid] = c;
+    }
+    __syncthreads();
+    int ok = 1;
+    if (tid < nt) {
+      const int idx = k - 1 - tid;   // ascending index of the tid-th largest
+      const double lo = lo_s[tid], hi = hi_s[tid];
+      double nlo = lo, nhi = hi;
+      for (int gg = 0; gg < G; ++gg) {
+        const double x = lo + (hi - lo) * (double)(gg + 1) / (double)(G + 1);
+        if (cnt_s[tid * G + gg] <= idx) nlo = fmax(nlo, x);
+        else nhi = fmin(nhi, x);
+      }
+      lo_s[tid] = nlo;
+      hi_s[tid] = nhi;
+      ok = (nhi - nlo) <= fmax(atol, 2.0 * eps * fmax(fabs(nlo), fabs(nhi)));
+    }
+    if (__syncthreads_and(ok)) break;
+  }
+  if (tid < nt) lam[tid] = 0.5 * (lo_s[tid] + hi_s[tid]);
+  __syncthreads();
+  if constexpr (ST) { if (tid == 0) stamps[2] = clock64(); }
+
+  // ---- 3. twisted-factorisation eigenvectors (wave 0, lane = vector) -------
+  const double gtol = 1e-3 * tnorm;
+  if (wid == 0) {
+    const int v = lane;
+    if (v < r) {
+      const double l = lam[v];
+      const double gap = fmin(v > 0 ? lam[v - 1] - l : 1e300, v + 1 < nt ? l - lam[v + 1] : 1e300);
+      if (!(gap > 1e-14 * tnorm)) atomicOr(&bad_s, 1);   // numerically repeated
+      if (gap < gtol) atomicOr(&clus_s, 1);
+      // backward pivots D-_i (slot i)
+      double dm = dd[k - 1] - l;
+      if (fabs(dm) < pivmin) dm = -pivmin;
+      T1[k - 1][v] = dm;
+      for (int i = k - 2; i >= 0; --i) {
+        dm = (dd[i] - l) - e2[i] / dm;
+        if (fabs(dm) < pivmin) dm = -pivmin;
+        T1[i][v] = dm;
+      }
+      // forward pivots D+_i and the twist gamma_i = D+_i + D-_i - (d_i - l)
+      double dp = dd[0] - l;
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      int rt = 0;
+      double best = fabs(T1[0][v]);
+      for (int i = 1; i < k; ++i) {
+        dp = (dd[i] - l) - e2[i - 1] / dp;
+        if (fabs(dp) < pivmin) dp = -pivmin;
+        const double gm = fabs(dp + T1[i][v] - (dd[i] - l));
+        if (gm < best) { best = gm; rt = i; }
+      }
+      // D+_i below the twist (slots 0..rt-1), then the two recurrences
+      dp = dd[0] - l;
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      for (int i = 0; i < rt; ++i) {
+        T1[i][v] = dp;
+        dp = (dd[i + 1] - l) - e2[i] / dp;
+        if (fabs(dp) < pivmin) dp = -pivmin;
+      }
+      double x = 1.0, nrm = 1.0;
+      for (int i = rt - 1; i >= 0; --i) {
+        x = -(ee[i] / T1[i][v]) * x;
+        T1[i][v] = x;
+        nrm = fma(x, x, nrm);
+      }
+      T1[rt][v] = 1.0;
+      x = 1.0;
+      for (int i = rt; i + 1 < k; ++i) {
+        x = -(ee[i] / T1[i + 1][v]) * x;
+        T1[i + 1][v] = x;
+        nrm = fma(x, x, nrm);
+      }
+      const double sc = 1.0 / sqrt(nrm);
+      if (!isfinite(sc) || !(sc > 0.0)) atomicOr(&bad_s, 1);
+      for (int i = 0; i < k; ++i) T1[i][v] *= sc;
+    }
+    wave_lds_sync();
+    if (clus_s) {
+      // MGS inside close clusters (lane = component)
+      const int i = lane;
+      for (int c = 1; c < r; ++c) {
+        double xc = i < k ? T1[i][c] : 0.0;
+        bool touched = false;
+        for (int u = 0; u < c; ++u) {
+          if (lam[u] - lam[c] >= gtol) continue;
+          const double dt = wave_sum_d(i < k ? T1[i][u] * xc : 0.0);
+          if (i < k) xc -= dt * T1[i][u];
+          touched = true;
+        }
+        if (touched) {
+          const double n2 = wave_sum_d(xc * xc);
+          if (i < k) T1[i][c] = xc / sqrt(n2);
+        }
+        wave_lds_sync();
+      }
+    }
+    // safety net: every vector must be an eigenvector of T to ~eps ||T||
+    if (lane < r) {
+      const double l = lam[lane];
+      double r2 = 0.0;
+      for (int i = 0; i < k; ++i) {
+        double tx = dd[i] * T1[i][lane];
+        if (i > 0) tx += ee[i - 1] * T1[i - 1][lane];
+        if (i + 1 < k) tx += ee[i] * T1[i + 1][lane];
+        const double d = tx - l * T1[i][lane];
+        r2 = fma(d, d, r2);
+      }
+      if (!(sqrt(r2) <= 1e-11 * tnorm + 1e-300)) atomicOr(&bad_s, 1);
+    }
+  }
+  __syncthreads();
+  if constexpr (ST) { if (tid == 0) stamps[3] = clock64(); }
+
+  // ---- 4. back-transform x <- H_0 ... H_{k-3} x (4 lanes per vector) --------
+  {
+    const int v = tid >> 2, q = tid & 3;
+    if (v < r) {
+      double xv[K / 4];
+#pragma unroll
+      for (int u = 0; u < K / 4; ++u) {
+        const int i = q + 4 * u;
+        xv[u] = i < k ? T1[i][v] : 0.0;
+      }
+      for (int j = k - 3; j >= 0; --j) {
+        double part = 0.0;
+#pragma unroll
+        for (int u = 0; u < K / 4; ++u) part = fma(refl[q + 4 * u][j], xv[u], part);
+        part += dppd<0xB1>(part);
+        part += dppd<0x4E>(part);
+#pragma unroll
+        for (int u = 0; u < K / 4; ++u) xv[u] -= 2.0 * part * refl[q + 4 * u][j];
+      }
+#pragma unroll
+      for (int u = 0; u < K / 4; ++u) {
+        const int i = q + 4 * u;
+        if (i < k) T1[i][v] = xv[u];
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (ST) { if (tid == 0) stamps[4] = clock64(); }
+  for (int t = tid; t < k * r; t += NT) {
+    const int i = t / r, c = t - i * r;
+    out[t] = T1[i][c];
+  }
+  if (tid < r) {
+    const double l = lam[tid];
+    out[k * r + tid] = want_sqrt ? sqrt(l > 0.0 ? l : 0.0) : l;
+  }
+  if (tid == 0) {
+    // with want_sqrt (singular values of a Gram) a vanishing r-th eigenvalue
+    // means fewer than r resolvable directions: the host path decides
+    const int bad = bad_s || (want_sqrt && !(lam[r - 1] > 1e-30 * fmax(lam[0], 1e-300)));
+    if (bad && status) atomicOr(status, 1);
+  }
+}
+
+template <bool ST>
+int launch_tridiag(const double* C, int k, int ldc, int r, double* out, int want_sqrt, int* status,
+                   long long* stamps, hipStream_t s) {
+  if (k <= 16)
+    k_sym_eig_tridiag<16, ST><<<1, NT, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, stamps);
+  else if (k <= 32)
+    k_sym_eig_tridiag<32, ST><<<1, NT, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, stamps);
+  else if (k <= 48)
+    k_sym_eig_tridiag<48, ST><<<1, NT, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, stamps);
+  else
+    k_sym_eig_tridiag<64, ST><<<1, NT, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, stamps);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
 }  // namespace
+
+// Top-r eigenpairs by the tridiagonal path (k <= 64, r <= 32); status bit 1 =
+// the caller should redo this matrix on the host (see the kernel comment).
+SL_API int sl_sym_eig_tridiag(const double* C, int k, int ldc, int r, double* out, int want_sqrt, int* status,
+                              void* stream) {
+  if (k <= 0 || k > TRK || r <= 0 || r > k || r > TRV || ldc < k) return SL_ERR_DIMENSION;
+  return launch_tridiag<false>(C, k, ldc, r, out, want_sqrt, status, nullptr, (hipStream_t)stream);
+}
+
+// diagnostic: shader-clock stamps at the phase boundaries (5 x int64)
+SL_API int sl_sym_eig_tridiag_stamps(const double* C, int k, int ldc, int r, double* out, int* status,
+                                     long long* stamps, void* stream) {
+  if (k <= 0 || k > TRK || r <= 0 || r > k || r > TRV || ldc < k) return SL_ERR_DIMENSION;
+  return launch_tridiag<true>(C, k, ldc, r, out, 0, status, stamps, (hipStream_t)stream);
+}
 
 SL_API int sl_sym_eig_topr(const double* C, int k, int ldc, int r, double* out, int want_sqrt,
                            int max_sweeps, int* sweeps_out, void* stream) {

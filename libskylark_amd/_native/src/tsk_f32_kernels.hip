@@ -367,6 +367,28 @@ k_xm_pipe(const float* __restrict__ Y, int64_t m, int k, const float* __restrict
   }
 }
 
+// Q^T = (Y M)^T as bf16 (k2 x m, row stride ldo): the CholeskyQR step between
+// randSVD power passes writes the next pass's operand directly in the fused
+// pass's "Zt" layout (one launch instead of Q store + bf16 cast + transpose).
+// Small m (the n x k iterate): M staged in LDS, one output per thread, r
+// fastest so the bf16 stores coalesce.
+__global__ void __launch_bounds__(256)
+k_xm_bf16t(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, const float* __restrict__ M, int k2,
+           bf16_t* __restrict__ out, int64_t ldo) {
+  __shared__ float ms[KMAX * KMAX];
+  for (int e = threadIdx.x; e < k * k2; e += 256) ms[e] = M[e];
+  __syncthreads();
+  const int64_t total = m * k2;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int c = (int)(t / m);
+    const int64_t r = t - (int64_t)c * m;
+    const float* y = Y + r * ldy;
+    float acc = 0.f;
+    for (int j = 0; j < k; ++j) acc = fmaf(y[j], ms[j * k2 + c], acc);
+    out[(int64_t)c * ldo + r] = f_to_bf16(acc);
+  }
+}
+
 constexpr int XM_PIPE_GRID_MAX = 2048;
 
 constexpr int G64_PIPE_GRID_MAX = 1024;
@@ -463,5 +485,19 @@ SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const fl
 #undef SL_F
   SL_LAUNCH_CHECK();
   if (G) return sl_slab_reduce_launch_f64(slab, g, (int64_t)KMAX * KMAX, KMAX, kq, kq, G, kq, s);
+  return SL_OK;
+}
+
+// outT (k2 x m bf16, row stride ldo) = (Y M)^T, Y m x k f32 (row stride ldy), M k x k2 f32.
+SL_API int sl_tsk_f32_xm_bf16t(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, void* outT,
+                               int64_t ldo, void* stream) {
+  if (m <= 0) return SL_OK;
+  if (k < 1 || k > KMAX || k2 < 1 || k2 > KMAX || ldo < m) {
+    sl_set_last_error("tsk_f32_xm_bf16t: needs 1 <= k, k2 <= 64 and ldo >= m");
+    return SL_ERR_UNSUPPORTED;
+  }
+  const unsigned grid = sl_grid_for((size_t)(m * k2), 256, 2048);
+  k_xm_bf16t<<<grid, 256, 0, (hipStream_t)stream>>>(Y, m, k, ldy, M, k2, (bf16_t*)outT, ldo);
+  SL_LAUNCH_CHECK();
   return SL_OK;
 }

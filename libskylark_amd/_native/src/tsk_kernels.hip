@@ -798,7 +798,10 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
 #undef SL_TSK
   g_flags = 0;
   if (rc != SL_OK) return rc;
-  rc = sl_slab_reduce_launch(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k, s);
+  // flags & 16: W is an f64 output (reduced straight from the f32 slabs; the
+  // randSVD final pass writes it into its [W; G] buffer with no extra cast/cat)
+  rc = (flags & 16) ? sl_slab_reduce_launch_f64(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, (double*)W, k, s)
+                    : sl_slab_reduce_launch(Wslab, g, (int64_t)NWT * KP, KP, (int)n, k, W, k, s);
   if (rc != SL_OK || (flags & 1)) return rc;
   if (g64) return sl_slab_reduce_launch_d2d((const double*)Gslab, g, (int64_t)KP * KP, KP, k, k, (double*)G, k, s);
   return sl_slab_reduce_launch(Gslab, g, (int64_t)KP * KP, KP, k, k, G, k, s);

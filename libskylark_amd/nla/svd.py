@@ -23,6 +23,7 @@ fp64 CholeskyQR only.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 import sys
@@ -282,6 +283,12 @@ class _DevicePlan:
         self.dev = dev
         self.comm, self.n, self.rank, self.k, self.q, self.skip_qr = comm, n, rank, k, q, skip_qr
         self.Zs = torch.empty(n, k, dtype=torch.float32, device=dev)
+        # the fused pass's operand in its bf16 k x n layout, written in place by
+        # the FJLT realisation and by each CholeskyQR step (no cast/transpose
+        # launches between the passes)
+        self.Zt = torch.empty(k, n, dtype=torch.bfloat16, device=dev)
+        # [W; G] of the final pass, reduced straight into one f64 buffer
+        self.WG = torch.empty(n + k, k, dtype=torch.float64, device=dev)
         # FJLT sketches are realised inside segment 1 from device-held stream
         # coordinates {seed, base_D, base_samples} (ops.fut.fjlt_operator)
         self.prm = torch.zeros(3, dtype=torch.int64, device=dev)
@@ -290,10 +297,21 @@ class _DevicePlan:
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.small = torch.zeros(k * rank + rank, dtype=torch.float64, device=dev)
         self.small_host = torch.zeros(k * rank + rank, dtype=torch.float64).pin_memory()
+        self.small_np = self.small_host.numpy()
+        self.host_pin = self.host_ev = None
         self.ws = torch.empty(T.fused_workspace_bytes(m, n, k), dtype=torch.uint8, device=dev)
         self.ws32 = torch.empty(max(T.f32_workspace_bytes(m), T.f32_workspace_bytes(n)), dtype=torch.uint8,
                                 device=dev)
+        # k x k eigensolve on the device (sym_eig.hip tridiagonal path): the
+        # whole call is then one graph with no host round trip; status bit 1
+        # sends that call's eigensolve back to host LAPACK.  Opt-in: measured
+        # 178 us for k = 40 (serial f64 division chains on one CU) against
+        # ~70 us host LAPACK + ~60 us of round trip (profiles/eig_device_r2.jsonl)
+        self.dev_eig = (k <= 64 and rank <= 32 and os.environ.get("SL_SVD_DEVICE_EIG", "0") == "1"
+                        and dev.type == "cuda")
+        self.eig_status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.use_graph = use_graph
+        self._xm_fn = None
         self.g1 = self.g2 = None
         self.piece_graphs = None   # multi-rank: per-piece graphs (False: capture failed)
         self._Wout = [None] * (q + 1)
@@ -310,31 +328,39 @@ class _DevicePlan:
         A = self.Aref()
         if i == 0:
             self.status.zero_()
+            self.eig_status.zero_()
             if self.fjlt_scale is not None:
                 from ..ops import fut as F
                 with prof.phase("svd.sketch"):
-                    F.fjlt_operator(self.prm, self.k, self.n, self.fjlt_scale, self.Zs, transpose=True)
-            Z = self.Zs
+                    F.fjlt_operator(self.prm, self.k, self.n, self.fjlt_scale, self.Zt, transpose=False)
+            else:
+                self.Zt.copy_(self.Zs.t())
+            Z = None
         else:
             with prof.phase("svd.orth"):
                 # only the subspace matters between passes: one CholeskyQR step
                 W = self._Wout[i - 1]
-                Z = W / W.norm(dim=0, keepdim=True).clamp_min(1e-30) if self.skip_qr else \
-                    SL.cholqr(W, self.status, ws=self.ws32)
+                if self.skip_qr:
+                    self.Zt.copy_((W / W.norm(dim=0, keepdim=True).clamp_min(1e-30)).t())
+                else:
+                    SL.cholqr(W, self.status, ws=self.ws32, zt_out=self.Zt)
+                Z = None
         if i < self.q:
             with prof.phase("svd.fused_pass"):
                 # every piece writes its own output slot: a piece's capture then
                 # reads its predecessor's graph-owned result, never its own warm-up's
-                self._Wout[i], _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws)
+                self._Wout[i], _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws,
+                                                   zt=self.Zt)
             return self._Wout[i]
         with prof.phase("svd.fused_pass"):
             # fp64 Gram of the f32 Y on the f64 matrix cores, formed inside the
             # same pass (no second read of Y): one fp64 CholeskyQR then leaves
             # Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2 with an
-            # f32 second Gram only reached ~eps32, at three times the work)
-            W, G, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True)
-        with prof.phase("svd.final_qr"):
-            self._WG = torch.cat([W.double(), G], 0)
+            # f32 second Gram only reached ~eps32, at three times the work);
+            # W (f64) and G land in the [W; G] buffer the all-reduce takes
+            _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True,
+                                   zt=self.Zt, wg_out=self.WG)
+        self._WG = self.WG
         self.Y = Y
         return self._WG
 
@@ -352,6 +378,11 @@ class _DevicePlan:
             # breakdown status as [C | status] (2 launches)
             Vt, self.host_src = SL.svd_core(W, Rti, self.status)
         self.Rti, self.Vt = Rti, Vt
+        if self.dev_eig:
+            with PROFILER.phase("svd.eig"):
+                SL.sym_eig_tridiag(self.host_src, self.rank, out=self.small, sqrt=True, status=self.eig_status,
+                                   ldc=self.k)
+            self.seg2()
 
     def pieces(self):
         """[(graph-able piece, tensor to all-reduce after it or None)]"""
@@ -382,6 +413,31 @@ class _DevicePlan:
         self.g1 = self.g2 = None
         self.piece_graphs = None
         self.calls = 0
+
+    def _form_u(self):
+        """U = Y M (m x r f32) with the launch arguments bound once: this launch
+        sits between the second replay and the end of the call, so its
+        Python overhead is on the critical path (~25 -> ~8 us)."""
+        from ..ops import tallskinny as T
+        Y, M = self.Y, self.M
+        if not (Y.is_cuda and Y.is_contiguous() and M.is_contiguous() and M.dtype == torch.float32):
+            return T.f32_xm(Y, M, store=True)[0]
+        if self._xm_fn is None:
+            from ..ops import _lib
+            T.f32_xm  # noqa: B018 - registers the signature
+            fn = getattr(_lib.require(), "sl_tsk_f32_xm")
+            if fn.argtypes is None:
+                fn.argtypes = _lib.SIGNATURES["sl_tsk_f32_xm"]
+                fn.restype = ctypes.c_int
+            self._xm_fn = fn
+        m, k = Y.shape
+        r = M.shape[1]
+        U = torch.empty(m, r, dtype=torch.float32, device=self.dev)
+        rc = self._xm_fn(Y.data_ptr(), m, k, k, M.data_ptr(), r, U.data_ptr(), r, None, None,
+                         torch.cuda.current_stream(self.dev).cuda_stream)
+        if rc != 0:
+            return T.f32_xm(Y, M, store=True)[0]
+        return U
 
     def _capture(self, fn, want_out=False):
         s = torch.cuda.Stream(device=self.dev)
@@ -448,8 +504,28 @@ class _DevicePlan:
             self.Zs.copy_(Z)
         tr = _TRACE and [time.perf_counter()]
         self._run(1)
+        if self.dev_eig:
+            from ..ops import tallskinny as T
+            with PROFILER.phase("svd.form_U"):
+                U, _ = T.f32_xm(self.Y, self.M, store=True)
+            if not int(self.eig_status.item()):
+                self.calls += 1
+                if tr:
+                    tr.append(time.perf_counter())
+                    print(f"[svd.trace] device_eig call={(tr[1] - tr[0]) * 1e6:.0f}us", file=sys.stderr)
+                return U, self.s.clone(), self.V.clone()
+            # flagged (near-repeated eigenvalues, non-finite data or a vanishing
+            # r-th eigenvalue): this call's k x k eigensolve goes to host LAPACK
         tr and tr.append(time.perf_counter())
-        host = self.host_src.cpu()
+        # [C | status] into a pinned buffer; wait for that copy only
+        if self.host_pin is None:
+            self.host_pin = torch.empty(self.host_src.numel(), dtype=torch.float64).pin_memory()
+            self.host_np = self.host_pin.numpy()
+            self.host_ev = torch.cuda.Event()
+        self.host_pin.copy_(self.host_src, non_blocking=True)
+        self.host_ev.record()
+        self.host_ev.synchronize()
+        host = self.host_pin
         tr and tr.append(time.perf_counter())
         k, r = self.k, self.rank
         # host[-1] != 0: a CholeskyQR pivot was dropped (rank-deficient block --
@@ -457,30 +533,42 @@ class _DevicePlan:
         # dropped direction is an exactly-zero column from then on, harmless
         # while at least r directions survive.  Non-finite data or fewer than
         # r surviving directions send the call to the robust host path.
-        Cm = host[:k * k].view(k, k)
-        if not bool(torch.isfinite(Cm).all()):
+        # numpy views of the pinned buffers: no torch dispatch on this path
+        Cm = self.host_np[:k * k].reshape(k, k)
+        if not np.isfinite(Cm).all():
             return None
         # C is exactly symmetric (svd_core.hip); eigh returns ascending eigenpairs
-        evals, evecs = _host_eigh(Cm)
-        if not float(evals[k - r]) > 1e-30 * max(float(evals[-1]), 1e-300):
+        got = _host_eigh_np(Cm)
+        if got is None:
             return None
-        pin = self.small_host
-        pin[:k * r].view(k, r).copy_(evecs[:, k - r:].flip(1))
-        torch.sqrt(evals[k - r:].flip(0).clamp_min(0.0), out=pin[k * r:])
+        evals, evecs = got
+        if not evals[k - r] > 1e-30 * max(evals[-1], 1e-300):
+            return None
+        pin = self.small_np
+        pin[:k * r].reshape(k, r)[:] = evecs[:, ::-1][:, :r]
+        np.sqrt(np.maximum(evals[::-1][:r], 0.0), out=pin[k * r:])
         tr and tr.append(time.perf_counter())
         # pinned + non_blocking: the copy is ordered on the stream, the host
         # does not wait (the buffer is rewritten only after the next call's
         # synchronising D2H, which follows this copy in stream order)
-        self.small.copy_(pin, non_blocking=True)
+        self.small.copy_(self.small_host, non_blocking=True)
         tr and tr.append(time.perf_counter())
+        from ..ops import small_la as SL
+        from ..ops import tallskinny as T
+        if self.dev_eig:
+            # eager, into fresh tensors: the graph's own V / M / s buffers stay
+            # bound to the device-eigensolver variant captured in segment 1
+            V, M, s = SL.svd_finish(self.Vt, self.Rti, self.small, r)
+            U, _ = T.f32_xm(self.Y, M, store=True)
+            self.calls += 1
+            return U, s, V
         self._run(2)
         tr and tr.append(time.perf_counter())
         self.calls += 1
-        from ..ops import tallskinny as T
         with PROFILER.phase("svd.form_U"):
             # outside the graph: U lands in a fresh allocation, so the m x r
             # result needs no copy out of the graph's static memory
-            U, _ = T.f32_xm(self.Y, self.M, store=True)
+            U = self._form_u()
         out = U, self.s.clone(), self.V.clone()
         if tr:
             tr.append(time.perf_counter())
@@ -488,6 +576,25 @@ class _DevicePlan:
             print("[svd.trace] " + " ".join(f"{n}={(b - a) * 1e6:.0f}us" for n, a, b in zip(names, tr, tr[1:])),
                   file=sys.stderr)
         return out
+
+
+_EIG_BACKEND = os.environ.get("SL_HOST_EIG", "torch")
+
+
+def _host_eigh_np(C: np.ndarray):
+    """(w ascending, V) of a small symmetric f64 matrix (numpy in / out), or
+    None on a LAPACK failure.  ``SL_HOST_EIG`` picks the LAPACK route:
+    "torch" (single-threaded torch.linalg.eigh on a zero-copy view, the
+    measured fastest), "scipy" (dsyevd through scipy.linalg.lapack) or
+    "numpy"."""
+    if _EIG_BACKEND == "scipy":
+        from scipy.linalg import lapack
+        w, v, info = lapack.dsyevd(C, compute_v=1, lower=0)
+        return (w, v) if info == 0 else None
+    if _EIG_BACKEND == "numpy":
+        return np.linalg.eigh(C)
+    w, v = _host_eigh(torch.from_numpy(C))
+    return w.numpy(), v.numpy()
 
 
 def _host_eigh(C: torch.Tensor):

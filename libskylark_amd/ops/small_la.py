@@ -35,6 +35,28 @@ def sym_eig_topr(C: torch.Tensor, r: int, out: torch.Tensor | None = None, sqrt:
     return out
 
 
+_lib.register("sl_sym_eig_tridiag", [vp, i32, i32, i32, vp, i32, vp, vp])
+
+
+def sym_eig_tridiag(C: torch.Tensor, r: int, out: torch.Tensor | None = None, sqrt: bool = False,
+                    status: torch.Tensor | None = None, ldc: int | None = None):
+    """Top-``r`` eigenpairs (descending) of a symmetric k x k matrix (k <= 64,
+    r <= 32) in one launch: Householder tridiagonalisation, multisection on
+    Sturm counts, twisted-factorisation eigenvectors, back-transform
+    (``sym_eig.hip``).  Output packed as :func:`sym_eig_topr`; ``status`` (int32)
+    gets bit 1 when the result must be recomputed on the host (near-repeated
+    eigenvalues, non-finite data or a vanishing r-th eigenvalue).  ``C`` may be
+    any f64 device buffer holding the matrix with row stride ``ldc``."""
+    k = int(C.shape[0]) if ldc is None else int(ldc)
+    if ldc is None:
+        C = C.to(torch.float64).contiguous()
+    if out is None:
+        out = torch.empty(k * r + r, dtype=torch.float64, device=C.device)
+    _lib.call("sl_sym_eig_tridiag", _lib.ptr(C), k, k, r, _lib.ptr(out), int(bool(sqrt)),
+              _lib.ptr(status) if status is not None else None, vp(_lib.stream_of(C)))
+    return out
+
+
 def chol_inv(G: torch.Tensor, status: torch.Tensor | None = None):
     """R (upper, G = R^T R), R^{-1} (f64) and R^{-1} as f32, all on G's device."""
     k = G.shape[0]
@@ -59,12 +81,17 @@ def small_matmul(A: torch.Tensor, B: torch.Tensor, want32: bool = False):
     return (Cm, C32) if want32 else Cm
 
 
-def cholqr(W: torch.Tensor, status: torch.Tensor | None = None, ws: torch.Tensor | None = None):
+def cholqr(W: torch.Tensor, status: torch.Tensor | None = None, ws: torch.Tensor | None = None,
+           zt_out: torch.Tensor | None = None):
     """One CholeskyQR step (basis of the column space, orthonormal to ~eps*cond(W)):
-    enough to re-condition an intermediate power-iteration block."""
+    enough to re-condition an intermediate power-iteration block.  With
+    ``zt_out`` (bf16 k x n) Q is written there transposed, in the fused pass's
+    operand layout, and returned in that form."""
     W = W.float().contiguous()
     _, G1 = T.f32_xm(W, None, store=False, gram=True, ws=ws)
     _, _, R1i = chol_inv(G1, status)
+    if zt_out is not None:
+        return T.f32_xm_bf16t(W, R1i, zt_out)
     Q, _ = T.f32_xm(W, R1i, store=True)
     return Q
 

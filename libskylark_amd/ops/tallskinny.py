@@ -72,7 +72,8 @@ _WS = FusedWorkspace()
 
 
 def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: bool = True,
-               exact: bool = True, ws: torch.Tensor | None = None, gram64: bool = False):
+               exact: bool = True, ws: torch.Tensor | None = None, gram64: bool = False,
+               zt: torch.Tensor | None = None, wg_out: torch.Tensor | None = None):
     """Return ``(W, G, Y)`` with ``Y = A Z``, ``W = A^T Y`` (n x k), ``G = Y^T Y`` (k x k).
 
     W and G are float32 (A bf16/fp32) or float64 (A fp64); Y is float32/64 or
@@ -84,11 +85,18 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
     with f64 products and f64 accumulation inside the same pass (the fp64
     Gram a CholeskyQR of an ill-conditioned ``Y`` needs; same numbers as
     :func:`gram64` of the returned ``Y`` up to summation order).
+
+    Native-path extras (randSVD device plan): ``zt`` is ``Z`` already in the
+    kernel's bf16 ``k x n`` layout (``Z`` may then be None); ``wg_out`` is an
+    f64 ``(n + k) x k`` buffer that receives ``[W; G]`` directly (with
+    ``gram64``), returned as ``W`` and ``G`` views.
     """
     m, n = A.shape
-    k = Z.shape[1]
+    k = Z.shape[1] if Z is not None else zt.shape[0]
     if _native_ok(A, k):
-        return _fused_native(A, Z, keep_y, gram, exact, ws, gram64)
+        return _fused_native(A, Z, keep_y, gram, exact, ws, gram64, zt, wg_out)
+    if Z is None:
+        Z = zt.t().float()
     wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
     # low-precision A: Z is rounded to A's dtype (as the MFMA kernel does) and
     # the products are formed in f32
@@ -111,6 +119,10 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
         if keep_y:
             Ys.append(y)
     Y = torch.cat(Ys, 0) if keep_y and Ys else (torch.zeros(0, k, dtype=wdt, device=A.device) if keep_y else None)
+    if wg_out is not None:
+        wg_out[:n].copy_(W)
+        wg_out[n:].copy_(G)
+        return wg_out[:n], wg_out[n:], Y
     return W, G, Y
 
 
@@ -122,22 +134,36 @@ def f32_workspace_bytes(m: int) -> int:
     return int(_lib.require().sl_tsk_f32_workspace(m))
 
 
-def _fused_native(A: torch.Tensor, Z: torch.Tensor, keep_y: bool, gram: bool = True, exact: bool = True,
-                  ws: torch.Tensor | None = None, gram64: bool = False):
+def _fused_native(A: torch.Tensor, Z: torch.Tensor | None, keep_y: bool, gram: bool = True, exact: bool = True,
+                  ws: torch.Tensor | None = None, gram64: bool = False, zt: torch.Tensor | None = None,
+                  wg_out: torch.Tensor | None = None):
     m, n = A.shape
-    k = Z.shape[1]
     dev = A.device
-    Zb = Z.t().to(torch.bfloat16).contiguous()  # Zt layout (k x n)
-    W = torch.empty(n, k, dtype=torch.float32, device=dev)
+    if zt is not None:
+        k = zt.shape[0]
+        if zt.dtype != torch.bfloat16 or tuple(zt.shape) != (k, n) or zt.stride(1) != 1 or zt.stride(0) != n:
+            raise ValueError("fused_pass: zt must be a contiguous bf16 k x n tensor")
+        Zb = zt
+    else:
+        k = Z.shape[1]
+        Zb = Z.t().to(torch.bfloat16).contiguous()  # Zt layout (k x n)
     g64 = bool(gram64 and gram and keep_y and exact)
-    G = torch.empty(k, k, dtype=torch.float64 if g64 else torch.float32, device=dev)
+    flags = (0 if gram else 1) | (0 if exact else 2) | (4 if g64 else 0)
+    if wg_out is not None:
+        if not g64 or wg_out.dtype != torch.float64 or tuple(wg_out.shape) != (n + k, k) or not wg_out.is_contiguous():
+            raise ValueError("fused_pass: wg_out needs gram64 and a contiguous f64 (n + k) x k buffer")
+        W, G = wg_out[:n], wg_out[n:]
+        flags |= 16
+    else:
+        W = torch.empty(n, k, dtype=torch.float32, device=dev)
+        G = torch.empty(k, k, dtype=torch.float64 if g64 else torch.float32, device=dev)
     Y = torch.empty(m, k, dtype=torch.float32, device=dev) if keep_y else None
     if ws is None:
         ws = _WS.get(dev, fused_workspace_bytes(m, n, k))
     _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zb), k, _lib.ptr(W), _lib.ptr(G),
               _lib.ptr(Y) if Y is not None else None, 0 if Y is None else Y.stride(0), _lib.ptr(ws),
-              (0 if gram else 1) | (0 if exact else 2) | (4 if g64 else 0), vp(_lib.stream_of(A)))
-    return W, (G.double() if gram else None), Y
+              flags, vp(_lib.stream_of(A)))
+    return W, (G if G.dtype == torch.float64 else G.double()) if gram else None, Y
 
 
 _lib.register("sl_tsk_f32_xm", [vp, i64, i32, i64, vp, i32, vp, i64, vp, vp, vp])
@@ -171,6 +197,25 @@ def f32_xm(Y: torch.Tensor, M: torch.Tensor | None = None, store: bool = True, g
         from ..base.linalg import gram as _g
         G = _g(Q, None)
     return (Q if store else None), G
+
+
+_lib.register("sl_tsk_f32_xm_bf16t", [vp, i64, i32, i64, vp, i32, vp, i64, vp])
+
+
+def f32_xm_bf16t(Y: torch.Tensor, M: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``(Y M)^T`` as a contiguous bf16 ``k2 x m`` tensor (the fused pass's Zt
+    operand layout) in one launch; torch on CPU."""
+    m, k = Y.shape
+    k2 = M.shape[1]
+    if out is None:
+        out = torch.empty(k2, m, dtype=torch.bfloat16, device=Y.device)
+    if Y.is_cuda and Y.dtype == torch.float32 and Y.stride(1) == 1 and k <= 64 and k2 <= 64 and _lib.available():
+        Mc = M.to(device=Y.device, dtype=torch.float32).contiguous()
+        _lib.call("sl_tsk_f32_xm_bf16t", _lib.ptr(Y), m, k, Y.stride(0), _lib.ptr(Mc), k2, _lib.ptr(out),
+                  out.stride(0), vp(_lib.stream_of(Y)))
+        return out
+    out.copy_((Y.float() @ M.float()).t())
+    return out
 
 
 _lib.register("sl_tsk_gram64", [vp, i64, i32, i64, vp, vp, vp])

@@ -274,3 +274,40 @@ def test_approximate_svd_graph_replay_matches_eager(dev):
     # a different sketch (fresh context) still gives the same top spectrum
     _, s2, _ = sk.nla.approximate_svd(A, 8, context=sk.Context(10), params=p)
     torch.testing.assert_close(s2.cpu(), s0[:8], rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("force_fallback", [False, True])
+def test_approximate_svd_device_eig_matches_host(dev, monkeypatch, force_fallback):
+    """The device k x k eigensolver (one graph per call) gives the host-LAPACK
+    plan's answer; a flagged eigensolve (forced here) re-runs on the host
+    inside the same call and still matches, on eager, capture and replay calls."""
+    from libskylark_amd.nla import svd as SV
+    from libskylark_amd.ops import small_la as SLm
+    A = _fullrank_decaying(20000, 256, 0.9, 5).to(dev, torch.bfloat16)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT")
+    monkeypatch.setenv("SL_SVD_DEVICE_EIG", "0")
+    SV._PLANS.clear()
+    Uh, sh, Vh = sk.nla.approximate_svd(A, 10, context=sk.Context(3), params=p)
+    assert not list(SV._PLANS.values())[0].dev_eig
+    monkeypatch.setenv("SL_SVD_DEVICE_EIG", "1")
+    SV._PLANS.clear()
+    if force_fallback:
+        orig = SLm.sym_eig_tridiag
+
+        def flagged(*a, **kw):
+            out = orig(*a, **kw)
+            kw["status"].fill_(1)
+            return out
+        monkeypatch.setattr(SLm, "sym_eig_tridiag", flagged)
+    for _ in range(3):                       # eager, capture, replay
+        U, s, V = sk.nla.approximate_svd(A, 10, context=sk.Context(3), params=p)
+        plan = list(SV._PLANS.values())[0]
+        assert plan.dev_eig
+        assert bool(plan.eig_status.item()) == force_fallback
+        torch.testing.assert_close(s, sh, rtol=1e-6, atol=0)
+        torch.testing.assert_close((U.double().t() @ Uh.double()).abs().diagonal(),
+                                   torch.ones(10, dtype=torch.float64, device=dev), atol=1e-5, rtol=0)
+        torch.testing.assert_close((V.double().t() @ Vh.double()).abs().diagonal(),
+                                   torch.ones(10, dtype=torch.float64, device=dev), atol=1e-5, rtol=0)
+    assert plan.graph_built()

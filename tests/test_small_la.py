@@ -125,3 +125,85 @@ def test_svd_core_and_finish_gpu(dev):
     torch.testing.assert_close(V.cpu().double(), (Vref @ Ub) / sv, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(M.cpu().double(), Rti @ Ub, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(s.cpu().double(), sv, rtol=1e-6, atol=0)
+
+
+def _eig_check(C, out, k, r):
+    V, lam = out[:k * r].view(k, r), out[k * r:]
+    ref = torch.sort(torch.linalg.eigvalsh(C), descending=True).values[:r]
+    nrm = float(torch.linalg.eigvalsh(C).abs().max())
+    assert float((lam - ref).abs().max()) / nrm < 1e-13, (lam - ref).abs().max()
+    res = (C @ V - V * lam).norm(dim=0) / nrm
+    assert float(res.max()) < 1e-10, res.max()
+    assert torch.allclose(V.t() @ V, torch.eye(r, dtype=torch.float64), atol=1e-10)
+
+
+@pytest.mark.parametrize("k,r", [(40, 20), (7, 3), (64, 32), (48, 10), (2, 1), (1, 1), (3, 3), (33, 32)])
+@pytest.mark.parametrize("kind", ["uniform", "logspace", "planted", "gram", "indefinite"])
+def test_sym_eig_tridiag_vs_lapack(dev, k, r, kind):
+    """Device tridiagonal eigensolver (Householder + multisection + twisted
+    factorisation) against LAPACK: eigenvalues to eps ||C||, residuals,
+    orthogonality, and no host-fallback flag on well-separated spectra."""
+    g = torch.Generator().manual_seed(k * 7 + r)
+    Q, _ = torch.linalg.qr(torch.randn(k, k, generator=g, dtype=torch.float64))
+    if kind == "uniform":
+        lam = torch.rand(k, generator=g, dtype=torch.float64) + 0.1
+    elif kind == "logspace":
+        lam = torch.logspace(0, -12, k, dtype=torch.float64)
+    elif kind == "planted":
+        lam = (1000.0 * 0.9 ** torch.arange(k, dtype=torch.float64)) ** 2
+    elif kind == "indefinite":
+        lam = torch.randn(k, generator=g, dtype=torch.float64) * 3
+    else:
+        X = torch.randn(1000, k, generator=g, dtype=torch.float64)
+        C = X.t() @ X
+        lam = None
+    if lam is not None:
+        C = (Q * lam) @ Q.t()
+        C = 0.5 * (C + C.t())
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = SL.sym_eig_tridiag(C.to(dev), r, status=st).cpu()
+    assert int(st.item()) == 0
+    _eig_check(C, out, k, r)
+    # sqrt packing as the randSVD plan consumes it
+    out2 = SL.sym_eig_tridiag(C.to(dev), r, sqrt=True).cpu()
+    lam2 = out[k * r:]
+    torch.testing.assert_close(out2[k * r:], lam2.clamp_min(0).sqrt(), rtol=4e-16, atol=0)
+
+
+def test_sym_eig_tridiag_close_cluster(dev):
+    """Relative gaps 1e-6 inside the top block: re-orthogonalised, no fallback."""
+    k, r = 40, 20
+    g = torch.Generator().manual_seed(5)
+    Q, _ = torch.linalg.qr(torch.randn(k, k, generator=g, dtype=torch.float64))
+    lam = torch.linspace(10, 1, k, dtype=torch.float64)
+    lam[3:6] = torch.tensor([7.11, 7.11 - 1e-6 * 10, 7.11 - 2e-6 * 10], dtype=torch.float64)
+    C = (Q * lam) @ Q.t()
+    C = 0.5 * (C + C.t())
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = SL.sym_eig_tridiag(C.to(dev), r, status=st).cpu()
+    assert int(st.item()) == 0
+    V, lv = out[:k * r].view(k, r), out[k * r:]
+    assert torch.allclose(V.t() @ V, torch.eye(r, dtype=torch.float64), atol=1e-10)
+    ref = torch.sort(torch.linalg.eigvalsh(C), descending=True).values[:r]
+    assert float((lv - ref).abs().max()) < 1e-12 * 10
+    # the cluster's invariant subspace is right even if its basis is not LAPACK's
+    res = (C @ V - V * lv).norm(dim=0) / 10
+    assert float(res.max()) < 1e-8
+
+
+@pytest.mark.parametrize("case", ["repeated", "low_rank", "nan"])
+def test_sym_eig_tridiag_flags_host_fallback(dev, case):
+    k, r = 32, 20
+    g = torch.Generator().manual_seed(9)
+    Q, _ = torch.linalg.qr(torch.randn(k, k, generator=g, dtype=torch.float64))
+    if case == "repeated":
+        lam = torch.tensor([2.0] * 16 + [1.0] * 16, dtype=torch.float64)
+    else:
+        lam = torch.cat([torch.linspace(5, 1, 10, dtype=torch.float64), torch.zeros(k - 10, dtype=torch.float64)])
+    C = (Q * lam) @ Q.t()
+    if case == "nan":
+        C = (Q * (torch.rand(k, generator=g, dtype=torch.float64) + 1)) @ Q.t()
+        C[3, 4] = float("nan")
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    SL.sym_eig_tridiag(C.to(dev), r, status=st, sqrt=True)
+    assert int(st.item()) & 1
