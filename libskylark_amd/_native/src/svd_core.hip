@@ -188,3 +188,17 @@ SL_API int sl_svd_finish(const double* Vt, int n, int k, const double* Rti, cons
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
+
+SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
+                         int64_t ldo, double* G, void* ws, void* stream);
+
+// The randSVD call's last two launches from one host call: V, M, s from the
+// eigenpairs (sl_svd_finish), then U = Y M (m x r, sl_tsk_f32_xm) -- the
+// host-side launch cost sits on the critical path between the eigensolve
+// and the end of the call.
+SL_API int sl_svd_finish_u(const double* Vt, int n, int k, const double* Rti, const double* small, int r, float* V,
+                           float* M, float* s32, const float* Y, int64_t m, float* U, void* stream) {
+  int rc = sl_svd_finish(Vt, n, k, Rti, small, r, V, M, s32, stream);
+  if (rc != SL_OK) return rc;
+  return sl_tsk_f32_xm(Y, m, k, k, M, r, U, r, nullptr, nullptr, stream);
+}

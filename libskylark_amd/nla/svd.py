@@ -312,6 +312,7 @@ class _DevicePlan:
         self.eig_status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.use_graph = use_graph
         self._xm_fn = None
+        self._fu_fn = None
         self.g1 = self.g2 = None
         self.piece_graphs = None   # multi-rank: per-piece graphs (False: capture failed)
         self._Wout = [None] * (q + 1)
@@ -406,6 +407,15 @@ class _DevicePlan:
             # V = A^T Q Ub S^{-1} = Vt Ub S^{-1};  U = Y M with M = Rt^{-1} Ub (one launch)
             self.V, self.M, self.s = SL.svd_finish(self.Vt, self.Rti, self.small, r)
 
+    def _collectives_capturable(self):
+        """True once this communicator's one-shot path holds every operand the
+        segment all-reduces (set up by the first, eager call)."""
+        os_ = getattr(self.comm, "_oneshot", None)
+        if not os_ or self.calls < 1:
+            return False
+        outs = [w for w in self._Wout if w is not None] + [self.WG]
+        return all(os_.fits(t) for t in outs)
+
     def graph_built(self):
         return self.g1 is not None or bool(self.piece_graphs)
 
@@ -413,6 +423,38 @@ class _DevicePlan:
         self.g1 = self.g2 = None
         self.piece_graphs = None
         self.calls = 0
+
+    def _finish_u_ok(self):
+        Y = self.Y
+        return (not PROFILER.enabled and Y is not None and Y.is_cuda and Y.dtype == torch.float32
+                and Y.is_contiguous() and self.Vt.is_contiguous() and self.Rti.is_contiguous())
+
+    def _finish_u(self):
+        if self._fu_fn is None:
+            from ..ops import _lib
+            fn = getattr(_lib.require(), "sl_svd_finish_u")
+            P, I, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+            fn.argtypes = [P, I, I, P, P, I, P, P, P, P, L, P, P]
+            fn.restype = ctypes.c_int
+            self._fu_fn = fn
+        n, k = self.Vt.shape
+        r = self.rank
+        m = self.Y.shape[0]
+        dev = self.dev
+        V = torch.empty(n, r, dtype=torch.float32, device=dev)
+        M = torch.empty(k, r, dtype=torch.float32, device=dev)
+        s = torch.empty(r, dtype=torch.float32, device=dev)
+        U = torch.empty(m, r, dtype=torch.float32, device=dev)
+        rc = self._fu_fn(self.Vt.data_ptr(), n, k, self.Rti.data_ptr(), self.small.data_ptr(), r, V.data_ptr(),
+                         M.data_ptr(), s.data_ptr(), self.Y.data_ptr(), m, U.data_ptr(),
+                         torch.cuda.current_stream(dev).cuda_stream)
+        if rc != 0:
+            from ..ops import _lib
+            _lib.call("sl_svd_finish", _lib.ptr(self.Vt), n, k, _lib.ptr(self.Rti), _lib.ptr(self.small), r,
+                      _lib.ptr(V), _lib.ptr(M), _lib.ptr(s), ctypes.c_void_p(_lib.stream_of(V)))
+            from ..ops import tallskinny as T
+            U = T.f32_xm(self.Y, M, store=True)[0]
+        return U, s, V
 
     def _form_u(self):
         """U = Y M (m x r f32) with the launch arguments bound once: this launch
@@ -456,7 +498,12 @@ class _DevicePlan:
         fn = self.seg1 if which == 1 else self.seg2
         g = self.g1 if which == 1 else self.g2
         warm = self.use_graph and self.calls >= 1 and not PROFILER.enabled
-        if which == 1 and self.comm.size > 1 and self.piece_graphs is not False:
+        if which == 1 and self.comm.size > 1 and self._collectives_capturable():
+            # every all-reduce of segment 1 is the one-shot kernel
+            # (parallel/oneshot.py): the whole segment, collectives included,
+            # is one graph, as with a single rank
+            pass
+        elif which == 1 and self.comm.size > 1 and self.piece_graphs is not False:
             # multi-rank: one graph per piece, eager collectives in between
             if self.piece_graphs is None and warm:
                 try:
@@ -562,14 +609,21 @@ class _DevicePlan:
             U, _ = T.f32_xm(self.Y, M, store=True)
             self.calls += 1
             return U, s, V
-        self._run(2)
-        tr and tr.append(time.perf_counter())
-        self.calls += 1
-        with PROFILER.phase("svd.form_U"):
-            # outside the graph: U lands in a fresh allocation, so the m x r
-            # result needs no copy out of the graph's static memory
-            U = self._form_u()
-        out = U, self.s.clone(), self.V.clone()
+        if self._finish_u_ok():
+            # V, M, s and U = Y M into fresh tensors from ONE host call (two
+            # launches): no second graph replay, no clones out of graph memory
+            out = self._finish_u()
+            tr and tr.append(time.perf_counter())
+            self.calls += 1
+        else:
+            self._run(2)
+            tr and tr.append(time.perf_counter())
+            self.calls += 1
+            with PROFILER.phase("svd.form_U"):
+                # outside the graph: U lands in a fresh allocation, so the m x r
+                # result needs no copy out of the graph's static memory
+                U = self._form_u()
+            out = U, self.s.clone(), self.V.clone()
         if tr:
             tr.append(time.perf_counter())
             names = ["replay1", "d2h_sync", "eigh", "h2d", "replay2", "form_U"]

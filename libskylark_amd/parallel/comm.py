@@ -81,7 +81,30 @@ class Comm:
     def _count(self, nbytes: int):
         self.bytes_sent = getattr(self, "bytes_sent", 0) + int(nbytes)
 
+    def _oneshot_for(self, t: torch.Tensor):
+        """The one-shot path for a small device SUM operand, or None (opt-in,
+        parallel/oneshot.py; set up collectively on first use)."""
+        from . import oneshot
+        if not oneshot.enabled() or not t.is_cuda:
+            return None
+        os_ = getattr(self, "_oneshot", None)
+        if os_ is None:
+            try:
+                os_ = oneshot.OneShotAllReduce(self, device=t.device)
+            except Exception:  # noqa: BLE001 - no IPC / no native library: stay on RCCL
+                os_ = False
+            if os_ is not False and not os_.ok:
+                os_ = False
+            self._oneshot = os_
+        return os_ if (os_ and os_.fits(t)) else None
+
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM if dist.is_available() else None):
+        if self._active and op == dist.ReduceOp.SUM:
+            os_ = self._oneshot_for(t)
+            if os_ is not None:
+                os_.all_reduce(t)
+                self._count(t.numel() * t.element_size() * (self.size - 1))
+                return t
         if self._active:
             st = self._stage(t)
             dist.all_reduce(st, op=op, group=self.group)

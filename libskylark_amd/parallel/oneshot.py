@@ -1,0 +1,137 @@
+"""One-shot all-reduce for small device operands.
+
+The Krylov scalars, the CondEst norms and the (n + k) x k partial results of
+the randSVD passes are tens to hundreds of KB: a ring all-reduce over the
+point-to-point xGMI mesh pays 2(p-1) latency-bound steps for them.  Here each
+rank pushes its operand once into every peer's receive buffer (mapped into
+this process by IPC), waits for the peers' flags in its own buffer and sums
+the p slots in rank order -- one kernel, one xGMI hop, the same bits on
+every rank, capturable in a hipGraph (``_native/src/oneshot_kernels.hip``).
+
+Reference reduction sites: ``base/inner.hpp:22,84,170`` (MPI_Allreduce of
+column norms / dots), ``nla/svd.hpp`` (El::AllReduce of the small factors).
+
+Opt-in (``SL_ONESHOT=1`` or :func:`enable`): :class:`~.comm.Comm` then routes
+f32 / f64 device all-reduces of at most ``cap`` bytes here and everything
+else to RCCL.  Setup is collective; if any rank cannot export or map the
+buffers, every rank stays on RCCL.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+from ..ops import _lib
+
+vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+_lib.register("sl_oneshot_alloc", [i64, i32, C.POINTER(C.c_void_p), vp])
+_lib.register("sl_oneshot_open", [vp, C.POINTER(C.c_void_p)])
+_lib.register("sl_oneshot_close", [vp])
+_lib.register("sl_oneshot_free", [vp])
+_lib.register("sl_oneshot_handle_bytes", [])
+_lib.register("sl_oneshot_buffer_bytes", [i64, i32], C.c_int64)
+_lib.register("sl_oneshot_allreduce", [vp, i64, i32, i32, i32, vp, i64, vp, vp, C.c_double, vp])
+
+DEFAULT_CAP = 1 << 20      # bytes per slot: covers (n + k) x k f64 for n <= 3000, k = 40
+TIMEOUT_S = 30.0
+
+
+class OneShotError(RuntimeError):
+    pass
+
+
+class OneShotAllReduce:
+    """Peer-mapped receive buffers of one communicator (collective constructor)."""
+
+    def __init__(self, comm, cap: int = DEFAULT_CAP, device=None):
+        self.comm = comm
+        self.p, self.rank = comm.size, comm.rank
+        self.cap = int(cap)
+        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.ok = False
+        self._local = None
+        self._peers = []
+        lib = _lib.load()
+        hb = int(lib.sl_oneshot_handle_bytes()) if lib is not None and hasattr(lib, "sl_oneshot_alloc") else 0
+        mine = None
+        if hb and 2 <= self.p <= 16:
+            with torch.cuda.device(self.dev):
+                buf = C.c_void_p()
+                h = (C.c_char * hb)()
+                if _lib.require().sl_oneshot_alloc(self.cap, self.p, C.byref(buf), h) == 0:
+                    self._local = buf
+                    mine = bytes(h)
+        handles = comm.all_gather_object(mine)
+        ok = all(x is not None for x in handles)
+        bases = []
+        if ok:
+            with torch.cuda.device(self.dev):
+                for q, h in enumerate(handles):
+                    if q == self.rank:
+                        bases.append(self._local.value)
+                        continue
+                    ptr = C.c_void_p()
+                    hbuf = (C.c_char * len(h)).from_buffer_copy(h)
+                    if _lib.require().sl_oneshot_open(hbuf, C.byref(ptr)) != 0:
+                        ok = False
+                        break
+                    self._peers.append(ptr)
+                    bases.append(ptr.value)
+        # every rank must agree before anyone uses the path
+        flags = comm.all_gather_object(bool(ok))
+        self.ok = all(flags)
+        if not self.ok:
+            self.close()
+            return
+        self.bases = torch.tensor(bases, dtype=torch.int64, device=self.dev)
+        self.state = torch.zeros(2, dtype=torch.int64, device=self.dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        # the collective must not start before every peer has mapped this buffer
+        comm.barrier()
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return (self.ok and t.is_cuda and t.device == self.dev and t.dtype in (torch.float32, torch.float64)
+                and t.is_contiguous() and t.numel() * t.element_size() <= self.cap)
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum of ``t`` over the ranks (stream-ordered, no host sync)."""
+        if not self.fits(t):
+            raise OneShotError("one-shot all-reduce: operand does not fit this buffer")
+        _lib.call("sl_oneshot_allreduce", _lib.ptr(t), t.numel(), _lib.dtype_code(t.dtype), self.rank, self.p,
+                  _lib.ptr(self.bases), self.cap, _lib.ptr(self.state), _lib.ptr(self.err), float(TIMEOUT_S),
+                  vp(_lib.stream_of(t)))
+        return t
+
+    def check(self):
+        """Raise if any earlier call timed out waiting for a peer (host sync)."""
+        if int(self.err.item()):
+            raise OneShotError("one-shot all-reduce: a peer did not arrive within the timeout")
+
+    def close(self):
+        lib = _lib.load()
+        if lib is None:
+            return
+        for ptr in self._peers:
+            lib.sl_oneshot_close(ptr)
+        self._peers = []
+        if self._local is not None:
+            lib.sl_oneshot_free(self._local)
+            self._local = None
+        self.ok = False
+
+
+_ENABLED = os.environ.get("SL_ONESHOT", "0") == "1"
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def enable(flag: bool = True):
+    """Route small device all-reduces of every :class:`Comm` through the
+    one-shot path (buffers are set up lazily, collectively, per communicator
+    on its first eligible all-reduce)."""
+    global _ENABLED
+    _ENABLED = bool(flag)

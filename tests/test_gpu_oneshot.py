@@ -1,0 +1,65 @@
+"""One-shot all-reduce over IPC-mapped receive buffers (oneshot_kernels.hip):
+two processes on the box's one GPU (the kernel path is the same as across
+GPUs: remote stores into a peer's buffer, flags, rank-ordered sums), handle
+exchange over gloo.  Against the sum of the ranks' inputs computed on the
+host; repeated calls exercise both buffer sets and the device generation
+counter; one call is replayed from a captured hipGraph."""
+import pytest
+import torch
+
+from mp_utils import run_distributed
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world):
+    import torch
+    from libskylark_amd.parallel import oneshot
+    from libskylark_amd.parallel.comm import world as W
+    torch.cuda.set_device(0)
+    comm = W()
+    os_ = oneshot.OneShotAllReduce(comm, cap=1 << 16)
+    if not os_.ok:
+        return "unavailable"
+    dev = torch.device("cuda", 0)
+    for it, (n, dt) in enumerate([(1, torch.float64), (37, torch.float32), (4096, torch.float64),
+                                  (8192, torch.float32), (300, torch.float64)] * 6):
+        xs = [torch.arange(n, dtype=torch.float64) * (q + 1) + it for q in range(world)]
+        ref = sum(xs)
+        x = xs[rank].to(dev, dt)
+        os_.all_reduce(x)
+        torch.cuda.synchronize()
+        assert torch.allclose(x.double().cpu(), ref, rtol=1e-6 if dt == torch.float32 else 1e-14), (it, n)
+    # rank-ordered sums: bitwise identical on every rank
+    y = (torch.randn(1000, dtype=torch.float64, generator=torch.Generator().manual_seed(rank)) * 1e3).to(dev)
+    os_.all_reduce(y)
+    got = comm.all_gather_object(y.cpu().numpy().tobytes())
+    assert all(g == got[0] for g in got)
+    # graph capture and replay
+    z = torch.zeros(64, dtype=torch.float64, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        z.fill_(rank + 1.0)
+        os_.all_reduce(z)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        z.fill_(rank + 1.0)
+        os_.all_reduce(z)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.all(z.cpu() == sum(q + 1.0 for q in range(world)))
+    os_.check()
+    comm.barrier()
+    os_.close()
+    return "ok"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_oneshot_allreduce_two_processes_one_gpu(world):
+    res = run_distributed(_worker, world, timeout=180)
+    if all(r == "unavailable" for r in res):
+        pytest.skip("IPC export of uncached device memory unavailable here")
+    assert res == ["ok"] * world
