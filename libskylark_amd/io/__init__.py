@@ -203,3 +203,30 @@ def _csr(e, row0, nrows, ncols, dtype):
 
 ReadArcList = read_arc_list
 ReadHDF5 = read_hdf5
+
+
+def readlibsvm(fname: str, X=None, Y=None, direction="rows", min_d: int = 0, max_n: int = -1, comm=None,
+               sparse: bool = False, dtype=torch.float64):
+    """python-skylark ``skylark.io.readlibsvm`` (``python-skylark/skylark/io.py``):
+    ``(X, Y)`` with examples as rows (``direction`` "rows" / 1) or columns
+    ("columns" / 0).  ``X`` / ``Y`` given as DistMatrix templates select a
+    distributed read over their communicator; otherwise a local read."""
+    if direction in (0, "columns"):
+        cols = True
+    elif direction in (1, "rows"):
+        cols = False
+    else:
+        raise ValueError("Direction must be either columns/rows or 0/1")
+    from ..parallel.distmatrix import DistMatrix
+    tmpl = X if isinstance(X, DistMatrix) else (Y if isinstance(Y, DistMatrix) else None)
+    if tmpl is not None or comm is not None:
+        c = comm or tmpl.comm
+        Xd, Yd = read_libsvm_dist(fname, c, min_d=min_d, sparse=sparse, dtype=dtype)
+        if cols:
+            Xd = Xd.redistribute("STAR_VC") if hasattr(Xd, "redistribute") and not sparse else Xd
+        return Xd, Yd
+    Xl, Yl = read_libsvm(fname, min_d=min_d, max_n=max_n, sparse=sparse, dtype=dtype)
+    if cols:
+        Xl = Xl.t().to_sparse_csr() if sparse else Xl.t().contiguous()
+    return Xl, Yl
+
