@@ -4,10 +4,18 @@ rank-20 SVD (q = 2 power iterations) of a dense bf16 1e6 x 1e3 matrix held
 2-D block-cyclic ([MC,MR]) over the N GPUs of one node, one process per GPU,
 RCCL over xGMI.
 
-Scaling is STRONG by default: the GLOBAL matrix is 1e6 x 1e3 for every N
-(1 GPU: a 1 x 1 grid; 8 GPUs: a 2 x 4 grid of 4096 x 128 tiles).  One
-"step" = one complete ``approximate_svd`` call on the [MC,MR] operand: the
-one all-to-all that brings it to row shards, the FJLT sketch, q = 2 fused
+Scaling is STRONG by default: the GLOBAL matrix is 1e6 x 1e3 for every N.
+The process grid is shaped for the operand: a tall-skinny 1e6 x 1e3 matrix
+goes on an N x 1 grid of 4096-row tiles (``--grid-rows``; Elemental's
+``Grid(comm, height)``), where every rank's cyclic row tiles already hold
+whole rows, so randSVD reads them in place and the only traffic is the
+(n + k) x k all-reduces.  A square-ish grid (2 x 4 at N = 8) would have to
+move ~3/4 of A over xGMI on every call (~190 MB per rank, about 1 ms on the
+point-to-point links -- more than the whole 8-GPU compute); for N > 1 that
+grid is still timed, as the secondary key ``square_grid``.  One
+"step" = one complete ``approximate_svd`` call on the [MC,MR] operand: (on
+a grid with several columns, the one all-to-all that brings it to row
+shards,) the FJLT sketch, q = 2 fused
 power passes, the final basis pass, the small SVD and U returned in A's
 [MC,MR] layout.  Nothing is cached between steps except the input matrix
 and reusable workspaces.  ``--scaling weak`` times 1e6 rows PER GPU in
@@ -83,7 +91,7 @@ def check_answer(A, U, s, V, comm):
     return orth, resid
 
 
-def run(a, comm, dev, scaling):
+def run(a, comm, dev, scaling, square=False):
     import libskylark_amd as sk
     from libskylark_amd.ops import tallskinny
     from libskylark_amd.parallel.distmatrix import Grid
@@ -95,7 +103,10 @@ def run(a, comm, dev, scaling):
     else:
         m = a.rows * N
         layout = "VC_STAR"
-    grid = Grid.default(comm) if layout == "MC_MR" else None
+    grid = None
+    if layout == "MC_MR":
+        pr = None if square else (a.grid_rows or N)
+        grid = Grid.default(comm, pr)
     block = (a.tile_rows, a.tile_cols) if layout == "MC_MR" else None
     A = planted_matrix((m, n), layout, comm, dev, grid, block)
     torch.cuda.synchronize()
@@ -104,7 +115,8 @@ def run(a, comm, dev, scaling):
     def step():
         return sk.nla.approximate_svd(A, a.rank, context=sk.Context(seed=38734), params=params)
 
-    steps, warmup = (a.steps, a.warmup) if scaling == a.scaling else (max(3, a.steps // 2), 2)
+    primary = scaling == a.scaling and not square
+    steps, warmup = (a.steps, a.warmup) if primary else (max(3, a.steps // 2), 2)
     for _ in range(warmup):
         U, s, V = step()
     torch.cuda.synchronize()
@@ -122,14 +134,16 @@ def run(a, comm, dev, scaling):
     ms = float(t.item()) / steps * 1e3
     orth, resid = check_answer(A, U, s, V, comm)
     if grid is not None:
+        how = "tiles read in place (whole rows per rank)" if grid.pc == 1 else "one all-to-all to [VC,*]"
         par = f"2-D block-cyclic [MC,MR] {grid.pr}x{grid.pc} grid, tile {block[0]}x{block[1]}, " \
-              f"one all-to-all to [VC,*] + RCCL all-reduces"
+              f"{how} + RCCL all-reduces"
     else:
         par = f"dp{N} ([VC,*] row blocks, RCCL all-reduce)"
     return {
         "m": m, "n": n, "ms": ms, "gbs": m * n * 2 / (ms / 1e3) / 1e9, "steps": steps, "warmup": warmup,
         "parallelism": par, "orth_err": orth, "resid_rel": resid,
         "top_singular_values": [round(float(x), 3) for x in s[:3].tolist()],
+        "grid_pc": grid.pc if grid is not None else 0,
         "native_fused_pass": bool(tallskinny._native_ok(torch.empty(8, 8, dtype=torch.bfloat16, device=dev),
                                                         2 * a.rank)),
     }
@@ -149,12 +163,15 @@ def main(argv=None):
     ap.add_argument("--layout", default="MC_MR", help="layout of A for strong scaling")
     ap.add_argument("--tile-rows", type=int, default=4096)
     ap.add_argument("--tile-cols", type=int, default=128)
+    ap.add_argument("--grid-rows", type=int, default=0, help="process-grid height for [MC,MR] (0: N, i.e. N x 1)")
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling run (N > 1)")
+    ap.add_argument("--no-square", action="store_true", help="skip the secondary square-grid run (N > 1)")
     ap.add_argument("--native", type=int, default=1, help="use the fused HIP pass kernel")
     a = ap.parse_args(argv)
 
     from libskylark_amd.ops import tallskinny
     from libskylark_amd.parallel import init_distributed
+    from libskylark_amd.parallel.distmatrix import Grid
 
     tallskinny.USE_NATIVE = bool(a.native)
     if not torch.cuda.is_available():
@@ -166,7 +183,10 @@ def main(argv=None):
     dev = torch.device("cuda", torch.cuda.current_device())
     N = comm.size
     res = run(a, comm, dev, a.scaling)
-    weak = None
+    weak = sq = None
+    if N > 1 and a.scaling == "strong" and a.layout == "MC_MR" and not a.no_square and \
+            Grid.default(comm).pc != res["grid_pc"]:
+        sq = run(a, comm, dev, "strong", square=True)
     if N > 1 and a.scaling == "strong" and not a.no_weak:
         weak = run(a, comm, dev, "weak")
     ok = res["orth_err"] < 1e-3 and res["resid_rel"] < 5e-2
@@ -196,6 +216,10 @@ def main(argv=None):
             "top_singular_values": res["top_singular_values"],
             "native_fused_pass": res["native_fused_pass"],
         }
+        if sq is not None:
+            out["square_grid"] = {"value": round(sq["gbs"], 2), "ms_per_step": round(sq["ms"], 4),
+                                  "steps": sq["steps"], "parallelism": sq["parallelism"],
+                                  "check": {"orth_err": sq["orth_err"], "resid_rel": sq["resid_rel"]}}
         if weak is not None:
             out["weak"] = {"value": round(weak["gbs"], 2), "ms_per_step": round(weak["ms"], 4),
                            "global_rows": weak["m"], "steps": weak["steps"], "parallelism": weak["parallelism"],

@@ -86,6 +86,11 @@ def _sketch_operator(kind: str, n: int, k: int, ctx: Context, device, dtype) -> 
 _ROWBUF: dict = {}
 
 
+def _whole_rows(A) -> bool:
+    """[MC,MR] whose grid has one column: each rank stores complete rows."""
+    return A.layout == "MC_MR" and A.grid is not None and A.grid.pc == 1
+
+
 def _as_rowdist(A):
     """(local row shard tensor, comm, m_global, DistMatrix or None).
 
@@ -94,6 +99,12 @@ def _as_rowdist(A):
     repeated calls on the same operand keep a stable shard address (the
     device plan and its graphs stay valid) and allocate nothing."""
     if isinstance(A, DistMatrix):
+        if _whole_rows(A):
+            # [MC,MR] on a p x 1 grid: every rank already holds whole rows (its
+            # cyclic row tiles).  randSVD only ever reduces over rows, so the
+            # local tile IS a row shard -- no data moves; U comes back in the
+            # same local row order (_u_like)
+            return A.local, A.comm, A.shape[0], A
         if A.layout not in ("VC_STAR", "VR_STAR"):
             key = (A.layout, A.shape, A.block, None if A.grid is None else (A.grid.pr, A.grid.pc),
                    A.comm.rank, A.comm.size, id(A.comm.group), A.local.dtype, str(A.local.device))
@@ -113,6 +124,9 @@ def _u_like(U_loc, m, rank, comm, Ad, A):
     """U as a DistMatrix in A's layout (the reference's UType follows A's
     type, nla/svd.hpp:222); computed row-distributed, moved by one
     all-to-all of the m x rank factor when A is 2-D."""
+    if isinstance(A, DistMatrix) and _whole_rows(A):
+        # local rows of U are A's local rows (its cyclic row tiles), all r columns
+        return DistMatrix(U_loc.contiguous(), (m, rank), "MC_MR", comm, A.grid, (A.block[0], max(1, rank)))
     U = DistMatrix(U_loc.contiguous(), (m, rank), "VC_STAR", comm)
     if isinstance(A, DistMatrix) and A.layout not in ("VC_STAR", "VR_STAR"):
         with PROFILER.phase("svd.redistribute"):

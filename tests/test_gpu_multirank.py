@@ -92,3 +92,36 @@ def test_two_rank_randsvd_oneshot_whole_graph(dev):
         assert res[r]["calls"] == 4 and res[r]["whole_graph"], res[r]
         for s in res[r]["s"]:
             torch.testing.assert_close(s, s1.cpu(), rtol=1e-5, atol=0)
+
+
+def _rank_bench(rank, world):
+    import importlib.util
+    import os
+    import types
+    from libskylark_amd.parallel import Comm
+    torch.cuda.set_device(0)
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = types.SimpleNamespace(rows=60000, cols=512, rank=20, iters=2, sketch="FJLT", scaling="strong",
+                              layout="MC_MR", tile_rows=4096, tile_cols=128, grid_rows=0, steps=3, warmup=2)
+    comm = Comm()
+    dev = torch.device("cuda", 0)
+    out = {}
+    for sq in (False, True):
+        r = bench.run(a, comm, dev, "strong", square=sq)
+        out[sq] = (r["grid_pc"], r["orth_err"], r["resid_rel"], r["top_singular_values"])
+    return out
+
+
+def test_two_rank_bench_grids(dev):
+    """bench.py's strong-scaling step on 2 ranks: the 2 x 1 grid (tiles read
+    in place) and the square 1 x 2 grid (one all-to-all) both pass the
+    answer check and agree on the spectrum."""
+    res = run_distributed(_rank_bench, 2, timeout=300)
+    for r in res:
+        assert r[False][0] == 1 and r[True][0] == 2, r
+        for sq in (False, True):
+            assert r[sq][1] < 1e-3 and r[sq][2] < 5e-2, r
+        assert r[False][3] == pytest.approx(r[True][3], rel=1e-3)

@@ -115,6 +115,24 @@ def _svd_mcmr_worker(rank, world):
     assert isinstance(Uw, DistMatrix) and Uw.layout == "MC_MR" and Uw.shape == (n, r)
     assert torch.is_tensor(Vw) and Vw.shape == (m, r)
     torch.testing.assert_close(sw, s0, rtol=1e-9, atol=1e-9)
+    # 8 x 1 grid (bench.py's strong-scaling grid for a tall-skinny A): the
+    # cyclic row tiles are read in place -- only the small (n + k) x k
+    # reductions touch the wire, never a share of A
+    from libskylark_amd.parallel.distmatrix import Grid
+    g81 = Grid.default(comm, world)
+    D8 = DistMatrix.from_global(A, "MC_MR", comm, grid=g81, block=(16, 8))
+    def _no_a2a(*a, **k):
+        raise AssertionError("the 8 x 1 grid must not redistribute A")
+    a2a, comm.all_to_all_v = comm.all_to_all_v, _no_a2a
+    try:
+        U8, s8, V8 = sk.nla.approximate_svd(D8, r, context=sk.Context(7), params=params)
+    finally:
+        comm.all_to_all_v = a2a
+    assert isinstance(U8, DistMatrix) and U8.layout == "MC_MR" and U8.grid is g81 and U8.shape == (m, r)
+    assert U8.local.shape == (D8.local.shape[0], r)
+    torch.testing.assert_close(s8, s0, rtol=1e-9, atol=1e-9)
+    torch.testing.assert_close(V8.abs(), V0.abs(), rtol=1e-7, atol=1e-9)
+    torch.testing.assert_close(U8.to_global().abs(), U0.abs(), rtol=1e-7, atol=1e-9)
 
 
 def test_randsvd_mcmr_world8():
