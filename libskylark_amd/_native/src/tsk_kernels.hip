@@ -205,11 +205,18 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     for (int s = 0; s < GG::GS; ++s) accG[s] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+  // ab & 128: walk the row blocks last-to-first.  Alternate passes over the
+  // same A run in opposite directions, so a pass starts on the rows its
+  // predecessor read last -- still resident in the 256 MB Infinity Cache --
+  // instead of on rows long evicted from it.
+  const bool rev = (ab & 128) != 0;
+  auto phys = [&](int64_t blk) { return rev ? nblocks - 1 - blk : blk; };
+
   // ---- LDS-DMA of one row block (this wave's columns) into buffer `buf`
   auto issue_impl = [&](int64_t blk, int buf, auto nt_c) {
     constexpr bool NT = decltype(nt_c)::value;
     char* region = abuf + (buf * WAVES + w) * GG::REGION;
-    const int64_t r0 = blk * BM;
+    const int64_t r0 = phys(blk) * BM;
 #pragma unroll
     for (int i = 0; i < GG::LPB; ++i) {
       const int byte = i * 1024 + lane * 16;
@@ -304,7 +311,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     SL_STAMP(3)
     {
       constexpr int CPW = GG::KP / WAVES;  // columns reduced per wave
-      const int64_t r0 = blk * BM;
+      const int64_t r0 = phys(blk) * BM;
       const bool full = r0 + BM <= m;        // wave-uniform: only the last block is ragged
       if (lane < CPW * 4) {
         const int col = w * CPW + (lane >> 2), rg = lane & 3;
@@ -755,6 +762,9 @@ SL_API int64_t sl_tsk_fused_workspace(int64_t m, int64_t n, int k) {
 // (bf16-rounded y: for intermediate power iterations, whose W is only
 // orthonormalised), bit2 (4) G in f64 (G is a double*; exact products of the
 // f32 y accumulated in f64 — needs Y stored, i.e. the final pass).
+// bit5 (32) walks the row blocks last-to-first (same results up to the
+// summation order of the per-workgroup slabs; alternating passes then start
+// on rows still held in the Infinity Cache).
 // Default 0 = exact-f32-equivalent W and G.
 SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k,
                              float* W, float* G, float* Y, int64_t ldy, void* ws, int flags, void* stream) {
@@ -774,7 +784,7 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   int rc = SL_ERR_UNSUPPORTED;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
-  g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0);
+  g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0) | ((flags & 32) ? 128 : 0);
   // intermediate power-iteration passes (no Gram, bf16 y): compile-time specialisation
   const bool inter = (flags & 3) == 3 && !Y;
   // final pass whose Gram is taken separately (fp64 Gram of the stored Y)

@@ -325,6 +325,7 @@ class _DevicePlan:
                         and dev.type == "cuda")
         self.eig_status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.use_graph = use_graph
+        self.snake = os.environ.get("SL_SVD_SNAKE", "0") == "1"  # measured: no gain (1.77 vs 1.78 ms)
         self._xm_fn = None
         self._fu_fn = None
         self.g1 = self.g2 = None
@@ -364,8 +365,10 @@ class _DevicePlan:
             with prof.phase("svd.fused_pass"):
                 # every piece writes its own output slot: a piece's capture then
                 # reads its predecessor's graph-owned result, never its own warm-up's
+                # odd passes walk the rows backwards: each pass starts on the
+                # rows the previous one read last (Infinity-Cache resident)
                 self._Wout[i], _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws,
-                                                   zt=self.Zt)
+                                                   zt=self.Zt, reverse=self.snake and i % 2 == 1)
             return self._Wout[i]
         with prof.phase("svd.fused_pass"):
             # fp64 Gram of the f32 Y on the f64 matrix cores, formed inside the
@@ -374,7 +377,7 @@ class _DevicePlan:
             # f32 second Gram only reached ~eps32, at three times the work);
             # W (f64) and G land in the [W; G] buffer the all-reduce takes
             _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True,
-                                   zt=self.Zt, wg_out=self.WG)
+                                   zt=self.Zt, wg_out=self.WG, reverse=self.snake and i % 2 == 1)
         self._WG = self.WG
         self.Y = Y
         return self._WG

@@ -73,7 +73,7 @@ _WS = FusedWorkspace()
 
 def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: bool = True,
                exact: bool = True, ws: torch.Tensor | None = None, gram64: bool = False,
-               zt: torch.Tensor | None = None, wg_out: torch.Tensor | None = None):
+               zt: torch.Tensor | None = None, wg_out: torch.Tensor | None = None, reverse: bool = False):
     """Return ``(W, G, Y)`` with ``Y = A Z``, ``W = A^T Y`` (n x k), ``G = Y^T Y`` (k x k).
 
     W and G are float32 (A bf16/fp32) or float64 (A fp64); Y is float32/64 or
@@ -89,12 +89,14 @@ def fused_pass(A: torch.Tensor, Z: torch.Tensor, keep_y: bool = False, gram: boo
     Native-path extras (randSVD device plan): ``zt`` is ``Z`` already in the
     kernel's bf16 ``k x n`` layout (``Z`` may then be None); ``wg_out`` is an
     f64 ``(n + k) x k`` buffer that receives ``[W; G]`` directly (with
-    ``gram64``), returned as ``W`` and ``G`` views.
+    ``gram64``), returned as ``W`` and ``G`` views; ``reverse`` walks the rows
+    last-to-first (alternating directions over repeated passes re-reads the
+    tail a previous pass left in the Infinity Cache).
     """
     m, n = A.shape
     k = Z.shape[1] if Z is not None else zt.shape[0]
     if _native_ok(A, k):
-        return _fused_native(A, Z, keep_y, gram, exact, ws, gram64, zt, wg_out)
+        return _fused_native(A, Z, keep_y, gram, exact, ws, gram64, zt, wg_out, reverse)
     if Z is None:
         Z = zt.t().float()
     wdt = torch.float64 if A.dtype == torch.float64 else torch.float32
@@ -136,7 +138,7 @@ def f32_workspace_bytes(m: int) -> int:
 
 def _fused_native(A: torch.Tensor, Z: torch.Tensor | None, keep_y: bool, gram: bool = True, exact: bool = True,
                   ws: torch.Tensor | None = None, gram64: bool = False, zt: torch.Tensor | None = None,
-                  wg_out: torch.Tensor | None = None):
+                  wg_out: torch.Tensor | None = None, reverse: bool = False):
     m, n = A.shape
     dev = A.device
     if zt is not None:
@@ -148,7 +150,7 @@ def _fused_native(A: torch.Tensor, Z: torch.Tensor | None, keep_y: bool, gram: b
         k = Z.shape[1]
         Zb = Z.t().to(torch.bfloat16).contiguous()  # Zt layout (k x n)
     g64 = bool(gram64 and gram and keep_y and exact)
-    flags = (0 if gram else 1) | (0 if exact else 2) | (4 if g64 else 0)
+    flags = (0 if gram else 1) | (0 if exact else 2) | (4 if g64 else 0) | (32 if reverse else 0)
     if wg_out is not None:
         if not g64 or wg_out.dtype != torch.float64 or tuple(wg_out.shape) != (n + k, k) or not wg_out.is_contiguous():
             raise ValueError("fused_pass: wg_out needs gram64 and a contiguous f64 (n + k) x k buffer")

@@ -147,6 +147,15 @@ def test_fused_pass_native_gram64(dev, shape):
     W0, _, Y0 = tallskinny.fused_pass(A, Z, keep_y=True, gram=False)
     torch.testing.assert_close(W, W0, rtol=0, atol=0)
     torch.testing.assert_close(Y, Y0, rtol=0, atol=0)
+    # rows walked last-to-first: the same Y bit for bit, W / G up to the order
+    # of the per-workgroup partial sums
+    Wr, Gr2, Yr2 = tallskinny.fused_pass(A, Z, keep_y=True, gram64=True, reverse=True)
+    torch.testing.assert_close(Yr2, Y, rtol=0, atol=0)
+    torch.testing.assert_close(Gr2, G, rtol=1e-12, atol=1e-12 * float(Gr.abs().max()))
+    torch.testing.assert_close(Wr, W, rtol=1e-5, atol=1e-5 * float(W.abs().max()))
+    Wi, _, _ = tallskinny.fused_pass(A, Z, keep_y=False, gram=False, exact=False)
+    Wir, _, _ = tallskinny.fused_pass(A, Z, keep_y=False, gram=False, exact=False, reverse=True)
+    torch.testing.assert_close(Wir, Wi, rtol=1e-5, atol=1e-5 * float(Wi.abs().max()))
 
 
 @pytest.mark.gpu
