@@ -1,6 +1,7 @@
 """Run the fused tall-skinny pass N times (for rocprofv3 --pmc counter runs).
-usage: fused_once.py [flags=0|3] [reps=20] [lda=1000] [gram=1|0]
-(gram=0 with flags=3 is the randSVD inter-pass variant)"""
+usage: fused_once.py [flags=0|3|4] [reps=20] [lda=1000] [gram=1|0]
+(gram=0 with flags=3 is the randSVD inter-pass variant; flags=4 is the final
+pass: Y stored, fp64 in-pass Gram)"""
 from __future__ import annotations
 
 import os
@@ -29,12 +30,14 @@ def main():
     A = buf[:, :n]
     Zt = (torch.randn(k, n, device=dev) / 30).to(torch.bfloat16)
     W = torch.empty(n, k, device=dev)
-    G = torch.empty(k, k, device=dev)
+    final = flags == 4
+    G = torch.empty(k, k, device=dev, dtype=torch.float64 if final else torch.float32)
+    Y = torch.empty(m, k, device=dev) if final else None
     ws = torch.empty(int(lib.sl_tsk_fused_workspace(m, n, k)), dtype=torch.uint8, device=dev)
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     for _ in range(reps):
         _lib.call("sl_tsk_fused_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zt), k, _lib.ptr(W), _lib.ptr(G) if gram else None,
-                  None, 0, _lib.ptr(ws), flags, st)
+                  _lib.ptr(Y) if final else None, k if final else 0, _lib.ptr(ws), flags, st)
     torch.cuda.synchronize()
     print("ok", flags, reps, ld)
 
