@@ -344,7 +344,8 @@ class _DevicePlan:
         A = self.Aref()
         if i == 0:
             self.status.zero_()
-            self.eig_status.zero_()
+            if self.dev_eig:
+                self.eig_status.zero_()
             if self.fjlt_scale is not None:
                 from ..ops import fut as F
                 with prof.phase("svd.sketch"):
