@@ -85,7 +85,7 @@ class Comm:
         """The one-shot path for a small device SUM operand, or None (opt-in,
         parallel/oneshot.py; set up collectively on first use)."""
         from . import oneshot
-        if not oneshot.enabled() or not t.is_cuda:
+        if not oneshot.enabled(self) or not t.is_cuda:
             return None
         os_ = getattr(self, "_oneshot", None)
         if os_ is None:

@@ -11,10 +11,12 @@ every rank, capturable in a hipGraph (``_native/src/oneshot_kernels.hip``).
 Reference reduction sites: ``base/inner.hpp:22,84,170`` (MPI_Allreduce of
 column norms / dots), ``nla/svd.hpp`` (El::AllReduce of the small factors).
 
-Opt-in (``SL_ONESHOT=1`` or :func:`enable`): :class:`~.comm.Comm` then routes
-f32 / f64 device all-reduces of at most ``cap`` bytes here and everything
-else to RCCL.  Setup is collective; if any rank cannot export or map the
-buffers, every rank stays on RCCL.
+On by default for RCCL communicators (``SL_ONESHOT=auto``; ``1`` forces it,
+``0`` disables it): :class:`~.comm.Comm` then routes f32 / f64 device
+all-reduces of at most ``cap`` bytes here and everything else to RCCL.
+Setup is collective and ends with a self-test (exact sums over both
+generation buffers); if any rank cannot export or map the buffers, or the
+test fails or times out anywhere, every rank stays on RCCL.
 """
 from __future__ import annotations
 
@@ -90,6 +92,31 @@ class OneShotAllReduce:
         self.err = torch.zeros(1, dtype=torch.int32, device=self.dev)
         # the collective must not start before every peer has mapped this buffer
         comm.barrier()
+        # self-test on this hardware before any caller relies on the path: both
+        # generation buffers, f32 and f64, rank-dependent operands, exact
+        # expected sums; any mismatch or timed-out wait on any rank -> every
+        # rank falls back to RCCL
+        good = self._self_test()
+        self.ok = all(comm.all_gather_object(bool(good)))
+        if not self.ok:
+            self.close()
+
+    def _self_test(self, timeout_s: float = 5.0) -> bool:
+        try:
+            p = self.p
+            for it, dt in enumerate((torch.float64, torch.float32, torch.float64, torch.float32)):
+                n = 257 + 64 * it
+                base = torch.arange(1, n + 1, dtype=dt, device=self.dev)
+                x = base * float(self.rank + 1)
+                _lib.call("sl_oneshot_allreduce", _lib.ptr(x), x.numel(), _lib.dtype_code(x.dtype), self.rank, p,
+                          _lib.ptr(self.bases), self.cap, _lib.ptr(self.state), _lib.ptr(self.err), float(timeout_s),
+                          vp(_lib.stream_of(x)))
+                want = base * float(p * (p + 1) // 2)
+                if not torch.equal(x, want) or int(self.err.item()):
+                    return False
+            return True
+        except Exception:  # noqa: BLE001 - any failure: stay on RCCL
+            return False
 
     def fits(self, t: torch.Tensor) -> bool:
         return (self.ok and t.is_cuda and t.device == self.dev and t.dtype in (torch.float32, torch.float64)
@@ -122,16 +149,24 @@ class OneShotAllReduce:
         self.ok = False
 
 
-_ENABLED = os.environ.get("SL_ONESHOT", "0") == "1"
+# "1": always (also for gloo process groups over CUDA tensors, e.g. several
+# ranks sharing one GPU in tests); "auto" (default): RCCL process groups, i.e.
+# one rank per GPU -- each communicator still self-tests its buffers first;
+# "0": never
+_MODE = os.environ.get("SL_ONESHOT", "auto")
+_ENABLED = _MODE == "1"
 
 
-def enabled() -> bool:
-    return _ENABLED
+def enabled(comm=None) -> bool:
+    if _ENABLED:
+        return True
+    return _MODE == "auto" and comm is not None and getattr(comm, "backend", None) == "nccl"
 
 
 def enable(flag: bool = True):
     """Route small device all-reduces of every :class:`Comm` through the
     one-shot path (buffers are set up lazily, collectively, per communicator
     on its first eligible all-reduce)."""
-    global _ENABLED
+    global _ENABLED, _MODE
     _ENABLED = bool(flag)
+    _MODE = "1" if flag else "0"
