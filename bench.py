@@ -133,12 +133,13 @@ def run(a, comm, dev, scaling, square=False):
     comm.all_reduce_max(t)
     ms = float(t.item()) / steps * 1e3
     orth, resid = check_answer(A, U, s, V, comm)
+    red = "one-shot IPC all-reduces" if getattr(comm, "_oneshot", None) else "RCCL all-reduces"
     if grid is not None:
         how = "tiles read in place (whole rows per rank)" if grid.pc == 1 else "one all-to-all to [VC,*]"
         par = f"2-D block-cyclic [MC,MR] {grid.pr}x{grid.pc} grid, tile {block[0]}x{block[1]}, " \
-              f"{how} + RCCL all-reduces"
+              f"{how} + {red}"
     else:
-        par = f"dp{N} ([VC,*] row blocks, RCCL all-reduce)"
+        par = f"dp{N} ([VC,*] row blocks, {red})"
     return {
         "m": m, "n": n, "ms": ms, "gbs": m * n * 2 / (ms / 1e3) / 1e9, "steps": steps, "warmup": warmup,
         "parallelism": par, "orth_err": orth, "resid_rel": resid,
