@@ -19,6 +19,7 @@
 //     accumulated in LDS with ds_add_f32 / ds_add_f64 (value dtype), then one
 //     coalesced store.
 #include "sl_common.hpp"
+#include <stdlib.h>
 #include <type_traits>
 
 // pval[p] = val[perm[p]] (bucket-ordered signs, built once per sketch): the
@@ -249,7 +250,14 @@ SL_API int sl_hash_csr_colwise2(const int64_t* rowptr, const void* col, int idx3
   int64_t CW = m < cwmax ? m : cwmax;
   dim3 grid((unsigned)((m + CW - 1) / CW), (unsigned)S);
   size_t lds = (size_t)CW * esz;
-#define SL_CSR(IT, VT, G, DET) k_hash_csr_col<IT, VT, G, 4, DET><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, (const VT*)pval, (VT*)out, ldo, m, CW, row_offset, vmax, wmax)
+  static int urows = -1;   // rows in flight per lane group (SL_CWT_U: 4, 8 or 16; tuning)
+  if (urows < 0) {
+    const char* e = getenv("SL_CWT_U");
+    urows = e ? atoi(e) : 8;
+  }
+#define SL_CSR_U(IT, VT, G, DET, U) k_hash_csr_col<IT, VT, G, U, DET><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, (const VT*)pval, (VT*)out, ldo, m, CW, row_offset, vmax, wmax)
+#define SL_CSR(IT, VT, G, DET) \
+  { if (urows >= 16) SL_CSR_U(IT, VT, G, DET, 16); else if (urows >= 8) SL_CSR_U(IT, VT, G, DET, 8); else SL_CSR_U(IT, VT, G, DET, 4); }
 #define SL_CSR_G(IT, VT, DET)                              \
   switch (group) {                                         \
     case 1: SL_CSR(IT, VT, 1, DET); break;                 \
@@ -266,6 +274,7 @@ SL_API int sl_hash_csr_colwise2(const int64_t* rowptr, const void* col, int idx3
 #undef SL_CSR_D
 #undef SL_CSR_G
 #undef SL_CSR
+#undef SL_CSR_U
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
