@@ -34,6 +34,7 @@
 //   * XCD-aware tile order: W is split over the 8 XCDs (each XCD's slice of W
 //     stays L2 resident while A streams past), see the kernel's mapping.
 #include "sl_common.hpp"
+#include <stdlib.h>
 
 namespace {
 
@@ -341,10 +342,250 @@ k_feat_gemm(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int6
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile variant for row-major output (the feature-map / dense-sketch hot
+// path): 256 x 128 output tile per 512-thread workgroup (4 x 2 waves of
+// 64 x 64, the same MFMA block per wave as k_feat_gemm), one workgroup per CU.
+//   * operands move HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB
+//     per wave-instruction) into a 3-stage ring, two K-slices in flight while
+//     the third is consumed: no register staging, ONE s_barrier per K-slice
+//     (the waves consume each other's DMA'd rows, so the barrier both
+//     publishes slice kt and retires slot kt-1 for the next DMA);
+//   * the LDS image uses the same k-chunk ^ row-bit-2 swizzle as lds_swz,
+//     applied through the DMA's SOURCE address (the DMA writes each wave-
+//     instruction's 1 KiB contiguously);
+//   * 256-row A tiles halve the A traffic per feature tile against 128 x 128,
+//     and the XCD map is 2 (rows) x 4 (features): XCD (i, j) owns the feature
+//     tiles of quarter j (W slice L2-resident) and the row tiles of parity i,
+//     so A is fetched by 4 XCDs (not 8) and W by 2.
+constexpr int L_BM = 256, L_BN = 128, L_NT = 512, L_NBUF = 3;
+
+__device__ __forceinline__ void fg_glds16(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+template <bool ALO, bool WLO, int EPI, typename OutT>
+__global__ void __launch_bounds__(L_NT, 1)
+k_feat_gemm_l(const bf16_t* __restrict__ Ahi, const bf16_t* __restrict__ Alo, int64_t M, int64_t K, int64_t lda,
+              const bf16_t* __restrict__ Whi, const bf16_t* __restrict__ Wlo, int64_t Nf, int64_t ldw,
+              const float* __restrict__ scales, const float* __restrict__ shifts, float outscale,
+              OutT* __restrict__ out, int64_t ldo, int ntm, int ntn, const float* __restrict__ rowterm, float p0) {
+  constexpr int APL = L_BM * BK;                        // bf16 elements per A plane per stage
+  constexpr int WPL = L_BN * BK;
+  constexpr int STAGE = APL * (ALO ? 2 : 1) + WPL * (WLO ? 2 : 1);
+  constexpr int EPI_LD = 64 + 4;
+  constexpr int EPI_ELEMS = 8 * 64 * EPI_LD * 2;        // 8 waves' 64 x 64 f32 blocks, as bf16 elements
+  constexpr int LDS_ELEMS = (L_NBUF * STAGE > EPI_ELEMS) ? L_NBUF * STAGE : EPI_ELEMS;
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds_l[];
+  static_assert(LDS_ELEMS * 2 <= 160 * 1024, "LDS budget");
+
+  // ---- tile of this workgroup (XCD b % 8 = (i, j): row parity i, feature quarter j)
+  const int b = blockIdx.x, xcd = b & 7, li = b >> 3;
+  int tm, tn;
+  {
+    const int nq = ntn >> 2;                 // feature tiles per quarter (host guarantees ntn % 4 == 0)
+    const int xi = xcd & 1, xj = xcd >> 1;
+    const int mi = li / nq, nj = li - mi * nq;
+    tm = 2 * mi + xi;
+    tn = xj * nq + nj;
+    if (tm >= ntm) return;
+  }
+  const int64_t row0 = (int64_t)tm * L_BM;
+  const int64_t col0 = (int64_t)tn * L_BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;             // 4 x 2 waves, 64 x 64 each
+  const int nk = (int)((K + BK - 1) / BK);
+
+  // ---- DMA plan: a plane of R rows x 32 k is R/16 wave-instructions of 1 KiB
+  // (16 rows x 64 B); lane l fills LDS row l/4, slot l%4 of its instruction's
+  // block, i.e. fetches global k-chunk (l%4) ^ swizzle(row).
+  const int drow = lane >> 2;                           // row within the 16-row block
+  const int dchunk = (lane & 3) ^ ((drow >> 1) & 2);    // global k-chunk for this lane's LDS slot
+  // A: 16 blocks per plane over 8 waves -> 2 per wave; W: 8 blocks -> 1 per wave
+  const bf16_t* pa[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = wave + 8 * i;
+    int64_t gr = row0 + blk * 16 + drow;
+    gr = gr < M ? gr : M - 1;
+    pa[i] = Ahi + gr * lda + dchunk * 8;
+  }
+  const bf16_t* pw = Whi + (col0 + wave * 16 + drow) * ldw + dchunk * 8;
+  const int64_t alo_off = ALO ? (Alo - Ahi) : 0;
+  const int64_t wlo_off = WLO ? (Wlo - Whi) : 0;
+  constexpr int NDMA = 2 * (ALO ? 2 : 1) + (WLO ? 2 : 1);   // DMA instructions per wave per stage
+
+  auto lds_addr = [&](int elem) -> unsigned {
+    return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)(lds_l + elem));
+  };
+  auto issue = [&](int kt) {
+    const int slot = kt % L_NBUF;
+    const int base = slot * STAGE;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int blk = wave + 8 * i;
+      fg_glds16(pa[i] + k0, lds_addr(base + blk * 16 * BK));
+      if constexpr (ALO) fg_glds16(pa[i] + alo_off + k0, lds_addr(base + APL + blk * 16 * BK));
+    }
+    const int wb = base + APL * (ALO ? 2 : 1);
+    fg_glds16(pw + k0, lds_addr(wb + wave * 16 * BK));
+    if constexpr (WLO) fg_glds16(pw + wlo_off + k0, lds_addr(wb + WPL + wave * 16 * BK));
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int frag_off = (lane & 15) * BK + lds_swz(lane & 15, (lane >> 4) * 8);
+
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // own DMAs of slice kt landed (slice kt+1's may still be in flight) ...
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ... and every wave's: slice kt is readable, slot (kt-1)%3 is free
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2);
+    const int base = (kt % L_NBUF) * STAGE;
+    const bf16_t* sAh = lds_l + base;
+    const bf16_t* sAl = lds_l + base + APL;
+    const bf16_t* sWh = lds_l + base + APL * (ALO ? 2 : 1);
+    const bf16_t* sWl = sWh + WPL;
+    bf16x8 ah[4], al[4], wh[4], wl[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int o = (wc * 64 + cb * 16) * BK + frag_off;
+      wh[cb] = *(const bf16x8*)&sWh[o];
+      if (WLO) wl[cb] = *(const bf16x8*)&sWl[o];
+    }
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const int o = (wr * 64 + rb * 16) * BK + frag_off;
+      ah[rb] = *(const bf16x8*)&sAh[o];
+      if (ALO) al[rb] = *(const bf16x8*)&sAl[o];
+    }
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+        acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rb], wh[cb], acc[rb][cb], 0, 0, 0);
+    if (ALO) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rb], wh[cb], acc[rb][cb], 0, 0, 0);
+    }
+    if (WLO) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rb], wl[cb], acc[rb][cb], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue: stage each wave's 64 x 64 block (after the map), then
+  // row-contiguous 16-B stores
+  __syncthreads();
+  float* blkp = (float*)lds_l + wave * 64 * EPI_LD;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int64_t f = col0 + wc * 64 + cb * 16 + (lane & 15);
+    const float sc = (scales && f < Nf) ? scales[f] : 1.f;
+    const float sh = (shifts && f < Nf) ? shifts[f] : 0.f;
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float rt = 0.f;
+        if constexpr (EPI == EPI_GAUSS) {
+          const int64_t r = row0 + wr * 64 + rb * 16 + 4 * (lane >> 4) + e;
+          rt = (rowterm && r < M) ? rowterm[r] : 0.f;
+        }
+        blkp[(rb * 16 + 4 * (lane >> 4) + e) * EPI_LD + cb * 16 + (lane & 15)] =
+            epilogue<EPI>(acc[rb][cb][e], sc, sh, outscale, rt, p0);
+      }
+  }
+  __syncthreads();
+  const int64_t rbase = row0 + wr * 64;
+  const int64_t fbase = col0 + wc * 64;
+  const bool fullc = fbase + 64 <= Nf && ((ldo & 3) == 0);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 64 + lane;
+    const int rr = idx >> 4, c4 = (idx & 15) * 4;
+    const int64_t r = rbase + rr;
+    if (r >= M) continue;
+    const f32x4 v = *(const f32x4*)&blkp[rr * EPI_LD + c4];
+    OutT* p = out + r * ldo + fbase + c4;
+    if (fullc) {
+      if constexpr (sizeof(OutT) == 4) {
+        *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        *(uint2*)p = make_uint2(f2bf_bits(v[0]) | (f2bf_bits(v[1]) << 16), f2bf_bits(v[2]) | (f2bf_bits(v[3]) << 16));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (fbase + c4 + e < Nf) p[e] = cvt_out<OutT>(v[e]);
+    }
+  }
+}
+
+template <bool ALO, bool WLO, int EPI, typename OutT>
+int launch_large(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda, const bf16_t* Whi,
+                 const bf16_t* Wlo, int64_t Nf, int64_t ldw, const float* sc, const float* sh, float outscale,
+                 OutT* out, int64_t ldo, hipStream_t s, const float* rt, float p0) {
+  const int ntm = (int)((M + L_BM - 1) / L_BM), ntn = (int)((Nf + L_BN - 1) / L_BN);
+  constexpr int APL = L_BM * BK, WPL = L_BN * BK;
+  constexpr int STAGE = APL * (ALO ? 2 : 1) + WPL * (WLO ? 2 : 1);
+  constexpr int EPI_ELEMS = 8 * 64 * (64 + 4) * 2;
+  constexpr size_t LDS = (size_t)((L_NBUF * STAGE > EPI_ELEMS) ? L_NBUF * STAGE : EPI_ELEMS) * 2;
+  auto kern = k_feat_gemm_l<ALO, WLO, EPI, OutT>;
+  static bool attr = false;
+  if (!attr) {
+    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
+    attr = true;
+  }
+  const unsigned grid = (unsigned)(8 * ((ntm + 1) / 2) * (ntn / 4));
+  kern<<<grid, L_NT, LDS, s>>>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale, out, ldo, ntm, ntn, rt, p0);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+int g_fg_large = -1;   // SL_FG_LARGE: 0 off, 1 on (default)
+
 template <bool ALO, bool WLO, int EPI>
 int launch_out(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda, const bf16_t* Whi,
                const bf16_t* Wlo, int64_t Nf, int64_t ldw, const float* sc, const float* sh, float outscale,
                void* out, int out_dtype, int64_t ldo, int out_t, hipStream_t s, const float* rt, float p0) {
+  if (g_fg_large < 0) {
+    const char* e = getenv("SL_FG_LARGE");
+    g_fg_large = e ? atoi(e) : 1;
+  }
+  // large tiles: row-major output, the feature tiles split into 4 XCD quarters,
+  // and W padded to whole 128-row tiles (the host pads to 128)
+  if (g_fg_large && !out_t && ((Nf + L_BN - 1) / L_BN) % 4 == 0 && M >= L_BM) {
+    if (out_dtype == SL_F32)
+      return launch_large<ALO, WLO, EPI, float>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale,
+                                                 (float*)out, ldo, s, rt, p0);
+    if (out_dtype == SL_BF16)
+      return launch_large<ALO, WLO, EPI, bf16_t>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale,
+                                                  (bf16_t*)out, ldo, s, rt, p0);
+  }
   const int ntm = (int)((M + BM - 1) / BM), ntn = (int)((Nf + BN - 1) / BN);
   const int T = ntm * ntn, per = (T + 7) / 8;
   const unsigned grid = (unsigned)(8 * per);
@@ -434,6 +675,12 @@ SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int6
                            void* out, int out_dtype, int64_t ldo, int out_t, void* stream) {
   return sl_feature_gemm2(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, epi, out, out_dtype, ldo,
                           out_t, nullptr, 0.f, stream);
+}
+
+// tuning / testing hook: 1 = large-tile variant where it applies (default), 0 = 128 x 128 only
+SL_API int sl_fg_set_large(int on) {
+  g_fg_large = on ? 1 : 0;
+  return SL_OK;
 }
 
 // hi / lo planes of width wpad (zero padded past K) with row stride ldp >= wpad

@@ -53,6 +53,40 @@ def test_feature_gemm_matches_fp64(dev, adt, dim, epi):
     assert err < tol, (err, tol)
 
 
+@pytest.mark.parametrize("adt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(1000, 301, 500), (2048, 512, 1024), (777, 64, 4096)])
+@pytest.mark.parametrize("epi", [F.EPI_NONE, F.EPI_COS])
+def test_feature_gemm_large_tiles_match_fp64(dev, adt, shape, epi):
+    """256 x 128-tile LDS-DMA variant (row-major output, feature tiles in
+    multiples of 4 x 128): ragged rows / features / K against fp64, and equal
+    to the 128 x 128 kernel's result (SL_FG_LARGE=0 path) up to summation order."""
+    torch.manual_seed(3)
+    M, K, NF = shape
+    A = torch.randn(M, K)
+    W = torch.randn(NF, K) / math.sqrt(K)
+    sc = torch.rand(NF) + 0.5
+    sh = torch.rand(NF) * 2 * math.pi
+    Ad = A.to(dev, adt)
+    Wd = F.SplitW(W.to(dev))
+    kw = dict(scales=sc if epi == F.EPI_COS else None, shifts=sh if epi == F.EPI_COS else None, outscale=0.7, epi=epi)
+    out = F.feature_gemm(Ad, Wd, 1, **kw)
+    ref = _ref(Ad, W, 1, sc, sh, 0.7, epi)
+    mag = Ad.double().cpu().abs() @ W.abs().double().t()
+    tol = 4e-5 * float(mag.max()) + 2e-6
+    assert (out.double().cpu() - ref).abs().max().item() < tol
+    import ctypes
+    from libskylark_amd.ops import _lib
+    lib = _lib.require()
+    # same launch through the 128 x 128 kernel
+    try:
+        lib.sl_fg_set_large.argtypes = [ctypes.c_int]
+        lib.sl_fg_set_large(0)
+        out_small = F.feature_gemm(Ad, Wd, 1, **kw)
+    finally:
+        lib.sl_fg_set_large(1)
+    assert (out.double().cpu() - out_small.double().cpu()).abs().max().item() < tol
+
+
 def test_feature_gemm_transposed_view_and_unaligned(dev):
     torch.manual_seed(1)
     M, K, NF = 700, 77, 130
