@@ -63,3 +63,40 @@ def _symsvd_worker(rank, world):
 @pytest.mark.parametrize("world", [2, 4])
 def test_symmetric_svd_distributed(world):
     run_distributed(_symsvd_worker, world)
+
+
+def _lsrn_worker(rank, world):
+    import libskylark_amd as sk
+    from libskylark_amd.algorithms.krylov import KrylovIterParams
+    from libskylark_amd.parallel.comm import world as W
+    from libskylark_amd.parallel.distmatrix import DistMatrix
+    comm = W()
+    g = torch.Generator().manual_seed(5)
+    m, n = 1600, 12
+    U, _ = torch.linalg.qr(torch.randn(m, n, generator=g, dtype=torch.float64))
+    V, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    A = (U * torch.logspace(0, 3, n, dtype=torch.float64)) @ V.t()       # cond 1e3
+    b = torch.randn(m, 2, generator=g, dtype=torch.float64)
+    ref = torch.linalg.lstsq(A, b).solution
+    D = DistMatrix.from_global(A, "VC_STAR", comm)
+    Bd = DistMatrix.from_global(b, "VC_STAR", comm)
+    p = KrylovIterParams(tolerance=1e-12, iter_lim=300)
+    comm.bytes_sent = 0
+    xl = sk.nla.lsrn_least_squares(D, Bd, sk.Context(2), params=p)
+    # A is never gathered: the traffic is the t x n sketch reduction plus
+    # n-sized Krylov reductions, well under one rank's share of A
+    assert comm.bytes_sent < A.numel() * 8 // world, comm.bytes_sent
+    x1 = sk.nla.lsrn_least_squares(A, b, sk.Context(2), params=p)
+    for x in (xl, x1):
+        x = x.to_global() if hasattr(x, "to_global") else x
+        r = float((A @ x - b).norm() / (A @ ref - b).norm())
+        assert r < 1 + 1e-8, r
+    return True
+
+
+def test_lsrn_distributed_world8():
+    """LSRN (JLT sketch of the row-sharded A -> one t x n all-reduce, QR/SVD
+    preconditioner, preconditioned Krylov with all-reduced n-vectors) on 8
+    ranks reaches the least-squares optimum like the one-process solve
+    (reference accelerated_linearl2_regression_solver_Elemental.hpp:531-616)."""
+    assert all(run_distributed(_lsrn_worker, 8))
