@@ -193,6 +193,75 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One Householder step j of the register-resident tridiagonalisation (wave 0,
+// lane i holds row i): reflector from column j, p = A v, w = p - (v.p) v,
+// A -= 2 (v w^T + w v^T) on the trailing columns only.
+template <int K, int J>
+__device__ __forceinline__ void tri_step(double (&arow)[K], int i, double safmin, double* vsh, double* wsh,
+                                         double (*refl)[K + 1], double* dd, double* ee) {
+  constexpr int c0 = (J + 1) & ~1;               // first active column, 16-B aligned
+  double xi = arow[J];
+  const double ajj = xi;                         // lane J: its diagonal (final now)
+  xi = (i > J) ? xi : 0.0;
+  const double s2 = wave_sum_d(xi * xi);
+  const double x0 = lane_d(xi, J + 1);
+  double vi = 0.0, alpha = x0;
+  if (s2 - x0 * x0 > safmin * 4.0) {
+    alpha = x0 >= 0.0 ? -sqrt(s2) : sqrt(s2);
+    const double vn = sqrt(2.0 * (s2 - alpha * x0));
+    vi = (xi - (i == J + 1 ? alpha : 0.0)) / vn;
+    vi = (i > J) ? vi : 0.0;
+  }
+  if (i == J) { dd[J] = ajj; ee[J] = alpha; }
+  if (i < K) {
+    vsh[i] = vi;
+    refl[i][J] = vi;
+  }
+  wave_lds_sync();
+  // the whole broadcast vector in registers first (one LDS round trip per
+  // vector, not one per pair of elements)
+  double vv[K];
+#pragma unroll
+  for (int c = c0; c < K; c += 2) {
+    const double2 t = *(const double2*)(vsh + c);
+    vv[c] = t.x;
+    vv[c + 1] = t.y;
+  }
+  double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+  for (int c = c0; c < K; c += 2) {
+    p0 = fma(arow[c], vv[c], p0);
+    p1 = fma(arow[c + 1], vv[c + 1], p1);
+  }
+  const double p = (i > J) ? p0 + p1 : 0.0;
+  const double Kd = wave_sum_d(vi * p);
+  const double wi = (i > J) ? p - Kd * vi : 0.0;
+  if (i < K) wsh[i] = wi;
+  wave_lds_sync();
+  double ww[K];
+#pragma unroll
+  for (int c = c0; c < K; c += 2) {
+    const double2 t = *(const double2*)(wsh + c);
+    ww[c] = t.x;
+    ww[c + 1] = t.y;
+  }
+  const double v2 = 2.0 * vi, w2 = 2.0 * wi;
+#pragma unroll
+  for (int c = c0; c < K; ++c) arow[c] = fma(-v2, ww[c], fma(-w2, vv[c], arow[c]));
+  wave_lds_sync();   // vsh / wsh are rewritten next step
+}
+
+template <int K, int J>
+__device__ __forceinline__ void tri_steps(double (&arow)[K], int i, int k, double safmin, double* vsh, double* wsh,
+                                          double (*refl)[K + 1], double* dd, double* ee) {
+  if constexpr (J + 2 < K) {
+    if (J + 2 < k) {
+      tri_step<K, J>(arow, i, safmin, vsh, wsh, refl, dd, ee);
+      tri_steps<K, J + 1>(arow, i, k, safmin, vsh, wsh, refl, dd, ee);
+    }
+  }
+}
+
 template <int K, bool ST>
 __global__ void __launch_bounds__(NT)
 k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double* __restrict__ out, int want_sqrt,
@@ -200,9 +269,8 @@ k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double*
   __shared__ double refl[K][K + 1];     // Householder vectors (column j = step j)
   __shared__ __attribute__((aligned(16))) double vsh[K], wsh[K];
   __shared__ double dd[K], ee[K], e2[K];
-  __shared__ double lo_s[K], hi_s[K], lam[K];
+  __shared__ double lam[K];
   __shared__ double T1[K][TRV + 1];     // per-vector pivots, then the vector itself
-  __shared__ int cnt_s[NT];
   __shared__ double bnd[2];
   __shared__ int bad_s, clus_s;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -224,52 +292,11 @@ k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double*
       arow[c] = v;
     }
     if (nf) bad_s = 1;
-    for (int j = 0; j + 2 < k; ++j) {
-      double xi = 0.0;
-#pragma unroll
-      for (int c = 0; c < K; ++c)
-        if (c == j) { xi = arow[c]; }
-      const double ajj = xi;                      // lane j: its diagonal (final now)
-      xi = (i > j) ? xi : 0.0;
-      const double s2 = wave_sum_d(xi * xi);
-      const double x0 = lane_d(xi, j + 1);
-      double vi = 0.0, alpha = x0;
-      if (s2 - x0 * x0 > safmin * 4.0) {
-        alpha = x0 >= 0.0 ? -sqrt(s2) : sqrt(s2);
-        const double vn = sqrt(2.0 * (s2 - alpha * x0));
-        vi = (xi - (i == j + 1 ? alpha : 0.0)) / vn;
-        vi = (i > j) ? vi : 0.0;
-      }
-      if (i == j) { dd[j] = ajj; ee[j] = alpha; }
-      if (i < K) {
-        vsh[i] = vi;
-        refl[i][j] = vi;
-      }
-      wave_lds_sync();
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-#pragma unroll
-      for (int c = 0; c < K; c += 4) {
-        const double2 va = *(const double2*)(vsh + c);
-        const double2 vb = *(const double2*)(vsh + c + 2);
-        p0 = fma(arow[c], va.x, p0);
-        p1 = fma(arow[c + 1], va.y, p1);
-        p2 = fma(arow[c + 2], vb.x, p2);
-        p3 = fma(arow[c + 3], vb.y, p3);
-      }
-      double p = (i > j) ? (p0 + p1) + (p2 + p3) : 0.0;
-      const double Kd = wave_sum_d(vi * p);
-      const double wi = (i > j) ? p - Kd * vi : 0.0;
-      if (i < K) wsh[i] = wi;
-      wave_lds_sync();
-#pragma unroll
-      for (int c = 0; c < K; c += 2) {
-        const double2 vv = *(const double2*)(vsh + c);
-        const double2 ww = *(const double2*)(wsh + c);
-        arow[c] -= 2.0 * (vi * ww.x + wi * vv.x);
-        arow[c + 1] -= 2.0 * (vi * ww.y + wi * vv.y);
-      }
-      wave_lds_sync();   // vsh / wsh are rewritten next step
-    }
+    // steps instantiated per compile-time j (template recursion, a uniform
+    // exit at k): the column j and the active range c >= j + 1 are static
+    // register indices, so arow stays in registers and each step only touches
+    // the trailing columns
+    tri_steps<K, 0>(arow, i, k, safmin, vsh, wsh, refl, dd, ee);
     // the last two diagonal entries and the last off-diagonal one
     double dl = 0.0, el = 0.0;
 #pragma unroll
@@ -301,50 +328,65 @@ k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double*
 
   // ---- 2. multisection for the nt largest eigenvalues ----------------------
   const int nt = r < k ? r + 1 : k;
-  const int G = NT / nt;
   double pivmin = 1.0;
   for (int i = 0; i + 1 < k; ++i) pivmin = fmax(pivmin, e2[i]);
   pivmin *= safmin;
   const double tnorm = fmax(fabs(bnd[0]), fabs(bnd[1]));
   const double atol = 2.0 * eps * tnorm + 2.0 * pivmin;
-  if (tid < nt) { lo_s[tid] = bnd[0]; hi_s[tid] = bnd[1]; }
-  __syncthreads();
-  const int tg = tid / G, g = tid - tg * G;
+  // One small lane group per wanted eigenvalue (8 lanes, 4 when more than 32
+  // are wanted), groups never straddle a wave: each round every lane takes
+  // one multisection point, and the group's new bracket is a 3-step DPP
+  // max / min over its lanes -- no LDS, no workgroup barrier; the waves run
+  // their rounds independently until all of their brackets are converged.
+  const int GL = nt <= NT / 8 ? 8 : 4;
+  const int tg = tid / GL, g = tid - tg * GL;
+  const bool act = tg < nt;
+  const int idx = k - 1 - tg;        // ascending index of this group's eigenvalue
+  // T in registers for the whole multisection (the Sturm recurrence is one
+  // dependent chain; LDS reads inside it exposed their latency every step)
+  double dR[K], e2R[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    dR[i] = i < k ? dd[i] : 0.0;
+    e2R[i] = (i + 1 < k) ? e2[i] : 0.0;
+  }
+  const double gfrac = 1.0 / (double)(GL + 1);
+  double lo = bnd[0], hi = bnd[1];
   for (int round = 0; round < 80; ++round) {
-    if (tg < nt) {
-      const double lo = lo_s[tg], hi = hi_s[tg];
-      const double x = lo + (hi - lo) * (double)(g + 1) / (double)(G + 1);
-      double q = dd[0] - x;
+    const bool conv = !act || (hi - lo) <= fmax(atol, 2.0 * eps * fmax(fabs(lo), fabs(hi)));
+    if (__all(conv)) break;
+    if (act) {
+      const double x = lo + (hi - lo) * (double)(g + 1) * gfrac;
+      double q = dR[0] - x;
       if (fabs(q) < pivmin) q = -pivmin;
       int c = q < 0.0;
 #pragma unroll
       for (int i = 1; i < K; ++i) {
         if (i < k) {
-          q = (dd[i] - x) - e2[i - 1] / q;
+          // e2 / q by v_rcp_f64 + one Newton step (~full precision; only
+          // the sign of q enters the count)
+          double y = __builtin_amdgcn_rcp(q);
+          y = fma(fma(-q, y, 1.0), y, y);
+          q = (dR[i] - x) - e2R[i - 1] * y;
           if (fabs(q) < pivmin) q = -pivmin;
           c += q < 0.0;
         }
       }
-      cnt_s[tid] = c;
-    }
-    __syncthreads();
-    int ok = 1;
-    if (tid < nt) {
-      const int idx = k - 1 - tid;   // ascending index of the tid-th largest
-      const double lo = lo_s[tid], hi = hi_s[tid];
-      double nlo = lo, nhi = hi;
-      for (int gg = 0; gg < G; ++gg) {
-        const double x = lo + (hi - lo) * (double)(gg + 1) / (double)(G + 1);
-        if (cnt_s[tid * G + gg] <= idx) nlo = fmax(nlo, x);
-        else nhi = fmin(nhi, x);
+      // fewer than idx + 1 eigenvalues below x: x is a lower bound
+      double nlo = c <= idx ? x : lo, nhi = c <= idx ? hi : x;
+      nlo = fmax(nlo, dppd<0xB1>(nlo));
+      nhi = fmin(nhi, dppd<0xB1>(nhi));
+      nlo = fmax(nlo, dppd<0x4E>(nlo));
+      nhi = fmin(nhi, dppd<0x4E>(nhi));
+      if (GL == 8) {
+        nlo = fmax(nlo, dppd<0x141>(nlo));
+        nhi = fmin(nhi, dppd<0x141>(nhi));
       }
-      lo_s[tid] = nlo;
-      hi_s[tid] = nhi;
-      ok = (nhi - nlo) <= fmax(atol, 2.0 * eps * fmax(fabs(nlo), fabs(nhi)));
+      lo = nlo;
+      hi = nhi;
     }
-    if (__syncthreads_and(ok)) break;
   }
-  if (tid < nt) lam[tid] = 0.5 * (lo_s[tid] + hi_s[tid]);
+  if (act && g == 0) lam[tg] = 0.5 * (lo + hi);
   __syncthreads();
   if constexpr (ST) { if (tid == 0) stamps[2] = clock64(); }
 
@@ -357,50 +399,81 @@ k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double*
       const double gap = fmin(v > 0 ? lam[v - 1] - l : 1e300, v + 1 < nt ? l - lam[v + 1] : 1e300);
       if (!(gap > 1e-14 * tnorm)) atomicOr(&bad_s, 1);   // numerically repeated
       if (gap < gtol) atomicOr(&clus_s, 1);
-      // backward pivots D-_i (slot i)
-      double dm = dd[k - 1] - l;
-      if (fabs(dm) < pivmin) dm = -pivmin;
-      T1[k - 1][v] = dm;
-      for (int i = k - 2; i >= 0; --i) {
-        dm = (dd[i] - l) - e2[i] / dm;
-        if (fabs(dm) < pivmin) dm = -pivmin;
-        T1[i][v] = dm;
+      // twisted factorisation with the pivots and the vector in registers
+      // (loops unrolled over the compile-time bound, predicated on k / the
+      // twist index), e2 / pivot by reciprocal + one Newton step
+      auto rcpn = [](double q) {
+        double y = __builtin_amdgcn_rcp(q);
+        return fma(fma(-q, y, 1.0), y, y);
+      };
+      double tv[K];
+      // backward pivots D-_i
+      double dm = 0.0;
+#pragma unroll
+      for (int i = K - 1; i >= 0; --i) {
+        tv[i] = 0.0;
+        if (i == k - 1) {
+          dm = dd[i] - l;
+          if (fabs(dm) < pivmin) dm = -pivmin;
+          tv[i] = dm;
+        } else if (i < k - 1) {
+          dm = (dd[i] - l) - e2[i] * rcpn(dm);
+          if (fabs(dm) < pivmin) dm = -pivmin;
+          tv[i] = dm;
+        }
       }
       // forward pivots D+_i and the twist gamma_i = D+_i + D-_i - (d_i - l)
       double dp = dd[0] - l;
       if (fabs(dp) < pivmin) dp = -pivmin;
       int rt = 0;
-      double best = fabs(T1[0][v]);
-      for (int i = 1; i < k; ++i) {
-        dp = (dd[i] - l) - e2[i - 1] / dp;
-        if (fabs(dp) < pivmin) dp = -pivmin;
-        const double gm = fabs(dp + T1[i][v] - (dd[i] - l));
-        if (gm < best) { best = gm; rt = i; }
+      double best = fabs(tv[0]);
+#pragma unroll
+      for (int i = 1; i < K; ++i) {
+        if (i < k) {
+          dp = (dd[i] - l) - e2[i - 1] * rcpn(dp);
+          if (fabs(dp) < pivmin) dp = -pivmin;
+          const double gm = fabs(dp + tv[i] - (dd[i] - l));
+          if (gm < best) { best = gm; rt = i; }
+        }
       }
-      // D+_i below the twist (slots 0..rt-1), then the two recurrences
+      // D+_i below the twist (slots 0..rt-1)
       dp = dd[0] - l;
       if (fabs(dp) < pivmin) dp = -pivmin;
-      for (int i = 0; i < rt; ++i) {
-        T1[i][v] = dp;
-        dp = (dd[i + 1] - l) - e2[i] / dp;
-        if (fabs(dp) < pivmin) dp = -pivmin;
+#pragma unroll
+      for (int i = 0; i + 1 < K; ++i) {
+        if (i < rt) {
+          tv[i] = dp;
+          dp = (dd[i + 1] - l) - e2[i] * rcpn(dp);
+          if (fabs(dp) < pivmin) dp = -pivmin;
+        }
       }
+      // the two recurrences out from the twist
       double x = 1.0, nrm = 1.0;
-      for (int i = rt - 1; i >= 0; --i) {
-        x = -(ee[i] / T1[i][v]) * x;
-        T1[i][v] = x;
-        nrm = fma(x, x, nrm);
+#pragma unroll
+      for (int i = K - 1; i >= 0; --i) {
+        if (i < rt) {
+          x = -(ee[i] * rcpn(tv[i])) * x;
+          tv[i] = x;
+          nrm = fma(x, x, nrm);
+        }
       }
-      T1[rt][v] = 1.0;
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+        if (i == rt) tv[i] = 1.0;
       x = 1.0;
-      for (int i = rt; i + 1 < k; ++i) {
-        x = -(ee[i] / T1[i + 1][v]) * x;
-        T1[i + 1][v] = x;
-        nrm = fma(x, x, nrm);
+#pragma unroll
+      for (int i = 0; i + 1 < K; ++i) {
+        if (i >= rt && i + 1 < k) {
+          x = -(ee[i] * rcpn(tv[i + 1])) * x;
+          tv[i + 1] = x;
+          nrm = fma(x, x, nrm);
+        }
       }
       const double sc = 1.0 / sqrt(nrm);
       if (!isfinite(sc) || !(sc > 0.0)) atomicOr(&bad_s, 1);
-      for (int i = 0; i < k; ++i) T1[i][v] *= sc;
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+        if (i < k) T1[i][v] = tv[i] * sc;
     }
     wave_lds_sync();
     if (clus_s) {
