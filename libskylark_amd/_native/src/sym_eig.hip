@@ -399,81 +399,50 @@ k_sym_eig_tridiag(const double* __restrict__ Cin, int k, int ldc, int r, double*
       const double gap = fmin(v > 0 ? lam[v - 1] - l : 1e300, v + 1 < nt ? l - lam[v + 1] : 1e300);
       if (!(gap > 1e-14 * tnorm)) atomicOr(&bad_s, 1);   // numerically repeated
       if (gap < gtol) atomicOr(&clus_s, 1);
-      // twisted factorisation with the pivots and the vector in registers
-      // (loops unrolled over the compile-time bound, predicated on k / the
-      // twist index), e2 / pivot by reciprocal + one Newton step
-      auto rcpn = [](double q) {
-        double y = __builtin_amdgcn_rcp(q);
-        return fma(fma(-q, y, 1.0), y, y);
-      };
-      double tv[K];
-      // backward pivots D-_i
-      double dm = 0.0;
-#pragma unroll
-      for (int i = K - 1; i >= 0; --i) {
-        tv[i] = 0.0;
-        if (i == k - 1) {
-          dm = dd[i] - l;
-          if (fabs(dm) < pivmin) dm = -pivmin;
-          tv[i] = dm;
-        } else if (i < k - 1) {
-          dm = (dd[i] - l) - e2[i] * rcpn(dm);
-          if (fabs(dm) < pivmin) dm = -pivmin;
-          tv[i] = dm;
-        }
+      // backward pivots D-_i (slot i)
+      double dm = dd[k - 1] - l;
+      if (fabs(dm) < pivmin) dm = -pivmin;
+      T1[k - 1][v] = dm;
+      for (int i = k - 2; i >= 0; --i) {
+        dm = (dd[i] - l) - e2[i] / dm;
+        if (fabs(dm) < pivmin) dm = -pivmin;
+        T1[i][v] = dm;
       }
       // forward pivots D+_i and the twist gamma_i = D+_i + D-_i - (d_i - l)
       double dp = dd[0] - l;
       if (fabs(dp) < pivmin) dp = -pivmin;
       int rt = 0;
-      double best = fabs(tv[0]);
-#pragma unroll
-      for (int i = 1; i < K; ++i) {
-        if (i < k) {
-          dp = (dd[i] - l) - e2[i - 1] * rcpn(dp);
-          if (fabs(dp) < pivmin) dp = -pivmin;
-          const double gm = fabs(dp + tv[i] - (dd[i] - l));
-          if (gm < best) { best = gm; rt = i; }
-        }
+      double best = fabs(T1[0][v]);
+      for (int i = 1; i < k; ++i) {
+        dp = (dd[i] - l) - e2[i - 1] / dp;
+        if (fabs(dp) < pivmin) dp = -pivmin;
+        const double gm = fabs(dp + T1[i][v] - (dd[i] - l));
+        if (gm < best) { best = gm; rt = i; }
       }
-      // D+_i below the twist (slots 0..rt-1)
+      // D+_i below the twist (slots 0..rt-1), then the two recurrences
       dp = dd[0] - l;
       if (fabs(dp) < pivmin) dp = -pivmin;
-#pragma unroll
-      for (int i = 0; i + 1 < K; ++i) {
-        if (i < rt) {
-          tv[i] = dp;
-          dp = (dd[i + 1] - l) - e2[i] * rcpn(dp);
-          if (fabs(dp) < pivmin) dp = -pivmin;
-        }
+      for (int i = 0; i < rt; ++i) {
+        T1[i][v] = dp;
+        dp = (dd[i + 1] - l) - e2[i] / dp;
+        if (fabs(dp) < pivmin) dp = -pivmin;
       }
-      // the two recurrences out from the twist
       double x = 1.0, nrm = 1.0;
-#pragma unroll
-      for (int i = K - 1; i >= 0; --i) {
-        if (i < rt) {
-          x = -(ee[i] * rcpn(tv[i])) * x;
-          tv[i] = x;
-          nrm = fma(x, x, nrm);
-        }
+      for (int i = rt - 1; i >= 0; --i) {
+        x = -(ee[i] / T1[i][v]) * x;
+        T1[i][v] = x;
+        nrm = fma(x, x, nrm);
       }
-#pragma unroll
-      for (int i = 0; i < K; ++i)
-        if (i == rt) tv[i] = 1.0;
+      T1[rt][v] = 1.0;
       x = 1.0;
-#pragma unroll
-      for (int i = 0; i + 1 < K; ++i) {
-        if (i >= rt && i + 1 < k) {
-          x = -(ee[i] * rcpn(tv[i + 1])) * x;
-          tv[i + 1] = x;
-          nrm = fma(x, x, nrm);
-        }
+      for (int i = rt; i + 1 < k; ++i) {
+        x = -(ee[i] / T1[i + 1][v]) * x;
+        T1[i + 1][v] = x;
+        nrm = fma(x, x, nrm);
       }
       const double sc = 1.0 / sqrt(nrm);
       if (!isfinite(sc) || !(sc > 0.0)) atomicOr(&bad_s, 1);
-#pragma unroll
-      for (int i = 0; i < K; ++i)
-        if (i < k) T1[i][v] = tv[i] * sc;
+      for (int i = 0; i < k; ++i) T1[i][v] *= sc;
     }
     wave_lds_sync();
     if (clus_s) {
