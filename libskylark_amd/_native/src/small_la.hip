@@ -306,27 +306,33 @@ k_wave_chol_inv_rolled(const double* __restrict__ G, int k, int ldg, double* __r
 // LDS slot, one barrier, and every thread reads the 13 values it needs.  No
 // slot is ever rewritten, so one barrier per step is race free, and the slots
 // hold the whole eliminated matrix for the final output pass.
+// KA = padded size (16, 32, 48 or 64): thread (tr, tc) of the 16 x 16 grid
+// holds rows tr + 16 a and columns tc + 16 b of both halves (NA = KA / 16 of
+// each), so a k = 40 matrix does 9 + 9 FMAs per thread per step instead of
+// the 64-padded 16 + 16; the pivot reciprocal is v_rcp_f64 + one Newton step.
+template <int KA>
 __global__ void __launch_bounds__(256)
 k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __restrict__ R,
                     double* __restrict__ Rinv, float* __restrict__ Rinv32, int* __restrict__ status) {
-  __shared__ double rows[KM][2 * KM];
-  __shared__ double dsh[KM];
+  constexpr int NA = KA / 16;
+  __shared__ double rows[KA][2 * KA];
+  __shared__ double dsh[KA];
   const int t = threadIdx.x, tr = t >> 4, tc = t & 15;
-  __shared__ double diag[KM];
-  double m[4][8];
+  __shared__ double diag[KA];
+  double m[NA][2 * NA];
   // diagonal staged through LDS: a rolled loop of k global loads here waited
   // on one load at a time (~0.7 us each -> most of the kernel's 37 us)
   if (t < k) diag[t] = fabs(G[t * ldg + t]);
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
+  for (int a = 0; a < NA; ++a) {
     const int i = tr + 16 * a;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < NA; ++b) {
       const int c = tc + 16 * b;
       double v = (i == c) ? 1.0 : 0.0;
       if (i < k && c < k) v = 0.5 * (G[i * ldg + c] + G[c * ldg + i]);
       m[a][b] = v;
-      m[a][4 + b] = (i == c) ? 1.0 : 0.0;
+      m[a][NA + b] = (i == c) ? 1.0 : 0.0;
     }
   }
   __syncthreads();
@@ -337,12 +343,12 @@ k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __rest
     const int ja = j >> 4;
     if (tr == (j & 15)) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < NA; ++a)
         if (a == ja) {
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
+          for (int b = 0; b < NA; ++b) {
             rows[j][tc + 16 * b] = m[a][b];
-            rows[j][KM + tc + 16 * b] = m[a][4 + b];
+            rows[j][KA + tc + 16 * b] = m[a][NA + b];
           }
         }
     }
@@ -352,22 +358,23 @@ k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __rest
       bad = 1;
       d = 1e300;
     }
-    const double dinv = 1.0 / d;
-    double mult[4], rv[8];
+    double dinv = __builtin_amdgcn_rcp(d);
+    dinv = fma(fma(-d, dinv, 1.0), dinv, dinv);
+    double mult[NA], rv[2 * NA];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+    for (int a = 0; a < NA; ++a) {
       const int i = tr + 16 * a;
       mult[a] = (i > j) ? rows[j][i] * dinv : 0.0;
     }
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < NA; ++b) {
       rv[b] = rows[j][tc + 16 * b];
-      rv[4 + b] = rows[j][KM + tc + 16 * b];
+      rv[NA + b] = rows[j][KA + tc + 16 * b];
     }
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) m[a][b] = fma(-mult[a], rv[b], m[a][b]);
+      for (int b = 0; b < 2 * NA; ++b) m[a][b] = fma(-mult[a], rv[b], m[a][b]);
     if (t == j) dsh[j] = d;
   }
   __syncthreads();
@@ -379,7 +386,7 @@ k_aug_elim_chol_inv(const double* __restrict__ G, int k, int ldg, double* __rest
     if (c >= i) {
       const double si = sqrt(dsh[i]);
       r = (c == i) ? si : rows[i][c] / si;
-      ri = rows[c][KM + i] / sqrt(dsh[c]);
+      ri = rows[c][KA + i] / sqrt(dsh[c]);
     }
     if (R) R[e] = r;
     if (Rinv) Rinv[e] = ri;
@@ -416,8 +423,12 @@ SL_API int sl_small_chol_inv(const double* G, int k, int ldg, double* R, double*
   // workgroup 61 us vs wave 57; k=64: wave 95 vs workgroup 121 -> pick per size
   int impl = g_chol_impl;
   if (impl == 0) impl = 5;
-  if (impl == 5)
-    k_aug_elim_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  if (impl == 5) {
+    if (k <= 16) k_aug_elim_chol_inv<16><<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+    else if (k <= 32) k_aug_elim_chol_inv<32><<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+    else if (k <= 48) k_aug_elim_chol_inv<48><<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+    else k_aug_elim_chol_inv<64><<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
+  }
   else if (impl == 1)
     k_small_chol_inv<<<1, 256, 0, s>>>(G, k, ldg, R, Rinv, Rinv32, status);
   else if (impl == 4)
