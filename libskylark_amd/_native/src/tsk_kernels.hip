@@ -335,7 +335,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         }
         *(f32x4*)&yfc[yidx<GG::YFS>(col, rg)] = sum;
         if constexpr (STORE_Y) {
-          if (col < k) {
+          if (col < k && !(ab & 256)) {
             float* yrow = Y + (r0 + 4 * rg) * ldy + col;
             if (full) {
 #pragma unroll
@@ -352,6 +352,26 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     if constexpr (!PIPE) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      if constexpr (STORE_Y) {
+        if (ab & 256) {
+          // Y rows as 16-B pieces (k % 4 == 0, 16-B aligned rows): thread t of
+          // the workgroup stores columns 4 (t % (k/4)) .. +3 of row t / (k/4),
+          // gathered from the reduced, column-major y in LDS -- 160 b128
+          // stores per 16 x 40 block instead of 640 scattered dword stores
+          const int tq = k >> 2;
+          const int t = w * 64 + lane;
+          const int64_t r0 = phys(blk) * BM;
+          if (t < BM * tq) {
+            const int row = t / tq, c4 = 4 * (t - row * tq);
+            if (r0 + row < m) {
+              f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = yfc[yidx<GG::YFS>(c4 + e, row >> 2) + (row & 3)];
+              *(f32x4*)(Y + (r0 + row) * ldy + c4) = v;
+            }
+          }
+        }
+      }
     }
     }
     SL_STAMP(4)
@@ -796,7 +816,8 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   int rc = SL_ERR_UNSUPPORTED;
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
-  g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0) | ((flags & 32) ? 128 : 0);
+  g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0) | ((flags & 32) ? 128 : 0) |
+            ((Y && (k & 3) == 0 && (ldy & 3) == 0 && ((uintptr_t)Y & 15) == 0 && !(g_x & 4)) ? 256 : 0);
   // intermediate power-iteration passes (no Gram, bf16 y): compile-time specialisation
   const bool inter = (flags & 3) == 3 && !Y;
   // final pass whose Gram is taken separately (fp64 Gram of the stored Y)
