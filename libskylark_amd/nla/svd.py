@@ -325,7 +325,12 @@ class _DevicePlan:
                         and dev.type == "cuda")
         self.eig_status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.use_graph = use_graph
-        self.snake = os.environ.get("SL_SVD_SNAKE", "0") == "1"  # measured: no gain (1.77 vs 1.78 ms)
+        self.snake = os.environ.get("SL_SVD_SNAKE", "0") == "1"
+        # final pass: fp64 Gram of Y by a separate streaming kernel (default)
+        # or inside the pass (SL_SVD_SPLIT_GRAM=0)
+        self.split_gram = os.environ.get("SL_SVD_SPLIT_GRAM", "1") == "1"
+        self.ws32g = torch.empty(T.gram64_workspace_bytes(m, k), dtype=torch.uint8, device=dev) \
+            if self.split_gram else None  # measured: no gain (1.77 vs 1.78 ms)
         self._xm_fn = None
         self._fu_fn = None
         self.g1 = self.g2 = None
@@ -377,8 +382,16 @@ class _DevicePlan:
             # Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2 with an
             # f32 second Gram only reached ~eps32, at three times the work);
             # W (f64) and G land in the [W; G] buffer the all-reduce takes
-            _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True,
-                                   zt=self.Zt, wg_out=self.WG, reverse=self.snake and i % 2 == 1)
+            if self.split_gram:
+                # the pass without its Gram specialisation (~160 us faster at
+                # 1e6 x 1e3), then the fp64 Gram of the stored f32 Y by its own
+                # streaming kernel (~80 us) straight into [W; G]
+                _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=False, exact=True, ws=self.ws, zt=self.Zt,
+                                       wg_out=self.WG, reverse=self.snake and i % 2 == 1)
+                T.gram64(Y, ws=self.ws32g, out=self.WG[self.n:])
+            else:
+                _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True,
+                                       zt=self.Zt, wg_out=self.WG, reverse=self.snake and i % 2 == 1)
         self._WG = self.WG
         self.Y = Y
         return self._WG

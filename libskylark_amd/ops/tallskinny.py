@@ -152,8 +152,11 @@ def _fused_native(A: torch.Tensor, Z: torch.Tensor | None, keep_y: bool, gram: b
     g64 = bool(gram64 and gram and keep_y and exact)
     flags = (0 if gram else 1) | (0 if exact else 2) | (4 if g64 else 0) | (32 if reverse else 0)
     if wg_out is not None:
-        if not g64 or wg_out.dtype != torch.float64 or tuple(wg_out.shape) != (n + k, k) or not wg_out.is_contiguous():
-            raise ValueError("fused_pass: wg_out needs gram64 and a contiguous f64 (n + k) x k buffer")
+        # f64 W straight into wg_out[:n]; with the in-pass fp64 Gram also G
+        # into wg_out[n:] (gram=False leaves that block to the caller)
+        if not (g64 or not gram) or wg_out.dtype != torch.float64 or tuple(wg_out.shape) != (n + k, k) \
+                or not wg_out.is_contiguous():
+            raise ValueError("fused_pass: wg_out needs gram64 (or gram=False) and a contiguous f64 (n + k) x k buffer")
         W, G = wg_out[:n], wg_out[n:]
         flags |= 16
     else:
@@ -228,14 +231,16 @@ def gram64_workspace_bytes(m: int, k: int) -> int:
     return int(_lib.require().sl_tsk_gram64_workspace(m, k))
 
 
-def gram64(Y: torch.Tensor, ws: torch.Tensor | None = None) -> torch.Tensor:
+def gram64(Y: torch.Tensor, ws: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """``G = Y^T Y`` in float64 for tall f32 ``Y`` (k <= 64), partial over this
     shard: fp64 products and sums on the f64 matrix cores, so one fp64
     CholeskyQR of ``Y`` from this ``G`` is as orthogonal as CholeskyQR2 with an
     f32 second Gram.  Torch (fp64) on CPU."""
     m, k = Y.shape
     if Y.is_cuda and Y.dtype == torch.float32 and k <= 64 and Y.stride(1) == 1 and _lib.available():
-        G = torch.empty(k, k, dtype=torch.float64, device=Y.device)
+        G = out if out is not None else torch.empty(k, k, dtype=torch.float64, device=Y.device)
+        if not (G.dtype == torch.float64 and G.is_contiguous() and tuple(G.shape) == (k, k)):
+            raise ValueError("gram64: out must be a contiguous f64 k x k tensor")
         if ws is None:
             ws = _WS32.get(Y.device, gram64_workspace_bytes(m, k))
         _lib.call("sl_tsk_gram64", _lib.ptr(Y), m, k, Y.stride(0), _lib.ptr(G), _lib.ptr(ws), vp(_lib.stream_of(Y)))
