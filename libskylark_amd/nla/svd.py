@@ -325,12 +325,15 @@ class _DevicePlan:
                         and dev.type == "cuda")
         self.eig_status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.use_graph = use_graph
+        # alternate row directions across passes (Infinity-Cache reuse; measured
+        # no gain: 1.77 vs 1.78 ms)
         self.snake = os.environ.get("SL_SVD_SNAKE", "0") == "1"
         # final pass: fp64 Gram of Y inside the pass (default) or by a separate
-        # streaming kernel after a Gram-free pass (SL_SVD_SPLIT_GRAM=1)
-        self.split_gram = os.environ.get("SL_SVD_SPLIT_GRAM", "0") == "1"  # measured equal (rocprof: 551 + 73 + 10 vs 624 + 5 us)
+        # streaming kernel after a Gram-free pass (SL_SVD_SPLIT_GRAM=1; measured
+        # equal under rocprof: 551 + 73 + 10 vs 624 + 5 us)
+        self.split_gram = os.environ.get("SL_SVD_SPLIT_GRAM", "0") == "1"
         self.ws32g = torch.empty(T.gram64_workspace_bytes(m, k), dtype=torch.uint8, device=dev) \
-            if self.split_gram else None  # measured: no gain (1.77 vs 1.78 ms)
+            if self.split_gram else None
         self._xm_fn = None
         self._fu_fn = None
         self.g1 = self.g2 = None
