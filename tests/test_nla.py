@@ -320,3 +320,25 @@ def test_approximate_svd_device_eig_matches_host(dev, monkeypatch, force_fallbac
         torch.testing.assert_close((V.double().t() @ Vh.double()).abs().diagonal(),
                                    torch.ones(10, dtype=torch.float64, device=dev), atol=1e-5, rtol=0)
     assert plan.graph_built()
+
+
+@pytest.mark.gpu
+def test_randsvd_split_gram_final_pass_matches(dev, monkeypatch):
+    """SL_SVD_SPLIT_GRAM=1 (Gram-free final pass + separate fp64 Gram of the
+    stored Y) gives the default path's factors."""
+    import libskylark_amd as sk
+    from libskylark_amd.nla import svd as SV
+    torch.manual_seed(4)
+    A = (torch.randn(30000, 12, device=dev) @ torch.randn(12, 256, device=dev)
+         + 0.01 * torch.randn(30000, 256, device=dev)).to(torch.bfloat16)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT")
+    SV._PLANS.clear()
+    U0, s0, V0 = sk.nla.approximate_svd(A, 8, context=sk.Context(3), params=p)
+    monkeypatch.setenv("SL_SVD_SPLIT_GRAM", "1")
+    SV._PLANS.clear()
+    for _ in range(3):   # eager call, graph capture, replay
+        U1, s1, V1 = sk.nla.approximate_svd(A, 8, context=sk.Context(3), params=p)
+    SV._PLANS.clear()
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=0)
+    torch.testing.assert_close(U1.abs(), U0.abs(), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(V1.abs(), V0.abs(), rtol=1e-3, atol=1e-4)
