@@ -49,7 +49,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int WAVES = 8;
 constexpr int THREADS = WAVES * 64;
 constexpr int BM = 16;
-constexpr int NBUF_DEFAULT = 3;   // 2..4 measured equal; 3 fits the padded y buffers
+constexpr int NBUF_DEFAULT = 2;   // r2s2 A/B on the headline bench: 2 -> 1.70-1.71 ms, 3 -> 1.755-1.767 ms
 int g_flags = 0;   // per-call mode bits (8: no Gram, 32: y_hi only)
 int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, bit3 step 4; bit6 nt loads
 
