@@ -14,7 +14,7 @@
 //     each); a wave keeps its slice of Z (bf16 MFMA B-fragments) and its
 //     slice of W (f32 accumulators) in registers for the whole kernel;
 //   * row blocks of BM = 16 rows stream HBM -> LDS by LDS-DMA
-//     (global_load_lds_dwordx4, 1 KiB per wave-instruction), triple
+//     (global_load_lds_dwordx4, 1 KiB per wave-instruction), double
 //     buffered, each wave fetching only its own columns; the LDS image is
 //     XOR-swizzled through the SOURCE address (chunk ^ row) so both reads
 //     below are (nearly) conflict-free:
