@@ -119,12 +119,18 @@ def run(a, comm, dev, scaling, square=False):
     steps, warmup = (a.steps, a.warmup) if primary else (max(3, a.steps // 2), 2)
     for _ in range(warmup):
         U, s, V = step()
+    # per-step device time from events recorded between the steps (no host
+    # synchronisation inside the timed loop); the headline number is the
+    # wall clock of all K steps, bracketed by barrier + synchronize
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    evs[0].record()
+    for i in range(steps):
         U, s, V = step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -132,6 +138,8 @@ def run(a, comm, dev, scaling, square=False):
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     comm.all_reduce_max(t)
     ms = float(t.item()) / steps * 1e3
+    per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    step_ms = {"min": round(per[0], 4), "median": round(per[len(per) // 2], 4), "max": round(per[-1], 4)}
     orth, resid = check_answer(A, U, s, V, comm)
     red = "one-shot IPC all-reduces" if getattr(comm, "_oneshot", None) else "RCCL all-reduces"
     if grid is not None:
@@ -141,7 +149,7 @@ def run(a, comm, dev, scaling, square=False):
     else:
         par = f"dp{N} ([VC,*] row blocks, {red})"
     return {
-        "m": m, "n": n, "ms": ms, "gbs": m * n * 2 / (ms / 1e3) / 1e9, "steps": steps, "warmup": warmup,
+        "m": m, "n": n, "ms": ms, "step_ms": step_ms, "gbs": m * n * 2 / (ms / 1e3) / 1e9, "steps": steps, "warmup": warmup,
         "parallelism": par, "orth_err": orth, "resid_rel": resid,
         "top_singular_values": [round(float(x), 3) for x in s[:3].tolist()],
         "grid_pc": grid.pc if grid is not None else 0,
@@ -213,6 +221,7 @@ def main(argv=None):
                 "parallelism": res["parallelism"],
             },
             "randsvd_ms": round(res["ms"], 4),
+            "step_ms": res["step_ms"],
             "check": {"orth_err": res["orth_err"], "resid_rel": res["resid_rel"], "ok": ok},
             "top_singular_values": res["top_singular_values"],
             "native_fused_pass": res["native_fused_pass"],
@@ -233,6 +242,8 @@ def main(argv=None):
                       f"({r['calls']} calls)", file=sys.stderr)
     if N > 1:
         import torch.distributed as dist
+        comm.check_collectives()
+        comm.close()
         dist.destroy_process_group()
     return 0 if ok else 3
 

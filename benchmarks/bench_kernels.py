@@ -12,7 +12,6 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import argparse
-import ctypes as C
 import json
 import statistics
 import time
@@ -47,20 +46,14 @@ def main():
     Z = torch.randn(n, k, device=dev) / 30
     Y = torch.randn(m, k, device=dev)
     Mx = torch.randn(k, k, device=dev)
-    lib = _lib.require()
-    lib.sl_tsk_set_nbuf.argtypes = [C.c_int]
+    _lib.require()
     abytes = A.numel() * 2
     res = {}
 
-    def setnb(nb):
-        return lambda: lib.sl_tsk_set_nbuf(nb)
-
     variants = {
-        "fused_nb3": (setnb(3), lambda: tallskinny.fused_pass(A, Z), abytes),
-        "fused_nb4": (setnb(4), lambda: tallskinny.fused_pass(A, Z), abytes),
-        "fused_nb5": (setnb(5), lambda: tallskinny.fused_pass(A, Z), abytes),
-        "fused_keepy_nb4": (setnb(4), lambda: tallskinny.fused_pass(A, Z, keep_y=True), abytes + m * k * 4),
-        "matmul_zsplit": (setnb(4), lambda: tallskinny.matmul(A, Z), abytes + m * k * 4),
+        "fused": (None, lambda: tallskinny.fused_pass(A, Z), abytes),
+        "fused_keepy": (None, lambda: tallskinny.fused_pass(A, Z, keep_y=True), abytes + m * k * 4),
+        "matmul_zsplit": (None, lambda: tallskinny.matmul(A, Z), abytes + m * k * 4),
         "f32_gram_ident": (None, lambda: tallskinny.f32_xm(Y, None, store=False, gram=True), m * k * 4),
         "f32_gram_xm": (None, lambda: tallskinny.f32_xm(Y, Mx, store=False, gram=True), m * k * 4),
         "f32_xm_store20": (None, lambda: tallskinny.f32_xm(Y, Mx[:, :20].contiguous(), store=True), m * k * 4 + m * 20 * 4),

@@ -79,7 +79,10 @@ k_oneshot_allreduce(T* __restrict__ x, int64_t n, int rank, int p, const uint64_
   }
   __syncthreads();
   if (timed_out) {
+    // never a silent partial sum: the operand is poisoned (NaN) on this rank
+    // and the error word set; Comm.check_collectives() raises on it
     if (t == 0) atomicOr(err, 1);
+    for (int64_t i = lo + t; i < hi; i += OS_NT) x[i] = (T)NAN;
   } else {
     // 4. sum the p contributions in rank order (identical bits on every rank)
     for (int64_t i = lo + t; i < hi; i += OS_NT) {

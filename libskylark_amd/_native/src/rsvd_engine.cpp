@@ -1,0 +1,297 @@
+// Randomized SVD engine: the whole device-resident ApproximateSVD call of a
+// row-distributed bf16 A (reference nla/svd.hpp:222-318 with the power
+// iteration of :71-149), driven from C++ with no Python and no host round trip.
+//
+// One call = q + 2 segments on a HIP stream:
+//   seg 0        pass 0 over A (Z = the sketch operator) + slab reduction
+//   seg 1 .. q   CholeskyQR of the previous W (last-arriver Gram + Cholesky
+//                + R^{-1}), Z^T = (W R^{-1})^T, pass i, slab reduction
+//                (pass q is the FINAL form: Y stored, fp64 Gram of Y)
+//   seg q + 1    fp64 core: Cholesky of Y^T Y, C = Rt^{-T} W^T W Rt^{-1},
+//                Jacobi, M = Rt^{-1} Ub_r, N = M S^{-1}, s
+// then the finish (U = Y M, V = W N, s) into the caller's buffers.
+//
+// Single rank: the segments are captured ONCE as a hipGraph (per A pointer)
+// and replayed; the sketch operator and the finish are plain launches
+// (kernel arguments carry the per-call sketch counters, the outputs are the
+// caller's fresh buffers).  Several ranks: after every reducing segment the
+// [W; G] buffer is summed over the ranks, either by the caller (Python:
+// torch.distributed / one-shot IPC between sl_rsvd_segment calls) or, from
+// C, by a NativeComm RCCL communicator (sl_rsvd_run_comm) -- no interpreter.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+
+#include "sl_common.hpp"
+
+// kernels of rsvd_pass.hip / rsvd_core.hip / svd_core.hip / native_comm.cpp
+SL_API int sl_rsvd_pass_grid(int64_t m);
+SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k);
+SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws, float* Y,
+                        int64_t ldy, int final_pass, int variant, void* stream);
+SL_API int sl_rsvd_reduce(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw, double* Gout,
+                          int ldg, void* stream);
+SL_API int64_t sl_rsvd_gram_workspace(int k);
+SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, double* Rinv, int* status, void* stream);
+SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double* Rinv, void* Zt, void* stream);
+SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
+                            double* N, double* s, int* status, int max_sweeps, void* stream);
+SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
+                          float* s32, void* stream);
+SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
+                           void* stream);
+SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
+                         int64_t ldo, double* G, void* ws, void* stream);
+SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
+                              void* stream);
+
+namespace {
+
+struct Plan {
+  int64_t m = 0, n = 0, lda = 0;
+  int k = 0, r = 0, q = 0;
+  int variant = 0;
+  // device buffers (one allocation, carved)
+  char* base = nullptr;
+  void* pass_ws = nullptr;
+  uint16_t* Zt = nullptr;   // k x n bf16
+  double* WG = nullptr;     // [W (n x k) ; G (k x k)] f64: the reduced pass outputs
+  float* Y = nullptr;       // m x k f32
+  void* gram_ws = nullptr;  // counter + partial Grams (zeroed once)
+  double* Rinv = nullptr;   // k x k
+  float* M = nullptr;       // k x r
+  double* N = nullptr;      // k x r
+  double* s64 = nullptr;    // r
+  int* status = nullptr;
+  // graph of the segments (single rank), valid for graph_A
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  const void* graph_A = nullptr;
+  hipStream_t cap_stream = nullptr;   // capture happens here (never the legacy null stream)
+  hipEvent_t cap_ev = nullptr;
+};
+
+int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+int seg(Plan* p, const void* A, int i, hipStream_t s) {
+  const bool final_pass = i == p->q;
+  if (i > p->q + 1 || i < 0) { sl_set_last_error("rsvd: segment out of range"); return SL_ERR_INVALID; }
+  int rc = SL_OK;
+  if (i == p->q + 1) {
+    return sl_rsvd_final_la(p->WG, (int)p->n, p->k, p->k, p->WG + p->n * p->k, p->r, p->gram_ws, p->M, p->N,
+                            p->s64, p->status, 0, s);
+  }
+  if (i == 0) {
+    SL_HIP_CHECK(hipMemsetAsync(p->status, 0, sizeof(int), s));
+  } else {
+    // CholeskyQR of the previous (reduced) W and the next pass operand
+    rc = sl_rsvd_inter_la(p->WG, (int)p->n, p->k, p->k, p->gram_ws, p->Rinv, p->status, s);
+    if (rc != SL_OK) return rc;
+    rc = sl_rsvd_make_zt(p->WG, (int)p->n, p->k, p->k, p->Rinv, p->Zt, s);
+    if (rc != SL_OK) return rc;
+  }
+  rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
+                    final_pass ? 1 : 0, p->variant, s);
+  if (rc != SL_OK) return rc;
+  return sl_rsvd_reduce(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
+                        p->k, s);
+}
+
+void drop_graph(Plan* p) {
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  p->exec = nullptr;
+  p->graph = nullptr;
+  p->graph_A = nullptr;
+}
+
+}  // namespace
+
+// A: m x n bf16 row shard (lda), k = sketch width (<= 48), r = rank (<= k),
+// q = power iterations.  Allocates every device buffer of the call once.
+SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, int q, void** out) {
+  *out = nullptr;
+  if (m < 1 || n < 16 || n > 1024 || n % 8 || lda % 8 || k < 1 || k > 48 || r < 1 || r > k || q < 0) {
+    sl_set_last_error("rsvd_plan: needs m >= 1, 16 <= n <= 1024, n % 8 == 0, lda % 8 == 0, 1 <= r <= k <= 48, q >= 0");
+    return SL_ERR_UNSUPPORTED;
+  }
+  Plan* p = new (std::nothrow) Plan();
+  if (!p) return SL_ERR_GENERIC;
+  p->m = m; p->n = n; p->lda = lda; p->k = k; p->r = r; p->q = q;
+  int64_t off = 0;
+  const int64_t o_pass = off; off = align256(off + sl_rsvd_pass_workspace(m, n, k));
+  const int64_t o_zt = off;   off = align256(off + n * k * 2);
+  const int64_t o_wg = off;   off = align256(off + (n + k) * k * 8);
+  const int64_t o_y = off;    off = align256(off + m * k * 4);
+  const int64_t o_gram = off; off = align256(off + sl_rsvd_gram_workspace(k));
+  const int64_t o_ri = off;   off = align256(off + (int64_t)k * k * 8);
+  const int64_t o_m = off;    off = align256(off + (int64_t)k * r * 4);
+  const int64_t o_n = off;    off = align256(off + (int64_t)k * r * 8);
+  const int64_t o_s = off;    off = align256(off + (int64_t)r * 8);
+  const int64_t o_st = off;   off = align256(off + 16);
+  if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
+    delete p;
+    sl_set_last_error("rsvd_plan: device allocation failed");
+    return SL_ERR_HIP;
+  }
+  p->pass_ws = p->base + o_pass;
+  p->Zt = (uint16_t*)(p->base + o_zt);
+  p->WG = (double*)(p->base + o_wg);
+  p->Y = (float*)(p->base + o_y);
+  p->gram_ws = p->base + o_gram;
+  p->Rinv = (double*)(p->base + o_ri);
+  p->M = (float*)(p->base + o_m);
+  p->N = (double*)(p->base + o_n);
+  p->s64 = (double*)(p->base + o_s);
+  p->status = (int*)(p->base + o_st);
+  if (hipMemset(p->gram_ws, 0, (size_t)sl_rsvd_gram_workspace(k)) != hipSuccess ||
+      hipMemset(p->status, 0, 16) != hipSuccess) {
+    (void)hipFree(p->base);
+    delete p;
+    sl_set_last_error("rsvd_plan: memset failed");
+    return SL_ERR_HIP;
+  }
+  *out = p;
+  return SL_OK;
+}
+
+SL_API int sl_rsvd_plan_destroy(void* plan) {
+  Plan* p = (Plan*)plan;
+  if (!p) return SL_OK;
+  drop_graph(p);
+  if (p->cap_ev) (void)hipEventDestroy(p->cap_ev);
+  if (p->cap_stream) (void)hipStreamDestroy(p->cap_stream);
+  (void)hipFree(p->base);
+  delete p;
+  return SL_OK;
+}
+
+// Use caller-owned buffers for the [W; G] reduce buffer ((n + k) * k f64)
+// and / or the status word (e.g. torch tensors the caller all-reduces / reads);
+// null keeps the plan's own.
+SL_API int sl_rsvd_plan_bind(void* plan, double* WG, int* status) {
+  Plan* p = (Plan*)plan;
+  drop_graph(p);
+  if (WG) p->WG = WG;
+  if (status) p->status = status;
+  return SL_OK;
+}
+
+// pass-kernel tuning variant (3: 3-deep DMA ring instead of 4)
+SL_API int sl_rsvd_plan_set_variant(void* plan, int variant) {
+  Plan* p = (Plan*)plan;
+  if (p->variant != variant) drop_graph(p);
+  p->variant = variant;
+  return SL_OK;
+}
+
+// Sketch operator of the call: the FJLT of reference FJLT_data (N Rademacher
+// signs at baseD, k DCT frequencies at baseS, scale sqrt(n / k)) realised as
+// the pass's bf16 Z^T.
+SL_API int sl_rsvd_set_fjlt(void* plan, uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, void* stream) {
+  Plan* p = (Plan*)plan;
+  return sl_rsvd_fjlt_zt(seed, baseD, baseS, scale, p->k, (int)p->n, p->Zt, stream);
+}
+
+// Sketch operator given explicitly (k x n bf16, device).
+SL_API int sl_rsvd_set_zt(void* plan, const void* Zt, void* stream) {
+  Plan* p = (Plan*)plan;
+  SL_HIP_CHECK(hipMemcpyAsync(p->Zt, Zt, (size_t)(p->n * p->k * 2), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return SL_OK;
+}
+
+SL_API int sl_rsvd_segment(void* plan, const void* A, int i, void* stream) {
+  return seg((Plan*)plan, A, i, (hipStream_t)stream);
+}
+
+// the [W (n x k) ; G (k x k)] f64 buffer every reducing segment leaves for
+// the cross-rank sum ((n + k) * k doubles after segment q, n * k before)
+SL_API double* sl_rsvd_reduce_buffer(void* plan) { return ((Plan*)plan)->WG; }
+SL_API float* sl_rsvd_y(void* plan) { return ((Plan*)plan)->Y; }
+
+// U (m x r, row stride ldu), s (r), V (n x r) f32 from the core's factors
+SL_API int sl_rsvd_finish(void* plan, float* U, int64_t ldu, float* s, float* V, void* stream) {
+  Plan* p = (Plan*)plan;
+  int rc = sl_rsvd_make_v(p->WG, (int)p->n, p->k, p->k, p->N, p->r, V, p->s64, s, stream);
+  if (rc != SL_OK) return rc;
+  return sl_tsk_f32_xm(p->Y, p->m, p->k, p->k, p->M, p->r, U, ldu, nullptr, nullptr, stream);
+}
+
+// Single-rank call: every segment (one graph replay when use_graph) then the
+// finish.  The sketch operator must have been set for this call.
+SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64_t ldu, float* s, float* V,
+                       void* stream) {
+  Plan* p = (Plan*)plan;
+  hipStream_t st = (hipStream_t)stream;
+  if (use_graph) {
+    if (p->exec && p->graph_A != A) drop_graph(p);
+    if (!p->exec) {
+      if (!p->cap_stream) {
+        SL_HIP_CHECK(hipStreamCreateWithFlags(&p->cap_stream, hipStreamNonBlocking));
+        SL_HIP_CHECK(hipEventCreateWithFlags(&p->cap_ev, hipEventDisableTiming));
+      }
+      // the capture stream starts after everything queued on the caller's
+      // stream (nothing is enqueued on it while it captures)
+      SL_HIP_CHECK(hipEventRecord(p->cap_ev, st));
+      SL_HIP_CHECK(hipStreamWaitEvent(p->cap_stream, p->cap_ev, 0));
+      SL_HIP_CHECK(hipStreamSynchronize(p->cap_stream));
+      hipStream_t cst = p->cap_stream;
+      SL_HIP_CHECK(hipStreamBeginCapture(cst, hipStreamCaptureModeThreadLocal));
+      int rc = SL_OK;
+      for (int i = 0; i <= p->q + 1 && rc == SL_OK; ++i) rc = seg(p, A, i, cst);
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(cst, &g);
+      if (rc != SL_OK || e != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        if (rc == SL_OK) { sl_set_last_error(hipGetErrorString(e)); rc = SL_ERR_HIP; }
+        return rc;
+      }
+      hipGraphExec_t ex = nullptr;
+      if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        sl_set_last_error("rsvd_run: graph instantiate failed");
+        return SL_ERR_HIP;
+      }
+      p->graph = g;
+      p->exec = ex;
+      p->graph_A = A;
+    }
+    SL_HIP_CHECK(hipGraphLaunch(p->exec, st));
+  } else {
+    for (int i = 0; i <= p->q + 1; ++i) {
+      const int rc = seg(p, A, i, st);
+      if (rc != SL_OK) return rc;
+    }
+  }
+  return sl_rsvd_finish(plan, U, ldu, s, V, stream);
+}
+
+// Several ranks from C: the segments with a NativeComm (RCCL) sum of the
+// [W; G] buffer after each pass -- the interpreter-free distributed call.
+SL_API int sl_rsvd_run_comm(void* plan, const void* A, void* comm, float* U, int64_t ldu, float* s, float* V,
+                            void* stream) {
+  Plan* p = (Plan*)plan;
+  for (int i = 0; i <= p->q + 1; ++i) {
+    int rc = seg(p, A, i, (hipStream_t)stream);
+    if (rc != SL_OK) return rc;
+    if (i <= p->q && comm) {
+      const int64_t cnt = (i == p->q ? p->n + p->k : p->n) * p->k;
+      rc = sl_comm_all_reduce(comm, p->WG, p->WG, cnt, SL_F64, 0, stream);
+      if (rc != SL_OK) return rc;
+    }
+  }
+  return sl_rsvd_finish(plan, U, ldu, s, V, stream);
+}
+
+// Status bits of the last call (1 pivot dropped, 2 non-finite, 4 Jacobi not
+// converged, 8 fewer than r positive eigenvalues); synchronises the stream.
+SL_API int sl_rsvd_status(void* plan, int* out, void* stream) {
+  Plan* p = (Plan*)plan;
+  SL_HIP_CHECK(hipMemcpyAsync(out, p->status, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  SL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  return SL_OK;
+}
+
+// device pointer of the status word (for asynchronous checks)
+SL_API int* sl_rsvd_status_ptr(void* plan) { return ((Plan*)plan)->status; }

@@ -49,21 +49,12 @@ typedef __attribute__((address_space(3))) void lds_void;
 constexpr int WAVES = 8;
 constexpr int THREADS = WAVES * 64;
 constexpr int BM = 16;
-constexpr int NBUF_DEFAULT = 2;   // r2s2 A/B on the headline bench: 2 -> 1.70-1.71 ms, 3 -> 1.755-1.767 ms
-int g_flags = 0;   // per-call mode bits (8: no Gram, 32: y_hi only)
-int g_ablate = 0;  // tuning only: bit0 skips step 1, bit1 step 2, bit2 step 3, bit3 step 4; bit6 nt loads
+constexpr int NBUF_DEFAULT = 2;   // LDS-DMA ring depth (the randSVD engine uses rsvd_pass.hip)
+int g_flags = 0;   // per-call mode bits (8: no Gram, 32: y_hi only, 128: reverse, 256: b128 Y rows)
 
 // hardware round-to-nearest-even (v_cvt_pk_bf16_f32), NaN-preserving, branch-free
 __device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
 __device__ __forceinline__ float bf16_val(short h) { return (float)__builtin_bit_cast(__bf16, h); }
-
-// value of x held by lane (l ^ 32) (inline asm: hipcc merged distinct
-// __builtin_amdgcn_permlane32_swap(x, x) calls into one; see tsk3_kernels.hip)
-__device__ __forceinline__ unsigned partner32(unsigned x, bool low) {
-  unsigned a = x, b = x;
-  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-  return low ? b : a;
-}
 
 // LDS-DMA of 16 B per lane into LDS[lds_base + lane*16], issued as inline asm
 // so hipcc does not insert its own (draining) vmcnt(0) before later LDS
@@ -75,20 +66,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-
-// same with the non-temporal policy (A is read exactly once per pass)
-__device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_base) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
@@ -141,21 +118,13 @@ __device__ __forceinline__ int swz(int row) {
 }
 
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false, int X = 0, bool ST = false>
+          bool G64 = false, int X = 0>
 __global__ void __launch_bounds__(THREADS, 1)
 k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
            const bf16_t* __restrict__ Zt, int k,  // Zt: (ZSPLIT ? 2k : k) x n, row-major
            float* __restrict__ Wslab, float* __restrict__ Gslab,
-           float* __restrict__ Y, int64_t ldy, int ab, unsigned long long* __restrict__ dbg = nullptr) {
-  using GG = Geo<NW, KT, NBUF, (X & 4) ? 2 : 1>;
-  // diagnostic build only (ST): per-phase s_memtime sums per wave -> dbg
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-#define SL_STAMP(I)                                                      \
-  if constexpr (ST) {                                                    \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
-    if constexpr ((I) > 0) { if (my > 1) st_acc[(I) > 0 ? (I) - 1 : 0] += t_ - st_prev; } \
-    st_prev = t_;                                                        \
-  }
+           float* __restrict__ Y, int64_t ldy, int ab) {
+  using GG = Geo<NW, KT, NBUF, 1>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* abuf = smem;
   float* yp = (float*)(smem + GG::ABYTES);
@@ -223,8 +192,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
   auto phys = [&](int64_t blk) { return rev ? nblocks - 1 - blk : blk; };
 
   // ---- LDS-DMA of one row block (this wave's columns) into buffer `buf`
-  auto issue_impl = [&](int64_t blk, int buf, auto nt_c) {
-    constexpr bool NT = decltype(nt_c)::value;
+  auto issue = [&](int64_t blk, int buf) {
     char* region = abuf + (buf * WAVES + w) * GG::REGION;
     const int64_t r0 = phys(blk) * BM;
 #pragma unroll
@@ -240,23 +208,12 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       const bf16_t* src = A + grow * lda + col;
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           (unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-      if constexpr (NT) glds16_nt((const void*)src, dst);
-      else glds16((const void*)src, dst);
+      glds16((const void*)src, dst);
     }
   };
-  auto issue = [&](int64_t blk, int buf) {
-    if (ab & 64) issue_impl(blk, buf, std::true_type{});
-    else issue_impl(blk, buf, std::false_type{});
-  };
 
-  // PIPE (X & 4): step 3/4 of block j-1 runs between the two barriers of
-  // block j, beside the cross-wave reduction of block j (which only 24 lanes
-  // of each wave work on), instead of after the second barrier: the
-  // reduction's LDS latency and the barrier waits overlap MFMA work.  Needs
-  // the A tile of block j-1 resident while block j is consumed (prefetch
-  // depth NBUF - 2) and the reduced y double-buffered.
-  constexpr bool PIPE = (X & 4) != 0;
-  constexpr int PD = PIPE ? NBUF - 2 : NBUF - 1;
+  constexpr bool PIPE = false;
+  constexpr int PD = NBUF - 1;
   static_assert(PD >= 1, "ring too shallow");
   constexpr int YFSZ = GG::YFS * GG::KP;   // floats per reduced-y buffer
 #pragma unroll
@@ -268,7 +225,6 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
   const int64_t niter = nloc + (PIPE && nloc > 0 ? 1 : 0);
   int64_t my = 0;  // local iteration index
   for (; my < niter; ++my) {
-    SL_STAMP(0)
     const int64_t blk = b0 + my * bstep;
     const bool have = my < nloc;   // false only on PIPE's drain iteration
     const int buf = (int)(my % NBUF);
@@ -289,7 +245,6 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GG::LPB) : "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GG::LPB) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    SL_STAMP(1)
 
     // ---- step 1: partial y over this wave's columns
     f32x4 accY[KT];
@@ -297,7 +252,6 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     for (int t = 0; t < KT; ++t) accY[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NW / 32; ++ks) {
-      if (ab & 1) break;  // ablation (tuning only)
       const int row = lane & 15;
       const int chunk = (lane >> 4) + 4 * ks;
       const int slot = chunk ^ swz<GG::NCH>(row);
@@ -311,14 +265,12 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     // ---- step 2: cross-wave reduction of y through LDS.  Partials are stored
     //      column-major ([wave][col][16 rows]) so that every access is b128:
     //      a lane's C fragment is 4 consecutive rows of one column.
-    SL_STAMP(2)
-    if (!(ab & 2)) {
+    {
 #pragma unroll
     for (int t = 0; t < KT; ++t)
       *(f32x4*)&yp[((w * GG::KP) + 16 * t + i16) * GG::YPS + 4 * g4] = accY[t];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    SL_STAMP(3)
     {
       constexpr int CPW = GG::KP / WAVES;  // columns reduced per wave
       const int64_t r0 = phys(blk) * BM;
@@ -374,7 +326,6 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
       }
     }
     }
-    SL_STAMP(4)
     }  // have
 
     // prefetch PD blocks ahead into the buffer this wave consumed last iteration
@@ -388,7 +339,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     const float* s3yf = PIPE ? yf + ((my - 1) & 1) * YFSZ : yf;
     // y fragments with rows 4(l>>4)+j of column 16t+(l&15) (K=16 MFMA layout), hi/lo
     const bool hi_only = (ab & 32) != 0;
-    const bool need_g = DO_G && !(ab & 8);
+    const bool need_g = DO_G;
     s16x4 yh[KT], yl[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
@@ -400,8 +351,7 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
         yl[t][j] = bf16_bits(v[j] - bf16_val(h));
       }
     }
-    SL_STAMP(5)
-    if (DO_W && !(ab & 4)) {
+    if (DO_W) {
       const int q = i16 >> 2, p = i16 & 3;
       // ---- step 3: one transposed LDS read per 16-column tile of A,
       //      W += A^T y_hi (+ A^T y_lo).
@@ -506,26 +456,13 @@ k_tsk_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
     }
     }  // steps 3/4
     if constexpr (PIPE) {
-      if (have && !(ab & 2)) {
+      if (have) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
     }
-    if constexpr (ST) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      SL_STAMP(6)
-    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (ST) {
-    if (lane == 0) {
-      unsigned long long* d = dbg + ((int64_t)blockIdx.x * WAVES + w) * 8;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) d[i] = st_acc[i];
-      d[6] = (unsigned long long)my;
-    }
-  }
-#undef SL_STAMP
 
   // ---- partial slabs: W rows = A columns, layout [WAVES*NW][KP]
   if constexpr (DO_W) {
@@ -658,129 +595,33 @@ int grid_for(int64_t m) {
   return (int)(nb < ncu ? nb : ncu);
 }
 
-int g_x = -1;  // SL_TSK_X bits: 1 top-of-loop prefetch, 2 K = 32 hi/lo step 3, 4 PIPE, 8 nt loads (default 3)
-
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false, int X = 0>
+template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T, bool G64, int X>
 int launch_x(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
-  using GG = Geo<NW, KT, NBUF, (X & 4) ? 2 : 1>;
+  using GG = Geo<NW, KT, NBUF, 1>;
   auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, X>;
   static bool attr = false;
   if (!attr) {
     SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
     attr = true;
   }
-  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy,
-                                             g_ablate | g_flags | ((g_x & 8) ? 64 : 0), nullptr);
+  kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, g_flags);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
-template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, int NBUF, bool HI_T = false,
-          bool G64 = false>
-int launch(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
-           float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
-  if (g_x < 0) {
-    const char* e = getenv("SL_TSK_X");
-    g_x = e ? atoi(e) : 3;
-  }
-  // the K = 32 step 3 needs the W update (DO_W) and a non-split Z
-  // bit 0: top-of-loop prefetch; bit 1: K = 32 hi/lo step 3 (exact passes only:
-  // the hi-only intermediate form costs the same on K = 16)
-  if constexpr (DO_W && !ZSPLIT && KT <= 3) {
-    // bit 2: PIPE (step 3/4 of the previous block between the barriers of the
-    // current one); needs a 3-deep ring and room for the second y buffer
-    constexpr bool PIPE_OK = NBUF >= 3 && Geo<NW, KT, NBUF, 2>::LDS <= 160 * 1024;
-    const int x = (g_x & 3) | ((PIPE_OK && (g_x & 4)) ? 4 : 0);
-#define SL_LX(XX) return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, XX>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s)
-    switch (x) {
-      case 1: SL_LX(1);
-      case 2: if constexpr (!HI_T) { SL_LX(2); } break;
-      case 3: if constexpr (!HI_T) { SL_LX(3); } SL_LX(1);
-      case 4: if constexpr (PIPE_OK) { SL_LX(4); } break;
-      case 5: if constexpr (PIPE_OK) { SL_LX(5); } break;
-      case 6: if constexpr (PIPE_OK && !HI_T) { SL_LX(6); } break;
-      case 7: if constexpr (PIPE_OK) { if constexpr (!HI_T) { SL_LX(7); } SL_LX(5); } break;
-      default: break;
-    }
-#undef SL_LX
-  }
-  return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, 0>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-}
-
-// buffer depth: SL_TSK_NBUF env (A/B tuning), default NBUF_DEFAULT, clamped to the LDS budget
-int g_nbuf = -1;
-
-int nbuf_request() {
-  int& nb = g_nbuf;
-  if (nb < 0) {
-    const char* e = getenv("SL_TSK_NBUF");
-    nb = e ? atoi(e) : NBUF_DEFAULT;
-    if (nb < 2) nb = 2;
-    if (nb > 5) nb = 5;
-  }
-  return nb;
-}
-
+// X bit 0: the prefetch goes out at the top of the iteration; bit 1: the
+// exact step 3 as one K = 32 MFMA per tile over [y_hi | y_lo] (needs the W
+// update, a non-split Z and a non-hi-only pass).  2-deep LDS-DMA ring.
 template <int NW, int KT, bool DO_W, bool DO_G, bool STORE_Y, bool ZSPLIT, bool HI_T = false, bool G64 = false>
 int launch_nb(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
               float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
-  int nb = nbuf_request();
-  constexpr int LIM = 160 * 1024;
-  if (nb >= 5 && Geo<NW, KT, 5>::LDS <= LIM)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 5, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-  if (nb >= 4 && Geo<NW, KT, 4>::LDS <= LIM)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 4, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-  if (nb >= 3)
-    return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 3, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
-  return launch<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, 2, HI_T, G64>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, s);
+  constexpr int X = (DO_W && !ZSPLIT && KT <= 3 && !HI_T) ? 3 : 1;
+  return launch_x<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF_DEFAULT, HI_T, G64, X>(A, m, n, lda, Zt, k, Wslab, Gslab,
+                                                                                   Y, ldy, s);
 }
 
 }  // namespace
-
-// Diagnostic: the headline-shape intermediate (flags 3, no Gram) or final
-// (G64 + Y) pass with per-phase s_memtime sums per wave:
-// dbg[(wg * 8 + wave) * 8 + i], i < 6 = (dma wait, step 1, partial write +
-// barrier 1, reduce + barrier 2, y fragments, step 3/4), 6 = blocks.
-SL_API int sl_tsk_stamp_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
-                             float* Y, unsigned long long* dbg, int final_pass, void* stream) {
-  if (n > 1024 || n <= 512 || k > 48 || k <= 32) return SL_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
-  const bf16_t* a = (const bf16_t*)A;
-  const bf16_t* z = (const bf16_t*)Zt;
-  float* Wslab = (float*)ws;
-  const int g = grid_for(m);
-  float* Gslab = Wslab + (int64_t)g * 1024 * 48;
-  using GG = Geo<128, 3, 3>;
-  if (final_pass) {
-    auto kern = k_tsk_pass<128, 3, true, true, true, false, 3, false, true, 3, true>;
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
-    kern<<<g, THREADS, GG::LDS, s>>>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, k, 0, dbg);
-  } else {
-    auto kern = k_tsk_pass<128, 3, true, false, false, false, 3, true, false, 1, true>;
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
-    kern<<<g, THREADS, GG::LDS, s>>>(a, m, (int)n, lda, z, k, Wslab, nullptr, nullptr, 0, 0, dbg);
-  }
-  SL_LAUNCH_CHECK();
-  return SL_OK;
-}
-
-SL_API int sl_tsk_set_x(int x) {
-  g_x = x;
-  return SL_OK;
-}
-
-SL_API int sl_tsk_set_ablate(int ab) {
-  g_ablate = ab;
-  return SL_OK;
-}
-
-// tuning hook: LDS-DMA ring depth (2..5) for subsequent launches
-SL_API int sl_tsk_set_nbuf(int nb) {
-  g_nbuf = nb < 2 ? 2 : (nb > 5 ? 5 : nb);
-  return SL_OK;
-}
 
 // workspace bytes needed by sl_tsk_fused_pass
 SL_API int64_t sl_tsk_fused_workspace(int64_t m, int64_t n, int k) {
@@ -817,7 +658,7 @@ SL_API int sl_tsk_fused_pass(const void* A, int64_t m, int64_t n, int64_t lda, c
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
   g_flags = ((flags & 1) ? 8 : 0) | ((flags & 2) ? 32 : 0) | ((flags & 32) ? 128 : 0) |
-            ((Y && (k & 3) == 0 && (ldy & 3) == 0 && ((uintptr_t)Y & 15) == 0 && !(g_x & 4)) ? 256 : 0);
+            ((Y && (k & 3) == 0 && (ldy & 3) == 0 && ((uintptr_t)Y & 15) == 0) ? 256 : 0);
   // intermediate power-iteration passes (no Gram, bf16 y): compile-time specialisation
   const bool inter = (flags & 3) == 3 && !Y;
   // final pass whose Gram is taken separately (fp64 Gram of the stored Y)

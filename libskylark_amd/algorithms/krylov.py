@@ -199,7 +199,10 @@ def lsqr(A, B, X=None, params: KrylovIterParams | None = None, R: Precond | None
 
     fused = params.fused_normal
     if fused is None:
-        fused = op.has_fused_normal(k)
+        # the n-space recurrence T = (G - alpha T) / beta scales its error by
+        # alpha / beta every step: only on by default for a preconditioned
+        # (well-conditioned) system, where that ratio stays near one
+        fused = op.has_fused_normal(k) and not isinstance(R, IdPrecond)
     refresh = 16 if params.refresh_every is None else max(0, int(params.refresh_every))
     beta = op.long_colnorm(U)
     U = U / beta.clamp_min(torch.finfo(dt).tiny)

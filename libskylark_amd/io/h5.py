@@ -175,6 +175,8 @@ class _Reader:
 
         def name_at(o):
             e = d.find(b"\x00", hdata + o)
+            if e < 0:
+                raise H5Error("unterminated link name in the local heap")
             return d[hdata + o:e].decode()
 
         def walk(node):

@@ -185,7 +185,7 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
     from ..ops import tallskinny as T
 
-    if A_loc.is_cuda and work == torch.float32 and T._native_ok(A_loc, k):
+    if A_loc.is_cuda and work == torch.float32 and A_loc.dtype == torch.bfloat16:
         res = _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params)
         if res is not None:
             U_loc, s, V = res
@@ -270,435 +270,163 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     return U_loc, s, V
 
 
-class _DevicePlan:
-    """Device randSVD for one (A, k, rank, q) configuration, replayed as two
-    hipGraphs once warm (``ApproximateSVDParams.graph``).
+vp_, i32_, i64_, u64_, f64_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 
-    Segment 1 (sketch Z -> power passes -> final pass -> fp64 Gram and
-    CholeskyQR of Y -> k x k Gram of A^T Q) and segment 2 (V and the k x r
-    map of U from the host eigensolve) are each one graph: the ~30 launches
-    per call collapse into two replays, so the short kernels between the
-    streaming passes no longer wait on host launch latency.  Graph inputs are
-    static buffers (the sketch Z and the eigenpairs); A is read in place, so
-    replays always see A's current contents.  The small outputs (s, V) are
-    cloned out of graph memory; U = Y M is one eager launch into a fresh
-    tensor (no m x r copy).  With more than
-    one rank segment 1 is split at its all-reduces: each piece is its own
-    graph and the collectives run eagerly between the replays (no RCCL
-    capture); if a capture fails the plan stays eager.
-    """
 
-    def __init__(self, A_loc, comm, n, rank, k, q, skip_qr, use_graph):
-        from ..ops import tallskinny as T
-        dev = A_loc.device
+_ENGINE_REG = [False]
+
+
+def _engine_lib():
+    from ..ops import _lib
+    if not _ENGINE_REG[0]:
+        _ENGINE_REG[0] = True
+        _lib.register("sl_rsvd_plan_create", [i64_, i64_, i64_, i32_, i32_, i32_, ctypes.POINTER(vp_)])
+        _lib.register("sl_rsvd_plan_destroy", [vp_])
+        _lib.register("sl_rsvd_set_fjlt", [vp_, u64_, u64_, u64_, f64_, vp_])
+        _lib.register("sl_rsvd_set_zt", [vp_, vp_, vp_])
+        _lib.register("sl_rsvd_segment", [vp_, vp_, i32_, vp_])
+        _lib.register("sl_rsvd_reduce_buffer", [vp_], vp_)
+        _lib.register("sl_rsvd_finish", [vp_, vp_, i64_, vp_, vp_, vp_])
+        _lib.register("sl_rsvd_run", [vp_, vp_, i32_, vp_, i64_, vp_, vp_, vp_])
+        _lib.register("sl_rsvd_plan_bind", [vp_, vp_, vp_])
+    return _lib
+
+
+# status bits of a device call (rsvd_core.hip)
+ST_PIVOT, ST_NONFINITE, ST_NOCONV, ST_RANK = 1, 2, 4, 8
+
+
+class _EnginePlan:
+    """Device randSVD for one (A, k, rank, q) configuration on the C++ engine
+    (``_native/src/rsvd_engine.cpp``): every stage of the call -- sketch
+    operator, q + 1 fused passes, the CholeskyQRs between them, the fp64
+    core (Cholesky, C = Rt^-T W^T W Rt^-1, Jacobi eigensolve) and the
+    U = Y M / V = W N finish -- runs on the GPU; nothing returns to the host
+    inside a call.
+
+    One rank: one ctypes call replays the engine's own hipGraph of the
+    segments and launches the finish into fresh U / s / V tensors.  Several
+    ranks: the engine's segments with ``comm.all_reduce`` of the [W; G]
+    buffer between them; when every all-reduce is the one-shot IPC kernel
+    the segments and collectives are captured as one torch CUDA graph.
+
+    The device status word (pivot dropped, non-finite data, no Jacobi
+    convergence, rank < r) is copied back asynchronously; a flag of a call
+    is reported by the next one (``last_status``), never by a host sync."""
+
+    def __init__(self, A_loc, comm, n, rank, k, q, use_graph):
+        L = _engine_lib()
         m = A_loc.shape[0]
-        # weak: a cached plan must not keep a multi-GB operand alive
+        self.dev = A_loc.device
         self.Aref = weakref.ref(A_loc)
-        self.dev = dev
-        self.comm, self.n, self.rank, self.k, self.q, self.skip_qr = comm, n, rank, k, q, skip_qr
-        self.Zs = torch.empty(n, k, dtype=torch.float32, device=dev)
-        # the fused pass's operand in its bf16 k x n layout, written in place by
-        # the FJLT realisation and by each CholeskyQR step (no cast/transpose
-        # launches between the passes)
-        self.Zt = torch.empty(k, n, dtype=torch.bfloat16, device=dev)
-        # [W; G] of the final pass, reduced straight into one f64 buffer
-        self.WG = torch.empty(n + k, k, dtype=torch.float64, device=dev)
-        # FJLT sketches are realised inside segment 1 from device-held stream
-        # coordinates {seed, base_D, base_samples} (ops.fut.fjlt_operator)
-        self.prm = torch.zeros(3, dtype=torch.int64, device=dev)
-        self.prm_host = torch.zeros(3, dtype=torch.int64).pin_memory()
-        self.fjlt_scale = None
-        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.small = torch.zeros(k * rank + rank, dtype=torch.float64, device=dev)
-        self.small_host = torch.zeros(k * rank + rank, dtype=torch.float64).pin_memory()
-        self.small_np = self.small_host.numpy()
-        self.host_pin = self.host_ev = None
-        self.ws = torch.empty(T.fused_workspace_bytes(m, n, k), dtype=torch.uint8, device=dev)
-        self.ws32 = torch.empty(max(T.f32_workspace_bytes(m), T.f32_workspace_bytes(n)), dtype=torch.uint8,
-                                device=dev)
-        # k x k eigensolve on the device (sym_eig.hip tridiagonal path): the
-        # whole call is then one graph with no host round trip; status bit 1
-        # sends that call's eigensolve back to host LAPACK.  Opt-in: measured
-        # 178 us for k = 40 (serial f64 division chains on one CU) against
-        # ~70 us host LAPACK + ~60 us of round trip (profiles/eig_device_r2.jsonl)
-        self.dev_eig = (k <= 64 and rank <= 32 and os.environ.get("SL_SVD_DEVICE_EIG", "0") == "1"
-                        and dev.type == "cuda")
-        self.eig_status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.comm, self.n, self.rank, self.k, self.q = comm, n, rank, k, q
+        self.m = m
         self.use_graph = use_graph
-        # alternate row directions across passes (Infinity-Cache reuse; measured
-        # no gain: 1.77 vs 1.78 ms)
-        self.snake = os.environ.get("SL_SVD_SNAKE", "0") == "1"
-        # final pass: fp64 Gram of Y inside the pass (default) or by a separate
-        # streaming kernel after a Gram-free pass (SL_SVD_SPLIT_GRAM=1; measured
-        # equal under rocprof: 551 + 73 + 10 vs 624 + 5 us)
-        self.split_gram = os.environ.get("SL_SVD_SPLIT_GRAM", "0") == "1"
-        self.ws32g = torch.empty(T.gram64_workspace_bytes(m, k), dtype=torch.uint8, device=dev) \
-            if self.split_gram else None
-        self._xm_fn = None
-        self._fu_fn = None
-        self.g1 = self.g2 = None
-        self.piece_graphs = None   # multi-rank: per-piece graphs (False: capture failed)
-        self._Wout = [None] * (q + 1)
+        h = ctypes.c_void_p()
+        L.call("sl_rsvd_plan_create", m, n, A_loc.stride(0), k, rank, q, ctypes.byref(h))
+        self.h = h
+        self._fin = weakref.finalize(self, _destroy_plan, h.value)
+        # [W (n x k); G (k x k)] f64 reduce buffer (all-reduced across ranks
+        # between the segments) and the device status word, torch-owned
+        self.WG = torch.empty((n + k) * k, dtype=torch.float64, device=self.dev)
+        self.status_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        L.call("sl_rsvd_plan_bind", h, ctypes.c_void_p(self.WG.data_ptr()), ctypes.c_void_p(self.status_dev.data_ptr()))
+        self.status_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.status_ev = None
+        self.last_status = 0
         self.calls = 0
-
-    # ---- segment 1 as pieces separated by the collectives: with one rank the
-    # pieces are captured into one graph; with several, each piece is its own
-    # graph and the all-reduces run eagerly between replays, so multi-GPU
-    # steps replay ~5 graphs instead of launching ~35 kernels from Python.
-    def _piece_pass(self, i):
-        from ..ops import small_la as SL
-        from ..ops import tallskinny as T
-        prof = PROFILER
-        A = self.Aref()
-        if i == 0:
-            self.status.zero_()
-            if self.dev_eig:
-                self.eig_status.zero_()
-            if self.fjlt_scale is not None:
-                from ..ops import fut as F
-                with prof.phase("svd.sketch"):
-                    F.fjlt_operator(self.prm, self.k, self.n, self.fjlt_scale, self.Zt, transpose=False)
-            else:
-                self.Zt.copy_(self.Zs.t())
-            Z = None
-        else:
-            with prof.phase("svd.orth"):
-                # only the subspace matters between passes: one CholeskyQR step
-                W = self._Wout[i - 1]
-                if self.skip_qr:
-                    self.Zt.copy_((W / W.norm(dim=0, keepdim=True).clamp_min(1e-30)).t())
-                else:
-                    SL.cholqr(W, self.status, ws=self.ws32, zt_out=self.Zt)
-                Z = None
-        if i < self.q:
-            with prof.phase("svd.fused_pass"):
-                # every piece writes its own output slot: a piece's capture then
-                # reads its predecessor's graph-owned result, never its own warm-up's
-                # odd passes walk the rows backwards: each pass starts on the
-                # rows the previous one read last (Infinity-Cache resident)
-                self._Wout[i], _, _ = T.fused_pass(A, Z, keep_y=False, gram=False, exact=False, ws=self.ws,
-                                                   zt=self.Zt, reverse=self.snake and i % 2 == 1)
-            return self._Wout[i]
-        with prof.phase("svd.fused_pass"):
-            # fp64 Gram of the f32 Y on the f64 matrix cores, formed inside the
-            # same pass (no second read of Y): one fp64 CholeskyQR then leaves
-            # Q = Y R^{-1} orthogonal to ~kappa(Y)^2 eps64 (CholeskyQR2 with an
-            # f32 second Gram only reached ~eps32, at three times the work);
-            # W (f64) and G land in the [W; G] buffer the all-reduce takes
-            if self.split_gram:
-                # the pass without its Gram specialisation (~160 us faster at
-                # 1e6 x 1e3), then the fp64 Gram of the stored f32 Y by its own
-                # streaming kernel (~80 us) straight into [W; G]
-                _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=False, exact=True, ws=self.ws, zt=self.Zt,
-                                       wg_out=self.WG, reverse=self.snake and i % 2 == 1)
-                T.gram64(Y, ws=self.ws32g, out=self.WG[self.n:])
-            else:
-                _, _, Y = T.fused_pass(A, Z, keep_y=True, gram=True, exact=True, ws=self.ws, gram64=True,
-                                       zt=self.Zt, wg_out=self.WG, reverse=self.snake and i % 2 == 1)
-        self._WG = self.WG
-        self.Y = Y
-        return self._WG
-
-    def _piece_core(self):
-        from ..ops import small_la as SL
-        n = self.n
-        W, G = self._WG[:n], self._WG[n:]
-        with PROFILER.phase("svd.final_qr"):
-            _, Rti, _ = SL.chol_inv(G, self.status)
-            # B^T = A^T Q = W Rt^{-1} (n x k); its right singular pairs come from the
-            # k x k f64 Gram C = Rt^{-T} (W^T W) Rt^{-1} = Ub S^2 Ub^T (host eigensolve).
-            # sigma_i keeps relative accuracy ~eps64 (sigma_1/sigma_i)^2, far below
-            # the bf16 data error for every rank the sketch resolves.
-            # svd_core.hip: Vt = W Rt^{-1} and the symmetric C, staged with the
-            # breakdown status as [C | status] (2 launches)
-            Vt, self.host_src = SL.svd_core(W, Rti, self.status)
-        self.Rti, self.Vt = Rti, Vt
-        if self.dev_eig:
-            with PROFILER.phase("svd.eig"):
-                SL.sym_eig_tridiag(self.host_src, self.rank, out=self.small, sqrt=True, status=self.eig_status,
-                                   ldc=self.k)
-            self.seg2()
-
-    def pieces(self):
-        """[(graph-able piece, tensor to all-reduce after it or None)]"""
-        out = [(lambda i=i: self._piece_pass(i), True) for i in range(self.q + 1)]
-        out.append((self._piece_core, False))
-        return out
-
-    def seg1(self):
-        with PROFILER.phase("svd.allreduce_small"):
-            pass
-        for fn, reduce_after in self.pieces():
-            t = fn()
-            if reduce_after:
-                with PROFILER.phase("svd.allreduce_small"):
-                    self.comm.all_reduce(t)
-
-    def seg2(self):
-        from ..ops import small_la as SL
-        r = self.rank
-        with PROFILER.phase("svd.form_U"):
-            # V = A^T Q Ub S^{-1} = Vt Ub S^{-1};  U = Y M with M = Rt^{-1} Ub (one launch)
-            self.V, self.M, self.s = SL.svd_finish(self.Vt, self.Rti, self.small, r)
-
-    def _collectives_capturable(self):
-        """True once this communicator's one-shot path holds every operand the
-        segment all-reduces (set up by the first, eager call)."""
-        os_ = getattr(self.comm, "_oneshot", None)
-        if not os_ or self.calls < 1:
-            return False
-        outs = [w for w in self._Wout if w is not None] + [self.WG]
-        return all(os_.fits(t) for t in outs)
+        self.g = None          # multi-rank: torch graph of segments + one-shot all-reduces
+        self.g_failed = False
 
     def graph_built(self):
-        return self.g1 is not None or bool(self.piece_graphs)
+        return self.calls >= 2 and self.use_graph
 
-    def reset_graphs(self):
-        self.g1 = self.g2 = None
-        self.piece_graphs = None
-        self.calls = 0
+    def _segments(self, A):
+        L = _engine_lib()
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        for i in range(self.q + 2):
+            with PROFILER.phase("svd.segment"):
+                L.call("sl_rsvd_segment", self.h, ctypes.c_void_p(A.data_ptr()), i, st)
+            if i <= self.q:
+                cnt = (self.n + self.k if i == self.q else self.n) * self.k
+                with PROFILER.phase("svd.allreduce_small"):
+                    self.comm.all_reduce(self.WG[:cnt])
 
-    def _finish_u_ok(self):
-        Y = self.Y
-        return (not PROFILER.enabled and Y is not None and Y.is_cuda and Y.dtype == torch.float32
-                and Y.is_contiguous() and self.Vt.is_contiguous() and self.Rti.is_contiguous())
+    def _collectives_capturable(self):
+        os_ = getattr(self.comm, "_oneshot", None)
+        return bool(os_) and self.calls >= 1 and os_.fits(self.WG)
 
-    def _finish_u(self):
-        if self._fu_fn is None:
-            from ..ops import _lib
-            fn = getattr(_lib.require(), "sl_svd_finish_u")
-            P, I, L = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
-            fn.argtypes = [P, I, I, P, P, I, P, P, P, P, L, P, P]
-            fn.restype = ctypes.c_int
-            self._fu_fn = fn
-        n, k = self.Vt.shape
-        r = self.rank
-        m = self.Y.shape[0]
+    def __call__(self, A, Z=None, fjlt=None):
+        L = _engine_lib()
         dev = self.dev
-        V = torch.empty(n, r, dtype=torch.float32, device=dev)
-        M = torch.empty(k, r, dtype=torch.float32, device=dev)
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        self._poll_status()
+        if fjlt is not None:
+            L.call("sl_rsvd_set_fjlt", self.h, int(fjlt[0]), int(fjlt[1]), int(fjlt[2]), float(fjlt[3]), st)
+        else:
+            Zt = Z.t().to(torch.bfloat16).contiguous()
+            L.call("sl_rsvd_set_zt", self.h, ctypes.c_void_p(Zt.data_ptr()), st)
+        r = self.rank
+        U = torch.empty(self.m, r, dtype=torch.float32, device=dev)
         s = torch.empty(r, dtype=torch.float32, device=dev)
-        U = torch.empty(m, r, dtype=torch.float32, device=dev)
-        rc = self._fu_fn(self.Vt.data_ptr(), n, k, self.Rti.data_ptr(), self.small.data_ptr(), r, V.data_ptr(),
-                         M.data_ptr(), s.data_ptr(), self.Y.data_ptr(), m, U.data_ptr(),
-                         torch.cuda.current_stream(dev).cuda_stream)
-        if rc != 0:
-            from ..ops import _lib
-            _lib.call("sl_svd_finish", _lib.ptr(self.Vt), n, k, _lib.ptr(self.Rti), _lib.ptr(self.small), r,
-                      _lib.ptr(V), _lib.ptr(M), _lib.ptr(s), ctypes.c_void_p(_lib.stream_of(V)))
-            from ..ops import tallskinny as T
-            U = T.f32_xm(self.Y, M, store=True)[0]
+        V = torch.empty(self.n, r, dtype=torch.float32, device=dev)
+        warm = self.use_graph and self.calls >= 1 and not PROFILER.enabled
+        if self.comm.size == 1:
+            L.call("sl_rsvd_run", self.h, ctypes.c_void_p(A.data_ptr()), 1 if warm else 0,
+                   ctypes.c_void_p(U.data_ptr()), r, ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(V.data_ptr()), st)
+        else:
+            if warm and self.g is None and not self.g_failed and self._collectives_capturable():
+                try:
+                    g = torch.cuda.CUDAGraph()
+                    side = torch.cuda.Stream(device=dev)
+                    side.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+                        self._segments(A)
+                    torch.cuda.current_stream(dev).wait_stream(side)
+                    self.g = g
+                except Exception:  # noqa: BLE001 - capture unsupported here: stay eager
+                    self.g, self.g_failed = None, True
+            if self.g is not None:
+                self.g.replay()
+            else:
+                self._segments(A)
+            with PROFILER.phase("svd.form_U"):
+                L.call("sl_rsvd_finish", self.h, ctypes.c_void_p(U.data_ptr()), r, ctypes.c_void_p(s.data_ptr()),
+                       ctypes.c_void_p(V.data_ptr()), st)
+        # status word of this call back to the host, no wait
+        if self.status_ev is None:
+            self.status_ev = torch.cuda.Event()
+        self.status_host.copy_(self.status_dev, non_blocking=True)
+        self.status_ev.record()
+        self.calls += 1
         return U, s, V
 
-    def _form_u(self):
-        """U = Y M (m x r f32) with the launch arguments bound once: this launch
-        sits between the second replay and the end of the call, so its
-        Python overhead is on the critical path (~25 -> ~8 us)."""
-        from ..ops import tallskinny as T
-        Y, M = self.Y, self.M
-        if not (Y.is_cuda and Y.is_contiguous() and M.is_contiguous() and M.dtype == torch.float32):
-            return T.f32_xm(Y, M, store=True)[0]
-        if self._xm_fn is None:
-            from ..ops import _lib
-            T.f32_xm  # noqa: B018 - registers the signature
-            fn = getattr(_lib.require(), "sl_tsk_f32_xm")
-            if fn.argtypes is None:
-                fn.argtypes = _lib.SIGNATURES["sl_tsk_f32_xm"]
-                fn.restype = ctypes.c_int
-            self._xm_fn = fn
-        m, k = Y.shape
-        r = M.shape[1]
-        U = torch.empty(m, r, dtype=torch.float32, device=self.dev)
-        rc = self._xm_fn(Y.data_ptr(), m, k, k, M.data_ptr(), r, U.data_ptr(), r, None, None,
-                         torch.cuda.current_stream(self.dev).cuda_stream)
-        if rc != 0:
-            return T.f32_xm(Y, M, store=True)[0]
-        return U
+    def _poll_status(self):
+        if self.status_ev is not None and self.status_ev.query():
+            self.last_status = int(self.status_host[0])
+            if self.last_status & (ST_NONFINITE | ST_RANK | ST_NOCONV):
+                import warnings
+                warnings.warn(f"approximate_svd (device): previous call flagged status {self.last_status} "
+                              "(2: non-finite data, 4: eigensolver not converged, 8: numerical rank < r)",
+                              RuntimeWarning, stacklevel=3)
 
-    def _capture(self, fn, want_out=False):
-        s = torch.cuda.Stream(device=self.dev)
-        s.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(s):
-            fn()
-        torch.cuda.current_stream(self.dev).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        # thread-local capture: with RCCL the process group's watchdog thread
-        # polls events concurrently, which a global-mode capture would reject
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            out = fn()
-        return (g, out) if want_out else g
-
-    def _run(self, which):
-        fn = self.seg1 if which == 1 else self.seg2
-        g = self.g1 if which == 1 else self.g2
-        warm = self.use_graph and self.calls >= 1 and not PROFILER.enabled
-        if which == 1 and self.comm.size > 1 and self._collectives_capturable():
-            # every all-reduce of segment 1 is the one-shot kernel
-            # (parallel/oneshot.py): the whole segment, collectives included,
-            # is one graph, as with a single rank
-            pass
-        elif which == 1 and self.comm.size > 1 and self.piece_graphs is not False:
-            # multi-rank: one graph per piece, eager collectives in between
-            if self.piece_graphs is None and warm:
-                try:
-                    self.piece_graphs = [(*self._capture(f, want_out=True), r) for f, r in self.pieces()]
-                except Exception:  # noqa: BLE001 - capture unsupported here: stay eager
-                    self.piece_graphs = False
-            if self.piece_graphs:
-                for gp, out, reduce_after in self.piece_graphs:
-                    gp.replay()
-                    if reduce_after:
-                        with PROFILER.phase("svd.allreduce_small"):
-                            self.comm.all_reduce(out)
-                return
-            fn()
-            return
-        if g is None and warm:
-            try:
-                g = self._capture(fn)
-            except Exception:  # noqa: BLE001 - capture unsupported here: stay eager
-                self.use_graph, g = False, None
-            if which == 1:
-                self.g1 = g
-            else:
-                self.g2 = g
-        if g is not None:
-            g.replay()
-        else:
-            fn()
-
-    def __call__(self, Z=None, fjlt=None):
-        """``Z``: realised sketch operator (n x k), or ``fjlt`` = (seed, base_D,
-        base_samples, scale) to realise an FJLT inside the graph."""
-        if fjlt is not None:
-            if self.fjlt_scale is None and self.graph_built():
-                self.reset_graphs()
-            self.fjlt_scale = float(fjlt[3])
-            # pinned + non_blocking (no host wait): the previous call's copy of
-            # this buffer finished before that call's synchronising D2H
-            self.prm_host[0], self.prm_host[1], self.prm_host[2] = int(fjlt[0]), int(fjlt[1]), int(fjlt[2])
-            self.prm.copy_(self.prm_host, non_blocking=True)
-        else:
-            if self.fjlt_scale is not None:
-                self.fjlt_scale = None
-                self.reset_graphs()
-            self.Zs.copy_(Z)
-        tr = _TRACE and [time.perf_counter()]
-        self._run(1)
-        if self.dev_eig:
-            from ..ops import tallskinny as T
-            with PROFILER.phase("svd.form_U"):
-                U, _ = T.f32_xm(self.Y, self.M, store=True)
-            if not int(self.eig_status.item()):
-                self.calls += 1
-                if tr:
-                    tr.append(time.perf_counter())
-                    print(f"[svd.trace] device_eig call={(tr[1] - tr[0]) * 1e6:.0f}us", file=sys.stderr)
-                return U, self.s.clone(), self.V.clone()
-            # flagged (near-repeated eigenvalues, non-finite data or a vanishing
-            # r-th eigenvalue): this call's k x k eigensolve goes to host LAPACK
-        tr and tr.append(time.perf_counter())
-        # [C | status] into a pinned buffer; wait for that copy only
-        if self.host_pin is None:
-            self.host_pin = torch.empty(self.host_src.numel(), dtype=torch.float64).pin_memory()
-            self.host_np = self.host_pin.numpy()
-            self.host_ev = torch.cuda.Event()
-        self.host_pin.copy_(self.host_src, non_blocking=True)
-        self.host_ev.record()
-        self.host_ev.synchronize()
-        host = self.host_pin
-        tr and tr.append(time.perf_counter())
-        k, r = self.k, self.rank
-        # host[-1] != 0: a CholeskyQR pivot was dropped (rank-deficient block --
-        # e.g. an FJLT that sampled the same row twice, or a low-rank A); the
-        # dropped direction is an exactly-zero column from then on, harmless
-        # while at least r directions survive.  Non-finite data or fewer than
-        # r surviving directions send the call to the robust host path.
-        # numpy views of the pinned buffers: no torch dispatch on this path
-        Cm = self.host_np[:k * k].reshape(k, k)
-        if not np.isfinite(Cm).all():
-            return None
-        # C is exactly symmetric (svd_core.hip); eigh returns ascending eigenpairs
-        got = _host_eigh_np(Cm)
-        if got is None:
-            return None
-        evals, evecs = got
-        if not evals[k - r] > 1e-30 * max(evals[-1], 1e-300):
-            return None
-        pin = self.small_np
-        pin[:k * r].reshape(k, r)[:] = evecs[:, ::-1][:, :r]
-        np.sqrt(np.maximum(evals[::-1][:r], 0.0), out=pin[k * r:])
-        tr and tr.append(time.perf_counter())
-        # pinned + non_blocking: the copy is ordered on the stream, the host
-        # does not wait (the buffer is rewritten only after the next call's
-        # synchronising D2H, which follows this copy in stream order)
-        self.small.copy_(self.small_host, non_blocking=True)
-        tr and tr.append(time.perf_counter())
-        from ..ops import small_la as SL
-        from ..ops import tallskinny as T
-        if self.dev_eig:
-            # eager, into fresh tensors: the graph's own V / M / s buffers stay
-            # bound to the device-eigensolver variant captured in segment 1
-            V, M, s = SL.svd_finish(self.Vt, self.Rti, self.small, r)
-            U, _ = T.f32_xm(self.Y, M, store=True)
-            self.calls += 1
-            return U, s, V
-        if self._finish_u_ok():
-            # V, M, s and U = Y M into fresh tensors from ONE host call (two
-            # launches): no second graph replay, no clones out of graph memory
-            out = self._finish_u()
-            tr and tr.append(time.perf_counter())
-            self.calls += 1
-        else:
-            self._run(2)
-            tr and tr.append(time.perf_counter())
-            self.calls += 1
-            with PROFILER.phase("svd.form_U"):
-                # outside the graph: U lands in a fresh allocation, so the m x r
-                # result needs no copy out of the graph's static memory
-                U = self._form_u()
-            out = U, self.s.clone(), self.V.clone()
-        if tr:
-            tr.append(time.perf_counter())
-            names = ["replay1", "d2h_sync", "eigh", "h2d", "replay2", "form_U"]
-            print("[svd.trace] " + " ".join(f"{n}={(b - a) * 1e6:.0f}us" for n, a, b in zip(names, tr, tr[1:])),
-                  file=sys.stderr)
-        return out
+    def wait_status(self) -> int:
+        """Synchronise with the last call and return its status bits."""
+        if self.status_ev is not None:
+            self.status_ev.synchronize()
+            self.last_status = int(self.status_host[0])
+        return self.last_status
 
 
-_EIG_BACKEND = os.environ.get("SL_HOST_EIG", "torch")
-
-
-def _host_eigh_np(C: np.ndarray):
-    """(w ascending, V) of a small symmetric f64 matrix (numpy in / out), or
-    None on a LAPACK failure.  ``SL_HOST_EIG`` picks the LAPACK route:
-    "torch" (single-threaded torch.linalg.eigh on a zero-copy view, the
-    measured fastest), "scipy" (dsyevd through scipy.linalg.lapack) or
-    "numpy"."""
-    if _EIG_BACKEND == "scipy":
-        from scipy.linalg import lapack
-        w, v, info = lapack.dsyevd(C, compute_v=1, lower=0)
-        return (w, v) if info == 0 else None
-    if _EIG_BACKEND == "numpy":
-        return np.linalg.eigh(C)
-    w, v = _host_eigh(torch.from_numpy(C))
-    return w.numpy(), v.numpy()
-
-
-def _host_eigh(C: torch.Tensor):
-    """LAPACK eigh of the k x k core on ONE host thread: for k ~ 40 the
-    threaded BLAS costs 2-4x more than it saves (measured 177 us single
-    threaded vs 290-700 us threaded on the build host).  A device Jacobi
-    (ops.small_la.sym_eig_topr) was measured at ~500 us for k = 40, so the
-    host solve stays on the randSVD critical path."""
-    n = torch.get_num_threads()
-    if n == 1:
-        return torch.linalg.eigh(C)
-    torch.set_num_threads(1)
+def _destroy_plan(ptr):
     try:
-        return torch.linalg.eigh(C)
-    finally:
-        torch.set_num_threads(n)
+        from ..ops import _lib
+        lib = _lib.load(build_if_missing=False)
+        if lib is not None and ptr:
+            torch.cuda.synchronize()
+            lib.sl_rsvd_plan_destroy(ctypes.c_void_p(ptr))
+    except Exception:  # noqa: BLE001 - interpreter shutdown
+        pass
 
 
 _PLANS: dict = {}
@@ -706,46 +434,53 @@ _TRACE = os.environ.get("SKH_TRACE_SVD", "0") == "1"   # host-side phase timesta
 _T0 = [0.0]
 
 
-def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
-    """GPU-resident path (bf16 A on gfx950): every iteration stays on the device;
-    one host synchronisation per call (the k x k eigensolve + status check).
+def _engine_ok(A_loc, n, k) -> bool:
+    return (A_loc.is_cuda and A_loc.dtype == torch.bfloat16 and A_loc.stride(1) == 1 and A_loc.stride(0) % 8 == 0
+            and n % 8 == 0 and 16 <= n <= 1024 and 1 <= k <= 48)
 
-    Returns None when a Cholesky breakdown was flagged (the caller then reruns
-    the robust host path with the same, rewound, context)."""
+
+def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
+    """GPU-resident path (bf16 A on gfx950): the C++ engine runs the whole
+    call; no host synchronisation inside it.  Returns None when the engine
+    does not cover the shape (the caller then runs the host-driven path)."""
+    if not _engine_ok(A_loc, n, k):
+        return None
     if _TRACE:
         print(f"[svd.trace] python_prep={(time.perf_counter() - _T0[0]) * 1e6:.0f}us", file=sys.stderr)
-    ctx0 = ctx.copy()
     dev = A_loc.device
     fjlt = None
+    Z = None
     if params.sketch.upper() == "FJLT":
         # FJLT_data draw layout: N Rademacher signs, then S sample rows; the
-        # operator itself is realised on the device inside the plan's graph
+        # operator itself is realised on the device by the engine
         base_d = ctx.counter
         base_s = base_d + n
         ctx.counter = base_s + k
         fjlt = (ctx.seed, base_d, base_s, math.sqrt(n / k))
-        Z = None
     else:
         with PROFILER.phase("svd.sketch"):
             Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float32)
     q = max(0, int(params.num_iterations))
-    key = (A_loc.data_ptr(), tuple(A_loc.shape), tuple(A_loc.stride()), A_loc.dtype, str(dev), rank, k, q,
-           bool(params.skip_qr), comm.size, id(getattr(comm, "group", None)))
+    key = (A_loc.data_ptr(), tuple(A_loc.shape), tuple(A_loc.stride()), str(dev), rank, k, q, comm.size,
+           id(getattr(comm, "group", None)))
     plan = _PLANS.get(key)
     if plan is not None and plan.Aref() is None:
         plan = None  # the operand this plan was built for is gone
     if plan is None:
         if len(_PLANS) >= 4:
             _PLANS.pop(next(iter(_PLANS)))
-        # multi-rank: capture collectives only on request — a capture that fails on
-        # one rank but not another would desynchronise the collectives
-        use_graph = bool(params.graph) and dev.type == "cuda"
-        plan = _DevicePlan(A_loc, comm, n, rank, k, q, params.skip_qr, use_graph)
+        plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
         _PLANS[key] = plan
-    res = plan(Z, fjlt=fjlt)
-    if res is None:
-        ctx.seed, ctx.counter = ctx0.seed, ctx0.counter
-    return res
+    return plan(A_loc, Z=Z, fjlt=fjlt)
+
+
+def last_device_status(wait: bool = True) -> int:
+    """Status bits of the most recent device randSVD call (0 = clean; see
+    ``ST_*``)."""
+    if not _PLANS:
+        return 0
+    plan = list(_PLANS.values())[-1]
+    return plan.wait_status() if wait else plan.last_status
 
 
 # ------------------------------------------------------- host small LA (fp64)

@@ -33,8 +33,10 @@ def native_ok(A: torch.Tensor, k: int) -> bool:
 
 
 def _ws(A, n, k):
+    """Slab workspace per (device, stream): launches on different streams
+    (side-stream overlap, concurrent solvers) never share scratch."""
     nb = int(_lib.require().sl_ata_workspace(n, k))
-    key = str(A.device)
+    key = (str(A.device), torch.cuda.current_stream(A.device).cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() < nb:
         ws = _WS[key] = torch.empty(nb, dtype=torch.uint8, device=A.device)

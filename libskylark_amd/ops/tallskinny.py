@@ -24,11 +24,6 @@ vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_tsk_fused_pass", [vp, i64, i64, i64, vp, i32, vp, vp, vp, i64, vp, i32, vp])
 _lib.register("sl_tsk_fused_workspace", [i64, i64, i32], C.c_int64)
 _lib.register("sl_tsk_matmul", [vp, i64, i64, i64, vp, i32, vp, i64, i32, vp])
-_lib.register("sl_tsk2_fused_pass", [vp, i64, i64, i64, vp, i32, vp, vp, vp, i64, vp, i64, i32, vp])
-_lib.register("sl_tsk2_set_tuning", [i32, i32])
-_lib.register("sl_tsk3_fused_pass", [vp, i64, i64, i64, vp, i32, vp, vp, vp, i64, vp, i64, i32, vp])
-_lib.register("sl_tsk3_set_tuning", [i32])
-_lib.register("sl_tsk_set_x", [i32])
 
 # rows per chunk in the torch fallback (bounds the y temporary)
 CHUNK_ROWS = 1 << 16

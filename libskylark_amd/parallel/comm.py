@@ -113,6 +113,21 @@ class Comm:
             self._count(2 * t.numel() * t.element_size() * (self.size - 1) // self.size)
         return t
 
+    def check_collectives(self):
+        """Raise if an asynchronous collective of this communicator failed
+        (a one-shot all-reduce whose peer missed the timeout)."""
+        os_ = getattr(self, "_oneshot", None)
+        if os_:
+            os_.check()
+
+    def close(self):
+        """Release this communicator's one-shot IPC buffers collectively
+        (barrier before any rank frees a buffer its peers map)."""
+        os_ = getattr(self, "_oneshot", None)
+        if os_:
+            os_.close(self)
+        self._oneshot = None
+
     def all_reduce_max(self, t):
         return self.all_reduce(t, op=dist.ReduceOp.MAX)
 

@@ -122,27 +122,54 @@ class OneShotAllReduce:
         return (self.ok and t.is_cuda and t.device == self.dev and t.dtype in (torch.float32, torch.float64)
                 and t.is_contiguous() and t.numel() * t.element_size() <= self.cap)
 
-    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum of ``t`` over the ranks (stream-ordered, no host sync)."""
+    def all_reduce(self, t: torch.Tensor, timeout_s: float | None = None) -> torch.Tensor:
+        """In-place sum of ``t`` over the ranks (stream-ordered, no host sync).
+
+        A peer later than the timeout leaves NaN in ``t`` on the waiting rank
+        (never a silent partial sum) and sets the error word; the error word
+        is copied back asynchronously after every eager call and a flagged
+        earlier call raises :class:`OneShotError` at the next one
+        (:meth:`check` raises synchronously)."""
         if not self.fits(t):
             raise OneShotError("one-shot all-reduce: operand does not fit this buffer")
+        self._poll()
         _lib.call("sl_oneshot_allreduce", _lib.ptr(t), t.numel(), _lib.dtype_code(t.dtype), self.rank, self.p,
-                  _lib.ptr(self.bases), self.cap, _lib.ptr(self.state), _lib.ptr(self.err), float(TIMEOUT_S),
-                  vp(_lib.stream_of(t)))
+                  _lib.ptr(self.bases), self.cap, _lib.ptr(self.state), _lib.ptr(self.err),
+                  float(TIMEOUT_S if timeout_s is None else timeout_s), vp(_lib.stream_of(t)))
+        if not torch.cuda.is_current_stream_capturing():
+            if getattr(self, "_err_host", None) is None:
+                self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+                self._err_ev = torch.cuda.Event()
+            self._err_host.copy_(self.err, non_blocking=True)
+            self._err_ev.record()
         return t
+
+    def _poll(self):
+        ev = getattr(self, "_err_ev", None)
+        if ev is not None and ev.query() and int(self._err_host[0]):
+            raise OneShotError("one-shot all-reduce: a peer did not arrive within the timeout "
+                               "(the operand of that call was poisoned with NaN)")
 
     def check(self):
         """Raise if any earlier call timed out waiting for a peer (host sync)."""
         if int(self.err.item()):
-            raise OneShotError("one-shot all-reduce: a peer did not arrive within the timeout")
+            raise OneShotError("one-shot all-reduce: a peer did not arrive within the timeout "
+                               "(the operand of that call was poisoned with NaN)")
 
-    def close(self):
+    def close(self, comm=None):
+        """Unmap the peers' buffers and free this rank's (collectively when a
+        communicator is given: nobody frees a buffer a peer still maps)."""
         lib = _lib.load()
         if lib is None:
             return
+        if comm is not None and self.ok:
+            torch.cuda.synchronize(self.dev)
+            comm.barrier()
         for ptr in self._peers:
             lib.sl_oneshot_close(ptr)
         self._peers = []
+        if comm is not None and self.ok:
+            comm.barrier()
         if self._local is not None:
             lib.sl_oneshot_free(self._local)
             self._local = None

@@ -119,3 +119,33 @@ def test_admm_one_pass_matches_four_products(dev):
     assert ef <= 3 * e4 + 1e-6, (ef, e4)
     for a, b in zip(res["f64"][1], res["f32_fused"][1]):
         assert abs(a - b) <= 1e-3 * abs(a)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cond", [1e4, 1e6])
+def test_normal_form_lsqr_unpreconditioned_ill_conditioned(dev, cond):
+    """the n-space recurrence of normal-form LSQR on an
+    UNpreconditioned ill-conditioned A.  The default for an identity
+    preconditioner is the classic form; the explicitly requested fused form
+    (refreshed every 16 iterations) must still end at a residual within 1 %
+    of the classic one and not report a better stop than classic."""
+    g = torch.Generator().manual_seed(int(math.log10(cond)))
+    m, n = 20000, 200
+    U, _ = torch.linalg.qr(torch.randn(m, n, generator=g, dtype=torch.float64))
+    Vq, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    s = torch.logspace(0, -math.log10(cond), n, dtype=torch.float64)
+    A = ((U * s) @ Vq.t()).float().to(dev)
+    b = (A @ torch.randn(n, 1, generator=g).to(dev)) + 1e-4 * torch.randn(m, 1, generator=g).to(dev)
+    from libskylark_amd.algorithms import operators as O
+    assert O.DenseOp(A).has_fused_normal(1)
+    pd = K.KrylovIterParams(tolerance=1e-8, iter_lim=400)
+    Xd, cd = K.lsqr(A, b, params=pd)
+    pc = K.KrylovIterParams(tolerance=1e-8, iter_lim=400, fused_normal=False)
+    Xc, cc = K.lsqr(A, b, params=pc)
+    pf = K.KrylovIterParams(tolerance=1e-8, iter_lim=400, fused_normal=True)
+    Xf, cf = K.lsqr(A, b, params=pf)
+    # default == classic for the identity preconditioner
+    assert torch.equal(Xd, Xc) and cd == cc
+    rc = float((A @ Xc - b).norm())
+    rf = float((A @ Xf - b).norm())
+    assert rf <= 1.01 * rc, (rf, rc, cf, cc)

@@ -63,3 +63,41 @@ def test_oneshot_allreduce_two_processes_one_gpu(world):
     if all(r == "unavailable" for r in res):
         pytest.skip("IPC export of uncached device memory unavailable here")
     assert res == ["ok"] * world
+
+
+def _late_worker(rank, world):
+    import time
+    import torch
+    from libskylark_amd.parallel import oneshot
+    from libskylark_amd.parallel.comm import world as W
+    torch.cuda.set_device(0)
+    comm = W()
+    os_ = oneshot.OneShotAllReduce(comm, cap=1 << 12)
+    if not os_.ok:
+        return "unavailable"
+    dev = torch.device("cuda", 0)
+    x = torch.full((100,), float(rank + 1), dtype=torch.float64, device=dev)
+    if rank == 1:
+        time.sleep(2.0)          # far past rank 0's 0.3 s timeout
+    os_.all_reduce(x, timeout_s=0.3)
+    torch.cuda.synchronize()
+    out = {"nan": bool(torch.isnan(x).all()), "sum_ok": bool(torch.all(x == 3.0))}
+    try:
+        comm.check_collectives()
+        out["raised"] = False
+    except oneshot.OneShotError:
+        out["raised"] = True
+    comm.barrier()
+    comm.close()
+    return out
+
+
+def test_oneshot_late_peer_is_an_error_not_a_partial_sum():
+    """a peer later than the timeout must not leave a
+    silent partial sum -- the waiting rank's operand is NaN and the
+    communicator raises; the late rank itself still gets the true sum."""
+    res = run_distributed(_late_worker, 2, timeout=120)
+    if all(r == "unavailable" for r in res):
+        pytest.skip("IPC export of uncached device memory unavailable here")
+    assert res[0] == {"nan": True, "sum_ok": False, "raised": True}, res
+    assert res[1] == {"nan": False, "sum_ok": True, "raised": False}, res
