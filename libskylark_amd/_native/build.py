@@ -109,8 +109,10 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
 
 def build_capi(force: bool = False) -> str:
-    """C API library (host C++, embeds/joins CPython; no device code)."""
-    srcs = [CAPI_SRC, os.path.join(HERE, "capi", "native_sketch.hpp"), os.path.join(INC, "sl_rng.hpp")]
+    """C API library (host C++; embeds/joins CPython for the runtime paths, loads
+    libskylark_hip.so + rocBLAS for the DeviceMatrix paths; no device code)."""
+    srcs = [CAPI_SRC, os.path.join(HERE, "capi", "native_sketch.hpp"), os.path.join(HERE, "capi", "native_device.hpp"),
+            os.path.join(INC, "sl_rng.hpp")]
     if not force and os.path.exists(CAPI_LIB) and all(os.path.getmtime(CAPI_LIB) >= os.path.getmtime(f) for f in srcs):
         return CAPI_LIB
     import sysconfig

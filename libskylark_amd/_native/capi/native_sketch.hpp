@@ -1,7 +1,8 @@
 // Native (interpreter-free) C API path for the reference's core sketches:
 // JLT, CT (dense transforms, sketch/dense_transform_data.hpp) and CWT, MMT,
 // WZT (hash transforms, sketch/hash_transform_data.hpp) on host column-major
-// double matrices ("Matrix"), plus their JSON (de)serialisation.
+// double matrices ("Matrix"), plus their JSON (de)serialisation.  FJLT is a
+// native object too (its device application is native_device.hpp's).
 //
 // Same parameters as the Python / GPU runtime, drawn from the same
 // counter-based streams (sl_rng.hpp: Threefry-2x64-13, sample_d /
@@ -42,8 +43,12 @@ struct Sketch {
 };
 
 inline bool supported(const char* t) {
-  return !strcmp(t, "JLT") || !strcmp(t, "CT") || !strcmp(t, "CWT") || !strcmp(t, "MMT") || !strcmp(t, "WZT");
+  return !strcmp(t, "JLT") || !strcmp(t, "CT") || !strcmp(t, "CWT") || !strcmp(t, "MMT") || !strcmp(t, "WZT") ||
+         !strcmp(t, "FJLT");
 }
+
+// host "Matrix" application is native for all but FJLT (its host path is the runtime's)
+inline bool host_apply(const Sketch& s) { return s.type != "FJLT"; }
 
 inline bool takes_param(const std::string& t) { return t == "CT" || t == "WZT"; }
 
@@ -51,6 +56,12 @@ inline bool takes_param(const std::string& t) { return t == "CT" || t == "WZT"; 
 // counter after the sketch's draws.
 inline uint64_t build(Sketch& s) {
   uint64_t c = s.ctr0;
+  if (s.type == "FJLT") {
+    // FJLT_data: N Rademacher signs (D), then S uniform frequencies; the
+    // operator is realised on the device from (seed, ctr0, ctr0 + N)
+    s.dense = false;
+    return c + (uint64_t)(s.N + s.S);
+  }
   if (s.type == "JLT" || s.type == "CT") {
     s.dense = true;
     s.dist = s.type == "JLT" ? sl::DIST_NORMAL : sl::DIST_CAUCHY;
@@ -187,7 +198,7 @@ inline void realise_panel(const Sketch& s, int64_t k0, int64_t kb, double* P) {
 }
 
 // SA = S A (dim 0: A is N x n) or A S^T (dim 1: A is m x N); host col-major,
-// SA overwritten.  Returns 104 on a dimension mismatch.
+// SA overwritten.  Returns 104 on a dimension mismatch (host_apply(s) only).
 inline int apply(const Sketch& s, const double* A, int64_t am, int64_t an, double* SA, int64_t sm, int64_t sn,
                  int dim) {
   if (dim == 0) {

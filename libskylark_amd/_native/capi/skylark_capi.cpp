@@ -1,11 +1,17 @@
 // C API of the framework: the reference's sl_* ABI (capi/basec.hpp,
 // sketchc.hpp, nlac.hpp, kernelc.hpp, ioc.hpp) over the MI355X runtime.
 //
-// Native path (no interpreter): contexts, and the core sketches JLT / CT /
-// CWT / MMT / WZT on host "Matrix" operands -- creation, application and
-// JSON (de)serialisation -- run in C++ (native_sketch.hpp, the same
-// counter-based streams as the runtime).  Everything else (other sketch
-// types, sparse operands, NLA, kernels, IO) goes through the Python/HIP
+// Native paths (no interpreter):
+//  - contexts, kernels objects, and the core sketches JLT / CT / FJLT / CWT /
+//    MMT / WZT -- creation and JSON (de)serialisation -- in C++
+//    (native_sketch.hpp, the same counter-based streams as the runtime);
+//  - host "Matrix" application of JLT / CT / CWT / MMT / WZT (host C++);
+//  - "DeviceMatrix" operands (GPU buffers wrapped by
+//    sl_wrap_raw_device_matrix): sketch application, sl_approximate_svd (the
+//    C++ randSVD engine) and sl_kernel_gram call libskylark_hip.so directly
+//    (native_device.hpp).
+// Everything else (other sketch types, sparse operands, NLA and kernels on
+// host matrices, IO) goes through the Python/HIP
 // runtime (libskylark_amd + libskylark_hip.so); a natively created sketch
 // or context is handed to it lazily (via its JSON / seed + counter), so the
 // two paths see the same objects and the same random streams.  This library
@@ -30,6 +36,7 @@
 #include <string>
 
 #include "native_sketch.hpp"
+#include "native_device.hpp"
 
 #define SL_CAPI extern "C" __attribute__((visibility("default")))
 
@@ -39,13 +46,19 @@ struct sl_context_t {
   PyObject* obj;
   uint64_t seed;
   uint64_t counter;
+  void* dcomm;   // NativeComm (RCCL) of the DeviceMatrix paths, or null
 };
 struct sl_sketch_transform_t {
   PyObject* obj;          // runtime object (created lazily for native sketches)
   slnat::Sketch* nat;     // native operator, or null
 };
 struct sl_kernel_t {
-  PyObject* obj;
+  PyObject* obj;          // runtime object (created lazily for natively known kernels)
+  sldev::Kern nat;        // native parameters (type K_NONE: runtime-only kernel)
+  std::string type;
+};
+struct sl_raw_device_matrix_t {
+  sldev::DevMat d;
 };
 struct sl_raw_matrix_t {
   double* data;
@@ -188,6 +201,15 @@ PyObject* py_sketch(sl_sketch_transform_t* S) {
   return S->obj;
 }
 
+bool is_device(const char* type) { return !strcmp(type, "DeviceMatrix"); }
+
+sldev::DevMat& devmat(void* A) { return ((sl_raw_device_matrix_t*)A)->d; }
+
+int native_fail(int code) {
+  g_last_error = sldev::error();
+  return code;
+}
+
 PyObject* dense_desc(void* A) {
   auto* M = (sl_raw_matrix_t*)A;
   return Py_BuildValue("(Kii)", (unsigned long long)(uintptr_t)M->data, M->m, M->n);
@@ -285,14 +307,55 @@ SL_CAPI void sl_get_exception_info(char** info) { *info = strdup(g_last_error.c_
 SL_CAPI void sl_print_exception_trace() { fprintf(stderr, "%s\n", g_last_error.c_str()); }
 
 SL_CAPI int sl_create_default_context(int seed, sl_context_t** ctxt) {
-  *ctxt = new sl_context_t{nullptr, (uint64_t)(int64_t)seed, 0};
+  *ctxt = new sl_context_t{nullptr, (uint64_t)(int64_t)seed, 0, nullptr};
   return 0;
 }
 
-// The communicator argument is accepted for ABI shape only: the process group
-// is torch.distributed's (RCCL) world, set up by the launcher.
-SL_CAPI int sl_create_context(int seed, void* /*comm*/, sl_context_t** ctxt) {
-  return sl_create_default_context(seed, ctxt);
+// comm: null, or a device communicator from sl_device_comm_create (RCCL over
+// xGMI); the DeviceMatrix randSVD of a context with a communicator is the
+// distributed call over the ranks' row shards.  (The runtime paths use
+// torch.distributed's world, set up by the launcher.)
+SL_CAPI int sl_create_context(int seed, void* comm, sl_context_t** ctxt) {
+  const int rc = sl_create_default_context(seed, ctxt);
+  if (rc == 0) (*ctxt)->dcomm = comm;
+  return rc;
+}
+
+// ----------------------------------------------------- device communicator
+// RCCL communicator of the C ABI's distributed device paths (NativeComm):
+// rank 0 gets an id, the caller ships it to every rank (MPI, a file, ...),
+// every rank creates its communicator with it (collective).
+SL_CAPI int sl_device_comm_id_bytes() {
+  auto& L = sldev::lib();
+  return L.loaded ? L.comm_id_bytes() : -1;
+}
+
+SL_CAPI int sl_device_comm_unique_id(void* out) {
+  auto& L = sldev::lib();
+  if (!L.loaded) { g_last_error = L.err; return 106; }
+  if (L.comm_unique_id(out)) { g_last_error = L.last_error(); return 106; }
+  return 0;
+}
+
+SL_CAPI int sl_device_comm_create(const void* id, int nranks, int rank, void** comm) {
+  auto& L = sldev::lib();
+  if (!L.loaded) { g_last_error = L.err; return 106; }
+  if (L.comm_init(id, nranks, rank, comm)) { g_last_error = L.last_error(); return 106; }
+  return 0;
+}
+
+SL_CAPI int sl_device_comm_free(void* comm) {
+  auto& L = sldev::lib();
+  if (!L.loaded || !comm) return 0;
+  return L.comm_destroy(comm) ? 106 : 0;
+}
+
+// HIP device of the calling thread (one process per GPU)
+SL_CAPI int sl_device_set(int dev) {
+  auto& L = sldev::lib();
+  if (!L.loaded) { g_last_error = L.err; return 106; }
+  if (L.set_device(dev)) { g_last_error = L.last_error(); return 106; }
+  return 0;
 }
 
 SL_CAPI int sl_free_context(sl_context_t* ctxt) {
@@ -315,6 +378,42 @@ SL_CAPI int sl_wrap_raw_matrix(double* data, int m, int n, void** A) {
 
 SL_CAPI int sl_free_raw_matrix_wrap(void* A) {
   delete (sl_raw_matrix_t*)A;
+  return 0;
+}
+
+// A GPU buffer as a "DeviceMatrix": row-major m x n, leading dimension ld
+// (elements), dtype 0 f32 / 1 f64 / 2 bf16.  The caller owns the memory.
+SL_CAPI int sl_wrap_raw_device_matrix(void* data, int dtype, int m, int n, int64_t ld, void** A) {
+  if (dtype < 0 || dtype > 2 || m < 0 || n < 0 || ld < n) return 109;
+  *A = new sl_raw_device_matrix_t{sldev::DevMat{data, dtype, m, n, ld}};
+  return 0;
+}
+
+SL_CAPI int sl_free_raw_device_matrix_wrap(void* A) {
+  delete (sl_raw_device_matrix_t*)A;
+  return 0;
+}
+
+// device memory helpers for C callers of the DeviceMatrix paths (kind: 0
+// host->device, 1 device->host, 2 device->device)
+SL_CAPI int sl_device_malloc(int64_t bytes, void** p) {
+  auto& L = sldev::lib();
+  if (!L.loaded) { g_last_error = L.err; return 106; }
+  return L.dev_malloc(bytes, p) ? 101 : 0;
+}
+
+SL_CAPI int sl_device_free(void* p) {
+  auto& L = sldev::lib();
+  return L.loaded ? (L.dev_free(p) ? 106 : 0) : 106;
+}
+
+SL_CAPI int sl_device_memcpy(void* dst, const void* src, int64_t bytes, int kind) {
+  auto& L = sldev::lib();
+  if (!L.loaded) { g_last_error = L.err; return 106; }
+  if (L.dev_memcpy(dst, src, bytes, kind, nullptr) || L.dev_sync(nullptr)) {
+    g_last_error = L.last_error();
+    return 106;
+  }
   return 0;
 }
 
@@ -503,7 +602,19 @@ SL_CAPI int sl_free_sketch_transform(sl_sketch_transform_t* S) {
 
 SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type, void* A, char* output_type,
                                       void* SA, int dim) {
-  if (S->nat && !strcmp(input_type, "Matrix") && !strcmp(output_type, "Matrix")) {
+  if (is_device(input_type) || is_device(output_type)) {
+    if (!is_device(input_type) || !is_device(output_type)) {
+      g_last_error = "sl_apply_sketch_transform: DeviceMatrix input needs a DeviceMatrix output";
+      return 109;
+    }
+    if (!S->nat) {
+      g_last_error = "sl_apply_sketch_transform: this sketch type has no device C path";
+      return 103;
+    }
+    const int rc = sldev::apply_sketch(*S->nat, devmat(A), devmat(SA), dim);
+    return rc ? native_fail(rc) : 0;
+  }
+  if (S->nat && slnat::host_apply(*S->nat) && !strcmp(input_type, "Matrix") && !strcmp(output_type, "Matrix")) {
     auto* a = (sl_raw_matrix_t*)A;
     auto* o = (sl_raw_matrix_t*)SA;
     const int rc = slnat::apply(*S->nat, a->data, a->m, a->n, o->data, o->m, o->n, dim);
@@ -529,6 +640,15 @@ SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type
 // --------------------------------------------------------------------- NLA
 SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, char* S_type, void* Sv, char* V_type,
                                void* V, uint16_t k, char* params, sl_context_t* ctxt) {
+  if (is_device(A_type)) {
+    if (!is_device(U_type) || !is_device(S_type) || !is_device(V_type)) {
+      g_last_error = "sl_approximate_svd: DeviceMatrix A needs DeviceMatrix U, S, V";
+      return 109;
+    }
+    const int rc = sldev::approximate_svd(devmat(A), devmat(U), devmat(Sv), devmat(V), (int)k, params, ctxt->seed,
+                                          ctxt->counter, ctxt->dcomm);
+    return rc ? native_fail(rc) : 0;
+  }
   Gil g;
   (void)U_type;
   (void)S_type;
@@ -575,7 +695,56 @@ SL_CAPI int sl_faster_least_squares(int orientation, char* A_type, void* A, char
 }
 
 // ----------------------------------------------------------------- kernels
+namespace {
+// runtime object of a kernel (a native one is created on first host use)
+PyObject* py_kernel(sl_kernel_t* k) {
+  if (k->obj) return k->obj;
+  const auto& n = k->nat;
+  PyObject* params = nullptr;
+  switch (n.type) {
+    case sldev::K_LINEAR: params = PyTuple_New(0); break;
+    case sldev::K_GAUSSIAN:
+    case sldev::K_LAPLACIAN:
+    case sldev::K_EXPSEMIGROUP: params = Py_BuildValue("(d)", n.p[0]); break;
+    case sldev::K_POLYNOMIAL: params = Py_BuildValue("(idd)", (int)n.p[0], n.p[1], n.p[2]); break;
+    case sldev::K_MATERN: params = Py_BuildValue("(dd)", n.p[0], n.p[1]); break;
+    default: PyErr_SetString(PyExc_ValueError, "unknown kernel"); return nullptr;
+  }
+  k->obj = call("create_kernel", Py_BuildValue("(siN)", k->type.c_str(), n.N, params));
+  return k->obj;
+}
+}  // namespace
+
+// Kernels known to the native layer (linear, gaussian(sigma), laplacian(sigma),
+// expsemigroup(beta), polynomial(int q, c, gamma), matern(nu, l)) are created
+// without the interpreter; others go to the runtime.
 SL_CAPI int sl_create_kernel(char* type, int N, sl_kernel_t** kernel, ...) {
+  const int kt = sldev::kernel_type_of(type);
+  if (kt != sldev::K_NONE) {
+    auto* k = new sl_kernel_t{nullptr, sldev::Kern{}, type};
+    k->nat.type = kt;
+    k->nat.N = N;
+    va_list ap;
+    va_start(ap, kernel);
+    switch (kt) {
+      case sldev::K_GAUSSIAN:
+      case sldev::K_LAPLACIAN:
+      case sldev::K_EXPSEMIGROUP: k->nat.p[0] = va_arg(ap, double); break;
+      case sldev::K_POLYNOMIAL:
+        k->nat.p[0] = (double)va_arg(ap, int);
+        k->nat.p[1] = va_arg(ap, double);
+        k->nat.p[2] = va_arg(ap, double);
+        break;
+      case sldev::K_MATERN:
+        k->nat.p[0] = va_arg(ap, double);
+        k->nat.p[1] = va_arg(ap, double);
+        break;
+      default: break;
+    }
+    va_end(ap);
+    *kernel = k;
+    return 0;
+  }
   Gil g;
   std::string spec = spec_of("kernel_param_spec", type);
   va_list ap;
@@ -584,22 +753,38 @@ SL_CAPI int sl_create_kernel(char* type, int N, sl_kernel_t** kernel, ...) {
   va_end(ap);
   PyObject* r = call("create_kernel", Py_BuildValue("(siN)", type, N, params));
   if (!r) return fail();
-  *kernel = new sl_kernel_t{r};
+  *kernel = new sl_kernel_t{r, sldev::Kern{}, type};
   return 0;
 }
 
 SL_CAPI int sl_free_kernel(sl_kernel_t* k) {
   if (!k) return 0;
-  Gil g;
-  Py_XDECREF(k->obj);
+  if (k->obj) {
+    Gil g;
+    Py_XDECREF(k->obj);
+  }
   delete k;
   return 0;
 }
 
 SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, void* X, char* Y_type, void* Y,
                            char* K_type, void* K) {
+  if (is_device(X_type) || is_device(Y_type) || is_device(K_type)) {
+    if (!is_device(X_type) || !is_device(Y_type) || !is_device(K_type)) {
+      g_last_error = "sl_kernel_gram: mix of DeviceMatrix and host operands";
+      return 109;
+    }
+    if (k->nat.type == sldev::K_NONE) {
+      g_last_error = "sl_kernel_gram: this kernel has no device C path";
+      return 103;
+    }
+    const int rc = sldev::kernel_gram(k->nat, dirX, dirY, devmat(X), devmat(Y), devmat(K));
+    return rc ? native_fail(rc) : 0;
+  }
   Gil g;
   (void)K_type;
+  PyObject* ko = py_kernel(k);
+  if (!ko) return fail();
   PyObject* x = in_desc(X_type, X);
   if (!x) return fail();
   PyObject* y = in_desc(Y_type, Y);
@@ -607,7 +792,7 @@ SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, voi
     Py_DECREF(x);
     return fail();
   }
-  PyObject* r = call("kernel_gram", Py_BuildValue("(iiOsNsNN)", dirX, dirY, k->obj, X_type, x, Y_type, y,
+  PyObject* r = call("kernel_gram", Py_BuildValue("(iiOsNsNN)", dirX, dirY, ko, X_type, x, Y_type, y,
                                                   dense_desc(K)));
   if (!r) return fail();
   Py_DECREF(r);

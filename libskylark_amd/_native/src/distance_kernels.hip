@@ -18,7 +18,7 @@
 namespace {
 
 enum { PW_L1 = 0, PW_SEMIGROUP = 1 };
-enum { GM_GAUSSIAN = 0, GM_POLYNOMIAL = 1, GM_EXPNEG = 2 };
+enum { GM_GAUSSIAN = 0, GM_POLYNOMIAL = 1, GM_EXPNEG = 2, GM_MATERN05 = 3, GM_MATERN15 = 4, GM_MATERN25 = 5 };
 
 constexpr int TB = 64;   // output tile edge
 constexpr int KC = 32;   // d slab
@@ -34,7 +34,7 @@ __device__ __forceinline__ double dev_sqrt<double>(double x) { return __builtin_
 template <typename T, int MODE, bool EXP>
 __global__ void __launch_bounds__(256)
 k_pairwise(const T* __restrict__ X, const T* __restrict__ Y, T* __restrict__ K, int64_t m, int64_t n,
-           int64_t d, int64_t ldx, int64_t ldy, int64_t ldk, double scale) {
+           int64_t d, int64_t ldx, int64_t sdx, int64_t ldy, int64_t sdy, int64_t ldk, double scale) {
   __shared__ T xs[KC][LDS_LD];
   __shared__ T ys[KC][LDS_LD];
   const int tid = threadIdx.x;
@@ -54,8 +54,8 @@ k_pairwise(const T* __restrict__ X, const T* __restrict__ Y, T* __restrict__ K, 
       const int kk = flat & (KC - 1), rr = flat / KC;
       const int64_t gk = k0 + kk;
       const int64_t gx = r0 + rr, gy = c0 + rr;
-      xs[kk][rr] = (gx < m && gk < d) ? X[gx * ldx + gk] : T(0);
-      ys[kk][rr] = (gy < n && gk < d) ? Y[gy * ldy + gk] : T(0);
+      xs[kk][rr] = (gx < m && gk < d) ? X[gx * ldx + gk * sdx] : T(0);
+      ys[kk][rr] = (gy < n && gk < d) ? Y[gy * ldy + gk * sdy] : T(0);
     }
     __syncthreads();
     const int kmax = (int)((d - k0) < KC ? (d - k0) : KC);
@@ -107,25 +107,53 @@ k_gram_map(T* __restrict__ K, int64_t m, int64_t n, int64_t ldk, const T* __rest
     } else if (KIND == GM_POLYNOMIAL) {
       const double base = a * (double)g + c;
       *p = (sizeof(T) == 8) ? (T)pow(base, q) : (T)powf((float)base, (float)q);
-    } else {
+    } else if (KIND == GM_EXPNEG) {
       *p = (sizeof(T) == 8) ? (T)exp(-a * (double)g) : (T)__expf(-(float)a * (float)g);
+    } else {
+      // Matern nu = 1/2, 3/2, 5/2 of r = |x - y| / l (a = 1 / l)
+      double d2 = (double)xn[r] + (double)yn[col] - 2.0 * (double)g;
+      const double rr = sqrt(d2 > 0.0 ? d2 : 0.0) * a;
+      double v;
+      if (KIND == GM_MATERN05) v = exp(-rr);
+      else if (KIND == GM_MATERN15) { const double t = 1.7320508075688772 * rr; v = (1.0 + t) * exp(-t); }
+      else { const double t = 2.23606797749979 * rr; v = (1.0 + t + t * t / 3.0) * exp(-t); }
+      *p = (T)v;
     }
   }
 }
 
 template <typename T>
-int launch_pairwise(const T* X, const T* Y, T* K, int64_t m, int64_t n, int64_t d, int64_t ldx, int64_t ldy,
-                    int64_t ldk, int mode, double scale, hipStream_t s) {
+int launch_pairwise(const T* X, const T* Y, T* K, int64_t m, int64_t n, int64_t d, int64_t ldx, int64_t sdx,
+                    int64_t ldy, int64_t sdy, int64_t ldk, int mode, double scale, hipStream_t s) {
   dim3 grid((unsigned)((n + TB - 1) / TB), (unsigned)((m + TB - 1) / TB));
   const bool ex = scale > 0;
+#define SL_PW(MODE, EX) k_pairwise<T, MODE, EX><<<grid, 256, 0, s>>>(X, Y, K, m, n, d, ldx, sdx, ldy, sdy, ldk, scale)
   if (mode == PW_L1) {
-    if (ex) k_pairwise<T, PW_L1, true><<<grid, 256, 0, s>>>(X, Y, K, m, n, d, ldx, ldy, ldk, scale);
-    else k_pairwise<T, PW_L1, false><<<grid, 256, 0, s>>>(X, Y, K, m, n, d, ldx, ldy, ldk, scale);
+    if (ex) SL_PW(PW_L1, true);
+    else SL_PW(PW_L1, false);
   } else {
-    if (ex) k_pairwise<T, PW_SEMIGROUP, true><<<grid, 256, 0, s>>>(X, Y, K, m, n, d, ldx, ldy, ldk, scale);
-    else k_pairwise<T, PW_SEMIGROUP, false><<<grid, 256, 0, s>>>(X, Y, K, m, n, d, ldx, ldy, ldk, scale);
+    if (ex) SL_PW(PW_SEMIGROUP, true);
+    else SL_PW(PW_SEMIGROUP, false);
   }
+#undef SL_PW
   return SL_OK;
+}
+
+// squared norms of m points (point stride sp, coordinate stride sd)
+template <typename T>
+__global__ void __launch_bounds__(256) k_point_sqnorms(const T* __restrict__ X, int64_t m, int64_t d, int64_t sp,
+                                                       int64_t sd, T* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= m) return;
+  double a = 0.0;
+  for (int64_t c = lane; c < d; c += 64) {
+    const double v = (double)X[i * sp + c * sd];
+    a += v * v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+  if (lane == 0) out[i] = (T)a;
 }
 
 }  // namespace
@@ -137,17 +165,52 @@ SL_API int sl_pairwise_map(const void* X, const void* Y, void* K, int dtype, int
   if ((m + TB - 1) / TB > 65535) { sl_set_last_error("pairwise: too many rows"); return SL_ERR_DIMENSION; }
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SL_F32)
-    launch_pairwise<float>((const float*)X, (const float*)Y, (float*)K, m, n, d, ldx, ldy, ldk, mode, scale, s);
+    launch_pairwise<float>((const float*)X, (const float*)Y, (float*)K, m, n, d, ldx, 1, ldy, 1, ldk, mode, scale, s);
   else if (dtype == SL_F64)
-    launch_pairwise<double>((const double*)X, (const double*)Y, (double*)K, m, n, d, ldx, ldy, ldk, mode, scale, s);
+    launch_pairwise<double>((const double*)X, (const double*)Y, (double*)K, m, n, d, ldx, 1, ldy, 1, ldk, mode, scale,
+                            s);
   else
     { sl_set_last_error("pairwise: dtype must be f32/f64"); return SL_ERR_UNSUPPORTED; }
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
+// As sl_pairwise_map with general operand strides: point i, coordinate c of X
+// at X[i * ldx + c * sdx] (columns-as-points operands need no transpose copy).
+SL_API int sl_pairwise_map_strided(const void* X, int64_t ldx, int64_t sdx, const void* Y, int64_t ldy, int64_t sdy,
+                                   void* K, int64_t ldk, int dtype, int64_t m, int64_t n, int64_t d, int mode,
+                                   double scale, void* stream) {
+  if (m <= 0 || n <= 0) return SL_OK;
+  if ((m + TB - 1) / TB > 65535) { sl_set_last_error("pairwise: too many rows"); return SL_ERR_DIMENSION; }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SL_F32)
+    launch_pairwise<float>((const float*)X, (const float*)Y, (float*)K, m, n, d, ldx, sdx, ldy, sdy, ldk, mode, scale,
+                           s);
+  else if (dtype == SL_F64)
+    launch_pairwise<double>((const double*)X, (const double*)Y, (double*)K, m, n, d, ldx, sdx, ldy, sdy, ldk, mode,
+                            scale, s);
+  else
+    { sl_set_last_error("pairwise: dtype must be f32/f64"); return SL_ERR_UNSUPPORTED; }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// out[i] = |x_i|^2 for m points of dimension d (point stride sp, coordinate stride sd)
+SL_API int sl_point_sqnorms(const void* X, int dtype, int64_t m, int64_t d, int64_t sp, int64_t sd, void* out,
+                            void* stream) {
+  if (m <= 0) return SL_OK;
+  const unsigned g = (unsigned)((m + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SL_F32) k_point_sqnorms<float><<<g, 256, 0, s>>>((const float*)X, m, d, sp, sd, (float*)out);
+  else if (dtype == SL_F64) k_point_sqnorms<double><<<g, 256, 0, s>>>((const double*)X, m, d, sp, sd, (double*)out);
+  else { sl_set_last_error("point_sqnorms: dtype must be f32/f64"); return SL_ERR_UNSUPPORTED; }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
 // kind 0 Gaussian (needs xn, yn = squared row norms; a = 1/(2 sigma^2)),
-// kind 1 polynomial (a = gamma, c, q), kind 2 exp(-a K).
+// kind 1 polynomial (a = gamma, c, q), kind 2 exp(-a K), kinds 3/4/5 Matern
+// nu = 1/2, 3/2, 5/2 (xn, yn; a = 1/l).
 SL_API int sl_gram_map(void* K, int dtype, int64_t m, int64_t n, int64_t ldk, const void* xn, const void* yn,
                        int kind, double a, double c, double q, void* stream) {
   if (m * n <= 0) return SL_OK;
@@ -159,6 +222,12 @@ SL_API int sl_gram_map(void* K, int dtype, int64_t m, int64_t n, int64_t ldk, co
       k_gram_map<T, GM_GAUSSIAN><<<grid, 256, 0, s>>>((T*)K, m, n, ldk, (const T*)xn, (const T*)yn, a, c, q); \
     else if (kind == GM_POLYNOMIAL)                                                                  \
       k_gram_map<T, GM_POLYNOMIAL><<<grid, 256, 0, s>>>((T*)K, m, n, ldk, (const T*)xn, (const T*)yn, a, c, q); \
+    else if (kind == GM_MATERN05)                                                                    \
+      k_gram_map<T, GM_MATERN05><<<grid, 256, 0, s>>>((T*)K, m, n, ldk, (const T*)xn, (const T*)yn, a, c, q); \
+    else if (kind == GM_MATERN15)                                                                    \
+      k_gram_map<T, GM_MATERN15><<<grid, 256, 0, s>>>((T*)K, m, n, ldk, (const T*)xn, (const T*)yn, a, c, q); \
+    else if (kind == GM_MATERN25)                                                                    \
+      k_gram_map<T, GM_MATERN25><<<grid, 256, 0, s>>>((T*)K, m, n, ldk, (const T*)xn, (const T*)yn, a, c, q); \
     else                                                                                             \
       k_gram_map<T, GM_EXPNEG><<<grid, 256, 0, s>>>((T*)K, m, n, ldk, (const T*)xn, (const T*)yn, a, c, q); \
   } while (0)

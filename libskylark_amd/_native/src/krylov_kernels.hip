@@ -326,6 +326,163 @@ __global__ void __launch_bounds__(NT) k_rows_gemm(const T* __restrict__ M, int64
   }
 }
 
+
+// ---------------------------------------------------------------- CG / FCG
+// Device-resident (flexible) CG (reference algorithms/Krylov/CG.hpp:24-163,
+// FlexibleCG.hpp:23-153): per-column scalars in st[C_NS][k], every column
+// reduction finished by the LAST block of its own pass (agent-scope release,
+// ticket counter, acquire), so an unpreconditioned CG iteration is 3 launches
+// of its own plus the operator product:
+//   k_cg_p   P = Z + beta P (CG) / Z - beta P (FCG)
+//   k_cg_dot P . Q -> alpha = rho / pq   |  R . Z -> rho, beta  |  FCG dots
+//   k_cg_xr  X += alpha P, R -= alpha Q, |R|^2 -> rho, beta (unpreconditioned),
+//            convergence flags |R| < tol |B|
+enum { C_RHO, C_RHO0, C_ALPHA, C_BETA, C_PQ, C_RR, C_NRMB, C_NS };
+
+// After each block wrote part[b * k + c] (threads ty == 0): the last block to
+// arrive reduces them; returns true there, with the column total in `tot` on
+// threads tid < KP.  The counter is left at zero for the next launch.
+template <int KP>
+__device__ __forceinline__ bool last_block_total(const double* part, int k, unsigned* counter, double* sh,
+                                                 double& tot) {
+  __shared__ int last_sh;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last_sh = atomicAdd(counter, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last_sh) return false;
+  __threadfence();
+  const int tx = threadIdx.x % KP, ty = threadIdx.x / KP;
+  constexpr int RS = NT / KP;
+  double v = 0.0;
+  if (tx < k)
+    for (int b = ty; b < (int)gridDim.x; b += RS) v += __hip_atomic_load(part + (int64_t)b * k + tx, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT);
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int st = NT / 2; st >= KP; st >>= 1) {
+    if ((int)threadIdx.x < st) sh[threadIdx.x] += sh[threadIdx.x + st];
+    __syncthreads();
+  }
+  tot = sh[threadIdx.x % KP];
+  if (threadIdx.x == 0) *counter = 0u;
+  return true;
+}
+
+// per-column dot(s) with a last-block epilogue on the CG state:
+//   MODE 0 (CG)        alpha = rho / (X . Y)
+//   MODE 1 (CG, M)     rho0 = rho, rho = X . Y, beta = rho / rho0 (0 first)
+//   MODE 2 (FCG)       beta = (X . Y) / pq
+//   MODE 3 (FCG)       pq = X . Y, alpha = (X . Y2) / pq
+template <typename T, int KP, int MODE>
+__global__ void __launch_bounds__(NT) k_cg_dot(const T* __restrict__ X, int64_t ldx, const T* __restrict__ Yv,
+                                              int64_t ldy, const T* __restrict__ Y2, int64_t ldy2, int64_t m, int k,
+                                              double* __restrict__ part, double* __restrict__ part2,
+                                              unsigned* __restrict__ counter, double* __restrict__ st) {
+  __shared__ double sh[NT];
+  const int tx = threadIdx.x % KP, ty = threadIdx.x / KP;
+  constexpr int RS = NT / KP;
+  double a1 = 0.0, a2 = 0.0;
+  if (tx < k) {
+    for (int64_t r = (int64_t)blockIdx.x * RS + ty; r < m; r += (int64_t)gridDim.x * RS) {
+      const double x = ld_d(X + r * ldx + tx);
+      a1 += x * ld_d(Yv + r * ldy + tx);
+      if (MODE == 3) a2 += x * ld_d(Y2 + r * ldy2 + tx);
+    }
+  }
+  block_col_reduce<KP>(a1, sh, part, k);
+  if (MODE == 3) {
+    __syncthreads();
+    block_col_reduce<KP>(a2, sh, part2, k);
+  }
+  double t1, t2 = 0.0;
+  if (!last_block_total<KP>(part, k, counter, sh, t1)) return;
+  if (MODE == 3) {
+    // second total: the ticket is spent, reduce part2 directly
+    const int ty2 = threadIdx.x / KP;
+    double v = 0.0;
+    if (tx < k)
+      for (int b = ty2; b < (int)gridDim.x; b += RS)
+        v += __hip_atomic_load(part2 + (int64_t)b * k + tx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int s2 = NT / 2; s2 >= KP; s2 >>= 1) {
+      if ((int)threadIdx.x < s2) sh[threadIdx.x] += sh[threadIdx.x + s2];
+      __syncthreads();
+    }
+    t2 = sh[threadIdx.x % KP];
+  }
+  const int c = threadIdx.x;
+  if (c >= k) return;
+  if (MODE == 0) {
+    st[C_ALPHA * k + c] = t1 != 0.0 ? st[C_RHO * k + c] / t1 : 0.0;
+  } else if (MODE == 1) {
+    const double rho0 = st[C_RHO * k + c];
+    st[C_RHO0 * k + c] = rho0;
+    st[C_RHO * k + c] = t1;
+    st[C_BETA * k + c] = rho0 != 0.0 ? t1 / rho0 : 0.0;
+  } else if (MODE == 2) {
+    const double pq = st[C_PQ * k + c];
+    st[C_BETA * k + c] = pq != 0.0 ? t1 / pq : 0.0;
+  } else {
+    st[C_PQ * k + c] = t1;
+    st[C_ALPHA * k + c] = t1 != 0.0 ? t2 / t1 : 0.0;
+  }
+}
+
+// P = Z + sb * beta .* P
+template <typename T, int KP>
+__global__ void __launch_bounds__(NT) k_cg_p(const T* __restrict__ Z, int64_t ldz, T* __restrict__ P, int64_t ldp,
+                                            int64_t m, int k, const double* __restrict__ st, double sb) {
+  const int tx = threadIdx.x % KP, ty = threadIdx.x / KP;
+  constexpr int RS = NT / KP;
+  if (tx >= k) return;
+  const double b = sb * st[C_BETA * k + tx];
+  for (int64_t r = (int64_t)blockIdx.x * RS + ty; r < m; r += (int64_t)gridDim.x * RS) {
+    T* p = P + r * ldp + tx;
+    *p = Cvt<T>::from_d(ld_d(Z + r * ldz + tx) + b * ld_d(p));
+  }
+}
+
+// X += alpha P, R -= alpha Q, |R|^2 -> rr, flags; IDP: rho0 = rho, rho = rr, beta
+template <typename T, int KP, bool IDP>
+__global__ void __launch_bounds__(NT) k_cg_xr(T* __restrict__ X, int64_t ldx, const T* __restrict__ P, int64_t ldp,
+                                             T* __restrict__ R, int64_t ldr, const T* __restrict__ Q, int64_t ldq,
+                                             int64_t m, int k, double* __restrict__ part,
+                                             unsigned* __restrict__ counter, double* __restrict__ st,
+                                             int* __restrict__ flags, double tol) {
+  __shared__ double sh[NT];
+  const int tx = threadIdx.x % KP, ty = threadIdx.x / KP;
+  constexpr int RS = NT / KP;
+  double acc = 0.0;
+  if (tx < k) {
+    const double al = st[C_ALPHA * k + tx];
+    for (int64_t r = (int64_t)blockIdx.x * RS + ty; r < m; r += (int64_t)gridDim.x * RS) {
+      T* x = X + r * ldx + tx;
+      *x = Cvt<T>::from_d(ld_d(x) + al * ld_d(P + r * ldp + tx));
+      T* rr = R + r * ldr + tx;
+      const T nv = Cvt<T>::from_d(ld_d(rr) - al * ld_d(Q + r * ldq + tx));
+      *rr = nv;
+      const double vd = Cvt<T>::to_d(nv);
+      acc += vd * vd;
+    }
+  }
+  block_col_reduce<KP>(acc, sh, part, k);
+  double tot;
+  if (!last_block_total<KP>(part, k, counter, sh, tot)) return;
+  const int c = threadIdx.x;
+  if (c >= k) return;
+  st[C_RR * k + c] = tot;
+  flags[c] = sqrt(tot) < tol * st[C_NRMB * k + c] ? 1 : 0;
+  if (IDP) {
+    const double rho0 = st[C_RHO * k + c];
+    st[C_RHO0 * k + c] = rho0;
+    st[C_RHO * k + c] = tot;
+    st[C_BETA * k + c] = rho0 != 0.0 ? tot / rho0 : 0.0;
+  }
+}
+
 }  // namespace
 
 // Y (nr x k) = M (nr x nc, row-major, ld ldm) X (nc x k, ld ldx), k <= 8, f32/f64
@@ -452,6 +609,76 @@ SL_API int sl_lsqr_step(void* X, int64_t ldx, void* W, int64_t ldw, const void* 
     SL_HIP_CHECK(hipMemsetAsync(part, 0, (size_t)k * 8, s));
   }
   k_lsqr_scalars<<<1, NT, 0, s>>>(part, (int)g, k, st, flags, tol, eps, max_stag);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ---------------------------------------------------------------- CG / FCG
+SL_API int sl_cg_nstate() { return C_NS; }
+
+// grid of the CG passes: at most one block per CU-ish (the last block reduces
+// every block's partial, so fewer, fatter blocks keep that tail short)
+static unsigned cg_blocks(int64_t m, int kp) {
+  unsigned g = part_blocks(m, kp);
+  return g > 256 ? 256 : g;
+}
+
+// dots with the CG state epilogue (mode: 0 alpha = rho / X.Y; 1 rho, beta from
+// X.Y; 2 FCG beta = X.Y / pq; 3 FCG pq = X.Y, alpha = X.Y2 / pq).  ws: 2 x
+// sl_krylov_ws_bytes; counter: a zeroed unsigned the kernel leaves zeroed.
+SL_API int sl_cg_dot(const void* X, int64_t ldx, const void* Y, int64_t ldy, const void* Y2, int64_t ldy2, int64_t m,
+                     int k, int dtype, int mode, double* st, void* ws, unsigned* counter, void* stream) {
+  if (k < 1 || k > 64 || m < 1 || mode < 0 || mode > 3) { sl_set_last_error("cg_dot: 1 <= k <= 64, m >= 1"); return SL_ERR_UNSUPPORTED; }
+  hipStream_t s = (hipStream_t)stream;
+  const int kp = kp_of(k);
+  const unsigned g = cg_blocks(m, kp);
+  double* part = (double*)ws;
+  double* part2 = part + (int64_t)MAXPART * k;
+  SL_DISPATCH_FLOAT(dtype, T, {
+    SL_KP_DISPATCH(kp, {
+      const T* x = (const T*)X; const T* y = (const T*)Y; const T* y2 = (const T*)Y2;
+      switch (mode) {
+        case 0: k_cg_dot<T, KP, 0><<<g, NT, 0, s>>>(x, ldx, y, ldy, y2, ldy2, m, k, part, part2, counter, st); break;
+        case 1: k_cg_dot<T, KP, 1><<<g, NT, 0, s>>>(x, ldx, y, ldy, y2, ldy2, m, k, part, part2, counter, st); break;
+        case 2: k_cg_dot<T, KP, 2><<<g, NT, 0, s>>>(x, ldx, y, ldy, y2, ldy2, m, k, part, part2, counter, st); break;
+        default: k_cg_dot<T, KP, 3><<<g, NT, 0, s>>>(x, ldx, y, ldy, y2, ldy2, m, k, part, part2, counter, st); break;
+      }
+    })
+  });
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// P = Z + sb * beta .* P
+SL_API int sl_cg_p(const void* Z, int64_t ldz, void* P, int64_t ldp, int64_t m, int k, int dtype, const double* st,
+                   double sb, void* stream) {
+  if (m <= 0) return SL_OK;
+  if (k < 1 || k > 64) { sl_set_last_error("cg_p: 1 <= k <= 64"); return SL_ERR_UNSUPPORTED; }
+  hipStream_t s = (hipStream_t)stream;
+  const int kp = kp_of(k);
+  const unsigned g = part_blocks(m, kp);
+  SL_DISPATCH_FLOAT(dtype, T, {
+    SL_KP_DISPATCH(kp, k_cg_p<T, KP><<<g, NT, 0, s>>>((const T*)Z, ldz, (T*)P, ldp, m, k, st, sb))
+  });
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// X += alpha P, R -= alpha Q, |R|^2, flags (|R| < tol |B|); idp: also rho, beta
+SL_API int sl_cg_xr(void* X, int64_t ldx, const void* P, int64_t ldp, void* R, int64_t ldr, const void* Q, int64_t ldq,
+                    int64_t m, int k, int dtype, int idp, double* st, int* flags, double tol, void* ws,
+                    unsigned* counter, void* stream) {
+  if (k < 1 || k > 64 || m < 1) { sl_set_last_error("cg_xr: 1 <= k <= 64, m >= 1"); return SL_ERR_UNSUPPORTED; }
+  hipStream_t s = (hipStream_t)stream;
+  const int kp = kp_of(k);
+  const unsigned g = cg_blocks(m, kp);
+  double* part = (double*)ws;
+  SL_DISPATCH_FLOAT(dtype, T, {
+    SL_KP_DISPATCH(kp, {
+      if (idp) k_cg_xr<T, KP, true><<<g, NT, 0, s>>>((T*)X, ldx, (const T*)P, ldp, (T*)R, ldr, (const T*)Q, ldq, m, k, part, counter, st, flags, tol);
+      else k_cg_xr<T, KP, false><<<g, NT, 0, s>>>((T*)X, ldx, (const T*)P, ldp, (T*)R, ldr, (const T*)Q, ldq, m, k, part, counter, st, flags, tol);
+    })
+  });
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

@@ -33,66 +33,109 @@ namespace {
 
 constexpr int NT = 512;      // threads per workgroup of the small-LA kernels
 constexpr int KMAX = 64;
+constexpr int RED = KMAX + 16;   // doubles of small scratch (max diag, D^{-1/2})
+constexpr int CH_MAX = 64;       // rows of W per workgroup of the partial-Gram phase
+
+#ifdef SL_CORE_STAMPS
+// diagnostic build only: phase times (100 MHz s_memrealtime) of k_gram_la
+__device__ unsigned long long g_core_st[32];
+#define SL_CST(I) \
+  if (threadIdx.x == 0) g_core_st[(I)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define SL_CST(I)
+#endif
 
 enum : int { ST_PIVOT = 1, ST_NONFINITE = 2, ST_NOCONV = 4, ST_RANK = 8 };
 
 // ---------------------------------------------------------------- Cholesky
-// In LDS: G (k x ld) symmetric (upper triangle read) -> R (upper, k x ld,
-// lower part zeroed).  A pivot at or below 1e-13 * max diag drops that
-// direction (its row of R is zero) and sets ST_PIVOT.  One barrier per step:
-// every thread scales the pivot row entries it needs itself.
-__device__ void chol_upper(const double* G, double* R, double* T, int k, int ld, int* st, double* red) {
-  const int tid = threadIdx.x;
-  for (int e = tid; e < k * ld; e += NT) T[e] = G[e];
-  if (tid == 0) {
-    double mx = 0.0;
-    for (int i = 0; i < k; ++i) mx = fmax(mx, fabs(G[i * ld + i]));
-    red[0] = mx;
+// f64 reciprocal / reciprocal square root: hardware estimate + two Newton steps
+__device__ __forceinline__ double rcp64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = r * fma(-d, r, 2.0);
+  r = r * fma(-d, r, 2.0);
+  return r;
+}
+__device__ __forceinline__ double rsq64(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  r = r * fma(-0.5 * d * r, r, 1.5);
+  r = r * fma(-0.5 * d * r, r, 1.5);
+  return r;
+}
+
+// X = R^{-1} (upper, k x k) of the Cholesky factor G = R^T R, from ONE LDL^T
+// elimination of the augmented [G | I]: eliminating below pivot j turns the
+// right block into L^{-1} (unit lower), and R^{-1} = L^{-T} D^{-1/2}.
+// Register-resident: thread (g = tid >> 6, c = tid & 63) holds entries
+// (i, c) of both blocks for its rows i = g + 8u, u < 8; a step reads the
+// pivot row from a 2-deep LDS row buffer (written by its owner one step
+// earlier), updates in registers and publishes the next pivot row: ONE
+// barrier and one LDS round trip per step.  Full rows are updated, so the
+// trailing block stays symmetric and T[j][i] is the multiplier numerator of
+// row i.  A pivot at or below 1e-13 x max diag drops its direction (that
+// column of X is zero) and sets ST_PIVOT.  G and X may be LDS or global (ldg,
+// ldx) and may alias.  red: >= KMAX + 2 doubles of LDS scratch.
+__device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
+  __shared__ double rb[2][2][KMAX];
+  const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
+  constexpr int RU = KMAX / (NT / 64);
+  double T[RU], L[RU];
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int i = g + 8 * u;
+    T[u] = (i < k && c < k) ? G[i * ldg + c] : 0.0;
+    L[u] = (i == c && i < k) ? 1.0 : 0.0;
+  }
+  if (g == 0) {
+    double v = c < k ? fabs(G[c * ldg + c]) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    if (c == 0) red[0] = v;
+    rb[0][0][c] = T[0];
+    rb[0][1][c] = L[0];
   }
   __syncthreads();
   const double thr = 1e-13 * red[0];
   for (int j = 0; j < k; ++j) {
-    const double d = T[j * ld + j];
+    const int buf = j & 1;
+    const double d = rb[buf][0][j];
+    const double tj = rb[buf][0][c], lj = rb[buf][1][c];
+    double num[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) num[u] = rb[buf][0][(g + 8 * u) & (KMAX - 1)];
     const bool ok = d > thr && d == d;
-    const double rs = ok ? 1.0 / sqrt(d) : 0.0;
-    // row j of R
-    for (int l = tid; l < k; l += NT) R[j * ld + l] = l < j ? 0.0 : T[j * ld + l] * rs;
-    // trailing update of the upper triangle (reads only row j of T)
-    if (ok) {
-      const double rd = 1.0 / d;
-      for (int e = tid; e < k * k; e += NT) {
-        const int i = e / k, l = e - i * k;
-        if (i > j && l >= i) T[i * ld + l] -= T[j * ld + i] * T[j * ld + l] * rd;
+    const double rd = ok ? rcp64(d) : 0.0;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int i = g + 8 * u;
+      if (i > j && i < k) {
+        const double f = num[u] * rd;
+        T[u] = fma(-f, tj, T[u]);
+        L[u] = fma(-f, lj, L[u]);
       }
-    } else if (tid == 0) {
-      *st |= ST_PIVOT;
+    }
+    // publish pivot row j + 1 (final after this step's update)
+    const int j1 = j + 1;
+    if (j1 < k && g == (j1 & 7)) {
+      double t1 = 0.0, l1 = 0.0;
+#pragma unroll
+      for (int u = 0; u < RU; ++u)
+        if (u == (j1 >> 3)) { t1 = T[u]; l1 = L[u]; }
+      rb[buf ^ 1][0][c] = t1;
+      rb[buf ^ 1][1][c] = l1;
+    }
+    if (tid == 0) {
+      red[2 + j] = ok ? rsq64(d) : 0.0;
+      if (!ok) *st |= ST_PIVOT;
     }
     __syncthreads();
   }
-}
-
-// X = R^{-1} for upper-triangular R (zero rows stay zero): eliminate column i
-// of R from the identity, i = k-1 .. 0; two barriers per step.
-__device__ void tri_inv_upper(const double* R, double* X, int k, int ld) {
-  const int tid = threadIdx.x;
-  for (int e = tid; e < k * ld; e += NT) {
-    const int i = e / ld, c = e - i * ld;
-    X[e] = (i == c && c < k) ? 1.0 : 0.0;
+  // X[c][i] = L[i][c] D_i^{-1/2} for c <= i
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int i = g + 8 * u;
+    if (i < k && c < k) X[c * ldx + i] = c <= i ? L[u] * red[2 + i] : 0.0;
   }
   __syncthreads();
-  for (int i = k - 1; i >= 0; --i) {
-    const double rii = R[i * ld + i];
-    const double ri = rii != 0.0 ? 1.0 / rii : 0.0;
-    // X[i][*] /= R[i][i]  (row i of X only has entries at c >= i)
-    for (int c = tid; c < k; c += NT) X[i * ld + c] *= ri;
-    __syncthreads();
-    // rows p < i:  X[p][c] -= R[p][i] X[i][c]
-    for (int e = tid; e < i * k; e += NT) {
-      const int p = e / k, c = e - p * k;
-      if (c >= i) X[p * ld + c] -= R[p * ld + i] * X[i * ld + c];
-    }
-    __syncthreads();
-  }
 }
 
 // C = A^T B (transa) or A B for k x k LDS matrices, four outputs per thread
@@ -121,11 +164,14 @@ __device__ void small_gemm(const double* A, const double* B, double* C, int k, i
 struct Rot { double c, s, t; bool rot; };
 
 // rotation zeroing a_pq of the (p, q) plane (J = [[c, s], [-s, c]]).
-// big: this pair was still coupled above 1e-6 relative before the rotation.
-__device__ __forceinline__ Rot jrot(double app, double aqq, double apq, bool* big) {
+// big: this pair was still coupled above 1e-6 relative before the rotation
+// and above the roundoff floor of the matrix (noise2 = (1e-14 max|a_ii|)^2:
+// rotations of other pairs keep re-seeding off-diagonals at eps * |A|, which
+// a purely relative test on tiny eigenvalues would chase for many sweeps).
+__device__ __forceinline__ Rot jrot(double app, double aqq, double apq, double noise2, bool* big) {
   Rot r{1.0, 0.0, 0.0, false};
   const double pq2 = apq * apq, dd = fabs(app * aqq);
-  *big = pq2 > 1e-12 * dd;
+  *big = pq2 > 1e-12 * dd && pq2 > noise2;
   if (!(pq2 > 2.5e-32 * dd) || apq == 0.0) return r;
   const double d = aqq - app;
   // f32 estimate of the tangent of the smaller angle (t^2 + 2 tau t - 1 = 0)
@@ -160,7 +206,8 @@ __device__ __forceinline__ int player(int pos, int rd, int kp) { return pos == 0
 // into an LDS table; barrier; (2) waves 4-7 apply them to the upper 2 x 2
 // blocks of A (and mirror), waves 0-3 to the rows of V (lane = row);
 // barrier.  The pair schedule of every round is tabulated once.
-__device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int max_sweeps, int* flags, int* st) {
+__device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int max_sweeps, int* flags, int* st,
+                          bool v_given = false) {
   (void)B;
   __shared__ unsigned short btab[KMAX / 2 * (KMAX / 2 + 1) / 2];
   __shared__ unsigned short rtab[(KMAX - 1) * (KMAX / 2)];
@@ -168,9 +215,11 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hp = kp / 2;
   const int nA = hp * (hp + 1) / 2;
-  for (int e = tid; e < kp * ld; e += NT) {
-    const int i = e / ld, c = e - i * ld;
-    V[e] = (i == c) ? 1.0 : 0.0;
+  if (!v_given) {
+    for (int e = tid; e < kp * ld; e += NT) {
+      const int i = e / ld, c = e - i * ld;
+      V[e] = (i == c) ? 1.0 : 0.0;
+    }
   }
   if (tid < 3) flags[tid] = 0;
   for (int b = tid; b < nA; b += NT) {
@@ -185,7 +234,20 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
     if (p > q) { const int x = p; p = q; q = x; }
     rtab[e] = (unsigned short)(p | (q << 8));
   }
+  if (tid < 64) {
+    double v = tid < kp ? fabs(A[tid * ld + tid]) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    if (tid == 0) rot_c[0] = v;
+  }
   __syncthreads();
+  const double amax = rot_c[0];
+  const double noise2 = (1e-14 * amax) * (1e-14 * amax);
+  __syncthreads();
+#ifdef SL_CORE_STAMPS
+  unsigned long long c1 = 0, c2 = 0, nr = 0;
+  const unsigned long long ct0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // this thread's first A block (held in registers)
   int b0i = 0, b0j = 0;
   if (tid >= 256 && tid - 256 < nA) { b0i = btab[tid - 256] & 255; b0j = btab[tid - 256] >> 8; }
@@ -196,17 +258,24 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
     if (tid == 0) flags[(sweep + 1) % 3] = 0;
     for (int rd = 0; rd < kp - 1; ++rd) {
       const unsigned short* rt = rtab + rd * hp;
+#ifdef SL_CORE_STAMPS
+      const unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
       // (1) rotations of the round's pairs
       if (tid < hp) {
         const int p = rt[tid] & 255, q = rt[tid] >> 8;
         bool big;
-        const Rot R = jrot(A[p * ld + p], A[q * ld + q], A[p * ld + q], &big);
+        const Rot R = jrot(A[p * ld + p], A[q * ld + q], A[p * ld + q], noise2, &big);
         if (big) *flag = 1;
         rot_c[tid] = R.c;
         rot_s[tid] = R.s;
         rot_t[tid] = R.rot ? R.t : 0.0;
       }
       __syncthreads();
+#ifdef SL_CORE_STAMPS
+      const unsigned long long tb = __builtin_amdgcn_s_memtime();
+      c1 += tb - ta;
+#endif
       // (2) apply: waves 4-7 the blocks of A, waves 0-3 the rows of V
       if (wid >= 4) {
 #pragma unroll 1
@@ -232,28 +301,54 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
             A[pj * ld + pi] = z00; A[qj * ld + pi] = z01; A[pj * ld + qi] = z10; A[qj * ld + qi] = z11;
           }
         }
-      } else {
-        // V <- V J: item e = (row v, pair j), e = tid, tid + 256, ...
-#pragma unroll 1
-        for (int e = tid; e < kp * hp; e += 256) {
-          const int v = e / hp, j = e - v * hp;
-          const unsigned short pq = rt[j];
-          const double t = rot_t[j], c = rot_c[j], sn = rot_s[j];
-          const int p = pq & 255, q = pq >> 8;
-          double* vr = V + v * ld;
-          const double vp = vr[p], vq = vr[q];
-          if (t != 0.0) {
-            vr[p] = c * vp - sn * vq;
-            vr[q] = sn * vp + c * vq;
+      } else if (lane < kp) {
+        // V <- V J: row `lane`, pairs wid, wid + 4, ... (loads first, then
+        // the rotations: no dependent LDS round trips inside the loop)
+        double* vr = V + lane * ld;
+        constexpr int JU = KMAX / 2 / 4;
+        int pp[JU], qq[JU];
+        double vp[JU], vq[JU];
+#pragma unroll
+        for (int u = 0; u < JU; ++u) {
+          const int j = wid + 4 * u;
+          const unsigned short pq = j < hp ? rt[j] : (unsigned short)0;
+          pp[u] = pq & 255;
+          qq[u] = pq >> 8;
+        }
+#pragma unroll
+        for (int u = 0; u < JU; ++u) {
+          vp[u] = vr[pp[u]];
+          vq[u] = vr[qq[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < JU; ++u) {
+          const int j = wid + 4 * u;
+          if (j < hp && rot_t[j] != 0.0) {
+            const double c = rot_c[j], sn = rot_s[j];
+            vr[pp[u]] = c * vp[u] - sn * vq[u];
+            vr[qq[u]] = sn * vp[u] + c * vq[u];
           }
         }
       }
       __syncthreads();
+#ifdef SL_CORE_STAMPS
+      c2 += __builtin_amdgcn_s_memtime() - tb;
+      ++nr;
+#endif
     }
     if (!*flag) { conv = true; ++sweep; break; }
   }
   if (!conv && tid == 0) *st |= ST_NOCONV;
   if (tid == 0) flags[3] = sweep;
+#ifdef SL_CORE_STAMPS
+  if (tid == 0) {
+    g_core_st[25] = c1;
+    g_core_st[26] = c2;
+    g_core_st[27] = nr;
+    g_core_st[28] = __builtin_amdgcn_s_memtime() - ct0;
+    g_core_st[29] = __builtin_amdgcn_s_memrealtime() - rt0;
+  }
+#endif
   __syncthreads();
   return A;
 }
@@ -264,7 +359,7 @@ __global__ void __launch_bounds__(NT)
 k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restrict__ part,
           unsigned* __restrict__ counter, const double* __restrict__ Gy, int r, double* __restrict__ Rinv,
           float* __restrict__ M, double* __restrict__ N, double* __restrict__ s_out, int* __restrict__ status,
-          int max_sweeps) {
+          int max_sweeps, double* __restrict__ V0, int* __restrict__ v0_valid) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int tid = threadIdx.x;
   const int ld = k + 1;
@@ -273,31 +368,57 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
   double* b1 = sm + mat;
   double* b2 = sm + 2 * mat;
   double* b3 = sm + 3 * mat;
-  double* red = sm + 4 * mat;           // small scratch (16 doubles)
-  int* iscr = (int*)(red + 16);         // flags[4], order[KMAX], is_last
+  double* red = sm + 4 * mat;           // small scratch (RED doubles)
+  int* iscr = (int*)(red + RED);        // flags[4], order[KMAX], is_last
   int* flags = iscr;
   int* order = iscr + 4;
   int* is_last = iscr + 4 + KMAX;
   __shared__ int st_sh;
+  constexpr int SO = FINAL ? 16 : 0;
+  if (blockIdx.x == 0) { SL_CST(SO + 0) }
 
-  // ---- partial Gram of this workgroup's rows (upper triangle, f64)
+  // ---- partial Gram of this workgroup's rows (upper triangle, f64).
+  //      Thread (g, c) = (tid >> 6, tid & 63) owns entries (g + 8u, c), u < 8;
+  //      the row operand is a wave-wide broadcast from LDS.
   const int ng = gridDim.x;
   const int ch = (n + ng - 1) / ng;
   const int r0 = blockIdx.x * ch, r1 = min(n, r0 + ch);
   const int nr = r1 > r0 ? r1 - r0 : 0;
-  double* chunk = b0;   // nr x k (row stride k)
-  for (int e = tid; e < nr * k; e += NT) {
-    const int i = e / k, c = e - i * k;
-    chunk[e] = W[(int64_t)(r0 + i) * ldw + c];
+  const int gq = tid >> 6, cq = tid & 63;
+  double* chunk = b0;   // nr x KMAX
+  {
+    // every row load of this thread in flight at once (a chunk is <= CH_MAX rows)
+    constexpr int CU = CH_MAX / (NT / 64);
+    double v[CU];
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const int row = gq + 8 * u;
+      v[u] = (row < nr && cq < k) ? W[(int64_t)(r0 + row) * ldw + cq] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < CU; ++u) {
+      const int row = gq + 8 * u;
+      if (row < nr && cq < k) chunk[row * KMAX + cq] = v[u];
+    }
   }
   __syncthreads();
   double* myp = part + (int64_t)blockIdx.x * k * k;
-  for (int e = tid; e < k * k; e += NT) {
-    const int i = e / k, c = e - i * k;
-    if (c < i) continue;
-    double a = 0.0;
-    for (int row = 0; row < nr; ++row) a += chunk[row * k + i] * chunk[row * k + c];
-    myp[e] = a;
+  {
+    double acc[KMAX / 8];
+#pragma unroll
+    for (int u = 0; u < KMAX / 8; ++u) acc[u] = 0.0;
+    if (cq < k) {
+      for (int row = 0; row < nr; ++row) {
+        const double x = chunk[row * KMAX + cq];
+#pragma unroll
+        for (int u = 0; u < KMAX / 8; ++u) acc[u] += chunk[row * KMAX + gq + 8 * u] * x;
+      }
+#pragma unroll
+      for (int u = 0; u < KMAX / 8; ++u) {
+        const int i = gq + 8 * u;
+        if (i <= cq) myp[i * k + cq] = acc[u];
+      }
+    }
   }
   // ---- publish, count, last arriver continues (release / acquire, agent scope)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -315,40 +436,62 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
   }
   __syncthreads();
   if (!*is_last) return;
+  SL_CST(SO + 1)
 
   // ---- H = sum of the partials (symmetric, f64) -> b0
-  for (int e = tid; e < k * k; e += NT) {
-    const int i = e / k, c = e - i * k;
-    if (c < i) continue;
-    double a = 0.0;
-    for (int g = 0; g < ng; ++g) a += part[(int64_t)g * k * k + e];
-    b0[i * ld + c] = a;
-    b0[c * ld + i] = a;
+  {
+    // H entries (i, cq), i = gq + 8u: the ng partials of all of them in flight together
+    constexpr int RU = KMAX / (NT / 64);
+    double a[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) a[u] = 0.0;
+    for (int g0 = 0; g0 < ng; g0 += 4) {
+      double v[4][RU];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int i = gq + 8 * u, gg = g0 + q;
+          v[q][u] = (gg < ng && i < k && cq < k && cq >= i)
+                        ? __builtin_nontemporal_load(part + (int64_t)gg * k * k + i * k + cq) : 0.0;
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < RU; ++u) a[u] += v[q][u];
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int i = gq + 8 * u;
+      if (i < k && cq < k && cq >= i) {
+        b0[i * ld + cq] = a[u];
+        b0[cq * ld + i] = a[u];
+      }
+    }
   }
   if (tid == 0) *counter = 0u;   // ready for the next launch (graph replays)
   __syncthreads();
+  SL_CST(SO + 2)
   if (!FINAL) {
     // ---- INTER: H = R^T R, X = R^{-1} (f64, k x k) -> Rinv
-    chol_upper(b0, b1, b2, k, ld, &st_sh, red);
-    tri_inv_upper(b1, b2, k, ld);
-    for (int e = tid; e < k * k; e += NT) {
-      const int i = e / k, c = e - i * k;
-      const double v = b2[i * ld + c];
-      if (!(fabs(v) < 1e300)) atomicOr(&st_sh, ST_NONFINITE);
-      Rinv[e] = v;
+    chol_inv(b0, ld, b2, ld, k, &st_sh, red);
+    SL_CST(SO + 3)
+    for (int i = tid >> 6; i < k; i += NT / 64) {
+      const int c = tid & 63;
+      if (c < k) {
+        const double v = b2[i * ld + c];
+        if (!(fabs(v) < 1e300)) atomicOr(&st_sh, ST_NONFINITE);
+        Rinv[i * k + c] = v;
+      }
     }
     __syncthreads();
     if (tid == 0) atomicOr(status, st_sh);
+    SL_CST(SO + 4)
     return;
   }
-  // ---- FINAL: Y^T Y = Rt^T Rt (b1 <- Gy, Rt -> b2), Rti -> b3
-  for (int e = tid; e < k * k; e += NT) {
-    const int i = e / k, c = e - i * k;
-    b1[i * ld + c] = Gy[e];
-  }
-  __syncthreads();
-  chol_upper(b1, b2, b3, k, ld, &st_sh, red);   // b3 scratch
-  tri_inv_upper(b2, b3, k, ld);                 // Rti in b3
+  // ---- FINAL: Y^T Y = Rt^T Rt, Rti = Rt^{-1} -> b3 (straight from Gy; H in b0 survives)
+  chol_inv(Gy, k, b3, ld, k, &st_sh, red);
+  SL_CST(SO + 3)
   // C = Rti^T H Rti:  T = H Rti -> b1, C = Rti^T T -> b2
   small_gemm(b0, b3, b1, k, ld, false);
   __syncthreads();
@@ -363,13 +506,45 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
     b0[i * ld + c] = v;
   }
   __syncthreads();
-  for (int e = tid; e < kp * kp; e += NT) {
-    const int i = e / kp, c = e - i * kp;
-    b2[i * ld + c] = b0[i * ld + c];
+  // warm start: C' = V0^T C V0 with the previous call's eigenvectors V0
+  // (any orthogonal V0 is a valid start; on a repeated problem C' is already
+  // diagonal and one sweep confirms it)
+  const bool warm = V0 != nullptr && v0_valid != nullptr && *v0_valid == kp;
+  if (warm) {
+    for (int e = tid; e < kp * kp; e += NT) {
+      const int i = e / kp, c = e - i * kp;
+      b1[i * ld + c] = V0[e];
+    }
+    __syncthreads();
+    small_gemm(b0, b1, b2, kp, ld, false);    // T = C V0
+    __syncthreads();
+    small_gemm(b1, b2, b0, kp, ld, true);     // C' = V0^T T
+    __syncthreads();
+    for (int e = tid; e < kp * kp; e += NT) {
+      const int i = e / kp, c = e - i * kp;
+      b2[i * ld + c] = 0.5 * (b0[i * ld + c] + b0[c * ld + i]);
+    }
+  } else {
+    for (int e = tid; e < kp * kp; e += NT) {
+      const int i = e / kp, c = e - i * kp;
+      b2[i * ld + c] = b0[i * ld + c];
+    }
   }
   __syncthreads();
-  // Jacobi on b2 (ping-pong b0), V in b1
-  double* Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, &st_sh);
+  SL_CST(SO + 4)
+  // Jacobi on b2, V in b1 (V0 when warm)
+  double* Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, &st_sh, warm);
+  SL_CST(SO + 5)
+#ifdef SL_CORE_STAMPS
+  if (tid == 0) g_core_st[SO + 8] = flags[3];
+#endif
+  if (V0 != nullptr) {
+    for (int e = tid; e < kp * kp; e += NT) {
+      const int i = e / kp, c = e - i * kp;
+      V0[e] = b1[i * ld + c];
+    }
+    if (tid == 0) *v0_valid = kp;
+  }
   // ---- descending order of the k eigenvalues (rank by comparison)
   for (int i = tid; i < k; i += NT) {
     const double li = Af[i * ld + i];
@@ -399,30 +574,58 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
     N[e] = lam > 0.0 ? a / sqrt(lam) : 0.0;
   }
   if (tid == 0) atomicOr(status, st_sh);
+  SL_CST(SO + 6)
+}
+
+// Out (rows of W, k x nc) = W (n x k f64) B (k x nc f64, row-major), a 32-row
+// slab of W and all of B staged in LDS with coalesced loads; thread
+// (row = t & 31, column group t >> 5) forms columns cg, cg + 8, ... of its row.
+template <typename Store>
+__device__ __forceinline__ void rows_times_small(const double* __restrict__ W, int n, int k, int ldw,
+                                                 const double* __restrict__ B, int nc, Store store) {
+  __shared__ double Ws[32][KMAX + 1];
+  __shared__ double Bs[KMAX][KMAX];
+  const int t = threadIdx.x, row = t & 31, cg = t >> 5;
+  const int i0 = blockIdx.x * 32;
+  for (int e = t; e < k * nc; e += 256) {
+    const int l = e / nc;
+    Bs[l][e - l * nc] = B[e];
+  }
+  const int nr = min(32, n - i0);
+  for (int e = t; e < nr * k; e += 256) {
+    const int rr = e / k;
+    Ws[rr][e - rr * k] = W[(int64_t)(i0 + rr) * ldw + (e - rr * k)];
+  }
+  __syncthreads();
+  if (row >= nr) return;
+  double acc[KMAX / 8];
+#pragma unroll
+  for (int u = 0; u < KMAX / 8; ++u) acc[u] = 0.0;
+  for (int l = 0; l < k; ++l) {
+    const double w = Ws[row][l];
+#pragma unroll
+    for (int u = 0; u < KMAX / 8; ++u) acc[u] += w * Bs[l][(cg + 8 * u) & (KMAX - 1)];
+  }
+#pragma unroll
+  for (int u = 0; u < KMAX / 8; ++u) {
+    const int c = cg + 8 * u;
+    if (c < nc) store(i0 + row, c, acc[u]);
+  }
 }
 
 // Z^T (k x n bf16) = (W R^{-1})^T, R^{-1} upper triangular (k x k f64)
 __global__ void __launch_bounds__(256)
 k_make_zt(const double* __restrict__ W, int n, int k, int ldw, const double* __restrict__ Rinv, bf16_t* __restrict__ Zt) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)n * k) return;
-  const int c = (int)(t / n), i = (int)(t - (int64_t)c * n);
-  double a = 0.0;
-  for (int l = 0; l <= c; ++l) a += W[(int64_t)i * ldw + l] * Rinv[l * k + c];
-  Zt[(int64_t)c * n + i] = f_to_bf16((float)a);
+  rows_times_small(W, n, k, ldw, Rinv, k,
+                   [&](int i, int c, double v) { Zt[(int64_t)c * n + i] = f_to_bf16((float)v); });
 }
 
 // V (n x r f32) = W (n x k f64) N (k x r f64); s32 = s64 (r)
 __global__ void __launch_bounds__(256)
 k_make_v(const double* __restrict__ W, int n, int k, int ldw, const double* __restrict__ N, int r, float* __restrict__ V,
          const double* __restrict__ s64, float* __restrict__ s32) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s32 && t < r) s32[t] = (float)s64[t];
-  if (t >= (int64_t)n * r) return;
-  const int i = (int)(t / r), c = (int)(t - (int64_t)i * r);
-  double a = 0.0;
-  for (int l = 0; l < k; ++l) a += W[(int64_t)i * ldw + l] * N[l * r + c];
-  V[t] = (float)a;
+  if (s32 && blockIdx.x == 0 && threadIdx.x < r) s32[threadIdx.x] = (float)s64[threadIdx.x];
+  rows_times_small(W, n, k, ldw, N, r, [&](int i, int c, double v) { V[(int64_t)i * r + c] = (float)v; });
 }
 
 // FJLT operator of the rowwise sketch A Omega^T, as the pass operand Z^T
@@ -442,11 +645,24 @@ k_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, in
   Zt[t] = f_to_bf16((float)(cos(w * (double)a) * (p == 0 ? c0 : c1) * scale * d));
 }
 
-size_t gram_la_lds() { return (size_t)(4 * KMAX * (KMAX + 1) + 16) * sizeof(double) + (4 + KMAX + 1) * sizeof(int); }
+// bf16(f32(x)): the realised f64 sketch operator as the pass operand, rounded
+// exactly as the Python path's tensor casts (f64 -> f32 -> bf16, both RNE)
+__global__ void __launch_bounds__(256) k_f64_to_bf16(const double* __restrict__ x, int64_t count, bf16_t* __restrict__ y) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < count) y[t] = f_to_bf16((float)x[t]);
+}
+
+size_t gram_la_lds() { return (size_t)(4 * KMAX * (KMAX + 1) + RED) * sizeof(double) + (4 + KMAX + 1) * sizeof(int); }
 
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
+#ifdef SL_CORE_STAMPS
+SL_API int sl_core_stamps(unsigned long long* host) {
+  SL_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_core_st), sizeof(g_core_st)));
+  return SL_OK;
+}
+#endif
 constexpr int SL_GRAM_NG = 16;   // workgroups of the partial-Gram phase
 
 SL_API int64_t sl_rsvd_gram_workspace(int k) { return (int64_t)SL_GRAM_NG * k * k * 8 + 256; }
@@ -455,8 +671,8 @@ SL_API int64_t sl_rsvd_gram_workspace(int k) { return (int64_t)SL_GRAM_NG * k * 
 // ws: sl_rsvd_gram_workspace(k) bytes, its first 4 bytes a zeroed counter
 // (the kernel leaves it zero again).
 SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, double* Rinv, int* status, void* stream) {
-  if (k < 1 || k > KMAX || n < 1 || (int64_t)((n + SL_GRAM_NG - 1) / SL_GRAM_NG) * k > 4 * KMAX * (KMAX + 1)) {
-    sl_set_last_error("rsvd_inter_la: 1 <= k <= 64 and n * k <= 266240");
+  if (k < 1 || k > KMAX || n < 1 || n > SL_GRAM_NG * CH_MAX) {
+    sl_set_last_error("rsvd_inter_la: 1 <= k <= 64 and 1 <= n <= 1024");
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -470,25 +686,28 @@ SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, do
   double* part = (double*)((char*)ws + 256);
   const int ng = n < SL_GRAM_NG ? n : SL_GRAM_NG;
   k_gram_la<false><<<ng, NT, gram_la_lds(), s>>>(W, n, k, ldw, part, counter, nullptr, 0, Rinv, nullptr, nullptr,
-                                                nullptr, status, 0);
+                                                nullptr, status, 0, nullptr, nullptr);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
 // Z^T = (W Rinv)^T as bf16 (k x n)
 SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double* Rinv, void* Zt, void* stream) {
-  const int64_t tot = (int64_t)n * k;
-  k_make_zt<<<(unsigned)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, Rinv, (bf16_t*)Zt);
+  if (k < 1 || k > KMAX) { sl_set_last_error("rsvd_make_zt: 1 <= k <= 64"); return SL_ERR_UNSUPPORTED; }
+  k_make_zt<<<(unsigned)((n + 31) / 32), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, Rinv, (bf16_t*)Zt);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
 // After the final pass: s (r), M (k x r f32), N (k x r f64) from W (n x k
 // f64) and the fp64 Gram of Y (k x k).
+// V0 (kp x kp f64, kp = k rounded up to even) + v0_valid: warm start of the
+// Jacobi from the previous call's eigenvectors (null: cold start each call).
 SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                            double* N, double* s, int* status, int max_sweeps, void* stream) {
-  if (k < 1 || k > KMAX || r < 1 || r > k || (int64_t)((n + SL_GRAM_NG - 1) / SL_GRAM_NG) * k > 4 * KMAX * (KMAX + 1)) {
-    sl_set_last_error("rsvd_final_la: 1 <= r <= k <= 64 and n * k <= 266240");
+                            double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
+                            void* stream) {
+  if (k < 1 || k > KMAX || r < 1 || r > k || n < 1 || n > SL_GRAM_NG * CH_MAX) {
+    sl_set_last_error("rsvd_final_la: 1 <= r <= k <= 64 and 1 <= n <= 1024");
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t st = (hipStream_t)stream;
@@ -502,15 +721,15 @@ SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double
   double* part = (double*)((char*)ws + 256);
   const int ng = n < SL_GRAM_NG ? n : SL_GRAM_NG;
   k_gram_la<true><<<ng, NT, gram_la_lds(), st>>>(W, n, k, ldw, part, counter, Gy, r, nullptr, M, N, s, status,
-                                                max_sweeps > 0 ? max_sweeps : 40);
+                                                max_sweeps > 0 ? max_sweeps : 40, V0, v0_valid);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream) {
-  const int64_t tot = (int64_t)n * r;
-  k_make_v<<<(unsigned)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, N, r, V, s64, s32);
+  if (k < 1 || k > KMAX || r > k) { sl_set_last_error("rsvd_make_v: 1 <= r <= k <= 64"); return SL_ERR_UNSUPPORTED; }
+  k_make_v<<<(unsigned)((n + 31) / 32), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, N, r, V, s64, s32);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -535,7 +754,7 @@ k_sym_eig_jacobi2(const double* __restrict__ C, int k, double* __restrict__ w, d
   const int ld = k + 1, mat = KMAX * (KMAX + 1);
   double *b0 = sm, *b1 = sm + mat, *b2 = sm + 2 * mat;
   double* red = sm + 4 * mat;
-  int* iscr = (int*)(red + 16);
+  int* iscr = (int*)(red + RED);
   int* flags = iscr;
   int* order = iscr + 4;
   __shared__ int st_sh;
@@ -575,6 +794,13 @@ SL_API int sl_sym_eig_jacobi2(const double* C, int k, double* w, double* V, int*
     attr = true;
   }
   k_sym_eig_jacobi2<<<1, NT, gram_la_lds(), (hipStream_t)stream>>>(C, k, w, V, status, max_sweeps > 0 ? max_sweeps : 40);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void* stream) {
+  if (count <= 0) return SL_OK;
+  k_f64_to_bf16<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(src, count, (bf16_t*)Zt);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

@@ -36,13 +36,18 @@ SL_API int64_t sl_rsvd_gram_workspace(int k);
 SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, double* Rinv, int* status, void* stream);
 SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double* Rinv, void* Zt, void* stream);
 SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                            double* N, double* s, int* status, int max_sweeps, void* stream);
+                            double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
+                            void* stream);
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream);
 SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
                            void* stream);
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
                          int64_t ldo, double* G, void* ws, void* stream);
+SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void* stream);
+SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_t base, int64_t rows, int64_t cols,
+                          int64_t sr, int64_t sc, int64_t r0, int64_t c0, int64_t ir, int64_t ic, double p0, double p1,
+                          double scale, int precise, void* stream);
 SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
                               void* stream);
 
@@ -63,6 +68,9 @@ struct Plan {
   float* M = nullptr;       // k x r
   double* N = nullptr;      // k x r
   double* s64 = nullptr;    // r
+  double* V0 = nullptr;     // kp x kp: the last core eigenvectors (Jacobi warm start)
+  int* v0_valid = nullptr;
+  bool warm = true;
   int* status = nullptr;
   // graph of the segments (single rank), valid for graph_A
   hipGraph_t graph = nullptr;
@@ -80,7 +88,7 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
   int rc = SL_OK;
   if (i == p->q + 1) {
     return sl_rsvd_final_la(p->WG, (int)p->n, p->k, p->k, p->WG + p->n * p->k, p->r, p->gram_ws, p->M, p->N,
-                            p->s64, p->status, 0, s);
+                            p->s64, p->status, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr, s);
   }
   if (i == 0) {
     SL_HIP_CHECK(hipMemsetAsync(p->status, 0, sizeof(int), s));
@@ -130,6 +138,8 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   const int64_t o_n = off;    off = align256(off + (int64_t)k * r * 8);
   const int64_t o_s = off;    off = align256(off + (int64_t)r * 8);
   const int64_t o_st = off;   off = align256(off + 16);
+  const int kp = k + (k & 1);
+  const int64_t o_v0 = off;   off = align256(off + (int64_t)kp * kp * 8 + 16);
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;
     sl_set_last_error("rsvd_plan: device allocation failed");
@@ -145,8 +155,10 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   p->N = (double*)(p->base + o_n);
   p->s64 = (double*)(p->base + o_s);
   p->status = (int*)(p->base + o_st);
+  p->V0 = (double*)(p->base + o_v0);
+  p->v0_valid = (int*)(p->base + o_v0 + (int64_t)kp * kp * 8);
   if (hipMemset(p->gram_ws, 0, (size_t)sl_rsvd_gram_workspace(k)) != hipSuccess ||
-      hipMemset(p->status, 0, 16) != hipSuccess) {
+      hipMemset(p->status, 0, 16) != hipSuccess || hipMemset(p->v0_valid, 0, 16) != hipSuccess) {
     (void)hipFree(p->base);
     delete p;
     sl_set_last_error("rsvd_plan: memset failed");
@@ -178,6 +190,15 @@ SL_API int sl_rsvd_plan_bind(void* plan, double* WG, int* status) {
   return SL_OK;
 }
 
+// Jacobi warm start from the previous call's core eigenvectors (default on;
+// off: every call starts the eigensolve from the identity)
+SL_API int sl_rsvd_plan_set_warm(void* plan, int warm) {
+  Plan* p = (Plan*)plan;
+  if (p->warm != (warm != 0)) drop_graph(p);
+  p->warm = warm != 0;
+  return SL_OK;
+}
+
 // pass-kernel tuning variant (3: 3-deep DMA ring instead of 4)
 SL_API int sl_rsvd_plan_set_variant(void* plan, int variant) {
   Plan* p = (Plan*)plan;
@@ -192,6 +213,19 @@ SL_API int sl_rsvd_plan_set_variant(void* plan, int variant) {
 SL_API int sl_rsvd_set_fjlt(void* plan, uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, void* stream) {
   Plan* p = (Plan*)plan;
   return sl_rsvd_fjlt_zt(seed, baseD, baseS, scale, p->k, (int)p->n, p->Zt, stream);
+}
+
+// Dense sketch operator (JLT: Normal, CT: Cauchy, ...) of the call: the k x n
+// matrix scale * dist(seed, base + j k + i) (reference dense_transform_data
+// column-major stream) realised in f64 on the device (in the W buffer, free
+// until the first reduce), then rounded f64 -> f32 -> bf16 into Z^T.
+SL_API int sl_rsvd_set_dense(void* plan, int dist, uint64_t seed, uint64_t base, double p0, double p1, double scale,
+                             void* stream) {
+  Plan* p = (Plan*)plan;
+  int rc = sl_fill_random(p->WG, SL_F64, dist, seed, base, p->k, p->n, p->n, 1, 0, 0, 1, p->k, p0, p1, scale, 1,
+                          stream);
+  if (rc != SL_OK) return rc;
+  return sl_rsvd_zt_from_f64(p->WG, p->n * p->k, p->Zt, stream);
 }
 
 // Sketch operator given explicitly (k x n bf16, device).

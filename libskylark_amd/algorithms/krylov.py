@@ -408,6 +408,8 @@ def cg(A, B, X=None, params: KrylovIterParams | None = None, M: Precond | None =
     # X lives where B does (row-distributed for a DistSymOp)
     X = torch.zeros_like(Bv) if X is None else op.long_like(X).to(dt).clone()
     Rr = Bv - op.matmul(X).to(dt)
+    if _kn.ok(Bv) and not op.distributed:
+        return _cg_native(op, Bv, X, Rr, params, M, tol, flexible=False)
     nrmb = op.long_colnorm(Bv)
     ressqr = op.long_coldot(Rr, Rr)
     P = torch.zeros_like(Rr)
@@ -442,6 +444,64 @@ def cg(A, B, X=None, params: KrylovIterParams | None = None, M: Precond | None =
     return X, code
 
 
+def _cg_native(op, Bv, X, Rr, params, M, tol, flexible: bool):
+    """Single-GPU (flexible) CG with device-resident scalars
+    (``krylov_kernels.hip``: every column reduction finished by its pass's last
+    block).  Per iteration, besides ``A P`` and the preconditioner:
+    CG 3 launches (``P = R + beta P``; ``P.Q`` -> alpha; ``X += alpha P``,
+    ``R -= alpha Q``, ``|R|`` -> rho, beta, flags), 4 with a preconditioner
+    (``R.Z`` -> rho, beta first); flexible CG 4 (``Q_prev.Z`` -> beta,
+    ``P = Z - beta P``, ``P.Q`` and ``P.R`` -> alpha, the X / R update).  The
+    stop flags reach the host every ``check_every`` iterations."""
+    k = Bv.shape[1]
+    dt = Bv.dtype
+    cs = _kn.CGState(k, Bv.device)
+    X = X.contiguous()
+    R = Rr.contiguous()
+    cs.st[_kn.C_NRMB] = _kn.colsumsq(Bv).sqrt()
+    idp = M.is_id and not flexible
+    if idp:
+        cs.st[_kn.C_RHO] = _kn.colsumsq(R)
+    P = torch.zeros_like(R)
+    Q = None
+    name = "FlexibleCG" if flexible else "CG"
+    code = -6
+    for itn in range(params.iter_lim):
+        if flexible:
+            Z = M.apply(R).to(dt)
+            if itn == 0:
+                P.copy_(Z)
+            else:
+                _kn.cg_dot(Q, Z, 2, cs)          # beta = Q_prev . Z / pq_prev
+                _kn.cg_p(Z, P, cs, -1.0)         # P = Z - beta P
+        elif idp:
+            _kn.cg_p(R, P, cs)                   # P = R + beta P
+        else:
+            Z = M.apply(R).to(dt)
+            _kn.cg_dot(R, Z, 1, cs)              # rho, beta
+            _kn.cg_p(Z, P, cs)
+        Q = op.matmul(P).to(dt)
+        if Q.stride(1) != 1:
+            Q = Q.contiguous()
+        if flexible:
+            _kn.cg_dot(P, Q, 3, cs, Y2=R)        # pq, alpha = P.R / pq
+        else:
+            _kn.cg_dot(P, Q, 0, cs)              # alpha = rho / P.Q
+        _kn.cg_xr(X, P, R, Q, cs, idp, tol)
+        if (itn + 1) % params.check_every == 0 or itn == params.iter_lim - 1:
+            conv = int(cs.flags.sum())
+            if params.log_level >= 2 and itn % max(1, params.res_print) == 0:
+                relres = float(cs.st[_kn.C_RR].sum().sqrt() / cs.st[_kn.C_NRMB].pow(2).sum().sqrt())
+                _log(params, f"{name}: Iteration {itn}, Relres = {relres:.2e}, {conv} rhs converged")
+            if conv == k:
+                _log(params, f"{name}: Convergence!")
+                code = -1
+                break
+    else:
+        _log(params, f"{name}: No convergence within iteration limit.")
+    return X, code
+
+
 def CG(uplo, A, B, X, params=None, M=None) -> int:
     Xs, code = cg(A, B, None, params, M, uplo)
     X.copy_(Xs.to(X.dtype))
@@ -463,6 +523,8 @@ def flexible_cg(A, B, X=None, params: KrylovIterParams | None = None, M: Precond
     tol = _clamp_tol(params.tolerance, dt)
     X = torch.zeros(n, k, dtype=dt, device=Bv.device) if X is None else X.to(dt).clone()
     Rr = Bv - op.matmul(X).to(dt)
+    if _kn.ok(Bv) and not op.distributed:
+        return _cg_native(op, Bv, X, Rr, params, M, tol, flexible=True)
     nrmb = op.long_colnorm(Bv)
     Ps, Qs, PQs = [], [], []
     code = -6

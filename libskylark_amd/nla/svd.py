@@ -284,6 +284,7 @@ def _engine_lib():
         _lib.register("sl_rsvd_plan_destroy", [vp_])
         _lib.register("sl_rsvd_set_fjlt", [vp_, u64_, u64_, u64_, f64_, vp_])
         _lib.register("sl_rsvd_set_zt", [vp_, vp_, vp_])
+        _lib.register("sl_rsvd_set_dense", [vp_, i32_, u64_, u64_, f64_, f64_, f64_, vp_])
         _lib.register("sl_rsvd_segment", [vp_, vp_, i32_, vp_])
         _lib.register("sl_rsvd_reduce_buffer", [vp_], vp_)
         _lib.register("sl_rsvd_finish", [vp_, vp_, i64_, vp_, vp_, vp_])
@@ -356,13 +357,16 @@ class _EnginePlan:
         os_ = getattr(self.comm, "_oneshot", None)
         return bool(os_) and self.calls >= 1 and os_.fits(self.WG)
 
-    def __call__(self, A, Z=None, fjlt=None):
+    def __call__(self, A, Z=None, fjlt=None, dense=None):
         L = _engine_lib()
         dev = self.dev
         st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         self._poll_status()
         if fjlt is not None:
             L.call("sl_rsvd_set_fjlt", self.h, int(fjlt[0]), int(fjlt[1]), int(fjlt[2]), float(fjlt[3]), st)
+        elif dense is not None:
+            code, seed, base, p0, p1, scale = dense
+            L.call("sl_rsvd_set_dense", self.h, int(code), int(seed), int(base), float(p0), float(p1), float(scale), st)
         else:
             Zt = Z.t().to(torch.bfloat16).contiguous()
             L.call("sl_rsvd_set_zt", self.h, ctypes.c_void_p(Zt.data_ptr()), st)
@@ -403,7 +407,7 @@ class _EnginePlan:
 
     def _poll_status(self):
         if self.status_ev is not None and self.status_ev.query():
-            self.last_status = int(self.status_host[0])
+            self.last_status = int(self.status_host[0]) & 15
             if self.last_status & (ST_NONFINITE | ST_RANK | ST_NOCONV):
                 import warnings
                 warnings.warn(f"approximate_svd (device): previous call flagged status {self.last_status} "
@@ -414,7 +418,7 @@ class _EnginePlan:
         """Synchronise with the last call and return its status bits."""
         if self.status_ev is not None:
             self.status_ev.synchronize()
-            self.last_status = int(self.status_host[0])
+            self.last_status = int(self.status_host[0]) & 15
         return self.last_status
 
 
@@ -450,7 +454,16 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     dev = A_loc.device
     fjlt = None
     Z = None
-    if params.sketch.upper() == "FJLT":
+    dense = None
+    kind = params.sketch.upper()
+    if kind in ("JLT", "CT"):
+        # dense operator: the engine realises it on the device from the
+        # sketch's stream (same f64 -> f32 -> bf16 values as realize())
+        from .. import sketch as S
+        sk = (S.JLT if kind == "JLT" else S.CT)(n, k, context=ctx)
+        p0, p1 = sk.dist.params()
+        dense = (sk.dist.code, sk.entries.seed, sk.entries.base, p0, p1, sk.scale)
+    elif kind == "FJLT":
         # FJLT_data draw layout: N Rademacher signs, then S sample rows; the
         # operator itself is realised on the device by the engine
         base_d = ctx.counter
@@ -471,7 +484,7 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
             _PLANS.pop(next(iter(_PLANS)))
         plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
         _PLANS[key] = plan
-    return plan(A_loc, Z=Z, fjlt=fjlt)
+    return plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
 
 
 def last_device_status(wait: bool = True) -> int:

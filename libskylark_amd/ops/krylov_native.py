@@ -149,3 +149,58 @@ def thin_gemm(M: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     _lib.call("sl_rows_gemm", _lib.ptr(M), M.stride(0), nr, nc, _lib.ptr(X), X.stride(0), k, _lib.ptr(Y),
               Y.stride(0), _lib.dtype_code(M.dtype), _st(M))
     return Y
+
+
+# ------------------------------------------------------------------ CG / FCG
+_lib.register("sl_cg_nstate", [], C.c_int)
+_lib.register("sl_cg_dot", [vp, i64, vp, i64, vp, i64, i64, i32, i32, i32, vp, vp, vp, vp])
+_lib.register("sl_cg_p", [vp, i64, vp, i64, i64, i32, i32, vp, f64, vp])
+_lib.register("sl_cg_xr", [vp, i64, vp, i64, vp, i64, vp, i64, i64, i32, i32, i32, vp, vp, f64, vp, vp, vp])
+
+# CG scalar-state rows (krylov_kernels.hip enum)
+C_RHO, C_RHO0, C_ALPHA, C_BETA, C_PQ, C_RR, C_NRMB = range(7)
+
+
+class CGState:
+    """Device state of a (flexible) CG run: per-column f64 scalars, the
+    reduction workspace, the last-block ticket counter and the stop flags."""
+
+    def __init__(self, k: int, device):
+        L = _lib.require()
+        self.k = k
+        self.st = torch.zeros(int(L.sl_cg_nstate()), k, dtype=torch.float64, device=device)
+        self.ws = torch.empty(2 * int(L.sl_krylov_ws_bytes(k)), dtype=torch.uint8, device=device)
+        self.counter = torch.zeros(4, dtype=torch.int32, device=device)
+        self.flags = torch.zeros(k, dtype=torch.int32, device=device)
+
+
+def _c(t):
+    return t if t.stride(1) == 1 else t.contiguous()
+
+
+def cg_dot(X: torch.Tensor, Y: torch.Tensor, mode: int, cs: CGState, Y2: torch.Tensor | None = None):
+    """Column dots finished on the device into the CG state (see sl_cg_dot)."""
+    m, k = X.shape
+    Y = _c(Y.to(X.dtype))
+    Y2 = _c(Y2.to(X.dtype)) if Y2 is not None else None
+    _lib.call("sl_cg_dot", _lib.ptr(X), X.stride(0), _lib.ptr(Y), Y.stride(0),
+              _lib.ptr(Y2) if Y2 is not None else None, Y2.stride(0) if Y2 is not None else 0, m, k,
+              _lib.dtype_code(X.dtype), int(mode), _lib.ptr(cs.st), _lib.ptr(cs.ws), _lib.ptr(cs.counter), _st(X))
+
+
+def cg_p(Z: torch.Tensor, P: torch.Tensor, cs: CGState, sb: float = 1.0):
+    """In place ``P = Z + sb * beta .* P``."""
+    m, k = P.shape
+    Z = _c(Z.to(P.dtype))
+    _lib.call("sl_cg_p", _lib.ptr(Z), Z.stride(0), _lib.ptr(P), P.stride(0), m, k, _lib.dtype_code(P.dtype),
+              _lib.ptr(cs.st), float(sb), _st(P))
+
+
+def cg_xr(X, P, R, Q, cs: CGState, idp: bool, tol: float):
+    """In place ``X += alpha P``, ``R -= alpha Q``; |R|^2, stop flags and (idp)
+    rho / beta into the state."""
+    m, k = X.shape
+    Q = _c(Q.to(X.dtype))
+    _lib.call("sl_cg_xr", _lib.ptr(X), X.stride(0), _lib.ptr(P), P.stride(0), _lib.ptr(R), R.stride(0), _lib.ptr(Q),
+              Q.stride(0), m, k, _lib.dtype_code(X.dtype), int(bool(idp)), _lib.ptr(cs.st), _lib.ptr(cs.flags),
+              float(tol), _lib.ptr(cs.ws), _lib.ptr(cs.counter), _st(X))

@@ -296,3 +296,180 @@ def test_native_c_program_is_interpreter_free(capi, tmp_path):
     np.testing.assert_allclose(vals[:12].reshape(2, 6).T, J.apply(torch.from_numpy(a)).numpy(), rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(vals[12:].reshape(2, 6).T, W.apply(torch.from_numpy(a)).numpy(), rtol=1e-12, atol=1e-12)
     assert json.loads(lines[1])["sketch_type"] == "WZT"
+
+
+C_DEVICE_PROGRAM = textwrap.dedent(r"""
+    #include <math.h>
+    #include <stdint.h>
+    #include <stdio.h>
+    #include <stdlib.h>
+    #include <string.h>
+    typedef struct sl_context_t sl_context_t;
+    typedef struct sl_sketch_transform_t sl_sketch_transform_t;
+    typedef struct sl_kernel_t sl_kernel_t;
+    int sl_create_default_context(int, sl_context_t**);
+    int sl_create_sketch_transform(sl_context_t*, char*, int, int, sl_sketch_transform_t**, ...);
+    int sl_apply_sketch_transform(sl_sketch_transform_t*, char*, void*, char*, void*, int);
+    int sl_free_sketch_transform(sl_sketch_transform_t*);
+    int sl_approximate_svd(char*, void*, char*, void*, char*, void*, char*, void*, uint16_t, char*, sl_context_t*);
+    int sl_create_kernel(char*, int, sl_kernel_t**, ...);
+    int sl_kernel_gram(int, int, sl_kernel_t*, char*, void*, char*, void*, char*, void*);
+    int sl_free_kernel(sl_kernel_t*);
+    int sl_free_context(sl_context_t*);
+    int sl_runtime_started(void);
+    int sl_wrap_raw_device_matrix(void*, int, int, int, int64_t, void**);
+    int sl_free_raw_device_matrix_wrap(void*);
+    int sl_device_malloc(int64_t, void**);
+    int sl_device_free(void*);
+    int sl_device_memcpy(void*, const void*, int64_t, int);
+    void sl_get_exception_info(char**);
+    int sl_create_context(int, void*, sl_context_t**);
+    int sl_device_comm_id_bytes(void);
+    int sl_device_comm_unique_id(void*);
+    int sl_device_comm_create(const void*, int, int, void**);
+    int sl_device_comm_free(void*);
+
+    static uint64_t st = 88172645463325252ull;
+    static double urand(void) { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return (st >> 11) * (1.0 / 9007199254740992.0) - 0.5; }
+    static int fail(int code, int rc) { char* e; sl_get_exception_info(&e); fprintf(stderr, "step %d rc %d: %s\n", code, rc, e); return code; }
+    static void* up(const void* h, int64_t bytes) { void* d; if (sl_device_malloc(bytes, &d)) return NULL; sl_device_memcpy(d, h, bytes, 0); return d; }
+    static void* dev(int64_t bytes) { void* d; return sl_device_malloc(bytes, &d) ? NULL : d; }
+    static void dump(const char* dir, const char* name, const void* d, int64_t bytes) {
+        void* h = malloc(bytes); sl_device_memcpy(h, d, bytes, 1);
+        char p[1024]; snprintf(p, sizeof p, "%s/%s.bin", dir, name);
+        FILE* f = fopen(p, "wb"); fwrite(h, 1, bytes, f); fclose(f); free(h);
+    }
+    static void* wrap(void* d, int dt, int m, int n) { void* w; sl_wrap_raw_device_matrix(d, dt, m, n, n, &w); return w; }
+    static uint16_t bf16(float f) { uint32_t u; memcpy(&u, &f, 4); u += 0x7fffu + ((u >> 16) & 1u); return (uint16_t)(u >> 16); }
+
+    int main(int argc, char** argv) {
+        const char* out = argv[1];
+        int rc;
+        sl_context_t* ctx; if (sl_create_default_context(17, &ctx)) return 1;
+        sl_sketch_transform_t *J, *F, *W;
+        if ((rc = sl_create_sketch_transform(ctx, "JLT", 300, 20, &J))) return fail(2, rc);
+        if ((rc = sl_create_sketch_transform(ctx, "FJLT", 300, 16, &F))) return fail(3, rc);
+        if ((rc = sl_create_sketch_transform(ctx, "CWT", 300, 10, &W))) return fail(4, rc);
+        /* JLT columnwise, f64: A 300 x 7 -> 20 x 7 */
+        double* a = malloc(300 * 7 * 8); for (int i = 0; i < 300 * 7; ++i) a[i] = urand();
+        void* dA = up(a, 300 * 7 * 8); void* dSA = dev(20 * 7 * 8);
+        if ((rc = sl_apply_sketch_transform(J, "DeviceMatrix", wrap(dA, 1, 300, 7), "DeviceMatrix", wrap(dSA, 1, 20, 7), 0))) return fail(5, rc);
+        dump(out, "jlt_A", dA, 300 * 7 * 8); dump(out, "jlt_SA", dSA, 20 * 7 * 8);
+        /* FJLT rowwise, f32: A 9 x 300 -> 9 x 16 */
+        float* b = malloc(9 * 300 * 4); for (int i = 0; i < 9 * 300; ++i) b[i] = (float)urand();
+        void* dB = up(b, 9 * 300 * 4); void* dSB = dev(9 * 16 * 4);
+        if ((rc = sl_apply_sketch_transform(F, "DeviceMatrix", wrap(dB, 0, 9, 300), "DeviceMatrix", wrap(dSB, 0, 9, 16), 1))) return fail(6, rc);
+        dump(out, "fjlt_A", dB, 9 * 300 * 4); dump(out, "fjlt_SA", dSB, 9 * 16 * 4);
+        /* CWT columnwise, f32: A 300 x 5 -> 10 x 5 */
+        float* c = malloc(300 * 5 * 4); for (int i = 0; i < 300 * 5; ++i) c[i] = (float)urand();
+        void* dC = up(c, 300 * 5 * 4); void* dSC = dev(10 * 5 * 4);
+        if ((rc = sl_apply_sketch_transform(W, "DeviceMatrix", wrap(dC, 0, 300, 5), "DeviceMatrix", wrap(dSC, 0, 10, 5), 0))) return fail(7, rc);
+        dump(out, "cwt_A", dC, 300 * 5 * 4); dump(out, "cwt_SA", dSC, 10 * 5 * 4);
+        /* randSVD of a bf16 4096 x 64 matrix with a decaying spectrum, rank 5, q = 2 */
+        const int m = 4096, n = 64, r = 5;
+        float* u = malloc(m * 8 * 4); float* v = malloc(n * 8 * 4);
+        for (int i = 0; i < m * 8; ++i) u[i] = (float)urand();
+        for (int i = 0; i < n * 8; ++i) v[i] = (float)urand();
+        uint16_t* ab = malloc((size_t)m * n * 2);
+        for (int i = 0; i < m; ++i) for (int j = 0; j < n; ++j) {
+            double x = 0.01 * urand();
+            for (int t = 0; t < 8; ++t) x += pow(0.5, t) * u[i * 8 + t] * v[j * 8 + t];
+            ab[(size_t)i * n + j] = bf16((float)x);
+        }
+        void* dX = up(ab, (int64_t)m * n * 2); void* dU = dev(m * r * 4); void* dS = dev(r * 4); void* dV = dev(n * r * 4);
+        void *wX = wrap(dX, 2, m, n), *wU = wrap(dU, 0, m, r), *wS = wrap(dS, 0, r, 1), *wV = wrap(dV, 0, n, r);
+        char prm[] = "{\"num_iterations\": 2, \"sketch\": \"JLT\"}";
+        if ((rc = sl_approximate_svd("DeviceMatrix", wX, "DeviceMatrix", wU, "DeviceMatrix", wS, "DeviceMatrix", wV, r, prm, ctx))) return fail(8, rc);
+        dump(out, "svd_A", dX, (int64_t)m * n * 2); dump(out, "svd_U", dU, m * r * 4); dump(out, "svd_S", dS, r * 4); dump(out, "svd_V", dV, n * r * 4);
+        /* second call replays the engine's graph: same operator counter advances */
+        if ((rc = sl_approximate_svd("DeviceMatrix", wX, "DeviceMatrix", wU, "DeviceMatrix", wS, "DeviceMatrix", wV, r, prm, ctx))) return fail(9, rc);
+        dump(out, "svd_S2", dS, r * 4);
+        /* Gaussian Gram: X 50 points as rows (f64, 50 x 8), Y 30 points as columns (8 x 30) */
+        double* x = malloc(50 * 8 * 8); double* y = malloc(8 * 30 * 8);
+        for (int i = 0; i < 400; ++i) x[i] = urand();
+        for (int i = 0; i < 240; ++i) y[i] = urand();
+        void* dXk = up(x, 50 * 8 * 8); void* dYk = up(y, 8 * 30 * 8); void* dK = dev(50 * 30 * 8); void* dK2 = dev(50 * 30 * 8);
+        sl_kernel_t *G, *Lk;
+        if ((rc = sl_create_kernel("gaussian", 8, &G, 0.7))) return fail(10, rc);
+        if ((rc = sl_create_kernel("laplacian", 8, &Lk, 1.3))) return fail(11, rc);
+        if ((rc = sl_kernel_gram(2, 1, G, "DeviceMatrix", wrap(dXk, 1, 50, 8), "DeviceMatrix", wrap(dYk, 1, 8, 30), "DeviceMatrix", wrap(dK, 1, 50, 30)))) return fail(12, rc);
+        if ((rc = sl_kernel_gram(2, 1, Lk, "DeviceMatrix", wrap(dXk, 1, 50, 8), "DeviceMatrix", wrap(dYk, 1, 8, 30), "DeviceMatrix", wrap(dK2, 1, 50, 30)))) return fail(13, rc);
+        dump(out, "k_X", dXk, 400 * 8); dump(out, "k_Y", dYk, 240 * 8); dump(out, "k_G", dK, 1500 * 8); dump(out, "k_L", dK2, 1500 * 8);
+        /* the distributed call over a (1-rank) RCCL device communicator equals the local call */
+        char id[512]; int nb = sl_device_comm_id_bytes(); if (nb <= 0 || nb > 512) return fail(14, nb);
+        if ((rc = sl_device_comm_unique_id(id))) return fail(15, rc);
+        void* comm; if ((rc = sl_device_comm_create(id, 1, 0, &comm))) return fail(16, rc);
+        sl_context_t *c2, *c3; sl_create_context(5, comm, &c2); sl_create_default_context(5, &c3);
+        char prm2[] = "{\"num_iterations\": 1, \"sketch\": \"FJLT\"}";
+        if ((rc = sl_approximate_svd("DeviceMatrix", wX, "DeviceMatrix", wU, "DeviceMatrix", wS, "DeviceMatrix", wV, r, prm2, c2))) return fail(17, rc);
+        dump(out, "svd_S_comm", dS, r * 4);
+        if ((rc = sl_approximate_svd("DeviceMatrix", wX, "DeviceMatrix", wU, "DeviceMatrix", wS, "DeviceMatrix", wV, r, prm2, c3))) return fail(18, rc);
+        dump(out, "svd_S_local", dS, r * 4);
+        sl_device_comm_free(comm); sl_free_context(c2); sl_free_context(c3);
+        printf("%d\n", sl_runtime_started());
+        sl_free_kernel(G); sl_free_kernel(Lk);
+        sl_free_sketch_transform(J); sl_free_sketch_transform(F); sl_free_sketch_transform(W); sl_free_context(ctx);
+        return 0;
+    }
+""")
+
+
+@pytest.mark.gpu
+def test_device_c_program_is_interpreter_free(capi, tmp_path):
+    """A C program runs device sketches (JLT / FJLT / CWT), the randSVD engine
+    and a kernel Gram on GPU buffers through the C ABI without ever starting
+    the interpreter, and matches the Python runtime's results on the same
+    contexts (reference capi/csketch.cpp:614-680,
+    capi/cnla.cpp:15-84, capi/ckernel.cpp:34-128)."""
+    import sysconfig
+    src = tmp_path / "dev.c"
+    src.write_text(C_DEVICE_PROGRAM)
+    exe = tmp_path / "dev"
+    libdir = os.path.dirname(B.CAPI_LIB)
+    r = subprocess.run(["gcc", str(src), "-o", str(exe), f"-L{libdir}", "-lskylark_capi", f"-Wl,-rpath,{libdir}",
+                        f"-Wl,-rpath,{sysconfig.get_config_var('LIBDIR')}", "-lm"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe), str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().split("\n")[-1] == "0"      # the runtime never started
+
+    def ld(name, dt, shape):
+        return torch.from_numpy(np.fromfile(tmp_path / f"{name}.bin", dtype=dt).reshape(shape))
+
+    dev = torch.device("cuda")
+    ctx = sk.Context(17)
+    J = sk.sketch.JLT(300, 20, context=ctx)
+    F = sk.sketch.FJLT(300, 16, context=ctx)
+    W = sk.sketch.CWT(300, 10, context=ctx)
+    A = ld("jlt_A", np.float64, (300, 7))
+    torch.testing.assert_close(ld("jlt_SA", np.float64, (20, 7)), J.apply(A, dim=0), rtol=1e-10, atol=1e-10)
+    B_ = ld("fjlt_A", np.float32, (9, 300))
+    ref = F.apply(B_.double(), dim=1).float()
+    torch.testing.assert_close(ld("fjlt_SA", np.float32, (9, 16)), ref, rtol=1e-4, atol=1e-4)
+    Cm = ld("cwt_A", np.float32, (300, 5))
+    torch.testing.assert_close(ld("cwt_SA", np.float32, (10, 5)), W.apply(Cm.double(), dim=0).float(),
+                               rtol=1e-5, atol=1e-5)
+    # randSVD: same engine, same sketch stream -> same factors
+    Ab = ld("svd_A", np.int16, (4096, 64)).view(torch.bfloat16).to(dev)
+    p = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="JLT")
+    U, s, V = sk.nla.approximate_svd(Ab, 5, ctx, p)
+    sc = ld("svd_S", np.float32, (5,))
+    torch.testing.assert_close(sc, s.cpu(), rtol=1e-5, atol=1e-5)
+    Uc = ld("svd_U", np.float32, (4096, 5)).double()
+    cos = torch.linalg.svdvals(Uc.t() @ U.cpu().double())
+    assert float(cos.min()) > 0.9999, cos
+    s_true = torch.linalg.svdvals(Ab.double().cpu())[:5]
+    assert float(((sc.double() - s_true).abs() / s_true).max()) < 1e-2
+    U2, s2, _ = sk.nla.approximate_svd(Ab, 5, ctx, p)
+    torch.testing.assert_close(ld("svd_S2", np.float32, (5,)), s2.cpu(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ld("svd_S_comm", np.float32, (5,)), ld("svd_S_local", np.float32, (5,)),
+                               rtol=1e-6, atol=1e-6)
+    # kernel Grams (points: X rows, Y columns)
+    X = ld("k_X", np.float64, (50, 8))
+    Y = ld("k_Y", np.float64, (8, 30))
+    G = sk.ml.kernel("gaussian", 8, 0.7)
+    Lk = sk.ml.kernel("laplacian", 8, 1.3)
+    torch.testing.assert_close(ld("k_G", np.float64, (50, 30)), G.gram(X, dirX="rows", dirY="columns", Y=Y),
+                               rtol=1e-10, atol=1e-12)
+    torch.testing.assert_close(ld("k_L", np.float64, (50, 30)), Lk.gram(X, dirX="rows", dirY="columns", Y=Y),
+                               rtol=1e-10, atol=1e-12)

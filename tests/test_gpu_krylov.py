@@ -107,3 +107,37 @@ def test_csr_spmm_and_sparse_operator(dev, m, n, density, k, vdt):
     op = SparseOp(Acsr)
     got_t = op.rmatmul(Yv.to(dev)).double().cpu()
     assert float((got_t - Ad.t() @ Yv).norm() / (Ad.t() @ Yv).norm()) < tol
+
+
+def _spd(n, k, dt, dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    Q, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    A = (Q * torch.logspace(0, 3, n, dtype=torch.float64)) @ Q.t()
+    B = torch.randn(n, k, generator=g, dtype=torch.float64)
+    return A.to(dev, dt), B.to(dev, dt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,k,precond,flexible", [(torch.float64, 3, False, False), (torch.float64, 1, True, False),
+                                                   (torch.float32, 40, False, False), (torch.float64, 2, True, True),
+                                                   (torch.float64, 5, False, True)])
+def test_native_cg_matches_torch_cg(dev, dt, k, precond, flexible):
+    """Device-scalar (flexible) CG (sl_cg_*: last-block reductions, no host
+    sync but the stop flags) against the torch-op iteration on the same SPD
+    system (reference algorithms/Krylov/CG.hpp:24-163, FlexibleCG.hpp)."""
+    n = 600
+    A, B = _spd(n, k, dt, dev, 7 + k)
+    M = K.MatPrecond(torch.diag(1.0 / torch.diagonal(A))) if precond else None
+    tol = 1e-10 if dt == torch.float64 else 1e-4
+    p = K.KrylovIterParams(tolerance=tol, iter_lim=3000, check_every=5)
+    f = K.flexible_cg if flexible else K.cg
+    Xn, cn = f(A, B, params=p, M=M)
+    kn.ENABLED = False
+    try:
+        Xt, ct = f(A, B, params=p, M=M)
+    finally:
+        kn.ENABLED = True
+    assert cn == -1 and ct == -1
+    rn = ((A.double() @ Xn.double() - B.double()).norm(dim=0) / B.double().norm(dim=0)).max()
+    assert float(rn) < (1e-9 if dt == torch.float64 else 5e-3)
+    assert float((Xn.double() - Xt.double()).norm() / Xt.double().norm()) < (1e-7 if dt == torch.float64 else 1e-2)

@@ -1,0 +1,134 @@
+"""Device small linear algebra of the randSVD engine (rsvd_core.hip) against
+fp64 numpy references: the CholeskyQR inverse between passes
+(sl_rsvd_inter_la), the next pass operand (sl_rsvd_make_zt), the fp64 core
+(sl_rsvd_final_la: Cholesky of Y^T Y, C = Rt^-T H Rt^-1, Jacobi, factors),
+V = W N (sl_rsvd_make_v), pivot dropping and the Jacobi warm start."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+
+
+@pytest.fixture(scope="module")
+def L():
+    from libskylark_amd.ops import _lib
+    _lib.require()
+    _lib.register("sl_rsvd_gram_workspace", [i32], C.c_int64)
+    _lib.register("sl_rsvd_inter_la", [vp, i32, i32, i32, vp, vp, vp, vp])
+    _lib.register("sl_rsvd_make_zt", [vp, i32, i32, i32, vp, vp, vp])
+    _lib.register("sl_rsvd_final_la", [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp])
+    _lib.register("sl_rsvd_make_v", [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp])
+    return _lib
+
+
+def _p(t):
+    return vp(t.data_ptr()) if t is not None else None
+
+
+def _graded(n, k, lo, hi, seed):
+    g = np.random.RandomState(seed)
+    Q1, _ = np.linalg.qr(g.randn(n, k))
+    Q2, _ = np.linalg.qr(g.randn(k, k))
+    return (Q1 * np.logspace(hi, lo, k)) @ Q2.T
+
+
+def _ws(L, k, dev):
+    return torch.zeros(int(L.require().sl_rsvd_gram_workspace(k)), dtype=torch.uint8, device=dev)
+
+
+@pytest.mark.parametrize("n,k", [(1000, 40), (64, 17), (1024, 48), (16, 1)])
+def test_inter_la_is_cholesky_inverse(L, n, k):
+    dev = torch.device("cuda")
+    W = _graded(n, k, 0, 5, n + k)
+    Wd = torch.from_numpy(W).to(dev)
+    ws = _ws(L, k, dev)
+    Rinv = torch.empty(k, k, dtype=torch.float64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = vp(torch.cuda.current_stream().cuda_stream)
+    for _ in range(2):   # the ticket counter is reset for the next launch
+        L.call("sl_rsvd_inter_la", _p(Wd), n, k, k, _p(ws), _p(Rinv), _p(st), s)
+    torch.cuda.synchronize()
+    assert int(st[0]) == 0
+    Ri = Rinv.cpu().numpy()
+    assert np.abs(np.tril(Ri, -1)).max() == 0.0
+    H = W.T @ W
+    np.testing.assert_allclose(Ri.T @ H @ Ri, np.eye(k), atol=1e-9)
+    R = np.linalg.cholesky(H).T
+    np.testing.assert_allclose(Ri, np.linalg.inv(R), rtol=1e-8, atol=1e-8 * np.abs(Ri).max())
+    # next pass operand: Z^T = (W R^-1)^T in bf16
+    Zt = torch.empty(k, n, dtype=torch.bfloat16, device=dev)
+    L.call("sl_rsvd_make_zt", _p(Wd), n, k, k, _p(Rinv), _p(Zt), s)
+    Zr = (W @ Ri).T
+    np.testing.assert_allclose(Zt.double().cpu().numpy(), Zr, atol=8e-3 * np.abs(Zr).max())
+
+
+def test_inter_la_drops_dependent_direction(L):
+    dev = torch.device("cuda")
+    n, k = 200, 12
+    W = _graded(n, k, 0, 2, 3)
+    W[:, 5] = W[:, 2] * 2.0          # exactly dependent column
+    Wd = torch.from_numpy(W).to(dev)
+    ws = _ws(L, k, dev)
+    Rinv = torch.empty(k, k, dtype=torch.float64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    L.call("sl_rsvd_inter_la", _p(Wd), n, k, k, _p(ws), _p(Rinv), _p(st), vp(torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert int(st[0]) & 1
+    Ri = Rinv.cpu().numpy()
+    assert np.abs(Ri[:, 5]).max() == 0.0
+    Q = W @ Ri
+    keep = [j for j in range(k) if j != 5]
+    np.testing.assert_allclose(Q[:, keep].T @ Q[:, keep], np.eye(k - 1), atol=1e-8)
+
+
+@pytest.mark.parametrize("n,k,r", [(1000, 40, 20), (96, 17, 5), (512, 48, 48)])
+def test_final_la_matches_fp64_core(L, n, k, r):
+    dev = torch.device("cuda")
+    g = np.random.RandomState(k)
+    W = _graded(n, k, -1, 4, 7 * k)
+    Yg = g.randn(4 * k, k) @ np.diag(np.logspace(0, 2, k))
+    Gy = Yg.T @ Yg
+    Wd, Gyd = torch.from_numpy(W).to(dev), torch.from_numpy(Gy).to(dev)
+    ws = _ws(L, k, dev)
+    M = torch.empty(k, r, device=dev)
+    N = torch.empty(k, r, dtype=torch.float64, device=dev)
+    s64 = torch.empty(r, dtype=torch.float64, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    kp = k + (k & 1)
+    V0 = torch.empty(kp, kp, dtype=torch.float64, device=dev)
+    v0v = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = vp(torch.cuda.current_stream().cuda_stream)
+    # reference: C = Rt^-T H Rt^-1, eigenpairs descending
+    Rt = np.linalg.cholesky(Gy).T
+    Rti = np.linalg.inv(Rt)
+    Cm = Rti.T @ (W.T @ W) @ Rti
+    ev, Ub = np.linalg.eigh(0.5 * (Cm + Cm.T))
+    ev, Ub = ev[::-1][:r], Ub[:, ::-1][:, :r]
+    outs = []
+    for warm in (0, 1, 1):
+        L.call("sl_rsvd_final_la", _p(Wd), n, k, k, _p(Gyd), r, _p(ws), _p(M), _p(N), _p(s64), _p(st), 0,
+               _p(V0) if warm else None, _p(v0v) if warm else None, s)
+        torch.cuda.synchronize()
+        assert int(st[0]) & ~1 == 0, int(st[0])
+        sv = s64.cpu().numpy()
+        np.testing.assert_allclose(sv, np.sqrt(ev), rtol=1e-9)
+        # M = Rt^-1 Ub_r up to column signs
+        Mr = Rti @ Ub
+        Mn = M.double().cpu().numpy()
+        sg = np.sign(np.sum(Mn * Mr, axis=0))
+        np.testing.assert_allclose(Mn * sg, Mr, atol=2e-6 * np.abs(Mr).max())
+        np.testing.assert_allclose(N.cpu().numpy() * sg, Mr / np.sqrt(ev), atol=2e-6 * np.abs(Mr / np.sqrt(ev)).max())
+        outs.append(sv)
+    # V = W N
+    Vt = torch.empty(n, r, device=dev)
+    s32 = torch.empty(r, device=dev)
+    L.call("sl_rsvd_make_v", _p(Wd), n, k, k, _p(N), r, _p(Vt), _p(s64), _p(s32), s)
+    torch.cuda.synchronize()
+    Vr = W @ N.cpu().numpy()
+    np.testing.assert_allclose(Vt.double().cpu().numpy(), Vr, atol=1e-6 * np.abs(Vr).max())
+    np.testing.assert_allclose(s32.cpu().numpy(), outs[-1].astype(np.float32))
