@@ -146,7 +146,9 @@ class OneShotAllReduce:
 
     def _poll(self):
         ev = getattr(self, "_err_ev", None)
-        if ev is not None and ev.query() and int(self._err_host[0]):
+        if ev is None or torch.cuda.is_current_stream_capturing():
+            return   # event queries are not permitted while a stream captures
+        if ev.query() and int(self._err_host[0]):
             raise OneShotError("one-shot all-reduce: a peer did not arrive within the timeout "
                                "(the operand of that call was poisoned with NaN)")
 

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pt_full.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=5 -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pt_full.log 2>&1
 rc=$?; tail -4 $OUT/pt_full.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1; rc=$?; tail -1 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --steps 30 --warmup 5 > $OUT/bench_full.log 2>&1; rc=$?; tail -1 $OUT/bench_full.log; [ $rc -eq 0 ] || exit $rc

@@ -83,12 +83,11 @@ def _late_worker(rank, world):
     torch.cuda.synchronize()
     out = {"nan": bool(torch.isnan(x).all()), "sum_ok": bool(torch.all(x == 3.0))}
     try:
-        comm.check_collectives()
+        os_.check()
         out["raised"] = False
     except oneshot.OneShotError:
         out["raised"] = True
-    comm.barrier()
-    comm.close()
+    os_.close(comm)
     return out
 
 
