@@ -1,6 +1,7 @@
 """FJLT sketch with many samples on a tall f32 matrix (Blendenpik's t = 4n
-sketch): the fused pre-pass + rocFFT rfft + sampled post-gather against the
-torch DCT-II + index_select composition.  Prints one JSON line per variant."""
+sketch): the four-step sampled DCT (fjlt_fourstep.hip, the default), the
+fused pre-pass + rocFFT rfft + sampled post-gather, and the torch DCT-II +
+index_select composition.  Prints one JSON line per variant."""
 from __future__ import annotations
 
 import json
@@ -39,11 +40,20 @@ def main():
         X = A * d.to(dev, torch.float32)[:, None]
         return fut.dct2(X, 0).index_select(0, smp.to(dev)) * scale
 
-    def new():
-        return fut.fjlt_sampled(A, 0, d, smp, scale)
+    def rfft():
+        ok = fut.fourstep_ok
+        fut.fourstep_ok = lambda *a: False
+        try:
+            return fut.fjlt_sampled(A, 0, d, smp, scale)
+        finally:
+            fut.fourstep_ok = ok
 
-    err = float((new().double() - old().double()).norm() / old().double().norm())
-    for name, fn in (("torch_dct_gather", old), ("fused_rfft_sampled", new)):
+    def new():
+        return fut.fjlt_fourstep(A, d, smp, scale)
+
+    ref = old().double()
+    for name, fn in (("torch_dct_gather", old), ("fused_rfft_sampled", rfft), ("fourstep_sampled", new)):
+        err = float((fn().double() - ref).norm() / ref.norm())
         t = timeit(fn)
         print(json.dumps({"bench": "fjlt_sampled", "variant": name, "m": m, "n": n, "S": S, "ms": round(t * 1e3, 3),
                           "GBps_of_A": round(nbytes / t / 1e9, 1), "rel_diff_vs_torch": err}), flush=True)

@@ -1,0 +1,402 @@
+// Sampled DCT-II along the long dimension of a tall matrix -- the FJLT
+// P F D A of reference sketch/FJLT_Elemental.hpp:144-171 (F the orthonormal
+// DCT-II of utility/fft/fftw_futs.h:50-108, P the S sampled rows) -- as a
+// four-step FFT that never forms the full spectrum.
+//
+// x = D A (N x m, row-major, the m columns are the batch).  Makhoul:
+//   v[n] = x[2n] (n < N/2),  v[N-1-n] = x[2n+1],   X[k] = Re(W_4N^k V[k]),
+// real-to-complex packing z[j] = v[2j] + i v[2j+1] (M = N/2 points):
+//   V[k] = E + W_N^k O,  E = (Z[k] + conj Z[M-k]) / 2,  O = -i (Z[k] - conj Z[M-k]) / 2.
+// Four-step split M = N1 N2, j = j1 + N1 j2, k = k2 + N2 k1:
+//   stage 1  Y[k2][j1] = W_M^{j1 k2} FFT_N2(z[j1 + N1 j2])[k2]      (all j1)
+//   stage 2  Z[k]      = sum_j1 W_N1^{j1 k1} Y[k2][j1]              (needed k only)
+//   stage 3  out[s]    = scale c_k Re(W_4N^k (E + W_N^k O)),  k = sample s
+//
+// Stage 1: one workgroup per (j1, 32-column chunk).  The 2 N2 rows of x it
+// needs are read as 128-B row pieces (D applied on load) into an LDS tile of
+// N2 x 32 complex values; the length-N2 FFT runs in place in that tile as
+// mixed-radix Stockham passes (radix 8/4/5/3/7/2: every thread reads its
+// butterflies' inputs, barrier, writes the outputs, barrier) with a W_N2
+// table in LDS; the W_M twiddle is applied on the way out.  Y is laid out
+// [k2][j1][column], so stage 2 streams one contiguous N1 x m slab per k2.
+// Stage 2: one workgroup per (k2, 64-column chunk); lane = column, the four
+// waves split j1 and reduce through LDS; the frequencies with this k2 (a
+// CSR group built on the host) accumulate in registers, twiddles from a
+// W_N1 table in LDS indexed by (j1 k1) mod N1 (exact, no drift).
+// HBM traffic: A once, Y written and read once (M x m complex = A's f32
+// bytes each way); the dense m x N copy and the N/2-point spectrum of the
+// rocFFT pipeline (ops/fut.py) are gone.
+#include "sl_common.hpp"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int WC = 32;          // columns per stage-1 workgroup
+constexpr int N2_MAX = 512;     // LDS tile N2 x WC float2 = 128 KB
+constexpr int GMAX = 16;        // frequencies per stage-2 register pass
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// multiply by -i
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
+
+// forward DFT of R points in registers (W = e^{-2 pi i / R})
+template <int R>
+__device__ __forceinline__ void dft(float2* v);
+
+template <>
+__device__ __forceinline__ void dft<2>(float2* v) {
+  const float2 a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+template <>
+__device__ __forceinline__ void dft<4>(float2* v) {
+  const float2 s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+  const float2 s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+  v[0] = cadd(s02, s13);
+  v[2] = csub(s02, s13);
+  v[1] = cadd(d02, d13);
+  v[3] = csub(d02, d13);
+}
+template <>
+__device__ __forceinline__ void dft<8>(float2* v) {
+  // two radix-4 on even / odd, twiddles W8^k, combine
+  float2 e[4] = {v[0], v[2], v[4], v[6]};
+  float2 o[4] = {v[1], v[3], v[5], v[7]};
+  dft<4>(e);
+  dft<4>(o);
+  constexpr float h = 0.70710678118654752f;
+  o[1] = make_float2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));     // * (1 - i)/sqrt2
+  o[2] = mul_mi(o[2]);                                                  // * -i
+  o[3] = make_float2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));    // * (-1 - i)/sqrt2
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = cadd(e[k], o[k]);
+    v[k + 4] = csub(e[k], o[k]);
+  }
+}
+template <>
+__device__ __forceinline__ void dft<3>(float2* v) {
+  constexpr float c1 = -0.5f, s1 = 0.86602540378443865f;
+  const float2 a = v[0], b = v[1], c = v[2];
+  const float2 t = cadd(b, c), d = csub(b, c);
+  v[0] = cadd(a, t);
+  const float2 m = make_float2(a.x + c1 * t.x, a.y + c1 * t.y);
+  // -i s1 d
+  const float2 r = make_float2(s1 * d.y, -s1 * d.x);
+  v[1] = cadd(m, r);
+  v[2] = csub(m, r);
+}
+template <>
+__device__ __forceinline__ void dft<5>(float2* v) {
+  constexpr float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;
+  constexpr float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;
+  const float2 a = v[0];
+  const float2 t1 = cadd(v[1], v[4]), d1 = csub(v[1], v[4]);
+  const float2 t2 = cadd(v[2], v[3]), d2 = csub(v[2], v[3]);
+  v[0] = cadd(a, cadd(t1, t2));
+  const float2 m1 = make_float2(a.x + c1 * t1.x + c2 * t2.x, a.y + c1 * t1.y + c2 * t2.y);
+  const float2 m2 = make_float2(a.x + c2 * t1.x + c1 * t2.x, a.y + c2 * t1.y + c1 * t2.y);
+  // -i (s1 d1 + s2 d2), -i (s2 d1 - s1 d2)
+  const float2 n1 = make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y);
+  const float2 n2 = make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y);
+  v[1] = cadd(m1, mul_mi(n1));
+  v[4] = csub(m1, mul_mi(n1));
+  v[2] = cadd(m2, mul_mi(n2));
+  v[3] = csub(m2, mul_mi(n2));
+}
+template <>
+__device__ __forceinline__ void dft<7>(float2* v) {
+  // direct (7 is rare): v_k = sum_n v_n W7^{nk}
+  float2 in[7];
+#pragma unroll
+  for (int n = 0; n < 7; ++n) in[n] = v[n];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    float2 acc = in[0];
+#pragma unroll
+    for (int n = 1; n < 7; ++n) {
+      float sn, cs;
+      sincospif(-2.0f * (float)((n * k) % 7) / 7.0f, &sn, &cs);
+      acc = cadd(acc, cmul(in[n], make_float2(cs, sn)));
+    }
+    v[k] = acc;
+  }
+}
+
+// One Stockham pass of radix R over the N2 x WC tile (in place: all reads,
+// barrier, all writes, barrier).  Ns = product of the earlier radices.
+template <int R>
+__device__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict__ tw, int N2, int Ns) {
+  constexpr int QMAX = (N2_MAX / R * WC + NT - 1) / NT;
+  const int tid = threadIdx.x;
+  const int nb = N2 / R * WC;
+  const int stride = N2 / R;
+  const int tstep = N2 / (Ns * R);
+  float2 v[QMAX][R];
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int b = tid + NT * q;
+    if (b < nb) {
+      const int col = b & (WC - 1), j = b / WC, k = j % Ns;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float2 x = buf[(j + r * stride) * WC + col];
+        v[q][r] = r == 0 ? x : cmul(x, tw[r * k * tstep]);
+      }
+      dft<R>(v[q]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int b = tid + NT * q;
+    if (b < nb) {
+      const int col = b & (WC - 1), j = b / WC, k = j % Ns;
+      const int d0 = (j / Ns) * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) buf[(d0 + r * Ns) * WC + col] = v[q][r];
+    }
+  }
+  __syncthreads();
+}
+
+template <typename T>
+__device__ __forceinline__ float ld_f(const T* p) {
+  if constexpr (sizeof(T) == 2) return bf16_to_f(*(const bf16_t*)p);
+  else return (float)*p;
+}
+
+// radix plan: up to 12 radices, 4 bits each, packed low first
+template <typename T>
+__global__ void __launch_bounds__(NT)
+k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double* __restrict__ d, int N1, int N2,
+            uint64_t rplan, int npass, float2* __restrict__ Y) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  float2* buf = lds;                 // N2 x WC
+  float2* tw = lds + N2 * WC;        // N2: W_N2^t
+  const int tid = threadIdx.x;
+  const int j1 = blockIdx.x;
+  const int c0 = blockIdx.y * WC;
+  const int64_t M = N >> 1;
+  for (int t = tid; t < N2; t += NT) {
+    float s, c;
+    sincospif(-2.0f * (float)t / (float)N2, &s, &c);
+    tw[t] = make_float2(c, s);
+  }
+  // ---- load z[j1 + N1 j2] (D applied), 32 columns, rows in flight in batches of 8
+  const int col = tid & (WC - 1), rg = tid / WC;   // 8 row groups
+  const bool cok = c0 + col < m;
+  for (int jb = rg; jb < N2; jb += 8 * (NT / WC)) {
+    float re[8], im[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j2 = jb + u * (NT / WC);
+      re[u] = im[u] = 0.f;
+      if (j2 < N2 && cok) {
+        const int64_t j = (int64_t)j1 + (int64_t)N1 * j2;
+        const int64_t n0 = 2 * j, n1 = 2 * j + 1;
+        const int64_t x0 = n0 < M ? 2 * n0 : 2 * N - 2 * n0 - 1;
+        const int64_t x1 = n1 < M ? 2 * n1 : 2 * N - 2 * n1 - 1;
+        re[u] = ld_f(A + x0 * lda + c0 + col) * (float)d[x0];
+        im[u] = ld_f(A + x1 * lda + c0 + col) * (float)d[x1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j2 = jb + u * (NT / WC);
+      if (j2 < N2) buf[j2 * WC + col] = make_float2(re[u], im[u]);
+    }
+  }
+  __syncthreads();
+  // ---- length-N2 FFT along the tile's rows
+  int Ns = 1;
+  for (int p = 0; p < npass; ++p) {
+    const int R = (int)((rplan >> (4 * p)) & 15);
+    switch (R) {
+      case 8: stockham_pass<8>(buf, tw, N2, Ns); break;
+      case 4: stockham_pass<4>(buf, tw, N2, Ns); break;
+      case 5: stockham_pass<5>(buf, tw, N2, Ns); break;
+      case 3: stockham_pass<3>(buf, tw, N2, Ns); break;
+      case 7: stockham_pass<7>(buf, tw, N2, Ns); break;
+      default: stockham_pass<2>(buf, tw, N2, Ns); break;
+    }
+    Ns *= R;
+  }
+  // ---- W_M^{j1 k2} and out: Y[k2][j1][c]
+  if (!cok) return;
+  for (int k2 = rg; k2 < N2; k2 += NT / WC) {
+    const int64_t r = ((int64_t)j1 * k2) % M;
+    float s, c;
+    sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
+    Y[((int64_t)k2 * N1 + j1) * m + c0 + col] = cmul(buf[k2 * WC + col], make_float2(c, s));
+  }
+}
+
+// Stage 2: Zs[slot][c] = sum_j1 W_N1^{j1 k1} Y[k2][j1][c] for the (k1, slot)
+// pairs of group k2 (gptr CSR over k2, gk1 / gslot entries).
+__global__ void __launch_bounds__(NT)
+k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __restrict__ gptr,
+            const int* __restrict__ gk1, const int* __restrict__ gslot, float2* __restrict__ Zs) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  float2* tw = lds;                       // N1: W_N1^t
+  float2* red = lds + N1;                 // 4 waves x GMAX x 64
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int k2 = blockIdx.x;
+  const int c = blockIdx.y * 64 + lane;
+  const int g0 = gptr[k2], g1 = gptr[k2 + 1];
+  if (g0 == g1) return;
+  for (int t = tid; t < N1; t += NT) {
+    float s, cc;
+    sincospif(-2.0f * (float)((double)t / (double)N1), &s, &cc);
+    tw[t] = make_float2(cc, s);
+  }
+  __syncthreads();
+  const float2* Yk = Y + (int64_t)k2 * N1 * m;
+  const bool cok = c < m;
+  for (int gb = g0; gb < g1; gb += GMAX) {
+    const int ng = min(GMAX, g1 - gb);
+    int k1[GMAX], idx[GMAX], st[GMAX];
+    float2 acc[GMAX];
+#pragma unroll
+    for (int g = 0; g < GMAX; ++g) {
+      k1[g] = g < ng ? gk1[gb + g] : 0;
+      idx[g] = (int)(((int64_t)w * k1[g]) % N1);   // (j1 k1) mod N1 at j1 = w
+      st[g] = (int)((4 * (int64_t)k1[g]) % N1);
+      acc[g] = make_float2(0.f, 0.f);
+    }
+    for (int j1 = w; j1 < N1; j1 += 4) {
+      const float2 y = cok ? Yk[(int64_t)j1 * m + c] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int g = 0; g < GMAX; ++g) {
+        if (g < ng) {
+          const float2 t = tw[idx[g]];
+          acc[g].x = fmaf(t.x, y.x, fmaf(-t.y, y.y, acc[g].x));
+          acc[g].y = fmaf(t.x, y.y, fmaf(t.y, y.x, acc[g].y));
+          idx[g] += st[g];
+          if (idx[g] >= N1) idx[g] -= N1;
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < GMAX; ++g) red[(w * GMAX + g) * 64 + lane] = acc[g];
+    __syncthreads();
+    for (int g = w; g < ng; g += 4) {
+      const float2 s = cadd(cadd(red[(0 * GMAX + g) * 64 + lane], red[(1 * GMAX + g) * 64 + lane]),
+                            cadd(red[(2 * GMAX + g) * 64 + lane], red[(3 * GMAX + g) * 64 + lane]));
+      if (cok) Zs[(int64_t)gslot[gb + g] * m + c] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// Stage 3: out[s][c] (row stride ldo) = scale c_k Re(W_4N^k (E + W_N^k O)).
+__global__ void __launch_bounds__(NT)
+k_fs_post(const float2* __restrict__ Zs, int m, int64_t N, const int64_t* __restrict__ samples, int S,
+          const int* __restrict__ sa, const int* __restrict__ sb, double scale, float* __restrict__ out,
+          int64_t ldo) {
+  const int64_t t = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (t >= (int64_t)S * m) return;
+  const int s = (int)(t / m), c = (int)(t - (int64_t)s * m);
+  const int64_t k = samples[s];
+  const float2 za = Zs[(int64_t)sa[s] * m + c], zb = Zs[(int64_t)sb[s] * m + c];
+  // E = (Za + conj Zb) / 2, O = -i (Za - conj Zb) / 2
+  const double er = 0.5 * ((double)za.x + zb.x), ei = 0.5 * ((double)za.y - zb.y);
+  const double dr = 0.5 * ((double)za.x - zb.x), di = 0.5 * ((double)za.y + zb.y);
+  const double orr = di, oi = -dr;
+  double sn, cs;
+  sincospi(-2.0 * (double)k / (double)N, &sn, &cs);          // W_N^k
+  const double vr = er + cs * orr - sn * oi, vi = ei + cs * oi + sn * orr;
+  sincospi(-0.5 * (double)k / (double)N, &sn, &cs);          // W_4N^k
+  const double x = cs * vr - sn * vi;
+  const double ck = k == 0 ? sqrt(1.0 / (double)N) : sqrt(2.0 / (double)N);
+  out[(int64_t)s * ldo + c] = (float)(scale * ck * x);
+}
+
+size_t stage1_lds(int N2) { return (size_t)(N2 * WC + N2) * sizeof(float2); }
+size_t stage2_lds(int N1) { return (size_t)(N1 + 4 * GMAX * 64) * sizeof(float2); }
+
+}  // namespace
+
+SL_API int64_t sl_fs_limits(int which) {
+  return which == 0 ? N2_MAX : which == 1 ? WC : GMAX;
+}
+
+// Stage 1.  A: N x m (lda, f32 or bf16), d: N f64 signs, radix plan (4-bit
+// radices, low first, product N2), Y: N2 x N1 x m complex f32.
+SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m, const double* d, int N1, int N2,
+                        uint64_t rplan, int npass, void* Y, void* stream) {
+  if (N % 2 || (int64_t)N1 * N2 != N / 2 || N2 < 2 || N2 > N2_MAX || m < 1 || npass < 1 || npass > 16) {
+    sl_set_last_error("fs_stage1: needs N even, N1 N2 = N/2, 2 <= N2 <= 512");
+    return SL_ERR_INVALID;
+  }
+  int64_t prod = 1;
+  for (int p = 0; p < npass; ++p) {
+    const int R = (int)((rplan >> (4 * p)) & 15);
+    if (R != 2 && R != 3 && R != 4 && R != 5 && R != 7 && R != 8) {
+      sl_set_last_error("fs_stage1: radices must be 2, 3, 4, 5, 7, 8");
+      return SL_ERR_INVALID;
+    }
+    prod *= R;
+  }
+  if (prod != N2) { sl_set_last_error("fs_stage1: radix plan does not multiply to N2"); return SL_ERR_INVALID; }
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = stage1_lds(N2);
+  dim3 grid((unsigned)N1, (unsigned)((m + WC - 1) / WC));
+  if (dtype == SL_F32) {
+    static bool attr = false;
+    if (!attr) {
+      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_fs_stage1<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)stage1_lds(N2_MAX)));
+      attr = true;
+    }
+    k_fs_stage1<float><<<grid, NT, lds, s>>>((const float*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
+  } else if (dtype == SL_BF16) {
+    static bool attr = false;
+    if (!attr) {
+      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_fs_stage1<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)stage1_lds(N2_MAX)));
+      attr = true;
+    }
+    k_fs_stage1<bf16_t><<<grid, NT, lds, s>>>((const bf16_t*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
+  } else {
+    sl_set_last_error("fs_stage1: f32 / bf16 input");
+    return SL_ERR_UNSUPPORTED;
+  }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// Stage 2.  gptr: N2 + 1 offsets into gk1 / gslot; Zs: nslots x m complex.
+SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, const int* gk1, const int* gslot,
+                        void* Zs, void* stream) {
+  if (N1 < 1 || N1 > 8192 || N2 < 1 || m < 1) {
+    sl_set_last_error("fs_stage2: needs 1 <= N1 <= 8192");
+    return SL_ERR_INVALID;
+  }
+  static bool attr = false;
+  if (!attr) {
+    SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_fs_stage2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)stage2_lds(8192)));
+    attr = true;
+  }
+  dim3 grid((unsigned)N2, (unsigned)((m + 63) / 64));
+  k_fs_stage2<<<grid, NT, stage2_lds(N1), (hipStream_t)stream>>>((const float2*)Y, N1, N2, m, gptr, gk1, gslot,
+                                                                  (float2*)Zs);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+SL_API int sl_fs_post(const void* Zs, int m, int64_t N, const int64_t* samples, int S, const int* sa, const int* sb,
+                      double scale, float* out, int64_t ldo, void* stream) {
+  if (S < 1 || m < 1) return SL_OK;
+  const int64_t tot = (int64_t)S * m;
+  k_fs_post<<<(unsigned)((tot + NT - 1) / NT), NT, 0, (hipStream_t)stream>>>((const float2*)Zs, m, N, samples, S, sa,
+                                                                            sb, scale, out, ldo);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

@@ -188,6 +188,122 @@ def fjlt_operator(prm: torch.Tensor, S: int, N: int, scale: float, out: torch.Te
     return out
 
 
+# ------------------------------------------------------------ four-step path
+_FS_REG = [False]
+
+
+def _fs_lib():
+    import ctypes as C
+    from . import _lib
+    if not _FS_REG[0]:
+        _FS_REG[0] = True
+        vp, i32, i64, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
+        _lib.register("sl_fs_stage1", [vp, i32, i64, i64, i32, vp, i32, i32, u64, i32, vp, vp])
+        _lib.register("sl_fs_stage2", [vp, i32, i32, i32, vp, vp, vp, vp, vp])
+        _lib.register("sl_fs_post", [vp, i32, i64, vp, i32, vp, vp, C.c_double, vp, i64, vp])
+    return _lib
+
+
+FS_N2_MAX = 512
+FS_N1_MAX = 8192
+
+
+def _radix_plan(n2: int):
+    """Radices (8, 4, 5, 3, 7, 2 greedily) multiplying to n2, or None."""
+    rs = []
+    for r in (8, 4, 5, 3, 7, 2):
+        while n2 % r == 0:
+            rs.append(r)
+            n2 //= r
+    return rs if n2 == 1 else None
+
+
+def fourstep_split(N: int):
+    """(N1, N2, radices) of the four-step sampled DCT for length N, or None:
+    N even, M = N / 2 = N1 N2 with N2 <= 512 a 7-smooth divisor (largest
+    such: fewest stage-2 terms) and N1 <= 8192."""
+    if N % 2 or N < 4096:
+        return None
+    M = N // 2
+    for n2 in range(min(FS_N2_MAX, M), 63, -1):
+        if M % n2 == 0 and M // n2 <= FS_N1_MAX:
+            rs = _radix_plan(n2)
+            if rs is not None:
+                return M // n2, n2, rs
+    return None
+
+
+class _FourStepPlan:
+    """Host-side grouping of the needed spectrum points of one sample set:
+    the frequencies k and M - k (mod M) of every sample, their slots, and
+    the CSR of slots by k2 = f mod N2 for stage 2."""
+
+    def __init__(self, N: int, samples: torch.Tensor, dev):
+        self.N = N
+        self.N1, self.N2, rs = fourstep_split(N)
+        self.rplan = sum(r << (4 * i) for i, r in enumerate(rs))
+        self.npass = len(rs)
+        M = N // 2
+        k = samples.detach().to("cpu", torch.int64)
+        fa, fb = k % M, (M - k) % M
+        F = torch.unique(torch.cat([fa, fb]))             # sorted
+        k2, k1 = F % self.N2, F // self.N2
+        order = torch.argsort(k2, stable=True)
+        cnt = torch.bincount(k2, minlength=self.N2)
+        gptr = torch.zeros(self.N2 + 1, dtype=torch.int64)
+        gptr[1:] = torch.cumsum(cnt, 0)
+        i32 = torch.int32
+        self.nslots = F.numel()
+        self.gptr = gptr.to(dev, i32)
+        self.gk1 = k1[order].to(dev, i32)
+        self.gslot = order.to(dev, i32)
+        self.sa = torch.searchsorted(F, fa).to(dev, i32)
+        self.sb = torch.searchsorted(F, fb).to(dev, i32)
+        self.samples = k.to(dev)
+        self.S = k.numel()
+
+
+_FS_PLANS: dict = {}
+
+
+def fourstep_ok(A: torch.Tensor, dim: int, S: int) -> bool:
+    """The four-step path covers dim-0 transforms of row-major f32 / bf16
+    GPU operands whose length splits (``fourstep_split``) and whose sample
+    count keeps stage 2 (2 S N1 terms per column) below a few passes' work."""
+    if dim != 0 or not A.is_cuda or A.dtype not in (torch.float32, torch.bfloat16) or A.stride(1) != 1:
+        return False
+    sp = fourstep_split(A.shape[0])
+    return sp is not None and 2 * S * sp[0] <= 64 * (A.shape[0] // 2)
+
+
+def fjlt_fourstep(A: torch.Tensor, d: torch.Tensor, samples: torch.Tensor, scale: float) -> torch.Tensor:
+    """``scale * P F D A`` along dim 0 (F the orthonormal DCT-II) by the
+    four-step kernels of ``fjlt_fourstep.hip``; returns S x m f32."""
+    import ctypes as C
+    L = _fs_lib()
+    N, m = A.shape
+    key = (samples.data_ptr(), samples.numel(), N, str(A.device))
+    plan = _FS_PLANS.get(key)
+    if plan is None:
+        if len(_FS_PLANS) >= 8:
+            _FS_PLANS.pop(next(iter(_FS_PLANS)))
+        plan = _FourStepPlan(N, samples, A.device)
+        _FS_PLANS[key] = plan
+    st = C.c_void_p(L.stream_of(A))
+    dd = d.to(device=A.device, dtype=torch.float64).contiguous()
+    Y = torch.empty(plan.N2 * plan.N1 * m * 2, dtype=torch.float32, device=A.device)
+    L.call("sl_fs_stage1", L.ptr(A), L.dtype_code(A.dtype), A.stride(0), N, m, L.ptr(dd), plan.N1, plan.N2,
+           C.c_uint64(plan.rplan), plan.npass, L.ptr(Y), st)
+    Zs = torch.empty(plan.nslots * m * 2, dtype=torch.float32, device=A.device)
+    L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1), L.ptr(plan.gslot),
+           L.ptr(Zs), st)
+    del Y
+    out = torch.empty(plan.S, m, dtype=torch.float32, device=A.device)
+    L.call("sl_fs_post", L.ptr(Zs), m, N, L.ptr(plan.samples), plan.S, L.ptr(plan.sa), L.ptr(plan.sb),
+           float(scale), L.ptr(out), out.stride(0), st)
+    return out
+
+
 def fjlt_sampled(A: torch.Tensor, dim: int, d: torch.Tensor, samples: torch.Tensor, scale: float) -> torch.Tensor:
     """``scale * P F D A`` along ``dim`` with F the orthonormal DCT-II and P the
     rows ``samples`` (FJLT with many samples, Blendenpik's t = 4n sketch).
@@ -199,6 +315,8 @@ def fjlt_sampled(A: torch.Tensor, dim: int, d: torch.Tensor, samples: torch.Tens
     torch DCT + index_select composition (same numbers up to rounding)."""
     N = A.shape[dim]
     m = A.shape[1 - dim]
+    if fourstep_ok(A, dim, samples.numel()):
+        return fjlt_fourstep(A, d, samples, scale)
     if A.is_cuda and A.dtype in (torch.float32, torch.bfloat16) and A.stride(1) == 1 and N >= 2:
         import ctypes as C
         from . import _lib

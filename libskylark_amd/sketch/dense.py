@@ -66,10 +66,12 @@ class DenseSketch(SketchTransform):
     # distributed hook: partial product of a shard along the sketched dim
     def apply_local_shard(self, A_local, dim, in_offset, out_rows=None):
         if A_local.layout == torch.sparse_csr:
-            if in_offset != 0 or out_rows is not None:
-                A_local = A_local.to_dense()
-            else:
-                return self._apply_sparse(A_local, dim, False)
+            if out_rows is None:
+                # panels of exactly this shard's sketch columns (no densification)
+                return _ds.apply_sparse(A_local, dim, dist=self.dist, seed=self.entries.seed,
+                                        base=self.entries.base, S=self._S, N=self._N, scale=self.scale,
+                                        in_offset=in_offset)
+            A_local = A_local.to_dense()
         return self._apply_dense(A_local, dim, in_offset=in_offset, out_rows=out_rows)
 
 

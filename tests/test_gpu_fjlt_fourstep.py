@@ -1,0 +1,55 @@
+"""Four-step sampled DCT (fjlt_fourstep.hip) against an fp64 host DCT-II
+(scipy, orthonormal) of D A at the sampled rows: radix plans 8/4/5/3/7/2,
+partial column chunks, bf16 input, repeated samples, k = 0, k = M and
+k > M (the packed real-to-complex partner frequencies), and the FJLT sketch
+class end to end (S > the direct-GEMM limit)."""
+import numpy as np
+import pytest
+import torch
+from scipy.fft import dct
+
+import libskylark_amd as sk
+from libskylark_amd.ops import fut
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(A64, d, samples, scale):
+    return scale * dct(A64 * d[:, None], type=2, norm="ortho", axis=0)[samples]
+
+
+@pytest.mark.parametrize("N,m", [(8192, 37), (13440, 64), (100000, 100), (7392, 5)])
+def test_fourstep_matches_fp64_dct(N, m):
+    split = fut.fourstep_split(N)
+    assert split is not None
+    g = np.random.default_rng(N)
+    A = g.standard_normal((N, m))
+    d = g.choice([-1.0, 1.0], N)
+    M = N // 2
+    samples = np.concatenate([[0, M, M - 1, M + 1, N - 1, 5, 5], g.integers(0, N, 300)])
+    Ad = torch.from_numpy(A).float().cuda()
+    out = fut.fjlt_fourstep(Ad, torch.from_numpy(d), torch.from_numpy(samples), 1.7)
+    ref = _ref(A.astype(np.float32).astype(np.float64), d, samples, 1.7)
+    got = out.double().cpu().numpy()
+    assert np.abs(got - ref).max() <= 2e-5 * np.abs(ref).max(), (np.abs(got - ref).max(), np.abs(ref).max())
+
+
+def test_fourstep_bf16_input():
+    N, m = 20000, 48
+    g = np.random.default_rng(1)
+    A = torch.from_numpy(g.standard_normal((N, m))).to(torch.bfloat16)
+    d = g.choice([-1.0, 1.0], N)
+    samples = g.integers(0, N, 500)
+    out = fut.fjlt_fourstep(A.cuda(), torch.from_numpy(d), torch.from_numpy(samples), 1.0)
+    ref = _ref(A.double().numpy(), d, samples, 1.0)
+    assert np.abs(out.double().cpu().numpy() - ref).max() <= 2e-5 * np.abs(ref).max()
+
+
+def test_fjlt_sketch_uses_fourstep_and_matches_operator():
+    N, m, S = 65536, 40, 1000
+    A = torch.randn(N, m, dtype=torch.float64)
+    T = sk.sketch.FJLT(N, S, context=sk.Context(21))
+    assert fut.fourstep_ok(A.float().cuda(), 0, S)
+    got = T.apply(A.float().cuda(), dim="columnwise").double().cpu()
+    ref = T.realize(torch.float64, "cpu") @ A
+    torch.testing.assert_close(got, ref, rtol=0, atol=3e-5 * float(ref.abs().max()))
