@@ -1,0 +1,56 @@
+"""Hand-written bf16 NT GEMM (gemm_nt.hip) against hipBLASLt (torch.matmul)
+on the framework's shapes: square 8192^3, LSRN's sketch panel product
+(t = 2e4 sketch rows x 26.8k panel x 1e4 [A_hi | A_lo] columns) and the
+random-feature map (1e6 x 512 -> 4096, cos epilogue, bf16 / f32 out).
+Prints one JSON line per case: ms and TFLOP/s of both."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from libskylark_amd.ops import gemm  # noqa: E402
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def case(name, M, N, K, out_dtype=torch.float32, cos=False):
+    A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+    B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+    C = torch.empty(M, N, device="cuda", dtype=out_dtype)
+    sc = torch.rand(N, device="cuda") if cos else None
+    sh = torch.rand(N, device="cuda") if cos else None
+    ours = timeit(lambda: gemm.gemm_nt(A, B, out=C, cos_scales=sc, cos_shifts=sh))
+    Bt = B.t()
+    if out_dtype == torch.float32:
+        lib = timeit(lambda: torch.mm(A, Bt, out_dtype=torch.float32))
+    else:
+        lib = timeit(lambda: torch.mm(A, Bt))
+    err = None
+    if M * N <= 1 << 26:
+        ref = A.float() @ B.float().t()
+        if cos:
+            ref = torch.cos(ref * sc + sh)
+        err = float((C.float() - ref).abs().max() / ref.abs().max())
+    fl = 2.0 * M * N * K
+    print(json.dumps({"case": name, "M": M, "N": N, "K": K, "out": str(out_dtype).split(".")[-1], "cos": cos,
+                      "ours_ms": round(ours, 3), "ours_TF": round(fl / ours / 1e9, 1),
+                      "hipblaslt_ms": round(lib, 3), "hipblaslt_TF": round(fl / lib / 1e9, 1),
+                      "rel_err": err}), flush=True)
+
+
+if __name__ == "__main__":
+    case("square", 8192, 8192, 8192)
+    case("lsrn_panel", 20000, 10000, 26816)
+    case("rft_bf16", 1_000_000, 4096, 512, torch.bfloat16, cos=True)
+    case("rft_f32", 1_000_000, 4096, 512, torch.float32, cos=True)

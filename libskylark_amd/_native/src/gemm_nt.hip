@@ -1,0 +1,315 @@
+// Large bf16 NT GEMM on MFMA for the dense-sketch / random-feature hot path
+// (K1 / K6 of SURVEY §2.4): C (M x N) = epi(A (M x K) B^T), A and B both
+// K-contiguous bf16 (B is the realised sketch panel or the feature frequency
+// matrix: reference sketch/dense_transform_data.hpp:79-152 realises S panel
+// by panel and hands it to a BLAS GEMM; sketch/RFT_Elemental.hpp:83-160 then
+// applies the cosine in a separate loop -- here it is the GEMM's epilogue).
+//
+// gfx950 design (one 256 x 256 output tile per 512-thread workgroup, one
+// workgroup per CU):
+//   * 8 waves as 2 (M) x 4 (N), each a 128 x 64 block = 8 x 4 accumulators
+//     of v_mfma_f32_16x16x32_bf16 (128 VGPRs of C);
+//   * K slices of 64 staged global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//     1 KB = 8 rows x 128 B per wave instruction), two 64 KB stages: the DMA
+//     of slice t + 1 is issued right after the barrier that opens slice t and
+//     has the whole of slice t's 64 MFMAs per wave to land; one counted wait
+//     and one raw s_barrier per slice (no __syncthreads: its fence would
+//     drain the DMA early);
+//   * LDS image [row][8 x 16-B chunks] with chunk ^= (row >> 1) & 7, set by
+//     the per-lane SOURCE address of the DMA: every ds_read_b128 fragment
+//     read is conflict-free under gfx950's b128 lane groups
+//     ({0-3,12-15,20-27}, ...: MI355X_MICROARCH.md §LDS);
+//   * XCD-aware grouped tile order: the 32 tiles an XCD runs at once form a
+//     4 x 8 block of (row, column) tiles, so they share 4 A and 8 B panels
+//     in that XCD's L2 as the K slices advance;
+//   * epilogue straight from the C fragments: alpha * acc (optionally
+//     += into C), or the random-feature map outscale * cos(scale_f acc +
+//     shift_f), f32 or bf16 out.
+// Rows / columns past M / N are clamped on load and never stored; K must be
+// a multiple of 64 (callers zero-pad).
+#include "sl_common.hpp"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int OPB = BM * BK * 2;        // bytes of one operand slice (32 KB)
+constexpr int STAGE = 2 * OPB;          // A + B slice (64 KB)
+constexpr int GM = 4;                   // tile rows per XCD group
+
+enum { EPI_LINEAR = 0, EPI_COS = 1 };
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+template <typename OutT> __device__ __forceinline__ OutT cvt(float v);
+template <> __device__ __forceinline__ float cvt<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t cvt<bf16_t>(float v) { return f_to_bf16(v); }
+template <typename OutT> __device__ __forceinline__ float ld_out(const OutT* p);
+template <> __device__ __forceinline__ float ld_out<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld_out<bf16_t>(const bf16_t* p) { return bf16_to_f(*p); }
+
+template <int EPI, typename OutT, bool ACC>
+__global__ void __launch_bounds__(NT, 1)
+k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, int M, int N, int K,
+          OutT* __restrict__ C, int64_t ldc, float alpha, const float* __restrict__ scales,
+          const float* __restrict__ shifts, int ntm, int ntn, int per) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
+
+  // ---- XCD-aware grouped tile order
+  const int b = blockIdx.x, xcd = b & 7, li = b >> 3;
+  const int id = xcd * per + li;
+  if (id >= ntm * ntn) return;
+  const int gsz = GM * ntn;
+  const int g = id / gsz, gi = id - g * gsz;
+  const int gm0 = g * GM;
+  const int gh = min(GM, ntm - gm0);
+  const int tm = gm0 + gi % gh, tn = gi / gh;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+
+  // ---- DMA sources: instruction i of wave w fills LDS rows (4w + i) * 8 + lane / 8,
+  //      chunk slot lane % 8, with the global chunk (lane % 8) ^ swz(row)
+  const bf16_t* ga[4];
+  const bf16_t* gb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (4 * w + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz(r);
+    const int ar = min(row0 + r, M - 1), br = min(col0 + r, N - 1);
+    ga[i] = A + (int64_t)ar * lda + c * 8;
+    gb[i] = B + (int64_t)br * ldb + c * 8;
+  }
+  auto issue = [&](int kt, int st) {
+    char* base = lds + st * STAGE + w * 4 * 1024;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(ga[i] + k0, base + i * 1024);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(gb[i] + k0, base + OPB + i * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes within an operand slice) for k-half kh:
+  // row = base + (lane & 15), chunk = 4 kh + (lane >> 4)
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / BK;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+    const char* sA = lds + st * STAGE;
+    const char* sB = sA + OPB;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      bf16x8 a[8], bb[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wm * 128 + i * 16 + fr;
+        a[i] = *(const bf16x8*)(sA + r * 128 + (((4 * kh + fq) ^ swz(r)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 64 + j * 16 + fr;
+        bb[j] = *(const bf16x8*)(sB + r * 128 + (((4 * kh + fq) ^ swz(r)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+    }
+    // slice kt + 1 landed (this wave's DMA), everyone done reading stage st
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // ---- epilogue: lane holds C[4 fq + e][fr] of each 16 x 16 block.  The
+  //      wave's 128 x 64 block goes out in four 32-row passes through a
+  //      wave-private LDS patch (row stride 68 floats: the four fq row groups
+  //      of one write land 16 banks apart), re-read as row-contiguous float4
+  //      so every store instruction writes 4 rows x 256 B (f32) / 128 B (bf16).
+  constexpr int EP_LD = 68;
+  float* ep = (float*)lds + w * (32 * EP_LD);
+  float csc[4], csh[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = min(col0 + wn * 64 + j * 16 + fr, N - 1);
+    csc[j] = alpha;
+    csh[j] = 0.f;
+    if (EPI == EPI_COS) { csc[j] = scales ? scales[col] : 1.f; csh[j] = shifts ? shifts[col] : 0.f; }
+  }
+  const int rr = lane >> 4, cq = (lane & 15) * 4;     // read-back: row rr + 4 u, columns cq .. cq + 3
+  const int gcol = col0 + wn * 64 + cq;
+#pragma unroll
+  for (int pss = 0; pss < 4; ++pss) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      const int i = 2 * pss + ii;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[i][j][e];
+          if (EPI == EPI_COS) {
+            const float rev = __builtin_amdgcn_fractf((v * csc[j] + csh[j]) * 0.15915494309189535f);
+            v = alpha * __builtin_amdgcn_cosf(rev);
+          } else {
+            v *= csc[j];
+          }
+          ep[(ii * 16 + 4 * fq + e) * EP_LD + j * 16 + fr] = v;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int lr = rr + 4 * u;
+      const int row = row0 + wm * 128 + pss * 32 + lr;
+      const float4 v = *(const float4*)(ep + lr * EP_LD + cq);
+      if (row < M) {
+        OutT* p = C + (int64_t)row * ldc + gcol;
+        if (gcol + 3 < N && (((uintptr_t)p) & (4 * sizeof(OutT) - 1)) == 0) {
+          if constexpr (sizeof(OutT) == 4) {
+            float4 o = v;
+            if (ACC) { const float4 c = *(const float4*)p; o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w; }
+            *(float4*)p = o;
+          } else {
+            float o[4] = {v.x, v.y, v.z, v.w};
+            if (ACC) {
+              const uint2 c = *(const uint2*)p;
+              o[0] += bf16_to_f((bf16_t)(c.x & 0xffff)); o[1] += bf16_to_f((bf16_t)(c.x >> 16));
+              o[2] += bf16_to_f((bf16_t)(c.y & 0xffff)); o[3] += bf16_to_f((bf16_t)(c.y >> 16));
+            }
+            *(uint2*)p = make_uint2((uint32_t)f_to_bf16(o[0]) | ((uint32_t)f_to_bf16(o[1]) << 16),
+                                    (uint32_t)f_to_bf16(o[2]) | ((uint32_t)f_to_bf16(o[3]) << 16));
+          }
+        } else {
+          const float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (gcol + q < N) {
+              float x = o[q];
+              if (ACC) x += ld_out<OutT>(p + q);
+              p[q] = cvt<OutT>(x);
+            }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+template <int EPI, typename OutT, bool ACC>
+int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, void* C, int64_t ldc,
+           float alpha, const float* scales, const float* shifts, hipStream_t s) {
+  const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
+  const int tiles = ntm * ntn;
+  const int per = (tiles + 7) / 8;
+  k_gemm_nt<EPI, OutT, ACC><<<(unsigned)(per * 8), NT, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, M, N, K,
+                                                              (OutT*)C, ldc, alpha, scales, shifts, ntm, ntn, per);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// Transposing bf16 hi / lo split of an f32 panel: X (w x m, ldx) ->
+// Ht, Lt (m x wpad, ldt; Ht + Lt = X^T to ~2^-17, zero for k >= w), the
+// K-contiguous B operand of a columnwise sketch panel product S_panel X.
+// 64 (k) x 64 (column) tiles through LDS: coalesced row reads of X, one
+// 128-B bf16 row piece per output row and plane.
+__global__ void __launch_bounds__(256)
+k_split_t(const float* __restrict__ X, int w, int m, int64_t ldx, bf16_t* __restrict__ Ht, bf16_t* __restrict__ Lt,
+          int wpad, int64_t ldt) {
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int kk = e >> 6, cc = e & 63;
+    const int k = k0 + kk, c = c0 + cc;
+    tile[kk][cc] = (k < w && c < m) ? X[(int64_t)k * ldx + c] : 0.f;
+  }
+  __syncthreads();
+  const int cc = t >> 2, q = t & 3;
+  const int c = c0 + cc;
+  if (c >= m || k0 + 16 * q >= wpad) return;
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    uint32_t hh[2], ll[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const float x = tile[16 * q + 2 * u + v][cc];
+      const bf16_t hb = f_to_bf16(x);
+      hh[v] = hb;
+      ll[v] = f_to_bf16(x - bf16_to_f(hb));
+    }
+    h[u] = hh[0] | (hh[1] << 16);
+    l[u] = ll[0] | (ll[1] << 16);
+  }
+  uint4* ph = (uint4*)(Ht + (int64_t)c * ldt + k0 + 16 * q);
+  uint4* pl = (uint4*)(Lt + (int64_t)c * ldt + k0 + 16 * q);
+  ph[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  ph[1] = make_uint4(h[4], h[5], h[6], h[7]);
+  pl[0] = make_uint4(l[0], l[1], l[2], l[3]);
+  pl[1] = make_uint4(l[4], l[5], l[6], l[7]);
+}
+
+}  // namespace
+
+// C (M x N, ldc) = alpha A B^T (+ C when accumulate) with A M x K, B N x K
+// bf16 row-major (lda, ldb elements, 16-B aligned rows), K % 64 == 0.
+// epi 1: C = alpha * cos(scales[n] * (A B^T) + shifts[n]).  out: SL_F32 / SL_BF16.
+SL_API int sl_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, void* C,
+                           int64_t ldc, int out_dtype, int accumulate, int epi, float alpha, const float* scales,
+                           const float* shifts, void* stream) {
+  if (M <= 0 || N <= 0) return SL_OK;
+  if (K <= 0 || K % BK || lda % 8 || ldb % 8 || lda < K || ldb < K || ldc < N) {
+    sl_set_last_error("gemm_nt_bf16: needs K % 64 == 0, lda / ldb multiples of 8 and >= K, ldc >= N");
+    return SL_ERR_INVALID;
+  }
+  if ((epi == EPI_COS && accumulate) || (epi != EPI_LINEAR && epi != EPI_COS)) {
+    sl_set_last_error("gemm_nt_bf16: epilogue 0 (linear, optional accumulate) or 1 (cos)");
+    return SL_ERR_INVALID;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (out_dtype == SL_F32) {
+    if (epi == EPI_COS) return launch<EPI_COS, float, false>(A, lda, B, ldb, M, N, K, C, ldc, alpha, scales, shifts, s);
+    if (accumulate) return launch<EPI_LINEAR, float, true>(A, lda, B, ldb, M, N, K, C, ldc, alpha, nullptr, nullptr, s);
+    return launch<EPI_LINEAR, float, false>(A, lda, B, ldb, M, N, K, C, ldc, alpha, nullptr, nullptr, s);
+  }
+  if (out_dtype == SL_BF16) {
+    if (epi == EPI_COS) return launch<EPI_COS, bf16_t, false>(A, lda, B, ldb, M, N, K, C, ldc, alpha, scales, shifts, s);
+    if (accumulate) return launch<EPI_LINEAR, bf16_t, true>(A, lda, B, ldb, M, N, K, C, ldc, alpha, nullptr, nullptr, s);
+    return launch<EPI_LINEAR, bf16_t, false>(A, lda, B, ldb, M, N, K, C, ldc, alpha, nullptr, nullptr, s);
+  }
+  sl_set_last_error("gemm_nt_bf16: f32 / bf16 output");
+  return SL_ERR_UNSUPPORTED;
+}
+
+// Ht / Lt (m x wpad bf16, row stride ldt, wpad % 64 == 0, 16-B aligned rows)
+// from the f32 panel X (w x m, ldx): see k_split_t.
+SL_API int sl_split_bf16_t(const float* X, int w, int m, int64_t ldx, void* Ht, void* Lt, int wpad, int64_t ldt,
+                           void* stream) {
+  if (w < 0 || m <= 0 || wpad % 64 || wpad < w || ldt < wpad || ldt % 8) {
+    sl_set_last_error("split_bf16_t: needs wpad % 64 == 0, wpad >= w, ldt >= wpad, ldt % 8 == 0");
+    return SL_ERR_INVALID;
+  }
+  dim3 grid((unsigned)((m + 63) / 64), (unsigned)(wpad / 64));
+  k_split_t<<<grid, 256, 0, (hipStream_t)stream>>>(X, w, m, ldx, (bf16_t*)Ht, (bf16_t*)Lt, wpad, ldt);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

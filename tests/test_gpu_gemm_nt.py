@@ -1,0 +1,47 @@
+"""Hand-written bf16 NT GEMM (gemm_nt.hip) against fp32 torch products of
+the same bf16 operands: edge tiles (M, N not multiples of 256), several K
+slices, accumulate, bf16 output, the cosine feature epilogue, strided views."""
+import pytest
+import torch
+
+from libskylark_amd.ops import gemm
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops(M, N, K, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    B = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    return A, B, A.float() @ B.float().t()
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (1000, 700, 320), (513, 1300, 1024), (37, 5, 128)])
+def test_gemm_nt_f32_matches(M, N, K):
+    A, B, ref = _ops(M, N, K, M + N)
+    C = gemm.gemm_nt(A, B, alpha=0.5)
+    torch.testing.assert_close(C, 0.5 * ref, rtol=0, atol=1e-4 * float(ref.abs().max()))
+
+
+def test_gemm_nt_accumulate_and_views():
+    M, N, K = 700, 520, 192
+    A, B, ref = _ops(M, N, K, 3)
+    big = torch.zeros(M, N + 40, device="cuda")
+    base = torch.randn(M, N, device="cuda")
+    big[:, 7:7 + N] = base
+    Bv = torch.zeros(N, K + 64, device="cuda", dtype=torch.bfloat16)
+    Bv[:, :K] = B
+    gemm.gemm_nt(A, Bv[:, :K], out=big[:, 7:7 + N], accumulate=True)
+    torch.testing.assert_close(big[:, 7:7 + N], base + ref, rtol=0, atol=1e-4 * float(ref.abs().max()))
+    assert float(big[:, :7].abs().max()) == 0.0 and float(big[:, 7 + N:].abs().max()) == 0.0
+
+
+def test_gemm_nt_bf16_out_and_cos_epilogue():
+    M, N, K = 900, 640, 256
+    A, B, ref = _ops(M, N, K, 4)
+    Cb = gemm.gemm_nt(A, B, out_dtype=torch.bfloat16)
+    torch.testing.assert_close(Cb.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    sc = torch.rand(N, device="cuda") * 0.2
+    sh = torch.rand(N, device="cuda") * 6.28
+    Z = gemm.gemm_nt(A, B, alpha=0.3, cos_scales=sc, cos_shifts=sh)
+    torch.testing.assert_close(Z, 0.3 * torch.cos(ref * sc + sh), rtol=0, atol=2e-4)
