@@ -60,7 +60,7 @@ def fused_ok(A: torch.Tensor, dim: int, k: int, nf: int) -> bool:
 class SplitW:
     """A realised S x N block of W as zero-padded bf16 hi/lo planes."""
 
-    __slots__ = ("hi", "lo", "nf", "k", "ldw")
+    __slots__ = ("hi", "lo", "nf", "k", "ldw", "cat")
 
     def __init__(self, W: torch.Tensor):
         nf, k = W.shape
@@ -71,6 +71,21 @@ class SplitW:
         self.hi = Wf.to(torch.bfloat16)
         self.lo = (Wf - self.hi.float()).to(torch.bfloat16)
         self.nf, self.k, self.ldw = nf, k, ldw
+        self.cat = {}
+
+    def concat(self, terms):
+        """``[W_t1 | W_t2 | ...]`` (nf x n kp, kp = k rounded up to 64): the
+        B operand of a multi-term product as ONE NT GEMM over the
+        concatenated K (``terms``: "h" / "l" per term)."""
+        key = tuple(terms)
+        B = self.cat.get(key)
+        if B is None:
+            kp = -(-self.k // 64) * 64
+            B = torch.zeros(self.nf, len(terms) * kp, dtype=torch.bfloat16, device=self.hi.device)
+            for i, t in enumerate(terms):
+                B[:, i * kp:i * kp + self.k] = (self.hi if t == "h" else self.lo)[:self.nf, :self.k]
+            self.cat[key] = B
+        return B
 
 
 def split_planes(X: torch.Tensor):
@@ -105,6 +120,8 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
     m, k = X.shape
     if k != W.k:
         raise ValueError(f"feature_gemm: inner dimension {k} != {W.k}")
+    if dim == 1 and epi in (EPI_NONE, EPI_COS) and rowterm is None and _gemm_nt_ok(X):
+        return _feature_gemm_nt(X, W, scales, shifts, outscale, epi, out_dtype, use_lo)
     hi, lo, ld = split_planes(X)
     dev = A.device
     if dim == 1:
@@ -124,6 +141,49 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
               float(outscale), int(epi), _lib.ptr(out), _lib.dtype_code(out_dtype), ldo, out_t,
               _lib.ptr(rt) if rt is not None else None, float(p0), C.c_void_p(_lib.stream_of(out)))
     return out
+
+
+# rowwise linear / cosine maps on the 256 x 256 NT GEMM (gemm_nt.hip) with
+# the hi / lo terms concatenated along K (one launch, no per-term passes)
+USE_GEMM_NT = os.environ.get("SL_FEATURE_GEMM_NT", "1") == "1"
+
+
+def _gemm_nt_ok(X):
+    return USE_GEMM_NT and X.stride(1) == 1 and X.dtype in (torch.float32, torch.bfloat16)
+
+
+def _feature_gemm_nt(X, W, scales, shifts, outscale, epi, out_dtype, use_lo):
+    """``[X_h | X_l | X_h] [W_h | W_h | W_l]^T`` (f32 X; bf16 X: ``[X | X]
+    [W_h | W_l]^T``, or one term without W's lo plane) with the epilogue."""
+    from . import gemm as _g
+    m, k = X.shape
+    kp = -(-k // 64) * 64
+    if X.dtype == torch.float32:
+        ta, tb = ("h", "l", "h"), ("h", "h", "l")
+        if not use_lo:
+            ta, tb = ("h", "l"), ("h", "h")
+    else:
+        ta, tb = (("h", "h"), ("h", "l")) if use_lo else (("h",), ("h",))
+    Ap = torch.empty(m, len(ta) * kp, dtype=torch.bfloat16, device=X.device)
+    if X.dtype == torch.float32:
+        Xc = X if X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0 else X.contiguous()
+        _lib.call("sl_split_bf16_2", _lib.ptr(Xc), m, k, Xc.stride(0), _lib.ptr(Ap), _lib.ptr(Ap[:, kp:]), kp,
+                  Ap.stride(0), C.c_void_p(_lib.stream_of(X)))
+        if len(ta) == 3:
+            Ap[:, 2 * kp:].copy_(Ap[:, :kp])
+    else:
+        Ap[:, :k] = X
+        if kp > k:
+            Ap[:, k:kp].zero_()
+        for i in range(1, len(ta)):
+            Ap[:, i * kp:(i + 1) * kp].copy_(Ap[:, :kp])
+    B = W.concat(tb)
+    out = torch.empty(m, W.nf, dtype=out_dtype, device=X.device)
+    if epi == EPI_COS:
+        sc = scales if scales is not None else torch.ones(W.nf, device=X.device)
+        sh = shifts if shifts is not None else torch.zeros(W.nf, device=X.device)
+        return _g.gemm_nt(Ap, B, out=out, alpha=outscale, cos_scales=sc.to(X.device), cos_shifts=sh.to(X.device))
+    return _g.gemm_nt(Ap, B, out=out, alpha=outscale)
 
 
 class WCache:
