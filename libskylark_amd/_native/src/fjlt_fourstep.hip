@@ -30,10 +30,13 @@
 
 namespace {
 
-constexpr int NT = 256;
+constexpr int NT = 256;         // stage-2 / post threads
+constexpr int NT1 = 512;        // stage-1 threads (8 waves)
 constexpr int WC = 32;          // columns per stage-1 workgroup
 constexpr int N2_MAX = 512;     // LDS tile N2 x WC float2 = 128 KB
 constexpr int GMAX = 16;        // frequencies per stage-2 register pass
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -131,8 +134,8 @@ __device__ __forceinline__ void dft<7>(float2* v) {
 // One Stockham pass of radix R over the N2 x WC tile (in place: all reads,
 // barrier, all writes, barrier).  Ns = product of the earlier radices.
 template <int R>
-__device__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict__ tw, int N2, int Ns) {
-  constexpr int QMAX = (N2_MAX / R * WC + NT - 1) / NT;
+__device__ __noinline__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict__ tw, int N2, int Ns) {
+  constexpr int QMAX = (N2_MAX / R * WC + NT1 - 1) / NT1;
   const int tid = threadIdx.x;
   const int nb = N2 / R * WC;
   const int stride = N2 / R;
@@ -140,7 +143,7 @@ __device__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict
   float2 v[QMAX][R];
 #pragma unroll
   for (int q = 0; q < QMAX; ++q) {
-    const int b = tid + NT * q;
+    const int b = tid + NT1 * q;
     if (b < nb) {
       const int col = b & (WC - 1), j = b / WC, k = j % Ns;
 #pragma unroll
@@ -154,7 +157,7 @@ __device__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < QMAX; ++q) {
-    const int b = tid + NT * q;
+    const int b = tid + NT1 * q;
     if (b < nb) {
       const int col = b & (WC - 1), j = b / WC, k = j % Ns;
       const int d0 = (j / Ns) * Ns * R + k;
@@ -173,7 +176,7 @@ __device__ __forceinline__ float ld_f(const T* p) {
 
 // radix plan: up to 12 radices, 4 bits each, packed low first
 template <typename T>
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(NT1)
 k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double* __restrict__ d, int N1, int N2,
             uint64_t rplan, int npass, float2* __restrict__ Y) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -183,32 +186,35 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
   const int j1 = blockIdx.x;
   const int c0 = blockIdx.y * WC;
   const int64_t M = N >> 1;
-  for (int t = tid; t < N2; t += NT) {
+  for (int t = tid; t < N2; t += NT1) {
     float s, c;
     sincospif(-2.0f * (float)t / (float)N2, &s, &c);
     tw[t] = make_float2(c, s);
   }
-  // ---- load z[j1 + N1 j2] (D applied), 32 columns, rows in flight in batches of 8
-  const int col = tid & (WC - 1), rg = tid / WC;   // 8 row groups
+  // ---- load z[j1 + N1 j2] (D applied), 32 columns, 16 rows (32 loads) in
+  //      flight per thread per batch
+  constexpr int RG = NT1 / WC;                     // 16 row groups
+  constexpr int UB = 16;
+  const int col = tid & (WC - 1), rg = tid / WC;
   const bool cok = c0 + col < m;
-  for (int jb = rg; jb < N2; jb += 8 * (NT / WC)) {
-    float re[8], im[8];
+  const T* Ac = A + c0 + col;
+  for (int jb = rg; jb < N2; jb += UB * RG) {
+    float re[UB], im[UB];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j2 = jb + u * (NT / WC);
+    for (int u = 0; u < UB; ++u) {
+      const int j2 = jb + u * RG;
       re[u] = im[u] = 0.f;
       if (j2 < N2 && cok) {
-        const int64_t j = (int64_t)j1 + (int64_t)N1 * j2;
-        const int64_t n0 = 2 * j, n1 = 2 * j + 1;
-        const int64_t x0 = n0 < M ? 2 * n0 : 2 * N - 2 * n0 - 1;
-        const int64_t x1 = n1 < M ? 2 * n1 : 2 * N - 2 * n1 - 1;
-        re[u] = ld_f(A + x0 * lda + c0 + col) * (float)d[x0];
-        im[u] = ld_f(A + x1 * lda + c0 + col) * (float)d[x1];
+        const int64_t j4 = 4 * ((int64_t)j1 + (int64_t)N1 * j2);      // 2 n0
+        const int64_t x0 = j4 < 2 * M ? j4 : 2 * N - j4 - 1;         // n0 = 2j < M ?
+        const int64_t x1 = j4 + 2 < 2 * M ? j4 + 2 : 2 * N - j4 - 3;  // n1 = 2j + 1 < M ?
+        re[u] = ld_f(Ac + x0 * lda) * (float)d[x0];
+        im[u] = ld_f(Ac + x1 * lda) * (float)d[x1];
       }
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int j2 = jb + u * (NT / WC);
+    for (int u = 0; u < UB; ++u) {
+      const int j2 = jb + u * RG;
       if (j2 < N2) buf[j2 * WC + col] = make_float2(re[u], im[u]);
     }
   }
@@ -229,7 +235,7 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
   }
   // ---- W_M^{j1 k2} and out: Y[k2][j1][c]
   if (!cok) return;
-  for (int k2 = rg; k2 < N2; k2 += NT / WC) {
+  for (int k2 = rg; k2 < N2; k2 += RG) {
     const int64_t r = ((int64_t)j1 * k2) % M;
     float s, c;
     sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
@@ -269,7 +275,30 @@ k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __re
       st[g] = (int)((4 * (int64_t)k1[g]) % N1);
       acc[g] = make_float2(0.f, 0.f);
     }
-    for (int j1 = w; j1 < N1; j1 += 4) {
+    // two rows of Y in flight per step; complex MAC as two packed FMAs
+    int j1 = w;
+    for (; j1 + 4 < N1; j1 += 8) {
+      const float2 ya = cok ? Yk[(int64_t)j1 * m + c] : make_float2(0.f, 0.f);
+      const float2 yb = cok ? Yk[(int64_t)(j1 + 4) * m + c] : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int g = 0; g < GMAX; ++g) {
+        if (g < ng) {
+          const float2 ta = tw[idx[g]];
+          idx[g] += st[g];
+          if (idx[g] >= N1) idx[g] -= N1;
+          const float2 tb = tw[idx[g]];
+          idx[g] += st[g];
+          if (idx[g] >= N1) idx[g] -= N1;
+          f2 a = f2{acc[g].x, acc[g].y};
+          a = __builtin_elementwise_fma(f2{ta.x, ta.x}, f2{ya.x, ya.y}, a);
+          a = __builtin_elementwise_fma(f2{-ta.y, ta.y}, f2{ya.y, ya.x}, a);
+          a = __builtin_elementwise_fma(f2{tb.x, tb.x}, f2{yb.x, yb.y}, a);
+          a = __builtin_elementwise_fma(f2{-tb.y, tb.y}, f2{yb.y, yb.x}, a);
+          acc[g] = make_float2(a.x, a.y);
+        }
+      }
+    }
+    for (; j1 < N1; j1 += 4) {
       const float2 y = cok ? Yk[(int64_t)j1 * m + c] : make_float2(0.f, 0.f);
 #pragma unroll
       for (int g = 0; g < GMAX; ++g) {
@@ -354,7 +383,7 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
                                        (int)stage1_lds(N2_MAX)));
       attr = true;
     }
-    k_fs_stage1<float><<<grid, NT, lds, s>>>((const float*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
+    k_fs_stage1<float><<<grid, NT1, lds, s>>>((const float*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
   } else if (dtype == SL_BF16) {
     static bool attr = false;
     if (!attr) {
@@ -362,7 +391,7 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
                                        (int)stage1_lds(N2_MAX)));
       attr = true;
     }
-    k_fs_stage1<bf16_t><<<grid, NT, lds, s>>>((const bf16_t*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
+    k_fs_stage1<bf16_t><<<grid, NT1, lds, s>>>((const bf16_t*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
   } else {
     sl_set_last_error("fs_stage1: f32 / bf16 input");
     return SL_ERR_UNSUPPORTED;

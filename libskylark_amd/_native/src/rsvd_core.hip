@@ -62,7 +62,66 @@ __device__ __forceinline__ double rsq64(double d) {
   return r;
 }
 
+__device__ __forceinline__ double readlane64(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)x, l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // X = R^{-1} (upper, k x k) of the Cholesky factor G = R^T R, from ONE LDL^T
+// elimination of the augmented [G | I]: eliminating below pivot j turns the
+// right block into L^{-1} (unit lower), and R^{-1} = L^{-T} D^{-1/2}.
+// One wave, no barriers: lane c holds column c of both blocks in registers
+// (rows unrolled at compile time, KP >= k), the multipliers T[i][j] and the
+// pivot come from lane j by v_readlane (wave-uniform), each step is two f64
+// FMAs per row and lane.  (The 8-wave LDS-broadcast form this replaces spent
+// ~22 us on k = 40 in barrier / LDS latency; core_stamps r3.)  A pivot at or
+// below 1e-13 x max diag drops its direction (that column of X is zero) and
+// sets ST_PIVOT.  G and X may be LDS or global (ldg, ldx) and may alias.
+template <int KP>
+__device__ __forceinline__ void chol_inv_wave(const double* G, int ldg, double* X, int ldx, int k, int* st,
+                                              double* Dr) {
+  const int c = threadIdx.x & 63;
+  double T[KP], L[KP];
+#pragma unroll
+  for (int i = 0; i < KP; ++i) {
+    T[i] = (i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0);
+    L[i] = (i == c) ? 1.0 : 0.0;
+  }
+  double v = c < k ? fabs(G[c * ldg + c]) : 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  const double thr = 1e-13 * v;
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    if (j < k) {
+      const double d = readlane64(T[j], j);
+      const bool ok = d > thr && d == d;
+      const double rd = ok ? rcp64(d) : 0.0;
+      if (c == 0) Dr[j] = ok ? rsq64(d) : 0.0;
+      bad |= ok ? 0 : 1;
+#pragma unroll
+      for (int i = j + 1; i < KP; ++i) {
+        if (i < k) {
+          const double f = readlane64(T[i], j) * rd;
+          T[i] = fma(-f, T[j], T[i]);
+          L[i] = fma(-f, L[j], L[i]);
+        }
+      }
+    }
+  }
+  if (bad && c == 0) *st |= ST_PIVOT;
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // X[c][i] = L[i][c] D_i^{-1/2} for c <= i
+#pragma unroll
+  for (int i = 0; i < KP; ++i)
+    if (i < k && c < k) X[c * ldx + i] = c <= i ? L[i] * Dr[i] : 0.0;
+}
+
+// (k > 48) X = R^{-1} by the same LDL^T elimination, eight waves, LDS row broadcast:
 // elimination of the augmented [G | I]: eliminating below pivot j turns the
 // right block into L^{-1} (unit lower), and R^{-1} = L^{-T} D^{-1/2}.
 // Register-resident: thread (g = tid >> 6, c = tid & 63) holds entries
@@ -74,7 +133,7 @@ __device__ __forceinline__ double rsq64(double d) {
 // row i.  A pivot at or below 1e-13 x max diag drops its direction (that
 // column of X is zero) and sets ST_PIVOT.  G and X may be LDS or global (ldg,
 // ldx) and may alias.  red: >= KMAX + 2 doubles of LDS scratch.
-__device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
+__device__ void chol_inv_lds(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
   __shared__ double rb[2][2][KMAX];
   const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
   constexpr int RU = KMAX / (NT / 64);
@@ -135,6 +194,18 @@ __device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, in
     const int i = g + 8 * u;
     if (i < k && c < k) X[c * ldx + i] = c <= i ? L[u] * red[2 + i] : 0.0;
   }
+  __syncthreads();
+}
+
+
+// all threads call; k <= 48: wave 0 factors in registers while the others
+// wait at the closing barrier (red: >= KMAX + 2 doubles of LDS scratch)
+__device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
+  if (k > 48) {
+    chol_inv_lds(G, ldg, X, ldx, k, st, red);
+    return;
+  }
+  if ((threadIdx.x >> 6) == 0) chol_inv_wave<48>(G, ldg, X, ldx, k, st, red + 2);
   __syncthreads();
 }
 
@@ -359,7 +430,7 @@ __global__ void __launch_bounds__(NT)
 k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restrict__ part,
           unsigned* __restrict__ counter, const double* __restrict__ Gy, int r, double* __restrict__ Rinv,
           float* __restrict__ M, double* __restrict__ N, double* __restrict__ s_out, int* __restrict__ status,
-          int max_sweeps, double* __restrict__ V0, int* __restrict__ v0_valid) {
+          int max_sweeps, double* __restrict__ V0, int* __restrict__ v0_valid, int* __restrict__ mirror) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int tid = threadIdx.x;
   const int ld = k + 1;
@@ -573,7 +644,11 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
     const double lam = Af[oc * ld + oc];
     N[e] = lam > 0.0 ? a / sqrt(lam) : 0.0;
   }
-  if (tid == 0) atomicOr(status, st_sh);
+  if (tid == 0) {
+    const int all = atomicOr(status, st_sh) | st_sh;
+    // the call's final status word, straight to host-mapped memory (no D2H copy)
+    if (mirror) __hip_atomic_store(mirror, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   SL_CST(SO + 6)
 }
 
@@ -686,7 +761,7 @@ SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, do
   double* part = (double*)((char*)ws + 256);
   const int ng = n < SL_GRAM_NG ? n : SL_GRAM_NG;
   k_gram_la<false><<<ng, NT, gram_la_lds(), s>>>(W, n, k, ldw, part, counter, nullptr, 0, Rinv, nullptr, nullptr,
-                                                nullptr, status, 0, nullptr, nullptr);
+                                                nullptr, status, 0, nullptr, nullptr, nullptr);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -703,9 +778,9 @@ SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double*
 // f64) and the fp64 Gram of Y (k x k).
 // V0 (kp x kp f64, kp = k rounded up to even) + v0_valid: warm start of the
 // Jacobi from the previous call's eigenvectors (null: cold start each call).
-SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                            double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
-                            void* stream) {
+SL_API int sl_rsvd_final_la2(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
+                             double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
+                             int* mirror, void* stream) {
   if (k < 1 || k > KMAX || r < 1 || r > k || n < 1 || n > SL_GRAM_NG * CH_MAX) {
     sl_set_last_error("rsvd_final_la: 1 <= r <= k <= 64 and 1 <= n <= 1024");
     return SL_ERR_UNSUPPORTED;
@@ -721,9 +796,15 @@ SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double
   double* part = (double*)((char*)ws + 256);
   const int ng = n < SL_GRAM_NG ? n : SL_GRAM_NG;
   k_gram_la<true><<<ng, NT, gram_la_lds(), st>>>(W, n, k, ldw, part, counter, Gy, r, nullptr, M, N, s, status,
-                                                max_sweeps > 0 ? max_sweeps : 40, V0, v0_valid);
+                                                max_sweeps > 0 ? max_sweeps : 40, V0, v0_valid, mirror);
   SL_LAUNCH_CHECK();
   return SL_OK;
+}
+
+SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
+                            double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
+                            void* stream) {
+  return sl_rsvd_final_la2(W, n, k, ldw, Gy, r, ws, M, N, s, status, max_sweeps, V0, v0_valid, nullptr, stream);
 }
 
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,

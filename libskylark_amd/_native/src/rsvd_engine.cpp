@@ -30,14 +30,14 @@ SL_API int sl_rsvd_pass_grid(int64_t m);
 SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k);
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws, float* Y,
                         int64_t ldy, int final_pass, int variant, void* stream);
-SL_API int sl_rsvd_reduce(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw, double* Gout,
-                          int ldg, void* stream);
+SL_API int sl_rsvd_reduce_z(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw,
+                            double* Gout, int ldg, int* zero_word, void* stream);
 SL_API int64_t sl_rsvd_gram_workspace(int k);
 SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, double* Rinv, int* status, void* stream);
 SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double* Rinv, void* Zt, void* stream);
-SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                            double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
-                            void* stream);
+SL_API int sl_rsvd_final_la2(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
+                             double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
+                             int* mirror, void* stream);
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream);
 SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
@@ -72,6 +72,8 @@ struct Plan {
   int* v0_valid = nullptr;
   bool warm = true;
   int* status = nullptr;
+  int* mirror_host = nullptr;   // host-mapped copy of the status word, written by the final kernel
+  int* mirror_dev = nullptr;
   // graph of the segments (single rank), valid for graph_A
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
@@ -87,12 +89,11 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
   if (i > p->q + 1 || i < 0) { sl_set_last_error("rsvd: segment out of range"); return SL_ERR_INVALID; }
   int rc = SL_OK;
   if (i == p->q + 1) {
-    return sl_rsvd_final_la(p->WG, (int)p->n, p->k, p->k, p->WG + p->n * p->k, p->r, p->gram_ws, p->M, p->N,
-                            p->s64, p->status, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr, s);
+    return sl_rsvd_final_la2(p->WG, (int)p->n, p->k, p->k, p->WG + p->n * p->k, p->r, p->gram_ws, p->M, p->N,
+                             p->s64, p->status, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr,
+                             p->mirror_dev, s);
   }
-  if (i == 0) {
-    SL_HIP_CHECK(hipMemsetAsync(p->status, 0, sizeof(int), s));
-  } else {
+  if (i > 0) {
     // CholeskyQR of the previous (reduced) W and the next pass operand
     rc = sl_rsvd_inter_la(p->WG, (int)p->n, p->k, p->k, p->gram_ws, p->Rinv, p->status, s);
     if (rc != SL_OK) return rc;
@@ -102,8 +103,9 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
                     final_pass ? 1 : 0, p->variant, s);
   if (rc != SL_OK) return rc;
-  return sl_rsvd_reduce(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
-                        p->k, s);
+  // the first reduce of the call also clears the status word (no memset node)
+  return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
+                          p->k, i == 0 ? p->status : nullptr, s);
 }
 
 void drop_graph(Plan* p) {
@@ -164,6 +166,13 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
     sl_set_last_error("rsvd_plan: memset failed");
     return SL_ERR_HIP;
   }
+  if (hipHostMalloc((void**)&p->mirror_host, 64, hipHostMallocMapped) == hipSuccess) {
+    *p->mirror_host = 0;
+    if (hipHostGetDevicePointer((void**)&p->mirror_dev, p->mirror_host, 0) != hipSuccess) {
+      (void)hipHostFree(p->mirror_host);
+      p->mirror_host = p->mirror_dev = nullptr;
+    }
+  }
   *out = p;
   return SL_OK;
 }
@@ -174,6 +183,7 @@ SL_API int sl_rsvd_plan_destroy(void* plan) {
   drop_graph(p);
   if (p->cap_ev) (void)hipEventDestroy(p->cap_ev);
   if (p->cap_stream) (void)hipStreamDestroy(p->cap_stream);
+  if (p->mirror_host) (void)hipHostFree(p->mirror_host);
   (void)hipFree(p->base);
   delete p;
   return SL_OK;
@@ -326,6 +336,10 @@ SL_API int sl_rsvd_status(void* plan, int* out, void* stream) {
   SL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
   return SL_OK;
 }
+
+// host pointer of the status word's mirror (written by the final kernel of
+// every call; valid once the call has completed), or null if unavailable
+SL_API int* sl_rsvd_status_mirror(void* plan) { return ((Plan*)plan)->mirror_host; }
 
 // device pointer of the status word (for asynchronous checks)
 SL_API int* sl_rsvd_status_ptr(void* plan) { return ((Plan*)plan)->status; }

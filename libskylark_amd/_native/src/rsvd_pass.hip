@@ -435,8 +435,10 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 // sums slabs v, v + 8, ... with four loads in flight; 8 partials through LDS.
 template <typename IT, typename OT>
 __global__ void __launch_bounds__(512)
-k_rsvd_reduce(const IT* __restrict__ slab, int nslab, int64_t total, int cols, OT* __restrict__ out, int ldo) {
+k_rsvd_reduce(const IT* __restrict__ slab, int nslab, int64_t total, int cols, OT* __restrict__ out, int ldo,
+              int* __restrict__ zero_word) {
   __shared__ double part[8][128];
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
   const int64_t e0 = (int64_t)blockIdx.x * 128 + 2 * lane;
   double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
@@ -564,22 +566,31 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
 
 // Sum the v4 pass slabs: W (n x k, into Wout with row stride ldw; f64 when
 // w_f64) and, when Gout is given, the fp64 Gram (k x k, row stride ldg).
-SL_API int sl_rsvd_reduce(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw,
-                          double* Gout, int ldg, void* stream) {
+// as sl_rsvd_reduce, and zero_word (if given) is set to 0 by the same launch
+// (the engine clears the call's status word here instead of a memset node)
+SL_API int sl_rsvd_reduce_z(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw,
+                            double* Gout, int ldg, int* zero_word, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int grid = sl_rsvd_pass_grid(m);
   const char* base = (const char*)ws;
   const int64_t tw = n * k;
   const unsigned gw = (unsigned)((tw + 127) / 128);
-  if (w_f64) k_rsvd_reduce<float, double><<<gw, 512, 0, s>>>((const float*)base, grid, tw, k, (double*)Wout, ldw);
-  else k_rsvd_reduce<float, float><<<gw, 512, 0, s>>>((const float*)base, grid, tw, k, (float*)Wout, ldw);
+  if (w_f64)
+    k_rsvd_reduce<float, double><<<gw, 512, 0, s>>>((const float*)base, grid, tw, k, (double*)Wout, ldw, zero_word);
+  else
+    k_rsvd_reduce<float, float><<<gw, 512, 0, s>>>((const float*)base, grid, tw, k, (float*)Wout, ldw, zero_word);
   SL_LAUNCH_CHECK();
   if (Gout) {
     const int64_t off = ((int64_t)grid * n * k * 4 + 255) & ~(int64_t)255;
     const int64_t tg = (int64_t)k * k;
     k_rsvd_reduce<double, double><<<(unsigned)((tg + 127) / 128), 512, 0, s>>>((const double*)(base + off), grid, tg,
-                                                                               k, Gout, ldg);
+                                                                               k, Gout, ldg, nullptr);
     SL_LAUNCH_CHECK();
   }
   return SL_OK;
+}
+
+SL_API int sl_rsvd_reduce(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw,
+                          double* Gout, int ldg, void* stream) {
+  return sl_rsvd_reduce_z(ws, m, n, k, Wout, w_f64, ldw, Gout, ldg, nullptr, stream);
 }

@@ -290,6 +290,7 @@ def _engine_lib():
         _lib.register("sl_rsvd_finish", [vp_, vp_, i64_, vp_, vp_, vp_])
         _lib.register("sl_rsvd_run", [vp_, vp_, i32_, vp_, i64_, vp_, vp_, vp_])
         _lib.register("sl_rsvd_plan_bind", [vp_, vp_, vp_])
+        _lib.register("sl_rsvd_status_mirror", [vp_], vp_)
     return _lib
 
 
@@ -332,7 +333,13 @@ class _EnginePlan:
         self.WG = torch.empty((n + k) * k, dtype=torch.float64, device=self.dev)
         self.status_dev = torch.zeros(1, dtype=torch.int32, device=self.dev)
         L.call("sl_rsvd_plan_bind", h, ctypes.c_void_p(self.WG.data_ptr()), ctypes.c_void_p(self.status_dev.data_ptr()))
-        self.status_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        # the final kernel writes the call's status word into host-mapped
+        # memory (no D2H copy node); fallback: a pinned copy after the call
+        fn = L.require().sl_rsvd_status_mirror
+        fn.argtypes, fn.restype = [vp_], vp_
+        mp = fn(h)
+        self.mirror = ctypes.c_int.from_address(mp) if mp else None
+        self.status_host = torch.zeros(1, dtype=torch.int32).pin_memory() if self.mirror is None else None
         self.status_ev = None
         self.last_status = 0
         self.calls = 0
@@ -400,25 +407,35 @@ class _EnginePlan:
         # status word of this call back to the host, no wait
         if self.status_ev is None:
             self.status_ev = torch.cuda.Event()
-        self.status_host.copy_(self.status_dev, non_blocking=True)
+        if self.mirror is None or self.comm.size > 1:
+            # several ranks: the finish runs outside the engine's graph and the
+            # mirror is written by the final kernel too; one path for both
+            if self.status_host is None:
+                self.status_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self.status_host.copy_(self.status_dev, non_blocking=True)
         self.status_ev.record()
         self.calls += 1
         return U, s, V
 
     def _poll_status(self):
         if self.status_ev is not None and self.status_ev.query():
-            self.last_status = int(self.status_host[0]) & 15
+            self.last_status = self._status_word()
             if self.last_status & (ST_NONFINITE | ST_RANK | ST_NOCONV):
                 import warnings
                 warnings.warn(f"approximate_svd (device): previous call flagged status {self.last_status} "
                               "(2: non-finite data, 4: eigensolver not converged, 8: numerical rank < r)",
                               RuntimeWarning, stacklevel=3)
 
+    def _status_word(self) -> int:
+        if self.mirror is not None and self.comm.size == 1:
+            return int(self.mirror.value) & 15
+        return int(self.status_host[0]) & 15
+
     def wait_status(self) -> int:
         """Synchronise with the last call and return its status bits."""
         if self.status_ev is not None:
             self.status_ev.synchronize()
-            self.last_status = int(self.status_host[0]) & 15
+            self.last_status = self._status_word()
         return self.last_status
 
 

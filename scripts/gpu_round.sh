@@ -1,0 +1,10 @@
+#!/bin/bash
+# engine-focused GPU step: core / engine tests, phase stamps, bench + trace, FJLT four-step tests + bench
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+bash scripts/gpu_tests_from.sh tests/test_gpu_rsvd_core.py tests/test_nla.py tests/test_capi.py || exit 1
+timeout -k 10 120 python benchmarks/core_stamps.py > $OUT/core_stamps.log 2>&1; rc=$?; grep '^{' $OUT/core_stamps.log; [ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_bench_prof.sh || exit 1
+bash scripts/gpu_tests_from.sh tests/test_gpu_fjlt_fourstep.py || exit 1
+timeout -k 10 200 python benchmarks/bench_fjlt.py > $OUT/fjlt.log 2>&1; rc=$?; cat $OUT/fjlt.log | grep '^{'; exit $rc
