@@ -183,8 +183,10 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
   float2* buf = lds;                 // N2 x WC
   float2* tw = lds + N2 * WC;        // N2: W_N2^t
   const int tid = threadIdx.x;
-  const int j1 = blockIdx.x;
-  const int c0 = blockIdx.y * WC;
+  // column chunk fastest: the workgroups in flight together cover whole rows of
+  // A (and of Y), so every DRAM page they open is read / written in full
+  const int j1 = blockIdx.y;
+  const int c0 = blockIdx.x * WC;
   const int64_t M = N >> 1;
   for (int t = tid; t < N2; t += NT1) {
     float s, c;
@@ -252,8 +254,8 @@ k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __re
   float2* tw = lds;                       // N1: W_N1^t
   float2* red = lds + N1;                 // 4 waves x GMAX x 64
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int k2 = blockIdx.x;
-  const int c = blockIdx.y * 64 + lane;
+  const int k2 = blockIdx.y;                 // column chunk fastest (whole Y rows in flight)
+  const int c = blockIdx.x * 64 + lane;
   const int g0 = gptr[k2], g1 = gptr[k2 + 1];
   if (g0 == g1) return;
   for (int t = tid; t < N1; t += NT) {
@@ -375,7 +377,7 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
   if (prod != N2) { sl_set_last_error("fs_stage1: radix plan does not multiply to N2"); return SL_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = stage1_lds(N2);
-  dim3 grid((unsigned)N1, (unsigned)((m + WC - 1) / WC));
+  dim3 grid((unsigned)((m + WC - 1) / WC), (unsigned)N1);
   if (dtype == SL_F32) {
     static bool attr = false;
     if (!attr) {
@@ -413,7 +415,7 @@ SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, c
                                      (int)stage2_lds(8192)));
     attr = true;
   }
-  dim3 grid((unsigned)N2, (unsigned)((m + 63) / 64));
+  dim3 grid((unsigned)((m + 63) / 64), (unsigned)N2);
   k_fs_stage2<<<grid, NT, stage2_lds(N1), (hipStream_t)stream>>>((const float2*)Y, N1, N2, m, gptr, gk1, gslot,
                                                                   (float2*)Zs);
   SL_LAUNCH_CHECK();

@@ -62,66 +62,7 @@ __device__ __forceinline__ double rsq64(double d) {
   return r;
 }
 
-__device__ __forceinline__ double readlane64(double v, int l) {
-  const long long x = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)x, l);
-  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
 // X = R^{-1} (upper, k x k) of the Cholesky factor G = R^T R, from ONE LDL^T
-// elimination of the augmented [G | I]: eliminating below pivot j turns the
-// right block into L^{-1} (unit lower), and R^{-1} = L^{-T} D^{-1/2}.
-// One wave, no barriers: lane c holds column c of both blocks in registers
-// (rows unrolled at compile time, KP >= k), the multipliers T[i][j] and the
-// pivot come from lane j by v_readlane (wave-uniform), each step is two f64
-// FMAs per row and lane.  (The 8-wave LDS-broadcast form this replaces spent
-// ~22 us on k = 40 in barrier / LDS latency; core_stamps r3.)  A pivot at or
-// below 1e-13 x max diag drops its direction (that column of X is zero) and
-// sets ST_PIVOT.  G and X may be LDS or global (ldg, ldx) and may alias.
-template <int KP>
-__device__ __forceinline__ void chol_inv_wave(const double* G, int ldg, double* X, int ldx, int k, int* st,
-                                              double* Dr) {
-  const int c = threadIdx.x & 63;
-  double T[KP], L[KP];
-#pragma unroll
-  for (int i = 0; i < KP; ++i) {
-    T[i] = (i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0);
-    L[i] = (i == c) ? 1.0 : 0.0;
-  }
-  double v = c < k ? fabs(G[c * ldg + c]) : 0.0;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  const double thr = 1e-13 * v;
-  int bad = 0;
-#pragma unroll
-  for (int j = 0; j < KP; ++j) {
-    if (j < k) {
-      const double d = readlane64(T[j], j);
-      const bool ok = d > thr && d == d;
-      const double rd = ok ? rcp64(d) : 0.0;
-      if (c == 0) Dr[j] = ok ? rsq64(d) : 0.0;
-      bad |= ok ? 0 : 1;
-#pragma unroll
-      for (int i = j + 1; i < KP; ++i) {
-        if (i < k) {
-          const double f = readlane64(T[i], j) * rd;
-          T[i] = fma(-f, T[j], T[i]);
-          L[i] = fma(-f, L[j], L[i]);
-        }
-      }
-    }
-  }
-  if (bad && c == 0) *st |= ST_PIVOT;
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  // X[c][i] = L[i][c] D_i^{-1/2} for c <= i
-#pragma unroll
-  for (int i = 0; i < KP; ++i)
-    if (i < k && c < k) X[c * ldx + i] = c <= i ? L[i] * Dr[i] : 0.0;
-}
-
-// (k > 48) X = R^{-1} by the same LDL^T elimination, eight waves, LDS row broadcast:
 // elimination of the augmented [G | I]: eliminating below pivot j turns the
 // right block into L^{-1} (unit lower), and R^{-1} = L^{-T} D^{-1/2}.
 // Register-resident: thread (g = tid >> 6, c = tid & 63) holds entries
@@ -133,7 +74,7 @@ __device__ __forceinline__ void chol_inv_wave(const double* G, int ldg, double* 
 // row i.  A pivot at or below 1e-13 x max diag drops its direction (that
 // column of X is zero) and sets ST_PIVOT.  G and X may be LDS or global (ldg,
 // ldx) and may alias.  red: >= KMAX + 2 doubles of LDS scratch.
-__device__ void chol_inv_lds(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
+__device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
   __shared__ double rb[2][2][KMAX];
   const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
   constexpr int RU = KMAX / (NT / 64);
@@ -198,36 +139,31 @@ __device__ void chol_inv_lds(const double* G, int ldg, double* X, int ldx, int k
 }
 
 
-// all threads call; k <= 48: wave 0 factors in registers while the others
-// wait at the closing barrier (red: >= KMAX + 2 doubles of LDS scratch)
-__device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
-  if (k > 48) {
-    chol_inv_lds(G, ldg, X, ldx, k, st, red);
-    return;
-  }
-  if ((threadIdx.x >> 6) == 0) chol_inv_wave<48>(G, ldg, X, ldx, k, st, red + 2);
-  __syncthreads();
-}
-
-// C = A^T B (transa) or A B for k x k LDS matrices, four outputs per thread
+// C = A^T B (transa) or A B for k x k LDS matrices (row stride ld) on f64
+// MFMA: 16 x 16 output tiles over the 8 waves, K in steps of 4
+// (v_mfma_f64_16x16x4_f64: lane l holds A[l & 15][l >> 4], B[l >> 4][l & 15];
+// C/D col = l & 15, row = (l >> 4) + 4 r).  Out-of-range rows / k read 0.
+// (The 512-thread FMA loop this replaces took ~6.5 us per k = 40 product.)
+typedef __attribute__((ext_vector_type(4))) double f64x4;
 __device__ void small_gemm(const double* A, const double* B, double* C, int k, int ld, bool transa) {
-  const int tid = threadIdx.x;
-  const int nq = (k + 3) / 4;
-  for (int e = tid; e < k * nq; e += NT) {
-    const int i = e / nq, c0 = 4 * (e - i * nq);
-    double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    for (int l = 0; l < k; ++l) {
-      const double a = transa ? A[l * ld + i] : A[i * ld + l];
-      const double* b = B + l * ld + c0;
-      a0 += a * b[0];
-      if (c0 + 1 < k) a1 += a * b[1];
-      if (c0 + 2 < k) a2 += a * b[2];
-      if (c0 + 3 < k) a3 += a * b[3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nt = (k + 15) >> 4;
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = w; t < nt * nt; t += NT / 64) {
+    const int ti = t / nt, tj = t - ti * nt;
+    const int row = ti * 16 + fr, col = tj * 16 + fr;
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < k; k0 += 4) {
+      const int kk = k0 + fq;
+      const double a = (row < k && kk < k) ? (transa ? A[kk * ld + row] : A[row * ld + kk]) : 0.0;
+      const double b = (col < k && kk < k) ? B[kk * ld + col] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
-    C[i * ld + c0] = a0;
-    if (c0 + 1 < k) C[i * ld + c0 + 1] = a1;
-    if (c0 + 2 < k) C[i * ld + c0 + 2] = a2;
-    if (c0 + 3 < k) C[i * ld + c0 + 3] = a3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int orow = ti * 16 + fq + 4 * r;
+      if (orow < k && col < k) C[orow * ld + col] = acc[r];
+    }
   }
 }
 
@@ -603,8 +539,36 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
   }
   __syncthreads();
   SL_CST(SO + 4)
+  // warm start already diagonal to roundoff (a repeated problem: |c'_pq|^2 <=
+  // max(1e-24 c'_pp c'_qq, (1e-14 max|c'_ii|)^2) for every pair): the
+  // eigenpairs are diag(C') and V0 as they stand, no confirming sweep
+  bool diag_ok = false;
+  if (warm) {
+    if (tid == 0) flags[3] = 0;
+    __syncthreads();
+    double amax = 0.0;
+    for (int i = 0; i < kp; ++i) amax = fmax(amax, fabs(b2[i * ld + i]));
+    const double noise2 = (1e-14 * amax) * (1e-14 * amax);
+    int off = 0;
+    for (int e = tid; e < kp * kp; e += NT) {
+      const int i = e / kp, c = e - i * kp;
+      if (i < c) {
+        const double apq = b2[i * ld + c];
+        if (apq * apq > fmax(1e-24 * fabs(b2[i * ld + i] * b2[c * ld + c]), noise2)) off = 1;
+      }
+    }
+    if (off) flags[3] = 1;
+    __syncthreads();
+    diag_ok = flags[3] == 0;
+    __syncthreads();
+  }
   // Jacobi on b2, V in b1 (V0 when warm)
-  double* Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, &st_sh, warm);
+  double* Af = b2;
+  if (diag_ok) {
+    if (tid == 0) flags[3] = 0;
+  } else {
+    Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, &st_sh, warm);
+  }
   SL_CST(SO + 5)
 #ifdef SL_CORE_STAMPS
   if (tid == 0) g_core_st[SO + 8] = flags[3];
