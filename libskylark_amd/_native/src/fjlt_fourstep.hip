@@ -12,17 +12,23 @@
 //   stage 2  Z[k]      = sum_j1 W_N1^{j1 k1} Y[k2][j1]              (needed k only)
 //   stage 3  out[s]    = scale c_k Re(W_4N^k (E + W_N^k O)),  k = sample s
 //
-// Stage 1: one workgroup per (j1, 32-column chunk).  The 2 N2 rows of x it
-// needs are read as 128-B row pieces (D applied on load) into an LDS tile of
-// N2 x 32 complex values; the length-N2 FFT runs in place in that tile as
-// mixed-radix Stockham passes (radix 8/4/5/3/7/2: every thread reads its
-// butterflies' inputs, barrier, writes the outputs, barrier) with a W_N2
-// table in LDS; the W_M twiddle is applied on the way out.  Y is laid out
-// [k2][j1][column], so stage 2 streams one contiguous N1 x m slab per k2.
+// Stage 1: one workgroup per (j1, 16-column chunk), two per CU.  The 2 N2
+// rows of x it needs are read as 64-B row pieces (D applied on load; every
+// load of a batch in flight: clamped addresses, no per-element branches)
+// into an LDS tile of N2 x 16 complex values; the length-N2 FFT runs in place
+// in that tile as mixed-radix Stockham passes (radix 8/4/5/3/7/2: every
+// thread reads its butterflies' inputs, barrier, writes the outputs,
+// barrier) with a W_N2 table in LDS; the W_M twiddles of the workgroup's j1
+// come from a second LDS table.  Y is laid out [k2][j1][column], so stage 2
+// streams one contiguous N1 x m slab per k2.  Both grids are XCD-aware: an
+// XCD walks (row, column chunk) with the chunk fastest, so the workgroups in
+// flight on it cover whole rows of A / Y in its own L2.
 // Stage 2: one workgroup per (k2, 64-column chunk); lane = column, the four
 // waves split j1 and reduce through LDS; the frequencies with this k2 (a
-// CSR group built on the host) accumulate in registers, twiddles from a
-// W_N1 table in LDS indexed by (j1 k1) mod N1 (exact, no drift).
+// CSR group built on the host) accumulate in registers (packed f32 FMAs),
+// twiddles from a W_N1 table in LDS indexed by (j1 k1) mod N1 (exact, no
+// drift).  (Stage 2 as a length-N1 LDS FFT measured slower: 3.74 vs 2.36 ms
+// at N1 = 1000, m = 1000.)
 // HBM traffic: A once, Y written and read once (M x m complex = A's f32
 // bytes each way); the dense m x N copy and the N/2-point spectrum of the
 // rocFFT pipeline (ops/fut.py) are gone.
@@ -31,9 +37,9 @@
 namespace {
 
 constexpr int NT = 256;         // stage-2 / post threads
-constexpr int NT1 = 512;        // stage-1 threads (8 waves)
-constexpr int WC = 32;          // columns per stage-1 workgroup
-constexpr int N2_MAX = 512;     // LDS tile N2 x WC float2 = 128 KB
+constexpr int NT1 = 256;        // stage-1 threads (4 waves)
+constexpr int WC = 16;          // columns per stage-1 workgroup
+constexpr int N2_MAX = 512;     // LDS tile N2 x WC float2 = 64 KB: two workgroups per CU
 constexpr int GMAX = 16;        // frequencies per stage-2 register pass
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -133,9 +139,9 @@ __device__ __forceinline__ void dft<7>(float2* v) {
 
 // One Stockham pass of radix R over the N2 x WC tile (in place: all reads,
 // barrier, all writes, barrier).  Ns = product of the earlier radices.
-template <int R>
+template <int R, int NMAX>
 __device__ __noinline__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict__ tw, int N2, int Ns) {
-  constexpr int QMAX = (N2_MAX / R * WC + NT1 - 1) / NT1;
+  constexpr int QMAX = (NMAX / R * WC + NT1 - 1) / NT1;
   const int tid = threadIdx.x;
   const int nb = N2 / R * WC;
   const int stride = N2 / R;
@@ -168,6 +174,24 @@ __device__ __noinline__ void stockham_pass(float2* __restrict__ buf, const float
   __syncthreads();
 }
 
+// in-place length-n FFT of the n x WC LDS tile (radix plan: 4-bit radices, low first)
+template <int NMAX>
+__device__ void fft_tile(float2* buf, const float2* tw, int n, uint64_t rplan, int npass) {
+  int Ns = 1;
+  for (int p = 0; p < npass; ++p) {
+    const int R = (int)((rplan >> (4 * p)) & 15);
+    switch (R) {
+      case 8: stockham_pass<8, NMAX>(buf, tw, n, Ns); break;
+      case 4: stockham_pass<4, NMAX>(buf, tw, n, Ns); break;
+      case 5: stockham_pass<5, NMAX>(buf, tw, n, Ns); break;
+      case 3: stockham_pass<3, NMAX>(buf, tw, n, Ns); break;
+      case 7: stockham_pass<7, NMAX>(buf, tw, n, Ns); break;
+      default: stockham_pass<2, NMAX>(buf, tw, n, Ns); break;
+    }
+    Ns *= R;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ float ld_f(const T* p) {
   if constexpr (sizeof(T) == 2) return bf16_to_f(*(const bf16_t*)p);
@@ -178,20 +202,28 @@ __device__ __forceinline__ float ld_f(const T* p) {
 template <typename T>
 __global__ void __launch_bounds__(NT1)
 k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double* __restrict__ d, int N1, int N2,
-            uint64_t rplan, int npass, float2* __restrict__ Y) {
+            uint64_t rplan, int npass, float2* __restrict__ Y, int per) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   float2* buf = lds;                 // N2 x WC
   float2* tw = lds + N2 * WC;        // N2: W_N2^t
   const int tid = threadIdx.x;
-  // column chunk fastest: the workgroups in flight together cover whole rows of
-  // A (and of Y), so every DRAM page they open is read / written in full
-  const int j1 = blockIdx.y;
-  const int c0 = blockIdx.x * WC;
+  // XCD-aware order (block b runs on XCD b % 8): each XCD walks a contiguous
+  // range of (j1, column chunk) with the chunk fastest, so the workgroups in
+  // flight on one XCD cover whole rows of A and Y in that XCD's L2
+  const int nch = (m + WC - 1) / WC;
+  const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= nch * N1) return;
+  const int j1 = L / nch;
+  const int c0 = (L - j1 * nch) * WC;
   const int64_t M = N >> 1;
+  float2* tm = tw + N2;              // N2: W_M^{(j1 k2) mod M} of this j1
   for (int t = tid; t < N2; t += NT1) {
     float s, c;
     sincospif(-2.0f * (float)t / (float)N2, &s, &c);
     tw[t] = make_float2(c, s);
+    const int64_t r = ((int64_t)j1 * t) % M;
+    sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
+    tm[t] = make_float2(c, s);
   }
   // ---- load z[j1 + N1 j2] (D applied), 32 columns, 16 rows (32 loads) in
   //      flight per thread per batch
@@ -199,63 +231,51 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
   constexpr int UB = 16;
   const int col = tid & (WC - 1), rg = tid / WC;
   const bool cok = c0 + col < m;
-  const T* Ac = A + c0 + col;
+  // unconditional loads from clamped addresses (a per-element "load or zero"
+  // branch makes hipcc wait for each load before the next: one L2 round trip
+  // per element instead of all of them in flight)
+  const T* Ac = A + min(c0 + col, m - 1);
   for (int jb = rg; jb < N2; jb += UB * RG) {
     float re[UB], im[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int j2 = jb + u * RG;
-      re[u] = im[u] = 0.f;
-      if (j2 < N2 && cok) {
-        const int64_t j4 = 4 * ((int64_t)j1 + (int64_t)N1 * j2);      // 2 n0
-        const int64_t x0 = j4 < 2 * M ? j4 : 2 * N - j4 - 1;         // n0 = 2j < M ?
-        const int64_t x1 = j4 + 2 < 2 * M ? j4 + 2 : 2 * N - j4 - 3;  // n1 = 2j + 1 < M ?
-        re[u] = ld_f(Ac + x0 * lda) * (float)d[x0];
-        im[u] = ld_f(Ac + x1 * lda) * (float)d[x1];
-      }
+      const int j2 = min(jb + u * RG, N2 - 1);
+      const int64_t j4 = 4 * ((int64_t)j1 + (int64_t)N1 * j2);      // 2 n0
+      const int64_t x0 = j4 < 2 * M ? j4 : 2 * N - j4 - 1;         // n0 = 2j < M ?
+      const int64_t x1 = j4 + 2 < 2 * M ? j4 + 2 : 2 * N - j4 - 3;  // n1 = 2j + 1 < M ?
+      re[u] = ld_f(Ac + x0 * lda) * (float)d[x0];
+      im[u] = ld_f(Ac + x1 * lda) * (float)d[x1];
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int j2 = jb + u * RG;
-      if (j2 < N2) buf[j2 * WC + col] = make_float2(re[u], im[u]);
+      if (j2 < N2) buf[j2 * WC + col] = cok ? make_float2(re[u], im[u]) : make_float2(0.f, 0.f);
     }
   }
   __syncthreads();
   // ---- length-N2 FFT along the tile's rows
-  int Ns = 1;
-  for (int p = 0; p < npass; ++p) {
-    const int R = (int)((rplan >> (4 * p)) & 15);
-    switch (R) {
-      case 8: stockham_pass<8>(buf, tw, N2, Ns); break;
-      case 4: stockham_pass<4>(buf, tw, N2, Ns); break;
-      case 5: stockham_pass<5>(buf, tw, N2, Ns); break;
-      case 3: stockham_pass<3>(buf, tw, N2, Ns); break;
-      case 7: stockham_pass<7>(buf, tw, N2, Ns); break;
-      default: stockham_pass<2>(buf, tw, N2, Ns); break;
-    }
-    Ns *= R;
-  }
+  fft_tile<N2_MAX>(buf, tw, N2, rplan, npass);
   // ---- W_M^{j1 k2} and out: Y[k2][j1][c]
   if (!cok) return;
-  for (int k2 = rg; k2 < N2; k2 += RG) {
-    const int64_t r = ((int64_t)j1 * k2) % M;
-    float s, c;
-    sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
-    Y[((int64_t)k2 * N1 + j1) * m + c0 + col] = cmul(buf[k2 * WC + col], make_float2(c, s));
-  }
+  for (int k2 = rg; k2 < N2; k2 += RG)
+    Y[((int64_t)k2 * N1 + j1) * m + c0 + col] = cmul(buf[k2 * WC + col], tm[k2]);
 }
 
 // Stage 2: Zs[slot][c] = sum_j1 W_N1^{j1 k1} Y[k2][j1][c] for the (k1, slot)
 // pairs of group k2 (gptr CSR over k2, gk1 / gslot entries).
 __global__ void __launch_bounds__(NT)
 k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __restrict__ gptr,
-            const int* __restrict__ gk1, const int* __restrict__ gslot, float2* __restrict__ Zs) {
+            const int* __restrict__ gk1, const int* __restrict__ gslot, float2* __restrict__ Zs, int per) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   float2* tw = lds;                       // N1: W_N1^t
   float2* red = lds + N1;                 // 4 waves x GMAX x 64
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int k2 = blockIdx.y;                 // column chunk fastest (whole Y rows in flight)
-  const int c = blockIdx.x * 64 + lane;
+  // XCD-aware order as in stage 1: an XCD walks (k2, 64-column chunk) with the chunk fastest
+  const int nch = (m + 63) / 64;
+  const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= nch * N2) return;
+  const int k2 = L / nch;
+  const int c = (L - k2 * nch) * 64 + lane;
   const int g0 = gptr[k2], g1 = gptr[k2 + 1];
   if (g0 == g1) return;
   for (int t = tid; t < N1; t += NT) {
@@ -279,9 +299,10 @@ k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __re
     }
     // two rows of Y in flight per step; complex MAC as two packed FMAs
     int j1 = w;
+    const float2* Yc = Yk + min(c, m - 1);     // clamped: unconditional loads (see stage 1)
     for (; j1 + 4 < N1; j1 += 8) {
-      const float2 ya = cok ? Yk[(int64_t)j1 * m + c] : make_float2(0.f, 0.f);
-      const float2 yb = cok ? Yk[(int64_t)(j1 + 4) * m + c] : make_float2(0.f, 0.f);
+      const float2 ya = Yc[(int64_t)j1 * m];
+      const float2 yb = Yc[(int64_t)(j1 + 4) * m];
 #pragma unroll
       for (int g = 0; g < GMAX; ++g) {
         if (g < ng) {
@@ -301,7 +322,7 @@ k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __re
       }
     }
     for (; j1 < N1; j1 += 4) {
-      const float2 y = cok ? Yk[(int64_t)j1 * m + c] : make_float2(0.f, 0.f);
+      const float2 y = Yc[(int64_t)j1 * m];
 #pragma unroll
       for (int g = 0; g < GMAX; ++g) {
         if (g < ng) {
@@ -348,7 +369,7 @@ k_fs_post(const float2* __restrict__ Zs, int m, int64_t N, const int64_t* __rest
   out[(int64_t)s * ldo + c] = (float)(scale * ck * x);
 }
 
-size_t stage1_lds(int N2) { return (size_t)(N2 * WC + N2) * sizeof(float2); }
+size_t stage1_lds(int N2) { return (size_t)(N2 * WC + 2 * N2) * sizeof(float2); }
 size_t stage2_lds(int N1) { return (size_t)(N1 + 4 * GMAX * 64) * sizeof(float2); }
 
 }  // namespace
@@ -377,7 +398,9 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
   if (prod != N2) { sl_set_last_error("fs_stage1: radix plan does not multiply to N2"); return SL_ERR_INVALID; }
   hipStream_t s = (hipStream_t)stream;
   const size_t lds = stage1_lds(N2);
-  dim3 grid((unsigned)((m + WC - 1) / WC), (unsigned)N1);
+  const int64_t nblk = (int64_t)((m + WC - 1) / WC) * N1;
+  const int per = (int)((nblk + 7) / 8);
+  const unsigned grid = (unsigned)(8 * (int64_t)per);
   if (dtype == SL_F32) {
     static bool attr = false;
     if (!attr) {
@@ -385,7 +408,7 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
                                        (int)stage1_lds(N2_MAX)));
       attr = true;
     }
-    k_fs_stage1<float><<<grid, NT1, lds, s>>>((const float*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
+    k_fs_stage1<float><<<grid, NT1, lds, s>>>((const float*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y, per);
   } else if (dtype == SL_BF16) {
     static bool attr = false;
     if (!attr) {
@@ -393,7 +416,7 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
                                        (int)stage1_lds(N2_MAX)));
       attr = true;
     }
-    k_fs_stage1<bf16_t><<<grid, NT1, lds, s>>>((const bf16_t*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y);
+    k_fs_stage1<bf16_t><<<grid, NT1, lds, s>>>((const bf16_t*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y, per);
   } else {
     sl_set_last_error("fs_stage1: f32 / bf16 input");
     return SL_ERR_UNSUPPORTED;
@@ -415,9 +438,10 @@ SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, c
                                      (int)stage2_lds(8192)));
     attr = true;
   }
-  dim3 grid((unsigned)((m + 63) / 64), (unsigned)N2);
-  k_fs_stage2<<<grid, NT, stage2_lds(N1), (hipStream_t)stream>>>((const float2*)Y, N1, N2, m, gptr, gk1, gslot,
-                                                                  (float2*)Zs);
+  const int64_t nblk = (int64_t)((m + 63) / 64) * N2;
+  const int per = (int)((nblk + 7) / 8);
+  k_fs_stage2<<<(unsigned)(8 * (int64_t)per), NT, stage2_lds(N1), (hipStream_t)stream>>>(
+      (const float2*)Y, N1, N2, m, gptr, gk1, gslot, (float2*)Zs, per);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -431,3 +455,4 @@ SL_API int sl_fs_post(const void* Zs, int m, int64_t N, const int64_t* samples, 
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
+

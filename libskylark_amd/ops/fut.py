@@ -243,6 +243,7 @@ class _FourStepPlan:
         self.N1, self.N2, rs = fourstep_split(N)
         self.rplan = sum(r << (4 * i) for i, r in enumerate(rs))
         self.npass = len(rs)
+
         M = N // 2
         k = samples.detach().to("cpu", torch.int64)
         fa, fb = k % M, (M - k) % M
@@ -295,8 +296,8 @@ def fjlt_fourstep(A: torch.Tensor, d: torch.Tensor, samples: torch.Tensor, scale
     L.call("sl_fs_stage1", L.ptr(A), L.dtype_code(A.dtype), A.stride(0), N, m, L.ptr(dd), plan.N1, plan.N2,
            C.c_uint64(plan.rplan), plan.npass, L.ptr(Y), st)
     Zs = torch.empty(plan.nslots * m * 2, dtype=torch.float32, device=A.device)
-    L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1), L.ptr(plan.gslot),
-           L.ptr(Zs), st)
+    L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1),
+           L.ptr(plan.gslot), L.ptr(Zs), st)
     del Y
     out = torch.empty(plan.S, m, dtype=torch.float32, device=A.device)
     L.call("sl_fs_post", L.ptr(Zs), m, N, L.ptr(plan.samples), plan.S, L.ptr(plan.sa), L.ptr(plan.sb),
