@@ -68,14 +68,18 @@ __device__ __forceinline__ double rsq64(double d) {
 // Register-resident: thread (g = tid >> 6, c = tid & 63) holds entries
 // (i, c) of both blocks for its rows i = g + 8u, u < 8; a step reads the
 // pivot row from a 2-deep LDS row buffer (written by its owner one step
-// earlier), updates in registers and publishes the next pivot row: ONE
-// barrier and one LDS round trip per step.  Full rows are updated, so the
+// earlier), updates in registers and publishes the next pivot rows: two
+// pivots per barrier (see the body).  Full rows are updated, so the
 // trailing block stays symmetric and T[j][i] is the multiplier numerator of
 // row i.  A pivot at or below 1e-13 x max diag drops its direction (that
 // column of X is zero) and sets ST_PIVOT.  G and X may be LDS or global (ldg,
 // ldx) and may alias.  red: >= KMAX + 2 doubles of LDS scratch.
 __device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
-  __shared__ double rb[2][2][KMAX];
+  // rb[buf][0 / 1]: T / L of pivot row p, [2 / 3]: T / L of row p + 1 (both as
+  // of before pivots p and p + 1); TWO pivots per barrier: every thread forms
+  // row p + 1 after pivot p itself (its own column) and the pivot-(p + 1)
+  // multiplier numerators from the two published rows (symmetry)
+  __shared__ double rb[2][4][KMAX];
   const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
   constexpr int RU = KMAX / (NT / 64);
   double T[RU], L[RU];
@@ -92,40 +96,75 @@ __device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, in
     if (c == 0) red[0] = v;
     rb[0][0][c] = T[0];
     rb[0][1][c] = L[0];
+  } else if (g == 1) {
+    rb[0][2][c] = T[0];
+    rb[0][3][c] = L[0];
   }
   __syncthreads();
   const double thr = 1e-13 * red[0];
-  for (int j = 0; j < k; ++j) {
-    const int buf = j & 1;
-    const double d = rb[buf][0][j];
-    const double tj = rb[buf][0][c], lj = rb[buf][1][c];
-    double num[RU];
+  for (int j = 0; j < k; j += 2) {
+    const int buf = (j >> 1) & 1;
+    const bool two = j + 1 < k;
+    const double* R0 = rb[buf][0];
+    const double* R1 = rb[buf][2];
+    const double d0 = R0[j];
+    const double tj = R0[c], lj = rb[buf][1][c];
+    const bool ok0 = d0 > thr && d0 == d0;
+    const double r0 = ok0 ? rcp64(d0) : 0.0;
+    // row j + 1 after pivot j, column c; its pivot d1
+    double f10 = 0.0, t1c = 0.0, l1c = 0.0, d1 = 0.0, r1 = 0.0;
+    bool ok1 = true;
+    if (two) {
+      f10 = R1[j] * r0;
+      t1c = fma(-f10, tj, R1[c]);
+      l1c = fma(-f10, lj, rb[buf][3][c]);
+      d1 = fma(-f10, R0[j + 1], R1[j + 1]);
+      ok1 = d1 > thr && d1 == d1;
+      r1 = ok1 ? rcp64(d1) : 0.0;
+    }
+    double n0[RU], n1[RU];
 #pragma unroll
-    for (int u = 0; u < RU; ++u) num[u] = rb[buf][0][(g + 8 * u) & (KMAX - 1)];
-    const bool ok = d > thr && d == d;
-    const double rd = ok ? rcp64(d) : 0.0;
+    for (int u = 0; u < RU; ++u) {
+      const int i = (g + 8 * u) & (KMAX - 1);
+      n0[u] = R0[i];
+      n1[u] = R1[i];
+    }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int i = g + 8 * u;
       if (i > j && i < k) {
-        const double f = num[u] * rd;
-        T[u] = fma(-f, tj, T[u]);
-        L[u] = fma(-f, lj, L[u]);
+        const double f0 = n0[u] * r0;
+        T[u] = fma(-f0, tj, T[u]);
+        L[u] = fma(-f0, lj, L[u]);
+        if (i > j + 1) {
+          const double f1 = fma(-f10, n0[u], n1[u]) * r1;
+          T[u] = fma(-f1, t1c, T[u]);
+          L[u] = fma(-f1, l1c, L[u]);
+        }
       }
     }
-    // publish pivot row j + 1 (final after this step's update)
-    const int j1 = j + 1;
-    if (j1 < k && g == (j1 & 7)) {
-      double t1 = 0.0, l1 = 0.0;
+    // publish rows j + 2 and j + 3 (final after both pivots)
+    const int p2 = j + 2, p3 = j + 3;
+    if (p2 < k && g == (p2 & 7)) {
+      double t = 0.0, l = 0.0;
 #pragma unroll
       for (int u = 0; u < RU; ++u)
-        if (u == (j1 >> 3)) { t1 = T[u]; l1 = L[u]; }
-      rb[buf ^ 1][0][c] = t1;
-      rb[buf ^ 1][1][c] = l1;
+        if (u == (p2 >> 3)) { t = T[u]; l = L[u]; }
+      rb[buf ^ 1][0][c] = t;
+      rb[buf ^ 1][1][c] = l;
+    }
+    if (p3 < k && g == (p3 & 7)) {
+      double t = 0.0, l = 0.0;
+#pragma unroll
+      for (int u = 0; u < RU; ++u)
+        if (u == (p3 >> 3)) { t = T[u]; l = L[u]; }
+      rb[buf ^ 1][2][c] = t;
+      rb[buf ^ 1][3][c] = l;
     }
     if (tid == 0) {
-      red[2 + j] = ok ? rsq64(d) : 0.0;
-      if (!ok) *st |= ST_PIVOT;
+      red[2 + j] = ok0 ? rsq64(d0) : 0.0;
+      if (two) red[3 + j] = ok1 ? rsq64(d1) : 0.0;
+      if (!ok0 || !ok1) *st |= ST_PIVOT;
     }
     __syncthreads();
   }
@@ -137,7 +176,6 @@ __device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, in
   }
   __syncthreads();
 }
-
 
 // C = A^T B (transa) or A B for k x k LDS matrices (row stride ld) on f64
 // MFMA: 16 x 16 output tiles over the 8 waves, K in steps of 4

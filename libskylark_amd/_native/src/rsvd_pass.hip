@@ -434,13 +434,10 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 // 128 consecutive elements per 512-thread workgroup (two per lane); wave v
 // sums slabs v, v + 8, ... with four loads in flight; 8 partials through LDS.
 template <typename IT, typename OT>
-__global__ void __launch_bounds__(512)
-k_rsvd_reduce(const IT* __restrict__ slab, int nslab, int64_t total, int cols, OT* __restrict__ out, int ldo,
-              int* __restrict__ zero_word) {
-  __shared__ double part[8][128];
-  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+__device__ __forceinline__ void reduce_body(const IT* __restrict__ slab, int nslab, int64_t total, int cols,
+                                            OT* __restrict__ out, int ldo, int blk, double (*part)[128]) {
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
-  const int64_t e0 = (int64_t)blockIdx.x * 128 + 2 * lane;
+  const int64_t e0 = (int64_t)blk * 128 + 2 * lane;
   double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
   if (e0 + 1 < total) {
     int s = v;
@@ -461,7 +458,7 @@ k_rsvd_reduce(const IT* __restrict__ slab, int nslab, int64_t total, int cols, O
   part[v][2 * lane + 1] = a1 + b1;
   __syncthreads();
   if (threadIdx.x < 128) {
-    const int64_t e = (int64_t)blockIdx.x * 128 + threadIdx.x;
+    const int64_t e = (int64_t)blk * 128 + threadIdx.x;
     if (e < total) {
       double sum = 0;
 #pragma unroll
@@ -470,6 +467,27 @@ k_rsvd_reduce(const IT* __restrict__ slab, int nslab, int64_t total, int cols, O
       out[i * ldo + j] = (OT)sum;
     }
   }
+}
+
+template <typename IT, typename OT>
+__global__ void __launch_bounds__(512)
+k_rsvd_reduce(const IT* __restrict__ slab, int nslab, int64_t total, int cols, OT* __restrict__ out, int ldo,
+              int* __restrict__ zero_word) {
+  __shared__ double part[8][128];
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  reduce_body<IT, OT>(slab, nslab, total, cols, out, ldo, blockIdx.x, part);
+}
+
+// the final pass's two sums in ONE launch: blocks [0, gw) the f32 W slabs
+// into f64, the rest the fp64 Gram slabs
+__global__ void __launch_bounds__(512)
+k_rsvd_reduce_wg(const float* __restrict__ wslab, int64_t tw, int cols, double* __restrict__ wout, int ldw,
+                 const double* __restrict__ gslab, int64_t tg, double* __restrict__ gout, int ldg, int nslab, int gw,
+                 int* __restrict__ zero_word) {
+  __shared__ double part[8][128];
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  if ((int)blockIdx.x < gw) reduce_body<float, double>(wslab, nslab, tw, cols, wout, ldw, blockIdx.x, part);
+  else reduce_body<double, double>(gslab, nslab, tg, cols, gout, ldg, blockIdx.x - gw, part);
 }
 
 int cu_count() {
@@ -575,6 +593,15 @@ SL_API int sl_rsvd_reduce_z(const void* ws, int64_t m, int64_t n, int k, void* W
   const char* base = (const char*)ws;
   const int64_t tw = n * k;
   const unsigned gw = (unsigned)((tw + 127) / 128);
+  if (Gout && w_f64) {
+    const int64_t off = ((int64_t)grid * n * k * 4 + 255) & ~(int64_t)255;
+    const int64_t tg = (int64_t)k * k;
+    const unsigned gg = (unsigned)((tg + 127) / 128);
+    k_rsvd_reduce_wg<<<gw + gg, 512, 0, s>>>((const float*)base, tw, k, (double*)Wout, ldw,
+                                              (const double*)(base + off), tg, Gout, ldg, grid, (int)gw, zero_word);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  }
   if (w_f64)
     k_rsvd_reduce<float, double><<<gw, 512, 0, s>>>((const float*)base, grid, tw, k, (double*)Wout, ldw, zero_word);
   else
