@@ -25,7 +25,7 @@
 
 #include "sl_common.hpp"
 
-// kernels of rsvd_pass.hip / rsvd_core.hip / svd_core.hip / native_comm.cpp
+// kernels of rsvd_pass.hip / rsvd_core.hip / tsk_f32_kernels.hip / native_comm.cpp
 SL_API int sl_rsvd_pass_grid(int64_t m);
 SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k);
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws, float* Y,
@@ -56,7 +56,6 @@ namespace {
 struct Plan {
   int64_t m = 0, n = 0, lda = 0;
   int k = 0, r = 0, q = 0;
-  int variant = 0;
   // device buffers (one allocation, carved)
   char* base = nullptr;
   void* pass_ws = nullptr;
@@ -101,7 +100,7 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
     if (rc != SL_OK) return rc;
   }
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
-                    final_pass ? 1 : 0, p->variant, s);
+                    final_pass ? 1 : 0, 0, s);
   if (rc != SL_OK) return rc;
   // the first reduce of the call also clears the status word (no memset node)
   return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
@@ -206,14 +205,6 @@ SL_API int sl_rsvd_plan_set_warm(void* plan, int warm) {
   Plan* p = (Plan*)plan;
   if (p->warm != (warm != 0)) drop_graph(p);
   p->warm = warm != 0;
-  return SL_OK;
-}
-
-// pass-kernel tuning variant (3: 3-deep DMA ring instead of 4)
-SL_API int sl_rsvd_plan_set_variant(void* plan, int variant) {
-  Plan* p = (Plan*)plan;
-  if (p->variant != variant) drop_graph(p);
-  p->variant = variant;
   return SL_OK;
 }
 

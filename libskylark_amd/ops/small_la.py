@@ -110,46 +110,3 @@ def cholqr2(W: torch.Tensor, status: torch.Tensor | None = None, want_r: bool = 
     if want_r:
         return Q, small_matmul(R2, R1)
     return Q
-
-
-_lib.register("sl_svd_core", [vp, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp])
-_lib.register("sl_svd_finish", [vp, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp, vp])
-
-
-def svd_core(W: torch.Tensor, Rti: torch.Tensor, status: torch.Tensor | None = None):
-    """``(Vt, host_src)``: ``Vt = W Rti`` (n x k f64, Rti upper triangular) and
-    ``host_src = [C.flatten(), status]`` with ``C = Vt^T Vt`` (exactly
-    symmetric).  GPU: svd_core.hip (2 launches); CPU: torch."""
-    n, k = W.shape
-    if not W.is_cuda:
-        Vt = W.double() @ Rti.double()
-        Cm = Vt.t() @ Vt
-        Cm = 0.5 * (Cm + Cm.t())
-        st = status.double() if status is not None else torch.zeros(1, dtype=torch.float64)
-        return Vt, torch.cat([Cm.reshape(-1), st.reshape(-1).cpu()])
-    W = W.to(torch.float64)
-    if W.stride(1) != 1:
-        W = W.contiguous()
-    Rti = Rti.to(torch.float64).contiguous()
-    Vt = torch.empty(n, k, dtype=torch.float64, device=W.device)
-    slabs = torch.empty(-(-n // 16) * k * k, dtype=torch.float64, device=W.device)
-    host_src = torch.empty(k * k + 1, dtype=torch.float64, device=W.device)
-    _lib.call("sl_svd_core", _lib.ptr(W), n, k, W.stride(0), _lib.ptr(Rti), _lib.ptr(Vt), _lib.ptr(slabs),
-              _lib.ptr(host_src), _lib.ptr(status) if status is not None else None, vp(_lib.stream_of(W)))
-    return Vt, host_src
-
-
-def svd_finish(Vt: torch.Tensor, Rti: torch.Tensor, small: torch.Tensor, r: int):
-    """``(V, M, s)`` in f32 from ``small = [Ub (k x r row-major) | s (r)]``:
-    ``V = Vt Ub diag(1/s)``, ``M = Rti Ub``."""
-    n, k = Vt.shape
-    Ub = small[:k * r].view(k, r)
-    s64 = small[k * r:k * r + r]
-    if not Vt.is_cuda:
-        return ((Vt @ Ub) / s64.clamp_min(1e-300)).float(), (Rti @ Ub).float(), s64.float()
-    V = torch.empty(n, r, dtype=torch.float32, device=Vt.device)
-    M = torch.empty(k, r, dtype=torch.float32, device=Vt.device)
-    s32 = torch.empty(r, dtype=torch.float32, device=Vt.device)
-    _lib.call("sl_svd_finish", _lib.ptr(Vt), n, k, _lib.ptr(Rti), _lib.ptr(small), r, _lib.ptr(V), _lib.ptr(M),
-              _lib.ptr(s32), vp(_lib.stream_of(Vt)))
-    return V, M, s32

@@ -100,33 +100,6 @@ def test_sym_eig_converges_in_few_sweeps(dev):
     assert 2 <= int(sweeps.item()) <= 12
 
 
-@pytest.mark.gpu
-def test_svd_core_and_finish_gpu(dev):
-    """svd_core.hip vs torch fp64: Vt = W Rti, C = Vt^T Vt (exactly symmetric),
-    status staged last; V = Vt Ub / s, M = Rti Ub."""
-    from libskylark_amd.ops import small_la as SL
-    n, k, r = 1000, 40, 20
-    g = torch.Generator().manual_seed(3)
-    W = torch.randn(n + k, k, dtype=torch.float64, generator=g)[:n]
-    Rti = torch.triu(torch.randn(k, k, dtype=torch.float64, generator=g)) + 3 * torch.eye(k, dtype=torch.float64)
-    status = torch.tensor([1], dtype=torch.int32, device=dev)
-    Vt, hs = SL.svd_core(W.to(dev), Rti.to(dev), status)
-    Vref = W @ Rti
-    Cref = Vref.t() @ Vref
-    torch.testing.assert_close(Vt.cpu(), Vref, rtol=1e-12, atol=1e-12)
-    C = hs[:k * k].view(k, k).cpu()
-    assert torch.equal(C, C.t())
-    torch.testing.assert_close(C, Cref, rtol=1e-12, atol=1e-9)
-    assert float(hs[-1]) == 1.0
-    small = torch.cat([torch.randn(k * r, dtype=torch.float64, generator=g),
-                       torch.rand(r, dtype=torch.float64, generator=g) + 0.5])
-    V, M, s = SL.svd_finish(Vt, Rti.to(dev), small.to(dev), r)
-    Ub, sv = small[:k * r].view(k, r), small[k * r:]
-    torch.testing.assert_close(V.cpu().double(), (Vref @ Ub) / sv, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(M.cpu().double(), Rti @ Ub, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(s.cpu().double(), sv, rtol=1e-6, atol=0)
-
-
 def _eig_check(C, out, k, r):
     V, lam = out[:k * r].view(k, r), out[k * r:]
     ref = torch.sort(torch.linalg.eigvalsh(C), descending=True).values[:r]
