@@ -68,3 +68,20 @@ def test_csr_sketch_shard_offset():
                              panel_elems=S * 64)
     ref = A @ _explicit(S, N, 3, 10, 1.0)[:, k0:k0 + k].t()
     torch.testing.assert_close(Y.cpu(), ref, rtol=0, atol=1e-12 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("dtype,idx", [(torch.float32, torch.int32), (torch.float64, torch.int64)])
+def test_csr_transpose_native_exact(dtype, idx):
+    """csr_transpose.hip: A^T as CSR with ascending row indices per column,
+    bit-identical to the dense transpose (empty rows and columns, a long row)."""
+    A, _ = _csr(700, 450, 0.02, dtype, 12, empty_rows=(3, 699))
+    A[:, 17] = 0
+    A[5, :] = torch.randn(450, dtype=torch.float64).to(dtype).double()
+    Ad = A.to(dtype).to_sparse_csr()
+    Ad = torch.sparse_csr_tensor(Ad.crow_indices().to(idx), Ad.col_indices().to(idx), Ad.values(), Ad.shape).cuda()
+    T = DS._csr_transpose(Ad)
+    assert T.shape == (450, 700)
+    ref = A.to(dtype).t().contiguous().to_sparse_csr()
+    assert torch.equal(T.crow_indices().long().cpu(), ref.crow_indices().long())
+    assert torch.equal(T.col_indices().long().cpu(), ref.col_indices().long())
+    assert torch.equal(T.values().cpu(), ref.values())
