@@ -18,6 +18,8 @@ from __future__ import annotations
 
 import torch
 
+from ..ops.spmm import csr_transpose as _csr_transpose
+
 from ..ops import krylov_native as _kn
 from ..parallel.comm import Comm
 from ..parallel.distmatrix import DistMatrix
@@ -147,7 +149,7 @@ class SparseOp(Operator):
         # the CSR of A^T is built once per operator (deterministic sums; an
         # atomic scatter A^T Y would not be)
         if self._At is None:
-            self._At = self.A.to_sparse_coo().t().coalesce().to_sparse_csr()
+            self._At = _csr_transpose(self.A)
         from ..ops import spmm
         if Y.dim() == 2 and spmm.ok(self._At, Y):
             return spmm.csr_mm(self._At, Y)

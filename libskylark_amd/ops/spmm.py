@@ -14,6 +14,8 @@ from . import _lib
 
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_csr_spmm", [vp, vp, i32, vp, i32, i64, vp, i64, i32, vp, i64, i32, vp])
+_lib.register("sl_csr_transpose_workspace", [i64, i64], i64)
+_lib.register("sl_csr_transpose", [vp, vp, i32, vp, i32, i64, i64, i64, vp, vp, vp, vp, i64, vp])
 
 
 def _group_for(avg: float) -> int:
@@ -53,3 +55,33 @@ def csr_mm(A: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     _lib.call("sl_csr_spmm", _lib.ptr(rp), _lib.ptr(ci), idx32, _lib.ptr(vals.contiguous()), _lib.dtype_code(vdt), m,
               _lib.ptr(Xc), Xc.stride(0), k, _lib.ptr(Y), Y.stride(0), _group_for(avg), vp(_lib.stream_of(X)))
     return Y
+
+
+def csr_transpose(A: torch.Tensor) -> torch.Tensor:
+    """CSR of A^T (sorted column indices), on A's device: ``csr_transpose.hip``
+    (one stable radix sort of (column, position) over the column bits, a
+    gather, binary-searched column pointers) on the GPU, torch's COO coalesce
+    elsewhere."""
+    nnz = A.values().numel()
+    if (A.is_cuda and _lib.available() and nnz < (1 << 31) and max(A.shape) < (1 << 31)
+            and A.values().dtype in (torch.float32, torch.float64)):
+        import ctypes as C
+        rp = A.crow_indices().to(torch.int64)
+        ci = A.col_indices()
+        if ci.dtype not in (torch.int32, torch.int64):
+            ci = ci.to(torch.int64)
+        vals = A.values().contiguous()
+        m, n = A.shape
+        ws_bytes = int(_lib.require().sl_csr_transpose_workspace(nnz, n))
+        if ws_bytes > 0:
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=A.device)
+            colptr = torch.empty(n + 1, dtype=torch.int64, device=A.device)
+            orow = torch.empty(nnz, dtype=torch.int32, device=A.device)
+            oval = torch.empty(nnz, dtype=vals.dtype, device=A.device)
+            _lib.call("sl_csr_transpose", _lib.ptr(rp), _lib.ptr(ci), 1 if ci.dtype == torch.int32 else 0,
+                      _lib.ptr(vals), _lib.dtype_code(vals.dtype), m, n, nnz, _lib.ptr(colptr), _lib.ptr(orow),
+                      _lib.ptr(oval), _lib.ptr(ws), ws_bytes, C.c_void_p(_lib.stream_of(vals)))
+            return torch.sparse_csr_tensor(colptr.to(torch.int32), orow, oval, (n, m))
+    coo = A.to_sparse_coo()
+    idx = coo.indices()
+    return torch.sparse_coo_tensor(idx.flip(0), coo.values(), (A.shape[1], A.shape[0])).coalesce().to_sparse_csr()

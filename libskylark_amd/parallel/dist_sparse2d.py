@@ -24,6 +24,8 @@ from __future__ import annotations
 
 import torch
 
+from ..ops.spmm import csr_transpose as _csr_transpose
+
 from .comm import Comm
 from .distmatrix import Grid, _cyclic_blocks
 
@@ -170,7 +172,7 @@ class DistSparse2D:
     # ------------------------------------------------------------ sketches
     def _transposed(self):
         if self._At is None:
-            self._At = self.local.to_sparse_coo().t().coalesce().to_sparse_csr()
+            self._At = _csr_transpose(self.local)
         return self._At
 
     def sketch(self, sk, dim: int = COLUMNWISE) -> torch.Tensor:
