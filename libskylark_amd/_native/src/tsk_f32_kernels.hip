@@ -236,11 +236,19 @@ k_gram64_pipe(const float* __restrict__ Y, int64_t m, int k, double* __restrict_
   const int64_t step = (int64_t)gridDim.x * WPB * 32;
   int64_t r0 = ((int64_t)blockIdx.x * WPB + w) * 32;
   float4 nx[NLMAX];
+  // unconditional loads (rows past m read row 0, zeroed after the load): a
+  // per-element "load or zero" branch makes hipcc wait vmcnt(0) inside the
+  // loop, which serialised the prefetch of the next chunk with this chunk's
+  // MFMAs
   auto load = [&](int64_t rb) {
 #pragma unroll
-    for (int j = 0; j < NLMAX; ++j)
-      if (j < nl)
-        nx[j] = (rb + lrow[j] < m) ? *(const float4*)(Y + rb * k + 4 * (64 * j + lane)) : float4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NLMAX; ++j) {
+      // every slot loads (slots past k / 8 read Y[0..3]: no branch, so no
+      // conservative vmcnt(0) at the join points)
+      const bool in = j < nl && rb + lrow[j] < m;
+      const float4 v = *(const float4*)(Y + (in ? rb * k + 4 * (64 * j + lane) : 0));
+      nx[j] = in ? v : float4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   if (r0 < m) load(r0);
   for (; r0 < m; r0 += step) {
@@ -310,6 +318,12 @@ k_xm_pipe(const float* __restrict__ Y, int64_t m, int k, const float* __restrict
       const int r = 2 * s + h, col = 32 * ct + c;
       mreg[s][ct] = (r < k && col < k2) ? M[r * k2 + col] : 0.f;
     }
+  // consume M here so hipcc's wait for its loads sits before the loop (else
+  // the loop's first MFMA carries a vmcnt(0) that also drains the prefetch)
+#pragma unroll
+  for (int s = 0; s < KMAX / 2; ++s)
+#pragma unroll
+    for (int ct = 0; ct < KT2; ++ct) asm volatile("" ::"v"(mreg[s][ct]));
   constexpr int NLMAX = KMAX / 8;
   const int nl = k >> 3;
   int loff[NLMAX], lrow[NLMAX];
@@ -322,11 +336,19 @@ k_xm_pipe(const float* __restrict__ Y, int64_t m, int k, const float* __restrict
   const int64_t step = (int64_t)gridDim.x * WPB * 32;
   int64_t r0 = ((int64_t)blockIdx.x * WPB + w) * 32;
   float4 nx[NLMAX];
+  // unconditional loads (rows past m read row 0, zeroed after the load): a
+  // per-element "load or zero" branch makes hipcc wait vmcnt(0) inside the
+  // loop, which serialised the prefetch of the next chunk with this chunk's
+  // MFMAs
   auto load = [&](int64_t rb) {
 #pragma unroll
-    for (int j = 0; j < NLMAX; ++j)
-      if (j < nl)
-        nx[j] = (rb + lrow[j] < m) ? *(const float4*)(Y + rb * k + 4 * (64 * j + lane)) : float4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NLMAX; ++j) {
+      // every slot loads (slots past k / 8 read Y[0..3]: no branch, so no
+      // conservative vmcnt(0) at the join points)
+      const bool in = j < nl && rb + lrow[j] < m;
+      const float4 v = *(const float4*)(Y + (in ? rb * k + 4 * (64 * j + lane) : 0));
+      nx[j] = in ? v : float4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   if (r0 < m) load(r0);
   for (; r0 < m; r0 += step) {
