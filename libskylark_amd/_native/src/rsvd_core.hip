@@ -664,14 +664,37 @@ __device__ __forceinline__ void rows_times_small(const double* __restrict__ W, i
   __shared__ double Bs[KMAX][KMAX];
   const int t = threadIdx.x, row = t & 31, cg = t >> 5;
   const int i0 = blockIdx.x * 32;
-  for (int e = t; e < k * nc; e += 256) {
-    const int l = e / nc;
-    Bs[l][e - l * nc] = B[e];
-  }
   const int nr = min(32, n - i0);
-  for (int e = t; e < nr * k; e += 256) {
+  // every staging load of the thread issued before the first LDS store, from
+  // clamped addresses (a rolled load -> store loop waits on one load at a time)
+  constexpr int UB = KMAX * KMAX / 256, UW = 32 * KMAX / 256;
+  double vb[UB], vw[UW];
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    const int e = t + 256 * u;
+    vb[u] = B[e < k * nc ? e : 0];
+  }
+#pragma unroll
+  for (int u = 0; u < UW; ++u) {
+    const int e = t + 256 * u;
     const int rr = e / k;
-    Ws[rr][e - rr * k] = W[(int64_t)(i0 + rr) * ldw + (e - rr * k)];
+    vw[u] = W[e < nr * k ? (int64_t)(i0 + rr) * ldw + (e - rr * k) : (int64_t)i0 * ldw];
+  }
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    const int e = t + 256 * u;
+    if (e < k * nc) {
+      const int l = e / nc;
+      Bs[l][e - l * nc] = vb[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UW; ++u) {
+    const int e = t + 256 * u;
+    if (e < nr * k) {
+      const int rr = e / k;
+      Ws[rr][e - rr * k] = vw[u];
+    }
   }
   __syncthreads();
   if (row >= nr) return;
