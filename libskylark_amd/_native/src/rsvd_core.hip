@@ -723,7 +723,12 @@ k_make_zt(const double* __restrict__ W, int n, int k, int ldw, const double* __r
 // V (n x r f32) = W (n x k f64) N (k x r f64); s32 = s64 (r)
 __global__ void __launch_bounds__(256)
 k_make_v(const double* __restrict__ W, int n, int k, int ldw, const double* __restrict__ N, int r, float* __restrict__ V,
-         const double* __restrict__ s64, float* __restrict__ s32) {
+         const double* __restrict__ s64, float* __restrict__ s32, float* const* __restrict__ optr) {
+  // optr: {U, s, V} read at run time (the graph-captured finish)
+  if (optr) {
+    s32 = optr[1];
+    V = optr[2];
+  }
   if (s32 && blockIdx.x == 0 && threadIdx.x < r) s32[threadIdx.x] = (float)s64[threadIdx.x];
   rows_times_small(W, n, k, ldw, N, r, [&](int i, int c, double v) { V[(int64_t)i * r + c] = (float)v; });
 }
@@ -835,7 +840,33 @@ SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream) {
   if (k < 1 || k > KMAX || r > k) { sl_set_last_error("rsvd_make_v: 1 <= r <= k <= 64"); return SL_ERR_UNSUPPORTED; }
-  k_make_v<<<(unsigned)((n + 31) / 32), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, N, r, V, s64, s32);
+  k_make_v<<<(unsigned)((n + 31) / 32), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, N, r, V, s64, s32, nullptr);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// V and s from optr[2] / optr[1] at run time (a graph node replayed into a
+// new caller buffer each call; sl_rsvd_set_ptrs writes the table)
+SL_API int sl_rsvd_make_v_ind(const double* W, int n, int k, int ldw, const double* N, int r, const double* s64,
+                              float* const* optr, void* stream) {
+  if (k < 1 || k > KMAX || r > k) { sl_set_last_error("rsvd_make_v: 1 <= r <= k <= 64"); return SL_ERR_UNSUPPORTED; }
+  k_make_v<<<(unsigned)((n + 31) / 32), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, N, r, nullptr, s64, nullptr,
+                                                                       optr);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+namespace {
+__global__ void k_set_ptrs(float** tab, float* a, float* b, float* c) {
+  if (threadIdx.x == 0) tab[0] = a;
+  if (threadIdx.x == 1) tab[1] = b;
+  if (threadIdx.x == 2) tab[2] = c;
+}
+}  // namespace
+
+// tab[0..2] = {a, b, c} in stream order (one vector-store kernel)
+SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* stream) {
+  k_set_ptrs<<<1, 64, 0, (hipStream_t)stream>>>(tab, a, b, c);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

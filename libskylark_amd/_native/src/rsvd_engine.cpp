@@ -11,10 +11,11 @@
 //                Jacobi, M = Rt^{-1} Ub_r, N = M S^{-1}, s
 // then the finish (U = Y M, V = W N, s) into the caller's buffers.
 //
-// Single rank: the segments are captured ONCE as a hipGraph (per A pointer)
-// and replayed; the sketch operator and the finish are plain launches
-// (kernel arguments carry the per-call sketch counters, the outputs are the
-// caller's fresh buffers).  Several ranks: after every reducing segment the
+// Single rank: the segments and the finish are captured ONCE as a hipGraph
+// (per A pointer) and replayed; the sketch operator is a plain launch (its
+// arguments carry the per-call sketch counters) and the finish writes the
+// caller's fresh U / s / V through a device pointer table that one tiny
+// kernel fills in front of the replay.  Several ranks: after every reducing segment the
 // [W; G] buffer is summed over the ranks, either by the caller (Python:
 // torch.distributed / one-shot IPC between sl_rsvd_segment calls) or, from
 // C, by a NativeComm RCCL communicator (sl_rsvd_run_comm) -- no interpreter.
@@ -40,6 +41,11 @@ SL_API int sl_rsvd_final_la2(const double* W, int n, int k, int ldw, const doubl
                              int* mirror, void* stream);
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream);
+SL_API int sl_rsvd_make_v_ind(const double* W, int n, int k, int ldw, const double* N, int r, const double* s64,
+                              float* const* optr, void* stream);
+SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* stream);
+SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, int k2, float* const* optr,
+                             void* stream);
 SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
                            void* stream);
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
@@ -69,13 +75,15 @@ struct Plan {
   double* s64 = nullptr;    // r
   double* V0 = nullptr;     // kp x kp: the last core eigenvectors (Jacobi warm start)
   int* v0_valid = nullptr;
+  float** optr = nullptr;   // {U, s, V} of the current call (the graph's finish reads them)
   bool warm = true;
   int* status = nullptr;
   int* mirror_host = nullptr;   // host-mapped copy of the status word, written by the final kernel
   int* mirror_dev = nullptr;
-  // graph of the segments (single rank), valid for graph_A
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  // graphs of the segments (single rank), valid for graph_A: [0] segments
+  // only, [1] segments + the finish writing through optr
+  hipGraph_t graph[2] = {nullptr, nullptr};
+  hipGraphExec_t exec[2] = {nullptr, nullptr};
   const void* graph_A = nullptr;
   hipStream_t cap_stream = nullptr;   // capture happens here (never the legacy null stream)
   hipEvent_t cap_ev = nullptr;
@@ -108,11 +116,56 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
 }
 
 void drop_graph(Plan* p) {
-  if (p->exec) (void)hipGraphExecDestroy(p->exec);
-  if (p->graph) (void)hipGraphDestroy(p->graph);
-  p->exec = nullptr;
-  p->graph = nullptr;
+  for (int v = 0; v < 2; ++v) {
+    if (p->exec[v]) (void)hipGraphExecDestroy(p->exec[v]);
+    if (p->graph[v]) (void)hipGraphDestroy(p->graph[v]);
+    p->exec[v] = nullptr;
+    p->graph[v] = nullptr;
+  }
   p->graph_A = nullptr;
+}
+
+// the finish through the pointer table (inside the graph: no graph -> stream
+// gap before it, no per-call launches)
+int finish_ind(Plan* p, hipStream_t s) {
+  int rc = sl_rsvd_make_v_ind(p->WG, (int)p->n, p->k, p->k, p->N, p->r, p->s64, p->optr, s);
+  if (rc != SL_OK) return rc;
+  return sl_tsk_f32_xm_ind(p->Y, p->m, p->k, p->M, p->r, p->optr, s);
+}
+
+// capture every segment (+ the indirect finish) once on the plan's own stream
+int capture(Plan* p, const void* A, int with_finish, hipStream_t st) {
+  if (!p->cap_stream) {
+    SL_HIP_CHECK(hipStreamCreateWithFlags(&p->cap_stream, hipStreamNonBlocking));
+    SL_HIP_CHECK(hipEventCreateWithFlags(&p->cap_ev, hipEventDisableTiming));
+  }
+  // the capture stream starts after everything queued on the caller's
+  // stream (nothing is enqueued on it while it captures)
+  SL_HIP_CHECK(hipEventRecord(p->cap_ev, st));
+  SL_HIP_CHECK(hipStreamWaitEvent(p->cap_stream, p->cap_ev, 0));
+  SL_HIP_CHECK(hipStreamSynchronize(p->cap_stream));
+  hipStream_t cst = p->cap_stream;
+  SL_HIP_CHECK(hipStreamBeginCapture(cst, hipStreamCaptureModeThreadLocal));
+  int rc = SL_OK;
+  for (int i = 0; i <= p->q + 1 && rc == SL_OK; ++i) rc = seg(p, A, i, cst);
+  if (rc == SL_OK && with_finish) rc = finish_ind(p, cst);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(cst, &g);
+  if (rc != SL_OK || e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    if (rc == SL_OK) { sl_set_last_error(hipGetErrorString(e)); rc = SL_ERR_HIP; }
+    return rc;
+  }
+  hipGraphExec_t ex = nullptr;
+  if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    sl_set_last_error("rsvd_run: graph instantiate failed");
+    return SL_ERR_HIP;
+  }
+  p->graph[with_finish] = g;
+  p->exec[with_finish] = ex;
+  p->graph_A = A;
+  return SL_OK;
 }
 
 }  // namespace
@@ -141,6 +194,7 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   const int64_t o_st = off;   off = align256(off + 16);
   const int kp = k + (k & 1);
   const int64_t o_v0 = off;   off = align256(off + (int64_t)kp * kp * 8 + 16);
+  const int64_t o_op = off;   off = align256(off + 4 * (int64_t)sizeof(float*));
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;
     sl_set_last_error("rsvd_plan: device allocation failed");
@@ -158,6 +212,7 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   p->status = (int*)(p->base + o_st);
   p->V0 = (double*)(p->base + o_v0);
   p->v0_valid = (int*)(p->base + o_v0 + (int64_t)kp * kp * 8);
+  p->optr = (float**)(p->base + o_op);
   if (hipMemset(p->gram_ws, 0, (size_t)sl_rsvd_gram_workspace(k)) != hipSuccess ||
       hipMemset(p->status, 0, 16) != hipSuccess || hipMemset(p->v0_valid, 0, 16) != hipSuccess) {
     (void)hipFree(p->base);
@@ -259,46 +314,28 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
                        void* stream) {
   Plan* p = (Plan*)plan;
   hipStream_t st = (hipStream_t)stream;
-  if (use_graph) {
-    if (p->exec && p->graph_A != A) drop_graph(p);
-    if (!p->exec) {
-      if (!p->cap_stream) {
-        SL_HIP_CHECK(hipStreamCreateWithFlags(&p->cap_stream, hipStreamNonBlocking));
-        SL_HIP_CHECK(hipEventCreateWithFlags(&p->cap_ev, hipEventDisableTiming));
-      }
-      // the capture stream starts after everything queued on the caller's
-      // stream (nothing is enqueued on it while it captures)
-      SL_HIP_CHECK(hipEventRecord(p->cap_ev, st));
-      SL_HIP_CHECK(hipStreamWaitEvent(p->cap_stream, p->cap_ev, 0));
-      SL_HIP_CHECK(hipStreamSynchronize(p->cap_stream));
-      hipStream_t cst = p->cap_stream;
-      SL_HIP_CHECK(hipStreamBeginCapture(cst, hipStreamCaptureModeThreadLocal));
-      int rc = SL_OK;
-      for (int i = 0; i <= p->q + 1 && rc == SL_OK; ++i) rc = seg(p, A, i, cst);
-      hipGraph_t g = nullptr;
-      const hipError_t e = hipStreamEndCapture(cst, &g);
-      if (rc != SL_OK || e != hipSuccess) {
-        if (g) (void)hipGraphDestroy(g);
-        if (rc == SL_OK) { sl_set_last_error(hipGetErrorString(e)); rc = SL_ERR_HIP; }
-        return rc;
-      }
-      hipGraphExec_t ex = nullptr;
-      if (hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
-        (void)hipGraphDestroy(g);
-        sl_set_last_error("rsvd_run: graph instantiate failed");
-        return SL_ERR_HIP;
-      }
-      p->graph = g;
-      p->exec = ex;
-      p->graph_A = A;
-    }
-    SL_HIP_CHECK(hipGraphLaunch(p->exec, st));
-  } else {
+  if (!use_graph) {
     for (int i = 0; i <= p->q + 1; ++i) {
       const int rc = seg(p, A, i, st);
       if (rc != SL_OK) return rc;
     }
+    return sl_rsvd_finish(plan, U, ldu, s, V, stream);
   }
+  if (p->graph_A != A) drop_graph(p);
+  // the finish joins the graph when its streaming kernel can take this U
+  // (contiguous rows, 16-byte aligned) -- else a plain launch after it
+  const int fin = (p->k % 8 == 0 && ldu == p->r && ((uintptr_t)U & 15) == 0 && V != nullptr) ? 1 : 0;
+  if (!p->exec[fin]) {
+    const int rc = capture(p, A, fin, st);
+    if (rc != SL_OK) return rc;
+  }
+  if (fin) {
+    int rc = sl_rsvd_set_ptrs(p->optr, U, s, V, st);
+    if (rc != SL_OK) return rc;
+    SL_HIP_CHECK(hipGraphLaunch(p->exec[1], st));
+    return SL_OK;
+  }
+  SL_HIP_CHECK(hipGraphLaunch(p->exec[0], st));
   return sl_rsvd_finish(plan, U, ldu, s, V, stream);
 }
 

@@ -302,7 +302,10 @@ k_gram64_pipe(const float* __restrict__ Y, int64_t m, int k, double* __restrict_
 template <int KT2>
 __global__ void __launch_bounds__(256)
 k_xm_pipe(const float* __restrict__ Y, int64_t m, int k, const float* __restrict__ M, int k2,
-          float* __restrict__ out) {
+          float* __restrict__ out, float* const* __restrict__ optr) {
+  // optr: the output pointer read from device memory (a graph node whose
+  // destination changes every replay)
+  if (optr) out = optr[0];
   __shared__ float tin[WPB][32 * (KMAX + 1)];
   __shared__ float tout[WPB][32 * 32 * KT2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -472,6 +475,23 @@ SL_API int sl_tsk_gram64(const float* Y, int64_t m, int k, int64_t ldy, double* 
   return sl_slab_reduce_launch_d2d(slab, g, (int64_t)k * k, k, k, k, G, k, s);
 }
 
+// U = Y M with U read from optr[0] at run time (contiguous: ldy == k, k % 8
+// == 0, U rows of k2 floats, U 16-byte aligned -- the caller checks U).
+SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, int k2, float* const* optr,
+                             void* stream) {
+  if (m <= 0) return SL_OK;
+  if (k < 8 || k > KMAX || k % 8 || k2 < 1 || k2 > KMAX || ((uintptr_t)Y & 15)) {
+    sl_set_last_error("tsk_f32_xm_ind: needs 8 <= k <= 64, k % 8 == 0, 1 <= k2 <= 64, Y 16-byte aligned");
+    return SL_ERR_UNSUPPORTED;
+  }
+  int64_t gx = (m + WPB * 32 - 1) / (WPB * 32);
+  if (gx > XM_PIPE_GRID_MAX) gx = XM_PIPE_GRID_MAX;
+  if (k2 > 32) k_xm_pipe<2><<<(int)gx, 256, 0, (hipStream_t)stream>>>(Y, m, k, M, k2, nullptr, optr);
+  else k_xm_pipe<1><<<(int)gx, 256, 0, (hipStream_t)stream>>>(Y, m, k, M, k2, nullptr, optr);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2,
                          float* out, int64_t ldo, double* G, void* ws, void* stream) {
   if (m <= 0) return SL_OK;
@@ -491,8 +511,8 @@ SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const fl
       ((uintptr_t)out & 15) == 0) {
     int64_t gx = (m + WPB * 32 - 1) / (WPB * 32);
     if (gx > XM_PIPE_GRID_MAX) gx = XM_PIPE_GRID_MAX;
-    if (two) k_xm_pipe<2><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out);
-    else k_xm_pipe<1><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out);
+    if (two) k_xm_pipe<2><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out, nullptr);
+    else k_xm_pipe<1><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out, nullptr);
     SL_LAUNCH_CHECK();
     return SL_OK;
   }
