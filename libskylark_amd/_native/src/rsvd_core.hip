@@ -3,20 +3,23 @@
 // :278-317 ApproximateSVD's El::SVD of the k x k core), so the whole call runs
 // on the GPU with no host round trip.
 //
-//   k_gram_la<INTER>  between two power passes: H = W^T W of the reduced
-//                     W (n x k, f64), Cholesky H = R^T R with pivot dropping,
-//                     R^{-1}; k_make_zt then forms the next pass operand
-//                     Z^T = (W R^{-1})^T in bf16.  ("orth(W)": CholeskyQR.)
-//   k_gram_la<FINAL>  after the final pass: H = W^T W (W = A^T Y), the
-//                     Cholesky Y^T Y = Rt^T Rt of the pass's fp64 Gram, Rt^{-1},
-//                     the symmetric core C = Rt^{-T} H Rt^{-1} = Ub S^2 Ub^T,
-//                     a cyclic Jacobi eigensolve of C, and the small factors
-//                     M = Rt^{-1} Ub_r (U = Y M) and N = M S^{-1} (V = W N).
+//   k_boundary<INTER>  at each boundary between two power passes: the pass's
+//                      W slabs summed (f64), H = W^T W, Cholesky H = R^T R with
+//                      pivot dropping, R^{-1}, and the next pass operand
+//                      Z^T = (W R^{-1})^T in bf16.  ("orth(W)": CholeskyQR.)
+//   k_boundary<FINAL>  after the final pass: the same sums (+ the fp64 Gram of
+//                      Y), H = W^T W (W = A^T Y), the Cholesky Y^T Y = Rt^T Rt,
+//                      Rt^{-1}, the symmetric core C = Rt^{-T} H Rt^{-1} =
+//                      Ub S^2 Ub^T, a cyclic Jacobi eigensolve of C, the small
+//                      factors M = Rt^{-1} Ub_r (U = Y M) and N = M S^{-1}, and
+//                      V = W N.
 //
-// Structure: the n rows of W are split over NG workgroups, each forms the
-// partial Gram of its rows (f64) and publishes it with an agent-scope release
-// and a ticket counter; the LAST arriving workgroup (agent-scope acquire)
-// sums the partials and runs the k x k algebra alone in LDS (k <= 64).
+// Structure: the n rows of W are split over n / 16 workgroups; each sums its
+// rows, forms their partial Gram (f64) and publishes it with an agent-scope
+// release and a ticket counter; the LAST arriving workgroup (agent-scope
+// acquire) sums the partials and runs the k x k algebra alone in LDS (k <= 48)
+// while the others wait on a generation word, then every workgroup forms its
+// rows of Z^T / V.  One launch per boundary (see k_boundary).
 //
 // Jacobi: round-robin (circle) ordering, k/2 disjoint rotations per round,
 // ONE workgroup barrier per round (A ping-pongs between two LDS copies, every
@@ -34,10 +37,11 @@ namespace {
 constexpr int NT = 512;      // threads per workgroup of the small-LA kernels
 constexpr int KMAX = 64;
 constexpr int RED = KMAX + 16;   // doubles of small scratch (max diag, D^{-1/2})
-constexpr int CH_MAX = 64;       // rows of W per workgroup of the partial-Gram phase
+// dynamic LDS of the small-LA kernels: four k x k f64 buffers, RED doubles, int flags / order
+constexpr size_t GRAM_LA_LDS = (size_t)(4 * KMAX * (KMAX + 1) + RED) * sizeof(double) + (4 + KMAX + 1) * sizeof(int);
 
 #ifdef SL_CORE_STAMPS
-// diagnostic build only: phase times (100 MHz s_memrealtime) of k_gram_la
+// diagnostic build only: phase times (100 MHz s_memrealtime) of the final core
 __device__ unsigned long long g_core_st[32];
 #define SL_CST(I) \
   if (threadIdx.x == 0) g_core_st[(I)] = __builtin_amdgcn_s_memrealtime();
@@ -398,144 +402,23 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
   return A;
 }
 
-// ---------------------------------------------------------------- kernel
-template <bool FINAL>
-__global__ void __launch_bounds__(NT)
-k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restrict__ part,
-          unsigned* __restrict__ counter, const double* __restrict__ Gy, int r, double* __restrict__ Rinv,
-          float* __restrict__ M, double* __restrict__ N, double* __restrict__ s_out, int* __restrict__ status,
-          int max_sweeps, double* __restrict__ V0, int* __restrict__ v0_valid, int* __restrict__ mirror) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
+// ---------------------------------------------------------------- final core
+// After the final pass (H = W^T W in b0, Gy = Y^T Y in global / LDS, row stride k):
+// Y^T Y = Rt^T Rt, Rti = Rt^{-1}, C = Rti^T H Rti = Ub S^2 Ub^T (Jacobi, warm
+// started from V0), s, M = Rti Ub_r (f32) and N = M S^{-1} (f64).  Run by ONE
+// workgroup; b0..b3 are k x k LDS scratch (row stride k + 1).  status_or: OR
+// the call's status bits into *status (0: store them -- the call's first writer).
+__device__ void final_core(double* b0, double* b1, double* b2, double* b3, double* red, int* flags, int* order,
+                           const double* Gy, int k, int r, float* __restrict__ M, double* __restrict__ N,
+                           double* __restrict__ s_out, int* __restrict__ status, int max_sweeps, double* V0,
+                           int* v0_valid, int* mirror, int* st_sh_p, int status_or) {
+  int& st_sh = *st_sh_p;
   const int tid = threadIdx.x;
   const int ld = k + 1;
-  const int mat = KMAX * (KMAX + 1);
-  double* b0 = sm;
-  double* b1 = sm + mat;
-  double* b2 = sm + 2 * mat;
-  double* b3 = sm + 3 * mat;
-  double* red = sm + 4 * mat;           // small scratch (RED doubles)
-  int* iscr = (int*)(red + RED);        // flags[4], order[KMAX], is_last
-  int* flags = iscr;
-  int* order = iscr + 4;
-  int* is_last = iscr + 4 + KMAX;
-  __shared__ int st_sh;
-  constexpr int SO = FINAL ? 16 : 0;
-  if (blockIdx.x == 0) { SL_CST(SO + 0) }
-
-  // ---- partial Gram of this workgroup's rows (upper triangle, f64).
-  //      Thread (g, c) = (tid >> 6, tid & 63) owns entries (g + 8u, c), u < 8;
-  //      the row operand is a wave-wide broadcast from LDS.
-  const int ng = gridDim.x;
-  const int ch = (n + ng - 1) / ng;
-  const int r0 = blockIdx.x * ch, r1 = min(n, r0 + ch);
-  const int nr = r1 > r0 ? r1 - r0 : 0;
-  const int gq = tid >> 6, cq = tid & 63;
-  double* chunk = b0;   // nr x KMAX
-  {
-    // every row load of this thread in flight at once (a chunk is <= CH_MAX rows)
-    constexpr int CU = CH_MAX / (NT / 64);
-    double v[CU];
-#pragma unroll
-    for (int u = 0; u < CU; ++u) {
-      const int row = gq + 8 * u;
-      v[u] = (row < nr && cq < k) ? W[(int64_t)(r0 + row) * ldw + cq] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < CU; ++u) {
-      const int row = gq + 8 * u;
-      if (row < nr && cq < k) chunk[row * KMAX + cq] = v[u];
-    }
-  }
-  __syncthreads();
-  double* myp = part + (int64_t)blockIdx.x * k * k;
-  {
-    double acc[KMAX / 8];
-#pragma unroll
-    for (int u = 0; u < KMAX / 8; ++u) acc[u] = 0.0;
-    if (cq < k) {
-      for (int row = 0; row < nr; ++row) {
-        const double x = chunk[row * KMAX + cq];
-#pragma unroll
-        for (int u = 0; u < KMAX / 8; ++u) acc[u] += chunk[row * KMAX + gq + 8 * u] * x;
-      }
-#pragma unroll
-      for (int u = 0; u < KMAX / 8; ++u) {
-        const int i = gq + 8 * u;
-        if (i <= cq) myp[i * k + cq] = acc[u];
-      }
-    }
-  }
-  // ---- publish, count, last arriver continues (release / acquire, agent scope)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *is_last = (t == (unsigned)ng - 1);
-    if (*is_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    st_sh = 0;
-  }
-  __syncthreads();
-  if (!*is_last) return;
-  SL_CST(SO + 1)
-
-  // ---- H = sum of the partials (symmetric, f64) -> b0
-  {
-    // H entries (i, cq), i = gq + 8u: the ng partials of all of them in flight together
-    constexpr int RU = KMAX / (NT / 64);
-    double a[RU];
-#pragma unroll
-    for (int u = 0; u < RU; ++u) a[u] = 0.0;
-    for (int g0 = 0; g0 < ng; g0 += 4) {
-      double v[4][RU];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int u = 0; u < RU; ++u) {
-          const int i = gq + 8 * u, gg = g0 + q;
-          v[q][u] = (gg < ng && i < k && cq < k && cq >= i)
-                        ? __builtin_nontemporal_load(part + (int64_t)gg * k * k + i * k + cq) : 0.0;
-        }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int u = 0; u < RU; ++u) a[u] += v[q][u];
-    }
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int i = gq + 8 * u;
-      if (i < k && cq < k && cq >= i) {
-        b0[i * ld + cq] = a[u];
-        b0[cq * ld + i] = a[u];
-      }
-    }
-  }
-  if (tid == 0) *counter = 0u;   // ready for the next launch (graph replays)
-  __syncthreads();
-  SL_CST(SO + 2)
-  if (!FINAL) {
-    // ---- INTER: H = R^T R, X = R^{-1} (f64, k x k) -> Rinv
-    chol_inv(b0, ld, b2, ld, k, &st_sh, red);
-    SL_CST(SO + 3)
-    for (int i = tid >> 6; i < k; i += NT / 64) {
-      const int c = tid & 63;
-      if (c < k) {
-        const double v = b2[i * ld + c];
-        if (!(fabs(v) < 1e300)) atomicOr(&st_sh, ST_NONFINITE);
-        Rinv[i * k + c] = v;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) atomicOr(status, st_sh);
-    SL_CST(SO + 4)
-    return;
-  }
+  constexpr int SO = 16;
+  (void)SO;
   // ---- FINAL: Y^T Y = Rt^T Rt, Rti = Rt^{-1} -> b3 (straight from Gy; H in b0 survives)
-  chol_inv(Gy, k, b3, ld, k, &st_sh, red);
+  chol_inv(Gy, k, b3, ld, k, st_sh_p, red);
   SL_CST(SO + 3)
   // C = Rti^T H Rti:  T = H Rti -> b1, C = Rti^T T -> b2
   small_gemm(b0, b3, b1, k, ld, false);
@@ -605,7 +488,7 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
   if (diag_ok) {
     if (tid == 0) flags[3] = 0;
   } else {
-    Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, &st_sh, warm);
+    Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, st_sh_p, warm);
   }
   SL_CST(SO + 5)
 #ifdef SL_CORE_STAMPS
@@ -633,8 +516,8 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
   for (int c = tid; c < r; c += NT) {
     const double lam = Af[order[c] * ld + order[c]];
     s_out[c] = lam > 0.0 ? sqrt(lam) : 0.0;
-    if (!(lam > 0.0)) atomicOr(&st_sh, ST_RANK);
-    if (!(lam == lam)) atomicOr(&st_sh, ST_NONFINITE);
+    if (!(lam > 0.0)) atomicOr(st_sh_p, ST_RANK);
+    if (!(lam == lam)) atomicOr(st_sh_p, ST_NONFINITE);
   }
   __syncthreads();
   for (int e = tid; e < k * r; e += NT) {
@@ -647,11 +530,315 @@ k_gram_la(const double* __restrict__ W, int n, int k, int ldw, double* __restric
     N[e] = lam > 0.0 ? a / sqrt(lam) : 0.0;
   }
   if (tid == 0) {
-    const int all = atomicOr(status, st_sh) | st_sh;
+    int all = st_sh;
+    if (status_or) all |= atomicOr(status, st_sh);
+    else __hip_atomic_store(status, st_sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the call's final status word, straight to host-mapped memory (no D2H copy)
     if (mirror) __hip_atomic_store(mirror, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   SL_CST(SO + 6)
+}
+
+// ---------------------------------------------------------------- fused boundary
+// ONE launch at each pass boundary of a single-rank call, replacing the slab
+// reduce, the Gram / small-LA kernel and the Z^T kernel (+ V = W N after the last pass):
+//   1. workgroup b sums the pass's f32 W slabs of its BR rows (all slabs, f64
+//      accumulation) into LDS (and WG); FINAL: also its share of the fp64 Gram
+//      slabs (Y^T Y) into WG
+//   2. the packed upper partial Gram of its rows -> global, then a ticket
+//   3. the last arriving workgroup sums the partials (16-B loads, all of a
+//      batch in flight), runs the k x k algebra (INTER: Cholesky inverse;
+//      FINAL: final_core) and bumps the generation word (agent-scope release)
+//   4. every workgroup (the others spin on the generation word meanwhile; the
+//      <= BMAX workgroups are co-resident on the 256 CUs) forms its rows of
+//      the next pass operand Z^T = (W R^{-1})^T (INTER) or of V = W N (FINAL)
+//      from the W rows it still holds in LDS.
+// Graph replays: the last arriver resets the ticket; the generation only
+// grows (a waiter compares with the value it read before arriving).
+// Without slabs (wslab null) the rows come from WG (multi-rank: WG all-reduced).
+constexpr int BR = 16;     // rows of W per workgroup
+constexpr int BMAX = 64;   // workgroups (n <= 1024)
+constexpr int BK = 48;     // largest k of the pass
+
+struct BndArgs {
+  const float* wslab;     // [nslab][n][k] f32 W slabs of the pass (null: rows from WG)
+  const double* gslab;    // [nslab][k][k] fp64 Gram slabs (FINAL with wslab)
+  int nslab, n, k, r;
+  double* WG;             // [W (n x k); Gy (k x k)] f64
+  double* part;           // BMAX packed partial Grams, stride ldp doubles
+  int ldp;
+  unsigned* sync;         // [0] ticket, [16] generation
+  int* status;
+  int status_or;
+  double* Rinv;           // INTER: k x k
+  bf16_t* Zt;             // INTER: k x n
+  float* M;               // FINAL: k x r, N (k x r), s64 (r)
+  double* N;
+  double* s64;
+  int max_sweeps;
+  double* V0;
+  int* v0_valid;
+  int* mirror;
+  float* V;               // FINAL: n x r (null: no V), s32 (r)
+  float* s32;
+  float* const* optr;     // {U, s, V} read at run time when set (graph replays)
+};
+
+enum : int { ST_TIMEOUT = 16 };
+
+// dynamic LDS: the small-LA layout (GRAM_LA_LDS), then the BR x KMAX rows of W
+constexpr size_t BND_WR_OFF = (GRAM_LA_LDS + 15) / 16 * 2;   // in doubles
+constexpr size_t BND_LDS = BND_WR_OFF * sizeof(double) + (size_t)BR * KMAX * sizeof(double);
+
+template <bool FINAL>
+__global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = a.n, k = a.k, nb = gridDim.x;
+  const int ld = k + 1;
+  const int mat = KMAX * (KMAX + 1);
+  double* b0 = sm;
+  double* b1 = sm + mat;
+  double* b2 = sm + 2 * mat;
+  double* b3 = sm + 3 * mat;
+  double* red = sm + 4 * mat;
+  int* iscr = (int*)(red + RED);
+  int* flags = iscr;
+  int* order = iscr + 4;
+  double* Wr = sm + BND_WR_OFF;   // BR x KMAX rows of W
+  __shared__ int st_sh;
+  __shared__ int is_last;
+  __shared__ unsigned gen0;
+  const int r0 = blockIdx.x * BR;
+  const int nr = min(BR, n - r0);
+  const int E = nr * k;   // a multiple of 8 (n % 8 == 0)
+
+  // ---- 1. this workgroup's rows of W
+  if (a.wslab) {
+    constexpr int U4 = BR * BK / 4 / 64;   // float4 per lane and slab
+    const int E4 = E >> 2;
+    const int64_t ss4 = (int64_t)n * k / 4;
+    const float4* base = (const float4*)(a.wslab + (int64_t)r0 * k);
+    double acc[U4][4];
+#pragma unroll
+    for (int u = 0; u < U4; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[u][c] = 0.0;
+    const float4 z4 = {0.f, 0.f, 0.f, 0.f};
+    int s = wv;
+    // wave wv sums slabs wv, wv + 8, ...: four slabs' loads in flight
+    for (; s + 24 < a.nslab; s += 32) {
+      float4 v[4][U4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < U4; ++u) {
+          const int j = lane + 64 * u;
+          v[q][u] = j < E4 ? base[(int64_t)(s + 8 * q) * ss4 + j] : z4;
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < U4; ++u) {
+          acc[u][0] += (double)v[q][u].x;
+          acc[u][1] += (double)v[q][u].y;
+          acc[u][2] += (double)v[q][u].z;
+          acc[u][3] += (double)v[q][u].w;
+        }
+    }
+    for (; s < a.nslab; s += 8) {
+#pragma unroll
+      for (int u = 0; u < U4; ++u) {
+        const int j = lane + 64 * u;
+        const float4 v = j < E4 ? base[(int64_t)s * ss4 + j] : z4;
+        acc[u][0] += (double)v.x;
+        acc[u][1] += (double)v.y;
+        acc[u][2] += (double)v.z;
+        acc[u][3] += (double)v.w;
+      }
+    }
+    // the 8 wave partials through LDS (b1..b2: 8 x BR * BK doubles)
+    double* P = b1;
+#pragma unroll
+    for (int u = 0; u < U4; ++u) {
+      const int j = lane + 64 * u;
+      if (j < E4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) P[wv * (BR * BK) + 4 * j + c] = acc[u][c];
+    }
+    __syncthreads();
+    for (int e = tid; e < E; e += NT) {
+      double sum = 0.0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) sum += P[w * (BR * BK) + e];
+      const int row = e / k, col = e - row * k;
+      Wr[row * KMAX + col] = sum;
+      a.WG[(int64_t)r0 * k + e] = sum;
+    }
+    if (FINAL) {
+      // this workgroup's share [g0, g1) of the k * k Gram entries
+      const int kk = k * k, ch = (kk + nb - 1) / nb;
+      const int g0 = blockIdx.x * ch, g1 = min(kk, g0 + ch);
+      for (int e0 = g0; e0 < g1; e0 += 64) {
+        __syncthreads();   // P reuse
+        const int e = e0 + lane;
+        double sum = 0.0;
+        if (e < g1) {
+          int t = wv;
+          for (; t + 56 < a.nslab; t += 64) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = a.gslab[(int64_t)(t + 8 * q) * kk + e];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) sum += v[q];
+          }
+          for (; t < a.nslab; t += 8) sum += a.gslab[(int64_t)t * kk + e];
+        }
+        P[wv * 64 + lane] = sum;
+        __syncthreads();
+        if (tid < 64 && e0 + tid < g1) {
+          double t = 0.0;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) t += P[w * 64 + tid];
+          a.WG[(int64_t)n * k + e0 + tid] = t;
+        }
+      }
+    }
+  } else {
+    for (int e = tid; e < E; e += NT) {
+      const int row = e / k, col = e - row * k;
+      Wr[row * KMAX + col] = a.WG[(int64_t)r0 * k + e];
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. packed upper partial Gram of the rows: thread (gq, cq) owns (gq + 8u, cq)
+  {
+    const int gq = wv, cq = lane;
+    double acc[KMAX / 8];
+#pragma unroll
+    for (int u = 0; u < KMAX / 8; ++u) acc[u] = 0.0;
+    if (cq < k) {
+      for (int row = 0; row < nr; ++row) {
+        const double x = Wr[row * KMAX + cq];
+#pragma unroll
+        for (int u = 0; u < KMAX / 8; ++u) acc[u] += Wr[row * KMAX + gq + 8 * u] * x;
+      }
+      double* myp = a.part + (int64_t)blockIdx.x * a.ldp;
+#pragma unroll
+      for (int u = 0; u < KMAX / 8; ++u) {
+        const int i = gq + 8 * u;
+        if (i <= cq) myp[i * k - (i * (i - 1)) / 2 + (cq - i)] = acc[u];
+      }
+    }
+  }
+
+  // ---- 3. ticket (every wave's stores released at agent scope first)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (tid == 0) {
+    gen0 = __hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(&a.sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = t == (unsigned)nb - 1;
+    st_sh = 0;
+  }
+  __syncthreads();
+  if (is_last) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // sum of the nb packed partials, two entries per thread and load
+    const int npair = a.ldp >> 1;
+    const int kk2 = k * (k + 1) / 2;
+    double* Hp = b1;
+    for (int p = tid; p < npair; p += NT) {
+      const double2* src = (const double2*)a.part + p;
+      double2 s2 = {0.0, 0.0};
+      for (int g0 = 0; g0 < nb; g0 += 16) {
+        double2 v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = g0 + q < nb ? src[(int64_t)(g0 + q) * npair] : double2{0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          s2.x += v[q].x;
+          s2.y += v[q].y;
+        }
+      }
+      Hp[2 * p] = s2.x;
+      Hp[2 * p + 1] = s2.y;
+    }
+    __syncthreads();
+    (void)kk2;
+    for (int e = tid; e < k * k; e += NT) {
+      const int i = e / k, c = e - i * k;
+      const int lo = min(i, c), hi = max(i, c);
+      b0[i * ld + c] = Hp[lo * k - (lo * (lo - 1)) / 2 + (hi - lo)];
+    }
+    __syncthreads();
+    if (tid == 0) a.sync[0] = 0u;   // ready for the next launch
+    if (!FINAL) {
+      chol_inv(b0, ld, b2, ld, k, &st_sh, red);
+      for (int e = tid; e < k * k; e += NT) {
+        const int i = e / k, c = e - i * k;
+        const double v = b2[i * ld + c];
+        if (!(fabs(v) < 1e300)) atomicOr(&st_sh, ST_NONFINITE);
+        a.Rinv[e] = v;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        if (a.status_or) atomicOr(a.status, st_sh);
+        else __hip_atomic_store(a.status, st_sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      final_core(b0, b1, b2, b3, red, flags, order, a.WG + (int64_t)n * k, k, a.r, a.M, a.N, a.s64, a.status,
+                 a.max_sweeps, a.V0, a.v0_valid, a.mirror, &st_sh, a.status_or);
+    }
+    // release the waiters
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&a.sync[16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (tid == 0) {
+      // bounded wait (never reached on a sane run: the last arriver has no
+      // further dependency); a timeout flags the call instead of hanging
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > 200000000ull) {
+          atomicOr(a.status, ST_TIMEOUT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+
+  // ---- 4. rows of Z^T = (W Rinv)^T (INTER) or V = W N (FINAL)
+  float* V = FINAL ? (a.optr ? a.optr[2] : a.V) : nullptr;
+  if (FINAL) {
+    float* s32 = a.optr ? a.optr[1] : a.s32;
+    if (blockIdx.x == 0 && s32 && tid < a.r) s32[tid] = (float)a.s64[tid];
+    if (!V) return;
+  }
+  const int nc = FINAL ? a.r : k;
+  const double* Bsrc = FINAL ? a.N : a.Rinv;
+  double* Bs = b3;
+  for (int e = tid; e < k * nc; e += NT) Bs[e] = Bsrc[e];
+  __syncthreads();
+  const int row = tid & (BR - 1);
+  if (row < nr) {
+    for (int c = tid / BR; c < nc; c += NT / BR) {
+      double s0 = 0.0, s1 = 0.0;
+      int l = 0;
+      for (; l + 1 < k; l += 2) {
+        s0 += Wr[row * KMAX + l] * Bs[l * nc + c];
+        s1 += Wr[row * KMAX + l + 1] * Bs[(l + 1) * nc + c];
+      }
+      if (l < k) s0 += Wr[row * KMAX + l] * Bs[l * nc + c];
+      const double v = s0 + s1;
+      if (FINAL) V[(int64_t)(r0 + row) * nc + c] = (float)v;
+      else a.Zt[(int64_t)c * n + r0 + row] = f_to_bf16((float)v);
+    }
+  }
 }
 
 // Out (rows of W, k x nc) = W (n x k f64) B (k x nc f64, row-major), a 32-row
@@ -713,13 +900,6 @@ __device__ __forceinline__ void rows_times_small(const double* __restrict__ W, i
   }
 }
 
-// Z^T (k x n bf16) = (W R^{-1})^T, R^{-1} upper triangular (k x k f64)
-__global__ void __launch_bounds__(256)
-k_make_zt(const double* __restrict__ W, int n, int k, int ldw, const double* __restrict__ Rinv, bf16_t* __restrict__ Zt) {
-  rows_times_small(W, n, k, ldw, Rinv, k,
-                   [&](int i, int c, double v) { Zt[(int64_t)c * n + i] = f_to_bf16((float)v); });
-}
-
 // V (n x r f32) = W (n x k f64) N (k x r f64); s32 = s64 (r)
 __global__ void __launch_bounds__(256)
 k_make_v(const double* __restrict__ W, int n, int k, int ldw, const double* __restrict__ N, int r, float* __restrict__ V,
@@ -757,7 +937,7 @@ __global__ void __launch_bounds__(256) k_f64_to_bf16(const double* __restrict__ 
   if (t < count) y[t] = f_to_bf16((float)x[t]);
 }
 
-size_t gram_la_lds() { return (size_t)(4 * KMAX * (KMAX + 1) + RED) * sizeof(double) + (4 + KMAX + 1) * sizeof(int); }
+size_t gram_la_lds() { return GRAM_LA_LDS; }
 
 }  // namespace
 
@@ -768,75 +948,6 @@ SL_API int sl_core_stamps(unsigned long long* host) {
   return SL_OK;
 }
 #endif
-constexpr int SL_GRAM_NG = 16;   // workgroups of the partial-Gram phase
-
-SL_API int64_t sl_rsvd_gram_workspace(int k) { return (int64_t)SL_GRAM_NG * k * k * 8 + 256; }
-
-// Between two passes: Rinv (k x k f64) of the Cholesky factor of W^T W.
-// ws: sl_rsvd_gram_workspace(k) bytes, its first 4 bytes a zeroed counter
-// (the kernel leaves it zero again).
-SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, double* Rinv, int* status, void* stream) {
-  if (k < 1 || k > KMAX || n < 1 || n > SL_GRAM_NG * CH_MAX) {
-    sl_set_last_error("rsvd_inter_la: 1 <= k <= 64 and 1 <= n <= 1024");
-    return SL_ERR_UNSUPPORTED;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_gram_la<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)gram_la_lds()));
-    attr = true;
-  }
-  unsigned* counter = (unsigned*)ws;
-  double* part = (double*)((char*)ws + 256);
-  const int ng = n < SL_GRAM_NG ? n : SL_GRAM_NG;
-  k_gram_la<false><<<ng, NT, gram_la_lds(), s>>>(W, n, k, ldw, part, counter, nullptr, 0, Rinv, nullptr, nullptr,
-                                                nullptr, status, 0, nullptr, nullptr, nullptr);
-  SL_LAUNCH_CHECK();
-  return SL_OK;
-}
-
-// Z^T = (W Rinv)^T as bf16 (k x n)
-SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double* Rinv, void* Zt, void* stream) {
-  if (k < 1 || k > KMAX) { sl_set_last_error("rsvd_make_zt: 1 <= k <= 64"); return SL_ERR_UNSUPPORTED; }
-  k_make_zt<<<(unsigned)((n + 31) / 32), 256, 0, (hipStream_t)stream>>>(W, n, k, ldw, Rinv, (bf16_t*)Zt);
-  SL_LAUNCH_CHECK();
-  return SL_OK;
-}
-
-// After the final pass: s (r), M (k x r f32), N (k x r f64) from W (n x k
-// f64) and the fp64 Gram of Y (k x k).
-// V0 (kp x kp f64, kp = k rounded up to even) + v0_valid: warm start of the
-// Jacobi from the previous call's eigenvectors (null: cold start each call).
-SL_API int sl_rsvd_final_la2(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                             double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
-                             int* mirror, void* stream) {
-  if (k < 1 || k > KMAX || r < 1 || r > k || n < 1 || n > SL_GRAM_NG * CH_MAX) {
-    sl_set_last_error("rsvd_final_la: 1 <= r <= k <= 64 and 1 <= n <= 1024");
-    return SL_ERR_UNSUPPORTED;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_gram_la<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)gram_la_lds()));
-    attr = true;
-  }
-  unsigned* counter = (unsigned*)ws;
-  double* part = (double*)((char*)ws + 256);
-  const int ng = n < SL_GRAM_NG ? n : SL_GRAM_NG;
-  k_gram_la<true><<<ng, NT, gram_la_lds(), st>>>(W, n, k, ldw, part, counter, Gy, r, nullptr, M, N, s, status,
-                                                max_sweeps > 0 ? max_sweeps : 40, V0, v0_valid, mirror);
-  SL_LAUNCH_CHECK();
-  return SL_OK;
-}
-
-SL_API int sl_rsvd_final_la(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                            double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
-                            void* stream) {
-  return sl_rsvd_final_la2(W, n, k, ldw, Gy, r, ws, M, N, s, status, max_sweeps, V0, v0_valid, nullptr, stream);
-}
-
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream) {
   if (k < 1 || k > KMAX || r > k) { sl_set_last_error("rsvd_make_v: 1 <= r <= k <= 64"); return SL_ERR_UNSUPPORTED; }
@@ -938,6 +1049,75 @@ SL_API int sl_sym_eig_jacobi2(const double* C, int k, double* w, double* V, int*
 SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void* stream) {
   if (count <= 0) return SL_OK;
   k_f64_to_bf16<<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(src, count, (bf16_t*)Zt);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ------------------------------------------------------------ fused boundary
+SL_API int sl_rsvd_pass_grid(int64_t m);
+
+// workspace of sl_rsvd_boundary: sync words (256 B, zeroed once; the kernel
+// leaves the ticket zero and only advances the generation) + BMAX partials
+SL_API int64_t sl_rsvd_bnd_workspace(int k) {
+  const int64_t ldp = ((int64_t)k * (k + 1) / 2 + 1) & ~(int64_t)1;
+  return 256 + (int64_t)BMAX * ldp * 8;
+}
+
+// One pass boundary of a single-rank call (pass_ws: the v4 pass slabs of an
+// m-row pass) or, with pass_ws null, from the all-reduced [W; G] in WG.
+// final_ = 0: Rinv and Z^T (bf16, k x n) for the next pass.  final_ = 1: the
+// core (s64, M, N, status, mirror, warm start V0) and, when V or optr is
+// given, V = W N (n x r f32) and s (f32).  status_or = 0 stores the status
+// bits (the call's first writer), 1 ORs them.
+SL_API int sl_rsvd_boundary(int final_, const void* pass_ws, int64_t m, int n, int k, int r, double* WG, void* bws,
+                            int* status, int status_or, double* Rinv, void* Zt, float* M, double* N, double* s64,
+                            int max_sweeps, double* V0, int* v0_valid, int* mirror, float* V, float* s32,
+                            float* const* optr, void* stream) {
+  if (k < 1 || k > BK || n < 16 || n > BMAX * BR || n % 8 || (final_ && (r < 1 || r > k))) {
+    sl_set_last_error("rsvd_boundary: needs 1 <= k <= 48, 16 <= n <= 1024, n % 8 == 0, 1 <= r <= k");
+    return SL_ERR_UNSUPPORTED;
+  }
+  BndArgs a{};
+  if (pass_ws) {
+    const int grid = sl_rsvd_pass_grid(m);
+    const char* base = (const char*)pass_ws;
+    a.wslab = (const float*)base;
+    a.gslab = (const double*)(base + (((int64_t)grid * n * k * 4 + 255) & ~(int64_t)255));
+    a.nslab = grid;
+  }
+  a.n = n; a.k = k; a.r = r;
+  a.WG = WG;
+  a.sync = (unsigned*)bws;
+  a.part = (double*)((char*)bws + 256);
+  a.ldp = (int)(((int64_t)k * (k + 1) / 2 + 1) & ~(int64_t)1);
+  a.status = status;
+  a.status_or = status_or;
+  a.Rinv = Rinv;
+  a.Zt = (bf16_t*)Zt;
+  a.M = M; a.N = N; a.s64 = s64;
+  a.max_sweeps = max_sweeps > 0 ? max_sweeps : 40;
+  a.V0 = V0; a.v0_valid = v0_valid; a.mirror = mirror;
+  a.V = V; a.s32 = s32; a.optr = optr;
+  const unsigned nb = (unsigned)((n + BR - 1) / BR);
+  hipStream_t s = (hipStream_t)stream;
+  if (final_) {
+    static bool attr = false;
+    if (!attr) {
+      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_boundary<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)BND_LDS));
+      attr = true;
+    }
+    k_boundary<true><<<nb, NT, BND_LDS, s>>>(a);
+  } else {
+    if (!Rinv || !Zt) { sl_set_last_error("rsvd_boundary: Rinv and Zt required"); return SL_ERR_INVALID; }
+    static bool attr = false;
+    if (!attr) {
+      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_boundary<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)BND_LDS));
+      attr = true;
+    }
+    k_boundary<false><<<nb, NT, BND_LDS, s>>>(a);
+  }
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

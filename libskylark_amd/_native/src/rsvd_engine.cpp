@@ -33,17 +33,16 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
                         int64_t ldy, int final_pass, int variant, void* stream);
 SL_API int sl_rsvd_reduce_z(const void* ws, int64_t m, int64_t n, int k, void* Wout, int w_f64, int ldw,
                             double* Gout, int ldg, int* zero_word, void* stream);
-SL_API int64_t sl_rsvd_gram_workspace(int k);
-SL_API int sl_rsvd_inter_la(const double* W, int n, int k, int ldw, void* ws, double* Rinv, int* status, void* stream);
-SL_API int sl_rsvd_make_zt(const double* W, int n, int k, int ldw, const double* Rinv, void* Zt, void* stream);
-SL_API int sl_rsvd_final_la2(const double* W, int n, int k, int ldw, const double* Gy, int r, void* ws, float* M,
-                             double* N, double* s, int* status, int max_sweeps, double* V0, int* v0_valid,
-                             int* mirror, void* stream);
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream);
 SL_API int sl_rsvd_make_v_ind(const double* W, int n, int k, int ldw, const double* N, int r, const double* s64,
                               float* const* optr, void* stream);
 SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* stream);
+SL_API int64_t sl_rsvd_bnd_workspace(int k);
+SL_API int sl_rsvd_boundary(int final_, const void* pass_ws, int64_t m, int n, int k, int r, double* WG, void* bws,
+                            int* status, int status_or, double* Rinv, void* Zt, float* M, double* N, double* s64,
+                            int max_sweeps, double* V0, int* v0_valid, int* mirror, float* V, float* s32,
+                            float* const* optr, void* stream);
 SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, int k2, float* const* optr,
                              void* stream);
 SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
@@ -68,7 +67,9 @@ struct Plan {
   uint16_t* Zt = nullptr;   // k x n bf16
   double* WG = nullptr;     // [W (n x k) ; G (k x k)] f64: the reduced pass outputs
   float* Y = nullptr;       // m x k f32
-  void* gram_ws = nullptr;  // counter + partial Grams (zeroed once)
+  void* bnd_ws = nullptr;   // fused boundary: sync words + partial Grams (zeroed once)
+  float* last_ptrs[3] = {nullptr, nullptr, nullptr};   // optr contents written last (and on which stream)
+  hipStream_t last_ptrs_stream = nullptr;
   double* Rinv = nullptr;   // k x k
   float* M = nullptr;       // k x r
   double* N = nullptr;      // k x r
@@ -95,17 +96,14 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
   const bool final_pass = i == p->q;
   if (i > p->q + 1 || i < 0) { sl_set_last_error("rsvd: segment out of range"); return SL_ERR_INVALID; }
   int rc = SL_OK;
-  if (i == p->q + 1) {
-    return sl_rsvd_final_la2(p->WG, (int)p->n, p->k, p->k, p->WG + p->n * p->k, p->r, p->gram_ws, p->M, p->N,
-                             p->s64, p->status, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr,
-                             p->mirror_dev, s);
-  }
   if (i > 0) {
-    // CholeskyQR of the previous (reduced) W and the next pass operand
-    rc = sl_rsvd_inter_la(p->WG, (int)p->n, p->k, p->k, p->gram_ws, p->Rinv, p->status, s);
-    if (rc != SL_OK) return rc;
-    rc = sl_rsvd_make_zt(p->WG, (int)p->n, p->k, p->k, p->Rinv, p->Zt, s);
-    if (rc != SL_OK) return rc;
+    // the boundary on the (all-reduced) [W; G]: CholeskyQR of W and the next
+    // pass operand, or after the last pass the core (V is left to the finish)
+    const int fin = i == p->q + 1 ? 1 : 0;
+    rc = sl_rsvd_boundary(fin, nullptr, p->m, (int)p->n, p->k, p->r, p->WG, p->bnd_ws, p->status, 1, p->Rinv, p->Zt,
+                          p->M, p->N, p->s64, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr,
+                          p->mirror_dev, nullptr, nullptr, nullptr, s);
+    if (rc != SL_OK || fin) return rc;
   }
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
                     final_pass ? 1 : 0, 0, s);
@@ -113,6 +111,26 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
   // the first reduce of the call also clears the status word (no memset node)
   return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
                           p->k, i == 0 ? p->status : nullptr, s);
+}
+
+// Single-rank segment: pass i, preceded (i > 0) by ONE fused boundary launch
+// on the previous pass's slabs (reduce + Gram + Cholesky inverse + Z^T, or
+// after the last pass: reduce + the whole core + V = W N).  Segment q + 1 is
+// the final boundary alone.  V / s32 / optr: where the final boundary writes
+// V and s (all null: V is left to sl_rsvd_finish).
+int seg_fused(Plan* p, const void* A, int i, hipStream_t s, float* V, float* s32, float* const* optr) {
+  if (i > p->q + 1 || i < 0) { sl_set_last_error("rsvd: segment out of range"); return SL_ERR_INVALID; }
+  if (i > 0) {
+    const int fin = i == p->q + 1 ? 1 : 0;
+    // the call's first status writer stores (no memset node), later ones OR
+    const int rc = sl_rsvd_boundary(fin, p->pass_ws, p->m, (int)p->n, p->k, p->r, p->WG, p->bnd_ws, p->status,
+                                    i > 1 ? 1 : 0, p->Rinv, p->Zt, p->M, p->N, p->s64, 0,
+                                    p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr, p->mirror_dev,
+                                    V, s32, optr, s);
+    if (rc != SL_OK || fin) return rc;
+  }
+  return sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, i == p->q ? p->Y : nullptr, p->k,
+                      i == p->q ? 1 : 0, 0, s);
 }
 
 void drop_graph(Plan* p) {
@@ -127,9 +145,8 @@ void drop_graph(Plan* p) {
 
 // the finish through the pointer table (inside the graph: no graph -> stream
 // gap before it, no per-call launches)
+// (V and s were written by the final boundary through the same table)
 int finish_ind(Plan* p, hipStream_t s) {
-  int rc = sl_rsvd_make_v_ind(p->WG, (int)p->n, p->k, p->k, p->N, p->r, p->s64, p->optr, s);
-  if (rc != SL_OK) return rc;
   return sl_tsk_f32_xm_ind(p->Y, p->m, p->k, p->M, p->r, p->optr, s);
 }
 
@@ -147,7 +164,8 @@ int capture(Plan* p, const void* A, int with_finish, hipStream_t st) {
   hipStream_t cst = p->cap_stream;
   SL_HIP_CHECK(hipStreamBeginCapture(cst, hipStreamCaptureModeThreadLocal));
   int rc = SL_OK;
-  for (int i = 0; i <= p->q + 1 && rc == SL_OK; ++i) rc = seg(p, A, i, cst);
+  for (int i = 0; i <= p->q + 1 && rc == SL_OK; ++i)
+    rc = seg_fused(p, A, i, cst, nullptr, nullptr, with_finish ? p->optr : nullptr);
   if (rc == SL_OK && with_finish) rc = finish_ind(p, cst);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cst, &g);
@@ -186,7 +204,7 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   const int64_t o_zt = off;   off = align256(off + n * k * 2);
   const int64_t o_wg = off;   off = align256(off + (n + k) * k * 8);
   const int64_t o_y = off;    off = align256(off + m * k * 4);
-  const int64_t o_gram = off; off = align256(off + sl_rsvd_gram_workspace(k));
+  const int64_t o_bnd = off;  off = align256(off + sl_rsvd_bnd_workspace(k));
   const int64_t o_ri = off;   off = align256(off + (int64_t)k * k * 8);
   const int64_t o_m = off;    off = align256(off + (int64_t)k * r * 4);
   const int64_t o_n = off;    off = align256(off + (int64_t)k * r * 8);
@@ -204,7 +222,7 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   p->Zt = (uint16_t*)(p->base + o_zt);
   p->WG = (double*)(p->base + o_wg);
   p->Y = (float*)(p->base + o_y);
-  p->gram_ws = p->base + o_gram;
+  p->bnd_ws = p->base + o_bnd;
   p->Rinv = (double*)(p->base + o_ri);
   p->M = (float*)(p->base + o_m);
   p->N = (double*)(p->base + o_n);
@@ -213,7 +231,7 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   p->V0 = (double*)(p->base + o_v0);
   p->v0_valid = (int*)(p->base + o_v0 + (int64_t)kp * kp * 8);
   p->optr = (float**)(p->base + o_op);
-  if (hipMemset(p->gram_ws, 0, (size_t)sl_rsvd_gram_workspace(k)) != hipSuccess ||
+  if (hipMemset(p->bnd_ws, 0, (size_t)sl_rsvd_bnd_workspace(k)) != hipSuccess ||
       hipMemset(p->status, 0, 16) != hipSuccess || hipMemset(p->v0_valid, 0, 16) != hipSuccess) {
     (void)hipFree(p->base);
     delete p;
@@ -316,10 +334,11 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
   hipStream_t st = (hipStream_t)stream;
   if (!use_graph) {
     for (int i = 0; i <= p->q + 1; ++i) {
-      const int rc = seg(p, A, i, st);
+      const int rc = seg_fused(p, A, i, st, V, s, nullptr);
       if (rc != SL_OK) return rc;
     }
-    return sl_rsvd_finish(plan, U, ldu, s, V, stream);
+    if (!V) return sl_rsvd_finish(plan, U, ldu, s, V, stream);
+    return sl_tsk_f32_xm(p->Y, p->m, p->k, p->k, p->M, p->r, U, ldu, nullptr, nullptr, stream);
   }
   if (p->graph_A != A) drop_graph(p);
   // the finish joins the graph when its streaming kernel can take this U
@@ -330,8 +349,14 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
     if (rc != SL_OK) return rc;
   }
   if (fin) {
-    int rc = sl_rsvd_set_ptrs(p->optr, U, s, V, st);
-    if (rc != SL_OK) return rc;
+    // the table already holds these pointers when the last call on this
+    // stream wrote the same ones (a caching allocator hands them back)
+    if (!(p->last_ptrs[0] == U && p->last_ptrs[1] == s && p->last_ptrs[2] == V && p->last_ptrs_stream == st)) {
+      int rc = sl_rsvd_set_ptrs(p->optr, U, s, V, st);
+      if (rc != SL_OK) return rc;
+      p->last_ptrs[0] = U; p->last_ptrs[1] = s; p->last_ptrs[2] = V;
+      p->last_ptrs_stream = st;
+    }
     SL_HIP_CHECK(hipGraphLaunch(p->exec[1], st));
     return SL_OK;
   }

@@ -295,7 +295,7 @@ def _engine_lib():
 
 
 # status bits of a device call (rsvd_core.hip)
-ST_PIVOT, ST_NONFINITE, ST_NOCONV, ST_RANK = 1, 2, 4, 8
+ST_PIVOT, ST_NONFINITE, ST_NOCONV, ST_RANK, ST_TIMEOUT = 1, 2, 4, 8, 16
 
 
 class _EnginePlan:
@@ -420,6 +420,9 @@ class _EnginePlan:
     def _poll_status(self):
         if self.status_ev is not None and self.status_ev.query():
             self.last_status = self._status_word()
+            if self.last_status & ST_TIMEOUT:
+                raise RuntimeError("approximate_svd (device): a pass-boundary kernel timed out waiting for its "
+                                   "last workgroup (status 16); the previous call's results are invalid")
             if self.last_status & (ST_NONFINITE | ST_RANK | ST_NOCONV):
                 import warnings
                 warnings.warn(f"approximate_svd (device): previous call flagged status {self.last_status} "

@@ -1,8 +1,9 @@
 """Device small linear algebra of the randSVD engine (rsvd_core.hip) against
-fp64 numpy references: the CholeskyQR inverse between passes
-(sl_rsvd_inter_la), the next pass operand (sl_rsvd_make_zt), the fp64 core
-(sl_rsvd_final_la: Cholesky of Y^T Y, C = Rt^-T H Rt^-1, Jacobi, factors),
-V = W N (sl_rsvd_make_v), pivot dropping and the Jacobi warm start."""
+fp64 numpy references, through the pass-boundary kernel on an all-reduced
+[W; G] buffer (sl_rsvd_boundary, the multi-rank form): the CholeskyQR
+inverse between passes and the next pass operand, the fp64 core (Cholesky
+of Y^T Y, C = Rt^-T H Rt^-1, Jacobi, factors), V = W N (sl_rsvd_make_v),
+pivot dropping and the Jacobi warm start."""
 import ctypes as C
 
 import numpy as np
@@ -18,10 +19,9 @@ vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 def L():
     from libskylark_amd.ops import _lib
     _lib.require()
-    _lib.register("sl_rsvd_gram_workspace", [i32], C.c_int64)
-    _lib.register("sl_rsvd_inter_la", [vp, i32, i32, i32, vp, vp, vp, vp])
-    _lib.register("sl_rsvd_make_zt", [vp, i32, i32, i32, vp, vp, vp])
-    _lib.register("sl_rsvd_final_la", [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp])
+    _lib.register("sl_rsvd_bnd_workspace", [i32], C.c_int64)
+    _lib.register("sl_rsvd_boundary", [i32, vp, i64, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, i32,
+                                       vp, vp, vp, vp, vp, vp, vp])
     _lib.register("sl_rsvd_make_v", [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp])
     return _lib
 
@@ -38,20 +38,40 @@ def _graded(n, k, lo, hi, seed):
 
 
 def _ws(L, k, dev):
-    return torch.zeros(int(L.require().sl_rsvd_gram_workspace(k)), dtype=torch.uint8, device=dev)
+    return torch.zeros(int(L.require().sl_rsvd_bnd_workspace(k)), dtype=torch.uint8, device=dev)
+
+
+def _wg(W, Gy=None):
+    n, k = W.shape
+    WG = torch.zeros((n + k) * k, dtype=torch.float64, device="cuda")
+    WG[: n * k] = torch.from_numpy(np.ascontiguousarray(W).ravel()).to("cuda")
+    if Gy is not None:
+        WG[n * k:] = torch.from_numpy(np.ascontiguousarray(Gy).ravel()).to("cuda")
+    return WG
+
+
+def _inter(L, WG, n, k, ws, Rinv, Zt, st, s):
+    L.call("sl_rsvd_boundary", 0, None, 0, n, k, 0, _p(WG), _p(ws), _p(st), 1, _p(Rinv), _p(Zt),
+           None, None, None, 0, None, None, None, None, None, None, s)
+
+
+def _final(L, WG, n, k, r, ws, M, N, s64, st, V0, v0v, s):
+    L.call("sl_rsvd_boundary", 1, None, 0, n, k, r, _p(WG), _p(ws), _p(st), 1, None, None,
+           _p(M), _p(N), _p(s64), 0, _p(V0), _p(v0v), None, None, None, None, s)
 
 
 @pytest.mark.parametrize("n,k", [(1000, 40), (64, 17), (1024, 48), (16, 1)])
 def test_inter_la_is_cholesky_inverse(L, n, k):
     dev = torch.device("cuda")
     W = _graded(n, k, 0, 5, n + k)
-    Wd = torch.from_numpy(W).to(dev)
+    WG = _wg(W)
     ws = _ws(L, k, dev)
     Rinv = torch.empty(k, k, dtype=torch.float64, device=dev)
+    Zt = torch.empty(k, n, dtype=torch.bfloat16, device=dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     s = vp(torch.cuda.current_stream().cuda_stream)
     for _ in range(2):   # the ticket counter is reset for the next launch
-        L.call("sl_rsvd_inter_la", _p(Wd), n, k, k, _p(ws), _p(Rinv), _p(st), s)
+        _inter(L, WG, n, k, ws, Rinv, Zt, st, s)
     torch.cuda.synchronize()
     assert int(st[0]) == 0
     Ri = Rinv.cpu().numpy()
@@ -64,8 +84,6 @@ def test_inter_la_is_cholesky_inverse(L, n, k):
     assert np.abs(Ri.T @ H @ Ri - np.eye(k)).max() <= max(4 * e_ref, 1e-12)
     np.testing.assert_allclose(Ri, np.linalg.inv(R), rtol=1e-5, atol=1e-6 * np.abs(Ri).max())
     # next pass operand: Z^T = (W R^-1)^T in bf16
-    Zt = torch.empty(k, n, dtype=torch.bfloat16, device=dev)
-    L.call("sl_rsvd_make_zt", _p(Wd), n, k, k, _p(Rinv), _p(Zt), s)
     Zr = (W @ Ri).T
     np.testing.assert_allclose(Zt.double().cpu().numpy(), Zr, atol=8e-3 * np.abs(Zr).max())
 
@@ -75,11 +93,12 @@ def test_inter_la_drops_dependent_direction(L):
     n, k = 200, 12
     W = _graded(n, k, 0, 2, 3)
     W[:, 5] = W[:, 2] * 2.0          # exactly dependent column
-    Wd = torch.from_numpy(W).to(dev)
+    WG = _wg(W)
     ws = _ws(L, k, dev)
     Rinv = torch.empty(k, k, dtype=torch.float64, device=dev)
+    Zt = torch.empty(k, n, dtype=torch.bfloat16, device=dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
-    L.call("sl_rsvd_inter_la", _p(Wd), n, k, k, _p(ws), _p(Rinv), _p(st), vp(torch.cuda.current_stream().cuda_stream))
+    _inter(L, WG, n, k, ws, Rinv, Zt, st, vp(torch.cuda.current_stream().cuda_stream))
     torch.cuda.synchronize()
     assert int(st[0]) & 1
     Ri = Rinv.cpu().numpy()
@@ -96,7 +115,7 @@ def test_final_la_matches_fp64_core(L, n, k, r):
     W = _graded(n, k, -1, 4, 7 * k)
     Yg = g.randn(4 * k, k) @ np.diag(np.logspace(0, 2, k))
     Gy = Yg.T @ Yg
-    Wd, Gyd = torch.from_numpy(W).to(dev), torch.from_numpy(Gy).to(dev)
+    Wd, WG = torch.from_numpy(W).to(dev), _wg(W, Gy)
     ws = _ws(L, k, dev)
     M = torch.empty(k, r, device=dev)
     N = torch.empty(k, r, dtype=torch.float64, device=dev)
@@ -114,8 +133,7 @@ def test_final_la_matches_fp64_core(L, n, k, r):
     ev, Ub = ev[::-1][:r], Ub[:, ::-1][:, :r]
     outs = []
     for warm in (0, 1, 1):
-        L.call("sl_rsvd_final_la", _p(Wd), n, k, k, _p(Gyd), r, _p(ws), _p(M), _p(N), _p(s64), _p(st), 0,
-               _p(V0) if warm else None, _p(v0v) if warm else None, s)
+        _final(L, WG, n, k, r, ws, M, N, s64, st, V0 if warm else None, v0v if warm else None, s)
         torch.cuda.synchronize()
         assert int(st[0]) & ~1 == 0, int(st[0])
         sv = s64.cpu().numpy()
