@@ -540,30 +540,30 @@ __device__ void final_core(double* b0, double* b1, double* b2, double* b3, doubl
 }
 
 // ---------------------------------------------------------------- fused boundary
-// ONE launch at each pass boundary of a single-rank call, replacing the slab
-// reduce, the Gram / small-LA kernel and the Z^T kernel (+ V = W N after the last pass):
-//   1. workgroup b sums the pass's f32 W slabs of its BR rows (all slabs, f64
-//      accumulation) into LDS (and WG); FINAL: also its share of the fp64 Gram
-//      slabs (Y^T Y) into WG
+// ONE launch at each pass boundary, after the (full-chip) slab reduce and, on
+// several ranks, the all-reduce of [W; G]; it replaces the Gram / small-LA
+// kernel, the Z^T kernel and (after the last pass) the V = W N kernel:
+//   1. workgroup b loads its BR rows of W (one batch of loads) into LDS
 //   2. the packed upper partial Gram of its rows -> global, then a ticket
-//   3. the last arriving workgroup sums the partials (16-B loads, all of a
-//      batch in flight), runs the k x k algebra (INTER: Cholesky inverse;
-//      FINAL: final_core) and bumps the generation word (agent-scope release)
+//   3. the last arriving workgroup sums the partials (16-B loads, a batch in
+//      flight), runs the k x k algebra (INTER: Cholesky inverse; FINAL:
+//      final_core) and bumps the generation word (agent-scope release)
 //   4. every workgroup (the others spin on the generation word meanwhile; the
 //      <= BMAX workgroups are co-resident on the 256 CUs) forms its rows of
 //      the next pass operand Z^T = (W R^{-1})^T (INTER) or of V = W N (FINAL)
 //      from the W rows it still holds in LDS.
 // Graph replays: the last arriver resets the ticket; the generation only
 // grows (a waiter compares with the value it read before arriving).
-// Without slabs (wslab null) the rows come from WG (multi-rank: WG all-reduced).
+// (Summing the 256 pass slabs inside this kernel was measured: 63 workgroups
+// pulling 655 KB each of 2.5 KB pieces took 58 us, against 9 us for the
+// full-chip reduce kernel, so the reduce stays a launch of its own.)
 constexpr int BR = 16;     // rows of W per workgroup
 constexpr int BMAX = 64;   // workgroups (n <= 1024)
 constexpr int BK = 48;     // largest k of the pass
+constexpr int WLD = KMAX + 1;   // LDS row stride of the W rows (odd: rows on distinct banks)
 
 struct BndArgs {
-  const float* wslab;     // [nslab][n][k] f32 W slabs of the pass (null: rows from WG)
-  const double* gslab;    // [nslab][k][k] fp64 Gram slabs (FINAL with wslab)
-  int nslab, n, k, r;
+  int n, k, r;
   double* WG;             // [W (n x k); Gy (k x k)] f64
   double* part;           // BMAX packed partial Grams, stride ldp doubles
   int ldp;
@@ -588,7 +588,7 @@ enum : int { ST_TIMEOUT = 16 };
 
 // dynamic LDS: the small-LA layout (GRAM_LA_LDS), then the BR x KMAX rows of W
 constexpr size_t BND_WR_OFF = (GRAM_LA_LDS + 15) / 16 * 2;   // in doubles
-constexpr size_t BND_LDS = BND_WR_OFF * sizeof(double) + (size_t)BR * KMAX * sizeof(double);
+constexpr size_t BND_LDS = BND_WR_OFF * sizeof(double) + (size_t)BR * WLD * sizeof(double);
 
 template <bool FINAL>
 __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
@@ -605,113 +605,38 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   int* iscr = (int*)(red + RED);
   int* flags = iscr;
   int* order = iscr + 4;
-  double* Wr = sm + BND_WR_OFF;   // BR x KMAX rows of W
+  double* Wr = sm + BND_WR_OFF;   // BR x WLD rows of W
   __shared__ int st_sh;
   __shared__ int is_last;
   __shared__ unsigned gen0;
   const int r0 = blockIdx.x * BR;
   const int nr = min(BR, n - r0);
   const int E = nr * k;   // a multiple of 8 (n % 8 == 0)
+#ifdef SL_CORE_STAMPS
+  const unsigned long long st_start = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0) { SL_CST(0) }
+#endif
 
-  // ---- 1. this workgroup's rows of W
-  if (a.wslab) {
-    constexpr int U4 = BR * BK / 4 / 64;   // float4 per lane and slab
-    const int E4 = E >> 2;
-    const int64_t ss4 = (int64_t)n * k / 4;
-    const float4* base = (const float4*)(a.wslab + (int64_t)r0 * k);
-    double acc[U4][4];
+  // ---- 1. this workgroup's rows of W (E <= BR * BK = 768: two loads per
+  //      thread, both issued before the LDS stores, clamped addresses)
+  {
+    constexpr int UE = BR * BK / NT + 1;
+    double v[UE];
 #pragma unroll
-    for (int u = 0; u < U4; ++u)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[u][c] = 0.0;
-    const float4 z4 = {0.f, 0.f, 0.f, 0.f};
-    int s = wv;
-    // wave wv sums slabs wv, wv + 8, ...: four slabs' loads in flight
-    for (; s + 24 < a.nslab; s += 32) {
-      float4 v[4][U4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int u = 0; u < U4; ++u) {
-          const int j = lane + 64 * u;
-          v[q][u] = j < E4 ? base[(int64_t)(s + 8 * q) * ss4 + j] : z4;
-        }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int u = 0; u < U4; ++u) {
-          acc[u][0] += (double)v[q][u].x;
-          acc[u][1] += (double)v[q][u].y;
-          acc[u][2] += (double)v[q][u].z;
-          acc[u][3] += (double)v[q][u].w;
-        }
+    for (int u = 0; u < UE; ++u) {
+      const int e = tid + NT * u;
+      v[u] = a.WG[(int64_t)r0 * k + (e < E ? e : 0)];
     }
-    for (; s < a.nslab; s += 8) {
 #pragma unroll
-      for (int u = 0; u < U4; ++u) {
-        const int j = lane + 64 * u;
-        const float4 v = j < E4 ? base[(int64_t)s * ss4 + j] : z4;
-        acc[u][0] += (double)v.x;
-        acc[u][1] += (double)v.y;
-        acc[u][2] += (double)v.z;
-        acc[u][3] += (double)v.w;
+    for (int u = 0; u < UE; ++u) {
+      const int e = tid + NT * u;
+      if (e < E) {
+        const int row = e / k, col = e - row * k;
+        Wr[row * WLD + col] = v[u];
       }
-    }
-    // the 8 wave partials through LDS (b1..b2: 8 x BR * BK doubles)
-    double* P = b1;
-#pragma unroll
-    for (int u = 0; u < U4; ++u) {
-      const int j = lane + 64 * u;
-      if (j < E4)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) P[wv * (BR * BK) + 4 * j + c] = acc[u][c];
-    }
-    __syncthreads();
-    for (int e = tid; e < E; e += NT) {
-      double sum = 0.0;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) sum += P[w * (BR * BK) + e];
-      const int row = e / k, col = e - row * k;
-      Wr[row * KMAX + col] = sum;
-      a.WG[(int64_t)r0 * k + e] = sum;
-    }
-    if (FINAL) {
-      // this workgroup's share [g0, g1) of the k * k Gram entries
-      const int kk = k * k, ch = (kk + nb - 1) / nb;
-      const int g0 = blockIdx.x * ch, g1 = min(kk, g0 + ch);
-      for (int e0 = g0; e0 < g1; e0 += 64) {
-        __syncthreads();   // P reuse
-        const int e = e0 + lane;
-        double sum = 0.0;
-        if (e < g1) {
-          int t = wv;
-          for (; t + 56 < a.nslab; t += 64) {
-            double v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = a.gslab[(int64_t)(t + 8 * q) * kk + e];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) sum += v[q];
-          }
-          for (; t < a.nslab; t += 8) sum += a.gslab[(int64_t)t * kk + e];
-        }
-        P[wv * 64 + lane] = sum;
-        __syncthreads();
-        if (tid < 64 && e0 + tid < g1) {
-          double t = 0.0;
-#pragma unroll
-          for (int w = 0; w < 8; ++w) t += P[w * 64 + tid];
-          a.WG[(int64_t)n * k + e0 + tid] = t;
-        }
-      }
-    }
-  } else {
-    for (int e = tid; e < E; e += NT) {
-      const int row = e / k, col = e - row * k;
-      Wr[row * KMAX + col] = a.WG[(int64_t)r0 * k + e];
     }
   }
   __syncthreads();
-
   // ---- 2. packed upper partial Gram of the rows: thread (gq, cq) owns (gq + 8u, cq)
   {
     const int gq = wv, cq = lane;
@@ -720,9 +645,9 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     for (int u = 0; u < KMAX / 8; ++u) acc[u] = 0.0;
     if (cq < k) {
       for (int row = 0; row < nr; ++row) {
-        const double x = Wr[row * KMAX + cq];
+        const double x = Wr[row * WLD + cq];
 #pragma unroll
-        for (int u = 0; u < KMAX / 8; ++u) acc[u] += Wr[row * KMAX + gq + 8 * u] * x;
+        for (int u = 0; u < KMAX / 8; ++u) acc[u] += Wr[row * WLD + gq + 8 * u] * x;
       }
       double* myp = a.part + (int64_t)blockIdx.x * a.ldp;
 #pragma unroll
@@ -733,18 +658,25 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     }
   }
 
-  // ---- 3. ticket (every wave's stores released at agent scope first)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // ---- 3. ticket: every wave's stores complete, then ONE agent-scope release
+  //      (a fence per wave would write the L2 back once per wave)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
     gen0 = __hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(&a.sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = t == (unsigned)nb - 1;
+    if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     st_sh = 0;
   }
   __syncthreads();
+  if (blockIdx.x == 0) { SL_CST(2) }
   if (is_last) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#ifdef SL_CORE_STAMPS
+    if (tid == 0) g_core_st[10] = st_start;
+#endif
+    SL_CST(3)
     // sum of the nb packed partials, two entries per thread and load
     const int npair = a.ldp >> 1;
     const int kk2 = k * (k + 1) / 2;
@@ -752,12 +684,16 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     for (int p = tid; p < npair; p += NT) {
       const double2* src = (const double2*)a.part + p;
       double2 s2 = {0.0, 0.0};
-      for (int g0 = 0; g0 < nb; g0 += 16) {
-        double2 v[16];
+      for (int g0 = 0; g0 < nb; g0 += 32) {
+        // clamped addresses, all 32 loads in flight, out-of-range ones zeroed
+        double2 v[32];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = g0 + q < nb ? src[(int64_t)(g0 + q) * npair] : double2{0.0, 0.0};
+        for (int q = 0; q < 32; ++q) v[q] = src[(int64_t)min(g0 + q, nb - 1) * npair];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
+        for (int q = 0; q < 32; ++q)
+          if (g0 + q >= nb) v[q] = double2{0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
           s2.x += v[q].x;
           s2.y += v[q].y;
         }
@@ -774,6 +710,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     }
     __syncthreads();
     if (tid == 0) a.sync[0] = 0u;   // ready for the next launch
+    SL_CST(4)
     if (!FINAL) {
       chol_inv(b0, ld, b2, ld, k, &st_sh, red);
       for (int e = tid; e < k * k; e += NT) {
@@ -791,10 +728,15 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       final_core(b0, b1, b2, b3, red, flags, order, a.WG + (int64_t)n * k, k, a.r, a.M, a.N, a.s64, a.status,
                  a.max_sweeps, a.V0, a.v0_valid, a.mirror, &st_sh, a.status_or);
     }
+    SL_CST(5)
     // release the waiters
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&a.sync[16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(&a.sync[16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    SL_CST(6)
   } else {
     if (tid == 0) {
       // bounded wait (never reached on a sane run: the last arriver has no
@@ -807,11 +749,12 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
           break;
         }
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 
+  if (blockIdx.x == 0) { SL_CST(7) }
   // ---- 4. rows of Z^T = (W Rinv)^T (INTER) or V = W N (FINAL)
   float* V = FINAL ? (a.optr ? a.optr[2] : a.V) : nullptr;
   if (FINAL) {
@@ -822,7 +765,21 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   const int nc = FINAL ? a.r : k;
   const double* Bsrc = FINAL ? a.N : a.Rinv;
   double* Bs = b3;
-  for (int e = tid; e < k * nc; e += NT) Bs[e] = Bsrc[e];
+  {
+    // k * nc <= 48 * 48: five loads per thread in flight, then the stores
+    constexpr int UB = BK * BK / NT + 1;
+    double v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e = tid + NT * u;
+      v[u] = Bsrc[e < k * nc ? e : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e = tid + NT * u;
+      if (e < k * nc) Bs[e] = v[u];
+    }
+  }
   __syncthreads();
   const int row = tid & (BR - 1);
   if (row < nr) {
@@ -830,15 +787,19 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       double s0 = 0.0, s1 = 0.0;
       int l = 0;
       for (; l + 1 < k; l += 2) {
-        s0 += Wr[row * KMAX + l] * Bs[l * nc + c];
-        s1 += Wr[row * KMAX + l + 1] * Bs[(l + 1) * nc + c];
+        s0 += Wr[row * WLD + l] * Bs[l * nc + c];
+        s1 += Wr[row * WLD + l + 1] * Bs[(l + 1) * nc + c];
       }
-      if (l < k) s0 += Wr[row * KMAX + l] * Bs[l * nc + c];
+      if (l < k) s0 += Wr[row * WLD + l] * Bs[l * nc + c];
       const double v = s0 + s1;
       if (FINAL) V[(int64_t)(r0 + row) * nc + c] = (float)v;
       else a.Zt[(int64_t)c * n + r0 + row] = f_to_bf16((float)v);
     }
   }
+#ifdef SL_CORE_STAMPS
+  __syncthreads();
+  if (blockIdx.x == 0) { SL_CST(8) }
+#endif
 }
 
 // Out (rows of W, k x nc) = W (n x k f64) B (k x nc f64, row-major), a 32-row
@@ -1054,7 +1015,6 @@ SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void*
 }
 
 // ------------------------------------------------------------ fused boundary
-SL_API int sl_rsvd_pass_grid(int64_t m);
 
 // workspace of sl_rsvd_boundary: sync words (256 B, zeroed once; the kernel
 // leaves the ticket zero and only advances the generation) + BMAX partials
@@ -1063,28 +1023,20 @@ SL_API int64_t sl_rsvd_bnd_workspace(int k) {
   return 256 + (int64_t)BMAX * ldp * 8;
 }
 
-// One pass boundary of a single-rank call (pass_ws: the v4 pass slabs of an
-// m-row pass) or, with pass_ws null, from the all-reduced [W; G] in WG.
+// One pass boundary on the reduced (and, on several ranks, all-reduced)
+// [W (n x k); Gy (k x k)] f64 buffer WG.
 // final_ = 0: Rinv and Z^T (bf16, k x n) for the next pass.  final_ = 1: the
 // core (s64, M, N, status, mirror, warm start V0) and, when V or optr is
 // given, V = W N (n x r f32) and s (f32).  status_or = 0 stores the status
 // bits (the call's first writer), 1 ORs them.
-SL_API int sl_rsvd_boundary(int final_, const void* pass_ws, int64_t m, int n, int k, int r, double* WG, void* bws,
-                            int* status, int status_or, double* Rinv, void* Zt, float* M, double* N, double* s64,
-                            int max_sweeps, double* V0, int* v0_valid, int* mirror, float* V, float* s32,
-                            float* const* optr, void* stream) {
+SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* bws, int* status, int status_or,
+                            double* Rinv, void* Zt, float* M, double* N, double* s64, int max_sweeps, double* V0,
+                            int* v0_valid, int* mirror, float* V, float* s32, float* const* optr, void* stream) {
   if (k < 1 || k > BK || n < 16 || n > BMAX * BR || n % 8 || (final_ && (r < 1 || r > k))) {
     sl_set_last_error("rsvd_boundary: needs 1 <= k <= 48, 16 <= n <= 1024, n % 8 == 0, 1 <= r <= k");
     return SL_ERR_UNSUPPORTED;
   }
   BndArgs a{};
-  if (pass_ws) {
-    const int grid = sl_rsvd_pass_grid(m);
-    const char* base = (const char*)pass_ws;
-    a.wslab = (const float*)base;
-    a.gslab = (const double*)(base + (((int64_t)grid * n * k * 4 + 255) & ~(int64_t)255));
-    a.nslab = grid;
-  }
   a.n = n; a.k = k; a.r = r;
   a.WG = WG;
   a.sync = (unsigned*)bws;

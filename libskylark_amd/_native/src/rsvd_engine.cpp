@@ -39,10 +39,9 @@ SL_API int sl_rsvd_make_v_ind(const double* W, int n, int k, int ldw, const doub
                               float* const* optr, void* stream);
 SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* stream);
 SL_API int64_t sl_rsvd_bnd_workspace(int k);
-SL_API int sl_rsvd_boundary(int final_, const void* pass_ws, int64_t m, int n, int k, int r, double* WG, void* bws,
-                            int* status, int status_or, double* Rinv, void* Zt, float* M, double* N, double* s64,
-                            int max_sweeps, double* V0, int* v0_valid, int* mirror, float* V, float* s32,
-                            float* const* optr, void* stream);
+SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* bws, int* status, int status_or,
+                            double* Rinv, void* Zt, float* M, double* N, double* s64, int max_sweeps, double* V0,
+                            int* v0_valid, int* mirror, float* V, float* s32, float* const* optr, void* stream);
 SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, int k2, float* const* optr,
                              void* stream);
 SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
@@ -92,17 +91,21 @@ struct Plan {
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
-int seg(Plan* p, const void* A, int i, hipStream_t s) {
+// Segment i: [the boundary after pass i - 1] + pass i + its slab reduce
+// into [W; G] (between segments several ranks all-reduce [W; G]).  The
+// boundary is ONE launch (k_boundary): CholeskyQR of W and the next pass
+// operand, or after the last pass (segment q + 1, the boundary alone) the
+// fp64 core and, when V / s32 / optr are given, V = W N and s.
+int seg(Plan* p, const void* A, int i, hipStream_t s, float* V = nullptr, float* s32 = nullptr,
+        float* const* optr = nullptr) {
   const bool final_pass = i == p->q;
   if (i > p->q + 1 || i < 0) { sl_set_last_error("rsvd: segment out of range"); return SL_ERR_INVALID; }
   int rc = SL_OK;
   if (i > 0) {
-    // the boundary on the (all-reduced) [W; G]: CholeskyQR of W and the next
-    // pass operand, or after the last pass the core (V is left to the finish)
     const int fin = i == p->q + 1 ? 1 : 0;
-    rc = sl_rsvd_boundary(fin, nullptr, p->m, (int)p->n, p->k, p->r, p->WG, p->bnd_ws, p->status, 1, p->Rinv, p->Zt,
-                          p->M, p->N, p->s64, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr,
-                          p->mirror_dev, nullptr, nullptr, nullptr, s);
+    rc = sl_rsvd_boundary(fin, (int)p->n, p->k, p->r, p->WG, p->bnd_ws, p->status, 1, p->Rinv, p->Zt, p->M, p->N,
+                          p->s64, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr, p->mirror_dev,
+                          V, s32, optr, s);
     if (rc != SL_OK || fin) return rc;
   }
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
@@ -111,26 +114,6 @@ int seg(Plan* p, const void* A, int i, hipStream_t s) {
   // the first reduce of the call also clears the status word (no memset node)
   return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
                           p->k, i == 0 ? p->status : nullptr, s);
-}
-
-// Single-rank segment: pass i, preceded (i > 0) by ONE fused boundary launch
-// on the previous pass's slabs (reduce + Gram + Cholesky inverse + Z^T, or
-// after the last pass: reduce + the whole core + V = W N).  Segment q + 1 is
-// the final boundary alone.  V / s32 / optr: where the final boundary writes
-// V and s (all null: V is left to sl_rsvd_finish).
-int seg_fused(Plan* p, const void* A, int i, hipStream_t s, float* V, float* s32, float* const* optr) {
-  if (i > p->q + 1 || i < 0) { sl_set_last_error("rsvd: segment out of range"); return SL_ERR_INVALID; }
-  if (i > 0) {
-    const int fin = i == p->q + 1 ? 1 : 0;
-    // the call's first status writer stores (no memset node), later ones OR
-    const int rc = sl_rsvd_boundary(fin, p->pass_ws, p->m, (int)p->n, p->k, p->r, p->WG, p->bnd_ws, p->status,
-                                    i > 1 ? 1 : 0, p->Rinv, p->Zt, p->M, p->N, p->s64, 0,
-                                    p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr, p->mirror_dev,
-                                    V, s32, optr, s);
-    if (rc != SL_OK || fin) return rc;
-  }
-  return sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, i == p->q ? p->Y : nullptr, p->k,
-                      i == p->q ? 1 : 0, 0, s);
 }
 
 void drop_graph(Plan* p) {
@@ -165,7 +148,7 @@ int capture(Plan* p, const void* A, int with_finish, hipStream_t st) {
   SL_HIP_CHECK(hipStreamBeginCapture(cst, hipStreamCaptureModeThreadLocal));
   int rc = SL_OK;
   for (int i = 0; i <= p->q + 1 && rc == SL_OK; ++i)
-    rc = seg_fused(p, A, i, cst, nullptr, nullptr, with_finish ? p->optr : nullptr);
+    rc = seg(p, A, i, cst, nullptr, nullptr, with_finish ? p->optr : nullptr);
   if (rc == SL_OK && with_finish) rc = finish_ind(p, cst);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(cst, &g);
@@ -334,7 +317,7 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
   hipStream_t st = (hipStream_t)stream;
   if (!use_graph) {
     for (int i = 0; i <= p->q + 1; ++i) {
-      const int rc = seg_fused(p, A, i, st, V, s, nullptr);
+      const int rc = seg(p, A, i, st, V, s, nullptr);
       if (rc != SL_OK) return rc;
     }
     if (!V) return sl_rsvd_finish(plan, U, ldu, s, V, stream);

@@ -20,7 +20,7 @@ def L():
     from libskylark_amd.ops import _lib
     _lib.require()
     _lib.register("sl_rsvd_bnd_workspace", [i32], C.c_int64)
-    _lib.register("sl_rsvd_boundary", [i32, vp, i64, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, i32,
+    _lib.register("sl_rsvd_boundary", [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, i32,
                                        vp, vp, vp, vp, vp, vp, vp])
     _lib.register("sl_rsvd_make_v", [vp, i32, i32, i32, vp, i32, vp, vp, vp, vp])
     return _lib
@@ -51,12 +51,12 @@ def _wg(W, Gy=None):
 
 
 def _inter(L, WG, n, k, ws, Rinv, Zt, st, s):
-    L.call("sl_rsvd_boundary", 0, None, 0, n, k, 0, _p(WG), _p(ws), _p(st), 1, _p(Rinv), _p(Zt),
+    L.call("sl_rsvd_boundary", 0, n, k, 0, _p(WG), _p(ws), _p(st), 1, _p(Rinv), _p(Zt),
            None, None, None, 0, None, None, None, None, None, None, s)
 
 
 def _final(L, WG, n, k, r, ws, M, N, s64, st, V0, v0v, s):
-    L.call("sl_rsvd_boundary", 1, None, 0, n, k, r, _p(WG), _p(ws), _p(st), 1, None, None,
+    L.call("sl_rsvd_boundary", 1, n, k, r, _p(WG), _p(ws), _p(st), 1, None, None,
            _p(M), _p(N), _p(s64), 0, _p(V0), _p(v0v), None, None, None, None, s)
 
 
