@@ -879,8 +879,11 @@ k_make_v(const double* __restrict__ W, int n, int k, int ldw, const double* __re
 // with d the n Rademacher signs at stream offset baseD and p_j the k sampled
 // DCT-II frequencies at baseS (reference FJLT_data.hpp:79-86, sketch/fjlt.py)
 __global__ void __launch_bounds__(256)
-k_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, bf16_t* __restrict__ Zt) {
+k_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, bf16_t* __restrict__ Zt,
+          float** tab, float* ta, float* tb, float* tc) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the engine's {U, s, V} pointer table for this call (no launch of its own)
+  if (tab && t < 3) tab[t] = t == 0 ? ta : (t == 1 ? tb : tc);
   if (t >= (int64_t)n * k) return;
   const int j = (int)(t / n), i = (int)(t - (int64_t)j * n);
   const int64_t p = sl::uniform_int(sl::stream_block(seed, baseS + (uint64_t)j).x, 0, n - 1);
@@ -943,13 +946,19 @@ SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* str
   return SL_OK;
 }
 
-SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
-                           void* stream) {
+// tab (optional): {a, b, c} written by the same launch (the engine's pointer table)
+SL_API int sl_rsvd_fjlt_zt_tab(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
+                               float** tab, float* a, float* b, float* c, void* stream) {
   const int64_t tot = (int64_t)n * k;
   k_fjlt_zt<<<(unsigned)((tot + 255) / 256), 256, 0, (hipStream_t)stream>>>(seed, baseD, baseS, scale, k, n,
-                                                                            (bf16_t*)Zt);
+                                                                            (bf16_t*)Zt, tab, a, b, c);
   SL_LAUNCH_CHECK();
   return SL_OK;
+}
+
+SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
+                           void* stream) {
+  return sl_rsvd_fjlt_zt_tab(seed, baseD, baseS, scale, k, n, Zt, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 // Standalone symmetric eigensolver on the device (same Jacobi), for tests:

@@ -44,6 +44,8 @@ SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* b
                             int* v0_valid, int* mirror, float* V, float* s32, float* const* optr, void* stream);
 SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, int k2, float* const* optr,
                              void* stream);
+SL_API int sl_rsvd_fjlt_zt_tab(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
+                               float** tab, float* a, float* b, float* c, void* stream);
 SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
                            void* stream);
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
@@ -69,6 +71,11 @@ struct Plan {
   void* bnd_ws = nullptr;   // fused boundary: sync words + partial Grams (zeroed once)
   float* last_ptrs[3] = {nullptr, nullptr, nullptr};   // optr contents written last (and on which stream)
   hipStream_t last_ptrs_stream = nullptr;
+  // FJLT operator set for the next call but not yet launched: the run launches
+  // it together with the pointer-table write (one small kernel, not two)
+  bool fjlt_pending = false;
+  uint64_t fj_seed = 0, fj_baseD = 0, fj_baseS = 0;
+  double fj_scale = 0.0;
   double* Rinv = nullptr;   // k x k
   float* M = nullptr;       // k x r
   double* N = nullptr;      // k x r
@@ -90,6 +97,15 @@ struct Plan {
 };
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+// launch a deferred FJLT operator (and, with tab, the pointer-table write)
+int flush_fjlt(Plan* p, hipStream_t s, float** tab = nullptr, float* a = nullptr, float* b = nullptr,
+               float* c = nullptr) {
+  if (!p->fjlt_pending) return SL_OK;
+  p->fjlt_pending = false;
+  return sl_rsvd_fjlt_zt_tab(p->fj_seed, p->fj_baseD, p->fj_baseS, p->fj_scale, p->k, (int)p->n, p->Zt, tab, a, b,
+                             c, s);
+}
 
 // Segment i: [the boundary after pass i - 1] + pass i + its slab reduce
 // into [W; G] (between segments several ranks all-reduce [W; G]).  The
@@ -267,9 +283,13 @@ SL_API int sl_rsvd_plan_set_warm(void* plan, int warm) {
 // Sketch operator of the call: the FJLT of reference FJLT_data (N Rademacher
 // signs at baseD, k DCT frequencies at baseS, scale sqrt(n / k)) realised as
 // the pass's bf16 Z^T.
+// (deferred: launched by the next run / first segment, in that call's stream order)
 SL_API int sl_rsvd_set_fjlt(void* plan, uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, void* stream) {
+  (void)stream;
   Plan* p = (Plan*)plan;
-  return sl_rsvd_fjlt_zt(seed, baseD, baseS, scale, p->k, (int)p->n, p->Zt, stream);
+  p->fjlt_pending = true;
+  p->fj_seed = seed; p->fj_baseD = baseD; p->fj_baseS = baseS; p->fj_scale = scale;
+  return SL_OK;
 }
 
 // Dense sketch operator (JLT: Normal, CT: Cauchy, ...) of the call: the k x n
@@ -279,6 +299,7 @@ SL_API int sl_rsvd_set_fjlt(void* plan, uint64_t seed, uint64_t baseD, uint64_t 
 SL_API int sl_rsvd_set_dense(void* plan, int dist, uint64_t seed, uint64_t base, double p0, double p1, double scale,
                              void* stream) {
   Plan* p = (Plan*)plan;
+  p->fjlt_pending = false;
   int rc = sl_fill_random(p->WG, SL_F64, dist, seed, base, p->k, p->n, p->n, 1, 0, 0, 1, p->k, p0, p1, scale, 1,
                           stream);
   if (rc != SL_OK) return rc;
@@ -288,11 +309,20 @@ SL_API int sl_rsvd_set_dense(void* plan, int dist, uint64_t seed, uint64_t base,
 // Sketch operator given explicitly (k x n bf16, device).
 SL_API int sl_rsvd_set_zt(void* plan, const void* Zt, void* stream) {
   Plan* p = (Plan*)plan;
+  p->fjlt_pending = false;
   SL_HIP_CHECK(hipMemcpyAsync(p->Zt, Zt, (size_t)(p->n * p->k * 2), hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return SL_OK;
 }
 
+// launch a deferred sketch operator now (callers that replay their own
+// captured segments flush before the replay)
+SL_API int sl_rsvd_flush(void* plan, void* stream) { return flush_fjlt((Plan*)plan, (hipStream_t)stream); }
+
 SL_API int sl_rsvd_segment(void* plan, const void* A, int i, void* stream) {
+  if (i == 0) {
+    const int rc = flush_fjlt((Plan*)plan, (hipStream_t)stream);
+    if (rc != SL_OK) return rc;
+  }
   return seg((Plan*)plan, A, i, (hipStream_t)stream);
 }
 
@@ -316,6 +346,8 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
   Plan* p = (Plan*)plan;
   hipStream_t st = (hipStream_t)stream;
   if (!use_graph) {
+    int rc0 = flush_fjlt(p, st);
+    if (rc0 != SL_OK) return rc0;
     for (int i = 0; i <= p->q + 1; ++i) {
       const int rc = seg(p, A, i, st, V, s, nullptr);
       if (rc != SL_OK) return rc;
@@ -327,19 +359,31 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
   // the finish joins the graph when its streaming kernel can take this U
   // (contiguous rows, 16-byte aligned) -- else a plain launch after it
   const int fin = (p->k % 8 == 0 && ldu == p->r && ((uintptr_t)U & 15) == 0 && V != nullptr) ? 1 : 0;
+  // the table already holds U / s / V when the last call on this stream
+  // wrote the same ones (a caching allocator hands them back); else the
+  // deferred FJLT launch writes it, or a one-thread kernel
+  const bool need_tab = fin && !(p->last_ptrs[0] == U && p->last_ptrs[1] == s && p->last_ptrs[2] == V &&
+                                 p->last_ptrs_stream == st);
+  if (need_tab && p->fjlt_pending) {
+    const int rc = flush_fjlt(p, st, p->optr, U, s, V);
+    if (rc != SL_OK) return rc;
+  } else {
+    const int rc = flush_fjlt(p, st);
+    if (rc != SL_OK) return rc;
+    if (need_tab) {
+      const int rc2 = sl_rsvd_set_ptrs(p->optr, U, s, V, st);
+      if (rc2 != SL_OK) return rc2;
+    }
+  }
+  if (need_tab) {
+    p->last_ptrs[0] = U; p->last_ptrs[1] = s; p->last_ptrs[2] = V;
+    p->last_ptrs_stream = st;
+  }
   if (!p->exec[fin]) {
     const int rc = capture(p, A, fin, st);
     if (rc != SL_OK) return rc;
   }
   if (fin) {
-    // the table already holds these pointers when the last call on this
-    // stream wrote the same ones (a caching allocator hands them back)
-    if (!(p->last_ptrs[0] == U && p->last_ptrs[1] == s && p->last_ptrs[2] == V && p->last_ptrs_stream == st)) {
-      int rc = sl_rsvd_set_ptrs(p->optr, U, s, V, st);
-      if (rc != SL_OK) return rc;
-      p->last_ptrs[0] = U; p->last_ptrs[1] = s; p->last_ptrs[2] = V;
-      p->last_ptrs_stream = st;
-    }
     SL_HIP_CHECK(hipGraphLaunch(p->exec[1], st));
     return SL_OK;
   }
@@ -352,6 +396,8 @@ SL_API int sl_rsvd_run(void* plan, const void* A, int use_graph, float* U, int64
 SL_API int sl_rsvd_run_comm(void* plan, const void* A, void* comm, float* U, int64_t ldu, float* s, float* V,
                             void* stream) {
   Plan* p = (Plan*)plan;
+  const int rc0 = flush_fjlt(p, (hipStream_t)stream);
+  if (rc0 != SL_OK) return rc0;
   for (int i = 0; i <= p->q + 1; ++i) {
     int rc = seg(p, A, i, (hipStream_t)stream);
     if (rc != SL_OK) return rc;

@@ -291,6 +291,7 @@ def _engine_lib():
         _lib.register("sl_rsvd_run", [vp_, vp_, i32_, vp_, i64_, vp_, vp_, vp_])
         _lib.register("sl_rsvd_plan_bind", [vp_, vp_, vp_])
         _lib.register("sl_rsvd_status_mirror", [vp_], vp_)
+        _lib.register("sl_rsvd_flush", [vp_, vp_])
     return _lib
 
 
@@ -386,6 +387,8 @@ class _EnginePlan:
             L.call("sl_rsvd_run", self.h, ctypes.c_void_p(A.data_ptr()), 1 if warm else 0,
                    ctypes.c_void_p(U.data_ptr()), r, ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(V.data_ptr()), st)
         else:
+            # the deferred FJLT operator launches here, never inside a capture
+            L.call("sl_rsvd_flush", self.h, st)
             if warm and self.g is None and not self.g_failed and self._collectives_capturable():
                 try:
                     g = torch.cuda.CUDAGraph()
