@@ -411,14 +411,15 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
 __device__ void final_core(double* b0, double* b1, double* b2, double* b3, double* red, int* flags, int* order,
                            const double* Gy, int k, int r, float* __restrict__ M, double* __restrict__ N,
                            double* __restrict__ s_out, int* __restrict__ status, int max_sweeps, double* V0,
-                           int* v0_valid, int* mirror, int* st_sh_p, int status_or) {
+                           int* v0_valid, int* mirror, int* st_sh_p, int status_or, bool rti_given = false) {
   int& st_sh = *st_sh_p;
   const int tid = threadIdx.x;
   const int ld = k + 1;
   constexpr int SO = 16;
   (void)SO;
-  // ---- FINAL: Y^T Y = Rt^T Rt, Rti = Rt^{-1} -> b3 (straight from Gy; H in b0 survives)
-  chol_inv(Gy, k, b3, ld, k, st_sh_p, red);
+  // ---- FINAL: Y^T Y = Rt^T Rt, Rti = Rt^{-1} -> b3 (straight from Gy; H in b0
+  //      survives), unless the caller already placed Rti in b3
+  if (!rti_given) chol_inv(Gy, k, b3, ld, k, st_sh_p, red);
   SL_CST(SO + 3)
   // C = Rti^T H Rti:  T = H Rti -> b1, C = Rti^T T -> b2
   small_gemm(b0, b3, b1, k, ld, false);
@@ -564,10 +565,12 @@ constexpr int WLD = KMAX + 1;   // LDS row stride of the W rows (odd: rows on di
 
 struct BndArgs {
   int n, k, r;
+  int nbr;                // workgroups holding rows (FINAL: one more, the Y^T Y Cholesky worker)
+  double* rti;            // FINAL: the worker's Rt^{-1} (k x k) and status word
   double* WG;             // [W (n x k); Gy (k x k)] f64
   double* part;           // BMAX packed partial Grams, stride ldp doubles
   int ldp;
-  unsigned* sync;         // [0] ticket, [16] generation
+  unsigned* sync;         // [0] ticket, [16] generation, [32] FINAL worker epoch
   int* status;
   int status_or;
   double* Rinv;           // INTER: k x k
@@ -594,7 +597,7 @@ template <bool FINAL>
 __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int n = a.n, k = a.k, nb = gridDim.x;
+  const int n = a.n, k = a.k, nb = a.nbr;
   const int ld = k + 1;
   const int mat = KMAX * (KMAX + 1);
   double* b0 = sm;
@@ -609,6 +612,28 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   __shared__ int st_sh;
   __shared__ int is_last;
   __shared__ unsigned gen0;
+  if (FINAL && (int)blockIdx.x == nb) {
+    // the Y^T Y worker: Rt^{-1} of the reduced Gram (independent of W) while
+    // the row workgroups form and sum H; published with the launch's epoch
+    if (tid == 0) {
+      gen0 = __hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_sh = 0;
+    }
+    __syncthreads();
+    chol_inv(a.WG + (int64_t)n * k, k, b3, ld, k, &st_sh, red);
+    for (int e = tid; e < k * k; e += NT) {
+      const int i = e / k, c = e - i * k;
+      a.rti[e] = b3[i * ld + c];
+    }
+    if (tid == 0) ((int*)(a.rti + k * k))[0] = st_sh;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&a.sync[32], gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   const int r0 = blockIdx.x * BR;
   const int nr = min(BR, n - r0);
   const int E = nr * k;   // a multiple of 8 (n % 8 == 0)
@@ -725,8 +750,40 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
         else __hip_atomic_store(a.status, st_sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else {
+      // the worker's Rt^{-1} (bounded wait for this launch's epoch)
+      if (tid == 0) {
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(&a.sync[32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen0 + 1u) {
+          __builtin_amdgcn_s_sleep(1);
+          if (wall_clock64() - t0 > 200000000ull) {
+            st_sh |= ST_TIMEOUT;
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        st_sh |= ((const int*)(a.rti + k * k))[0];
+      }
+      __syncthreads();
+      {
+        constexpr int UB = BK * BK / NT + 1;
+        double v[UB];
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int e = tid + NT * u;
+          v[u] = a.rti[e < k * k ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          const int e = tid + NT * u;
+          if (e < k * k) {
+            const int i = e / k, c = e - i * k;
+            b3[i * ld + c] = v[u];
+          }
+        }
+      }
+      __syncthreads();
       final_core(b0, b1, b2, b3, red, flags, order, a.WG + (int64_t)n * k, k, a.r, a.M, a.N, a.s64, a.status,
-                 a.max_sweeps, a.V0, a.v0_valid, a.mirror, &st_sh, a.status_or);
+                 a.max_sweeps, a.V0, a.v0_valid, a.mirror, &st_sh, a.status_or, true);
     }
     SL_CST(5)
     // release the waiters
@@ -1029,7 +1086,7 @@ SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void*
 // leaves the ticket zero and only advances the generation) + BMAX partials
 SL_API int64_t sl_rsvd_bnd_workspace(int k) {
   const int64_t ldp = ((int64_t)k * (k + 1) / 2 + 1) & ~(int64_t)1;
-  return 256 + (int64_t)BMAX * ldp * 8;
+  return 256 + (int64_t)BMAX * ldp * 8 + (int64_t)k * k * 8 + 256;
 }
 
 // One pass boundary on the reduced (and, on several ranks, all-reduced)
@@ -1051,6 +1108,7 @@ SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* b
   a.sync = (unsigned*)bws;
   a.part = (double*)((char*)bws + 256);
   a.ldp = (int)(((int64_t)k * (k + 1) / 2 + 1) & ~(int64_t)1);
+  a.rti = a.part + (int64_t)BMAX * a.ldp;
   a.status = status;
   a.status_or = status_or;
   a.Rinv = Rinv;
@@ -1060,6 +1118,7 @@ SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* b
   a.V0 = V0; a.v0_valid = v0_valid; a.mirror = mirror;
   a.V = V; a.s32 = s32; a.optr = optr;
   const unsigned nb = (unsigned)((n + BR - 1) / BR);
+  a.nbr = (int)nb;
   hipStream_t s = (hipStream_t)stream;
   if (final_) {
     static bool attr = false;
@@ -1068,7 +1127,7 @@ SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* b
                                        (int)BND_LDS));
       attr = true;
     }
-    k_boundary<true><<<nb, NT, BND_LDS, s>>>(a);
+    k_boundary<true><<<nb + 1, NT, BND_LDS, s>>>(a);   // + the Y^T Y worker
   } else {
     if (!Rinv || !Zt) { sl_set_last_error("rsvd_boundary: Rinv and Zt required"); return SL_ERR_INVALID; }
     static bool attr = false;

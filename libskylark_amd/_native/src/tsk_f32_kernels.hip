@@ -306,12 +306,13 @@ k_xm_pipe(const float* __restrict__ Y, int64_t m, int k, const float* __restrict
   // optr: the output pointer read from device memory (a graph node whose
   // destination changes every replay)
   if (optr) out = optr[0];
-  __shared__ float tin[WPB][32 * (KMAX + 1)];
-  __shared__ float tout[WPB][32 * 32 * KT2];
+  // wave tiles sized by k / k2 (dynamic LDS: xm_pipe_lds): 32 x (k + 1) in,
+  // 32 x k2 out -- 31 KB per block at k = 40, k2 = 20, five blocks per CU
+  extern __shared__ __attribute__((aligned(16))) float xsm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c = lane & 31;
-  float* Ti = tin[w];
-  float* To = tout[w];
+  float* Ti = xsm + w * 32 * (k + 1);
+  float* To = xsm + WPB * 32 * (k + 1) + w * 32 * k2;
   const int lda = k + 1;
   float mreg[KMAX / 2][KT2];
 #pragma unroll
@@ -415,6 +416,16 @@ k_xm_bf16t(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, const flo
 }
 
 constexpr int XM_PIPE_GRID_MAX = 2048;
+size_t xm_pipe_lds(int k, int k2) {
+  const size_t b = (size_t)WPB * 32 * ((k + 1) + k2) * sizeof(float);
+  static bool attr = false;
+  if (b > 64 * 1024 && !attr) {   // k, k2 near 64: past the default dynamic-LDS cap
+    (void)hipFuncSetAttribute((const void*)k_xm_pipe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_xm_pipe<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    attr = true;
+  }
+  return b;
+}
 
 constexpr int G64_PIPE_GRID_MAX = 1024;
 
@@ -486,8 +497,9 @@ SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, i
   }
   int64_t gx = (m + WPB * 32 - 1) / (WPB * 32);
   if (gx > XM_PIPE_GRID_MAX) gx = XM_PIPE_GRID_MAX;
-  if (k2 > 32) k_xm_pipe<2><<<(int)gx, 256, 0, (hipStream_t)stream>>>(Y, m, k, M, k2, nullptr, optr);
-  else k_xm_pipe<1><<<(int)gx, 256, 0, (hipStream_t)stream>>>(Y, m, k, M, k2, nullptr, optr);
+  const size_t lds = xm_pipe_lds(k, k2);
+  if (k2 > 32) k_xm_pipe<2><<<(int)gx, 256, lds, (hipStream_t)stream>>>(Y, m, k, M, k2, nullptr, optr);
+  else k_xm_pipe<1><<<(int)gx, 256, lds, (hipStream_t)stream>>>(Y, m, k, M, k2, nullptr, optr);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -511,8 +523,9 @@ SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const fl
       ((uintptr_t)out & 15) == 0) {
     int64_t gx = (m + WPB * 32 - 1) / (WPB * 32);
     if (gx > XM_PIPE_GRID_MAX) gx = XM_PIPE_GRID_MAX;
-    if (two) k_xm_pipe<2><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out, nullptr);
-    else k_xm_pipe<1><<<(int)gx, 256, 0, s>>>(Y, m, k, M, k2, out, nullptr);
+    const size_t lds = xm_pipe_lds(k, k2);
+    if (two) k_xm_pipe<2><<<(int)gx, 256, lds, s>>>(Y, m, k, M, k2, out, nullptr);
+    else k_xm_pipe<1><<<(int)gx, 256, lds, s>>>(Y, m, k, M, k2, out, nullptr);
     SL_LAUNCH_CHECK();
     return SL_OK;
   }
