@@ -1,7 +1,7 @@
 #!/bin/bash
 # multi-rank rehearsal on the one GPU of the box: multirank / one-shot tests,
 # then bench.py under torchrun with 2 and 4 ranks sharing the GPU (gloo: RCCL
-# refuses two ranks on one device; one-shot IPC all-reduce still used; answer
+# refuses two ranks on one device; answer
 # checks; timings are not scaling numbers)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
