@@ -441,6 +441,22 @@ __device__ __forceinline__ void reduce_body(const IT* __restrict__ slab, int nsl
   double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
   if (e0 + 1 < total) {
     int s = v;
+    // eight slabs' loads in flight per wave (a round trip to the slabs is
+    // ~0.5 us; two in flight left the reduce latency-bound)
+    for (; s + 56 < nslab; s += 64) {
+      IT x0[8], x1[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const IT* p = slab + (int64_t)(s + 8 * q) * total + e0;
+        x0[q] = p[0];
+        x1[q] = p[1];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        a0 += (double)x0[q]; a1 += (double)x1[q];
+        b0 += (double)x0[q + 1]; b1 += (double)x1[q + 1];
+      }
+    }
     for (; s + 8 < nslab; s += 16) {
       const IT* p = slab + (int64_t)s * total + e0;
       const IT* q = p + 8 * total;
