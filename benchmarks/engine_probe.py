@@ -30,7 +30,6 @@ _lib.register("sl_rsvd_set_fjlt", [vp, u64, u64, u64, f64, vp])
 _lib.register("sl_rsvd_run", [vp, vp, i32, vp, i64, vp, vp, vp])
 _lib.register("sl_rsvd_status", [vp, C.POINTER(i32), vp])
 _lib.register("sl_sym_eig_jacobi2", [vp, i32, vp, vp, vp, i32, vp])
-_lib.register("sl_rsvd_plan_set_warm", [vp, i32])
 
 
 def jacobi_check(dev):
@@ -109,9 +108,6 @@ def main():
 
     plan = vp()
     _lib.call("sl_rsvd_plan_create", m, n, A.stride(0), k, r, q, C.byref(plan))
-    plan_cold = vp()
-    _lib.call("sl_rsvd_plan_create", m, n, A.stride(0), k, r, q, C.byref(plan_cold))
-    _lib.call("sl_rsvd_plan_set_warm", plan_cold, 0)
     st = vp(torch.cuda.current_stream().cuda_stream)
     ctx = sk.Context(seed=38734)
     base_d = ctx.counter
@@ -141,7 +137,7 @@ def main():
                           "U_subspace_min_cos": float(sv.min()), "orth_err": orth, "resid_rel": resid,
                           "s_top3": [round(float(x), 3) for x in s[:3]], "s_py_top3": [round(float(x), 3) for x in s0[:3]]}),
               flush=True)
-    ts = {"engine_graph": [], "engine_graph_cold": [], "python_path": []}
+    ts = {"engine_graph": [], "python_path": []}
     for _ in range(5):
         for name in ts:
             torch.cuda.synchronize()
@@ -150,8 +146,6 @@ def main():
             for _ in range(10):
                 if name == "engine_graph":
                     call(1)
-                elif name == "engine_graph_cold":
-                    call(1, plan_cold)
                 else:
                     sk.nla.approximate_svd(A, r, context=sk.Context(seed=38734), params=params)
             e1.record()

@@ -336,6 +336,16 @@ inline PlanCache& plans() {
   return c;
 }
 
+inline void drop_rsvd_plan(void* plan) {
+  auto& v = plans().v;
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i].second == plan) {
+      lib().plan_destroy(plan);
+      v.erase(v.begin() + (long)i);
+      return;
+    }
+}
+
 // U (m x rank f32), S (rank f32, any 1-column / 1-row shape), V (n x rank f32)
 // of bf16 A (m x n, m >= n).  ctr: the context counter (advanced by the
 // sketch's draws exactly as the runtime advances it).  comm (a NativeComm
@@ -419,6 +429,12 @@ inline int approximate_svd(const DevMat& A, const DevMat& U, const DevMat& Sv, c
   }
   int status = 0;
   SLDEV_TRY(L.status(plan, &status, st), "rsvd status");
+  if (status & 16) {
+    // a pass-boundary wait timed out: the outputs are invalid and the plan's
+    // sync words are mid-protocol -- drop it so the next call builds a fresh one
+    drop_rsvd_plan(plan);
+    return fail(106, "device approximate_svd: a pass-boundary kernel timed out (status 16); outputs invalid");
+  }
   if (status & 2) return fail(108, "device approximate_svd: non-finite values in A");
   return 0;
 }

@@ -29,6 +29,14 @@ enum SlError : int {
 
 void sl_set_last_error(const char* msg);
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize, bytes) once per (kernel, device)
+int sl_lds_attr(const void* fn, int bytes);
+#define SL_LDS_ATTR(fn, bytes)                                   \
+  do {                                                           \
+    const int _rc = sl_lds_attr((const void*)(fn), (int)(bytes)); \
+    if (_rc != SL_OK) return _rc;                                \
+  } while (0)
+
 typedef uint16_t bf16_t;
 
 __host__ __device__ __forceinline__ float bf16_to_f(bf16_t v) {

@@ -1,0 +1,524 @@
+// Latency-oriented small dense linear algebra for ONE workgroup on gfx950:
+// the k x k (k <= 64) algebra of the randomized SVD's pass boundaries
+// (reference nla/svd.hpp:71-149 re-orthonormalisation, :278-317 the core SVD
+// of the k x k Rayleigh-Ritz matrix), where every microsecond is on the
+// critical path of the call.
+//
+// Design rules (MI355X: one wave issues an f64 FMA every ~4-8 cycles, a DS
+// read returns in ~50 cycles, an 8-wave s_barrier costs ~100+):
+//   * the sequential k-step factorisations run in ONE wave with the matrix
+//     in registers (lane = row or column, register index = the other index,
+//     every step unrolled at a compile-time K so register indices are
+//     static): no workgroup barrier inside the chain, only wave-local LDS
+//     broadcasts and DPP reductions;
+//   * the embarrassingly parallel phases (bisection per eigenvalue, the
+//     back-transformation per eigenvector) spread over all waves.
+//
+//   wave_chol_inv<K>   X = R^{-1} of G = R^T R: in-place LDL^T elimination of
+//                      [G | I] with lane c holding column c of whichever half
+//                      is live (T column c until pivot c, then L^{-1} column c)
+//   wave_tridiag<K>    Householder tridiagonalisation T = Q^T C Q (lane = row)
+//   sym_top_eig<K>     top-nt eigenvalues of T by multisection on a
+//                      division-free Sturm count, eigenvectors of T by the
+//                      twisted factorisation, MGS inside close clusters, and
+//                      the back-transformation Q x (16 lanes per vector)
+#pragma once
+#include "sl_common.hpp"
+
+// diagnostic builds only (benchmarks/native, -DSL_EIG_STAMPS): shader-clock
+// stamps at the phase boundaries of the solvers below
+#ifdef SL_EIG_STAMPS
+__device__ unsigned long long g_eig_st[64];
+#define SLW_STAMP(I) \
+  if (threadIdx.x == 0) g_eig_st[(I)] = __builtin_amdgcn_s_memtime();
+#else
+#define SLW_STAMP(I)
+#endif
+
+namespace slw {
+
+// ------------------------------------------------------------ wave helpers
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+  // every pattern used here is a full permutation (no invalid source lane):
+  // mov_dpp needs no initialised destination
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// value of x in lane l (l wave-uniform)
+__device__ __forceinline__ double lane_d(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+
+// sum over each DPP row of 16 lanes, result in every lane of the row
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp<0x141>(x);   // row_half_mirror
+  x += dpp<0x140>(x);   // row_mirror
+  return x;
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+  x = row16_sum(x);
+  return (lane_d(x, 0) + lane_d(x, 16)) + (lane_d(x, 32) + lane_d(x, 48));
+}
+
+__device__ __forceinline__ double wave_max(double x) {
+  x = fmax(x, dpp<0xB1>(x));
+  x = fmax(x, dpp<0x4E>(x));
+  x = fmax(x, dpp<0x141>(x));
+  x = fmax(x, dpp<0x140>(x));
+  return fmax(fmax(lane_d(x, 0), lane_d(x, 16)), fmax(lane_d(x, 32), lane_d(x, 48)));
+}
+
+__device__ __forceinline__ double wave_min(double x) {
+  x = fmin(x, dpp<0xB1>(x));
+  x = fmin(x, dpp<0x4E>(x));
+  x = fmin(x, dpp<0x141>(x));
+  x = fmin(x, dpp<0x140>(x));
+  return fmin(fmin(lane_d(x, 0), lane_d(x, 16)), fmin(lane_d(x, 32), lane_d(x, 48)));
+}
+
+// LDS written by this wave is visible to this wave's later reads (and the
+// compiler may not move LDS accesses across it)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// f64 reciprocal / reciprocal square root: hardware estimate + two Newton steps
+__device__ __forceinline__ double rcp64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = r * fma(-d, r, 2.0);
+  r = r * fma(-d, r, 2.0);
+  return r;
+}
+__device__ __forceinline__ double rsq64(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  r = r * fma(-0.5 * d * r, r, 1.5);
+  r = r * fma(-0.5 * d * r, r, 1.5);
+  return r;
+}
+
+// ------------------------------------------------------ Cholesky inverse
+// X = R^{-1} (upper, k x k) of G = R^T R, by ONE wave (all 64 lanes call it).
+// LDL^T elimination of the augmented [G | I] by columns, in place: lane c
+// keeps column c of the live half in registers -- the trailing G column
+// until pivot c, then column c of L^{-1} (L^{-1}[j][c] = 0 for c > j and
+// G[.][c] is dead for c <= j, so one array serves both).  The multiplier of
+// row i at pivot j is G[j][i] / d_j, held by lane i itself (the trailing
+// block is symmetric), so a step is: readlane the pivot, every lane
+// publishes its multiplier to LDS, one broadcast read, one FMA per live
+// entry, and the pivot lane (exec-masked) switches its column to
+// (0 .. 1, -f_{j+1} .. -f_{K-1}).  X[c][i] = L^{-1}[i][c] d_i^{-1/2}.  A pivot
+// at or below 1e-13 max_i G_ii drops its direction (column and row of X
+// zero) and sets bit 1 of *st.  G / X: LDS or global (ldg, ldx); fsh: >= 192
+// doubles of 16-B aligned LDS.  k <= K <= 64; the padding is the identity.
+template <int K>
+__device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
+                                              int* st) {
+  static_assert(K % 2 == 0 && K <= 64, "K");
+  const int c = threadIdx.x & 63;
+  double A[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) A[i] = (i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0);
+  const double thr = 1e-13 * wave_max(c < k ? fabs(G[c * ldg + c]) : 0.0);
+  double* rsh = fsh + 128;   // d_j^{-1/2}
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double d = lane_d(A[j], j);
+    const bool ok = (d > thr && d == d) || j >= k;
+    bad |= !ok;
+    const double r = ok ? rcp64(d) : 0.0;
+    if (c == 0) rsh[j] = ok ? rsq64(d) : 0.0;
+    if (j + 1 < K) {
+      double* fb_ = fsh + (j & 1) * 64;   // double-buffered: no second sync per step
+      fb_[c] = A[j] * r;    // multiplier of row c (valid for c > j)
+      wave_lds_sync();
+      const double aj = A[j];
+#pragma unroll
+      for (int i = (j + 1) & ~1; i < K; i += 2) {
+        const double2 f = *(const double2*)(fb_ + i);
+        if (i > j) A[i] = fma(-f.x, aj, A[i]);
+        A[i + 1] = fma(-f.y, aj, A[i + 1]);
+      }
+      if (c == j) {
+#pragma unroll
+        for (int i = (j + 1) & ~1; i < K; i += 2) {
+          const double2 f = *(const double2*)(fb_ + i);
+          if (i > j) A[i] = -f.x;
+          A[i + 1] = -f.y;
+        }
+      }
+    }
+    if (c == j) A[j] = 1.0;
+  }
+  if (bad && c == 0) atomicOr(st, 1);
+  wave_lds_sync();
+  if (c < k) {
+#pragma unroll
+    for (int i = 0; i < K; i += 2) {
+      const double2 rr = *(const double2*)(rsh + i);
+      if (i < k) X[c * ldx + i] = i >= c ? A[i] * rr.x : 0.0;
+      if (i + 1 < k) X[c * ldx + i + 1] = i + 1 >= c ? A[i + 1] * rr.y : 0.0;
+    }
+  }
+}
+
+// ------------------------------------------------- tridiagonalisation
+// T = Q^T C Q, Q = H_0 H_1 ... H_{K-3}, H_j = I - 2 v_j v_j^T, by ONE wave:
+// lane i keeps row i of the trailing matrix in registers.  Step j: ||x||
+// of column j below the diagonal (DPP sum), v, p = A v (broadcast v through
+// LDS), K_j = v^T p (DPP sum), w = 2 (p - K_j v), A -= v w^T + w v^T.
+// Output: dd[0..K-1], ee[0..K-2] (ee[j] = T[j+1][j]), refl[i * ldr + j] =
+// (v_j)_i (zero for i <= j).  The k x k input C (ldc) is padded to K with
+// -beta on the diagonal (beta > ||C||_2), so the padding's eigenvalues sit
+// below every eigenvalue of C and the top ones are C's.
+template <int K, int J>
+__device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* wsh, double* refl, int ldr,
+                                         double* dd, double* ee) {
+  constexpr int c0 = (J + 1) & ~1;
+  const double xi = (i > J) ? arow[J] : 0.0;
+  const double s2 = wave_sum(xi * xi);
+  const double x0 = lane_d(xi, J + 1);
+  const double sig2 = s2 - x0 * x0;
+  const bool refl_on = sig2 > 1e-300;
+  const double alpha = refl_on ? (x0 >= 0.0 ? -sqrt(s2) : sqrt(s2)) : x0;
+  const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
+  const double vi = (i > J) ? (xi - (i == J + 1 ? alpha : 0.0)) * rn : 0.0;
+  if (i == J) { dd[J] = arow[J]; ee[J] = alpha; }
+  if (i < K) {
+    vsh[i] = vi;
+    refl[i * ldr + J] = vi;
+  }
+  wave_lds_sync();
+  // p = A v, v streamed from LDS in pairs (entry J, when the first pair
+  // starts there, has v_J = 0)
+  double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+  for (int c = c0; c < K; c += 4) {
+    const double2 t = *(const double2*)(vsh + c);
+    p0 = fma(arow[c], t.x, p0);
+    p1 = fma(arow[c + 1], t.y, p1);
+    if (c + 2 < K) {
+      const double2 u = *(const double2*)(vsh + c + 2);
+      p2 = fma(arow[c + 2], u.x, p2);
+      p3 = fma(arow[c + 3], u.y, p3);
+    }
+  }
+  const double p = (p0 + p1) + (p2 + p3);
+  const double Kd = wave_sum(vi * p);
+  const double wi = (i > J) ? 2.0 * (p - Kd * vi) : 0.0;
+  if (i < K) wsh[i] = wi;
+  wave_lds_sync();
+  // A -= v w^T + w v^T on the trailing columns (v, w streamed again)
+#pragma unroll
+  for (int c = c0; c < K; c += 2) {
+    const double2 tv = *(const double2*)(vsh + c);
+    const double2 tw = *(const double2*)(wsh + c);
+    arow[c] = fma(-vi, tw.x, fma(-wi, tv.x, arow[c]));
+    arow[c + 1] = fma(-vi, tw.y, fma(-wi, tv.y, arow[c + 1]));
+  }
+}
+
+// vsh / wsh: 2 x K doubles each (alternate steps use alternate halves, so a
+// step's writes never meet the previous step's reads)
+template <int K, int J>
+__device__ __forceinline__ void tri_steps(double (&arow)[K], int i, double* vsh, double* wsh, double* refl, int ldr,
+                                          double* dd, double* ee) {
+  if constexpr (J + 2 < K) {
+    tri_step<K, J>(arow, i, vsh + (J & 1) * K, wsh + (J & 1) * K, refl, ldr, dd, ee);
+    tri_steps<K, J + 1>(arow, i, vsh, wsh, refl, ldr, dd, ee);
+  }
+}
+
+// returns ||T||-scale (max |Gershgorin bound|) in every lane; *bad |= non-finite input
+template <int K>
+__device__ __forceinline__ void wave_tridiag(const double* C, int ldc, int k, double* refl, int ldr, double* dd,
+                                             double* ee, double* vsh, double* wsh, int* bad) {
+  const int i = threadIdx.x & 63;
+  double arow[K];
+  double f2 = 0.0;
+  int nf = 0;
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const double v = (i < k && c < k) ? C[i * ldc + c] : 0.0;
+    nf |= !(fabs(v) <= 1.7e308);
+    f2 = fma(v, v, f2);
+    arow[c] = v;
+  }
+  if (nf) atomicOr(bad, 1);
+  const double beta = 1.0625 * sqrt(wave_sum(f2)) + 1e-300;   // > ||C||_F >= -lambda_min
+#pragma unroll
+  for (int c = 0; c < K; ++c)
+    if (c >= k && c == i) arow[c] = -beta;
+  tri_steps<K, 0>(arow, i, vsh, wsh, refl, ldr, dd, ee);
+  // the last 2 x 2 block
+  if (i == K - 2) dd[K - 2] = arow[K - 2];
+  if (i == K - 1) {
+    dd[K - 1] = arow[K - 1];
+    ee[K - 2] = arow[K - 2];
+    ee[K - 1] = 0.0;
+  }
+  wave_lds_sync();
+}
+
+// ------------------------------------------- symmetric tridiagonal eigen
+// Sturm count of eigenvalues of T below x, division-free: the characteristic
+// polynomials p_i(x) (p_{i+1} = (d_i - x) p_i - e_{i-1}^2 p_{i-1}); a sign
+// change between p_i and p_{i+1} is a negative LDL^T pivot.  T is pre-scaled
+// to ||T|| ~ 1 and p is re-normalised every 8 steps (exponent only), so
+// nothing over- or underflows.  One FMA of latency per step; de2[i] =
+// {d_i, e_{i-1}^2} is read from LDS (a broadcast: every lane of the wave
+// reads the same pair), 8 steps unrolled.
+template <int K>
+__device__ __forceinline__ int sturm_count(const double2* de2, double x) {
+  double pp = 1.0, p = de2[0].x - x;
+  if (p == 0.0) p = -0x1p-60;
+  int cnt = p < 0.0;
+#pragma unroll 8
+  for (int i = 1; i < K; ++i) {
+    const double2 q = de2[i];
+    double pn = fma(q.x - x, p, -q.y * pp);
+    if (pn == 0.0) pn = -p * 0x1p-60;
+    cnt += (pn < 0.0) != (p < 0.0);
+    pp = p;
+    p = pn;
+    if ((i & 7) == 7) {
+      const int ex = __builtin_amdgcn_frexp_exp(p);
+      p = __builtin_amdgcn_ldexp(p, -ex);
+      pp = __builtin_amdgcn_ldexp(pp, -ex);
+    }
+  }
+  return cnt;
+}
+
+// Eigenpairs of the symmetric K x K matrix given by its tridiagonal form
+// (dd, ee) and reflectors (refl): the nt largest eigenvalues, descending,
+// in lam[0..nt-1] and the eigenvectors of the ORIGINAL matrix (Q x) for the
+// first nv <= 64 of them in X[i * ldx + t] (rows i < kx <= K).  Every thread of the
+// workgroup (NT threads, NT % 64 == 0) calls it; dd / ee are overwritten
+// (scaled).  Scratch: sc >= nv * (K + 1) doubles of LDS.  *st bit 1: numerically repeated eigenvalues among the
+// wanted ones, a vector that fails the residual check or non-finite values --
+// the caller should fall back to a robust solver.
+template <int K, int NT>
+__device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double* refl, int ldr, int nt, int nv,
+                                            double* lam, double* X, int ldx, int kx, double* sc, int* st) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ double s_scale;
+  __shared__ int s_clus;
+  __shared__ double2 de2[K];
+  __shared__ double snorm[64];
+  SLW_STAMP(1)
+  // ---- scale to ||T|| ~ 1 (Gershgorin radius)
+  if (tid < 64) {
+    const int i = lane;
+    double g = 0.0;
+    if (i < K) g = fabs(dd[i]) + fabs(ee[i]) + (i > 0 ? fabs(ee[i - 1]) : 0.0);
+    g = wave_max(g);
+    if (lane == 0) { s_scale = g > 0.0 ? g : 1.0; s_clus = 0; }
+  }
+  __syncthreads();
+  const double tn = s_scale, itn = 1.0 / tn;
+  if (tid < K) {
+    const double em = tid > 0 ? ee[tid - 1] * itn : 0.0;
+    de2[tid] = double2{dd[tid] * itn, em * em};
+  }
+  __syncthreads();
+  // ---- multisection: 16 lanes (one DPP row) per eigenvalue, 16 points per
+  //      round (bracket / 17 per round), rows of a wave run independently
+  constexpr double eps = 2.220446049250313e-16;
+  const int row = tid >> 4, g = tid & 15;
+  constexpr int ROWS = NT / 16;
+  for (int t0 = 0; t0 < nt; t0 += ROWS) {
+    const int t = t0 + row;
+    const bool act = t < nt;
+    const int idx = K - 1 - t;   // ascending index of this row's eigenvalue
+    double lo = -1.0 - 4.0 * eps, hi = 1.0 + 4.0 * eps;
+    for (int it = 0; it < 64; ++it) {
+      const bool conv = !act || (hi - lo) <= fmax(4.0 * eps, 2.0 * eps * fmax(fabs(lo), fabs(hi)));
+      if (__builtin_amdgcn_ballot_w64(!conv) == 0) break;
+      const double x = lo + (hi - lo) * (double)(g + 1) * (1.0 / 17.0);
+      const int c = act ? sturm_count<K>(de2, x) : 0;
+      // fewer than idx + 1 eigenvalues below x: x is a lower bound
+      double nlo = c <= idx ? x : lo, nhi = c <= idx ? hi : x;
+      nlo = fmax(nlo, dpp<0xB1>(nlo));
+      nhi = fmin(nhi, dpp<0xB1>(nhi));
+      nlo = fmax(nlo, dpp<0x4E>(nlo));
+      nhi = fmin(nhi, dpp<0x4E>(nhi));
+      nlo = fmax(nlo, dpp<0x141>(nlo));
+      nhi = fmin(nhi, dpp<0x141>(nhi));
+      nlo = fmax(nlo, dpp<0x140>(nlo));
+      nhi = fmin(nhi, dpp<0x140>(nhi));
+      if (act && !conv) { lo = nlo; hi = nhi; }
+    }
+    if (act && g == 0) lam[t] = 0.5 * (lo + hi);   // scaled
+  }
+  __syncthreads();
+  SLW_STAMP(2)
+  // ---- eigenvectors of T: one lane per vector (twisted factorisation of
+  //      the scaled T - l I).  sc[t * LZ + i] first holds the backward
+  //      pivots D-_i, then the vector; the forward pivots' reciprocals stay
+  //      in registers; d / e come from LDS (uniform broadcast reads)
+  constexpr int LZ = K + 1;   // sc[t * LZ + i]: vector t, component i
+  if (tid < K) {
+    dd[tid] *= itn;
+    ee[tid] *= itn;
+  }
+  __syncthreads();
+  if (tid < nv) {
+    const int t = tid;
+    const double l = lam[t];
+    const double gap = fmin(t > 0 ? lam[t - 1] - l : 1e300, t + 1 < nt ? l - lam[t + 1] : 1e300);
+    if (!(gap > 1e-13)) atomicOr(st, 1);       // numerically repeated (~ bisection accuracy): the caller falls back
+    if (gap < 1e-3) atomicOr(&s_clus, 1);
+    const double pivmin = 1e-290;
+    // backward pivots D-_i = (d_i - l) - e_i^2 / D-_{i+1}
+    double dm = dd[K - 1] - l;
+    if (fabs(dm) < pivmin) dm = -pivmin;
+    sc[t * LZ + (K - 1)] = dm;
+#pragma unroll 4
+    for (int i = K - 2; i >= 0; --i) {
+      const double ei = ee[i];
+      dm = (dd[i] - l) - (ei * ei) * rcp64(dm);
+      if (fabs(dm) < pivmin) dm = -pivmin;
+      sc[t * LZ + i] = dm;
+    }
+    // forward pivots D+_i and the twist gamma_i = D+_i + D-_i - (d_i - l)
+    double rup[K];
+    double dp = dd[0] - l;
+    if (fabs(dp) < pivmin) dp = -pivmin;
+    int rt = 0;
+    double best = 1e300;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const double di = dd[i] - l;
+      if (i > 0) {
+        const double e = ee[i - 1];
+        dp = di - (e * e) * rup[i - 1];
+        if (fabs(dp) < pivmin) dp = -pivmin;
+      }
+      const double gm = fabs(dp + sc[t * LZ + i] - di);
+      if (gm < best) { best = gm; rt = i; }
+      rup[i] = rcp64(dp);
+    }
+    // above the twist: z_i = -(e_i / D+_i) z_{i+1}; below: z_i = -(e_{i-1} / D-_i)
+    // z_{i-1} (D-_i still in sc there); z overwrites sc as it goes, the norm
+    // is applied by the back-transform
+    double z = 1.0, nrm = 1.0;
+#pragma unroll
+    for (int i = K - 2; i >= 0; --i) {
+      if (i < rt) {
+        z = -(ee[i] * rup[i]) * z;
+        nrm = fma(z, z, nrm);
+        sc[t * LZ + i] = z;
+      }
+    }
+    z = 1.0;
+#pragma unroll 4
+    for (int i = 1; i < K; ++i) {
+      if (i > rt) {
+        z = -ee[i - 1] * rcp64(sc[t * LZ + i]) * z;
+        nrm = fma(z, z, nrm);
+        sc[t * LZ + i] = z;
+      }
+    }
+    sc[t * LZ + rt] = 1.0;
+    const double s = rsq64(nrm);
+    if (!(s > 0.0) || !(s < 1e300)) atomicOr(st, 1);
+    snorm[t] = s;
+  }
+  __syncthreads();
+  if (tid < nv) {
+    const double s = snorm[tid];
+#pragma unroll
+    for (int i = 0; i < K; ++i) sc[tid * LZ + i] *= s;
+  }
+  __syncthreads();
+  SLW_STAMP(3)
+  // ---- MGS inside close clusters (rare): wave 0, lane = component
+  if (s_clus && tid < 64) {
+    const int i = lane;
+    for (int t = 1; t < nv; ++t) {
+      double xc = i < K ? sc[t * LZ + i] : 0.0;
+      bool touched = false;
+      for (int u = 0; u < t; ++u) {
+        if (lam[u] - lam[t] >= 1e-3) continue;
+        const double dt = wave_sum(i < K ? sc[u * LZ + i] * xc : 0.0);
+        xc -= dt * (i < K ? sc[u * LZ + i] : 0.0);
+        touched = true;
+      }
+      if (touched) {
+        const double n2 = wave_sum(xc * xc);
+        if (i < K) sc[t * LZ + i] = xc * rsq64(n2);
+      }
+      wave_lds_sync();
+    }
+  }
+  __syncthreads();
+  // ---- residual check of every vector against T (scaled), lane = vector
+  if (tid < nv) {
+    const int t = tid;
+    const double l = lam[t];
+    double r2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      double tx = (dd[i] - l) * sc[t * LZ + i];
+      if (i > 0) tx = fma(ee[i - 1], sc[t * LZ + i - 1], tx);
+      if (i + 1 < K) tx = fma(ee[i], sc[t * LZ + i + 1], tx);
+      r2 = fma(tx, tx, r2);
+    }
+    if (!(r2 <= 1e-22)) atomicOr(st, 1);
+  }
+  SLW_STAMP(4)
+  // ---- back-transform x <- H_0 ... H_{K-3} x: 16 lanes (a DPP row) per vector
+  {
+    constexpr int U = (K + 15) / 16;
+    const int v = tid >> 4, q = tid & 15;
+    for (int vb = 0; vb < nv; vb += NT / 16) {
+      const int vv_ = vb + v;
+      const bool act = vv_ < nv;
+      double x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = q + 16 * u;
+        x[u] = (act && i < K) ? sc[vv_ * (K + 1) + i] : 0.0;
+      }
+#pragma unroll 2
+      for (int j = K - 3; j >= 0; --j) {
+        double h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = q + 16 * u;
+          h[u] = i < K ? refl[i * ldr + j] : 0.0;
+        }
+        double part = 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) part = fma(h[u], x[u], part);
+        part = 2.0 * row16_sum(part);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = fma(-part, h[u], x[u]);
+      }
+      if (act) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = q + 16 * u;
+          if (i < kx) X[i * ldx + vv_] = x[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // eigenvalues back to the matrix's scale
+  for (int t = tid; t < nt; t += NT) lam[t] *= tn;
+  __syncthreads();
+  SLW_STAMP(5)
+}
+
+}  // namespace slw

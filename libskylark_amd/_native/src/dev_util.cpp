@@ -42,3 +42,21 @@ SL_API int sl_dev_set_device(int dev) {
   SL_HIP_CHECK(hipSetDevice(dev));
   return SL_OK;
 }
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// a process that drives several GPUs (sl_dev_set_device) sets it on each.
+#include <mutex>
+#include <set>
+#include <utility>
+
+int sl_lds_attr(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  SL_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({fn, dev})) return SL_OK;
+  SL_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert({fn, dev});
+  return SL_OK;
+}

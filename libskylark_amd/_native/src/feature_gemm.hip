@@ -555,11 +555,7 @@ int launch_large(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int
   constexpr int EPI_ELEMS = 8 * 64 * (64 + 4) * 2;
   constexpr size_t LDS = (size_t)((L_NBUF * STAGE > EPI_ELEMS) ? L_NBUF * STAGE : EPI_ELEMS) * 2;
   auto kern = k_feat_gemm_l<ALO, WLO, EPI, OutT>;
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS));
-    attr = true;
-  }
+  SL_LDS_ATTR(kern, (int)LDS);
   const unsigned grid = (unsigned)(8 * ((ntm + 1) / 2) * (ntn / 4));
   kern<<<grid, L_NT, LDS, s>>>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale, out, ldo, ntm, ntn, rt, p0);
   SL_LAUNCH_CHECK();

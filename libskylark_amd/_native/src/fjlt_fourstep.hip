@@ -402,20 +402,10 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
   const int per = (int)((nblk + 7) / 8);
   const unsigned grid = (unsigned)(8 * (int64_t)per);
   if (dtype == SL_F32) {
-    static bool attr = false;
-    if (!attr) {
-      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_fs_stage1<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)stage1_lds(N2_MAX)));
-      attr = true;
-    }
+    SL_LDS_ATTR(k_fs_stage1<float>, (int)stage1_lds(N2_MAX));
     k_fs_stage1<float><<<grid, NT1, lds, s>>>((const float*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y, per);
   } else if (dtype == SL_BF16) {
-    static bool attr = false;
-    if (!attr) {
-      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_fs_stage1<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)stage1_lds(N2_MAX)));
-      attr = true;
-    }
+    SL_LDS_ATTR(k_fs_stage1<bf16_t>, (int)stage1_lds(N2_MAX));
     k_fs_stage1<bf16_t><<<grid, NT1, lds, s>>>((const bf16_t*)A, lda, N, m, d, N1, N2, rplan, npass, (float2*)Y, per);
   } else {
     sl_set_last_error("fs_stage1: f32 / bf16 input");
@@ -432,12 +422,7 @@ SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, c
     sl_set_last_error("fs_stage2: needs 1 <= N1 <= 8192");
     return SL_ERR_INVALID;
   }
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_fs_stage2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)stage2_lds(8192)));
-    attr = true;
-  }
+  SL_LDS_ATTR(k_fs_stage2, (int)stage2_lds(8192));
   const int64_t nblk = (int64_t)((m + 63) / 64) * N2;
   const int per = (int)((nblk + 7) / 8);
   k_fs_stage2<<<(unsigned)(8 * (int64_t)per), NT, stage2_lds(N1), (hipStream_t)stream>>>(

@@ -10,9 +10,8 @@
 //   k_boundary<FINAL>  after the final pass: the same sums (+ the fp64 Gram of
 //                      Y), H = W^T W (W = A^T Y), the Cholesky Y^T Y = Rt^T Rt,
 //                      Rt^{-1}, the symmetric core C = Rt^{-T} H Rt^{-1} =
-//                      Ub S^2 Ub^T, a cyclic Jacobi eigensolve of C, the small
-//                      factors M = Rt^{-1} Ub_r (U = Y M) and N = M S^{-1}, and
-//                      V = W N.
+//                      Ub S^2 Ub^T, its top eigenpairs, the small factors
+//                      M = Rt^{-1} Ub_r (U = Y M) and N = M S^{-1}, and V = W N.
 //
 // Structure: the n rows of W are split over n / 16 workgroups; each sums its
 // rows, forms their partial Gram (f64) and publishes it with an agent-scope
@@ -21,16 +20,19 @@
 // while the others wait on a generation word, then every workgroup forms its
 // rows of Z^T / V.  One launch per boundary (see k_boundary).
 //
-// Jacobi: round-robin (circle) ordering, k/2 disjoint rotations per round,
-// ONE workgroup barrier per round (A ping-pongs between two LDS copies, every
-// thread derives the rotations it needs from the old copy).  A rotation's
-// tangent comes from an f32 estimate refined by one f64 Newton step on
-// a_pq t^2 + (a_qq - a_pp) t - a_pq = 0 (no f64 division), its cosine from an
-// f32 rsqrt refined in f64: f64-accurate rotations at f32 latency.  Sweeps
-// stop once every pair's |a_pq| / sqrt|a_pp a_qq| was below 1e-8 before its
-// rotation (the quadratic convergence of that sweep leaves ~1e-16).
+// The k x k algebra is latency-bound, so it runs on ONE wave with the matrix
+// in registers (sl_wave_la.hpp): the Cholesky inverse as an in-place LDL^T
+// elimination of [G | I], the core eigenproblem as Householder
+// tridiagonalisation + multisection (division-free Sturm counts) + twisted
+// factorisation + a DPP back-transform over all waves.  Every call solves
+// its core from scratch; cyclic Jacobi (jacobi() below) is kept as the
+// fallback for numerically repeated eigenvalues.
 #include "sl_common.hpp"
 #include "sl_rng.hpp"
+#include "sl_wave_la.hpp"
+
+#include <map>
+#include <mutex>
 
 namespace {
 
@@ -49,137 +51,7 @@ __device__ unsigned long long g_core_st[32];
 #define SL_CST(I)
 #endif
 
-enum : int { ST_PIVOT = 1, ST_NONFINITE = 2, ST_NOCONV = 4, ST_RANK = 8 };
-
-// ---------------------------------------------------------------- Cholesky
-// f64 reciprocal / reciprocal square root: hardware estimate + two Newton steps
-__device__ __forceinline__ double rcp64(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = r * fma(-d, r, 2.0);
-  r = r * fma(-d, r, 2.0);
-  return r;
-}
-__device__ __forceinline__ double rsq64(double d) {
-  double r = __builtin_amdgcn_rsq(d);
-  r = r * fma(-0.5 * d * r, r, 1.5);
-  r = r * fma(-0.5 * d * r, r, 1.5);
-  return r;
-}
-
-// X = R^{-1} (upper, k x k) of the Cholesky factor G = R^T R, from ONE LDL^T
-// elimination of the augmented [G | I]: eliminating below pivot j turns the
-// right block into L^{-1} (unit lower), and R^{-1} = L^{-T} D^{-1/2}.
-// Register-resident: thread (g = tid >> 6, c = tid & 63) holds entries
-// (i, c) of both blocks for its rows i = g + 8u, u < 8; a step reads the
-// pivot row from a 2-deep LDS row buffer (written by its owner one step
-// earlier), updates in registers and publishes the next pivot rows: two
-// pivots per barrier (see the body).  Full rows are updated, so the
-// trailing block stays symmetric and T[j][i] is the multiplier numerator of
-// row i.  A pivot at or below 1e-13 x max diag drops its direction (that
-// column of X is zero) and sets ST_PIVOT.  G and X may be LDS or global (ldg,
-// ldx) and may alias.  red: >= KMAX + 2 doubles of LDS scratch.
-__device__ void chol_inv(const double* G, int ldg, double* X, int ldx, int k, int* st, double* red) {
-  // rb[buf][0 / 1]: T / L of pivot row p, [2 / 3]: T / L of row p + 1 (both as
-  // of before pivots p and p + 1); TWO pivots per barrier: every thread forms
-  // row p + 1 after pivot p itself (its own column) and the pivot-(p + 1)
-  // multiplier numerators from the two published rows (symmetry)
-  __shared__ double rb[2][4][KMAX];
-  const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
-  constexpr int RU = KMAX / (NT / 64);
-  double T[RU], L[RU];
-#pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int i = g + 8 * u;
-    T[u] = (i < k && c < k) ? G[i * ldg + c] : 0.0;
-    L[u] = (i == c && i < k) ? 1.0 : 0.0;
-  }
-  if (g == 0) {
-    double v = c < k ? fabs(G[c * ldg + c]) : 0.0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    if (c == 0) red[0] = v;
-    rb[0][0][c] = T[0];
-    rb[0][1][c] = L[0];
-  } else if (g == 1) {
-    rb[0][2][c] = T[0];
-    rb[0][3][c] = L[0];
-  }
-  __syncthreads();
-  const double thr = 1e-13 * red[0];
-  for (int j = 0; j < k; j += 2) {
-    const int buf = (j >> 1) & 1;
-    const bool two = j + 1 < k;
-    const double* R0 = rb[buf][0];
-    const double* R1 = rb[buf][2];
-    const double d0 = R0[j];
-    const double tj = R0[c], lj = rb[buf][1][c];
-    const bool ok0 = d0 > thr && d0 == d0;
-    const double r0 = ok0 ? rcp64(d0) : 0.0;
-    // row j + 1 after pivot j, column c; its pivot d1
-    double f10 = 0.0, t1c = 0.0, l1c = 0.0, d1 = 0.0, r1 = 0.0;
-    bool ok1 = true;
-    if (two) {
-      f10 = R1[j] * r0;
-      t1c = fma(-f10, tj, R1[c]);
-      l1c = fma(-f10, lj, rb[buf][3][c]);
-      d1 = fma(-f10, R0[j + 1], R1[j + 1]);
-      ok1 = d1 > thr && d1 == d1;
-      r1 = ok1 ? rcp64(d1) : 0.0;
-    }
-    double n0[RU], n1[RU];
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int i = (g + 8 * u) & (KMAX - 1);
-      n0[u] = R0[i];
-      n1[u] = R1[i];
-    }
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int i = g + 8 * u;
-      if (i > j && i < k) {
-        const double f0 = n0[u] * r0;
-        T[u] = fma(-f0, tj, T[u]);
-        L[u] = fma(-f0, lj, L[u]);
-        if (i > j + 1) {
-          const double f1 = fma(-f10, n0[u], n1[u]) * r1;
-          T[u] = fma(-f1, t1c, T[u]);
-          L[u] = fma(-f1, l1c, L[u]);
-        }
-      }
-    }
-    // publish rows j + 2 and j + 3 (final after both pivots)
-    const int p2 = j + 2, p3 = j + 3;
-    if (p2 < k && g == (p2 & 7)) {
-      double t = 0.0, l = 0.0;
-#pragma unroll
-      for (int u = 0; u < RU; ++u)
-        if (u == (p2 >> 3)) { t = T[u]; l = L[u]; }
-      rb[buf ^ 1][0][c] = t;
-      rb[buf ^ 1][1][c] = l;
-    }
-    if (p3 < k && g == (p3 & 7)) {
-      double t = 0.0, l = 0.0;
-#pragma unroll
-      for (int u = 0; u < RU; ++u)
-        if (u == (p3 >> 3)) { t = T[u]; l = L[u]; }
-      rb[buf ^ 1][2][c] = t;
-      rb[buf ^ 1][3][c] = l;
-    }
-    if (tid == 0) {
-      red[2 + j] = ok0 ? rsq64(d0) : 0.0;
-      if (two) red[3 + j] = ok1 ? rsq64(d1) : 0.0;
-      if (!ok0 || !ok1) *st |= ST_PIVOT;
-    }
-    __syncthreads();
-  }
-  // X[c][i] = L[i][c] D_i^{-1/2} for c <= i
-#pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int i = g + 8 * u;
-    if (i < k && c < k) X[c * ldx + i] = c <= i ? L[u] * red[2 + i] : 0.0;
-  }
-  __syncthreads();
-}
+enum : int { ST_PIVOT = 1, ST_NONFINITE = 2, ST_NOCONV = 4, ST_RANK = 8, ST_TIMEOUT = 16 };
 
 // C = A^T B (transa) or A B for k x k LDS matrices (row stride ld) on f64
 // MFMA: 16 x 16 output tiles over the 8 waves, K in steps of 4
@@ -403,119 +275,91 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
 }
 
 // ---------------------------------------------------------------- final core
-// After the final pass (H = W^T W in b0, Gy = Y^T Y in global / LDS, row stride k):
-// Y^T Y = Rt^T Rt, Rti = Rt^{-1}, C = Rti^T H Rti = Ub S^2 Ub^T (Jacobi, warm
-// started from V0), s, M = Rti Ub_r (f32) and N = M S^{-1} (f64).  Run by ONE
-// workgroup; b0..b3 are k x k LDS scratch (row stride k + 1).  status_or: OR
-// the call's status bits into *status (0: store them -- the call's first writer).
-__device__ void final_core(double* b0, double* b1, double* b2, double* b3, double* red, int* flags, int* order,
-                           const double* Gy, int k, int r, float* __restrict__ M, double* __restrict__ N,
-                           double* __restrict__ s_out, int* __restrict__ status, int max_sweeps, double* V0,
-                           int* v0_valid, int* mirror, int* st_sh_p, int status_or, bool rti_given = false) {
+// After the final pass (H = W^T W in b0, Rti = Rt^{-1} of Y^T Y = Rt^T Rt in
+// b3, row stride ld = k + 1): C = Rti^T H Rti = Ub S^2 Ub^T, its top r + 1
+// eigenvalues and top r eigenvectors (Householder tridiagonalisation on one
+// wave, multisection + twisted factorisation + back-transform on all waves,
+// sl_wave_la.hpp), s, M = Rti Ub_r (f32) and N = M S^{-1} (f64).  Every call
+// solves its core from scratch.  If the tridiagonal path reports
+// numerically repeated wanted eigenvalues or a vector that fails its
+// residual check, the core is re-solved by cyclic Jacobi (robust to
+// clusters, rare).  Run by ONE workgroup.  status_or: OR the call's status
+// bits into *status (0: store them -- the call's first writer).
+struct CoreLds {
+  __attribute__((aligned(16))) double dd[KMAX], ee[KMAX], lam[KMAX], vsh[2 * KMAX], wsh[2 * KMAX], fsh[3 * 64];
+  int bad, fb;
+};
+
+template <int K>
+__device__ __forceinline__ void final_core(double* b0, double* b1, double* b2, double* b3, int* flags, int* order, CoreLds& cs,
+                           double* Cbak, int k, int r, float* __restrict__ M, double* __restrict__ N,
+                           double* __restrict__ s_out, int* __restrict__ status, int* mirror, int* st_sh_p,
+                           int status_or) {
   int& st_sh = *st_sh_p;
   const int tid = threadIdx.x;
   const int ld = k + 1;
   constexpr int SO = 16;
   (void)SO;
-  // ---- FINAL: Y^T Y = Rt^T Rt, Rti = Rt^{-1} -> b3 (straight from Gy; H in b0
-  //      survives), unless the caller already placed Rti in b3
-  if (!rti_given) chol_inv(Gy, k, b3, ld, k, st_sh_p, red);
   SL_CST(SO + 3)
   // C = Rti^T H Rti:  T = H Rti -> b1, C = Rti^T T -> b2
   small_gemm(b0, b3, b1, k, ld, false);
   __syncthreads();
   small_gemm(b3, b1, b2, k, ld, true);
   __syncthreads();
-  // symmetrise, pad to an even order with an isolated zero row / column
-  const int kp = k + (k & 1);
-  for (int e = tid; e < kp * kp; e += NT) {
-    const int i = e / kp, c = e - i * kp;
-    double v = 0.0;
-    if (i < k && c < k) v = 0.5 * (b2[i * ld + c] + b2[c * ld + i]);
+  // symmetrise into b0 (+ a global copy for the rare fallback)
+  for (int e = tid; e < k * k; e += NT) {
+    const int i = e / k, c = e - i * k;
+    const double v = 0.5 * (b2[i * ld + c] + b2[c * ld + i]);
     b0[i * ld + c] = v;
+    Cbak[e] = v;
   }
-  __syncthreads();
-  // warm start: C' = V0^T C V0 with the previous call's eigenvectors V0
-  // (any orthogonal V0 is a valid start; on a repeated problem C' is already
-  // diagonal and one sweep confirms it)
-  const bool warm = V0 != nullptr && v0_valid != nullptr && *v0_valid == kp;
-  if (warm) {
-    for (int e = tid; e < kp * kp; e += NT) {
-      const int i = e / kp, c = e - i * kp;
-      b1[i * ld + c] = V0[e];
-    }
-    __syncthreads();
-    small_gemm(b0, b1, b2, kp, ld, false);    // T = C V0
-    __syncthreads();
-    small_gemm(b1, b2, b0, kp, ld, true);     // C' = V0^T T
-    __syncthreads();
-    for (int e = tid; e < kp * kp; e += NT) {
-      const int i = e / kp, c = e - i * kp;
-      b2[i * ld + c] = 0.5 * (b0[i * ld + c] + b0[c * ld + i]);
-    }
-  } else {
-    for (int e = tid; e < kp * kp; e += NT) {
-      const int i = e / kp, c = e - i * kp;
-      b2[i * ld + c] = b0[i * ld + c];
-    }
-  }
+  if (tid == 0) { cs.bad = 0; cs.fb = 0; }
   __syncthreads();
   SL_CST(SO + 4)
-  // warm start already diagonal to roundoff (a repeated problem: |c'_pq|^2 <=
-  // max(1e-24 c'_pp c'_qq, (1e-14 max|c'_ii|)^2) for every pair): the
-  // eigenpairs are diag(C') and V0 as they stand, no confirming sweep
-  bool diag_ok = false;
-  if (warm) {
-    if (tid == 0) flags[3] = 0;
-    __syncthreads();
-    double amax = 0.0;
-    for (int i = 0; i < kp; ++i) amax = fmax(amax, fabs(b2[i * ld + i]));
-    const double noise2 = (1e-14 * amax) * (1e-14 * amax);
-    int off = 0;
-    for (int e = tid; e < kp * kp; e += NT) {
-      const int i = e / kp, c = e - i * kp;
-      if (i < c) {
-        const double apq = b2[i * ld + c];
-        if (apq * apq > fmax(1e-24 * fabs(b2[i * ld + i] * b2[c * ld + c]), noise2)) off = 1;
-      }
-    }
-    if (off) flags[3] = 1;
-    __syncthreads();
-    diag_ok = flags[3] == 0;
-    __syncthreads();
-  }
-  // Jacobi on b2, V in b1 (V0 when warm)
-  double* Af = b2;
-  if (diag_ok) {
-    if (tid == 0) flags[3] = 0;
-  } else {
-    Af = jacobi(b2, b0, b1, kp, ld, max_sweeps, flags, st_sh_p, warm);
-  }
-  SL_CST(SO + 5)
-#ifdef SL_CORE_STAMPS
-  if (tid == 0) g_core_st[SO + 8] = flags[3];
-#endif
-  if (V0 != nullptr) {
-    for (int e = tid; e < kp * kp; e += NT) {
-      const int i = e / kp, c = e - i * kp;
-      V0[e] = b1[i * ld + c];
-    }
-    if (tid == 0) *v0_valid = kp;
-  }
-  // ---- descending order of the k eigenvalues (rank by comparison)
-  for (int i = tid; i < k; i += NT) {
-    const double li = Af[i * ld + i];
-    int rk = 0;
-    for (int j = 0; j < k; ++j) {
-      const double lj = Af[j * ld + j];
-      rk += (lj > li) || (lj == li && j < i);
-    }
-    order[rk] = i;
-  }
+  // tridiagonalise (wave 0; reflectors into b2, ld K + 1)
+  const int nt = r < k ? r + 1 : k;
+  if (tid < 64) slw::wave_tridiag<K>(b0, ld, k, b2, K + 1, cs.dd, cs.ee, cs.vsh, cs.wsh, &cs.bad);
   __syncthreads();
+  SL_CST(SO + 5)
+  // top nt eigenvalues, top r eigenvectors of C into b1 (ld), scratch b0
+  slw::sym_top_eig<K, NT>(cs.dd, cs.ee, b2, K + 1, nt, r, cs.lam, b1, ld, k, b0, &cs.fb);
+  SL_CST(SO + 6)
+  if (cs.fb | cs.bad) {
+    // robust path: Jacobi on the saved core (C in b2, V in b1, ld)
+    const int kp = k + (k & 1);
+    for (int e = tid; e < kp * kp; e += NT) {
+      const int i = e / kp, c = e - i * kp;
+      b2[i * ld + c] = (i < k && c < k) ? Cbak[i * k + c] : 0.0;
+    }
+    __syncthreads();
+    double* Af = jacobi(b2, b0, b1, kp, ld, 40, flags, st_sh_p);
+    for (int i = tid; i < k; i += NT) {
+      const double li = Af[i * ld + i];
+      int rk = 0;
+      for (int j = 0; j < k; ++j) {
+        const double lj = Af[j * ld + j];
+        rk += (lj > li) || (lj == li && j < i);
+      }
+      order[rk] = i;
+    }
+    __syncthreads();
+    // eigenvectors in descending order into b0 (ld), eigenvalues into lam
+    for (int e = tid; e < k * r; e += NT) {
+      const int i = e / r, c = e - i * r;
+      b0[i * ld + c] = b1[i * ld + order[c]];
+    }
+    for (int c = tid; c < nt; c += NT) cs.lam[c] = Af[order[c] * ld + order[c]];
+    __syncthreads();
+    for (int e = tid; e < k * r; e += NT) {
+      const int i = e / r, c = e - i * r;
+      b1[i * ld + c] = b0[i * ld + c];
+    }
+    if (tid == 0 && cs.bad) st_sh |= ST_NONFINITE;
+    __syncthreads();
+  }
   // ---- s, M = Rti Ub_r (f32), N = M S^{-1} (f64)
   for (int c = tid; c < r; c += NT) {
-    const double lam = Af[order[c] * ld + order[c]];
+    const double lam = cs.lam[c];
     s_out[c] = lam > 0.0 ? sqrt(lam) : 0.0;
     if (!(lam > 0.0)) atomicOr(st_sh_p, ST_RANK);
     if (!(lam == lam)) atomicOr(st_sh_p, ST_NONFINITE);
@@ -523,12 +367,11 @@ __device__ void final_core(double* b0, double* b1, double* b2, double* b3, doubl
   __syncthreads();
   for (int e = tid; e < k * r; e += NT) {
     const int i = e / r, c = e - i * r;
-    const int oc = order[c];
     double a = 0.0;
-    for (int l = i; l < k; ++l) a += b3[i * ld + l] * b1[l * ld + oc];
+    for (int l = i; l < k; ++l) a += b3[i * ld + l] * b1[l * ld + c];
     M[e] = (float)a;
-    const double lam = Af[oc * ld + oc];
-    N[e] = lam > 0.0 ? a / sqrt(lam) : 0.0;
+    const double lam = cs.lam[c];
+    N[e] = lam > 0.0 ? a * slw::rsq64(lam) : 0.0;
   }
   if (tid == 0) {
     int all = st_sh;
@@ -537,7 +380,7 @@ __device__ void final_core(double* b0, double* b1, double* b2, double* b3, doubl
     // the call's final status word, straight to host-mapped memory (no D2H copy)
     if (mirror) __hip_atomic_store(mirror, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  SL_CST(SO + 6)
+  SL_CST(SO + 7)
 }
 
 // ---------------------------------------------------------------- fused boundary
@@ -547,8 +390,8 @@ __device__ void final_core(double* b0, double* b1, double* b2, double* b3, doubl
 //   1. workgroup b loads its BR rows of W (one batch of loads) into LDS
 //   2. the packed upper partial Gram of its rows -> global, then a ticket
 //   3. the last arriving workgroup sums the partials (16-B loads, a batch in
-//      flight), runs the k x k algebra (INTER: Cholesky inverse; FINAL:
-//      final_core) and bumps the generation word (agent-scope release)
+//      flight), runs the k x k algebra (INTER: Cholesky inverse on one wave;
+//      FINAL: final_core) and bumps the generation word (agent-scope release)
 //   4. every workgroup (the others spin on the generation word meanwhile; the
 //      <= BMAX workgroups are co-resident on the 256 CUs) forms its rows of
 //      the next pass operand Z^T = (W R^{-1})^T (INTER) or of V = W N (FINAL)
@@ -567,10 +410,11 @@ struct BndArgs {
   int n, k, r;
   int nbr;                // workgroups holding rows (FINAL: one more, the Y^T Y Cholesky worker)
   double* rti;            // FINAL: the worker's Rt^{-1} (k x k) and status word
+  double* cbak;           // FINAL: k x k copy of the core (fallback)
   double* WG;             // [W (n x k); Gy (k x k)] f64
   double* part;           // BMAX packed partial Grams, stride ldp doubles
   int ldp;
-  unsigned* sync;         // [0] ticket, [16] generation, [32] FINAL worker epoch
+  unsigned* sync;         // [0] ticket, [16] generation, [32] finished FINAL workers, [33] consumed
   int* status;
   int status_or;
   double* Rinv;           // INTER: k x k
@@ -578,22 +422,19 @@ struct BndArgs {
   float* M;               // FINAL: k x r, N (k x r), s64 (r)
   double* N;
   double* s64;
-  int max_sweeps;
-  double* V0;
-  int* v0_valid;
   int* mirror;
   float* V;               // FINAL: n x r (null: no V), s32 (r)
   float* s32;
   float* const* optr;     // {U, s, V} read at run time when set (graph replays)
+  uint64_t bound;         // spin bound (100 MHz ticks)
+  int missing;            // test knob: arrivals expected beyond the grid (0 in production)
 };
 
-enum : int { ST_TIMEOUT = 16 };
-
-// dynamic LDS: the small-LA layout (GRAM_LA_LDS), then the BR x KMAX rows of W
+// dynamic LDS: four k x k f64 buffers + small scratch (GRAM_LA_LDS), then the BR x KMAX rows of W
 constexpr size_t BND_WR_OFF = (GRAM_LA_LDS + 15) / 16 * 2;   // in doubles
 constexpr size_t BND_LDS = BND_WR_OFF * sizeof(double) + (size_t)BR * WLD * sizeof(double);
 
-template <bool FINAL>
+template <bool FINAL, int K>
 __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -612,25 +453,24 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   __shared__ int st_sh;
   __shared__ int is_last;
   __shared__ unsigned gen0;
+  __shared__ CoreLds cls;
   if (FINAL && (int)blockIdx.x == nb) {
     // the Y^T Y worker: Rt^{-1} of the reduced Gram (independent of W) while
-    // the row workgroups form and sum H; published with the launch's epoch
-    if (tid == 0) {
-      gen0 = __hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      st_sh = 0;
-    }
+    // the row workgroups form and sum H, published as a finished-worker count
+    if (tid == 0) st_sh = 0;
     __syncthreads();
-    chol_inv(a.WG + (int64_t)n * k, k, b3, ld, k, &st_sh, red);
-    for (int e = tid; e < k * k; e += NT) {
-      const int i = e / k, c = e - i * k;
-      a.rti[e] = b3[i * ld + c];
-    }
+    if (tid < 64) slw::wave_chol_inv<K>(a.WG + (int64_t)n * k, k, a.rti, k, k, cls.fsh, &st_sh);
+    __syncthreads();
     if (tid == 0) ((int*)(a.rti + k * k))[0] = st_sh;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+      // publish: a monotone count of finished workers (sync[32]); the last
+      // arriver consumes one per launch (sync[33]), so a late worker of a
+      // timed-out launch can never satisfy a later launch's wait
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(&a.sync[32], gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(&a.sync[32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -691,7 +531,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     gen0 = __hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(&a.sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = t == (unsigned)nb - 1;
+    is_last = t == (unsigned)(nb + a.missing) - 1;
     if (is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     st_sh = 0;
   }
@@ -704,7 +544,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     SL_CST(3)
     // sum of the nb packed partials, two entries per thread and load
     const int npair = a.ldp >> 1;
-    const int kk2 = k * (k + 1) / 2;
     double* Hp = b1;
     for (int p = tid; p < npair; p += NT) {
       const double2* src = (const double2*)a.part + p;
@@ -727,7 +566,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       Hp[2 * p + 1] = s2.y;
     }
     __syncthreads();
-    (void)kk2;
     for (int e = tid; e < k * k; e += NT) {
       const int i = e / k, c = e - i * k;
       const int lo = min(i, c), hi = max(i, c);
@@ -737,7 +575,8 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     if (tid == 0) a.sync[0] = 0u;   // ready for the next launch
     SL_CST(4)
     if (!FINAL) {
-      chol_inv(b0, ld, b2, ld, k, &st_sh, red);
+      if (tid < 64) slw::wave_chol_inv<K>(b0, ld, b2, ld, k, cls.fsh, &st_sh);
+      __syncthreads();
       for (int e = tid; e < k * k; e += NT) {
         const int i = e / k, c = e - i * k;
         const double v = b2[i * ld + c];
@@ -750,16 +589,20 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
         else __hip_atomic_store(a.status, st_sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else {
-      // the worker's Rt^{-1} (bounded wait for this launch's epoch)
+      // the worker's Rt^{-1}: bounded wait until the finished-worker count
+      // passes the consumed count, then consume one (also after a timeout:
+      // the late worker's publish is then already accounted for)
       if (tid == 0) {
+        const unsigned want = __hip_atomic_load(&a.sync[33], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
         const uint64_t t0 = wall_clock64();
-        while (__hip_atomic_load(&a.sync[32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gen0 + 1u) {
+        while ((int)(__hip_atomic_load(&a.sync[32], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
           __builtin_amdgcn_s_sleep(1);
-          if (wall_clock64() - t0 > 200000000ull) {
+          if (wall_clock64() - t0 > a.bound) {
             st_sh |= ST_TIMEOUT;
             break;
           }
         }
+        __hip_atomic_store(&a.sync[33], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         st_sh |= ((const int*)(a.rti + k * k))[0];
       }
@@ -782,8 +625,8 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
         }
       }
       __syncthreads();
-      final_core(b0, b1, b2, b3, red, flags, order, a.WG + (int64_t)n * k, k, a.r, a.M, a.N, a.s64, a.status,
-                 a.max_sweeps, a.V0, a.v0_valid, a.mirror, &st_sh, a.status_or, true);
+      final_core<K>(b0, b1, b2, b3, flags, order, cls, a.cbak, k, a.r, a.M, a.N, a.s64, a.status, a.mirror, &st_sh,
+                    a.status_or);
     }
     SL_CST(5)
     // release the waiters
@@ -801,8 +644,9 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       const uint64_t t0 = wall_clock64();
       while (__hip_atomic_load(&a.sync[16], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
         __builtin_amdgcn_s_sleep(2);
-        if (wall_clock64() - t0 > 200000000ull) {
+        if (wall_clock64() - t0 > a.bound) {
           atomicOr(a.status, ST_TIMEOUT);
+          if (a.mirror) __hip_atomic_store(a.mirror, ST_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
@@ -1062,12 +906,7 @@ k_sym_eig_jacobi2(const double* __restrict__ C, int k, double* __restrict__ w, d
 
 SL_API int sl_sym_eig_jacobi2(const double* C, int k, double* w, double* V, int* status, int max_sweeps, void* stream) {
   if (k < 1 || k > KMAX) { sl_set_last_error("sym_eig_jacobi2: 1 <= k <= 64"); return SL_ERR_UNSUPPORTED; }
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_sym_eig_jacobi2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)gram_la_lds()));
-    attr = true;
-  }
+  SL_LDS_ATTR(k_sym_eig_jacobi2, (int)gram_la_lds());
   k_sym_eig_jacobi2<<<1, NT, gram_la_lds(), (hipStream_t)stream>>>(C, k, w, V, status, max_sweeps > 0 ? max_sweeps : 40);
   SL_LAUNCH_CHECK();
   return SL_OK;
@@ -1082,22 +921,59 @@ SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void*
 
 // ------------------------------------------------------------ fused boundary
 
+// Test-only fault injection per boundary workspace: `missing` arrivals the
+// kernel waits for beyond its grid (so no workgroup is last and every wait
+// times out) and the spin bound in 100 MHz ticks (0: the 2 s default).
+namespace {
+struct BndFault { int missing = 0; uint64_t bound = 0; };
+std::mutex g_fault_mu;
+std::map<const void*, BndFault> g_faults;
+BndFault bnd_fault(const void* bws) {
+  std::lock_guard<std::mutex> g(g_fault_mu);
+  auto it = g_faults.find(bws);
+  return it == g_faults.end() ? BndFault{} : it->second;
+}
+}  // namespace
+
+SL_API int sl_rsvd_bnd_set_fault(const void* bws, int missing, uint64_t bound_ticks) {
+  std::lock_guard<std::mutex> g(g_fault_mu);
+  if (missing == 0 && bound_ticks == 0) g_faults.erase(bws);
+  else g_faults[bws] = BndFault{missing, bound_ticks};
+  return SL_OK;
+}
+
 // workspace of sl_rsvd_boundary: sync words (256 B, zeroed once; the kernel
-// leaves the ticket zero and only advances the generation) + BMAX partials
+// leaves the ticket zero and only advances the generation and worker counts)
+// + BMAX partial Grams + the worker's Rt^{-1} and status + the core's copy
 SL_API int64_t sl_rsvd_bnd_workspace(int k) {
   const int64_t ldp = ((int64_t)k * (k + 1) / 2 + 1) & ~(int64_t)1;
-  return 256 + (int64_t)BMAX * ldp * 8 + (int64_t)k * k * 8 + 256;
+  return 256 + (int64_t)BMAX * ldp * 8 + (int64_t)k * k * 8 + 256 + (int64_t)k * k * 8;
 }
+
+namespace {
+template <int K>
+int launch_bnd(bool fin, unsigned nb, const BndArgs& a, hipStream_t s) {
+  if (fin) {
+    SL_LDS_ATTR((k_boundary<true, K>), (int)BND_LDS);
+    k_boundary<true, K><<<nb + 1, NT, BND_LDS, s>>>(a);   // + the Y^T Y worker
+  } else {
+    SL_LDS_ATTR((k_boundary<false, K>), (int)BND_LDS);
+    k_boundary<false, K><<<nb, NT, BND_LDS, s>>>(a);
+  }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+}  // namespace
 
 // One pass boundary on the reduced (and, on several ranks, all-reduced)
 // [W (n x k); Gy (k x k)] f64 buffer WG.
 // final_ = 0: Rinv and Z^T (bf16, k x n) for the next pass.  final_ = 1: the
-// core (s64, M, N, status, mirror, warm start V0) and, when V or optr is
-// given, V = W N (n x r f32) and s (f32).  status_or = 0 stores the status
-// bits (the call's first writer), 1 ORs them.
+// core (s64, M, N, status, mirror) and, when V or optr is given, V = W N
+// (n x r f32) and s (f32).  status_or = 0 stores the status bits (the call's
+// first writer), 1 ORs them.
 SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* bws, int* status, int status_or,
-                            double* Rinv, void* Zt, float* M, double* N, double* s64, int max_sweeps, double* V0,
-                            int* v0_valid, int* mirror, float* V, float* s32, float* const* optr, void* stream) {
+                            double* Rinv, void* Zt, float* M, double* N, double* s64, int* mirror, float* V,
+                            float* s32, float* const* optr, void* stream) {
   if (k < 1 || k > BK || n < 16 || n > BMAX * BR || n % 8 || (final_ && (r < 1 || r > k))) {
     sl_set_last_error("rsvd_boundary: needs 1 <= k <= 48, 16 <= n <= 1024, n % 8 == 0, 1 <= r <= k");
     return SL_ERR_UNSUPPORTED;
@@ -1109,35 +985,27 @@ SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* b
   a.part = (double*)((char*)bws + 256);
   a.ldp = (int)(((int64_t)k * (k + 1) / 2 + 1) & ~(int64_t)1);
   a.rti = a.part + (int64_t)BMAX * a.ldp;
+  a.cbak = a.rti + (int64_t)k * k + 32;
   a.status = status;
   a.status_or = status_or;
   a.Rinv = Rinv;
   a.Zt = (bf16_t*)Zt;
   a.M = M; a.N = N; a.s64 = s64;
-  a.max_sweeps = max_sweeps > 0 ? max_sweeps : 40;
-  a.V0 = V0; a.v0_valid = v0_valid; a.mirror = mirror;
+  a.mirror = mirror;
   a.V = V; a.s32 = s32; a.optr = optr;
+  {
+    // fault-injection knobs live in the plan (host side), keyed by workspace
+    const BndFault f = bnd_fault(bws);
+    a.missing = f.missing;
+    a.bound = f.bound ? f.bound : 200000000ull;   // 2 s of the 100 MHz clock
+  }
   const unsigned nb = (unsigned)((n + BR - 1) / BR);
   a.nbr = (int)nb;
   hipStream_t s = (hipStream_t)stream;
-  if (final_) {
-    static bool attr = false;
-    if (!attr) {
-      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_boundary<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)BND_LDS));
-      attr = true;
-    }
-    k_boundary<true><<<nb + 1, NT, BND_LDS, s>>>(a);   // + the Y^T Y worker
-  } else {
-    if (!Rinv || !Zt) { sl_set_last_error("rsvd_boundary: Rinv and Zt required"); return SL_ERR_INVALID; }
-    static bool attr = false;
-    if (!attr) {
-      SL_HIP_CHECK(hipFuncSetAttribute((const void*)k_boundary<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)BND_LDS));
-      attr = true;
-    }
-    k_boundary<false><<<nb, NT, BND_LDS, s>>>(a);
-  }
-  SL_LAUNCH_CHECK();
-  return SL_OK;
+  if (!final_ && (!Rinv || !Zt)) { sl_set_last_error("rsvd_boundary: Rinv and Zt required"); return SL_ERR_INVALID; }
+  const bool fin = final_ != 0;
+  if (k <= 16) return launch_bnd<16>(fin, nb, a, s);
+  if (k <= 32) return launch_bnd<32>(fin, nb, a, s);
+  if (k <= 40) return launch_bnd<40>(fin, nb, a, s);
+  return launch_bnd<48>(fin, nb, a, s);
 }

@@ -8,7 +8,8 @@
 //                + R^{-1}), Z^T = (W R^{-1})^T, pass i, slab reduction
 //                (pass q is the FINAL form: Y stored, fp64 Gram of Y)
 //   seg q + 1    fp64 core: Cholesky of Y^T Y, C = Rt^{-T} W^T W Rt^{-1},
-//                Jacobi, M = Rt^{-1} Ub_r, N = M S^{-1}, s
+//                its top eigenpairs (tridiagonal eigensolver, from scratch
+//                every call), M = Rt^{-1} Ub_r, N = M S^{-1}, s
 // then the finish (U = Y M, V = W N, s) into the caller's buffers.
 //
 // Single rank: the segments and the finish are captured ONCE as a hipGraph
@@ -39,9 +40,10 @@ SL_API int sl_rsvd_make_v_ind(const double* W, int n, int k, int ldw, const doub
                               float* const* optr, void* stream);
 SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* stream);
 SL_API int64_t sl_rsvd_bnd_workspace(int k);
+SL_API int sl_rsvd_bnd_set_fault(const void* bws, int missing, uint64_t bound_ticks);
 SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* bws, int* status, int status_or,
-                            double* Rinv, void* Zt, float* M, double* N, double* s64, int max_sweeps, double* V0,
-                            int* v0_valid, int* mirror, float* V, float* s32, float* const* optr, void* stream);
+                            double* Rinv, void* Zt, float* M, double* N, double* s64, int* mirror, float* V,
+                            float* s32, float* const* optr, void* stream);
 SL_API int sl_tsk_f32_xm_ind(const float* Y, int64_t m, int k, const float* M, int k2, float* const* optr,
                              void* stream);
 SL_API int sl_rsvd_fjlt_zt_tab(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k, int n, void* Zt,
@@ -80,10 +82,7 @@ struct Plan {
   float* M = nullptr;       // k x r
   double* N = nullptr;      // k x r
   double* s64 = nullptr;    // r
-  double* V0 = nullptr;     // kp x kp: the last core eigenvectors (Jacobi warm start)
-  int* v0_valid = nullptr;
   float** optr = nullptr;   // {U, s, V} of the current call (the graph's finish reads them)
-  bool warm = true;
   int* status = nullptr;
   int* mirror_host = nullptr;   // host-mapped copy of the status word, written by the final kernel
   int* mirror_dev = nullptr;
@@ -120,8 +119,7 @@ int seg(Plan* p, const void* A, int i, hipStream_t s, float* V = nullptr, float*
   if (i > 0) {
     const int fin = i == p->q + 1 ? 1 : 0;
     rc = sl_rsvd_boundary(fin, (int)p->n, p->k, p->r, p->WG, p->bnd_ws, p->status, 1, p->Rinv, p->Zt, p->M, p->N,
-                          p->s64, 0, p->warm ? p->V0 : nullptr, p->warm ? p->v0_valid : nullptr, p->mirror_dev,
-                          V, s32, optr, s);
+                          p->s64, p->mirror_dev, V, s32, optr, s);
     if (rc != SL_OK || fin) return rc;
   }
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
@@ -209,8 +207,6 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   const int64_t o_n = off;    off = align256(off + (int64_t)k * r * 8);
   const int64_t o_s = off;    off = align256(off + (int64_t)r * 8);
   const int64_t o_st = off;   off = align256(off + 16);
-  const int kp = k + (k & 1);
-  const int64_t o_v0 = off;   off = align256(off + (int64_t)kp * kp * 8 + 16);
   const int64_t o_op = off;   off = align256(off + 4 * (int64_t)sizeof(float*));
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;
@@ -227,11 +223,9 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   p->N = (double*)(p->base + o_n);
   p->s64 = (double*)(p->base + o_s);
   p->status = (int*)(p->base + o_st);
-  p->V0 = (double*)(p->base + o_v0);
-  p->v0_valid = (int*)(p->base + o_v0 + (int64_t)kp * kp * 8);
   p->optr = (float**)(p->base + o_op);
   if (hipMemset(p->bnd_ws, 0, (size_t)sl_rsvd_bnd_workspace(k)) != hipSuccess ||
-      hipMemset(p->status, 0, 16) != hipSuccess || hipMemset(p->v0_valid, 0, 16) != hipSuccess) {
+      hipMemset(p->status, 0, 16) != hipSuccess) {
     (void)hipFree(p->base);
     delete p;
     sl_set_last_error("rsvd_plan: memset failed");
@@ -252,6 +246,7 @@ SL_API int sl_rsvd_plan_destroy(void* plan) {
   Plan* p = (Plan*)plan;
   if (!p) return SL_OK;
   drop_graph(p);
+  (void)sl_rsvd_bnd_set_fault(p->bnd_ws, 0, 0);
   if (p->cap_ev) (void)hipEventDestroy(p->cap_ev);
   if (p->cap_stream) (void)hipStreamDestroy(p->cap_stream);
   if (p->mirror_host) (void)hipHostFree(p->mirror_host);
@@ -271,13 +266,15 @@ SL_API int sl_rsvd_plan_bind(void* plan, double* WG, int* status) {
   return SL_OK;
 }
 
-// Jacobi warm start from the previous call's core eigenvectors (default on;
-// off: every call starts the eigensolve from the identity)
-SL_API int sl_rsvd_plan_set_warm(void* plan, int warm) {
+// Test-only fault injection: the boundary kernels wait for `missing` arrivals
+// beyond their grid (no workgroup is ever last, every wait times out and sets
+// status bit 16) with a spin bound of `bound_ticks` of the 100 MHz clock
+// (0: 2 s).  A plan that has timed out is not reusable (its sync words are
+// left mid-protocol): destroy it.
+SL_API int sl_rsvd_plan_set_fault(void* plan, int missing, uint64_t bound_ticks) {
   Plan* p = (Plan*)plan;
-  if (p->warm != (warm != 0)) drop_graph(p);
-  p->warm = warm != 0;
-  return SL_OK;
+  drop_graph(p);   // launch arguments are baked into a captured graph
+  return sl_rsvd_bnd_set_fault(p->bnd_ws, missing, bound_ticks);
 }
 
 // Sketch operator of the call: the FJLT of reference FJLT_data (N Rademacher

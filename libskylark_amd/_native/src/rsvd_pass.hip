@@ -524,11 +524,7 @@ int launch_pass(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt
   constexpr int LDS = pass_lds<WAVES, NW, KT, NBUF, FINAL>();
   static_assert(LDS <= 160 * 1024, "LDS budget");
   auto kern = k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL>;
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
-    attr = true;
-  }
+  SL_LDS_ATTR(kern, LDS);
   kern<<<grid, G::THREADS, LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch);
   SL_LAUNCH_CHECK();
   return SL_OK;

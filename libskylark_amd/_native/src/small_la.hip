@@ -13,6 +13,7 @@
 // Reference counterpart: El::Cholesky / El::Trsm on [*,*] matrices inside
 // nla/svd.hpp and ml/krr.hpp.
 #include "sl_common.hpp"
+#include "sl_wave_la.hpp"
 #include <stdlib.h>
 
 namespace {
@@ -461,6 +462,37 @@ SL_API int sl_small_matmul(const double* A, const double* B, double* C, int m, i
   int blocks = (m * n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   k_small_matmul<<<blocks, 256, 0, (hipStream_t)stream>>>(A, B, C, m, kk, n, C32);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// ------------------------------------------------------------------------
+// X = R^{-1} (upper) of G = R^T R (k <= 64) by one wave with the matrix in
+// registers (sl_wave_la.hpp wave_chol_inv: in-place LDL^T of [G | I]); the
+// kernel the randSVD pass boundaries run, as a standalone launch.  Status
+// bit 1: a pivot at or below 1e-13 max G_ii was dropped.
+namespace {
+template <int K>
+__global__ void __launch_bounds__(64) k_chol_inv_wave(const double* __restrict__ G, int k, int ldg,
+                                                      double* __restrict__ X, int* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) double fsh[192];
+  __shared__ int st;
+  if (threadIdx.x == 0) st = 0;
+  __syncthreads();
+  slw::wave_chol_inv<K>(G, ldg, X, k, k, fsh, &st);
+  __syncthreads();
+  if (threadIdx.x == 0 && status && st) atomicOr(status, st);
+}
+}  // namespace
+
+SL_API int sl_chol_inv_wave(const double* G, int k, int ldg, double* X, int* status, void* stream) {
+  if (k < 1 || k > 64 || ldg < k) { sl_set_last_error("chol_inv_wave: 1 <= k <= 64"); return SL_ERR_DIMENSION; }
+  hipStream_t s = (hipStream_t)stream;
+  if (k <= 16) k_chol_inv_wave<16><<<1, 64, 0, s>>>(G, k, ldg, X, status);
+  else if (k <= 32) k_chol_inv_wave<32><<<1, 64, 0, s>>>(G, k, ldg, X, status);
+  else if (k <= 40) k_chol_inv_wave<40><<<1, 64, 0, s>>>(G, k, ldg, X, status);
+  else if (k <= 48) k_chol_inv_wave<48><<<1, 64, 0, s>>>(G, k, ldg, X, status);
+  else k_chol_inv_wave<64><<<1, 64, 0, s>>>(G, k, ldg, X, status);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

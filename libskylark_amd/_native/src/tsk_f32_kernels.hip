@@ -418,11 +418,9 @@ k_xm_bf16t(const float* __restrict__ Y, int64_t m, int k, int64_t ldy, const flo
 constexpr int XM_PIPE_GRID_MAX = 2048;
 size_t xm_pipe_lds(int k, int k2) {
   const size_t b = (size_t)WPB * 32 * ((k + 1) + k2) * sizeof(float);
-  static bool attr = false;
-  if (b > 64 * 1024 && !attr) {   // k, k2 near 64: past the default dynamic-LDS cap
-    (void)hipFuncSetAttribute((const void*)k_xm_pipe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_xm_pipe<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-    attr = true;
+  if (b > 64 * 1024) {   // k, k2 near 64: past the default dynamic-LDS cap (per device)
+    (void)sl_lds_attr((const void*)k_xm_pipe<1>, 96 * 1024);
+    (void)sl_lds_attr((const void*)k_xm_pipe<2>, 96 * 1024);
   }
   return b;
 }

@@ -600,11 +600,7 @@ int launch_x(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, i
            float* Gslab, float* Y, int64_t ldy, hipStream_t s) {
   using GG = Geo<NW, KT, NBUF, 1>;
   auto kern = k_tsk_pass<NW, KT, DO_W, DO_G, STORE_Y, ZSPLIT, NBUF, HI_T, G64, X>;
-  static bool attr = false;
-  if (!attr) {
-    SL_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, GG::LDS));
-    attr = true;
-  }
+  SL_LDS_ATTR(kern, GG::LDS);
   kern<<<grid_for(m), THREADS, GG::LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, g_flags);
   SL_LAUNCH_CHECK();
   return SL_OK;

@@ -52,6 +52,7 @@ class ApproximateSVDParams:
     skip_qr: bool = False
     sketch: str = "JLT"          # "JLT" (reference) | "FJLT" | "CWT"
     graph: bool = True           # replay the device path as hipGraphs once warm
+    check: bool = False          # device path: wait for this call's status word and raise on a failure
     am_i_printing: bool = False
     log_level: int = 0
     prefix: str = ""
@@ -292,6 +293,7 @@ def _engine_lib():
         _lib.register("sl_rsvd_plan_bind", [vp_, vp_, vp_])
         _lib.register("sl_rsvd_status_mirror", [vp_], vp_)
         _lib.register("sl_rsvd_flush", [vp_, vp_])
+        _lib.register("sl_rsvd_plan_set_fault", [vp_, i32_, u64_])
     return _lib
 
 
@@ -303,7 +305,7 @@ class _EnginePlan:
     """Device randSVD for one (A, k, rank, q) configuration on the C++ engine
     (``_native/src/rsvd_engine.cpp``): every stage of the call -- sketch
     operator, q + 1 fused passes, the CholeskyQRs between them, the fp64
-    core (Cholesky, C = Rt^-T W^T W Rt^-1, Jacobi eigensolve) and the
+    core (Cholesky, C = Rt^-T W^T W Rt^-1, tridiagonal eigensolve) and the
     U = Y M / V = W N finish -- runs on the GPU; nothing returns to the host
     inside a call.
 
@@ -313,9 +315,12 @@ class _EnginePlan:
     buffer between them; when every all-reduce is the one-shot IPC kernel
     the segments and collectives are captured as one torch CUDA graph.
 
-    The device status word (pivot dropped, non-finite data, no Jacobi
-    convergence, rank < r) is copied back asynchronously; a flag of a call
-    is reported by the next one (``last_status``), never by a host sync."""
+    The device status word (pivot dropped, non-finite data, no eigensolver
+    convergence, rank < r, a boundary wait timed out) is copied back
+    asynchronously: by default a flag of a call is reported by the next call
+    on the plan (``last_status``), never by a host sync.  With
+    ``ApproximateSVDParams(check=True)`` the call itself synchronises on its
+    own status word and raises (timeout, non-finite data) before returning."""
 
     def __init__(self, A_loc, comm, n, rank, k, q, use_graph):
         L = _engine_lib()
@@ -343,6 +348,7 @@ class _EnginePlan:
         self.status_host = torch.zeros(1, dtype=torch.int32).pin_memory() if self.mirror is None else None
         self.status_ev = None
         self.last_status = 0
+        self.poisoned = False
         self.calls = 0
         self.g = None          # multi-rank: torch graph of segments + one-shot all-reduces
         self.g_failed = False
@@ -422,27 +428,48 @@ class _EnginePlan:
 
     def _poll_status(self):
         if self.status_ev is not None and self.status_ev.query():
+            self.status_ev = None   # consumed: a flag is reported once
             self.last_status = self._status_word()
-            if self.last_status & ST_TIMEOUT:
-                raise RuntimeError("approximate_svd (device): a pass-boundary kernel timed out waiting for its "
-                                   "last workgroup (status 16); the previous call's results are invalid")
-            if self.last_status & (ST_NONFINITE | ST_RANK | ST_NOCONV):
-                import warnings
-                warnings.warn(f"approximate_svd (device): previous call flagged status {self.last_status} "
-                              "(2: non-finite data, 4: eigensolver not converged, 8: numerical rank < r)",
-                              RuntimeWarning, stacklevel=3)
+            self._report(self.last_status, "previous call")
+
+    def _report(self, st, which):
+        if st & ST_TIMEOUT:
+            self.poisoned = True   # sync words left mid-protocol: never reused
+            _drop_plan(self)
+            raise RuntimeError(f"approximate_svd (device): a pass-boundary wait timed out (status {st}); "
+                               f"the {which}'s results are invalid")
+        if st & (ST_NONFINITE | ST_RANK | ST_NOCONV):
+            import warnings
+            warnings.warn(f"approximate_svd (device): {which} flagged status {st} "
+                          "(2: non-finite data, 4: eigensolver not converged, 8: numerical rank < r)",
+                          RuntimeWarning, stacklevel=4)
 
     def _status_word(self) -> int:
+        mask = ST_PIVOT | ST_NONFINITE | ST_NOCONV | ST_RANK | ST_TIMEOUT
         if self.mirror is not None and self.comm.size == 1:
-            return int(self.mirror.value) & 15
-        return int(self.status_host[0]) & 15
+            return int(self.mirror.value) & mask
+        return int(self.status_host[0]) & mask
 
     def wait_status(self) -> int:
-        """Synchronise with the last call and return its status bits."""
+        """Synchronise with the last call and return its status bits (read
+        from the device status word itself)."""
         if self.status_ev is not None:
             self.status_ev.synchronize()
-            self.last_status = self._status_word()
+            self.status_ev = None
+            mask = ST_PIVOT | ST_NONFINITE | ST_NOCONV | ST_RANK | ST_TIMEOUT
+            self.last_status = (int(self.status_dev.cpu()[0]) | self._status_word()) & mask
         return self.last_status
+
+    def check(self):
+        """Raise / warn on this plan's most recent call (synchronises)."""
+        st = self.wait_status()
+        self._report(st, "call")
+
+
+def _drop_plan(plan):
+    for key, p in list(_PLANS.items()):
+        if p is plan:
+            _PLANS.pop(key, None)
 
 
 def _destroy_plan(ptr):
@@ -500,14 +527,17 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     key = (A_loc.data_ptr(), tuple(A_loc.shape), tuple(A_loc.stride()), str(dev), rank, k, q, comm.size,
            id(getattr(comm, "group", None)))
     plan = _PLANS.get(key)
-    if plan is not None and plan.Aref() is None:
-        plan = None  # the operand this plan was built for is gone
+    if plan is not None and (plan.Aref() is None or plan.poisoned):
+        plan = None  # the operand this plan was built for is gone / a timed-out plan
     if plan is None:
         if len(_PLANS) >= 4:
             _PLANS.pop(next(iter(_PLANS)))
         plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
         _PLANS[key] = plan
-    return plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
+    out = plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
+    if params.check:
+        plan.check()
+    return out
 
 
 def last_device_status(wait: bool = True) -> int:

@@ -41,9 +41,9 @@ _lib.register("sl_sym_eig_tridiag", [vp, i32, i32, i32, vp, i32, vp, vp])
 def sym_eig_tridiag(C: torch.Tensor, r: int, out: torch.Tensor | None = None, sqrt: bool = False,
                     status: torch.Tensor | None = None, ldc: int | None = None):
     """Top-``r`` eigenpairs (descending) of a symmetric k x k matrix (k <= 64,
-    r <= 32) in one launch: Householder tridiagonalisation, multisection on
-    Sturm counts, twisted-factorisation eigenvectors, back-transform
-    (``sym_eig.hip``).  Output packed as :func:`sym_eig_topr`; ``status`` (int32)
+    r <= k) in one launch: Householder tridiagonalisation on one wave,
+    multisection on division-free Sturm counts, twisted-factorisation
+    eigenvectors, back-transform (``sym_eig.hip`` on ``sl_wave_la.hpp``).  Output packed as :func:`sym_eig_topr`; ``status`` (int32)
     gets bit 1 when the result must be recomputed on the host (near-repeated
     eigenvalues, non-finite data or a vanishing r-th eigenvalue).  ``C`` may be
     any f64 device buffer holding the matrix with row stride ``ldc``."""
@@ -55,6 +55,21 @@ def sym_eig_tridiag(C: torch.Tensor, r: int, out: torch.Tensor | None = None, sq
     _lib.call("sl_sym_eig_tridiag", _lib.ptr(C), k, k, r, _lib.ptr(out), int(bool(sqrt)),
               _lib.ptr(status) if status is not None else None, vp(_lib.stream_of(C)))
     return out
+
+
+_lib.register("sl_chol_inv_wave", [vp, i32, i32, vp, vp, vp])
+
+
+def chol_inv_wave(G: torch.Tensor, status: torch.Tensor | None = None) -> torch.Tensor:
+    """R^{-1} (upper, f64) of G = R^T R (k <= 64) by the one-wave register
+    kernel the randSVD boundaries use; dropped pivots (<= 1e-13 max G_ii) give
+    zero rows / columns and set status bit 1."""
+    k = G.shape[0]
+    G = G.to(torch.float64).contiguous()
+    X = torch.empty(k, k, dtype=torch.float64, device=G.device)
+    _lib.call("sl_chol_inv_wave", _lib.ptr(G), k, k, _lib.ptr(X), _lib.ptr(status) if status is not None else None,
+              vp(_lib.stream_of(G)))
+    return X
 
 
 def chol_inv(G: torch.Tensor, status: torch.Tensor | None = None):

@@ -20,8 +20,8 @@ def L():
     from libskylark_amd.ops import _lib
     _lib.require()
     _lib.register("sl_rsvd_bnd_workspace", [i32], C.c_int64)
-    _lib.register("sl_rsvd_boundary", [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, i32,
-                                       vp, vp, vp, vp, vp, vp, vp])
+    _lib.register("sl_rsvd_boundary", [i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp,
+                                       vp, vp, vp, vp, vp])
     return _lib
 
 
@@ -49,7 +49,7 @@ def test_boundary_inter(L, n, k):
     s = vp(torch.cuda.current_stream().cuda_stream)
     for it in range(3):   # ticket reset / generation advance across launches
         L.call("sl_rsvd_boundary", 0, n, k, 0, _p(WG), _p(bws), _p(st), 0, _p(Rinv), _p(Zt),
-               None, None, None, 0, None, None, None, None, None, None, s)
+               None, None, None, None, None, None, None, s)
     torch.cuda.synchronize()
     assert int(st[0]) == 0          # stored (status_or = 0), not OR-ed into 99
     sync = bws[:256].view(torch.int32).cpu().numpy()
@@ -86,7 +86,7 @@ def test_boundary_final(L, n, k, r):
     s = vp(torch.cuda.current_stream().cuda_stream)
     for _ in range(2):
         L.call("sl_rsvd_boundary", 1, n, k, r, _p(WG), _p(bws), _p(st), 1, None, None,
-               _p(M), _p(N), _p(s64), 0, None, None, None, _p(V), _p(s32), None, s)
+               _p(M), _p(N), _p(s64), None, _p(V), _p(s32), None, s)
     torch.cuda.synchronize()
     assert int(st[0]) == 1, int(st[0])   # OR-ed into the preset pivot bit, nothing else
     Rt = np.linalg.cholesky(Gy).T
@@ -113,7 +113,7 @@ def test_boundary_rejects_bad_shapes(L):
     bws = torch.zeros(int(L.require().sl_rsvd_bnd_workspace(4)), dtype=torch.uint8, device=dev)
     fn = _lib.require().sl_rsvd_boundary
     # n % 8 != 0, k > 48: refused before any launch
-    assert fn(0, 20, 4, 0, _p(WG), _p(bws), None, 0, None, None, None, None, None, 0, None, None, None,
+    assert fn(0, 20, 4, 0, _p(WG), _p(bws), None, 0, None, None, None, None, None, None,
               None, None, None, None) != 0
-    assert fn(0, 64, 49, 0, _p(WG), _p(bws), None, 0, None, None, None, None, None, 0, None, None, None,
+    assert fn(0, 64, 49, 0, _p(WG), _p(bws), None, 0, None, None, None, None, None, None,
               None, None, None, None) != 0

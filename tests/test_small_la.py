@@ -32,6 +32,40 @@ def test_chol_inv(dev, k, impl):
     torch.testing.assert_close(Ri32.cpu().double(), Ri.cpu(), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("k", [1, 7, 16, 17, 33, 40, 41, 48, 64])
+def test_chol_inv_wave(dev, k):
+    """One-wave register Cholesky inverse (the randSVD boundary kernel) vs
+    LAPACK: R^{-1} R = I to the attainable ~eps cond(G)."""
+    g = torch.Generator().manual_seed(k)
+    X = torch.randn(3 * k + 5, k, generator=g, dtype=torch.float64) @ torch.diag(torch.logspace(0, 3, k,
+                                                                                               dtype=torch.float64))
+    G = X.t() @ X
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    Ri = SL.chol_inv_wave(G.to(dev), st).cpu()
+    assert int(st) == 0
+    Rr = torch.linalg.cholesky(G).t()
+    assert float(torch.tril(Ri, -1).abs().max()) == 0.0
+    e_ref = float((torch.linalg.inv(Rr).t() @ G @ torch.linalg.inv(Rr) - torch.eye(k, dtype=torch.float64)).abs().max())
+    e = float((Ri.t() @ G @ Ri - torch.eye(k, dtype=torch.float64)).abs().max())
+    assert e <= max(8 * e_ref, 1e-12), (e, e_ref)
+    torch.testing.assert_close(Ri, torch.linalg.inv(Rr), rtol=1e-8, atol=1e-8 * float(Ri.abs().max()))
+
+
+def test_chol_inv_wave_drops_dependent_direction(dev):
+    k = 12
+    g = torch.Generator().manual_seed(3)
+    W = torch.randn(200, k, generator=g, dtype=torch.float64)
+    W[:, 5] = 2.0 * W[:, 2]
+    G = W.t() @ W
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    Ri = SL.chol_inv_wave(G.to(dev), st).cpu()
+    assert int(st) & 1
+    assert float(Ri[:, 5].abs().max()) == 0.0 and float(Ri[5, :].abs().max()) == 0.0
+    Q = W @ Ri
+    keep = [j for j in range(k) if j != 5]
+    torch.testing.assert_close(Q[:, keep].t() @ Q[:, keep], torch.eye(k - 1, dtype=torch.float64), atol=1e-8, rtol=0)
+
+
 def test_chol_inv_flags_breakdown(dev, impl):
     G = torch.zeros(5, 5, dtype=torch.float64, device=dev)
     G[0, 0] = 1
@@ -110,7 +144,8 @@ def _eig_check(C, out, k, r):
     assert torch.allclose(V.t() @ V, torch.eye(r, dtype=torch.float64), atol=1e-10)
 
 
-@pytest.mark.parametrize("k,r", [(40, 20), (7, 3), (64, 32), (48, 10), (2, 1), (1, 1), (3, 3), (33, 32)])
+@pytest.mark.parametrize("k,r", [(40, 20), (7, 3), (64, 32), (48, 10), (2, 1), (1, 1), (3, 3), (33, 32), (40, 40),
+                                 (64, 64), (17, 16)])
 @pytest.mark.parametrize("kind", ["uniform", "logspace", "planted", "gram", "indefinite"])
 def test_sym_eig_tridiag_vs_lapack(dev, k, r, kind):
     """Device tridiagonal eigensolver (Householder + multisection + twisted
