@@ -26,6 +26,7 @@ for k, r in ((40, 20), (48, 24), (32, 16), (64, 32)):
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     s = vp(torch.cuda.current_stream().cuda_stream)
     acc = [0.0] * 5
+    sub = [0.0] * 5
     n = 20
     for it in range(n + 2):
         lib.sl_sym_eig_tridiag(vp(Cm.data_ptr()), k, k, r, vp(o.data_ptr()), 0, vp(st.data_ptr()), s)
@@ -35,5 +36,8 @@ for k, r in ((40, 20), (48, 24), (32, 16), (64, 32)):
         if it >= 2:
             for p in range(5):
                 acc[p] += (h[p + 1] - h[p]) / n
+                sub[p] += (h[11 + p] - h[10 + p]) / n
     print(json.dumps({"k": k, "r": r, "status": int(st.item()),
-                      "phase_cycles": {nm: round(a) for nm, a in zip(names, acc)}}))
+                      "phase_cycles": {nm: round(a) for nm, a in zip(names, acc)},
+                      "tridiag_step10_cycles": {nm: round(a) for nm, a in
+                                                zip(["s2+v+bcast", "p", "Kd", "w+bcast", "update"], sub)}}))

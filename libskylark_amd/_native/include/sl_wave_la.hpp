@@ -184,9 +184,18 @@ template <int K, int J>
 __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* wsh, double* refl, int ldr,
                                          double* dd, double* ee) {
   constexpr int c0 = (J + 1) & ~1;
+  if (J == 10) { SLW_STAMP(10) }
+  // ||x||^2 of column J below the diagonal and its first entry: row J of the
+  // (symmetric) trailing matrix, summed by lane J alone -- no cross-lane sum
+  double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+  for (int c = J + 1; c < K; c += 2) {
+    q0 = fma(arow[c], arow[c], q0);
+    if (c + 1 < K) q1 = fma(arow[c + 1], arow[c + 1], q1);
+  }
+  const double s2 = lane_d(q0 + q1, J);
+  const double x0 = lane_d(arow[J + 1], J);
   const double xi = (i > J) ? arow[J] : 0.0;
-  const double s2 = wave_sum(xi * xi);
-  const double x0 = lane_d(xi, J + 1);
   const double sig2 = s2 - x0 * x0;
   const bool refl_on = sig2 > 1e-300;
   const double alpha = refl_on ? (x0 >= 0.0 ? -sqrt(s2) : sqrt(s2)) : x0;
@@ -198,6 +207,7 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
     refl[i * ldr + J] = vi;
   }
   wave_lds_sync();
+  if (J == 10) { SLW_STAMP(11) }
   // p = A v, v streamed from LDS in pairs (entry J, when the first pair
   // starts there, has v_J = 0)
   double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
@@ -213,10 +223,13 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
     }
   }
   const double p = (p0 + p1) + (p2 + p3);
+  if (J == 10) { SLW_STAMP(12) }
   const double Kd = wave_sum(vi * p);
+  if (J == 10) { SLW_STAMP(13) }
   const double wi = (i > J) ? 2.0 * (p - Kd * vi) : 0.0;
   if (i < K) wsh[i] = wi;
   wave_lds_sync();
+  if (J == 10) { SLW_STAMP(14) }
   // A -= v w^T + w v^T on the trailing columns (v, w streamed again)
 #pragma unroll
   for (int c = c0; c < K; c += 2) {
@@ -225,6 +238,7 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
     arow[c] = fma(-vi, tw.x, fma(-wi, tv.x, arow[c]));
     arow[c + 1] = fma(-vi, tw.y, fma(-wi, tv.y, arow[c + 1]));
   }
+  if (J == 10) { SLW_STAMP(15) }
 }
 
 // vsh / wsh: 2 x K doubles each (alternate steps use alternate halves, so a
@@ -270,33 +284,47 @@ __device__ __forceinline__ void wave_tridiag(const double* C, int ldc, int k, do
 }
 
 // ------------------------------------------- symmetric tridiagonal eigen
-// Sturm count of eigenvalues of T below x, division-free: the characteristic
-// polynomials p_i(x) (p_{i+1} = (d_i - x) p_i - e_{i-1}^2 p_{i-1}); a sign
-// change between p_i and p_{i+1} is a negative LDL^T pivot.  T is pre-scaled
-// to ||T|| ~ 1 and p is re-normalised every 8 steps (exponent only), so
-// nothing over- or underflows.  One FMA of latency per step; de2[i] =
-// {d_i, e_{i-1}^2} is read from LDS (a broadcast: every lane of the wave
-// reads the same pair), 8 steps unrolled.
-template <int K>
-__device__ __forceinline__ int sturm_count(const double2* de2, double x) {
-  double pp = 1.0, p = de2[0].x - x;
-  if (p == 0.0) p = -0x1p-60;
-  int cnt = p < 0.0;
-#pragma unroll 8
+// Sturm counts of eigenvalues of T below P points at once, division-free:
+// the characteristic polynomials p_i(x) (p_{i+1} = (d_i - x) p_i - e_{i-1}^2
+// p_{i-1}); a sign change between p_i and p_{i+1} is a negative LDL^T pivot.
+// T is pre-scaled to ||T|| ~ 1 and p is re-normalised every 8 steps
+// (exponent only), so nothing over- or underflows.  One FMA of latency per
+// step and point; the P chains interleave.  (An exactly zero p_i -- measure
+// zero -- counts as positive, i.e. the count of a point a rounding error
+// away.)
+template <int K, int P>
+__device__ __forceinline__ void sturm_counts(const double (&d)[K], const double (&e2)[K], const double (&x)[P],
+                                             int (&cnt)[P]) {
+  double p[P], pp[P];
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    pp[q] = 1.0;
+    p[q] = d[0] - x[q];
+    cnt[q] = p[q] < 0.0;
+  }
+#pragma unroll
   for (int i = 1; i < K; ++i) {
-    const double2 q = de2[i];
-    double pn = fma(q.x - x, p, -q.y * pp);
-    if (pn == 0.0) pn = -p * 0x1p-60;
-    cnt += (pn < 0.0) != (p < 0.0);
-    pp = p;
-    p = pn;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const double pn = fma(d[i] - x[q], p[q], -e2[i - 1] * pp[q]);
+      cnt[q] += (pn < 0.0) != (p[q] < 0.0);
+      pp[q] = p[q];
+      p[q] = pn;
+    }
     if ((i & 7) == 7) {
-      const int ex = __builtin_amdgcn_frexp_exp(p);
-      p = __builtin_amdgcn_ldexp(p, -ex);
-      pp = __builtin_amdgcn_ldexp(pp, -ex);
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const int ex = __builtin_amdgcn_frexp_exp(p[q]);
+        p[q] = __builtin_amdgcn_ldexp(p[q], -ex);
+        pp[q] = __builtin_amdgcn_ldexp(pp[q], -ex);
+      }
     }
   }
-  return cnt;
+}
+
+__device__ __forceinline__ double rcp64n(double d) {   // estimate + one Newton step
+  const double r = __builtin_amdgcn_rcp(d);
+  return r * fma(-d, r, 2.0);
 }
 
 // Eigenpairs of the symmetric K x K matrix given by its tridiagonal form
@@ -304,7 +332,7 @@ __device__ __forceinline__ int sturm_count(const double2* de2, double x) {
 // in lam[0..nt-1] and the eigenvectors of the ORIGINAL matrix (Q x) for the
 // first nv <= 64 of them in X[i * ldx + t] (rows i < kx <= K).  Every thread of the
 // workgroup (NT threads, NT % 64 == 0) calls it; dd / ee are overwritten
-// (scaled).  Scratch: sc >= nv * (K + 1) doubles of LDS.  *st bit 1: numerically repeated eigenvalues among the
+// (scaled).  Scratch: sc >= 3 nv (K + 1) doubles of LDS.  *st bit 1: numerically repeated eigenvalues among the
 // wanted ones, a vector that fails the residual check or non-finite values --
 // the caller should fall back to a robust solver.
 template <int K, int NT>
@@ -331,41 +359,62 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     de2[tid] = double2{dd[tid] * itn, em * em};
   }
   __syncthreads();
-  // ---- multisection: 16 lanes (one DPP row) per eigenvalue, 16 points per
-  //      round (bracket / 17 per round), rows of a wave run independently
+  // ---- multisection: 16 lanes (one DPP row) per eigenvalue, MP points per
+  //      lane (16 MP per round: bracket / (16 MP + 1) per round), rows of a
+  //      wave run independently; T in registers
   constexpr double eps = 2.220446049250313e-16;
+  constexpr int MP = 2;
   const int row = tid >> 4, g = tid & 15;
   constexpr int ROWS = NT / 16;
-  for (int t0 = 0; t0 < nt; t0 += ROWS) {
-    const int t = t0 + row;
-    const bool act = t < nt;
-    const int idx = K - 1 - t;   // ascending index of this row's eigenvalue
-    double lo = -1.0 - 4.0 * eps, hi = 1.0 + 4.0 * eps;
-    for (int it = 0; it < 64; ++it) {
-      const bool conv = !act || (hi - lo) <= fmax(4.0 * eps, 2.0 * eps * fmax(fabs(lo), fabs(hi)));
-      if (__builtin_amdgcn_ballot_w64(!conv) == 0) break;
-      const double x = lo + (hi - lo) * (double)(g + 1) * (1.0 / 17.0);
-      const int c = act ? sturm_count<K>(de2, x) : 0;
-      // fewer than idx + 1 eigenvalues below x: x is a lower bound
-      double nlo = c <= idx ? x : lo, nhi = c <= idx ? hi : x;
-      nlo = fmax(nlo, dpp<0xB1>(nlo));
-      nhi = fmin(nhi, dpp<0xB1>(nhi));
-      nlo = fmax(nlo, dpp<0x4E>(nlo));
-      nhi = fmin(nhi, dpp<0x4E>(nhi));
-      nlo = fmax(nlo, dpp<0x141>(nlo));
-      nhi = fmin(nhi, dpp<0x141>(nhi));
-      nlo = fmax(nlo, dpp<0x140>(nlo));
-      nhi = fmin(nhi, dpp<0x140>(nhi));
-      if (act && !conv) { lo = nlo; hi = nhi; }
+  {
+    double d[K], e2[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const double2 q = de2[i];
+      d[i] = q.x;
+      e2[i] = i + 1 < K ? de2[i + 1].y : 0.0;
     }
-    if (act && g == 0) lam[t] = 0.5 * (lo + hi);   // scaled
+    for (int t0 = 0; t0 < nt; t0 += ROWS) {
+      const int t = t0 + row;
+      const bool act = t < nt;
+      const int idx = K - 1 - t;   // ascending index of this row's eigenvalue
+      double lo = -1.0 - 4.0 * eps, hi = 1.0 + 4.0 * eps;
+      for (int it = 0; it < 64; ++it) {
+        const bool conv = !act || (hi - lo) <= fmax(4.0 * eps, 2.0 * eps * fmax(fabs(lo), fabs(hi)));
+        if (__builtin_amdgcn_ballot_w64(!conv) == 0) break;
+        double x[MP];
+        int c[MP];
+#pragma unroll
+        for (int q = 0; q < MP; ++q) x[q] = lo + (hi - lo) * (double)(g * MP + q + 1) * (1.0 / (16 * MP + 1));
+        sturm_counts<K, MP>(d, e2, x, c);
+        // fewer than idx + 1 eigenvalues below x: x is a lower bound
+        double nlo = lo, nhi = hi;
+#pragma unroll
+        for (int q = 0; q < MP; ++q) {
+          if (c[q] <= idx) nlo = fmax(nlo, x[q]);
+          else nhi = fmin(nhi, x[q]);
+        }
+        nlo = fmax(nlo, dpp<0xB1>(nlo));
+        nhi = fmin(nhi, dpp<0xB1>(nhi));
+        nlo = fmax(nlo, dpp<0x4E>(nlo));
+        nhi = fmin(nhi, dpp<0x4E>(nhi));
+        nlo = fmax(nlo, dpp<0x141>(nlo));
+        nhi = fmin(nhi, dpp<0x141>(nhi));
+        nlo = fmax(nlo, dpp<0x140>(nlo));
+        nhi = fmin(nhi, dpp<0x140>(nhi));
+        if (act && !conv) { lo = nlo; hi = nhi; }
+      }
+      if (act && g == 0) lam[t] = 0.5 * (lo + hi);   // scaled
+    }
   }
   __syncthreads();
   SLW_STAMP(2)
   // ---- eigenvectors of T: one lane per vector (twisted factorisation of
-  //      the scaled T - l I).  sc[t * LZ + i] first holds the backward
-  //      pivots D-_i, then the vector; the forward pivots' reciprocals stay
-  //      in registers; d / e come from LDS (uniform broadcast reads)
+  //      the scaled T - l I).  Per lane t: zdm = sc[t * LZ + i] holds the
+  //      backward pivots D-_i (later the vector), zdp the forward pivots, zrd
+  //      the ratios -e_{i-1} / D-_i below the twist; the reciprocals of the
+  //      forward pivots stay in registers.  The backward and forward chains
+  //      run interleaved in one loop; d / e come from LDS (broadcast reads).
   constexpr int LZ = K + 1;   // sc[t * LZ + i]: vector t, component i
   if (tid < K) {
     dd[tid] *= itn;
@@ -379,57 +428,60 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     if (!(gap > 1e-13)) atomicOr(st, 1);       // numerically repeated (~ bisection accuracy): the caller falls back
     if (gap < 1e-3) atomicOr(&s_clus, 1);
     const double pivmin = 1e-290;
-    // backward pivots D-_i = (d_i - l) - e_i^2 / D-_{i+1}
+    double* zdm = sc + t * LZ;
+    double* zdp = sc + (nv + t) * LZ;
+    double* zrd = sc + (2 * nv + t) * LZ;
+    double rup[K];
     double dm = dd[K - 1] - l;
     if (fabs(dm) < pivmin) dm = -pivmin;
-    sc[t * LZ + (K - 1)] = dm;
-#pragma unroll 4
-    for (int i = K - 2; i >= 0; --i) {
-      const double ei = ee[i];
-      dm = (dd[i] - l) - (ei * ei) * rcp64(dm);
-      if (fabs(dm) < pivmin) dm = -pivmin;
-      sc[t * LZ + i] = dm;
-    }
-    // forward pivots D+_i and the twist gamma_i = D+_i + D-_i - (d_i - l)
-    double rup[K];
+    zdm[K - 1] = dm;
     double dp = dd[0] - l;
     if (fabs(dp) < pivmin) dp = -pivmin;
+    zdp[0] = dp;
+#pragma unroll
+    for (int s_ = 0; s_ < K - 1; ++s_) {
+      const int ib = K - 2 - s_, jf = s_ + 1;
+      const double eb = ee[ib], ef = ee[jf - 1];
+      const double rdm = rcp64n(dm);        // 1 / D-_{ib+1}
+      zrd[ib + 1] = -eb * rdm;
+      dm = (dd[ib] - l) - (eb * eb) * rdm;
+      if (fabs(dm) < pivmin) dm = -pivmin;
+      zdm[ib] = dm;
+      const double rdp = rcp64n(dp);        // 1 / D+_{jf-1}
+      rup[jf - 1] = rdp;
+      dp = (dd[jf] - l) - (ef * ef) * rdp;
+      if (fabs(dp) < pivmin) dp = -pivmin;
+      zdp[jf] = dp;
+    }
+    rup[K - 1] = rcp64n(dp);
+    // the twist: argmin |gamma_i|, gamma_i = D+_i + D-_i - (d_i - l)
     int rt = 0;
     double best = 1e300;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-      const double di = dd[i] - l;
-      if (i > 0) {
-        const double e = ee[i - 1];
-        dp = di - (e * e) * rup[i - 1];
-        if (fabs(dp) < pivmin) dp = -pivmin;
-      }
-      const double gm = fabs(dp + sc[t * LZ + i] - di);
+      const double gm = fabs(zdp[i] + zdm[i] - (dd[i] - l));
       if (gm < best) { best = gm; rt = i; }
-      rup[i] = rcp64(dp);
     }
-    // above the twist: z_i = -(e_i / D+_i) z_{i+1}; below: z_i = -(e_{i-1} / D-_i)
-    // z_{i-1} (D-_i still in sc there); z overwrites sc as it goes, the norm
-    // is applied by the back-transform
+    // above the twist: z_i = -(e_i / D+_i) z_{i+1}; below: z_i = ratio_i z_{i-1}
     double z = 1.0, nrm = 1.0;
 #pragma unroll
     for (int i = K - 2; i >= 0; --i) {
       if (i < rt) {
         z = -(ee[i] * rup[i]) * z;
         nrm = fma(z, z, nrm);
-        sc[t * LZ + i] = z;
+        zdm[i] = z;
       }
     }
     z = 1.0;
-#pragma unroll 4
+#pragma unroll
     for (int i = 1; i < K; ++i) {
       if (i > rt) {
-        z = -ee[i - 1] * rcp64(sc[t * LZ + i]) * z;
+        z = zrd[i] * z;
         nrm = fma(z, z, nrm);
-        sc[t * LZ + i] = z;
+        zdm[i] = z;
       }
     }
-    sc[t * LZ + rt] = 1.0;
+    zdm[rt] = 1.0;
     const double s = rsq64(nrm);
     if (!(s > 0.0) || !(s < 1e300)) atomicOr(st, 1);
     snorm[t] = s;

@@ -1,0 +1,536 @@
+// General-precision randomized SVD engine (reference nla/svd.hpp:222-318
+// ApproximateSVD with the power iteration of :71-149, templated there over
+// the operand type, double by default): f32 / f64 / bf16 row-distributed A,
+// any n (the bf16 fused engine, rsvd_engine.cpp, covers n <= 1024, k <= 48),
+// k <= 128, every stage on the device with no host round trip.
+//
+// One call = q + 2 segments on a HIP stream, the same contract as the fused
+// engine so one driver serves both (Python _EnginePlan, C sl_rsvd_gen_run_comm):
+//   seg 0        Y = A Z (Z = the sketch operator), W = A^T Y  -> WG[0 : n k]
+//   seg 1 .. q   H = W^T W, R^{-1} (Cholesky, pivot dropping), Z = W R^{-1},
+//                then the next pass (seg q also: G = Y^T Y in f64 -> WG[n k :])
+//   seg q + 1    the core: Rt^{-1} of G, C = Rt^{-T} W^T W Rt^{-1}, its top
+//                r + 1 eigenpairs, M = Rt^{-1} Ub_r, N = M S^{-1}, s
+// then the finish (V = W N, U = Y M) into the caller's buffers.  Between the
+// reducing segments several ranks all-reduce WG ((n + k) x k f64).
+//
+// The two products over A per pass are plain library GEMMs (rocBLAS: a tall
+// operand times an n x k panel, bandwidth-bound); the CholeskyQR factors and
+// the core eigensolver are the one-wave kernels of sl_wave_la.hpp for k <= 64
+// (sl_chol_inv_wave, sl_sym_eig_tridiag; Jacobi re-solve when flagged) and
+// rocSOLVER (potrf + trtri, syevd) for 64 < k <= 128.  W, H, G and the core
+// are f64 whatever A's precision.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <new>
+#include <type_traits>
+
+#include "sl_blas.hpp"
+#include "sl_common.hpp"
+#include "sl_rng.hpp"
+
+SL_API int sl_chol_inv_wave(const double* G, int k, int ldg, double* X, int* status, void* stream);
+SL_API int sl_sym_eig_tridiag(const double* C, int k, int ldc, int r, double* out, int want_sqrt, int* status,
+                              void* stream);
+SL_API int sl_sym_eig_topr_if(const double* C, int k, int ldc, int r, double* out, int want_sqrt, int max_sweeps,
+                              const int* flag, void* stream);
+SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_t base, int64_t rows, int64_t cols,
+                          int64_t sr, int64_t sc, int64_t r0, int64_t c0, int64_t ir, int64_t ic, double p0, double p1,
+                          double scale, int precise, void* stream);
+SL_API int64_t sl_tsk_gram64_workspace(int64_t m, int k);
+SL_API int sl_tsk_gram64(const float* Y, int64_t m, int k, int64_t ldy, double* G, void* ws, void* stream);
+SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
+                              void* stream);
+
+namespace {
+
+enum : int { ST_PIVOT = 1, ST_NONFINITE = 2, ST_NOCONV = 4, ST_RANK = 8 };
+
+template <typename T> __device__ __forceinline__ double ld_d(const T* p) { return (double)*p; }
+template <> __device__ __forceinline__ double ld_d<bf16_t>(const bf16_t* p) { return (double)bf16_to_f(*p); }
+template <typename T> __device__ __forceinline__ void st_d(T* p, double v) { *p = (T)v; }
+template <> __device__ __forceinline__ void st_d<bf16_t>(bf16_t* p, double v) { *p = f_to_bf16((float)v); }
+
+// out (rows x cols, ldo) = in (rows x cols, ldi), converted
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256) k_cast2d(const TI* __restrict__ in, int64_t ldi, int64_t rows, int cols,
+                                               TO* __restrict__ out, int64_t ldo, int* zero_word) {
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  const int64_t tot = rows * cols;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < tot; t += (int64_t)gridDim.x * 256) {
+    const int64_t i = t / cols;
+    const int j = (int)(t - i * cols);
+    st_d<TO>(out + i * ldo + j, ld_d<TI>(in + i * ldi + j));
+  }
+}
+
+// FJLT operator of the rowwise sketch A Omega^T as Z (n x k, row-major):
+// Z[i][j] = scale * d_i * c_{p_j} cos(pi p_j (2 i + 1) / 2n), d the n
+// Rademacher signs at stream offset baseD, p_j the k sampled DCT-II
+// frequencies at baseS (reference FJLT_data.hpp:79-86; the same operator as
+// the fused engine's k_fjlt_zt, transposed and in full precision)
+template <typename T>
+__global__ void __launch_bounds__(256) k_fjlt_z(uint64_t seed, uint64_t baseD, uint64_t baseS, double scale, int k,
+                                               int64_t n, T* __restrict__ Z) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * k) return;
+  const int64_t i = t / k;
+  const int j = (int)(t - i * k);
+  const int64_t p = sl::uniform_int(sl::stream_block(seed, baseS + (uint64_t)j).x, 0, n - 1);
+  const double d = (sl::stream_block(seed, baseD + (uint64_t)i).x >> 63) ? 1.0 : -1.0;
+  const int64_t a = (p * (2 * i + 1)) % (4 * n);
+  const double w = 3.14159265358979323846 / (2.0 * (double)n);
+  const double c0 = sqrt(1.0 / (double)n), c1 = sqrt(2.0 / (double)n);
+  st_d<T>(Z + t, cos(w * (double)a) * (p == 0 ? c0 : c1) * scale * d);
+}
+
+// bf16 hi / lo planes of an f32 matrix: hi = bf16(y), lo = bf16(y - hi)
+__global__ void __launch_bounds__(256) k_split_bf16(const float* __restrict__ y, int64_t tot, bf16_t* __restrict__ hi,
+                                                   bf16_t* __restrict__ lo) {
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < tot; t += (int64_t)gridDim.x * 256) {
+    const float v = y[t];
+    const bf16_t h = f_to_bf16(v);
+    hi[t] = h;
+    lo[t] = f_to_bf16(v - bf16_to_f(h));
+  }
+}
+
+// zero the strictly lower triangle of a row-major k x k (rocSOLVER leaves G there)
+__global__ void __launch_bounds__(256) k_triu(double* __restrict__ X, int k) {
+  for (int e = threadIdx.x; e < k * k; e += 256) {
+    const int i = e / k, c = e - i * k;
+    if (c < i) X[e] = 0.0;
+  }
+}
+
+// the core's epilogue: eig = [Ub_r (k x r); s (r)] from the eigensolver.
+// s_out (r, dtype T), N = M S^{-1} (k x r f64) from M (k x r f64), rank / finiteness status
+template <typename T>
+__global__ void __launch_bounds__(256) k_core_epi(const double* __restrict__ eig, int k, int r,
+                                                  const double* __restrict__ M, double* __restrict__ N,
+                                                  T* __restrict__ Md, int* __restrict__ status) {
+  const double* s = eig + k * r;
+  for (int e = threadIdx.x; e < k * r; e += 256) {
+    const int c = e % r;
+    const double sv = s[c];
+    N[e] = sv > 0.0 ? M[e] / sv : 0.0;
+    st_d<T>(Md + e, M[e]);
+  }
+  if (threadIdx.x == 0) {
+    int st = 0;
+    for (int c = 0; c < r; ++c) {
+      if (!(s[c] > 0.0)) st |= ST_RANK;
+      if (!(s[c] == s[c])) st |= ST_NONFINITE;
+    }
+    if (st) atomicOr(status, st);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_store_s(const double* __restrict__ s, int r, T* __restrict__ out) {
+  if ((int)threadIdx.x < r) st_d<T>(out + threadIdx.x, s[threadIdx.x]);
+}
+
+// Cholesky statuses (dropped pivots / rocSOLVER infos) -> the call's status word
+__global__ void k_status_merge(const int* __restrict__ chol_st, int nchol, int* __restrict__ status) {
+  if (threadIdx.x == 0) {
+    int st = 0;
+    for (int i = 0; i < nchol; ++i) st |= chol_st[i] ? ST_PIVOT : 0;
+    if (st) atomicOr(status, st);
+  }
+}
+
+int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
+
+constexpr int64_t GPIECE = 65536;   // rows per f64 staging piece of the k > 64 f32 Gram
+
+size_t esize(int dt) { return dt == SL_F64 ? 8 : dt == SL_F32 ? 4 : 2; }
+
+struct GPlan {
+  int64_t m = 0, n = 0, lda = 0;
+  int k = 0, r = 0, q = 0, dt = SL_F32;
+  char* base = nullptr;
+  void* Z = nullptr;       // n x k (dt)
+  void* Y = nullptr;       // m x k (dt; f32 when A is bf16)
+  void* Yh = nullptr;      // bf16 A: hi / lo planes of Y (m x k bf16 each)
+  void* Yl = nullptr;
+  void* Wt = nullptr;      // n x k pass output (dt; f32 when A is bf16)
+  double* WG = nullptr;    // [W (n x k); G (k x k)] f64
+  double* Zf = nullptr;    // n x k f64
+  double* H = nullptr;     // k x k
+  double* Ri = nullptr;    // k x k
+  double* T1 = nullptr;    // k x k
+  double* Cc = nullptr;    // k x k
+  double* eig = nullptr;   // k r + r (+ k for syevd eigenvalues, k scratch)
+  double* M = nullptr;     // k x r
+  double* N = nullptr;     // k x r
+  void* Md = nullptr;      // k x r (dt of U)
+  double* Vf = nullptr;    // n x r
+  void* gws = nullptr;     // f32 Gram workspace
+  int* st = nullptr;       // [0] status, [1..2] eig status, [4..11] chol statuses / infos
+  // sketch of the call
+  int sk = 0;              // 0 none, 1 FJLT, 2 dense
+  uint64_t seed = 0, b0 = 0, b1 = 0;
+  double p0 = 0, p1 = 0, scale = 1;
+  int dist = 0;
+};
+
+template <typename F>
+int dispatch_dt(int dt, F f) {
+  if (dt == SL_F32) return f((float*)nullptr);
+  if (dt == SL_F64) return f((double*)nullptr);
+  return f((bf16_t*)nullptr);
+}
+
+unsigned grid_of(int64_t tot) {
+  int64_t g = (tot + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+// X = R^{-1} of the SPD k x k G (row-major f64), status bit ST_PIVOT via st
+int chol_inv(GPlan* p, const double* G, double* X, int* st, hipStream_t s) {
+  if (p->k <= 64) return sl_chol_inv_wave(G, p->k, p->k, X, st, s);
+  SL_HIP_CHECK(hipMemcpyAsync(X, G, (size_t)p->k * p->k * 8, hipMemcpyDeviceToDevice, s));
+  int rc = slb_dpotrf_inv(p->k, X, p->k, st, s);
+  if (rc != SL_OK) return rc;
+  k_triu<<<1, 256, 0, s>>>(X, p->k);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// the sketch operator of the call into Z (dt)
+int make_z(GPlan* p, hipStream_t s) {
+  const int64_t tot = p->n * p->k;
+  if (p->sk == 1) {
+    return dispatch_dt(p->dt, [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      k_fjlt_z<T><<<(unsigned)((tot + 255) / 256), 256, 0, s>>>(p->seed, p->b0, p->b1, p->scale, p->k, p->n, (T*)p->Z);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    });
+  }
+  if (p->sk == 2) {
+    // dense: Z[i][j] = scale * dist(seed, base + i k + j) (column-major k x n stream of S = Z^T)
+    int rc = sl_fill_random(p->Zf, SL_F64, p->dist, p->seed, p->b0, p->n, p->k, p->k, 1, 0, 0, p->k, 1, p->p0, p->p1,
+                            p->scale, 1, s);
+    if (rc != SL_OK) return rc;
+    return dispatch_dt(p->dt, [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      k_cast2d<double, T><<<grid_of(tot), 256, 0, s>>>(p->Zf, p->k, p->n, p->k, (T*)p->Z, p->k, nullptr);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    });
+  }
+  return SL_OK;   // Z set explicitly
+}
+
+// one pass over A: Y = A Z, W = A^T Y (into WG f64), and on the final pass
+// G = Y^T Y (f64).  The first pass of the call clears the status word.
+int pass(GPlan* p, const void* A, bool final_pass, bool first, hipStream_t s) {
+  const int64_t m = p->m, n = p->n;
+  const int k = p->k;
+  int rc;
+  if (p->dt == SL_BF16) {
+    // bf16 A: Y (f32) = A Z; W = A^T (Y_hi + Y_lo) with Y split into two bf16 planes
+    rc = slb_gemm(SL_BF16, false, false, m, k, n, 1.0, A, p->lda, p->Z, k, 0.0, p->Y, k, s);
+    if (rc != SL_OK) return rc;
+    k_split_bf16<<<grid_of(m * k), 256, 0, s>>>((const float*)p->Y, m * k, (bf16_t*)p->Yh, (bf16_t*)p->Yl);
+    SL_LAUNCH_CHECK();
+    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yh, k, 0.0, p->Wt, k, s);
+    if (rc != SL_OK) return rc;
+    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yl, k, 1.0, p->Wt, k, s);
+    if (rc != SL_OK) return rc;
+  } else {
+    rc = slb_gemm(p->dt, false, false, m, k, n, 1.0, A, p->lda, p->Z, k, 0.0, p->Y, k, s);
+    if (rc != SL_OK) return rc;
+    rc = slb_gemm(p->dt, true, false, n, k, m, 1.0, A, p->lda, p->Y, k, 0.0, p->Wt, k, s);
+    if (rc != SL_OK) return rc;
+  }
+  const int wdt = p->dt == SL_BF16 ? SL_F32 : p->dt;
+  rc = dispatch_dt(wdt, [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    k_cast2d<T, double><<<grid_of(n * k), 256, 0, s>>>((const T*)p->Wt, k, n, k, p->WG, k, first ? p->st : nullptr);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  });
+  if (rc != SL_OK || !final_pass) return rc;
+  double* G = p->WG + n * k;
+  if (p->dt == SL_F64) return slb_gemm(SL_F64, true, false, k, k, m, 1.0, p->Y, k, p->Y, k, 0.0, G, k, s);
+  if (k <= 64) return sl_tsk_gram64((const float*)p->Y, m, k, k, G, p->gws, s);
+  // k > 64, f32 Y: Gram of f64 copies of row pieces (GPIECE rows per piece)
+  SL_HIP_CHECK(hipMemsetAsync(G, 0, (size_t)k * k * 8, s));
+  for (int64_t r0 = 0; r0 < m; r0 += GPIECE) {
+    const int64_t rows = (m - r0 < GPIECE) ? m - r0 : GPIECE;
+    k_cast2d<float, double><<<grid_of(rows * k), 256, 0, s>>>((const float*)p->Y + r0 * k, k, rows, k,
+                                                               (double*)p->gws, k, nullptr);
+    SL_LAUNCH_CHECK();
+    rc = slb_gemm(SL_F64, true, false, k, k, rows, 1.0, p->gws, k, p->gws, k, 1.0, G, k, s);
+    if (rc != SL_OK) return rc;
+  }
+  return SL_OK;
+}
+
+// the boundary between pass i - 1 and pass i: CholeskyQR of the (all-reduced) W
+int inter(GPlan* p, int i, hipStream_t s) {
+  const int k = p->k;
+  const int64_t n = p->n;
+  int rc = slb_gemm(SL_F64, true, false, k, k, n, 1.0, p->WG, k, p->WG, k, 0.0, p->H, k, s);
+  if (rc != SL_OK) return rc;
+  rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
+  if (rc != SL_OK) return rc;
+  rc = slb_gemm(SL_F64, false, false, n, k, k, 1.0, p->WG, k, p->Ri, k, 0.0, p->Zf, k, s);
+  if (rc != SL_OK) return rc;
+  return dispatch_dt(p->dt, [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    k_cast2d<double, T><<<grid_of(n * k), 256, 0, s>>>(p->Zf, k, n, k, (T*)p->Z, k, nullptr);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  });
+}
+
+// eigenvectors (rows of Vt, ascending eigenvalues D) -> eig = [Ub_r (k x r, descending); sqrt(max(D, 0))]
+__global__ void __launch_bounds__(256) k_pack_syevd(const double* __restrict__ Vt, const double* __restrict__ D,
+                                                    int k, int r, double* __restrict__ eig) {
+  for (int e = threadIdx.x; e < k * r; e += 256) {
+    const int i = e / r, c = e % r;
+    eig[e] = Vt[(int64_t)(k - 1 - c) * k + i];
+  }
+  for (int c = threadIdx.x; c < r; c += 256) {
+    const double l = D[k - 1 - c];
+    eig[k * r + c] = sqrt(l > 0.0 ? l : 0.0);
+  }
+}
+
+int gen_pack_syevd(const double* Vt, const double* D, int k, int r, double* eig, hipStream_t s) {
+  k_pack_syevd<<<1, 256, 0, s>>>(Vt, D, k, r, eig);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// the core after the final pass: Rt^{-1}, C, top eigenpairs, M, N, s
+int core(GPlan* p, hipStream_t s) {
+  const int k = p->k, r = p->r;
+  const int64_t n = p->n;
+  const double* W = p->WG;
+  const double* G = p->WG + n * k;
+  int rc = slb_gemm(SL_F64, true, false, k, k, n, 1.0, W, k, W, k, 0.0, p->H, k, s);   // H = W^T W
+  if (rc != SL_OK) return rc;
+  rc = chol_inv(p, G, p->Ri, p->st + 8, s);
+  if (rc != SL_OK) return rc;
+  rc = slb_gemm(SL_F64, false, false, k, k, k, 1.0, p->H, k, p->Ri, k, 0.0, p->T1, k, s);   // T = H Rti
+  if (rc != SL_OK) return rc;
+  rc = slb_gemm(SL_F64, true, false, k, k, k, 1.0, p->Ri, k, p->T1, k, 0.0, p->Cc, k, s);   // C = Rti^T T
+  if (rc != SL_OK) return rc;
+  if (k <= 64) {
+    SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 8, s));
+    rc = sl_sym_eig_tridiag(p->Cc, k, k, r, p->eig, 1, p->st + 1, s);
+    if (rc != SL_OK) return rc;
+    // re-solve by Jacobi only when the tridiagonal path flagged the core (device-side condition)
+    rc = sl_sym_eig_topr_if(p->Cc, k, k, r, p->eig, 1, 40, p->st + 1, s);
+    if (rc != SL_OK) return rc;
+  } else {
+    // rocSOLVER divide and conquer; eigenvectors in the rows of T1 (ascending)
+    SL_HIP_CHECK(hipMemcpyAsync(p->T1, p->Cc, (size_t)k * k * 8, hipMemcpyDeviceToDevice, s));
+    rc = slb_dsyevd(k, p->T1, k, p->eig + k * r + r, p->eig + k * r + r + k, p->st + 12, s);
+    if (rc != SL_OK) return rc;
+    rc = gen_pack_syevd(p->T1, p->eig + k * r + r, k, r, p->eig, s);
+    if (rc != SL_OK) return rc;
+  }
+  // M = Rti Ub_r (k x r), N = M S^{-1}, s
+  rc = slb_gemm(SL_F64, false, false, k, r, k, 1.0, p->Ri, k, p->eig, r, 0.0, p->M, r, s);
+  if (rc != SL_OK) return rc;
+  const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
+  rc = dispatch_dt(udt, [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    k_core_epi<T><<<1, 256, 0, s>>>(p->eig, k, r, p->M, p->N, (T*)p->Md, p->st);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  });
+  if (rc != SL_OK) return rc;
+  k_status_merge<<<1, 64, 0, s>>>(p->st + 4, 6, p->st);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+int seg(GPlan* p, const void* A, int i, hipStream_t s) {
+  if (i < 0 || i > p->q + 1) { sl_set_last_error("rsvd_gen: segment out of range"); return SL_ERR_INVALID; }
+  int rc = SL_OK;
+  if (i == 0) {
+    SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 15 * sizeof(int), s));
+    rc = make_z(p, s);
+    if (rc != SL_OK) return rc;
+  } else if (i <= p->q) {
+    rc = inter(p, i, s);
+    if (rc != SL_OK) return rc;
+  } else {
+    return core(p, s);
+  }
+  return pass(p, A, i == p->q, i == 0, s);
+}
+
+}  // namespace
+
+// A: m x n row shard (lda) of dtype dt (SL_F32 / SL_F64 / SL_BF16), k <= 128
+// sketch columns, r <= k rank, q power iterations.  Allocates every device
+// buffer of the call once.
+SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, int q, int dt, void** out) {
+  *out = nullptr;
+  if (m < 1 || n < 1 || lda < n || k < 1 || k > 128 || r < 1 || r > k || q < 0 || k > n ||
+      (dt != SL_F32 && dt != SL_F64 && dt != SL_BF16)) {
+    sl_set_last_error("rsvd_gen: needs m, n >= 1, lda >= n, 1 <= r <= k <= min(n, 128), q >= 0, dtype f32/f64/bf16");
+    return SL_ERR_UNSUPPORTED;
+  }
+  if (!slb_available() || (k > 64 && !slb_solver_available())) {
+    sl_set_last_error("rsvd_gen: rocBLAS / rocSOLVER not available");
+    return SL_ERR_UNSUPPORTED;
+  }
+  GPlan* p = new (std::nothrow) GPlan();
+  if (!p) return SL_ERR_GENERIC;
+  p->m = m; p->n = n; p->lda = lda; p->k = k; p->r = r; p->q = q; p->dt = dt;
+  const size_t es = esize(dt);
+  const size_t ys = dt == SL_BF16 ? 4 : es;   // Y / Wt element size
+  int64_t off = 0;
+  const int64_t o_z = off;   off = align256(off + n * k * (int64_t)es);
+  const int64_t o_y = off;   off = align256(off + m * k * (int64_t)ys);
+  const int64_t o_yh = off;  off = align256(off + (dt == SL_BF16 ? m * k * 2 : 0));
+  const int64_t o_yl = off;  off = align256(off + (dt == SL_BF16 ? m * k * 2 : 0));
+  const int64_t o_w = off;   off = align256(off + n * k * (int64_t)ys);
+  const int64_t o_wg = off;  off = align256(off + (n + k) * k * 8);
+  const int64_t o_zf = off;  off = align256(off + n * k * 8);
+  const int64_t o_h = off;   off = align256(off + (int64_t)k * k * 8);
+  const int64_t o_ri = off;  off = align256(off + (int64_t)k * k * 8);
+  const int64_t o_t1 = off;  off = align256(off + (int64_t)k * k * 8);
+  const int64_t o_c = off;   off = align256(off + (int64_t)k * k * 8);
+  const int64_t o_e = off;   off = align256(off + ((int64_t)k * r + r + 2 * k) * 8);
+  const int64_t o_m = off;   off = align256(off + (int64_t)k * r * 8);
+  const int64_t o_n = off;   off = align256(off + (int64_t)k * r * 8);
+  const int64_t o_md = off;  off = align256(off + (int64_t)k * r * 8);
+  const int64_t o_vf = off;  off = align256(off + n * r * 8);
+  const int64_t o_gw = off;
+  off = align256(off + (k <= 64 ? sl_tsk_gram64_workspace(m, k) : (dt == SL_F32 ? GPIECE * k * 8 : 256)));
+  const int64_t o_st = off;  off = align256(off + 64 * 4);
+  if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
+    delete p;
+    sl_set_last_error("rsvd_gen: device allocation failed");
+    return SL_ERR_HIP;
+  }
+  char* b = p->base;
+  p->Z = b + o_z; p->Y = b + o_y; p->Yh = b + o_yh; p->Yl = b + o_yl; p->Wt = b + o_w;
+  p->WG = (double*)(b + o_wg); p->Zf = (double*)(b + o_zf); p->H = (double*)(b + o_h); p->Ri = (double*)(b + o_ri);
+  p->T1 = (double*)(b + o_t1); p->Cc = (double*)(b + o_c); p->eig = (double*)(b + o_e); p->M = (double*)(b + o_m);
+  p->N = (double*)(b + o_n); p->Md = b + o_md; p->Vf = (double*)(b + o_vf); p->gws = b + o_gw;
+  p->st = (int*)(b + o_st);
+  if (hipMemset(p->st, 0, 64 * 4) != hipSuccess) {
+    (void)hipFree(p->base);
+    delete p;
+    return SL_ERR_HIP;
+  }
+  *out = p;
+  return SL_OK;
+}
+
+SL_API int sl_rsvd_gen_destroy(void* plan) {
+  GPlan* p = (GPlan*)plan;
+  if (!p) return SL_OK;
+  (void)hipFree(p->base);
+  delete p;
+  return SL_OK;
+}
+
+// the sketch operator of the next call: FJLT (N Rademacher signs at baseD, k
+// DCT frequencies at baseS, scale sqrt(n / k)), realised on the device
+SL_API int sl_rsvd_gen_set_fjlt(void* plan, uint64_t seed, uint64_t baseD, uint64_t baseS, double scale) {
+  GPlan* p = (GPlan*)plan;
+  p->sk = 1; p->seed = seed; p->b0 = baseD; p->b1 = baseS; p->scale = scale;
+  return SL_OK;
+}
+
+// dense operator (JLT: Normal, CT: Cauchy, ...): scale * dist(seed, base + i k + j)
+SL_API int sl_rsvd_gen_set_dense(void* plan, int dist, uint64_t seed, uint64_t base, double p0, double p1,
+                                 double scale) {
+  GPlan* p = (GPlan*)plan;
+  p->sk = 2; p->dist = dist; p->seed = seed; p->b0 = base; p->p0 = p0; p->p1 = p1; p->scale = scale;
+  return SL_OK;
+}
+
+// explicit operator Z (n x k, row-major, A's dtype, device)
+SL_API int sl_rsvd_gen_set_z(void* plan, const void* Z, void* stream) {
+  GPlan* p = (GPlan*)plan;
+  p->sk = 0;
+  SL_HIP_CHECK(hipMemcpyAsync(p->Z, Z, (size_t)(p->n * p->k) * esize(p->dt), hipMemcpyDeviceToDevice,
+                              (hipStream_t)stream));
+  return SL_OK;
+}
+
+SL_API double* sl_rsvd_gen_reduce_buffer(void* plan) { return ((GPlan*)plan)->WG; }
+
+// Use caller-owned buffers for the [W; G] reduce buffer ((n + k) * k f64) and
+// / or the status words (16 ints; [0] is the call's status), e.g. torch
+// tensors the caller all-reduces / reads; null keeps the plan's own.
+SL_API int sl_rsvd_gen_bind(void* plan, double* WG, int* status) {
+  GPlan* p = (GPlan*)plan;
+  if (WG) p->WG = WG;
+  if (status) p->st = status;
+  return SL_OK;
+}
+SL_API int* sl_rsvd_gen_status_ptr(void* plan) { return ((GPlan*)plan)->st; }
+
+SL_API int sl_rsvd_gen_segment(void* plan, const void* A, int i, void* stream) {
+  return seg((GPlan*)plan, A, i, (hipStream_t)stream);
+}
+
+// U (m x r, row stride ldu), s (r), V (n x r): f32 for f32 / bf16 A, f64 for f64 A
+SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, void* V, void* stream) {
+  GPlan* p = (GPlan*)plan;
+  hipStream_t s = (hipStream_t)stream;
+  const int k = p->k, r = p->r;
+  int rc = slb_gemm(SL_F64, false, false, p->n, r, k, 1.0, p->WG, k, p->N, r, 0.0, p->Vf, r, s);   // V = W N
+  if (rc != SL_OK) return rc;
+  const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
+  rc = dispatch_dt(udt, [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    k_cast2d<double, T><<<grid_of(p->n * r), 256, 0, s>>>(p->Vf, r, p->n, r, (T*)V, r, nullptr);
+    SL_LAUNCH_CHECK();
+    k_store_s<T><<<1, 256, 0, s>>>(p->eig + k * r, r, (T*)s_out);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  });
+  if (rc != SL_OK) return rc;
+  return slb_gemm(udt, false, false, p->m, r, k, 1.0, p->Y, k, p->Md, r, 0.0, U, ldu, s);   // U = Y M
+}
+
+// single rank: every segment, then the finish
+SL_API int sl_rsvd_gen_run(void* plan, const void* A, void* U, int64_t ldu, void* s, void* V, void* stream) {
+  GPlan* p = (GPlan*)plan;
+  for (int i = 0; i <= p->q + 1; ++i) {
+    const int rc = seg(p, A, i, (hipStream_t)stream);
+    if (rc != SL_OK) return rc;
+  }
+  return sl_rsvd_gen_finish(plan, U, ldu, s, V, stream);
+}
+
+// several ranks from C: the segments with a NativeComm (RCCL) sum of the
+// [W; G] buffer after each pass
+SL_API int sl_rsvd_gen_run_comm(void* plan, const void* A, void* comm, void* U, int64_t ldu, void* s, void* V,
+                                void* stream) {
+  GPlan* p = (GPlan*)plan;
+  for (int i = 0; i <= p->q + 1; ++i) {
+    int rc = seg(p, A, i, (hipStream_t)stream);
+    if (rc != SL_OK) return rc;
+    if (i <= p->q && comm) {
+      const int64_t cnt = (i == p->q ? p->n + p->k : p->n) * p->k;
+      rc = sl_comm_all_reduce(comm, p->WG, p->WG, cnt, SL_F64, 0, stream);
+      if (rc != SL_OK) return rc;
+    }
+  }
+  return sl_rsvd_gen_finish(plan, U, ldu, s, V, stream);
+}
+
+// status bits of the last call (synchronises the stream)
+SL_API int sl_rsvd_gen_status(void* plan, int* out, void* stream) {
+  GPlan* p = (GPlan*)plan;
+  SL_HIP_CHECK(hipMemcpyAsync(out, p->st, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  SL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  return SL_OK;
+}

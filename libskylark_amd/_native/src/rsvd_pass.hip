@@ -113,10 +113,10 @@ struct Geo4 {
   static constexpr int GS64 = (GT64 + WAVES - 1) / WAVES;
 };
 
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL>
+template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM = FINAL>
 constexpr int pass_lds() {
   using G = Geo4<WAVES, NW, KT, NBUF>;
-  return G::RING + G::PART + G::Y16 + (FINAL ? G::YF : 0);
+  return G::RING + G::PART + G::Y16 + (GRAM ? G::YF : 0);
 }
 
 // swizzle of 16-B chunk slots by row (see tsk_kernels.hip: a GF(2) map that
@@ -133,8 +133,8 @@ __device__ __forceinline__ int swz4(int row) {
 // conflict-free (gfx950 LDS lane groups) with no padding
 __device__ __forceinline__ int qidx(int col, int q) { return col * 16 + 4 * (q ^ ((col >> 1) & 3)); }
 
-// FINAL: exact W, stored Y (ldy = KP), fp64 Gram slab.  Otherwise W only.
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL>
+// FINAL: stored Y (ldy = KP) and, with GRAM, the fp64 Gram slab.  Otherwise W only.
+template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM>
 __global__ void __launch_bounds__(WAVES * 64, 1)
 k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const bf16_t* __restrict__ Zt, int k,
             float* __restrict__ Wslab, double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
@@ -181,9 +181,9 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
   for (int a = 0; a < NW / 16; ++a)
 #pragma unroll
     for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f64x4 accG[FINAL ? G::GS64 : 1];
+  f64x4 accG[GRAM ? G::GS64 : 1];
 #pragma unroll
-  for (int s = 0; s < (FINAL ? G::GS64 : 1); ++s) accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < (GRAM ? G::GS64 : 1); ++s) accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
 
   // ---- LDS-DMA of row block `blk` (this wave's columns) into ring slot `slot`.
   //      The per-lane source offsets inside a block are fixed: precomputed
@@ -305,7 +305,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       *(s16x4*)(y16 + rc * 32 + rq * 8) = hi;
       *(s16x4*)(y16 + G::Y16P + rc * 32 + rq * 8) = lo;
       if constexpr (FINAL) {
-        *(f32x4*)&yf[qidx(rc, rq)] = sum;
+        if constexpr (GRAM) *(f32x4*)&yf[qidx(rc, rq)] = sum;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int64_t row = r0 + 4 * rq + e;
@@ -318,7 +318,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
     lds_barrier();   // (B) y of block j is complete
     SL_STAMP(5)
 
-    if constexpr (FINAL) {
+    if constexpr (GRAM) {
       // ---- fp64 Gram of y: upper tile tau = (t1, t2) on wave tau % WAVES;
       //      K step u pairs lane group g with row 4 g + u
       int tau = 0;
@@ -406,7 +406,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
           if (row < n && col < k) ws[(int64_t)row * k + col] = accW[ct][t][e];
         }
   }
-  if constexpr (FINAL) {
+  if constexpr (GRAM) {
     // fp64 Gram slab [k][k]: each upper tile and its mirror (f64 C/D map:
     // row = (lane >> 4) + 4 r, col = lane & 15)
     double* gs = Gslab + (int64_t)blockIdx.x * k * k;
@@ -517,13 +517,13 @@ int cu_count() {
   return ncu;
 }
 
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL>
+template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM = FINAL>
 int launch_pass(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
                 double* Gslab, float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s, int variant) {
   using G = Geo4<WAVES, NW, KT, NBUF>;
-  constexpr int LDS = pass_lds<WAVES, NW, KT, NBUF, FINAL>();
+  constexpr int LDS = pass_lds<WAVES, NW, KT, NBUF, FINAL, GRAM>();
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL>;
+  auto kern = k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL, GRAM>;
   SL_LDS_ATTR(kern, LDS);
   kern<<<grid, G::THREADS, LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch);
   SL_LAUNCH_CHECK();
@@ -553,7 +553,8 @@ SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k) {
 // One v4 pass.  A: m x n bf16 (lda % 8 == 0, 16 <= n <= 1024, n % 8 == 0);
 // Zt: k x n bf16 (1 <= k <= 48).  ws: sl_rsvd_pass_workspace bytes.
 // final = 0: W slabs only.  final = 1: also Y (m x k f32, row stride ldy >=
-// k) and the fp64 Gram slabs.  variant selects the
+// k) and the fp64 Gram slabs; final = 2: W slabs and Y (the Gram formed
+// afterwards from the stored Y, off the per-block chain).  variant selects the
 // ring depth (tuning: 0 default, 3/4 = NBUF).
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
                         float* Y, int64_t ldy, int final_pass, int variant, void* stream) {
@@ -577,8 +578,9 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   const bool small = n <= 512;
   const int nbuf = variant == 3 ? 3 : 4;
 #define SL_P(NW, KTT, NB)                                                                                    \
-  return final_pass ? launch_pass<8, NW, KTT, NB, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
-                    : launch_pass<8, NW, KTT, NB, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant)
+  return final_pass == 1 ? launch_pass<8, NW, KTT, NB, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
+       : final_pass == 2 ? launch_pass<8, NW, KTT, NB, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
+                         : launch_pass<8, NW, KTT, NB, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant)
 #define SL_PK(NW, NB)                        \
   switch (KT) {                              \
     case 1: SL_P(NW, 1, NB);                 \

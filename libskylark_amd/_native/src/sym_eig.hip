@@ -28,13 +28,14 @@ constexpr int NT = 256;
 
 __global__ void __launch_bounds__(NT)
 k_sym_eig_jacobi(const double* __restrict__ Cin, int k, int ldc, int r, double* __restrict__ out,
-                 int want_sqrt, int max_sweeps, int* __restrict__ sweeps_out) {
+                 int want_sqrt, int max_sweeps, int* __restrict__ sweeps_out, const int* __restrict__ flag) {
   __shared__ double AB[2][KMAX][KMAX + 1];   // ping-pong copies of A
   __shared__ double V[KMAX][KMAX + 1];
   __shared__ double cs[KMAX / 2], sn[KMAX / 2];
   __shared__ int pp[KMAX / 2], qq[KMAX / 2];
   __shared__ int rotated;
   const int tid = threadIdx.x;
+  if (flag && *flag == 0) return;   // conditional re-solve: only when the caller's solver flagged the matrix
   const int kp = (k + 1) & ~1;  // even number of players (a padded index is an isolated 0 row)
   const int half = kp / 2;
 
@@ -143,7 +144,7 @@ template <int K>
 __global__ void __launch_bounds__(512) k_sym_eig_wave(const double* __restrict__ C, int k, int ldc, int r,
                                                       double* __restrict__ out, int want_sqrt, int* __restrict__ status) {
   __shared__ double refl[K * (K + 1)];
-  __shared__ double sc[64 * (K + 1)];
+  __shared__ double sc[3 * 64 * (K + 1)];
   __shared__ __attribute__((aligned(16))) double dd[K], ee[K], lam[K], vsh[2 * K], wsh[2 * K];
   __shared__ int bad, fb;
   const int tid = threadIdx.x;
@@ -185,7 +186,18 @@ SL_API int sl_sym_eig_topr(const double* C, int k, int ldc, int r, double* out, 
                            int max_sweeps, int* sweeps_out, void* stream) {
   if (k <= 0 || k > KMAX || r <= 0 || r > k || ldc < k) return SL_ERR_DIMENSION;
   k_sym_eig_jacobi<<<1, NT, 0, (hipStream_t)stream>>>(C, k, ldc, r, out, want_sqrt,
-                                                       max_sweeps > 0 ? max_sweeps : 30, sweeps_out);
+                                                       max_sweeps > 0 ? max_sweeps : 30, sweeps_out, nullptr);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// the same, run only when *flag (device) is non-zero: the robust re-solve of a
+// matrix the tridiagonal path flagged, decided on the device (no host sync)
+SL_API int sl_sym_eig_topr_if(const double* C, int k, int ldc, int r, double* out, int want_sqrt, int max_sweeps,
+                              const int* flag, void* stream) {
+  if (k <= 0 || k > KMAX || r <= 0 || r > k || ldc < k) return SL_ERR_DIMENSION;
+  k_sym_eig_jacobi<<<1, NT, 0, (hipStream_t)stream>>>(C, k, ldc, r, out, want_sqrt,
+                                                       max_sweeps > 0 ? max_sweeps : 30, nullptr, flag);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

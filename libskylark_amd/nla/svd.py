@@ -186,7 +186,7 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
     from ..ops import tallskinny as T
 
-    if A_loc.is_cuda and work == torch.float32 and A_loc.dtype == torch.bfloat16:
+    if A_loc.is_cuda:
         res = _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params)
         if res is not None:
             U_loc, s, V = res
@@ -274,6 +274,7 @@ def approximate_svd(A, rank: int, context: Context | None = None,
 vp_, i32_, i64_, u64_, f64_ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 
 
+
 _ENGINE_REG = [False]
 
 
@@ -294,6 +295,15 @@ def _engine_lib():
         _lib.register("sl_rsvd_status_mirror", [vp_], vp_)
         _lib.register("sl_rsvd_flush", [vp_, vp_])
         _lib.register("sl_rsvd_plan_set_fault", [vp_, i32_, u64_])
+        _lib.register("sl_rsvd_gen_create", [i64_, i64_, i64_, i32_, i32_, i32_, i32_, ctypes.POINTER(vp_)])
+        _lib.register("sl_rsvd_gen_destroy", [vp_])
+        _lib.register("sl_rsvd_gen_bind", [vp_, vp_, vp_])
+        _lib.register("sl_rsvd_gen_set_fjlt", [vp_, u64_, u64_, u64_, f64_])
+        _lib.register("sl_rsvd_gen_set_dense", [vp_, i32_, u64_, u64_, f64_, f64_, f64_])
+        _lib.register("sl_rsvd_gen_set_z", [vp_, vp_, vp_])
+        _lib.register("sl_rsvd_gen_segment", [vp_, vp_, i32_, vp_])
+        _lib.register("sl_rsvd_gen_finish", [vp_, vp_, i64_, vp_, vp_, vp_])
+        _lib.register("sl_rsvd_gen_run", [vp_, vp_, vp_, i64_, vp_, vp_, vp_])
     return _lib
 
 
@@ -472,6 +482,99 @@ def _drop_plan(plan):
             _PLANS.pop(key, None)
 
 
+class _GenPlan(_EnginePlan):
+    """Device randSVD of f32 / f64 / bf16 A of any width (k <= 128) on the
+    general-precision engine (``_native/src/rsvd_general.hip``): the two
+    products over A per pass are rocBLAS GEMMs, the CholeskyQR factors and the
+    core eigensolver the one-wave kernels (k <= 64) or rocSOLVER (k <= 128),
+    W / H / G and the core in f64 -- no host round trip inside a call.  U, s,
+    V come back in A's precision (f32 for bf16 A).  Same segment contract,
+    status handling and multi-rank all-reduces as :class:`_EnginePlan`."""
+
+    def __init__(self, A_loc, comm, n, rank, k, q):
+        L = _engine_lib()
+        from ..ops import _lib as OL
+        m = A_loc.shape[0]
+        self.dev = A_loc.device
+        self.Aref = weakref.ref(A_loc)
+        self.comm, self.n, self.rank, self.k, self.q, self.m = comm, n, rank, k, q, m
+        self.use_graph = False
+        self.out_dtype = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
+        dt = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2}[A_loc.dtype]
+        self.A_dtype = A_loc.dtype
+        h = ctypes.c_void_p()
+        L.call("sl_rsvd_gen_create", m, n, A_loc.stride(0), k, rank, q, dt, ctypes.byref(h))
+        self.h = h
+        self._fin = weakref.finalize(self, _destroy_gen_plan, h.value)
+        self.WG = torch.empty((n + k) * k, dtype=torch.float64, device=self.dev)
+        self.status_words = torch.zeros(16, dtype=torch.int32, device=self.dev)
+        self.status_dev = self.status_words[:1]
+        L.call("sl_rsvd_gen_bind", h, ctypes.c_void_p(self.WG.data_ptr()),
+               ctypes.c_void_p(self.status_words.data_ptr()))
+        self.mirror = None
+        self.status_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.status_ev = None
+        self.last_status = 0
+        self.poisoned = False
+        self.calls = 0
+        self.g, self.g_failed = None, True
+        del OL
+
+    def _segments(self, A):
+        L = _engine_lib()
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        for i in range(self.q + 2):
+            with PROFILER.phase("svd.segment"):
+                L.call("sl_rsvd_gen_segment", self.h, ctypes.c_void_p(A.data_ptr()), i, st)
+            if i <= self.q:
+                cnt = (self.n + self.k if i == self.q else self.n) * self.k
+                with PROFILER.phase("svd.allreduce_small"):
+                    self.comm.all_reduce(self.WG[:cnt])
+
+    def __call__(self, A, Z=None, fjlt=None, dense=None):
+        L = _engine_lib()
+        dev = self.dev
+        st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        self._poll_status()
+        if fjlt is not None:
+            L.call("sl_rsvd_gen_set_fjlt", self.h, int(fjlt[0]), int(fjlt[1]), int(fjlt[2]), float(fjlt[3]))
+        elif dense is not None:
+            code, seed, base, p0, p1, scale = dense
+            L.call("sl_rsvd_gen_set_dense", self.h, int(code), int(seed), int(base), float(p0), float(p1), float(scale))
+        else:
+            Zc = Z.to(self.A_dtype).contiguous()
+            L.call("sl_rsvd_gen_set_z", self.h, ctypes.c_void_p(Zc.data_ptr()), st)
+        r = self.rank
+        U = torch.empty(self.m, r, dtype=self.out_dtype, device=dev)
+        s = torch.empty(r, dtype=self.out_dtype, device=dev)
+        V = torch.empty(self.n, r, dtype=self.out_dtype, device=dev)
+        if self.comm.size == 1:
+            L.call("sl_rsvd_gen_run", self.h, ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(U.data_ptr()), r,
+                   ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(V.data_ptr()), st)
+        else:
+            self._segments(A)
+            with PROFILER.phase("svd.form_U"):
+                L.call("sl_rsvd_gen_finish", self.h, ctypes.c_void_p(U.data_ptr()), r, ctypes.c_void_p(s.data_ptr()),
+                       ctypes.c_void_p(V.data_ptr()), st)
+        if self.status_ev is None:
+            self.status_ev = torch.cuda.Event()
+        self.status_host.copy_(self.status_dev, non_blocking=True)
+        self.status_ev.record()
+        self.calls += 1
+        return U, s, V
+
+
+def _destroy_gen_plan(ptr):
+    try:
+        from ..ops import _lib
+        lib = _lib.load(build_if_missing=False)
+        if lib is not None and ptr:
+            torch.cuda.synchronize()
+            lib.sl_rsvd_gen_destroy(ctypes.c_void_p(ptr))
+    except Exception:  # noqa: BLE001 - interpreter shutdown
+        pass
+
+
 def _destroy_plan(ptr):
     try:
         from ..ops import _lib
@@ -493,11 +596,19 @@ def _engine_ok(A_loc, n, k) -> bool:
             and n % 8 == 0 and 16 <= n <= 1024 and 1 <= k <= 48)
 
 
+def _gen_ok(A_loc, n, k) -> bool:
+    return (A_loc.is_cuda and A_loc.dtype in (torch.float32, torch.float64, torch.bfloat16)
+            and A_loc.stride(1) == 1 and A_loc.stride(0) >= n and 1 <= k <= min(n, 128))
+
+
 def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
-    """GPU-resident path (bf16 A on gfx950): the C++ engine runs the whole
-    call; no host synchronisation inside it.  Returns None when the engine
-    does not cover the shape (the caller then runs the host-driven path)."""
-    if not _engine_ok(A_loc, n, k):
+    """GPU-resident path: the C++ engines run the whole call; no host
+    synchronisation inside it.  bf16 A with n <= 1024, k <= 48: the fused
+    engine (one read of A per pass); any other f32 / f64 / bf16 A with k <= 128:
+    the general-precision engine.  Returns None when neither covers the call
+    (the caller then runs the host-driven path)."""
+    fused = _engine_ok(A_loc, n, k)
+    if not fused and not _gen_ok(A_loc, n, k):
         return None
     if _TRACE:
         print(f"[svd.trace] python_prep={(time.perf_counter() - _T0[0]) * 1e6:.0f}us", file=sys.stderr)
@@ -525,14 +636,17 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
             Z = _sketch_operator(params.sketch, n, k, ctx, dev, torch.float32)
     q = max(0, int(params.num_iterations))
     key = (A_loc.data_ptr(), tuple(A_loc.shape), tuple(A_loc.stride()), str(dev), rank, k, q, comm.size,
-           id(getattr(comm, "group", None)))
+           id(getattr(comm, "group", None)), A_loc.dtype, fused)
     plan = _PLANS.get(key)
     if plan is not None and (plan.Aref() is None or plan.poisoned):
         plan = None  # the operand this plan was built for is gone / a timed-out plan
     if plan is None:
         if len(_PLANS) >= 4:
             _PLANS.pop(next(iter(_PLANS)))
-        plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
+        if fused:
+            plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
+        else:
+            plan = _GenPlan(A_loc, comm, n, rank, k, q)
         _PLANS[key] = plan
     out = plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
     if params.check:

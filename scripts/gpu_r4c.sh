@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-bash scripts/gpu_tests_from.sh tests/test_small_la.py tests/test_gpu_rsvd_faults.py tests/test_gpu_rsvd_boundary.py tests/test_gpu_rsvd_core.py tests/test_nla.py || exit 1
+bash scripts/gpu_tests_from.sh tests/test_gpu_rsvd_general.py tests/test_small_la.py tests/test_gpu_rsvd_faults.py tests/test_gpu_rsvd_boundary.py tests/test_gpu_rsvd_core.py tests/test_nla.py || exit 1
 timeout -k 10 120 python benchmarks/eig_stamps.py > $OUT/eig_stamps.log 2>&1; rc=$?; grep '^{' $OUT/eig_stamps.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python benchmarks/eig_tridiag_bench.py > $OUT/eig_bench.log 2>&1; rc=$?; grep '^{' $OUT/eig_bench.log | grep -v jacobi; [ $rc -eq 0 ] || exit $rc
 bash scripts/gpu_bench_prof.sh || exit 1
