@@ -112,7 +112,7 @@ def build_capi(force: bool = False) -> str:
     """C API library (host C++; embeds/joins CPython for the runtime paths, loads
     libskylark_hip.so + rocBLAS for the DeviceMatrix paths; no device code)."""
     srcs = [CAPI_SRC, os.path.join(HERE, "capi", "native_sketch.hpp"), os.path.join(HERE, "capi", "native_device.hpp"),
-            os.path.join(INC, "sl_rng.hpp")]
+            os.path.join(INC, "sl_rng.hpp"), os.path.join(INC, "sl_perm.hpp")]
     if not force and os.path.exists(CAPI_LIB) and all(os.path.getmtime(CAPI_LIB) >= os.path.getmtime(f) for f in srcs):
         return CAPI_LIB
     import sysconfig

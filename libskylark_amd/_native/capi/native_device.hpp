@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -82,6 +83,35 @@ struct Lib {
   int (*comm_init)(const void*, int, int, void**) = nullptr;
   int (*comm_destroy)(void*) = nullptr;
   int (*set_device)(int) = nullptr;
+  int (*dev_count)(int*) = nullptr;
+  int (*dct2_rows)(const int64_t*, int64_t, int64_t, const double*, double, void*, int, int64_t, int, void*) = nullptr;
+  int (*feature_epi)(void*, int, int64_t, int64_t, int64_t, const double*, const double*, double, int, int,
+                     void*) = nullptr;
+  int (*transpose)(const void*, int, int64_t, int64_t, int64_t, void*, int64_t, void*) = nullptr;
+  int (*csr_to_dense)(const int*, const int*, const double*, int64_t, void*, int, int64_t, void*) = nullptr;
+  int (*dft_cs)(int64_t, int64_t, void*, void*, int, void*) = nullptr;
+  int (*ppt_spectrum)(const void*, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, const int64_t*,
+                      const double*, double, void*, int, void*) = nullptr;
+  int (*hash_csr_col)(const int64_t*, const void*, int, const void*, int, const int64_t*, const int64_t*, const void*,
+                      int64_t, int64_t, void*, int64_t, int64_t, int, int, const double*, double, void*) = nullptr;
+  int (*hash_csr_row)(const int64_t*, const void*, int, const void*, int, int64_t, const int64_t*, const double*, void*,
+                      int64_t, int64_t, int, void*) = nullptr;
+  // general-precision randSVD engine (rsvd_general.hip)
+  int (*gen_create)(int64_t, int64_t, int64_t, int, int, int, int, void**) = nullptr;
+  int (*gen_destroy)(void*) = nullptr;
+  int (*gen_set_fjlt)(void*, uint64_t, uint64_t, uint64_t, double) = nullptr;
+  int (*gen_set_dense)(void*, int, uint64_t, uint64_t, double, double, double) = nullptr;
+  int (*gen_set_z)(void*, const void*, void*) = nullptr;
+  int (*gen_run)(void*, const void*, void*, int64_t, void*, void*, void*) = nullptr;
+  int (*gen_status)(void*, int*, void*) = nullptr;
+  // host-operand NLA drivers (nla_native.hip) and the LIBSVM reader (libsvm_io.cpp)
+  int (*sym_rsvd)(const double*, int64_t, int64_t, int, int, int, int, int, uint64_t, uint64_t, double*, int64_t,
+                  double*, void*) = nullptr;
+  int (*blendenpik)(const double*, int64_t, int64_t, int64_t, const double*, int, int64_t, double*, int64_t, uint64_t,
+                    uint64_t*, double, int, int*, void*) = nullptr;
+  int (*libsvm_scan)(const char*, int64_t, int, int64_t*, int64_t*, int64_t*, int*) = nullptr;
+  int (*libsvm_fill)(const char*, const int64_t*, const int64_t*, int, int64_t, double*, int64_t*, int64_t*,
+                     double*) = nullptr;
   // rocBLAS (plain library GEMMs)
   void* rb_handle = nullptr;
   int (*rb_dgemm)(void*, int, int, int, int, int, const double*, const double*, int, const double*, int,
@@ -135,7 +165,20 @@ inline Lib& lib() {
               bind(L.h, "sl_comm_unique_id_bytes", L.comm_id_bytes, L.err) &&
               bind(L.h, "sl_comm_unique_id", L.comm_unique_id, L.err) &&
               bind(L.h, "sl_comm_init", L.comm_init, L.err) && bind(L.h, "sl_comm_destroy", L.comm_destroy, L.err) &&
-              bind(L.h, "sl_dev_set_device", L.set_device, L.err);
+              bind(L.h, "sl_dev_set_device", L.set_device, L.err) && bind(L.h, "sl_dev_count", L.dev_count, L.err) &&
+              bind(L.h, "sl_dct2_rows", L.dct2_rows, L.err) && bind(L.h, "sl_feature_epilogue", L.feature_epi, L.err) &&
+              bind(L.h, "sl_transpose", L.transpose, L.err) && bind(L.h, "sl_csr_to_dense", L.csr_to_dense, L.err) &&
+              bind(L.h, "sl_dft_cs", L.dft_cs, L.err) && bind(L.h, "sl_ppt_spectrum", L.ppt_spectrum, L.err) &&
+              bind(L.h, "sl_hash_csr_colwise2", L.hash_csr_col, L.err) &&
+              bind(L.h, "sl_hash_csr_rowwise", L.hash_csr_row, L.err) &&
+              bind(L.h, "sl_rsvd_gen_create", L.gen_create, L.err) &&
+              bind(L.h, "sl_rsvd_gen_destroy", L.gen_destroy, L.err) &&
+              bind(L.h, "sl_rsvd_gen_set_fjlt", L.gen_set_fjlt, L.err) &&
+              bind(L.h, "sl_rsvd_gen_set_dense", L.gen_set_dense, L.err) &&
+              bind(L.h, "sl_rsvd_gen_set_z", L.gen_set_z, L.err) && bind(L.h, "sl_rsvd_gen_run", L.gen_run, L.err) &&
+              bind(L.h, "sl_rsvd_gen_status", L.gen_status, L.err) &&
+              bind(L.h, "sl_nat_sym_rsvd", L.sym_rsvd, L.err) && bind(L.h, "sl_nat_blendenpik", L.blendenpik, L.err) &&
+              bind(L.h, "sl_libsvm_scan", L.libsvm_scan, L.err) && bind(L.h, "sl_libsvm_fill", L.libsvm_fill, L.err);
     if (!ok) return;
     L.rb = dlopen("librocblas.so", RTLD_NOW | RTLD_LOCAL);
     if (!L.rb) L.rb = dlopen("/opt/rocm/lib/librocblas.so", RTLD_NOW | RTLD_LOCAL);
@@ -191,16 +234,16 @@ struct Buf {
 // Row-major C (M x N, ldc) = alpha op(A) op(B) + beta C on rocBLAS (column-major:
 // the row-major product is the column-major C^T = op(B)^T op(A)^T).
 inline int gemm_rm(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
-                   const void* B, int64_t ldb, double beta, void* C, int64_t ldc) {
+                   const void* B, int64_t ldb, double beta, void* C, int64_t ldc, double alpha = 1.0) {
   Lib& L = lib();
   const int opA = ta ? 112 : 111, opB = tb ? 112 : 111;
   int rc;
   if (dt == F64) {
-    const double al = 1.0, be = beta;
+    const double al = alpha, be = beta;
     rc = L.rb_dgemm(L.rb_handle, opB, opA, (int)N, (int)M, (int)K, &al, (const double*)B, (int)ldb,
                     (const double*)A, (int)lda, &be, (double*)C, (int)ldc);
   } else {
-    const float al = 1.f, be = (float)beta;
+    const float al = (float)alpha, be = (float)beta;
     rc = L.rb_sgemm(L.rb_handle, opB, opA, (int)N, (int)M, (int)K, &al, (const float*)B, (int)ldb, (const float*)A,
                     (int)lda, &be, (float*)C, (int)ldc);
   }
@@ -208,15 +251,119 @@ inline int gemm_rm(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, co
 }
 
 // ---------------------------------------------------------------- sketches
-inline bool device_sketch_type(const std::string& t) {
-  return t == "JLT" || t == "CT" || t == "FJLT" || t == "CWT" || t == "MMT" || t == "WZT";
+inline bool device_present() {
+  Lib& L = lib();
+  if (!L.loaded) return false;
+  const char* e = getenv("SL_CAPI_HOST");   // force the host path (tests compare both)
+  if (e && *e && *e != '0') return false;
+  static int n = -1;
+  if (n < 0) {
+    int c = 0;
+    L.dev_count(&c);
+    n = c;
+  }
+  return n > 0;
 }
 
-// SA = S A (dim 0: A is N x n, SA is S x n) or A S^T (dim 1: A is m x N, SA is m x S)
+// host vector -> device (freed with the Buf)
+template <typename T>
+inline int upload(Buf& b, const std::vector<T>& v) {
+  if (!b.p) return fail(101, "device C API: allocation failed");
+  if (v.empty()) return 0;
+  return check(lib().dev_memcpy(b.p, v.data(), (int64_t)(v.size() * sizeof(T)), 0, nullptr), "copy");
+}
+
+// host f64 values as a device buffer of dtype dt
+inline int upload_as(Buf& b, const double* v, int64_t n, int dt) {
+  if (!b.p) return fail(101, "device C API: allocation failed");
+  if (dt == F64) return check(lib().dev_memcpy(b.p, v, n * 8, 0, nullptr), "copy");
+  std::vector<float> f((size_t)n);
+  for (int64_t i = 0; i < n; ++i) f[(size_t)i] = (float)v[i];
+  return check(lib().dev_memcpy(b.p, f.data(), n * 4, 0, nullptr), "copy");
+}
+
+inline int zero(const DevMat& M) {
+  const size_t es = esize(M.dtype);
+  if (M.ld == M.n) return check(lib().dev_memset(M.data, 0, M.m * M.n * (int64_t)es, nullptr), "memset");
+  for (int64_t i = 0; i < M.m; ++i)
+    SLDEV_TRY(lib().dev_memset((char*)M.data + i * M.ld * es, 0, M.n * (int64_t)es, nullptr), "memset");
+  return 0;
+}
+
+// bucket structure of the hash kernels: perm (inputs sorted by bucket),
+// bptr (S + 1), and the values in bucket order (pval) and input order (val)
+struct HashDev {
+  Buf perm, bptr, pval, val, idx;
+  HashDev(int64_t N, int64_t S) : perm(N * 8), bptr((S + 1) * 8), pval(N * 8), val(N * 8), idx(N * 8) {}
+};
+
+inline int hash_upload(HashDev& H, const std::vector<int64_t>& idx, const std::vector<double>& val, int64_t S,
+                       double mul = 1.0) {
+  const int64_t N = (int64_t)idx.size();
+  std::vector<int64_t> perm((size_t)N), bptr((size_t)S + 1, 0);
+  for (int64_t j = 0; j < N; ++j) ++bptr[(size_t)idx[(size_t)j] + 1];
+  for (int64_t b = 0; b < S; ++b) bptr[(size_t)b + 1] += bptr[(size_t)b];
+  {
+    std::vector<int64_t> fill(bptr.begin(), bptr.end() - 1);
+    for (int64_t j = 0; j < N; ++j) perm[(size_t)fill[(size_t)idx[(size_t)j]]++] = j;
+  }
+  std::vector<double> pv((size_t)N), v((size_t)N);
+  for (int64_t j = 0; j < N; ++j) {
+    pv[(size_t)j] = mul * val[(size_t)perm[(size_t)j]];
+    v[(size_t)j] = mul * val[(size_t)j];
+  }
+  int rc;
+  if ((rc = upload(H.perm, perm)) || (rc = upload(H.bptr, bptr)) || (rc = upload(H.pval, pv)) || (rc = upload(H.val, v)) ||
+      (rc = upload(H.idx, idx)))
+    return rc;
+  return 0;
+}
+
+// SA (= or +=) bucket sums of A along dim (rowwise needs the row in LDS)
+inline int hash_apply(const HashDev& H, int64_t N, int64_t S, const DevMat& A, const DevMat& SA, int dim, int acc) {
+  Lib& L = lib();
+  if (dim == 0)
+    return check(L.hash_colwise(A.data, A.dtype, A.ld, A.n, (const int64_t*)H.perm.p, (const int64_t*)H.bptr.p,
+                                (const double*)H.pval.p, S, SA.data, SA.dtype, SA.ld, 0, acc, nullptr),
+                 "hash colwise");
+  return check(L.hash_rowwise(A.data, A.dtype, A.ld, A.m, N, (const int64_t*)H.perm.p, (const int64_t*)H.bptr.p,
+                              (const double*)H.val.p, S, SA.data, SA.dtype, SA.ld, 0, acc, nullptr),
+               "hash rowwise");
+}
+
+inline bool rowwise_fits(int64_t N, int dt) { return N * (int64_t)esize(dt) <= 160 * 1024; }
+
+inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim);
+
+// dim-1 application through dim 0 on the transposes (rows longer than LDS)
+inline int apply_by_transpose(const slnat::Sketch& s, const DevMat& A, const DevMat& SA) {
+  Lib& L = lib();
+  const int dt = A.dtype;
+  const size_t es = esize(dt);
+  Buf At(A.n * A.m * (int64_t)es), T(s.S * A.m * (int64_t)es);
+  if (!At.p || !T.p) return fail(101, "device sketch: allocation failed");
+  SLDEV_TRY(L.transpose(A.data, dt, A.m, A.n, A.ld, At.p, A.m, nullptr), "transpose");
+  const int rc = apply_sketch(s, DevMat{At.p, dt, A.n, A.m, A.m}, DevMat{T.p, dt, s.S, A.m, A.m}, 0);
+  if (rc) return rc;
+  return check(L.transpose(T.p, dt, s.S, A.m, A.m, SA.data, SA.ld, nullptr), "transpose");
+}
+
+inline int epilogue_dev(const slnat::Sketch& s, const DevMat& SA, int dim) {
+  if (s.epi == slnat::EPI_NONE) return 0;
+  Buf sc(s.scales.empty() ? 8 : (int64_t)s.scales.size() * 8), sh(s.shifts.empty() ? 8 : (int64_t)s.shifts.size() * 8);
+  int rc;
+  if ((rc = upload(sc, s.scales)) || (rc = upload(sh, s.shifts))) return rc;
+  return check(lib().feature_epi(SA.data, SA.dtype, SA.m, SA.n, SA.ld, s.scales.empty() ? nullptr : (const double*)sc.p,
+                                 s.shifts.empty() ? nullptr : (const double*)sh.p, s.outscale, dim, s.epi, nullptr),
+               "feature epilogue");
+}
+
+// SA = S A (dim 0: A is N x n, SA is S x n) or A S^T (dim 1: A is m x N, SA
+// is m x S), row-major device operands of one dtype (f32 / f64): every
+// sketch type of native_sketch.hpp.
 inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim) {
   Lib& L = lib();
   if (!L.loaded) return fail(106, "device C API: " + L.err);
-  if (!device_sketch_type(s.type)) return fail(103, "sketch " + s.type + " has no device C path");
   if ((A.dtype != F32 && A.dtype != F64) || SA.dtype != A.dtype)
     return fail(103, "device sketch: A and SA must both be f32 or both f64");
   const int64_t sk_in = dim == 0 ? A.m : A.n;   // the sketched dimension (N)
@@ -225,76 +372,246 @@ inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& S
     return fail(104, "device sketch: dimension mismatch");
   const int dt = A.dtype;
   const size_t es = esize(dt);
+  const int64_t N = s.N, S = s.S;
   void* st = nullptr;
-  if (s.type == "JLT" || s.type == "CT") {
-    // S panels of b columns (<= 2^24 entries), accumulated into SA
-    const int64_t b = std::max<int64_t>(1, std::min<int64_t>(s.N, (int64_t(1) << 24) / std::max<int64_t>(s.S, 1)));
-    Buf P(s.S * b * (int64_t)es);
+  if (other == 0) return 0;
+  using namespace slnat;
+  if (dim == 1 && (s.kind == K_HASH || s.kind == K_SAMPLE || s.kind == K_PPT) && !rowwise_fits(N, dt))
+    return apply_by_transpose(s, A, SA);
+  // column k0.. of the operator against rows k0.. of A (dim 0) / columns (dim 1)
+  auto acc_panel = [&](const void* P, bool p_rowmajor_sxk, int64_t k0, int64_t kb, double beta) -> int {
+    // P: S x kb row-major (ld kb) if p_rowmajor_sxk, else kb x S row-major (ld S)
+    if (dim == 0)
+      return gemm_rm(dt, !p_rowmajor_sxk, false, S, other, kb, P, p_rowmajor_sxk ? kb : S,
+                     (const char*)A.data + k0 * A.ld * es, A.ld, beta, SA.data, SA.ld);
+    return gemm_rm(dt, false, p_rowmajor_sxk, other, S, kb, (const char*)A.data + k0 * es, A.ld, P,
+                   p_rowmajor_sxk ? kb : S, beta, SA.data, SA.ld);
+  };
+  if (s.kind == K_DENSE || s.kind == K_QMC) {
+    const int64_t b = std::max<int64_t>(1, std::min<int64_t>(N, (int64_t(1) << 24) / std::max<int64_t>(S, 1)));
+    Buf P(S * b * (int64_t)es);
     if (!P.p) return fail(101, "device sketch: allocation failed");
-    for (int64_t k0 = 0; k0 < s.N; k0 += b) {
-      const int64_t kb = std::min(b, s.N - k0);
-      SLDEV_TRY(L.fill_random(P.p, dt, s.dist, s.seed, s.ctr0, s.S, kb, kb, 1, 0, k0, 1, s.S, 0.0, 0.0, s.scale,
-                              dt == F64 ? 1 : 0, st),
-                "sketch panel");
-      const double beta = k0 == 0 ? 0.0 : 1.0;
-      int rc;
-      if (dim == 0)
-        rc = gemm_rm(dt, false, false, s.S, other, kb, P.p, kb, (const char*)A.data + k0 * A.ld * es, A.ld, beta,
-                     SA.data, SA.ld);
-      else
-        rc = gemm_rm(dt, false, true, other, s.S, kb, (const char*)A.data + k0 * es, A.ld, P.p, kb, beta, SA.data,
-                     SA.ld);
+    std::vector<double> hp;
+    for (int64_t k0 = 0; k0 < N; k0 += b) {
+      const int64_t kb = std::min(b, N - k0);
+      if (s.kind == K_DENSE) {
+        SLDEV_TRY(L.fill_random(P.p, dt, s.dist, s.seed, s.wbase, S, kb, kb, 1, 0, k0, 1, S, s.p0, 0.0, s.scale,
+                                dt == F64 ? 1 : 0, st),
+                  "sketch panel");
+      } else {
+        hp.resize((size_t)(S * kb));
+        realise_cols(s, k0, kb, hp.data());   // column-major S x kb = row-major kb x S
+        const int rc = upload_as(P, hp.data(), S * kb, dt);
+        if (rc) return rc;
+      }
+      const int rc = acc_panel(P.p, s.kind == K_DENSE, k0, kb, k0 == 0 ? 0.0 : 1.0);
       if (rc) return rc;
     }
-    return check(L.dev_sync(st), "sync");
+  } else if (s.kind == K_FJLT) {
+    Buf dsamp(S * 8), dD(N * 8);
+    int rc;
+    if ((rc = upload(dsamp, s.samples)) || (rc = upload(dD, s.dsign))) return rc;
+    const int64_t pb = std::max<int64_t>(1, std::min<int64_t>(S, (int64_t(1) << 25) / N));
+    Buf W(pb * N * (int64_t)es);
+    if (!W.p) return fail(101, "device FJLT: allocation failed");
+    for (int64_t j0 = 0; j0 < S; j0 += pb) {
+      const int64_t nb = std::min(pb, S - j0);
+      SLDEV_TRY(L.dct2_rows((const int64_t*)dsamp.p + j0, nb, N, (const double*)dD.p, s.scale, W.p, dt, N, 0, st),
+                "fjlt rows");
+      rc = dim == 0 ? gemm_rm(dt, false, false, nb, other, N, W.p, N, A.data, A.ld, 0.0,
+                              (char*)SA.data + j0 * SA.ld * es, SA.ld)
+                    : gemm_rm(dt, false, true, other, nb, N, A.data, A.ld, W.p, N, 0.0, (char*)SA.data + j0 * es,
+                              SA.ld);
+      if (rc) return rc;
+    }
+  } else if (s.kind == K_FASTFOOD) {
+    // block b: SA[rows s..e] = F[0:e-s] diag(G_b) (F[perm_b] diag(B_b) A)
+    const int64_t NB = N;
+    std::vector<int64_t> iota((size_t)NB);
+    for (int64_t i = 0; i < NB; ++i) iota[(size_t)i] = i;
+    Buf drows(NB * 8), dperm(s.nb * NB * 8), dB(s.nb * NB * 8), dG(s.nb * NB * 8), A2(NB * N * (int64_t)es),
+        A1(NB * N * (int64_t)es), T(NB * other * (int64_t)es);
+    int rc;
+    if ((rc = upload(drows, iota)) || (rc = upload(dperm, s.perms)) || (rc = upload(dB, s.fB)) || (rc = upload(dG, s.fG)))
+      return rc;
+    if (!A2.p || !A1.p || !T.p) return fail(101, "device Fastfood: allocation failed");
+    for (int64_t b = 0; b < s.nb; ++b) {
+      const int64_t r0 = b * NB, r1 = std::min(S, r0 + NB), nr = r1 - r0;
+      SLDEV_TRY(L.dct2_rows((const int64_t*)dperm.p + b * NB, NB, N, (const double*)dB.p + b * NB, 1.0, A2.p, dt, N, 0,
+                            st),
+                "fastfood F P B");
+      SLDEV_TRY(L.dct2_rows((const int64_t*)drows.p, nr, N, (const double*)dG.p + b * NB, 1.0, A1.p, dt, N, 0, st),
+                "fastfood F G");
+      if (dim == 0) {
+        if ((rc = gemm_rm(dt, false, false, NB, other, N, A2.p, N, A.data, A.ld, 0.0, T.p, other))) return rc;
+        if ((rc = gemm_rm(dt, false, false, nr, other, NB, A1.p, N, T.p, other, 0.0, (char*)SA.data + r0 * SA.ld * es,
+                          SA.ld)))
+          return rc;
+      } else {
+        if ((rc = gemm_rm(dt, false, true, other, NB, N, A.data, A.ld, A2.p, N, 0.0, T.p, NB))) return rc;
+        if ((rc = gemm_rm(dt, false, true, other, nr, NB, T.p, NB, A1.p, N, 0.0, (char*)SA.data + r0 * es, SA.ld)))
+          return rc;
+      }
+    }
+  } else if (s.kind == K_HASH || s.kind == K_SAMPLE) {
+    if (s.kind == K_HASH) {
+      HashDev H(N, S);
+      const int rc = hash_upload(H, s.idx, s.val, S);
+      if (rc) return rc;
+      if (hash_apply(H, N, S, A, SA, dim, 0)) return 106;
+    } else {
+      // output i = input samples[i]: the bucket structure of a gather
+      std::vector<int64_t> bptr((size_t)S + 1);
+      for (int64_t i = 0; i <= S; ++i) bptr[(size_t)i] = i;
+      std::vector<double> ones((size_t)std::max(N, S), 1.0);
+      Buf perm(S * 8), dbptr((S + 1) * 8), dones((int64_t)ones.size() * 8);
+      int rc;
+      if ((rc = upload(perm, s.samples)) || (rc = upload(dbptr, bptr)) || (rc = upload(dones, ones))) return rc;
+      if (dim == 0)
+        SLDEV_TRY(L.hash_colwise(A.data, dt, A.ld, A.n, (const int64_t*)perm.p, (const int64_t*)dbptr.p,
+                                 (const double*)dones.p, S, SA.data, dt, SA.ld, 0, 0, st),
+                  "gather rows");
+      else
+        SLDEV_TRY(L.hash_rowwise(A.data, dt, A.ld, A.m, N, (const int64_t*)perm.p, (const int64_t*)dbptr.p,
+                                 (const double*)dones.p, S, SA.data, dt, SA.ld, 0, 0, st),
+                  "gather columns");
+    }
+  } else {   // PPT: q CountSketches, DFTs as GEMMs, spectrum product, inverse DFT
+    const int64_t q = s.q, K = S / 2 + 1;
+    if (q == 0) return zero(SA) ? 106 : check(L.dev_sync(st), "sync");
+    const int64_t plane = K * other;
+    Buf U(S * other * (int64_t)es), F(2 * q * plane * (int64_t)es), P(2 * plane * (int64_t)es), Cm(K * S * (int64_t)es),
+        Sm(K * S * (int64_t)es), hidx(q * 8), hval(q * 8);
+    if (!U.p || !F.p || !P.p || !Cm.p || !Sm.p) return fail(101, "device PPT: allocation failed");
+    int rc;
+    if ((rc = upload(hidx, s.hidx)) || (rc = upload(hval, s.hval))) return rc;
+    SLDEV_TRY(L.dft_cs(S, K, Cm.p, Sm.p, dt, st), "dft tables");
+    const double sg = std::sqrt(s.gamma);
+    for (int64_t i = 0; i < q; ++i) {
+      HashDev H(N, S);
+      std::vector<int64_t> idx(s.pidx.begin() + i * N, s.pidx.begin() + (i + 1) * N);
+      std::vector<double> val(s.pval.begin() + i * N, s.pval.begin() + (i + 1) * N);
+      if ((rc = hash_upload(H, idx, val, S, sg))) return rc;
+      const DevMat Ui = dim == 0 ? DevMat{U.p, dt, S, other, other} : DevMat{U.p, dt, other, S, S};
+      if (hash_apply(H, N, S, A, Ui, dim, 0)) return 106;
+      char* Fr = (char*)F.p + i * plane * (int64_t)es;
+      char* Fi = (char*)F.p + (q + i) * plane * (int64_t)es;
+      if (dim == 0) {   // K x other = (K x S)(S x other)
+        if ((rc = gemm_rm(dt, false, false, K, other, S, Cm.p, S, U.p, other, 0.0, Fr, other))) return rc;
+        if ((rc = gemm_rm(dt, false, false, K, other, S, Sm.p, S, U.p, other, 0.0, Fi, other))) return rc;
+      } else {          // other x K = (other x S)(S x K)
+        if ((rc = gemm_rm(dt, false, true, other, K, S, U.p, S, Cm.p, S, 0.0, Fr, K))) return rc;
+        if ((rc = gemm_rm(dt, false, true, other, K, S, U.p, S, Sm.p, S, 0.0, Fi, K))) return rc;
+      }
+    }
+    const int64_t sk = dim == 0 ? other : 1, sc = dim == 0 ? 1 : K;
+    SLDEV_TRY(L.ppt_spectrum(F.p, (int)q, K, other, sk, sc, plane, S, (const int64_t*)hidx.p, (const double*)hval.p,
+                             std::sqrt(s.c), P.p, dt, st),
+              "ppt spectrum");
+    const char* Pr = (const char*)P.p;
+    const char* Pi = (const char*)P.p + plane * (int64_t)es;
+    if (dim == 0) {   // S x other = C^T Pr - Sn^T Pi
+      if ((rc = gemm_rm(dt, true, false, S, other, K, Cm.p, S, Pr, other, 0.0, SA.data, SA.ld))) return rc;
+      if ((rc = gemm_rm(dt, true, false, S, other, K, Sm.p, S, Pi, other, 1.0, SA.data, SA.ld, -1.0))) return rc;
+    } else {          // other x S = Pr C - Pi Sn
+      if ((rc = gemm_rm(dt, false, false, other, S, K, Pr, K, Cm.p, S, 0.0, SA.data, SA.ld))) return rc;
+      if ((rc = gemm_rm(dt, false, false, other, S, K, Pi, K, Sm.p, S, 1.0, SA.data, SA.ld, -1.0))) return rc;
+    }
   }
-  if (s.type == "FJLT") {
-    if (s.S * s.N > (int64_t(1) << 28)) return fail(103, "device FJLT: S x N operator too large for the explicit path");
-    // FJLT_data draws: N Rademacher signs, then S frequencies
-    const uint64_t prm_h[3] = {s.seed, s.ctr0, s.ctr0 + (uint64_t)s.N};
-    Buf prm(sizeof prm_h), F(s.S * s.N * (int64_t)es);
-    if (!prm.p || !F.p) return fail(101, "device FJLT: allocation failed");
-    SLDEV_TRY(L.dev_memcpy(prm.p, prm_h, sizeof prm_h, 0, st), "copy");
-    SLDEV_TRY(L.fjlt_operator((const uint64_t*)prm.p, s.S, s.N, std::sqrt((double)s.N / (double)s.S), F.p, dt, s.N, 0,
-                              st),
-              "fjlt operator");
-    const int rc = dim == 0 ? gemm_rm(dt, false, false, s.S, other, s.N, F.p, s.N, A.data, A.ld, 0.0, SA.data, SA.ld)
-                            : gemm_rm(dt, false, true, other, s.S, s.N, A.data, A.ld, F.p, s.N, 0.0, SA.data, SA.ld);
-    if (rc) return rc;
-    return check(L.dev_sync(st), "sync");
-  }
-  // hash sketches: bucket order of the N inputs (stable), bucket pointers
-  std::vector<int64_t> perm((size_t)s.N), bptr((size_t)s.S + 1, 0);
-  for (int64_t j = 0; j < s.N; ++j) ++bptr[(size_t)s.idx[(size_t)j] + 1];
-  for (int64_t b = 0; b < s.S; ++b) bptr[(size_t)b + 1] += bptr[(size_t)b];
-  {
-    std::vector<int64_t> fill(bptr.begin(), bptr.end() - 1);
-    for (int64_t j = 0; j < s.N; ++j) perm[(size_t)fill[(size_t)s.idx[(size_t)j]]++] = j;
-  }
-  std::vector<double> vals((size_t)s.N);
-  for (int64_t j = 0; j < s.N; ++j) vals[(size_t)j] = dim == 0 ? s.val[(size_t)perm[(size_t)j]] : s.val[(size_t)j];
-  Buf dperm(s.N * 8), dbptr((s.S + 1) * 8), dval(s.N * 8);
-  if (!dperm.p || !dbptr.p || !dval.p) return fail(101, "device hash sketch: allocation failed");
-  SLDEV_TRY(L.dev_memcpy(dperm.p, perm.data(), s.N * 8, 0, st), "copy");
-  SLDEV_TRY(L.dev_memcpy(dbptr.p, bptr.data(), (s.S + 1) * 8, 0, st), "copy");
-  SLDEV_TRY(L.dev_memcpy(dval.p, vals.data(), s.N * 8, 0, st), "copy");
-  for (int64_t i = 0; i < SA.m; ++i)
-    SLDEV_TRY(L.dev_memset((char*)SA.data + i * SA.ld * es, 0, SA.n * (int64_t)es, st), "memset");
-  if (dim == 0) {
-    SLDEV_TRY(L.hash_colwise(A.data, dt, A.ld, other, (const int64_t*)dperm.p, (const int64_t*)dbptr.p,
-                             (const double*)dval.p, s.S, SA.data, dt, SA.ld, 0, 1, st),
-              "hash colwise");
-  } else {
-    SLDEV_TRY(L.hash_rowwise(A.data, dt, A.ld, other, s.N, (const int64_t*)dperm.p, (const int64_t*)dbptr.p,
-                             (const double*)dval.p, s.S, SA.data, dt, SA.ld, 0, 1, st),
-              "hash rowwise");
-  }
+  const int rc = epilogue_dev(s, SA, dim);
+  if (rc) return rc;
   return check(L.dev_sync(st), "sync");
+}
+
+// CSR on the device (rowptr int64, col int32, val f64): rows x cols.
+struct DevCsr {
+  const int64_t* rowptr;
+  const int* col;
+  const double* val;
+  int64_t rows, cols, nnz;
+  const int* rowptr32;   // the same row pointers as int32 (densify kernel)
+};
+
+// SA (f64 row-major) = sketch of the CSR matrix along dim; hash sketches run
+// on the CSR directly, the rest on its dense form
+inline int apply_sketch_csr(const slnat::Sketch& s, const DevCsr& A, const DevMat& SA, int dim) {
+  Lib& L = lib();
+  using namespace slnat;
+  const int64_t sk_in = dim == 0 ? A.rows : A.cols, other = dim == 0 ? A.cols : A.rows;
+  if (sk_in != s.N || (dim == 0 ? (SA.m != s.S || SA.n != other) : (SA.m != other || SA.n != s.S)))
+    return fail(104, "device sketch: dimension mismatch");
+  if (s.kind == K_HASH && SA.dtype == F64) {
+    HashDev H(s.N, s.S);
+    int rc = hash_upload(H, s.idx, s.val, s.S);
+    if (rc) return rc;
+    if (zero(SA)) return 106;
+    const int64_t avg = A.rows ? A.nnz / A.rows : 0;
+    if (dim == 0) {
+      const int group = avg >= 48 ? 64 : avg >= 12 ? 16 : avg >= 3 ? 4 : 1;
+      SLDEV_TRY(L.hash_csr_col(A.rowptr, A.col, 1, A.val, F64, (const int64_t*)H.perm.p, (const int64_t*)H.bptr.p,
+                               H.pval.p, s.S, A.cols, SA.data, SA.ld, 0, group, 0, nullptr, 0.0, nullptr),
+                "hash csr colwise");
+    } else {
+      SLDEV_TRY(L.hash_csr_row(A.rowptr, A.col, 1, A.val, F64, A.rows, (const int64_t*)H.idx.p, (const double*)H.val.p,
+                               SA.data, SA.ld, 0, 1, nullptr),
+                "hash csr rowwise");
+    }
+    return check(L.dev_sync(nullptr), "sync");
+  }
+  Buf D(A.rows * A.cols * 8);
+  if (!D.p) return fail(101, "device sketch: allocation failed (dense form of the sparse input)");
+  SLDEV_TRY(L.dev_memset(D.p, 0, A.rows * A.cols * 8, nullptr), "memset");
+  SLDEV_TRY(L.csr_to_dense(A.rowptr32, A.col, A.val, A.rows, D.p, F64, A.cols, nullptr), "densify");
+  return apply_sketch(s, DevMat{D.p, F64, A.rows, A.cols, A.cols}, SA, dim);
+}
+
+// ------------------------------------------- host operands staged to the GPU
+// A "Matrix" (column-major m x n) is the row-major n x m A^T on the device, so
+// sketching dim d of A is sketching dim 1 - d of that view, and the row-major
+// result is the column-major SA: no transposes, one copy each way.
+inline int apply_host_dense(const slnat::Sketch& s, const double* A, int64_t m, int64_t n, double* SA, int64_t sm,
+                            int64_t sn, int dim) {
+  Lib& L = lib();
+  if (dim == 0 ? (m != s.N || sm != s.S || sn != n) : (n != s.N || sn != s.S || sm != m))
+    return fail(104, "sl_apply_sketch_transform: dimension mismatch");
+  Buf dA(std::max<int64_t>(1, m * n) * 8), dS(std::max<int64_t>(1, sm * sn) * 8);
+  if (!dA.p || !dS.p) return fail(101, "device sketch: allocation failed");
+  SLDEV_TRY(L.dev_memcpy(dA.p, A, m * n * 8, 0, nullptr), "copy");
+  const int rc = apply_sketch(s, DevMat{dA.p, F64, n, m, m}, DevMat{dS.p, F64, sn, sm, sm}, 1 - dim);
+  if (rc) return rc;
+  SLDEV_TRY(L.dev_memcpy(SA, dS.p, sm * sn * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
+// A "SparseMatrix" (CSC of m x n) is the CSR of the n x m A^T
+inline int apply_host_csc(const slnat::Sketch& s, const int* indptr, const int* ind, const double* val, int64_t nnz,
+                          int64_t m, int64_t n, double* SA, int64_t sm, int64_t sn, int dim) {
+  Lib& L = lib();
+  if (dim == 0 ? (m != s.N || sm != s.S || sn != n) : (n != s.N || sn != s.S || sm != m))
+    return fail(104, "sl_apply_sketch_transform: dimension mismatch");
+  std::vector<int64_t> rp64((size_t)n + 1);
+  for (int64_t j = 0; j <= n; ++j) rp64[(size_t)j] = indptr[j];
+  Buf drp(rp64.size() * 8), drp32((n + 1) * 4), dcol(std::max<int64_t>(1, nnz) * 4), dval(std::max<int64_t>(1, nnz) * 8),
+      dS(std::max<int64_t>(1, sm * sn) * 8);
+  int rc = upload(drp, rp64);
+  if (rc) return rc;
+  if (!drp32.p || !dcol.p || !dval.p || !dS.p) return fail(101, "device sketch: allocation failed");
+  SLDEV_TRY(L.dev_memcpy(drp32.p, indptr, (n + 1) * 4, 0, nullptr), "copy");
+  if (nnz) {
+    SLDEV_TRY(L.dev_memcpy(dcol.p, ind, nnz * 4, 0, nullptr), "copy");
+    SLDEV_TRY(L.dev_memcpy(dval.p, val, nnz * 8, 0, nullptr), "copy");
+  }
+  const DevCsr C{(const int64_t*)drp.p, (const int*)dcol.p, (const double*)dval.p, n, m, nnz, (const int*)drp32.p};
+  rc = apply_sketch_csr(s, C, DevMat{dS.p, F64, sn, sm, sm}, 1 - dim);
+  if (rc) return rc;
+  SLDEV_TRY(L.dev_memcpy(SA, dS.p, sm * sn * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
 }
 
 // ---------------------------------------------------------------- randSVD
 struct SvdParams {
   int ratio = 2, additive = 0, iters = 0;
+  bool skip_qr = false;
   std::string sketch = "JLT";
 };
 
@@ -305,6 +622,7 @@ inline SvdParams parse_svd_params(const char* js) {
   if (slnat::get_number(js, "oversampling_ratio", v)) p.ratio = (int)v;
   if (slnat::get_number(js, "oversampling_additive", v)) p.additive = (int)v;
   if (slnat::get_number(js, "num_iterations", v)) p.iters = (int)v;
+  slnat::get_bool(js, "skip_qr", p.skip_qr);
   std::string sk;
   if (slnat::get_string(js, "sketch", sk)) {
     for (auto& c : sk) c = (char)toupper(c);
@@ -436,6 +754,179 @@ inline int approximate_svd(const DevMat& A, const DevMat& U, const DevMat& Sv, c
     return fail(106, "device approximate_svd: a pass-boundary kernel timed out (status 16); outputs invalid");
   }
   if (status & 2) return fail(108, "device approximate_svd: non-finite values in A");
+  return 0;
+}
+
+
+// ------------------------------------------ NLA on host ("Matrix") operands
+// Return value HOST_DECLINED: the call is outside the native coverage and the
+// caller runs it on the runtime instead.
+constexpr int HOST_DECLINED = -1;
+
+// column-major host (m x n, ld m) <- row-major device-order host buffer (m x n, ld n)
+inline void rm_to_cm(const double* rm, int64_t m, int64_t n, double* cm) {
+  for (int64_t i = 0; i < m; ++i)
+    for (int64_t j = 0; j < n; ++j) cm[i + j * m] = rm[i * n + j];
+}
+
+// ApproximateSVD of a column-major host A (m x n): U (m x rank), s (rank), V
+// (n x rank), column-major.  The tall operand (A, or A^T for m < n) runs on
+// the general-precision device engine in f64 with the sketch drawn from
+// (seed, ctr) exactly as the runtime draws it (nla/svd.py
+// _approximate_svd_device): JLT / CT dense, FJLT, CWT explicit.
+inline int approximate_svd_host(const double* A, int64_t m, int64_t n, double* U, double* s, double* V, int rank,
+                                const char* params, uint64_t seed, uint64_t& ctr) {
+  Lib& L = lib();
+  if (rank < 1 || rank > std::min(m, n)) return fail(109, "approximate_svd: incompatible matrix dimensions and rank");
+  const SvdParams p = parse_svd_params(params);
+  const bool tall = m >= n;
+  const int64_t M = tall ? m : n, Nn = tall ? n : m;   // the tall operand T (M x Nn)
+  const int k = (int)std::max<int64_t>(rank, std::min<int64_t>(Nn, (int64_t)p.ratio * rank + p.additive));
+  if (k > 128 || k > Nn) return HOST_DECLINED;
+  if (p.sketch != "JLT" && p.sketch != "CT" && p.sketch != "FJLT" && p.sketch != "CWT")
+    return fail(109, "approximate_svd: sketch must be JLT, CT, FJLT or CWT");
+  const int q = std::max(0, p.iters);
+  Buf dA(m * n * 8), dT(tall ? m * n * 8 : 8), dU(M * rank * 8), dS(rank * 8), dV(Nn * rank * 8);
+  if (!dA.p || !dT.p || !dU.p || !dS.p || !dV.p) return fail(101, "approximate_svd: device allocation failed");
+  SLDEV_TRY(L.dev_memcpy(dA.p, A, m * n * 8, 0, nullptr), "copy");
+  // the upload is the row-major n x m A^T: tall A needs the transpose
+  const void* T = dA.p;
+  if (tall) {
+    SLDEV_TRY(L.transpose(dA.p, F64, n, m, m, dT.p, n, nullptr), "transpose");
+    T = dT.p;
+  }
+  void* plan = nullptr;
+  SLDEV_TRY(L.gen_create(M, Nn, Nn, k, rank, q, F64, &plan), "rsvd plan");
+  struct Guard {
+    void* p;
+    ~Guard() { lib().gen_destroy(p); }
+  } guard{plan};
+  const uint64_t base = ctr;
+  if (p.sketch == "JLT" || p.sketch == "CT") {
+    const bool jlt = p.sketch == "JLT";
+    SLDEV_TRY(L.gen_set_dense(plan, jlt ? sl::DIST_NORMAL : sl::DIST_CAUCHY, seed, base, 0.0, 0.0,
+                              jlt ? std::sqrt(1.0 / k) : 1.0 / k),
+              "sketch operator");
+    ctr = base + (uint64_t)(Nn * k);
+  } else if (p.sketch == "FJLT") {
+    SLDEV_TRY(L.gen_set_fjlt(plan, seed, base, base + (uint64_t)Nn, std::sqrt((double)Nn / k)), "sketch operator");
+    ctr = base + (uint64_t)(Nn + k);
+  } else {
+    slnat::Sketch cw;
+    cw.type = "CWT";
+    cw.N = Nn;
+    cw.S = k;
+    cw.seed = seed;
+    cw.ctr0 = base;
+    ctr = slnat::build(cw);
+    std::vector<double> z((size_t)(Nn * k), 0.0);   // Z = Omega^T (Nn x k)
+    for (int64_t j = 0; j < Nn; ++j) z[(size_t)(j * k + cw.idx[(size_t)j])] = cw.val[(size_t)j];
+    Buf dz(Nn * k * 8);
+    const int rc = upload(dz, z);
+    if (rc) return rc;
+    SLDEV_TRY(L.gen_set_z(plan, dz.p, nullptr), "sketch operator");
+    SLDEV_TRY(L.dev_sync(nullptr), "sync");
+  }
+  SLDEV_TRY(L.gen_run(plan, T, dU.p, rank, dS.p, dV.p, nullptr), "rsvd run");
+  int status = 0;
+  SLDEV_TRY(L.gen_status(plan, &status, nullptr), "rsvd status");
+  if (status & 2) return fail(108, "approximate_svd: non-finite values in A");
+  std::vector<double> hU((size_t)(M * rank)), hV((size_t)(Nn * rank));
+  SLDEV_TRY(L.dev_memcpy(hU.data(), dU.p, M * rank * 8, 1, nullptr), "copy");
+  SLDEV_TRY(L.dev_memcpy(hV.data(), dV.p, Nn * rank * 8, 1, nullptr), "copy");
+  SLDEV_TRY(L.dev_memcpy(s, dS.p, rank * 8, 1, nullptr), "copy");
+  SLDEV_TRY(L.dev_sync(nullptr), "sync");
+  rm_to_cm(hU.data(), M, rank, tall ? U : V);
+  rm_to_cm(hV.data(), Nn, rank, tall ? V : U);
+  return 0;
+}
+
+// ApproximateSymmetricSVD of the column-major host A (n x n, lower triangle
+// read): V (n x rank), s (rank), column-major (sl_nat_sym_rsvd)
+inline int approximate_symmetric_svd_host(const double* A, int64_t n, double* s, double* V, int rank,
+                                          const char* params, uint64_t seed, uint64_t& ctr) {
+  Lib& L = lib();
+  if (rank < 1 || rank > n) return fail(109, "approximate_symmetric_svd: incompatible matrix dimensions and rank");
+  const SvdParams p = parse_svd_params(params);
+  const int k = (int)std::max<int64_t>(rank, std::min<int64_t>(n, (int64_t)p.ratio * rank + p.additive));
+  Buf dA(n * n * 8), dV(n * rank * 8), dS(rank * 8);
+  if (!dA.p || !dV.p || !dS.p) return fail(101, "approximate_symmetric_svd: device allocation failed");
+  SLDEV_TRY(L.dev_memcpy(dA.p, A, n * n * 8, 0, nullptr), "copy");
+  SLDEV_TRY(L.sym_rsvd((const double*)dA.p, n, n, 1, k, rank, std::max(0, p.iters), p.skip_qr ? 1 : 0, seed, ctr,
+                       (double*)dV.p, n, (double*)dS.p, nullptr),
+            "symmetric randSVD");
+  ctr += (uint64_t)(n * k);
+  SLDEV_TRY(L.dev_memcpy(V, dV.p, n * rank * 8, 1, nullptr), "copy");
+  SLDEV_TRY(L.dev_memcpy(s, dS.p, rank * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
+// FasterLeastSquares (Blendenpik) of the column-major host A (m x n; orientation
+// 1: solve with A^T), B (rows x nrhs), X (cols x nrhs) (sl_nat_blendenpik)
+inline int faster_least_squares_host(int orientation, const double* A, int64_t m, int64_t n, const double* B,
+                                     int64_t bm, int64_t bn, double* X, int64_t xm, int64_t xn, const char* params,
+                                     uint64_t seed, uint64_t& ctr) {
+  Lib& L = lib();
+  const bool adj = orientation != 0;
+  const int64_t rows = adj ? n : m, cols = adj ? m : n;
+  if (bm != rows || xm != cols || xn != bn) return fail(104, "faster_least_squares: dimension mismatch");
+  if (rows < cols) return HOST_DECLINED;
+  double tol = 1e-14, v;
+  int iter_lim = 100;
+  if (params && *params) {
+    if (slnat::get_number(params, "tolerance", v)) tol = v;
+    if (slnat::get_number(params, "iter_lim", v)) iter_lim = (int)v;
+  }
+  Buf dA(m * n * 8), dO(adj ? m * n * 8 : 8), dB(bm * bn * 8), dX(xm * xn * 8);
+  if (!dA.p || !dO.p || !dB.p || !dX.p) return fail(101, "faster_least_squares: device allocation failed");
+  SLDEV_TRY(L.dev_memcpy(dA.p, A, m * n * 8, 0, nullptr), "copy");
+  SLDEV_TRY(L.dev_memcpy(dB.p, B, bm * bn * 8, 0, nullptr), "copy");
+  const void* op = dA.p;
+  if (adj) {   // column-major A^T (n x m) = the row-major transpose of the uploaded row-major A^T
+    SLDEV_TRY(L.transpose(dA.p, F64, n, m, m, dO.p, n, nullptr), "transpose");
+    op = dO.p;
+  }
+  int code = 0;
+  SLDEV_TRY(L.blendenpik((const double*)op, rows, cols, rows, (const double*)dB.p, (int)bn, bm, (double*)dX.p, xm, seed,
+                         &ctr, tol, iter_lim, &code, nullptr),
+            "faster least squares");
+  SLDEV_TRY(L.dev_memcpy(X, dX.p, xm * xn * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
+// ------------------------------------------------------------- LIBSVM input
+struct Libsvm {
+  std::vector<double> labels, vals;
+  std::vector<int64_t> rowptr, cols;
+  int64_t rows = 0, d = 0;
+};
+
+inline int read_libsvm(const char* fname, int64_t min_d, int64_t max_n, Libsvm& out) {
+  Lib& L = lib();
+  FILE* f = fopen(fname, "rb");
+  if (!f) return fail(107, std::string("readlibsvm: cannot open ") + fname);
+  std::vector<char> buf;
+  char tmp[1 << 16];
+  size_t got;
+  while ((got = fread(tmp, 1, sizeof tmp, f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+  fclose(f);
+  const int nt = 16;
+  int64_t stats[4] = {0, 0, 0, 0}, ranges[2 * nt], counts[2 * nt];
+  int nch = 0;
+  if (!buf.empty()) {
+    if (L.libsvm_scan(buf.data(), (int64_t)buf.size(), nt, stats, ranges, counts, &nch))
+      return fail(107, std::string("readlibsvm: ") + L.last_error());
+  }
+  const int64_t rows = max_n < 0 ? stats[0] : std::min<int64_t>(stats[0], max_n);
+  out.labels.assign((size_t)rows, 0.0);
+  out.rowptr.assign((size_t)rows + 1, 0);
+  out.cols.assign((size_t)stats[1], 0);
+  out.vals.assign((size_t)stats[1], 0.0);
+  if (nch)
+    L.libsvm_fill(buf.data(), ranges, counts, nch, max_n, out.labels.data(), out.rowptr.data(), out.cols.data(),
+                  out.vals.data());
+  out.rows = rows;
+  out.d = std::max<int64_t>(stats[2], min_d);
   return 0;
 }
 

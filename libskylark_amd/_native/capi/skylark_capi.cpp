@@ -35,6 +35,8 @@
 #include <mutex>
 #include <string>
 
+#include <algorithm>
+
 #include "native_sketch.hpp"
 #include "native_device.hpp"
 
@@ -69,7 +71,12 @@ struct sl_raw_sp_matrix_t {
   int* ind;
   double* data;
   int nnz, m, n;
-  PyObject* out;  // library-owned result (capi.SparseOut) when used as output
+  PyObject* out;  // library-owned result (capi.SparseOut) when a runtime call produced it
+  // library-owned result of a native call (CSC), read back by sl_raw_sp_matrix_*
+  bool nat = false, nat_updated = false;
+  int nat_m = 0, nat_n = 0;
+  std::vector<int> nat_indptr, nat_ind;
+  std::vector<double> nat_val;
 };
 
 namespace {
@@ -418,7 +425,9 @@ SL_CAPI int sl_device_memcpy(void* dst, const void* src, int64_t bytes, int kind
 }
 
 SL_CAPI int sl_wrap_raw_sp_matrix(int* indptr, int* ind, double* data, int nnz, int n_rows, int n_cols, void** A) {
-  *A = new sl_raw_sp_matrix_t{indptr, ind, data, nnz, n_rows, n_cols, nullptr};
+  auto* M = new sl_raw_sp_matrix_t();
+  *M = sl_raw_sp_matrix_t{indptr, ind, data, nnz, n_rows, n_cols, nullptr};
+  *A = M;
   return 0;
 }
 
@@ -475,9 +484,50 @@ void copy_array(PyObject* o, const char* name, void* dst, size_t elem) {
   (void)elem;
   Py_DECREF(a);
 }
+sl_raw_sp_matrix_t* sp_nat(void* A) {
+  auto* M = (sl_raw_sp_matrix_t*)A;
+  return M->nat && !M->out ? M : nullptr;
+}
+// store a column-major dense m x n result as the native CSC output (exact zeros dropped)
+void set_sparse_out(void* A, const double* X, int64_t m, int64_t n) {
+  auto* M = (sl_raw_sp_matrix_t*)A;
+  if (M->out) {
+    Gil g;
+    Py_DECREF(M->out);
+    M->out = nullptr;
+  }
+  M->nat = true;
+  M->nat_updated = true;
+  M->nat_m = (int)m;
+  M->nat_n = (int)n;
+  M->nat_indptr.assign((size_t)n + 1, 0);
+  M->nat_ind.clear();
+  M->nat_val.clear();
+  for (int64_t j = 0; j < n; ++j) {
+    for (int64_t i = 0; i < m; ++i) {
+      const double v = X[i + j * m];
+      if (v != 0.0) {
+        M->nat_ind.push_back((int)i);
+        M->nat_val.push_back(v);
+      }
+    }
+    M->nat_indptr[(size_t)j + 1] = (int)M->nat_ind.size();
+  }
+}
+// dense column-major copy of a CSC input
+std::vector<double> csc_dense(const sl_raw_sp_matrix_t* M) {
+  std::vector<double> D((size_t)M->m * (size_t)M->n, 0.0);
+  for (int j = 0; j < M->n; ++j)
+    for (int q = M->indptr[j]; q < M->indptr[j + 1]; ++q) D[(size_t)M->ind[q] + (size_t)j * (size_t)M->m] += M->data[q];
+  return D;
+}
 }  // namespace
 
 SL_CAPI int sl_raw_sp_matrix_struct_updated(void* A, bool* updated) {
+  if (auto* M = sp_nat(A)) {
+    *updated = M->nat_updated;
+    return 0;
+  }
   return sp_query(A, [&](PyObject* o) {
     *updated = attr_long(o, "updated") != 0;
     return 0;
@@ -485,6 +535,10 @@ SL_CAPI int sl_raw_sp_matrix_struct_updated(void* A, bool* updated) {
 }
 
 SL_CAPI int sl_raw_sp_matrix_reset_update_flag(void* A) {
+  if (auto* M = sp_nat(A)) {
+    M->nat_updated = false;
+    return 0;
+  }
   return sp_query(A, [&](PyObject* o) {
     PyObject_SetAttrString(o, "updated", Py_False);
     return 0;
@@ -492,6 +546,10 @@ SL_CAPI int sl_raw_sp_matrix_reset_update_flag(void* A) {
 }
 
 SL_CAPI int sl_raw_sp_matrix_nnz(void* A, int* nnz) {
+  if (auto* M = sp_nat(A)) {
+    *nnz = (int)M->nat_val.size();
+    return 0;
+  }
   return sp_query(A, [&](PyObject* o) {
     *nnz = (int)array_len(o, "values");
     return 0;
@@ -499,6 +557,10 @@ SL_CAPI int sl_raw_sp_matrix_nnz(void* A, int* nnz) {
 }
 
 SL_CAPI int sl_raw_sp_matrix_height(void* A, int* h) {
+  if (auto* M = sp_nat(A)) {
+    *h = M->nat_m;
+    return 0;
+  }
   return sp_query(A, [&](PyObject* o) {
     *h = (int)attr_long(o, "shape", 0);
     return 0;
@@ -506,6 +568,10 @@ SL_CAPI int sl_raw_sp_matrix_height(void* A, int* h) {
 }
 
 SL_CAPI int sl_raw_sp_matrix_width(void* A, int* w) {
+  if (auto* M = sp_nat(A)) {
+    *w = M->nat_n;
+    return 0;
+  }
   return sp_query(A, [&](PyObject* o) {
     *w = (int)attr_long(o, "shape", 1);
     return 0;
@@ -513,6 +579,14 @@ SL_CAPI int sl_raw_sp_matrix_width(void* A, int* w) {
 }
 
 SL_CAPI int sl_raw_sp_matrix_data(void* A, int32_t* indptr, int32_t* indices, double* values) {
+  if (auto* M = sp_nat(A)) {
+    memcpy(indptr, M->nat_indptr.data(), sizeof(int) * M->nat_indptr.size());
+    if (!M->nat_ind.empty()) {
+      memcpy(indices, M->nat_ind.data(), sizeof(int) * M->nat_ind.size());
+      memcpy(values, M->nat_val.data(), sizeof(double) * M->nat_val.size());
+    }
+    return 0;
+  }
   return sp_query(A, [&](PyObject* o) {
     copy_array(o, "indptr", indptr, 4);
     copy_array(o, "indices", indices, 4);
@@ -524,21 +598,32 @@ SL_CAPI int sl_raw_sp_matrix_data(void* A, int32_t* indptr, int32_t* indices, do
 // ---------------------------------------------------------------- sketches
 SL_CAPI int sl_create_sketch_transform(sl_context_t* ctxt, char* type, int n, int s, sl_sketch_transform_t** sketch,
                                        ...) {
-  if (slnat::supported(type) && n > 0 && s > 0) {
+  if (slnat::supported(type) && n > 0 && s > 0 && strcmp(type, "NURST") != 0) {
     auto* ns = new slnat::Sketch();
     ns->type = type;
     ns->N = n;
     ns->S = s;
     ns->seed = ctxt->seed;
     ns->ctr0 = ctxt->counter;
-    ns->param = 1.0;
-    if (slnat::takes_param(ns->type)) {
-      va_list ap;
-      va_start(ap, sketch);
-      ns->param = va_arg(ap, double);
-      va_end(ap);
+    const std::string spec = slnat::vararg_spec(ns->type);
+    double dv[4] = {0, 0, 0, 0};
+    int64_t iv[4] = {0, 0, 0, 0};
+    va_list ap;
+    va_start(ap, sketch);
+    for (size_t i = 0; i < spec.size() && i < 4; ++i) {
+      if (spec[i] == 'i') iv[i] = va_arg(ap, int);
+      else dv[i] = va_arg(ap, double);
     }
-    ctxt->counter = slnat::build(*ns);
+    va_end(ap);
+    slnat::set_params(*ns, dv, iv);
+    std::string err;
+    const uint64_t c = slnat::build(*ns, &err);
+    if (!err.empty()) {
+      g_last_error = "sl_create_sketch_transform: " + err;
+      delete ns;
+      return 109;
+    }
+    ctxt->counter = c;
     *sketch = new sl_sketch_transform_t{nullptr, ns};
     return 0;
   }
@@ -614,12 +699,62 @@ SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type
     const int rc = sldev::apply_sketch(*S->nat, devmat(A), devmat(SA), dim);
     return rc ? native_fail(rc) : 0;
   }
-  if (S->nat && slnat::host_apply(*S->nat) && !strcmp(input_type, "Matrix") && !strcmp(output_type, "Matrix")) {
-    auto* a = (sl_raw_matrix_t*)A;
-    auto* o = (sl_raw_matrix_t*)SA;
-    const int rc = slnat::apply(*S->nat, a->data, a->m, a->n, o->data, o->m, o->n, dim);
-    if (rc) g_last_error = "sl_apply_sketch_transform: dimension mismatch";
-    return rc;
+  const bool in_dense = !strcmp(input_type, "Matrix"), in_sparse = !strcmp(input_type, "SparseMatrix");
+  const bool out_dense = !strcmp(output_type, "Matrix"), out_sparse = !strcmp(output_type, "SparseMatrix");
+  if (S->nat && (in_dense || in_sparse) && (out_dense || (out_sparse && in_sparse))) {
+    // host operands: staged to the GPU when one is present, else the host path
+    const slnat::Sketch& sk = *S->nat;
+    if (dim != 0 && dim != 1) {
+      g_last_error = "sl_apply_sketch_transform: dim must be 0 (columnwise) or 1 (rowwise)";
+      return 109;
+    }
+    int64_t m, n;
+    if (in_dense) {
+      m = ((sl_raw_matrix_t*)A)->m;
+      n = ((sl_raw_matrix_t*)A)->n;
+    } else {
+      m = ((sl_raw_sp_matrix_t*)A)->m;
+      n = ((sl_raw_sp_matrix_t*)A)->n;
+    }
+    const int64_t sm = dim == 0 ? sk.S : m, sn = dim == 0 ? n : sk.S;
+    if (out_dense && (((sl_raw_matrix_t*)SA)->m != sm || ((sl_raw_matrix_t*)SA)->n != sn)) {
+      g_last_error = "sl_apply_sketch_transform: dimension mismatch (output)";
+      return 104;
+    }
+    if ((dim == 0 ? m : n) != sk.N) {
+      g_last_error = "sl_apply_sketch_transform: dimension mismatch (input)";
+      return 104;
+    }
+    std::vector<double> tmp;
+    double* out = out_dense ? ((sl_raw_matrix_t*)SA)->data : nullptr;
+    if (!out) {
+      tmp.assign((size_t)(sm * sn), 0.0);
+      out = tmp.data();
+    }
+    int rc;
+    if (sldev::device_present()) {
+      if (in_dense) {
+        rc = sldev::apply_host_dense(sk, ((sl_raw_matrix_t*)A)->data, m, n, out, sm, sn, dim);
+      } else {
+        auto* M = (sl_raw_sp_matrix_t*)A;
+        rc = sldev::apply_host_csc(sk, M->indptr, M->ind, M->data, M->nnz, m, n, out, sm, sn, dim);
+      }
+      if (rc) return native_fail(rc);
+    } else {
+      std::vector<double> dense;
+      const double* a = in_dense ? ((sl_raw_matrix_t*)A)->data : nullptr;
+      if (!a) {
+        dense = csc_dense((sl_raw_sp_matrix_t*)A);
+        a = dense.data();
+      }
+      rc = slnat::apply(sk, a, m, n, out, sm, sn, dim);
+      if (rc) {
+        g_last_error = "sl_apply_sketch_transform: dimension mismatch";
+        return rc;
+      }
+    }
+    if (out_sparse) set_sparse_out(SA, out, sm, sn);
+    return 0;
   }
   Gil g;
   PyObject* so = py_sketch(S);
@@ -649,6 +784,22 @@ SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, cha
                                           ctxt->counter, ctxt->dcomm);
     return rc ? native_fail(rc) : 0;
   }
+  if (!strcmp(A_type, "Matrix") && !strcmp(U_type, "Matrix") && !strcmp(S_type, "Matrix") && !strcmp(V_type, "Matrix") &&
+      sldev::device_present()) {
+    auto *a = (sl_raw_matrix_t*)A, *u = (sl_raw_matrix_t*)U, *sv = (sl_raw_matrix_t*)Sv, *v = (sl_raw_matrix_t*)V;
+    if (u->m != a->m || u->n != (int)k || v->m != a->n || v->n != (int)k || (int64_t)sv->m * sv->n != (int64_t)k) {
+      g_last_error = "sl_approximate_svd: output shapes (U m x k, S k x 1, V n x k)";
+      return 104;
+    }
+    uint64_t ctr = ctxt->counter;
+    const int rc = sldev::approximate_svd_host(a->data, a->m, a->n, u->data, sv->data, v->data, (int)k, params,
+                                               ctxt->seed, ctr);
+    if (rc != sldev::HOST_DECLINED) {
+      if (rc) return native_fail(rc);
+      ctxt->counter = ctr;
+      return 0;
+    }
+  }
   Gil g;
   (void)U_type;
   (void)S_type;
@@ -665,6 +816,23 @@ SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, cha
 
 SL_CAPI int sl_approximate_symmetric_svd(char* A_type, void* A, char* S_type, void* Sv, char* V_type, void* V,
                                          uint16_t k, char* params, sl_context_t* ctxt) {
+  if (!strcmp(A_type, "Matrix") && !strcmp(S_type, "Matrix") && !strcmp(V_type, "Matrix") && sldev::device_present()) {
+    auto *a = (sl_raw_matrix_t*)A, *sv = (sl_raw_matrix_t*)Sv, *v = (sl_raw_matrix_t*)V;
+    if (a->m != a->n) {
+      g_last_error = "sl_approximate_symmetric_svd: matrix is not square -- symmetric matrix required";
+      return 109;
+    }
+    if (v->m != a->n || v->n != (int)k || (int64_t)sv->m * sv->n != (int64_t)k) {
+      g_last_error = "sl_approximate_symmetric_svd: output shapes (S k x 1, V n x k)";
+      return 104;
+    }
+    uint64_t ctr = ctxt->counter;
+    const int rc = sldev::approximate_symmetric_svd_host(a->data, a->n, sv->data, v->data, (int)k, params, ctxt->seed,
+                                                         ctr);
+    if (rc) return native_fail(rc);
+    ctxt->counter = ctr;
+    return 0;
+  }
   Gil g;
   (void)S_type;
   (void)V_type;
@@ -681,6 +849,17 @@ SL_CAPI int sl_approximate_symmetric_svd(char* A_type, void* A, char* S_type, vo
 
 SL_CAPI int sl_faster_least_squares(int orientation, char* A_type, void* A, char* B_type, void* B, char* X_type,
                                     void* X, char* params, sl_context_t* ctxt) {
+  if (!strcmp(A_type, "Matrix") && !strcmp(B_type, "Matrix") && !strcmp(X_type, "Matrix") && sldev::device_present()) {
+    auto *a = (sl_raw_matrix_t*)A, *b = (sl_raw_matrix_t*)B, *x = (sl_raw_matrix_t*)X;
+    uint64_t ctr = ctxt->counter;
+    const int rc = sldev::faster_least_squares_host(orientation, a->data, a->m, a->n, b->data, b->m, b->n, x->data, x->m,
+                                                    x->n, params, ctxt->seed, ctr);
+    if (rc != sldev::HOST_DECLINED) {
+      if (rc) return native_fail(rc);
+      ctxt->counter = ctr;
+      return 0;
+    }
+  }
   Gil g;
   (void)B_type;
   (void)X_type;
@@ -802,6 +981,75 @@ SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, voi
 // ---------------------------------------------------------------------- IO
 SL_CAPI int sl_readlibsvm(char* fname, char* X_type, void* X, char* Y_type, void* Y, int direction, int min_d,
                           int max_n) {
+  const bool xd = !strcmp(X_type, "Matrix"), xs = !strcmp(X_type, "SparseMatrix");
+  if ((xd || xs) && (!Y || !strcmp(Y_type, "Matrix")) && sldev::lib().loaded) {
+    // native LIBSVM reader (libsvm_io.cpp): examples are columns (direction
+    // 0 / 1, d x n, labels 1 x n) or rows (n x d, labels n x 1)
+    sldev::Libsvm L;
+    const int rc = sldev::read_libsvm(fname, min_d, max_n, L);
+    if (rc) return native_fail(rc);
+    const bool cols = direction == 0 || direction == 1;
+    const int64_t n = L.rows, d = L.d;
+    const int64_t xm = cols ? d : n, xn = cols ? n : d;
+    if (Y) {
+      auto* y = (sl_raw_matrix_t*)Y;
+      if (y->m != (cols ? 1 : n) || y->n != (cols ? n : 1)) {
+        g_last_error = "sl_readlibsvm: Y wrap has the wrong shape";
+        return 109;
+      }
+      memcpy(y->data, L.labels.data(), sizeof(double) * (size_t)n);
+    }
+    // (example i, feature j) -> column-major (j, i) or (i, j)
+    auto at = [&](int64_t i, int64_t j) -> size_t { return cols ? (size_t)(j + i * xm) : (size_t)(i + j * xm); };
+    if (xd) {
+      auto* x = (sl_raw_matrix_t*)X;
+      if (x->m != xm || x->n != xn) {
+        g_last_error = "sl_readlibsvm: X wrap has the wrong shape";
+        return 109;
+      }
+      memset(x->data, 0, sizeof(double) * (size_t)(xm * xn));
+      for (int64_t i = 0; i < n; ++i)
+        for (int64_t q = L.rowptr[(size_t)i]; q < L.rowptr[(size_t)i + 1]; ++q)
+          x->data[at(i, L.cols[(size_t)q])] += L.vals[(size_t)q];
+      return 0;
+    }
+    // CSC built directly (entries sorted, duplicates summed): columns are the
+    // examples (direction columns) or the features (rows)
+    std::vector<std::vector<std::pair<int, double>>> colv((size_t)xn);
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t q = L.rowptr[(size_t)i]; q < L.rowptr[(size_t)i + 1]; ++q) {
+        const int64_t j = L.cols[(size_t)q];
+        if (cols) colv[(size_t)i].push_back({(int)j, L.vals[(size_t)q]});
+        else colv[(size_t)j].push_back({(int)i, L.vals[(size_t)q]});
+      }
+    auto* M = (sl_raw_sp_matrix_t*)X;
+    if (M->out) {
+      Gil g;
+      Py_DECREF(M->out);
+      M->out = nullptr;
+    }
+    M->nat = M->nat_updated = true;
+    M->nat_m = (int)xm;
+    M->nat_n = (int)xn;
+    M->nat_indptr.assign((size_t)xn + 1, 0);
+    M->nat_ind.clear();
+    M->nat_val.clear();
+    for (int64_t j = 0; j < xn; ++j) {
+      auto& v = colv[(size_t)j];
+      std::stable_sort(v.begin(), v.end(), [](const std::pair<int, double>& a, const std::pair<int, double>& b) {
+        return a.first < b.first;
+      });
+      for (size_t t = 0; t < v.size(); ++t) {
+        if (t && v[t].first == v[t - 1].first) M->nat_val.back() += v[t].second;
+        else {
+          M->nat_ind.push_back(v[t].first);
+          M->nat_val.push_back(v[t].second);
+        }
+      }
+      M->nat_indptr[(size_t)j + 1] = (int)M->nat_ind.size();
+    }
+    return 0;
+  }
   Gil g;
   (void)Y_type;
   PyObject* xo = out_desc(X_type, X);

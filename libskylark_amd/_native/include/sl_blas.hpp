@@ -14,3 +14,14 @@ int slb_dsyevd(int n, double* A, int lda, double* D, double* E, int* info, hipSt
 // row-major G = R^T R: R^{-1} (lower triangle of the column-major storage =
 // upper of the row-major one) in place; info[0] potrf, info[1] trtri
 int slb_dpotrf_inv(int n, double* G, int ldg, int* info, hipStream_t s);
+
+// column-major LAPACK-style helpers (C API host-operand NLA paths)
+int slb_dgeqrf_cm(int m, int n, double* A, int lda, double* tau, hipStream_t s);
+int slb_dorgqr_cm(int m, int n, int k, double* A, int lda, double* tau, hipStream_t s);
+int slb_dgesvd_cm(int m, int n, double* A, int lda, double* S, double* U, int ldu, double* VT, int ldvt, double* E,
+                  int* info, hipStream_t s);
+int slb_dtrtri_upper_cm(int n, double* R, int ldr, int* info, hipStream_t s);
+int slb_dgemv_cm(bool trans, int m, int n, double alpha, const double* A, int lda, const double* x, double beta,
+                 double* y, hipStream_t s);
+int slb_dnrm2(int n, const double* x, double* result, hipStream_t s);
+int slb_dtrsv_upper_cm(bool trans, int n, const double* R, int ldr, double* x, hipStream_t s);

@@ -29,6 +29,14 @@ struct Blas {
   int (*dsyevd)(void*, int, int, int, double*, int, double*, double*, int*) = nullptr;
   int (*dpotrf)(void*, int, int, double*, int, int*) = nullptr;
   int (*dtrtri)(void*, int, int, int, double*, int, int*) = nullptr;
+  int (*dgeqrf)(void*, int, int, double*, int, double*) = nullptr;
+  int (*dorgqr)(void*, int, int, int, double*, int, double*) = nullptr;
+  int (*dgesvd)(void*, int, int, int, int, double*, int, double*, double*, int, double*, int, double*, int,
+                int*) = nullptr;
+  int (*dgemv)(void*, int, int, int, const double*, const double*, int, const double*, int, const double*, double*,
+               int) = nullptr;
+  int (*dnrm2)(void*, int, const double*, int, double*) = nullptr;
+  int (*dtrsv)(void*, int, int, int, int, const double*, int, double*, int) = nullptr;
   void* handle[64] = {};
 };
 
@@ -53,12 +61,18 @@ Blas& blas() {
   B.dgemm = (decltype(B.dgemm))sym(B.rb, "rocblas_dgemm");
   B.sgemm = (decltype(B.sgemm))sym(B.rb, "rocblas_sgemm");
   B.gemm_ex = (decltype(B.gemm_ex))sym(B.rb, "rocblas_gemm_ex");
+  B.dgemv = (decltype(B.dgemv))sym(B.rb, "rocblas_dgemv");
+  B.dnrm2 = (decltype(B.dnrm2))sym(B.rb, "rocblas_dnrm2");
+  B.dtrsv = (decltype(B.dtrsv))sym(B.rb, "rocblas_dtrsv");
   if (B.rs) {
     B.dsyevd = (decltype(B.dsyevd))dlsym(B.rs, "rocsolver_dsyevd");
     B.dpotrf = (decltype(B.dpotrf))dlsym(B.rs, "rocsolver_dpotrf");
     B.dtrtri = (decltype(B.dtrtri))dlsym(B.rs, "rocsolver_dtrtri");
+    B.dgeqrf = (decltype(B.dgeqrf))dlsym(B.rs, "rocsolver_dgeqrf");
+    B.dorgqr = (decltype(B.dorgqr))dlsym(B.rs, "rocsolver_dorgqr");
+    B.dgesvd = (decltype(B.dgesvd))dlsym(B.rs, "rocsolver_dgesvd");
   }
-  B.ok = B.create && B.set_stream && B.dgemm && B.sgemm && B.gemm_ex;
+  B.ok = B.create && B.set_stream && B.dgemm && B.sgemm && B.gemm_ex && B.dgemv && B.dnrm2 && B.dtrsv;
   return B;
 }
 
@@ -95,7 +109,7 @@ int rc_of(int st, const char* what) {
 bool slb_available() { return blas().ok; }
 bool slb_solver_available() {
   Blas& B = blas();
-  return B.ok && B.dsyevd && B.dpotrf && B.dtrtri;
+  return B.ok && B.dsyevd && B.dpotrf && B.dtrtri && B.dgeqrf && B.dorgqr && B.dgesvd;
 }
 
 // Row-major C (M x N, ldc) = alpha op(A) op(B) + beta C, as the column-major
@@ -149,4 +163,71 @@ int slb_dpotrf_inv(int n, double* G, int ldg, int* info, hipStream_t s) {
   int r1 = rc_of(L.dpotrf(h, 122 /* lower */, n, G, ldg, info), "rocsolver_dpotrf");
   if (r1 != SL_OK) return r1;
   return rc_of(L.dtrtri(h, 122, 131 /* non-unit */, n, G, ldg, info + 1), "rocsolver_dtrtri");
+}
+
+// ---------------------------------------------------------------- column-major
+// LAPACK-style entry points of the C API's host-operand NLA paths
+// (nla_native.cpp); every matrix column-major with its leading dimension.
+int slb_dgeqrf_cm(int m, int n, double* A, int lda, double* tau, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  Blas& L = blas();
+  if (!L.dgeqrf) { sl_set_last_error("librocsolver.so: rocsolver_dgeqrf unavailable"); return SL_ERR_UNSUPPORTED; }
+  return rc_of(L.dgeqrf(h, m, n, A, lda, tau), "rocsolver_dgeqrf");
+}
+
+int slb_dorgqr_cm(int m, int n, int k, double* A, int lda, double* tau, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  Blas& L = blas();
+  if (!L.dorgqr) { sl_set_last_error("librocsolver.so: rocsolver_dorgqr unavailable"); return SL_ERR_UNSUPPORTED; }
+  return rc_of(L.dorgqr(h, m, n, k, A, lda, tau), "rocsolver_dorgqr");
+}
+
+// thin SVD A = U diag(S) VT (U m x min, VT min x n), E scratch (min - 1)
+int slb_dgesvd_cm(int m, int n, double* A, int lda, double* S, double* U, int ldu, double* VT, int ldvt, double* E,
+                  int* info, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  Blas& L = blas();
+  if (!L.dgesvd) { sl_set_last_error("librocsolver.so: rocsolver_dgesvd unavailable"); return SL_ERR_UNSUPPORTED; }
+  return rc_of(L.dgesvd(h, 192 /* singular */, 192, m, n, A, lda, S, U, ldu, VT, ldvt, E, 201 /* out of place */,
+                        info), "rocsolver_dgesvd");
+}
+
+// upper (row-major lower) triangular inverse in place, column-major upper
+int slb_dtrtri_upper_cm(int n, double* R, int ldr, int* info, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  Blas& L = blas();
+  if (!L.dtrtri) { sl_set_last_error("librocsolver.so unavailable"); return SL_ERR_UNSUPPORTED; }
+  return rc_of(L.dtrtri(h, 121 /* upper */, 131, n, R, ldr, info), "rocsolver_dtrtri");
+}
+
+int slb_dgemv_cm(bool trans, int m, int n, double alpha, const double* A, int lda, const double* x, double beta,
+                 double* y, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  return rc_of(blas().dgemv(h, trans ? OP_T : OP_N, m, n, &alpha, A, lda, x, 1, &beta, y, 1), "rocblas_dgemv");
+}
+
+// Euclidean norm into a host double (synchronises the stream)
+int slb_dnrm2(int n, const double* x, double* result, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  return rc_of(blas().dnrm2(h, n, x, 1, result), "rocblas_dnrm2");
+}
+
+// x = op(R)^{-1} x for the column-major upper triangular R
+int slb_dtrsv_upper_cm(bool trans, int n, const double* R, int ldr, double* x, hipStream_t s) {
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  return rc_of(blas().dtrsv(h, 121, trans ? OP_T : OP_N, 131, n, R, ldr, x, 1), "rocblas_dtrsv");
 }

@@ -473,3 +473,159 @@ def test_device_c_program_is_interpreter_free(capi, tmp_path):
                                rtol=1e-10, atol=1e-12)
     torch.testing.assert_close(ld("k_L", np.float64, (50, 30)), Lk.gram(X, dirX="rows", dirY="columns", Y=Y),
                                rtol=1e-10, atol=1e-12)
+
+
+# every sketch type of the runtime, created natively by the C ABI (varargs as
+# the reference's csketch.cpp) -- parity with the runtime's operator on the
+# same context stream, JSON both ways, dense and sparse host operands
+ALL_TYPES = [
+    ("SJLT", []), ("UST", []), ("FJLT", []),
+    ("GaussianRFT", [1.5]), ("LaplacianRFT", [0.8]), ("MaternRFT", [1.5, 2.0]),
+    ("GaussianQRFT", [1.2, 3]), ("LaplacianQRFT", [0.9, 0]), ("ExpSemigroupRLT", [0.7]),
+    ("ExpSemigroupQRLT", [0.6, 2]), ("FastGaussianRFT", [1.3]), ("FastMaternRFT", [2.5, 1.1]),
+    ("PPT", [3, 0.5, 0.7]),
+]
+
+
+def _cargs(typ, params):
+    spec = {"GaussianQRFT": "di", "LaplacianQRFT": "di", "ExpSemigroupQRLT": "di", "PPT": "idd"}.get(typ, "d" * len(params))
+    return [C.c_int(int(p)) if c == "i" else C.c_double(float(p)) for c, p in zip(spec, params)]
+
+
+def _pysketch(typ, N, S, params, ctx):
+    cls = getattr(sk.sketch, typ)
+    if typ in ("GaussianQRFT", "LaplacianQRFT", "ExpSemigroupQRLT"):
+        return cls(N, S, params[0], skip=int(params[1]), context=ctx)
+    if typ == "PPT":
+        return cls(N, S, int(params[0]), params[1], params[2], context=ctx)
+    return cls(N, S, *params, context=ctx)
+
+
+def _apply_both(capi, h, T, A, dim, S):
+    Aw, hA = _wrap(capi, A)
+    shape = (S, A.shape[1]) if dim == 0 else (A.shape[0], S)
+    SA, hSA = _wrap(capi, np.zeros(shape))
+    assert capi.sl_apply_sketch_transform(h, b"Matrix", hA, b"Matrix", hSA, dim) == 0
+    ref = T.apply(torch.from_numpy(A.copy()), dim=dim)
+    ref = ref.to_dense() if ref.layout != torch.strided else ref
+    return SA, ref.double().numpy()
+
+
+@pytest.mark.parametrize("typ,params", ALL_TYPES, ids=[t for t, _ in ALL_TYPES])
+def test_native_all_sketch_types(capi, typ, params):
+    N, S, n = 37, 80 if typ.startswith("Fast") else 16, 5
+    ctx = C.c_void_p()
+    assert capi.sl_create_default_context(29, C.byref(ctx)) == 0
+    pctx = sk.Context(29)
+    rng = np.random.default_rng(3)
+    pos = typ.startswith("ExpSemigroup")
+    for rep in range(2):   # the second sketch checks the counter bookkeeping
+        h = C.c_void_p()
+        assert capi.sl_create_sketch_transform(ctx, typ.encode(), N, S, C.byref(h), *_cargs(typ, params)) == 0
+        T = _pysketch(typ, N, S, params, pctx)
+        A = rng.standard_normal((N, n))
+        B = rng.standard_normal((n, N))
+        if pos:
+            A, B = np.abs(A) * 0.1, np.abs(B) * 0.1
+        got, ref = _apply_both(capi, h, T, A, 0, S)
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10, err_msg=f"{typ} columnwise rep {rep}")
+        got, ref = _apply_both(capi, h, T, B, 1, S)
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10, err_msg=f"{typ} rowwise rep {rep}")
+        # C JSON -> runtime, runtime JSON -> C
+        data = C.c_char_p()
+        assert capi.sl_serialize_sketch_transform(h, C.byref(data)) == 0
+        T2 = sk.sketch.deserialize_sketch(json.loads(data.value.decode()))
+        got, _ = _apply_both(capi, h, T2, A, 0, S)
+        np.testing.assert_allclose(T2.apply(torch.from_numpy(A.copy()), dim=0).double().numpy(), got, rtol=1e-9,
+                                   atol=1e-10)
+        h2 = C.c_void_p()
+        assert capi.sl_deserialize_sketch_transform(T.to_json().encode(), C.byref(h2)) == 0
+        got2, ref = _apply_both(capi, h2, T, A, 0, S)
+        np.testing.assert_allclose(got2, ref, rtol=1e-9, atol=1e-10)
+        capi.sl_free_sketch_transform(h2)
+        capi.sl_free_sketch_transform(h)
+    capi.sl_free_context(ctx)
+
+
+def _wrap_csc(capi, Ad):
+    import scipy.sparse as sp
+    Acsc = sp.csc_matrix(Ad)
+    arrs = (Acsc.indptr.astype(np.int32), Acsc.indices.astype(np.int32), Acsc.data.astype(np.float64))
+    h = C.c_void_p()
+    capi.sl_wrap_raw_sp_matrix(arrs[0].ctypes.data_as(C.c_void_p), arrs[1].ctypes.data_as(C.c_void_p),
+                               arrs[2].ctypes.data_as(C.c_void_p), len(arrs[2]), Ad.shape[0], Ad.shape[1], C.byref(h))
+    return arrs, h
+
+
+def _read_sparse(capi, hO):
+    import scipy.sparse as sp
+    nnz, h, w = C.c_int(), C.c_int(), C.c_int()
+    capi.sl_raw_sp_matrix_nnz(hO, C.byref(nnz))
+    capi.sl_raw_sp_matrix_height(hO, C.byref(h))
+    capi.sl_raw_sp_matrix_width(hO, C.byref(w))
+    oip = np.zeros(w.value + 1, dtype=np.int32)
+    oind = np.zeros(nnz.value, dtype=np.int32)
+    oval = np.zeros(nnz.value)
+    capi.sl_raw_sp_matrix_data(hO, oip.ctypes.data_as(C.c_void_p), oind.ctypes.data_as(C.c_void_p),
+                               oval.ctypes.data_as(C.c_void_p))
+    return sp.csc_matrix((oval, oind, oip), shape=(h.value, w.value)).toarray()
+
+
+@pytest.mark.parametrize("typ,params,sparse_out", [("JLT", [], False), ("CWT", [], True), ("WZT", [1.3], True),
+                                                   ("GaussianRFT", [1.1], False), ("UST", [], True),
+                                                   ("PPT", [2, 1.0, 0.5], False)])
+def test_native_sparse_input(capi, typ, params, sparse_out):
+    """SparseMatrix (CSC) inputs on the native path, dense or sparse outputs,
+    both directions, against the runtime on the dense equivalent."""
+    N, S, n = 40, 12, 6
+    ctx = C.c_void_p()
+    capi.sl_create_default_context(31, C.byref(ctx))
+    h = C.c_void_p()
+    assert capi.sl_create_sketch_transform(ctx, typ.encode(), N, S, C.byref(h), *_cargs(typ, params)) == 0
+    T = _pysketch(typ, N, S, params, sk.Context(31))
+    rng = np.random.default_rng(4)
+    for dim in (0, 1):
+        Ad = rng.standard_normal((N, n) if dim == 0 else (n, N)) * (rng.random((N, n) if dim == 0 else (n, N)) < 0.3)
+        arrs, hA = _wrap_csc(capi, Ad)
+        shape = (S, n) if dim == 0 else (n, S)
+        if sparse_out:
+            hO = C.c_void_p()
+            capi.sl_wrap_raw_sp_matrix(None, None, None, 0, 0, 0, C.byref(hO))
+            assert capi.sl_apply_sketch_transform(h, b"SparseMatrix", hA, b"SparseMatrix", hO, dim) == 0
+            got = _read_sparse(capi, hO)
+            upd = C.c_bool()
+            capi.sl_raw_sp_matrix_struct_updated(hO, C.byref(upd))
+            assert upd.value
+            capi.sl_free_raw_sp_matrix_wrap(hO)
+        else:
+            got, hO = _wrap(capi, np.zeros(shape))
+            assert capi.sl_apply_sketch_transform(h, b"SparseMatrix", hA, b"Matrix", hO, dim) == 0
+        ref = T.apply(torch.from_numpy(Ad.copy()), dim=dim).double().numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10, err_msg=f"{typ} dim {dim}")
+        capi.sl_free_raw_sp_matrix_wrap(hA)
+    capi.sl_free_sketch_transform(h)
+
+
+@pytest.mark.parametrize("js", [
+    {"sketch_type": "UST", "replace": False},
+    {"sketch_type": "NURST", "p": list(np.linspace(0.1, 2.0, 30))},
+    {"sketch_type": "GaussianQRFT", "sigma": 2.0, "skip": 5,
+     "sequence": {"skylark_object_type": "qmc_sequence", "sequence_type": "leaped halton", "d": 31, "leap": 7}},
+])
+def test_native_deserialized_types(capi, js):
+    """Types / parameters reachable only through JSON (UST without
+    replacement, NURST's probability vector, a custom QMC leap)."""
+    d = {"skylark_object_type": "sketch", "skylark_version": "0.1.0", "N": 30, "S": 9,
+         "creation_context": {"skylark_object_type": "context", "seed": 77, "counter": 1234}}
+    d.update(js)
+    T = sk.sketch.deserialize_sketch(d)
+    h = C.c_void_p()
+    assert capi.sl_deserialize_sketch_transform(json.dumps(d).encode(), C.byref(h)) == 0
+    A = np.random.default_rng(5).standard_normal((30, 4))
+    got, ref = _apply_both(capi, h, T, A, 0, 9)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-10)
+    data = C.c_char_p()
+    capi.sl_serialize_sketch_transform(h, C.byref(data))
+    T2 = sk.sketch.deserialize_sketch(json.loads(data.value.decode()))
+    np.testing.assert_allclose(T2.apply(torch.from_numpy(A.copy()), dim=0).numpy(), ref, rtol=1e-12, atol=1e-12)
+    capi.sl_free_sketch_transform(h)
