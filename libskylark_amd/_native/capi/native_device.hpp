@@ -113,7 +113,8 @@ struct Lib {
   int (*libsvm_fill)(const char*, const int64_t*, const int64_t*, int, int64_t, double*, int64_t*, int64_t*,
                      double*) = nullptr;
   // rocBLAS (plain library GEMMs)
-  void* rb_handle = nullptr;
+  void* rb_handle = nullptr;   // created on first use (needs a device)
+  int (*rb_create)(void**) = nullptr;
   int (*rb_dgemm)(void*, int, int, int, int, int, const double*, const double*, int, const double*, int,
                   const double*, double*, int) = nullptr;
   int (*rb_sgemm)(void*, int, int, int, int, int, const float*, const float*, int, const float*, int, const float*,
@@ -186,14 +187,9 @@ inline Lib& lib() {
       L.err = "cannot load librocblas.so";
       return;
     }
-    int (*create)(void**) = nullptr;
-    if (!bind(L.rb, "rocblas_create_handle", create, L.err) || !bind(L.rb, "rocblas_dgemm", L.rb_dgemm, L.err) ||
+    if (!bind(L.rb, "rocblas_create_handle", L.rb_create, L.err) || !bind(L.rb, "rocblas_dgemm", L.rb_dgemm, L.err) ||
         !bind(L.rb, "rocblas_sgemm", L.rb_sgemm, L.err))
       return;
-    if (create(&L.rb_handle) != 0) {
-      L.err = "rocblas_create_handle failed";
-      return;
-    }
     L.loaded = true;
   });
   return L;
@@ -236,6 +232,10 @@ struct Buf {
 inline int gemm_rm(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                    const void* B, int64_t ldb, double beta, void* C, int64_t ldc, double alpha = 1.0) {
   Lib& L = lib();
+  if (!L.rb_handle && L.rb_create(&L.rb_handle) != 0) {
+    L.rb_handle = nullptr;
+    return fail(106, "rocblas_create_handle failed");
+  }
   const int opA = ta ? 112 : 111, opB = tb ? 112 : 111;
   int rc;
   if (dt == F64) {

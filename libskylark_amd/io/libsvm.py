@@ -74,10 +74,29 @@ def _parse(addr: int, start: int, end: int, max_n: int = -1):
     return labels, rowptr, cols[:nnz], vals[:nnz], int(stats[2])
 
 
+def _rows_sorted(rowptr, cols) -> bool:
+    """Column indices strictly increasing inside every row."""
+    inc = np.diff(cols) > 0
+    if len(inc) == 0:
+        return True
+    starts = rowptr[1:-1] - 1            # positions where a new row begins (diff across rows is free)
+    starts = starts[(starts >= 0) & (starts < len(inc))]
+    inc[starts] = True
+    return bool(inc.all())
+
+
 def _to_tensor(labels, rowptr, cols, vals, d, sparse, dtype, device):
     n = len(labels)
-    X = torch.sparse_csr_tensor(torch.from_numpy(rowptr), torch.from_numpy(cols), torch.from_numpy(vals).to(dtype),
-                                (n, d), check_invariants=True)
+    rp = np.asarray(rowptr, dtype=np.int64)
+    cl = np.asarray(cols, dtype=np.int64)
+    if len(cl) and not (np.all(np.diff(cl) > 0) or _rows_sorted(rp, cl)):
+        # entries out of order / repeated within a row (legal LIBSVM): sort, sum duplicates
+        rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+        coo = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, cl])), torch.from_numpy(vals).to(dtype), (n, d))
+        X = coo.coalesce().to_sparse_csr()
+    else:
+        X = torch.sparse_csr_tensor(torch.from_numpy(rp), torch.from_numpy(cl), torch.from_numpy(vals).to(dtype),
+                                    (n, d), check_invariants=True)
     if not sparse:
         X = X.to_dense()
     if device is not None:

@@ -701,6 +701,9 @@ def _transpose(A):
     if isinstance(A, DistMatrix):
         g = A.redistribute("STAR_VC")
         return DistMatrix(g.local.t().contiguous(), (A.shape[1], A.shape[0]), "VC_STAR", A.comm)
+    if isinstance(A, torch.Tensor) and A.is_cuda and A.layout == torch.strided:
+        # one transposing copy: the device engines need unit column stride
+        return A.t().contiguous()
     return A.t()
 
 
