@@ -7,7 +7,6 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-import ctypes as C
 import statistics
 
 import torch
@@ -34,17 +33,15 @@ def timeit(fn, reps=50):
 
 def main():
     dev = torch.device("cuda")
-    lib = _lib.require()
-    lib.sl_small_chol_impl.argtypes = [C.c_int]
+    _lib.require()
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     for k in (16, 40, 64):
         X = torch.randn(4 * k, k, dtype=torch.float64, device=dev)
         G = X.t() @ X
-        for impl, name in ((0, "auto"), (1, "lds"), (3, "wave"), (4, "lds1b"), (5, "aug")):
-            lib.sl_small_chol_impl(impl)
-            us = timeit(lambda: SL.chol_inv(G, st))
-            print(f"chol_inv k={k:2d} {name:4s} {us:8.1f} us", flush=True)
-    lib.sl_small_chol_impl(0)
+        us = timeit(lambda: SL.chol_inv(G, st))
+        print(f"chol_inv k={k:2d} aug  {us:8.1f} us", flush=True)
+        us = timeit(lambda: SL.chol_inv_wave(G, st))
+        print(f"chol_inv k={k:2d} wave {us:8.1f} us", flush=True)
     W = torch.randn(1000, 40, device=dev)
     print(f"cholqr2 1000x40      {timeit(lambda: SL.cholqr2(W, st)):8.1f} us", flush=True)
 

@@ -562,19 +562,13 @@ int launch_large(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int
   return SL_OK;
 }
 
-int g_fg_large = -1;   // SL_FG_LARGE: 0 off, 1 on (default)
-
 template <bool ALO, bool WLO, int EPI>
 int launch_out(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int64_t K, int64_t lda, const bf16_t* Whi,
                const bf16_t* Wlo, int64_t Nf, int64_t ldw, const float* sc, const float* sh, float outscale,
                void* out, int out_dtype, int64_t ldo, int out_t, hipStream_t s, const float* rt, float p0) {
-  if (g_fg_large < 0) {
-    const char* e = getenv("SL_FG_LARGE");
-    g_fg_large = e ? atoi(e) : 1;
-  }
   // large tiles: row-major output, the feature tiles split into 4 XCD quarters,
   // and W padded to whole 128-row tiles (the host pads to 128)
-  if (g_fg_large && !out_t && ((Nf + L_BN - 1) / L_BN) % 4 == 0 && M >= L_BM) {
+  if (!out_t && ((Nf + L_BN - 1) / L_BN) % 4 == 0 && M >= L_BM) {
     if (out_dtype == SL_F32)
       return launch_large<ALO, WLO, EPI, float>(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, sc, sh, outscale,
                                                  (float*)out, ldo, s, rt, p0);
@@ -671,12 +665,6 @@ SL_API int sl_feature_gemm(const bf16_t* Ahi, const bf16_t* Alo, int64_t M, int6
                            void* out, int out_dtype, int64_t ldo, int out_t, void* stream) {
   return sl_feature_gemm2(Ahi, Alo, M, K, lda, Whi, Wlo, Nf, ldw, scales, shifts, outscale, epi, out, out_dtype, ldo,
                           out_t, nullptr, 0.f, stream);
-}
-
-// tuning / testing hook: 1 = large-tile variant where it applies (default), 0 = 128 x 128 only
-SL_API int sl_fg_set_large(int on) {
-  g_fg_large = on ? 1 : 0;
-  return SL_OK;
 }
 
 // hi / lo planes of width wpad (zero padded past K) with row stride ldp >= wpad

@@ -250,14 +250,8 @@ SL_API int sl_hash_csr_colwise2(const int64_t* rowptr, const void* col, int idx3
   int64_t CW = m < cwmax ? m : cwmax;
   dim3 grid((unsigned)((m + CW - 1) / CW), (unsigned)S);
   size_t lds = (size_t)CW * esz;
-  static int urows = -1;   // rows in flight per lane group (SL_CWT_U: 4, 8 or 16; tuning)
-  if (urows < 0) {
-    const char* e = getenv("SL_CWT_U");
-    urows = e ? atoi(e) : 8;
-  }
 #define SL_CSR_U(IT, VT, G, DET, U) k_hash_csr_col<IT, VT, G, U, DET><<<grid, 512, lds, s>>>(rowptr, (const IT*)col, (const VT*)vals, perm, bptr, (const VT*)pval, (VT*)out, ldo, m, CW, row_offset, vmax, wmax)
-#define SL_CSR(IT, VT, G, DET) \
-  { if (urows >= 16) SL_CSR_U(IT, VT, G, DET, 16); else if (urows >= 8) SL_CSR_U(IT, VT, G, DET, 8); else SL_CSR_U(IT, VT, G, DET, 4); }
+#define SL_CSR(IT, VT, G, DET) SL_CSR_U(IT, VT, G, DET, 8)   /* 8 rows in flight per lane group */
 #define SL_CSR_G(IT, VT, DET)                              \
   switch (group) {                                         \
     case 1: SL_CSR(IT, VT, 1, DET); break;                 \

@@ -88,8 +88,6 @@ __global__ void __launch_bounds__(256) k_fill_normal_lines(T* __restrict__ out, 
   }
 }
 
-static int g_fast_lines = 1;   // 0: always the generic kernel (A/B tests)
-SL_API void sl_rng_set_fast_lines(int on) { g_fast_lines = on; }
 
 // precise != 0 forces the double-precision sampler for fp32/bf16 outputs.
 SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_t base,
@@ -100,7 +98,7 @@ SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_
   FillArgs a{dist, seed, base, rows, cols, sr, sc, r0, c0, ir, ic, p0, p1, scale};
   unsigned grid = sl_grid_for((size_t)(rows * cols), 256, 4096);
   hipStream_t s = (hipStream_t)stream;
-  if (g_fast_lines && dist == sl::DIST_NORMAL && !precise && (dtype == SL_F32 || dtype == SL_BF16) && (sc == 1 || sr == 1)) {
+  if (dist == sl::DIST_NORMAL && !precise && (dtype == SL_F32 || dtype == SL_BF16) && (sc == 1 || sr == 1)) {
     // lines = the slow dimension, fast = the contiguous one
     const bool rowmajor = sc == 1 && (sr != 1 || cols >= rows);
     const int64_t nlines = rowmajor ? rows : cols, nfast = rowmajor ? cols : rows;

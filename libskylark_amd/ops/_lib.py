@@ -35,7 +35,6 @@ SIGNATURES = {
     "sl_fastfood_perms_host": [vp, u64, u64, i64, i64],
     "sl_last_error": [],
     "sl_fill_random": [vp, i32, i32, u64, u64, i64, i64, i64, i64, i64, i64, i64, i64, f64, f64, f64, i32, vp],
-    "sl_rng_set_fast_lines": [i32],
     "sl_fill_random_host": [vp, i32, i32, u64, u64, i64, i64, i64, i64, i64, i64, i64, i64, f64, f64, f64, i32],
     "sl_random_int": [vp, u64, u64, i64, i64, i64, vp],
     "sl_random_int_host": [vp, u64, u64, i64, i64, i64],

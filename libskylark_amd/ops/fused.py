@@ -145,11 +145,8 @@ def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=No
 
 # rowwise linear / cosine maps on the 256 x 256 NT GEMM (gemm_nt.hip) with
 # the hi / lo terms concatenated along K (one launch, no per-term passes)
-USE_GEMM_NT = os.environ.get("SL_FEATURE_GEMM_NT", "1") == "1"
-
-
 def _gemm_nt_ok(X):
-    return USE_GEMM_NT and X.stride(1) == 1 and X.dtype in (torch.float32, torch.bfloat16)
+    return X.stride(1) == 1 and X.dtype in (torch.float32, torch.bfloat16)
 
 
 def _feature_gemm_nt(X, W, scales, shifts, outscale, epi, out_dtype, use_lo):

@@ -58,8 +58,7 @@ def test_feature_gemm_matches_fp64(dev, adt, dim, epi):
 @pytest.mark.parametrize("epi", [F.EPI_NONE, F.EPI_COS])
 def test_feature_gemm_large_tiles_match_fp64(dev, adt, shape, epi):
     """256 x 128-tile LDS-DMA variant (row-major output, feature tiles in
-    multiples of 4 x 128): ragged rows / features / K against fp64, and equal
-    to the 128 x 128 kernel's result (SL_FG_LARGE=0 path) up to summation order."""
+    multiples of 4 x 128): ragged rows / features / K against fp64, ."""
     torch.manual_seed(3)
     M, K, NF = shape
     A = torch.randn(M, K)
@@ -74,17 +73,6 @@ def test_feature_gemm_large_tiles_match_fp64(dev, adt, shape, epi):
     mag = Ad.double().cpu().abs() @ W.abs().double().t()
     tol = 4e-5 * float(mag.max()) + 2e-6
     assert (out.double().cpu() - ref).abs().max().item() < tol
-    import ctypes
-    from libskylark_amd.ops import _lib
-    lib = _lib.require()
-    # same launch through the 128 x 128 kernel
-    try:
-        lib.sl_fg_set_large.argtypes = [ctypes.c_int]
-        lib.sl_fg_set_large(0)
-        out_small = F.feature_gemm(Ad, Wd, 1, **kw)
-    finally:
-        lib.sl_fg_set_large(1)
-    assert (out.double().cpu() - out_small.double().cpu()).abs().max().item() < tol
 
 
 def test_feature_gemm_transposed_view_and_unaligned(dev):

@@ -8,19 +8,8 @@ from libskylark_amd.ops import small_la as SL
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["auto", "lds", "rolled", "wave", "lds1b", "aug"])
-def impl(request):
-    import ctypes
-    from libskylark_amd.ops import _lib
-    lib = _lib.require()
-    lib.sl_small_chol_impl.argtypes = [ctypes.c_int]
-    lib.sl_small_chol_impl(request.param)
-    yield request.param
-    lib.sl_small_chol_impl(0)
-
-
 @pytest.mark.parametrize("k", [1, 7, 16, 17, 33, 40, 48, 64])
-def test_chol_inv(dev, k, impl):
+def test_chol_inv(dev, k):
     X = torch.randn(3 * k + 5, k, dtype=torch.float64)
     G = X.t() @ X
     st = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -66,7 +55,7 @@ def test_chol_inv_wave_drops_dependent_direction(dev):
     torch.testing.assert_close(Q[:, keep].t() @ Q[:, keep], torch.eye(k - 1, dtype=torch.float64), atol=1e-8, rtol=0)
 
 
-def test_chol_inv_flags_breakdown(dev, impl):
+def test_chol_inv_flags_breakdown(dev):
     G = torch.zeros(5, 5, dtype=torch.float64, device=dev)
     G[0, 0] = 1
     st = torch.zeros(1, dtype=torch.int32, device=dev)
