@@ -1,0 +1,81 @@
+"""General-precision device randSVD engine (rsvd_general.hip) at the
+reference's precisions and sizes: 1e6 x 1000 f32 and
+2e5 x 5000 f64, plus k = 128 -- the whole call on the device (rocBLAS passes,
+one-wave / rocSOLVER small algebra, f64 core), timed with HIP events over
+repeated cold calls (a fresh sketch seed per call).  Prints one JSON line per
+case: ms per call, effective HBM traffic of the passes (2 (q + 1) reads of A),
+and the relative error of the leading singular values against a reference
+(dense SVD of the planted factors, exact by construction).
+
+Reference: nla/svd.hpp:222-318 (ApproximateSVD), :71-149 (power iteration)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import libskylark_amd as sk  # noqa: E402
+from libskylark_amd.nla import svd as S  # noqa: E402
+
+
+def planted(m, n, r, dtype, dev, seed=0):
+    """A = U diag(s) V^T + tiny noise, built on the device panel by panel."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    U, _ = torch.linalg.qr(torch.randn(m, r, device=dev, dtype=torch.float64, generator=g))
+    V, _ = torch.linalg.qr(torch.randn(n, r, device=dev, dtype=torch.float64, generator=g))
+    s = 100.0 * 0.85 ** torch.arange(r, device=dev, dtype=torch.float64)
+    A = torch.empty(m, n, device=dev, dtype=dtype)
+    step = max(1, (1 << 27) // n)
+    for i in range(0, m, step):
+        blk = (U[i:i + step] * s) @ V.t()
+        blk += 1e-6 * torch.randn(blk.shape, device=dev, dtype=torch.float64, generator=g)
+        A[i:i + step] = blk.to(dtype)
+    return A, s
+
+
+def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
+    dev = torch.device("cuda")
+    A, s_true = planted(m, n, max(2 * rank, 32), dtype, dev)
+    prm = sk.nla.ApproximateSVDParams(num_iterations=q, sketch=sketch)
+    ctx = sk.Context(seed=11)
+    U, s, V = sk.nla.approximate_svd(A, rank, ctx, prm)       # plan + first call
+    torch.cuda.synchronize()
+    plan = [p for p in S._PLANS.values() if p.Aref() is A][0]
+    times = []
+    for i in range(reps):
+        ctx = sk.Context(seed=1000 + i)                         # cold: a new sketch every call
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        U, s, V = sk.nla.approximate_svd(A, rank, ctx, prm)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    times.sort()
+    ms = times[len(times) // 2]
+    es = A.element_size()
+    bytes_passes = 2 * (q + 1) * m * n * es
+    err = float(((s.double() - s_true[:rank]).abs() / s_true[:rank]).max())
+    k = max(rank, min(n, 2 * rank))
+    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}",
+           "engine": type(plan).__name__, "ms": round(ms, 3), "ms_min": round(times[0], 3),
+           "pass_traffic_GBps": round(bytes_passes / (ms * 1e-3) / 1e9, 1), "max_rel_err_s": err}
+    print(json.dumps(out), flush=True)
+    del A, U, V
+    S._PLANS.clear()
+    torch.cuda.empty_cache()
+
+
+def main():
+    run(1_000_000, 1000, 20, 2, torch.float32)
+    run(200_000, 5000, 20, 2, torch.float64)
+    run(200_000, 5000, 64, 1, torch.float64)            # k = 128: rocSOLVER small algebra
+    run(1_000_000, 1000, 20, 2, torch.bfloat16)         # n <= 1024 bf16: the fused engine, for comparison
+
+
+if __name__ == "__main__":
+    main()

@@ -27,6 +27,8 @@
 // factorisation + a DPP back-transform over all waves.  Every call solves
 // its core from scratch; cyclic Jacobi (jacobi() below) is kept as the
 // fallback for numerically repeated eigenvalues.
+#include <string>
+
 #include "sl_common.hpp"
 #include "sl_rng.hpp"
 #include "sl_wave_la.hpp"
@@ -964,6 +966,45 @@ int launch_bnd(bool fin, unsigned nb, const BndArgs& a, hipStream_t s) {
   return SL_OK;
 }
 }  // namespace
+
+namespace {
+template <int K>
+int bnd_capacity(int* cap) {
+  int per_cu_f = 0, per_cu_i = 0, dev = 0, cus = 0;
+  SL_LDS_ATTR((k_boundary<true, K>), (int)BND_LDS);
+  SL_LDS_ATTR((k_boundary<false, K>), (int)BND_LDS);
+  SL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_f, k_boundary<true, K>, NT, BND_LDS));
+  SL_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_i, k_boundary<false, K>, NT, BND_LDS));
+  SL_HIP_CHECK(hipGetDevice(&dev));
+  SL_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  *cap = std::min(per_cu_f, per_cu_i) * cus;
+  return SL_OK;
+}
+}  // namespace
+
+// Co-residency of the pass-boundary grid: k_boundary's workgroups wait on
+// each other (a generation word), so every one of them must be resident at
+// once.  The plan checks at creation that the device holds the whole grid
+// (the FINAL launch has the most workgroups) with nothing else running; a
+// concurrent kernel that still starves one of them is caught by the bounded
+// wait (status bit 16, raised on that call).  *ok = 1 when it fits.
+SL_API int sl_rsvd_bnd_coresident(int n, int k, int* ok) {
+  *ok = 0;
+  if (k < 1 || k > BK || n < 16 || n > BMAX * BR) {
+    sl_set_last_error("rsvd_boundary: needs 1 <= k <= 48, 16 <= n <= 1024");
+    return SL_ERR_UNSUPPORTED;
+  }
+  int cap = 0;
+  const int rc = k <= 16 ? bnd_capacity<16>(&cap) : k <= 32 ? bnd_capacity<32>(&cap)
+               : k <= 40 ? bnd_capacity<40>(&cap) : bnd_capacity<48>(&cap);
+  if (rc != SL_OK) return rc;
+  const int need = (n + BR - 1) / BR + 1;
+  *ok = cap >= need ? 1 : 0;
+  if (!*ok)
+    sl_set_last_error(("rsvd_boundary: " + std::to_string(need) + " workgroups must be co-resident, the device holds " +
+                       std::to_string(cap)).c_str());
+  return SL_OK;
+}
 
 // One pass boundary on the reduced (and, on several ranks, all-reduced)
 // [W (n x k); Gy (k x k)] f64 buffer WG.

@@ -40,6 +40,7 @@ SL_API int sl_rsvd_make_v_ind(const double* W, int n, int k, int ldw, const doub
                               float* const* optr, void* stream);
 SL_API int sl_rsvd_set_ptrs(float** tab, float* a, float* b, float* c, void* stream);
 SL_API int64_t sl_rsvd_bnd_workspace(int k);
+SL_API int sl_rsvd_bnd_coresident(int n, int k, int* ok);
 SL_API int sl_rsvd_bnd_set_fault(const void* bws, int missing, uint64_t bound_ticks);
 SL_API int sl_rsvd_boundary(int final_, int n, int k, int r, double* WG, void* bws, int* status, int status_or,
                             double* Rinv, void* Zt, float* M, double* N, double* s64, int* mirror, float* V,
@@ -201,6 +202,13 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   if (m < 1 || n < 16 || n > 1024 || n % 8 || lda % 8 || k < 1 || k > 48 || r < 1 || r > k || q < 0) {
     sl_set_last_error("rsvd_plan: needs m >= 1, 16 <= n <= 1024, n % 8 == 0, lda % 8 == 0, 1 <= r <= k <= 48, q >= 0");
     return SL_ERR_UNSUPPORTED;
+  }
+  {
+    // the boundary grid spins on itself: refuse a plan whose grid cannot be co-resident
+    int ok = 0;
+    const int rc = sl_rsvd_bnd_coresident((int)n, k, &ok);
+    if (rc != SL_OK) return rc;
+    if (!ok) return SL_ERR_UNSUPPORTED;
   }
   Plan* p = new (std::nothrow) Plan();
   if (!p) return SL_ERR_GENERIC;

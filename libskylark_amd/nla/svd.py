@@ -38,7 +38,7 @@ from scipy.linalg import solve_triangular
 
 from ..base import linalg as L
 from ..base.context import Context
-from ..base.exceptions import InvalidParametersError
+from ..base.exceptions import InvalidParametersError, SkylarkError
 from ..parallel.comm import Comm
 from ..parallel.distmatrix import DistMatrix
 from ..utils.timer import PROFILER
@@ -643,9 +643,15 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     if plan is None:
         if len(_PLANS) >= 4:
             _PLANS.pop(next(iter(_PLANS)))
+        plan = None
         if fused:
-            plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
-        else:
+            try:
+                plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
+            except (RuntimeError, SkylarkError):
+                # e.g. the boundary grid cannot be co-resident on this device
+                if not _gen_ok(A_loc, n, k):
+                    raise
+        if plan is None:
             plan = _GenPlan(A_loc, comm, n, rank, k, q)
         _PLANS[key] = plan
     out = plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
