@@ -24,29 +24,57 @@ def timeit(fn, reps=5):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
-def case(name, M, N, K, out_dtype=torch.float32, cos=False):
+def set_variant(v):
+    import ctypes
+    from libskylark_amd.ops import _lib
+    fn = getattr(_lib.require(), "sl_gemm_nt_variant", None)
+    if fn is not None:
+        fn.argtypes = [ctypes.c_int]
+        fn(v)
+    return fn is not None
+
+
+def case(name, M, N, K, out_dtype=torch.float32, cos=False, variants=(0, 4, 5)):
     A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
     C = torch.empty(M, N, device="cuda", dtype=out_dtype)
     sc = torch.rand(N, device="cuda") if cos else None
     sh = torch.rand(N, device="cuda") if cos else None
-    ours = timeit(lambda: gemm.gemm_nt(A, B, out=C, cos_scales=sc, cos_shifts=sh))
+    ours = {}
+    outs = {}
+    for v in variants:
+        if v and not set_variant(v):
+            continue
+        set_variant(v)
+        ours[v] = timeit(lambda: gemm.gemm_nt(A, B, out=C, cos_scales=sc, cos_shifts=sh))
+        if M * N <= 1 << 27:
+            outs[v] = C.float().clone()
+    set_variant(0)
     Bt = B.t()
     if out_dtype == torch.float32:
         lib = timeit(lambda: torch.mm(A, Bt, out_dtype=torch.float32))
     else:
         lib = timeit(lambda: torch.mm(A, Bt))
-    err = None
-    if M * N <= 1 << 26:
-        ref = A.float() @ B.float().t()
-        if cos:
-            ref = torch.cos(ref * sc + sh)
-        err = float((C.float() - ref).abs().max() / ref.abs().max())
+    errs = {}
+    if outs:
+        if out_dtype == torch.float32 and not cos:
+            ref = torch.mm(A, Bt, out_dtype=torch.float32)
+        else:
+            ref = A.float() @ B.float().t() if M * N <= 1 << 26 else None
+            if ref is not None and cos:
+                ref = torch.cos(ref * sc + sh)
+        if ref is not None:
+            for v, o in outs.items():
+                errs[v] = float((o - ref).abs().max() / ref.abs().max())
     fl = 2.0 * M * N * K
-    print(json.dumps({"case": name, "M": M, "N": N, "K": K, "out": str(out_dtype).split(".")[-1], "cos": cos,
-                      "ours_ms": round(ours, 3), "ours_TF": round(fl / ours / 1e9, 1),
-                      "hipblaslt_ms": round(lib, 3), "hipblaslt_TF": round(fl / lib / 1e9, 1),
-                      "rel_err": err}), flush=True)
+    rec = {"case": name, "M": M, "N": N, "K": K, "out": str(out_dtype).split(".")[-1], "cos": cos,
+           "hipblaslt_ms": round(lib, 3), "hipblaslt_TF": round(fl / lib / 1e9, 1)}
+    for v, ms in ours.items():
+        tag = "v1" if v == 0 else f"v2ring{v}"
+        rec[f"{tag}_ms"] = round(ms, 3)
+        rec[f"{tag}_TF"] = round(fl / ms / 1e9, 1)
+        rec[f"{tag}_rel_err"] = errs.get(v)
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
