@@ -24,32 +24,14 @@ def timeit(fn, reps=5):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
-def set_variant(v):
-    import ctypes
-    from libskylark_amd.ops import _lib
-    fn = getattr(_lib.require(), "sl_gemm_nt_variant", None)
-    if fn is not None:
-        fn.argtypes = [ctypes.c_int]
-        fn(v)
-    return fn is not None
-
-
-def case(name, M, N, K, out_dtype=torch.float32, cos=False, variants=(0, 4, 5)):
+def case(name, M, N, K, out_dtype=torch.float32, cos=False):
     A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
     C = torch.empty(M, N, device="cuda", dtype=out_dtype)
     sc = torch.rand(N, device="cuda") if cos else None
     sh = torch.rand(N, device="cuda") if cos else None
-    ours = {}
-    outs = {}
-    for v in variants:
-        if v and not set_variant(v):
-            continue
-        set_variant(v)
-        ours[v] = timeit(lambda: gemm.gemm_nt(A, B, out=C, cos_scales=sc, cos_shifts=sh))
-        if M * N <= 1 << 27:
-            outs[v] = C.float().clone()
-    set_variant(0)
+    ours = {0: timeit(lambda: gemm.gemm_nt(A, B, out=C, cos_scales=sc, cos_shifts=sh))}
+    outs = {0: C.float().clone()} if M * N <= 1 << 27 else {}
     Bt = B.t()
     if out_dtype == torch.float32:
         lib = timeit(lambda: torch.mm(A, Bt, out_dtype=torch.float32))
@@ -70,7 +52,7 @@ def case(name, M, N, K, out_dtype=torch.float32, cos=False, variants=(0, 4, 5)):
     rec = {"case": name, "M": M, "N": N, "K": K, "out": str(out_dtype).split(".")[-1], "cos": cos,
            "hipblaslt_ms": round(lib, 3), "hipblaslt_TF": round(fl / lib / 1e9, 1)}
     for v, ms in ours.items():
-        tag = "v1" if v == 0 else f"v2ring{v}"
+        tag = "ours"
         rec[f"{tag}_ms"] = round(ms, 3)
         rec[f"{tag}_TF"] = round(fl / ms / 1e9, 1)
         rec[f"{tag}_rel_err"] = errs.get(v)

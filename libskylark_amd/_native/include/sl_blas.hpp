@@ -9,11 +9,12 @@ bool slb_solver_available();
 // SL_BF16 (bf16 A and B, f32 C and accumulation)
 int slb_gemm(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha, const void* A, int64_t lda,
              const void* B, int64_t ldb, double beta, void* C, int64_t ldc, hipStream_t s);
+// batched row-major products, element strides between batches (SL_F32 / SL_F64)
+int slb_gemm_strided(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha, const void* A,
+                     int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB, double beta, void* C, int64_t ldc,
+                     int64_t sC, int batch, hipStream_t s);
 // eigenvectors of the row-major symmetric A in its rows, eigenvalues ascending
 int slb_dsyevd(int n, double* A, int lda, double* D, double* E, int* info, hipStream_t s);
-// row-major G = R^T R: R^{-1} (lower triangle of the column-major storage =
-// upper of the row-major one) in place; info[0] potrf, info[1] trtri
-int slb_dpotrf_inv(int n, double* G, int ldg, int* info, hipStream_t s);
 
 // column-major LAPACK-style helpers (C API host-operand NLA paths)
 int slb_dgeqrf_cm(int m, int n, double* A, int lda, double* tau, hipStream_t s);

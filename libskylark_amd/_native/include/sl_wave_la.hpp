@@ -426,7 +426,7 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     const double l = lam[t];
     const double gap = fmin(t > 0 ? lam[t - 1] - l : 1e300, t + 1 < nt ? l - lam[t + 1] : 1e300);
     if (!(gap > 1e-13)) atomicOr(st, 1);       // numerically repeated (~ bisection accuracy): the caller falls back
-    if (gap < 1e-3) atomicOr(&s_clus, 1);
+    if (gap < 1e-2) atomicOr(&s_clus, 1);
     const double pivmin = 1e-290;
     double* zdm = sc + t * LZ;
     double* zdp = sc + (nv + t) * LZ;
@@ -501,7 +501,7 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
       double xc = i < K ? sc[t * LZ + i] : 0.0;
       bool touched = false;
       for (int u = 0; u < t; ++u) {
-        if (lam[u] - lam[t] >= 1e-3) continue;
+        if (lam[u] - lam[t] >= 1e-2) continue;
         const double dt = wave_sum(i < K ? sc[u * LZ + i] * xc : 0.0);
         xc -= dt * (i < K ? sc[u * LZ + i] : 0.0);
         touched = true;

@@ -22,6 +22,7 @@
 // are f64 whatever A's precision.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <new>
 #include <type_traits>
@@ -96,11 +97,15 @@ __global__ void __launch_bounds__(256) k_split_bf16(const float* __restrict__ y,
   }
 }
 
-// zero the strictly lower triangle of a row-major k x k (rocSOLVER leaves G there)
-__global__ void __launch_bounds__(256) k_triu(double* __restrict__ X, int k) {
-  for (int e = threadIdx.x; e < k * k; e += 256) {
-    const int i = e / k, c = e - i * k;
-    if (c < i) X[e] = 0.0;
+// out (f64, tot) = sum of np slabs (stride tot) of T; zero_word cleared when given
+template <typename T>
+__global__ void __launch_bounds__(256) k_sum_parts(const T* __restrict__ parts, int np, int64_t tot,
+                                                   double* __restrict__ out, int* zero_word) {
+  if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    double acc = 0.0;
+    for (int p_ = 0; p_ < np; ++p_) acc += (double)parts[(int64_t)p_ * tot + e];
+    out[e] = acc;
   }
 }
 
@@ -168,6 +173,9 @@ struct GPlan {
   void* Md = nullptr;      // k x r (dt of U)
   double* Vf = nullptr;    // n x r
   void* gws = nullptr;     // f32 Gram workspace
+  void* parts = nullptr;   // f32 / f64 A: per-row-chunk partials of A^T Y (np + 1 slabs of n x k, dt)
+  int np = 0;              // row chunks of ch rows (+ one for the remainder)
+  int64_t ch = 0;
   int* st = nullptr;       // [0] status, [1..2] eig status, [4..11] chol statuses / infos
   // sketch of the call
   int sk = 0;              // 0 none, 1 FJLT, 2 dense
@@ -189,12 +197,39 @@ unsigned grid_of(int64_t tot) {
 }
 
 // X = R^{-1} of the SPD k x k G (row-major f64), status bit ST_PIVOT via st
+// X (row-major k x k) = V diag(lambda^{-1/2}) from G = V diag(lambda) V^T
+// (eigenvectors in the rows of Vt, ascending), directions with lambda at or
+// below 1e-13 max lambda dropped (zero columns; status bit 1): X^T G X = I
+// on the retained subspace -- the rank-revealing counterpart of the one-wave
+// kernel's pivot dropping.
+__global__ void __launch_bounds__(256) k_whiten(const double* __restrict__ Vt, const double* __restrict__ D, int k,
+                                                double* __restrict__ X, int* __restrict__ st) {
+  __shared__ double scale[128];
+  const double lmax = D[k - 1];
+  for (int j = threadIdx.x; j < k; j += 256) {
+    const double l = D[j];
+    const bool keep = l > 1e-13 * lmax && lmax > 0.0;
+    scale[j] = keep ? 1.0 / sqrt(l) : 0.0;
+    if (!keep) atomicOr(st, 1);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < k * k; e += 256) {
+    const int i = e / k, j = e % k;
+    X[e] = Vt[(int64_t)j * k + i] * scale[j];
+  }
+}
+
 int chol_inv(GPlan* p, const double* G, double* X, int* st, hipStream_t s) {
   if (p->k <= 64) return sl_chol_inv_wave(G, p->k, p->k, X, st, s);
-  SL_HIP_CHECK(hipMemcpyAsync(X, G, (size_t)p->k * p->k * 8, hipMemcpyDeviceToDevice, s));
-  int rc = slb_dpotrf_inv(p->k, X, p->k, st, s);
+  // k > 64: eigen-whitening on rocSOLVER (a Cholesky of a numerically
+  // rank-deficient Gram breaks down; the whitening drops those directions)
+  const int k = p->k;
+  double* T = (double*)p->gws;                 // k x k eigenvectors (reuses the Gram workspace)
+  double* D = p->eig + k * p->r + p->r;         // k eigenvalues + k scratch (the core's syevd region)
+  SL_HIP_CHECK(hipMemcpyAsync(T, G, (size_t)k * k * 8, hipMemcpyDeviceToDevice, s));
+  int rc = slb_dsyevd(k, T, k, D, D + k, st + 1, s);
   if (rc != SL_OK) return rc;
-  k_triu<<<1, 256, 0, s>>>(X, p->k);
+  k_whiten<<<1, 256, 0, s>>>(T, D, k, X, st);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -244,8 +279,60 @@ int pass(GPlan* p, const void* A, bool final_pass, bool first, hipStream_t s) {
   } else {
     rc = slb_gemm(p->dt, false, false, m, k, n, 1.0, A, p->lda, p->Z, k, 0.0, p->Y, k, s);
     if (rc != SL_OK) return rc;
-    rc = slb_gemm(p->dt, true, false, n, k, m, 1.0, A, p->lda, p->Y, k, 0.0, p->Wt, k, s);
+    // W = A^T Y as np row-chunk products (one strided-batched launch fills the
+    // chip; a single K = m product runs on a handful of workgroups), then one
+    // f64 sum of the partial slabs straight into WG
+    const size_t es = p->dt == SL_F64 ? 8 : 4;
+    const int64_t tot = n * k;
+    rc = slb_gemm_strided(p->dt, true, false, n, k, p->ch, 1.0, A, p->lda, p->ch * p->lda, p->Y, k, p->ch * k, 0.0,
+                          p->parts, k, tot, p->np, s);
     if (rc != SL_OK) return rc;
+    const int64_t r0 = p->ch * p->np;
+    int nparts = p->np;
+    if (r0 < m) {
+      rc = slb_gemm(p->dt, true, false, n, k, m - r0, 1.0, (const char*)A + r0 * p->lda * es, p->lda,
+                    (const char*)p->Y + r0 * k * es, k, 0.0, (char*)p->parts + (int64_t)p->np * tot * es, k, s);
+      if (rc != SL_OK) return rc;
+      ++nparts;
+    }
+    rc = dispatch_dt(p->dt, [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      k_sum_parts<T><<<grid_of(tot), 256, 0, s>>>((const T*)p->parts, nparts, tot, p->WG, first ? p->st : nullptr);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    });
+    if (rc != SL_OK || !final_pass) return rc;
+    if (p->dt == SL_F64) {
+      // G = Y^T Y the same way (k x k slabs in the same workspace)
+      double* G = p->WG + n * k;
+      const int64_t tg = (int64_t)k * k;
+      rc = slb_gemm_strided(SL_F64, true, false, k, k, p->ch, 1.0, p->Y, k, p->ch * k, p->Y, k, p->ch * k, 0.0,
+                            p->parts, k, tg, p->np, s);
+      if (rc != SL_OK) return rc;
+      if (r0 < m) {
+        rc = slb_gemm(SL_F64, true, false, k, k, m - r0, 1.0, (const double*)p->Y + r0 * k, k,
+                      (const double*)p->Y + r0 * k, k, 0.0, (double*)p->parts + (int64_t)p->np * tg, k, s);
+        if (rc != SL_OK) return rc;
+      }
+      k_sum_parts<double><<<grid_of(tg), 256, 0, s>>>((const double*)p->parts, nparts, tg, G, nullptr);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    }
+  }
+  if (p->dt != SL_BF16) {
+    // f32 Y: the fp64 Gram below
+    double* G = p->WG + n * k;
+    if (k <= 64) return sl_tsk_gram64((const float*)p->Y, m, k, k, G, p->gws, s);
+    SL_HIP_CHECK(hipMemsetAsync(G, 0, (size_t)k * k * 8, s));
+    for (int64_t q0 = 0; q0 < m; q0 += GPIECE) {
+      const int64_t rows = (m - q0 < GPIECE) ? m - q0 : GPIECE;
+      k_cast2d<float, double><<<grid_of(rows * k), 256, 0, s>>>((const float*)p->Y + q0 * k, k, rows, k,
+                                                                 (double*)p->gws, k, nullptr);
+      SL_LAUNCH_CHECK();
+      rc = slb_gemm(SL_F64, true, false, k, k, rows, 1.0, p->gws, k, p->gws, k, 1.0, G, k, s);
+      if (rc != SL_OK) return rc;
+    }
+    return SL_OK;
   }
   const int wdt = p->dt == SL_BF16 ? SL_F32 : p->dt;
   rc = dispatch_dt(wdt, [&](auto* tag) {
@@ -408,7 +495,17 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   const int64_t o_md = off;  off = align256(off + (int64_t)k * r * 8);
   const int64_t o_vf = off;  off = align256(off + n * r * 8);
   const int64_t o_gw = off;
-  off = align256(off + (k <= 64 ? sl_tsk_gram64_workspace(m, k) : (dt == SL_F32 ? GPIECE * k * 8 : 256)));
+  off = align256(off + (k <= 64 ? sl_tsk_gram64_workspace(m, k)
+                                 : std::max<int64_t>(dt == SL_F32 ? GPIECE * k * 8 : 0, (int64_t)k * k * 8)));
+  // f32 / f64 A: row-chunk partials of A^T Y (and of Y^T Y), <= 64 MB of slabs
+  int np = 0;
+  int64_t ch = 0;
+  if (dt != SL_BF16) {
+    const int64_t slab = std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es;
+    np = (int)std::max<int64_t>(1, std::min<int64_t>({128, (int64_t(64) << 20) / slab, m / 512}));
+    ch = m / np;
+  }
+  const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
   const int64_t o_st = off;  off = align256(off + 64 * 4);
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;
@@ -421,6 +518,9 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   p->T1 = (double*)(b + o_t1); p->Cc = (double*)(b + o_c); p->eig = (double*)(b + o_e); p->M = (double*)(b + o_m);
   p->N = (double*)(b + o_n); p->Md = b + o_md; p->Vf = (double*)(b + o_vf); p->gws = b + o_gw;
   p->st = (int*)(b + o_st);
+  p->parts = b + o_pt;
+  p->np = np;
+  p->ch = ch;
   if (hipMemset(p->st, 0, 64 * 4) != hipSuccess) {
     (void)hipFree(p->base);
     delete p;

@@ -27,7 +27,6 @@ struct Blas {
   int (*gemm_ex)(void*, int, int, int, int, int, const void*, const void*, int, int, const void*, int, int,
                  const void*, const void*, int, int, void*, int, int, int, int, int, uint32_t) = nullptr;
   int (*dsyevd)(void*, int, int, int, double*, int, double*, double*, int*) = nullptr;
-  int (*dpotrf)(void*, int, int, double*, int, int*) = nullptr;
   int (*dtrtri)(void*, int, int, int, double*, int, int*) = nullptr;
   int (*dgeqrf)(void*, int, int, double*, int, double*) = nullptr;
   int (*dorgqr)(void*, int, int, int, double*, int, double*) = nullptr;
@@ -36,6 +35,10 @@ struct Blas {
   int (*dgemv)(void*, int, int, int, const double*, const double*, int, const double*, int, const double*, double*,
                int) = nullptr;
   int (*dnrm2)(void*, int, const double*, int, double*) = nullptr;
+  int (*dgemm_sb)(void*, int, int, int, int, int, const double*, const double*, int, int64_t, const double*, int,
+                  int64_t, const double*, double*, int, int64_t, int) = nullptr;
+  int (*sgemm_sb)(void*, int, int, int, int, int, const float*, const float*, int, int64_t, const float*, int,
+                  int64_t, const float*, float*, int, int64_t, int) = nullptr;
   int (*dtrsv)(void*, int, int, int, int, const double*, int, double*, int) = nullptr;
   void* handle[64] = {};
 };
@@ -63,16 +66,17 @@ Blas& blas() {
   B.gemm_ex = (decltype(B.gemm_ex))sym(B.rb, "rocblas_gemm_ex");
   B.dgemv = (decltype(B.dgemv))sym(B.rb, "rocblas_dgemv");
   B.dnrm2 = (decltype(B.dnrm2))sym(B.rb, "rocblas_dnrm2");
+  B.dgemm_sb = (decltype(B.dgemm_sb))sym(B.rb, "rocblas_dgemm_strided_batched");
+  B.sgemm_sb = (decltype(B.sgemm_sb))sym(B.rb, "rocblas_sgemm_strided_batched");
   B.dtrsv = (decltype(B.dtrsv))sym(B.rb, "rocblas_dtrsv");
   if (B.rs) {
     B.dsyevd = (decltype(B.dsyevd))dlsym(B.rs, "rocsolver_dsyevd");
-    B.dpotrf = (decltype(B.dpotrf))dlsym(B.rs, "rocsolver_dpotrf");
     B.dtrtri = (decltype(B.dtrtri))dlsym(B.rs, "rocsolver_dtrtri");
     B.dgeqrf = (decltype(B.dgeqrf))dlsym(B.rs, "rocsolver_dgeqrf");
     B.dorgqr = (decltype(B.dorgqr))dlsym(B.rs, "rocsolver_dorgqr");
     B.dgesvd = (decltype(B.dgesvd))dlsym(B.rs, "rocsolver_dgesvd");
   }
-  B.ok = B.create && B.set_stream && B.dgemm && B.sgemm && B.gemm_ex && B.dgemv && B.dnrm2 && B.dtrsv;
+  B.ok = B.create && B.set_stream && B.dgemm && B.sgemm && B.gemm_ex && B.dgemv && B.dnrm2 && B.dtrsv && B.dgemm_sb && B.sgemm_sb;
   return B;
 }
 
@@ -109,7 +113,7 @@ int rc_of(int st, const char* what) {
 bool slb_available() { return blas().ok; }
 bool slb_solver_available() {
   Blas& B = blas();
-  return B.ok && B.dsyevd && B.dpotrf && B.dtrtri && B.dgeqrf && B.dorgqr && B.dgesvd;
+  return B.ok && B.dsyevd && B.dtrtri && B.dgeqrf && B.dorgqr && B.dgesvd;
 }
 
 // Row-major C (M x N, ldc) = alpha op(A) op(B) + beta C, as the column-major
@@ -138,6 +142,30 @@ int slb_gemm(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, double a
                          C, DT_F32, (int)ldc, C, DT_F32, (int)ldc, DT_F32, 0, 0, 0), "rocblas_gemm_ex");
 }
 
+// batch of row-major products C_b = alpha op(A_b) op(B_b) + beta C_b with
+// element strides sA / sB / sC between the operands of consecutive batches
+// (SL_F32 / SL_F64)
+int slb_gemm_strided(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha, const void* A,
+                     int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB, double beta, void* C, int64_t ldc,
+                     int64_t sC, int batch, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return SL_OK;
+  void* h = nullptr;
+  const int rc = handle(&h, s);
+  if (rc != SL_OK) return rc;
+  Blas& L = blas();
+  const int opA = ta ? OP_T : OP_N, opB = tb ? OP_T : OP_N;
+  if (dt == SL_F64) {
+    const double al = alpha, be = beta;
+    return rc_of(L.dgemm_sb(h, opB, opA, (int)N, (int)M, (int)K, &al, (const double*)B, (int)ldb, sB,
+                            (const double*)A, (int)lda, sA, &be, (double*)C, (int)ldc, sC, batch),
+                 "rocblas_dgemm_strided_batched");
+  }
+  const float al = (float)alpha, be = (float)beta;
+  return rc_of(L.sgemm_sb(h, opB, opA, (int)N, (int)M, (int)K, &al, (const float*)B, (int)ldb, sB, (const float*)A,
+                          (int)lda, sA, &be, (float*)C, (int)ldc, sC, batch),
+               "rocblas_sgemm_strided_batched");
+}
+
 // Symmetric eigendecomposition of the row-major n x n f64 A in place
 // (eigenvectors in A's ROWS on return: the column-major solver sees A^T = A
 // and returns column-major eigenvectors, i.e. row-major transposed); D
@@ -149,20 +177,6 @@ int slb_dsyevd(int n, double* A, int lda, double* D, double* E, int* info, hipSt
   Blas& L = blas();
   if (!L.dsyevd) { sl_set_last_error("librocsolver.so: rocsolver_dsyevd unavailable"); return SL_ERR_UNSUPPORTED; }
   return rc_of(L.dsyevd(h, 211 /* evect_original */, 122 /* fill_lower */, n, A, lda, D, E, info), "rocsolver_dsyevd");
-}
-
-// Upper Cholesky factor R of the row-major SPD n x n f64 G in place (lower
-// triangle of the column-major view = upper of the row-major one), then R^{-1}
-int slb_dpotrf_inv(int n, double* G, int ldg, int* info, hipStream_t s) {
-  void* h = nullptr;
-  const int rc = handle(&h, s);
-  if (rc != SL_OK) return rc;
-  Blas& L = blas();
-  if (!L.dpotrf || !L.dtrtri) { sl_set_last_error("librocsolver.so unavailable"); return SL_ERR_UNSUPPORTED; }
-  // row-major upper R (G = R^T R) is the column-major lower L = R^T (G = L L^T)
-  int r1 = rc_of(L.dpotrf(h, 122 /* lower */, n, G, ldg, info), "rocsolver_dpotrf");
-  if (r1 != SL_OK) return r1;
-  return rc_of(L.dtrtri(h, 122, 131 /* non-unit */, n, G, ldg, info + 1), "rocsolver_dtrtri");
 }
 
 // ---------------------------------------------------------------- column-major

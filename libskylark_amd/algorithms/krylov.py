@@ -499,6 +499,7 @@ def _cg_native(op, Bv, X, Rr, params, M, tol, flexible: bool):
                 break
     else:
         _log(params, f"{name}: No convergence within iteration limit.")
+    params.iterations = itn + 1 if params.iter_lim > 0 else 0   # iterations run (reporting)
     return X, code
 
 

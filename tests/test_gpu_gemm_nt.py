@@ -9,24 +9,6 @@ from libskylark_amd.ops import gemm
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 4, 5], ids=["v1", "v2ring4", "v2ring5"], autouse=True)
-def variant(request):
-    """every test on both pipelines (sl_gemm_nt_variant: A/B hook)"""
-    import ctypes
-    from libskylark_amd.ops import _lib
-    lib = _lib.require()
-    fn = getattr(lib, "sl_gemm_nt_variant", None)
-    if fn is None:
-        if request.param:
-            pytest.skip("no v2 pipeline in this build")
-        yield request.param
-        return
-    fn.argtypes = [ctypes.c_int]
-    fn(request.param)
-    yield request.param
-    fn(0)
-
-
 def _ops(M, N, K, seed):
     g = torch.Generator(device="cuda").manual_seed(seed)
     A = torch.randn(M, K, device="cuda", generator=g).bfloat16()
