@@ -53,8 +53,6 @@ SL_API int sl_rsvd_fjlt_zt(uint64_t seed, uint64_t baseD, uint64_t baseS, double
                            void* stream);
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
                          int64_t ldo, double* G, void* ws, void* stream);
-SL_API int64_t sl_tsk_gram64_workspace(int64_t m, int k);
-SL_API int sl_tsk_gram64(const float* Y, int64_t m, int k, int64_t ldy, double* G, void* ws, void* stream);
 SL_API int sl_rsvd_zt_from_f64(const double* src, int64_t count, void* Zt, void* stream);
 SL_API int sl_fill_random(void* out, int dtype, int dist, uint64_t seed, uint64_t base, int64_t rows, int64_t cols,
                           int64_t sr, int64_t sc, int64_t r0, int64_t c0, int64_t ir, int64_t ic, double p0, double p1,
@@ -74,7 +72,6 @@ struct Plan {
   double* WG = nullptr;     // [W (n x k) ; G (k x k)] f64: the reduced pass outputs
   float* Y = nullptr;       // m x k f32
   void* bnd_ws = nullptr;   // fused boundary: sync words + partial Grams (zeroed once)
-  void* gram_ws = nullptr;  // fp64 Gram of the stored Y (slabs)
   float* last_ptrs[3] = {nullptr, nullptr, nullptr};   // optr contents written last (and on which stream)
   hipStream_t last_ptrs_stream = nullptr;
   // FJLT operator set for the next call but not yet launched: the run launches
@@ -126,18 +123,15 @@ int seg(Plan* p, const void* A, int i, hipStream_t s, float* V = nullptr, float*
                           p->s64, p->mirror_dev, V, s32, optr, s);
     if (rc != SL_OK || fin) return rc;
   }
-  // the final pass stores Y; its fp64 Gram is one separate streaming kernel
-  // over the stored Y (in-pass it lengthened every block's dependent chain)
+  // the final pass stores Y and forms its fp64 Gram in-pass (bf16 hi / lo
+  // products on the fragments the W update already holds); one reduce sums
+  // the W and Gram slabs into [W; G]
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
-                    final_pass ? 2 : 0, 0, s);
+                    final_pass ? 1 : 0, 0, s);
   if (rc != SL_OK) return rc;
-  if (final_pass) {
-    rc = sl_tsk_gram64(p->Y, p->m, p->k, p->k, p->WG + p->n * p->k, p->gram_ws, s);
-    if (rc != SL_OK) return rc;
-  }
   // the first reduce of the call also clears the status word (no memset node)
-  return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, nullptr, p->k, i == 0 ? p->status : nullptr,
-                          s);
+  return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
+                          p->k, i == 0 ? p->status : nullptr, s);
 }
 
 void drop_graph(Plan* p) {
@@ -219,7 +213,6 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   const int64_t o_wg = off;   off = align256(off + (n + k) * k * 8);
   const int64_t o_y = off;    off = align256(off + m * k * 4);
   const int64_t o_bnd = off;  off = align256(off + sl_rsvd_bnd_workspace(k));
-  const int64_t o_gw = off;   off = align256(off + sl_tsk_gram64_workspace(m, k));
   const int64_t o_ri = off;   off = align256(off + (int64_t)k * k * 8);
   const int64_t o_m = off;    off = align256(off + (int64_t)k * r * 4);
   const int64_t o_n = off;    off = align256(off + (int64_t)k * r * 8);
@@ -236,7 +229,6 @@ SL_API int sl_rsvd_plan_create(int64_t m, int64_t n, int64_t lda, int k, int r, 
   p->WG = (double*)(p->base + o_wg);
   p->Y = (float*)(p->base + o_y);
   p->bnd_ws = p->base + o_bnd;
-  p->gram_ws = p->base + o_gw;
   p->Rinv = (double*)(p->base + o_ri);
   p->M = (float*)(p->base + o_m);
   p->N = (double*)(p->base + o_n);

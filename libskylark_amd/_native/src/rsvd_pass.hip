@@ -106,17 +106,16 @@ struct Geo4 {
   static constexpr int PART = WAVES * KP * BM * 4; // per-wave partial y tiles (f32, [w][col][row])
   static constexpr int Y16P = KP * BM * 2 + 16;    // bytes per part (hi / lo) of the bf16 y image
   static constexpr int Y16 = 2 * Y16P;
-  static constexpr int YF = KP * BM * 4;           // reduced f32 y ([col][row], FINAL only)
   static constexpr int CPW = KP / WAVES;           // y columns reduced per wave
   static constexpr int RL = CPW * 4;               // reducer lanes per wave (one row quad each)
-  static constexpr int GT64 = KT * (KT + 1) / 2;   // upper 16 x 16 Gram tiles
-  static constexpr int GS64 = (GT64 + WAVES - 1) / WAVES;
+  static constexpr int GT = KT * (KT + 1) / 2;     // upper 16 x 16 Gram tiles
+  static constexpr int GS = (GT + WAVES - 1) / WAVES;  // Gram tiles per wave
 };
 
 template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM = FINAL>
 constexpr int pass_lds() {
   using G = Geo4<WAVES, NW, KT, NBUF>;
-  return G::RING + G::PART + G::Y16 + (GRAM ? G::YF : 0);
+  return G::RING + G::PART + G::Y16;
 }
 
 // swizzle of 16-B chunk slots by row (see tsk_kernels.hip: a GF(2) map that
@@ -146,7 +145,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
   char* ring = smem;
   float* part = (float*)(smem + G::RING);
   char* y16 = smem + G::RING + G::PART;
-  float* yf = (float*)(smem + G::RING + G::PART + G::Y16);
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -181,9 +179,9 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
   for (int a = 0; a < NW / 16; ++a)
 #pragma unroll
     for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f64x4 accG[GRAM ? G::GS64 : 1];
+  f64x4 accG[GRAM ? G::GS : 1];
 #pragma unroll
-  for (int s = 0; s < (GRAM ? G::GS64 : 1); ++s) accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < (GRAM ? G::GS : 1); ++s) accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
 
   // ---- LDS-DMA of row block `blk` (this wave's columns) into ring slot `slot`.
   //      The per-lane source offsets inside a block are fixed: precomputed
@@ -305,12 +303,13 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       *(s16x4*)(y16 + rc * 32 + rq * 8) = hi;
       *(s16x4*)(y16 + G::Y16P + rc * 32 + rq * 8) = lo;
       if constexpr (FINAL) {
-        if constexpr (GRAM) *(f32x4*)&yf[qidx(rc, rq)] = sum;
+        // the stored Y is y' = y_hi + y_lo (exact in f32): the rows W and
+        // the in-pass Gram are formed from, so Y, W and G stay consistent
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int64_t row = r0 + 4 * rq + e;
           float* dst = (row < m && rc < k) ? Y + row * ldy + rc : scratch + lane;
-          *dst = sum[e];
+          *dst = bf16_val(hi[e]) + bf16_val(lo[e]);
         }
       }
     }
@@ -318,24 +317,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
     lds_barrier();   // (B) y of block j is complete
     SL_STAMP(5)
 
-    if constexpr (GRAM) {
-      // ---- fp64 Gram of y: upper tile tau = (t1, t2) on wave tau % WAVES;
-      //      K step u pairs lane group g with row 4 g + u
-      int tau = 0;
-#pragma unroll
-      for (int t1 = 0; t1 < KT; ++t1)
-#pragma unroll
-        for (int t2 = t1; t2 < KT; ++t2, ++tau) {
-          if ((tau % WAVES) == w) {
-            const int s = tau / WAVES;
-            const f32x4 qa = *(const f32x4*)&yf[qidx(16 * t1 + i16, g4)];
-            const f32x4 qb = *(const f32x4*)&yf[qidx(16 * t2 + i16, g4)];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              accG[s] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)qa[u], (double)qb[u], accG[s], 0, 0, 0);
-          }
-        }
-    }
     SL_STAMP(6)
 
     // ---- step 3: W += A^T (y_hi + y_lo).  K = 32 packs [8 rows of y_hi |
@@ -347,6 +328,27 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       bf16x8 yfr[KT];
 #pragma unroll
       for (int t = 0; t < KT; ++t) yfr[t] = *(const bf16x8*)(yp + (16 * t + i16) * 32);
+      // Gram of y' = y_hi + y_lo on the same fragments: with K = (part, row),
+      // yfr[t1]^T yfr[t2] = hi^T hi + lo^T lo and, against the fragment of
+      // the other part, hi^T lo + lo^T hi.  Every bf16 x bf16 product is
+      // exact in f32; a block's 64 products are summed in f32 by two MFMAs
+      // and added to the fp64 accumulator after the W MFMAs are issued.
+      f32x4 gblk[GRAM ? G::GS : 1];
+      if constexpr (GRAM) {
+        int tau = 0;
+#pragma unroll
+        for (int t1 = 0; t1 < KT; ++t1)
+#pragma unroll
+          for (int t2 = t1; t2 < KT; ++t2, ++tau) {
+            if ((tau % WAVES) == w) {
+              const int s = tau / WAVES;
+              const bf16x8 ysw = *(const bf16x8*)(y16 + ((g4 & 1) ^ 1) * G::Y16P + rb * 2 + (16 * t2 + i16) * 32);
+              const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+              gblk[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yfr[t1], yfr[t2], z4, 0, 0, 0);
+              gblk[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yfr[t1], ysw, gblk[s], 0, 0, 0);
+            }
+          }
+      }
       const int q = i16 >> 2, p = i16 & 3;
 #pragma unroll
       for (int ct = 0; ct < NW / 16; ++ct) {
@@ -365,6 +367,18 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
         const bf16x8 af8 = __builtin_bit_cast(bf16x8, a8);
 #pragma unroll
         for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
+      }
+      if constexpr (GRAM) {
+        int tau = 0;
+#pragma unroll
+        for (int t1 = 0; t1 < KT; ++t1)
+#pragma unroll
+          for (int t2 = t1; t2 < KT; ++t2, ++tau)
+            if ((tau % WAVES) == w) {
+              const int s = tau / WAVES;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) accG[s][e] += (double)gblk[s][e];
+            }
       }
     }
 #ifdef SL_PASS_STAMPS
@@ -407,8 +421,8 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
         }
   }
   if constexpr (GRAM) {
-    // fp64 Gram slab [k][k]: each upper tile and its mirror (f64 C/D map:
-    // row = (lane >> 4) + 4 r, col = lane & 15)
+    // fp64 Gram slab [k][k]: each upper tile and its mirror (f32 C/D map:
+    // row = 4 (lane >> 4) + r, col = lane & 15)
     double* gs = Gslab + (int64_t)blockIdx.x * k * k;
     int tau = 0;
 #pragma unroll
@@ -419,7 +433,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
           const int s = tau / WAVES;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int i = 16 * t1 + g4 + 4 * r, jj = 16 * t2 + i16;
+            const int i = 16 * t1 + 4 * g4 + r, jj = 16 * t2 + i16;
             if (i < k && jj < k) {
               gs[i * k + jj] = accG[s][r];
               if (t1 != t2) gs[jj * k + i] = accG[s][r];
@@ -553,9 +567,10 @@ SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k) {
 // One v4 pass.  A: m x n bf16 (lda % 8 == 0, 16 <= n <= 1024, n % 8 == 0);
 // Zt: k x n bf16 (1 <= k <= 48).  ws: sl_rsvd_pass_workspace bytes.
 // final = 0: W slabs only.  final = 1: also Y (m x k f32, row stride ldy >=
-// k) and the fp64 Gram slabs; final = 2: W slabs and Y (the Gram formed
-// afterwards from the stored Y, off the per-block chain).  variant selects the
-// ring depth (tuning: 0 default, 3/4 = NBUF).
+// k; Y = y_hi + y_lo, the bf16 pair W is formed from) and the fp64 Gram slabs
+// of that Y (exact bf16 products, f32 per 16-row block, f64 across blocks);
+// final = 2: W slabs and Y only.  variant selects the ring depth (tuning: 0
+// default, 3/4 = NBUF).
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
                         float* Y, int64_t ldy, int final_pass, int variant, void* stream) {
   if (m <= 0) return SL_OK;
