@@ -198,7 +198,10 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
   const double xi = (i > J) ? arow[J] : 0.0;
   const double sig2 = s2 - x0 * x0;
   const bool refl_on = sig2 > 1e-300;
-  const double alpha = refl_on ? (x0 >= 0.0 ? -sqrt(s2) : sqrt(s2)) : x0;
+  // sqrt(s2) as s2 / sqrt(s2) on the rsq estimate + Newton (shorter chain
+  // than the library sqrt's denormal-scaling sequence; s2 > 1e-300 here)
+  const double rs = rsq64(refl_on ? s2 : 1.0);
+  const double alpha = refl_on ? (x0 >= 0.0 ? -s2 * rs : s2 * rs) : x0;
   const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
   const double vi = (i > J) ? (xi - (i == J + 1 ? alpha : 0.0)) * rn : 0.0;
   if (i == J) { dd[J] = arow[J]; ee[J] = alpha; }
@@ -327,6 +330,73 @@ __device__ __forceinline__ double rcp64n(double d) {   // estimate + one Newton 
   return r * fma(-d, r, 2.0);
 }
 
+// Eigenvector of the (scaled) tridiagonal T for the eigenvalue l by the
+// twisted factorisation T - l I = N_r D_r N_r^T, one lane per vector:
+// backward pivots D-_i and forward pivots D+_i (their reciprocals in
+// registers), the twist r = argmin |gamma_i|, then z by the two one-term
+// recurrences.  zdm receives z (unnormalised), zdp / zrd are scratch; the
+// return value is 1 / ||z||.  The LDS inputs are __restrict__: the loads of
+// d / e are then free to run ahead of the pivot stores (with may-alias LDS
+// pointers every step waited for its loads after the previous stores).
+template <int K>
+__device__ __forceinline__ double twisted_vec(const double* __restrict__ dd, const double* __restrict__ ee, double l,
+                                              double* __restrict__ zdm, double* __restrict__ zdp,
+                                              double* __restrict__ zrd) {
+  const double pivmin = 1e-290;
+  double rup[K];
+  double dm = dd[K - 1] - l;
+  if (fabs(dm) < pivmin) dm = -pivmin;
+  zdm[K - 1] = dm;
+  double dp = dd[0] - l;
+  if (fabs(dp) < pivmin) dp = -pivmin;
+  zdp[0] = dp;
+#pragma unroll
+  for (int s_ = 0; s_ < K - 1; ++s_) {
+    const int ib = K - 2 - s_, jf = s_ + 1;
+    const double eb = ee[ib], ef = ee[jf - 1];
+    const double rdm = rcp64n(dm);        // 1 / D-_{ib+1}
+    zrd[ib + 1] = -eb * rdm;
+    dm = (dd[ib] - l) - (eb * eb) * rdm;
+    if (fabs(dm) < pivmin) dm = -pivmin;
+    zdm[ib] = dm;
+    const double rdp = rcp64n(dp);        // 1 / D+_{jf-1}
+    rup[jf - 1] = rdp;
+    dp = (dd[jf] - l) - (ef * ef) * rdp;
+    if (fabs(dp) < pivmin) dp = -pivmin;
+    zdp[jf] = dp;
+  }
+  rup[K - 1] = rcp64n(dp);
+  // the twist: argmin |gamma_i|, gamma_i = D+_i + D-_i - (d_i - l)
+  int rt = 0;
+  double best = 1e300;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const double gm = fabs(zdp[i] + zdm[i] - (dd[i] - l));
+    if (gm < best) { best = gm; rt = i; }
+  }
+  // above the twist: z_i = -(e_i / D+_i) z_{i+1}; below: z_i = ratio_i z_{i-1}
+  double z = 1.0, nrm = 1.0;
+#pragma unroll
+  for (int i = K - 2; i >= 0; --i) {
+    if (i < rt) {
+      z = -(ee[i] * rup[i]) * z;
+      nrm = fma(z, z, nrm);
+      zdm[i] = z;
+    }
+  }
+  z = 1.0;
+#pragma unroll
+  for (int i = 1; i < K; ++i) {
+    if (i > rt) {
+      z = zrd[i] * z;
+      nrm = fma(z, z, nrm);
+      zdm[i] = z;
+    }
+  }
+  zdm[rt] = 1.0;
+  return rsq64(nrm);
+}
+
 // Eigenpairs of the symmetric K x K matrix given by its tridiagonal form
 // (dd, ee) and reflectors (refl): the nt largest eigenvalues, descending,
 // in lam[0..nt-1] and the eigenvectors of the ORIGINAL matrix (Q x) for the
@@ -364,6 +434,10 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
   //      wave run independently; T in registers
   constexpr double eps = 2.220446049250313e-16;
   constexpr int MP = 2;
+  // eigenvalues closer than CLUS (scaled: ||T|| = 1) are orthogonalised
+  // against each other; farther apart the twisted vectors are orthogonal to
+  // ~eps / gap < 1e-11 on their own
+  constexpr double CLUS = 1e-4;
   const int row = tid >> 4, g = tid & 15;
   constexpr int ROWS = NT / 16;
   {
@@ -380,7 +454,10 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
       const int idx = K - 1 - t;   // ascending index of this row's eigenvalue
       double lo = -1.0 - 4.0 * eps, hi = 1.0 + 4.0 * eps;
       for (int it = 0; it < 64; ++it) {
-        const bool conv = !act || (hi - lo) <= fmax(4.0 * eps, 2.0 * eps * fmax(fabs(lo), fabs(hi)));
+        // absolute accuracy eps ||T|| (||T|| = 1 after the scaling): what the
+        // backward-stable reduction determines; resolving tiny eigenvalues to
+        // full relative precision cost ~20 more bits (4 rounds)
+        const bool conv = !act || (hi - lo) <= 4.0 * eps;
         if (__builtin_amdgcn_ballot_w64(!conv) == 0) break;
         double x[MP];
         int c[MP];
@@ -426,63 +503,8 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     const double l = lam[t];
     const double gap = fmin(t > 0 ? lam[t - 1] - l : 1e300, t + 1 < nt ? l - lam[t + 1] : 1e300);
     if (!(gap > 1e-13)) atomicOr(st, 1);       // numerically repeated (~ bisection accuracy): the caller falls back
-    if (gap < 1e-2) atomicOr(&s_clus, 1);
-    const double pivmin = 1e-290;
-    double* zdm = sc + t * LZ;
-    double* zdp = sc + (nv + t) * LZ;
-    double* zrd = sc + (2 * nv + t) * LZ;
-    double rup[K];
-    double dm = dd[K - 1] - l;
-    if (fabs(dm) < pivmin) dm = -pivmin;
-    zdm[K - 1] = dm;
-    double dp = dd[0] - l;
-    if (fabs(dp) < pivmin) dp = -pivmin;
-    zdp[0] = dp;
-#pragma unroll
-    for (int s_ = 0; s_ < K - 1; ++s_) {
-      const int ib = K - 2 - s_, jf = s_ + 1;
-      const double eb = ee[ib], ef = ee[jf - 1];
-      const double rdm = rcp64n(dm);        // 1 / D-_{ib+1}
-      zrd[ib + 1] = -eb * rdm;
-      dm = (dd[ib] - l) - (eb * eb) * rdm;
-      if (fabs(dm) < pivmin) dm = -pivmin;
-      zdm[ib] = dm;
-      const double rdp = rcp64n(dp);        // 1 / D+_{jf-1}
-      rup[jf - 1] = rdp;
-      dp = (dd[jf] - l) - (ef * ef) * rdp;
-      if (fabs(dp) < pivmin) dp = -pivmin;
-      zdp[jf] = dp;
-    }
-    rup[K - 1] = rcp64n(dp);
-    // the twist: argmin |gamma_i|, gamma_i = D+_i + D-_i - (d_i - l)
-    int rt = 0;
-    double best = 1e300;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const double gm = fabs(zdp[i] + zdm[i] - (dd[i] - l));
-      if (gm < best) { best = gm; rt = i; }
-    }
-    // above the twist: z_i = -(e_i / D+_i) z_{i+1}; below: z_i = ratio_i z_{i-1}
-    double z = 1.0, nrm = 1.0;
-#pragma unroll
-    for (int i = K - 2; i >= 0; --i) {
-      if (i < rt) {
-        z = -(ee[i] * rup[i]) * z;
-        nrm = fma(z, z, nrm);
-        zdm[i] = z;
-      }
-    }
-    z = 1.0;
-#pragma unroll
-    for (int i = 1; i < K; ++i) {
-      if (i > rt) {
-        z = zrd[i] * z;
-        nrm = fma(z, z, nrm);
-        zdm[i] = z;
-      }
-    }
-    zdm[rt] = 1.0;
-    const double s = rsq64(nrm);
+    if (gap < CLUS) atomicOr(&s_clus, 1);
+    const double s = twisted_vec<K>(dd, ee, l, sc + t * LZ, sc + (nv + t) * LZ, sc + (2 * nv + t) * LZ);
     if (!(s > 0.0) || !(s < 1e300)) atomicOr(st, 1);
     snorm[t] = s;
   }
@@ -494,20 +516,28 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
   }
   __syncthreads();
   SLW_STAMP(3)
-  // ---- MGS inside close clusters (rare): wave 0, lane = component
+  // ---- MGS inside close clusters (rare): wave 0, lane = component.  Two
+  //      passes ("twice is enough"): inside a tight cluster the twisted
+  //      vectors can be nearly parallel, and one pass then leaves a small
+  //      remainder that is not orthogonal to the others.  A vector that
+  //      vanishes under both passes flags the core (Jacobi re-solve).
   if (s_clus && tid < 64) {
     const int i = lane;
     for (int t = 1; t < nv; ++t) {
       double xc = i < K ? sc[t * LZ + i] : 0.0;
       bool touched = false;
-      for (int u = 0; u < t; ++u) {
-        if (lam[u] - lam[t] >= 1e-2) continue;
-        const double dt = wave_sum(i < K ? sc[u * LZ + i] * xc : 0.0);
-        xc -= dt * (i < K ? sc[u * LZ + i] : 0.0);
-        touched = true;
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int u = 0; u < t; ++u) {
+          if (lam[u] - lam[t] >= CLUS) continue;
+          const double dt = wave_sum(i < K ? sc[u * LZ + i] * xc : 0.0);
+          xc -= dt * (i < K ? sc[u * LZ + i] : 0.0);
+          touched = true;
+        }
+        if (!touched) break;
       }
       if (touched) {
         const double n2 = wave_sum(xc * xc);
+        if (!(n2 > 1e-24) && lane == 0) atomicOr(st, 1);
         if (i < K) sc[t * LZ + i] = xc * rsq64(n2);
       }
       wave_lds_sync();

@@ -460,9 +460,11 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     // the Y^T Y worker: Rt^{-1} of the reduced Gram (independent of W) while
     // the row workgroups form and sum H, published as a finished-worker count
     if (tid == 0) st_sh = 0;
+    SL_CST(11)
     __syncthreads();
     if (tid < 64) slw::wave_chol_inv<K>(a.WG + (int64_t)n * k, k, a.rti, k, k, cls.fsh, &st_sh);
     __syncthreads();
+    SL_CST(12)
     if (tid == 0) ((int*)(a.rti + k * k))[0] = st_sh;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -609,6 +611,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
         st_sh |= ((const int*)(a.rti + k * k))[0];
       }
       __syncthreads();
+      SL_CST(13)
       {
         constexpr int UB = BK * BK / NT + 1;
         double v[UB];

@@ -180,8 +180,22 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 #pragma unroll
     for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   f64x4 accG[GRAM ? G::GS : 1];
+  f32x4 gblk[GRAM ? G::GS : 1];   // this block's f32 Gram tile, added to accG one block later
 #pragma unroll
-  for (int s = 0; s < (GRAM ? G::GS : 1); ++s) accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < (GRAM ? G::GS : 1); ++s) {
+    accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+    gblk[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // fp64 accumulation of the previous block's Gram tile: placed a barrier
+  // after its MFMAs were issued, so the adds never wait on the MFMA pipe
+  auto gram_acc = [&]() {
+    if constexpr (GRAM) {
+#pragma unroll
+      for (int s = 0; s < G::GS; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) accG[s][e] += (double)gblk[s][e];
+    }
+  };
 
   // ---- LDS-DMA of row block `blk` (this wave's columns) into ring slot `slot`.
   //      The per-lane source offsets inside a block are fixed: precomputed
@@ -280,6 +294,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
     }
     SL_STAMP(2)
     lds_barrier();   // (A) the partials of block j are complete
+    gram_acc();
     SL_STAMP(3)
     // ---- step 2: each wave sums its CPW columns over the WAVES partials,
     //      emits y as bf16 hi / lo B-fragment images (and, FINAL, f32 y and
@@ -333,7 +348,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       // the other part, hi^T lo + lo^T hi.  Every bf16 x bf16 product is
       // exact in f32; a block's 64 products are summed in f32 by two MFMAs
       // and added to the fp64 accumulator after the W MFMAs are issued.
-      f32x4 gblk[GRAM ? G::GS : 1];
       if constexpr (GRAM) {
         int tau = 0;
 #pragma unroll
@@ -368,18 +382,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 #pragma unroll
         for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
       }
-      if constexpr (GRAM) {
-        int tau = 0;
-#pragma unroll
-        for (int t1 = 0; t1 < KT; ++t1)
-#pragma unroll
-          for (int t2 = t1; t2 < KT; ++t2, ++tau)
-            if ((tau % WAVES) == w) {
-              const int s = tau / WAVES;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) accG[s][e] += (double)gblk[s][e];
-            }
-      }
     }
 #ifdef SL_PASS_STAMPS
     // drain the MFMAs so the stamp sees their time
@@ -405,6 +407,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
   }
 #endif
 #undef SL_STAMP
+  gram_acc();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- W partial slab [n][k] (rows past n / columns past k dropped)
@@ -434,9 +437,9 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = 16 * t1 + 4 * g4 + r, jj = 16 * t2 + i16;
-            if (i < k && jj < k) {
+            if (i < k && jj < k && (t1 != t2 || i <= jj)) {
               gs[i * k + jj] = accG[s][r];
-              if (t1 != t2) gs[jj * k + i] = accG[s][r];
+              if (i != jj) gs[jj * k + i] = accG[s][r];
             }
           }
         }

@@ -203,6 +203,33 @@ SL_API int sl_sym_eig_topr_if(const double* C, int k, int ldc, int r, double* ou
 }
 
 #ifdef SL_EIG_STAMPS
+namespace {
+// diagnostic: the tridiagonal (d, e) of the one-wave reduction and the
+// multisection eigenvalues of it (ascending index order as sym_top_eig
+// returns them, descending values), for accuracy checks against LAPACK
+template <int K>
+__global__ void __launch_bounds__(512) k_tridiag_dbg(const double* __restrict__ C, int k, double* __restrict__ out) {
+  __shared__ double refl[K * (K + 1)];
+  __shared__ double sc[3 * 64 * (K + 1)];
+  __shared__ __attribute__((aligned(16))) double dd[K], ee[K], lam[K], vsh[2 * K], wsh[2 * K];
+  __shared__ int bad, fb;
+  const int tid = threadIdx.x;
+  if (tid == 0) { bad = 0; fb = 0; }
+  __syncthreads();
+  if (tid < 64) slw::wave_tridiag<K>(C, k, k, refl, K + 1, dd, ee, vsh, wsh, &bad);
+  __syncthreads();
+  if (tid < K) { out[tid] = dd[tid]; out[K + tid] = ee[tid]; }
+  __syncthreads();
+  slw::sym_top_eig<K, 512>(dd, ee, refl, K + 1, k, 1, lam, out + 3 * K, 1, k, sc, &fb);
+  if (tid < k) out[2 * K + tid] = lam[tid];
+}
+}  // namespace
+SL_API int sl_tridiag_dbg(const double* C, int k, double* out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (k <= 40) k_tridiag_dbg<40><<<1, 512, 0, s>>>(C, k, out);
+  else k_tridiag_dbg<64><<<1, 512, 0, s>>>(C, k, out);
+  return SL_OK;
+}
 SL_API int sl_eig_stamps(unsigned long long* host) {
   SL_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_eig_st), sizeof(g_eig_st)));
   return SL_OK;

@@ -4,7 +4,6 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_rsvd_pass.py tests/test_gpu_oneshot.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pt_pass.log 2>&1; prc=$?; tail -3 $OUT/pt_pass.log; case $prc in 124|134|137|139) exit $prc ;; esac
 timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=30 -q -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pt_all.log 2>&1
 trc=$?; grep -E "^(FAILED|ERROR)" $OUT/pt_all.log; tail -2 $OUT/pt_all.log
 case $trc in 124|134|137|139) exit $trc ;; esac

@@ -62,5 +62,10 @@ def test_pass_matches_fp64(L, m, n, k, final):
         Gref = Yd.t() @ Yd
         d = Gref.diagonal().sqrt()
         rel = ((G - Gref).abs() / torch.outer(d, d)).max().item()
-        assert rel < 1e-8, rel
+        # per 16-row block the 64 exact products are summed in f32 (2^-24
+        # relative to the block's sum of |products|), blocks in f64: bounded by
+        # ~2^-23 sqrt(G_ii G_jj), far below that for many blocks
+        assert rel < 1.2e-7, rel
+        if m > 50_000:
+            assert rel < 1e-8, rel
         assert torch.equal(G, G.t())
