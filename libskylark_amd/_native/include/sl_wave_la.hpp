@@ -185,17 +185,14 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
                                          double* dd, double* ee) {
   constexpr int c0 = (J + 1) & ~1;
   if (J == 10) { SLW_STAMP(10) }
-  // ||x||^2 of column J below the diagonal and its first entry: row J of the
-  // (symmetric) trailing matrix, summed by lane J alone -- no cross-lane sum
-  double q0 = 0.0, q1 = 0.0;
-#pragma unroll
-  for (int c = J + 1; c < K; c += 2) {
-    q0 = fma(arow[c], arow[c], q0);
-    if (c + 1 < K) q1 = fma(arow[c + 1], arow[c + 1], q1);
-  }
-  const double s2 = lane_d(q0 + q1, J);
-  const double x0 = lane_d(arow[J + 1], J);
+  // ||x||^2 of column J below the diagonal and its first entry, from the
+  // column itself (lane i > J holds x_i): the rank-2 updates keep the
+  // register matrix symmetric only to rounding, and a norm taken from row J
+  // while v is built from column J left H non-orthogonal by eps ||A|| / ||x||
+  // (backward errors of 1e-12 on graded trailing blocks)
   const double xi = (i > J) ? arow[J] : 0.0;
+  const double s2 = wave_sum(xi * xi);
+  const double x0 = lane_d(arow[J], J + 1);
   const double sig2 = s2 - x0 * x0;
   const bool refl_on = sig2 > 1e-300;
   // sqrt(s2) as s2 / sqrt(s2) on the rsq estimate + Newton (shorter chain

@@ -461,9 +461,34 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     // the row workgroups form and sum H, published as a finished-worker count
     if (tid == 0) st_sh = 0;
     SL_CST(11)
+    // G staged into LDS with coalesced loads (all in flight), the elimination
+    // on LDS operands, X back with coalesced stores: the wave's per-lane
+    // strided global reads / writes cost ~10 us on this critical path
+    {
+      const double* Gg = a.WG + (int64_t)n * k;
+      constexpr int UB = BK * BK / NT + 1;
+      double v[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e = tid + NT * u;
+        v[u] = Gg[e < k * k ? e : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int e = tid + NT * u;
+        if (e < k * k) {
+          const int i = e / k, c = e - i * k;
+          b0[i * ld + c] = v[u];
+        }
+      }
+    }
     __syncthreads();
-    if (tid < 64) slw::wave_chol_inv<K>(a.WG + (int64_t)n * k, k, a.rti, k, k, cls.fsh, &st_sh);
+    if (tid < 64) slw::wave_chol_inv<K>(b0, ld, b2, ld, k, cls.fsh, &st_sh);
     __syncthreads();
+    for (int e = tid; e < k * k; e += NT) {
+      const int i = e / k, c = e - i * k;
+      a.rti[e] = b2[i * ld + c];
+    }
     SL_CST(12)
     if (tid == 0) ((int*)(a.rti + k * k))[0] = st_sh;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

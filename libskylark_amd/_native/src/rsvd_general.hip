@@ -4,16 +4,19 @@
 // any n (the bf16 fused engine, rsvd_engine.cpp, covers n <= 1024, k <= 48),
 // k <= 128, every stage on the device with no host round trip.
 //
-// One call = q + 2 segments on a HIP stream, the same contract as the fused
-// engine so one driver serves both (Python _EnginePlan, C sl_rsvd_gen_run_comm):
-//   seg 0        Y = A Z (Z = the sketch operator), W = A^T Y  -> WG[0 : n k]
-//   seg 1 .. q   H = W^T W, R^{-1} (Cholesky, pivot dropping), Z = W R^{-1},
-//                then the next pass (seg q also: G = Y^T Y in f64 -> WG[n k :])
-//   seg q + 1    the core: Rt^{-1} of G, C = Rt^{-T} W^T W Rt^{-1}, its top
+// One call = 2 q + 3 segments on a HIP stream (sl_rsvd_gen_num_segments),
+// driven by one loop (Python _GenPlan, C sl_rsvd_gen_run_comm) that sums the
+// span sl_rsvd_gen_reduce_span(i) of WG across ranks after each segment:
+//   seg 2 j      [j > 0: H = W^T W, R^{-1} (Cholesky, pivot dropping),
+//                Z = W R^{-1}] then Y = A Z and Y^T Y (f64) -> WG[n k :]
+//   seg 2 j + 1  Ry = R^{-1} of Y^T Y, Q = Y Ry, W = A^T Q -> WG[0 : n k]
+//                (j = q also G = Q^T Q -> WG[n k :])
+//   seg 2 q + 2  the core: Rt^{-1} of G, C = Rt^{-T} W^T W Rt^{-1}, its top
 //                r + 1 eigenpairs, M = Rt^{-1} Ub_r, N = M S^{-1}, s
-// then the finish (V = W N, U = Y M) into the caller's buffers.  Between the
-// reducing segments several ranks all-reduce WG ((n + k) x k f64).
-//
+// then the finish (V = W N, U = Q M) into the caller's buffers.  Y and W are
+// both re-orthonormalised, as the reference's power iteration does after
+// every application of A (W = A^T A Z without it squares the condition
+// number, and the trailing wanted directions drowned at k = 128).
 // The two products over A per pass are plain library GEMMs (rocBLAS: a tall
 // operand times an n x k panel, bandwidth-bound); the CholeskyQR factors and
 // the core eigensolver are the one-wave kernels of sl_wave_la.hpp for k <= 64
@@ -86,14 +89,17 @@ __global__ void __launch_bounds__(256) k_fjlt_z(uint64_t seed, uint64_t baseD, u
   st_d<T>(Z + t, cos(w * (double)a) * (p == 0 ? c0 : c1) * scale * d);
 }
 
-// bf16 hi / lo planes of an f32 matrix: hi = bf16(y), lo = bf16(y - hi)
-__global__ void __launch_bounds__(256) k_split_bf16(const float* __restrict__ y, int64_t tot, bf16_t* __restrict__ hi,
+// bf16 hi / lo planes of an f32 matrix: hi = bf16(y), lo = bf16(y - hi), and
+// y <- hi + lo (exact in f32): the rows the bf16 products actually see
+__global__ void __launch_bounds__(256) k_split_bf16(float* __restrict__ y, int64_t tot, bf16_t* __restrict__ hi,
                                                    bf16_t* __restrict__ lo) {
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < tot; t += (int64_t)gridDim.x * 256) {
     const float v = y[t];
     const bf16_t h = f_to_bf16(v);
+    const bf16_t l = f_to_bf16(v - bf16_to_f(h));
     hi[t] = h;
-    lo[t] = f_to_bf16(v - bf16_to_f(h));
+    lo[t] = l;
+    y[t] = bf16_to_f(h) + bf16_to_f(l);
   }
 }
 
@@ -161,6 +167,8 @@ struct GPlan {
   void* Yh = nullptr;      // bf16 A: hi / lo planes of Y (m x k bf16 each)
   void* Yl = nullptr;
   void* Wt = nullptr;      // n x k pass output (dt; f32 when A is bf16)
+  void* Qb = nullptr;      // m x k orthonormalised Y (dt; f32 when A is bf16): the basis U is formed from
+  void* Rf = nullptr;      // k x k f32 copy of R^{-1} (f32 / bf16 A)
   double* WG = nullptr;    // [W (n x k); G (k x k)] f64
   double* Zf = nullptr;    // n x k f64
   double* H = nullptr;     // k x k
@@ -176,7 +184,7 @@ struct GPlan {
   void* parts = nullptr;   // f32 / f64 A: per-row-chunk partials of A^T Y (np + 1 slabs of n x k, dt)
   int np = 0;              // row chunks of ch rows (+ one for the remainder)
   int64_t ch = 0;
-  int* st = nullptr;       // [0] status, [1..2] eig status, [4..11] chol statuses / infos
+  int* st = nullptr;       // [0] status, [1..2] eig status, [4..11] chol statuses / infos (4 / 6 inter, 8 core, 10 Y)
   // sketch of the call
   int sk = 0;              // 0 none, 1 FJLT, 2 dense
   uint64_t seed = 0, b0 = 0, b1 = 0;
@@ -260,102 +268,109 @@ int make_z(GPlan* p, hipStream_t s) {
   return SL_OK;   // Z set explicitly
 }
 
-// one pass over A: Y = A Z, W = A^T Y (into WG f64), and on the final pass
-// G = Y^T Y (f64).  The first pass of the call clears the status word.
-int pass(GPlan* p, const void* A, bool final_pass, bool first, hipStream_t s) {
-  const int64_t m = p->m, n = p->n;
+// G (k x k f64) = Yb^T Yb of an m x k matrix in the pass precision (f64:
+// strided-batched row-chunk products + one f64 slab sum; f32: the fp64 Gram
+// kernel for k <= 64, else f64 copies of row pieces)
+int gram(GPlan* p, const void* Yb, double* G, hipStream_t s) {
+  const int64_t m = p->m;
   const int k = p->k;
   int rc;
-  if (p->dt == SL_BF16) {
-    // bf16 A: Y (f32) = A Z; W = A^T (Y_hi + Y_lo) with Y split into two bf16 planes
-    rc = slb_gemm(SL_BF16, false, false, m, k, n, 1.0, A, p->lda, p->Z, k, 0.0, p->Y, k, s);
-    if (rc != SL_OK) return rc;
-    k_split_bf16<<<grid_of(m * k), 256, 0, s>>>((const float*)p->Y, m * k, (bf16_t*)p->Yh, (bf16_t*)p->Yl);
-    SL_LAUNCH_CHECK();
-    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yh, k, 0.0, p->Wt, k, s);
-    if (rc != SL_OK) return rc;
-    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yl, k, 1.0, p->Wt, k, s);
-    if (rc != SL_OK) return rc;
-  } else {
-    rc = slb_gemm(p->dt, false, false, m, k, n, 1.0, A, p->lda, p->Z, k, 0.0, p->Y, k, s);
-    if (rc != SL_OK) return rc;
-    // W = A^T Y as np row-chunk products (one strided-batched launch fills the
-    // chip; a single K = m product runs on a handful of workgroups), then one
-    // f64 sum of the partial slabs straight into WG
-    const size_t es = p->dt == SL_F64 ? 8 : 4;
-    const int64_t tot = n * k;
-    rc = slb_gemm_strided(p->dt, true, false, n, k, p->ch, 1.0, A, p->lda, p->ch * p->lda, p->Y, k, p->ch * k, 0.0,
-                          p->parts, k, tot, p->np, s);
+  if (p->dt == SL_F64) {
+    const int64_t tg = (int64_t)k * k;
+    rc = slb_gemm_strided(SL_F64, true, false, k, k, p->ch, 1.0, Yb, k, p->ch * k, Yb, k, p->ch * k, 0.0, p->parts,
+                          k, tg, p->np, s);
     if (rc != SL_OK) return rc;
     const int64_t r0 = p->ch * p->np;
     int nparts = p->np;
     if (r0 < m) {
-      rc = slb_gemm(p->dt, true, false, n, k, m - r0, 1.0, (const char*)A + r0 * p->lda * es, p->lda,
-                    (const char*)p->Y + r0 * k * es, k, 0.0, (char*)p->parts + (int64_t)p->np * tot * es, k, s);
+      rc = slb_gemm(SL_F64, true, false, k, k, m - r0, 1.0, (const double*)Yb + r0 * k, k,
+                    (const double*)Yb + r0 * k, k, 0.0, (double*)p->parts + (int64_t)p->np * tg, k, s);
       if (rc != SL_OK) return rc;
       ++nparts;
     }
-    rc = dispatch_dt(p->dt, [&](auto* tag) {
-      using T = std::remove_pointer_t<decltype(tag)>;
-      k_sum_parts<T><<<grid_of(tot), 256, 0, s>>>((const T*)p->parts, nparts, tot, p->WG, first ? p->st : nullptr);
-      SL_LAUNCH_CHECK();
-      return SL_OK;
-    });
-    if (rc != SL_OK || !final_pass) return rc;
-    if (p->dt == SL_F64) {
-      // G = Y^T Y the same way (k x k slabs in the same workspace)
-      double* G = p->WG + n * k;
-      const int64_t tg = (int64_t)k * k;
-      rc = slb_gemm_strided(SL_F64, true, false, k, k, p->ch, 1.0, p->Y, k, p->ch * k, p->Y, k, p->ch * k, 0.0,
-                            p->parts, k, tg, p->np, s);
-      if (rc != SL_OK) return rc;
-      if (r0 < m) {
-        rc = slb_gemm(SL_F64, true, false, k, k, m - r0, 1.0, (const double*)p->Y + r0 * k, k,
-                      (const double*)p->Y + r0 * k, k, 0.0, (double*)p->parts + (int64_t)p->np * tg, k, s);
-        if (rc != SL_OK) return rc;
-      }
-      k_sum_parts<double><<<grid_of(tg), 256, 0, s>>>((const double*)p->parts, nparts, tg, G, nullptr);
-      SL_LAUNCH_CHECK();
-      return SL_OK;
-    }
-  }
-  if (p->dt != SL_BF16) {
-    // f32 Y: the fp64 Gram below
-    double* G = p->WG + n * k;
-    if (k <= 64) return sl_tsk_gram64((const float*)p->Y, m, k, k, G, p->gws, s);
-    SL_HIP_CHECK(hipMemsetAsync(G, 0, (size_t)k * k * 8, s));
-    for (int64_t q0 = 0; q0 < m; q0 += GPIECE) {
-      const int64_t rows = (m - q0 < GPIECE) ? m - q0 : GPIECE;
-      k_cast2d<float, double><<<grid_of(rows * k), 256, 0, s>>>((const float*)p->Y + q0 * k, k, rows, k,
-                                                                 (double*)p->gws, k, nullptr);
-      SL_LAUNCH_CHECK();
-      rc = slb_gemm(SL_F64, true, false, k, k, rows, 1.0, p->gws, k, p->gws, k, 1.0, G, k, s);
-      if (rc != SL_OK) return rc;
-    }
-    return SL_OK;
-  }
-  const int wdt = p->dt == SL_BF16 ? SL_F32 : p->dt;
-  rc = dispatch_dt(wdt, [&](auto* tag) {
-    using T = std::remove_pointer_t<decltype(tag)>;
-    k_cast2d<T, double><<<grid_of(n * k), 256, 0, s>>>((const T*)p->Wt, k, n, k, p->WG, k, first ? p->st : nullptr);
+    k_sum_parts<double><<<grid_of(tg), 256, 0, s>>>((const double*)p->parts, nparts, tg, G, nullptr);
     SL_LAUNCH_CHECK();
     return SL_OK;
-  });
-  if (rc != SL_OK || !final_pass) return rc;
-  double* G = p->WG + n * k;
-  if (p->dt == SL_F64) return slb_gemm(SL_F64, true, false, k, k, m, 1.0, p->Y, k, p->Y, k, 0.0, G, k, s);
-  if (k <= 64) return sl_tsk_gram64((const float*)p->Y, m, k, k, G, p->gws, s);
-  // k > 64, f32 Y: Gram of f64 copies of row pieces (GPIECE rows per piece)
+  }
+  if (k <= 64) return sl_tsk_gram64((const float*)Yb, m, k, k, G, p->gws, s);
   SL_HIP_CHECK(hipMemsetAsync(G, 0, (size_t)k * k * 8, s));
-  for (int64_t r0 = 0; r0 < m; r0 += GPIECE) {
-    const int64_t rows = (m - r0 < GPIECE) ? m - r0 : GPIECE;
-    k_cast2d<float, double><<<grid_of(rows * k), 256, 0, s>>>((const float*)p->Y + r0 * k, k, rows, k,
+  for (int64_t q0 = 0; q0 < m; q0 += GPIECE) {
+    const int64_t rows = (m - q0 < GPIECE) ? m - q0 : GPIECE;
+    k_cast2d<float, double><<<grid_of(rows * k), 256, 0, s>>>((const float*)Yb + q0 * k, k, rows, k,
                                                                (double*)p->gws, k, nullptr);
     SL_LAUNCH_CHECK();
     rc = slb_gemm(SL_F64, true, false, k, k, rows, 1.0, p->gws, k, p->gws, k, 1.0, G, k, s);
     if (rc != SL_OK) return rc;
   }
   return SL_OK;
+}
+
+// first half of pass i: Y = A Z and its Gram Y^T Y -> WG[n k :] (all-reduced
+// across ranks before the second half)
+int apply_z(GPlan* p, const void* A, hipStream_t s) {
+  const int dt = p->dt == SL_BF16 ? SL_BF16 : p->dt;
+  int rc = slb_gemm(dt, false, false, p->m, p->k, p->n, 1.0, A, p->lda, p->Z, p->k, 0.0, p->Y, p->k, s);
+  if (rc != SL_OK) return rc;
+  return gram(p, p->Y, p->WG + p->n * p->k, s);
+}
+
+// second half of pass i: Ry = R^{-1} of the (all-reduced) Y^T Y (pivot
+// dropping / eigen-whitening), Q = Y Ry (orthonormal: the power iteration
+// re-orthonormalises after every application of A, so the condition number
+// never squares -- reference nla/svd.hpp:71-149), W = A^T Q -> WG[0 : n k],
+// and on the final pass G = Q^T Q (~ I: the core's second CholeskyQR step).
+// bf16 A: Q is split into bf16 hi / lo planes, and Q' = hi + lo is kept as
+// the stored basis so W, G and U = Q' M all see the same rows.
+int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
+  const int64_t m = p->m, n = p->n;
+  const int k = p->k;
+  int rc = chol_inv(p, p->WG + n * k, p->Ri, p->st + 10, s);
+  if (rc != SL_OK) return rc;
+  if (p->dt == SL_F64) {
+    rc = slb_gemm(SL_F64, false, false, m, k, k, 1.0, p->Y, k, p->Ri, k, 0.0, p->Qb, k, s);
+  } else {
+    k_cast2d<double, float><<<grid_of((int64_t)k * k), 256, 0, s>>>(p->Ri, k, k, k, (float*)p->Rf, k, nullptr);
+    SL_LAUNCH_CHECK();
+    rc = slb_gemm(SL_F32, false, false, m, k, k, 1.0, p->Y, k, p->Rf, k, 0.0, p->Qb, k, s);
+  }
+  if (rc != SL_OK) return rc;
+  (void)i;
+  if (p->dt == SL_BF16) {
+    k_split_bf16<<<grid_of(m * k), 256, 0, s>>>((float*)p->Qb, m * k, (bf16_t*)p->Yh, (bf16_t*)p->Yl);
+    SL_LAUNCH_CHECK();
+    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yh, k, 0.0, p->Wt, k, s);
+    if (rc != SL_OK) return rc;
+    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yl, k, 1.0, p->Wt, k, s);
+    if (rc != SL_OK) return rc;
+    k_cast2d<float, double><<<grid_of(n * k), 256, 0, s>>>((const float*)p->Wt, k, n, k, p->WG, k, nullptr);
+    SL_LAUNCH_CHECK();
+  } else {
+    // W = A^T Q as np row-chunk products (one strided-batched launch fills the
+    // chip; a single K = m product runs on a handful of workgroups), then one
+    // f64 sum of the partial slabs straight into WG
+    const size_t es = p->dt == SL_F64 ? 8 : 4;
+    const int64_t tot = n * k;
+    rc = slb_gemm_strided(p->dt, true, false, n, k, p->ch, 1.0, A, p->lda, p->ch * p->lda, p->Qb, k, p->ch * k, 0.0,
+                          p->parts, k, tot, p->np, s);
+    if (rc != SL_OK) return rc;
+    const int64_t r0 = p->ch * p->np;
+    int nparts = p->np;
+    if (r0 < m) {
+      rc = slb_gemm(p->dt, true, false, n, k, m - r0, 1.0, (const char*)A + r0 * p->lda * es, p->lda,
+                    (const char*)p->Qb + r0 * k * es, k, 0.0, (char*)p->parts + (int64_t)p->np * tot * es, k, s);
+      if (rc != SL_OK) return rc;
+      ++nparts;
+    }
+    rc = dispatch_dt(p->dt, [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      k_sum_parts<T><<<grid_of(tot), 256, 0, s>>>((const T*)p->parts, nparts, tot, p->WG, nullptr);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    });
+    if (rc != SL_OK) return rc;
+  }
+  if (!final_pass) return SL_OK;
+  return gram(p, p->Qb, p->WG + n * k, s);
 }
 
 // the boundary between pass i - 1 and pass i: CholeskyQR of the (all-reduced) W
@@ -435,25 +450,39 @@ int core(GPlan* p, hipStream_t s) {
     return SL_OK;
   });
   if (rc != SL_OK) return rc;
-  k_status_merge<<<1, 64, 0, s>>>(p->st + 4, 6, p->st);
+  k_status_merge<<<1, 64, 0, s>>>(p->st + 4, 8, p->st);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
+int nseg(const GPlan* p) { return 2 * p->q + 3; }
+
+// segment i of the call: even 2 j = [the boundary before pass j] + Y = A Z +
+// Y^T Y; odd 2 j + 1 = Q = Y R^{-1} + W = A^T Q (+ Q^T Q on the last pass);
+// the last = the core.  After segment i < nseg - 1, several ranks sum the
+// WG span reduce_span(i) (Y^T Y after an even segment, W (+ G) after an odd).
 int seg(GPlan* p, const void* A, int i, hipStream_t s) {
-  if (i < 0 || i > p->q + 1) { sl_set_last_error("rsvd_gen: segment out of range"); return SL_ERR_INVALID; }
-  int rc = SL_OK;
-  if (i == 0) {
-    SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 15 * sizeof(int), s));
+  if (i < 0 || i >= nseg(p)) { sl_set_last_error("rsvd_gen: segment out of range"); return SL_ERR_INVALID; }
+  if (i == nseg(p) - 1) return core(p, s);
+  const int j = i / 2;
+  if (i % 2) return apply_t(p, A, j == p->q, j, s);
+  int rc;
+  if (j == 0) {
+    SL_HIP_CHECK(hipMemsetAsync(p->st, 0, 16 * sizeof(int), s));
     rc = make_z(p, s);
-    if (rc != SL_OK) return rc;
-  } else if (i <= p->q) {
-    rc = inter(p, i, s);
-    if (rc != SL_OK) return rc;
   } else {
-    return core(p, s);
+    rc = inter(p, j, s);
   }
-  return pass(p, A, i == p->q, i == 0, s);
+  if (rc != SL_OK) return rc;
+  return apply_z(p, A, s);
+}
+
+void reduce_span(const GPlan* p, int i, int64_t* off, int64_t* cnt) {
+  const int64_t nk = p->n * p->k, kk = (int64_t)p->k * p->k;
+  if (i < 0 || i >= nseg(p) - 1) { *off = 0; *cnt = 0; return; }
+  if (i % 2 == 0) { *off = nk; *cnt = kk; return; }
+  *off = 0;
+  *cnt = (i / 2 == p->q) ? nk + kk : nk;
 }
 
 }  // namespace
@@ -483,6 +512,8 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   const int64_t o_yh = off;  off = align256(off + (dt == SL_BF16 ? m * k * 2 : 0));
   const int64_t o_yl = off;  off = align256(off + (dt == SL_BF16 ? m * k * 2 : 0));
   const int64_t o_w = off;   off = align256(off + n * k * (int64_t)ys);
+  const int64_t o_qb = off;  off = align256(off + m * k * (int64_t)ys);
+  const int64_t o_rf = off;  off = align256(off + (int64_t)k * k * 4);
   const int64_t o_wg = off;  off = align256(off + (n + k) * k * 8);
   const int64_t o_zf = off;  off = align256(off + n * k * 8);
   const int64_t o_h = off;   off = align256(off + (int64_t)k * k * 8);
@@ -514,6 +545,7 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   }
   char* b = p->base;
   p->Z = b + o_z; p->Y = b + o_y; p->Yh = b + o_yh; p->Yl = b + o_yl; p->Wt = b + o_w;
+  p->Qb = b + o_qb; p->Rf = b + o_rf;
   p->WG = (double*)(b + o_wg); p->Zf = (double*)(b + o_zf); p->H = (double*)(b + o_h); p->Ri = (double*)(b + o_ri);
   p->T1 = (double*)(b + o_t1); p->Cc = (double*)(b + o_c); p->eig = (double*)(b + o_e); p->M = (double*)(b + o_m);
   p->N = (double*)(b + o_n); p->Md = b + o_md; p->Vf = (double*)(b + o_vf); p->gws = b + o_gw;
@@ -576,6 +608,14 @@ SL_API int sl_rsvd_gen_bind(void* plan, double* WG, int* status) {
 }
 SL_API int* sl_rsvd_gen_status_ptr(void* plan) { return ((GPlan*)plan)->st; }
 
+// segments of one call (2 q + 3) and the WG span (f64 elements) that several
+// ranks sum after segment i (count 0: none)
+SL_API int sl_rsvd_gen_num_segments(void* plan) { return nseg((GPlan*)plan); }
+SL_API int sl_rsvd_gen_reduce_span(void* plan, int i, int64_t* off, int64_t* cnt) {
+  reduce_span((GPlan*)plan, i, off, cnt);
+  return SL_OK;
+}
+
 SL_API int sl_rsvd_gen_segment(void* plan, const void* A, int i, void* stream) {
   return seg((GPlan*)plan, A, i, (hipStream_t)stream);
 }
@@ -597,13 +637,13 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
     return SL_OK;
   });
   if (rc != SL_OK) return rc;
-  return slb_gemm(udt, false, false, p->m, r, k, 1.0, p->Y, k, p->Md, r, 0.0, U, ldu, s);   // U = Y M
+  return slb_gemm(udt, false, false, p->m, r, k, 1.0, p->Qb, k, p->Md, r, 0.0, U, ldu, s);   // U = Q M
 }
 
 // single rank: every segment, then the finish
 SL_API int sl_rsvd_gen_run(void* plan, const void* A, void* U, int64_t ldu, void* s, void* V, void* stream) {
   GPlan* p = (GPlan*)plan;
-  for (int i = 0; i <= p->q + 1; ++i) {
+  for (int i = 0; i < nseg(p); ++i) {
     const int rc = seg(p, A, i, (hipStream_t)stream);
     if (rc != SL_OK) return rc;
   }
@@ -615,12 +655,13 @@ SL_API int sl_rsvd_gen_run(void* plan, const void* A, void* U, int64_t ldu, void
 SL_API int sl_rsvd_gen_run_comm(void* plan, const void* A, void* comm, void* U, int64_t ldu, void* s, void* V,
                                 void* stream) {
   GPlan* p = (GPlan*)plan;
-  for (int i = 0; i <= p->q + 1; ++i) {
+  for (int i = 0; i < nseg(p); ++i) {
     int rc = seg(p, A, i, (hipStream_t)stream);
     if (rc != SL_OK) return rc;
-    if (i <= p->q && comm) {
-      const int64_t cnt = (i == p->q ? p->n + p->k : p->n) * p->k;
-      rc = sl_comm_all_reduce(comm, p->WG, p->WG, cnt, SL_F64, 0, stream);
+    int64_t off, cnt;
+    reduce_span(p, i, &off, &cnt);
+    if (cnt && comm) {
+      rc = sl_comm_all_reduce(comm, p->WG + off, p->WG + off, cnt, SL_F64, 0, stream);
       if (rc != SL_OK) return rc;
     }
   }

@@ -302,6 +302,7 @@ def _engine_lib():
         _lib.register("sl_rsvd_gen_set_dense", [vp_, i32_, u64_, u64_, f64_, f64_, f64_])
         _lib.register("sl_rsvd_gen_set_z", [vp_, vp_, vp_])
         _lib.register("sl_rsvd_gen_segment", [vp_, vp_, i32_, vp_])
+        _lib.register("sl_rsvd_gen_reduce_span", [vp_, i32_, ctypes.POINTER(i64_), ctypes.POINTER(i64_)])
         _lib.register("sl_rsvd_gen_finish", [vp_, vp_, i64_, vp_, vp_, vp_])
         _lib.register("sl_rsvd_gen_run", [vp_, vp_, vp_, i64_, vp_, vp_, vp_])
     return _lib
@@ -523,13 +524,16 @@ class _GenPlan(_EnginePlan):
     def _segments(self, A):
         L = _engine_lib()
         st = ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
-        for i in range(self.q + 2):
+        off, cnt = ctypes.c_int64(), ctypes.c_int64()
+        fn = L.require().sl_rsvd_gen_num_segments   # returns the count (not a status code)
+        fn.argtypes, fn.restype = [ctypes.c_void_p], ctypes.c_int
+        for i in range(fn(self.h)):
             with PROFILER.phase("svd.segment"):
                 L.call("sl_rsvd_gen_segment", self.h, ctypes.c_void_p(A.data_ptr()), i, st)
-            if i <= self.q:
-                cnt = (self.n + self.k if i == self.q else self.n) * self.k
+            L.call("sl_rsvd_gen_reduce_span", self.h, i, ctypes.byref(off), ctypes.byref(cnt))
+            if cnt.value:
                 with PROFILER.phase("svd.allreduce_small"):
-                    self.comm.all_reduce(self.WG[:cnt])
+                    self.comm.all_reduce(self.WG[off.value:off.value + cnt.value])
 
     def __call__(self, A, Z=None, fjlt=None, dense=None):
         L = _engine_lib()
