@@ -173,43 +173,55 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
 
 // ------------------------------------------------- tridiagonalisation
 // T = Q^T C Q, Q = H_0 H_1 ... H_{K-3}, H_j = I - 2 v_j v_j^T, by ONE wave:
-// lane i keeps row i of the trailing matrix in registers.  Step j: ||x||
-// of column j below the diagonal (DPP sum), v, p = A v (broadcast v through
-// LDS), K_j = v^T p (DPP sum), w = 2 (p - K_j v), A -= v w^T + w v^T.
+// lane i keeps row i of the trailing matrix in registers.  Step j:
+//   lane j alone: ||x||, alpha and the whole reflector v from its row j
+//     (x = A[j][j+1:]; norm and v from the same data keep H orthogonal --
+//     the register matrix is symmetric only to rounding), v -> LDS;
+//   every lane: p_i = (A v)_i, p -> LDS;
+//   every lane, redundantly: K_j = v^T p from the broadcast v and p (no
+//     cross-lane reduction on the chain), then A -= 2 v p^T + u v^T with
+//     u = 2 p - 4 K_j v  (= H A H).
 // Output: dd[0..K-1], ee[0..K-2] (ee[j] = T[j+1][j]), refl[i * ldr + j] =
 // (v_j)_i (zero for i <= j).  The k x k input C (ldc) is padded to K with
 // -beta on the diagonal (beta > ||C||_2), so the padding's eigenvalues sit
 // below every eigenvalue of C and the top ones are C's.
 template <int K, int J>
-__device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* wsh, double* refl, int ldr,
+__device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* psh, double* refl, int ldr,
                                          double* dd, double* ee) {
   constexpr int c0 = (J + 1) & ~1;
   if (J == 10) { SLW_STAMP(10) }
-  // ||x||^2 of column J below the diagonal and its first entry, from the
-  // column itself (lane i > J holds x_i): the rank-2 updates keep the
-  // register matrix symmetric only to rounding, and a norm taken from row J
-  // while v is built from column J left H non-orthogonal by eps ||A|| / ||x||
-  // (backward errors of 1e-12 on graded trailing blocks)
-  const double xi = (i > J) ? arow[J] : 0.0;
-  const double s2 = wave_sum(xi * xi);
-  const double x0 = lane_d(arow[J], J + 1);
-  const double sig2 = s2 - x0 * x0;
-  const bool refl_on = sig2 > 1e-300;
-  // sqrt(s2) as s2 / sqrt(s2) on the rsq estimate + Newton (shorter chain
-  // than the library sqrt's denormal-scaling sequence; s2 > 1e-300 here)
-  const double rs = rsq64(refl_on ? s2 : 1.0);
-  const double alpha = refl_on ? (x0 >= 0.0 ? -s2 * rs : s2 * rs) : x0;
-  const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
-  const double vi = (i > J) ? (xi - (i == J + 1 ? alpha : 0.0)) * rn : 0.0;
-  if (i == J) { dd[J] = arow[J]; ee[J] = alpha; }
-  if (i < K) {
-    vsh[i] = vi;
-    refl[i * ldr + J] = vi;
+  if (i == J) {
+    double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+    for (int c = J + 1; c < K; c += 2) {
+      q0 = fma(arow[c], arow[c], q0);
+      if (c + 1 < K) q1 = fma(arow[c + 1], arow[c + 1], q1);
+    }
+    const double s2 = q0 + q1;
+    const double x0 = arow[J + 1];
+    const bool refl_on = s2 - x0 * x0 > 1e-300;
+    // sqrt(s2) as s2 / sqrt(s2) on the rsq estimate + Newton (a shorter
+    // chain than the library sqrt's denormal-scaling sequence)
+    const double rs = rsq64(refl_on ? s2 : 1.0);
+    const double alpha = refl_on ? (x0 >= 0.0 ? -s2 * rs : s2 * rs) : x0;
+    const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
+    dd[J] = arow[J];
+    ee[J] = alpha;
+#pragma unroll
+    for (int c = c0; c < K; c += 2) {
+      double2 t;
+      t.x = c > J ? (arow[c] - (c == J + 1 ? alpha : 0.0)) * rn : 0.0;
+      t.y = c + 1 > J ? (arow[c + 1] - (c + 1 == J + 1 ? alpha : 0.0)) * rn : 0.0;
+      *(double2*)(vsh + c) = t;
+    }
   }
   wave_lds_sync();
   if (J == 10) { SLW_STAMP(11) }
   // p = A v, v streamed from LDS in pairs (entry J, when the first pair
   // starts there, has v_J = 0)
+  // (K >= 48: a compiler barrier per 16 entries keeps the streamed reads
+  // from all being hoisted ahead -- that spilled the K = 48 / 64 rows)
+  const double vi = (i > J && i < K) ? vsh[i] : 0.0;
   double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
   for (int c = c0; c < K; c += 4) {
@@ -221,22 +233,49 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
       p2 = fma(arow[c + 2], u.x, p2);
       p3 = fma(arow[c + 3], u.y, p3);
     }
+    if constexpr (K >= 48)
+      if (((c - c0) & 15) == 12) asm volatile("" ::: "memory");
   }
   const double p = (p0 + p1) + (p2 + p3);
-  if (J == 10) { SLW_STAMP(12) }
-  const double Kd = wave_sum(vi * p);
-  if (J == 10) { SLW_STAMP(13) }
-  const double wi = (i > J) ? 2.0 * (p - Kd * vi) : 0.0;
-  if (i < K) wsh[i] = wi;
+  if (i < K) {
+    psh[i] = p;
+    refl[i * ldr + J] = vi;
+  }
   wave_lds_sync();
+  if (J == 10) { SLW_STAMP(12) }
+  // K_J = v^T p in every lane from the broadcast pairs
+  double k0 = 0.0, k1 = 0.0, k2 = 0.0, k3 = 0.0;
+#pragma unroll
+  for (int c = c0; c < K; c += 4) {
+    const double2 tv = *(const double2*)(vsh + c);
+    const double2 tp = *(const double2*)(psh + c);
+    k0 = fma(tv.x, tp.x, k0);
+    k1 = fma(tv.y, tp.y, k1);
+    if (c + 2 < K) {
+      const double2 uv = *(const double2*)(vsh + c + 2);
+      const double2 up = *(const double2*)(psh + c + 2);
+      k2 = fma(uv.x, up.x, k2);
+      k3 = fma(uv.y, up.y, k3);
+    }
+    if (((c - c0) & 15) == 12) asm volatile("" ::: "memory");
+  }
+  const double Kd = (k0 + k1) + (k2 + k3);
+  // no reuse of the Kd loop's v / p registers in the update (re-read from
+  // LDS): keeping all of them live spilled the step's state to scratch
+  asm volatile("" ::: "memory");
+  if (J == 10) { SLW_STAMP(13) }
+  const double vi2 = 2.0 * vi;
+  const double ui = (i > J) ? fma(-4.0 * Kd, vi, 2.0 * p) : 0.0;
   if (J == 10) { SLW_STAMP(14) }
-  // A -= v w^T + w v^T on the trailing columns (v, w streamed again)
+  // A -= 2 v p^T + u v^T on the trailing columns (v, p streamed again)
 #pragma unroll
   for (int c = c0; c < K; c += 2) {
     const double2 tv = *(const double2*)(vsh + c);
-    const double2 tw = *(const double2*)(wsh + c);
-    arow[c] = fma(-vi, tw.x, fma(-wi, tv.x, arow[c]));
-    arow[c + 1] = fma(-vi, tw.y, fma(-wi, tv.y, arow[c + 1]));
+    const double2 tp = *(const double2*)(psh + c);
+    arow[c] = fma(-vi2, tp.x, fma(-ui, tv.x, arow[c]));
+    arow[c + 1] = fma(-vi2, tp.y, fma(-ui, tv.y, arow[c + 1]));
+    if constexpr (K >= 48)
+      if (((c - c0) & 15) == 14) asm volatile("" ::: "memory");
   }
   if (J == 10) { SLW_STAMP(15) }
 }
@@ -293,20 +332,34 @@ __device__ __forceinline__ void wave_tridiag(const double* C, int ldc, int k, do
 // zero -- counts as positive, i.e. the count of a point a rounding error
 // away.)
 template <int K, int P>
-__device__ __forceinline__ void sturm_counts(const double (&d)[K], const double (&e2)[K], const double (&x)[P],
-                                             int (&cnt)[P]) {
-  double p[P], pp[P];
+__device__ __forceinline__ void sturm_counts(const double2* de2, const double (&x)[P], int (&cnt)[P]) {
+  // (d_i, e_{i-1}^2) broadcast from LDS, fetched PF steps ahead into a
+  // register ring (a full register copy of T per lane -- 4 K VGPRs, the same
+  // values in every lane -- spilled the K >= 48 solvers)
+  constexpr int PF = 4;
+  double2 ring[PF];
 #pragma unroll
-  for (int q = 0; q < P; ++q) {
-    pp[q] = 1.0;
-    p[q] = d[0] - x[q];
-    cnt[q] = p[q] < 0.0;
+  for (int q = 0; q < PF; ++q)
+    if (q < K) ring[q] = de2[q];
+  double p[P], pp[P];
+  {
+    const double2 t0 = ring[0];
+    if (PF < K) ring[0] = de2[PF];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      pp[q] = 1.0;
+      p[q] = t0.x - x[q];
+      cnt[q] = p[q] < 0.0;
+    }
   }
 #pragma unroll
   for (int i = 1; i < K; ++i) {
+    const double2 t = ring[i % PF];
+    if (i + PF < K) ring[i % PF] = de2[i + PF];
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-      const double pn = fma(d[i] - x[q], p[q], -e2[i - 1] * pp[q]);
+      const double pn = fma(t.x - x[q], p[q], -t.y * pp[q]);
       cnt[q] += (pn < 0.0) != (p[q] < 0.0);
       pp[q] = p[q];
       p[q] = pn;
@@ -329,40 +382,55 @@ __device__ __forceinline__ double rcp64n(double d) {   // estimate + one Newton 
 
 // Eigenvector of the (scaled) tridiagonal T for the eigenvalue l by the
 // twisted factorisation T - l I = N_r D_r N_r^T, one lane per vector:
-// backward pivots D-_i and forward pivots D+_i (their reciprocals in
-// registers), the twist r = argmin |gamma_i|, then z by the two one-term
-// recurrences.  zdm receives z (unnormalised), zdp / zrd are scratch; the
-// return value is 1 / ||z||.  The LDS inputs are __restrict__: the loads of
-// d / e are then free to run ahead of the pivot stores (with may-alias LDS
-// pointers every step waited for its loads after the previous stores).
+// backward pivots D-_i and forward pivots D+_i, the twist r = argmin
+// |gamma_i|, then z by the two one-term recurrences.  zdm receives z
+// (unnormalised), zdp / zrd are scratch; the return value is 1 / ||z||.
+// The d / e operands (LDS broadcasts) are fetched PF steps ahead into a
+// register ring, with a compiler barrier per step: the pivot chain never
+// waits on an LDS round trip, and the loads are not all hoisted to the top
+// (which spilled the unrolled K = 40 chain to scratch).
 template <int K>
-__device__ __forceinline__ double twisted_vec(const double* __restrict__ dd, const double* __restrict__ ee, double l,
-                                              double* __restrict__ zdm, double* __restrict__ zdp,
-                                              double* __restrict__ zrd) {
+__device__ __forceinline__ void twisted_vec(const double* dd, const double* ee, double l, double* zdm, double* zdp,
+                                            double* zrd, int* rt_out) {
+  constexpr int PF = 4;
   const double pivmin = 1e-290;
-  double rup[K];
   double dm = dd[K - 1] - l;
   if (fabs(dm) < pivmin) dm = -pivmin;
   zdm[K - 1] = dm;
   double dp = dd[0] - l;
   if (fabs(dp) < pivmin) dp = -pivmin;
   zdp[0] = dp;
+  // ring slot q holds the operands of step s_ = q (mod PF)
+  double rb_e[PF], rb_d[PF], rf_e[PF], rf_d[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
+    if (q < K - 1) {
+      rb_e[q] = ee[K - 2 - q];
+      rb_d[q] = dd[K - 2 - q];
+      rf_e[q] = ee[q];
+      rf_d[q] = dd[q + 1];
+    }
 #pragma unroll
   for (int s_ = 0; s_ < K - 1; ++s_) {
-    const int ib = K - 2 - s_, jf = s_ + 1;
-    const double eb = ee[ib], ef = ee[jf - 1];
+    const int ib = K - 2 - s_, jf = s_ + 1, q = s_ % PF;
+    const double eb = rb_e[q], db = rb_d[q], ef = rf_e[q], df = rf_d[q];
+    if (s_ + PF < K - 1) {
+      rb_e[q] = ee[ib - PF];
+      rb_d[q] = dd[ib - PF];
+      rf_e[q] = ee[jf - 1 + PF];
+      rf_d[q] = dd[jf + PF];
+    }
+    asm volatile("" ::: "memory");
     const double rdm = rcp64n(dm);        // 1 / D-_{ib+1}
     zrd[ib + 1] = -eb * rdm;
-    dm = (dd[ib] - l) - (eb * eb) * rdm;
+    dm = (db - l) - (eb * eb) * rdm;
     if (fabs(dm) < pivmin) dm = -pivmin;
     zdm[ib] = dm;
     const double rdp = rcp64n(dp);        // 1 / D+_{jf-1}
-    rup[jf - 1] = rdp;
-    dp = (dd[jf] - l) - (ef * ef) * rdp;
+    dp = (df - l) - (ef * ef) * rdp;
     if (fabs(dp) < pivmin) dp = -pivmin;
     zdp[jf] = dp;
   }
-  rup[K - 1] = rcp64n(dp);
   // the twist: argmin |gamma_i|, gamma_i = D+_i + D-_i - (d_i - l)
   int rt = 0;
   double best = 1e300;
@@ -370,28 +438,30 @@ __device__ __forceinline__ double twisted_vec(const double* __restrict__ dd, con
   for (int i = 0; i < K; ++i) {
     const double gm = fabs(zdp[i] + zdm[i] - (dd[i] - l));
     if (gm < best) { best = gm; rt = i; }
+    if ((i & 7) == 7) asm volatile("" ::: "memory");
   }
-  // above the twist: z_i = -(e_i / D+_i) z_{i+1}; below: z_i = ratio_i z_{i-1}
-  double z = 1.0, nrm = 1.0;
+  // above the twist: z_i = -(e_i / D+_i) z_{i+1} (the reciprocals formed
+  // again here, off the z chain), into zdp; below: z_i = ratio_i z_{i-1},
+  // into zrd.  Branch-free: every lane runs both full recurrences with z
+  // held at 1 outside its range (a masked branch per entry cost more than
+  // the arithmetic); the caller picks zdp / 1 / zrd by the twist (*rt_out).
+  double z = 1.0;
 #pragma unroll
   for (int i = K - 2; i >= 0; --i) {
-    if (i < rt) {
-      z = -(ee[i] * rup[i]) * z;
-      nrm = fma(z, z, nrm);
-      zdm[i] = z;
-    }
+    const double f = -(ee[i] * rcp64n(zdp[i]));
+    z = i < rt ? f * z : 1.0;
+    zdp[i] = z;
+    if ((i & 7) == 0) asm volatile("" ::: "memory");
   }
   z = 1.0;
+  asm volatile("" ::: "memory");
 #pragma unroll
   for (int i = 1; i < K; ++i) {
-    if (i > rt) {
-      z = zrd[i] * z;
-      nrm = fma(z, z, nrm);
-      zdm[i] = z;
-    }
+    z = i > rt ? zrd[i] * z : 1.0;
+    zrd[i] = z;
+    if ((i & 7) == 7) asm volatile("" ::: "memory");
   }
-  zdm[rt] = 1.0;
-  return rsq64(nrm);
+  *rt_out = rt;
 }
 
 // Eigenpairs of the symmetric K x K matrix given by its tridiagonal form
@@ -409,7 +479,6 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
   __shared__ double s_scale;
   __shared__ int s_clus;
   __shared__ double2 de2[K];
-  __shared__ double snorm[64];
   SLW_STAMP(1)
   // ---- scale to ||T|| ~ 1 (Gershgorin radius)
   if (tid < 64) {
@@ -437,21 +506,19 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
   constexpr double CLUS = 1e-4;
   const int row = tid >> 4, g = tid & 15;
   constexpr int ROWS = NT / 16;
+  static_assert(NT % 256 == 0, "NT: whole groups of four waves");
+  // eigenvalue of this row: consecutive t go to consecutive SIMDs (wave w
+  // runs on SIMD w % 4), so the nt active rows load the 4 SIMDs evenly
+  // (row-major filled 2 : 2 : 1 : 1 waves per SIMD for nt = 21)
+  const int wv_ = row >> 2, tmap = (((wv_ >> 2) << 2) + (row & 3)) * 4 + (wv_ & 3);
   {
-    double d[K], e2[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const double2 q = de2[i];
-      d[i] = q.x;
-      e2[i] = i + 1 < K ? de2[i + 1].y : 0.0;
-    }
     for (int t0 = 0; t0 < nt; t0 += ROWS) {
-      const int t = t0 + row;
+      const int t = t0 + tmap;
       const bool act = t < nt;
       const int idx = K - 1 - t;   // ascending index of this row's eigenvalue
       double lo = -1.0 - 4.0 * eps, hi = 1.0 + 4.0 * eps;
       for (int it = 0; it < 64; ++it) {
-        // absolute accuracy eps ||T|| (||T|| = 1 after the scaling): what the
+        // absolute accuracy 2 eps ||T|| (||T|| = 1 after the scaling): what the
         // backward-stable reduction determines; resolving tiny eigenvalues to
         // full relative precision cost ~20 more bits (4 rounds)
         const bool conv = !act || (hi - lo) <= 4.0 * eps;
@@ -460,7 +527,7 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
         int c[MP];
 #pragma unroll
         for (int q = 0; q < MP; ++q) x[q] = lo + (hi - lo) * (double)(g * MP + q + 1) * (1.0 / (16 * MP + 1));
-        sturm_counts<K, MP>(d, e2, x, c);
+        sturm_counts<K, MP>(de2, x, c);
         // fewer than idx + 1 eigenvalues below x: x is a lower bound
         double nlo = lo, nhi = hi;
 #pragma unroll
@@ -501,15 +568,33 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     const double gap = fmin(t > 0 ? lam[t - 1] - l : 1e300, t + 1 < nt ? l - lam[t + 1] : 1e300);
     if (!(gap > 1e-13)) atomicOr(st, 1);       // numerically repeated (~ bisection accuracy): the caller falls back
     if (gap < CLUS) atomicOr(&s_clus, 1);
-    const double s = twisted_vec<K>(dd, ee, l, sc + t * LZ, sc + (nv + t) * LZ, sc + (2 * nv + t) * LZ);
-    if (!(s > 0.0) || !(s < 1e300)) atomicOr(st, 1);
-    snorm[t] = s;
-  }
-  __syncthreads();
-  if (tid < nv) {
-    const double s = snorm[tid];
+    int rt;
+    twisted_vec<K>(dd, ee, l, sc + t * LZ, sc + (nv + t) * LZ, sc + (2 * nv + t) * LZ, &rt);
+    // the normalised vector into sc[t * LZ + .] (its own lane's scratch):
+    // the pieces gathered and squared from LDS, then scaled (the norm summed
+    // inside the z recurrences held all of z live and spilled it)
+    asm volatile("" ::: "memory");
+    const double* za = sc + (nv + t) * LZ;
+    const double* zb = sc + (2 * nv + t) * LZ;
+    double n0 = 0.0, n1 = 0.0;
 #pragma unroll
-    for (int i = 0; i < K; ++i) sc[tid * LZ + i] *= s;
+    for (int i = 0; i < K; i += 2) {
+      const double a0 = i < rt ? za[i] : (i > rt ? zb[i] : 1.0);
+      const double a1 = i + 1 < rt ? za[i + 1] : (i + 1 > rt ? zb[i + 1] : 1.0);
+      sc[t * LZ + i] = a0;
+      sc[t * LZ + i + 1] = a1;
+      n0 = fma(a0, a0, n0);
+      n1 = fma(a1, a1, n1);
+      if ((i & 7) == 6) asm volatile("" ::: "memory");
+    }
+    const double s = rsq64(n0 + n1);
+    if (!(s > 0.0) || !(s < 1e300)) atomicOr(st, 1);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      sc[t * LZ + i] *= s;
+      if ((i & 7) == 7) asm volatile("" ::: "memory");
+    }
   }
   __syncthreads();
   SLW_STAMP(3)
