@@ -173,55 +173,43 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
 
 // ------------------------------------------------- tridiagonalisation
 // T = Q^T C Q, Q = H_0 H_1 ... H_{K-3}, H_j = I - 2 v_j v_j^T, by ONE wave:
-// lane i keeps row i of the trailing matrix in registers.  Step j:
-//   lane j alone: ||x||, alpha and the whole reflector v from its row j
-//     (x = A[j][j+1:]; norm and v from the same data keep H orthogonal --
-//     the register matrix is symmetric only to rounding), v -> LDS;
-//   every lane: p_i = (A v)_i, p -> LDS;
-//   every lane, redundantly: K_j = v^T p from the broadcast v and p (no
-//     cross-lane reduction on the chain), then A -= 2 v p^T + u v^T with
-//     u = 2 p - 4 K_j v  (= H A H).
+// lane i keeps row i of the trailing matrix in registers.  Step j: ||x||
+// of column j below the diagonal (DPP sum), v, p = A v (broadcast v through
+// LDS), K_j = v^T p (DPP sum), w = 2 (p - K_j v), A -= v w^T + w v^T.
 // Output: dd[0..K-1], ee[0..K-2] (ee[j] = T[j+1][j]), refl[i * ldr + j] =
 // (v_j)_i (zero for i <= j).  The k x k input C (ldc) is padded to K with
 // -beta on the diagonal (beta > ||C||_2), so the padding's eigenvalues sit
 // below every eigenvalue of C and the top ones are C's.
 template <int K, int J>
-__device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* psh, double* refl, int ldr,
+__device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* wsh, double* refl, int ldr,
                                          double* dd, double* ee) {
   constexpr int c0 = (J + 1) & ~1;
   if (J == 10) { SLW_STAMP(10) }
-  if (i == J) {
-    double q0 = 0.0, q1 = 0.0;
-#pragma unroll
-    for (int c = J + 1; c < K; c += 2) {
-      q0 = fma(arow[c], arow[c], q0);
-      if (c + 1 < K) q1 = fma(arow[c + 1], arow[c + 1], q1);
-    }
-    const double s2 = q0 + q1;
-    const double x0 = arow[J + 1];
-    const bool refl_on = s2 - x0 * x0 > 1e-300;
-    // sqrt(s2) as s2 / sqrt(s2) on the rsq estimate + Newton (a shorter
-    // chain than the library sqrt's denormal-scaling sequence)
-    const double rs = rsq64(refl_on ? s2 : 1.0);
-    const double alpha = refl_on ? (x0 >= 0.0 ? -s2 * rs : s2 * rs) : x0;
-    const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
-    dd[J] = arow[J];
-    ee[J] = alpha;
-#pragma unroll
-    for (int c = c0; c < K; c += 2) {
-      double2 t;
-      t.x = c > J ? (arow[c] - (c == J + 1 ? alpha : 0.0)) * rn : 0.0;
-      t.y = c + 1 > J ? (arow[c + 1] - (c + 1 == J + 1 ? alpha : 0.0)) * rn : 0.0;
-      *(double2*)(vsh + c) = t;
-    }
+  // ||x||^2 of column J below the diagonal and its first entry, from the
+  // column itself (lane i > J holds x_i): the rank-2 updates keep the
+  // register matrix symmetric only to rounding, and a norm taken from row J
+  // while v is built from column J left H non-orthogonal by eps ||A|| / ||x||
+  // (backward errors of 1e-12 on graded trailing blocks)
+  const double xi = (i > J) ? arow[J] : 0.0;
+  const double s2 = wave_sum(xi * xi);
+  const double x0 = lane_d(arow[J], J + 1);
+  const double sig2 = s2 - x0 * x0;
+  const bool refl_on = sig2 > 1e-300;
+  // sqrt(s2) as s2 / sqrt(s2) on the rsq estimate + Newton (shorter chain
+  // than the library sqrt's denormal-scaling sequence; s2 > 1e-300 here)
+  const double rs = rsq64(refl_on ? s2 : 1.0);
+  const double alpha = refl_on ? (x0 >= 0.0 ? -s2 * rs : s2 * rs) : x0;
+  const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
+  const double vi = (i > J) ? (xi - (i == J + 1 ? alpha : 0.0)) * rn : 0.0;
+  if (i == J) { dd[J] = arow[J]; ee[J] = alpha; }
+  if (i < K) {
+    vsh[i] = vi;
+    refl[i * ldr + J] = vi;
   }
   wave_lds_sync();
   if (J == 10) { SLW_STAMP(11) }
   // p = A v, v streamed from LDS in pairs (entry J, when the first pair
   // starts there, has v_J = 0)
-  // (K >= 48: a compiler barrier per 16 entries keeps the streamed reads
-  // from all being hoisted ahead -- that spilled the K = 48 / 64 rows)
-  const double vi = (i > J && i < K) ? vsh[i] : 0.0;
   double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
   for (int c = c0; c < K; c += 4) {
@@ -233,47 +221,26 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
       p2 = fma(arow[c + 2], u.x, p2);
       p3 = fma(arow[c + 3], u.y, p3);
     }
+    // (K >= 48: a compiler barrier per 16 entries keeps the streamed reads
+    // from all being hoisted ahead -- that spilled the K = 48 / 64 rows)
     if constexpr (K >= 48)
       if (((c - c0) & 15) == 12) asm volatile("" ::: "memory");
   }
   const double p = (p0 + p1) + (p2 + p3);
-  if (i < K) {
-    psh[i] = p;
-    refl[i * ldr + J] = vi;
-  }
-  wave_lds_sync();
   if (J == 10) { SLW_STAMP(12) }
-  // K_J = v^T p in every lane from the broadcast pairs
-  double k0 = 0.0, k1 = 0.0, k2 = 0.0, k3 = 0.0;
-#pragma unroll
-  for (int c = c0; c < K; c += 4) {
-    const double2 tv = *(const double2*)(vsh + c);
-    const double2 tp = *(const double2*)(psh + c);
-    k0 = fma(tv.x, tp.x, k0);
-    k1 = fma(tv.y, tp.y, k1);
-    if (c + 2 < K) {
-      const double2 uv = *(const double2*)(vsh + c + 2);
-      const double2 up = *(const double2*)(psh + c + 2);
-      k2 = fma(uv.x, up.x, k2);
-      k3 = fma(uv.y, up.y, k3);
-    }
-    if (((c - c0) & 15) == 12) asm volatile("" ::: "memory");
-  }
-  const double Kd = (k0 + k1) + (k2 + k3);
-  // no reuse of the Kd loop's v / p registers in the update (re-read from
-  // LDS): keeping all of them live spilled the step's state to scratch
-  asm volatile("" ::: "memory");
+  const double Kd = wave_sum(vi * p);
   if (J == 10) { SLW_STAMP(13) }
-  const double vi2 = 2.0 * vi;
-  const double ui = (i > J) ? fma(-4.0 * Kd, vi, 2.0 * p) : 0.0;
+  const double wi = (i > J) ? 2.0 * (p - Kd * vi) : 0.0;
+  if (i < K) wsh[i] = wi;
+  wave_lds_sync();
   if (J == 10) { SLW_STAMP(14) }
-  // A -= 2 v p^T + u v^T on the trailing columns (v, p streamed again)
+  // A -= v w^T + w v^T on the trailing columns (v, w streamed again)
 #pragma unroll
   for (int c = c0; c < K; c += 2) {
     const double2 tv = *(const double2*)(vsh + c);
-    const double2 tp = *(const double2*)(psh + c);
-    arow[c] = fma(-vi2, tp.x, fma(-ui, tv.x, arow[c]));
-    arow[c + 1] = fma(-vi2, tp.y, fma(-ui, tv.y, arow[c + 1]));
+    const double2 tw = *(const double2*)(wsh + c);
+    arow[c] = fma(-vi, tw.x, fma(-wi, tv.x, arow[c]));
+    arow[c + 1] = fma(-vi, tw.y, fma(-wi, tv.y, arow[c + 1]));
     if constexpr (K >= 48)
       if (((c - c0) & 15) == 14) asm volatile("" ::: "memory");
   }
@@ -495,54 +462,50 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     de2[tid] = double2{dd[tid] * itn, em * em};
   }
   __syncthreads();
-  // ---- multisection: 16 lanes (one DPP row) per eigenvalue, MP points per
-  //      lane (16 MP per round: bracket / (16 MP + 1) per round), rows of a
-  //      wave run independently; T in registers
+  // ---- multisection: 8 lanes (a DPP half-row) per eigenvalue, one point
+  //      per lane (bracket / 9 per round).  The Sturm count is issue-bound
+  //      (~9 VALU per point and step): 16 lanes x 2 points put 21 wanted
+  //      eigenvalues on 5.25 waves, two waves on some SIMD, for 5 bits per
+  //      round; 8 x 1 fits them on 3 waves (one per SIMD) for 3.2 bits per
+  //      round at a quarter of the issue per round (measured 58k -> see
+  //      profiles/r4).  T streamed from LDS.
   constexpr double eps = 2.220446049250313e-16;
-  constexpr int MP = 2;
+  constexpr int LPE = 8;
   // eigenvalues closer than CLUS (scaled: ||T|| = 1) are orthogonalised
   // against each other; farther apart the twisted vectors are orthogonal to
   // ~eps / gap < 1e-11 on their own
   constexpr double CLUS = 1e-4;
-  const int row = tid >> 4, g = tid & 15;
-  constexpr int ROWS = NT / 16;
+  const int row = tid / LPE, g = tid % LPE;
+  constexpr int ROWS = NT / LPE;
   static_assert(NT % 256 == 0, "NT: whole groups of four waves");
   // eigenvalue of this row: consecutive t go to consecutive SIMDs (wave w
-  // runs on SIMD w % 4), so the nt active rows load the 4 SIMDs evenly
-  // (row-major filled 2 : 2 : 1 : 1 waves per SIMD for nt = 21)
-  const int wv_ = row >> 2, tmap = (((wv_ >> 2) << 2) + (row & 3)) * 4 + (wv_ & 3);
+  // runs on SIMD w % 4), so the nt active rows fill one wave per SIMD first
+  const int wv_ = row >> 3, tmap = (((wv_ >> 2) << 3) + (row & 7)) * 4 + (wv_ & 3);
   {
     for (int t0 = 0; t0 < nt; t0 += ROWS) {
       const int t = t0 + tmap;
       const bool act = t < nt;
       const int idx = K - 1 - t;   // ascending index of this row's eigenvalue
       double lo = -1.0 - 4.0 * eps, hi = 1.0 + 4.0 * eps;
-      for (int it = 0; it < 64; ++it) {
+      for (int it = 0; it < 96; ++it) {
         // absolute accuracy 2 eps ||T|| (||T|| = 1 after the scaling): what the
         // backward-stable reduction determines; resolving tiny eigenvalues to
-        // full relative precision cost ~20 more bits (4 rounds)
+        // full relative precision cost ~20 more bits
         const bool conv = !act || (hi - lo) <= 4.0 * eps;
         if (__builtin_amdgcn_ballot_w64(!conv) == 0) break;
-        double x[MP];
-        int c[MP];
-#pragma unroll
-        for (int q = 0; q < MP; ++q) x[q] = lo + (hi - lo) * (double)(g * MP + q + 1) * (1.0 / (16 * MP + 1));
-        sturm_counts<K, MP>(de2, x, c);
+        double x[1];
+        int c[1];
+        x[0] = lo + (hi - lo) * (double)(g + 1) * (1.0 / (LPE + 1));
+        sturm_counts<K, 1>(de2, x, c);
         // fewer than idx + 1 eigenvalues below x: x is a lower bound
-        double nlo = lo, nhi = hi;
-#pragma unroll
-        for (int q = 0; q < MP; ++q) {
-          if (c[q] <= idx) nlo = fmax(nlo, x[q]);
-          else nhi = fmin(nhi, x[q]);
-        }
+        double nlo = c[0] <= idx ? fmax(lo, x[0]) : lo;
+        double nhi = c[0] <= idx ? hi : fmin(hi, x[0]);
         nlo = fmax(nlo, dpp<0xB1>(nlo));
         nhi = fmin(nhi, dpp<0xB1>(nhi));
         nlo = fmax(nlo, dpp<0x4E>(nlo));
         nhi = fmin(nhi, dpp<0x4E>(nhi));
         nlo = fmax(nlo, dpp<0x141>(nlo));
         nhi = fmin(nhi, dpp<0x141>(nhi));
-        nlo = fmax(nlo, dpp<0x140>(nlo));
-        nhi = fmin(nhi, dpp<0x140>(nhi));
         if (act && !conv) { lo = nlo; hi = nhi; }
       }
       if (act && g == 0) lam[t] = 0.5 * (lo + hi);   // scaled
