@@ -75,6 +75,43 @@ __device__ __forceinline__ void glds16s(unsigned voff, const void* sbase, unsign
       : "memory");
 }
 
+// the same two with the non-temporal hint (streaming reads of A that no
+// later pass re-reads from the caches)
+__device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+__device__ __forceinline__ void glds16s_nt(unsigned voff, const void* sbase, unsigned lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_base)
+      : "memory");
+}
+template <bool NTL>
+__device__ __forceinline__ void dma16s(unsigned voff, const void* sbase, unsigned lds_base) {
+  if constexpr (NTL) glds16s_nt(voff, sbase, lds_base);
+  else glds16s(voff, sbase, lds_base);
+}
+template <bool NTL>
+__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_base) {
+  if constexpr (NTL) glds16_nt(gsrc, lds_base);
+  else glds16(gsrc, lds_base);
+}
+
 // s_waitcnt vmcnt(n) for a run-time (wave-uniform) n
 __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {
@@ -133,7 +170,7 @@ __device__ __forceinline__ int swz4(int row) {
 __device__ __forceinline__ int qidx(int col, int q) { return col * 16 + 4 * (q ^ ((col >> 1) & 3)); }
 
 // FINAL: stored Y (ldy = KP) and, with GRAM, the fp64 Gram slab.  Otherwise W only.
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM>
+template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM, bool NTL>
 __global__ void __launch_bounds__(WAVES * 64, 1)
 k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const bf16_t* __restrict__ Zt, int k,
             float* __restrict__ Wslab, double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
@@ -221,7 +258,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 #pragma unroll
       for (int i = 0; i < G::LPB; ++i) {
         const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-        glds16s(voff[i], (const void*)base, dst);
+        dma16s<NTL>(voff[i], (const void*)base, dst);
       }
     } else {
 #pragma unroll
@@ -231,7 +268,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
         int64_t grow = r0 + row;
         grow = grow < m ? grow : m - 1;
         const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-        glds16((const void*)((const char*)(A + grow * lda) + (voff[i] - (unsigned)(row * lda * 2))), dst);
+        dma16<NTL>((const void*)((const char*)(A + grow * lda) + (voff[i] - (unsigned)(row * lda * 2))), dst);
       }
     }
   };
@@ -540,7 +577,8 @@ int launch_pass(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt
   using G = Geo4<WAVES, NW, KT, NBUF>;
   constexpr int LDS = pass_lds<WAVES, NW, KT, NBUF, FINAL, GRAM>();
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL, GRAM>;
+  auto kern = (variant & 16) ? k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL, GRAM, true>
+                             : k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL, GRAM, false>;
   SL_LDS_ATTR(kern, LDS);
   kern<<<grid, G::THREADS, LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch);
   SL_LAUNCH_CHECK();
@@ -594,7 +632,7 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   const bf16_t* z = (const bf16_t*)Zt;
   const int KT = (k + 15) / 16;
   const bool small = n <= 512;
-  const int nbuf = variant == 3 ? 3 : 4;
+  const int nbuf = (variant & 15) == 3 ? 3 : 4;
 #define SL_P(NW, KTT, NB)                                                                                    \
   return final_pass == 1 ? launch_pass<8, NW, KTT, NB, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
        : final_pass == 2 ? launch_pass<8, NW, KTT, NB, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
