@@ -1,6 +1,8 @@
-"""Breakdown of the random-feature GEMM (1e6 x 512 -> 4096): the fused
-kernel with/without the cos epilogue, f32 vs bf16 output, bf16 vs bf16x3
-operands, against hipBLASLt's bf16 GEMM alone.  One JSON line per variant."""
+"""Breakdown of the random-feature GEMM (1e6 x 512 -> 4096) on gemm_nt.hip's
+map epilogues: with/without the cos map, f32 vs bf16 output, bf16 vs bf16x3
+operands, rowwise vs columnwise (features along the output rows), the
+Gaussian-kernel Gram map, against hipBLASLt's bf16 GEMM alone.  One JSON line
+per variant."""
 from __future__ import annotations
 
 import json
@@ -42,6 +44,14 @@ def main():
         ("fused_bf16_cos_bf16out", lambda: F.feature_gemm(Ab, Ws, 1, scales=sc, shifts=sh, epi=F.EPI_COS,
                                                           use_lo=False, out_dtype=torch.bfloat16)),
         ("fused_f32x3_cos_f32out", lambda: F.feature_gemm(A, Ws, 1, scales=sc, shifts=sh, epi=F.EPI_COS)),
+        ("fused_f32x3_cos_f32out_columnwise", lambda: F.feature_gemm(A.t(), Ws, 0, scales=sc, shifts=sh,
+                                                                    epi=F.EPI_COS)),
+        ("fused_bf16_cos_bf16out_columnwise", lambda: F.feature_gemm(Ab.t(), Ws, 0, scales=sc, shifts=sh,
+                                                                     epi=F.EPI_COS, use_lo=False,
+                                                                     out_dtype=torch.bfloat16)),
+        ("fused_f32x3_gauss_gram_f32out", lambda: F.feature_gemm(A, Ws, 1, scales=2 * sc, shifts=-sc,
+                                                                 rowterm=-torch.ones(M, device=dev),
+                                                                 epi=F.EPI_GAUSS)),
         ("hipblaslt_bf16_gemm_f32out", lambda: torch.mm(Ab, Ws.hi[:N, :K].t(), out_dtype=torch.float32)),
         ("hipblaslt_bf16_gemm_bf16out", lambda: torch.mm(Ab, Ws.hi[:N, :K].t())),
     ]

@@ -23,8 +23,16 @@
 //     4 x 8 block of (row, column) tiles, so they share 4 A and 8 B panels
 //     in that XCD's L2 as the K slices advance;
 //   * epilogue straight from the C fragments: alpha * acc (optionally
-//     += into C), or the random-feature map outscale * cos(scale_f acc +
-//     shift_f), f32 or bf16 out.
+//     += into C), or a feature / kernel map of t = scale_f acc + shift_f
+//     (+ u_d): outscale * cos(t) (random Fourier features), exp(-acc)
+//     (Laplacian / exp-semigroup features), exp(min(t + u_d, 0)) (Gaussian
+//     kernel Gram: t = 2a x.y - a|y|^2, u = -a|x|^2), t^p (polynomial
+//     kernel); the feature index f runs along the columns (rowwise maps,
+//     C = X W^T) or, FROW, along the rows (columnwise maps, C = W X^T), the
+//     data index d along the other side.  f32 or bf16 out.
+//     (This kernel replaced feature_gemm.hip's 128 x 128 / 256 x 128 tiles
+//     for every map: the f32-exact products go in as hi / lo terms
+//     concatenated along K.)
 // Rows / columns past M / N are clamped on load and never stored; K must be
 // a multiple of 64 (callers zero-pad).
 #include "sl_common.hpp"
@@ -39,7 +47,26 @@ constexpr int OPB = BM * BK * 2;        // bytes of one operand slice (32 KB)
 constexpr int STAGE = 2 * OPB;          // A + B slice (64 KB)
 constexpr int GM = 4;                   // tile rows per XCD group
 
-enum { EPI_LINEAR = 0, EPI_COS = 1 };
+enum { EPI_LINEAR = 0, EPI_COS = 1, EPI_EXPNEG = 2, EPI_GAUSS = 3, EPI_POLY = 4 };
+
+// the map of one accumulator: s / t the feature's scale / shift, u the data
+// point's term, a = alpha (outscale)
+template <int EPI>
+__device__ __forceinline__ float epi_map(float acc, float a, float s, float t, float u, float p0) {
+  if constexpr (EPI == EPI_COS) {
+    // v_cos_f32 takes revolutions: reduce to [0, 1) with v_fract_f32 first
+    const float rev = __builtin_amdgcn_fractf((acc * s + t) * 0.15915494309189535f);
+    return a * __builtin_amdgcn_cosf(rev);
+  } else if constexpr (EPI == EPI_EXPNEG) {
+    return a * __expf(-acc);
+  } else if constexpr (EPI == EPI_GAUSS) {
+    return a * __expf(fminf(acc * s + t + u, 0.f));   // the squared distance can round below 0
+  } else if constexpr (EPI == EPI_POLY) {
+    return a * powf(acc * s + t, p0);
+  } else {
+    return a * acc;
+  }
+}
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
@@ -54,11 +81,11 @@ template <typename OutT> __device__ __forceinline__ float ld_out(const OutT* p);
 template <> __device__ __forceinline__ float ld_out<float>(const float* p) { return *p; }
 template <> __device__ __forceinline__ float ld_out<bf16_t>(const bf16_t* p) { return bf16_to_f(*p); }
 
-template <int EPI, typename OutT, bool ACC>
+template <int EPI, typename OutT, bool ACC, bool FROW>
 __global__ void __launch_bounds__(NT, 1)
 k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, int M, int N, int K,
           OutT* __restrict__ C, int64_t ldc, float alpha, const float* __restrict__ scales,
-          const float* __restrict__ shifts, int ntm, int ntn, int per) {
+          const float* __restrict__ shifts, const float* __restrict__ uterm, float p0, int ntm, int ntn, int per) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
 
   // ---- XCD-aware grouped tile order
@@ -144,13 +171,23 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
   //      so every store instruction writes 4 rows x 256 B (f32) / 128 B (bf16).
   constexpr int EP_LD = 68;
   float* ep = (float*)lds + w * (32 * EP_LD);
-  float csc[4], csh[4];
+  // per-column terms: the feature's scale / shift (rowwise maps) or the data
+  // point's term (FROW)
+  float csc[4], csh[4], cu[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = min(col0 + wn * 64 + j * 16 + fr, N - 1);
-    csc[j] = alpha;
+    csc[j] = 1.f;
     csh[j] = 0.f;
-    if (EPI == EPI_COS) { csc[j] = scales ? scales[col] : 1.f; csh[j] = shifts ? shifts[col] : 0.f; }
+    cu[j] = 0.f;
+    if constexpr (EPI != EPI_LINEAR) {
+      if constexpr (FROW) {
+        cu[j] = uterm ? uterm[col] : 0.f;
+      } else {
+        csc[j] = scales ? scales[col] : 1.f;
+        csh[j] = shifts ? shifts[col] : 0.f;
+      }
+    }
   }
   const int rr = lane >> 4, cq = (lane & 15) * 4;     // read-back: row rr + 4 u, columns cq .. cq + 3
   const int gcol = col0 + wn * 64 + cq;
@@ -159,17 +196,30 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
       const int i = 2 * pss + ii;
+      // per-row terms of this fragment row group: the data point's term
+      // (rowwise maps) or the feature's scale / shift (FROW)
+      float rs[4], rt[4], ru[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = min(row0 + wm * 128 + i * 16 + 4 * fq + e, M - 1);
+        rs[e] = 1.f;
+        rt[e] = 0.f;
+        ru[e] = 0.f;
+        if constexpr (EPI != EPI_LINEAR) {
+          if constexpr (FROW) {
+            rs[e] = scales ? scales[r] : 1.f;
+            rt[e] = shifts ? shifts[r] : 0.f;
+          } else if constexpr (EPI == EPI_GAUSS) {
+            ru[e] = uterm ? uterm[r] : 0.f;
+          }
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float v = acc[i][j][e];
-          if (EPI == EPI_COS) {
-            const float rev = __builtin_amdgcn_fractf((v * csc[j] + csh[j]) * 0.15915494309189535f);
-            v = alpha * __builtin_amdgcn_cosf(rev);
-          } else {
-            v *= csc[j];
-          }
+          const float v = FROW ? epi_map<EPI>(acc[i][j][e], alpha, rs[e], rt[e], cu[j], p0)
+                               : epi_map<EPI>(acc[i][j][e], alpha, csc[j], csh[j], ru[e], p0);
           ep[(ii * 16 + 4 * fq + e) * EP_LD + j * 16 + fr] = v;
         }
     }
@@ -216,16 +266,48 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
 
 
 
-template <int EPI, typename OutT, bool ACC>
+template <int EPI, typename OutT, bool ACC, bool FROW = false>
 int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, void* C, int64_t ldc,
-           float alpha, const float* scales, const float* shifts, hipStream_t s) {
+           float alpha, const float* scales, const float* shifts, hipStream_t s, const float* uterm = nullptr,
+           float p0 = 0.f) {
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   const int tiles = ntm * ntn;
   const int per = (tiles + 7) / 8;
-  k_gemm_nt<EPI, OutT, ACC><<<(unsigned)(per * 8), NT, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, M, N, K,
-                                                                (OutT*)C, ldc, alpha, scales, shifts, ntm, ntn, per);
+  k_gemm_nt<EPI, OutT, ACC, FROW><<<(unsigned)(per * 8), NT, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, M,
+                                                                      N, K, (OutT*)C, ldc, alpha, scales, shifts,
+                                                                      uterm, p0, ntm, ntn, per);
   SL_LAUNCH_CHECK();
   return SL_OK;
+}
+
+// f32 rows -> bf16 hi + lo planes (hi = rne(x), lo = rne(x - hi)), zero padded
+// to wpad columns, row stride ldp: one streaming pass, so the GEMM's K loop
+// carries no conversion work (the X operand is re-read by every feature tile)
+__global__ void __launch_bounds__(256)
+k_split_bf16(const float* __restrict__ A, int64_t M, int64_t K, int64_t lda, bf16_t* __restrict__ hi,
+             bf16_t* __restrict__ lo, int64_t ldp, int64_t wpad) {
+  const int64_t per_row = wpad / 4;
+  const int64_t total = M * per_row;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = t / per_row, k = (t - r * per_row) * 4;
+    float x[4];
+    if (k + 4 <= K && (lda & 3) == 0) {
+      const float4 v = *(const float4*)(A + r * lda + k);
+      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = (k + e < K) ? A[r * lda + k + e] : 0.f;
+    }
+    uint32_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      h[e] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x[e]);
+      const float res = x[e] - __uint_as_float(h[e] << 16);
+      l[e] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)res);
+    }
+    *(uint2*)(hi + r * ldp + k) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    *(uint2*)(lo + r * ldp + k) = make_uint2(l[0] | (l[1] << 16), l[2] | (l[3] << 16));
+  }
 }
 
 // Transposing bf16 hi / lo split of an f32 panel: X (w x m, ldx) ->
@@ -300,6 +382,59 @@ SL_API int sl_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ld
   }
   sl_set_last_error("gemm_nt_bf16: f32 / bf16 output");
   return SL_ERR_UNSUPPORTED;
+}
+
+// C (M x N, ldc) = map(A B^T) (see epi_map): epi 0 linear (alpha A B^T), 1
+// cos, 2 exp(-x), 3 Gaussian-kernel exp, 4 polynomial; scales / shifts per
+// feature, uterm per data point, frow = features along C's rows.
+SL_API int sl_gemm_nt_map(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, void* C,
+                          int64_t ldc, int out_dtype, int epi, int frow, float alpha, const float* scales,
+                          const float* shifts, const float* uterm, float p0, void* stream) {
+  if (M <= 0 || N <= 0) return SL_OK;
+  if (K <= 0 || K % BK || lda % 8 || ldb % 8 || lda < K || ldb < K || ldc < N) {
+    sl_set_last_error("gemm_nt_map: needs K % 64 == 0, lda / ldb multiples of 8 and >= K, ldc >= N");
+    return SL_ERR_INVALID;
+  }
+  if (epi < EPI_LINEAR || epi > EPI_POLY || (out_dtype != SL_F32 && out_dtype != SL_BF16)) {
+    sl_set_last_error("gemm_nt_map: epilogue 0..4, f32 / bf16 output");
+    return SL_ERR_INVALID;
+  }
+  hipStream_t s = (hipStream_t)stream;
+#define SL_GM(E, T, FR) \
+  return launch<E, T, false, FR>(A, lda, B, ldb, M, N, K, C, ldc, alpha, scales, shifts, s, uterm, p0)
+#define SL_GM_T(E, FR)                                    \
+  if (out_dtype == SL_F32) { SL_GM(E, float, FR); }       \
+  else { SL_GM(E, bf16_t, FR); }
+#define SL_GM_E(FR)                                       \
+  switch (epi) {                                          \
+    case EPI_LINEAR: SL_GM_T(EPI_LINEAR, FR)              \
+    case EPI_COS: SL_GM_T(EPI_COS, FR)                    \
+    case EPI_EXPNEG: SL_GM_T(EPI_EXPNEG, FR)              \
+    case EPI_GAUSS: SL_GM_T(EPI_GAUSS, FR)                \
+    default: SL_GM_T(EPI_POLY, FR)                        \
+  }
+  if (frow) { SL_GM_E(true) }
+  else { SL_GM_E(false) }
+#undef SL_GM_E
+#undef SL_GM_T
+#undef SL_GM
+}
+
+// hi / lo planes of width wpad (zero padded past K) with row stride ldp >= wpad
+SL_API int sl_split_bf16_2(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t wpad,
+                           int64_t ldp, void* stream) {
+  if (M <= 0) return SL_OK;
+  if (wpad % 4 != 0 || wpad < K || ldp < wpad || ldp % 4 != 0 || ((uintptr_t)hi & 7) || ((uintptr_t)lo & 7))
+    return SL_ERR_INVALID;
+  const unsigned grid = sl_grid_for((size_t)(M * (wpad / 4)), 256, 8192);
+  k_split_bf16<<<grid, 256, 0, (hipStream_t)stream>>>(A, M, K, lda, hi, lo, ldp, wpad);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+SL_API int sl_split_bf16(const float* A, int64_t M, int64_t K, int64_t lda, bf16_t* hi, bf16_t* lo, int64_t ldp,
+                         void* stream) {
+  return sl_split_bf16_2(A, M, K, lda, hi, lo, ldp, ldp, stream);
 }
 
 // Ht / Lt (m x wpad bf16, row stride ldt, wpad % 64 == 0, 16-B aligned rows)

@@ -1,16 +1,20 @@
-"""Fused dense-sketch / random-feature GEMM (``_native/src/feature_gemm.hip``).
+"""Fused dense-sketch / random-feature / kernel-Gram GEMM on the 256 x 256
+bf16 NT GEMM (``_native/src/gemm_nt.hip``, ``sl_gemm_nt_map``).
 
-``Z = outscale * epi(scale_f * (A W^T)[r, f] + shift_f)`` in one launch on
+``Z = outscale * map(scale_f * (A W^T)[r, f] + shift_f)`` in one launch on
 bf16 MFMA: f32 inputs are split once into bf16 hi + lo planes (one streaming
-pass, ``sl_split_bf16``) and the realised sketching matrix W is held as a
-bf16 hi + lo pair, so the 3-term product is f32-class accurate
-(|err| ~ 2^-16 of sum |a w|) at 3/16 of the bf16 MFMA cost.
+pass) and the realised sketching matrix W is held as a bf16 hi + lo pair; the
+3-term product ``Ah Wh + Al Wh + Ah Wl`` goes in as ONE GEMM over the terms
+concatenated along K (f32-class accuracy, |err| ~ 2^-16 of sum |a w|).
+Rowwise maps (dim 1) compute ``X W^T`` with the features along the output
+columns; columnwise maps (dim 0) compute ``W X^T`` with the features along
+the output rows (the kernel's FROW epilogue), no transposed copy of Z.
 
-Used by the dense transforms (JLT / CT / SJLT, ``epi = none``) and the
-feature maps (RFT / QRFT ``cos``, RLT / QRLT ``exp(-x)``) whenever the
-sketched dimension is small enough for W (``S x N``) to be realised once and
-cached on the device (``MAX_W_ELEMS``); tall sketched dimensions stream W
-panels through ``ops.dense_sketch`` instead.
+Used by the dense transforms (JLT / CT / SJLT, ``map = none``), the feature
+maps (RFT / QRFT ``cos``, RLT / QRLT ``exp(-x)``) and the Gaussian /
+polynomial kernel Grams (``ml.kernels``) whenever W (``S x N``) is small
+enough to realise once and cache on the device (``MAX_W_ELEMS``); tall
+sketched dimensions stream W panels through ``ops.dense_sketch`` instead.
 """
 from __future__ import annotations
 
@@ -22,20 +26,17 @@ import torch
 from . import _lib
 
 EPI_NONE, EPI_COS, EPI_EXPNEG, EPI_GAUSS, EPI_POLY = 0, 1, 2, 3, 4
-BN, BK = 128, 32
+BN, BK = 128, 32                # SplitW padding of W (rows, K)
 MAX_W_ELEMS = 1 << 26          # W (S x N) realised whole up to 64 M entries (256 MB as hi+lo)
 
-_lib.register("sl_feature_gemm", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
-                                  C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
-                                  C.c_void_p, C.c_void_p, C.c_float, C.c_int,
-                                  C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p])
-_lib.register("sl_feature_gemm2", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
-                                   C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
-                                   C.c_void_p, C.c_void_p, C.c_float, C.c_int,
-                                   C.c_void_p, C.c_int, C.c_int64, C.c_int, C.c_void_p, C.c_float, C.c_void_p])
+_lib.register("sl_gemm_nt_map", [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                 C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_float,
+                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p])
 _lib.register("sl_split_bf16", [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                 C.c_void_p])
 _lib.register("sl_split_bf16_2", [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                  C.c_int64, C.c_void_p])
+_lib.register("sl_split_bf16_t", [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
                                   C.c_int64, C.c_void_p])
 
 
@@ -88,99 +89,68 @@ class SplitW:
         return B
 
 
-def split_planes(X: torch.Tensor):
-    """Row-major bf16 operand planes for the kernel: ``(hi, lo, ld)`` with
-    ``ld`` a multiple of 32 and zero padding.  f32 input -> hi + lo (one
-    ``sl_split_bf16`` streaming pass; x = hi + lo to ~2^-17); bf16 input ->
-    the data itself (lo = None), copied only when its rows are not padded."""
+def _x_terms(X: torch.Tensor, use_lo: bool):
+    """The data operand as bf16 terms concatenated along K: ``(P, terms_W)``
+    with ``P = [X_h | X_l | X_h]`` (f32 X; ``[X_h | X_l]`` without W's lo
+    plane) or ``[X | X]`` / ``[X]`` (bf16 X), each term ``kp`` wide (k
+    rounded up to 64, zero padded), and the matching W terms."""
     m, k = X.shape
-    ld = -(-k // BK) * BK
+    kp = -(-k // 64) * 64
     dev = X.device
-    if X.dtype == torch.bfloat16:
-        if X.stride(1) == 1 and X.stride(0) == ld and X.data_ptr() % 16 == 0 and ld == k:
-            return X, None, ld
-        buf = torch.zeros(m, ld, dtype=torch.bfloat16, device=dev)
-        buf[:, :k] = X
-        return buf, None, ld
-    if X.stride(1) != 1:
-        X = X.contiguous()
-    hi = torch.empty(m, ld, dtype=torch.bfloat16, device=dev)
-    lo = torch.empty(m, ld, dtype=torch.bfloat16, device=dev)
-    _lib.call("sl_split_bf16", _lib.ptr(X), m, k, X.stride(0), _lib.ptr(hi), _lib.ptr(lo), ld,
-              C.c_void_p(_lib.stream_of(X)))
-    return hi, lo, ld
+    if X.dtype == torch.float32:
+        ta, tb = (("h", "l", "h"), ("h", "h", "l")) if use_lo else (("h", "l"), ("h", "h"))
+    else:
+        ta, tb = (("h", "h"), ("h", "l")) if use_lo else (("h",), ("h",))
+    P = torch.empty(m, len(ta) * kp, dtype=torch.bfloat16, device=dev)
+    st = C.c_void_p(_lib.stream_of(X))
+    if X.dtype == torch.float32:
+        if X.stride(1) != 1 and X.stride(0) == 1 and X.t().stride(0) % 4 == 0:
+            # X = A^T of a row-major A (k x m): the transposing split reads A directly
+            At = X.t()
+            _lib.call("sl_split_bf16_t", _lib.ptr(At), k, m, At.stride(0), _lib.ptr(P), _lib.ptr(P[:, kp:]), kp,
+                      P.stride(0), st)
+        else:
+            Xc = X if (X.stride(1) == 1 and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0) else X.contiguous()
+            _lib.call("sl_split_bf16_2", _lib.ptr(Xc), m, k, Xc.stride(0), _lib.ptr(P), _lib.ptr(P[:, kp:]), kp,
+                      P.stride(0), st)
+        if len(ta) == 3:
+            P[:, 2 * kp:].copy_(P[:, :kp])
+    else:
+        P[:, :k] = X
+        if kp > k:
+            P[:, k:kp].zero_()
+        for i in range(1, len(ta)):
+            P[:, i * kp:(i + 1) * kp].copy_(P[:, :kp])
+    return P, tb
 
 
 def feature_gemm(A: torch.Tensor, W: SplitW, dim: int, *, scales=None, shifts=None,
                  outscale: float = 1.0, epi: int = EPI_NONE, out_dtype=torch.float32,
                  use_lo: bool = True, rowterm=None, p0: float = 0.0) -> torch.Tensor:
     """Columnwise (dim 0: A is K x m -> Z is nf x m) or rowwise (dim 1: A is
-    m x K -> Z is m x nf) fused product with W^T and the epilogue."""
+    m x K -> Z is m x nf) fused product with W^T and the map; ``rowterm`` is
+    the per-data-point term of the Gaussian Gram."""
     X = A if dim == 1 else A.t()
     m, k = X.shape
     if k != W.k:
         raise ValueError(f"feature_gemm: inner dimension {k} != {W.k}")
-    if dim == 1 and epi in (EPI_NONE, EPI_COS) and rowterm is None and _gemm_nt_ok(X):
-        return _feature_gemm_nt(X, W, scales, shifts, outscale, epi, out_dtype, use_lo)
-    hi, lo, ld = split_planes(X)
+    P, tb = _x_terms(X, use_lo)
+    B = W.concat(tb)
     dev = A.device
-    if dim == 1:
-        out = torch.empty(m, W.nf, dtype=out_dtype, device=dev)
-        ldo, out_t = W.nf, 0
-    else:
-        out = torch.empty(W.nf, m, dtype=out_dtype, device=dev)
-        ldo, out_t = m, 1
     sc = scales.to(device=dev, dtype=torch.float32).contiguous() if scales is not None else None
     sh = shifts.to(device=dev, dtype=torch.float32).contiguous() if shifts is not None else None
-    if W.ldw != ld:
-        raise ValueError("feature_gemm: W and A planes must share the padded inner dimension")
     rt = rowterm.to(device=dev, dtype=torch.float32).contiguous() if rowterm is not None else None
-    _lib.call("sl_feature_gemm2", _lib.ptr(hi), _lib.ptr(lo) if lo is not None else None, m, k, ld,
-              _lib.ptr(W.hi), _lib.ptr(W.lo) if use_lo else None, W.nf, W.ldw,
+    if dim == 1:
+        out = torch.empty(m, W.nf, dtype=out_dtype, device=dev)
+        Aop, Bop, M, N = P, B, m, W.nf
+    else:
+        out = torch.empty(W.nf, m, dtype=out_dtype, device=dev)
+        Aop, Bop, M, N = B, P, W.nf, m
+    _lib.call("sl_gemm_nt_map", _lib.ptr(Aop), Aop.stride(0), _lib.ptr(Bop), Bop.stride(0), M, N, P.shape[1],
+              _lib.ptr(out), out.stride(0), _lib.dtype_code(out_dtype), int(epi), int(dim == 0), float(outscale),
               _lib.ptr(sc) if sc is not None else None, _lib.ptr(sh) if sh is not None else None,
-              float(outscale), int(epi), _lib.ptr(out), _lib.dtype_code(out_dtype), ldo, out_t,
               _lib.ptr(rt) if rt is not None else None, float(p0), C.c_void_p(_lib.stream_of(out)))
     return out
-
-
-# rowwise linear / cosine maps on the 256 x 256 NT GEMM (gemm_nt.hip) with
-# the hi / lo terms concatenated along K (one launch, no per-term passes)
-def _gemm_nt_ok(X):
-    return X.stride(1) == 1 and X.dtype in (torch.float32, torch.bfloat16)
-
-
-def _feature_gemm_nt(X, W, scales, shifts, outscale, epi, out_dtype, use_lo):
-    """``[X_h | X_l | X_h] [W_h | W_h | W_l]^T`` (f32 X; bf16 X: ``[X | X]
-    [W_h | W_l]^T``, or one term without W's lo plane) with the epilogue."""
-    from . import gemm as _g
-    m, k = X.shape
-    kp = -(-k // 64) * 64
-    if X.dtype == torch.float32:
-        ta, tb = ("h", "l", "h"), ("h", "h", "l")
-        if not use_lo:
-            ta, tb = ("h", "l"), ("h", "h")
-    else:
-        ta, tb = (("h", "h"), ("h", "l")) if use_lo else (("h",), ("h",))
-    Ap = torch.empty(m, len(ta) * kp, dtype=torch.bfloat16, device=X.device)
-    if X.dtype == torch.float32:
-        Xc = X if X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0 else X.contiguous()
-        _lib.call("sl_split_bf16_2", _lib.ptr(Xc), m, k, Xc.stride(0), _lib.ptr(Ap), _lib.ptr(Ap[:, kp:]), kp,
-                  Ap.stride(0), C.c_void_p(_lib.stream_of(X)))
-        if len(ta) == 3:
-            Ap[:, 2 * kp:].copy_(Ap[:, :kp])
-    else:
-        Ap[:, :k] = X
-        if kp > k:
-            Ap[:, k:kp].zero_()
-        for i in range(1, len(ta)):
-            Ap[:, i * kp:(i + 1) * kp].copy_(Ap[:, :kp])
-    B = W.concat(tb)
-    out = torch.empty(m, W.nf, dtype=out_dtype, device=X.device)
-    if epi == EPI_COS:
-        sc = scales if scales is not None else torch.ones(W.nf, device=X.device)
-        sh = shifts if shifts is not None else torch.zeros(W.nf, device=X.device)
-        return _g.gemm_nt(Ap, B, out=out, alpha=outscale, cos_scales=sc.to(X.device), cos_shifts=sh.to(X.device))
-    return _g.gemm_nt(Ap, B, out=out, alpha=outscale)
 
 
 class WCache:

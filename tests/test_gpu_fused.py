@@ -1,4 +1,4 @@
-"""Fused dense-sketch / random-feature MFMA GEMM (feature_gemm.hip) vs fp64
+"""Fused dense-sketch / random-feature / kernel-Gram maps on the NT GEMM (gemm_nt.hip, sl_gemm_nt_map) vs fp64
 torch references of the same op."""
 import math
 
