@@ -159,10 +159,9 @@ def test_lsrn_gpu_preconditioner_paths(dev, cond, dt):
     assert res < 1e-4, (res, code)
 
 
-@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("dim", [0, 1])
 @pytest.mark.parametrize("block", [0, 1000, 1003])
-def test_dense_sketch_bf16x2_panels(dev, dim, block, native):
+def test_dense_sketch_bf16x2_panels(dev, dim, block):
     """LSRN's internal sketch: bf16-realised S panels times the
     bf16 hi/lo split of f32 A (sl_split_bf16) in reused buffers; equals
     S_bf16 @ A to ~2^-16 for one or many panels (block 1003: ragged, the
@@ -172,15 +171,13 @@ def test_dense_sketch_bf16x2_panels(dev, dim, block, native):
     N, S, M = 4100, 96, 333
     T = sk.sketch.JLT(N, S, context=sk.Context(21))
     A = torch.randn(N, M, device=dev) if dim == 0 else torch.randn(M, N, device=dev)
-    old, old_native = params.get_blocksize(), DS.USE_NATIVE_GEMM
+    old = params.get_blocksize()
     params.set_blocksize(block)
-    DS.USE_NATIVE_GEMM = native       # gemm_nt.hip panels / hipBLASLt panels
     try:
         out = DS.apply_dense(A, dim, dist=T.dist, seed=T.entries.seed, base=T.entries.base, S=S, N=N,
                              scale=T.scale, precision="bf16x2")
     finally:
         params.set_blocksize(old)
-        DS.USE_NATIVE_GEMM = old_native
     Sb = DS.realize_panel(T.dist, T.entries.seed, T.entries.base, S, (0, S), (0, N), scale=T.scale,
                           dtype=torch.bfloat16, device=dev).double()
     ref = Sb @ A.double() if dim == 0 else A.double() @ Sb.t()
