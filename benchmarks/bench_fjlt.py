@@ -52,7 +52,10 @@ def main():
         return fut.fjlt_fourstep(A, d, smp, scale)
 
     ref = old().double()
+    only = os.environ.get("VARIANTS")
     for name, fn in (("torch_dct_gather", old), ("fused_rfft_sampled", rfft), ("fourstep_sampled", new)):
+        if only and name not in only.split(","):
+            continue
         err = float((fn().double() - ref).norm() / ref.norm())
         t = timeit(fn)
         print(json.dumps({"bench": "fjlt_sampled", "variant": name, "m": m, "n": n, "S": S, "ms": round(t * 1e3, 3),
