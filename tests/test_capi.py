@@ -867,7 +867,12 @@ def test_host_operands_on_device_interpreter_free(capi, tmp_path):
     Vr, sr = sk.nla.approximate_symmetric_svd(torch.from_numpy(Sy), 8, ctx, sk.nla.ApproximateSVDParams(num_iterations=2))
     np.testing.assert_allclose(ld("sym_S", (8,)), sr.numpy(), rtol=1e-9, atol=1e-12)
     Vc = ld("sym_V", (400, 8))
-    np.testing.assert_allclose(Vc @ Vc.T, Vr.numpy() @ Vr.numpy().T, atol=1e-8)
+    # the rank-12 indefinite matrix has 6 positive eigenvalues: the top 8 by
+    # signed value end in its null space, where any orthonormal pair is right;
+    # the well-determined columns span the same subspace
+    good = int((np.abs(sr.numpy()) > 1e-8 * abs(float(sr[0]))).sum())
+    Vg, Vrg = Vc[:, :good], Vr.numpy()[:, :good]
+    np.testing.assert_allclose(Vg @ Vg.T, Vrg @ Vrg.T, atol=1e-8)
     LA, Lb = ld("ls_A", (3000, 60)), ld("ls_b", (3000, 2))
     X = np.linalg.lstsq(LA, Lb, rcond=None)[0]
     np.testing.assert_allclose(ld("ls_x", (60, 2)), X, rtol=1e-9, atol=1e-11)
