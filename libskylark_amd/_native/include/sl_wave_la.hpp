@@ -136,7 +136,7 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
     const bool ok = (d > thr && d == d) || j >= k;
     bad |= !ok;
     const double r = ok ? rcp64(d) : 0.0;
-    if (c == 0) rsh[j] = ok ? rsq64(d) : 0.0;
+    if (c == 0) rsh[j] = ok ? d : 0.0;      // d_j^{-1/2} formed after the loop (off the pivot chain)
     if (j + 1 < K) {
       double* fb_ = fsh + (j & 1) * 64;   // double-buffered: no second sync per step
       fb_[c] = A[j] * r;    // multiplier of row c (valid for c > j)
@@ -160,6 +160,11 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
     if (c == j) A[j] = 1.0;
   }
   if (bad && c == 0) atomicOr(st, 1);
+  wave_lds_sync();
+  if (c < K) {
+    const double dj = rsh[c];
+    rsh[c] = dj > 0.0 ? rsq64(dj) : 0.0;
+  }
   wave_lds_sync();
   if (c < k) {
 #pragma unroll
@@ -424,7 +429,8 @@ __device__ __forceinline__ void twisted_vec(const double* dd, const double* ee, 
   asm volatile("" ::: "memory");
 #pragma unroll
   for (int i = 1; i < K; ++i) {
-    z = i > rt ? zrd[i] * z : 1.0;
+    const double rd = zrd[i];           // loaded unconditionally: a load inside the select
+    z = i > rt ? rd * z : 1.0;          // became a branch with an LDS round trip per entry
     zrd[i] = z;
     if ((i & 7) == 7) asm volatile("" ::: "memory");
   }
@@ -542,8 +548,9 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     double n0 = 0.0, n1 = 0.0;
 #pragma unroll
     for (int i = 0; i < K; i += 2) {
-      const double a0 = i < rt ? za[i] : (i > rt ? zb[i] : 1.0);
-      const double a1 = i + 1 < rt ? za[i + 1] : (i + 1 > rt ? zb[i + 1] : 1.0);
+      const double xa0 = za[i], xb0 = zb[i], xa1 = za[i + 1], xb1 = zb[i + 1];
+      const double a0 = i < rt ? xa0 : (i > rt ? xb0 : 1.0);
+      const double a1 = i + 1 < rt ? xa1 : (i + 1 > rt ? xb1 : 1.0);
       sc[t * LZ + i] = a0;
       sc[t * LZ + i + 1] = a1;
       n0 = fma(a0, a0, n0);
