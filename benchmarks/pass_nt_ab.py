@@ -34,11 +34,16 @@ def main():
     dense = base[:, :n].contiguous()
     st = vp(torch.cuda.current_stream().cuda_stream)
     cases = []
-    for lda in (1000, 1024):
-        A = dense if lda == 1000 else base
-        for nt in (0, 16):
-            for final in (0, 1):
-                cases.append((lda, nt, final, A))
+    if os.environ.get("FINAL_AB"):
+        # same-box A/B of the last-pass forms: W only / + Y / + Y + in-pass Gram
+        for final in (0, 2, 1):
+            cases.append((1000, 0, final, dense))
+    else:
+        for lda in (1000, 1024):
+            A = dense if lda == 1000 else base
+            for nt in (0, 16):
+                for final in (0, 1):
+                    cases.append((lda, nt, final, A))
     times = {c[:3]: [] for c in cases}
     for rnd in range(5):
         for lda, nt, final, A in cases:

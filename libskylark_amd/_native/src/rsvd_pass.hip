@@ -143,6 +143,7 @@ struct Geo4 {
   static constexpr int PART = WAVES * KP * BM * 4; // per-wave partial y tiles (f32, [w][col][row])
   static constexpr int Y16P = KP * BM * 2 + 16;    // bytes per part (hi / lo) of the bf16 y image
   static constexpr int Y16 = 2 * Y16P;
+  static constexpr int YF = BM * KP * 4;           // FINAL: the block's stored Y rows ([row][k] f32)
   static constexpr int CPW = KP / WAVES;           // y columns reduced per wave
   static constexpr int RL = CPW * 4;               // reducer lanes per wave (one row quad each)
   static constexpr int GT = KT * (KT + 1) / 2;     // upper 16 x 16 Gram tiles
@@ -152,7 +153,7 @@ struct Geo4 {
 template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM = FINAL>
 constexpr int pass_lds() {
   using G = Geo4<WAVES, NW, KT, NBUF>;
-  return G::RING + G::PART + G::Y16;
+  return G::RING + G::PART + G::Y16 + (FINAL ? G::YF : 0);
 }
 
 // swizzle of 16-B chunk slots by row (see tsk_kernels.hip: a GF(2) map that
@@ -182,6 +183,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
   char* ring = smem;
   float* part = (float*)(smem + G::RING);
   char* y16 = smem + G::RING + G::PART;
+  float* yf = (float*)(smem + G::RING + G::PART + G::Y16);
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -275,7 +277,15 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 
   // reducer role of this lane: row quad rq of y column rc
   const int rc = w * G::CPW + (lane >> 2), rq = lane & 3;
-  constexpr int NST = FINAL ? 4 : 0;   // Y stores per wave per block (vmcnt bookkeeping)
+  // FINAL: the block's Y rows are one contiguous k * 16-float chunk when
+  // ldy == k: the reducers stage y' in LDS and the first waves write it as
+  // float4 rows (one store instruction per wave) instead of four scattered
+  // 4-B stores per reducer lane
+  const bool vecY = FINAL && (k % 4 == 0) && (ldy == k);
+  const int nvec = BM * k / 4;
+  // Y store instructions per wave per block (vmcnt bookkeeping: exact, every
+  // store issues even for rows past m -- they go to the scratch line)
+  const int nst = !FINAL ? 0 : (vecY ? (w * 64 < nvec ? 1 : 0) : 4);
 
 #ifdef SL_PASS_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
@@ -307,7 +317,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       const int64_t ydma = nloc - 1 - j;
       const int nd = (int)(ydma < NBUF - 1 ? ydma : NBUF - 1);
       const int ns = (int)(j < NBUF - 1 ? j : NBUF - 1);
-      wait_vm(nd * G::LPB + ns * NST);
+      wait_vm(nd * G::LPB + ns * nst);
     }
     SL_STAMP(1)
     const char* region = ring + (slot * WAVES + w) * G::REGION;
@@ -357,17 +367,34 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       if constexpr (FINAL) {
         // the stored Y is y' = y_hi + y_lo (exact in f32): the rows W and
         // the in-pass Gram are formed from, so Y, W and G stay consistent
+        if (vecY) {
+          if (rc < k) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t row = r0 + 4 * rq + e;
-          float* dst = (row < m && rc < k) ? Y + row * ldy + rc : scratch + lane;
-          *dst = bf16_val(hi[e]) + bf16_val(lo[e]);
+            for (int e = 0; e < 4; ++e) yf[(4 * rq + e) * k + rc] = bf16_val(hi[e]) + bf16_val(lo[e]);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t row = r0 + 4 * rq + e;
+            float* dst = (row < m && rc < k) ? Y + row * ldy + rc : scratch + lane;
+            *dst = bf16_val(hi[e]) + bf16_val(lo[e]);
+          }
         }
       }
     }
     SL_STAMP(4)
     lds_barrier();   // (B) y of block j is complete
     SL_STAMP(5)
+    if (FINAL && vecY && w * 64 < nvec) {
+      // one float4 per lane of the block's contiguous Y image (ragged rows /
+      // idle lanes write the scratch line: the store count stays exact)
+      const int t = w * 64 + lane;
+      const bool ok = t < nvec && r0 + (4 * t) / k < m;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (ok) v = *(const f32x4*)&yf[4 * t];
+      float* dst = ok ? Y + r0 * ldy + 4 * t : scratch + 4 * lane;
+      *(f32x4*)dst = v;
+    }
 
     SL_STAMP(6)
 
