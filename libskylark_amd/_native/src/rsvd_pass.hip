@@ -393,7 +393,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (ok) v = *(const f32x4*)&yf[4 * t];
       float* dst = ok ? Y + r0 * ldy + 4 * t : scratch + 4 * lane;
-      *(f32x4*)dst = v;
+      *(f32x4*)dst = v;   // (a non-temporal store measured 507 vs 446 us for the pass)
     }
 
     SL_STAMP(6)
