@@ -84,18 +84,38 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
     }
   }
   const int64_t nblk = (m + BM - 1) / BM;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int64_t r0 = blk * BM;
-    float a[BM][J];
+  // the next block's rows are loaded into a second register set while this
+  // block's dots, cross-wave reduction and W update run (the loads of block
+  // i + 1 stay in flight across block i's two barriers); only for J <= 4,
+  // wider rows would spill the second set
+  constexpr bool PF = J <= 4;
+  float an[PF ? BM : 1][J];
+  auto load_block = [&](int64_t blk_, float (&dst)[BM][J]) {
+    const int64_t r0_ = blk_ * BM;
 #pragma unroll
     for (int b = 0; b < BM; ++b) {
-      const int64_t r = r0 + b < m ? r0 + b : m - 1;
+      const int64_t r = r0_ + b < m ? r0_ + b : m - 1;
       const float* row = A + r * lda;
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         const int c = tid + NT * j;
-        a[b][j] = (c < n && r0 + b < m) ? row[c] : 0.f;
+        dst[b][j] = (c < n && r0_ + b < m) ? row[c] : 0.f;
       }
+    }
+  };
+  if constexpr (PF)
+    if ((int64_t)blockIdx.x < nblk) load_block(blockIdx.x, an);
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t r0 = blk * BM;
+    float a[BM][J];
+    if constexpr (PF) {
+#pragma unroll
+      for (int b = 0; b < BM; ++b)
+#pragma unroll
+        for (int j = 0; j < J; ++j) a[b][j] = an[b][j];
+      if (blk + gridDim.x < nblk) load_block(blk + gridDim.x, an);
+    } else {
+      load_block(blk, a);
     }
     if (!NEED_DOT) {
       // W = A^T D: the D rows of this block straight from memory (tiny, cached)
