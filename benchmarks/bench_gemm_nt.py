@@ -11,7 +11,11 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from libskylark_amd.ops import gemm  # noqa: E402
+from libskylark_amd.ops import _lib, gemm  # noqa: E402
+import ctypes  # noqa: E402
+
+# A/B builds of gemm_nt.hip: GEMM_AB_LIBS="tag:path,tag:path"
+AB = [(t, ctypes.CDLL(p)) for t, p in (e.split(":", 1) for e in os.environ.get("GEMM_AB_LIBS", "").split(",") if e)]
 
 
 def timeit(fn, reps=5):
@@ -32,6 +36,18 @@ def case(name, M, N, K, out_dtype=torch.float32, cos=False):
     sh = torch.rand(N, device="cuda") if cos else None
     ours = {0: timeit(lambda: gemm.gemm_nt(A, B, out=C, cos_scales=sc, cos_shifts=sh))}
     outs = {0: C.float().clone()} if M * N <= 1 << 27 else {}
+    tags = {0: "ours"}
+    for vi, (tag, L) in enumerate(AB, start=1):   # A/B against other builds of gemm_nt.hip
+        vp = ctypes.c_void_p
+        f = lambda L=L: L.sl_gemm_nt_bf16(vp(A.data_ptr()), ctypes.c_int64(K), vp(B.data_ptr()), ctypes.c_int64(K),
+                                          M, N, K, vp(C.data_ptr()), ctypes.c_int64(N),
+                                          _lib.dtype_code(out_dtype), 0, int(cos), ctypes.c_float(1.0),
+                                          vp(sc.data_ptr() if cos else None), vp(sh.data_ptr() if cos else None),
+                                          vp(_lib.stream_of(A)))
+        ours[vi] = timeit(f)
+        tags[vi] = tag
+        if outs:
+            outs[vi] = C.float().clone()
     Bt = B.t()
     if out_dtype == torch.float32:
         lib = timeit(lambda: torch.mm(A, Bt, out_dtype=torch.float32))
@@ -52,7 +68,7 @@ def case(name, M, N, K, out_dtype=torch.float32, cos=False):
     rec = {"case": name, "M": M, "N": N, "K": K, "out": str(out_dtype).split(".")[-1], "cos": cos,
            "hipblaslt_ms": round(lib, 3), "hipblaslt_TF": round(fl / lib / 1e9, 1)}
     for v, ms in ours.items():
-        tag = "ours"
+        tag = tags[v]
         rec[f"{tag}_ms"] = round(ms, 3)
         rec[f"{tag}_TF"] = round(fl / ms / 1e9, 1)
         rec[f"{tag}_rel_err"] = errs.get(v)

@@ -33,6 +33,7 @@
 // bytes each way); the dense m x N copy and the N/2-point spectrum of the
 // rocFFT pipeline (ops/fut.py) are gone.
 #include "sl_common.hpp"
+#include <algorithm>
 
 namespace {
 
@@ -40,7 +41,6 @@ constexpr int NT = 256;         // stage-2 / post threads
 constexpr int NT1 = 256;        // stage-1 threads (4 waves)
 constexpr int WC = 16;          // columns per stage-1 workgroup
 constexpr int N2_MAX = 512;     // LDS tile N2 x WC float2 = 64 KB: two workgroups per CU
-constexpr int GMAX = 16;        // frequencies per stage-2 register pass
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -49,6 +49,12 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 }
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// workgroup barrier that waits for LDS traffic only (global loads in flight
+// stay in flight across it; __syncthreads would drain them)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
 // multiply by -i
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
 
@@ -142,33 +148,48 @@ __device__ __forceinline__ void dft<7>(float2* v) {
 template <int R, int NMAX>
 __device__ __noinline__ void stockham_pass(float2* __restrict__ buf, const float2* __restrict__ tw, int N2, int Ns) {
   constexpr int QMAX = (NMAX / R * WC + NT1 - 1) / NT1;
+  constexpr int JS = NT1 / WC;            // j step per q
   const int tid = threadIdx.x;
   const int nb = N2 / R * WC;
   const int stride = N2 / R;
   const int tstep = N2 / (Ns * R);
+  const int col = tid & (WC - 1), j0 = tid / WC;
+  // (j / Ns, j % Ns) stepped per q (j += JS) instead of two runtime integer
+  // divisions per butterfly: one division per pass
+  const int jq0 = j0 / Ns, jr0 = j0 - jq0 * Ns, sq = JS / Ns, sr = JS - sq * Ns;
   float2 v[QMAX][R];
+  {
+    int jq = jq0, jr = jr0;
 #pragma unroll
-  for (int q = 0; q < QMAX; ++q) {
-    const int b = tid + NT1 * q;
-    if (b < nb) {
-      const int col = b & (WC - 1), j = b / WC, k = j % Ns;
+    for (int q = 0; q < QMAX; ++q) {
+      const int b = tid + NT1 * q, j = j0 + JS * q;
+      if (b < nb) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float2 x = buf[(j + r * stride) * WC + col];
-        v[q][r] = r == 0 ? x : cmul(x, tw[r * k * tstep]);
+        for (int r = 0; r < R; ++r) {
+          const float2 x = buf[(j + r * stride) * WC + col];
+          v[q][r] = r == 0 ? x : cmul(x, tw[r * jr * tstep]);
+        }
+        dft<R>(v[q]);
       }
-      dft<R>(v[q]);
+      jq += sq;
+      jr += sr;
+      if (jr >= Ns) { jr -= Ns; ++jq; }
     }
   }
   __syncthreads();
+  {
+    int jq = jq0, jr = jr0;
 #pragma unroll
-  for (int q = 0; q < QMAX; ++q) {
-    const int b = tid + NT1 * q;
-    if (b < nb) {
-      const int col = b & (WC - 1), j = b / WC, k = j % Ns;
-      const int d0 = (j / Ns) * Ns * R + k;
+    for (int q = 0; q < QMAX; ++q) {
+      const int b = tid + NT1 * q;
+      if (b < nb) {
+        const int d0 = jq * Ns * R + jr;
 #pragma unroll
-      for (int r = 0; r < R; ++r) buf[(d0 + r * Ns) * WC + col] = v[q][r];
+        for (int r = 0; r < R; ++r) buf[(d0 + r * Ns) * WC + col] = v[q][r];
+      }
+      jq += sq;
+      jr += sr;
+      if (jr >= Ns) { jr -= Ns; ++jq; }
     }
   }
   __syncthreads();
@@ -221,7 +242,7 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
     float s, c;
     sincospif(-2.0f * (float)t / (float)N2, &s, &c);
     tw[t] = make_float2(c, s);
-    const int64_t r = ((int64_t)j1 * t) % M;
+    const int64_t r = (int64_t)j1 * t;   // < N1 N2 = M: no reduction needed
     sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
     tm[t] = make_float2(c, s);
   }
@@ -263,86 +284,112 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
 
 // Stage 2: Zs[slot][c] = sum_j1 W_N1^{j1 k1} Y[k2][j1][c] for the (k1, slot)
 // pairs of group k2 (gptr CSR over k2, gk1 / gslot entries).
-__global__ void __launch_bounds__(NT)
+// Workgroup = (k2, 64 S2_NW columns): each wave owns 64 columns (lane =
+// column) and runs over ALL N1 rows, so there is no cross-wave reduction.
+// The group's twiddles W_N1^{j1 k1} are laid out per row in LDS, a 64-row
+// chunk at a time ([row][g], zero-padded to NG = ng rounded up to 4 and for
+// rows >= N1), built one chunk ahead by the whole workgroup from the W_N1
+// table; the inner loop reads them as uniform-address float4 broadcasts and
+// does 2 packed FMAs per (row, frequency) -- no per-element index math.  The
+// rows of Y stream through an 8-deep register ring (loads issued 8 rows
+// ahead; the chunk barriers wait on LDS only, never drain the ring).
+// (Before: 4 waves split j1 with 2 rows in flight and per-frequency index
+// arithmetic in the loop, 2.4 ms at N1 = 1000, m = 1000.)
+constexpr int S2_NW = 4;        // waves per workgroup (column slices)
+constexpr int S2_JC = 64;       // rows per twiddle chunk
+constexpr int S2_U = 8;         // rows in flight per wave
+constexpr int S2_G = 24;        // frequencies per pass
+
+template <int NG>
+__device__ __forceinline__ void fs2_pass(const float2* __restrict__ Yc, int m, int N1, const float2* tw,
+                                         float2* Tg, const int* k1s, int ng, float2* __restrict__ Zs,
+                                         const int* __restrict__ slots, int c, bool cok) {
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int nch = (N1 + S2_JC - 1) / S2_JC;
+  auto build = [&](int ch, float2* dst) {
+    for (int e = tid; e < S2_JC * NG; e += nthr) {
+      const int r = e / NG, g = e - r * NG;
+      const int j = ch * S2_JC + r;
+      float2 t = make_float2(0.f, 0.f);
+      if (j < N1 && g < ng) t = tw[(int)(((int64_t)j * k1s[g]) % N1)];
+      dst[e] = t;
+    }
+  };
+  f2 acc[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) acc[g] = f2{0.f, 0.f};
+  float2 y[S2_U];
+#pragma unroll
+  for (int u = 0; u < S2_U; ++u) y[u] = Yc[(int64_t)min(u, N1 - 1) * m];
+  build(0, Tg);
+  lds_barrier();
+  for (int ch = 0; ch < nch; ++ch) {
+    const float2* T = Tg + (ch & 1) * S2_JC * NG;
+    if (ch + 1 < nch) build(ch + 1, Tg + ((ch + 1) & 1) * S2_JC * NG);
+    for (int r0 = 0; r0 < S2_JC; r0 += S2_U) {
+#pragma unroll
+      for (int u = 0; u < S2_U; ++u) {
+        const int r = r0 + u;
+        const float2 yv = y[u];
+        y[u] = Yc[(int64_t)min(ch * S2_JC + r + S2_U, N1 - 1) * m];
+        const f2 ya = f2{yv.x, yv.y}, yb = f2{yv.y, yv.x};
+        const float4* Tr = (const float4*)(T + r * NG);
+#pragma unroll
+        for (int g = 0; g < NG; g += 2) {
+          const float4 t = Tr[g >> 1];
+          acc[g] = __builtin_elementwise_fma(f2{t.x, t.x}, ya, acc[g]);
+          acc[g] = __builtin_elementwise_fma(f2{-t.y, t.y}, yb, acc[g]);
+          acc[g + 1] = __builtin_elementwise_fma(f2{t.z, t.z}, ya, acc[g + 1]);
+          acc[g + 1] = __builtin_elementwise_fma(f2{-t.w, t.w}, yb, acc[g + 1]);
+        }
+      }
+    }
+    lds_barrier();
+  }
+  if (cok) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+      if (g < ng) Zs[(int64_t)slots[g] * m + c] = make_float2(acc[g].x, acc[g].y);
+  }
+}
+
+__global__ void __launch_bounds__(64 * S2_NW, 4)
 k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __restrict__ gptr,
             const int* __restrict__ gk1, const int* __restrict__ gslot, float2* __restrict__ Zs, int per) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  float2* tw = lds;                       // N1: W_N1^t
-  float2* red = lds + N1;                 // 4 waves x GMAX x 64
+  float2* Tg = lds;                          // 2 x S2_JC x S2_G
+  float2* tw = lds + 2 * S2_JC * S2_G;       // N1: W_N1^t
+  __shared__ int k1s[S2_G];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // XCD-aware order as in stage 1: an XCD walks (k2, 64-column chunk) with the chunk fastest
-  const int nch = (m + 63) / 64;
+  const int cw = 64 * (int)(blockDim.x >> 6);
+  // XCD-aware order as in stage 1: an XCD walks (k2, column chunk) with the chunk fastest
+  const int nch = (m + cw - 1) / cw;
   const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
   if (L >= nch * N2) return;
   const int k2 = L / nch;
-  const int c = (L - k2 * nch) * 64 + lane;
+  const int c = (L - k2 * nch) * cw + w * 64 + lane;
   const int g0 = gptr[k2], g1 = gptr[k2 + 1];
   if (g0 == g1) return;
-  for (int t = tid; t < N1; t += NT) {
-    float s, cc;
-    sincospif(-2.0f * (float)((double)t / (double)N1), &s, &cc);
-    tw[t] = make_float2(cc, s);
+  for (int t = tid; t < N1; t += blockDim.x) {
+    float sn, cs;
+    sincospif(-2.0f * (float)((double)t / (double)N1), &sn, &cs);
+    tw[t] = make_float2(cs, sn);
   }
-  __syncthreads();
-  const float2* Yk = Y + (int64_t)k2 * N1 * m;
   const bool cok = c < m;
-  for (int gb = g0; gb < g1; gb += GMAX) {
-    const int ng = min(GMAX, g1 - gb);
-    int k1[GMAX], idx[GMAX], st[GMAX];
-    float2 acc[GMAX];
-#pragma unroll
-    for (int g = 0; g < GMAX; ++g) {
-      k1[g] = g < ng ? gk1[gb + g] : 0;
-      idx[g] = (int)(((int64_t)w * k1[g]) % N1);   // (j1 k1) mod N1 at j1 = w
-      st[g] = (int)((4 * (int64_t)k1[g]) % N1);
-      acc[g] = make_float2(0.f, 0.f);
+  const float2* Yc = Y + (int64_t)k2 * N1 * m + min(c, m - 1);   // clamped: unconditional loads
+  for (int gb = g0; gb < g1; gb += S2_G) {
+    const int ng = min(S2_G, g1 - gb);
+    if (tid < S2_G) k1s[tid] = tid < ng ? gk1[gb + tid] : 0;
+    lds_barrier();    // tw and k1s visible (and the previous pass's chunk reads done)
+    const int* sl = gslot + gb;
+    switch ((ng + 3) >> 2) {
+      case 1: fs2_pass<4>(Yc, m, N1, tw, Tg, k1s, ng, Zs, sl, c, cok); break;
+      case 2: fs2_pass<8>(Yc, m, N1, tw, Tg, k1s, ng, Zs, sl, c, cok); break;
+      case 3: fs2_pass<12>(Yc, m, N1, tw, Tg, k1s, ng, Zs, sl, c, cok); break;
+      case 4: fs2_pass<16>(Yc, m, N1, tw, Tg, k1s, ng, Zs, sl, c, cok); break;
+      case 5: fs2_pass<20>(Yc, m, N1, tw, Tg, k1s, ng, Zs, sl, c, cok); break;
+      default: fs2_pass<24>(Yc, m, N1, tw, Tg, k1s, ng, Zs, sl, c, cok); break;
     }
-    // two rows of Y in flight per step; complex MAC as two packed FMAs
-    int j1 = w;
-    const float2* Yc = Yk + min(c, m - 1);     // clamped: unconditional loads (see stage 1)
-    for (; j1 + 4 < N1; j1 += 8) {
-      const float2 ya = Yc[(int64_t)j1 * m];
-      const float2 yb = Yc[(int64_t)(j1 + 4) * m];
-#pragma unroll
-      for (int g = 0; g < GMAX; ++g) {
-        if (g < ng) {
-          const float2 ta = tw[idx[g]];
-          idx[g] += st[g];
-          if (idx[g] >= N1) idx[g] -= N1;
-          const float2 tb = tw[idx[g]];
-          idx[g] += st[g];
-          if (idx[g] >= N1) idx[g] -= N1;
-          f2 a = f2{acc[g].x, acc[g].y};
-          a = __builtin_elementwise_fma(f2{ta.x, ta.x}, f2{ya.x, ya.y}, a);
-          a = __builtin_elementwise_fma(f2{-ta.y, ta.y}, f2{ya.y, ya.x}, a);
-          a = __builtin_elementwise_fma(f2{tb.x, tb.x}, f2{yb.x, yb.y}, a);
-          a = __builtin_elementwise_fma(f2{-tb.y, tb.y}, f2{yb.y, yb.x}, a);
-          acc[g] = make_float2(a.x, a.y);
-        }
-      }
-    }
-    for (; j1 < N1; j1 += 4) {
-      const float2 y = Yc[(int64_t)j1 * m];
-#pragma unroll
-      for (int g = 0; g < GMAX; ++g) {
-        if (g < ng) {
-          const float2 t = tw[idx[g]];
-          acc[g].x = fmaf(t.x, y.x, fmaf(-t.y, y.y, acc[g].x));
-          acc[g].y = fmaf(t.x, y.y, fmaf(t.y, y.x, acc[g].y));
-          idx[g] += st[g];
-          if (idx[g] >= N1) idx[g] -= N1;
-        }
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < GMAX; ++g) red[(w * GMAX + g) * 64 + lane] = acc[g];
-    __syncthreads();
-    for (int g = w; g < ng; g += 4) {
-      const float2 s = cadd(cadd(red[(0 * GMAX + g) * 64 + lane], red[(1 * GMAX + g) * 64 + lane]),
-                            cadd(red[(2 * GMAX + g) * 64 + lane], red[(3 * GMAX + g) * 64 + lane]));
-      if (cok) Zs[(int64_t)gslot[gb + g] * m + c] = s;
-    }
-    __syncthreads();
   }
 }
 
@@ -370,12 +417,12 @@ k_fs_post(const float2* __restrict__ Zs, int m, int64_t N, const int64_t* __rest
 }
 
 size_t stage1_lds(int N2) { return (size_t)(N2 * WC + 2 * N2) * sizeof(float2); }
-size_t stage2_lds(int N1) { return (size_t)(N1 + 4 * GMAX * 64) * sizeof(float2); }
+size_t stage2_lds(int N1) { return (size_t)(N1 + 2 * S2_JC * S2_G) * sizeof(float2); }
 
 }  // namespace
 
 SL_API int64_t sl_fs_limits(int which) {
-  return which == 0 ? N2_MAX : which == 1 ? WC : GMAX;
+  return which == 0 ? N2_MAX : which == 1 ? WC : S2_G;
 }
 
 // Stage 1.  A: N x m (lda, f32 or bf16), d: N f64 signs, radix plan (4-bit
@@ -423,9 +470,11 @@ SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, c
     return SL_ERR_INVALID;
   }
   SL_LDS_ATTR(k_fs_stage2, (int)stage2_lds(8192));
-  const int64_t nblk = (int64_t)((m + 63) / 64) * N2;
+  // narrow batches: fewer waves per workgroup (each wave owns 64 columns)
+  const int nw = (int)std::min<int64_t>(S2_NW, (m + 63) / 64);
+  const int64_t nblk = (int64_t)((m + 64 * nw - 1) / (64 * nw)) * N2;
   const int per = (int)((nblk + 7) / 8);
-  k_fs_stage2<<<(unsigned)(8 * (int64_t)per), NT, stage2_lds(N1), (hipStream_t)stream>>>(
+  k_fs_stage2<<<(unsigned)(8 * (int64_t)per), 64 * nw, stage2_lds(N1), (hipStream_t)stream>>>(
       (const float2*)Y, N1, N2, m, gptr, gk1, gslot, (float2*)Zs, per);
   SL_LAUNCH_CHECK();
   return SL_OK;

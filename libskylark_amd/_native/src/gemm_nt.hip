@@ -133,36 +133,54 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
   // row = base + (lane & 15), chunk = 4 kh + (lane >> 4)
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = K / BK;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int st = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+  auto read_frags = [&](int st, int kh, bf16x8 (&a)[8], bf16x8 (&bb)[4]) {
     const char* sA = lds + st * STAGE;
     const char* sB = sA + OPB;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      bf16x8 a[8], bb[4];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = wm * 128 + i * 16 + fr;
-        a[i] = *(const bf16x8*)(sA + r * 128 + (((4 * kh + fq) ^ swz(r)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = wn * 64 + j * 16 + fr;
-        bb[j] = *(const bf16x8*)(sB + r * 128 + (((4 * kh + fq) ^ swz(r)) << 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+    for (int i = 0; i < 8; ++i) {
+      const int r = wm * 128 + i * 16 + fr;
+      a[i] = *(const bf16x8*)(sA + r * 128 + (((4 * kh + fq) ^ swz(r)) << 4));
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wn * 64 + j * 16 + fr;
+      bb[j] = *(const bf16x8*)(sB + r * 128 + (((4 * kh + fq) ^ swz(r)) << 4));
+    }
+  };
+  auto mfmas = [&](const bf16x8 (&a)[8], const bf16x8 (&bb)[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+  };
+  // Per slice kt: the second K-half's fragments are read BEFORE the slice's
+  // closing barrier but their 32 MFMAs run AFTER it, under the first
+  // ds_reads of slice kt + 1, and the MFMA stretch runs at raised wave
+  // priority.  The barrier still closes every read of stage kt & 1
+  // (lgkmcnt(0) before it), which is all the DMA into that stage needs.
+  // Same-box A/B (profiles/r4/gemm_nt_prio_ab.jsonl): 1160 / 1138 TF square
+  // 8192^3 / LSRN panel against 1143 / 1119 for the plain loop; the deferral
+  // alone (no priority) measured 1013 / 1115.
+  bf16x8 a0[8], b0[4], a1[8], b1[4];
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, st ^ 1);
+    read_frags(st, 0, a0, b0);
+    __builtin_amdgcn_s_setprio(1);
+    if (kt > 0) mfmas(a1, b1);            // slice kt - 1, second half
+    read_frags(st, 1, a1, b1);
+    mfmas(a0, b0);
+    __builtin_amdgcn_s_setprio(0);
     // slice kt + 1 landed (this wave's DMA), everyone done reading stage st
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
   }
+  if (nk > 0) mfmas(a1, b1);
 
   // ---- epilogue: lane holds C[4 fq + e][fr] of each 16 x 16 block.  The
   //      wave's 128 x 64 block goes out in four 32-row passes through a

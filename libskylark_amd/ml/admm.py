@@ -38,7 +38,7 @@ import time
 
 import torch
 
-from ..algorithms.loss import Loss, make_loss
+from ..algorithms.loss import Loss, _targets_matrix, make_loss
 from ..algorithms.regularizers import Regularizer, make_regularizer
 from ..base import quasirand as Q
 from ..base.context import Context
@@ -47,15 +47,6 @@ from ..parallel.comm import Comm
 from ..parallel.distmatrix import DistMatrix
 from ..sketch import ROWWISE
 from .model import HilbertModel
-
-
-def _pad_cols(W: torch.Tensor, kp: int) -> torch.Tensor:
-    """W (n x k) zero-padded to kp columns, contiguous (one-pass kernel operand)."""
-    if W.shape[1] == kp:
-        return W.contiguous()
-    out = torch.zeros(W.shape[0], kp, dtype=W.dtype, device=W.device)
-    out[:, :W.shape[1]] = W
-    return out
 
 
 def _partition(D: int, P: int):
@@ -181,11 +172,23 @@ class BlockADMMSolver:
         ZtObar = torch.zeros_like(W)
         del_o = torch.zeros(k, ni, dtype=dt, device=dev)
         cache, zcache = [None] * P, [None] * P
-        Yt = Y if regression or Y.dim() == 1 else Y
+        # class labels -> the k x n_i +-1 target matrix, built once (every loss
+        # prox / evaluation takes it as given targets)
+        Yt = Y if regression or Y.dim() != 1 or k == 1 else _targets_matrix(Y, k, Wbar)
         # one-pass kernels for the two Z pairs per block (f32 on the GPU, k <= 4)
         kp = 1 if k == 1 else (2 if k == 2 else 4)
         fused = self.one_pass and dev.type == "cuda" and dt == torch.float32 and k <= 4
         Dp = torch.zeros(kp, ni, dtype=dt, device=dev) if fused else None
+        # padded (s_j x kp) operands of the one-pass kernels, allocated once
+        pads = {}
+
+        def padded(tag, j, Wj):
+            if Wj.shape[1] == kp:
+                return Wj.contiguous()
+            if (tag, j) not in pads:
+                pads[tag, j] = torch.zeros(Wj.shape[0], kp, dtype=dt, device=dev)
+            pads[tag, j][:, :Wj.shape[1]] = Wj
+            return pads[tag, j]
         t0 = time.time()
         self.history = []
         pending = []
@@ -199,6 +202,10 @@ class BlockADMMSolver:
             dsum = del_o + (P + 1.0) * nu  # k x ni
             if fused:
                 Dp[:k] = dsum
+                # the one-pass kernels' n_i x kp outputs summed as they come
+                # (contiguous adds); folded into the k x n_i sums once
+                zw_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
+                zo_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
             for j in range(P):
                 st, sj = self.starts[j], self.sizes[j]
                 if self.cache_transforms and zcache[j] is not None:
@@ -215,8 +222,8 @@ class BlockADMMSolver:
                 one_pass = fused and normal_eq.native_ok(Z, kp)
                 if one_pass:
                     # pass 1: {Z Wbar_j, Z^T dsum^T} from one read of Z
-                    ztd, zw = normal_eq.dual(Z, Dp.t(), _pad_cols(Wb, kp))
-                    wbar_out += zw[:, :k].t()
+                    ztd, zw = normal_eq.dual(Z, Dp.t(), padded("wb", j, Wb))
+                    zw_sum += zw
                     ztd = ztd[:, :k]
                 else:
                     wbar_out += (Z @ Wb).t()
@@ -226,14 +233,17 @@ class BlockADMMSolver:
                 Wi[st:st + sj] = Wi_j
                 if one_pass:
                     # pass 2: {o = Z Wi_j, Z^T o} from one read of Z
-                    zto, zo = normal_eq.ata(Z, _pad_cols(Wi_j, kp), want_y=True)
-                    o = zo[:, :k].t()
+                    zto, zo = normal_eq.ata(Z, padded("wi", j, Wi_j), want_y=True)
+                    zo_sum += zo
                     ZtObar[st:st + sj] = zto[:, :k]
                 else:
                     o = (Z @ Wi_j).t()  # k x ni
                     ZtObar[st:st + sj] = Z.t() @ o.t()
+                    sum_o += o
                 mu_ij[st:st + sj] += Wi_j
-                sum_o += o
+            if fused:
+                wbar_out += zw_sum[:, :k].t()
+                sum_o += zo_sum[:, :k].t()
             sum_o = O - sum_o
             del_o = sum_o.clone()
             # ---- one all-reduce: [Wi | loss | validation stats]; all on the device
@@ -247,27 +257,49 @@ class BlockADMMSolver:
                 comm.all_reduce(buf)
             Wsum = buf[:D * k].reshape(D, k).to(dt)
             tail = torch.cat([buf[D * k:], (self.lam * self.regularizer.evaluate_t(Wbar)).to(torch.float64)[None]])
-            pending.append((it, tail, time.time() - t0))
+            pending.append((it, *self._stage(tail), time.time() - t0))
             if log is not None:
-                rec = self._record(*pending.pop(), Xv is not None, regression)
-                if comm.rank == 0:
-                    msg = f"iteration {it} objective {rec['objective']:g}"
-                    if "accuracy" in rec:
-                        msg += f" accuracy {rec['accuracy']:.2f}"
-                    log(msg + f" time {rec['time']:.3f} seconds")
+                # iteration it - 1 is logged once iteration it is queued: the host
+                # waits on that iteration's event while the GPU runs this one
+                while len(pending) > 1:
+                    self._log(self._record(*pending.pop(0), Xv is not None, regression), comm, log)
             Obar = O - sum_o / (P + 1.0)
             nu = nu + O - Obar
             Wbar = (Wsum + W) / (rank_count + 1.0)
             mu = mu + W - Wbar
             model.coef = Wbar
-        for p_ in pending:   # iterations not logged: one host transfer at the end
-            self._record(*p_, Xv is not None, regression)
+        for p_ in pending:   # iterations not logged yet: host transfers at the end
+            rec = self._record(*p_, Xv is not None, regression)
+            if log is not None:
+                self._log(rec, comm, log)
         self.history.sort(key=lambda r: r["iteration"])
         model.coef = Wbar.to(torch.float64).cpu() if not Wbar.is_cuda else Wbar.to(torch.float64)
         return model
 
-    def _record(self, it, tail, elapsed, has_val, regression):
-        totalloss, s0, s1, reg = (float(v) for v in tail.cpu())
+    @staticmethod
+    def _stage(tail):
+        """Starts the device -> host copy of an iteration's statistics (pinned
+        buffer, non-blocking) and returns it with the event that completes it."""
+        if not tail.is_cuda:
+            return tail, None
+        host = torch.empty(tail.shape, dtype=tail.dtype, pin_memory=True)
+        host.copy_(tail, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
+
+    @staticmethod
+    def _log(rec, comm, log):
+        if comm.rank == 0:
+            msg = f"iteration {rec['iteration']} objective {rec['objective']:g}"
+            if "accuracy" in rec:
+                msg += f" accuracy {rec['accuracy']:.2f}"
+            log(msg + f" time {rec['time']:.3f} seconds")
+
+    def _record(self, it, tail, ev, elapsed, has_val, regression):
+        if ev is not None:
+            ev.synchronize()
+        totalloss, s0, s1, reg = (float(v) for v in tail)
         rec = {"iteration": it, "objective": totalloss + reg, "time": elapsed}
         if has_val:
             rec["accuracy"] = math.sqrt(s0 / s1) if regression else 100.0 * s0 / max(s1, 1)

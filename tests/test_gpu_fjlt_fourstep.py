@@ -53,3 +53,16 @@ def test_fjlt_sketch_uses_fourstep_and_matches_operator():
     got = T.apply(A.float().cuda(), dim="columnwise").double().cpu()
     ref = T.realize(torch.float64, "cpu") @ A
     torch.testing.assert_close(got, ref, rtol=0, atol=3e-5 * float(ref.abs().max()))
+
+
+def test_fourstep_dense_groups_and_wide_batch():
+    """Many sampled frequencies per k2 group (several stage-2 passes of 24) and a
+    batch wider than one stage-2 workgroup (300 columns: 256 + a partial 44)."""
+    N, m = 8192, 300
+    g = np.random.default_rng(7)
+    A = g.standard_normal((N, m))
+    d = g.choice([-1.0, 1.0], N)
+    samples = g.integers(0, N, 3000)
+    out = fut.fjlt_fourstep(torch.from_numpy(A).float().cuda(), torch.from_numpy(d), torch.from_numpy(samples), 1.0)
+    ref = _ref(A.astype(np.float32).astype(np.float64), d, samples, 1.0)
+    assert np.abs(out.double().cpu().numpy() - ref).max() <= 2e-5 * np.abs(ref).max()
