@@ -39,7 +39,7 @@ namespace {
 
 constexpr int NT = 256;         // stage-2 / post threads
 constexpr int NT1 = 256;        // stage-1 threads (4 waves)
-constexpr int WC = 16;          // columns per stage-1 workgroup
+constexpr int WC = 16;          // columns per stage-1 workgroup (8: 3.72 vs 3.58 ms)
 constexpr int N2_MAX = 512;     // LDS tile N2 x WC float2 = 64 KB: two workgroups per CU
 
 typedef float f2 __attribute__((ext_vector_type(2)));
