@@ -18,12 +18,13 @@ def main():
     A = torch.randn(N, m, device="cuda")
     d = (torch.randint(0, 2, (N,), device="cuda") * 2 - 1).double()
     N1, N2, rs = fut.fourstep_split(N)
-    rplan = sum(r << (4 * i) for i, r in enumerate(rs))
     Y = torch.empty(N2 * N1 * m * 2, dtype=torch.float32, device="cuda")
     st = C.c_void_p(_lib.stream_of(A))
-    for e in os.environ.get("FS_AB_LIBS", "").split(","):
-        if not e:
-            continue
+    # FS_PLANS="4-5-5-5,25-20": radix plans to time (default: the planner's)
+    plans = [[int(r) for r in p.split("-")] for p in os.environ.get("FS_PLANS", "").split(",") if p] or [rs]
+    runs = [(e, p) for e in os.environ.get("FS_AB_LIBS", "").split(",") if e for p in plans]
+    for e, rs in runs:
+        rplan = sum(r << (4 * i) for i, r in enumerate(rs))
         tag, path = e.split(":", 1)
         L = C.CDLL(path)
         f = lambda: L.sl_fs_stage1(C.c_void_p(A.data_ptr()), _lib.dtype_code(A.dtype), C.c_int64(A.stride(0)),
@@ -36,7 +37,8 @@ def main():
             f()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / 5 * 1e3
-        print(json.dumps({"build": tag, "rc": rc, "stage1_ms": round(ms, 3), "N1": N1, "N2": N2, "radices": rs}),
+        ref = Y[:4 * m].clone()
+        print(json.dumps({"build": tag, "rc": rc, "checksum": float(ref.double().abs().sum()), "stage1_ms": round(ms, 3), "N1": N1, "N2": N2, "radices": rs}),
               flush=True)
 
 

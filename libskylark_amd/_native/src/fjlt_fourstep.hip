@@ -195,7 +195,10 @@ __device__ __noinline__ void stockham_pass(float2* __restrict__ buf, const float
   __syncthreads();
 }
 
-// in-place length-n FFT of the n x WC LDS tile (radix plan: 4-bit radices, low first)
+// in-place length-n FFT of the n x WC LDS tile (radix plan: 4-bit radices, low first).
+// (Composite register radices 20 = 4 x 5 / 25 = 5 x 5 measured: plan 25-20
+// 3.73 ms, 20-5-5 3.23, 25-4-5 3.79 against 3.24-3.45 for 4-5-5-5 -- the
+// radix-25 pass needs ~250 VGPRs; not kept.)
 template <int NMAX>
 __device__ void fft_tile(float2* buf, const float2* tw, int n, uint64_t rplan, int npass) {
   int Ns = 1;
@@ -246,10 +249,10 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
     sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
     tm[t] = make_float2(c, s);
   }
-  // ---- load z[j1 + N1 j2] (D applied), 32 columns, 16 rows (32 loads) in
-  //      flight per thread per batch
+  // ---- load z[j1 + N1 j2] (D applied): 16 columns, every row of the tile
+  //      (up to 32 per thread, 64 loads) in flight at once
   constexpr int RG = NT1 / WC;                     // 16 row groups
-  constexpr int UB = 16;
+  constexpr int UB = 32;                           // one batch covers N2 <= 512 (16: 3.36-3.51 ms, 32: 3.23 ms)
   const int col = tid & (WC - 1), rg = tid / WC;
   const bool cok = c0 + col < m;
   // unconditional loads from clamped addresses (a per-element "load or zero"
