@@ -12,7 +12,9 @@
 //   stage 2  Z[k]      = sum_j1 W_N1^{j1 k1} Y[k2][j1]              (needed k only)
 //   stage 3  out[s]    = scale c_k Re(W_4N^k (E + W_N^k O)),  k = sample s
 //
-// Stage 1: one workgroup per (j1, 16-column chunk), two per CU.  The 2 N2
+// Stage 1: one workgroup per (j1, 16-column chunk), two per CU.  The first
+// radix pass runs on the rows as they arrive and the last one stores Y
+// directly (2.8-2.9 vs 3.2-3.4 ms staging both through LDS).  The 2 N2
 // rows of x it needs are read as 64-B row pieces (D applied on load; every
 // load of a batch in flight: clamped addresses, no per-element branches)
 // into an LDS tile of N2 x 16 complex values; the length-N2 FFT runs in place
@@ -200,9 +202,9 @@ __device__ __noinline__ void stockham_pass(float2* __restrict__ buf, const float
 // 3.73 ms, 20-5-5 3.23, 25-4-5 3.79 against 3.24-3.45 for 4-5-5-5 -- the
 // radix-25 pass needs ~250 VGPRs; not kept.)
 template <int NMAX>
-__device__ void fft_tile(float2* buf, const float2* tw, int n, uint64_t rplan, int npass) {
-  int Ns = 1;
-  for (int p = 0; p < npass; ++p) {
+__device__ void fft_tile(float2* buf, const float2* tw, int n, uint64_t rplan, int npass, int p0 = 0, int Ns0 = 1) {
+  int Ns = Ns0;
+  for (int p = p0; p < npass; ++p) {
     const int R = (int)((rplan >> (4 * p)) & 15);
     switch (R) {
       case 8: stockham_pass<8, NMAX>(buf, tw, n, Ns); break;
@@ -216,10 +218,83 @@ __device__ void fft_tile(float2* buf, const float2* tw, int n, uint64_t rplan, i
   }
 }
 
+// The last Stockham pass (Ns = N2 / R: its butterfly j writes rows k2 = j + r Ns)
+// straight to Y with the W_M^{j1 k2} twiddles -- no LDS write-back, barrier
+// and re-read for the output.
+template <int R>
+__device__ __forceinline__ void last_pass_store(const float2* __restrict__ buf, const float2* __restrict__ tw,
+                                                const float2* __restrict__ tm, int N2, float2* __restrict__ Yc,
+                                                int64_t ystride, bool cok) {
+  constexpr int QMAX = (N2_MAX / R * WC + NT1 - 1) / NT1;
+  const int tid = threadIdx.x, col = tid & (WC - 1);
+  const int Ns = N2 / R, nb = Ns * WC;
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int b = tid + NT1 * q;
+    if (b < nb) {
+      const int j = b / WC;
+      float2 v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float2 x = buf[(j + r * Ns) * WC + col];
+        v[r] = r == 0 ? x : cmul(x, tw[r * j]);
+      }
+      dft<R>(v);
+      if (cok) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int k2 = j + r * Ns;
+          Yc[(int64_t)k2 * ystride] = cmul(v[r], tm[k2]);
+        }
+      }
+    }
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ float ld_f(const T* p) {
   if constexpr (sizeof(T) == 2) return bf16_to_f(*(const bf16_t*)p);
   else return (float)*p;
+}
+
+// The tile's rows loaded straight into the first Stockham pass (Ns = 1: no
+// twiddles): each thread loads the R0 rows j + r N2 / R0 of its butterflies
+// (D applied, every load of the tile in flight at once), runs the radix-R0
+// DFT in registers and writes the pass's output -- one LDS write + read +
+// barrier fewer than staging the rows first.
+template <typename T, int R0>
+__device__ __forceinline__ void load_first_pass(const T* __restrict__ Ac, const double* __restrict__ d, int64_t lda,
+                                                int64_t N, int N1, int N2, int j1, bool cok, float2* buf) {
+  constexpr int QM = (N2_MAX / R0 * WC + NT1 - 1) / NT1;
+  const int64_t M = N >> 1;
+  const int tid = threadIdx.x, col = tid & (WC - 1);
+  const int stride = N2 / R0, nb = stride * WC;
+  float2 v[QM][R0];
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int j = min(tid + NT1 * q, nb - 1) / WC;     // clamped: unconditional loads
+#pragma unroll
+    for (int r = 0; r < R0; ++r) {
+      const int64_t j4 = 4 * ((int64_t)j1 + (int64_t)N1 * (j + r * stride));   // 2 n0
+      const int64_t x0 = j4 < 2 * M ? j4 : 2 * N - j4 - 1;                   // n0 = 2j < M ?
+      const int64_t x1 = j4 + 2 < 2 * M ? j4 + 2 : 2 * N - j4 - 3;           // n1 = 2j + 1 < M ?
+      v[q][r] = make_float2(ld_f(Ac + x0 * lda) * (float)d[x0], ld_f(Ac + x1 * lda) * (float)d[x1]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < QM; ++q) {
+    const int b = tid + NT1 * q;
+    if (b < nb) {
+      const int j = b / WC;
+      if (!cok) {
+#pragma unroll
+        for (int r = 0; r < R0; ++r) v[q][r] = make_float2(0.f, 0.f);
+      }
+      dft<R0>(v[q]);
+#pragma unroll
+      for (int r = 0; r < R0; ++r) buf[(j * R0 + r) * WC + col] = v[q][r];
+    }
+  }
 }
 
 // radix plan: up to 12 radices, 4 bits each, packed low first
@@ -249,40 +324,33 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
     sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
     tm[t] = make_float2(c, s);
   }
-  // ---- load z[j1 + N1 j2] (D applied): 16 columns, every row of the tile
-  //      (up to 32 per thread, 64 loads) in flight at once
-  constexpr int RG = NT1 / WC;                     // 16 row groups
-  constexpr int UB = 32;                           // one batch covers N2 <= 512 (16: 3.36-3.51 ms, 32: 3.23 ms)
-  const int col = tid & (WC - 1), rg = tid / WC;
+  // ---- rows of z[j1 + N1 j2] (D applied) -> first radix pass -> tile
+  const int col = tid & (WC - 1);
   const bool cok = c0 + col < m;
-  // unconditional loads from clamped addresses (a per-element "load or zero"
-  // branch makes hipcc wait for each load before the next: one L2 round trip
-  // per element instead of all of them in flight)
   const T* Ac = A + min(c0 + col, m - 1);
-  for (int jb = rg; jb < N2; jb += UB * RG) {
-    float re[UB], im[UB];
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int j2 = min(jb + u * RG, N2 - 1);
-      const int64_t j4 = 4 * ((int64_t)j1 + (int64_t)N1 * j2);      // 2 n0
-      const int64_t x0 = j4 < 2 * M ? j4 : 2 * N - j4 - 1;         // n0 = 2j < M ?
-      const int64_t x1 = j4 + 2 < 2 * M ? j4 + 2 : 2 * N - j4 - 3;  // n1 = 2j + 1 < M ?
-      re[u] = ld_f(Ac + x0 * lda) * (float)d[x0];
-      im[u] = ld_f(Ac + x1 * lda) * (float)d[x1];
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int j2 = jb + u * RG;
-      if (j2 < N2) buf[j2 * WC + col] = cok ? make_float2(re[u], im[u]) : make_float2(0.f, 0.f);
-    }
+  const int R0 = (int)(rplan & 15);
+  switch (R0) {
+    case 8: load_first_pass<T, 8>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 4: load_first_pass<T, 4>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 5: load_first_pass<T, 5>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 3: load_first_pass<T, 3>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 7: load_first_pass<T, 7>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    default: load_first_pass<T, 2>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
   }
   __syncthreads();
-  // ---- length-N2 FFT along the tile's rows
-  fft_tile<N2_MAX>(buf, tw, N2, rplan, npass);
-  // ---- W_M^{j1 k2} and out: Y[k2][j1][c]
-  if (!cok) return;
-  for (int k2 = rg; k2 < N2; k2 += RG)
-    Y[((int64_t)k2 * N1 + j1) * m + c0 + col] = cmul(buf[k2 * WC + col], tm[k2]);
+  // ---- the middle passes of the length-N2 FFT along the tile's rows
+  fft_tile<N2_MAX>(buf, tw, N2, rplan, npass - 1, 1, R0);
+  // ---- the last pass, times W_M^{j1 k2}, out to Y[k2][j1][c]
+  float2* Yc = Y + (int64_t)j1 * m + c0 + col;
+  const int64_t ys = (int64_t)N1 * m;
+  switch ((int)((rplan >> (4 * (npass - 1))) & 15)) {
+    case 8: last_pass_store<8>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 4: last_pass_store<4>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 5: last_pass_store<5>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 3: last_pass_store<3>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 7: last_pass_store<7>(buf, tw, tm, N2, Yc, ys, cok); break;
+    default: last_pass_store<2>(buf, tw, tm, N2, Yc, ys, cok); break;
+  }
 }
 
 // Stage 2: Zs[slot][c] = sum_j1 W_N1^{j1 k1} Y[k2][j1][c] for the (k1, slot)
@@ -432,8 +500,8 @@ SL_API int64_t sl_fs_limits(int which) {
 // radices, low first, product N2), Y: N2 x N1 x m complex f32.
 SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m, const double* d, int N1, int N2,
                         uint64_t rplan, int npass, void* Y, void* stream) {
-  if (N % 2 || (int64_t)N1 * N2 != N / 2 || N2 < 2 || N2 > N2_MAX || m < 1 || npass < 1 || npass > 16) {
-    sl_set_last_error("fs_stage1: needs N even, N1 N2 = N/2, 2 <= N2 <= 512");
+  if (N % 2 || (int64_t)N1 * N2 != N / 2 || N2 < 2 || N2 > N2_MAX || m < 1 || npass < 2 || npass > 16) {
+    sl_set_last_error("fs_stage1: needs N even, N1 N2 = N/2, 2 <= N2 <= 512, at least two radix passes");
     return SL_ERR_INVALID;
   }
   int64_t prod = 1;
