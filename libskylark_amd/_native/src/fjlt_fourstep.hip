@@ -366,6 +366,8 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const double
 // ahead; the chunk barriers wait on LDS only, never drain the ring).
 // (Before: 4 waves split j1 with 2 rows in flight and per-frequency index
 // arithmetic in the loop, 2.4 ms at N1 = 1000, m = 1000.)
+// (Two columns per lane -- 16-B rows, each twiddle broadcast used twice --
+// needs 192 VGPRs, 2 waves per SIMD: 1.51 vs 1.28 ms; not kept.)
 constexpr int S2_NW = 4;        // waves per workgroup (column slices)
 constexpr int S2_JC = 64;       // rows per twiddle chunk
 constexpr int S2_U = 8;         // rows in flight per wave
