@@ -1009,4 +1009,31 @@ inline int kernel_gram(const Kern& kk, int dirX, int dirY, const DevMat& X, cons
   return check(L.dev_sync(st), "sync");
 }
 
+// Host "Matrix" operands (column-major, f64) staged to the GPU, the same way
+// apply_host_dense stages a sketch operand (reference capi/ckernel.cpp:34-128
+// runs sl_kernel_gram on host matrices natively): a column-major m x n X is
+// the row-major n x m X^T on the device, so its points flip direction (dir 1
+// "columns" -> rows of the uploaded view), and the column-major K (#X x #Y)
+// is the row-major K^T = Gram(Y, X) -- every kernel here is symmetric in its
+// two arguments -- so nothing is transposed.  One copy each way.
+inline int kernel_gram_host(const Kern& kk, int dirX, int dirY, const double* X, int64_t xm, int64_t xn,
+                            const double* Y, int64_t ym, int64_t yn, double* K, int64_t km, int64_t kn) {
+  Lib& L = lib();
+  const int64_t nx = dirX == 2 ? xm : xn, ny = dirY == 2 ? ym : yn;
+  if (km != nx || kn != ny) return fail(104, "sl_kernel_gram: K must be (#X points) x (#Y points)");
+  Buf dX(std::max<int64_t>(1, xm * xn) * 8), dY(std::max<int64_t>(1, ym * yn) * 8),
+      dK(std::max<int64_t>(1, km * kn) * 8);
+  if (!dX.p || !dY.p || !dK.p) return fail(101, "sl_kernel_gram: device allocation failed");
+  SLDEV_TRY(L.dev_memcpy(dX.p, X, xm * xn * 8, 0, nullptr), "copy");
+  if (Y != X || ym != xm || yn != xn) SLDEV_TRY(L.dev_memcpy(dY.p, Y, ym * yn * 8, 0, nullptr), "copy");
+  const void* yd = (Y == X && ym == xm && yn == xn) ? dX.p : dY.p;
+  // uploaded views: row-major xn x xm (points = rows iff dirX == 1), likewise Y
+  const DevMat Xv{dX.p, F64, xn, xm, xm}, Yv{const_cast<void*>(yd), F64, yn, ym, ym};
+  const DevMat Kv{dK.p, F64, kn, km, km};
+  const int rc = kernel_gram(kk, dirY == 1 ? 2 : 1, dirX == 1 ? 2 : 1, Yv, Xv, Kv);
+  if (rc) return rc;
+  SLDEV_TRY(L.dev_memcpy(K, dK.p, km * kn * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
 }  // namespace sldev

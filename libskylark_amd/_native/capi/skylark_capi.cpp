@@ -2,23 +2,27 @@
 // sketchc.hpp, nlac.hpp, kernelc.hpp, ioc.hpp) over the MI355X runtime.
 //
 // Native paths (no interpreter):
-//  - contexts, kernels objects, and the core sketches JLT / CT / FJLT / CWT /
-//    MMT / WZT -- creation and JSON (de)serialisation -- in C++
-//    (native_sketch.hpp, the same counter-based streams as the runtime);
-//  - host "Matrix" application of JLT / CT / CWT / MMT / WZT (host C++);
-//  - "DeviceMatrix" operands (GPU buffers wrapped by
-//    sl_wrap_raw_device_matrix): sketch application, sl_approximate_svd (the
-//    C++ randSVD engine) and sl_kernel_gram call libskylark_hip.so directly
-//    (native_device.hpp).
-// Everything else (other sketch types, sparse operands, NLA and kernels on
-// host matrices, IO) goes through the Python/HIP
-// runtime (libskylark_amd + libskylark_hip.so); a natively created sketch
-// or context is handed to it lazily (via its JSON / seed + counter), so the
-// two paths see the same objects and the same random streams.  This library
-// embeds CPython when called from a plain C/C++ program (first call
-// initialises the interpreter, adds this library's package root to
-// sys.path, and imports libskylark_amd.capi), or joins the running
-// interpreter when loaded from Python.  Every entry point:
+//  - contexts, kernel objects and EVERY sketch type of the reference (all
+//    19): creation and JSON (de)serialisation in C++ (native_sketch.hpp, the
+//    same counter-based streams as the runtime), application on host
+//    "Matrix" / "SparseMatrix" operands (staged to the GPU, or on host
+//    threads when there is none) and on "DeviceMatrix" operands;
+//  - sl_approximate_svd / sl_approximate_symmetric_svd /
+//    sl_faster_least_squares on "Matrix" and "DeviceMatrix" operands (the C++
+//    randSVD engines of libskylark_hip.so);
+//  - sl_kernel_gram on "Matrix" and "DeviceMatrix" operands (the Gram
+//    kernels of libskylark_hip.so, host matrices staged to the GPU);
+//  - sl_readlibsvm into "Matrix" / "SparseMatrix" (libsvm_io.cpp).
+// Everything else (DistMatrix-typed operands, runtime-only kernels, the
+// remaining entry points) goes through the Python/HIP runtime
+// (libskylark_amd + libskylark_hip.so); a natively created sketch or context
+// is handed to it lazily (via its JSON / seed + counter), so the two paths
+// see the same objects and the same random streams (sl_runtime_started()
+// reports whether it ever started).  This library embeds CPython when such a
+// call comes from a plain C/C++ program (first call initialises the
+// interpreter, adds this library's package root to sys.path, and imports
+// libskylark_amd.capi), or joins the running interpreter when loaded from
+// Python.  Every runtime entry point:
 //   - takes the GIL (PyGILState_Ensure),
 //   - converts handles / raw matrix wraps / varargs to Python objects,
 //   - calls libskylark_amd.capi.<fn>,
@@ -960,6 +964,16 @@ SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, voi
     const int rc = sldev::kernel_gram(k->nat, dirX, dirY, devmat(X), devmat(Y), devmat(K));
     return rc ? native_fail(rc) : 0;
   }
+  if (!strcmp(X_type, "Matrix") && !strcmp(Y_type, "Matrix") && !strcmp(K_type, "Matrix") &&
+      k->nat.type != sldev::K_NONE && sldev::device_present()) {
+    // host operands, natively: staged to the GPU (no interpreter)
+    const auto* x = (const sl_raw_matrix_t*)X;
+    const auto* y = (const sl_raw_matrix_t*)Y;
+    const auto* kk = (const sl_raw_matrix_t*)K;
+    const int rc = sldev::kernel_gram_host(k->nat, dirX, dirY, x->data, x->m, x->n, y->data, y->m, y->n, kk->data,
+                                           kk->m, kk->n);
+    return rc ? native_fail(rc) : 0;
+  }
   Gil g;
   (void)K_type;
   PyObject* ko = py_kernel(k);
@@ -984,11 +998,12 @@ SL_CAPI int sl_readlibsvm(char* fname, char* X_type, void* X, char* Y_type, void
   const bool xd = !strcmp(X_type, "Matrix"), xs = !strcmp(X_type, "SparseMatrix");
   if ((xd || xs) && (!Y || !strcmp(Y_type, "Matrix")) && sldev::lib().loaded) {
     // native LIBSVM reader (libsvm_io.cpp): examples are columns (direction
-    // 0 / 1, d x n, labels 1 x n) or rows (n x d, labels n x 1)
+    // SL_COLUMNS = 1: d x n, labels 1 x n) or rows (anything else, as the
+    // reference's cio.cpp:17-18 maps it: n x d, labels n x 1)
     sldev::Libsvm L;
     const int rc = sldev::read_libsvm(fname, min_d, max_n, L);
     if (rc) return native_fail(rc);
-    const bool cols = direction == 0 || direction == 1;
+    const bool cols = direction == 1;
     const int64_t n = L.rows, d = L.d;
     const int64_t xm = cols ? d : n, xn = cols ? n : d;
     if (Y) {

@@ -25,15 +25,6 @@
 #pragma once
 #include "sl_common.hpp"
 
-// diagnostic builds only (benchmarks/native, -DSL_EIG_STAMPS): shader-clock
-// stamps at the phase boundaries of the solvers below
-#ifdef SL_EIG_STAMPS
-__device__ unsigned long long g_eig_st[64];
-#define SLW_STAMP(I) \
-  if (threadIdx.x == 0) g_eig_st[(I)] = __builtin_amdgcn_s_memtime();
-#else
-#define SLW_STAMP(I)
-#endif
 
 namespace slw {
 
@@ -189,7 +180,6 @@ template <int K, int J>
 __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, double* wsh, double* refl, int ldr,
                                          double* dd, double* ee) {
   constexpr int c0 = (J + 1) & ~1;
-  if (J == 10) { SLW_STAMP(10) }
   // ||x||^2 of column J below the diagonal and its first entry, from the
   // column itself (lane i > J holds x_i): the rank-2 updates keep the
   // register matrix symmetric only to rounding, and a norm taken from row J
@@ -212,7 +202,6 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
     refl[i * ldr + J] = vi;
   }
   wave_lds_sync();
-  if (J == 10) { SLW_STAMP(11) }
   // p = A v, v streamed from LDS in pairs (entry J, when the first pair
   // starts there, has v_J = 0)
   double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
@@ -232,13 +221,10 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
       if (((c - c0) & 15) == 12) asm volatile("" ::: "memory");
   }
   const double p = (p0 + p1) + (p2 + p3);
-  if (J == 10) { SLW_STAMP(12) }
   const double Kd = wave_sum(vi * p);
-  if (J == 10) { SLW_STAMP(13) }
   const double wi = (i > J) ? 2.0 * (p - Kd * vi) : 0.0;
   if (i < K) wsh[i] = wi;
   wave_lds_sync();
-  if (J == 10) { SLW_STAMP(14) }
   // A -= v w^T + w v^T on the trailing columns (v, w streamed again)
 #pragma unroll
   for (int c = c0; c < K; c += 2) {
@@ -249,7 +235,6 @@ __device__ __forceinline__ void tri_step(double (&arow)[K], int i, double* vsh, 
     if constexpr (K >= 48)
       if (((c - c0) & 15) == 14) asm volatile("" ::: "memory");
   }
-  if (J == 10) { SLW_STAMP(15) }
 }
 
 // vsh / wsh: 2 x K doubles each (alternate steps use alternate halves, so a
@@ -452,7 +437,6 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
   __shared__ double s_scale;
   __shared__ int s_clus;
   __shared__ double2 de2[K];
-  SLW_STAMP(1)
   // ---- scale to ||T|| ~ 1 (Gershgorin radius)
   if (tid < 64) {
     const int i = lane;
@@ -518,7 +502,6 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     }
   }
   __syncthreads();
-  SLW_STAMP(2)
   // ---- eigenvectors of T: one lane per vector (twisted factorisation of
   //      the scaled T - l I).  Per lane t: zdm = sc[t * LZ + i] holds the
   //      backward pivots D-_i (later the vector), zdp the forward pivots, zrd
@@ -567,7 +550,6 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     }
   }
   __syncthreads();
-  SLW_STAMP(3)
   // ---- MGS inside close clusters (rare): wave 0, lane = component.  Two
   //      passes ("twice is enough"): inside a tight cluster the twisted
   //      vectors can be nearly parallel, and one pass then leaves a small
@@ -610,7 +592,6 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     }
     if (!(r2 <= 1e-22)) atomicOr(st, 1);
   }
-  SLW_STAMP(4)
   // ---- back-transform x <- H_0 ... H_{K-3} x: 16 lanes (a DPP row) per vector
   {
     constexpr int U = (K + 15) / 16;
@@ -652,7 +633,6 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
   // eigenvalues back to the matrix's scale
   for (int t = tid; t < nt; t += NT) lam[t] *= tn;
   __syncthreads();
-  SLW_STAMP(5)
 }
 
 }  // namespace slw

@@ -44,14 +44,6 @@ constexpr int RED = KMAX + 16;   // doubles of small scratch (max diag, D^{-1/2}
 // dynamic LDS of the small-LA kernels: four k x k f64 buffers, RED doubles, int flags / order
 constexpr size_t GRAM_LA_LDS = (size_t)(4 * KMAX * (KMAX + 1) + RED) * sizeof(double) + (4 + KMAX + 1) * sizeof(int);
 
-#ifdef SL_CORE_STAMPS
-// diagnostic build only: phase times (100 MHz s_memrealtime) of the final core
-__device__ unsigned long long g_core_st[32];
-#define SL_CST(I) \
-  if (threadIdx.x == 0) g_core_st[(I)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define SL_CST(I)
-#endif
 
 enum : int { ST_PIVOT = 1, ST_NONFINITE = 2, ST_NOCONV = 4, ST_RANK = 8, ST_TIMEOUT = 16 };
 
@@ -167,10 +159,6 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
   const double amax = rot_c[0];
   const double noise2 = (1e-14 * amax) * (1e-14 * amax);
   __syncthreads();
-#ifdef SL_CORE_STAMPS
-  unsigned long long c1 = 0, c2 = 0, nr = 0;
-  const unsigned long long ct0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
   // this thread's first A block (held in registers)
   int b0i = 0, b0j = 0;
   if (tid >= 256 && tid - 256 < nA) { b0i = btab[tid - 256] & 255; b0j = btab[tid - 256] >> 8; }
@@ -181,9 +169,6 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
     if (tid == 0) flags[(sweep + 1) % 3] = 0;
     for (int rd = 0; rd < kp - 1; ++rd) {
       const unsigned short* rt = rtab + rd * hp;
-#ifdef SL_CORE_STAMPS
-      const unsigned long long ta = __builtin_amdgcn_s_memtime();
-#endif
       // (1) rotations of the round's pairs
       if (tid < hp) {
         const int p = rt[tid] & 255, q = rt[tid] >> 8;
@@ -195,10 +180,6 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
         rot_t[tid] = R.rot ? R.t : 0.0;
       }
       __syncthreads();
-#ifdef SL_CORE_STAMPS
-      const unsigned long long tb = __builtin_amdgcn_s_memtime();
-      c1 += tb - ta;
-#endif
       // (2) apply: waves 4-7 the blocks of A, waves 0-3 the rows of V
       if (wid >= 4) {
 #pragma unroll 1
@@ -254,24 +235,11 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
         }
       }
       __syncthreads();
-#ifdef SL_CORE_STAMPS
-      c2 += __builtin_amdgcn_s_memtime() - tb;
-      ++nr;
-#endif
     }
     if (!*flag) { conv = true; ++sweep; break; }
   }
   if (!conv && tid == 0) *st |= ST_NOCONV;
   if (tid == 0) flags[3] = sweep;
-#ifdef SL_CORE_STAMPS
-  if (tid == 0) {
-    g_core_st[25] = c1;
-    g_core_st[26] = c2;
-    g_core_st[27] = nr;
-    g_core_st[28] = __builtin_amdgcn_s_memtime() - ct0;
-    g_core_st[29] = __builtin_amdgcn_s_memrealtime() - rt0;
-  }
-#endif
   __syncthreads();
   return A;
 }
@@ -302,7 +270,6 @@ __device__ __forceinline__ void final_core(double* b0, double* b1, double* b2, d
   const int ld = k + 1;
   constexpr int SO = 16;
   (void)SO;
-  SL_CST(SO + 3)
   // C = Rti^T H Rti:  T = H Rti -> b1, C = Rti^T T -> b2
   small_gemm(b0, b3, b1, k, ld, false);
   __syncthreads();
@@ -317,15 +284,12 @@ __device__ __forceinline__ void final_core(double* b0, double* b1, double* b2, d
   }
   if (tid == 0) { cs.bad = 0; cs.fb = 0; }
   __syncthreads();
-  SL_CST(SO + 4)
   // tridiagonalise (wave 0; reflectors into b2, ld K + 1)
   const int nt = r < k ? r + 1 : k;
   if (tid < 64) slw::wave_tridiag<K>(b0, ld, k, b2, K + 1, cs.dd, cs.ee, cs.vsh, cs.wsh, &cs.bad);
   __syncthreads();
-  SL_CST(SO + 5)
   // top nt eigenvalues, top r eigenvectors of C into b1 (ld), scratch b0
   slw::sym_top_eig<K, NT>(cs.dd, cs.ee, b2, K + 1, nt, r, cs.lam, b1, ld, k, b0, &cs.fb);
-  SL_CST(SO + 6)
   if (cs.fb | cs.bad) {
     // robust path: Jacobi on the saved core (C in b2, V in b1, ld)
     const int kp = k + (k & 1);
@@ -382,7 +346,6 @@ __device__ __forceinline__ void final_core(double* b0, double* b1, double* b2, d
     // the call's final status word, straight to host-mapped memory (no D2H copy)
     if (mirror) __hip_atomic_store(mirror, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  SL_CST(SO + 7)
 }
 
 // ---------------------------------------------------------------- fused boundary
@@ -460,7 +423,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     // the Y^T Y worker: Rt^{-1} of the reduced Gram (independent of W) while
     // the row workgroups form and sum H, published as a finished-worker count
     if (tid == 0) st_sh = 0;
-    SL_CST(11)
     // G staged into LDS with coalesced loads (all in flight), the elimination
     // on LDS operands, X back with coalesced stores: the wave's per-lane
     // strided global reads / writes cost ~10 us on this critical path
@@ -489,7 +451,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       const int i = e / k, c = e - i * k;
       a.rti[e] = b2[i * ld + c];
     }
-    SL_CST(12)
     if (tid == 0) ((int*)(a.rti + k * k))[0] = st_sh;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -506,10 +467,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
   const int r0 = blockIdx.x * BR;
   const int nr = min(BR, n - r0);
   const int E = nr * k;   // a multiple of 8 (n % 8 == 0)
-#ifdef SL_CORE_STAMPS
-  const unsigned long long st_start = __builtin_amdgcn_s_memrealtime();
-  if (blockIdx.x == 0) { SL_CST(0) }
-#endif
 
   // ---- 1. this workgroup's rows of W (E <= BR * BK = 768: two loads per
   //      thread, both issued before the LDS stores, clamped addresses)
@@ -565,12 +522,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     st_sh = 0;
   }
   __syncthreads();
-  if (blockIdx.x == 0) { SL_CST(2) }
   if (is_last) {
-#ifdef SL_CORE_STAMPS
-    if (tid == 0) g_core_st[10] = st_start;
-#endif
-    SL_CST(3)
     // sum of the nb packed partials, two entries per thread and load
     const int npair = a.ldp >> 1;
     double* Hp = b1;
@@ -602,7 +554,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     }
     __syncthreads();
     if (tid == 0) a.sync[0] = 0u;   // ready for the next launch
-    SL_CST(4)
     if (!FINAL) {
       if (tid < 64) slw::wave_chol_inv<K>(b0, ld, b2, ld, k, cls.fsh, &st_sh);
       __syncthreads();
@@ -636,7 +587,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
         st_sh |= ((const int*)(a.rti + k * k))[0];
       }
       __syncthreads();
-      SL_CST(13)
       {
         constexpr int UB = BK * BK / NT + 1;
         double v[UB];
@@ -658,7 +608,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       final_core<K>(b0, b1, b2, b3, flags, order, cls, a.cbak, k, a.r, a.M, a.N, a.s64, a.status, a.mirror, &st_sh,
                     a.status_or);
     }
-    SL_CST(5)
     // release the waiters
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -666,7 +615,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __hip_atomic_fetch_add(&a.sync[16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    SL_CST(6)
   } else {
     if (tid == 0) {
       // bounded wait (never reached on a sane run: the last arriver has no
@@ -685,7 +633,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     __syncthreads();
   }
 
-  if (blockIdx.x == 0) { SL_CST(7) }
   // ---- 4. rows of Z^T = (W Rinv)^T (INTER) or V = W N (FINAL)
   float* V = FINAL ? (a.optr ? a.optr[2] : a.V) : nullptr;
   if (FINAL) {
@@ -727,10 +674,6 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       else a.Zt[(int64_t)c * n + r0 + row] = f_to_bf16((float)v);
     }
   }
-#ifdef SL_CORE_STAMPS
-  __syncthreads();
-  if (blockIdx.x == 0) { SL_CST(8) }
-#endif
 }
 
 // Out (rows of W, k x nc) = W (n x k f64) B (k x nc f64, row-major), a 32-row
@@ -837,12 +780,6 @@ size_t gram_la_lds() { return GRAM_LA_LDS; }
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
-#ifdef SL_CORE_STAMPS
-SL_API int sl_core_stamps(unsigned long long* host) {
-  SL_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_core_st), sizeof(g_core_st)));
-  return SL_OK;
-}
-#endif
 SL_API int sl_rsvd_make_v(const double* W, int n, int k, int ldw, const double* N, int r, float* V, const double* s64,
                           float* s32, void* stream) {
   if (k < 1 || k > KMAX || r > k) { sl_set_last_error("rsvd_make_v: 1 <= r <= k <= 64"); return SL_ERR_UNSUPPORTED; }

@@ -143,12 +143,16 @@ __global__ void __launch_bounds__(256) k_store_s(const double* __restrict__ s, i
   if ((int)threadIdx.x < r) st_d<T>(out + threadIdx.x, s[threadIdx.x]);
 }
 
-// Cholesky statuses (dropped pivots / rocSOLVER infos) -> the call's status word
-__global__ void k_status_merge(const int* __restrict__ chol_st, int nchol, int* __restrict__ status) {
+// Cholesky statuses (dropped pivots / rocSOLVER infos) and eigensolver
+// statuses -> the call's status word.  st[2]: the Jacobi re-solve of a core
+// the tridiagonal path flagged (st[1]) ran out of sweeps; st[12]: rocSOLVER
+// syevd info (k > 64).  Both mean the core's eigenpairs did not converge.
+__global__ void k_status_merge(int* __restrict__ st) {
   if (threadIdx.x == 0) {
-    int st = 0;
-    for (int i = 0; i < nchol; ++i) st |= chol_st[i] ? ST_PIVOT : 0;
-    if (st) atomicOr(status, st);
+    int v = 0;
+    for (int i = 4; i < 12; ++i) v |= st[i] ? ST_PIVOT : 0;
+    if (st[2] || st[12]) v |= ST_NOCONV;
+    if (v) atomicOr(st, v);
   }
 }
 
@@ -425,7 +429,7 @@ int core(GPlan* p, hipStream_t s) {
   rc = slb_gemm(SL_F64, true, false, k, k, k, 1.0, p->Ri, k, p->T1, k, 0.0, p->Cc, k, s);   // C = Rti^T T
   if (rc != SL_OK) return rc;
   if (k <= 64) {
-    SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 8, s));
+    SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 8, s));   // st[1] flag, st[2] re-solve no-convergence
     rc = sl_sym_eig_tridiag(p->Cc, k, k, r, p->eig, 1, p->st + 1, s);
     if (rc != SL_OK) return rc;
     // re-solve by Jacobi only when the tridiagonal path flagged the core (device-side condition)
@@ -450,7 +454,7 @@ int core(GPlan* p, hipStream_t s) {
     return SL_OK;
   });
   if (rc != SL_OK) return rc;
-  k_status_merge<<<1, 64, 0, s>>>(p->st + 4, 8, p->st);
+  k_status_merge<<<1, 64, 0, s>>>(p->st);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -526,8 +530,10 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   const int64_t o_md = off;  off = align256(off + (int64_t)k * r * 8);
   const int64_t o_vf = off;  off = align256(off + n * r * 8);
   const int64_t o_gw = off;
+  // k > 64: f32 AND bf16 A keep Y in f32 and stage GPIECE-row f64 pieces of
+  // it here (gram()); f64 A only reuses it for the k x k eigenvectors
   off = align256(off + (k <= 64 ? sl_tsk_gram64_workspace(m, k)
-                                 : std::max<int64_t>(dt == SL_F32 ? GPIECE * k * 8 : 0, (int64_t)k * k * 8)));
+                                 : std::max<int64_t>(dt != SL_F64 ? GPIECE * k * 8 : 0, (int64_t)k * k * 8)));
   // f32 / f64 A: row-chunk partials of A^T Y (and of Y^T Y), <= 64 MB of slabs
   int np = 0;
   int64_t ch = 0;

@@ -287,19 +287,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
   // store issues even for rows past m -- they go to the scratch line)
   const int nst = !FINAL ? 0 : (vecY ? (w * 64 < nvec ? 1 : 0) : 4);
 
-#ifdef SL_PASS_STAMPS
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
-  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), ct0 = __builtin_amdgcn_s_memtime();
-#define SL_STAMP(I)                                                      \
-  {                                                                      \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                   \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
-    if ((I) > 0) st_acc[(I) - 1] += t_ - st_prev;                        \
-    st_prev = t_;                                                        \
-  }
-#else
-#define SL_STAMP(I)
-#endif
 
 #pragma unroll
   for (int p = 0; p < NBUF - 1; ++p)
@@ -307,7 +294,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 
   int slot = 0;
   for (int64_t j = 0; j < nloc; ++j) {
-    SL_STAMP(0)
     // refill the slot iteration j - 1 consumed (its reads were waited for by
     // the MFMAs that used them)
     if (j + NBUF - 1 < nloc) issue(j + NBUF - 1, slot == 0 ? NBUF - 1 : slot - 1);
@@ -319,7 +305,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       const int ns = (int)(j < NBUF - 1 ? j : NBUF - 1);
       wait_vm(nd * G::LPB + ns * nst);
     }
-    SL_STAMP(1)
     const char* region = ring + (slot * WAVES + w) * G::REGION;
     const int64_t r0 = (b0 + j * bstep) * BM;
 
@@ -339,10 +324,8 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
 #pragma unroll
       for (int t = 0; t < KT; ++t) *(f32x4*)&part[w * KP * BM + qidx(16 * t + i16, g4)] = accY[t];
     }
-    SL_STAMP(2)
     lds_barrier();   // (A) the partials of block j are complete
     gram_acc();
-    SL_STAMP(3)
     // ---- step 2: each wave sums its CPW columns over the WAVES partials,
     //      emits y as bf16 hi / lo B-fragment images (and, FINAL, f32 y and
     //      the Y rows straight from the sums)
@@ -382,9 +365,7 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
         }
       }
     }
-    SL_STAMP(4)
     lds_barrier();   // (B) y of block j is complete
-    SL_STAMP(5)
     if (FINAL && vecY && w * 64 < nvec) {
       // one float4 per lane of the block's contiguous Y image (ragged rows /
       // idle lanes write the scratch line: the store count stays exact)
@@ -396,7 +377,6 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
       *(f32x4*)dst = v;   // (a non-temporal store measured 507 vs 446 us for the pass)
     }
 
-    SL_STAMP(6)
 
     // ---- step 3: W += A^T (y_hi + y_lo).  K = 32 packs [8 rows of y_hi |
     //      the same 8 rows of y_lo]: lane group g covers rows 8 (g >> 1) .. +7
@@ -447,30 +427,8 @@ k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const b
         for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
       }
     }
-#ifdef SL_PASS_STAMPS
-    // drain the MFMAs so the stamp sees their time
-    {
-      float sink = 0.f;
-#pragma unroll
-      for (int a = 0; a < NW / 16; ++a)
-#pragma unroll
-        for (int t = 0; t < KT; ++t) sink += accW[a][t][0];
-      asm volatile("" ::"v"(sink));
-    }
-#endif
-    SL_STAMP(7)
     slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
-#ifdef SL_PASS_STAMPS
-  if (lane == 0 && scratch) {
-    unsigned long long* d = (unsigned long long*)scratch + 256 + ((int64_t)blockIdx.x * WAVES + w) * 10;
-    for (int i = 0; i < 7; ++i) d[i] = st_acc[i];
-    d[7] = (unsigned long long)nloc;
-    d[8] = __builtin_amdgcn_s_memtime() - ct0;
-    d[9] = __builtin_amdgcn_s_memrealtime() - rt0;
-  }
-#endif
-#undef SL_STAMP
   gram_acc();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 

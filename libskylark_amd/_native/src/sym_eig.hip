@@ -28,7 +28,8 @@ constexpr int NT = 256;
 
 __global__ void __launch_bounds__(NT)
 k_sym_eig_jacobi(const double* __restrict__ Cin, int k, int ldc, int r, double* __restrict__ out,
-                 int want_sqrt, int max_sweeps, int* __restrict__ sweeps_out, const int* __restrict__ flag) {
+                 int want_sqrt, int max_sweeps, int* __restrict__ sweeps_out, const int* __restrict__ flag,
+                 int* __restrict__ noconv = nullptr) {
   __shared__ double AB[2][KMAX][KMAX + 1];   // ping-pong copies of A
   __shared__ double V[KMAX][KMAX + 1];
   __shared__ double cs[KMAX / 2], sn[KMAX / 2];
@@ -127,6 +128,9 @@ k_sym_eig_jacobi(const double* __restrict__ Cin, int k, int ldc, int r, double* 
     out[k * r + tid] = want_sqrt ? sqrt(l > 0.0 ? l : 0.0) : l;
   }
   if (tid == 0 && sweeps_out) *sweeps_out = sweep;
+  // conditional re-solve: report a Jacobi run that used every sweep and was
+  // still rotating (the caller maps it to its "no convergence" status bit)
+  if (tid == 0 && noconv && sweep >= max_sweeps) *noconv = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -149,7 +153,6 @@ __global__ void __launch_bounds__(512) k_sym_eig_wave(const double* __restrict__
   __shared__ int bad, fb;
   const int tid = threadIdx.x;
   if (tid == 0) { bad = 0; fb = 0; }
-  SLW_STAMP(0)
   __syncthreads();
   if (tid < 64) slw::wave_tridiag<K>(C, ldc, k, refl, K + 1, dd, ee, vsh, wsh, &bad);
   __syncthreads();
@@ -196,42 +199,11 @@ SL_API int sl_sym_eig_topr(const double* C, int k, int ldc, int r, double* out, 
 SL_API int sl_sym_eig_topr_if(const double* C, int k, int ldc, int r, double* out, int want_sqrt, int max_sweeps,
                               const int* flag, void* stream) {
   if (k <= 0 || k > KMAX || r <= 0 || r > k || ldc < k) return SL_ERR_DIMENSION;
+  // flag[1]: set when the re-solve itself ran out of sweeps
   k_sym_eig_jacobi<<<1, NT, 0, (hipStream_t)stream>>>(C, k, ldc, r, out, want_sqrt,
-                                                       max_sweeps > 0 ? max_sweeps : 30, nullptr, flag);
+                                                       max_sweeps > 0 ? max_sweeps : 30, nullptr, flag,
+                                                       const_cast<int*>(flag) + 1);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
-#ifdef SL_EIG_STAMPS
-namespace {
-// diagnostic: the tridiagonal (d, e) of the one-wave reduction and the
-// multisection eigenvalues of it (ascending index order as sym_top_eig
-// returns them, descending values), for accuracy checks against LAPACK
-template <int K>
-__global__ void __launch_bounds__(512) k_tridiag_dbg(const double* __restrict__ C, int k, double* __restrict__ out) {
-  __shared__ double refl[K * (K + 1)];
-  __shared__ double sc[3 * 64 * (K + 1)];
-  __shared__ __attribute__((aligned(16))) double dd[K], ee[K], lam[K], vsh[2 * K], wsh[2 * K];
-  __shared__ int bad, fb;
-  const int tid = threadIdx.x;
-  if (tid == 0) { bad = 0; fb = 0; }
-  __syncthreads();
-  if (tid < 64) slw::wave_tridiag<K>(C, k, k, refl, K + 1, dd, ee, vsh, wsh, &bad);
-  __syncthreads();
-  if (tid < K) { out[tid] = dd[tid]; out[K + tid] = ee[tid]; }
-  __syncthreads();
-  slw::sym_top_eig<K, 512>(dd, ee, refl, K + 1, k, 1, lam, out + 3 * K, 1, k, sc, &fb);
-  if (tid < k) out[2 * K + tid] = lam[tid];
-}
-}  // namespace
-SL_API int sl_tridiag_dbg(const double* C, int k, double* out, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (k <= 40) k_tridiag_dbg<40><<<1, 512, 0, s>>>(C, k, out);
-  else k_tridiag_dbg<64><<<1, 512, 0, s>>>(C, k, out);
-  return SL_OK;
-}
-SL_API int sl_eig_stamps(unsigned long long* host) {
-  SL_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_eig_st), sizeof(g_eig_st)));
-  return SL_OK;
-}
-#endif

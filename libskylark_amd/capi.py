@@ -212,8 +212,9 @@ def kernel_gram(dirX: int, dirY: int, k, X_kind, X_desc, Y_kind, Y_desc, K_desc)
     """dir codes as the reference python binding: 1 = columns, 2 = rows."""
     X = _input(X_kind, X_desc)
     Y = _input(Y_kind, Y_desc)
-    d = {1: "columns", 2: "rows", 0: "columns"}
-    K = k.gram(X, dirX=d[int(dirX)], dirY=d[int(dirY)], Y=Y)
+    # reference ckernel.cpp:112-115: SL_COLUMNS (1) is columns, anything else rows
+    d = lambda v: "columns" if int(v) == 1 else "rows"  # noqa: E731
+    K = k.gram(X, dirX=d(dirX), dirY=d(dirY), Y=Y)
     _write_dense(K_desc, K)
 
 
@@ -221,7 +222,7 @@ def kernel_gram(dirX: int, dirY: int, k, X_kind, X_desc, Y_kind, Y_desc, K_desc)
 def readlibsvm(fname: str, X_kind, X_out, Y_desc, direction: int, min_d: int, max_n: int):
     from .io import read_libsvm
     X, Y = read_libsvm(fname, min_d=int(min_d), max_n=int(max_n), sparse=(X_kind == "SparseMatrix"))
-    if int(direction) in (0, 1):  # columns: examples are columns (d x n), as the reference default
+    if int(direction) == 1:  # SL_COLUMNS: examples are columns (d x n); anything else rows (reference cio.cpp:17-18)
         X = X.t()
         Yd = Y.reshape(1, -1)
     else:

@@ -52,7 +52,11 @@ class ApproximateSVDParams:
     skip_qr: bool = False
     sketch: str = "JLT"          # "JLT" (reference) | "FJLT" | "CWT"
     graph: bool = True           # replay the device path as hipGraphs once warm
-    check: bool = False          # device path: wait for this call's status word and raise on a failure
+    # device path: wait for this call's status word and raise / warn for THIS
+    # call.  None = True on the general-precision engine (f32 / f64 operands,
+    # the host path's synchronous failure semantics) and False on the fused
+    # bf16 engine (flags surface on the next call or last_device_status())
+    check: bool | None = None
     am_i_printing: bool = False
     log_level: int = 0
     prefix: str = ""
@@ -597,12 +601,35 @@ _T0 = [0.0]
 
 def _engine_ok(A_loc, n, k) -> bool:
     return (A_loc.is_cuda and A_loc.dtype == torch.bfloat16 and A_loc.stride(1) == 1 and A_loc.stride(0) % 8 == 0
-            and n % 8 == 0 and 16 <= n <= 1024 and 1 <= k <= 48)
+            and n % 8 == 0 and 16 <= n <= 1024 and 1 <= k <= 48 and A_loc.shape[0] >= 1)
 
 
 def _gen_ok(A_loc, n, k) -> bool:
     return (A_loc.is_cuda and A_loc.dtype in (torch.float32, torch.float64, torch.bfloat16)
-            and A_loc.stride(1) == 1 and A_loc.stride(0) >= n and 1 <= k <= min(n, 128))
+            and A_loc.stride(1) == 1 and A_loc.stride(0) >= n and 1 <= k <= min(n, 128) and A_loc.shape[0] >= 1)
+
+
+_AGREED: dict = {}
+
+
+def _agree_engines(comm, A_loc, fused: bool, gen: bool):
+    """(fused, gen) agreed by every rank: a rank that owns no rows (or any
+    other local reason) must not send the others into segments whose
+    collectives it never joins -- one all-reduce (min) per operand geometry,
+    cached."""
+    if comm.size <= 1:
+        return fused, gen
+    key = (A_loc.data_ptr(), tuple(A_loc.shape), A_loc.dtype, comm.size, id(getattr(comm, "group", None)))
+    got = _AGREED.get(key)
+    if got is None:
+        f = torch.tensor([1.0 if fused else 0.0, 1.0 if gen else 0.0], dtype=torch.float64, device=A_loc.device)
+        comm.all_reduce_min(f)
+        got = (bool(f[0] > 0.5), bool(f[1] > 0.5))
+        if len(_AGREED) >= 16:
+            _AGREED.pop(next(iter(_AGREED)))
+        _AGREED[key] = got
+    return got
+
 
 
 def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
@@ -611,8 +638,8 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     engine (one read of A per pass); any other f32 / f64 / bf16 A with k <= 128:
     the general-precision engine.  Returns None when neither covers the call
     (the caller then runs the host-driven path)."""
-    fused = _engine_ok(A_loc, n, k)
-    if not fused and not _gen_ok(A_loc, n, k):
+    fused, gen = _agree_engines(comm, A_loc, _engine_ok(A_loc, n, k), _gen_ok(A_loc, n, k))
+    if not fused and not gen:
         return None
     if _TRACE:
         print(f"[svd.trace] python_prep={(time.perf_counter() - _T0[0]) * 1e6:.0f}us", file=sys.stderr)
@@ -653,13 +680,15 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
                 plan = _EnginePlan(A_loc, comm, n, rank, k, q, bool(params.graph) and dev.type == "cuda")
             except (RuntimeError, SkylarkError):
                 # e.g. the boundary grid cannot be co-resident on this device
-                if not _gen_ok(A_loc, n, k):
+                # (a device property: the same on every rank of a node)
+                if not gen:
                     raise
         if plan is None:
             plan = _GenPlan(A_loc, comm, n, rank, k, q)
         _PLANS[key] = plan
     out = plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
-    if params.check:
+    check = params.check if params.check is not None else isinstance(plan, _GenPlan)
+    if check:
         plan.check()
     return out
 

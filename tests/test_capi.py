@@ -647,6 +647,10 @@ C_HOST_DEVICE_PROGRAM = textwrap.dedent(r"""
     int sl_approximate_symmetric_svd(char*, void*, char*, void*, char*, void*, uint16_t, char*, sl_context_t*);
     int sl_faster_least_squares(int, char*, void*, char*, void*, char*, void*, char*, sl_context_t*);
     int sl_readlibsvm(char*, char*, void*, char*, void*, int, int, int);
+    typedef struct sl_kernel_t sl_kernel_t;
+    int sl_create_kernel(char*, int, sl_kernel_t**, ...);
+    int sl_kernel_gram(int, int, sl_kernel_t*, char*, void*, char*, void*, char*, void*);
+    int sl_free_kernel(sl_kernel_t*);
     int sl_free_context(sl_context_t*);
     int sl_runtime_started(void);
     int sl_wrap_raw_matrix(double*, int, int, void**);
@@ -776,9 +780,12 @@ C_HOST_DEVICE_PROGRAM = textwrap.dedent(r"""
         /* LIBSVM reader: dense and sparse, both directions */
         char fn[1024]; snprintf(fn, sizeof fn, "%s/d.libsvm", OUT);
         FILE* f = fopen(fn, "w"); fprintf(f, "1 1:0.5 3:2\n-1 2:1.5\n# comment\n2 4:-1 1:0.25\n"); fclose(f);
-        double X1[4 * 3], Y1[3], X2[3 * 5];
+        double X1[4 * 3], Y1[3], X2[3 * 5], X0[3 * 4], Y0[3];
         if ((rc = sl_readlibsvm(fn, "Matrix", W(X1, 4, 3), "Matrix", W(Y1, 1, 3), 1, 0, -1))) return fail(60, rc);
         if ((rc = sl_readlibsvm(fn, "Matrix", W(X2, 3, 5), NULL, NULL, 2, 5, -1))) return fail(61, rc);
+        /* direction 0 is not SL_COLUMNS: rows, as the reference's cio.cpp maps it */
+        if ((rc = sl_readlibsvm(fn, "Matrix", W(X0, 3, 4), "Matrix", W(Y0, 3, 1), 0, 0, -1))) return fail(63, rc);
+        dump("lib_X0", X0, sizeof X0); dump("lib_Y0", Y0, sizeof Y0);
         void* xs; sl_wrap_raw_sp_matrix(NULL, NULL, NULL, 0, 0, 0, &xs);
         if ((rc = sl_readlibsvm(fn, "SparseMatrix", xs, "Matrix", W(Y1, 1, 3), 1, 0, -1))) return fail(62, rc);
         int xnnz; sl_raw_sp_matrix_nnz(xs, &xnnz);
@@ -786,6 +793,20 @@ C_HOST_DEVICE_PROGRAM = textwrap.dedent(r"""
         sl_raw_sp_matrix_data(xs, xip, xind, xval);
         dump("lib_X1", X1, sizeof X1); dump("lib_Y1", Y1, sizeof Y1); dump("lib_X2", X2, sizeof X2);
         dump("lib_sip", xip, sizeof xip); dump("lib_sind", xind, 4 * xnnz); dump("lib_sval", xval, 8 * xnnz);
+        /* kernel Grams on host Matrix operands (reference capi/ckernel.cpp):
+           X 7 x 300 points as columns, B 9 x 300 points as rows */
+        sl_kernel_t *kg, *kl, *kp;
+        if ((rc = sl_create_kernel("gaussian", N, &kg, 0.9))) return fail(70, rc);
+        if ((rc = sl_create_kernel("laplacian", N, &kl, 1.7))) return fail(71, rc);
+        if ((rc = sl_create_kernel("polynomial", N, &kp, 2, 1.0, 0.01))) return fail(72, rc);
+        double *Kg = malloc(8 * 9 * 7), *Kl = malloc(8 * 7 * 9), *Kp = malloc(8 * 9 * 9);
+        static double At[7 * N];
+        for (int i = 0; i < N; ++i) for (int j = 0; j < 7; ++j) At[j + 7 * i] = A[i + N * j];   /* 7 x N */
+        if ((rc = sl_kernel_gram(2, 1, kg, "Matrix", W(B, 9, N), "Matrix", W(At, 7, N), "Matrix", W(Kg, 9, 7)))) return fail(73, rc);
+        if ((rc = sl_kernel_gram(1, 2, kl, "Matrix", W(At, 7, N), "Matrix", W(B, 9, N), "Matrix", W(Kl, 7, 9)))) return fail(74, rc);
+        if ((rc = sl_kernel_gram(2, 2, kp, "Matrix", W(B, 9, N), "Matrix", W(B, 9, N), "Matrix", W(Kp, 9, 9)))) return fail(75, rc);
+        dump("kg", Kg, 8 * 9 * 7); dump("kl", Kl, 8 * 7 * 9); dump("kp", Kp, 8 * 9 * 9);
+        sl_free_kernel(kg); sl_free_kernel(kl); sl_free_kernel(kp);
         printf("%d\n", sl_runtime_started());
         for (int t = 0; t < 18; ++t) sl_free_sketch_transform(T[t]);
         sl_free_sketch_transform(TL); sl_free_context(ctx);
@@ -879,7 +900,21 @@ def test_host_operands_on_device_interpreter_free(capi, tmp_path):
     np.testing.assert_allclose(ld("lib_X1", (4, 3)), [[0.5, 0, 0.25], [0, 1.5, 0], [2, 0, 0], [0, 0, -1]])
     np.testing.assert_allclose(ld("lib_Y1", (1, 3)), [[1, -1, 2]])
     np.testing.assert_allclose(ld("lib_X2", (3, 5)), [[0.5, 0, 2, 0, 0], [0, 1.5, 0, 0, 0], [0.25, 0, 0, -1, 0]])
+    np.testing.assert_allclose(ld("lib_X0", (3, 4)), ld("lib_X1", (4, 3)).T)   # direction 0 = rows
+    np.testing.assert_allclose(ld("lib_Y0", (3, 1)), [[1], [-1], [2]])
     sip = np.fromfile(tmp_path / "lib_sip.bin", dtype=np.int32)
     Xs = sp.csc_matrix((np.fromfile(tmp_path / "lib_sval.bin"), np.fromfile(tmp_path / "lib_sind.bin", dtype=np.int32),
                         sip), shape=(4, 3)).toarray()
     np.testing.assert_allclose(Xs, ld("lib_X1", (4, 3)))
+    # kernel Grams on host matrices (native): against the runtime's kernels
+    Xp = torch.from_numpy(A.copy())            # 300 x 7: the 7 points as columns of A^T
+    Bp = torch.from_numpy(Bm.copy())           # 9 x 300: 9 points as rows
+    kg = sk.ml.Gaussian(300, sigma=0.9)
+    kl = sk.ml.Laplacian(300, sigma=1.7)
+    kp = sk.ml.Polynomial(300, q=2, c=1.0, gamma=0.01)
+    np.testing.assert_allclose(ld("kg", (9, 7)), kg.gram(Bp, dirX="rows", dirY="columns", Y=Xp).numpy(),
+                               rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(ld("kl", (7, 9)), kl.gram(Xp, dirX="columns", dirY="rows", Y=Bp).numpy(),
+                               rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(ld("kp", (9, 9)), kp.gram(Bp, dirX="rows", dirY="rows", Y=Bp).numpy(),
+                               rtol=1e-9, atol=1e-12)

@@ -73,3 +73,35 @@ def test_general_engine_matches_host_path_f64():
     Uc, sc, Vc = sk.nla.approximate_svd(torch.from_numpy(A64), 8, sk.Context(seed=9), prm)
     np.testing.assert_allclose(sg.cpu().numpy(), sc.numpy(), rtol=1e-10)
     np.testing.assert_allclose(np.abs(Vg.cpu().numpy()), np.abs(Vc.numpy()), atol=1e-8)
+
+
+def test_general_engine_bf16_k_above_64():
+    """bf16 A with rank 40 (k = 80 > 64): Y is kept in f32 and its Gram staged
+    in f64 pieces through the plan workspace -- sized for bf16 too (it was
+    sized for f32 only, and this call wrote past the plan allocation)."""
+    import libskylark_amd as sk
+    from libskylark_amd.nla import svd as S
+    A64 = _planted(6000, 1536, 48, decay=0.9, noise=1e-6, seed=4)
+    A = torch.from_numpy(A64).to("cuda", torch.bfloat16)
+    A64 = A.double().cpu().numpy()
+    prm = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="FJLT", check=True)
+    U, s, V = sk.nla.approximate_svd(A, 40, sk.Context(seed=3), prm)
+    plan = [p for p in S._PLANS.values() if p.Aref() is A][0]
+    assert isinstance(plan, S._GenPlan) and plan.k == 80
+    _check(A64, U, s, V, 40, 2e-2, 2e-3, 5e-2)
+
+
+def test_general_engine_rank_deficient_f32():
+    """f32 operand of exact rank 15 < k = 40: the CholeskyQR factors drop the
+    null directions (pivot dropping) and the top-10 SVD still matches numpy,
+    as the host path's TSQR fallback does on the same operand."""
+    import libskylark_amd as sk
+    g = np.random.RandomState(11)
+    A64 = (g.randn(5000, 15) * (10.0 * 0.8 ** np.arange(15))) @ g.randn(15, 600)
+    A = torch.from_numpy(A64).to("cuda", torch.float32)
+    A64 = A.double().cpu().numpy()
+    prm = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="JLT")
+    U, s, V = sk.nla.approximate_svd(A, 10, sk.Context(seed=2), prm)
+    _check(A64, U, s, V, 10, 1e-4, 1e-4, 1e-3)
+    Uc, sc, Vc = sk.nla.approximate_svd(torch.from_numpy(A64), 10, sk.Context(seed=2), prm)
+    np.testing.assert_allclose(s.double().cpu().numpy(), sc.double().numpy(), rtol=1e-4)
