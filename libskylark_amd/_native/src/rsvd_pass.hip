@@ -29,6 +29,8 @@
 //     from ds_read_b64_tr_b16 of the same swizzled LDS image step 1 read;
 //   * row-major y with stride KP + 4 floats keeps the ds_add and every y read
 //     conflict-free under the gfx950 lane grouping (4 * (KP + 4) = 16 mod 32).
+#include <algorithm>
+
 #include "sl_common.hpp"
 
 namespace {
@@ -545,6 +547,430 @@ k_rsvd_reduce_wg(const float* __restrict__ wslab, int64_t tw, int cols, double* 
   else reduce_body<double, double>(gslab, nslab, tg, cols, gout, ldg, blockIdx.x - gw, part);
 }
 
+// ---------------------------------------------------------------- pass v5
+// Role-split form of the fused pass (same slabs, same Y / Gram outputs as v4):
+//   * step 1 (y = A_blk Z) is owned by KT "y waves": wave t < KT computes the
+//     whole 16 x 16 tile t of y over ALL n columns (its Z^T slice, 32 bf16
+//     fragments, in registers), so y never needs a cross-wave sum -- the
+//     v4 partial tile, its reducer phase and one of its two barriers per block
+//     are gone;
+//   * step 3 (W += A^T (y_hi + y_lo)) is split over all 8 waves by 16-column
+//     W tiles, sized so every SIMD pair (waves w and w + 4 share a SIMD) gets
+//     about the same matrix-core work (the y waves take 0-2 W tiles);
+//   * ONE barrier per block: the phase after barrier j runs step 3 of block j
+//     (y(j) published before it) and, on the y waves, step 1 of block j + 1
+//     into the other half of a double-buffered y image; the DMA of block
+//     j + 1 is waited for by every wave (its own LDS-DMA, counted vmcnt)
+//     before barrier j, so any wave may read any region;
+//   * the ring keeps NBUF = 4 slots of 16 rows x 1024 columns: in phase j
+//     slots j (step 3) and j + 1 (step 1) are read, j + 2 and j + 3 in flight.
+// The two roles run separately instantiated loop bodies (the y waves hold
+// 32 Z fragments and <= 2 W tiles, the W waves <= 12 W tiles), so the
+// register allocation is the larger of the two, not their sum.
+struct P5Tiles {
+  int base[8];
+  int cnt[8];
+  int gown[8];   // Gram tiles: first tau owned and stride (FINAL), per wave
+};
+
+constexpr int P5_NBUF = 4, P5_BM = 16, P5_ROWB = 256, P5_REGION = 4096, P5_LPB = 4, P5_T1 = 2, P5_T2 = 12,
+              P5_GS = 2;
+
+template <int KT>
+constexpr int p5_y16p() { return 16 * KT * P5_BM * 2 + 16; }
+template <int KT, bool FINAL>
+constexpr int p5_lds() {
+  return P5_NBUF * 8 * P5_REGION + 4 * p5_y16p<KT>() + (FINAL ? 2 * P5_BM * 16 * KT * 4 : 0);
+}
+
+template <int KT, bool FINAL, bool GRAM, bool YROLE, int TM, int KS>
+__device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
+                                        const bf16_t* __restrict__ Zt, int k, float* __restrict__ Wslab,
+                                        double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
+                                        float* __restrict__ scratch, const P5Tiles& pt, char* smem, const int w) {
+  constexpr int KP = 16 * KT, BM = P5_BM, NBUF = P5_NBUF, ROWB = P5_ROWB, REGION = P5_REGION, LPB = P5_LPB;
+  constexpr int Y16P = p5_y16p<KT>();
+  char* ring = smem;
+  char* y16b = smem + NBUF * 8 * REGION;                 // [2 buffers][hi | lo]
+  float* yfb = (float*)(y16b + 4 * Y16P);                // FINAL: [2][BM * k] f32 rows of y'
+  const int lane = threadIdx.x & 63;
+  const int g4 = lane >> 4, i16 = lane & 15;
+  const int64_t nblocks = (m + BM - 1) / BM;
+  const int64_t b0 = blockIdx.x, bstep = gridDim.x;
+  const int64_t nloc = b0 < nblocks ? (nblocks - 1 - b0) / bstep + 1 : 0;
+  // step 1 runs KS (16 or 32) k-steps of 32 columns: regions past n were
+  // zeroed (below) and Z is zero past n, so the extra products add exact zeros
+  const bool dma_on = 128 * w < n;                        // this wave's 128-column region exists
+  const int tbase = pt.base[w], tcnt = pt.cnt[w];
+  if (!dma_on) {
+    // never DMA'd: zero this region of every slot once (stale LDS could hold NaNs)
+    for (int sl = 0; sl < NBUF; ++sl)
+      for (int o = lane * 16; o < REGION; o += 1024) *(f32x4*)(ring + (sl * 8 + w) * REGION + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // ---- y waves: Z^T slice of tile t = w (B operand: lane holds Z[32 ks + 8 g4 + j][16 w + i16])
+  bf16x8 zf[YROLE ? KS : 1];
+  if constexpr (YROLE) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int col = 16 * w + i16, kk = 32 * ks + 8 * g4;
+      bf16x8 v = {};
+      if (col < k && kk + 8 <= n) v = *(const bf16x8*)(Zt + (int64_t)col * n + kk);
+      zf[ks] = v;
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(zf[ks]));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  f32x4 accW[TM > 0 ? TM : 1][KT];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr bool G_ON = GRAM && !YROLE;
+  f64x4 accG[G_ON ? P5_GS : 1];
+  f32x4 gblk[G_ON ? P5_GS : 1];
+#pragma unroll
+  for (int s = 0; s < (G_ON ? P5_GS : 1); ++s) {
+    accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+    gblk[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr int GT = KT * (KT + 1) / 2;
+  const int gfirst = pt.gown[w] & 0xff, gstride = pt.gown[w] >> 8;   // Gram tiles gfirst, +gstride, ...
+  bool gpend = false;
+  auto gram_acc = [&]() {
+    if constexpr (G_ON) {
+      if (gpend) {
+#pragma unroll
+        for (int s = 0; s < P5_GS; ++s)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) accG[s][e] += (double)gblk[s][e];
+      }
+    }
+  };
+
+  // LDS-DMA of this wave's region of row block blk into slot `slot` (v4 image)
+  unsigned voff[LPB];
+#pragma unroll
+  for (int i = 0; i < LPB; ++i) {
+    const int byte = i * 1024 + lane * 16;
+    const int row = byte / ROWB;
+    const int sl = (byte % ROWB) / 16;
+    const int chunk = sl ^ swz4<16>(row);
+    int col = 128 * w + chunk * 8;
+    col = col + 8 <= n ? col : n - 8;
+    voff[i] = (unsigned)((row * lda + col) * 2);
+  }
+  // (vmcnt bookkeeping is analytic, see the main loop: no per-slot counters)
+  auto issue = [&](int64_t blk) {
+    if (!dma_on) return;
+    const int slot = (int)(blk % NBUF);
+    char* region = ring + (slot * 8 + w) * REGION;
+    const int64_t r0 = (b0 + blk * bstep) * BM;
+    if (r0 + BM <= m) {
+      const bf16_t* base = A + r0 * lda;
+#pragma unroll
+      for (int i = 0; i < LPB; ++i) {
+        const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
+        glds16s(voff[i], (const void*)base, dst);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LPB; ++i) {
+        const int byte = i * 1024 + lane * 16;
+        const int row = byte / ROWB;
+        int64_t grow = r0 + row;
+        grow = grow < m ? grow : m - 1;
+        const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
+        glds16((const void*)((const char*)(A + grow * lda) + (voff[i] - (unsigned)(row * lda * 2))), dst);
+      }
+    }
+  };
+  const int lpb = dma_on ? LPB : 0;
+
+  // ---- step 1 of block jb (y waves): tile w of y over all columns, published
+  //      as the bf16 hi / lo B-fragment images (and, FINAL, the f32 rows of y')
+  auto step1 = [&](int64_t jb) {
+    if constexpr (YROLE) {
+      const char* reg0 = ring + (int)(jb % NBUF) * 8 * REGION;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const int sw = swz4<16>(i16);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int chunk = ((ks & 3) << 2) + g4;
+        const bf16x8 af = *(const bf16x8*)(reg0 + (ks >> 2) * REGION + i16 * ROWB + ((chunk ^ sw) << 4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zf[ks], acc, 0, 0, 0);
+      }
+      const int64_t r0 = (b0 + jb * bstep) * BM;
+      if (r0 + BM > m) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (r0 + 4 * g4 + e >= m) acc[e] = 0.f;
+      }
+      s16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const short h = bf16_bits(acc[e]);
+        hi[e] = h;
+        lo[e] = bf16_bits(acc[e] - bf16_val(h));
+      }
+      char* y16 = y16b + (int)(jb & 1) * 2 * Y16P;
+      const int col = 16 * w + i16;
+      *(s16x4*)(y16 + col * 32 + g4 * 8) = hi;
+      *(s16x4*)(y16 + Y16P + col * 32 + g4 * 8) = lo;
+      if constexpr (FINAL) {
+        float* yf = yfb + (int)(jb & 1) * BM * KP;
+        if (col < k) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) yf[(4 * g4 + e) * k + col] = bf16_val(hi[e]) + bf16_val(lo[e]);
+        }
+      }
+    }
+  };
+
+  // ---- FINAL: this wave's share of block jb's stored Y (after the barrier that
+  //      published it).  Store waves: the W waves 0.. of the W role, one
+  //      instruction each (float4 rows when ldy == k, else 4-B elements).
+  const bool vecY = FINAL && (k % 4 == 0) && (ldy == k);
+  const int wy = YROLE ? -1 : w - KT;                 // index among the W waves
+  const int nyv = (BM * k + (vecY ? 255 : 63)) / (vecY ? 256 : 64);   // store instructions per block
+  const int nst = (!FINAL || wy < 0 || wy >= nyv) ? 0 : (nyv - wy + (8 - KT) - 1) / (8 - KT);
+  auto store_y = [&](int64_t jb) {
+    if constexpr (FINAL && !YROLE) {
+      const float* yf = yfb + (int)(jb & 1) * BM * KP;
+      const int64_t r0 = (b0 + jb * bstep) * BM;
+      for (int q = wy; q < nyv; q += 8 - KT) {
+        if (vecY) {
+          const int t = q * 64 + lane;
+          const bool ok = t < BM * k / 4 && r0 + (4 * t) / k < m;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (ok) v = *(const f32x4*)&yf[4 * t];
+          float* dst = ok ? Y + r0 * ldy + 4 * t : scratch + 4 * lane;
+          *(f32x4*)dst = v;
+        } else {
+          const int t = q * 64 + lane;
+          const int row = t / k, col = t - (t / k) * k;
+          const bool ok = t < BM * k && r0 + row < m;
+          const float v = ok ? yf[t] : 0.f;
+          float* dst = ok ? Y + (r0 + row) * ldy + col : scratch + lane;
+          *dst = v;
+        }
+      }
+    }
+  };
+
+  // ---- step 3 of block j: W tiles of this wave (+ FINAL Gram tiles of y')
+  auto step3 = [&](int64_t j) {
+    const char* slotp = ring + (int)(j % NBUF) * 8 * REGION;
+    const char* y16 = y16b + (int)(j & 1) * 2 * Y16P;
+    const int rb = 8 * (g4 >> 1);
+    const char* yp = y16 + (g4 & 1) * Y16P + rb * 2;
+    bf16x8 yfr[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) yfr[t] = *(const bf16x8*)(yp + (16 * t + i16) * 32);
+    if constexpr (G_ON) {
+      // this wave's Gram tiles tau = gfirst + s * gstride (slot s), operands
+      // picked by selects; a wave owning none skips, a second slot past GT
+      // multiplies a dummy pair that is never stored
+#pragma unroll
+      for (int sg = 0; sg < P5_GS; ++sg) {
+        if (gstride == 0) break;
+        int tau = gfirst + sg * gstride;
+        tau = tau < GT ? tau : 0;
+        const int t1 = tau < KT ? 0 : (tau < 2 * KT - 1 ? 1 : 2);
+        const int t2 = t1 == 0 ? tau : (t1 == 1 ? tau - KT + 1 : 2);
+        bf16x8 y1 = yfr[0], y2 = yfr[0];
+#pragma unroll
+        for (int t = 1; t < KT; ++t) {
+          y1 = t1 == t ? yfr[t] : y1;
+          y2 = t2 == t ? yfr[t] : y2;
+        }
+        const bf16x8 ysw = *(const bf16x8*)(y16 + ((g4 & 1) ^ 1) * Y16P + rb * 2 + (16 * t2 + i16) * 32);
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+        gblk[sg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y1, y2, z4, 0, 0, 0);
+        gblk[sg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(y1, ysw, gblk[sg], 0, 0, 0);
+      }
+      gpend = true;
+    }
+    (void)GT;
+    const int q = i16 >> 2, p = i16 & 3;
+#pragma unroll
+    for (int ct = 0; ct < TM; ++ct) {
+      {
+        // a slot past this wave's count re-reads its first tile into an
+        // accumulator that is never stored (no branch in the MFMA stream)
+        const int gt = tbase + (YROLE || ct < tcnt ? ct : 0);
+        const char* region = slotp + (gt >> 3) * REGION;
+        const int chunk = 2 * (gt & 7) + (p >> 1);
+        const int ra = rb + q, rbb = rb + 4 + q;
+        const char* aa = region + ra * ROWB + ((chunk ^ swz4<16>(ra)) << 4) + (p & 1) * 8;
+        const char* ab2 = region + rbb * ROWB + ((chunk ^ swz4<16>(rbb)) << 4) + (p & 1) * 8;
+        const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)aa);
+        const s16x4 b4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)ab2);
+        s16x8 a8;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a8[u] = a4[u];
+          a8[4 + u] = b4[u];
+        }
+        const bf16x8 af8 = __builtin_bit_cast(bf16x8, a8);
+#pragma unroll
+        for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: NBUF - 1 blocks in flight, block 0 landed everywhere, y(0)
+#pragma unroll
+  for (int b = 0; b < NBUF - 1; ++b)
+    if (b < nloc) issue(b);
+  // block 0 landed: younger are the DMAs of blocks 1 and 2
+  if (nloc > 0) wait_vm(lpb * ((1 < nloc) + (2 < nloc)));
+  lds_barrier();
+  if (nloc > 0) step1(0);
+
+  for (int64_t j = 0; j < nloc; ++j) {
+    // block j + 1 landed (own DMA), then the phase barrier: y(j) published,
+    // every wave past step 3 of block j - 1 (its slot is free again).  Issue
+    // order of a phase p: DMA(p + 3), then the Y stores of block p, so the
+    // ops younger than DMA(j + 1) are DMA(j + 2) and the stores of phases
+    // max(0, j - 2) .. j - 1
+    if (j + 1 < nloc) wait_vm(lpb * (j + 2 < nloc) + nst * (int)(j < 2 ? j : 2));
+    lds_barrier();
+    gram_acc();
+    if (j + NBUF - 1 < nloc) issue(j + NBUF - 1);
+    if constexpr (FINAL && !YROLE) store_y(j);
+    if (j + 1 < nloc) step1(j + 1);
+    step3(j);
+  }
+  gram_acc();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- W partial slab [n][k]: this wave's tiles
+  {
+    float* ws = Wslab + (int64_t)blockIdx.x * n * k;
+#pragma unroll
+    for (int ct = 0; ct < TM; ++ct)
+      if (ct < tcnt) {
+        const int gt = tbase + ct;
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 16 * gt + 4 * g4 + e, col = 16 * t + i16;
+            if (row < n && col < k) ws[(int64_t)row * k + col] = accW[ct][t][e];
+          }
+      }
+  }
+  if constexpr (G_ON) {
+    double* gs = Gslab + (int64_t)blockIdx.x * k * k;
+#pragma unroll
+    for (int sg = 0; sg < P5_GS; ++sg) {
+      const int tau = gfirst + sg * gstride;
+      if (gstride == 0 || tau >= GT) break;
+      const int t1 = tau < KT ? 0 : (tau < 2 * KT - 1 ? 1 : 2);
+      const int t2 = t1 == 0 ? tau : (t1 == 1 ? tau - KT + 1 : 2);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * t1 + 4 * g4 + r, jj = 16 * t2 + i16;
+        if (i < k && jj < k && (t1 != t2 || i <= jj)) {
+          gs[i * k + jj] = accG[sg][r];
+          if (i != jj) gs[jj * k + i] = accG[sg][r];
+        }
+      }
+    }
+  }
+}
+
+template <int KT, bool FINAL, bool GRAM, int KS>
+__global__ void __launch_bounds__(512, 1)
+k_rsvd_pass5(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const bf16_t* __restrict__ Zt, int k,
+             float* __restrict__ Wslab, double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
+             float* __restrict__ scratch, P5Tiles pt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w < KT) {
+    // the y waves' W-tile count is a compile-time constant of their body
+    const int yt = pt.cnt[0];
+    if (yt == 0)
+      p5_body<KT, FINAL, GRAM, true, 0, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+    else if (yt == 1)
+      p5_body<KT, FINAL, GRAM, true, 1, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+    else
+      p5_body<KT, FINAL, GRAM, true, 2, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+  } else {
+    p5_body<KT, FINAL, GRAM, false, P5_T2, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+  }
+}
+
+// W-tile / Gram-tile ownership for (n, KT): the y waves (0 .. KT-1) take T1 <=
+// 2 W tiles each, the W waves the rest in order; T1 minimises the largest
+// per-SIMD-pair (w, w + 4) matrix-core load.  Gram tiles round-robin over the
+// W waves.  Returns false when the tiles do not fit the register budget.
+bool p5_tiles(int n, int KT, P5Tiles* pt) {
+  const int nt16 = (n + 15) / 16, nks = (n + 31) / 32, nw = 8 - KT;
+  int best = 1 << 30, bestT1 = -1;
+  for (int T1 = 0; T1 <= P5_T1; ++T1) {
+    const int rem = nt16 - KT * T1;
+    if (rem < 0) break;
+    const int T2 = (rem + nw - 1) / nw;
+    if (T2 > P5_T2) continue;
+    int cnt[8];
+    int left = rem;
+    for (int w = 0; w < 8; ++w) {
+      if (w < KT) { cnt[w] = T1; continue; }
+      cnt[w] = left < T2 ? left : T2;
+      left -= cnt[w];
+    }
+    int worst = 0;
+    for (int w = 0; w < 4; ++w) {
+      auto load = [&](int v) { return (v < KT ? nks : 0) + KT * cnt[v]; };
+      worst = std::max(worst, load(w) + load(w + 4));
+    }
+    if (worst < best) { best = worst; bestT1 = T1; }
+  }
+  if (bestT1 < 0) return false;
+  const int rem = nt16 - KT * bestT1, T2 = (rem + nw - 1) / nw;
+  int left = rem, base = 0;
+  for (int w = 0; w < 8; ++w) {
+    const int c = w < KT ? bestT1 : (left < T2 ? left : T2);
+    if (w >= KT) left -= c;
+    pt->base[w] = base;
+    pt->cnt[w] = c;
+    base += c;
+  }
+  const int GT = KT * (KT + 1) / 2;
+  for (int w = 0; w < 8; ++w) {
+    const int wi = w - KT;
+    const bool own = wi >= 0 && wi < GT;
+    pt->gown[w] = own ? (wi | (nw << 8)) : 0;
+    if (own && (GT - wi + nw - 1) / nw > P5_GS) return false;
+  }
+  return true;
+}
+
+template <int KT, bool FINAL, bool GRAM>
+int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab, double* Gslab,
+                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s) {
+  P5Tiles pt{};
+  if (!p5_tiles(n, KT, &pt)) {
+    sl_set_last_error("rsvd_pass: no tile split for this n / k");
+    return SL_ERR_UNSUPPORTED;
+  }
+  constexpr int LDS = p5_lds<KT, FINAL>();
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  if (n > 512) {
+    SL_LDS_ATTR((k_rsvd_pass5<KT, FINAL, GRAM, 32>), LDS);
+    k_rsvd_pass5<KT, FINAL, GRAM, 32><<<grid, 512, LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt);
+  } else {
+    SL_LDS_ATTR((k_rsvd_pass5<KT, FINAL, GRAM, 16>), LDS);
+    k_rsvd_pass5<KT, FINAL, GRAM, 16><<<grid, 512, LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt);
+  }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
 int cu_count() {
   static int ncu = -1;
   if (ncu < 0) {
@@ -616,6 +1042,19 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
   const int KT = (k + 15) / 16;
+  if (!(variant & 32)) {
+    // v5 (default): role-split waves, one barrier per block
+#define SL_P5(KTT)                                                                                                 \
+  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s) \
+       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s) \
+                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s)
+    switch (KT) {
+      case 1: SL_P5(1);
+      case 2: SL_P5(2);
+      default: SL_P5(3);
+    }
+#undef SL_P5
+  }
   const bool small = n <= 512;
   const int nbuf = (variant & 15) == 3 ? 3 : 4;
 #define SL_P(NW, KTT, NB)                                                                                    \

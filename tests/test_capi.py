@@ -794,16 +794,14 @@ C_HOST_DEVICE_PROGRAM = textwrap.dedent(r"""
         dump("lib_X1", X1, sizeof X1); dump("lib_Y1", Y1, sizeof Y1); dump("lib_X2", X2, sizeof X2);
         dump("lib_sip", xip, sizeof xip); dump("lib_sind", xind, 4 * xnnz); dump("lib_sval", xval, 8 * xnnz);
         /* kernel Grams on host Matrix operands (reference capi/ckernel.cpp):
-           X 7 x 300 points as columns, B 9 x 300 points as rows */
+           A (300 x 7): 7 points as columns; B (9 x 300): 9 points as rows */
         sl_kernel_t *kg, *kl, *kp;
         if ((rc = sl_create_kernel("gaussian", N, &kg, 0.9))) return fail(70, rc);
         if ((rc = sl_create_kernel("laplacian", N, &kl, 1.7))) return fail(71, rc);
         if ((rc = sl_create_kernel("polynomial", N, &kp, 2, 1.0, 0.01))) return fail(72, rc);
         double *Kg = malloc(8 * 9 * 7), *Kl = malloc(8 * 7 * 9), *Kp = malloc(8 * 9 * 9);
-        static double At[7 * N];
-        for (int i = 0; i < N; ++i) for (int j = 0; j < 7; ++j) At[j + 7 * i] = A[i + N * j];   /* 7 x N */
-        if ((rc = sl_kernel_gram(2, 1, kg, "Matrix", W(B, 9, N), "Matrix", W(At, 7, N), "Matrix", W(Kg, 9, 7)))) return fail(73, rc);
-        if ((rc = sl_kernel_gram(1, 2, kl, "Matrix", W(At, 7, N), "Matrix", W(B, 9, N), "Matrix", W(Kl, 7, 9)))) return fail(74, rc);
+        if ((rc = sl_kernel_gram(2, 1, kg, "Matrix", W(B, 9, N), "Matrix", W(A, N, 7), "Matrix", W(Kg, 9, 7)))) return fail(73, rc);
+        if ((rc = sl_kernel_gram(1, 2, kl, "Matrix", W(A, N, 7), "Matrix", W(B, 9, N), "Matrix", W(Kl, 7, 9)))) return fail(74, rc);
         if ((rc = sl_kernel_gram(2, 2, kp, "Matrix", W(B, 9, N), "Matrix", W(B, 9, N), "Matrix", W(Kp, 9, 9)))) return fail(75, rc);
         dump("kg", Kg, 8 * 9 * 7); dump("kl", Kl, 8 * 7 * 9); dump("kp", Kp, 8 * 9 * 9);
         sl_free_kernel(kg); sl_free_kernel(kl); sl_free_kernel(kp);

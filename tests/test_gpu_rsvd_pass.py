@@ -23,9 +23,23 @@ def L():
     return _lib
 
 
-@pytest.mark.parametrize("m,n,k", [(100_003, 1000, 40), (70_001, 512, 20), (33_333, 256, 8), (4_097, 1000, 40)])
+@pytest.mark.parametrize("m,n,k", [(100_003, 1000, 40), (70_001, 512, 20), (33_333, 256, 8), (4_097, 1000, 40),
+                                   (257, 1024, 48), (9_999, 520, 33), (100, 16, 1)])
 @pytest.mark.parametrize("final", [0, 1, 2])
-def test_pass_matches_fp64(L, m, n, k, final):
+@pytest.mark.parametrize("variant", [0, 32])
+def test_pass_matches_fp64(L, m, n, k, final, variant, ldy_pad=0):
+    """variant 0: the role-split v5 pass; 32: the v4 pass (A/B reference)."""
+    if variant == 32 and (m, n, k) not in ((100_003, 1000, 40), (4_097, 1000, 40)):
+        pytest.skip("v4 A/B on the bench shapes only")
+    _run_pass(L, m, n, k, final, variant, ldy_pad)
+
+
+def test_pass_strided_y(L):
+    """ldy != k: the stored Y goes out as 4-B elements (not float4 rows)."""
+    _run_pass(L, 20_011, 1000, 40, 1, 0, 5)
+
+
+def _run_pass(L, m, n, k, final, variant, ldy_pad):
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(m + k)
     A = torch.randn(m, n, device=dev, generator=g).to(torch.bfloat16)
@@ -35,10 +49,11 @@ def test_pass_matches_fp64(L, m, n, k, final):
     ws = torch.zeros(int(L.require().sl_rsvd_pass_workspace(m, n, k)), dtype=torch.uint8, device=dev)
     W = torch.empty(n, k, device=dev, dtype=torch.float64)
     G = torch.zeros(k, k, device=dev, dtype=torch.float64)
-    Y = torch.full((m, k), float("nan"), device=dev)
+    Yfull = torch.full((m, k + ldy_pad), float("nan"), device=dev)
+    Y = Yfull[:, :k]
     st = vp(torch.cuda.current_stream().cuda_stream)
     L.call("sl_rsvd_pass", vp(A.data_ptr()), m, n, n, vp(Zt.data_ptr()), k, vp(ws.data_ptr()),
-           vp(Y.data_ptr()) if final else None, k, final, 0, st)
+           vp(Y.data_ptr()) if final else None, k + ldy_pad, final, variant, st)
     L.call("sl_rsvd_reduce", vp(ws.data_ptr()), m, n, k, vp(W.data_ptr()), 1, k,
            vp(G.data_ptr()) if final == 1 else None, k, st)
     torch.cuda.synchronize()
@@ -49,6 +64,8 @@ def test_pass_matches_fp64(L, m, n, k, final):
     mag = A.double().abs() @ Zd.abs()
     if final:
         assert torch.isfinite(Y).all()
+        if ldy_pad:
+            assert torch.isnan(Yfull[:, k:]).all()   # the padding columns are never written
         # Y = bf16 hi + lo pair of the f32 y: within 2^-16 |y| of y
         assert ((Y.double() - y).abs() <= 2.0 ** -16 * y.abs() + 2e-6 * mag).all()
         Yd = Y.double()
