@@ -148,6 +148,9 @@ def run(a, comm, dev, scaling, square=False):
     step_ms = {"min": round(per[0], 4), "median": round(per[len(per) // 2], 4), "max": round(per[-1], 4)}
     from libskylark_amd.nla.svd import last_device_status
     status = last_device_status(wait=True)
+    # a one-shot all-reduce whose peer missed its bounded wait poisoned that
+    # call's operand with NaN: never report a number from such a run
+    comm.check_collectives()
     orth, resid = check_answer(A, U, s, V, comm)
     red = "one-shot IPC all-reduces" if getattr(comm, "_oneshot", None) else "RCCL all-reduces"
     if grid is not None:
@@ -161,6 +164,7 @@ def run(a, comm, dev, scaling, square=False):
         "parallelism": par, "orth_err": orth, "resid_rel": resid, "status": status,
         "top_singular_values": [round(float(x), 3) for x in s[:3].tolist()],
         "grid_pc": grid.pc if grid is not None else 0,
+        "reduction": comm.oneshot_status() if N > 1 else None,
         "native_fused_pass": bool(tallskinny._native_ok(torch.empty(8, 8, dtype=torch.bfloat16, device=dev),
                                                         2 * a.rank)),
     }
@@ -236,6 +240,10 @@ def main(argv=None):
             "top_singular_values": res["top_singular_values"],
             "native_fused_pass": res["native_fused_pass"],
         }
+        if res["reduction"] is not None:
+            # which small all-reduce ran and, when the one-shot path is off,
+            # why (its collective self-test outcome on this node)
+            out["reduction"] = res["reduction"]
         if sq is not None:
             out["square_grid"] = {"value": round(sq["gbs"], 2), "ms_per_step": round(sq["ms"], 4),
                                   "steps": sq["steps"], "parallelism": sq["parallelism"],

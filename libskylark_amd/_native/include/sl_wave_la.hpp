@@ -133,19 +133,15 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
       fb_[c] = A[j] * r;    // multiplier of row c (valid for c > j)
       wave_lds_sync();
       const double aj = A[j];
+      // the pivot lane switches its column to (0 .. 1, -f_{j+1} .. -f_{K-1})
+      // by a select on the same loaded multipliers (a divergent second pass
+      // over them re-read every multiplier with the other lanes masked off)
+      const bool piv = c == j;
 #pragma unroll
       for (int i = (j + 1) & ~1; i < K; i += 2) {
         const double2 f = *(const double2*)(fb_ + i);
-        if (i > j) A[i] = fma(-f.x, aj, A[i]);
-        A[i + 1] = fma(-f.y, aj, A[i + 1]);
-      }
-      if (c == j) {
-#pragma unroll
-        for (int i = (j + 1) & ~1; i < K; i += 2) {
-          const double2 f = *(const double2*)(fb_ + i);
-          if (i > j) A[i] = -f.x;
-          A[i + 1] = -f.y;
-        }
+        if (i > j) A[i] = piv ? -f.x : fma(-f.x, aj, A[i]);
+        A[i + 1] = piv ? -f.y : fma(-f.y, aj, A[i + 1]);
       }
     }
     if (c == j) A[j] = 1.0;

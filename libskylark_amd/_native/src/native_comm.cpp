@@ -63,9 +63,17 @@ Rccl& rccl() {
   return r;
 }
 
+// all-reduce supplied by the caller (an MPI communicator, a test's process
+// group, ...): sum / prod / max / min of count elements of dtype, device
+// pointers, stream-ordered on `stream` (the callee synchronises as it needs)
+typedef int (*SlAllReduceFn)(const void* send, void* recv, int64_t count, int dtype, int op, void* stream,
+                             void* user);
+
 struct SlComm {
   ncclComm_t comm = nullptr;
   int rank = 0, size = 1;
+  SlAllReduceFn ar = nullptr;   // callback communicator (no RCCL) when set
+  void* user = nullptr;
 };
 
 int check(ncclResult_t r, const char* what) {
@@ -137,6 +145,21 @@ SL_API int sl_comm_init(const void* id, int nranks, int rank, void** comm_out) {
   return SL_OK;
 }
 
+// A communicator whose all-reduce is the caller's function (e.g. an MPI_Allreduce
+// wrapper from a C program, as the reference's C API takes MPI communicators);
+// sl_rsvd_run_comm / sl_rsvd_gen_run_comm only need the all-reduce.  The other
+// collectives report SL_ERR_UNSUPPORTED on such a communicator.
+SL_API int sl_comm_from_allreduce(int rank, int size, SlAllReduceFn fn, void* user, void** comm_out) {
+  if (!fn || size < 1 || rank < 0 || rank >= size) { sl_set_last_error("comm: bad callback communicator"); return SL_ERR_INVALID; }
+  SlComm* c = new SlComm;
+  c->rank = rank;
+  c->size = size;
+  c->ar = fn;
+  c->user = user;
+  *comm_out = c;
+  return SL_OK;
+}
+
 SL_API int sl_comm_destroy(void* comm) {
   SlComm* c = as_comm(comm);
   if (!c) return SL_OK;
@@ -147,6 +170,12 @@ SL_API int sl_comm_destroy(void* comm) {
 
 SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
                               void* stream) {
+  SlComm* c = as_comm(comm);
+  if (c->ar) {
+    const int rc = c->ar(send, recv, count, dtype, op, stream, c->user);
+    if (rc != 0) sl_set_last_error("comm: the caller's all-reduce failed");
+    return rc == 0 ? SL_OK : SL_ERR_GENERIC;
+  }
   ncclDataType_t t; ncclRedOp_t o;
   if (!to_nccl(dtype, &t) || !to_op(op, &o)) { sl_set_last_error("comm: dtype/op"); return SL_ERR_UNSUPPORTED; }
   return check(rccl().all_reduce(send, recv, (size_t)count, t, o, as_comm(comm)->comm, (hipStream_t)stream),
@@ -156,6 +185,7 @@ SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t 
 // recv (count) <- the rank's block of the sum of send (count * size)
 SL_API int sl_comm_reduce_scatter(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
                                   void* stream) {
+  if (as_comm(comm)->ar) { sl_set_last_error("comm: a callback communicator only all-reduces"); return SL_ERR_UNSUPPORTED; }
   ncclDataType_t t; ncclRedOp_t o;
   if (!to_nccl(dtype, &t) || !to_op(op, &o)) { sl_set_last_error("comm: dtype/op"); return SL_ERR_UNSUPPORTED; }
   return check(rccl().reduce_scatter(send, recv, (size_t)count, t, o, as_comm(comm)->comm, (hipStream_t)stream),
@@ -164,6 +194,7 @@ SL_API int sl_comm_reduce_scatter(void* comm, const void* send, void* recv, int6
 
 // recv (count * size) <- concatenation of every rank's send (count)
 SL_API int sl_comm_all_gather(void* comm, const void* send, void* recv, int64_t count, int dtype, void* stream) {
+  if (as_comm(comm)->ar) { sl_set_last_error("comm: a callback communicator only all-reduces"); return SL_ERR_UNSUPPORTED; }
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) { sl_set_last_error("comm: dtype"); return SL_ERR_UNSUPPORTED; }
   return check(rccl().all_gather(send, recv, (size_t)count, t, as_comm(comm)->comm, (hipStream_t)stream),
@@ -172,6 +203,7 @@ SL_API int sl_comm_all_gather(void* comm, const void* send, void* recv, int64_t 
 
 SL_API int sl_comm_broadcast(void* comm, const void* send, void* recv, int64_t count, int dtype, int root,
                              void* stream) {
+  if (as_comm(comm)->ar) { sl_set_last_error("comm: a callback communicator only all-reduces"); return SL_ERR_UNSUPPORTED; }
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) { sl_set_last_error("comm: dtype"); return SL_ERR_UNSUPPORTED; }
   return check(rccl().broadcast(send, recv, (size_t)count, t, root, as_comm(comm)->comm, (hipStream_t)stream),
@@ -185,6 +217,7 @@ SL_API int sl_comm_broadcast(void* comm, const void* send, void* recv, int64_t c
 SL_API int sl_comm_all_to_all_v(void* comm, const void* send, const int64_t* send_counts, const int64_t* send_offs,
                                 void* recv, const int64_t* recv_counts, const int64_t* recv_offs, int dtype,
                                 void* stream) {
+  if (as_comm(comm)->ar) { sl_set_last_error("comm: a callback communicator only all-reduces"); return SL_ERR_UNSUPPORTED; }
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) { sl_set_last_error("comm: dtype"); return SL_ERR_UNSUPPORTED; }
   SlComm* c = as_comm(comm);
@@ -205,12 +238,14 @@ SL_API int sl_comm_all_to_all_v(void* comm, const void* send, const int64_t* sen
 }
 
 SL_API int sl_comm_send(void* comm, const void* buf, int64_t count, int dtype, int peer, void* stream) {
+  if (as_comm(comm)->ar) { sl_set_last_error("comm: a callback communicator only all-reduces"); return SL_ERR_UNSUPPORTED; }
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) { sl_set_last_error("comm: dtype"); return SL_ERR_UNSUPPORTED; }
   return check(rccl().send(buf, (size_t)count, t, peer, as_comm(comm)->comm, (hipStream_t)stream), "ncclSend");
 }
 
 SL_API int sl_comm_recv(void* comm, void* buf, int64_t count, int dtype, int peer, void* stream) {
+  if (as_comm(comm)->ar) { sl_set_last_error("comm: a callback communicator only all-reduces"); return SL_ERR_UNSUPPORTED; }
   ncclDataType_t t;
   if (!to_nccl(dtype, &t)) { sl_set_last_error("comm: dtype"); return SL_ERR_UNSUPPORTED; }
   return check(rccl().recv(buf, (size_t)count, t, peer, as_comm(comm)->comm, (hipStream_t)stream), "ncclRecv");

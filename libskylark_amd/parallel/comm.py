@@ -91,12 +91,27 @@ class Comm:
         if os_ is None:
             try:
                 os_ = oneshot.OneShotAllReduce(self, device=t.device)
-            except Exception:  # noqa: BLE001 - no IPC / no native library: stay on RCCL
+                self.oneshot_reason = os_.reason
+            except Exception as e:  # noqa: BLE001 - no IPC / no native library: stay on RCCL
                 os_ = False
+                self.oneshot_reason = f"setup raised {type(e).__name__}: {e}"
             if os_ is not False and not os_.ok:
                 os_ = False
             self._oneshot = os_
         return os_ if (os_ and os_.fits(t)) else None
+
+    def oneshot_status(self) -> dict:
+        """Whether small device all-reduces go through the one-shot path, and
+        why not when they do not (set up lazily on the first eligible call)."""
+        from . import oneshot
+        os_ = getattr(self, "_oneshot", None)
+        if not self._active or self.size < 2:
+            return {"enabled": False, "reason": "single rank"}
+        if not oneshot.enabled(self):
+            return {"enabled": False, "reason": f"disabled (SL_ONESHOT={oneshot._MODE}, backend {self.backend})"}
+        if os_ is None:
+            return {"enabled": False, "reason": "never set up (no eligible all-reduce yet)"}
+        return {"enabled": bool(os_), "reason": getattr(self, "oneshot_reason", "unknown")}
 
     def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM if dist.is_available() else None):
         if self._active and op == dist.ReduceOp.SUM:

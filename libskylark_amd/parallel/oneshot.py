@@ -55,16 +55,26 @@ class OneShotAllReduce:
         self.ok = False
         self._local = None
         self._peers = []
+        # why the path is (not) in use, the same string on every rank
+        # (bench.py records it): "ok" or the first failing stage and ranks
+        self.reason = "not set up"
         lib = _lib.load()
         hb = int(lib.sl_oneshot_handle_bytes()) if lib is not None and hasattr(lib, "sl_oneshot_alloc") else 0
         mine = None
-        if hb and 2 <= self.p <= 16:
+        why = None
+        if not hb:
+            why = "no native one-shot kernels"
+        elif not 2 <= self.p <= 16:
+            why = f"world size {self.p} outside 2..16"
+        else:
             with torch.cuda.device(self.dev):
                 buf = C.c_void_p()
                 h = (C.c_char * hb)()
                 if _lib.require().sl_oneshot_alloc(self.cap, self.p, C.byref(buf), h) == 0:
                     self._local = buf
                     mine = bytes(h)
+                else:
+                    why = "IPC export of the receive buffer failed"
         handles = comm.all_gather_object(mine)
         ok = all(x is not None for x in handles)
         bases = []
@@ -78,13 +88,16 @@ class OneShotAllReduce:
                     hbuf = (C.c_char * len(h)).from_buffer_copy(h)
                     if _lib.require().sl_oneshot_open(hbuf, C.byref(ptr)) != 0:
                         ok = False
+                        why = f"IPC open of rank {q}'s buffer failed"
                         break
                     self._peers.append(ptr)
                     bases.append(ptr.value)
         # every rank must agree before anyone uses the path
-        flags = comm.all_gather_object(bool(ok))
-        self.ok = all(flags)
+        flags = comm.all_gather_object((bool(ok), why))
+        self.ok = all(f for f, _ in flags)
         if not self.ok:
+            bad = [(q, w) for q, (f, w) in enumerate(flags) if not f]
+            self.reason = "; ".join(f"rank {q}: {w or 'a peer could not export its buffer'}" for q, w in bad[:4])
             self.close()
             return
         self.bases = torch.tensor(bases, dtype=torch.int64, device=self.dev)
@@ -96,12 +109,17 @@ class OneShotAllReduce:
         # generation buffers, f32 and f64, rank-dependent operands, exact
         # expected sums; any mismatch or timed-out wait on any rank -> every
         # rank falls back to RCCL
-        good = self._self_test()
-        self.ok = all(comm.all_gather_object(bool(good)))
-        if not self.ok:
+        good, why = self._self_test()
+        res = comm.all_gather_object((bool(good), why))
+        self.ok = all(g for g, _ in res)
+        if self.ok:
+            self.reason = "ok"
+        else:
+            self.reason = "; ".join(f"rank {q}: self-test {w}" for q, (g, w) in enumerate(res) if not g)
             self.close()
 
-    def _self_test(self, timeout_s: float = 5.0) -> bool:
+    def _self_test(self, timeout_s: float = 5.0):
+        """(passed, failure description)"""
         try:
             p = self.p
             for it, dt in enumerate((torch.float64, torch.float32, torch.float64, torch.float32)):
@@ -112,11 +130,13 @@ class OneShotAllReduce:
                           _lib.ptr(self.bases), self.cap, _lib.ptr(self.state), _lib.ptr(self.err), float(timeout_s),
                           vp(_lib.stream_of(x)))
                 want = base * float(p * (p + 1) // 2)
-                if not torch.equal(x, want) or int(self.err.item()):
-                    return False
-            return True
-        except Exception:  # noqa: BLE001 - any failure: stay on RCCL
-            return False
+                if int(self.err.item()):
+                    return False, f"timed out waiting for a peer (round {it})"
+                if not torch.equal(x, want):
+                    return False, f"wrong sum (round {it}, {str(dt).split('.')[-1]})"
+            return True, None
+        except Exception as e:  # noqa: BLE001 - any failure: stay on RCCL
+            return False, f"raised {type(e).__name__}: {e}"
 
     def fits(self, t: torch.Tensor) -> bool:
         return (self.ok and t.is_cuda and t.device == self.dev and t.dtype in (torch.float32, torch.float64)

@@ -38,7 +38,7 @@ for step in "$@"; do
         --output-format csv -- python3 "$ROOT/${PMC_SCRIPT:-bench.py}" ${PMC_ARGS:---steps 2 --warmup 1} > "$log" 2>&1); rc=$?
       echo "pmc $name rc=$rc" ;;
     py)
-      timeout -k 10 ${PY_LIMIT:-600} python -u $arg > "$log" 2>&1; rc=$?
+      PYTHONPATH=$ROOT${PYTHONPATH:+:$PYTHONPATH} timeout -k 10 ${PY_LIMIT:-600} python -u $arg > "$log" 2>&1; rc=$?
       grep '^{' "$log" | tail -20; [ $rc -ne 0 ] && tail -20 "$log" ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac

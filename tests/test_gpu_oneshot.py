@@ -21,6 +21,7 @@ def _worker(rank, world):
     os_ = oneshot.OneShotAllReduce(comm, cap=1 << 16)
     if not os_.ok:
         return "unavailable"
+    assert os_.reason == "ok", os_.reason
     dev = torch.device("cuda", 0)
     for it, (n, dt) in enumerate([(1, torch.float64), (37, torch.float32), (4096, torch.float64),
                                   (8192, torch.float32), (300, torch.float64)] * 6):
@@ -100,3 +101,35 @@ def test_oneshot_late_peer_is_an_error_not_a_partial_sum():
         pytest.skip("IPC export of uncached device memory unavailable here")
     assert res[0] == {"nan": True, "sum_ok": False, "raised": True}, res
     assert res[1] == {"nan": False, "sum_ok": True, "raised": False}, res
+
+
+def _status_worker(rank, world):
+    """Comm.oneshot_status(): set up lazily by the first eligible all-reduce,
+    with the self-test outcome as the reason (what bench.py records)."""
+    import os
+    import torch
+    os.environ["SL_ONESHOT"] = "1"
+    from libskylark_amd.parallel import oneshot
+    oneshot.enable(True)
+    from libskylark_amd.parallel.comm import world as W
+    torch.cuda.set_device(0)
+    comm = W()
+    before = comm.oneshot_status()
+    x = torch.ones(10, dtype=torch.float64, device="cuda")
+    comm.all_reduce(x)
+    torch.cuda.synchronize()
+    after = comm.oneshot_status()
+    comm.check_collectives()
+    comm.close()
+    return before, after, float(x[0])
+
+
+def test_oneshot_status_reported():
+    res = run_distributed(_status_worker, 2, timeout=120)
+    for before, after, v in res:
+        assert before == {"enabled": False, "reason": "never set up (no eligible all-reduce yet)"}
+        assert v == 2.0
+        if after["enabled"]:
+            assert after["reason"] == "ok"
+        else:
+            assert after["reason"] and after["reason"] != "ok"   # the failing stage is named
