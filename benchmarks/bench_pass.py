@@ -3,10 +3,14 @@ sl_rsvd_pass variants (0 = v5 role-split, 32 = v4) for each form (final 0:
 inter, 1: + Y + fp64 Gram, 2: + Y), timed with events, variants interleaved
 so clock drift hits all of them alike.  One JSON line per (variant, form)."""
 import argparse
+import os
+import sys
 import ctypes as C
 import json
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 
@@ -18,6 +22,7 @@ def main():
     ap.add_argument("--k", type=int, default=40)
     ap.add_argument("--variants", default="0,32")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--finals", default="0,1,2")
     a = ap.parse_args()
     from libskylark_amd.ops import _lib
     _lib.require()
@@ -33,7 +38,7 @@ def main():
     variants = [int(v) for v in a.variants.split(",")]
     res = {}
     for rep in range(a.reps + 2):
-        for final in (0, 1, 2):
+        for final in [int(f) for f in a.finals.split(",")]:
             for v in variants:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

@@ -575,7 +575,6 @@ struct P5Tiles {
   int base[8];
   int cnt[8];
   int gown[8];   // Gram tiles: first tau owned and stride (FINAL), per wave
-  int dbg;       // diagnostic switches (0 in production)
 };
 
 constexpr int P5_NBUF = 4, P5_BM = 16, P5_ROWB = 256, P5_REGION = 4096, P5_LPB = 4, P5_T1 = 2, P5_T2 = 12,
@@ -736,19 +735,6 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
         hi[e] = (short)hb[e];
         lo[e] = (short)lb[e];
       }
-      if (!FINAL && (pt.dbg & 4) && jb == 0 && blockIdx.x == 0 && Y) {
-        // debug: the image this wave wrote (hi, lo) for block 0
-        *(s16x4*)((char*)Y + col * 32 + g4 * 8) = hi;
-        *(s16x4*)((char*)Y + 4096 + col * 32 + g4 * 8) = lo;
-        *(f32x4*)((char*)Y + 16384 + (col * 4 + g4) * 16) = acc;
-        if (w == 0) {
-          // the LDS slot step 1 just read (32 KB) and this wave's Z fragments
-          for (int o = lane * 16; o < 8 * REGION; o += 1024)
-            *(f32x4*)((char*)Y + 65536 + o) = *(const f32x4*)(reg0 + o);
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) *(bf16x8*)((char*)Y + 32768 + (ks * 64 + lane) * 16) = zf[ks];
-        }
-      }
       if constexpr (FINAL) {
         float* yf = yfb + (int)(jb & 1) * BM * KP;
         if (col < k) {
@@ -799,10 +785,6 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
     bf16x8 yfr[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) yfr[t] = *(const bf16x8*)(yp + (16 * t + i16) * 32);
-    if (!FINAL && !YROLE && (pt.dbg & 4) && j == 0 && blockIdx.x == 0 && w == KT && Y) {
-#pragma unroll
-      for (int t = 0; t < KT; ++t) *(bf16x8*)((char*)Y + 8192 + (t * 64 + lane) * 16) = yfr[t];
-    }
     if constexpr (G_ON) {
       // this wave's Gram tiles tau = gfirst + s * gstride (slot s), operands
       // picked by selects; a wave owning none skips, a second slot past GT
@@ -875,14 +857,8 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
     gram_acc();
     if (j + NBUF - 1 < nloc) issue(j + NBUF - 1);
     if constexpr (FINAL && !YROLE) store_y(j);
-    if (pt.dbg & 2) {
-      step3(j);
-      if (j + 1 < nloc) step1(j + 1);
-    } else {
-      if (j + 1 < nloc) step1(j + 1);
-      if (pt.dbg & 1) lds_barrier();
-      step3(j);
-    }
+    if (j + 1 < nloc) step1(j + 1);
+    step3(j);
   }
   gram_acc();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -992,9 +968,8 @@ bool p5_tiles(int n, int KT, P5Tiles* pt) {
 
 template <int KT, bool FINAL, bool GRAM>
 int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab, double* Gslab,
-                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s, int dbg) {
+                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s) {
   P5Tiles pt{};
-  pt.dbg = dbg;
   if (!p5_tiles(n, KT, &pt)) {
     sl_set_last_error("rsvd_pass: no tile split for this n / k");
     return SL_ERR_UNSUPPORTED;
@@ -1086,9 +1061,9 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   if (!(variant & 32)) {
     // v5 (default): role-split waves, one barrier per block
 #define SL_P5(KTT)                                                                                                 \
-  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 7) \
-       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 7) \
-                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 7)
+  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s) \
+       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s) \
+                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s)
     switch (KT) {
       case 1: SL_P5(1);
       case 2: SL_P5(2);
