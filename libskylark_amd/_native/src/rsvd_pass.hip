@@ -575,6 +575,7 @@ struct P5Tiles {
   int base[8];
   int cnt[8];
   int gown[8];   // Gram tiles: first tau owned and stride (FINAL), per wave
+  int prio;      // s_setprio of the y waves (tuning knob, variant bits 6-7)
 };
 
 constexpr int P5_NBUF = 4, P5_BM = 16, P5_ROWB = 256, P5_REGION = 4096, P5_LPB = 4, P5_T1 = 2, P5_T2 = 12,
@@ -791,9 +792,8 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
       // multiplies a dummy pair that is never stored
 #pragma unroll
       for (int sg = 0; sg < P5_GS; ++sg) {
-        if (gstride == 0) break;
-        int tau = gfirst + sg * gstride;
-        tau = tau < GT ? tau : 0;
+        const int tau = gfirst + sg * gstride;
+        if (gstride == 0 || tau >= GT) break;   // uniform: no dummy products
         const int t1 = tau < KT ? 0 : (tau < 2 * KT - 1 ? 1 : 2);
         const int t2 = t1 == 0 ? tau : (t1 == 1 ? tau - KT + 1 : 2);
         bf16x8 y1 = yfr[0], y2 = yfr[0];
@@ -907,6 +907,9 @@ k_rsvd_pass5(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w < KT) {
+    // the y waves carry each phase's critical path (step 1 of the next block)
+    if (pt.prio == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pt.prio >= 2) __builtin_amdgcn_s_setprio(2);
     // the y waves' W-tile count is a compile-time constant of their body
     const int yt = pt.cnt[0];
     if (yt == 0)
@@ -968,8 +971,9 @@ bool p5_tiles(int n, int KT, P5Tiles* pt) {
 
 template <int KT, bool FINAL, bool GRAM>
 int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab, double* Gslab,
-                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s) {
+                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s, int prio) {
   P5Tiles pt{};
+  pt.prio = prio;
   if (!p5_tiles(n, KT, &pt)) {
     sl_set_last_error("rsvd_pass: no tile split for this n / k");
     return SL_ERR_UNSUPPORTED;
@@ -1061,9 +1065,9 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   if (!(variant & 32)) {
     // v5 (default): role-split waves, one barrier per block
 #define SL_P5(KTT)                                                                                                 \
-  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s) \
-       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s) \
-                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s)
+  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 3) \
+       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 3) \
+                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 3)
     switch (KT) {
       case 1: SL_P5(1);
       case 2: SL_P5(2);
