@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--variants", default="0,32")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--finals", default="0,1,2")
+    ap.add_argument("--prev", type=int, default=-1,
+                    help="run an untimed forward inter pass right before each timed one "
+                         "(MALL reuse A/B: variant 256 = reverse walk)")
     a = ap.parse_args()
     from libskylark_amd.ops import _lib
     _lib.require()
@@ -40,6 +43,10 @@ def main():
     for rep in range(a.reps + 2):
         for final in [int(f) for f in a.finals.split(",")]:
             for v in variants:
+                if a.prev >= 0:
+                    _lib.call("sl_rsvd_pass", vp(A.data_ptr()), m, n, n, vp(Zt.data_ptr()), k, vp(ws.data_ptr()),
+                              None, k, 0, a.prev, st)
+                    torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 _lib.call("sl_rsvd_pass", vp(A.data_ptr()), m, n, n, vp(Zt.data_ptr()), k, vp(ws.data_ptr()),
@@ -52,7 +59,7 @@ def main():
         ts.sort()
         med = ts[len(ts) // 2]
         print(json.dumps({"variant": v, "final": final, "us_median": round(med, 1), "us_min": round(ts[0], 1),
-                          "TBps_median": round(m * n * 2 / med / 1e6, 2), "m": m, "n": n, "k": k}))
+                          "TBps_median": round(m * n * 2 / med / 1e6, 2), "m": m, "n": n, "k": k, "prev": a.prev}))
 
 
 if __name__ == "__main__":

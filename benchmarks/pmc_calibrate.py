@@ -7,6 +7,9 @@ HBM read volume is known exactly, in the access shapes our kernels use.
              1e6 x 1000 bf16 matrix: 2.0e9 B of A (+ Z, L2-resident)
   gather128  index_select of 2^21 random 128-B rows of a 4 GiB table
   gather64   index_select of 2^21 random 64-B rows of a 4 GiB table
+  rgather128 / rgather64  the same shapes (2^24 rows) through a gather kernel
+             that keeps 8 random 16-B pieces per lane in flight
+             (benchmarks/calib/gather.hip): the random-access bound
   cwt        the CSR CountSketch of config 2 (1e7 x 1e4, 1e8 nnz, S = 4096):
              0.88e9 B of CSR that must be read; the rows are visited in
              random (bucket) order
@@ -29,7 +32,7 @@ import torch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", required=True, choices=["stream", "ldsdma", "gather128", "gather64", "cwt"])
+    ap.add_argument("--op", required=True, choices=["stream", "ldsdma", "gather128", "gather64", "rgather128", "rgather64", "cwt"])
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -59,7 +62,19 @@ def main():
         idx = torch.randint(0, table.shape[0], (1 << 21,), generator=g, device=dev)
         out = torch.empty(idx.numel(), w, dtype=torch.float32, device=dev)
         fn = lambda: torch.index_select(table, 0, idx, out=out)  # noqa: E731
-        exp, hint = idx.numel() * w * 4, "index"
+        exp, hint = idx.numel() * w * 4, "gather_kernel"
+    elif a.op in ("rgather128", "rgather64"):
+        rb = 128 if a.op == "rgather128" else 64
+        lib = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "calib", "libcalib.so"))
+        lib.calib_rgather.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p]
+        table = torch.ones(1 << 30, dtype=torch.float32, device=dev)
+        nrow = table.numel() * 4 // rb
+        idx = torch.randint(0, nrow, (1 << 24,), generator=g, device=dev)
+        out = torch.empty(idx.numel() * rb // 4, dtype=torch.float32, device=dev)
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        fn = lambda: lib.calib_rgather(C.c_void_p(table.data_ptr()), C.c_void_p(idx.data_ptr()),  # noqa: E731
+                                       idx.numel(), rb, C.c_void_p(out.data_ptr()), st)
+        exp, hint = idx.numel() * rb, "k_rgather"
     else:
         import libskylark_amd as sk
         m, n, z = 10_000_000, 10_000, 10

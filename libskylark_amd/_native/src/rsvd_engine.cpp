@@ -126,8 +126,10 @@ int seg(Plan* p, const void* A, int i, hipStream_t s, float* V = nullptr, float*
   // the final pass stores Y and forms its fp64 Gram in-pass (bf16 hi / lo
   // products on the fragments the W update already holds); one reduce sums
   // the W and Gram slabs into [W; G]
+  // odd passes walk the row blocks backwards: each pass starts on the rows
+  // the previous one read last, which are still in the MALL
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
-                    final_pass ? 1 : 0, 0, s);
+                    final_pass ? 1 : 0, (i & 1) ? 256 : 0, s);
   if (rc != SL_OK) return rc;
   // the first reduce of the call also clears the status word (no memset node)
   return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,

@@ -576,6 +576,9 @@ struct P5Tiles {
   int cnt[8];
   int gown[8];   // Gram tiles: first tau owned and stride (FINAL), per wave
   int prio;      // s_setprio of the y waves (tuning knob, variant bits 6-7)
+  int rev;       // walk the row blocks last-to-first (variant bit 8): consecutive
+                 // passes alternate, so a pass starts on the rows the previous
+                 // one read last (still in the MALL)
 };
 
 constexpr int P5_NBUF = 4, P5_BM = 16, P5_ROWB = 256, P5_REGION = 4096, P5_LPB = 4, P5_T1 = 2, P5_T2 = 12,
@@ -603,6 +606,11 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
   const int64_t nblocks = (m + BM - 1) / BM;
   const int64_t b0 = blockIdx.x, bstep = gridDim.x;
   const int64_t nloc = b0 < nblocks ? (nblocks - 1 - b0) / bstep + 1 : 0;
+  const bool rev = pt.rev != 0;
+  auto row0 = [&](int64_t jb) -> int64_t {
+    const int64_t b = b0 + jb * bstep;
+    return (rev ? nblocks - 1 - b : b) * BM;
+  };
   // step 1 runs KS (16 or 32) k-steps of 32 columns: regions past n were
   // zeroed (below) and Z is zero past n, so the extra products add exact zeros
   const bool dma_on = 128 * w < n;                        // this wave's 128-column region exists
@@ -672,7 +680,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
     if (!dma_on) return;
     const int slot = (int)(blk % NBUF);
     char* region = ring + (slot * 8 + w) * REGION;
-    const int64_t r0 = (b0 + blk * bstep) * BM;
+    const int64_t r0 = row0(blk);
     if (r0 + BM <= m) {
       const bf16_t* base = A + r0 * lda;
 #pragma unroll
@@ -707,7 +715,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
         const bf16x8 af = *(const bf16x8*)(reg0 + (ks >> 2) * REGION + i16 * ROWB + ((chunk ^ sw) << 4));
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zf[ks], acc, 0, 0, 0);
       }
-      const int64_t r0 = (b0 + jb * bstep) * BM;
+      const int64_t r0 = row0(jb);
       if (r0 + BM > m) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -756,7 +764,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
   auto store_y = [&](int64_t jb) {
     if constexpr (FINAL && !YROLE) {
       const float* yf = yfb + (int)(jb & 1) * BM * KP;
-      const int64_t r0 = (b0 + jb * bstep) * BM;
+      const int64_t r0 = row0(jb);
       for (int q = wy; q < nyv; q += 8 - KT) {
         if (vecY) {
           const int t = q * 64 + lane;
@@ -971,9 +979,10 @@ bool p5_tiles(int n, int KT, P5Tiles* pt) {
 
 template <int KT, bool FINAL, bool GRAM>
 int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab, double* Gslab,
-                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s, int prio) {
+                 float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s, int variant) {
   P5Tiles pt{};
-  pt.prio = prio;
+  pt.prio = (variant >> 6) & 3;
+  pt.rev = (variant >> 8) & 1;
   if (!p5_tiles(n, KT, &pt)) {
     sl_set_last_error("rsvd_pass: no tile split for this n / k");
     return SL_ERR_UNSUPPORTED;
@@ -1041,8 +1050,8 @@ SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k) {
 // final = 0: W slabs only.  final = 1: also Y (m x k f32, row stride ldy >=
 // k; Y = y_hi + y_lo, the bf16 pair W is formed from) and the fp64 Gram slabs
 // of that Y (exact bf16 products, f32 per 16-row block, f64 across blocks);
-// final = 2: W slabs and Y only.  variant selects the ring depth (tuning: 0
-// default, 3/4 = NBUF).
+// final = 2: W slabs and Y only.  variant bits: 256 = walk the row blocks
+// last-to-first, 64/128 = y-wave priority (tuning), 32 = the v4 kernel (A/B).
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
                         float* Y, int64_t ldy, int final_pass, int variant, void* stream) {
   if (m <= 0) return SL_OK;
@@ -1065,9 +1074,9 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   if (!(variant & 32)) {
     // v5 (default): role-split waves, one barrier per block
 #define SL_P5(KTT)                                                                                                 \
-  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 3) \
-       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 3) \
-                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, (variant >> 6) & 3)
+  return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
+       : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
+                         : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant)
     switch (KT) {
       case 1: SL_P5(1);
       case 2: SL_P5(2);

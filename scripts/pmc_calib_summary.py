@@ -41,7 +41,7 @@ def main():
     root, dest = sys.argv[1], sys.argv[2]
     os.makedirs(dest, exist_ok=True)
     rows = []
-    for op in ("stream", "ldsdma", "gather128", "gather64", "cwt"):
+    for op in ("stream", "ldsdma", "gather128", "gather64", "rgather128", "rgather64", "cwt"):
         if not os.path.exists(os.path.join(root, f"{op}.log")):
             continue
         meta, per, paths = load(root, op)
@@ -66,11 +66,33 @@ def main():
     if "stream" in cal or "ldsdma" in cal:
         s = cal.get("ldsdma", cal.get("stream"))
         print(f"\nStreaming factor: true bytes = FETCH_SIZE x 1024 / {s:.3f} (wide coalesced reads).")
-    for op in ("gather128", "gather64"):
+    for op in ("gather128", "gather64", "rgather128", "rgather64"):
         if op in cal:
             print(f"{op}: a random-row gather shows {cal[op]:.2f} x its useful bytes in FETCH_SIZE.")
     if "cwt" in cal and "gather128" in cal:
         print(f"cwt: {cal['cwt']:.2f} x its CSR bytes in FETCH_SIZE.")
+    # useful-byte throughput: the random-row gathers bound what the CWT (rows
+    # of 10 nnz = 80 B of column + value, visited in random bucket order) can do
+    bw = {op: exp / (t * 1e-6) / 1e9 for op, exp, fetch, t, *_ in rows}
+    print("\n| workload | useful GB/s under counters |")
+    print("|---|---:|")
+    for op, v in bw.items():
+        print(f"| {op} | {v:.0f} |")
+    # line-request rate (FETCH_SIZE x 1024 / 64 B per second): what a random
+    # access kernel is bounded by, whatever its useful bytes per line
+    rate = {op: fetch / 64 / (t * 1e-6) / 1e9 for op, exp, fetch, t, *_ in rows}
+    print("\n| workload | 64-B fetch requests per ns (FETCH_SIZE x 1024 / 64 / time) |")
+    print("|---|---:|")
+    for op, v in rate.items():
+        print(f"| {op} | {v:.1f} |")
+    best = max((rate[o] for o in ("rgather128", "rgather64", "gather128", "gather64") if o in rate), default=None)
+    if "cwt" in rate and best:
+        print(f"\ncwt issues {rate['cwt']:.1f} fetch requests per ns: {100 * rate['cwt'] / best:.0f}% of the best "
+              f"random-gather rate measured here ({best:.1f}).")
+    if "cwt" in bw and "gather64" in bw and "gather128" in bw:
+        print(f"\ncwt moves its CSR at {bw['cwt']:.0f} GB/s: {100 * bw['cwt'] / bw['gather64']:.0f}% of the 64-B "
+              f"random-row gather ({bw['gather64']:.0f} GB/s) and {100 * bw['cwt'] / bw['gather128']:.0f}% of the "
+              f"128-B one ({bw['gather128']:.0f} GB/s); its 80-B rows sit between the two.")
     json.dump(cal, open(os.path.join(dest, "calibration.json"), "w"), indent=1)
 
 

@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/pmc_cal
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for OP in ${OPS:-stream ldsdma gather128 gather64 cwt}; do
+for OP in ${OPS:-stream ldsdma gather128 gather64 rgather128 rgather64 cwt}; do
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/$OP -o run -- \
     python3 $R/benchmarks/pmc_calibrate.py --op $OP > $OUT/$OP.log 2>&1 || { echo "pmc $OP failed"; tail -5 $OUT/$OP.log; exit 1; }
   grep '^{' $OUT/$OP.log

@@ -1,10 +1,15 @@
-"""Summarise the v4-pass PMC runs (scripts/pmc_pass4.sh): per counter, the
-mean per dispatch of k_rsvd_pass (first dispatch dropped: cold caches), for
-the inter (final 0) and last-pass (final 2) forms; markdown table on stdout,
-the raw counter CSVs copied to the given directory.
+"""Summarise the fused-pass PMC runs (scripts/pmc_pass.sh): per counter, the
+mean per dispatch of k_rsvd_pass* (first dispatch dropped: cold caches), for
+the inter (final 0) and last-pass (final 1) forms; markdown table on stdout,
+the raw counter CSVs copied to the given directory.  HBM bytes are
+FETCH_SIZE x 1024 divided by the MEASURED streaming ratio of the LDS-DMA
+workload in the calibration file (scripts/pmc_calibrate.sh ->
+profiles/r5/pmc_cal/calibration.json), not an assumed factor.
 
-usage: python scripts/pmc_summary4.py gpurun_out/pmc4 profiles/r4/pmc4"""
+usage: python scripts/pmc_summary.py gpurun_out/pmc5 profiles/r5/pmc5 profiles/r5/pmc_cal/calibration.json"""
 from __future__ import annotations
+
+import json
 
 import csv
 import glob
@@ -37,15 +42,17 @@ def collect(root, final):
 
 
 def main():
-    root, dest = sys.argv[1], sys.argv[2]
+    root, dest, calp = sys.argv[1], sys.argv[2], sys.argv[3]
+    cal = json.load(open(calp))
+    ratio = cal["ldsdma"]   # FETCH_SIZE x 1024 / true bytes of a known LDS-DMA stream
     os.makedirs(dest, exist_ok=True)
     for path in glob.glob(os.path.join(root, "f*_g*", "**", "*counter_collection.csv"), recursive=True):
         tag = os.path.relpath(path, root).split(os.sep)[0]
         shutil.copy(path, os.path.join(dest, f"{tag}.csv"))
     inter, ti = collect(root, 0)
-    fin, tf = collect(root, 2)
+    fin, tf = collect(root, 1)
     names = sorted(set(inter) | set(fin))
-    print("| counter | inter pass (final 0) | last pass (final 2) |")
+    print("| counter | inter pass (final 0) | last pass (final 1) |")
     print("|---|---:|---:|")
     for c in names:
         print(f"| {c} | {inter.get(c, float('nan')):.4g} | {fin.get(c, float('nan')):.4g} |")
@@ -63,8 +70,9 @@ def main():
             cyc = d["GRBM_GUI_ACTIVE"] / 8
             out.append(f"MFMA busy {100 * d['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / cyc:.0f}% (per SIMD over GRBM_GUI_ACTIVE/8)")
         if "FETCH_SIZE" in d and t:
-            by = 2 * d["FETCH_SIZE"] * 1024   # gfx950 FETCH_SIZE counts half of a wide streaming read
-            out.append(f"HBM read {by / 1e9:.2f} GB (2 x FETCH_SIZE) = {by / (t * 1e-6) / 1e12:.2f} TB/s under counters")
+            by = d["FETCH_SIZE"] * 1024 / ratio
+            out.append(f"HBM read {by / 1e9:.2f} GB (FETCH_SIZE x 1024 / {ratio:.3f} calibrated) = "
+                       f"{by / (t * 1e-6) / 1e12:.2f} TB/s under counters")
         if "SQ_LDS_BANK_CONFLICT" in d and "SQ_LDS_IDX_ACTIVE" in d:
             out.append(f"LDS bank conflicts {100 * d['SQ_LDS_BANK_CONFLICT'] / d['SQ_LDS_IDX_ACTIVE']:.0f}% of LDS cycles")
         print(f"\n{tag}: " + "; ".join(out))
