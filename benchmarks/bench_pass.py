@@ -1,5 +1,6 @@
 """Fused randSVD pass A/B on the headline shape (1e6 x 1000 bf16, k = 40):
-sl_rsvd_pass variants (0 = v5 role-split, 32 = v4) for each form (final 0:
+sl_rsvd_pass variants (0 = forward walk, 256 = backward walk, 64/128 = y-wave
+priority) for each form (final 0:
 inter, 1: + Y + fp64 Gram, 2: + Y), timed with events, variants interleaved
 so clock drift hits all of them alike.  One JSON line per (variant, form)."""
 import argparse
@@ -20,7 +21,7 @@ def main():
     ap.add_argument("--m", type=int, default=1_000_000)
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--k", type=int, default=40)
-    ap.add_argument("--variants", default="0,32")
+    ap.add_argument("--variants", default="0,256")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--finals", default="0,1,2")
     ap.add_argument("--prev", type=int, default=-1,

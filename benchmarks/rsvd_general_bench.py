@@ -1,7 +1,8 @@
 """General-precision device randSVD engine (rsvd_general.hip) at the
 reference's precisions and sizes: 1e6 x 1000 f32 and
 2e5 x 5000 f64, plus k = 128 -- the whole call on the device (rocBLAS passes,
-one-wave / rocSOLVER small algebra, f64 core), timed with HIP events over
+one-wave small algebra, f64 core; hand-written f32 / f64 products for
+k <= 64), timed with HIP events over
 repeated cold calls (a fresh sketch seed per call).  Prints one JSON line per
 case: ms per call, effective HBM traffic of the passes (2 (q + 1) reads of A),
 and the relative error of the leading singular values against a reference
@@ -39,6 +40,9 @@ def planted(m, n, r, dtype, dev, seed=0):
     return A, s
 
 
+NO_REF = False   # --no-ref: skip the f64 reference (kernel traces of the engine alone)
+
+
 def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     dev = torch.device("cuda")
     A, s_true = planted(m, n, max(2 * rank, 32), dtype, dev)
@@ -63,6 +67,15 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     # reference: the singular values of A itself (planted + noise), from the
     # f64 Gram A^T A summed over row chunks (the planted s alone is off by the
     # noise for the trailing wanted values)
+    if NO_REF:
+        print(json.dumps({"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} q {q} {sketch}",
+                          "engine": type(plan).__name__, "native": getattr(plan, "native", None),
+                          "ms": round(ms, 3), "ms_min": round(times[0], 3),
+                          "pass_traffic_GBps": round(bytes_passes / (ms * 1e-3) / 1e9, 1)}), flush=True)
+        del A, U, V
+        S._PLANS.clear()
+        torch.cuda.empty_cache()
+        return
     G = torch.zeros(n, n, device=A.device, dtype=torch.float64)
     step = max(1, (1 << 26) // n)
     for i in range(0, m, step):
@@ -74,7 +87,7 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     err_planted = float(((s.double() - s_true[:rank]).abs() / s_true[:rank]).max())
     k = max(rank, min(n, 2 * rank))
     out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}",
-           "engine": type(plan).__name__, "ms": round(ms, 3), "ms_min": round(times[0], 3),
+           "engine": type(plan).__name__, "native": getattr(plan, "native", None), "ms": round(ms, 3), "ms_min": round(times[0], 3),
            "pass_traffic_GBps": round(bytes_passes / (ms * 1e-3) / 1e9, 1), "max_rel_err_s": err,
            "max_rel_err_s_vs_planted": err_planted}
     print(json.dumps(out), flush=True)
@@ -83,11 +96,25 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     torch.cuda.empty_cache()
 
 
+CASES = {
+    "f32": lambda reps: run(1_000_000, 1000, 20, 2, torch.float32, reps=reps),
+    "f64": lambda reps: run(200_000, 5000, 20, 2, torch.float64, reps=reps),
+    "f64k128": lambda reps: run(200_000, 5000, 64, 1, torch.float64, reps=reps),   # k = 128: library small algebra
+    "bf16": lambda reps: run(1_000_000, 1000, 20, 2, torch.bfloat16, reps=reps),  # the fused engine, for comparison
+}
+
+
 def main():
-    run(1_000_000, 1000, 20, 2, torch.float32)
-    run(200_000, 5000, 20, 2, torch.float64)
-    run(200_000, 5000, 64, 1, torch.float64)            # k = 128: rocSOLVER small algebra
-    run(1_000_000, 1000, 20, 2, torch.bfloat16)         # n <= 1024 bf16: the fused engine, for comparison
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", default="f32,f64,f64k128,bf16")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-ref", action="store_true")
+    a = ap.parse_args()
+    global NO_REF
+    NO_REF = a.no_ref
+    for c in a.cases.split(","):
+        CASES[c](a.reps)
 
 
 if __name__ == "__main__":

@@ -30,6 +30,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 COMMON_FLAGS = [
     "-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INC,
     "-fvisibility=hidden", "-Wno-unused-result", "-munsafe-fp-atomics",
+    # zstd-compressed device code bundles (the HIP runtime inflates them at
+    # load): the library's fat binary shrinks ~3.5x, and so does every push
+    "--offload-compress",
 ]
 
 

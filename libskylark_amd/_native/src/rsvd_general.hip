@@ -17,12 +17,16 @@
 // both re-orthonormalised, as the reference's power iteration does after
 // every application of A (W = A^T A Z without it squares the condition
 // number, and the trailing wanted directions drowned at k = 128).
-// The two products over A per pass are plain library GEMMs (rocBLAS: a tall
-// operand times an n x k panel, bandwidth-bound); the CholeskyQR factors and
-// the core eigensolver are the one-wave kernels of sl_wave_la.hpp for k <= 64
-// (sl_chol_inv_wave, sl_sym_eig_tridiag; Jacobi re-solve when flagged) and
-// rocSOLVER (potrf + trtri, syevd) for 64 < k <= 128.  W, H, G and the core
-// are f64 whatever A's precision.
+// f32 / f64 A with k <= 64 ("hand" plans) run every product on hand-written
+// kernels: the two products over A per pass on the matrix cores in A's own
+// precision (rsvd_stream.hip: sl_ts_az, sl_ts_atq), the m x k / n x k / k x k
+// ones on sl_ts_xm64 / sl_ts_gram64 / sl_ts_small / sl_tsk_f32_xm /
+// sl_tsk_gram64, the CholeskyQR factors and the core eigensolver on the
+// one-wave kernels of sl_wave_la.hpp (sl_chol_inv_wave, sl_sym_eig_tridiag;
+// Jacobi re-solve when flagged) -- no rocBLAS / rocSOLVER call.  bf16 A (n >
+// 1024) and 64 < k <= 128 keep library GEMMs (rocBLAS) and rocSOLVER (syevd
+// eigen-whitening, syevd core).  W, H, G and the core are f64 whatever A's
+// precision.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,6 +50,20 @@ SL_API int64_t sl_tsk_gram64_workspace(int64_t m, int k);
 SL_API int sl_tsk_gram64(const float* Y, int64_t m, int k, int64_t ldy, double* G, void* ws, void* stream);
 SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
                               void* stream);
+SL_API int sl_ts_az(const void* A, int64_t m, int64_t n, int64_t lda, const void* Z, int k, void* Y, int64_t ldy,
+                    int dt, void* stream);
+SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt);
+SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const void* Q, int k, double* W, int ldw,
+                     void* ws, int dt, void* stream);
+SL_API int sl_ts_xm64(const double* X, int64_t rows, int k, int64_t ldx, const double* Mm, int k2, void* out,
+                      int64_t ldo, int out_dt, void* stream);
+SL_API int64_t sl_ts_gram64_workspace(int64_t rows, int k);
+SL_API int sl_ts_gram64(const double* X, int64_t rows, int k, int64_t ldx, double* G, int ldg, void* ws,
+                        void* stream);
+SL_API int sl_ts_small(int ta, int tb, int mr, int nc, int kd, const double* A, int lda, const double* B, int ldb,
+                       double* C, int ldc, void* stream);
+SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
+                         int64_t ldo, double* G, void* ws, void* stream);
 
 namespace {
 
@@ -189,6 +207,11 @@ struct GPlan {
   int np = 0;              // row chunks of ch rows (+ one for the remainder)
   int64_t ch = 0;
   int* st = nullptr;       // [0] status, [1..2] eig status, [4..11] chol statuses / infos (4 / 6 inter, 8 core, 10 Y)
+  // hand: f32 / f64 A with k <= 64 -- every product on the hand-written
+  // kernels (rsvd_stream.hip, tsk_f32_kernels.hip), no rocBLAS / rocSOLVER
+  bool hand = false;
+  void* atqw = nullptr;    // hand: A^T Q row-group slabs
+  void* g64w = nullptr;    // hand: f64 Gram slabs
   // sketch of the call
   int sk = 0;              // 0 none, 1 FJLT, 2 dense
   uint64_t seed = 0, b0 = 0, b1 = 0;
@@ -279,6 +302,7 @@ int gram(GPlan* p, const void* Yb, double* G, hipStream_t s) {
   const int64_t m = p->m;
   const int k = p->k;
   int rc;
+  if (p->hand && p->dt == SL_F64) return sl_ts_gram64((const double*)Yb, m, k, k, G, k, p->g64w, s);
   if (p->dt == SL_F64) {
     const int64_t tg = (int64_t)k * k;
     rc = slb_gemm_strided(SL_F64, true, false, k, k, p->ch, 1.0, Yb, k, p->ch * k, Yb, k, p->ch * k, 0.0, p->parts,
@@ -313,7 +337,8 @@ int gram(GPlan* p, const void* Yb, double* G, hipStream_t s) {
 // across ranks before the second half)
 int apply_z(GPlan* p, const void* A, hipStream_t s) {
   const int dt = p->dt == SL_BF16 ? SL_BF16 : p->dt;
-  int rc = slb_gemm(dt, false, false, p->m, p->k, p->n, 1.0, A, p->lda, p->Z, p->k, 0.0, p->Y, p->k, s);
+  int rc = p->hand ? sl_ts_az(A, p->m, p->n, p->lda, p->Z, p->k, p->Y, p->k, dt, s)
+                   : slb_gemm(dt, false, false, p->m, p->k, p->n, 1.0, A, p->lda, p->Z, p->k, 0.0, p->Y, p->k, s);
   if (rc != SL_OK) return rc;
   return gram(p, p->Y, p->WG + p->n * p->k, s);
 }
@@ -330,6 +355,21 @@ int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
   const int k = p->k;
   int rc = chol_inv(p, p->WG + n * k, p->Ri, p->st + 10, s);
   if (rc != SL_OK) return rc;
+  if (p->hand) {
+    // Q = Y Ry, then W = A^T Q straight into WG (row-group slabs summed in f64)
+    if (p->dt == SL_F64) {
+      rc = sl_ts_xm64((const double*)p->Y, m, k, k, p->Ri, k, p->Qb, k, SL_F64, s);
+    } else {
+      k_cast2d<double, float><<<grid_of((int64_t)k * k), 256, 0, s>>>(p->Ri, k, k, k, (float*)p->Rf, k, nullptr);
+      SL_LAUNCH_CHECK();
+      rc = sl_tsk_f32_xm((const float*)p->Y, m, k, k, (const float*)p->Rf, k, (float*)p->Qb, k, nullptr, nullptr, s);
+    }
+    if (rc != SL_OK) return rc;
+    rc = sl_ts_atq(A, m, n, p->lda, p->Qb, k, p->WG, k, p->atqw, p->dt, s);
+    if (rc != SL_OK) return rc;
+    if (!final_pass) return SL_OK;
+    return gram(p, p->Qb, p->WG + n * k, s);
+  }
   if (p->dt == SL_F64) {
     rc = slb_gemm(SL_F64, false, false, m, k, k, 1.0, p->Y, k, p->Ri, k, 0.0, p->Qb, k, s);
   } else {
@@ -381,6 +421,13 @@ int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
 int inter(GPlan* p, int i, hipStream_t s) {
   const int k = p->k;
   const int64_t n = p->n;
+  if (p->hand) {
+    int rc = sl_ts_gram64(p->WG, n, k, k, p->H, k, p->g64w, s);
+    if (rc != SL_OK) return rc;
+    rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
+    if (rc != SL_OK) return rc;
+    return sl_ts_xm64(p->WG, n, k, k, p->Ri, k, p->Z, k, p->dt, s);   // Z = W R^{-1} in A's dtype
+  }
   int rc = slb_gemm(SL_F64, true, false, k, k, n, 1.0, p->WG, k, p->WG, k, 0.0, p->H, k, s);
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
@@ -420,13 +467,16 @@ int core(GPlan* p, hipStream_t s) {
   const int64_t n = p->n;
   const double* W = p->WG;
   const double* G = p->WG + n * k;
-  int rc = slb_gemm(SL_F64, true, false, k, k, n, 1.0, W, k, W, k, 0.0, p->H, k, s);   // H = W^T W
+  int rc = p->hand ? sl_ts_gram64(W, n, k, k, p->H, k, p->g64w, s)
+                   : slb_gemm(SL_F64, true, false, k, k, n, 1.0, W, k, W, k, 0.0, p->H, k, s);   // H = W^T W
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, G, p->Ri, p->st + 8, s);
   if (rc != SL_OK) return rc;
-  rc = slb_gemm(SL_F64, false, false, k, k, k, 1.0, p->H, k, p->Ri, k, 0.0, p->T1, k, s);   // T = H Rti
+  rc = p->hand ? sl_ts_small(0, 0, k, k, k, p->H, k, p->Ri, k, p->T1, k, s)
+               : slb_gemm(SL_F64, false, false, k, k, k, 1.0, p->H, k, p->Ri, k, 0.0, p->T1, k, s);   // T = H Rti
   if (rc != SL_OK) return rc;
-  rc = slb_gemm(SL_F64, true, false, k, k, k, 1.0, p->Ri, k, p->T1, k, 0.0, p->Cc, k, s);   // C = Rti^T T
+  rc = p->hand ? sl_ts_small(1, 0, k, k, k, p->Ri, k, p->T1, k, p->Cc, k, s)
+               : slb_gemm(SL_F64, true, false, k, k, k, 1.0, p->Ri, k, p->T1, k, 0.0, p->Cc, k, s);   // C = Rti^T T
   if (rc != SL_OK) return rc;
   if (k <= 64) {
     SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 8, s));   // st[1] flag, st[2] re-solve no-convergence
@@ -444,7 +494,8 @@ int core(GPlan* p, hipStream_t s) {
     if (rc != SL_OK) return rc;
   }
   // M = Rti Ub_r (k x r), N = M S^{-1}, s
-  rc = slb_gemm(SL_F64, false, false, k, r, k, 1.0, p->Ri, k, p->eig, r, 0.0, p->M, r, s);
+  rc = p->hand ? sl_ts_small(0, 0, k, r, k, p->Ri, k, p->eig, r, p->M, r, s)
+               : slb_gemm(SL_F64, false, false, k, r, k, 1.0, p->Ri, k, p->eig, r, 0.0, p->M, r, s);
   if (rc != SL_OK) return rc;
   const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
   rc = dispatch_dt(udt, [&](auto* tag) {
@@ -501,13 +552,14 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
     sl_set_last_error("rsvd_gen: needs m, n >= 1, lda >= n, 1 <= r <= k <= min(n, 128), q >= 0, dtype f32/f64/bf16");
     return SL_ERR_UNSUPPORTED;
   }
-  if (!slb_available() || (k > 64 && !slb_solver_available())) {
+  const bool hand = k <= 64 && dt != SL_BF16;
+  if (!hand && (!slb_available() || (k > 64 && !slb_solver_available()))) {
     sl_set_last_error("rsvd_gen: rocBLAS / rocSOLVER not available");
     return SL_ERR_UNSUPPORTED;
   }
   GPlan* p = new (std::nothrow) GPlan();
   if (!p) return SL_ERR_GENERIC;
-  p->m = m; p->n = n; p->lda = lda; p->k = k; p->r = r; p->q = q; p->dt = dt;
+  p->m = m; p->n = n; p->lda = lda; p->k = k; p->r = r; p->q = q; p->dt = dt; p->hand = hand;
   const size_t es = esize(dt);
   const size_t ys = dt == SL_BF16 ? 4 : es;   // Y / Wt element size
   int64_t off = 0;
@@ -537,12 +589,14 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   // f32 / f64 A: row-chunk partials of A^T Y (and of Y^T Y), <= 64 MB of slabs
   int np = 0;
   int64_t ch = 0;
-  if (dt != SL_BF16) {
+  if (dt != SL_BF16 && !hand) {
     const int64_t slab = std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es;
     np = (int)std::max<int64_t>(1, std::min<int64_t>({128, (int64_t(64) << 20) / slab, m / 512}));
     ch = m / np;
   }
-  const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
+  const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 && !hand ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
+  const int64_t o_aw = off;  off = align256(off + (hand ? sl_ts_atq_workspace(m, n, k, dt) : 0));
+  const int64_t o_g6 = off;  off = align256(off + (hand ? sl_ts_gram64_workspace(std::max(m, n), k) : 0));
   const int64_t o_st = off;  off = align256(off + 64 * 4);
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;
@@ -557,6 +611,8 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   p->N = (double*)(b + o_n); p->Md = b + o_md; p->Vf = (double*)(b + o_vf); p->gws = b + o_gw;
   p->st = (int*)(b + o_st);
   p->parts = b + o_pt;
+  p->atqw = b + o_aw;
+  p->g64w = b + o_g6;
   p->np = np;
   p->ch = ch;
   if (hipMemset(p->st, 0, 64 * 4) != hipSuccess) {
@@ -603,6 +659,10 @@ SL_API int sl_rsvd_gen_set_z(void* plan, const void* Z, void* stream) {
 
 SL_API double* sl_rsvd_gen_reduce_buffer(void* plan) { return ((GPlan*)plan)->WG; }
 
+// 1: every product of this plan runs on the hand-written kernels (f32 / f64
+// A, k <= 64); 0: library GEMMs (bf16 A, or k > 64)
+SL_API int sl_rsvd_gen_native(void* plan) { return ((GPlan*)plan)->hand ? 1 : 0; }
+
 // Use caller-owned buffers for the [W; G] reduce buffer ((n + k) * k f64) and
 // / or the status words (16 ints; [0] is the call's status), e.g. torch
 // tensors the caller all-reduces / reads; null keeps the plan's own.
@@ -631,9 +691,22 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
   GPlan* p = (GPlan*)plan;
   hipStream_t s = (hipStream_t)stream;
   const int k = p->k, r = p->r;
+  const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
+  if (p->hand) {
+    int rc = sl_ts_xm64(p->WG, p->n, k, k, p->N, r, V, r, udt, s);   // V = W N
+    if (rc != SL_OK) return rc;
+    rc = dispatch_dt(udt, [&](auto* tag) {
+      using T = std::remove_pointer_t<decltype(tag)>;
+      k_store_s<T><<<1, 256, 0, s>>>(p->eig + k * r, r, (T*)s_out);
+      SL_LAUNCH_CHECK();
+      return SL_OK;
+    });
+    if (rc != SL_OK) return rc;
+    if (udt == SL_F64) return sl_ts_xm64((const double*)p->Qb, p->m, k, k, p->M, r, U, ldu, SL_F64, s);   // U = Q M
+    return sl_tsk_f32_xm((const float*)p->Qb, p->m, k, k, (const float*)p->Md, r, (float*)U, ldu, nullptr, nullptr, s);
+  }
   int rc = slb_gemm(SL_F64, false, false, p->n, r, k, 1.0, p->WG, k, p->N, r, 0.0, p->Vf, r, s);   // V = W N
   if (rc != SL_OK) return rc;
-  const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
   rc = dispatch_dt(udt, [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
     k_cast2d<double, T><<<grid_of(p->n * r), 256, 0, s>>>(p->Vf, r, p->n, r, (T*)V, r, nullptr);

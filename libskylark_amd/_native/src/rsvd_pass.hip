@@ -1,34 +1,23 @@
-// Fused randSVD pass, v4 (the streaming core of nla/svd.hpp:71-149 and :278-317).
+// Fused randSVD pass (the streaming core of nla/svd.hpp:71-149 and :278-317).
 //
 // ONE read of A (m x n bf16, row-major) produces, per workgroup,
-//     y = A_blk Z           (BM x k per row block, never leaves the chip)
+//     y = A_blk Z           (16 x k per row block, never leaves the chip)
 //     W_part += A_blk^T y   (n x k f32, held in registers for the whole kernel)
-// plus, in the FINAL form, the stored Y = A Z (m x KP f32) and the fp64 Gram
-// Y^T Y (f64 matrix cores).  W / G partials go to per-workgroup slabs that a
-// second kernel sums.
+// plus, in the FINAL form, the stored Y = A Z (m x k f32) and the fp64 Gram
+// Y^T Y.  W / G partials go to per-workgroup slabs that a second kernel
+// (k_rsvd_reduce*) sums.
 //
-// gfx950 structure (one 512-thread workgroup per CU, persistent grid):
-//   * the n columns are split over the 8 waves (NW = 128 each); a wave keeps
-//     its slice of Z (bf16 B-fragments) and of W (f32 accumulators) in
-//     registers, so the DMA ring below is PRIVATE to the wave: wave w only
-//     ever reads the LDS bytes its own LDS-DMA wrote, and a counted
-//     s_waitcnt vmcnt(N) is the only ordering the ring needs (no barrier);
-//   * a ring of NBUF row-block slots per wave (BM = 16 rows x 128 columns =
-//     4 KiB per wave per slot; 128 KiB per workgroup at NBUF = 4), refilled
-//     at the top of every iteration, keeps NBUF - 1 blocks (96 KiB per CU)
-//     of HBM reads in flight -- the ring depth, not the MFMA work, was what
-//     held the previous pass at 4.8 TB/s with all compute switched off;
-//   * the cross-wave sum y = sum_w y_w goes through LDS atomics (ds_add_f32)
-//     into a triple-buffered y tile: ONE workgroup barrier per block (the
-//     previous kernel needed two plus a partial/reduce round trip); the
-//     buffer two blocks ahead is re-zeroed right after the barrier;
+// gfx950 structure (one 512-thread workgroup per CU, persistent grid; the
+// role split is described at k_rsvd_pass5):
+//   * A arrives by LDS-DMA (global_load_lds_dwordx4, inline asm so the
+//     compiler neither tracks nor drains it) into a ring of 16-row slots in a
+//     swizzled image that both the row reads of step 1 and the transposed
+//     reads (ds_read_b64_tr_b16) of step 3 hit conflict-free;
+//   * completion is ordered by hand-counted s_waitcnt vmcnt(N), one workgroup
+//     barrier per block;
 //   * step 3 W += A^T (y_hi + y_lo) is one v_mfma_f32_16x16x32_bf16 per
 //     16 x 16 W tile and block: K = 32 packs [8 rows of y_hi | the same 8
-//     rows of y_lo] (lane groups g = 0/1 share rows 0-7, g = 2/3 rows 8-15,
-//     so the two halves of every LDS access broadcast), the A^T operand comes
-//     from ds_read_b64_tr_b16 of the same swizzled LDS image step 1 read;
-//   * row-major y with stride KP + 4 floats keeps the ds_add and every y read
-//     conflict-free under the gfx950 lane grouping (4 * (KP + 4) = 16 mod 32).
+//     rows of y_lo], so W sees y to ~16 bits while A streams as bf16.
 #include <algorithm>
 
 #include "sl_common.hpp"
@@ -43,8 +32,6 @@ typedef __attribute__((ext_vector_type(4))) double f64x4;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-__device__ __forceinline__ short bf16_bits(float f) { return __builtin_bit_cast(short, (__bf16)f); }
-__device__ __forceinline__ float bf16_val(short h) { return (float)__builtin_bit_cast(__bf16, h); }
 
 // LDS-DMA of 16 B per lane into LDS[lds_base + lane * 16], as inline asm so
 // hipcc neither tracks it nor drains it with its own vmcnt(0) before later
@@ -77,43 +64,6 @@ __device__ __forceinline__ void glds16s(unsigned voff, const void* sbase, unsign
       : "memory");
 }
 
-// the same two with the non-temporal hint (streaming reads of A that no
-// later pass re-reads from the caches)
-__device__ __forceinline__ void glds16_nt(const void* gsrc, unsigned lds_base) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-__device__ __forceinline__ void glds16s_nt(unsigned voff, const void* sbase, unsigned lds_base) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2 nt\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds_base)
-      : "memory");
-}
-template <bool NTL>
-__device__ __forceinline__ void dma16s(unsigned voff, const void* sbase, unsigned lds_base) {
-  if constexpr (NTL) glds16s_nt(voff, sbase, lds_base);
-  else glds16s(voff, sbase, lds_base);
-}
-template <bool NTL>
-__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_base) {
-  if constexpr (NTL) glds16_nt(gsrc, lds_base);
-  else glds16(gsrc, lds_base);
-}
-
 // s_waitcnt vmcnt(n) for a run-time (wave-uniform) n
 __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {
@@ -135,33 +85,6 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int WAVES_, int NW_, int KT_, int NBUF_>
-struct Geo4 {
-  static constexpr int WAVES = WAVES_, NW = NW_, KT = KT_, NBUF = NBUF_;
-  static constexpr int BM = 16;
-  static constexpr int THREADS = WAVES * 64;
-  static constexpr int KP = 16 * KT;
-  static constexpr int ROWB = NW * 2;              // bytes per row of a wave region
-  static constexpr int NCH = NW / 8;               // 16-B chunks per row
-  static constexpr int REGION = BM * ROWB;         // bytes per wave per slot
-  static constexpr int LPB = REGION / 1024;        // LDS-DMA instructions per block per wave
-  static constexpr int RING = NBUF * WAVES * REGION;
-  static constexpr int PART = WAVES * KP * BM * 4; // per-wave partial y tiles (f32, [w][col][row])
-  static constexpr int Y16P = KP * BM * 2 + 16;    // bytes per part (hi / lo) of the bf16 y image
-  static constexpr int Y16 = 2 * Y16P;
-  static constexpr int YF = BM * KP * 4;           // FINAL: the block's stored Y rows ([row][k] f32)
-  static constexpr int CPW = KP / WAVES;           // y columns reduced per wave
-  static constexpr int RL = CPW * 4;               // reducer lanes per wave (one row quad each)
-  static constexpr int GT = KT * (KT + 1) / 2;     // upper 16 x 16 Gram tiles
-  static constexpr int GS = (GT + WAVES - 1) / WAVES;  // Gram tiles per wave
-};
-
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM = FINAL>
-constexpr int pass_lds() {
-  using G = Geo4<WAVES, NW, KT, NBUF>;
-  return G::RING + G::PART + G::Y16 + (FINAL ? G::YF : 0);
-}
-
 // swizzle of 16-B chunk slots by row (see tsk_kernels.hip: a GF(2) map that
 // keeps the b128 row reads and the transposed reads conflict-free)
 template <int NCH>
@@ -170,310 +93,6 @@ __device__ __forceinline__ int swz4(int row) {
   else return row & (NCH - 1);
 }
 
-// float offset of row quad q (rows 4q .. 4q+3) of column col in a [col][16]
-// f32 tile: the quad slot is XOR-swizzled by (col >> 1) & 3, which makes the
-// b128 partial stores, the reducer's b128 reads and the Gram's b128 reads
-// conflict-free (gfx950 LDS lane groups) with no padding
-__device__ __forceinline__ int qidx(int col, int q) { return col * 16 + 4 * (q ^ ((col >> 1) & 3)); }
-
-// FINAL: stored Y (ldy = KP) and, with GRAM, the fp64 Gram slab.  Otherwise W only.
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM, bool NTL>
-__global__ void __launch_bounds__(WAVES * 64, 1)
-k_rsvd_pass(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const bf16_t* __restrict__ Zt, int k,
-            float* __restrict__ Wslab, double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
-            float* __restrict__ scratch) {
-  using G = Geo4<WAVES, NW, KT, NBUF>;
-  constexpr int BM = G::BM;
-  constexpr int KP = G::KP;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* ring = smem;
-  float* part = (float*)(smem + G::RING);
-  char* y16 = smem + G::RING + G::PART;
-  float* yf = (float*)(smem + G::RING + G::PART + G::Y16);
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g4 = lane >> 4, i16 = lane & 15;
-  const int c0w = w * NW;
-  const int64_t nblocks = (m + BM - 1) / BM;
-  const int64_t b0 = blockIdx.x;
-  const int64_t bstep = gridDim.x;
-  const int64_t nloc = b0 < nblocks ? (nblocks - 1 - b0) / bstep + 1 : 0;
-
-  // ---- Z fragments (B operand of step 1): lane holds Z[c0w+32ks+8g+j][16t+i16]
-  bf16x8 zf[NW / 32][KT];
-#pragma unroll
-  for (int ks = 0; ks < NW / 32; ++ks)
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      const int col = 16 * t + i16;
-      const int kk = c0w + 32 * ks + 8 * g4;
-      bf16x8 v = {};
-      if (col < k && kk + 8 <= n) v = *(const bf16x8*)(Zt + (int64_t)col * n + kk);
-      zf[ks][t] = v;
-    }
-  // consume the Z loads here so hipcc's wait for them sits before the loop
-#pragma unroll
-  for (int ks = 0; ks < NW / 32; ++ks)
-#pragma unroll
-    for (int t = 0; t < KT; ++t) asm volatile("" ::"v"(zf[ks][t]));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  f32x4 accW[NW / 16][KT];
-#pragma unroll
-  for (int a = 0; a < NW / 16; ++a)
-#pragma unroll
-    for (int t = 0; t < KT; ++t) accW[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f64x4 accG[GRAM ? G::GS : 1];
-  f32x4 gblk[GRAM ? G::GS : 1];   // this block's f32 Gram tile, added to accG one block later
-#pragma unroll
-  for (int s = 0; s < (GRAM ? G::GS : 1); ++s) {
-    accG[s] = f64x4{0.0, 0.0, 0.0, 0.0};
-    gblk[s] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  // fp64 accumulation of the previous block's Gram tile: placed a barrier
-  // after its MFMAs were issued, so the adds never wait on the MFMA pipe
-  auto gram_acc = [&]() {
-    if constexpr (GRAM) {
-#pragma unroll
-      for (int s = 0; s < G::GS; ++s)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) accG[s][e] += (double)gblk[s][e];
-    }
-  };
-
-  // ---- LDS-DMA of row block `blk` (this wave's columns) into ring slot `slot`.
-  //      The per-lane source offsets inside a block are fixed: precomputed
-  //      once (row, swizzled chunk, column clamp for the last wave), so a
-  //      full block costs one scalar base per block; only the ragged last
-  //      block clamps rows per lane.
-  unsigned voff[G::LPB];
-#pragma unroll
-  for (int i = 0; i < G::LPB; ++i) {
-    const int byte = i * 1024 + lane * 16;
-    const int row = byte / G::ROWB;
-    const int sl = (byte % G::ROWB) / 16;
-    const int chunk = sl ^ swz4<G::NCH>(row);
-    int col = c0w + chunk * 8;
-    col = col + 8 <= n ? col : n - 8;
-    voff[i] = (unsigned)((row * lda + col) * 2);
-  }
-  auto issue = [&](int64_t blk, int slot) {
-    char* region = ring + (slot * WAVES + w) * G::REGION;
-    const int64_t r0 = (b0 + blk * bstep) * BM;
-    if (r0 + BM <= m) {
-      const bf16_t* base = A + r0 * lda;
-#pragma unroll
-      for (int i = 0; i < G::LPB; ++i) {
-        const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-        dma16s<NTL>(voff[i], (const void*)base, dst);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < G::LPB; ++i) {
-        const int byte = i * 1024 + lane * 16;
-        const int row = byte / G::ROWB;
-        int64_t grow = r0 + row;
-        grow = grow < m ? grow : m - 1;
-        const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-        dma16<NTL>((const void*)((const char*)(A + grow * lda) + (voff[i] - (unsigned)(row * lda * 2))), dst);
-      }
-    }
-  };
-
-  // reducer role of this lane: row quad rq of y column rc
-  const int rc = w * G::CPW + (lane >> 2), rq = lane & 3;
-  // FINAL: the block's Y rows are one contiguous k * 16-float chunk when
-  // ldy == k: the reducers stage y' in LDS and the first waves write it as
-  // float4 rows (one store instruction per wave) instead of four scattered
-  // 4-B stores per reducer lane
-  const bool vecY = FINAL && (k % 4 == 0) && (ldy == k);
-  const int nvec = BM * k / 4;
-  // Y store instructions per wave per block (vmcnt bookkeeping: exact, every
-  // store issues even for rows past m -- they go to the scratch line)
-  const int nst = !FINAL ? 0 : (vecY ? (w * 64 < nvec ? 1 : 0) : 4);
-
-
-#pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
-    if (p < nloc) issue(p, p);
-
-  int slot = 0;
-  for (int64_t j = 0; j < nloc; ++j) {
-    // refill the slot iteration j - 1 consumed (its reads were waited for by
-    // the MFMAs that used them)
-    if (j + NBUF - 1 < nloc) issue(j + NBUF - 1, slot == 0 ? NBUF - 1 : slot - 1);
-    {
-      // wait for block j: younger ops are the DMA groups of blocks j+1.. and
-      // (FINAL) the Y stores of the iterations since block j's DMA was issued
-      const int64_t ydma = nloc - 1 - j;
-      const int nd = (int)(ydma < NBUF - 1 ? ydma : NBUF - 1);
-      const int ns = (int)(j < NBUF - 1 ? j : NBUF - 1);
-      wait_vm(nd * G::LPB + ns * nst);
-    }
-    const char* region = ring + (slot * WAVES + w) * G::REGION;
-    const int64_t r0 = (b0 + j * bstep) * BM;
-
-    // ---- step 1: partial y over this wave's columns -> part[w] ([col][row])
-    {
-      f32x4 accY[KT];
-#pragma unroll
-      for (int t = 0; t < KT; ++t) accY[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < NW / 32; ++ks) {
-        const int row = i16;
-        const int chunk = g4 + 4 * ks;
-        const bf16x8 af = *(const bf16x8*)(region + row * G::ROWB + (chunk ^ swz4<G::NCH>(row)) * 16);
-#pragma unroll
-        for (int t = 0; t < KT; ++t) accY[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zf[ks][t], accY[t], 0, 0, 0);
-      }
-#pragma unroll
-      for (int t = 0; t < KT; ++t) *(f32x4*)&part[w * KP * BM + qidx(16 * t + i16, g4)] = accY[t];
-    }
-    lds_barrier();   // (A) the partials of block j are complete
-    gram_acc();
-    // ---- step 2: each wave sums its CPW columns over the WAVES partials,
-    //      emits y as bf16 hi / lo B-fragment images (and, FINAL, f32 y and
-    //      the Y rows straight from the sums)
-    if (lane < G::RL) {
-      f32x4 sum = *(const f32x4*)&part[qidx(rc, rq)];
-#pragma unroll
-      for (int v = 1; v < WAVES; ++v) sum += *(const f32x4*)&part[v * KP * BM + qidx(rc, rq)];
-      if (r0 + BM > m) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (r0 + 4 * rq + e >= m) sum[e] = 0.f;
-      }
-      s16x4 hi, lo;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const short h = bf16_bits(sum[e]);
-        hi[e] = h;
-        lo[e] = bf16_bits(sum[e] - bf16_val(h));
-      }
-      *(s16x4*)(y16 + rc * 32 + rq * 8) = hi;
-      *(s16x4*)(y16 + G::Y16P + rc * 32 + rq * 8) = lo;
-      if constexpr (FINAL) {
-        // the stored Y is y' = y_hi + y_lo (exact in f32): the rows W and
-        // the in-pass Gram are formed from, so Y, W and G stay consistent
-        if (vecY) {
-          if (rc < k) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) yf[(4 * rq + e) * k + rc] = bf16_val(hi[e]) + bf16_val(lo[e]);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int64_t row = r0 + 4 * rq + e;
-            float* dst = (row < m && rc < k) ? Y + row * ldy + rc : scratch + lane;
-            *dst = bf16_val(hi[e]) + bf16_val(lo[e]);
-          }
-        }
-      }
-    }
-    lds_barrier();   // (B) y of block j is complete
-    if (FINAL && vecY && w * 64 < nvec) {
-      // one float4 per lane of the block's contiguous Y image (ragged rows /
-      // idle lanes write the scratch line: the store count stays exact)
-      const int t = w * 64 + lane;
-      const bool ok = t < nvec && r0 + (4 * t) / k < m;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (ok) v = *(const f32x4*)&yf[4 * t];
-      float* dst = ok ? Y + r0 * ldy + 4 * t : scratch + 4 * lane;
-      *(f32x4*)dst = v;   // (a non-temporal store measured 507 vs 446 us for the pass)
-    }
-
-
-    // ---- step 3: W += A^T (y_hi + y_lo).  K = 32 packs [8 rows of y_hi |
-    //      the same 8 rows of y_lo]: lane group g covers rows 8 (g >> 1) .. +7
-    //      of y_hi (g even) or y_lo (g odd)
-    {
-      const int rb = 8 * (g4 >> 1);
-      const char* yp = y16 + (g4 & 1) * G::Y16P + rb * 2;
-      bf16x8 yfr[KT];
-#pragma unroll
-      for (int t = 0; t < KT; ++t) yfr[t] = *(const bf16x8*)(yp + (16 * t + i16) * 32);
-      // Gram of y' = y_hi + y_lo on the same fragments: with K = (part, row),
-      // yfr[t1]^T yfr[t2] = hi^T hi + lo^T lo and, against the fragment of
-      // the other part, hi^T lo + lo^T hi.  Every bf16 x bf16 product is
-      // exact in f32; a block's 64 products are summed in f32 by two MFMAs
-      // and added to the fp64 accumulator after the W MFMAs are issued.
-      if constexpr (GRAM) {
-        int tau = 0;
-#pragma unroll
-        for (int t1 = 0; t1 < KT; ++t1)
-#pragma unroll
-          for (int t2 = t1; t2 < KT; ++t2, ++tau) {
-            if ((tau % WAVES) == w) {
-              const int s = tau / WAVES;
-              const bf16x8 ysw = *(const bf16x8*)(y16 + ((g4 & 1) ^ 1) * G::Y16P + rb * 2 + (16 * t2 + i16) * 32);
-              const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-              gblk[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yfr[t1], yfr[t2], z4, 0, 0, 0);
-              gblk[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yfr[t1], ysw, gblk[s], 0, 0, 0);
-            }
-          }
-      }
-      const int q = i16 >> 2, p = i16 & 3;
-#pragma unroll
-      for (int ct = 0; ct < NW / 16; ++ct) {
-        const int chunk = 2 * ct + (p >> 1);
-        const int ra = rb + q, rbb = rb + 4 + q;
-        const char* aa = region + ra * G::ROWB + (chunk ^ swz4<G::NCH>(ra)) * 16 + (p & 1) * 8;
-        const char* ab2 = region + rbb * G::ROWB + (chunk ^ swz4<G::NCH>(rbb)) * 16 + (p & 1) * 8;
-        const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)aa);
-        const s16x4 b4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)ab2);
-        s16x8 a8;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          a8[u] = a4[u];
-          a8[4 + u] = b4[u];
-        }
-        const bf16x8 af8 = __builtin_bit_cast(bf16x8, a8);
-#pragma unroll
-        for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
-      }
-    }
-    slot = slot == NBUF - 1 ? 0 : slot + 1;
-  }
-  gram_acc();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // ---- W partial slab [n][k] (rows past n / columns past k dropped)
-  {
-    float* ws = Wslab + (int64_t)blockIdx.x * n * k;
-#pragma unroll
-    for (int ct = 0; ct < NW / 16; ++ct)
-#pragma unroll
-      for (int t = 0; t < KT; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = c0w + 16 * ct + 4 * g4 + e, col = 16 * t + i16;
-          if (row < n && col < k) ws[(int64_t)row * k + col] = accW[ct][t][e];
-        }
-  }
-  if constexpr (GRAM) {
-    // fp64 Gram slab [k][k]: each upper tile and its mirror (f32 C/D map:
-    // row = 4 (lane >> 4) + r, col = lane & 15)
-    double* gs = Gslab + (int64_t)blockIdx.x * k * k;
-    int tau = 0;
-#pragma unroll
-    for (int t1 = 0; t1 < KT; ++t1)
-#pragma unroll
-      for (int t2 = t1; t2 < KT; ++t2, ++tau) {
-        if ((tau % WAVES) == w) {
-          const int s = tau / WAVES;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = 16 * t1 + 4 * g4 + r, jj = 16 * t2 + i16;
-            if (i < k && jj < k && (t1 != t2 || i <= jj)) {
-              gs[i * k + jj] = accG[s][r];
-              if (i != jj) gs[jj * k + i] = accG[s][r];
-            }
-          }
-        }
-      }
-  }
-}
 
 // out[i][j] (i < rows, j < cols) = sum_s slab[s][i * cols + j], summed in f64.
 // 128 consecutive elements per 512-thread workgroup (two per lane); wave v
@@ -552,12 +171,11 @@ k_rsvd_reduce_wg(const float* __restrict__ wslab, int64_t tw, int cols, double* 
 }
 
 // ---------------------------------------------------------------- pass v5
-// Role-split form of the fused pass (same slabs, same Y / Gram outputs as v4):
+// Role-split form of the fused pass:
 //   * step 1 (y = A_blk Z) is owned by KT "y waves": wave t < KT computes the
 //     whole 16 x 16 tile t of y over ALL n columns (its Z^T slice, 32 bf16
-//     fragments, in registers), so y never needs a cross-wave sum -- the
-//     v4 partial tile, its reducer phase and one of its two barriers per block
-//     are gone;
+//     fragments, in registers), so y never needs a cross-wave sum (no
+//     partial tiles, no reducer phase);
 //   * step 3 (W += A^T (y_hi + y_lo)) is split over all 8 waves by 16-column
 //     W tiles, sized so every SIMD pair (waves w and w + 4 share a SIMD) gets
 //     about the same matrix-core work (the y waves take 0-2 W tiles);
@@ -663,7 +281,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
     }
   };
 
-  // LDS-DMA of this wave's region of row block blk into slot `slot` (v4 image)
+  // LDS-DMA of this wave's region of row block blk into slot `slot` (swizzled image)
   unsigned voff[LPB];
 #pragma unroll
   for (int i = 0; i < LPB; ++i) {
@@ -1011,30 +629,16 @@ int cu_count() {
   return ncu;
 }
 
-template <int WAVES, int NW, int KT, int NBUF, bool FINAL, bool GRAM = FINAL>
-int launch_pass(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt, int k, float* Wslab,
-                double* Gslab, float* Y, int64_t ldy, float* scratch, int grid, hipStream_t s, int variant) {
-  using G = Geo4<WAVES, NW, KT, NBUF>;
-  constexpr int LDS = pass_lds<WAVES, NW, KT, NBUF, FINAL, GRAM>();
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto kern = (variant & 16) ? k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL, GRAM, true>
-                             : k_rsvd_pass<WAVES, NW, KT, NBUF, FINAL, GRAM, false>;
-  SL_LDS_ATTR(kern, LDS);
-  kern<<<grid, G::THREADS, LDS, s>>>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch);
-  SL_LAUNCH_CHECK();
-  return SL_OK;
-}
-
 }  // namespace
 
-// grid of the v4 pass for m rows (one workgroup per CU, at most one per block)
+// grid of the pass for m rows (one workgroup per CU, at most one per block)
 SL_API int sl_rsvd_pass_grid(int64_t m) {
   const int64_t nb = (m + 15) / 16;
   const int64_t c = cu_count();
   return (int)(nb < c ? (nb > 0 ? nb : 1) : c);
 }
 
-// bytes of slab workspace the v4 pass needs: W slabs [grid][n][k] f32 and
+// bytes of slab workspace the pass needs: W slabs [grid][n][k] f32 and
 // (final) G slabs [grid][k][k] f64, plus a 1 KiB scratch line
 SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k) {
   const int64_t g = sl_rsvd_pass_grid(m);
@@ -1045,13 +649,13 @@ SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k) {
   return b + 1024;
 }
 
-// One v4 pass.  A: m x n bf16 (lda % 8 == 0, 16 <= n <= 1024, n % 8 == 0);
+// One fused pass.  A: m x n bf16 (lda % 8 == 0, 16 <= n <= 1024, n % 8 == 0);
 // Zt: k x n bf16 (1 <= k <= 48).  ws: sl_rsvd_pass_workspace bytes.
 // final = 0: W slabs only.  final = 1: also Y (m x k f32, row stride ldy >=
 // k; Y = y_hi + y_lo, the bf16 pair W is formed from) and the fp64 Gram slabs
 // of that Y (exact bf16 products, f32 per 16-row block, f64 across blocks);
 // final = 2: W slabs and Y only.  variant bits: 256 = walk the row blocks
-// last-to-first, 64/128 = y-wave priority (tuning), 32 = the v4 kernel (A/B).
+// last-to-first, 64/128 = y-wave priority (tuning).
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
                         float* Y, int64_t ldy, int final_pass, int variant, void* stream) {
   if (m <= 0) return SL_OK;
@@ -1071,41 +675,19 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* z = (const bf16_t*)Zt;
   const int KT = (k + 15) / 16;
-  if (!(variant & 32)) {
-    // v5 (default): role-split waves, one barrier per block
 #define SL_P5(KTT)                                                                                                 \
   return final_pass == 1 ? launch_pass5<KTT, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
        : final_pass == 2 ? launch_pass5<KTT, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
                          : launch_pass5<KTT, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant)
-    switch (KT) {
-      case 1: SL_P5(1);
-      case 2: SL_P5(2);
-      default: SL_P5(3);
-    }
+  switch (KT) {
+    case 1: SL_P5(1);
+    case 2: SL_P5(2);
+    default: SL_P5(3);
+  }
 #undef SL_P5
-  }
-  const bool small = n <= 512;
-  const int nbuf = (variant & 15) == 3 ? 3 : 4;
-#define SL_P(NW, KTT, NB)                                                                                    \
-  return final_pass == 1 ? launch_pass<8, NW, KTT, NB, true, true>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
-       : final_pass == 2 ? launch_pass<8, NW, KTT, NB, true, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant) \
-                         : launch_pass<8, NW, KTT, NB, false, false>(a, m, (int)n, lda, z, k, Wslab, Gslab, Y, ldy, scratch, grid, s, variant)
-#define SL_PK(NW, NB)                        \
-  switch (KT) {                              \
-    case 1: SL_P(NW, 1, NB);                 \
-    case 2: SL_P(NW, 2, NB);                 \
-    default: SL_P(NW, 3, NB);                \
-  }
-  if (small) {
-    if (nbuf == 3) { SL_PK(64, 3) } else { SL_PK(64, 4) }
-  } else {
-    if (nbuf == 3) { SL_PK(128, 3) } else { SL_PK(128, 4) }
-  }
-#undef SL_PK
-#undef SL_P
 }
 
-// Sum the v4 pass slabs: W (n x k, into Wout with row stride ldw; f64 when
+// Sum the pass slabs: W (n x k, into Wout with row stride ldw; f64 when
 // w_f64) and, when Gout is given, the fp64 Gram (k x k, row stride ldg).
 // as sl_rsvd_reduce, and zero_word (if given) is set to 0 by the same launch
 // (the engine clears the call's status word here instead of a memset node)

@@ -1,0 +1,696 @@
+// Hand-written tall-skinny products of the general-precision randomized SVD
+// (rsvd_general.hip, f32 / f64 A, k <= 64; reference nla/svd.hpp:71-149 and
+// :222-318 ApproximateSVD<float / double>, whose power iteration applies A
+// and A^T to an n x k / m x k block and re-orthonormalises after each):
+//
+//   sl_ts_az     Y (m x k) = A (m x n) Z (n x k)          one streaming read of A
+//   sl_ts_atq    W (n x k, f64) = A^T Q (Q m x k)         one streaming read of A,
+//                                                         per-row-group slabs + f64 sum
+//   sl_ts_xm64   out (rows x k2, f32 / f64) = X (rows x k, f64) M (k x k2, f64)
+//   sl_ts_gram64 G (k x k, f64) = X^T X (X rows x k, f64)
+//   sl_ts_small  C = op(A) op(B), k x k operands, one workgroup (f64)
+//
+// Both big products run in A's own precision on the matrix cores
+// (v_mfma_f32_16x16x4_f32: exact f32 products in a k-ordered fmaf chain;
+// v_mfma_f64_16x16x4_f64) -- the reference's precision, not a split bf16
+// shortcut.  At k = 40 (three 16-column tiles) a pass over a 1e6 x 1000 f32 A
+// is 2 x 0.96e11 FLOP, i.e. 0.62 ms per product at the f32 matrix peak against
+// 0.67 ms of HBM for the 4 GB read: the kernels are built so neither the
+// matrix pipe nor the memory system waits on the other (software-pipelined
+// global loads straight into the MFMA operand registers, no LDS staging of A).
+//
+// MFMA operand trick shared by both: a 16x16x4 MFMA sums over 4 values of
+// its K index held by lane groups l >> 4; WHICH columns (rows) of A those are
+// is free as long as both operands agree.  So a lane loads 16 contiguous
+// bytes of one row of A (VW = 4 f32 / 2 f64 consecutive elements) and feeds
+// element s of that vector to the s-th MFMA of the group: global loads stay
+// 16-B per lane and 64-256 B contiguous per row, with no transposition.
+#include "sl_common.hpp"
+
+int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows, int cols,
+                              double* out, int ld_out, hipStream_t s);
+int sl_slab_reduce_launch_d2d(const double* slab, int nslab, int64_t slab_stride, int ld_in, int rows, int cols,
+                              double* out, int ld_out, hipStream_t s);
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) double f64x4;
+typedef __attribute__((ext_vector_type(2))) double f64x2;
+
+template <typename T>
+struct Mf;
+template <>
+struct Mf<float> {
+  using acc = f32x4;
+  using vec = f32x4;
+  static constexpr int VW = 4;
+  static __device__ __forceinline__ acc mfma(float a, float b, acc c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  // row of accumulator element r in lane l (f32 16x16 C/D map)
+  static __device__ __forceinline__ int drow(int l, int r) { return 4 * (l >> 4) + r; }
+};
+template <>
+struct Mf<double> {
+  using acc = f64x4;
+  using vec = f64x2;
+  static constexpr int VW = 2;
+  static __device__ __forceinline__ acc mfma(double a, double b, acc c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+  // the f64 MFMA's own C/D map (not the f32 one)
+  static __device__ __forceinline__ int drow(int l, int r) { return (l >> 4) + 4 * r; }
+};
+
+// Global loads as inline asm (the compiler neither tracks nor waits for
+// them): the A^T Q loop keeps a ring of loads in flight across its loop
+// back-edge, where the compiler's own wait insertion fell back to draining
+// every load each iteration.  The matching waits are explicit (wait_ring).
+template <typename V>
+__device__ __forceinline__ V ld16(const void* p) {
+  V v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float ld_el(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ double ld_el(const double* p) {
+  double v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// ------------------------------------------------------------------ Y = A Z
+// 256-thread workgroups (two per CU), persistent over 128-row blocks; wave w
+// owns rows 32 w .. 32 w + 31 of the block (RT = 2 row tiles) and all KT
+// column tiles of y.  The n columns stream in groups of GW = 4 EPL columns
+// (EPL = VL VW: VL = 2 adjacent 16-B loads per lane and row tile, so the 4
+// lanes of a row cover one whole 128-B line per group -- single 16-B pieces
+// per group left every line to two half-line fetches a group apart), 4
+// groups per chunk; the chunk's Z rows sit in LDS as ready-made B fragments
+// ([group][tile][lane] x EPL, VL ds_read_b128 per tile and group),
+// double-buffered: chunk c + 1 is loaded into registers while chunk c
+// computes and stored after it, one barrier per chunk.  A is prefetched PD =
+// 2 groups ahead in a register ring (slot g % 2, static in the unrolled body).
+constexpr int AZ_NT = 256, AZ_RT = 2, AZ_VL = 2, AZ_NG = 4, AZ_PD = 2, AZ_BR = 4 * 16 * AZ_RT;
+
+template <typename T, int KT>
+constexpr int az_lds() { return 2 * AZ_NG * KT * 64 * 16 * AZ_VL; }
+
+template <typename T, int KT, bool VEC>
+__global__ void __launch_bounds__(AZ_NT, 2)
+k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Z, int k, T* __restrict__ Y,
+        int64_t ldy) {
+  using M = Mf<T>;
+  using vec = typename M::vec;
+  using acc_t = typename M::acc;
+  constexpr int VW = M::VW, EPL = AZ_VL * VW, GW = 4 * EPL, CW = AZ_NG * GW, KP = 16 * KT;
+  constexpr int ZE = (CW * KP + AZ_NT - 1) / AZ_NT;   // Z elements per thread per chunk
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* zl = (T*)smem;                                    // [2][NG][KT][64][EPL]
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nchunk = (n + CW - 1) / CW;
+  const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
+  const int64_t nmine = (int64_t)blockIdx.x < nrb ? (nrb - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t nfc = nmine * nchunk;
+  if (nfc == 0) return;
+
+  // Every global load of the loop is inline asm (ld16 / ld_el) with explicit
+  // waits: the ring crosses the chunk loop's back-edge, where the compiler's
+  // own wait insertion kept only a few loads in flight.  Loads return in
+  // issue order, so waiting for "at most N outstanding" with N = the loads
+  // issued after the one needed is exact (stores in between only make it
+  // stricter).  Issue order per chunk: Z of the next chunk (ZE loads, always
+  // issued, clamped), then per group g its MFMAs and the refill of its slot
+  // g % PD with group g + PD (the first PD groups of the next chunk for the
+  // last PD groups).  When group g is used, the loads issued after its
+  // refill are the next PD - 1 refills, plus the chunk's Z loads for g < PD.
+  static_assert(AZ_NG == 2 * AZ_PD, "slot arithmetic");
+  constexpr int LPG = AZ_RT * AZ_VL * (VEC ? 1 : VW);
+  constexpr int RWA = (AZ_PD - 1) * LPG + ZE < 63 ? (AZ_PD - 1) * LPG + ZE : 63;   // g < PD
+  constexpr int RWB = (AZ_PD - 1) * LPG < 63 ? (AZ_PD - 1) * LPG : 63;             // g >= PD
+  constexpr int ZW = AZ_NG * LPG < 63 ? AZ_NG * LPG : 63;   // loads after a Z chunk's at its LDS store
+  T zr[ZE];
+  auto zload = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < ZE; ++u) {
+      const int e = tid + AZ_NT * u;
+      const int cc = e / KP, jj = e - cc * KP;
+      int col = c * CW + cc;
+      col = col < n ? col : n - 1;
+      zr[u] = ld_el(Z + (int64_t)col * k + (jj < k ? jj : k - 1));
+    }
+  };
+  auto zstore = [&](int buf, int c) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ZW) : "memory");
+#pragma unroll
+    for (int u = 0; u < ZE; ++u) asm volatile("" : "+v"(zr[u]));
+    T* zb = zl + buf * (AZ_NG * KT * 64 * EPL);
+#pragma unroll
+    for (int u = 0; u < ZE; ++u) {
+      const int e = tid + AZ_NT * u;
+      if (e < CW * KP) {
+        const int cc = e / KP, jj = e - cc * KP;
+        const int q = cc / GW, wq = cc - q * GW, kk = wq / EPL, s = wq - kk * EPL;
+        const int t = jj >> 4, j16 = jj & 15;
+        const bool ok = c * CW + cc < n && jj < k;
+        zb[((q * KT + t) * 64 + kk * 16 + j16) * EPL + s] = ok ? zr[u] : (T)0;
+      }
+    }
+  };
+
+  // A group loads: rows clamped to m - 1 (never stored), columns past n
+  // clamped to a valid position (their Z rows are zero), a flat chunk past
+  // the end re-reads the last one (never used)
+  vec ring[AZ_PD][AZ_RT][AZ_VL];
+  auto issue = [&](int64_t fc, int g, int slot) {
+    fc = fc < nfc ? fc : nfc - 1;
+    const int64_t j = fc / nchunk;
+    const int c = (int)(fc - j * nchunk);
+    const int64_t r0 = (blockIdx.x + j * gridDim.x) * AZ_BR + 32 * w;
+    const int col0 = c * CW + g * GW + EPL * (lane >> 4);
+#pragma unroll
+    for (int rt = 0; rt < AZ_RT; ++rt) {
+      int64_t row = r0 + 16 * rt + (lane & 15);
+      row = row < m ? row : m - 1;
+      const T* src = A + row * lda;
+#pragma unroll
+      for (int vl = 0; vl < AZ_VL; ++vl) {
+        const int col = col0 + VW * vl;
+        if constexpr (VEC) {
+          ring[slot][rt][vl] = ld16<vec>(src + (col < n ? col : n - VW));
+        } else {
+          vec v;
+#pragma unroll
+          for (int e = 0; e < VW; ++e) v[e] = ld_el(src + (col + e < n ? col + e : n - 1));
+          ring[slot][rt][vl] = v;
+        }
+      }
+    }
+  };
+  auto wait_slot = [&](int g) {
+    const int slot = g % AZ_PD;
+    if (g < AZ_PD) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ring[slot][0][0]) : "n"(RWA));
+    else asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ring[slot][0][0]) : "n"(RWB));
+#pragma unroll
+    for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+      for (int vl = 0; vl < AZ_VL; ++vl)
+        if (rt + vl > 0) asm volatile("" : "+v"(ring[slot][rt][vl]));
+  };
+
+  acc_t acc[AZ_RT][KT];
+#pragma unroll
+  for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) acc[rt][t] = acc_t{};
+
+  // prologue: chunk 0 of Z in buffer 0, groups 0 .. PD - 1 of flat chunk 0
+  // in flight (issued before the chunk loop's first Z loads, as the
+  // previous chunk's refills would be)
+  zload(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  zstore(0, 0);
+#pragma unroll
+  for (int g = 0; g < AZ_PD; ++g) issue(0, g, g);
+  __syncthreads();
+
+  for (int64_t fc = 0; fc < nfc; ++fc) {
+    const int c = (int)(fc % nchunk);
+    const int buf = nchunk > 1 ? (int)(fc & 1) : 0;   // one chunk: Z never reloads
+    const int cn = c + 1 < nchunk ? c + 1 : 0;
+    zload(cn);   // always issued: the wait arithmetic counts it
+    const T* zb = zl + buf * (AZ_NG * KT * 64 * EPL);
+#pragma unroll
+    for (int g = 0; g < AZ_NG; ++g) {
+      wait_slot(g);
+      const int slot = g % AZ_PD;
+#pragma unroll
+      for (int vl = 0; vl < AZ_VL; ++vl) {
+        vec zv[KT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) zv[t] = *(const vec*)(zb + ((g * KT + t) * 64 + lane) * EPL + VW * vl);
+#pragma unroll
+        for (int s = 0; s < VW; ++s)
+#pragma unroll
+          for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+            for (int t = 0; t < KT; ++t) acc[rt][t] = M::mfma(ring[slot][rt][vl][s], zv[t][s], acc[rt][t]);
+      }
+      // refill this slot with group g + PD (of the next flat chunk past the end)
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + AZ_PD < AZ_NG) issue(fc, g + AZ_PD, slot);
+      else issue(fc + 1, g + AZ_PD - AZ_NG, slot);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c == nchunk - 1) {
+      // the row block is complete: y out, accumulators cleared
+      const int64_t j = fc / nchunk;
+      const int64_t r0 = (blockIdx.x + j * gridDim.x) * AZ_BR + 32 * w;
+#pragma unroll
+      for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const int col = 16 * t + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + 16 * rt + M::drow(lane, r);
+            if (row < m && col < k) Y[row * ldy + col] = acc[rt][t][r];
+          }
+          acc[rt][t] = acc_t{};
+        }
+    }
+    zstore(buf ^ 1, cn);   // (one chunk: a scratch copy into the unused buffer)
+    __syncthreads();
+  }
+  // the clamped refills past the end: landed, and kept live until then (an
+  // asm load's register the compiler thinks dead could be reused in flight)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int g = 0; g < AZ_PD; ++g)
+#pragma unroll
+    for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+      for (int vl = 0; vl < AZ_VL; ++vl) asm volatile("" : "+v"(ring[g][rt][vl]));
+}
+
+// ---------------------------------------------------------------- W = A^T Q
+// 512-thread workgroups: blockIdx.x = a column slice of CS = 8 x V x 16 VW
+// columns (wave w: V vectors of 16 lanes x VW columns per row), blockIdx.y =
+// a row group.  Per row quad the lane (kk = l >> 4, nn = l & 15) loads row
+// r + kk, columns cb + VW nn .. + VW - 1 of each vector: element e of vector
+// v is the A^T operand of W tile (v, e), whose 16 rows are the columns
+// cb + VW nn + e (stride VW) -- so the loads are plain row segments and the
+// W tiles come out column-interleaved (undone at the slab store).  Q's B
+// fragments (Q[r + kk][16 t + nn]) load straight from global (the 8 waves of
+// a workgroup read the same rows: L1 / L2 hits).  W accumulates over the
+// whole row group in registers (A's precision), then one slab per row group.
+constexpr int AT_NT = 512, AT_V = 2;
+// ring depth: 8 row quads in flight, 4 at KT = 4 (register budget)
+template <int KT>
+constexpr int at_pd() { return KT >= 4 ? 4 : 8; }
+
+template <typename T, int KT, bool VEC>
+__global__ void __launch_bounds__(AT_NT, 1)
+k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Q, int k, int64_t rows_per,
+         T* __restrict__ slab) {
+  using M = Mf<T>;
+  using vec = typename M::vec;
+  using acc_t = typename M::acc;
+  constexpr int VW = M::VW, WC = AT_V * 16 * VW, CS = 8 * WC, PD = at_pd<KT>();
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kk = lane >> 4, nn = lane & 15;
+  const int64_t rbeg = (int64_t)blockIdx.y * rows_per;
+  int64_t rend = rbeg + rows_per;
+  rend = rend < m ? rend : m;
+  const int cbw = blockIdx.x * CS + w * WC;   // this wave's first column
+  // waves of the last slice past n idle (wave-uniform)
+  const int64_t nq = (rend > rbeg && cbw < n) ? (rend - rbeg + 3) / 4 : 0;
+
+  acc_t acc[AT_V][VW][KT];
+#pragma unroll
+  for (int v = 0; v < AT_V; ++v)
+#pragma unroll
+    for (int e = 0; e < VW; ++e)
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc[v][e][t] = acc_t{};
+
+  // loads branch-free (see k_ts_az): rows clamped into the group, columns
+  // into [0, n); the Q fragment of a row past the group (or a k column past
+  // k) is zeroed at USE time from a mask formed at issue time, so nothing
+  // touches a loaded value before its turn in the MFMA stream
+  vec ra[PD][AT_V];
+  T rq[PD][KT];
+  bool rok[PD];
+  auto issue = [&](int64_t qi, int slot) {
+    int64_t row = rbeg + 4 * qi + kk;
+    rok[slot] = row < rend;
+    row = row < rend ? row : rend - 1;
+    const T* src = A + row * lda;
+#pragma unroll
+    for (int v = 0; v < AT_V; ++v) {
+      const int col = cbw + v * 16 * VW + VW * nn;
+      if constexpr (VEC) {
+        ra[slot][v] = ld16<vec>(src + (col < n ? col : n - VW));
+      } else {
+        vec x;
+#pragma unroll
+        for (int e = 0; e < VW; ++e) x[e] = ld_el(src + (col + e < n ? col + e : n - 1));
+        ra[slot][v] = x;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int col = 16 * t + nn;
+      rq[slot][t] = ld_el(Q + row * k + (col < k ? col : k - 1));
+    }
+  };
+  // loads per slot; slot p is waited for with the PD - 1 later slots in flight
+  constexpr int LPS = AT_V * (VEC ? 1 : VW) + KT;
+  // (waiting for at most 63 when more are in flight is stricter, still exact-safe)
+  constexpr int INFLIGHT = (PD - 1) * LPS < 63 ? (PD - 1) * LPS : 63;
+  auto wait_ring = [&](int p) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ra[p][0]) : "n"(INFLIGHT));
+#pragma unroll
+    for (int v = 1; v < AT_V; ++v) asm volatile("" : "+v"(ra[p][v]));
+#pragma unroll
+    for (int t = 0; t < KT; ++t) asm volatile("" : "+v"(rq[p][t]));
+  };
+
+  if (nq > 0) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p) issue(p, p);
+    for (int64_t q0 = 0; q0 < nq; q0 += PD) {
+#pragma unroll
+      for (int p = 0; p < PD; ++p) {
+        wait_ring(p);
+        // a quad past nq has rok false in every lane: its Q operand is zero
+        T b[KT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) b[t] = (rok[p] && 16 * t + nn < k) ? rq[p][t] : (T)0;
+#pragma unroll
+        for (int v = 0; v < AT_V; ++v)
+#pragma unroll
+          for (int e = 0; e < VW; ++e)
+#pragma unroll
+            for (int t = 0; t < KT; ++t) acc[v][e][t] = M::mfma(ra[p][v][e], b[t], acc[v][e][t]);
+        // slot p's MFMAs, then its refill (scheduling barriers keep the
+        // order the vmcnt arithmetic assumes)
+        __builtin_amdgcn_sched_barrier(0);
+        issue(q0 + p + PD, p);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // the clamped refills past the end: landed, and kept live until then
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < PD; ++p) {
+#pragma unroll
+      for (int v = 0; v < AT_V; ++v) asm volatile("" : "+v"(ra[p][v]));
+#pragma unroll
+      for (int t = 0; t < KT; ++t) asm volatile("" : "+v"(rq[p][t]));
+    }
+  }
+  if (cbw >= n) return;
+  // slab (row group y) [n][k]: tile (v, e) row i is column cbw + v 16 VW + VW i + e
+  T* sb = slab + (int64_t)blockIdx.y * n * k;
+#pragma unroll
+  for (int v = 0; v < AT_V; ++v)
+#pragma unroll
+    for (int e = 0; e < VW; ++e)
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int kc = 16 * t + nn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = M::drow(lane, r);
+          const int col = cbw + v * 16 * VW + VW * i + e;
+          if (col < n && kc < k) sb[(int64_t)col * k + kc] = acc[v][e][t][r];
+        }
+      }
+}
+
+// ------------------------------------------------------- small f64 helpers
+// out (rows x k2, TO, ldo) = X (rows x k, f64, ldx) M (k x k2, f64): 64-row
+// tiles staged in LDS (coalesced), thread (row = t & 63, column group t >> 6)
+// forms columns cg, cg + 4, ...; the tile goes back through LDS so the
+// stores are row-contiguous.
+template <typename TO>
+__global__ void __launch_bounds__(256) k_ts_xm64(const double* __restrict__ X, int64_t rows, int k, int64_t ldx,
+                                                 const double* __restrict__ Mm, int k2, TO* __restrict__ out,
+                                                 int64_t ldo) {
+  __shared__ double ms[64 * 64];
+  __shared__ double xs[64 * 65];
+  for (int e = threadIdx.x; e < k * k2; e += 256) ms[e] = Mm[e];
+  const int tid = threadIdx.x, row = tid & 63, cg = tid >> 6;
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < rows; r0 += (int64_t)gridDim.x * 64) {
+    __syncthreads();
+    for (int e = tid; e < 64 * k; e += 256) {
+      const int rr = e / k, c = e - rr * k;
+      xs[rr * 65 + c] = r0 + rr < rows ? X[(r0 + rr) * ldx + c] : 0.0;
+    }
+    __syncthreads();
+    double acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+    for (int l = 0; l < k; ++l) {
+      const double x = xs[row * 65 + l];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int c = cg + 4 * j;
+        if (c < k2) acc[j] = fma(x, ms[l * k2 + c], acc[j]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = cg + 4 * j;
+      if (c < k2) xs[row * 65 + c] = acc[j];
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * k2; e += 256) {
+      const int rr = e / k2, c = e - rr * k2;
+      if (r0 + rr < rows) out[(r0 + rr) * ldo + c] = (TO)xs[rr * 65 + c];
+    }
+  }
+}
+
+// per-workgroup slab (k x k f64) of X^T X over its rows: 64-row tiles in
+// LDS, thread t owns entries t, t + 256, ... of the upper triangle
+__global__ void __launch_bounds__(256) k_ts_gram64(const double* __restrict__ X, int64_t rows, int k, int64_t ldx,
+                                                   double* __restrict__ slab) {
+  __shared__ double xs[64 * 65];
+  const int tid = threadIdx.x;
+  const int ntri = k * (k + 1) / 2;
+  int pi[9], pj[9];
+  double acc[9];
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    int e = tid + 256 * u, i = 0;
+    if (e < ntri) {
+      while (e >= k - i) { e -= k - i; ++i; }
+      pi[u] = i;
+      pj[u] = i + e;
+    } else {
+      pi[u] = pj[u] = 0;
+    }
+    acc[u] = 0.0;
+  }
+  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < rows; r0 += (int64_t)gridDim.x * 64) {
+    __syncthreads();
+    for (int e = tid; e < 64 * k; e += 256) {
+      const int rr = e / k, c = e - rr * k;
+      xs[rr * 65 + c] = r0 + rr < rows ? X[(r0 + rr) * ldx + c] : 0.0;
+    }
+    __syncthreads();
+    for (int rr = 0; rr < 64; ++rr) {
+#pragma unroll
+      for (int u = 0; u < 9; ++u) acc[u] = fma(xs[rr * 65 + pi[u]], xs[rr * 65 + pj[u]], acc[u]);
+    }
+  }
+  double* sb = slab + (int64_t)blockIdx.x * k * k;
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    if (tid + 256 * u < ntri) {
+      sb[pi[u] * k + pj[u]] = acc[u];
+      sb[pj[u] * k + pi[u]] = acc[u];
+    }
+  }
+}
+
+// C (mr x nc, ldc) = op(A) op(B), op(A) mr x kd, op(B) kd x nc, row-major f64,
+// one workgroup (k x k sizes of the core)
+__global__ void __launch_bounds__(256) k_ts_small(int ta, int tb, int mr, int nc, int kd, const double* __restrict__ A,
+                                                  int lda, const double* __restrict__ B, int ldb,
+                                                  double* __restrict__ C, int ldc) {
+  for (int e = threadIdx.x; e < mr * nc; e += 256) {
+    const int i = e / nc, j = e - i * nc;
+    double s = 0.0;
+    for (int l = 0; l < kd; ++l) {
+      const double a = ta ? A[l * lda + i] : A[i * lda + l];
+      const double b = tb ? B[j * ldb + l] : B[l * ldb + j];
+      s = fma(a, b, s);
+    }
+    C[i * ldc + j] = s;
+  }
+}
+
+int ncu() {
+  static int c = -1;
+  if (c < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      c = 256;
+  }
+  return c;
+}
+
+// 16-B loads: A 16-B aligned, lda and n multiples of the vector width (a
+// vector then never straddles the end of a row)
+template <typename T>
+bool vec_ok(const T* A, int64_t lda, int64_t n) {
+  const int64_t vw = 16 / (int64_t)sizeof(T);
+  return ((uintptr_t)A % 16) == 0 && lda % vw == 0 && n % vw == 0;
+}
+
+template <typename T, int KT>
+int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
+  constexpr int LDS = az_lds<T, KT>();
+  const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
+  const int64_t g = nrb < 2 * (int64_t)ncu() ? nrb : 2 * (int64_t)ncu();
+  if (vec_ok(A, lda, n)) {
+    SL_LDS_ATTR((k_ts_az<T, KT, true>), LDS);
+    k_ts_az<T, KT, true><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy);
+  } else {
+    SL_LDS_ATTR((k_ts_az<T, KT, false>), LDS);
+    k_ts_az<T, KT, false><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy);
+  }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+// row groups of the A^T Q product: ~2 workgroups per CU over all slices
+template <typename T>
+void atq_geometry(int64_t m, int n, int* slices, int* groups, int64_t* rows_per) {
+  constexpr int CS = 8 * AT_V * 16 * (16 / (int)sizeof(T));
+  *slices = (n + CS - 1) / CS;
+  int64_t g = (2 * (int64_t)ncu() + *slices - 1) / *slices;
+  const int64_t maxg = (m + 63) / 64;   // at least 64 rows per group
+  if (g > maxg) g = maxg;
+  if (g < 1) g = 1;
+  int64_t rp = (m + g - 1) / g;
+  rp = (rp + 3) & ~(int64_t)3;
+  *groups = (int)((m + rp - 1) / rp);
+  *rows_per = rp;
+}
+
+template <typename T, int KT>
+int launch_atq(const T* A, int64_t m, int n, int64_t lda, const T* Q, int k, T* slab, int slices, int groups,
+               int64_t rp, hipStream_t s) {
+  const dim3 grid((unsigned)slices, (unsigned)groups);
+  if (vec_ok(A, lda, n)) k_ts_atq<T, KT, true><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+  else k_ts_atq<T, KT, false><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+template <typename T>
+int az_dispatch(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
+  switch ((k + 15) / 16) {
+    case 1: return launch_az<T, 1>(A, m, n, lda, Z, k, Y, ldy, s);
+    case 2: return launch_az<T, 2>(A, m, n, lda, Z, k, Y, ldy, s);
+    case 3: return launch_az<T, 3>(A, m, n, lda, Z, k, Y, ldy, s);
+    default: return launch_az<T, 4>(A, m, n, lda, Z, k, Y, ldy, s);
+  }
+}
+
+template <typename T>
+int atq_dispatch(const T* A, int64_t m, int n, int64_t lda, const T* Q, int k, T* slab, int slices, int groups,
+                 int64_t rp, hipStream_t s) {
+  switch ((k + 15) / 16) {
+    case 1: return launch_atq<T, 1>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+    case 2: return launch_atq<T, 2>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+    case 3: return launch_atq<T, 3>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+    default: return launch_atq<T, 4>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+  }
+}
+
+int gram_grid(int64_t rows) {
+  const int64_t g = (rows + 255) / 256;
+  const int64_t cap = 2 * (int64_t)ncu();
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+// Y (m x k, row stride ldy) = A (m x n, lda) Z (n x k, row-major); dt SL_F32 / SL_F64, 1 <= k <= 64
+SL_API int sl_ts_az(const void* A, int64_t m, int64_t n, int64_t lda, const void* Z, int k, void* Y, int64_t ldy,
+                    int dt, void* stream) {
+  if (m <= 0) return SL_OK;
+  if (k < 1 || k > 64 || n < 1 || n > (int64_t)1 << 30 || lda < n || ldy < k || (dt != SL_F32 && dt != SL_F64)) {
+    sl_set_last_error("ts_az: needs 1 <= k <= 64, lda >= n, ldy >= k, f32 / f64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == SL_F32) return az_dispatch<float>((const float*)A, m, (int)n, lda, (const float*)Z, k, (float*)Y, ldy, s);
+  return az_dispatch<double>((const double*)A, m, (int)n, lda, (const double*)Z, k, (double*)Y, ldy, s);
+}
+
+// bytes of slab workspace sl_ts_atq needs
+SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt) {
+  int slices = 0, groups = 0;
+  int64_t rp = 0;
+  if (dt == SL_F64) atq_geometry<double>(m, (int)n, &slices, &groups, &rp);
+  else atq_geometry<float>(m, (int)n, &slices, &groups, &rp);
+  return (int64_t)groups * n * k * (dt == SL_F64 ? 8 : 4) + 256;
+}
+
+// W (n x k f64, row stride ldw) = A^T Q, A m x n (lda), Q m x k (row-major, A's dtype)
+SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const void* Q, int k, double* W, int ldw,
+                     void* ws, int dt, void* stream) {
+  if (k < 1 || k > 64 || n < 1 || n > (int64_t)1 << 30 || lda < n || ldw < k || (dt != SL_F32 && dt != SL_F64)) {
+    sl_set_last_error("ts_atq: needs 1 <= k <= 64, lda >= n, ldw >= k, f32 / f64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (m <= 0) return hipMemset2DAsync(W, (size_t)ldw * 8, 0, (size_t)k * 8, (size_t)n, s) == hipSuccess ? SL_OK : SL_ERR_HIP;
+  int slices = 0, groups = 0;
+  int64_t rp = 0;
+  int rc;
+  if (dt == SL_F32) {
+    atq_geometry<float>(m, (int)n, &slices, &groups, &rp);
+    rc = atq_dispatch<float>((const float*)A, m, (int)n, lda, (const float*)Q, k, (float*)ws, slices, groups, rp, s);
+    if (rc != SL_OK) return rc;
+    return sl_slab_reduce_launch_f64((const float*)ws, groups, n * k, k, (int)n, k, W, ldw, s);
+  }
+  atq_geometry<double>(m, (int)n, &slices, &groups, &rp);
+  rc = atq_dispatch<double>((const double*)A, m, (int)n, lda, (const double*)Q, k, (double*)ws, slices, groups, rp, s);
+  if (rc != SL_OK) return rc;
+  return sl_slab_reduce_launch_d2d((const double*)ws, groups, n * k, k, (int)n, k, W, ldw, s);
+}
+
+// out (rows x k2, ldo; out_dt SL_F32 / SL_F64) = X (rows x k f64, ldx) M (k x k2 f64, row-major), k, k2 <= 64
+SL_API int sl_ts_xm64(const double* X, int64_t rows, int k, int64_t ldx, const double* Mm, int k2, void* out,
+                      int64_t ldo, int out_dt, void* stream) {
+  if (rows <= 0) return SL_OK;
+  if (k < 1 || k > 64 || k2 < 1 || k2 > 64 || ldx < k || ldo < k2 || (out_dt != SL_F32 && out_dt != SL_F64)) {
+    sl_set_last_error("ts_xm64: needs 1 <= k, k2 <= 64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t tiles = (rows + 63) / 64;
+  const unsigned g = (unsigned)(tiles < 4 * (int64_t)ncu() ? tiles : 4 * (int64_t)ncu());
+  if (out_dt == SL_F32) k_ts_xm64<float><<<g, 256, 0, s>>>(X, rows, k, ldx, Mm, k2, (float*)out, ldo);
+  else k_ts_xm64<double><<<g, 256, 0, s>>>(X, rows, k, ldx, Mm, k2, (double*)out, ldo);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
+SL_API int64_t sl_ts_gram64_workspace(int64_t rows, int k) { return (int64_t)gram_grid(rows) * k * k * 8 + 256; }
+
+// G (k x k f64, ldg) = X^T X, X rows x k f64 (ldx), k <= 64 (ws: sl_ts_gram64_workspace bytes)
+SL_API int sl_ts_gram64(const double* X, int64_t rows, int k, int64_t ldx, double* G, int ldg, void* ws,
+                        void* stream) {
+  if (k < 1 || k > 64 || ldx < k || ldg < k) {
+    sl_set_last_error("ts_gram64: needs 1 <= k <= 64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (rows <= 0) return hipMemset2DAsync(G, (size_t)ldg * 8, 0, (size_t)k * 8, (size_t)k, s) == hipSuccess ? SL_OK : SL_ERR_HIP;
+  const int g = gram_grid(rows);
+  k_ts_gram64<<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws);
+  SL_LAUNCH_CHECK();
+  return sl_slab_reduce_launch_d2d((const double*)ws, g, (int64_t)k * k, k, k, k, G, ldg, s);
+}
+
+// C (mr x nc, ldc) = op(A) op(B) (row-major f64; ta / tb: transpose), one workgroup
+SL_API int sl_ts_small(int ta, int tb, int mr, int nc, int kd, const double* A, int lda, const double* B, int ldb,
+                       double* C, int ldc, void* stream) {
+  k_ts_small<<<1, 256, 0, (hipStream_t)stream>>>(ta, tb, mr, nc, kd, A, lda, B, ldb, C, ldc);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}

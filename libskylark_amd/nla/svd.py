@@ -302,6 +302,7 @@ def _engine_lib():
         _lib.register("sl_rsvd_gen_create", [i64_, i64_, i64_, i32_, i32_, i32_, i32_, ctypes.POINTER(vp_)])
         _lib.register("sl_rsvd_gen_destroy", [vp_])
         _lib.register("sl_rsvd_gen_bind", [vp_, vp_, vp_])
+        _lib.register("sl_rsvd_gen_native", [vp_], ctypes.c_int)
         _lib.register("sl_rsvd_gen_set_fjlt", [vp_, u64_, u64_, u64_, f64_])
         _lib.register("sl_rsvd_gen_set_dense", [vp_, i32_, u64_, u64_, f64_, f64_, f64_])
         _lib.register("sl_rsvd_gen_set_z", [vp_, vp_, vp_])
@@ -511,6 +512,8 @@ class _GenPlan(_EnginePlan):
         L.call("sl_rsvd_gen_create", m, n, A_loc.stride(0), k, rank, q, dt, ctypes.byref(h))
         self.h = h
         self._fin = weakref.finalize(self, _destroy_gen_plan, h.value)
+        # hand-written products only (f32 / f64 A, k <= 64): no rocBLAS call
+        self.native = bool(L.require().sl_rsvd_gen_native(h))
         self.WG = torch.empty((n + k) * k, dtype=torch.float64, device=self.dev)
         self.status_words = torch.zeros(16, dtype=torch.int32, device=self.dev)
         self.status_dev = self.status_words[:1]

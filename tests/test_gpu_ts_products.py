@@ -1,0 +1,128 @@
+"""Hand-written tall-skinny products of the general-precision randSVD engine
+(rsvd_stream.hip) against fp64 torch references of the same ops:
+Y = A Z and W = A^T Q in A's precision (f32 / f64 matrix cores), the f64
+helpers X M, X^T X and the one-workgroup k x k product.  Ragged shapes cover
+partial row blocks / row quads, n not a multiple of the column group, lda > n
+and an lda that rules out 16-B vector loads (scalar path)."""
+import ctypes as C
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
+F32, F64 = 0, 1   # SL_F32 / SL_F64 (sl_common.hpp SlDtype)
+
+
+@pytest.fixture(scope="module")
+def L():
+    from libskylark_amd.ops import _lib
+    _lib.require()
+    _lib.register("sl_ts_az", [vp, i64, i64, i64, vp, i32, vp, i64, i32, vp])
+    _lib.register("sl_ts_atq_workspace", [i64, i64, i32, i32], C.c_int64)
+    _lib.register("sl_ts_atq", [vp, i64, i64, i64, vp, i32, vp, i32, vp, i32, vp])
+    _lib.register("sl_ts_xm64", [vp, i64, i32, i64, vp, i32, vp, i64, i32, vp])
+    _lib.register("sl_ts_gram64_workspace", [i64, i32], C.c_int64)
+    _lib.register("sl_ts_gram64", [vp, i64, i32, i64, vp, i32, vp, vp])
+    _lib.register("sl_ts_small", [i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, i32, vp])
+    return _lib
+
+
+def _st():
+    return vp(torch.cuda.current_stream().cuda_stream)
+
+
+SHAPES = [(100_003, 1000, 40, 0), (4_097, 1000, 40, 8), (777, 37, 20, 0), (129, 16, 1, 0), (2_500, 530, 64, 3),
+          (20_000, 5000, 40, 0), (64, 2049, 33, 0)]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("m,n,k,pad", SHAPES)
+def test_az_and_atq(L, dt, m, n, k, pad):
+    if dt == torch.float32 and n == 5000 and m > 10_000:
+        m = 5_000
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(m + n + k)
+    lda = n + pad
+    Afull = torch.randn(m, lda, device=dev, dtype=dt, generator=g)
+    A = Afull[:, :n]
+    Z = torch.randn(n, k, device=dev, dtype=dt, generator=g)
+    Y = torch.full((m, k), float("nan"), device=dev, dtype=dt)
+    code = F32 if dt == torch.float32 else F64
+    L.call("sl_ts_az", vp(Afull.data_ptr()), m, n, lda, vp(Z.data_ptr()), k, vp(Y.data_ptr()), k, code, _st())
+    Q = torch.randn(m, k, device=dev, dtype=dt, generator=g)
+    ws = torch.zeros(int(L.require().sl_ts_atq_workspace(m, n, k, code)), dtype=torch.uint8, device=dev)
+    W = torch.full((n, k), float("nan"), device=dev, dtype=torch.float64)
+    L.call("sl_ts_atq", vp(Afull.data_ptr()), m, n, lda, vp(Q.data_ptr()), k, vp(W.data_ptr()), k,
+           vp(ws.data_ptr()), code, _st())
+    torch.cuda.synchronize()
+    Ad = A.double()
+    eps = 1.2e-7 if dt == torch.float32 else 2.3e-16
+    yref = Ad @ Z.double()
+    ymag = Ad.abs() @ Z.double().abs()
+    assert torch.isfinite(Y).all()
+    # one f32 / f64 rounding per product in a k-ordered chain: |err| <= ~n eps sum|a b|
+    assert ((Y.double() - yref).abs() <= 4 * eps * (n ** 0.5 + 4) * ymag + 1e-300).all(), \
+        float(((Y.double() - yref).abs() / ymag).max())
+    wref = Ad.t() @ Q.double()
+    wmag = Ad.abs().t() @ Q.double().abs()
+    assert torch.isfinite(W).all()
+    assert ((W - wref).abs() <= 4 * eps * (m ** 0.5 + 4) * wmag + 1e-300).all(), \
+        float(((W - wref).abs() / wmag).max())
+
+
+def test_unaligned_lda_scalar_path(L):
+    """lda = n + 1 (odd): 16-B loads are not allowed, the scalar path runs."""
+    dev = torch.device("cuda")
+    m, n, k = 3_001, 301, 24
+    for dt, code in ((torch.float32, F32), (torch.float64, F64)):
+        Afull = torch.randn(m, n + 1, device=dev, dtype=dt)
+        Z = torch.randn(n, k, device=dev, dtype=dt)
+        Y = torch.empty(m, k, device=dev, dtype=dt)
+        L.call("sl_ts_az", vp(Afull.data_ptr()), m, n, n + 1, vp(Z.data_ptr()), k, vp(Y.data_ptr()), k, code, _st())
+        ws = torch.zeros(int(L.require().sl_ts_atq_workspace(m, n, k, code)), dtype=torch.uint8, device=dev)
+        W = torch.empty(n, k, device=dev, dtype=torch.float64)
+        L.call("sl_ts_atq", vp(Afull.data_ptr()), m, n, n + 1, vp(Y.data_ptr()), k, vp(W.data_ptr()), k,
+               vp(ws.data_ptr()), code, _st())
+        torch.cuda.synchronize()
+        Ad = Afull[:, :n].double()
+        yref = Ad @ Z.double()
+        tol = 1e-4 if dt == torch.float32 else 1e-12
+        assert torch.allclose(Y.double(), yref, rtol=tol, atol=tol * yref.abs().max().item())
+        wref = Ad.t() @ Y.double()
+        assert torch.allclose(W, wref, rtol=tol, atol=tol * wref.abs().max().item())
+
+
+@pytest.mark.parametrize("rows,k,k2", [(200_001, 40, 40), (1000, 40, 20), (77, 64, 64), (5, 3, 1)])
+def test_xm64_gram64(L, rows, k, k2):
+    dev = torch.device("cuda")
+    X = torch.randn(rows, k, device=dev, dtype=torch.float64)
+    M = torch.randn(k, k2, device=dev, dtype=torch.float64)
+    for code, dt in ((F64, torch.float64), (F32, torch.float32)):
+        out = torch.empty(rows, k2, device=dev, dtype=dt)
+        L.call("sl_ts_xm64", vp(X.data_ptr()), rows, k, k, vp(M.data_ptr()), k2, vp(out.data_ptr()), k2, code, _st())
+        torch.cuda.synchronize()
+        ref = X @ M
+        tol = 1e-12 if dt == torch.float64 else 1e-6
+        assert torch.allclose(out.double(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+    ws = torch.zeros(int(L.require().sl_ts_gram64_workspace(rows, k)), dtype=torch.uint8, device=dev)
+    G = torch.empty(k, k, device=dev, dtype=torch.float64)
+    L.call("sl_ts_gram64", vp(X.data_ptr()), rows, k, k, vp(G.data_ptr()), k, vp(ws.data_ptr()), _st())
+    torch.cuda.synchronize()
+    ref = X.t() @ X
+    assert torch.allclose(G, ref, rtol=1e-12, atol=1e-12 * ref.abs().max().item())
+    assert torch.equal(G, G.t())
+
+
+def test_small(L):
+    dev = torch.device("cuda")
+    A = torch.randn(40, 40, device=dev, dtype=torch.float64)
+    B = torch.randn(40, 20, device=dev, dtype=torch.float64)
+    for ta in (0, 1):
+        C_ = torch.empty(40, 20, device=dev, dtype=torch.float64)
+        L.call("sl_ts_small", ta, 0, 40, 20, 40, vp(A.data_ptr()), 40, vp(B.data_ptr()), 20, vp(C_.data_ptr()), 20,
+               _st())
+        torch.cuda.synchronize()
+        ref = (A.t() if ta else A) @ B
+        assert torch.allclose(C_, ref, rtol=1e-13, atol=1e-12)
