@@ -1,5 +1,4 @@
-"""One-wave Cholesky inverse (sl_wave_la.hpp) variants: LDS-broadcast vs
-readlane-broadcast multipliers, us per call (200 back-to-back launches, so the
+"""One-wave Cholesky inverse (sl_wave_la.hpp), us per call (200 back-to-back launches, so the
 ~1.5 us launch boundary is included) and the max error of R^-T G R^-1 - I."""
 import ctypes as C
 import json
@@ -13,7 +12,7 @@ from libskylark_amd.ops import _lib  # noqa: E402
 
 vp = C.c_void_p
 _lib.require()
-_lib.register("sl_chol_inv_wave_v", [vp, C.c_int, C.c_int, vp, vp, C.c_int, vp])
+_lib.register("sl_chol_inv_wave", [vp, C.c_int, C.c_int, vp, vp, vp])
 dev = torch.device("cuda:0")
 for k in (40, 48, 32, 64):
     g = torch.Generator().manual_seed(1)
@@ -22,8 +21,8 @@ for k in (40, 48, 32, 64):
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     R = torch.empty(k, k, dtype=torch.float64, device=dev)
     s = vp(torch.cuda.current_stream().cuda_stream)
-    for v in (0, 1):
-        f = lambda: _lib.call("sl_chol_inv_wave_v", _lib.ptr(G), k, k, _lib.ptr(R), _lib.ptr(st), v, s)  # noqa: E731
+    for v in (0,):
+        f = lambda: _lib.call("sl_chol_inv_wave", _lib.ptr(G), k, k, _lib.ptr(R), _lib.ptr(st), s)  # noqa: E731
         for _ in range(5):
             f()
         torch.cuda.synchronize()
@@ -34,5 +33,5 @@ for k in (40, 48, 32, 64):
         e1.record()
         torch.cuda.synchronize()
         err = float((R.t() @ G @ R - torch.eye(k, dtype=torch.float64, device=dev)).abs().max())
-        print(json.dumps({"k": k, "variant": ["lds", "readlane"][v], "us": round(e0.elapsed_time(e1) * 1e3 / 200, 2),
+        print(json.dumps({"k": k, "us": round(e0.elapsed_time(e1) * 1e3 / 200, 2),
                           "orth_err": err, "status": int(st.item())}))

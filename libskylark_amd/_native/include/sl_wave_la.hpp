@@ -163,59 +163,6 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
   }
 }
 
-// The same elimination with the multipliers broadcast by readlane into
-// scalar registers instead of an LDS round trip: lane i holds multiplier
-// f_i = A[j] / d_j of row i (its own register), every lane reads f_{j+1..K-1}
-// with v_readlane (wave-uniform SGPR operands of the FMAs).  No LDS, no wave
-// barrier on the pivot chain, so the update of column j + 1 -- the next pivot
-// -- can be scheduled ahead of the rest of step j.
-template <int K>
-__device__ __forceinline__ void wave_chol_inv_rl(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
-                                                 int* st) {
-  static_assert(K % 2 == 0 && K <= 64, "K");
-  const int c = threadIdx.x & 63;
-  double A[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) A[i] = (i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0);
-  const double thr = 1e-13 * wave_max(c < k ? fabs(G[c * ldg + c]) : 0.0);
-  double* rsh = fsh + 128;   // d_j (lane 0 writes them; d_j^{-1/2} formed after the loop)
-  int bad = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const double d = lane_d(A[j], j);
-    const bool ok = (d > thr && d == d) || j >= k;
-    bad |= !ok;
-    const double r = ok ? rcp64(d) : 0.0;
-    if (c == 0) rsh[j] = ok ? d : 0.0;
-    if (j + 1 < K) {
-      const double aj = A[j];
-      const double fm = aj * r;             // this lane's multiplier (row c, valid for c > j)
-      const bool piv = c == j;
-#pragma unroll
-      for (int i = j + 1; i < K; ++i) {
-        const double fi = lane_d(fm, i);    // f_i, wave-uniform
-        A[i] = piv ? -fi : fma(-fi, aj, A[i]);
-      }
-    }
-    if (c == j) A[j] = 1.0;
-  }
-  if (bad && c == 0) atomicOr(st, 1);
-  wave_lds_sync();
-  if (c < K) {
-    const double dj = rsh[c];
-    rsh[c] = dj > 0.0 ? rsq64(dj) : 0.0;
-  }
-  wave_lds_sync();
-  if (c < k) {
-#pragma unroll
-    for (int i = 0; i < K; i += 2) {
-      const double2 rr = *(const double2*)(rsh + i);
-      if (i < k) X[c * ldx + i] = i >= c ? A[i] * rr.x : 0.0;
-      if (i + 1 < k) X[c * ldx + i + 1] = i + 1 >= c ? A[i + 1] * rr.y : 0.0;
-    }
-  }
-}
-
 // ------------------------------------------------- tridiagonalisation
 // T = Q^T C Q, Q = H_0 H_1 ... H_{K-3}, H_j = I - 2 v_j v_j^T, by ONE wave:
 // lane i keeps row i of the trailing matrix in registers.  Step j: ||x||

@@ -167,27 +167,23 @@ SL_API int sl_small_matmul(const double* A, const double* B, double* C, int m, i
 // kernel the randSVD pass boundaries run, as a standalone launch.  Status
 // bit 1: a pivot at or below 1e-13 max G_ii was dropped.
 namespace {
-template <int K, bool RL>
+template <int K>
 __global__ void __launch_bounds__(64) k_chol_inv_wave(const double* __restrict__ G, int k, int ldg,
                                                       double* __restrict__ X, int* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) double fsh[192];
   __shared__ int st;
   if (threadIdx.x == 0) st = 0;
   __syncthreads();
-  if constexpr (RL) slw::wave_chol_inv_rl<K>(G, ldg, X, k, k, fsh, &st);
-  else slw::wave_chol_inv<K>(G, ldg, X, k, k, fsh, &st);
+  slw::wave_chol_inv<K>(G, ldg, X, k, k, fsh, &st);
   __syncthreads();
   if (threadIdx.x == 0 && status && st) atomicOr(status, st);
 }
 }  // namespace
 
-// variant 0: multipliers through LDS; 1: through readlane (scalar operands)
-SL_API int sl_chol_inv_wave_v(const double* G, int k, int ldg, double* X, int* status, int variant, void* stream) {
+SL_API int sl_chol_inv_wave(const double* G, int k, int ldg, double* X, int* status, void* stream) {
   if (k < 1 || k > 64 || ldg < k) { sl_set_last_error("chol_inv_wave: 1 <= k <= 64"); return SL_ERR_DIMENSION; }
   hipStream_t s = (hipStream_t)stream;
-#define SL_CIW(KK)                                                                        \
-  if (variant == 1) k_chol_inv_wave<KK, true><<<1, 64, 0, s>>>(G, k, ldg, X, status);     \
-  else k_chol_inv_wave<KK, false><<<1, 64, 0, s>>>(G, k, ldg, X, status);
+#define SL_CIW(KK) k_chol_inv_wave<KK><<<1, 64, 0, s>>>(G, k, ldg, X, status);
   if (k <= 16) { SL_CIW(16) }
   else if (k <= 32) { SL_CIW(32) }
   else if (k <= 40) { SL_CIW(40) }
@@ -196,8 +192,4 @@ SL_API int sl_chol_inv_wave_v(const double* G, int k, int ldg, double* X, int* s
 #undef SL_CIW
   SL_LAUNCH_CHECK();
   return SL_OK;
-}
-
-SL_API int sl_chol_inv_wave(const double* G, int k, int ldg, double* X, int* status, void* stream) {
-  return sl_chol_inv_wave_v(G, k, ldg, X, status, 0, stream);
 }
