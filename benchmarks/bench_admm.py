@@ -32,6 +32,8 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--loss", default="hinge")
     ap.add_argument("--cache", type=int, default=1, help="cache the feature blocks (HBM is 288 GB)")
+    ap.add_argument("--cache-dtype", default="f32", choices=["f32", "bf16"],
+                    help="storage of the cached feature blocks (bf16: half the bytes per iteration)")
     a = ap.parse_args(argv)
     import libskylark_amd as sk
     from libskylark_amd import ml
@@ -47,6 +49,7 @@ def main(argv=None):
     solver = ml.BlockADMMSolver(a.loss, "l2", 1e-3, a.features, kernel=k, NumFeaturePartitions=a.partitions,
                                 context=sk.Context(5))
     solver.set_cache_transform(bool(a.cache))
+    solver.set_cache_dtype(torch.bfloat16 if a.cache_dtype == "bf16" else None)
     times = []
 
     def log(msg):
@@ -79,7 +82,8 @@ def main(argv=None):
                           "train_accuracy_sample": round(acc, 4),
                           "config": {"rows_per_gpu": m, "dim": d, "features": a.features,
                                      "partitions": a.partitions, "loss": a.loss, "iters": a.iters,
-                                     "cache_transforms": bool(a.cache)}}))
+                                     "cache_transforms": bool(a.cache),
+                                     "cache_dtype": a.cache_dtype}}))
     return 0
 
 

@@ -1,4 +1,5 @@
-"""One-wave Cholesky inverse (sl_wave_la.hpp), us per call (200 back-to-back launches, so the
+"""Cholesky inverse (sl_wave_la.hpp): variant 0 = one wave, 1 = the rows of
+the elimination over 4 waves (default), us per call (200 back-to-back launches, so the
 ~1.5 us launch boundary is included) and the max error of R^-T G R^-1 - I."""
 import ctypes as C
 import json
@@ -13,6 +14,7 @@ from libskylark_amd.ops import _lib  # noqa: E402
 vp = C.c_void_p
 _lib.require()
 _lib.register("sl_chol_inv_wave", [vp, C.c_int, C.c_int, vp, vp, vp])
+_lib.require().sl_chol_inv_set_variant.argtypes = [C.c_int]
 dev = torch.device("cuda:0")
 for k in (40, 48, 32, 64):
     g = torch.Generator().manual_seed(1)
@@ -21,7 +23,8 @@ for k in (40, 48, 32, 64):
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     R = torch.empty(k, k, dtype=torch.float64, device=dev)
     s = vp(torch.cuda.current_stream().cuda_stream)
-    for v in (0,):
+    for v in (0, 1):
+        _lib.require().sl_chol_inv_set_variant(v)
         f = lambda: _lib.call("sl_chol_inv_wave", _lib.ptr(G), k, k, _lib.ptr(R), _lib.ptr(st), s)  # noqa: E731
         for _ in range(5):
             f()
@@ -33,5 +36,5 @@ for k in (40, 48, 32, 64):
         e1.record()
         torch.cuda.synchronize()
         err = float((R.t() @ G @ R - torch.eye(k, dtype=torch.float64, device=dev)).abs().max())
-        print(json.dumps({"k": k, "us": round(e0.elapsed_time(e1) * 1e3 / 200, 2),
+        print(json.dumps({"k": k, "variant": ["one_wave", "rows_over_4_waves"][v], "us": round(e0.elapsed_time(e1) * 1e3 / 200, 2),
                           "orth_err": err, "status": int(st.item())}))

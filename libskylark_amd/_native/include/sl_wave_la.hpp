@@ -17,6 +17,8 @@
 //   wave_chol_inv<K>   X = R^{-1} of G = R^T R: in-place LDL^T elimination of
 //                      [G | I] with lane c holding column c of whichever half
 //                      is live (T column c until pivot c, then L^{-1} column c)
+//   wg_chol_inv<K,NW>  the same X with the elimination's rows split over NW
+//                      waves (one barrier per step)
 //   wave_tridiag<K>    Householder tridiagonalisation T = Q^T C Q (lane = row)
 //   sym_top_eig<K>     top-nt eigenvalues of T by multisection on a
 //                      division-free Sturm count, eigenvectors of T by the
@@ -159,6 +161,75 @@ __device__ __forceinline__ void wave_chol_inv(const double* G, int ldg, double* 
       const double2 rr = *(const double2*)(rsh + i);
       if (i < k) X[c * ldx + i] = i >= c ? A[i] * rr.x : 0.0;
       if (i + 1 < k) X[c * ldx + i + 1] = i + 1 >= c ? A[i + 1] * rr.y : 0.0;
+    }
+  }
+}
+
+// The same X = R^{-1} with the rows of the elimination split over NW waves of
+// the workgroup (every thread of the workgroup calls it; waves >= NW only
+// meet the barriers).  Row i of [G | I] lives in wave i % NW, register
+// i / NW, lane = column (the live-half trick as above: lane c holds column
+// c of G's part until pivot c, then column c of L^{-1}).  Step j: the owner
+// of row j publishes it to LDS (double-buffered, ONE workgroup barrier per
+// step), every wave reads the pivot d_j and its lane's entry of row j, and
+// updates its own rows below j with f_i = M[i][j] / d_j taken by readlane
+// from lane j of the same row -- K / NW FMAs per lane and step instead of
+// K - j on one wave (the one-wave form is issue-bound: time ~ K^2,
+// profiles/r5/chol_wave_variants.md).  fsh >= 192 doubles of LDS.
+template <int K, int NW>
+__device__ __forceinline__ void wg_chol_inv(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
+                                            int* st) {
+  static_assert(K % NW == 0 && K <= 64, "K");
+  constexpr int R = K / NW;
+  const int tid = threadIdx.x, c = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool act = w < NW;
+  double* rowbuf = fsh;        // [2][64]
+  double* dsh = fsh + 128;     // d_i (0: dropped)
+  double M[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int i = q * NW + w;
+    M[q] = !act ? 0.0 : ((i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0));
+  }
+  const double thr = 1e-13 * wave_max(c < k ? fabs(G[c * ldg + c]) : 0.0);
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int wj = j % NW, qj = j / NW;
+    double* rb = rowbuf + (j & 1) * 64;
+    if (w == wj) rb[c] = M[qj];
+    __syncthreads();
+    const double rj = rb[c];
+    const double d = rb[j];
+    const bool ok = (d > thr && d == d) || j >= k;
+    bad |= !ok;
+    const double r = ok ? rcp64(d) : 0.0;
+    if (w == wj && c == 0) dsh[j] = ok ? d : 0.0;
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int i = q * NW + w;
+        if (i > j) {
+          const double fi = lane_d(M[q], j) * r;
+          M[q] = c == j ? -fi : fma(-fi, rj, M[q]);
+        } else {
+          M[q] = c == j ? (i == j ? 1.0 : 0.0) : M[q];
+        }
+      }
+    }
+  }
+  if (bad && tid == 0) atomicOr(st, 1);
+  __syncthreads();
+  if (act && c < k) {
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = q * NW + w;
+      if (i < k) {
+        const double di = dsh[i];
+        const double rs = di > 0.0 ? rsq64(di) : 0.0;
+        X[c * ldx + i] = i >= c ? M[q] * rs : 0.0;
+      }
     }
   }
 }

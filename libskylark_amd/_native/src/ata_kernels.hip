@@ -20,6 +20,7 @@
 // workgroups per CU hide the load latency; per-workgroup W partial slabs are
 // summed by the shared slab-reduce kernel.
 #include "sl_common.hpp"
+#include <type_traits>
 
 namespace {
 
@@ -61,11 +62,25 @@ constexpr int log2c() { return V <= 1 ? 0 : 1 + log2c<V / 2>(); }
 // DUAL: the W update uses a GIVEN long block D (W = A^T D) instead of A Y;
 // with STORE_Y the pass still emits A Y (the BlockADMM pair {Z Wbar, Z^T d}).
 // BM rows per iteration: enough bytes in flight per workgroup (BM * n * 4 >= ~64 KB).
-template <int J, int K, int BM, bool STORE_Y, bool DUAL>
+// A element types: f32, or bf16 (a feature cache at half the bytes; the
+// values are exact bf16 widened to f32, every product and sum in f32).  The
+// prefetched rows stay in their storage type and widen at use: converting at
+// load would make the compiler wait for the loads right there.
+template <typename TA> __device__ __forceinline__ float widen(TA v);
+template <> __device__ __forceinline__ float widen<float>(float v) { return v; }
+template <> __device__ __forceinline__ float widen<bf16_t>(bf16_t v) { return bf16_to_f(v); }
+
+// PAIR (bf16 with n, lda even): a thread owns adjacent column pairs
+// (2 tid + 2 NT i, + 1), loaded as one 4-B word and kept packed until use --
+// half the load instructions and prefetch registers of one column per lane.
+// acc_y: Yout += A Y (callers summing several blocks' products).
+template <typename TA, int J, int K, int BM, bool STORE_Y, bool DUAL, bool PAIR>
 __global__ void __launch_bounds__(NT, 2)
-k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Y,
+k_ata_pass(const TA* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Y,
            float* __restrict__ Wslab, float* __restrict__ Yout, int64_t ldyo,
-           const float* __restrict__ Dm, int64_t ldd_r, int64_t ldd_c) {
+           const float* __restrict__ Dm, int64_t ldd_r, int64_t ldd_c, int acc_y) {
+  static_assert(!PAIR || (sizeof(TA) == 2 && J % 2 == 0), "pairs: bf16, even J");
+  auto colof = [&](int j) { return PAIR ? 2 * (threadIdx.x + NT * (j >> 1)) + (j & 1) : (int)threadIdx.x + NT * j; };
   constexpr int V = BM * K;
   static_assert(V <= 64 && (V & (V - 1)) == 0, "BM * K must be a power of two <= 64");
   constexpr int SH = 6 - log2c<V>();
@@ -76,7 +91,7 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
   float yv[J][K], wacc[J][K];
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int c = tid + NT * j;
+    const int c = colof(j);
 #pragma unroll
     for (int kk = 0; kk < K; ++kk) {
       yv[j][kk] = (c < n && NEED_DOT) ? Y[(int64_t)c * K + kk] : 0.f;
@@ -89,17 +104,32 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
   // i + 1 stay in flight across block i's two barriers); only for J <= 4,
   // wider rows would spill the second set
   constexpr bool PF = J <= 4;
-  float an[PF ? BM : 1][J];
-  auto load_block = [&](int64_t blk_, float (&dst)[BM][J]) {
+  // raw storage words: one element, or (PAIR) two packed bf16
+  using RW = typename std::conditional<PAIR, uint32_t, TA>::type;
+  constexpr int JW = PAIR ? J / 2 : J;
+  RW an[PF ? BM : 1][JW];
+  auto load_block = [&](int64_t blk_, RW (&dst)[BM][JW]) {
     const int64_t r0_ = blk_ * BM;
 #pragma unroll
     for (int b = 0; b < BM; ++b) {
       const int64_t r = r0_ + b < m ? r0_ + b : m - 1;
-      const float* row = A + r * lda;
+      const TA* row = A + r * lda;
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int c = tid + NT * j;
-        dst[b][j] = (c < n && r0_ + b < m) ? row[c] : 0.f;
+      for (int jw = 0; jw < JW; ++jw) {
+        const int c = colof(PAIR ? 2 * jw : jw);
+        if constexpr (PAIR) dst[b][jw] = (c < n && r0_ + b < m) ? *(const uint32_t*)(row + c) : 0u;
+        else dst[b][jw] = (c < n && r0_ + b < m) ? row[c] : (TA)0;
+      }
+    }
+  };
+  auto widen_row = [&](const RW (&src)[JW], float (&dst)[J]) {
+#pragma unroll
+    for (int jw = 0; jw < JW; ++jw) {
+      if constexpr (PAIR) {
+        dst[2 * jw] = __uint_as_float(src[jw] << 16);
+        dst[2 * jw + 1] = __uint_as_float(src[jw] & 0xffff0000u);
+      } else {
+        dst[jw] = widen<TA>(src[jw]);
       }
     }
   };
@@ -110,12 +140,13 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
     float a[BM][J];
     if constexpr (PF) {
 #pragma unroll
-      for (int b = 0; b < BM; ++b)
-#pragma unroll
-        for (int j = 0; j < J; ++j) a[b][j] = an[b][j];
+      for (int b = 0; b < BM; ++b) widen_row(an[b], a[b]);
       if (blk + gridDim.x < nblk) load_block(blk + gridDim.x, an);
     } else {
-      load_block(blk, a);
+      RW raw[BM][JW];
+      load_block(blk, raw);
+#pragma unroll
+      for (int b = 0; b < BM; ++b) widen_row(raw[b], a[b]);
     }
     if (!NEED_DOT) {
       // W = A^T D: the D rows of this block straight from memory (tiny, cached)
@@ -143,7 +174,10 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
 #pragma unroll
         for (int v = 0; v < NT / 64; ++v) s += red[v][tid];
         const int b = tid / K, kk = tid - (tid / K) * K;
-        if (STORE_Y && r0 + b < m) Yout[(r0 + b) * ldyo + kk] = s;
+        if (STORE_Y && r0 + b < m) {
+          float* yo = Yout + (r0 + b) * ldyo + kk;
+          *yo = acc_y ? *yo + s : s;
+        }
         yrow[tid] = DUAL ? (r0 + b < m ? Dm[(r0 + b) * ldd_r + kk * ldd_c] : 0.f) : s;
       }
       __syncthreads();
@@ -165,7 +199,7 @@ k_ata_pass(const float* __restrict__ A, int64_t m, int n, int64_t lda, const flo
   float* ws = Wslab + (int64_t)blockIdx.x * n * K;
 #pragma unroll
   for (int j = 0; j < J; ++j) {
-    const int c = tid + NT * j;
+    const int c = colof(j);
     if (c < n) {
 #pragma unroll
       for (int kk = 0; kk < K; ++kk) ws[(int64_t)c * K + kk] = wacc[j][kk];
@@ -190,11 +224,10 @@ int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int
 
 SL_API int64_t sl_ata_workspace(int64_t n, int k) { return (int64_t)ata_grid() * n * k * 4 + 256; }
 
-// W (n x k, row-major) = A^T (A Y) -- or A^T D when D is non-null (D(r, c) at
-// D[r * ldd_r + c * ldd_c]); Yout (m x k, ld ldyo) = A Y when non-null.
-SL_API int sl_ata_pass2(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
-                        float* Yout, int64_t ldyo, const float* D, int64_t ldd_r, int64_t ldd_c, void* ws,
-                        void* stream) {
+namespace {
+template <typename TA>
+int ata_run(const TA* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W, float* Yout,
+            int64_t ldyo, const float* D, int64_t ldd_r, int64_t ldd_c, void* ws, void* stream, int acc_y = 0) {
   if (m <= 0 || n <= 0) return SL_OK;
   const int64_t Jn = (n + NT - 1) / NT;
   // register budget (no spills): J <= 8 any k, J <= 16 k <= 2, J <= 24 k == 1
@@ -208,8 +241,11 @@ SL_API int sl_ata_pass2(const float* A, int64_t m, int64_t n, int64_t lda, const
   const int bm = J <= 4 ? 16 : (J <= 8 ? 8 : 4);
   const int g = (int)std::min<int64_t>((int64_t)ata_grid(), (m + bm - 1) / bm);
   float* slab = (float*)ws;
-#define SL_ATA_GO(JJ, KK, SY, DU) \
-  k_ata_pass<JJ, KK, (JJ <= 4 ? 16 : (JJ <= 8 ? 8 : 4)), SY, DU><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo, D, ldd_r, ldd_c);
+  constexpr bool BF = sizeof(TA) == 2;
+  const bool pair = BF && n % 2 == 0 && lda % 2 == 0 && ((uintptr_t)A & 3) == 0;
+#define SL_ATA_GO(JJ, KK, SY, DU)                                                                                    \
+  if (pair) k_ata_pass<TA, JJ, KK, (JJ <= 4 ? 16 : (JJ <= 8 ? 8 : 4)), SY, DU, BF><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo, D, ldd_r, ldd_c, acc_y); \
+  else k_ata_pass<TA, JJ, KK, (JJ <= 4 ? 16 : (JJ <= 8 ? 8 : 4)), SY, DU, false><<<g, NT, 0, s>>>(A, m, (int)n, lda, Y, slab, Yout, ldyo, D, ldd_r, ldd_c, acc_y);
 #define SL_ATA(JJ, KK)                                                      \
   if (D) {                                                                  \
     if (Yout) { SL_ATA_GO(JJ, KK, true, true) } else { SL_ATA_GO(JJ, KK, false, true) } \
@@ -227,6 +263,26 @@ SL_API int sl_ata_pass2(const float* A, int64_t m, int64_t n, int64_t lda, const
 #undef SL_ATA_GO
   SL_LAUNCH_CHECK();
   return sl_slab_reduce_launch(slab, g, n * k, k, (int)n, k, W, k, s);
+}
+}  // namespace
+
+// W (n x k, row-major) = A^T (A Y) -- or A^T D when D is non-null (D(r, c) at
+// D[r * ldd_r + c * ldd_c]); Yout (m x k, ld ldyo) = A Y when non-null.
+SL_API int sl_ata_pass2(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
+                        float* Yout, int64_t ldyo, const float* D, int64_t ldd_r, int64_t ldd_c, void* ws,
+                        void* stream) {
+  return ata_run<float>(A, m, n, lda, Y, k, W, Yout, ldyo, D, ldd_r, ldd_c, ws, stream);
+}
+
+// the same with A stored as bf16 (SL_BF16) or f32 (SL_F32), selected by a_dt
+// acc_y = 1: Yout += A Y (several blocks' products summed in place).
+SL_API int sl_ata_pass3(const void* A, int a_dt, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,
+                        float* Yout, int64_t ldyo, const float* D, int64_t ldd_r, int64_t ldd_c, void* ws,
+                        void* stream, int acc_y) {
+  if (a_dt == SL_BF16)
+    return ata_run<bf16_t>((const bf16_t*)A, m, n, lda, Y, k, W, Yout, ldyo, D, ldd_r, ldd_c, ws, stream, acc_y);
+  if (a_dt != SL_F32) { sl_set_last_error("ata_pass: A must be f32 or bf16"); return SL_ERR_UNSUPPORTED; }
+  return ata_run<float>((const float*)A, m, n, lda, Y, k, W, Yout, ldyo, D, ldd_r, ldd_c, ws, stream, acc_y);
 }
 
 SL_API int sl_ata_pass(const float* A, int64_t m, int64_t n, int64_t lda, const float* Y, int k, float* W,

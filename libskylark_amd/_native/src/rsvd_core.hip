@@ -355,7 +355,7 @@ __device__ __forceinline__ void final_core(double* b0, double* b1, double* b2, d
 //   1. workgroup b loads its BR rows of W (one batch of loads) into LDS
 //   2. the packed upper partial Gram of its rows -> global, then a ticket
 //   3. the last arriving workgroup sums the partials (16-B loads, a batch in
-//      flight), runs the k x k algebra (INTER: Cholesky inverse on one wave;
+//      flight), runs the k x k algebra (INTER: Cholesky inverse with its rows over 4 waves;
 //      FINAL: final_core) and bumps the generation word (agent-scope release)
 //   4. every workgroup (the others spin on the generation word meanwhile; the
 //      <= BMAX workgroups are co-resident on the 256 CUs) forms its rows of
@@ -445,7 +445,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       }
     }
     __syncthreads();
-    if (tid < 64) slw::wave_chol_inv<K>(b0, ld, b2, ld, k, cls.fsh, &st_sh);
+    slw::wg_chol_inv<K, 4>(b0, ld, b2, ld, k, cls.fsh, &st_sh);   // rows over 4 waves
     __syncthreads();
     for (int e = tid; e < k * k; e += NT) {
       const int i = e / k, c = e - i * k;
@@ -555,7 +555,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     __syncthreads();
     if (tid == 0) a.sync[0] = 0u;   // ready for the next launch
     if (!FINAL) {
-      if (tid < 64) slw::wave_chol_inv<K>(b0, ld, b2, ld, k, cls.fsh, &st_sh);
+      slw::wg_chol_inv<K, 4>(b0, ld, b2, ld, k, cls.fsh, &st_sh);   // rows over 4 waves
       __syncthreads();
       for (int e = tid; e < k * k; e += NT) {
         const int i = e / k, c = e - i * k;

@@ -87,6 +87,11 @@ class BlockADMMSolver:
         self.lam = float(lam)
         self.rho, self.maxiter, self.tol = 1.0, 1000, 0.1
         self.cache_transforms = False
+        # storage type of the cached feature blocks: None = the compute dtype;
+        # torch.bfloat16 halves the bytes every iteration streams (the one-pass
+        # kernels widen to f32; the block's (Z^T Z + I)^-1 is formed from the
+        # same rounded Z, so the solver is exact for the features it holds)
+        self.cache_dtype = None
         self.num_threads = 1
         self.one_pass = True      # fused Z-pair passes where the kernel applies
         if feature_maps is not None:
@@ -123,6 +128,14 @@ class BlockADMMSolver:
 
     def set_cache_transform(self, flag: bool):
         self.cache_transforms = bool(flag)
+
+    def set_cache_dtype(self, dtype):
+        """Storage type of the cached feature blocks (``torch.bfloat16``: half
+        the HBM traffic per iteration on the GPU one-pass path; ``None``: the
+        compute dtype).  An extension knob, not in the reference."""
+        if dtype not in (None, torch.float32, torch.float64, torch.bfloat16):
+            raise ValueError("cache dtype: None, float32, float64 or bfloat16")
+        self.cache_dtype = dtype
 
     def set_nthreads(self, n):
         self.num_threads = int(n)
@@ -212,18 +225,24 @@ class BlockADMMSolver:
                     Z = zcache[j]
                 else:
                     Z = self._Z(j, X, dt)  # ni x sj
+                    if (self.cache_transforms and self.cache_dtype is not None and fused
+                            and self.cache_dtype != Z.dtype):
+                        Z = Z.to(self.cache_dtype)   # the one-pass kernels read it as stored
                     if self.cache_transforms:
                         zcache[j] = Z
+                if Z.dtype != dt and not (fused and normal_eq.native_ok(Z, kp)):
+                    Z = Z.to(dt)   # stored narrower than the compute dtype, no native pass: widen
                 if cache[j] is None:
-                    C = (Z.t() @ Z).to(torch.float64)
+                    Zc = Z.to(dt) if Z.dtype != dt else Z
+                    C = (Zc.t() @ Zc).to(torch.float64)
+                    del Zc
                     C.diagonal().add_(1.0)
                     cache[j] = torch.cholesky_inverse(torch.linalg.cholesky(C)).to(dt)
                 Wb = Wbar[st:st + sj]
                 one_pass = fused and normal_eq.native_ok(Z, kp)
                 if one_pass:
                     # pass 1: {Z Wbar_j, Z^T dsum^T} from one read of Z
-                    ztd, zw = normal_eq.dual(Z, Dp.t(), padded("wb", j, Wb))
-                    zw_sum += zw
+                    ztd, _ = normal_eq.dual(Z, Dp.t(), padded("wb", j, Wb), y_out=zw_sum)   # zw_sum += Z Wb
                     ztd = ztd[:, :k]
                 else:
                     wbar_out += (Z @ Wb).t()
@@ -233,8 +252,7 @@ class BlockADMMSolver:
                 Wi[st:st + sj] = Wi_j
                 if one_pass:
                     # pass 2: {o = Z Wi_j, Z^T o} from one read of Z
-                    zto, zo = normal_eq.ata(Z, padded("wi", j, Wi_j), want_y=True)
-                    zo_sum += zo
+                    zto, _ = normal_eq.ata(Z, padded("wi", j, Wi_j), want_y=True, y_out=zo_sum)   # zo_sum += o
                     ZtObar[st:st + sj] = zto[:, :k]
                 else:
                     o = (Z @ Wi_j).t()  # k x ni

@@ -1,4 +1,4 @@
-"""One-pass ``A^T (A Y)`` for tall f32 operators (``ata_kernels.hip``).
+"""One-pass ``A^T (A Y)`` for tall f32 (or bf16-stored) operators (``ata_kernels.hip``).
 
 Used by the Krylov solvers (LSQR, Chebyshev) so that an iteration reads A
 once instead of twice (reference loops ``algorithms/Krylov/LSQR.hpp:113-248``,
@@ -17,12 +17,16 @@ vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_ata_pass", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, vp])
 _lib.register("sl_ata_workspace", [i64, i32], C.c_int64)
 _lib.register("sl_ata_pass2", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp])
+_lib.register("sl_ata_pass3", [vp, i32, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp, i32])
+_DT = {torch.float32: 0, torch.bfloat16: 2}   # SlDtype codes of the stored A
 
 _WS: dict = {}
 
 
 def native_ok(A: torch.Tensor, k: int) -> bool:
-    if not (isinstance(A, torch.Tensor) and A.is_cuda and A.dtype == torch.float32 and A.dim() == 2
+    """f32 A, or a bf16-stored A (e.g. BlockADMM's bf16 feature cache: the
+    kernel widens each element to f32, products and sums stay f32)."""
+    if not (isinstance(A, torch.Tensor) and A.is_cuda and A.dtype in _DT and A.dim() == 2
             and A.layout == torch.strided and A.stride(1) == 1 and _lib.available()):
         return False
     n = A.shape[1]
@@ -43,10 +47,11 @@ def _ws(A, n, k):
     return ws
 
 
-def dual(A: torch.Tensor, D: torch.Tensor, X: torch.Tensor | None = None):
+def dual(A: torch.Tensor, D: torch.Tensor, X: torch.Tensor | None = None, y_out: torch.Tensor | None = None):
     """``(A^T D, A X or None)`` from ONE read of A (m x n): D is m x k (any
     strides, e.g. the transpose of a k x m block), X n x k.  The BlockADMM pair
-    ``{Z Wbar, Z^T d}`` (``ml/BlockADMM.hpp:400-498``)."""
+    ``{Z Wbar, Z^T d}`` (``ml/BlockADMM.hpp:400-498``).  ``y_out`` (m x k f32,
+    contiguous): A X is ADDED into it (and returned) instead of a new tensor."""
     k = D.shape[1]
     if X is not None and X.shape[1] != k:
         raise ValueError("dual: X and D need the same number of columns")
@@ -54,25 +59,37 @@ def dual(A: torch.Tensor, D: torch.Tensor, X: torch.Tensor | None = None):
         m, n = A.shape
         W = torch.empty(n, k, dtype=torch.float32, device=A.device)
         Xc = X.to(torch.float32).contiguous() if X is not None else None
-        Yo = torch.empty(m, k, dtype=torch.float32, device=A.device) if X is not None else None
-        _lib.call("sl_ata_pass2", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Xc) if Xc is not None else None, k,
-                  _lib.ptr(W), _lib.ptr(Yo) if Yo is not None else None, k, _lib.ptr(D), D.stride(0), D.stride(1),
-                  _lib.ptr(_ws(A, n, k)), vp(_lib.stream_of(A)))
+        acc = y_out is not None and X is not None
+        Yo = y_out if acc else (torch.empty(m, k, dtype=torch.float32, device=A.device) if X is not None else None)
+        _lib.call("sl_ata_pass3", _lib.ptr(A), _DT[A.dtype], m, n, A.stride(0),
+                  _lib.ptr(Xc) if Xc is not None else None, k, _lib.ptr(W), _lib.ptr(Yo) if Yo is not None else None,
+                  k, _lib.ptr(D), D.stride(0), D.stride(1), _lib.ptr(_ws(A, n, k)), vp(_lib.stream_of(A)), int(acc))
         return W, Yo
-    return A.t() @ D.to(A.dtype), (A @ X.to(A.dtype) if X is not None else None)
+    Af = A.float() if A.dtype == torch.bfloat16 else A
+    AX = Af @ X.to(Af.dtype) if X is not None else None
+    if AX is not None and y_out is not None:
+        AX = y_out.add_(AX)
+    return Af.t() @ D.to(Af.dtype), AX
 
 
-def ata(A: torch.Tensor, Y: torch.Tensor, want_y: bool = False):
+def ata(A: torch.Tensor, Y: torch.Tensor, want_y: bool = False, y_out: torch.Tensor | None = None):
     """``(A^T (A Y), A Y or None)`` for the local block A (m x n) and Y (n x k).
-    Partial over a row shard: the caller all-reduces the first result."""
+    Partial over a row shard: the caller all-reduces the first result.
+    ``y_out`` (m x k f32, contiguous, with want_y): A Y is ADDED into it."""
     k = Y.shape[1]
     if native_ok(A, k):
         m, n = A.shape
         Yc = Y.to(torch.float32).contiguous()
         W = torch.empty(n, k, dtype=torch.float32, device=A.device)
-        Yo = torch.empty(m, k, dtype=torch.float32, device=A.device) if want_y else None
-        _lib.call("sl_ata_pass", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Yc), k, _lib.ptr(W),
-                  _lib.ptr(Yo) if Yo is not None else None, k, _lib.ptr(_ws(A, n, k)), vp(_lib.stream_of(A)))
+        acc = y_out is not None and want_y
+        Yo = y_out if acc else (torch.empty(m, k, dtype=torch.float32, device=A.device) if want_y else None)
+        _lib.call("sl_ata_pass3", _lib.ptr(A), _DT[A.dtype], m, n, A.stride(0), _lib.ptr(Yc), k, _lib.ptr(W),
+                  _lib.ptr(Yo) if Yo is not None else None, k, None, 0, 0, _lib.ptr(_ws(A, n, k)),
+                  vp(_lib.stream_of(A)), int(acc))
         return W, Yo
-    AY = A @ Y.to(A.dtype)
-    return A.t() @ AY, (AY if want_y else None)
+    Af = A.float() if A.dtype == torch.bfloat16 else A
+    AY = Af @ Y.to(Af.dtype)
+    WW = Af.t() @ AY
+    if want_y and y_out is not None:
+        AY = y_out.add_(AY)
+    return WW, (AY if want_y else None)

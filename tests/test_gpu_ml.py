@@ -96,3 +96,49 @@ def test_fused_gram_epilogue(dev, kind):
     K = k.gram(X.float().to(dev), Y=Y.float().to(dev)).double().cpu()
     err = float((K - ref).abs().max() / ref.abs().max())
     assert err < 1e-4, err
+
+
+def test_ata_pass_bf16_storage(dev):
+    """One-pass A^T D / A X / A^T (A Y) with A stored as bf16 (the BlockADMM
+    feature cache): exact bf16 values widened to f32, f32 products and sums --
+    compared with fp64 of the same (rounded) operand."""
+    from libskylark_amd.ops import normal_eq
+    g = torch.Generator(device=dev).manual_seed(7)
+    m, n = 50_001, 1024
+    A = torch.randn(m, n, device=dev, generator=g).to(torch.bfloat16)
+    Ad = A.double()
+    D = torch.randn(m, 4, device=dev, generator=g)
+    X = torch.randn(n, 4, device=dev, generator=g)
+    assert normal_eq.native_ok(A, 4)
+    W, Yo = normal_eq.dual(A, D, X)
+    torch.testing.assert_close(W.double(), Ad.t() @ D.double(), rtol=2e-4, atol=2e-3)
+    torch.testing.assert_close(Yo.double(), Ad @ X.double(), rtol=2e-4, atol=2e-3)
+    W2, Y2 = normal_eq.ata(A, X, want_y=True)
+    ay = Ad @ X.double()
+    torch.testing.assert_close(Y2.double(), ay, rtol=2e-4, atol=2e-3)
+    ref = Ad.t() @ Y2.double()   # W from the f32 y the kernel formed
+    torch.testing.assert_close(W2.double(), ref, rtol=2e-4, atol=2e-2)
+
+
+def test_admm_bf16_feature_cache_matches_f32(dev):
+    """BlockADMM with the feature blocks cached as bf16: same classification
+    accuracy and a training objective within 1% of the f32 cache."""
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(20000, 16, generator=g, dtype=torch.float64)
+    lab = ((X[:, 0] + 0.5 * X[:, 1]) > 0).to(torch.float64) * 2 - 1
+    k = ml.Gaussian(16, 3.0)
+    res = {}
+    for cd in (None, torch.bfloat16):
+        s = ml.BlockADMMSolver("hinge", "l2", 0.01, 1024, kernel=k, NumFeaturePartitions=2, context=sk.Context(3))
+        s.set_cache_transform(True)
+        s.set_cache_dtype(cd)
+        s.set_maxiter(15)
+        model = s.train(X.to(dev).float(), lab.to(dev), regression=False, log=None)
+        pred, _ = model.predict(X.to(dev).float())
+        res[cd] = (float((pred.cpu() == lab).double().mean()), s.history[-1]["objective"] if s.history else None,
+                   model.coef.double().cpu())
+    (a32, o32, w32), (a16, o16, w16) = res[None], res[torch.bfloat16]
+    assert a32 > 0.95 and abs(a16 - a32) < 0.005
+    if o32 is not None:
+        assert abs(o16 - o32) <= 0.01 * abs(o32)
+    assert float((w16 - w32).norm() / w32.norm()) < 0.02
