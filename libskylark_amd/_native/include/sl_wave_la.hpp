@@ -28,6 +28,18 @@
 #include "sl_common.hpp"
 
 
+// prefetch distances (steps) of the LDS-broadcast operands of the Sturm
+// count and the twisted factorisation (A/B knobs of benchmarks/probe: 4 to
+// 16 steps, and readlane broadcasts instead of LDS, all within 1% -- the
+// phases are f64 VALU issue-bound on one wave per eigenvalue group,
+// profiles/r5/eig_stamps_v2.jsonl)
+#ifndef SLW_STURM_PF
+#define SLW_STURM_PF 4
+#endif
+#ifndef SLW_TWIST_PF
+#define SLW_TWIST_PF 4
+#endif
+
 namespace slw {
 
 // ------------------------------------------------------------ wave helpers
@@ -360,7 +372,7 @@ __device__ __forceinline__ void sturm_counts(const double2* de2, const double (&
   // (d_i, e_{i-1}^2) broadcast from LDS, fetched PF steps ahead into a
   // register ring (a full register copy of T per lane -- 4 K VGPRs, the same
   // values in every lane -- spilled the K >= 48 solvers)
-  constexpr int PF = 4;
+  constexpr int PF = SLW_STURM_PF < K ? SLW_STURM_PF : K;
   double2 ring[PF];
 #pragma unroll
   for (int q = 0; q < PF; ++q)
@@ -416,7 +428,7 @@ __device__ __forceinline__ double rcp64n(double d) {   // estimate + one Newton 
 template <int K>
 __device__ __forceinline__ void twisted_vec(const double* dd, const double* ee, double l, double* zdm, double* zdp,
                                             double* zrd, int* rt_out) {
-  constexpr int PF = 4;
+  constexpr int PF = SLW_TWIST_PF < K - 1 ? SLW_TWIST_PF : K - 1;
   const double pivmin = 1e-290;
   double dm = dd[K - 1] - l;
   if (fabs(dm) < pivmin) dm = -pivmin;
