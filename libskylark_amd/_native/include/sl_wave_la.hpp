@@ -593,8 +593,11 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     ee[tid] *= itn;
   }
   __syncthreads();
-  if (tid < nv) {
-    const int t = tid;
+  // vector t on wave t % 4, lane t / 4: the per-vector chains (f64 VALU
+  // issue-bound) spread over the four SIMDs instead of one wave
+  const int tv = (tid >> 6) < 4 ? (tid & 63) * 4 + (tid >> 6) : nv;
+  if (tv < nv) {
+    const int t = tv;
     const double l = lam[t];
     const double gap = fmin(t > 0 ? lam[t - 1] - l : 1e300, t + 1 < nt ? l - lam[t + 1] : 1e300);
     if (!(gap > 1e-13)) atomicOr(st, 1);       // numerically repeated (~ bisection accuracy): the caller falls back
@@ -657,9 +660,10 @@ __device__ __forceinline__ void sym_top_eig(double* dd, double* ee, const double
     }
   }
   __syncthreads();
-  // ---- residual check of every vector against T (scaled), lane = vector
-  if (tid < nv) {
-    const int t = tid;
+  // ---- residual check of every vector against T (scaled), one lane per
+  //      vector, spread over the SIMDs as above
+  if (tv < nv) {
+    const int t = tv;
     const double l = lam[t];
     double r2 = 0.0;
 #pragma unroll
