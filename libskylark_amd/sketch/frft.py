@@ -26,8 +26,15 @@ import torch
 from ..base import distributions as D
 from ..ops import fut as _fut
 from ..ops import hash_sketch as _hs
-from .base import COLUMNWISE, SketchTransform, register
+from .base import COLUMNWISE, ROWWISE, SketchTransform, register
 from .rft import EPI_COS, _FeatureMap
+from ..ops import _lib as _L
+import ctypes as _C
+
+_vp, _i32, _i64, _f32 = _C.c_void_p, _C.c_int, _C.c_int64, _C.c_float
+_L.register("sl_fastfood_tables", [_i32, _vp, _vp])
+_L.register("sl_fastfood_apply", [_vp, _i32, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _f32, _i32, _i32, _i32, _i32,
+                                  _i32, _i32, _vp, _vp, _i64, _vp])
 
 
 class _Fastfood(_FeatureMap):
@@ -71,9 +78,65 @@ class _Fastfood(_FeatureMap):
         eye = torch.eye(self._N, dtype=torch.float64, device=device)
         return self._features_pre(eye, COLUMNWISE).to(dtype)
 
+    # ---- fused native path (fastfood.hip): one workgroup per (row, block)
+    FUSED_MIN_N, FUSED_MAX_N = 1024, 16384
+
+    def _fused_ok(self, A, dim) -> bool:
+        N = self._N
+        return (A.is_cuda and dim == ROWWISE and A.dtype in (torch.float32, torch.bfloat16)
+                and A.layout == torch.strided and A.dim() == 2 and A.stride(1) == 1
+                and self.FUSED_MIN_N <= N <= self.FUSED_MAX_N and (N & (N - 1)) == 0
+                and A.shape[0] < 2 ** 31 and self.numblks <= 65535)
+
+    def _fused_operands(self, dev):
+        """Device copies of the block draws and the per-N twiddle tables (cached)."""
+        key = str(dev)
+        cache = self.__dict__.setdefault("_ffdev", {})
+        if key not in cache:
+            import ctypes as C
+            from ..ops import _lib
+            M = self._N // 2
+            tabn = 2 * (M + (M + 1) + self._N)   # W_M, W_N (k <= M), W_4N complex (sl_fastfood_tables_size)
+            tab = torch.empty(tabn, dtype=torch.float32, device=dev)
+            _lib.call("sl_fastfood_tables", self._N, _lib.ptr(tab), C.c_void_p(_lib.stream_of(tab)))
+            cache[key] = {
+                "B": self.B.to(dev, torch.float32).contiguous(),
+                "P": self.perms.to(dev, torch.int32).contiguous(),
+                "G": self.G.to(dev, torch.float32).contiguous(),
+                "Sm": self._Sm.to(dev, torch.float32).contiguous(),
+                "sh": self.shifts.to(dev, torch.float32).contiguous(),
+                "tab": tab,
+            }
+        return cache[key]
+
+    def _fused_apply(self, A, out_rows, epi: bool):
+        """Rowwise features (m x (i1 - i0)) of A (m x N) in one launch; epi:
+        the cosine epilogue fused (outscale cos(. + shift))."""
+        import ctypes as C
+        from ..ops import _lib
+        i0, i1 = out_rows if out_rows is not None else (0, self._S)
+        m, N = A.shape
+        ops = self._fused_operands(A.device)
+        out = torch.empty(m, i1 - i0, dtype=torch.float32, device=A.device)
+        if m == 0 or i1 <= i0:
+            return out
+        b0, b1 = i0 // N, (i1 + N - 1) // N
+        _lib.call("sl_fastfood_apply", _lib.ptr(A), _lib.dtype_code(A.dtype), m, N, A.stride(0),
+                  _lib.ptr(ops["B"]), _lib.ptr(ops["P"]), _lib.ptr(ops["G"]), _lib.ptr(ops["Sm"]),
+                  _lib.ptr(ops["sh"]), float(self.outscale), 1 if epi else 0, self._S, b0, b1, i0, i1,
+                  _lib.ptr(ops["tab"]), _lib.ptr(out), out.stride(0), C.c_void_p(_lib.stream_of(A)))
+        return out
+
+    def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
+        if in_offset == 0 and A.shape[dim] == self._N and self._N > self.DENSE_MAX_N and self._fused_ok(A, dim):
+            return self._fused_apply(A, out_rows, epi=True)   # transform + cosine in one launch
+        return super()._apply_dense(A, dim, in_offset, out_rows)
+
     def _features_pre(self, A, dim, in_offset=0, out_rows=None):
         if in_offset != 0 or A.shape[dim] != self._N:
             raise ValueError("Fastfood needs the whole input dimension on one device")
+        if self._fused_ok(A, dim):
+            return self._fused_apply(A, out_rows, epi=False)
         if A.is_cuda and A.dtype in (torch.float32, torch.bfloat16) and A.layout == torch.strided and self._N >= 2:
             return self._features_pre_gpu(A, dim, out_rows)
         X = A if dim == COLUMNWISE else A.t()
