@@ -51,7 +51,9 @@ def main():
     out = {}
     for p in a.paths.split(","):
         if p == "fused":
-            fn = lambda: T.apply(X, dim=ROWWISE)  # noqa: E731
+            fn = lambda: T._fused_apply(X, None, epi=True)  # noqa: E731
+        elif p == "apply":
+            fn = lambda: T.apply(X, dim=ROWWISE)  # noqa: E731   (what the library picks)
         elif p == "pipeline":
             fn = lambda: T._post(T._features_pre_gpu(X, ROWWISE), ROWWISE)  # noqa: E731
         else:

@@ -127,8 +127,14 @@ class _Fastfood(_FeatureMap):
                   _lib.ptr(ops["tab"]), _lib.ptr(out), out.stride(0), C.c_void_p(_lib.stream_of(A)))
         return out
 
+    # the fused kernel replaces the dense-W GEMM from this N up (measured,
+    # profiles/r5/fastfood_v1.jsonl: N = 4096, S = 8192: 5.0 vs 11.7 ms;
+    # N = 2048: 5.96 vs 6.29 ms; at N = 1024 the GEMM wins, 3.4 vs 8.3 ms)
+    FUSED_PREFER_N = 2048
+
     def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
-        if in_offset == 0 and A.shape[dim] == self._N and self._N > self.DENSE_MAX_N and self._fused_ok(A, dim):
+        if (in_offset == 0 and A.shape[dim] == self._N and self._N >= self.FUSED_PREFER_N
+                and self._fused_ok(A, dim)):
             return self._fused_apply(A, out_rows, epi=True)   # transform + cosine in one launch
         return super()._apply_dense(A, dim, in_offset, out_rows)
 
