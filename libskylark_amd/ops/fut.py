@@ -201,7 +201,14 @@ def _fs_lib():
         _lib.register("sl_fs_stage1", [vp, i32, i64, i64, i32, vp, i32, i32, u64, i32, vp, vp])
         _lib.register("sl_fs_stage2", [vp, i32, i32, i32, vp, vp, vp, vp, vp])
         _lib.register("sl_fs_post", [vp, i32, i64, vp, i32, vp, vp, C.c_double, vp, i64, vp])
+        _lib.register("sl_fs_set_stage2_variant", [i32], None)
     return _lib
+
+
+def set_fourstep_stage2(variant: int) -> None:
+    """Stage-2 kernel of the four-step DCT: 1 (default) the MFMA kernel,
+    0 the VALU kernel (A/B, tests)."""
+    _fs_lib().require().sl_fs_set_stage2_variant(int(variant))
 
 
 FS_N2_MAX = 512
@@ -291,7 +298,7 @@ def fjlt_fourstep(A: torch.Tensor, d: torch.Tensor, samples: torch.Tensor, scale
         plan = _FourStepPlan(N, samples, A.device)
         _FS_PLANS[key] = plan
     st = C.c_void_p(L.stream_of(A))
-    dd = d.to(device=A.device, dtype=torch.float64).contiguous()
+    dd = d.to(device=A.device, dtype=torch.float32).contiguous()
     Y = torch.empty(plan.N2 * plan.N1 * m * 2, dtype=torch.float32, device=A.device)
     L.call("sl_fs_stage1", L.ptr(A), L.dtype_code(A.dtype), A.stride(0), N, m, L.ptr(dd), plan.N1, plan.N2,
            C.c_uint64(plan.rplan), plan.npass, L.ptr(Y), st)
@@ -323,7 +330,7 @@ def fjlt_sampled(A: torch.Tensor, dim: int, d: torch.Tensor, samples: torch.Tens
         from . import _lib
         _lib.require()
         st = C.c_void_p(_lib.stream_of(A))
-        dd = d.to(device=A.device, dtype=torch.float64).contiguous()
+        dd = d.to(device=A.device, dtype=torch.float64).contiguous()   # sl_fjlt_pre takes f64 D
         # always transform along contiguous rows of an m x N buffer (dim 0 input
         # is transposed by the pre-pass itself)
         v = torch.empty(m, N, dtype=torch.float32, device=A.device)

@@ -66,3 +66,42 @@ def test_fourstep_dense_groups_and_wide_batch():
     out = fut.fjlt_fourstep(torch.from_numpy(A).float().cuda(), torch.from_numpy(d), torch.from_numpy(samples), 1.0)
     ref = _ref(A.astype(np.float32).astype(np.float64), d, samples, 1.0)
     assert np.abs(out.double().cpu().numpy() - ref).max() <= 2e-5 * np.abs(ref).max()
+
+
+
+@pytest.mark.parametrize("dtype,N,m", [(torch.bfloat16, 100000, 100), (torch.float32, 13440, 1000),
+                                       (torch.float32, 8192, 36)])
+def test_fourstep_shapes_and_dtypes(dtype, N, m):
+    """Partial last column chunk (m = 100, 36), bf16 input on the long
+    length, a wide batch (1000 columns: 63 chunks per row of Y)."""
+    g = np.random.default_rng(N + m)
+    A = torch.from_numpy(g.standard_normal((N, m))).to(dtype)
+    d = g.choice([-1.0, 1.0], N)
+    samples = g.integers(0, N, 400)
+    out = fut.fjlt_fourstep(A.cuda(), torch.from_numpy(d), torch.from_numpy(samples), 1.0).double().cpu()
+    ref = _ref(A.double().numpy(), d, samples, 1.0)
+    assert np.abs(out.numpy() - ref).max() <= 2e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("N,m,S", [(100000, 100, 400), (13440, 70, 3000), (8192, 300, 3000), (65536, 16, 50)])
+def test_fourstep_stage2_mfma_matches_valu_and_dct(N, m, S):
+    """Stage 2 on the matrix cores (k_fs_stage2m) against the VALU kernel and
+    the fp64 DCT: N1 not a multiple of 4 (13440: N1 = 14, masked tail rows),
+    groups of more than 32 frequencies (several passes), partial 64-column
+    waves, a sparse sample set (groups of 0-2 frequencies)."""
+    g = np.random.default_rng(N + m)
+    A = torch.from_numpy(g.standard_normal((N, m))).float()
+    d = g.choice([-1.0, 1.0], N)
+    samples = g.integers(0, N, S)
+    outs = []
+    try:
+        for v in (1, 0):
+            fut.set_fourstep_stage2(v)
+            outs.append(fut.fjlt_fourstep(A.cuda(), torch.from_numpy(d), torch.from_numpy(samples), 1.0).double().cpu())
+    finally:
+        fut.set_fourstep_stage2(1)
+    ref = _ref(A.double().numpy(), d, samples, 1.0)
+    scale = np.abs(ref).max()
+    for o in outs:
+        assert np.abs(o.numpy() - ref).max() <= 2e-5 * scale
+    assert (outs[0] - outs[1]).abs().max().item() <= 2e-6 * scale
