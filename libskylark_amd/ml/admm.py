@@ -48,6 +48,22 @@ from ..parallel.distmatrix import DistMatrix
 from ..sketch import ROWWISE
 from .model import HilbertModel
 
+_LOSS_CODE = {"squared": 0, "lad": 1, "hinge": 2, "logistic": 3}
+_ADMM_REG = [False]
+
+
+def _admm_lib():
+    """admm_kernels.hip: the fused per-iteration pre / post passes."""
+    import ctypes as C
+    from ..ops import _lib
+    if not _ADMM_REG[0]:
+        _ADMM_REG[0] = True
+        vp, i32, i64, f64 = C.c_void_p, C.c_int, C.c_int64, C.c_double
+        _lib.register("sl_admm_partials", [i64], C.c_int64)
+        _lib.register("sl_admm_pre", [i32, i32, i64, vp, vp, vp, vp, f64, f64, vp, vp, vp])
+        _lib.register("sl_admm_post", [i32, i32, i32, i64, vp, vp, vp, vp, f64, vp, vp, vp, vp, vp])
+    return _lib
+
 
 def _partition(D: int, P: int):
     """Block sizes floor(nf/np) recursively (reference constructor ``:143-152``)."""
@@ -72,6 +88,20 @@ def num_targets(Y: torch.Tensor, comm: Comm) -> int:
     return 1 if int(mn.item()) == -1 else int(mx.item()) + 1
 
 
+def _gram(Z: torch.Tensor, dt) -> torch.Tensor:
+    """Z^T Z in f64 for the block's normal-equation inverse.  A bf16 feature
+    cache on the GPU takes a bf16 GEMM with f32 output (exact products, f32
+    sums: what the f32 GEMM of the widened values computes, ~9x faster);
+    otherwise the GEMM in the compute dtype."""
+    if Z.dtype == torch.bfloat16 and Z.is_cuda:
+        try:
+            return torch.mm(Z.t(), Z, out_dtype=torch.float32).to(torch.float64)
+        except (RuntimeError, TypeError):
+            pass
+    Zc = Z.to(dt) if Z.dtype != dt else Z
+    return (Zc.t() @ Zc).to(torch.float64)
+
+
 class BlockADMMSolver:
     """``BlockADMMSolver(loss, regularizer, lam, NumFeatures, kernel=None,
     tag="regular"|"fast"|"quasi", NumFeaturePartitions=1, context=None)`` or
@@ -94,6 +124,7 @@ class BlockADMMSolver:
         self.cache_dtype = None
         self.num_threads = 1
         self.one_pass = True      # fused Z-pair passes where the kernel applies
+        self.native_prox = True   # fused native prox / consensus passes (admm_kernels.hip) on that path
         if feature_maps is not None:
             self.maps = list(feature_maps)
             self.sizes = [S.get_S() for S in self.maps]
@@ -194,6 +225,21 @@ class BlockADMMSolver:
         Dp = torch.zeros(kp, ni, dtype=dt, device=dev) if fused else None
         # padded (s_j x kp) operands of the one-pass kernels, allocated once
         pads = {}
+        # the per-iteration element-wise work on the k x n_i block as two
+        # native passes (admm_kernels.hip) on the fused path: the block sums
+        # arrive in zw_sum / zo_sum (n_i x kp), which the post pass zeroes
+        lcode = _LOSS_CODE.get(getattr(self.loss, "name", ""))
+        native = (fused and self.native_prox and lcode is not None
+                  and ((Yt.dim() == 2 and Yt.shape[0] == k) or (Yt.dim() == 1 and k == 1))
+                  and (lcode != 3 or k >= 2))
+        if native:
+            L = _admm_lib()
+            L.require()
+            Yt = (Yt[None, :] if Yt.dim() == 1 else Yt).to(dt).contiguous()
+            zw_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
+            zo_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
+            partial = torch.zeros(int(L.require().sl_admm_partials(ni)), dtype=torch.float64, device=dev)
+            st_ = L.stream_of(O)
 
         def padded(tag, j, Wj):
             if Wj.shape[1] == kp:
@@ -207,18 +253,24 @@ class BlockADMMSolver:
         pending = []
         for it in range(1, self.maxiter + 1):
             mu_ij -= Wbar
-            Obar -= nu
-            O = self.loss.proxoperator(Obar, 1.0 / self.rho, Yt).to(dt)
+            if native:
+                # Obar -= nu; O = prox(Obar); Dp[:k] = del_o + (P + 1) nu
+                L.call("sl_admm_pre", lcode, k, ni, L.ptr(Obar), L.ptr(nu), L.ptr(del_o), L.ptr(Yt),
+                       1.0 / self.rho, P + 1.0, L.ptr(O), L.ptr(Dp), st_)
+                dsum = Dp[:k]
+            else:
+                Obar -= nu
+                O = self.loss.proxoperator(Obar, 1.0 / self.rho, Yt).to(dt)
+                sum_o = torch.zeros(k, ni, dtype=dt, device=dev)
+                wbar_out = torch.zeros(k, ni, dtype=dt, device=dev)
+                dsum = del_o + (P + 1.0) * nu  # k x ni
+                if fused:
+                    Dp[:k] = dsum
+                    # the one-pass kernels' n_i x kp outputs summed as they come
+                    # (contiguous adds); folded into the k x n_i sums once
+                    zw_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
+                    zo_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
             W = self.regularizer.proxoperator(Wbar - mu, self.lam / self.rho).to(dt)
-            sum_o = torch.zeros(k, ni, dtype=dt, device=dev)
-            wbar_out = torch.zeros(k, ni, dtype=dt, device=dev)
-            dsum = del_o + (P + 1.0) * nu  # k x ni
-            if fused:
-                Dp[:k] = dsum
-                # the one-pass kernels' n_i x kp outputs summed as they come
-                # (contiguous adds); folded into the k x n_i sums once
-                zw_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
-                zo_sum = torch.zeros(ni, kp, dtype=dt, device=dev)
             for j in range(P):
                 st, sj = self.starts[j], self.sizes[j]
                 if self.cache_transforms and zcache[j] is not None:
@@ -233,9 +285,7 @@ class BlockADMMSolver:
                 if Z.dtype != dt and not (fused and normal_eq.native_ok(Z, kp)):
                     Z = Z.to(dt)   # stored narrower than the compute dtype, no native pass: widen
                 if cache[j] is None:
-                    Zc = Z.to(dt) if Z.dtype != dt else Z
-                    C = (Zc.t() @ Zc).to(torch.float64)
-                    del Zc
+                    C = _gram(Z, dt)
                     C.diagonal().add_(1.0)
                     cache[j] = torch.cholesky_inverse(torch.linalg.cholesky(C)).to(dt)
                 Wb = Wbar[st:st + sj]
@@ -244,6 +294,9 @@ class BlockADMMSolver:
                     # pass 1: {Z Wbar_j, Z^T dsum^T} from one read of Z
                     ztd, _ = normal_eq.dual(Z, Dp.t(), padded("wb", j, Wb), y_out=zw_sum)   # zw_sum += Z Wb
                     ztd = ztd[:, :k]
+                elif native:
+                    zw_sum[:, :k] += Z @ Wb
+                    ztd = Z.t() @ dsum.t()
                 else:
                     wbar_out += (Z @ Wb).t()
                     ztd = Z.t() @ dsum.t()
@@ -257,15 +310,24 @@ class BlockADMMSolver:
                 else:
                     o = (Z @ Wi_j).t()  # k x ni
                     ZtObar[st:st + sj] = Z.t() @ o.t()
-                    sum_o += o
+                    if native:
+                        zo_sum[:, :k] += o.t()
+                    else:
+                        sum_o += o
                 mu_ij[st:st + sj] += Wi_j
-            if fused:
-                wbar_out += zw_sum[:, :k].t()
-                sum_o += zo_sum[:, :k].t()
-            sum_o = O - sum_o
-            del_o = sum_o.clone()
+            if native:
+                # del_o = O - sum o; Obar = O - del_o / (P + 1); nu += O - Obar; the loss partials
+                L.call("sl_admm_post", lcode, k, kp, ni, L.ptr(O), L.ptr(zo_sum), L.ptr(zw_sum), L.ptr(Yt),
+                       P + 1.0, L.ptr(Obar), L.ptr(nu), L.ptr(del_o), L.ptr(partial), st_)
+                stats = [partial.sum()]
+            else:
+                if fused:
+                    wbar_out += zw_sum[:, :k].t()
+                    sum_o += zo_sum[:, :k].t()
+                sum_o = O - sum_o
+                del_o = sum_o.clone()
+                stats = [self.loss.evaluate_t(wbar_out, Yt).to(torch.float64)]
             # ---- one all-reduce: [Wi | loss | validation stats]; all on the device
-            stats = [self.loss.evaluate_t(wbar_out, Yt).to(torch.float64)]
             if Xv is not None:
                 stats += list(self._validate_t(model, Wbar, Xv, Yv, regression))
             else:
@@ -281,8 +343,9 @@ class BlockADMMSolver:
                 # waits on that iteration's event while the GPU runs this one
                 while len(pending) > 1:
                     self._log(self._record(*pending.pop(0), Xv is not None, regression), comm, log)
-            Obar = O - sum_o / (P + 1.0)
-            nu = nu + O - Obar
+            if not native:
+                Obar = O - sum_o / (P + 1.0)
+                nu = nu + O - Obar
             Wbar = (Wsum + W) / (rank_count + 1.0)
             mu = mu + W - Wbar
             model.coef = Wbar
