@@ -160,7 +160,9 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
   // (lgkmcnt(0) before it), which is all the DMA into that stage needs.
   // Same-box A/B (profiles/r4/gemm_nt_prio_ab.jsonl): 1160 / 1138 TF square
   // 8192^3 / LSRN panel against 1143 / 1119 for the plain loop; the deferral
-  // alone (no priority) measured 1013 / 1115.
+  // alone (no priority) measured 1013 / 1115.  A ring of four K-half slots
+  // (each half's DMA three phases ahead, one counted wait + barrier per K
+  // half) lost: 938 / 1052 vs 1159 / 1158 TF (profiles/r5/gemm_nt_ring_ab.jsonl).
   bf16x8 a0[8], b0[4], a1[8], b1[4];
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
