@@ -102,6 +102,13 @@ class DenseOp(Operator):
             # ~6 TB/s against ~2.4 TB/s for the library GEMV on tall f32 A
             from ..ops import normal_eq
             return normal_eq.ata(self.A, X, want_y=True)[1]
+        from ..ops import normal_eq
+        if (X.dim() == 1 or X.shape[1] == 1) and normal_eq.gemv_ok(self.A, 1) and self.A.shape[1] > 6144:
+            # rows too wide for the one-pass kernel (a stored kernel Gram), one
+            # right-hand side: the streaming GEMV, 6.25 vs 5.46 TB/s for the
+            # library at n = 1e5 (k = 2, 4: the library is as fast or faster,
+            # profiles/r5/gemv_v1.jsonl)
+            return normal_eq.gemv(self.A, X)
         return self.A @ X.to(self.A.dtype)
 
     def rmatmul(self, Y):

@@ -18,6 +18,7 @@ _lib.register("sl_ata_pass", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, vp])
 _lib.register("sl_ata_workspace", [i64, i32], C.c_int64)
 _lib.register("sl_ata_pass2", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp])
 _lib.register("sl_ata_pass3", [vp, i32, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp, i32])
+_lib.register("sl_gemv_rows_f32", [vp, i64, i64, i64, vp, i32, vp, i64, vp])
 _DT = {torch.float32: 0, torch.bfloat16: 2}   # SlDtype codes of the stored A
 
 _WS: dict = {}
@@ -93,3 +94,25 @@ def ata(A: torch.Tensor, Y: torch.Tensor, want_y: bool = False, y_out: torch.Ten
     if want_y and y_out is not None:
         AY = y_out.add_(AY)
     return WW, (AY if want_y else None)
+
+
+def gemv_ok(A: torch.Tensor, k: int) -> bool:
+    """Can ``A @ X`` (X with k columns) take the wide-row streaming GEMV
+    (gemv_kernels.hip)?  f32 on the GPU, k in {1, 2, 4}, rows 16-B aligned."""
+    return (isinstance(A, torch.Tensor) and A.is_cuda and A.dtype == torch.float32 and A.dim() == 2
+            and A.stride(1) == 1 and A.shape[1] % 4 == 0 and A.stride(0) % 4 == 0 and A.data_ptr() % 16 == 0
+            and k in (1, 2, 4) and _lib.available())
+
+
+def gemv(A: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """``A @ X`` (A m x n f32, X n or n x k) by one streaming read of A:
+    every workgroup owns 4 rows, X is re-read from L2 (transposed to k x n)."""
+    vec = X.dim() == 1
+    X2 = X[:, None] if vec else X
+    m, n = A.shape
+    k = X2.shape[1]
+    Xt = X2.to(torch.float32).t().contiguous()
+    Y = torch.empty(m, k, dtype=torch.float32, device=A.device)
+    _lib.call("sl_gemv_rows_f32", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Xt), k, _lib.ptr(Y), Y.stride(0),
+              C.c_void_p(_lib.stream_of(A)))
+    return Y[:, 0] if vec else Y
