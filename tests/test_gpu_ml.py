@@ -171,3 +171,31 @@ def test_admm_native_prox_matches_torch(dev, loss, regression, ncls):
     assert float((w1 - w0).norm() / w0.norm()) < 2e-3, float((w1 - w0).norm() / w0.norm())
     for a, b in zip(h1, h0):
         assert abs(a - b) <= 2e-3 * abs(b) + 1e-6, (h1, h0)
+
+
+def test_feature_map_precond_f32_apply_matches_f64(dev):
+    """The GPU preconditioner application (f32 one-pass dual kernel + streaming
+    GEMV) against the f64 Woodbury product, and CG converging to the same
+    kernel-ridge solution with it."""
+    from libskylark_amd.algorithms import krylov as K
+    from libskylark_amd.algorithms.operators import DenseOp
+    from libskylark_amd.ml import krr
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(6000, 10, generator=g).to(dev)
+    B = torch.randn(6000, 1, generator=g).to(dev)
+    ker = ml.kernel("gaussian", 10, 3.0)
+    P = krr.FeatureMapPrecond(ker, 0.1, X, 256, sk.Context(7))
+    assert P._v32 is not None
+    got = P.apply(B)
+    V = P.V
+    ref = B.double() / P.lam - V @ (V.t() @ B.double())
+    assert float((got.double() - ref).norm() / ref.norm()) < 1e-5
+    Kg = ker.symmetric_gram(X)
+    Kg.diagonal().add_(0.1)
+    p = K.KrylovIterParams(tolerance=1e-6, iter_lim=500, check_every=5)
+    A32, code = K.cg(DenseOp(Kg), B, params=p, M=P)
+    P._v32 = None                       # the f64 application
+    p = K.KrylovIterParams(tolerance=1e-6, iter_lim=500, check_every=5)
+    A64, code64 = K.cg(DenseOp(Kg), B, params=p, M=P)
+    assert code == -1 and code64 == -1
+    assert float((A32 - A64).norm() / A64.norm()) < 1e-4
