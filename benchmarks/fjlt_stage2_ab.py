@@ -26,8 +26,12 @@ def main():
     for v in (1, 0):
         fut.set_fourstep_stage2(v)
         Zs = torch.zeros(plan.nslots * m * 2, device="cuda")
-        f = lambda: L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1),
-                           L.ptr(plan.gslot), L.ptr(Zs), st)
+        if v:
+            f = lambda: L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr_s),
+                               L.ptr(plan.gk1_s), L.ptr(plan.gslot_s), L.ptr(Zs), L.ptr(plan.gord), st)
+        else:
+            f = lambda: L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1),
+                               L.ptr(plan.gslot), L.ptr(Zs), None, st)
         f()
         torch.cuda.synchronize()
         t0 = time.perf_counter()

@@ -289,23 +289,27 @@ __device__ __forceinline__ void fft_tile(float2* buf, const float2* tw, int n, u
 
 // The last Stockham pass (Ns = N2 / R: its butterfly j writes rows k2 = j + r Ns)
 // straight to Y with the W_M^{j1 k2} twiddles -- no LDS write-back, barrier
-// and re-read for the output.
-template <int R>
+// and re-read for the output.  CP = 2: a thread's two adjacent columns as
+// one 16-B store (half the store instructions and address arithmetic).
+template <int R, int CP>
 __device__ __forceinline__ void last_pass_store(const float2* __restrict__ buf, const float2* __restrict__ tw,
                                                 const float2* __restrict__ tm, int N2, float2* __restrict__ Yc,
                                                 int64_t ystride, bool cok) {
-  constexpr int QMAX = (N2_MAX / R * WC + NT1 - 1) / NT1;
-  const int tid = threadIdx.x, col = tid & (WC - 1);
-  const int Ns = N2 / R, nb = Ns * WC;
+  using V = cvec<CP>;
+  constexpr int WCP = WC / CP;
+  constexpr int QMAX = (N2_MAX / R * WCP + NT1 - 1) / NT1;
+  const int tid = threadIdx.x, col = (tid & (WCP - 1)) * CP;
+  const int Ns = N2 / R, nb = Ns * WCP;
 #pragma unroll
   for (int q = 0; q < QMAX; ++q) {
     const int b = tid + NT1 * q;
     if (b < nb) {
-      const int j = b / WC;
-      float2 v[R];
+      const int j = b / WCP;
+      V v[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const float2 x = buf[(j + r * Ns) * WC + col];
+        V x;
+        ldv(buf + (j + r * Ns) * WC + col, x);
         v[r] = r == 0 ? x : cmul(x, tw[r * j]);
       }
       dft<R>(v);
@@ -313,7 +317,7 @@ __device__ __forceinline__ void last_pass_store(const float2* __restrict__ buf, 
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int k2 = j + r * Ns;
-          Yc[(int64_t)k2 * ystride] = cmul(v[r], tm[k2]);
+          stv(Yc + (int64_t)k2 * ystride, cmul(v[r], tm[k2]));
         }
       }
     }
@@ -325,49 +329,75 @@ __device__ __forceinline__ float ld_f(const T* p) {
   if constexpr (sizeof(T) == 2) return bf16_to_f(*(const bf16_t*)p);
   else return (float)*p;
 }
+// two adjacent elements (8-B f32 / 4-B bf16 aligned) as floats
+template <typename T>
+__device__ __forceinline__ void ld_pair(const T* p, float& a, float& b) {
+  if constexpr (sizeof(T) == 2) {
+    const unsigned u = *(const unsigned*)p;
+    a = __uint_as_float(u << 16);
+    b = __uint_as_float(u & 0xffff0000u);
+  } else {
+    const float2 t = *(const float2*)p;
+    a = t.x;
+    b = t.y;
+  }
+}
 
 // The tile's rows loaded straight into the first Stockham pass (Ns = 1: no
 // twiddles): each thread loads the R0 rows j + r N2 / R0 of its butterflies
 // (D applied, every load of the tile in flight at once), runs the radix-R0
 // DFT in registers and writes the pass's output -- one LDS write + read +
-// barrier fewer than staging the rows first.
-template <typename T, int R0>
+// barrier fewer than staging the rows first.  CP = 2: two adjacent columns
+// per thread and load (the row index arithmetic and the D loads shared).
+template <typename T, int R0, int CP>
 __device__ __forceinline__ void load_first_pass(const T* __restrict__ Ac, const float* __restrict__ d, int64_t lda,
                                                 int64_t N, int N1, int N2, int j1, bool cok, float2* buf) {
-  constexpr int QM = (N2_MAX / R0 * WC + NT1 - 1) / NT1;
+  using V = cvec<CP>;
+  constexpr int WCP = WC / CP;
+  constexpr int QM = (N2_MAX / R0 * WCP + NT1 - 1) / NT1;
   const int64_t M = N >> 1;
-  const int tid = threadIdx.x, col = tid & (WC - 1);
-  const int stride = N2 / R0, nb = stride * WC;
-  float2 v[QM][R0];
+  const int tid = threadIdx.x, col = (tid & (WCP - 1)) * CP;
+  const int stride = N2 / R0, nb = stride * WCP;
+  V v[QM][R0];
 #pragma unroll
   for (int q = 0; q < QM; ++q) {
-    const int j = min(tid + NT1 * q, nb - 1) / WC;     // clamped: unconditional loads
+    const int j = min(tid + NT1 * q, nb - 1) / WCP;     // clamped: unconditional loads
 #pragma unroll
     for (int r = 0; r < R0; ++r) {
       const int64_t j4 = 4 * ((int64_t)j1 + (int64_t)N1 * (j + r * stride));   // 2 n0
       const int64_t x0 = j4 < 2 * M ? j4 : 2 * N - j4 - 1;                   // n0 = 2j < M ?
       const int64_t x1 = j4 + 2 < 2 * M ? j4 + 2 : 2 * N - j4 - 3;           // n1 = 2j + 1 < M ?
-      v[q][r] = make_float2(ld_f(Ac + x0 * lda) * d[x0], ld_f(Ac + x1 * lda) * d[x1]);
+      if constexpr (CP == 2) {
+        float a0, a1, b0, b1;
+        ld_pair(Ac + x0 * lda, a0, a1);
+        ld_pair(Ac + x1 * lda, b0, b1);
+        const float d0 = d[x0], d1 = d[x1];
+        v[q][r] = {make_float2(a0 * d0, b0 * d1), make_float2(a1 * d0, b1 * d1)};
+      } else {
+        v[q][r] = make_float2(ld_f(Ac + x0 * lda) * d[x0], ld_f(Ac + x1 * lda) * d[x1]);
+      }
     }
   }
 #pragma unroll
   for (int q = 0; q < QM; ++q) {
     const int b = tid + NT1 * q;
     if (b < nb) {
-      const int j = b / WC;
+      const int j = b / WCP;
       if (!cok) {
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[q][r] = make_float2(0.f, 0.f);
+        for (int r = 0; r < R0; ++r) v[q][r] = V{};
       }
       dft<R0>(v[q]);
 #pragma unroll
-      for (int r = 0; r < R0; ++r) buf[(j * R0 + r) * WC + col] = v[q][r];
+      for (int r = 0; r < R0; ++r) stv(buf + (j * R0 + r) * WC + col, v[q][r]);
     }
   }
 }
 
-// radix plan: up to 12 radices, 4 bits each, packed low first
-template <typename T>
+// radix plan: up to 12 radices, 4 bits each, packed low first.  CP = 2 (two
+// adjacent columns per thread in the first / last passes) needs m, lda even
+// and the operand rows 8-B (f32) / 4-B (bf16) aligned.
+template <typename T, int CP>
 __global__ void __launch_bounds__(NT1, 2)
 k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const float* __restrict__ d, int N1, int N2,
             uint64_t rplan, int npass, float2* __restrict__ Y, int per) {
@@ -385,26 +415,27 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const float*
   const int c0 = (L - j1 * nch) * WC;
   const int64_t M = N >> 1;
   float2* tm = tw + N2;              // N2: W_M^{(j1 k2) mod M} of this j1
+  const double inv_m = 1.0 / (double)M;   // one f64 division per thread, not one per entry
   for (int t = tid; t < N2; t += NT1) {
     float s, c;
     sincospif(-2.0f * (float)t / (float)N2, &s, &c);
     tw[t] = make_float2(c, s);
     const int64_t r = (int64_t)j1 * t;   // < N1 N2 = M: no reduction needed
-    sincospif(-2.0f * (float)((double)r / (double)M), &s, &c);
+    sincospif(-2.0f * (float)((double)r * inv_m), &s, &c);
     tm[t] = make_float2(c, s);
   }
   // ---- rows of z[j1 + N1 j2] (D applied) -> first radix pass -> tile
-  const int col = tid & (WC - 1);
-  const bool cok = c0 + col < m;
-  const T* Ac = A + min(c0 + col, m - 1);
+  const int col = (tid & (WC / CP - 1)) * CP;
+  const bool cok = c0 + col < m;     // CP = 2: m even, so a pair is all in or all out
+  const T* Ac = A + min(c0 + col, m - CP);
   const int R0 = (int)(rplan & 15);
   switch (R0) {
-    case 8: load_first_pass<T, 8>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
-    case 4: load_first_pass<T, 4>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
-    case 5: load_first_pass<T, 5>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
-    case 3: load_first_pass<T, 3>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
-    case 7: load_first_pass<T, 7>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
-    default: load_first_pass<T, 2>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 8: load_first_pass<T, 8, CP>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 4: load_first_pass<T, 4, CP>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 5: load_first_pass<T, 5, CP>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 3: load_first_pass<T, 3, CP>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
+    case 7: load_first_pass<T, 7, 1>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;   // CP = 2 spills
+    default: load_first_pass<T, 2, CP>(Ac, d, lda, N, N1, N2, j1, cok, buf); break;
   }
   __syncthreads();
   // ---- the middle passes of the length-N2 FFT along the tile's rows
@@ -413,12 +444,12 @@ k_fs_stage1(const T* __restrict__ A, int64_t lda, int64_t N, int m, const float*
   float2* Yc = Y + (int64_t)j1 * m + c0 + col;
   const int64_t ys = (int64_t)N1 * m;
   switch ((int)((rplan >> (4 * (npass - 1))) & 15)) {
-    case 8: last_pass_store<8>(buf, tw, tm, N2, Yc, ys, cok); break;
-    case 4: last_pass_store<4>(buf, tw, tm, N2, Yc, ys, cok); break;
-    case 5: last_pass_store<5>(buf, tw, tm, N2, Yc, ys, cok); break;
-    case 3: last_pass_store<3>(buf, tw, tm, N2, Yc, ys, cok); break;
-    case 7: last_pass_store<7>(buf, tw, tm, N2, Yc, ys, cok); break;
-    default: last_pass_store<2>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 8: last_pass_store<8, CP>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 4: last_pass_store<4, CP>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 5: last_pass_store<5, CP>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 3: last_pass_store<3, CP>(buf, tw, tm, N2, Yc, ys, cok); break;
+    case 7: last_pass_store<7, CP>(buf, tw, tm, N2, Yc, ys, cok); break;
+    default: last_pass_store<2, CP>(buf, tw, tm, N2, Yc, ys, cok); break;
   }
 }
 
@@ -553,7 +584,7 @@ k_fs_stage2(const float2* __restrict__ Y, int N1, int N2, int m, const int* __re
 constexpr int M2_NT = 4;            // 16-column N tiles per wave (64 columns)
 constexpr int M2_MTMAX = 4;         // M tiles per pass (32 frequencies)
 constexpr int M2_G = 8 * M2_MTMAX;  // frequencies per pass
-constexpr int M2_PD = 6;            // 4-row steps in flight per wave
+constexpr int M2_PD = 4;            // 4-row steps in flight per wave
 constexpr int M2_SLOT = 4 * 64;     // float2 per ring slot (4 rows x 64 columns)
 typedef float f32x4m __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_v;
@@ -623,13 +654,18 @@ __device__ __forceinline__ void fs2m_pass(const float2* __restrict__ Yk, int m, 
       // slot read back into registers: refill it (steps past the end re-read the last row: uniform counts)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       issue(sl, step + M2_PD);
+      // all real-part products, then all imaginary-part ones: no MFMA waits
+      // on the one just before it (40-cycle dependent latency vs 32 issue)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < M2_NT; ++nt) {
+        for (int nt = 0; nt < M2_NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(are[mt], y[nt].x, acc[mt][nt], 0, 0, 0);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < M2_NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(aim[mt], y[nt].y, acc[mt][nt], 0, 0, 0);
-        }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's last (unused) refills, before the next pass reuses it
@@ -650,9 +686,10 @@ __device__ __forceinline__ void fs2m_pass(const float2* __restrict__ Yk, int m, 
     }
 }
 
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, 3)
 k_fs_stage2m(const float2* __restrict__ Y, int N1, int N2, int m, const int* __restrict__ gptr,
-             const int* __restrict__ gk1, const int* __restrict__ gslot, float2* __restrict__ Zs, int per) {
+             const int* __restrict__ gk1, const int* __restrict__ gslot, float2* __restrict__ Zs, int per,
+             const int* __restrict__ gord) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   float2* ringb = lds;                          // 4 waves x M2_PD slots
   float2* tw = lds + 4 * M2_PD * M2_SLOT;       // N1: W_N1^t
@@ -662,9 +699,10 @@ k_fs_stage2m(const float2* __restrict__ Y, int N1, int N2, int m, const int* __r
   const int nch = (m + cw - 1) / cw;
   const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
   if (L >= nch * N2) return;
-  const int k2 = L / nch;
-  const int cw0 = (L - k2 * nch) * cw + w * 64;
-  const int g0 = gptr[k2], g1 = gptr[k2 + 1];
+  const int gi = L / nch;             // group (largest first when gord is given)
+  const int k2 = gord ? gord[gi] : gi;
+  const int cw0 = (L - gi * nch) * cw + w * 64;
+  const int g0 = gptr[gi], g1 = gptr[gi + 1];
   if (g0 == g1) return;
   for (int t = tid; t < N1; t += blockDim.x) {
     float sn, cs;
@@ -723,9 +761,16 @@ int launch_stage1(const T* A, int64_t lda, int64_t N, int m, const float* d, int
                   int npass, float2* Y, hipStream_t s) {
   const int64_t ntiles = (int64_t)((m + WC - 1) / WC) * N1;
   const int per = (int)((ntiles + 7) / 8);
-  SL_LDS_ATTR(k_fs_stage1<T>, (int)stage1_lds(N2_MAX));
-  k_fs_stage1<T><<<(unsigned)(8 * (int64_t)per), NT1, stage1_lds(N2), s>>>(A, lda, N, m, d, N1, N2, rplan, npass, Y,
-                                                                            per);
+  const bool pair = m % 2 == 0 && m >= 2 && lda % 2 == 0 && (uintptr_t)A % (2 * sizeof(T)) == 0 &&
+                    (uintptr_t)Y % 16 == 0;
+  const unsigned grid = (unsigned)(8 * (int64_t)per);
+  if (pair) {
+    SL_LDS_ATTR((k_fs_stage1<T, 2>), (int)stage1_lds(N2_MAX));
+    k_fs_stage1<T, 2><<<grid, NT1, stage1_lds(N2), s>>>(A, lda, N, m, d, N1, N2, rplan, npass, Y, per);
+  } else {
+    SL_LDS_ATTR((k_fs_stage1<T, 1>), (int)stage1_lds(N2_MAX));
+    k_fs_stage1<T, 1><<<grid, NT1, stage1_lds(N2), s>>>(A, lda, N, m, d, N1, N2, rplan, npass, Y, per);
+  }
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -767,8 +812,11 @@ SL_API int sl_fs_stage1(const void* A, int dtype, int64_t lda, int64_t N, int m,
 }
 
 // Stage 2.  gptr: N2 + 1 offsets into gk1 / gslot; Zs: nslots x m complex.
+// gord (optional, MFMA kernel): group g of the CSR holds frequencies of
+// k2 = gord[g] (groups sorted by size, largest first: the big groups start
+// first and the grid's tail is short); null: group g is k2 = g.
 SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, const int* gk1, const int* gslot,
-                        void* Zs, void* stream) {
+                        void* Zs, const int* gord, void* stream) {
   if (N1 < 1 || N1 > 8192 || N2 < 1 || m < 1) {
     sl_set_last_error("fs_stage2: needs 1 <= N1 <= 8192");
     return SL_ERR_INVALID;
@@ -779,9 +827,13 @@ SL_API int sl_fs_stage2(const void* Y, int N1, int N2, int m, const int* gptr, c
     const int64_t nblk = (int64_t)((m + 64 * nw - 1) / (64 * nw)) * N2;
     const int per = (int)((nblk + 7) / 8);
     k_fs_stage2m<<<(unsigned)(8 * (int64_t)per), 64 * nw, stage2m_lds(N1), (hipStream_t)stream>>>(
-        (const float2*)Y, N1, N2, m, gptr, gk1, gslot, (float2*)Zs, per);
+        (const float2*)Y, N1, N2, m, gptr, gk1, gslot, (float2*)Zs, per, gord);
     SL_LAUNCH_CHECK();
     return SL_OK;
+  }
+  if (gord) {
+    sl_set_last_error("fs_stage2: a group order needs the MFMA kernel (even m)");
+    return SL_ERR_INVALID;
   }
   SL_LDS_ATTR(k_fs_stage2, (int)stage2_lds(8192));
   // narrow batches: fewer waves per workgroup (each wave owns 64 columns)

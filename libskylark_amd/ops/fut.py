@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import math
 
+import weakref
+
 import torch
 
 
@@ -199,15 +201,19 @@ def _fs_lib():
         _FS_REG[0] = True
         vp, i32, i64, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64
         _lib.register("sl_fs_stage1", [vp, i32, i64, i64, i32, vp, i32, i32, u64, i32, vp, vp])
-        _lib.register("sl_fs_stage2", [vp, i32, i32, i32, vp, vp, vp, vp, vp])
+        _lib.register("sl_fs_stage2", [vp, i32, i32, i32, vp, vp, vp, vp, vp, vp])
         _lib.register("sl_fs_post", [vp, i32, i64, vp, i32, vp, vp, C.c_double, vp, i64, vp])
         _lib.register("sl_fs_set_stage2_variant", [i32], None)
     return _lib
 
 
+_STAGE2 = [1]
+
+
 def set_fourstep_stage2(variant: int) -> None:
     """Stage-2 kernel of the four-step DCT: 1 (default) the MFMA kernel,
     0 the VALU kernel (A/B, tests)."""
+    _STAGE2[0] = int(variant)
     _fs_lib().require().sl_fs_set_stage2_variant(int(variant))
 
 
@@ -265,6 +271,17 @@ class _FourStepPlan:
         self.gptr = gptr.to(dev, i32)
         self.gk1 = k1[order].to(dev, i32)
         self.gslot = order.to(dev, i32)
+        # the same groups largest first, for the MFMA stage-2 kernel (gord:
+        # group -> k2): big groups start first and the grid's tail is short
+        gord = torch.argsort(cnt, descending=True, stable=True)
+        perm = torch.cat([torch.arange(int(gptr[g]), int(gptr[g + 1])) for g in gord.tolist()]) \
+            if self.nslots else torch.zeros(0, dtype=torch.int64)
+        gptr_s = torch.zeros(self.N2 + 1, dtype=torch.int64)
+        gptr_s[1:] = torch.cumsum(cnt[gord], 0)
+        self.gord = gord.to(dev, i32)
+        self.gptr_s = gptr_s.to(dev, i32)
+        self.gk1_s = k1[order][perm].to(dev, i32)
+        self.gslot_s = order[perm].to(dev, i32)
         self.sa = torch.searchsorted(F, fa).to(dev, i32)
         self.sb = torch.searchsorted(F, fb).to(dev, i32)
         self.samples = k.to(dev)
@@ -272,6 +289,25 @@ class _FourStepPlan:
 
 
 _FS_PLANS: dict = {}
+_D_COPIES: dict = {}
+
+
+def _device_copy(d: torch.Tensor, dev, dtype) -> torch.Tensor:
+    """The sketch's diagonal D as a contiguous device tensor, kept per source
+    tensor object (weak reference + version counter): a host-resident D
+    (the sketch's Rademacher vector) was re-uploaded on every application,
+    a pageable 4-8 MB copy at N = 1e6 (~10% of the FJLT)."""
+    if d.device == torch.device(dev) and d.dtype == dtype and d.is_contiguous():
+        return d
+    key = (id(d), str(dev), dtype)
+    hit = _D_COPIES.get(key)
+    if hit is not None and hit[0]() is d and hit[1] == d._version:
+        return hit[2]
+    out = d.to(device=dev, dtype=dtype).contiguous()
+    if len(_D_COPIES) >= 8:
+        _D_COPIES.pop(next(iter(_D_COPIES)))
+    _D_COPIES[key] = (weakref.ref(d), d._version, out)
+    return out
 
 
 def fourstep_ok(A: torch.Tensor, dim: int, S: int) -> bool:
@@ -290,21 +326,32 @@ def fjlt_fourstep(A: torch.Tensor, d: torch.Tensor, samples: torch.Tensor, scale
     import ctypes as C
     L = _fs_lib()
     N, m = A.shape
+    # cached per samples tensor OBJECT (weak reference + version counter): a
+    # key on the data pointer alone hit stale plans once a dead tensor's
+    # memory was reused for different samples
     key = (samples.data_ptr(), samples.numel(), N, str(A.device))
     plan = _FS_PLANS.get(key)
+    if plan is not None and (plan.src() is not samples or plan.version != samples._version):
+        plan = None
     if plan is None:
         if len(_FS_PLANS) >= 8:
             _FS_PLANS.pop(next(iter(_FS_PLANS)))
         plan = _FourStepPlan(N, samples, A.device)
+        plan.src, plan.version = weakref.ref(samples), samples._version
         _FS_PLANS[key] = plan
     st = C.c_void_p(L.stream_of(A))
-    dd = d.to(device=A.device, dtype=torch.float32).contiguous()
+    dd = _device_copy(d, A.device, torch.float32)
     Y = torch.empty(plan.N2 * plan.N1 * m * 2, dtype=torch.float32, device=A.device)
     L.call("sl_fs_stage1", L.ptr(A), L.dtype_code(A.dtype), A.stride(0), N, m, L.ptr(dd), plan.N1, plan.N2,
            C.c_uint64(plan.rplan), plan.npass, L.ptr(Y), st)
     Zs = torch.empty(plan.nslots * m * 2, dtype=torch.float32, device=A.device)
-    L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1),
-           L.ptr(plan.gslot), L.ptr(Zs), st)
+    if m % 2 == 0 and Y.data_ptr() % 16 == 0 and _STAGE2[0]:
+        # the MFMA kernel, groups largest first
+        L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr_s), L.ptr(plan.gk1_s),
+               L.ptr(plan.gslot_s), L.ptr(Zs), L.ptr(plan.gord), st)
+    else:
+        L.call("sl_fs_stage2", L.ptr(Y), plan.N1, plan.N2, m, L.ptr(plan.gptr), L.ptr(plan.gk1),
+               L.ptr(plan.gslot), L.ptr(Zs), None, st)
     del Y
     out = torch.empty(plan.S, m, dtype=torch.float32, device=A.device)
     L.call("sl_fs_post", L.ptr(Zs), m, N, L.ptr(plan.samples), plan.S, L.ptr(plan.sa), L.ptr(plan.sb),
@@ -330,7 +377,7 @@ def fjlt_sampled(A: torch.Tensor, dim: int, d: torch.Tensor, samples: torch.Tens
         from . import _lib
         _lib.require()
         st = C.c_void_p(_lib.stream_of(A))
-        dd = d.to(device=A.device, dtype=torch.float64).contiguous()   # sl_fjlt_pre takes f64 D
+        dd = _device_copy(d, A.device, torch.float64)   # sl_fjlt_pre takes f64 D
         # always transform along contiguous rows of an m x N buffer (dim 0 input
         # is transposed by the pre-pass itself)
         v = torch.empty(m, N, dtype=torch.float32, device=A.device)
