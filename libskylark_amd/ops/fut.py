@@ -289,25 +289,9 @@ class _FourStepPlan:
 
 
 _FS_PLANS: dict = {}
-_D_COPIES: dict = {}
-
-
 def _device_copy(d: torch.Tensor, dev, dtype) -> torch.Tensor:
-    """The sketch's diagonal D as a contiguous device tensor, kept per source
-    tensor object (weak reference + version counter): a host-resident D
-    (the sketch's Rademacher vector) was re-uploaded on every application,
-    a pageable 4-8 MB copy at N = 1e6 (~10% of the FJLT)."""
-    if d.device == torch.device(dev) and d.dtype == dtype and d.is_contiguous():
-        return d
-    key = (id(d), str(dev), dtype)
-    hit = _D_COPIES.get(key)
-    if hit is not None and hit[0]() is d and hit[1] == d._version:
-        return hit[2]
-    out = d.to(device=dev, dtype=dtype).contiguous()
-    if len(_D_COPIES) >= 8:
-        _D_COPIES.pop(next(iter(_D_COPIES)))
-    _D_COPIES[key] = (weakref.ref(d), d._version, out)
-    return out
+    from ..utils.devcache import device_copy
+    return device_copy(d, dev, dtype)
 
 
 def fourstep_ok(A: torch.Tensor, dim: int, S: int) -> bool:

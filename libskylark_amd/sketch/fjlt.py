@@ -21,6 +21,7 @@ import torch
 from ..base import distributions as D
 from ..ops import fut as _fut
 from ..ops import rng as _rng
+from ..utils.devcache import device_copy
 from .base import COLUMNWISE, SketchTransform, register
 
 DIRECT_MAX_S = 256
@@ -43,12 +44,12 @@ class RFUT:
             if getattr(self, "_all", None) is None or self._all.device != A.device:
                 self._all = torch.arange(self.N, dtype=torch.int64, device=A.device)
             return _fut.fjlt_sampled(A, dim, self.D, self._all, 1.0)
-        d = self.D.to(device=A.device, dtype=torch.float64 if A.dtype == torch.float64 else torch.float32)
+        d = device_copy(self.D, A.device, torch.float64 if A.dtype == torch.float64 else torch.float32)
         X = A * (d[:, None] if dim == COLUMNWISE else d[None, :])
         return _fut.FUTS[self.fut][0](X, dim)
 
     def apply_inverse(self, A: torch.Tensor, dim: int = COLUMNWISE) -> torch.Tensor:
-        d = self.D.to(device=A.device, dtype=torch.float64 if A.dtype == torch.float64 else torch.float32)
+        d = device_copy(self.D, A.device, torch.float64 if A.dtype == torch.float64 else torch.float32)
         X = _fut.FUTS[self.fut][1](A, dim)
         return X * (d[:, None] if dim == COLUMNWISE else d[None, :])
 
@@ -147,7 +148,7 @@ class UST(SketchTransform):
         return P
 
     def _apply_dense(self, A, dim, in_offset=0, out_rows=None):
-        idx = self.samples.to(A.device)
+        idx = device_copy(self.samples, A.device)
         return A.index_select(dim, idx)
 
     def _apply_sparse(self, A, dim, sparse_out):

@@ -291,8 +291,9 @@ class PPT(SketchTransform):
             _lib.require()
             F = F.contiguous()
             P = torch.empty(K, m, dtype=torch.complex64, device=A.device)
-            idx = self.hash_idx.to(device=A.device, dtype=torch.int64).contiguous()
-            hv = self.hash_val.to(device=A.device, dtype=torch.float64).contiguous()
+            from ..utils.devcache import device_copy
+            idx = device_copy(self.hash_idx, A.device, torch.int64)
+            hv = device_copy(self.hash_val, A.device, torch.float64)
             _lib.call("sl_ppt_product", _lib.ptr(F), q, K, m, S, _lib.ptr(idx), _lib.ptr(hv), sg, sc, _lib.ptr(P),
                       C.c_void_p(_lib.stream_of(F)))
         else:
