@@ -96,15 +96,31 @@ __device__ __forceinline__ double ld_el(const double* p) {
 // double-buffered: chunk c + 1 is loaded into registers while chunk c
 // computes and stored after it, one barrier per chunk.  A is prefetched PD =
 // 2 groups ahead in a register ring (slot g % 2, static in the unrolled body).
+// Work split: R = nrb / g - 1 interleaved rounds of whole row blocks
+// (workgroup b takes blocks b, b + g, ...: the blocks in flight at a time
+// stay within a window of ~g blocks of A -- contiguous per-workgroup ranges
+// over the whole operand ran the f32 product 14% slower), then the last g ..
+// 2g - 1 blocks stream-K style: their (block, chunk) pairs cut into g equal
+// contiguous ranges, so every workgroup streams the same number of chunks
+// (whole blocks only left 2e5-row f64 operands at 4 vs 3.05 blocks per
+// workgroup: a 30% tail).  A tail block cut by a range boundary is finished
+// by two workgroups, each adding its partial y with an atomic add (the block
+// is zeroed first by k_az_zero_cut; two addends onto zero sum the same in
+// either order, so the result stays deterministic: every tail range spans
+// at least one whole block, so no block has a third contributor).
 constexpr int AZ_NT = 256, AZ_RT = 2, AZ_VL = 2, AZ_NG = 4, AZ_PD = 2, AZ_BR = 4 * 16 * AZ_RT;
 
 template <typename T, int KT>
 constexpr int az_lds() { return 2 * AZ_NG * KT * 64 * 16 * AZ_VL; }
 
+// whole-block interleaved rounds before the stream-K tail (the tail keeps
+// g .. 2g - 1 blocks; g <= nrb)
+__host__ __device__ inline int64_t az_rounds(int64_t nrb, int64_t g) { return nrb >= 2 * g ? nrb / g - 1 : 0; }
+
 template <typename T, int KT, bool VEC>
 __global__ void __launch_bounds__(AZ_NT, 2)
 k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Z, int k, T* __restrict__ Y,
-        int64_t ldy) {
+        int64_t ldy, int split) {
   using M = Mf<T>;
   using vec = typename M::vec;
   using acc_t = typename M::acc;
@@ -115,9 +131,30 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nchunk = (n + CW - 1) / CW;
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
-  const int64_t nmine = (int64_t)blockIdx.x < nrb ? (nrb - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int64_t nfc = nmine * nchunk;
-  if (nfc == 0) return;
+  const int64_t G = gridDim.x;
+  // split 0 (A/B only): whole blocks round-robin, no tail
+  const int64_t R = split ? az_rounds(nrb, G) : (int64_t)blockIdx.x < nrb ? (nrb - 1 - blockIdx.x) / G + 1 : 0;
+  const int64_t tail = split ? (nrb - R * G) * nchunk : 0;   // flat (block, chunk) pairs of the tail
+  const int64_t FR = R * nchunk;                     // this workgroup's round chunks
+  const int64_t F0 = R * G * nchunk + tail * blockIdx.x / G;   // its tail range [F0, F0 + FT)
+  const int64_t FT = R * G * nchunk + tail * (blockIdx.x + 1) / G - F0;
+  const int64_t nfc = FR + FT;
+  if (nfc <= 0) return;
+  // (row block j, chunk c) of flat chunk f + 1 from that of f, clamped at
+  // the last one (no divisions in the loop: hipcc's 64-bit division expands
+  // into out-of-line blocks)
+  const int64_t jt0 = F0 / nchunk;
+  const int ct0 = (int)(F0 - jt0 * nchunk);
+  auto advance = [&](int64_t f, int64_t& j, int& c) {
+    if (f + 1 >= nfc) return;
+    if (f + 1 == FR) {
+      j = jt0;
+      c = ct0;
+    } else if (++c == nchunk) {
+      c = 0;
+      j += f + 1 < FR ? G : 1;
+    }
+  };
 
   // Every global load of the loop is inline asm (ld16 / ld_el) with explicit
   // waits: the ring crosses the chunk loop's back-edge, where the compiler's
@@ -167,11 +204,8 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   // clamped to a valid position (their Z rows are zero), a flat chunk past
   // the end re-reads the last one (never used)
   vec ring[AZ_PD][AZ_RT][AZ_VL];
-  auto issue = [&](int64_t fc, int g, int slot) {
-    fc = fc < nfc ? fc : nfc - 1;
-    const int64_t j = fc / nchunk;
-    const int c = (int)(fc - j * nchunk);
-    const int64_t r0 = (blockIdx.x + j * gridDim.x) * AZ_BR + 32 * w;
+  auto issue = [&](int64_t j, int c, int g, int slot) {
+    const int64_t r0 = j * AZ_BR + 32 * w;
     const int col0 = c * CW + g * GW + EPL * (lane >> 4);
 #pragma unroll
     for (int rt = 0; rt < AZ_RT; ++rt) {
@@ -212,17 +246,21 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   // prologue: chunk 0 of Z in buffer 0, groups 0 .. PD - 1 of flat chunk 0
   // in flight (issued before the chunk loop's first Z loads, as the
   // previous chunk's refills would be)
-  zload(0);
+  int64_t jb = FR > 0 ? (int64_t)blockIdx.x : jt0;   // flat chunk fc
+  int c = FR > 0 ? 0 : ct0;
+  int64_t jn = jb;                                     // flat chunk fc + 1
+  int cn = c;
+  advance(0, jn, cn);
+  const int c0 = c;
+  zload(c0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  zstore(0, 0);
+  zstore(0, c0);
 #pragma unroll
-  for (int g = 0; g < AZ_PD; ++g) issue(0, g, g);
+  for (int g = 0; g < AZ_PD; ++g) issue(jb, c, g, g);
   __syncthreads();
 
   for (int64_t fc = 0; fc < nfc; ++fc) {
-    const int c = (int)(fc % nchunk);
     const int buf = nchunk > 1 ? (int)(fc & 1) : 0;   // one chunk: Z never reloads
-    const int cn = c + 1 < nchunk ? c + 1 : 0;
     zload(cn);   // always issued: the wait arithmetic counts it
     const T* zb = zl + buf * (AZ_NG * KT * 64 * EPL);
 #pragma unroll
@@ -243,14 +281,15 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
       }
       // refill this slot with group g + PD (of the next flat chunk past the end)
       __builtin_amdgcn_sched_barrier(0);
-      if (g + AZ_PD < AZ_NG) issue(fc, g + AZ_PD, slot);
-      else issue(fc + 1, g + AZ_PD - AZ_NG, slot);
+      if (g + AZ_PD < AZ_NG) issue(jb, c, g + AZ_PD, slot);
+      else issue(jn, cn, g + AZ_PD - AZ_NG, slot);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (c == nchunk - 1) {
-      // the row block is complete: y out, accumulators cleared
-      const int64_t j = fc / nchunk;
-      const int64_t r0 = (blockIdx.x + j * gridDim.x) * AZ_BR + 32 * w;
+    if (c == nchunk - 1 || fc == nfc - 1) {
+      // this workgroup's part of the row block is complete: y out (added
+      // atomically into a block cut by a range boundary), accumulators cleared
+      const bool cut = fc >= FR && (jb * nchunk < F0 || (jb + 1) * nchunk > F0 + FT);
+      const int64_t r0 = jb * AZ_BR + 32 * w;
 #pragma unroll
       for (int rt = 0; rt < AZ_RT; ++rt)
 #pragma unroll
@@ -259,13 +298,19 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + 16 * rt + M::drow(lane, r);
-            if (row < m && col < k) Y[row * ldy + col] = acc[rt][t][r];
+            if (row < m && col < k) {
+              if (cut) atomicAdd(Y + row * ldy + col, acc[rt][t][r]);
+              else Y[row * ldy + col] = acc[rt][t][r];
+            }
           }
           acc[rt][t] = acc_t{};
         }
     }
     zstore(buf ^ 1, cn);   // (one chunk: a scratch copy into the unused buffer)
     __syncthreads();
+    jb = jn;
+    c = cn;
+    advance(fc + 1, jn, cn);
   }
   // the clamped refills past the end: landed, and kept live until then (an
   // asm load's register the compiler thinks dead could be reused in flight)
@@ -276,6 +321,22 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
     for (int rt = 0; rt < AZ_RT; ++rt)
 #pragma unroll
       for (int vl = 0; vl < AZ_VL; ++vl) asm volatile("" : "+v"(ring[g][rt][vl]));
+}
+
+// zero the row blocks of y that a range boundary of k_ts_az cuts (one
+// workgroup per boundary b = 1 .. grid - 1)
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_az_zero_cut(T* __restrict__ Y, int64_t m, int k, int64_t ldy, int64_t nrb, int nchunk, int grid) {
+  const int64_t R = az_rounds(nrb, grid);
+  const int64_t tail = (nrb - R * grid) * nchunk;
+  const int64_t F = R * grid * nchunk + tail * (blockIdx.x + 1) / grid;
+  if (F % nchunk == 0) return;
+  const int64_t r0 = F / nchunk * AZ_BR;
+  for (int e = threadIdx.x; e < AZ_BR * k; e += 256) {
+    const int64_t row = r0 + e / k;
+    if (row < m) Y[row * ldy + e % k] = (T)0;
+  }
 }
 
 // ---------------------------------------------------------------- W = A^T Q
@@ -289,19 +350,22 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
 // fragments (Q[r + kk][16 t + nn]) load straight from global (the 8 waves of
 // a workgroup read the same rows: L1 / L2 hits).  W accumulates over the
 // whole row group in registers (A's precision), then one slab per row group.
-constexpr int AT_NT = 512, AT_V = 2;
+// AV = vectors per wave and row: 2 (default: one workgroup per CU, > 128
+// VGPRs) or 1 (half the columns per wave, two workgroups per CU; A/B knob)
+constexpr int AT_NT = 512;
+int g_atq_av = 2;
 // ring depth: 8 row quads in flight, 4 at KT = 4 (register budget)
-template <int KT>
-constexpr int at_pd() { return KT >= 4 ? 4 : 8; }
+template <int KT, int AV>
+constexpr int at_pd() { return AV == 1 ? (KT >= 4 ? 4 : 6) : (KT >= 4 ? 4 : 8); }
 
-template <typename T, int KT, bool VEC>
-__global__ void __launch_bounds__(AT_NT, 1)
+template <typename T, int KT, bool VEC, int AV>
+__global__ void __launch_bounds__(AT_NT, AV == 1 ? 2 : 1)
 k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Q, int k, int64_t rows_per,
          T* __restrict__ slab) {
   using M = Mf<T>;
   using vec = typename M::vec;
   using acc_t = typename M::acc;
-  constexpr int VW = M::VW, WC = AT_V * 16 * VW, CS = 8 * WC, PD = at_pd<KT>();
+  constexpr int VW = M::VW, WC = AV * 16 * VW, CS = 8 * WC, PD = at_pd<KT, AV>();
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kk = lane >> 4, nn = lane & 15;
   const int64_t rbeg = (int64_t)blockIdx.y * rows_per;
@@ -311,9 +375,9 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
   // waves of the last slice past n idle (wave-uniform)
   const int64_t nq = (rend > rbeg && cbw < n) ? (rend - rbeg + 3) / 4 : 0;
 
-  acc_t acc[AT_V][VW][KT];
+  acc_t acc[AV][VW][KT];
 #pragma unroll
-  for (int v = 0; v < AT_V; ++v)
+  for (int v = 0; v < AV; ++v)
 #pragma unroll
     for (int e = 0; e < VW; ++e)
 #pragma unroll
@@ -323,7 +387,7 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
   // into [0, n); the Q fragment of a row past the group (or a k column past
   // k) is zeroed at USE time from a mask formed at issue time, so nothing
   // touches a loaded value before its turn in the MFMA stream
-  vec ra[PD][AT_V];
+  vec ra[PD][AV];
   T rq[PD][KT];
   bool rok[PD];
   auto issue = [&](int64_t qi, int slot) {
@@ -332,7 +396,7 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
     row = row < rend ? row : rend - 1;
     const T* src = A + row * lda;
 #pragma unroll
-    for (int v = 0; v < AT_V; ++v) {
+    for (int v = 0; v < AV; ++v) {
       const int col = cbw + v * 16 * VW + VW * nn;
       if constexpr (VEC) {
         ra[slot][v] = ld16<vec>(src + (col < n ? col : n - VW));
@@ -350,13 +414,13 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
     }
   };
   // loads per slot; slot p is waited for with the PD - 1 later slots in flight
-  constexpr int LPS = AT_V * (VEC ? 1 : VW) + KT;
+  constexpr int LPS = AV * (VEC ? 1 : VW) + KT;
   // (waiting for at most 63 when more are in flight is stricter, still exact-safe)
   constexpr int INFLIGHT = (PD - 1) * LPS < 63 ? (PD - 1) * LPS : 63;
   auto wait_ring = [&](int p) {
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ra[p][0]) : "n"(INFLIGHT));
 #pragma unroll
-    for (int v = 1; v < AT_V; ++v) asm volatile("" : "+v"(ra[p][v]));
+    for (int v = 1; v < AV; ++v) asm volatile("" : "+v"(ra[p][v]));
 #pragma unroll
     for (int t = 0; t < KT; ++t) asm volatile("" : "+v"(rq[p][t]));
   };
@@ -373,7 +437,7 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
 #pragma unroll
         for (int t = 0; t < KT; ++t) b[t] = (rok[p] && 16 * t + nn < k) ? rq[p][t] : (T)0;
 #pragma unroll
-        for (int v = 0; v < AT_V; ++v)
+        for (int v = 0; v < AV; ++v)
 #pragma unroll
           for (int e = 0; e < VW; ++e)
 #pragma unroll
@@ -390,7 +454,7 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
 #pragma unroll
     for (int p = 0; p < PD; ++p) {
 #pragma unroll
-      for (int v = 0; v < AT_V; ++v) asm volatile("" : "+v"(ra[p][v]));
+      for (int v = 0; v < AV; ++v) asm volatile("" : "+v"(ra[p][v]));
 #pragma unroll
       for (int t = 0; t < KT; ++t) asm volatile("" : "+v"(rq[p][t]));
     }
@@ -399,7 +463,7 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
   // slab (row group y) [n][k]: tile (v, e) row i is column cbw + v 16 VW + VW i + e
   T* sb = slab + (int64_t)blockIdx.y * n * k;
 #pragma unroll
-  for (int v = 0; v < AT_V; ++v)
+  for (int v = 0; v < AV; ++v)
 #pragma unroll
     for (int e = 0; e < VW; ++e)
 #pragma unroll
@@ -502,11 +566,175 @@ __global__ void __launch_bounds__(256) k_ts_gram64(const double* __restrict__ X,
   }
 }
 
+// The same two helpers on the f64 matrix cores (v_mfma_f64_16x16x4f64), for
+// even k / ldx with X 16-B aligned (k_ts_xm64 / k_ts_gram64 above serve the
+// rest).  The LDS-tile VALU forms ran at ~0.7-1.3 TB/s (95 / 101 us on the
+// 2e5 x 40 iterate of the f64 engine, ten Grams and seven X M per call).
+//
+// X M: a wave owns 16-row tiles (strided over the grid, two per iteration so
+// ten 16-B loads per lane are in flight); lane (kg = l >> 4, r = l & 15) loads
+// X[r][8 s + 2 kg .. + 1] for every 8-column step s and feeds element e to
+// the MFMA whose K index 8 s + 2 kg + e its M fragment (held in registers
+// for the whole kernel) agrees on.  Out tiles leave as 128-B row segments.
+template <typename TO, int KT2>
+__global__ void __launch_bounds__(256) k_ts_xm64m(const double* __restrict__ X, int64_t rows, int k, int64_t ldx,
+                                                  const double* __restrict__ Mm, int k2, TO* __restrict__ out,
+                                                  int64_t ldo) {
+  constexpr int KS = 8;   // 8-column steps (k <= 64)
+  const int lane = threadIdx.x & 63, kg = lane >> 4, r16 = lane & 15;
+  const int ks = (k + 7) >> 3;
+  double bm[KS][2][KT2];
+#pragma unroll
+  for (int st = 0; st < KS; ++st)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int tj = 0; tj < KT2; ++tj) {
+        const int kr = 8 * st + 2 * kg + e, c = 16 * tj + r16;
+        bm[st][e][tj] = (kr < k && c < k2) ? Mm[kr * k2 + c] : 0.0;
+      }
+  const int64_t ntile = (rows + 15) >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t t0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t0 < ntile; t0 += 2 * nw) {
+    f64x2 xv[2][KS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t t = t0 + u * nw;
+      int64_t row = 16 * t + r16;
+      row = row < rows ? row : rows - 1;   // clamped (never stored)
+      const double* src = X + row * ldx;
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        const int c = 8 * st + 2 * kg;
+        xv[u][st] = (st < ks && c < k) ? *(const f64x2*)(src + c) : f64x2{0.0, 0.0};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t t = t0 + u * nw;
+      if (t >= ntile) break;
+      f64x4 acc[KT2];
+#pragma unroll
+      for (int tj = 0; tj < KT2; ++tj) acc[tj] = f64x4{};
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        if (st >= ks) break;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int tj = 0; tj < KT2; ++tj)
+            acc[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[u][st][e], bm[st][e][tj], acc[tj], 0, 0, 0);
+      }
+#pragma unroll
+      for (int tj = 0; tj < KT2; ++tj) {
+        const int c = 16 * tj + r16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = 16 * t + Mf<double>::drow(lane, r);
+          if (row < rows && c < k2) out[row * ldo + c] = (TO)acc[tj][r];
+        }
+      }
+    }
+  }
+}
+
+// X^T X: a wave owns a contiguous range of 4-row K-steps (rows 4 q + kg,
+// columns 16 t + r16 per lane: the A and B fragments of every tile come from
+// the same KT loaded values), upper-triangle tiles only, four steps of
+// loads in flight; the four waves' tiles are summed in LDS and the slab is
+// written from the upper triangle (exactly symmetric).
+template <int KT>
+__global__ void __launch_bounds__(256) k_ts_gram64m(const double* __restrict__ X, int64_t rows, int k, int64_t ldx,
+                                                    double* __restrict__ slab) {
+  constexpr int KP = 16 * KT, U = 4;
+  __shared__ double red[KP][KP + 1];
+  const int lane = threadIdx.x & 63, kg = lane >> 4, r16 = lane & 15, w = threadIdx.x >> 6;
+  f64x4 acc[KT][KT];
+#pragma unroll
+  for (int a = 0; a < KT; ++a)
+#pragma unroll
+    for (int b = 0; b < KT; ++b) acc[a][b] = f64x4{};
+  const int64_t nq = (rows + 3) >> 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + w;
+  const int64_t q0 = nq * wid / nw, q1 = nq * (wid + 1) / nw;
+  for (int64_t q = q0; q < q1; q += U) {
+    double xv[U][KT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = 4 * (q + u) + kg;
+      const bool rok = q + u < q1 && row < rows;
+      const double* src = X + (rok ? row : 0) * ldx;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int c = 16 * t + r16;
+        xv[u][t] = (rok && c < k) ? src[c] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int a = 0; a < KT; ++a)
+#pragma unroll
+        for (int b = a; b < KT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[u][a], xv[u][b], acc[a][b], 0, 0, 0);
+  }
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int a = 0; a < KT; ++a)
+#pragma unroll
+        for (int b = a; b < KT; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * a + Mf<double>::drow(lane, r), j = 16 * b + r16;
+            red[i][j] = ww == 0 ? acc[a][b][r] : red[i][j] + acc[a][b][r];
+          }
+    }
+    __syncthreads();
+  }
+  double* sb = slab + (int64_t)blockIdx.x * k * k;
+  for (int e = threadIdx.x; e < k * k; e += 256) {
+    const int i = e / k, j = e - i * k;
+    sb[e] = i <= j ? red[i][j] : red[j][i];
+  }
+}
+
 // C (mr x nc, ldc) = op(A) op(B), op(A) mr x kd, op(B) kd x nc, row-major f64,
-// one workgroup (k x k sizes of the core)
+// one workgroup (k x k sizes of the core): both operands staged in LDS first
+// when they fit (coalesced reads; the strided global form took ~36 us)
 __global__ void __launch_bounds__(256) k_ts_small(int ta, int tb, int mr, int nc, int kd, const double* __restrict__ A,
                                                   int lda, const double* __restrict__ B, int ldb,
                                                   double* __restrict__ C, int ldc) {
+  __shared__ double as[64 * 65], bs[64 * 65];
+  if (mr <= 64 && nc <= 64 && kd <= 64) {
+    // as[i][l] = op(A)[i][l], bs[j][l] = op(B)[l][j] (pitch 65: conflict-free rows)
+    for (int e = threadIdx.x; e < mr * kd; e += 256) {
+      if (ta) {   // A is kd x mr: as[i][l] = A[l][i]
+        const int l = e / mr, i = e - l * mr;
+        as[i * 65 + l] = A[l * lda + i];
+      } else {
+        const int i = e / kd, l = e - i * kd;
+        as[i * 65 + l] = A[i * lda + l];
+      }
+    }
+    for (int e = threadIdx.x; e < kd * nc; e += 256) {
+      if (tb) {
+        const int j = e / kd, l = e - j * kd;
+        bs[j * 65 + l] = B[j * ldb + l];
+      } else {
+        const int l = e / nc, j = e - l * nc;
+        bs[j * 65 + l] = B[l * ldb + j];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < mr * nc; e += 256) {
+      const int i = e / nc, j = e - i * nc;
+      double s = 0.0;
+      for (int l = 0; l < kd; ++l) s = fma(as[i * 65 + l], bs[j * 65 + l], s);
+      C[i * ldc + j] = s;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < mr * nc; e += 256) {
     const int i = e / nc, j = e - i * nc;
     double s = 0.0;
@@ -537,17 +765,26 @@ bool vec_ok(const T* A, int64_t lda, int64_t n) {
   return ((uintptr_t)A % 16) == 0 && lda % vw == 0 && n % vw == 0;
 }
 
+int g_az_split = 1;
+
 template <typename T, int KT>
 int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
   constexpr int LDS = az_lds<T, KT>();
+  constexpr int CW = AZ_NG * 4 * AZ_VL * Mf<T>::VW;
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
+  const int nchunk = (n + CW - 1) / CW;
+  // g <= nrb: every stream-K range spans at least one whole row block
   const int64_t g = nrb < 2 * (int64_t)ncu() ? nrb : 2 * (int64_t)ncu();
+  if (g > 1 && g_az_split) {
+    k_az_zero_cut<T><<<(unsigned)(g - 1), 256, 0, s>>>(Y, m, k, ldy, nrb, nchunk, (int)g);
+    SL_LAUNCH_CHECK();
+  }
   if (vec_ok(A, lda, n)) {
     SL_LDS_ATTR((k_ts_az<T, KT, true>), LDS);
-    k_ts_az<T, KT, true><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy);
+    k_ts_az<T, KT, true><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
   } else {
     SL_LDS_ATTR((k_ts_az<T, KT, false>), LDS);
-    k_ts_az<T, KT, false><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy);
+    k_ts_az<T, KT, false><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
   }
   SL_LAUNCH_CHECK();
   return SL_OK;
@@ -556,9 +793,13 @@ int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y
 // row groups of the A^T Q product: ~2 workgroups per CU over all slices
 template <typename T>
 void atq_geometry(int64_t m, int n, int* slices, int* groups, int64_t* rows_per) {
-  constexpr int CS = 8 * AT_V * 16 * (16 / (int)sizeof(T));
+  const int CS = 8 * g_atq_av * 16 * (16 / (int)sizeof(T));
   *slices = (n + CS - 1) / CS;
-  int64_t g = (2 * (int64_t)ncu() + *slices - 1) / *slices;
+  // AV = 2: one 512-thread workgroup per CU is resident (k_ts_atq needs >
+  // 128 VGPRs): slices x groups <= 2 x CUs is two full rounds (rounding the
+  // group count up left a third round of a few workgroups: f64 n = 5000
+  // ran 520 workgroups, ~50% over); AV = 1: two resident, one round
+  int64_t g = 2 * (int64_t)ncu() / *slices;
   const int64_t maxg = (m + 63) / 64;   // at least 64 rows per group
   if (g > maxg) g = maxg;
   if (g < 1) g = 1;
@@ -572,8 +813,14 @@ template <typename T, int KT>
 int launch_atq(const T* A, int64_t m, int n, int64_t lda, const T* Q, int k, T* slab, int slices, int groups,
                int64_t rp, hipStream_t s) {
   const dim3 grid((unsigned)slices, (unsigned)groups);
-  if (vec_ok(A, lda, n)) k_ts_atq<T, KT, true><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
-  else k_ts_atq<T, KT, false><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+  const bool v = vec_ok(A, lda, n);
+  if (g_atq_av == 1) {
+    if (v) k_ts_atq<T, KT, true, 1><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+    else k_ts_atq<T, KT, false, 1><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+  } else {
+    if (v) k_ts_atq<T, KT, true, 2><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+    else k_ts_atq<T, KT, false, 2><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+  }
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -620,6 +867,13 @@ SL_API int sl_ts_az(const void* A, int64_t m, int64_t n, int64_t lda, const void
   return az_dispatch<double>((const double*)A, m, (int)n, lda, (const double*)Z, k, (double*)Y, ldy, s);
 }
 
+// A/B knob: vectors per wave and row of A^T Q (1 or 2; plans size their
+// workspace with sl_ts_atq_workspace after setting it)
+SL_API void sl_ts_set_atq_av(int v) { g_atq_av = v == 1 ? 1 : 2; }
+
+// A/B knob: 1 (default) whole-block rounds + stream-K tail, 0 whole blocks round-robin
+SL_API void sl_ts_set_az_split(int v) { g_az_split = v ? 1 : 0; }
+
 // bytes of slab workspace sl_ts_atq needs
 SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt) {
   int slices = 0, groups = 0;
@@ -662,6 +916,20 @@ SL_API int sl_ts_xm64(const double* X, int64_t rows, int k, int64_t ldx, const d
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
+  if (k % 2 == 0 && ldx % 2 == 0 && ((uintptr_t)X & 15) == 0) {
+    // matrix-core form: 16-row tiles, two per wave and iteration
+    const int64_t t8 = ((rows + 15) / 16 + 7) / 8;
+    const unsigned g = (unsigned)(t8 < 2 * (int64_t)ncu() ? t8 : 2 * (int64_t)ncu());
+#define SL_XM(TO, KT2) k_ts_xm64m<TO, KT2><<<g, 256, 0, s>>>(X, rows, k, ldx, Mm, k2, (TO*)out, ldo)
+#define SL_XM2(TO) switch ((k2 + 15) / 16) { case 1: SL_XM(TO, 1); break; case 2: SL_XM(TO, 2); break; \
+                                             case 3: SL_XM(TO, 3); break; default: SL_XM(TO, 4); break; }
+    if (out_dt == SL_F32) { SL_XM2(float) }
+    else { SL_XM2(double) }
+#undef SL_XM2
+#undef SL_XM
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  }
   const int64_t tiles = (rows + 63) / 64;
   const unsigned g = (unsigned)(tiles < 4 * (int64_t)ncu() ? tiles : 4 * (int64_t)ncu());
   if (out_dt == SL_F32) k_ts_xm64<float><<<g, 256, 0, s>>>(X, rows, k, ldx, Mm, k2, (float*)out, ldo);
@@ -682,7 +950,12 @@ SL_API int sl_ts_gram64(const double* X, int64_t rows, int k, int64_t ldx, doubl
   hipStream_t s = (hipStream_t)stream;
   if (rows <= 0) return hipMemset2DAsync(G, (size_t)ldg * 8, 0, (size_t)k * 8, (size_t)k, s) == hipSuccess ? SL_OK : SL_ERR_HIP;
   const int g = gram_grid(rows);
-  k_ts_gram64<<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws);
+  switch ((k + 15) / 16) {
+    case 1: k_ts_gram64m<1><<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws); break;
+    case 2: k_ts_gram64m<2><<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws); break;
+    case 3: k_ts_gram64m<3><<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws); break;
+    default: k_ts_gram64m<4><<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws); break;
+  }
   SL_LAUNCH_CHECK();
   return sl_slab_reduce_launch_d2d((const double*)ws, g, (int64_t)k * k, k, k, k, G, ldg, s);
 }

@@ -33,8 +33,9 @@ def _st():
     return vp(torch.cuda.current_stream().cuda_stream)
 
 
+# (300_007, 200, 24, 4): whole-block rounds then the stream-K tail of k_ts_az
 SHAPES = [(100_003, 1000, 40, 0), (4_097, 1000, 40, 8), (777, 37, 20, 0), (129, 16, 1, 0), (2_500, 530, 64, 3),
-          (20_000, 5000, 40, 0), (64, 2049, 33, 0)]
+          (20_000, 5000, 40, 0), (64, 2049, 33, 0), (300_007, 200, 24, 4)]
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
@@ -70,6 +71,51 @@ def test_az_and_atq(L, dt, m, n, k, pad):
     assert torch.isfinite(W).all()
     assert ((W - wref).abs() <= 4 * eps * (m ** 0.5 + 4) * wmag + 1e-300).all(), \
         float(((W - wref).abs() / wmag).max())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_az_stream_k_deterministic(L, dt):
+    """Row blocks cut by a stream-K range boundary are summed from two atomic
+    partials: repeated calls must agree bit for bit."""
+    dev = torch.device("cuda")
+    m, n, k = 200_000, 777, 40
+    A = torch.randn(m, n + 1, device=dev, dtype=dt)[:, :n]
+    Z = torch.randn(n, k, device=dev, dtype=dt)
+    code = F32 if dt == torch.float32 else F64
+    outs = []
+    for _ in range(3):
+        Y = torch.full((m, k), float("nan"), device=dev, dtype=dt)
+        L.call("sl_ts_az", vp(A.data_ptr()), m, n, n + 1, vp(Z.data_ptr()), k, vp(Y.data_ptr()), k, code, _st())
+        outs.append(Y)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ref = A.double() @ Z.double()
+    tol = 1e-4 if dt == torch.float32 else 1e-12
+    assert torch.allclose(outs[0].double(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("m,n,k", [(100_003, 1000, 40), (2_500, 530, 64), (777, 37, 20)])
+def test_atq_one_vector_variant(L, m, n, k):
+    """A^T Q with one vector per wave and row (two workgroups per CU)."""
+    dev = torch.device("cuda")
+    _lib = L
+    _lib.register("sl_ts_set_atq_av", [i32], None)
+    try:
+        _lib.require().sl_ts_set_atq_av(1)
+        for dt, code in ((torch.float32, F32), (torch.float64, F64)):
+            A = torch.randn(m, n, device=dev, dtype=dt)
+            Q = torch.randn(m, k, device=dev, dtype=dt)
+            ws = torch.zeros(int(_lib.require().sl_ts_atq_workspace(m, n, k, code)), dtype=torch.uint8, device=dev)
+            W = torch.full((n, k), float("nan"), device=dev, dtype=torch.float64)
+            _lib.call("sl_ts_atq", vp(A.data_ptr()), m, n, n, vp(Q.data_ptr()), k, vp(W.data_ptr()), k,
+                      vp(ws.data_ptr()), code, _st())
+            torch.cuda.synchronize()
+            ref = A.double().t() @ Q.double()
+            tol = 1e-4 if dt == torch.float32 else 1e-12
+            assert torch.allclose(W, ref, rtol=tol, atol=tol * ref.abs().max().item())
+    finally:
+        _lib.require().sl_ts_set_atq_av(2)
 
 
 def test_unaligned_lda_scalar_path(L):
