@@ -163,6 +163,9 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
   // alone (no priority) measured 1013 / 1115.  A ring of four K-half slots
   // (each half's DMA three phases ahead, one counted wait + barrier per K
   // half) lost: 938 / 1052 vs 1159 / 1158 TF (profiles/r5/gemm_nt_ring_ab.jsonl).
+  // A persistent short-K form (next tile's slice 0 in flight during the
+  // epilogue, +- a start stagger) measured no gain at K = 512 and lost at
+  // K = 1024 (profiles/r5/gemm_nt_pers_ab.jsonl).
   bf16x8 a0[8], b0[4], a1[8], b1[4];
   issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
