@@ -46,3 +46,18 @@ def test_gemm_nt_bf16_out_and_cos_epilogue():
     sh = torch.rand(N, device="cuda") * 6.28
     Z = gemm.gemm_nt(A, B, alpha=0.3, cos_scales=sc, cos_shifts=sh)
     torch.testing.assert_close(Z, 0.3 * torch.cos(ref * sc + sh), rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("cos", [False, True])
+def test_gemm_nt_bf16_out_is_rne_of_f32_out(cos):
+    """bf16 output = round-to-nearest-even of the f32 output, bit for bit (the
+    epilogue converts with the hardware v_cvt_pk_bf16_f32)."""
+    M, N, K = 1000, 777, 192
+    A, B, _ = _ops(M, N, K, 11)
+    kw = {}
+    if cos:
+        kw = dict(alpha=0.3, cos_scales=torch.rand(N, device="cuda") * 0.2,
+                  cos_shifts=torch.rand(N, device="cuda") * 6.28)
+    C32 = gemm.gemm_nt(A, B, **kw)
+    C16 = gemm.gemm_nt(A, B, out_dtype=torch.bfloat16, **kw)
+    assert torch.equal(C16, C32.bfloat16())
