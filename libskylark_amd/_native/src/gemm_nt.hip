@@ -93,7 +93,8 @@ template <int EPI, typename OutT, bool ACC, bool FROW>
 __global__ void __launch_bounds__(NT, 1)
 k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb, int M, int N, int K,
           OutT* __restrict__ C, int64_t ldc, float alpha, const float* __restrict__ scales,
-          const float* __restrict__ shifts, const float* __restrict__ uterm, float p0, int ntm, int ntn, int per) {
+          const float* __restrict__ shifts, const float* __restrict__ uterm, float p0, int ntm, int ntn, int per,
+          int ntst) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];
 
   // ---- XCD-aware grouped tile order
@@ -267,7 +268,8 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
           if constexpr (sizeof(OutT) == 4) {
             float4 o = v;
             if (ACC) { const float4 c = *(const float4*)p; o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w; }
-            *(float4*)p = o;
+            if (ntst) __builtin_nontemporal_store(f32x4{o.x, o.y, o.z, o.w}, (f32x4*)p);
+            else *(float4*)p = o;
           } else {
             float o[4] = {v.x, v.y, v.z, v.w};
             if (ACC) {
@@ -275,7 +277,10 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
               o[0] += bf16_to_f((bf16_t)(c.x & 0xffff)); o[1] += bf16_to_f((bf16_t)(c.x >> 16));
               o[2] += bf16_to_f((bf16_t)(c.y & 0xffff)); o[3] += bf16_to_f((bf16_t)(c.y >> 16));
             }
-            *(uint2*)p = make_uint2(hw_bf16x2(o[0], o[1]), hw_bf16x2(o[2], o[3]));
+            const uint2 q = make_uint2(hw_bf16x2(o[0], o[1]), hw_bf16x2(o[2], o[3]));
+            typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+            if (ntst) __builtin_nontemporal_store(u32x2{q.x, q.y}, (u32x2*)p);
+            else *(uint2*)p = q;
           }
         } else {
           const float o[4] = {v.x, v.y, v.z, v.w};
@@ -296,6 +301,13 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
 
 
 
+// C written with non-temporal stores when it is large (>= 64 MiB) and K is
+// short (<= 2048: the C write is then a large share of the traffic and would
+// only evict the A / B panels the K loop re-reads from L2; 1e6 x 4096 x 512
+// with the cos map: bf16 out 5.50 -> 5.03 ms, f32 out 5.99 -> 5.73 ms,
+// profiles/r5/gemm_nt_epilogue_v2.jsonl).  A/B knob: -1 auto, 0 off, 1 on.
+int g_nt_store = -1;
+
 template <int EPI, typename OutT, bool ACC, bool FROW = false>
 int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, void* C, int64_t ldc,
            float alpha, const float* scales, const float* shifts, hipStream_t s, const float* uterm = nullptr,
@@ -303,9 +315,11 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N,
   const int ntm = (M + BM - 1) / BM, ntn = (N + BN - 1) / BN;
   const int tiles = ntm * ntn;
   const int per = (tiles + 7) / 8;
+  const int nt = g_nt_store >= 0 ? g_nt_store
+                                 : ((double)M * N * sizeof(OutT) >= 64.0 * (1 << 20) && K <= 2048 ? 1 : 0);
   k_gemm_nt<EPI, OutT, ACC, FROW><<<(unsigned)(per * 8), NT, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)B, ldb, M,
                                                                       N, K, (OutT*)C, ldc, alpha, scales, shifts,
-                                                                      uterm, p0, ntm, ntn, per);
+                                                                      uterm, p0, ntm, ntn, per, nt);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
@@ -387,6 +401,9 @@ k_split_t(const float* __restrict__ X, int w, int m, int64_t ldx, bf16_t* __rest
 // C (M x N, ldc) = alpha A B^T (+ C when accumulate) with A M x K, B N x K
 // bf16 row-major (lda, ldb elements, 16-B aligned rows), K % 64 == 0.
 // epi 1: C = alpha * cos(scales[n] * (A B^T) + shifts[n]).  out: SL_F32 / SL_BF16.
+// A/B knob: non-temporal C stores, -1 auto (large C), 0 off, 1 on
+SL_API void sl_gemm_nt_set_nt_store(int v) { g_nt_store = v < 0 ? -1 : (v ? 1 : 0); }
+
 SL_API int sl_gemm_nt_bf16(const void* A, int64_t lda, const void* B, int64_t ldb, int M, int N, int K, void* C,
                            int64_t ldc, int out_dtype, int accumulate, int epi, float alpha, const float* scales,
                            const float* shifts, void* stream) {
