@@ -3,7 +3,7 @@ current Python device path: singular values, subspace agreement, U
 orthogonality, residual, per-call time (graph replay + finish) and the device
 Jacobi eigensolver against numpy on random symmetric matrices.
 
-usage: python benchmarks/engine_probe.py [m]"""
+usage: python benchmarks/probe/engine_probe.py [m]"""
 from __future__ import annotations
 
 import ctypes as C
@@ -13,7 +13,7 @@ import os
 import statistics
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -959,7 +959,7 @@ inline int kernel_gram(const Kern& kk, int dirX, int dirY, const DevMat& X, cons
   const int dt = X.dtype;
   if ((dt != F32 && dt != F64) || Y.dtype != dt || K.dtype != dt)
     return fail(103, "device kernel_gram: X, Y, K must share dtype f32 or f64");
-  const bool xr = dirX == 2, yr = dirY == 2;
+  const bool xr = dirX != 1, yr = dirY != 1;   // 1 = SL_COLUMNS, anything else rows
   const int64_t mx = xr ? X.m : X.n, dx = xr ? X.n : X.m;
   const int64_t ny = yr ? Y.m : Y.n, dy = yr ? Y.n : Y.m;
   if (dx != dy || dx != kk.N) return fail(104, "device kernel_gram: point dimension mismatch");
@@ -1019,7 +1019,8 @@ inline int kernel_gram(const Kern& kk, int dirX, int dirY, const DevMat& X, cons
 inline int kernel_gram_host(const Kern& kk, int dirX, int dirY, const double* X, int64_t xm, int64_t xn,
                             const double* Y, int64_t ym, int64_t yn, double* K, int64_t km, int64_t kn) {
   Lib& L = lib();
-  const int64_t nx = dirX == 2 ? xm : xn, ny = dirY == 2 ? ym : yn;
+  // SL_COLUMNS (1): points are the columns; any other value: rows (reference ckernel.cpp:112-115)
+  const int64_t nx = dirX == 1 ? xn : xm, ny = dirY == 1 ? yn : ym;
   if (km != nx || kn != ny) return fail(104, "sl_kernel_gram: K must be (#X points) x (#Y points)");
   Buf dX(std::max<int64_t>(1, xm * xn) * 8), dY(std::max<int64_t>(1, ym * yn) * 8),
       dK(std::max<int64_t>(1, km * kn) * 8);

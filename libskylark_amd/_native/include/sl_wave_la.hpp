@@ -246,6 +246,89 @@ __device__ __forceinline__ void wg_chol_inv(const double* G, int ldg, double* X,
   }
 }
 
+// The same X with the elimination taken TWO pivots per step: the owners of
+// rows j and j + 1 publish both (one barrier per pair instead of one per
+// pivot), every lane forms row j + 1 after pivot j itself (r1' = r_{j+1} -
+// f r_j, f = G[j+1][j] / d_j, d_{j+1} = r1'[j + 1]), and each row i > j + 1
+// takes both updates at once: f_i = M[i][j] / d_j, g_i = (M[i][j+1] - f_i
+// r_j[j+1]) / d_{j+1}, M[i][c] -= f_i r_j[c] + g_i r1'[c] (c outside the pair),
+// the pair's columns switching to the L^{-1} entries (-f_i + g_i f, -g_i)
+// exactly as two single steps would leave them.  Pivot dropping as above.
+// K even, K % NW == 0; fsh >= 320 doubles of LDS (two double-buffered row
+// pairs + d).  Every thread of the workgroup calls it (waves >= NW only meet
+// the barriers).
+template <int K, int NW>
+__device__ __forceinline__ void wg_chol_inv2(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
+                                             int* st) {
+  static_assert(K % NW == 0 && K % 2 == 0 && K <= 64, "K");
+  constexpr int R = K / NW;
+  const int tid = threadIdx.x, c = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool act = w < NW;
+  double* rowbuf = fsh;        // [2][2][64]
+  double* dsh = fsh + 256;     // d_i (0: dropped)
+  double M[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int i = q * NW + w;
+    M[q] = !act ? 0.0 : ((i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0));
+  }
+  const double thr = 1e-13 * wave_max(c < k ? fabs(G[c * ldg + c]) : 0.0);
+  int bad = 0;
+#pragma unroll
+  for (int j = 0; j < K; j += 2) {
+    double* rb = rowbuf + ((j >> 1) & 1) * 128;
+    if (w == j % NW) rb[c] = M[j / NW];
+    if (w == (j + 1) % NW) rb[64 + c] = M[(j + 1) / NW];
+    __syncthreads();
+    const double r0 = rb[c], r1 = rb[64 + c];
+    const double d0 = rb[j], e01 = rb[j + 1], e10 = rb[64 + j], d1r = rb[64 + j + 1];
+    const bool ok0 = (d0 > thr && d0 == d0) || j >= k;
+    const double rc0 = ok0 ? rcp64(d0) : 0.0;
+    const double f1 = e10 * rc0;
+    const double d1 = fma(-f1, e01, d1r);
+    const bool ok1 = (d1 > thr && d1 == d1) || j + 1 >= k;
+    const double rc1 = ok1 ? rcp64(d1) : 0.0;
+    bad |= !ok0 || !ok1;
+    if (tid == 0) {
+      dsh[j] = ok0 ? d0 : 0.0;
+      dsh[j + 1] = ok1 ? d1 : 0.0;
+    }
+    const double r1p = c == j ? -f1 : fma(-f1, r0, r1);   // row j + 1 after pivot j
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int i = q * NW + w;
+        if (i > j + 1) {
+          const double fi = lane_d(M[q], j) * rc0;
+          const double gi = fma(-fi, e01, lane_d(M[q], j + 1)) * rc1;
+          const double v = fma(-gi, r1p, fma(-fi, r0, M[q]));
+          M[q] = c == j ? fma(gi, f1, -fi) : (c == j + 1 ? -gi : v);
+        } else if (i == j + 1) {
+          M[q] = c == j + 1 ? 1.0 : r1p;
+        } else if (i == j) {
+          M[q] = c == j ? 1.0 : (c == j + 1 ? 0.0 : M[q]);
+        } else {
+          M[q] = (c == j || c == j + 1) ? 0.0 : M[q];
+        }
+      }
+    }
+  }
+  if (bad && tid == 0) atomicOr(st, 1);
+  __syncthreads();
+  if (act && c < k) {
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = q * NW + w;
+      if (i < k) {
+        const double di = dsh[i];
+        const double rs = di > 0.0 ? rsq64(di) : 0.0;
+        X[c * ldx + i] = i >= c ? M[q] * rs : 0.0;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------- tridiagonalisation
 // T = Q^T C Q, Q = H_0 H_1 ... H_{K-3}, H_j = I - 2 v_j v_j^T, by ONE wave:
 // lane i keeps row i of the trailing matrix in registers.  Step j: ||x||

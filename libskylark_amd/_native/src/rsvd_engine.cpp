@@ -22,6 +22,7 @@
 // C, by a NativeComm RCCL communicator (sl_rsvd_run_comm) -- no interpreter.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -98,6 +99,17 @@ struct Plan {
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
+// LDS-DMA cache policy of the passes (sl_rsvd_pass variant bits 9-11; env
+// SL_PASS_NT overrides, for A/B runs)
+int pass_nt_code() {
+  static int c = -1;
+  if (c < 0) {
+    const char* e = std::getenv("SL_PASS_NT");
+    c = e ? (std::atoi(e) & 7) : 0;
+  }
+  return c;
+}
+
 // launch a deferred FJLT operator (and, with tab, the pointer-table write)
 int flush_fjlt(Plan* p, hipStream_t s, float** tab = nullptr, float* a = nullptr, float* b = nullptr,
                float* c = nullptr) {
@@ -129,7 +141,7 @@ int seg(Plan* p, const void* A, int i, hipStream_t s, float* V = nullptr, float*
   // odd passes walk the row blocks backwards: each pass starts on the rows
   // the previous one read last, which are still in the MALL
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
-                    final_pass ? 1 : 0, (i & 1) ? 256 : 0, s);
+                    final_pass ? 1 : 0, ((i & 1) ? 256 : 0) | (pass_nt_code() << 9), s);
   if (rc != SL_OK) return rc;
   // the first reduce of the call also clears the status word (no memset node)
   return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,

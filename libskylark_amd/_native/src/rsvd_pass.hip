@@ -50,18 +50,32 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_base) {
 }
 
 // same with a wave-uniform 64-bit base in SGPRs and a per-lane 32-bit byte
-// offset (global_load_lds ... saddr form): no per-block address VALU
+// offset (global_load_lds ... saddr form): no per-block address VALU.
+// NT: the non-temporal policy (A is read once per pass: the stream alone
+// runs at 7.0 TB/s with it against 6.35 without, benchmarks/probe/dma_stream.hip)
+template <bool NT = false>
 __device__ __forceinline__ void glds16s(unsigned voff, const void* sbase, unsigned lds_base) {
   unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds_base)
-      : "memory");
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2 nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds_base)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds_base)
+        : "memory");
 }
 
 // s_waitcnt vmcnt(n) for a run-time (wave-uniform) n
@@ -197,8 +211,19 @@ struct P5Tiles {
   int rev;       // walk the row blocks last-to-first (variant bit 8): consecutive
                  // passes alternate, so a pass starts on the rows the previous
                  // one read last (still in the MALL)
+  int nt;        // LDS-DMA cache policy (variant bits 9-11): 0 default; 1 nt for
+                 // every block; c >= 2 nt except each workgroup's last
+                 // ntail = 8 (c - 1) blocks, which keep the default policy so
+                 // the next pass (walking the other way) finds them in the MALL
+  int ntail;
 };
 
+#ifndef P1_PD
+#define P1_PD 8   // step-1 A fragments in flight per y wave
+#endif
+#ifndef P3_PT
+#define P3_PT 4   // step-3 W tiles' A^T fragments in flight per wave
+#endif
 constexpr int P5_NBUF = 4, P5_BM = 16, P5_ROWB = 256, P5_REGION = 4096, P5_LPB = 4, P5_T1 = 2, P5_T2 = 12,
               P5_GS = 2;
 
@@ -301,10 +326,18 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
     const int64_t r0 = row0(blk);
     if (r0 + BM <= m) {
       const bf16_t* base = A + r0 * lda;
+      if (pt.nt && blk < nloc - pt.ntail) {
 #pragma unroll
-      for (int i = 0; i < LPB; ++i) {
-        const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
-        glds16s(voff[i], (const void*)base, dst);
+        for (int i = 0; i < LPB; ++i) {
+          const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
+          glds16s<true>(voff[i], (const void*)base, dst);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < LPB; ++i) {
+          const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(region + i * 1024));
+          glds16s<false>(voff[i], (const void*)base, dst);
+        }
       }
     } else {
 #pragma unroll
@@ -325,13 +358,50 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
   auto step1 = [&](int64_t jb) {
     if constexpr (YROLE) {
       const char* reg0 = ring + (int)(jb % NBUF) * 8 * REGION;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       const int sw = swz4<16>(i16);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
+      // The A fragments stream through a ring of P1_PD registers (that many
+      // LDS reads in flight) and the K steps alternate between two
+      // accumulators: written as one read -> MFMA chain, the compiler kept
+      // two reads in flight and every MFMA waited on an LDS round trip.
+      // Inter passes in the engine 361 -> 357 / 351 -> 338 us, the pass
+      // alone 409 -> 385 us (profiles/r6/pass_prefetch_ab_*.txt).
+      auto rd = [&](int ks) -> bf16x8 {
         const int chunk = ((ks & 3) << 2) + g4;
-        const bf16x8 af = *(const bf16x8*)(reg0 + (ks >> 2) * REGION + i16 * ROWB + ((chunk ^ sw) << 4));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zf[ks], acc, 0, 0, 0);
+        return *(const bf16x8*)(reg0 + (ks >> 2) * REGION + i16 * ROWB + ((chunk ^ sw) << 4));
+      };
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (FINAL) {
+        // (the FINAL form, whose W waves also store Y and form the Gram,
+        // keeps the compiler's order: the pinned ring below measured 20 us
+        // slower per pass there)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rd(ks), zf[ks], acc, 0, 0, 0);
+      } else {
+        constexpr int PD = P1_PD < KS ? P1_PD : KS;
+        // its own scheduling region, ordered: PD reads, then (MFMA, read)
+        // pairs, then the last PD MFMAs (left to itself the scheduler
+        // re-serialised the reads to save registers)
+        __builtin_amdgcn_sched_barrier(0);
+        bf16x8 afr[PD];
+#pragma unroll
+        for (int u = 0; u < PD; ++u) afr[u] = rd(u);
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 af = afr[ks % PD];
+          if (ks & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zf[ks], acc1, 0, 0, 0);
+          else acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, zf[ks], acc0, 0, 0, 0);
+          if (ks + PD < KS) afr[ks % PD] = rd(ks + PD);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
+#pragma unroll
+        for (int ks = 0; ks + PD < KS; ++ks) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, PD, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = acc0 + acc1;
       }
       const int64_t r0 = row0(jb);
       if (r0 + BM > m) {
@@ -437,29 +507,56 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
     }
     (void)GT;
     const int q = i16 >> 2, p = i16 & 3;
+    // the A^T fragment of W tile ct (two transposed LDS reads); a slot past
+    // this wave's count re-reads its first tile into an accumulator that is
+    // never stored (no branch in the MFMA stream)
+    auto tile_rd = [&](int ct) -> bf16x8 {
+      const int gt = tbase + (YROLE || ct < tcnt ? ct : 0);
+      const char* region = slotp + (gt >> 3) * REGION;
+      const int chunk = 2 * (gt & 7) + (p >> 1);
+      const int ra = rb + q, rbb = rb + 4 + q;
+      const char* aa = region + ra * ROWB + ((chunk ^ swz4<16>(ra)) << 4) + (p & 1) * 8;
+      const char* ab2 = region + rbb * ROWB + ((chunk ^ swz4<16>(rbb)) << 4) + (p & 1) * 8;
+      const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)aa);
+      const s16x4 b4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)ab2);
+      s16x8 a8;
 #pragma unroll
-    for (int ct = 0; ct < TM; ++ct) {
-      {
-        // a slot past this wave's count re-reads its first tile into an
-        // accumulator that is never stored (no branch in the MFMA stream)
-        const int gt = tbase + (YROLE || ct < tcnt ? ct : 0);
-        const char* region = slotp + (gt >> 3) * REGION;
-        const int chunk = 2 * (gt & 7) + (p >> 1);
-        const int ra = rb + q, rbb = rb + 4 + q;
-        const char* aa = region + ra * ROWB + ((chunk ^ swz4<16>(ra)) << 4) + (p & 1) * 8;
-        const char* ab2 = region + rbb * ROWB + ((chunk ^ swz4<16>(rbb)) << 4) + (p & 1) * 8;
-        const s16x4 a4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)aa);
-        const s16x4 b4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)ab2);
-        s16x8 a8;
+      for (int u = 0; u < 4; ++u) {
+        a8[u] = a4[u];
+        a8[4 + u] = b4[u];
+      }
+      return __builtin_bit_cast(bf16x8, a8);
+    };
+    if constexpr (FINAL) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          a8[u] = a4[u];
-          a8[4 + u] = b4[u];
-        }
-        const bf16x8 af8 = __builtin_bit_cast(bf16x8, a8);
+      for (int ct = 0; ct < TM; ++ct) {
+        const bf16x8 af8 = tile_rd(ct);
 #pragma unroll
         for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
       }
+    } else if constexpr (TM > 0) {
+      // P3_PT tiles' reads in flight, pinned like step 1's ring (the
+      // scheduler's own order kept one or two tiles ahead)
+      constexpr int PT = P3_PT < TM ? P3_PT : TM;
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 tfr[PT];
+#pragma unroll
+      for (int u = 0; u < PT; ++u) tfr[u] = tile_rd(u);
+#pragma unroll
+      for (int ct = 0; ct < TM; ++ct) {
+        const bf16x8 af8 = tfr[ct % PT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) accW[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af8, yfr[t], accW[ct][t], 0, 0, 0);
+        if (ct + PT < TM) tfr[ct % PT] = tile_rd(ct + PT);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * PT, 1);
+#pragma unroll
+      for (int ct = 0; ct + PT < TM; ++ct) {
+        __builtin_amdgcn_sched_group_barrier(0x008, KT, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, KT * PT, 1);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -601,6 +698,11 @@ int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Z
   P5Tiles pt{};
   pt.prio = (variant >> 6) & 3;
   pt.rev = (variant >> 8) & 1;
+  {
+    const int c = (variant >> 9) & 7;
+    pt.nt = c != 0;
+    pt.ntail = c >= 2 ? 8 * (c - 1) : 0;
+  }
   if (!p5_tiles(n, KT, &pt)) {
     sl_set_last_error("rsvd_pass: no tile split for this n / k");
     return SL_ERR_UNSUPPORTED;
@@ -655,7 +757,8 @@ SL_API int64_t sl_rsvd_pass_workspace(int64_t m, int64_t n, int k) {
 // k; Y = y_hi + y_lo, the bf16 pair W is formed from) and the fp64 Gram slabs
 // of that Y (exact bf16 products, f32 per 16-row block, f64 across blocks);
 // final = 2: W slabs and Y only.  variant bits: 256 = walk the row blocks
-// last-to-first, 64/128 = y-wave priority (tuning).
+// last-to-first, 64/128 = y-wave priority (tuning), bits 9-11 the LDS-DMA
+// cache policy (P5Tiles::nt).
 SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt, int k, void* ws,
                         float* Y, int64_t ldy, int final_pass, int variant, void* stream) {
   if (m <= 0) return SL_OK;

@@ -95,6 +95,14 @@ def _gram(Z: torch.Tensor, dt) -> torch.Tensor:
     otherwise the GEMM in the compute dtype."""
     if Z.dtype == torch.bfloat16 and Z.is_cuda:
         try:
+            # split-K as a batch: Z^T Z over 1e6 rows is a 1024 x 1024 output,
+            # 16 output tiles for one GEMM on 256 CUs; 16 row slices fill the
+            # chip (1e6 x 1024: 3.9 -> 2.0 ms, profiles/r6/admm_gram_ab.json)
+            ni = Z.shape[0]
+            b = next((b for b in (16, 8, 4, 2) if ni % b == 0 and ni // b >= 4096), 1)
+            if b > 1 and Z.is_contiguous():
+                Zb = Z.view(b, ni // b, Z.shape[1])
+                return torch.bmm(Zb.transpose(1, 2), Zb, out_dtype=torch.float32).sum(0).to(torch.float64)
             return torch.mm(Z.t(), Z, out_dtype=torch.float32).to(torch.float64)
         except (RuntimeError, TypeError):
             pass

@@ -612,27 +612,28 @@ def _gen_ok(A_loc, n, k) -> bool:
             and A_loc.stride(1) == 1 and A_loc.stride(0) >= n and 1 <= k <= min(n, 128) and A_loc.shape[0] >= 1)
 
 
-_AGREED: dict = {}
+_DUMMY: dict = {}
 
 
-def _agree_engines(comm, A_loc, fused: bool, gen: bool):
-    """(fused, gen) agreed by every rank: a rank that owns no rows (or any
-    other local reason) must not send the others into segments whose
-    collectives it never joins -- one all-reduce (min) per operand geometry,
-    cached."""
-    if comm.size <= 1:
-        return fused, gen
-    key = (A_loc.data_ptr(), tuple(A_loc.shape), A_loc.dtype, comm.size, id(getattr(comm, "group", None)))
-    got = _AGREED.get(key)
-    if got is None:
-        f = torch.tensor([1.0 if fused else 0.0, 1.0 if gen else 0.0], dtype=torch.float64, device=A_loc.device)
-        comm.all_reduce_min(f)
-        got = (bool(f[0] > 0.5), bool(f[1] > 0.5))
-        if len(_AGREED) >= 16:
-            _AGREED.pop(next(iter(_AGREED)))
-        _AGREED[key] = got
-    return got
-
+def _uniform_shard(A_loc, n):
+    """(shard, rows) with the engine choice a function of rank-uniform values
+    only (n, k, dtype, device type), so every rank of a multi-rank call picks
+    the same engine and joins the same collectives with no agreement round:
+    a rank that owns no rows runs on one zero row (it adds nothing to any
+    sum; its U slice is cut back to 0 rows), and a shard whose strides the
+    engines cannot take is made contiguous (rows % 8 == 0 then depends on n
+    alone).  (A rank-local cache of an agreement collective could let one
+    rank skip the collective another one enters.)"""
+    rows = A_loc.shape[0]
+    if rows == 0:
+        key = (n, A_loc.dtype, str(A_loc.device))
+        z = _DUMMY.get(key)
+        if z is None:
+            z = _DUMMY[key] = torch.zeros(1, n, dtype=A_loc.dtype, device=A_loc.device)
+        return z, 0
+    if A_loc.stride(1) != 1 or A_loc.stride(0) < n or (n % 8 == 0 and A_loc.stride(0) % 8 != 0):
+        A_loc = A_loc.contiguous()
+    return A_loc, rows
 
 
 def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
@@ -641,7 +642,10 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
     engine (one read of A per pass); any other f32 / f64 / bf16 A with k <= 128:
     the general-precision engine.  Returns None when neither covers the call
     (the caller then runs the host-driven path)."""
-    fused, gen = _agree_engines(comm, A_loc, _engine_ok(A_loc, n, k), _gen_ok(A_loc, n, k))
+    rows = A_loc.shape[0]
+    if comm.size > 1:
+        A_loc, rows = _uniform_shard(A_loc, n)
+    fused, gen = _engine_ok(A_loc, n, k), _gen_ok(A_loc, n, k)
     if not fused and not gen:
         return None
     if _TRACE:
@@ -690,6 +694,8 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
             plan = _GenPlan(A_loc, comm, n, rank, k, q)
         _PLANS[key] = plan
     out = plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
+    if rows != A_loc.shape[0]:
+        out = (out[0][:rows],) + tuple(out[1:])   # a rank without rows ran on one zero row
     check = params.check if params.check is not None else isinstance(plan, _GenPlan)
     if check:
         plan.check()

@@ -183,7 +183,3 @@ class WCache:
     def clear(self):
         self._d.clear()
 
-
-# kept for the dense_sketch hook
-def dense_sketch_fused_ok(A, dim, s, k, m) -> bool:
-    return False

@@ -19,6 +19,7 @@ import math
 import weakref
 
 import torch
+from ..utils.devcache import version_of
 
 
 def _move(x, dim):
@@ -315,13 +316,13 @@ def fjlt_fourstep(A: torch.Tensor, d: torch.Tensor, samples: torch.Tensor, scale
     # memory was reused for different samples
     key = (samples.data_ptr(), samples.numel(), N, str(A.device))
     plan = _FS_PLANS.get(key)
-    if plan is not None and (plan.src() is not samples or plan.version != samples._version):
+    if plan is not None and (plan.src() is not samples or plan.version != version_of(samples)):
         plan = None
     if plan is None:
         if len(_FS_PLANS) >= 8:
             _FS_PLANS.pop(next(iter(_FS_PLANS)))
         plan = _FourStepPlan(N, samples, A.device)
-        plan.src, plan.version = weakref.ref(samples), samples._version
+        plan.src, plan.version = weakref.ref(samples), version_of(samples)
         _FS_PLANS[key] = plan
     st = C.c_void_p(L.stream_of(A))
     dd = _device_copy(d, A.device, torch.float32)

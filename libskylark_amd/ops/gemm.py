@@ -18,6 +18,14 @@ from . import _lib
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_gemm_nt_bf16", [vp, i64, vp, i64, i32, i32, i32, vp, i64, i32, i32, i32, C.c_float, vp, vp, vp])
 _lib.register("sl_split_bf16_t", [vp, i32, i32, i64, vp, vp, i32, i64, vp])
+_lib.register("sl_gemm_nt_set_nt_store", [i32], None)
+
+
+def set_nt_store(mode: int) -> None:
+    """C-store cache policy of the NT GEMM: -1 auto (non-temporal stores for
+    C >= 64 MiB at K <= 2048, the default), 0 always default, 1 always
+    non-temporal.  Process-wide (an A/B and test knob)."""
+    _lib.require().sl_gemm_nt_set_nt_store(int(mode))
 
 BK = 64
 

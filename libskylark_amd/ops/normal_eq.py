@@ -112,6 +112,10 @@ def gemv(A: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     m, n = A.shape
     k = X2.shape[1]
     Xt = X2.to(torch.float32).t().contiguous()
+    if Xt.data_ptr() % 16:
+        # a contiguous view at an unaligned storage offset passes through
+        # .contiguous() unchanged; the kernel reads X in 16-B pieces
+        Xt = Xt.clone()
     Y = torch.empty(m, k, dtype=torch.float32, device=A.device)
     _lib.call("sl_gemv_rows_f32", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Xt), k, _lib.ptr(Y), Y.stride(0),
               C.c_void_p(_lib.stream_of(A)))

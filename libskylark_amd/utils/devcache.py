@@ -16,6 +16,15 @@ _COPIES: dict = {}
 _MAX = 32
 
 
+def version_of(t: torch.Tensor) -> int:
+    """``t._version``, or -1 for an inference tensor (created under
+    ``torch.inference_mode()``: it has no version counter, and it cannot be
+    modified in place outside inference mode, so identity alone keys it)."""
+    if t.is_inference():
+        return -1
+    return t._version
+
+
 def device_copy(t: torch.Tensor, dev, dtype=None) -> torch.Tensor:
     """``t.to(device=dev, dtype=dtype).contiguous()``, uploaded once per
     (tensor object, version, device, dtype)."""
@@ -25,10 +34,10 @@ def device_copy(t: torch.Tensor, dev, dtype=None) -> torch.Tensor:
         return t
     key = (id(t), str(dev), dtype)
     hit = _COPIES.get(key)
-    if hit is not None and hit[0]() is t and hit[1] == t._version:
+    if hit is not None and hit[0]() is t and hit[1] == version_of(t):
         return hit[2]
     out = t.to(device=dev, dtype=dtype).contiguous()
     if len(_COPIES) >= _MAX:
         _COPIES.pop(next(iter(_COPIES)))
-    _COPIES[key] = (weakref.ref(t), t._version, out)
+    _COPIES[key] = (weakref.ref(t), version_of(t), out)
     return out

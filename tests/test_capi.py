@@ -803,7 +803,10 @@ C_HOST_DEVICE_PROGRAM = textwrap.dedent(r"""
         if ((rc = sl_kernel_gram(2, 1, kg, "Matrix", W(B, 9, N), "Matrix", W(A, N, 7), "Matrix", W(Kg, 9, 7)))) return fail(73, rc);
         if ((rc = sl_kernel_gram(1, 2, kl, "Matrix", W(A, N, 7), "Matrix", W(B, 9, N), "Matrix", W(Kl, 7, 9)))) return fail(74, rc);
         if ((rc = sl_kernel_gram(2, 2, kp, "Matrix", W(B, 9, N), "Matrix", W(B, 9, N), "Matrix", W(Kp, 9, 9)))) return fail(75, rc);
-        dump("kg", Kg, 8 * 9 * 7); dump("kl", Kl, 8 * 7 * 9); dump("kp", Kp, 8 * 9 * 9);
+        /* direction 0 is not SL_COLUMNS: rows (reference ckernel.cpp maps only 1 to columns) */
+        double* Kg0 = malloc(8 * 9 * 7);
+        if ((rc = sl_kernel_gram(0, 1, kg, "Matrix", W(B, 9, N), "Matrix", W(A, N, 7), "Matrix", W(Kg0, 9, 7)))) return fail(76, rc);
+        dump("kg", Kg, 8 * 9 * 7); dump("kl", Kl, 8 * 7 * 9); dump("kp", Kp, 8 * 9 * 9); dump("kg0", Kg0, 8 * 9 * 7);
         sl_free_kernel(kg); sl_free_kernel(kl); sl_free_kernel(kp);
         printf("%d\n", sl_runtime_started());
         for (int t = 0; t < 18; ++t) sl_free_sketch_transform(T[t]);
@@ -910,6 +913,7 @@ def test_host_operands_on_device_interpreter_free(capi, tmp_path):
     kg = sk.ml.Gaussian(300, sigma=0.9)
     kl = sk.ml.Laplacian(300, sigma=1.7)
     kp = sk.ml.Polynomial(300, q=2, c=1.0, gamma=0.01)
+    np.testing.assert_array_equal(ld("kg0", (9, 7)), ld("kg", (9, 7)))
     np.testing.assert_allclose(ld("kg", (9, 7)), kg.gram(Bp, dirX="rows", dirY="columns", Y=Xp).numpy(),
                                rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(ld("kl", (7, 9)), kl.gram(Xp, dirX="columns", dirY="rows", Y=Bp).numpy(),

@@ -143,3 +143,25 @@ def test_fjlt_direct_fused_vs_explicit(dev, dim):
     out = T.apply(Ad, dim=dim).double().cpu()
     ref = P @ Ad.double().cpu() if dim == 0 else Ad.double().cpu() @ P.t()
     assert (out - ref).abs().max().item() < 3e-5 * float(ref.abs().max())
+
+
+def test_feature_map_large_output_nt_stores(dev):
+    """GaussianRFT rowwise on 4160 x 512 f32 -> 4096 features: a 68 MB f32
+    output at K = 3 x 512 (the f32-exact split), where the NT GEMM's auto rule
+    turns on non-temporal C stores; against the CPU fp64 path."""
+    N, S, M = 512, 4096, 4160
+    T = sk.sketch.GaussianRFT(N, S, context=sk.Context(21), sigma=8.0)
+    g = torch.Generator().manual_seed(4)
+    A = torch.rand(M, N, generator=g, dtype=torch.float64)
+    ref = T.apply(A, dim=1)
+    Ad = A.to(dev, torch.float32)
+    assert F.fused_ok(Ad, 1, N, S)
+    out = T.apply(Ad, dim=1)
+    assert out.numel() * out.element_size() >= 64 << 20
+    W = T.realize_W(torch.float64)
+    bound = W.abs().sum(1) * float(A.abs().max())
+    if getattr(T, "scales", None) is not None:
+        bound = bound * T.scales.double().cpu()
+    tol = T.outscale * (5e-5 * bound + 1e-4)
+    err = (out.double().cpu() - ref).abs().max(dim=0).values
+    assert bool((err <= tol).all()), float((err - tol).max())

@@ -61,3 +61,52 @@ def test_gemm_nt_bf16_out_is_rne_of_f32_out(cos):
     C32 = gemm.gemm_nt(A, B, **kw)
     C16 = gemm.gemm_nt(A, B, out_dtype=torch.bfloat16, **kw)
     assert torch.equal(C16, C32.bfloat16())
+
+
+@pytest.fixture
+def nt_store_on():
+    gemm.set_nt_store(1)
+    try:
+        yield
+    finally:
+        gemm.set_nt_store(-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 700, 320), (513, 1300, 1024), (2100, 600, 2048)])
+def test_gemm_nt_forced_nt_store_matches(nt_store_on, M, N, K):
+    """Non-temporal C stores forced on (the default only turns them on for C
+    >= 64 MiB at K <= 2048): f32 out, bf16 out, the cos map and the
+    accumulate path against fp32 torch, edge tiles included."""
+    A, B, ref = _ops(M, N, K, 7 * M + N)
+    tol = 1e-4 * float(ref.abs().max())
+    torch.testing.assert_close(gemm.gemm_nt(A, B, alpha=0.5), 0.5 * ref, rtol=0, atol=tol)
+    Cb = gemm.gemm_nt(A, B, out_dtype=torch.bfloat16)
+    torch.testing.assert_close(Cb.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    sc = torch.rand(N, device="cuda") * 0.2
+    sh = torch.rand(N, device="cuda") * 6.28
+    Z = gemm.gemm_nt(A, B, alpha=0.3, cos_scales=sc, cos_shifts=sh)
+    torch.testing.assert_close(Z, 0.3 * torch.cos(ref * sc + sh), rtol=0, atol=2e-4)
+    base = torch.randn(M, N, device="cuda")
+    out = base.clone()
+    gemm.gemm_nt(A, B, out=out, accumulate=True)
+    torch.testing.assert_close(out, base + ref, rtol=0, atol=tol)
+    # bit-identical to the default store policy (only the cache policy differs)
+    gemm.set_nt_store(0)
+    assert torch.equal(gemm.gemm_nt(A, B, alpha=0.3, cos_scales=sc, cos_shifts=sh), Z)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_nt_auto_nt_store_large_output(out_dtype):
+    """A cos-map output over the auto rule's 64 MiB threshold (f32: 16640 x
+    1040 x 4 B = 69 MB, bf16 at 2 x the rows) at K = 512: the production
+    feature-map path with non-temporal stores, against fp32 torch."""
+    M = 16640 if out_dtype == torch.float32 else 33280
+    N, K = 1040, 512
+    A, B, ref = _ops(M, N, K, 99)
+    assert M * N * (4 if out_dtype == torch.float32 else 2) >= 64 << 20
+    sc = torch.rand(N, device="cuda") * 0.2
+    sh = torch.rand(N, device="cuda") * 6.28
+    Z = gemm.gemm_nt(A, B, alpha=0.3, cos_scales=sc, cos_shifts=sh, out_dtype=out_dtype)
+    want = 0.3 * torch.cos(ref * sc + sh)
+    atol = 2e-4 if out_dtype == torch.float32 else 2e-3
+    torch.testing.assert_close(Z.float(), want, rtol=0, atol=atol)
