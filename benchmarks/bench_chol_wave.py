@@ -23,7 +23,7 @@ for k in (40, 48, 32, 64):
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     R = torch.empty(k, k, dtype=torch.float64, device=dev)
     s = vp(torch.cuda.current_stream().cuda_stream)
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2, 3, 4, 5):
         _lib.require().sl_chol_inv_set_variant(v)
         f = lambda: _lib.call("sl_chol_inv_wave", _lib.ptr(G), k, k, _lib.ptr(R), _lib.ptr(st), s)  # noqa: E731
         for _ in range(5):
@@ -36,5 +36,5 @@ for k in (40, 48, 32, 64):
         e1.record()
         torch.cuda.synchronize()
         err = float((R.t() @ G @ R - torch.eye(k, dtype=torch.float64, device=dev)).abs().max())
-        print(json.dumps({"k": k, "variant": ["one_wave", "rows_over_4_waves", "pairs_4_waves", "pairs_8_waves"][v], "us": round(e0.elapsed_time(e1) * 1e3 / 200, 2),
+        print(json.dumps({"k": k, "variant": ["one_wave", "rows_over_4_waves", "pairs_4_waves", "pairs_8_waves", "quads_4_waves", "quads_8_waves"][v], "us": round(e0.elapsed_time(e1) * 1e3 / 200, 2),
                           "orth_err": err, "status": int(st.item())}))

@@ -246,27 +246,31 @@ __device__ __forceinline__ void wg_chol_inv(const double* G, int ldg, double* X,
   }
 }
 
-// The same X with the elimination taken TWO pivots per step: the owners of
-// rows j and j + 1 publish both (one barrier per pair instead of one per
-// pivot), every lane forms row j + 1 after pivot j itself (r1' = r_{j+1} -
-// f r_j, f = G[j+1][j] / d_j, d_{j+1} = r1'[j + 1]), and each row i > j + 1
-// takes both updates at once: f_i = M[i][j] / d_j, g_i = (M[i][j+1] - f_i
-// r_j[j+1]) / d_{j+1}, M[i][c] -= f_i r_j[c] + g_i r1'[c] (c outside the pair),
-// the pair's columns switching to the L^{-1} entries (-f_i + g_i f, -g_i)
-// exactly as two single steps would leave them.  Pivot dropping as above.
-// K even, K % NW == 0; fsh >= 320 doubles of LDS (two double-buffered row
-// pairs + d).  Every thread of the workgroup calls it (waves >= NW only meet
-// the barriers).
-template <int K, int NW>
-__device__ __forceinline__ void wg_chol_inv2(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
+// The same X with the elimination taken B pivots per step (B = 2 or 4): the
+// owners of rows j .. j + B - 1 publish them (one barrier per block of
+// pivots instead of one per pivot); every lane runs the block's own
+// elimination on its column (the B x B pivot block's scalars -- pivots d and
+// multipliers f -- are formed redundantly by every lane from broadcast
+// reads), and each row i below the block takes all B updates at once: its
+// multipliers m_t come from its block-column entries, read by symmetry of
+// the trailing matrix as the published rows' entries at column i (broadcast
+// LDS reads instead of cross-lane moves), m_t = (G[j+t][i] - sum_{s<t} m_s
+// r'_s[j+t]) / d_t, then M[i][c] -= sum_t m_t r'_t[c] with the block's
+// columns switching to their L^{-1} entries exactly as B single steps would
+// leave them.  Pivot dropping as above.  K % B == 0, K % NW == 0; fsh >=
+// 2 * B * 64 + 64 doubles of LDS (double-buffered pivot rows + d).  Every
+// thread of the workgroup calls it (waves >= NW only meet the barriers).
+// k = 40: 14.1 us (one pivot per step, 4 waves) -> see profiles/r6/chol_*.
+template <int K, int NW, int B>
+__device__ __forceinline__ void wg_chol_invB(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
                                              int* st) {
-  static_assert(K % NW == 0 && K % 2 == 0 && K <= 64, "K");
+  static_assert(K % NW == 0 && K % B == 0 && K <= 64 && (B == 2 || B == 4), "K");
   constexpr int R = K / NW;
   const int tid = threadIdx.x, c = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool act = w < NW;
-  double* rowbuf = fsh;        // [2][2][64]
-  double* dsh = fsh + 256;     // d_i (0: dropped)
+  double* rowbuf = fsh;             // [2][B][64]
+  double* dsh = fsh + 2 * B * 64;   // d_i (0: dropped)
   double M[R];
 #pragma unroll
   for (int q = 0; q < R; ++q) {
@@ -276,40 +280,66 @@ __device__ __forceinline__ void wg_chol_inv2(const double* G, int ldg, double* X
   const double thr = 1e-13 * wave_max(c < k ? fabs(G[c * ldg + c]) : 0.0);
   int bad = 0;
 #pragma unroll
-  for (int j = 0; j < K; j += 2) {
-    double* rb = rowbuf + ((j >> 1) & 1) * 128;
-    if (w == j % NW) rb[c] = M[j / NW];
-    if (w == (j + 1) % NW) rb[64 + c] = M[(j + 1) / NW];
+  for (int j = 0; j < K; j += B) {
+    double* rb = rowbuf + ((j / B) & 1) * B * 64;
+#pragma unroll
+    for (int t = 0; t < B; ++t)
+      if (w == (j + t) % NW) rb[t * 64 + c] = M[(j + t) / NW];
     __syncthreads();
-    const double r0 = rb[c], r1 = rb[64 + c];
-    const double d0 = rb[j], e01 = rb[j + 1], e10 = rb[64 + j], d1r = rb[64 + j + 1];
-    const bool ok0 = (d0 > thr && d0 == d0) || j >= k;
-    const double rc0 = ok0 ? rcp64(d0) : 0.0;
-    const double f1 = e10 * rc0;
-    const double d1 = fma(-f1, e01, d1r);
-    const bool ok1 = (d1 > thr && d1 == d1) || j + 1 >= k;
-    const double rc1 = ok1 ? rcp64(d1) : 0.0;
-    bad |= !ok0 || !ok1;
-    if (tid == 0) {
-      dsh[j] = ok0 ? d0 : 0.0;
-      dsh[j + 1] = ok1 ? d1 : 0.0;
+    // the block rows at this lane's column, and the B x B pivot block
+    double rl[B], pb[B][B];
+#pragma unroll
+    for (int t = 0; t < B; ++t) {
+      rl[t] = rb[t * 64 + c];
+#pragma unroll
+      for (int u = 0; u < B; ++u) pb[t][u] = rb[t * 64 + j + u];
     }
-    const double r1p = c == j ? -f1 : fma(-f1, r0, r1);   // row j + 1 after pivot j
+    // the block's elimination: pivots d_t, multipliers f[u][t] (u > t); pb
+    // and rl updated in place (pb[u][v], v > t: row u's trailing entries)
+    double rc[B], f[B][B];
+#pragma unroll
+    for (int t = 0; t < B; ++t) {
+      const double d = pb[t][t];
+      const bool ok = (d > thr && d == d) || j + t >= k;
+      bad |= !ok;
+      rc[t] = ok ? rcp64(d) : 0.0;
+      if (tid == 0) dsh[j + t] = ok ? d : 0.0;
+#pragma unroll
+      for (int u = t + 1; u < B; ++u) {
+        f[u][t] = pb[u][t] * rc[t];
+#pragma unroll
+        for (int v = t + 1; v < B; ++v) pb[u][v] = fma(-f[u][t], pb[t][v], pb[u][v]);
+        rl[u] = c == j + t ? -f[u][t] : fma(-f[u][t], rl[t], rl[u]);
+      }
+    }
     if (act) {
 #pragma unroll
       for (int q = 0; q < R; ++q) {
-        const int i = q * NW + w;
-        if (i > j + 1) {
-          const double fi = lane_d(M[q], j) * rc0;
-          const double gi = fma(-fi, e01, lane_d(M[q], j + 1)) * rc1;
-          const double v = fma(-gi, r1p, fma(-fi, r0, M[q]));
-          M[q] = c == j ? fma(gi, f1, -fi) : (c == j + 1 ? -gi : v);
-        } else if (i == j + 1) {
-          M[q] = c == j + 1 ? 1.0 : r1p;
-        } else if (i == j) {
-          M[q] = c == j ? 1.0 : (c == j + 1 ? 0.0 : M[q]);
+        const int i = q * NW + w;   // wave-uniform
+        if (i >= j + B) {
+          // multipliers from the block rows' entries at column i (symmetry)
+          double a[B], m[B];
+#pragma unroll
+          for (int t = 0; t < B; ++t) a[t] = rb[t * 64 + i];
+#pragma unroll
+          for (int t = 0; t < B; ++t) {
+            m[t] = a[t] * rc[t];
+#pragma unroll
+            for (int v = t + 1; v < B; ++v) a[v] = fma(-m[t], pb[t][v], a[v]);
+          }
+          double x = M[q];
+#pragma unroll
+          for (int t = 0; t < B; ++t) x = c == j + t ? -m[t] : fma(-m[t], rl[t], x);
+          M[q] = x;
+        } else if (i >= j) {
+          // a block row: its eliminated row, 1 on its pivot, 0 right of it in the block
+          const int u = i - j;
+          double x = rl[0];
+#pragma unroll
+          for (int t = 1; t < B; ++t) x = u == t ? rl[t] : x;
+          M[q] = c == i ? 1.0 : ((c > i && c < j + B) ? 0.0 : x);
         } else {
-          M[q] = (c == j || c == j + 1) ? 0.0 : M[q];
+          M[q] = (c >= j && c < j + B) ? 0.0 : M[q];
         }
       }
     }
@@ -439,6 +469,109 @@ __device__ __forceinline__ void wave_tridiag(const double* C, int ldc, int k, do
     ee[K - 1] = 0.0;
   }
   wave_lds_sync();
+}
+
+// The same T by FOUR waves: wave w keeps columns [w K/4, (w + 1) K/4) of
+// the trailing matrix (lane = row).  Step J: the wave owning column J forms
+// v (norm by DPP sum, as above) and publishes it; barrier; every wave forms
+// its columns' share of p = A v; barrier; every wave sums the four shares,
+// K_J = v^T p (DPP sum), w = 2 (p - K_J v), and updates its own columns
+// (w_c by readlane).  Two barriers per step against the single wave's two
+// LDS round trips, and a quarter of the step's FMAs per wave.  Columns
+// already reduced take the (zero) updates of v_c = w_c = 0 instead of a
+// branch.  vsh: >= 128 doubles, psh: >= 256 doubles (LDS).  Every thread of
+// the workgroup calls it (waves >= 4 only meet the barriers).
+template <int K, int J>
+__device__ __forceinline__ void wtri_steps(double (&acol)[K / 4], int i, int w, double* vsh, double* psh,
+                                           double* refl, int ldr, double* dd, double* ee) {
+  if constexpr (J + 2 < K) {
+    constexpr int CW = K / 4, OW = J / CW, LC = J % CW;
+    const bool act = w < 4;
+    double* vb = vsh + (J & 1) * 64;
+    if (w == OW) {
+      const double xi = (i > J) ? acol[LC] : 0.0;
+      const double s2 = wave_sum(xi * xi);
+      const double x0 = lane_d(acol[LC], J + 1);
+      const double sig2 = s2 - x0 * x0;
+      const bool refl_on = sig2 > 1e-300;
+      const double rs = rsq64(refl_on ? s2 : 1.0);
+      const double alpha = refl_on ? (x0 >= 0.0 ? -s2 * rs : s2 * rs) : x0;
+      const double rn = refl_on ? rsq64(2.0 * (s2 - alpha * x0)) : 0.0;
+      const double vi = (i > J) ? (xi - (i == J + 1 ? alpha : 0.0)) * rn : 0.0;
+      if (i == J) { dd[J] = acol[LC]; ee[J] = alpha; }
+      vb[i] = i < K ? vi : 0.0;
+      if (i < K) refl[i * ldr + J] = vi;
+    }
+    __syncthreads();
+    double vi = 0.0;
+    if (act) {
+      vi = vb[i];
+      double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+      for (int l = 0; l < CW; l += 2) {
+        p0 = fma(acol[l], vb[w * CW + l], p0);
+        if (l + 1 < CW) p1 = fma(acol[l + 1], vb[w * CW + l + 1], p1);
+      }
+      psh[w * 64 + i] = p0 + p1;
+    }
+    __syncthreads();
+    if (act) {
+      const double p = (psh[i] + psh[64 + i]) + (psh[128 + i] + psh[192 + i]);
+      const double Kd = wave_sum(vi * p);
+      const double wi = (i > J) ? 2.0 * (p - Kd * vi) : 0.0;
+#pragma unroll
+      for (int l = 0; l < CW; ++l) {
+        const int c = w * CW + l;
+        acol[l] = fma(-vi, lane_d(wi, c), fma(-wi, vb[c], acol[l]));
+      }
+    }
+    wtri_steps<K, J + 1>(acol, i, w, vsh, psh, refl, ldr, dd, ee);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void wg_tridiag(const double* C, int ldc, int k, double* refl, int ldr, double* dd,
+                                           double* ee, double* vsh, double* psh, int* bad) {
+  static_assert(K % 4 == 0 && K <= 64, "K");
+  constexpr int CW = K / 4;
+  const int i = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool act = w < 4;
+  double acol[CW];
+  double f2 = 0.0;
+  int nf = 0;
+#pragma unroll
+  for (int l = 0; l < CW; ++l) {
+    const int c = w * CW + l;
+    const double v = (act && i < k && c < k) ? C[i * ldc + c] : 0.0;
+    nf |= !(fabs(v) <= 1.7e308);
+    f2 = fma(v, v, f2);
+    acol[l] = v;
+  }
+  if (act) {
+    f2 = wave_sum(f2);
+    if (i == 0) psh[w] = f2;
+    if (nf) atomicOr(bad, 1);
+  }
+  if (threadIdx.x < 128) vsh[threadIdx.x] = 0.0;
+  __syncthreads();
+  const double beta = 1.0625 * sqrt((psh[0] + psh[1]) + (psh[2] + psh[3])) + 1e-300;   // > ||C||_F
+  __syncthreads();
+#pragma unroll
+  for (int l = 0; l < CW; ++l) {
+    const int c = w * CW + l;
+    if (act && c >= k && c == i) acol[l] = -beta;
+  }
+  wtri_steps<K, 0>(acol, i, w, vsh, psh, refl, ldr, dd, ee);
+  // the last 2 x 2 block
+  constexpr int W2 = (K - 2) / CW, L2 = (K - 2) % CW, W1 = (K - 1) / CW, L1 = (K - 1) % CW;
+  if (w == W2 && i == K - 2) dd[K - 2] = acol[L2];
+  if (w == W2 && i == K - 1) ee[K - 2] = acol[L2];
+  if (w == W1 && i == K - 1) {
+    dd[K - 1] = acol[L1];
+    ee[K - 1] = 0.0;
+  }
+  __syncthreads();
 }
 
 // ------------------------------------------- symmetric tridiagonal eigen

@@ -396,7 +396,71 @@ k_split_t(const float* __restrict__ X, int w, int m, int64_t ldx, bf16_t* __rest
   pl[1] = make_uint4(l[4], l[5], l[6], l[7]);
 }
 
+// Exact three-plane split of an f32 panel, transposed, into the stacked
+// layout of the split Gram (ml/krr.py _gram_split): X (w x m, ldx) -> S (m x
+// 5 seg, row stride lds) with segments [L | H | M | H | L] of width seg
+// (H = rne(x), M = rne(x - H), L = rne(x - H - M): H + M + L == x for normal
+// f32), zero for k >= w.  Then [H M] [H M]^T + [H M H L] [L H M H]^T = X^T X
+// up to the M L / L L terms, both products NT on windows of S.
+__global__ void __launch_bounds__(256)
+k_split3_t(const float* __restrict__ X, int w, int m, int64_t ldx, bf16_t* __restrict__ S, int seg, int64_t lds) {
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int kk = e >> 6, cc = e & 63;
+    const int k = k0 + kk, c = c0 + cc;
+    tile[kk][cc] = (k < w && c < m) ? X[(int64_t)k * ldx + c] : 0.f;
+  }
+  __syncthreads();
+  const int cc = t >> 2, q = t & 3;
+  const int c = c0 + cc;
+  if (c >= m || k0 + 16 * q >= seg) return;
+  uint32_t h[8], md[8], l[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    uint32_t hh[2], mm[2], ll[2];
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const float x = tile[16 * q + 2 * u + v][cc];
+      const bf16_t hb = f_to_bf16(x);
+      const float r = x - bf16_to_f(hb);
+      const bf16_t mb = f_to_bf16(r);
+      hh[v] = hb;
+      mm[v] = mb;
+      ll[v] = f_to_bf16(r - bf16_to_f(mb));
+    }
+    h[u] = hh[0] | (hh[1] << 16);
+    md[u] = mm[0] | (mm[1] << 16);
+    l[u] = ll[0] | (ll[1] << 16);
+  }
+  bf16_t* row = S + (int64_t)c * lds + k0 + 16 * q;
+  auto put = [&](int sg, const uint32_t* v) {
+    uint4* p = (uint4*)(row + (int64_t)sg * seg);
+    p[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    p[1] = make_uint4(v[4], v[5], v[6], v[7]);
+  };
+  put(0, l);
+  put(1, h);
+  put(2, md);
+  put(3, h);
+  put(4, l);
+}
+
 }  // namespace
+
+// S (m x 5 seg bf16, row stride lds; seg % 64 == 0, 16-B aligned rows) =
+// [L | H | M | H | L] of the f32 panel X (w x m, ldx) transposed: see k_split3_t.
+SL_API int sl_split3_bf16_t(const float* X, int w, int m, int64_t ldx, void* S, int seg, int64_t lds, void* stream) {
+  if (w < 0 || m <= 0 || seg % 64 || seg < w || lds < 5 * (int64_t)seg || lds % 8) {
+    sl_set_last_error("split3_bf16_t: needs seg % 64 == 0, seg >= w, lds >= 5 seg, lds % 8 == 0");
+    return SL_ERR_INVALID;
+  }
+  dim3 grid((unsigned)((m + 63) / 64), (unsigned)(seg / 64));
+  k_split3_t<<<grid, 256, 0, (hipStream_t)stream>>>(X, w, m, ldx, (bf16_t*)S, seg, lds);
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
 
 // C (M x N, ldc) = alpha A B^T (+ C when accumulate) with A M x K, B N x K
 // bf16 row-major (lda, ldb elements, 16-B aligned rows), K % 64 == 0.

@@ -256,7 +256,7 @@ __device__ double* jacobi(double* A, double* B, double* V, int kp, int ld, int m
 // clusters, rare).  Run by ONE workgroup.  status_or: OR the call's status
 // bits into *status (0: store them -- the call's first writer).
 struct CoreLds {
-  __attribute__((aligned(16))) double dd[KMAX], ee[KMAX], lam[KMAX], vsh[2 * KMAX], wsh[2 * KMAX], fsh[3 * 64];
+  __attribute__((aligned(16))) double dd[KMAX], ee[KMAX], lam[KMAX], vsh[2 * KMAX], wsh[2 * KMAX], fsh[9 * 64];
   int bad, fb;
 };
 
@@ -445,7 +445,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
       }
     }
     __syncthreads();
-    slw::wg_chol_inv<K, 4>(b0, ld, b2, ld, k, cls.fsh, &st_sh);   // rows over 4 waves
+    slw::wg_chol_invB<K, 4, 4>(b0, ld, b2, ld, k, cls.fsh, &st_sh);   // 4 pivots per step, rows over 4 waves
     __syncthreads();
     for (int e = tid; e < k * k; e += NT) {
       const int i = e / k, c = e - i * k;
@@ -555,7 +555,7 @@ __global__ void __launch_bounds__(NT) k_boundary(BndArgs a) {
     __syncthreads();
     if (tid == 0) a.sync[0] = 0u;   // ready for the next launch
     if (!FINAL) {
-      slw::wg_chol_inv<K, 4>(b0, ld, b2, ld, k, cls.fsh, &st_sh);   // rows over 4 waves
+      slw::wg_chol_invB<K, 4, 4>(b0, ld, b2, ld, k, cls.fsh, &st_sh);   // 4 pivots per step, rows over 4 waves
       __syncthreads();
       for (int e = tid; e < k * k; e += NT) {
         const int i = e / k, c = e - i * k;

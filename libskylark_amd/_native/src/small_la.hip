@@ -167,25 +167,29 @@ SL_API int sl_small_matmul(const double* A, const double* B, double* C, int m, i
 // kernel the randSVD pass boundaries run, as a standalone launch.  Status
 // bit 1: a pivot at or below 1e-13 max G_ii was dropped.
 namespace {
-// V: 0 one wave, 1 rows over 4 waves, 2 / 3 two pivots per step over 4 / 8 waves
+// V: 0 one wave, 1 rows over 4 waves, 2 / 3 two pivots per step over 4 / 8
+// waves, 4 / 5 four pivots per step over 4 / 8 waves
 template <int K, int V>
-__global__ void __launch_bounds__(512) k_chol_inv_wave(const double* __restrict__ G, int k, int ldg,
+__global__ void __launch_bounds__(V == 3 || V == 5 ? 512 : 256) k_chol_inv_wave(const double* __restrict__ G, int k, int ldg,
                                                        double* __restrict__ X, int* __restrict__ status) {
-  __shared__ __attribute__((aligned(16))) double fsh[320];
+  __shared__ __attribute__((aligned(16))) double fsh[576];
   __shared__ int st;
   if (threadIdx.x == 0) st = 0;
   __syncthreads();
   if constexpr (V == 1) slw::wg_chol_inv<K, 4>(G, ldg, X, k, k, fsh, &st);
-  else if constexpr (V == 2) slw::wg_chol_inv2<K, 4>(G, ldg, X, k, k, fsh, &st);
-  else if constexpr (V == 3) slw::wg_chol_inv2<K, 8>(G, ldg, X, k, k, fsh, &st);
+  else if constexpr (V == 2) slw::wg_chol_invB<K, 4, 2>(G, ldg, X, k, k, fsh, &st);
+  else if constexpr (V == 3) slw::wg_chol_invB<K, 8, 2>(G, ldg, X, k, k, fsh, &st);
+  else if constexpr (V == 4) slw::wg_chol_invB<K, 4, 4>(G, ldg, X, k, k, fsh, &st);
+  else if constexpr (V == 5) slw::wg_chol_invB<K, 8, 4>(G, ldg, X, k, k, fsh, &st);
   else if (threadIdx.x < 64) slw::wave_chol_inv<K>(G, ldg, X, k, k, fsh, &st);
   __syncthreads();
   if (threadIdx.x == 0 && status && st) atomicOr(status, st);
 }
-// 1: rows over 4 waves for K <= 48 (default; 64 stays on one wave, where
-// the split measured slower), 0: one wave (A/B, profiles/r5/chol_wave_variants.md),
-// 2 / 3: two pivots per step over 4 / 8 waves (r6 A/B)
-int g_chol_variant = 1;
+// 4: four pivots per step, rows over 4 waves (default: k = 40 12.5 us, k = 64
+// 24.7 us against 14.0 / 40.4 for one pivot per step, profiles/r6/chol_wave_ab.jsonl);
+// 1: one pivot per step over 4 waves for K <= 48 (64 on one wave), 0: one wave,
+// 2 / 3 / 5: two pivots over 4 / 8 waves, four over 8 (A/B)
+int g_chol_variant = 4;
 }  // namespace
 
 SL_API void sl_chol_inv_set_variant(int v) { g_chol_variant = v; }
@@ -194,7 +198,9 @@ SL_API int sl_chol_inv_wave(const double* G, int k, int ldg, double* X, int* sta
   if (k < 1 || k > 64 || ldg < k) { sl_set_last_error("chol_inv_wave: 1 <= k <= 64"); return SL_ERR_DIMENSION; }
   hipStream_t s = (hipStream_t)stream;
 #define SL_CIW(KK)                                                                                      \
-  if (g_chol_variant == 3) k_chol_inv_wave<KK, 3><<<1, 512, 0, s>>>(G, k, ldg, X, status);               \
+  if (g_chol_variant == 5) k_chol_inv_wave<KK, 5><<<1, 512, 0, s>>>(G, k, ldg, X, status);               \
+  else if (g_chol_variant == 4) k_chol_inv_wave<KK, 4><<<1, 256, 0, s>>>(G, k, ldg, X, status);          \
+  else if (g_chol_variant == 3) k_chol_inv_wave<KK, 3><<<1, 512, 0, s>>>(G, k, ldg, X, status);          \
   else if (g_chol_variant == 2) k_chol_inv_wave<KK, 2><<<1, 256, 0, s>>>(G, k, ldg, X, status);          \
   else if (g_chol_variant && KK <= 48) k_chol_inv_wave<KK, 1><<<1, 256, 0, s>>>(G, k, ldg, X, status);   \
   else k_chol_inv_wave<KK, 0><<<1, 64, 0, s>>>(G, k, ldg, X, status);

@@ -144,18 +144,25 @@ k_sym_eig_jacobi(const double* __restrict__ Cin, int k, int ldc, int r, double* 
 // a vanishing r-th eigenvalue).  Output as k_sym_eig_jacobi:
 // out[i * r + c] = V[i][c] descending, then sqrt(max(lambda, 0)) (or lambda)
 // in out[k * r + c].
+// tridiagonalisation: 1 = four waves (wg_tridiag, default), 0 = one wave (A/B)
+int g_tri_host = 1;
 template <int K>
-__global__ void __launch_bounds__(512) k_sym_eig_wave(const double* __restrict__ C, int k, int ldc, int r,
-                                                      double* __restrict__ out, int want_sqrt, int* __restrict__ status) {
+__global__ void __launch_bounds__(512) k_sym_eig_wave_impl(const double* __restrict__ C, int k, int ldc, int r,
+                                                           double* __restrict__ out, int want_sqrt,
+                                                           int* __restrict__ status, int g_tri_variant) {
   __shared__ double refl[K * (K + 1)];
   __shared__ double sc[3 * 64 * (K + 1)];
-  __shared__ __attribute__((aligned(16))) double dd[K], ee[K], lam[K], vsh[2 * K], wsh[2 * K];
+  __shared__ __attribute__((aligned(16))) double dd[K], ee[K], lam[K], vsh[128], wsh[256];
   __shared__ int bad, fb;
   const int tid = threadIdx.x;
   if (tid == 0) { bad = 0; fb = 0; }
   __syncthreads();
-  if (tid < 64) slw::wave_tridiag<K>(C, ldc, k, refl, K + 1, dd, ee, vsh, wsh, &bad);
-  __syncthreads();
+  if (g_tri_variant) {
+    slw::wg_tridiag<K>(C, ldc, k, refl, K + 1, dd, ee, vsh, wsh, &bad);
+  } else {
+    if (tid < 64) slw::wave_tridiag<K>(C, ldc, k, refl, K + 1, dd, ee, vsh, wsh, &bad);
+    __syncthreads();
+  }
   const int nt = r < k ? r + 1 : k;
   slw::sym_top_eig<K, 512>(dd, ee, refl, K + 1, nt, r, lam, out, r, k, sc, &fb);
   if (tid < r) {
@@ -176,14 +183,16 @@ SL_API int sl_sym_eig_tridiag(const double* C, int k, int ldc, int r, double* ou
                               void* stream) {
   if (k <= 0 || k > 64 || r <= 0 || r > k || ldc < k) return SL_ERR_DIMENSION;
   hipStream_t s = (hipStream_t)stream;
-  if (k <= 16) k_sym_eig_wave<16><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status);
-  else if (k <= 32) k_sym_eig_wave<32><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status);
-  else if (k <= 40) k_sym_eig_wave<40><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status);
-  else if (k <= 48) k_sym_eig_wave<48><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status);
-  else k_sym_eig_wave<64><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status);
+  if (k <= 16) k_sym_eig_wave_impl<16><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
+  else if (k <= 32) k_sym_eig_wave_impl<32><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
+  else if (k <= 40) k_sym_eig_wave_impl<40><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
+  else if (k <= 48) k_sym_eig_wave_impl<48><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
+  else k_sym_eig_wave_impl<64><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
+
+SL_API void sl_sym_eig_set_tri_variant(int v) { g_tri_host = v; }
 
 SL_API int sl_sym_eig_topr(const double* C, int k, int ldc, int r, double* out, int want_sqrt,
                            int max_sweeps, int* sweeps_out, void* stream) {

@@ -23,6 +23,9 @@ blocks, sized for xGMI (few, large messages).
 """
 from __future__ import annotations
 
+import ctypes as C
+import os
+
 import math
 from dataclasses import dataclass
 
@@ -95,20 +98,84 @@ class _Data:
         return t
 
 
+SPLIT_GRAM_ROWS = 8192   # rows per f32-accumulated chunk of the split Gram
+
+
+def _split3(Zc: torch.Tensor):
+    """f32 -> three bf16 planes with H + M + L == Zc exactly (8 + 8 + 8
+    mantissa bits; values whose low parts underflow bf16's range lose them)."""
+    H = Zc.to(torch.bfloat16)
+    r = Zc - H.float()
+    Mp = r.to(torch.bfloat16)
+    L = (r - Mp.float()).to(torch.bfloat16)
+    return H, Mp, L
+
+
+def _gram_split(Z: torch.Tensor, G: torch.Tensor) -> None:
+    """G += Z^T Z for f32 Z on the GPU from exact bf16 products on the matrix
+    cores: Z = H + M + L (bf16 planes), Z^T Z = H^T H + M^T M + (H^T M + M^T H)
+    + (H^T L + L^T H) up to the M L / L L terms (< 2^-32 of |z|^2).  Per row
+    chunk one kernel (gemm_nt.hip k_split3_t) writes the planes transposed
+    and stacked, S = [L | H | M | H | L] (s x 5 R), and two NT GEMMs on
+    windows of S give [H M][H M]^T + [H M H L][L H M H]^T (hipBLASLt NT: 1.16-
+    1.44 PF on these shapes against 0.91-1.10 for the TN form of row-major
+    planes, profiles/r6/gemm_orient_ab.json).  Every product is exact in f32;
+    the sums are f32 within a chunk of SPLIT_GRAM_ROWS rows (relative error
+    ~2^-24 sqrt(4 x rows) of sum |z_i z_j|, ~1e-5 -- the level of the f32
+    feature map's own rounding) and f64 across chunks."""
+    from ..ops import _lib
+    n, s = Z.shape
+    R = SPLIT_GRAM_ROWS
+    if not _lib.available() or Z.stride(1) != 1:
+        for r0 in range(0, n, R):
+            H, Mp, L = _split3(Z[r0:r0 + R])
+            A1 = torch.cat([H, Mp])
+            Cm = torch.mm(A1.t(), A1, out_dtype=torch.float32)
+            Cm += torch.mm(torch.cat([H, Mp, H, L]).t(), torch.cat([L, H, Mp, H]), out_dtype=torch.float32)
+            G += Cm.double()
+        return
+    _lib.register("sl_split3_bf16_t", [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_int, C.c_int64,
+                                       C.c_void_p])
+    seg = -(-min(R, n) // 64) * 64
+    S = torch.empty(s, 5 * seg, dtype=torch.bfloat16, device=Z.device)
+    st = C.c_void_p(_lib.stream_of(Z))
+    for r0 in range(0, n, R):
+        w = min(R, n - r0)
+        _lib.call("sl_split3_bf16_t", _lib.ptr(Z[r0:]), w, s, Z.stride(0), _lib.ptr(S), seg, 5 * seg, st)
+        A = S[:, seg:3 * seg]
+        Cm = torch.mm(A, A.t(), out_dtype=torch.float32)
+        Cm += torch.mm(S[:, seg:5 * seg], S[:, :4 * seg].t(), out_dtype=torch.float32)
+        G += Cm.double()
+
+
 def _ridge(Z: torch.Tensor, Y: torch.Tensor, lam: float, data: _Data | None = None) -> torch.Tensor:
     """W = argmin |Z W - Y|^2 + lam |W|^2 via the s x s normal equations in
-    fp64 (reference ``El::Ridge``); distributed Z: all-reduce [Z^T Z | Z^T Y]."""
+    fp64 (reference ``El::Ridge``); distributed Z: all-reduce [Z^T Z | Z^T Y].
+    f32 Z on the GPU: Z^T Z from exact split products (:func:`_gram_split`)
+    and Z^T Y from one streaming pass (f32); otherwise fp64 products and sums."""
     s = Z.shape[1]
     t = Y.shape[1] if Y.dim() > 1 else 1
     Y2 = Y if Y.dim() > 1 else Y[:, None]
     # [Z^T Z | Z^T Y] accumulated in fp64 over row chunks: no n x s fp64 copy
     # of Z (32 GB for 1e6 x 4096 features), same fp64 products and sums
     G = torch.zeros(s, s + t, dtype=torch.float64, device=Z.device)
-    chunk = max(1, (1 << 27) // max(1, s + t))
-    for r0 in range(0, Z.shape[0], chunk):
-        Zc = Z[r0:r0 + chunk].to(torch.float64)
-        G[:, :s].addmm_(Zc.t(), Zc)
-        G[:, s:].addmm_(Zc.t(), Y2[r0:r0 + chunk].to(torch.float64))
+    split = Z.is_cuda and Z.dtype == torch.float32 and os.environ.get("SKH_KRR_F64_GRAM", "0") != "1"
+    from ..ops import normal_eq
+    if split:
+        Gzz = torch.zeros(s, s, dtype=torch.float64, device=Z.device)
+        _gram_split(Z, Gzz)
+        G[:, :s] = Gzz
+    if split and normal_eq.native_ok(Z, t) and Y2.shape[0] == Z.shape[0]:
+        # Z^T Y from one streaming read of Z (ata_kernels.hip dual pass: f32
+        # products and block sums) -- the fp64 chunk copies of Z took ~40 ms
+        G[:, s:] = normal_eq.dual(Z, Y2.to(torch.float32).contiguous())[0].double()
+    else:
+        chunk = max(1, (1 << 27) // max(1, s + t))
+        for r0 in range(0, Z.shape[0], chunk):
+            Zc = Z[r0:r0 + chunk].to(torch.float64)
+            if not split:
+                G[:, :s].addmm_(Zc.t(), Zc)
+            G[:, s:].addmm_(Zc.t(), Y2[r0:r0 + chunk].to(torch.float64))
     if data is not None:
         data.allreduce(G)
     C = G[:, :s]

@@ -199,3 +199,37 @@ def test_feature_map_precond_f32_apply_matches_f64(dev):
     A64, code64 = K.cg(DenseOp(Kg), B, params=p, M=P)
     assert code == -1 and code64 == -1
     assert float((A32 - A64).norm() / A64.norm()) < 1e-4
+
+
+@pytest.mark.parametrize("n,s", [(20000, 512), (9000, 300), (777, 64)])
+def test_krr_split_gram_matches_fp64(dev, n, s, monkeypatch):
+    """Z^T Z of f32 features from the exact three-plane bf16 split (gemm_nt.hip
+    k_split3_t + two NT GEMMs per row chunk, f32 sums per chunk, f64 across)
+    against the fp64 product, ragged last chunk included (reference
+    ml/krr.hpp:94-196 forms Z^T Z in the features' precision)."""
+    from libskylark_amd.ml import krr as K
+    monkeypatch.setattr(K, "SPLIT_GRAM_ROWS", 4096)
+    g = torch.Generator(device=dev).manual_seed(n)
+    Z = torch.cos(torch.randn(n, s, generator=g, device=dev) * 3.0) * (2.0 / s) ** 0.5
+    G = torch.zeros(s, s, dtype=torch.float64, device=dev)
+    K._gram_split(Z, G)
+    ref = Z.double().t() @ Z.double()
+    rel = float((G - ref).abs().max() / ref.abs().max())
+    assert rel < 1e-5, rel   # f32 sums over <= 4 x 4096 exact products per chunk: ~2^-24 sqrt(K)
+    assert torch.equal(G, G.t()) or float((G - G.t()).abs().max() / ref.abs().max()) < 1e-6
+
+
+def test_krr_ridge_split_matches_fp64_gram(dev, monkeypatch):
+    """approximate_kernel_ridge's weights with the split Gram against the
+    all-fp64 normal equations on the same features."""
+    import libskylark_amd as sk
+    from libskylark_amd import ml
+    g = torch.Generator(device=dev).manual_seed(5)
+    X = torch.randn(30000, 64, generator=g, device=dev)
+    Y = torch.sin(X[:, :1]) + 0.01 * torch.randn(30000, 1, generator=g, device=dev)
+    k = ml.Gaussian(64, sigma=8.0)
+    _, W = ml.approximate_kernel_ridge(k, X, Y, 1e-2, 512, context=sk.Context(3))
+    monkeypatch.setenv("SKH_KRR_F64_GRAM", "1")
+    _, W64 = ml.approximate_kernel_ridge(k, X, Y, 1e-2, 512, context=sk.Context(3))
+    rel = float((W.double() - W64.double()).norm() / W64.double().norm())
+    assert rel < 1e-4, rel
