@@ -149,8 +149,25 @@ def run(a, comm, dev, scaling, square=False):
     from libskylark_amd.nla.svd import last_device_status
     status = last_device_status(wait=True)
     # a one-shot all-reduce whose peer missed its bounded wait poisoned that
-    # call's operand with NaN: never report a number from such a run
-    comm.check_collectives()
+    # call's operand with NaN: never report a number from such a run.  Every
+    # rank learns every rank's failure (check_collectives(agree=True)), every
+    # rank must have run the same engine, and no rank may report a device
+    # timeout; any of these makes the run an error (non-zero exit, reason in
+    # the JSON line)
+    errors = []
+    try:
+        comm.check_collectives(agree=True)
+    except Exception as e:  # noqa: BLE001 - OneShotError (the same text on every rank)
+        errors.append(f"{type(e).__name__}: {e}")
+    if N > 1:
+        from libskylark_amd.nla.svd import last_engine
+        eng = comm.all_gather_object(last_engine())
+        if len(set(eng)) > 1:
+            errors.append(f"ranks ran different randSVD engines: {eng}")
+        sts = comm.all_gather_object(int(status))
+        late = [q for q, x in enumerate(sts) if x & 16]
+        if late:
+            errors.append(f"device engine timeout (status bit 16) on rank(s) {late}")
     orth, resid = check_answer(A, U, s, V, comm)
     red = "one-shot IPC all-reduces" if getattr(comm, "_oneshot", None) else "RCCL all-reduces"
     if grid is not None:
@@ -163,7 +180,7 @@ def run(a, comm, dev, scaling, square=False):
         "m": m, "n": n, "ms": ms, "step_ms": step_ms, "gbs": m * n * 2 / (ms / 1e3) / 1e9, "steps": steps, "warmup": warmup,
         "parallelism": par, "orth_err": orth, "resid_rel": resid, "status": status,
         "top_singular_values": [round(float(x), 3) for x in s[:3].tolist()],
-        "grid_pc": grid.pc if grid is not None else 0,
+        "grid_pc": grid.pc if grid is not None else 0, "errors": errors,
         "reduction": comm.oneshot_status() if N > 1 else None,
         "native_fused_pass": bool(tallskinny._native_ok(torch.empty(8, 8, dtype=torch.bfloat16, device=dev),
                                                         2 * a.rank)),
@@ -210,7 +227,8 @@ def main(argv=None):
         sq = run(a, comm, dev, "strong", square=True)
     if N > 1 and a.scaling == "strong" and not a.no_weak:
         weak = run(a, comm, dev, "weak")
-    ok = res["orth_err"] < 1e-3 and res["resid_rel"] < 5e-2 and not (res["status"] & 16)
+    errors = res["errors"] + (sq["errors"] if sq else []) + (weak["errors"] if weak else [])
+    ok = res["orth_err"] < 1e-3 and res["resid_rel"] < 5e-2 and not (res["status"] & 16) and not errors
     if comm.rank == 0:
         out = {
             "metric": METRIC,
@@ -240,6 +258,8 @@ def main(argv=None):
             "top_singular_values": res["top_singular_values"],
             "native_fused_pass": res["native_fused_pass"],
         }
+        if errors:
+            out["error"] = errors
         if res["reduction"] is not None:
             # which small all-reduce ran and, when the one-shot path is off,
             # why (its collective self-test outcome on this node)
@@ -260,9 +280,15 @@ def main(argv=None):
                       f"({r['calls']} calls)", file=sys.stderr)
     if N > 1:
         import torch.distributed as dist
-        comm.check_collectives()
+        try:
+            comm.check_collectives(agree=True)
+        except Exception as e:  # noqa: BLE001
+            print(f"collective failure after the bench: {e}", file=sys.stderr)
+            ok = False
         comm.close()
         dist.destroy_process_group()
+    if errors:
+        return 4
     return 0 if ok else 3
 
 

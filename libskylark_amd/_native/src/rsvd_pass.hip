@@ -216,6 +216,7 @@ struct P5Tiles {
                  // ntail = 8 (c - 1) blocks, which keep the default policy so
                  // the next pass (walking the other way) finds them in the MALL
   int ntail;
+  int nty;       // FINAL: non-temporal stores of Y (variant bit 12)
 };
 
 #ifndef P1_PD
@@ -460,7 +461,8 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           if (ok) v = *(const f32x4*)&yf[4 * t];
           float* dst = ok ? Y + r0 * ldy + 4 * t : scratch + 4 * lane;
-          *(f32x4*)dst = v;
+          if (pt.nty) __builtin_nontemporal_store(v, (f32x4*)dst);
+          else *(f32x4*)dst = v;
         } else {
           const int t = q * 64 + lane;
           const int row = t / k, col = t - (t / k) * k;
@@ -703,6 +705,7 @@ int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Z
     pt.nt = c != 0;
     pt.ntail = c >= 2 ? 8 * (c - 1) : 0;
   }
+  pt.nty = (variant >> 12) & 1;
   if (!p5_tiles(n, KT, &pt)) {
     sl_set_last_error("rsvd_pass: no tile split for this n / k");
     return SL_ERR_UNSUPPORTED;

@@ -190,6 +190,7 @@ def approximate_svd(A, rank: int, context: Context | None = None,
     work = torch.float64 if A_loc.dtype == torch.float64 else torch.float32
     from ..ops import tallskinny as T
 
+    _LAST_ENGINE[0] = "host"
     if A_loc.is_cuda:
         res = _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params)
         if res is not None:
@@ -694,12 +695,24 @@ def _approximate_svd_device(A_loc, comm, m, n, rank, k, ctx, params):
             plan = _GenPlan(A_loc, comm, n, rank, k, q)
         _PLANS[key] = plan
     out = plan(A_loc, Z=Z, fjlt=fjlt, dense=dense)
+    _LAST_ENGINE[0] = "fused" if type(plan) is _EnginePlan else "general"
     if rows != A_loc.shape[0]:
         out = (out[0][:rows],) + tuple(out[1:])   # a rank without rows ran on one zero row
     check = params.check if params.check is not None else isinstance(plan, _GenPlan)
     if check:
         plan.check()
     return out
+
+
+_LAST_ENGINE = ["none"]
+
+
+def last_engine() -> str:
+    """Which path ran this process's most recent approximate_svd call:
+    "fused" (one-read bf16 engine), "general" (general-precision engine) or
+    "host" (host-driven small algebra).  Multi-rank callers compare it
+    across ranks (bench.py): every rank must have run the same one."""
+    return _LAST_ENGINE[0]
 
 
 def last_device_status(wait: bool = True) -> int:

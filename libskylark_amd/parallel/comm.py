@@ -128,12 +128,42 @@ class Comm:
             self._count(2 * t.numel() * t.element_size() * (self.size - 1) // self.size)
         return t
 
-    def check_collectives(self):
+    def check_collectives(self, agree: bool = False):
         """Raise if an asynchronous collective of this communicator failed
-        (a one-shot all-reduce whose peer missed the timeout)."""
+        (a one-shot all-reduce whose peer missed the timeout).
+
+        ``agree=True`` (collective): every rank learns every rank's state
+        through the backend's own collective, so a timeout seen by ANY rank
+        raises :class:`~.oneshot.OneShotError` on EVERY rank -- the late rank
+        itself summed valid data and would not know -- and the one-shot path
+        of this communicator is dropped: its later all-reduces go to RCCL
+        (or gloo), and ``oneshot_status()`` names the ranks that timed out."""
         os_ = getattr(self, "_oneshot", None)
+        if not agree:
+            if os_:
+                os_.check()
+            return
+        mine = False
         if os_:
-            os_.check()
+            try:
+                os_.check()
+            except Exception:  # noqa: BLE001 - reported collectively below
+                mine = True
+        if not self._active or self.size < 2:
+            if mine:
+                os_.check()
+            return
+        flags = self.all_gather_object(bool(mine))
+        bad = [q for q, f in enumerate(flags) if f]
+        if bad:
+            from .oneshot import OneShotError
+            reason = (f"one-shot all-reduce timed out on rank(s) {bad} (their operands were poisoned with NaN); "
+                      "the path is dropped for this communicator, later all-reduces use the backend")
+            if os_:
+                os_.close(self)
+            self._oneshot = False
+            self.oneshot_reason = reason
+            raise OneShotError(reason)
 
     def close(self):
         """Release this communicator's one-shot IPC buffers collectively

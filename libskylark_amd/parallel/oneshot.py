@@ -40,6 +40,13 @@ DEFAULT_CAP = 1 << 20      # bytes per slot: covers (n + k) x k f64 for n <= 300
 TIMEOUT_S = 30.0
 
 
+def _timeout() -> float:
+    """Bounded wait of each call (SL_ONESHOT_TIMEOUT_S overrides TIMEOUT_S:
+    the fault rehearsals shorten it)."""
+    v = os.environ.get("SL_ONESHOT_TIMEOUT_S")
+    return float(v) if v else TIMEOUT_S
+
+
 class OneShotError(RuntimeError):
     pass
 
@@ -155,7 +162,7 @@ class OneShotAllReduce:
         self._poll()
         _lib.call("sl_oneshot_allreduce", _lib.ptr(t), t.numel(), _lib.dtype_code(t.dtype), self.rank, self.p,
                   _lib.ptr(self.bases), self.cap, _lib.ptr(self.state), _lib.ptr(self.err),
-                  float(TIMEOUT_S if timeout_s is None else timeout_s), vp(_lib.stream_of(t)))
+                  float(_timeout() if timeout_s is None else timeout_s), vp(_lib.stream_of(t)))
         if not torch.cuda.is_current_stream_capturing():
             if getattr(self, "_err_host", None) is None:
                 self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()

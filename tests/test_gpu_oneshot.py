@@ -133,3 +133,61 @@ def test_oneshot_status_reported():
             assert after["reason"] == "ok"
         else:
             assert after["reason"] and after["reason"] != "ok"   # the failing stage is named
+
+
+def _late4_worker(rank, world):
+    """4 ranks on the one GPU (gloo coordinates), the one-shot path forced
+    on every Comm all-reduce, the bounded wait shortened to 0.3 s; rank 2
+    arrives 2 s late.  The waiting ranks' operands are NaN; the collective
+    check raises OneShotError on EVERY rank (the late rank summed valid data
+    and would not know on its own); the communicator's next all-reduce runs
+    on the backend (gloo here, RCCL in production) and is exact."""
+    import os
+    import time
+    import torch
+    os.environ["SL_ONESHOT"] = "1"
+    os.environ["SL_ONESHOT_TIMEOUT_S"] = "0.3"
+    from libskylark_amd.parallel import oneshot
+    oneshot.enable(True)
+    from libskylark_amd.parallel.comm import world as W
+    torch.cuda.set_device(0)
+    comm = W()
+    dev = torch.device("cuda", 0)
+    warm = torch.ones(8, dtype=torch.float64, device=dev)
+    comm.all_reduce(warm)                       # sets the path up (collective self-test)
+    torch.cuda.synchronize()
+    if not comm.oneshot_status()["enabled"]:
+        return "unavailable"
+    x = torch.full((100,), float(rank + 1), dtype=torch.float64, device=dev)
+    if rank == 2:
+        time.sleep(2.0)
+    comm.all_reduce(x)
+    torch.cuda.synchronize()
+    out = {"nan": bool(torch.isnan(x).all()), "sum_ok": bool(torch.all(x == 10.0))}
+    try:
+        comm.check_collectives(agree=True)
+        out["raised"] = ""
+    except oneshot.OneShotError as e:
+        out["raised"] = str(e)
+    st = comm.oneshot_status()
+    out["enabled_after"] = st["enabled"]
+    y = torch.full((100,), float(rank + 1), dtype=torch.float64, device=dev)
+    comm.all_reduce(y)                          # the backend now
+    torch.cuda.synchronize()
+    out["fallback_ok"] = bool(torch.all(y == 10.0))
+    comm.close()
+    return out
+
+
+def test_oneshot_delayed_rank_fails_on_every_rank_then_falls_back():
+    """a rank delayed past the bounded wait poisons the
+    waiters' operands and raises OneShotError on all four ranks; then a clean
+    fallback to the backend's all-reduce on the same communicator."""
+    res = run_distributed(_late4_worker, 4, timeout=180)
+    if all(r == "unavailable" for r in res):
+        pytest.skip("IPC export of uncached device memory unavailable here")
+    for q, r in enumerate(res):
+        assert r["nan"] == (q != 2) and r["sum_ok"] == (q == 2), (q, r)
+        assert "timed out on rank(s)" in r["raised"], (q, r)
+        assert r["enabled_after"] is False and r["fallback_ok"], (q, r)
+    assert len({r["raised"] for r in res}) == 1      # the same reason on every rank
