@@ -441,6 +441,7 @@ def cg(A, B, X=None, params: KrylovIterParams | None = None, M: Precond | None =
                 break
     else:
         _log(params, "CG: No convergence within iteration limit.")
+    params.iterations = itn + 1 if params.iter_lim > 0 else 0   # iterations run (reporting)
     return X, code
 
 

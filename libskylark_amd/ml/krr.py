@@ -55,6 +55,11 @@ class KrrParams:
     tolerance: float = 1e-3
     max_split: int = 0
     precond_f32: bool = True   # GPU: apply the feature-map preconditioner in f32 single-read passes
+    # FasterKernelRidge preconditioner: "features" (the reference's random-
+    # feature Woodbury form, feature_map_precond_t) or "nystrom" (s landmark
+    # columns of the Gram the solver holds; converges at small lambda where
+    # the random-feature approximation error ||K - U U^T|| / lambda does not)
+    precond: str = "features"
 
 
 krr_params_t = KrrParams
@@ -330,10 +335,12 @@ class FeatureMapPrecond:
             from ..ops import normal_eq
             Bf = B.to(torch.float32).contiguous()
             VB = normal_eq.dual(self._v32, Bf)[0]      # s x t
-            self.data.allreduce(VB)
+            if self.data is not None:
+                self.data.allreduce(VB)
             return (Bf / self.lam - normal_eq.gemv(self._v32, VB)).to(B.dtype)
         VB = self.V.t() @ B.to(self.V.dtype)
-        self.data.allreduce(VB)
+        if self.data is not None:
+            self.data.allreduce(VB)
         # (lam I + U U^T)^{-1} B = B / lam - U C^{-1} U^T B / lam^2 = B / lam - V V^T B
         return (B.to(self.V.dtype) / self.lam - self.V @ VB).to(B.dtype)
 
@@ -341,6 +348,57 @@ class FeatureMapPrecond:
 
 
 feature_map_precond_t = FeatureMapPrecond
+
+
+class NystromPrecond(FeatureMapPrecond):
+    """Woodbury preconditioner for ``K + lam I`` from ``s`` landmark columns
+    of the Gram itself (Nystrom): ``U = K[:, L]`` (L: s examples sampled
+    without replacement from the context's stream), ``W = K[L, L]``,
+    ``(lam I + U W^{-1} U^T)^{-1} B = B / lam - V V^T B`` with ``lam W + U^T U
+    = L L^T`` and ``V = U L^{-T} / sqrt(lam)``.  The random-feature form
+    approximates K to O(n / sqrt(s)) in norm, so at small lam its
+    preconditioned condition number ``1 + ||K - U U^T|| / lam`` stays large
+    (lam = 1e-2 stalls at 1000 iterations); the Nystrom
+    error is the Gram's own spectral tail.  ``Kl``: the solver's local rows
+    of ``K + lam I`` (n_loc x n), ``row0``: their first global row."""
+
+    def __init__(self, Kl: torch.Tensor, lam: float, s: int, n: int, row0: int = 0,
+                 context: Context | None = None, params: KrrParams | None = None, data: _Data | None = None):
+        from .. import default_context
+        from ..sketch.fjlt import _fisher_yates_prefix
+        ctx = context or default_context()
+        p = params or KrrParams()
+        self.data = data
+        self.lam = float(lam)
+        s = min(int(s), n)
+        idx = torch.as_tensor(_fisher_yates_prefix(ctx, n, s), dtype=torch.long)
+        idx_d = idx.to(Kl.device)
+        U = Kl.index_select(1, idx_d).to(torch.float64)        # n_loc x s, lam on the landmark rows
+        nl = Kl.shape[0]
+        loc = (idx >= row0) & (idx < row0 + nl)
+        li = torch.nonzero(loc).flatten()
+        if li.numel():
+            rows = (idx[li] - row0).to(Kl.device)
+            U[rows, li.to(Kl.device)] -= self.lam                # K itself, not K + lam I
+        Wb = torch.zeros(s, s, dtype=torch.float64, device=Kl.device)
+        if li.numel():
+            Wb[li.to(Kl.device)] = U[(idx[li] - row0).to(Kl.device)]
+        M = U.t() @ U
+        if data is not None:
+            data.allreduce(Wb)
+            data.allreduce(M)
+        M += self.lam * 0.5 * (Wb + Wb.t())
+        # a landmark pair at (numerically) the same point leaves W singular;
+        # lam W + U^T U stays SPD up to rounding -- a relative jitter covers it
+        M.diagonal().add_(1e-12 * float(M.diagonal().abs().max()))
+        Lc = torch.linalg.cholesky(M)
+        self.V = torch.linalg.solve_triangular(Lc, U.t(), upper=False).t() / math.sqrt(self.lam)
+        self._v32 = None
+        if self.V.is_cuda and getattr(p, "precond_f32", True):
+            from ..ops import normal_eq
+            V32 = self.V.to(torch.float32).contiguous()
+            if normal_eq.native_ok(V32, 1) and normal_eq.gemv_ok(V32, 1):
+                self._v32 = V32
 
 
 def faster_kernel_ridge(k: Kernel, X, Y, lam: float, s: int, context: Context | None = None,
@@ -359,7 +417,14 @@ def faster_kernel_ridge(k: Kernel, X, Y, lam: float, s: int, context: Context | 
         K.diagonal().add_(lam)
         op = DenseOp(K)
     _log(p, 1, "Creating preconditioner...")
-    P = IdPrecond() if s == 0 else FeatureMapPrecond(k, lam, None, s, context, params=p, data=data)
+    if s == 0:
+        P = IdPrecond()
+    elif p.precond == "nystrom":
+        Kl = Kd.local if data.distributed else K
+        r0 = data.D.row_range()[0] if data.distributed else 0
+        P = NystromPrecond(Kl, lam, s, data.n, r0, context, params=p, data=data if data.distributed else None)
+    else:
+        P = FeatureMapPrecond(k, lam, None, s, context, params=p, data=data)
     Yl = data.rows_of(Y).to(op.dtype)
     kp = KrylovIterParams(tolerance=p.tolerance, iter_lim=p.iter_lim, res_print=p.res_print,
                           am_i_printing=p.am_i_printing, log_level=p.log_level - 1, prefix=p.prefix + "\t")

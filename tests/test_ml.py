@@ -366,3 +366,39 @@ def test_libsvm_parser_bounds(tmp_path):
         q.write_bytes(bad)
         with pytest.raises((NativeLibraryError, RuntimeError, ValueError)):
             read_libsvm(str(q))
+
+
+def test_nystrom_precond_converges_at_small_lambda():
+    """at lambda = 1e-2 the reference's random-feature
+    Woodbury preconditioner leaves CG slow (its approximation error of K
+    divided by lambda bounds the preconditioned condition number); the
+    Nystrom option (KrrParams.precond = "nystrom", landmark columns of the
+    Gram the solver already holds) converges in a fraction of the iterations.
+    CPU, fp64."""
+    import libskylark_amd as sk
+    from libskylark_amd.algorithms import krylov as K
+    from libskylark_amd.algorithms.operators import DenseOp
+    from libskylark_amd.ml import krr
+    g = torch.Generator().manual_seed(0)
+    n, d, lam = 3000, 16, 1e-2
+    X = torch.randn(n, d, generator=g, dtype=torch.float64)
+    Y = torch.randn(n, 1, generator=g, dtype=torch.float64)
+    ker = sk.ml.kernel("gaussian", d, 4.0)
+    Kg = ker.symmetric_gram(X)
+    Kg.diagonal().add_(lam)
+    op = DenseOp(Kg)
+
+    def iters(P):
+        p = K.KrylovIterParams(tolerance=1e-6, iter_lim=2000)
+        A, code = K.cg(op, Y, params=p, M=P)
+        assert code == -1
+        assert float((Kg @ A - Y).norm() / Y.norm()) < 1e-5
+        return p.iterations
+
+    it_f = iters(krr.FeatureMapPrecond(ker, lam, X, 512, sk.Context(seed=3)))
+    it_n = iters(krr.NystromPrecond(Kg, lam, 512, n, 0, sk.Context(seed=3)))
+    assert it_n * 3 < it_f, (it_n, it_f)
+    # the public entry point with the option
+    A = sk.ml.faster_kernel_ridge(ker, X, Y, lam, 512, sk.Context(seed=3),
+                                  params=krr.KrrParams(precond="nystrom", tolerance=1e-6))
+    assert float((Kg @ A - Y).norm() / Y.norm()) < 1e-4
