@@ -217,6 +217,13 @@ struct P5Tiles {
                  // the next pass (walking the other way) finds them in the MALL
   int ntail;
   int nty;       // FINAL: non-temporal stores of Y (variant bit 12)
+  // EXT forms (sl_rsvd_pass_ext): the operand Zt holds [X_hi^T; X_lo^T]
+  // (2 kx rows) and step 1 folds the two halves, y = A (X_hi + X_lo) in f32
+  // (kx <= 8 real columns); EXT 2 also streams a given column-major D (m x
+  // kx, column stride lddc) beside A and forms W = A^T D instead of A^T y
+  int kx;
+  const float* D;
+  int64_t lddc;
 };
 
 #ifndef P1_PD
@@ -230,12 +237,13 @@ constexpr int P5_NBUF = 4, P5_BM = 16, P5_ROWB = 256, P5_REGION = 4096, P5_LPB =
 
 template <int KT>
 constexpr int p5_y16p() { return 16 * KT * P5_BM * 2 + 16; }
-template <int KT, bool FINAL>
+template <int KT, bool FINAL, int EXT = 0>
 constexpr int p5_lds() {
-  return P5_NBUF * 8 * P5_REGION + 4 * p5_y16p<KT>() + (FINAL ? 2 * P5_BM * 16 * KT * 4 : 0);
+  return P5_NBUF * 8 * P5_REGION + 4 * p5_y16p<KT>() + (FINAL ? 2 * P5_BM * 16 * KT * 4 : 0) +
+         (EXT == 2 ? P5_NBUF * P5_BM * 16 * 4 : 0);
 }
 
-template <int KT, bool FINAL, bool GRAM, bool YROLE, int TM, int KS>
+template <int KT, bool FINAL, bool GRAM, bool YROLE, int TM, int KS, int EXT>
 __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda,
                                         const bf16_t* __restrict__ Zt, int k, float* __restrict__ Wslab,
                                         double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
@@ -245,6 +253,8 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
   char* ring = smem;
   char* y16b = smem + NBUF * 8 * REGION;                 // [2 buffers][hi | lo]
   float* yfb = (float*)(y16b + 4 * Y16P);                // FINAL: [2][BM * k] f32 rows of y'
+  float* dsl = yfb + 2 * BM * KP;                        // EXT 2: [NBUF][16 columns][BM rows] of D
+  const int kr = EXT ? pt.kx : k;                        // real columns of y / W / Y
   const int lane = threadIdx.x & 63;
   const int g4 = lane >> 4, i16 = lane & 15;
   const int64_t nblocks = (m + BM - 1) / BM;
@@ -340,6 +350,17 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
           glds16s<false>(voff[i], (const void*)base, dst);
         }
       }
+      if constexpr (EXT == 2) {
+        // the block's D rows: lane l < 4 kx loads column l / 4, rows 4 (l % 4)
+        // .. + 3 (16 B, column-major D) into dsl[slot][col][row]; m % 16 == 0
+        // (the host checks), so every block is whole
+        if (w == 0) {
+          const int c = lane >> 2, rq = lane & 3;
+          const float* src = pt.D + (c < kr ? (int64_t)c * pt.lddc + r0 + 4 * rq : 0);
+          const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void*)(dsl + slot * BM * 16));
+          glds16((const void*)src, dst);
+        }
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < LPB; ++i) {
@@ -352,7 +373,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
       }
     }
   };
-  const int lpb = dma_on ? LPB : 0;
+  const int lpb = dma_on ? (EXT == 2 && w == 0 ? LPB + 1 : LPB) : 0;
 
   // ---- step 1 of block jb (y waves): tile w of y over all columns, published
   //      as the bf16 hi / lo B-fragment images (and, FINAL, the f32 rows of y')
@@ -410,6 +431,22 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
         for (int e = 0; e < 4; ++e)
           if (r0 + 4 * g4 + e >= m) acc[e] = 0.f;
       }
+      f32x4 yfold = acc;
+      if constexpr (EXT != 0) {
+        // y = A X_hi + A X_lo: column c + kx of the tile is column c's low part
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float part = __shfl_down(acc[e], kr, 16);
+          yfold[e] = i16 < kr ? acc[e] + part : 0.f;
+        }
+        acc = yfold;
+        if constexpr (EXT == 2) {
+          // step 3 takes D, not y: D's block rows from the slot DMA'd with A
+          const float* dsp = dsl + (int)(jb % NBUF) * BM * 16;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[e] = i16 < kr ? dsp[i16 * 16 + 4 * g4 + e] : 0.f;
+        }
+      }
       // y = hi + lo as two bf16 planes, by integer round-to-nearest-even on
       // the f32 bits (f_to_bf16) and packed by hand: the __bf16-typed form
       // of this conversion was miscompiled in some instantiations (wrong
@@ -435,9 +472,9 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
       }
       if constexpr (FINAL) {
         float* yf = yfb + (int)(jb & 1) * BM * KP;
-        if (col < k) {
+        if (col < kr) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) yf[(4 * g4 + e) * k + col] = yv[e];
+          for (int e = 0; e < 4; ++e) yf[(4 * g4 + e) * kr + col] = EXT ? yfold[e] : yv[e];
         }
       }
     }
@@ -446,9 +483,9 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
   // ---- FINAL: this wave's share of block jb's stored Y (after the barrier that
   //      published it).  Store waves: the W waves 0.. of the W role, one
   //      instruction each (float4 rows when ldy == k, else 4-B elements).
-  const bool vecY = FINAL && (k % 4 == 0) && (ldy == k);
+  const bool vecY = FINAL && (kr % 4 == 0) && (ldy == kr);
   const int wy = YROLE ? -1 : w - KT;                 // index among the W waves
-  const int nyv = (BM * k + (vecY ? 255 : 63)) / (vecY ? 256 : 64);   // store instructions per block
+  const int nyv = (BM * kr + (vecY ? 255 : 63)) / (vecY ? 256 : 64);   // store instructions per block
   const int nst = (!FINAL || wy < 0 || wy >= nyv) ? 0 : (nyv - wy + (8 - KT) - 1) / (8 - KT);
   auto store_y = [&](int64_t jb) {
     if constexpr (FINAL && !YROLE) {
@@ -457,7 +494,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
       for (int q = wy; q < nyv; q += 8 - KT) {
         if (vecY) {
           const int t = q * 64 + lane;
-          const bool ok = t < BM * k / 4 && r0 + (4 * t) / k < m;
+          const bool ok = t < BM * kr / 4 && r0 + (4 * t) / kr < m;
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           if (ok) v = *(const f32x4*)&yf[4 * t];
           float* dst = ok ? Y + r0 * ldy + 4 * t : scratch + 4 * lane;
@@ -465,8 +502,8 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
           else *(f32x4*)dst = v;
         } else {
           const int t = q * 64 + lane;
-          const int row = t / k, col = t - (t / k) * k;
-          const bool ok = t < BM * k && r0 + row < m;
+          const int row = t / kr, col = t - (t / kr) * kr;
+          const bool ok = t < BM * kr && r0 + row < m;
           const float v = ok ? yf[t] : 0.f;
           float* dst = ok ? Y + (r0 + row) * ldy + col : scratch + lane;
           *dst = v;
@@ -590,7 +627,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
 
   // ---- W partial slab [n][k]: this wave's tiles
   {
-    float* ws = Wslab + (int64_t)blockIdx.x * n * k;
+    float* ws = Wslab + (int64_t)blockIdx.x * n * kr;
 #pragma unroll
     for (int ct = 0; ct < TM; ++ct)
       if (ct < tcnt) {
@@ -600,7 +637,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int row = 16 * gt + 4 * g4 + e, col = 16 * t + i16;
-            if (row < n && col < k) ws[(int64_t)row * k + col] = accW[ct][t][e];
+            if (row < n && col < kr) ws[(int64_t)row * kr + col] = accW[ct][t][e];
           }
       }
   }
@@ -624,7 +661,7 @@ __device__ __forceinline__ void p5_body(const bf16_t* __restrict__ A, int64_t m,
   }
 }
 
-template <int KT, bool FINAL, bool GRAM, int KS>
+template <int KT, bool FINAL, bool GRAM, int KS, int EXT = 0>
 __global__ void __launch_bounds__(512, 1)
 k_rsvd_pass5(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const bf16_t* __restrict__ Zt, int k,
              float* __restrict__ Wslab, double* __restrict__ Gslab, float* __restrict__ Y, int64_t ldy,
@@ -638,13 +675,13 @@ k_rsvd_pass5(const bf16_t* __restrict__ A, int64_t m, int n, int64_t lda, const 
     // the y waves' W-tile count is a compile-time constant of their body
     const int yt = pt.cnt[0];
     if (yt == 0)
-      p5_body<KT, FINAL, GRAM, true, 0, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+      p5_body<KT, FINAL, GRAM, true, 0, KS, EXT>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
     else if (yt == 1)
-      p5_body<KT, FINAL, GRAM, true, 1, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+      p5_body<KT, FINAL, GRAM, true, 1, KS, EXT>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
     else
-      p5_body<KT, FINAL, GRAM, true, 2, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+      p5_body<KT, FINAL, GRAM, true, 2, KS, EXT>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
   } else {
-    p5_body<KT, FINAL, GRAM, false, P5_T2, KS>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
+    p5_body<KT, FINAL, GRAM, false, P5_T2, KS, EXT>(A, m, n, lda, Zt, k, Wslab, Gslab, Y, ldy, scratch, pt, smem, w);
   }
 }
 
@@ -723,6 +760,36 @@ int launch_pass5(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Z
   return SL_OK;
 }
 
+// EXT forms (fixed KT = 1, FINAL with Y, no Gram): see P5Tiles::kx
+template <int EXT>
+int launch_pass5_ext(const bf16_t* A, int64_t m, int n, int64_t lda, const bf16_t* Zt2, int kx, float* Wslab,
+                     float* Y, int64_t ldy, const float* D, int64_t lddc, float* scratch, int grid, hipStream_t s,
+                     int variant) {
+  P5Tiles pt{};
+  pt.prio = (variant >> 6) & 3;
+  pt.rev = (variant >> 8) & 1;
+  pt.kx = kx;
+  pt.D = D;
+  pt.lddc = lddc;
+  if (!p5_tiles(n, 1, &pt)) {
+    sl_set_last_error("rsvd_pass_ext: no tile split for this n");
+    return SL_ERR_UNSUPPORTED;
+  }
+  constexpr int LDS = p5_lds<1, true, EXT>();
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  if (n > 512) {
+    SL_LDS_ATTR((k_rsvd_pass5<1, true, false, 32, EXT>), LDS);
+    k_rsvd_pass5<1, true, false, 32, EXT><<<grid, 512, LDS, s>>>(A, m, n, lda, Zt2, 2 * kx, Wslab, nullptr, Y, ldy,
+                                                                 scratch, pt);
+  } else {
+    SL_LDS_ATTR((k_rsvd_pass5<1, true, false, 16, EXT>), LDS);
+    k_rsvd_pass5<1, true, false, 16, EXT><<<grid, 512, LDS, s>>>(A, m, n, lda, Zt2, 2 * kx, Wslab, nullptr, Y, ldy,
+                                                                 scratch, pt);
+  }
+  SL_LAUNCH_CHECK();
+  return SL_OK;
+}
+
 int cu_count() {
   static int ncu = -1;
   if (ncu < 0) {
@@ -791,6 +858,37 @@ SL_API int sl_rsvd_pass(const void* A, int64_t m, int64_t n, int64_t lda, const 
     default: SL_P5(3);
   }
 #undef SL_P5
+}
+
+// One-read normal products on the fused pass for a bf16 A with few columns
+// of X (BlockADMM's {Z Wbar, Z^T d} and {o = Z W, Z^T o} on its bf16 feature
+// cache): Zt2 = [X_hi^T; X_lo^T] (2 kx x n bf16, the hi / lo planes of the
+// f32 X, kx <= 8), Y (m x kx f32, row stride ldy) = A X (products of the
+// bf16 A with both planes, f32 sums), and the W slabs (reduced by
+// sl_rsvd_reduce_z with k = kx) = A^T y (D null) or A^T D (D given:
+// column-major m x kx f32, column stride lddc % 4 == 0, 16-B aligned, m % 16
+// == 0), the long operand entering the matrix cores as bf16 hi + lo (~2^-17
+// relative).  ws: sl_rsvd_pass_workspace(m, n, kx).
+SL_API int sl_rsvd_pass_ext(const void* A, int64_t m, int64_t n, int64_t lda, const void* Zt2, int kx, void* ws,
+                            float* Y, int64_t ldy, const float* D, int64_t lddc, int variant, void* stream) {
+  if (m <= 0) return SL_OK;
+  if (n % 8 || lda % 8 || n > 1024 || n < 16 || kx < 1 || kx > 8 || !Y || ldy < kx ||
+      (D && (m % 16 || lddc % 4 || ((uintptr_t)D & 15) || lddc < m))) {
+    sl_set_last_error("rsvd_pass_ext: needs n % 8 == 0, lda % 8 == 0, 16 <= n <= 1024, 1 <= kx <= 8, Y; "
+                      "D: m % 16 == 0, lddc % 4 == 0, 16-B aligned");
+    return SL_ERR_UNSUPPORTED;
+  }
+  const int grid = sl_rsvd_pass_grid(m);
+  char* base = (char*)ws;
+  int64_t off = ((int64_t)grid * n * kx * 4 + 255) & ~(int64_t)255;
+  off += (int64_t)grid * kx * kx * 8;
+  off = (off + 255) & ~(int64_t)255;
+  float* scratch = (float*)(base + off);
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* z = (const bf16_t*)Zt2;
+  hipStream_t s = (hipStream_t)stream;
+  return D ? launch_pass5_ext<2>(a, m, (int)n, lda, z, kx, (float*)base, Y, ldy, D, lddc, scratch, grid, s, variant)
+           : launch_pass5_ext<1>(a, m, (int)n, lda, z, kx, (float*)base, Y, ldy, nullptr, 0, scratch, grid, s, variant);
 }
 
 // Sum the pass slabs: W (n x k, into Wout with row stride ldw; f64 when

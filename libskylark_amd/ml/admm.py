@@ -133,6 +133,7 @@ class BlockADMMSolver:
         self.num_threads = 1
         self.one_pass = True      # fused Z-pair passes where the kernel applies
         self.native_prox = True   # fused native prox / consensus passes (admm_kernels.hip) on that path
+        self.mfma_pass = True     # bf16 feature cache: the two Z passes on the matrix cores (normal_eq.pass_mfma)
         if feature_maps is not None:
             self.maps = list(feature_maps)
             self.sizes = [S.get_S() for S in self.maps]
@@ -298,7 +299,16 @@ class BlockADMMSolver:
                     cache[j] = torch.cholesky_inverse(torch.linalg.cholesky(C)).to(dt)
                 Wb = Wbar[st:st + sj]
                 one_pass = fused and normal_eq.native_ok(Z, kp)
-                if one_pass:
+                # bf16 feature cache: both passes on the matrix cores (the
+                # randSVD fused pass's EXT form) instead of the VALU widening
+                # kernel
+                mfma = (one_pass and self.mfma_pass and Z.dtype == torch.bfloat16
+                        and normal_eq.mfma_ok(Z, kp, Dp.t()))
+                if mfma:
+                    ztd, yz = normal_eq.pass_mfma(Z, padded("wb", j, Wb), D=Dp.t())
+                    zw_sum += yz
+                    ztd = ztd[:, :k]
+                elif one_pass:
                     # pass 1: {Z Wbar_j, Z^T dsum^T} from one read of Z
                     ztd, _ = normal_eq.dual(Z, Dp.t(), padded("wb", j, Wb), y_out=zw_sum)   # zw_sum += Z Wb
                     ztd = ztd[:, :k]
@@ -311,7 +321,11 @@ class BlockADMMSolver:
                 rhs = Wb - mu_ij[st:st + sj] + ZtObar[st:st + sj] + ztd / (P + 1.0)
                 Wi_j = cache[j] @ rhs
                 Wi[st:st + sj] = Wi_j
-                if one_pass:
+                if mfma:
+                    zto, yo = normal_eq.pass_mfma(Z, padded("wi", j, Wi_j))
+                    zo_sum += yo
+                    ZtObar[st:st + sj] = zto[:, :k]
+                elif one_pass:
                     # pass 2: {o = Z Wi_j, Z^T o} from one read of Z
                     zto, _ = normal_eq.ata(Z, padded("wi", j, Wi_j), want_y=True, y_out=zo_sum)   # zo_sum += o
                     ZtObar[st:st + sj] = zto[:, :k]

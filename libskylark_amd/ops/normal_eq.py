@@ -19,6 +19,9 @@ _lib.register("sl_ata_workspace", [i64, i32], C.c_int64)
 _lib.register("sl_ata_pass2", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp])
 _lib.register("sl_ata_pass3", [vp, i32, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i64, vp, vp, i32])
 _lib.register("sl_gemv_rows_f32", [vp, i64, i64, i64, vp, i32, vp, i64, vp])
+_lib.register("sl_rsvd_pass_ext", [vp, i64, i64, i64, vp, i32, vp, vp, i64, vp, i64, i32, vp])
+_lib.register("sl_rsvd_pass_workspace", [i64, i64, i32], C.c_int64)
+_lib.register("sl_rsvd_reduce_z", [vp, i64, i64, i32, vp, i32, i32, vp, i32, vp, vp])
 _DT = {torch.float32: 0, torch.bfloat16: 2}   # SlDtype codes of the stored A
 
 _WS: dict = {}
@@ -120,3 +123,48 @@ def gemv(A: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
     _lib.call("sl_gemv_rows_f32", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Xt), k, _lib.ptr(Y), Y.stride(0),
               C.c_void_p(_lib.stream_of(A)))
     return Y[:, 0] if vec else Y
+
+
+# ------------------------------------------------------------ matrix-core form
+def mfma_ok(A: torch.Tensor, k: int, D: torch.Tensor | None = None) -> bool:
+    """Can the fused pass's EXT form (rsvd_pass.hip sl_rsvd_pass_ext) take this
+    bf16 A (n <= 1024 columns) with k <= 8 right-hand sides (and D)?"""
+    if not (isinstance(A, torch.Tensor) and A.is_cuda and A.dtype == torch.bfloat16 and A.dim() == 2
+            and A.stride(1) == 1 and A.stride(0) % 8 == 0 and A.shape[1] % 8 == 0 and 16 <= A.shape[1] <= 1024
+            and 1 <= k <= 8 and A.data_ptr() % 16 == 0 and _lib.available()):
+        return False
+    if D is not None:
+        m = A.shape[0]
+        return (D.is_cuda and D.dtype == torch.float32 and D.shape == (m, k) and D.stride(0) == 1
+                and D.stride(1) % 4 == 0 and D.stride(1) >= m and D.data_ptr() % 16 == 0 and m % 16 == 0)
+    return True
+
+
+def pass_mfma(A: torch.Tensor, X: torch.Tensor, D: torch.Tensor | None = None):
+    """``(W, Y)`` with ``Y = A X`` (m x k f32) and ``W = A^T Y`` -- or ``W =
+    A^T D`` when D is given -- from ONE read of the bf16 A on the matrix
+    cores: the randSVD fused pass (LDS-DMA ring, MFMA) with X entering as its
+    bf16 hi / lo planes (products exact, f32 sums) and the long operand of
+    the W product as bf16 hi + lo (~2^-17 relative).  BlockADMM's two
+    passes per feature block over its bf16 cache (reference
+    ml/BlockADMM.hpp:400-498); the VALU widening kernel (``dual`` / ``ata``)
+    is issue-bound on bf16 (3.4-3.6 TB/s)."""
+    m, n = A.shape
+    k = X.shape[1]
+    Xf = X.to(torch.float32)
+    hi = Xf.to(torch.bfloat16)
+    lo = (Xf - hi.float()).to(torch.bfloat16)
+    Zt2 = torch.cat([hi.t(), lo.t()]).contiguous()            # 2k x n
+    lib = _lib.require()
+    nb = int(lib.sl_rsvd_pass_workspace(m, n, k))
+    key = ("mfma", str(A.device), torch.cuda.current_stream(A.device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nb:
+        ws = _WS[key] = torch.empty(nb, dtype=torch.uint8, device=A.device)
+    Y = torch.empty(m, k, dtype=torch.float32, device=A.device)
+    st = vp(_lib.stream_of(A))
+    _lib.call("sl_rsvd_pass_ext", _lib.ptr(A), m, n, A.stride(0), _lib.ptr(Zt2), k, _lib.ptr(ws), _lib.ptr(Y), k,
+              _lib.ptr(D) if D is not None else None, D.stride(1) if D is not None else 0, 0, st)
+    W = torch.empty(n, k, dtype=torch.float32, device=A.device)
+    _lib.call("sl_rsvd_reduce_z", _lib.ptr(ws), m, n, k, _lib.ptr(W), 0, k, None, 0, None, st)
+    return W, Y

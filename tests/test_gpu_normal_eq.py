@@ -149,3 +149,29 @@ def test_normal_form_lsqr_unpreconditioned_ill_conditioned(dev, cond):
     rc = float((A @ Xc - b).norm())
     rf = float((A @ Xf - b).norm())
     assert rf <= 1.01 * rc, (rf, rc, cf, cc)
+
+
+@pytest.mark.parametrize("m,n,k,with_d", [(50000, 1024, 4, True), (50000, 1024, 4, False), (20000, 512, 2, True),
+                                          (30000, 304, 1, True), (20003, 1000, 8, False), (4096, 16, 3, True)])
+def test_pass_mfma_matches_fp64(m, n, k, with_d):
+    """The fused pass's EXT form (rsvd_pass.hip sl_rsvd_pass_ext, BlockADMM's
+    bf16-cache passes): Y = A X from X's bf16 hi / lo planes, W = A^T Y or
+    A^T D with the long operand as bf16 hi + lo -- against fp64 products of the
+    same bf16 A (partial last row block, n not a multiple of 32, k = 1..8)."""
+    from libskylark_amd.ops import normal_eq as NE
+    g = torch.Generator(device="cuda").manual_seed(m + n + k)
+    A = (torch.randn(m, n, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    X = torch.randn(n, k, device="cuda", generator=g)
+    D = None
+    if with_d:
+        Db = torch.randn(k, m, device="cuda", generator=g)
+        D = Db.t()                       # column-major m x k, as BlockADMM's Dp.t()
+    assert NE.mfma_ok(A, k, D)
+    W, Y = NE.pass_mfma(A, X, D)
+    Ad = A.double()
+    Yr = Ad @ X.double()
+    torch.testing.assert_close(Y.double(), Yr, rtol=0, atol=1e-5 * float((Ad.abs() @ X.double().abs()).max()))
+    L = D.double() if with_d else Y.double()
+    Wr = Ad.t() @ L
+    tol = 3e-5 * float((Ad.abs().t() @ L.abs()).max())
+    torch.testing.assert_close(W.double(), Wr, rtol=0, atol=tol)
