@@ -56,4 +56,4 @@ for k, r in ((40, 20), (48, 24), (32, 16), (64, 32), (16, 8)):
             orth = float(np.max(np.abs(U.T @ U - np.eye(r))))
             print(json.dumps({"k": k, "r": r, "matrix": kind, "tri": ["one_wave", "four_waves"][v], "us": us,
                               "lam_err": lerr, "resid": res, "orth": orth, "status": int(st.item())}))
-_lib.require().sl_sym_eig_set_tri_variant(1)
+_lib.require().sl_sym_eig_set_tri_variant(-1)

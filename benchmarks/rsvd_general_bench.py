@@ -99,7 +99,8 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
 CASES = {
     "f32": lambda reps: run(1_000_000, 1000, 20, 2, torch.float32, reps=reps),
     "f64": lambda reps: run(200_000, 5000, 20, 2, torch.float64, reps=reps),
-    "f64k128": lambda reps: run(200_000, 5000, 64, 1, torch.float64, reps=reps),   # k = 128: library small algebra
+    "f64k128": lambda reps: run(200_000, 5000, 64, 1, torch.float64, reps=reps),   # k = 128
+    "f32k128": lambda reps: run(1_000_000, 1000, 64, 1, torch.float32, reps=reps),
     "bf16": lambda reps: run(1_000_000, 1000, 20, 2, torch.bfloat16, reps=reps),  # the fused engine, for comparison
 }
 

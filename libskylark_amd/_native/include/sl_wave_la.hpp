@@ -359,6 +359,123 @@ __device__ __forceinline__ void wg_chol_invB(const double* G, int ldg, double* X
   }
 }
 
+// The B-pivot elimination for 64 < k <= 128: a row of [G | I] spans TWO
+// waves (thread column c = tid & 127) and the rows cycle over the NG =
+// blockDim / 128 row groups (row i in group i % NG, register i / NG).
+// Everything else -- the block rows published to LDS once per B pivots, the
+// pivot block formed redundantly by every thread, the multipliers of row i
+// read by symmetry from the published rows at column i (one broadcast LDS
+// read per block row), pivot dropping -- is wg_chol_invB's.  NG % B == 0 so
+// the B block rows sit in B different groups.  fsh >= 2 * B * 128 + 136
+// doubles of 16-B aligned LDS.  Every thread of the (NG * 128)-thread
+// workgroup calls it.  The general randSVD engine's CholeskyQR at k = 65 ..
+// 128 (eigen-whitening on rocSOLVER syevd before: ~2.4 ms per factor).
+template <int K, int NG, int B>
+__device__ __forceinline__ void wg_chol_invW(const double* G, int ldg, double* X, int ldx, int k, double* fsh,
+                                             int* st) {
+  static_assert(K % NG == 0 && K % B == 0 && K <= 128 && NG % B == 0 && (B == 2 || B == 4), "K");
+  constexpr int R = K / NG, CW = 128;
+  const int tid = threadIdx.x, c = tid & (CW - 1);
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 7);
+  double* rowbuf = fsh;              // [2][B][128]
+  double* dsh = fsh + 2 * B * CW;    // d_i (0: dropped)
+  double* red = dsh + CW;            // max G_ii
+  double M[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int i = q * NG + g;
+    M[q] = (i < k && c < k) ? G[i * ldg + c] : (i == c ? 1.0 : 0.0);
+  }
+  if (tid < 64) {
+    const double a = tid < k ? fabs(G[tid * ldg + tid]) : 0.0;
+    const double b = tid + 64 < k ? fabs(G[(tid + 64) * ldg + tid + 64]) : 0.0;
+    const double mx = wave_max(fmax(a, b));
+    if (tid == 0) red[0] = mx;
+  }
+  __syncthreads();
+  const double thr = 1e-13 * red[0];
+  int bad = 0;
+#pragma unroll 1
+  for (int j = 0; j < K; j += B) {
+    double* rb = rowbuf + ((j / B) & 1) * B * CW;
+#pragma unroll
+    for (int t = 0; t < B; ++t)
+      if (g == (j + t) % NG) {
+        // (j + t) / NG is this group's register of row j + t; R is small and
+        // the index is wave-uniform, so a select chain keeps M in registers
+        const int qj = (j + t) / NG;
+        double v = M[0];
+#pragma unroll
+        for (int q = 1; q < R; ++q) v = q == qj ? M[q] : v;
+        rb[t * CW + c] = v;
+      }
+    __syncthreads();
+    double rl[B], pb[B][B];
+#pragma unroll
+    for (int t = 0; t < B; ++t) {
+      rl[t] = rb[t * CW + c];
+#pragma unroll
+      for (int u = 0; u < B; ++u) pb[t][u] = rb[t * CW + j + u];
+    }
+    double rc[B], f[B][B];
+#pragma unroll
+    for (int t = 0; t < B; ++t) {
+      const double d = pb[t][t];
+      const bool ok = (d > thr && d == d) || j + t >= k;
+      bad |= !ok;
+      rc[t] = ok ? rcp64(d) : 0.0;
+      if (tid == 0) dsh[j + t] = ok ? d : 0.0;
+#pragma unroll
+      for (int u = t + 1; u < B; ++u) {
+        f[u][t] = pb[u][t] * rc[t];
+#pragma unroll
+        for (int v = t + 1; v < B; ++v) pb[u][v] = fma(-f[u][t], pb[t][v], pb[u][v]);
+        rl[u] = c == j + t ? -f[u][t] : fma(-f[u][t], rl[t], rl[u]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = q * NG + g;   // wave-uniform
+      if (i >= j + B) {
+        double a[B], m[B];
+#pragma unroll
+        for (int t = 0; t < B; ++t) a[t] = rb[t * CW + i];
+#pragma unroll
+        for (int t = 0; t < B; ++t) {
+          m[t] = a[t] * rc[t];
+#pragma unroll
+          for (int v = t + 1; v < B; ++v) a[v] = fma(-m[t], pb[t][v], a[v]);
+        }
+        double x = M[q];
+#pragma unroll
+        for (int t = 0; t < B; ++t) x = c == j + t ? -m[t] : fma(-m[t], rl[t], x);
+        M[q] = x;
+      } else if (i >= j) {
+        const int u = i - j;
+        double x = rl[0];
+#pragma unroll
+        for (int t = 1; t < B; ++t) x = u == t ? rl[t] : x;
+        M[q] = c == i ? 1.0 : ((c > i && c < j + B) ? 0.0 : x);
+      } else {
+        M[q] = (c >= j && c < j + B) ? 0.0 : M[q];
+      }
+    }
+  }
+  if (bad && tid == 0) atomicOr(st, 1);
+  __syncthreads();
+  if (c < k) {
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = q * NG + g;
+      if (i < k) {
+        const double di = dsh[i];
+        const double rs = di > 0.0 ? rsq64(di) : 0.0;
+        X[c * ldx + i] = i >= c ? M[q] * rs : 0.0;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------- tridiagonalisation
 // T = Q^T C Q, Q = H_0 H_1 ... H_{K-3}, H_j = I - 2 v_j v_j^T, by ONE wave:
 // lane i keeps row i of the trailing matrix in registers.  Step j: ||x||

@@ -24,9 +24,10 @@
 // sl_tsk_gram64, the CholeskyQR factors and the core eigensolver on the
 // one-wave kernels of sl_wave_la.hpp (sl_chol_inv_wave, sl_sym_eig_tridiag;
 // Jacobi re-solve when flagged) -- no rocBLAS / rocSOLVER call.  bf16 A (n >
-// 1024) and 64 < k <= 128 keep library GEMMs (rocBLAS) and rocSOLVER (syevd
-// eigen-whitening, syevd core).  W, H, G and the core are f64 whatever A's
-// precision.
+// 1024) and 64 < k <= 128 keep library GEMMs (rocBLAS); the CholeskyQR
+// factors stay on the register kernels up to k = 128 (two waves per row), the
+// core of 64 < k <= 128 on rocSOLVER syevd.  W, H, G and the core are f64
+// whatever A's precision.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -62,6 +63,8 @@ SL_API int sl_ts_gram64(const double* X, int64_t rows, int k, int64_t ldx, doubl
                         void* stream);
 SL_API int sl_ts_small(int ta, int tb, int mr, int nc, int kd, const double* A, int lda, const double* B, int ldb,
                        double* C, int ldc, void* stream);
+SL_API int sl_ts_gram_w(const void* X, int dt, int64_t rows, int k, int64_t ldx, double* G, int ldg, void* ws,
+                        void* stream);
 SL_API int sl_tsk_f32_xm(const float* Y, int64_t m, int k, int64_t ldy, const float* M, int k2, float* out,
                          int64_t ldo, double* G, void* ws, void* stream);
 
@@ -176,8 +179,6 @@ __global__ void k_status_merge(int* __restrict__ st) {
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
-constexpr int64_t GPIECE = 65536;   // rows per f64 staging piece of the k > 64 f32 Gram
-
 size_t esize(int dt) { return dt == SL_F64 ? 8 : dt == SL_F32 ? 4 : 2; }
 
 struct GPlan {
@@ -231,42 +232,13 @@ unsigned grid_of(int64_t tot) {
   return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
 }
 
-// X = R^{-1} of the SPD k x k G (row-major f64), status bit ST_PIVOT via st
-// X (row-major k x k) = V diag(lambda^{-1/2}) from G = V diag(lambda) V^T
-// (eigenvectors in the rows of Vt, ascending), directions with lambda at or
-// below 1e-13 max lambda dropped (zero columns; status bit 1): X^T G X = I
-// on the retained subspace -- the rank-revealing counterpart of the one-wave
-// kernel's pivot dropping.
-__global__ void __launch_bounds__(256) k_whiten(const double* __restrict__ Vt, const double* __restrict__ D, int k,
-                                                double* __restrict__ X, int* __restrict__ st) {
-  __shared__ double scale[128];
-  const double lmax = D[k - 1];
-  for (int j = threadIdx.x; j < k; j += 256) {
-    const double l = D[j];
-    const bool keep = l > 1e-13 * lmax && lmax > 0.0;
-    scale[j] = keep ? 1.0 / sqrt(l) : 0.0;
-    if (!keep) atomicOr(st, 1);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < k * k; e += 256) {
-    const int i = e / k, j = e % k;
-    X[e] = Vt[(int64_t)j * k + i] * scale[j];
-  }
-}
-
+// X = R^{-1} of the SPD k x k G (row-major f64) by the register Cholesky
+// kernels (k <= 64: sl_wave_la.hpp wg_chol_invB; 64 < k <= 128: two waves per
+// row, wg_chol_invW), pivots at or below 1e-13 max G_ii dropped (zero row /
+// column, status bit ST_PIVOT via st).  (64 < k <= 128 ran eigen-whitening on
+// rocSOLVER syevd before: ~2.4 ms per factor, four factors per q = 1 call.)
 int chol_inv(GPlan* p, const double* G, double* X, int* st, hipStream_t s) {
-  if (p->k <= 64) return sl_chol_inv_wave(G, p->k, p->k, X, st, s);
-  // k > 64: eigen-whitening on rocSOLVER (a Cholesky of a numerically
-  // rank-deficient Gram breaks down; the whitening drops those directions)
-  const int k = p->k;
-  double* T = (double*)p->gws;                 // k x k eigenvectors (reuses the Gram workspace)
-  double* D = p->eig + k * p->r + p->r;         // k eigenvalues + k scratch (the core's syevd region)
-  SL_HIP_CHECK(hipMemcpyAsync(T, G, (size_t)k * k * 8, hipMemcpyDeviceToDevice, s));
-  int rc = slb_dsyevd(k, T, k, D, D + k, st + 1, s);
-  if (rc != SL_OK) return rc;
-  k_whiten<<<1, 256, 0, s>>>(T, D, k, X, st);
-  SL_LAUNCH_CHECK();
-  return SL_OK;
+  return sl_chol_inv_wave(G, p->k, p->k, X, st, s);
 }
 
 // the sketch operator of the call into Z (dt)
@@ -295,42 +267,15 @@ int make_z(GPlan* p, hipStream_t s) {
   return SL_OK;   // Z set explicitly
 }
 
-// G (k x k f64) = Yb^T Yb of an m x k matrix in the pass precision (f64:
-// strided-batched row-chunk products + one f64 slab sum; f32: the fp64 Gram
-// kernel for k <= 64, else f64 copies of row pieces)
+// G (k x k f64) = Yb^T Yb of an m x k matrix in the pass precision (f64, or
+// f32 for f32 / bf16 A), f64 products and sums: the matrix-core Gram kernels
+// (k <= 64: sl_ts_gram64 / sl_tsk_gram64; 64 < k <= 128: sl_ts_gram_w)
 int gram(GPlan* p, const void* Yb, double* G, hipStream_t s) {
   const int64_t m = p->m;
   const int k = p->k;
-  int rc;
-  if (p->hand && p->dt == SL_F64) return sl_ts_gram64((const double*)Yb, m, k, k, G, k, p->g64w, s);
-  if (p->dt == SL_F64) {
-    const int64_t tg = (int64_t)k * k;
-    rc = slb_gemm_strided(SL_F64, true, false, k, k, p->ch, 1.0, Yb, k, p->ch * k, Yb, k, p->ch * k, 0.0, p->parts,
-                          k, tg, p->np, s);
-    if (rc != SL_OK) return rc;
-    const int64_t r0 = p->ch * p->np;
-    int nparts = p->np;
-    if (r0 < m) {
-      rc = slb_gemm(SL_F64, true, false, k, k, m - r0, 1.0, (const double*)Yb + r0 * k, k,
-                    (const double*)Yb + r0 * k, k, 0.0, (double*)p->parts + (int64_t)p->np * tg, k, s);
-      if (rc != SL_OK) return rc;
-      ++nparts;
-    }
-    k_sum_parts<double><<<grid_of(tg), 256, 0, s>>>((const double*)p->parts, nparts, tg, G, nullptr);
-    SL_LAUNCH_CHECK();
-    return SL_OK;
-  }
-  if (k <= 64) return sl_tsk_gram64((const float*)Yb, m, k, k, G, p->gws, s);
-  SL_HIP_CHECK(hipMemsetAsync(G, 0, (size_t)k * k * 8, s));
-  for (int64_t q0 = 0; q0 < m; q0 += GPIECE) {
-    const int64_t rows = (m - q0 < GPIECE) ? m - q0 : GPIECE;
-    k_cast2d<float, double><<<grid_of(rows * k), 256, 0, s>>>((const float*)Yb + q0 * k, k, rows, k,
-                                                               (double*)p->gws, k, nullptr);
-    SL_LAUNCH_CHECK();
-    rc = slb_gemm(SL_F64, true, false, k, k, rows, 1.0, p->gws, k, p->gws, k, 1.0, G, k, s);
-    if (rc != SL_OK) return rc;
-  }
-  return SL_OK;
+  if (k > 64) return sl_ts_gram_w(Yb, p->dt == SL_F64 ? SL_F64 : SL_F32, m, k, k, G, k, p->g64w, s);
+  if (p->dt == SL_F64) return sl_ts_gram64((const double*)Yb, m, k, k, G, k, p->g64w, s);
+  return sl_tsk_gram64((const float*)Yb, m, k, k, G, p->gws, s);
 }
 
 // first half of pass i: Y = A Z and its Gram Y^T Y -> WG[n k :] (all-reduced
@@ -428,7 +373,8 @@ int inter(GPlan* p, int i, hipStream_t s) {
     if (rc != SL_OK) return rc;
     return sl_ts_xm64(p->WG, n, k, k, p->Ri, k, p->Z, k, p->dt, s);   // Z = W R^{-1} in A's dtype
   }
-  int rc = slb_gemm(SL_F64, true, false, k, k, n, 1.0, p->WG, k, p->WG, k, 0.0, p->H, k, s);
+  int rc = k > 64 ? sl_ts_gram_w(p->WG, SL_F64, n, k, k, p->H, k, p->g64w, s)
+                  : slb_gemm(SL_F64, true, false, k, k, n, 1.0, p->WG, k, p->WG, k, 0.0, p->H, k, s);
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
   if (rc != SL_OK) return rc;
@@ -468,7 +414,8 @@ int core(GPlan* p, hipStream_t s) {
   const double* W = p->WG;
   const double* G = p->WG + n * k;
   int rc = p->hand ? sl_ts_gram64(W, n, k, k, p->H, k, p->g64w, s)
-                   : slb_gemm(SL_F64, true, false, k, k, n, 1.0, W, k, W, k, 0.0, p->H, k, s);   // H = W^T W
+           : k > 64 ? sl_ts_gram_w(W, SL_F64, n, k, k, p->H, k, p->g64w, s)
+                    : slb_gemm(SL_F64, true, false, k, k, n, 1.0, W, k, W, k, 0.0, p->H, k, s);   // H = W^T W
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, G, p->Ri, p->st + 8, s);
   if (rc != SL_OK) return rc;
@@ -581,11 +528,7 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   const int64_t o_n = off;   off = align256(off + (int64_t)k * r * 8);
   const int64_t o_md = off;  off = align256(off + (int64_t)k * r * 8);
   const int64_t o_vf = off;  off = align256(off + n * r * 8);
-  const int64_t o_gw = off;
-  // k > 64: f32 AND bf16 A keep Y in f32 and stage GPIECE-row f64 pieces of
-  // it here (gram()); f64 A only reuses it for the k x k eigenvectors
-  off = align256(off + (k <= 64 ? sl_tsk_gram64_workspace(m, k)
-                                 : std::max<int64_t>(dt != SL_F64 ? GPIECE * k * 8 : 0, (int64_t)k * k * 8)));
+  const int64_t o_gw = off;  off = align256(off + (k <= 64 ? sl_tsk_gram64_workspace(m, k) : 256));
   // f32 / f64 A: row-chunk partials of A^T Y (and of Y^T Y), <= 64 MB of slabs
   int np = 0;
   int64_t ch = 0;
@@ -596,7 +539,7 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   }
   const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 && !hand ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
   const int64_t o_aw = off;  off = align256(off + (hand ? sl_ts_atq_workspace(m, n, k, dt) : 0));
-  const int64_t o_g6 = off;  off = align256(off + (hand ? sl_ts_gram64_workspace(std::max(m, n), k) : 0));
+  const int64_t o_g6 = off;  off = align256(off + (hand || k > 64 ? sl_ts_gram64_workspace(std::max(m, n), k) : 0));
   const int64_t o_st = off;  off = align256(off + 64 * 4);
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;

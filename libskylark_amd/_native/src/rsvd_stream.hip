@@ -8,6 +8,7 @@
 //                                                         per-row-group slabs + f64 sum
 //   sl_ts_xm64   out (rows x k2, f32 / f64) = X (rows x k, f64) M (k x k2, f64)
 //   sl_ts_gram64 G (k x k, f64) = X^T X (X rows x k, f64)
+//   sl_ts_gram_w G = X^T X for 64 < k <= 128 (X f32 / f64)
 //   sl_ts_small  C = op(A) op(B), k x k operands, one workgroup (f64)
 //
 // Both big products run in A's own precision on the matrix cores
@@ -699,6 +700,72 @@ __global__ void __launch_bounds__(256) k_ts_gram64m(const double* __restrict__ X
   }
 }
 
+// X^T X for 64 < k <= 128 (f32 or f64 X, f64 products and sums): the 36
+// upper 16 x 16 tile pairs of the 8 x 8 tile grid are dealt round-robin to
+// the four waves (9 accumulators each, 72 VGPRs: all 36 on one wave would
+// need 288), and the four waves of a workgroup walk the SAME rows -- wave w
+// loads all 8 column tiles of each 4-row step (the other waves' loads of the
+// same lines hit L1 / L2) and keeps only its own pairs.  Each workgroup owns
+// a contiguous row range and writes its k x k slab directly (the pairs are
+// disjoint: no LDS reduction), mirrored from the upper tiles.
+__host__ __device__ constexpr int gw_pa(int p) { int a = 0; while (p >= 8 - a) { p -= 8 - a; ++a; } return a; }
+__host__ __device__ constexpr int gw_pb(int p) { int a = 0; while (p >= 8 - a) { p -= 8 - a; ++a; } return a + p; }
+
+template <typename T, int W>
+__device__ __forceinline__ void gram_w_body(const T* __restrict__ X, int64_t rows, int k, int64_t ldx,
+                                            double* __restrict__ slab) {
+  constexpr int KT = 8, NP = 9, U = 4;
+  const int lane = threadIdx.x & 63, kg = lane >> 4, r16 = lane & 15;
+  f64x4 acc[NP];
+#pragma unroll
+  for (int e = 0; e < NP; ++e) acc[e] = f64x4{};
+  const int64_t nq = (rows + 3) >> 2;
+  const int64_t q0 = nq * blockIdx.x / gridDim.x, q1 = nq * (blockIdx.x + 1) / gridDim.x;
+  for (int64_t q = q0; q < q1; q += U) {
+    double xv[U][KT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = 4 * (q + u) + kg;
+      const bool rok = q + u < q1 && row < rows;
+      const T* src = X + (rok ? row : 0) * ldx;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int c = 16 * t + r16;
+        xv[u][t] = (rok && c < k) ? (double)src[c] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < NP; ++e)
+        acc[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[u][gw_pa(W + 4 * e)], xv[u][gw_pb(W + 4 * e)], acc[e], 0, 0, 0);
+  }
+  double* sb = slab + (int64_t)blockIdx.x * k * k;
+#pragma unroll
+  for (int e = 0; e < NP; ++e) {
+    const int a = gw_pa(W + 4 * e), b = gw_pb(W + 4 * e);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * a + Mf<double>::drow(lane, r), j = 16 * b + r16;
+      if (i < k && j < k) {
+        sb[(int64_t)i * k + j] = acc[e][r];
+        if (a != b) sb[(int64_t)j * k + i] = acc[e][r];
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_ts_gram_w(const T* __restrict__ X, int64_t rows, int k, int64_t ldx,
+                                                   double* __restrict__ slab) {
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: gram_w_body<T, 0>(X, rows, k, ldx, slab); break;
+    case 1: gram_w_body<T, 1>(X, rows, k, ldx, slab); break;
+    case 2: gram_w_body<T, 2>(X, rows, k, ldx, slab); break;
+    default: gram_w_body<T, 3>(X, rows, k, ldx, slab); break;
+  }
+}
+
 // C (mr x nc, ldc) = op(A) op(B), op(A) mr x kd, op(B) kd x nc, row-major f64,
 // one workgroup (k x k sizes of the core): both operands staged in LDS first
 // when they fit (coalesced reads; the strided global form took ~36 us)
@@ -956,6 +1023,23 @@ SL_API int sl_ts_gram64(const double* X, int64_t rows, int k, int64_t ldx, doubl
     case 3: k_ts_gram64m<3><<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws); break;
     default: k_ts_gram64m<4><<<g, 256, 0, s>>>(X, rows, k, ldx, (double*)ws); break;
   }
+  SL_LAUNCH_CHECK();
+  return sl_slab_reduce_launch_d2d((const double*)ws, g, (int64_t)k * k, k, k, k, G, ldg, s);
+}
+
+// G (k x k f64, ldg) = X^T X for 64 < k <= 128, X rows x k f32 (dt SL_F32) or
+// f64 (ldx); ws: sl_ts_gram64_workspace bytes
+SL_API int sl_ts_gram_w(const void* X, int dt, int64_t rows, int k, int64_t ldx, double* G, int ldg, void* ws,
+                        void* stream) {
+  if (k < 1 || k > 128 || ldx < k || ldg < k || (dt != SL_F32 && dt != SL_F64)) {
+    sl_set_last_error("ts_gram_w: needs 1 <= k <= 128, f32 / f64");
+    return SL_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (rows <= 0) return hipMemset2DAsync(G, (size_t)ldg * 8, 0, (size_t)k * 8, (size_t)k, s) == hipSuccess ? SL_OK : SL_ERR_HIP;
+  const int g = gram_grid(rows);
+  if (dt == SL_F64) k_ts_gram_w<double><<<g, 256, 0, s>>>((const double*)X, rows, k, ldx, (double*)ws);
+  else k_ts_gram_w<float><<<g, 256, 0, s>>>((const float*)X, rows, k, ldx, (double*)ws);
   SL_LAUNCH_CHECK();
   return sl_slab_reduce_launch_d2d((const double*)ws, g, (int64_t)k * k, k, k, k, G, ldg, s);
 }

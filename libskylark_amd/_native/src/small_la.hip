@@ -190,13 +190,33 @@ __global__ void __launch_bounds__(V == 3 || V == 5 ? 512 : 256) k_chol_inv_wave(
 // 1: one pivot per step over 4 waves for K <= 48 (64 on one wave), 0: one wave,
 // 2 / 3 / 5: two pivots over 4 / 8 waves, four over 8 (A/B)
 int g_chol_variant = 4;
+
+// 64 < k <= 128: rows of [G | I] over NG = 8 row groups of two waves each,
+// four pivots per block (sl_wave_la.hpp wg_chol_invW)
+template <int K>
+__global__ void __launch_bounds__(1024) k_chol_inv_wide(const double* __restrict__ G, int k, int ldg,
+                                                        double* __restrict__ X, int* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) double fsh[2 * 4 * 128 + 136];
+  __shared__ int st;
+  if (threadIdx.x == 0) st = 0;
+  __syncthreads();
+  slw::wg_chol_invW<K, 8, 4>(G, ldg, X, k, k, fsh, &st);
+  __syncthreads();
+  if (threadIdx.x == 0 && status && st) atomicOr(status, st);
+}
 }  // namespace
 
 SL_API void sl_chol_inv_set_variant(int v) { g_chol_variant = v; }
 
 SL_API int sl_chol_inv_wave(const double* G, int k, int ldg, double* X, int* status, void* stream) {
-  if (k < 1 || k > 64 || ldg < k) { sl_set_last_error("chol_inv_wave: 1 <= k <= 64"); return SL_ERR_DIMENSION; }
+  if (k < 1 || k > 128 || ldg < k) { sl_set_last_error("chol_inv_wave: 1 <= k <= 128"); return SL_ERR_DIMENSION; }
   hipStream_t s = (hipStream_t)stream;
+  if (k > 64) {
+    if (k <= 96) k_chol_inv_wide<96><<<1, 1024, 0, s>>>(G, k, ldg, X, status);
+    else k_chol_inv_wide<128><<<1, 1024, 0, s>>>(G, k, ldg, X, status);
+    SL_LAUNCH_CHECK();
+    return SL_OK;
+  }
 #define SL_CIW(KK)                                                                                      \
   if (g_chol_variant == 5) k_chol_inv_wave<KK, 5><<<1, 512, 0, s>>>(G, k, ldg, X, status);               \
   else if (g_chol_variant == 4) k_chol_inv_wave<KK, 4><<<1, 256, 0, s>>>(G, k, ldg, X, status);          \

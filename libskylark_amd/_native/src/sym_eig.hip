@@ -144,8 +144,10 @@ k_sym_eig_jacobi(const double* __restrict__ Cin, int k, int ldc, int r, double* 
 // a vanishing r-th eigenvalue).  Output as k_sym_eig_jacobi:
 // out[i * r + c] = V[i][c] descending, then sqrt(max(lambda, 0)) (or lambda)
 // in out[k * r + c].
-// tridiagonalisation: 1 = four waves (wg_tridiag, default), 0 = one wave (A/B)
-int g_tri_host = 1;
+// tridiagonalisation: 1 = four waves (wg_tridiag), 0 = one wave, -1 = by size
+// (default: four waves only at k > 48, where they win -- 128 vs 146 us at
+// k = 64; one wave is 1-4 us faster below, profiles/r6/tridiag_four_wave_ab.jsonl)
+int g_tri_host = -1;
 template <int K>
 __global__ void __launch_bounds__(512) k_sym_eig_wave_impl(const double* __restrict__ C, int k, int ldc, int r,
                                                            double* __restrict__ out, int want_sqrt,
@@ -183,11 +185,12 @@ SL_API int sl_sym_eig_tridiag(const double* C, int k, int ldc, int r, double* ou
                               void* stream) {
   if (k <= 0 || k > 64 || r <= 0 || r > k || ldc < k) return SL_ERR_DIMENSION;
   hipStream_t s = (hipStream_t)stream;
-  if (k <= 16) k_sym_eig_wave_impl<16><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
-  else if (k <= 32) k_sym_eig_wave_impl<32><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
-  else if (k <= 40) k_sym_eig_wave_impl<40><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
-  else if (k <= 48) k_sym_eig_wave_impl<48><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
-  else k_sym_eig_wave_impl<64><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, g_tri_host);
+  const int tv = g_tri_host < 0 ? (k > 48) : g_tri_host;
+  if (k <= 16) k_sym_eig_wave_impl<16><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, tv);
+  else if (k <= 32) k_sym_eig_wave_impl<32><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, tv);
+  else if (k <= 40) k_sym_eig_wave_impl<40><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, tv);
+  else if (k <= 48) k_sym_eig_wave_impl<48><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, tv);
+  else k_sym_eig_wave_impl<64><<<1, 512, 0, s>>>(C, k, ldc, r, out, want_sqrt, status, tv);
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

@@ -555,7 +555,6 @@ int sl_slab_reduce_launch_d2d(const double* slab, int nslab, int64_t slab_stride
 int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
                           int cols, float* out, int ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return SL_OK;
-  if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
   const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
   k_slab_reduce_rows<float, float><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();
@@ -565,7 +564,6 @@ int sl_slab_reduce_launch(const float* slab, int nslab, int64_t slab_stride, int
 int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
                               int cols, double* out, int ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return SL_OK;
-  if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
   const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
   k_slab_reduce_rows<float, double><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();
@@ -575,7 +573,6 @@ int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride,
 int sl_slab_reduce_launch_d2d(const double* slab, int nslab, int64_t slab_stride, int ld_in, int rows,
                               int cols, double* out, int ld_out, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return SL_OK;
-  if (cols > 64) { sl_set_last_error("slab reduce: cols > 64"); return SL_ERR_UNSUPPORTED; }
   const unsigned grid = (unsigned)(((int64_t)rows * cols + 63) / 64);
   k_slab_reduce_rows<double, double><<<grid, 1024, 0, s>>>(slab, nslab, slab_stride, ld_in, cols, out, ld_out, rows);
   SL_LAUNCH_CHECK();

@@ -61,7 +61,7 @@ _lib.register("sl_chol_inv_wave", [vp, i32, i32, vp, vp, vp])
 
 
 def chol_inv_wave(G: torch.Tensor, status: torch.Tensor | None = None) -> torch.Tensor:
-    """R^{-1} (upper, f64) of G = R^T R (k <= 64) by the one-wave register
+    """R^{-1} (upper, f64) of G = R^T R (k <= 128) by the register
     kernel the randSVD boundaries use; dropped pivots (<= 1e-13 max G_ii) give
     zero rows / columns and set status bit 1."""
     k = G.shape[0]

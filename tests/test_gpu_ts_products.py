@@ -26,6 +26,7 @@ def L():
     _lib.register("sl_ts_gram64_workspace", [i64, i32], C.c_int64)
     _lib.register("sl_ts_gram64", [vp, i64, i32, i64, vp, i32, vp, vp])
     _lib.register("sl_ts_small", [i32, i32, i32, i32, i32, vp, i32, vp, i32, vp, i32, vp])
+    _lib.register("sl_ts_gram_w", [vp, i32, i64, i32, i64, vp, i32, vp, vp])
     return _lib
 
 
@@ -159,6 +160,25 @@ def test_xm64_gram64(L, rows, k, k2):
     ref = X.t() @ X
     assert torch.allclose(G, ref, rtol=1e-12, atol=1e-12 * ref.abs().max().item())
     assert torch.equal(G, G.t())
+
+
+@pytest.mark.parametrize("rows,k,ldx", [(200_001, 128, 128), (5000, 100, 104), (3, 65, 65), (777, 128, 130)])
+def test_gram_wide(L, rows, k, ldx):
+    """X^T X for 64 < k <= 128 (pair-split matrix-core Gram) vs fp64 torch,
+    f64 and f32 X, padded row stride; exactly symmetric."""
+    dev = torch.device("cuda")
+    Xp = torch.randn(rows, ldx, device=dev, dtype=torch.float64)
+    for code, dt in ((F64, torch.float64), (F32, torch.float32)):
+        Xs = Xp.to(dt)
+        X = Xs[:, :k]
+        ws = torch.zeros(int(L.require().sl_ts_gram64_workspace(rows, k)), dtype=torch.uint8, device=dev)
+        G = torch.empty(k, k, device=dev, dtype=torch.float64)
+        L.call("sl_ts_gram_w", vp(Xs.data_ptr()), code, rows, k, ldx, vp(G.data_ptr()), k, vp(ws.data_ptr()), _st())
+        torch.cuda.synchronize()
+        Xd = X.double()
+        ref = Xd.t() @ Xd
+        assert torch.allclose(G, ref, rtol=1e-12, atol=1e-12 * ref.abs().max().item())
+        assert torch.equal(G, G.t())
 
 
 def test_small(L):

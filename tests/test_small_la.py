@@ -1,4 +1,4 @@
-"""GPU-resident small linear algebra (k <= 64) vs fp64 torch references."""
+"""GPU-resident small linear algebra (k <= 64; the Cholesky inverse to k = 128) vs fp64 torch references."""
 import math
 import pytest
 import torch
@@ -21,7 +21,7 @@ def test_chol_inv(dev, k):
     torch.testing.assert_close(Ri32.cpu().double(), Ri.cpu(), rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("k", [1, 7, 16, 17, 33, 40, 41, 48, 64])
+@pytest.mark.parametrize("k", [1, 7, 16, 17, 33, 40, 41, 48, 64, 65, 96, 97, 120, 128])
 def test_chol_inv_wave(dev, k):
     """One-wave register Cholesky inverse (the randSVD boundary kernel) vs
     LAPACK: R^{-1} R = I to the attainable ~eps cond(G)."""
@@ -40,18 +40,18 @@ def test_chol_inv_wave(dev, k):
     torch.testing.assert_close(Ri, torch.linalg.inv(Rr), rtol=1e-8, atol=1e-8 * float(Ri.abs().max()))
 
 
-def test_chol_inv_wave_drops_dependent_direction(dev):
-    k = 12
+@pytest.mark.parametrize("k,dep", [(12, 5), (100, 77)])
+def test_chol_inv_wave_drops_dependent_direction(dev, k, dep):
     g = torch.Generator().manual_seed(3)
-    W = torch.randn(200, k, generator=g, dtype=torch.float64)
-    W[:, 5] = 2.0 * W[:, 2]
+    W = torch.randn(400, k, generator=g, dtype=torch.float64)
+    W[:, dep] = 2.0 * W[:, 2]
     G = W.t() @ W
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     Ri = SL.chol_inv_wave(G.to(dev), st).cpu()
     assert int(st) & 1
-    assert float(Ri[:, 5].abs().max()) == 0.0 and float(Ri[5, :].abs().max()) == 0.0
+    assert float(Ri[:, dep].abs().max()) == 0.0 and float(Ri[dep, :].abs().max()) == 0.0
     Q = W @ Ri
-    keep = [j for j in range(k) if j != 5]
+    keep = [j for j in range(k) if j != dep]
     torch.testing.assert_close(Q[:, keep].t() @ Q[:, keep], torch.eye(k - 1, dtype=torch.float64), atol=1e-8, rtol=0)
 
 
