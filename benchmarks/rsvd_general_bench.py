@@ -40,6 +40,7 @@ def planted(m, n, r, dtype, dev, seed=0):
     return A, s
 
 
+BIG = 1
 NO_REF = False   # --no-ref: skip the f64 reference (kernel traces of the engine alone)
 
 
@@ -86,7 +87,7 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     err = float(((s.double() - s_ref).abs() / s_ref).max())
     err_planted = float(((s.double() - s_true[:rank]).abs() / s_true[:rank]).max())
     k = max(rank, min(n, 2 * rank))
-    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}",
+    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}", "big": BIG,
            "engine": type(plan).__name__, "native": getattr(plan, "native", None), "ms": round(ms, 3), "ms_min": round(times[0], 3),
            "pass_traffic_GBps": round(bytes_passes / (ms * 1e-3) / 1e9, 1), "max_rel_err_s": err,
            "max_rel_err_s_vs_planted": err_planted}
@@ -111,9 +112,15 @@ def main():
     ap.add_argument("--cases", default="f32,f64,f64k128,bf16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--big", type=int, default=1, help="0: rocBLAS products past k = 64 (A/B)")
     a = ap.parse_args()
-    global NO_REF
+    import ctypes
+    from libskylark_amd.ops import _lib
+    _lib.require().sl_rsvd_gen_set_big.argtypes = [ctypes.c_int]
+    _lib.require().sl_rsvd_gen_set_big(a.big)
+    global NO_REF, BIG
     NO_REF = a.no_ref
+    BIG = a.big
     for c in a.cases.split(","):
         CASES[c](a.reps)
 

@@ -179,6 +179,10 @@ __global__ void k_status_merge(int* __restrict__ st) {
 
 int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
+// A/B knob (plans created after setting it): 1 = the hand-written products
+// over A for f32 / f64 at any k <= 128 (default), 0 = rocBLAS past k = 64
+int g_gen_big = 1;
+
 size_t esize(int dt) { return dt == SL_F64 ? 8 : dt == SL_F32 ? 4 : 2; }
 
 struct GPlan {
@@ -211,7 +215,11 @@ struct GPlan {
   // hand: f32 / f64 A with k <= 64 -- every product on the hand-written
   // kernels (rsvd_stream.hip, tsk_f32_kernels.hip), no rocBLAS / rocSOLVER
   bool hand = false;
-  void* atqw = nullptr;    // hand: A^T Q row-group slabs
+  // big: f32 / f64 A (k <= 128) -- the two products over A per pass on the
+  // hand-written kernels (sl_ts_az / sl_ts_atq; KT = 6 / 8 column tiles past
+  // k = 64), whatever runs the k x k algebra
+  bool big = false;
+  void* atqw = nullptr;    // big: A^T Q row-group slabs
   void* g64w = nullptr;    // hand: f64 Gram slabs
   // sketch of the call
   int sk = 0;              // 0 none, 1 FJLT, 2 dense
@@ -282,7 +290,7 @@ int gram(GPlan* p, const void* Yb, double* G, hipStream_t s) {
 // across ranks before the second half)
 int apply_z(GPlan* p, const void* A, hipStream_t s) {
   const int dt = p->dt == SL_BF16 ? SL_BF16 : p->dt;
-  int rc = p->hand ? sl_ts_az(A, p->m, p->n, p->lda, p->Z, p->k, p->Y, p->k, dt, s)
+  int rc = p->big ? sl_ts_az(A, p->m, p->n, p->lda, p->Z, p->k, p->Y, p->k, dt, s)
                    : slb_gemm(dt, false, false, p->m, p->k, p->n, 1.0, A, p->lda, p->Z, p->k, 0.0, p->Y, p->k, s);
   if (rc != SL_OK) return rc;
   return gram(p, p->Y, p->WG + p->n * p->k, s);
@@ -333,6 +341,10 @@ int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
     if (rc != SL_OK) return rc;
     k_cast2d<float, double><<<grid_of(n * k), 256, 0, s>>>((const float*)p->Wt, k, n, k, p->WG, k, nullptr);
     SL_LAUNCH_CHECK();
+  } else if (p->big) {
+    // 64 < k <= 128, f32 / f64 A: the hand-written A^T Q (row-group slabs summed in f64)
+    rc = sl_ts_atq(A, m, n, p->lda, p->Qb, k, p->WG, k, p->atqw, p->dt, s);
+    if (rc != SL_OK) return rc;
   } else {
     // W = A^T Q as np row-chunk products (one strided-batched launch fills the
     // chip; a single K = m product runs on a handful of workgroups), then one
@@ -507,6 +519,7 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   GPlan* p = new (std::nothrow) GPlan();
   if (!p) return SL_ERR_GENERIC;
   p->m = m; p->n = n; p->lda = lda; p->k = k; p->r = r; p->q = q; p->dt = dt; p->hand = hand;
+  p->big = dt != SL_BF16 && (hand || g_gen_big);
   const size_t es = esize(dt);
   const size_t ys = dt == SL_BF16 ? 4 : es;   // Y / Wt element size
   int64_t off = 0;
@@ -532,13 +545,13 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   // f32 / f64 A: row-chunk partials of A^T Y (and of Y^T Y), <= 64 MB of slabs
   int np = 0;
   int64_t ch = 0;
-  if (dt != SL_BF16 && !hand) {
+  if (dt != SL_BF16 && !p->big) {
     const int64_t slab = std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es;
     np = (int)std::max<int64_t>(1, std::min<int64_t>({128, (int64_t(64) << 20) / slab, m / 512}));
     ch = m / np;
   }
-  const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 && !hand ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
-  const int64_t o_aw = off;  off = align256(off + (hand ? sl_ts_atq_workspace(m, n, k, dt) : 0));
+  const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 && !p->big ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
+  const int64_t o_aw = off;  off = align256(off + (p->big ? sl_ts_atq_workspace(m, n, k, dt) : 0));
   const int64_t o_g6 = off;  off = align256(off + (hand || k > 64 ? sl_ts_gram64_workspace(std::max(m, n), k) : 0));
   const int64_t o_st = off;  off = align256(off + 64 * 4);
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
@@ -566,6 +579,8 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   *out = p;
   return SL_OK;
 }
+
+SL_API void sl_rsvd_gen_set_big(int v) { g_gen_big = v ? 1 : 0; }
 
 SL_API int sl_rsvd_gen_destroy(void* plan) {
   GPlan* p = (GPlan*)plan;

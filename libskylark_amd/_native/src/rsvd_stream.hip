@@ -109,7 +109,13 @@ __device__ __forceinline__ double ld_el(const double* p) {
 // is zeroed first by k_az_zero_cut; two addends onto zero sum the same in
 // either order, so the result stays deterministic: every tail range spans
 // at least one whole block, so no block has a third contributor).
-constexpr int AZ_NT = 256, AZ_RT = 2, AZ_VL = 2, AZ_NG = 4, AZ_PD = 2, AZ_BR = 4 * 16 * AZ_RT;
+constexpr int AZ_VL = 2, AZ_NG = 4, AZ_PD = 2, AZ_BR = 128;
+// KT <= 4: 256 threads, each wave two 16-row tiles (two workgroups per CU);
+// KT = 5..8 (64 < k <= 128): 512 threads, one row tile per wave (the
+// accumulators of eight column tiles, one workgroup per CU: the Z chunk
+// buffers take KT x 16 KB of LDS) -- the same 128-row blocks either way
+template <int KT> constexpr int az_nt() { return KT > 4 ? 512 : 256; }
+template <int KT> constexpr int az_rt() { return KT > 4 ? 1 : 2; }
 
 template <typename T, int KT>
 constexpr int az_lds() { return 2 * AZ_NG * KT * 64 * 16 * AZ_VL; }
@@ -119,12 +125,13 @@ constexpr int az_lds() { return 2 * AZ_NG * KT * 64 * 16 * AZ_VL; }
 __host__ __device__ inline int64_t az_rounds(int64_t nrb, int64_t g) { return nrb >= 2 * g ? nrb / g - 1 : 0; }
 
 template <typename T, int KT, bool VEC>
-__global__ void __launch_bounds__(AZ_NT, 2)
+__global__ void __launch_bounds__(az_nt<KT>(), KT > 4 ? 1 : 2)
 k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Z, int k, T* __restrict__ Y,
         int64_t ldy, int split) {
   using M = Mf<T>;
   using vec = typename M::vec;
   using acc_t = typename M::acc;
+  constexpr int AZ_NT = az_nt<KT>(), AZ_RT = az_rt<KT>(), RW = 16 * AZ_RT;   // RW rows per wave
   constexpr int VW = M::VW, EPL = AZ_VL * VW, GW = 4 * EPL, CW = AZ_NG * GW, KP = 16 * KT;
   constexpr int ZE = (CW * KP + AZ_NT - 1) / AZ_NT;   // Z elements per thread per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -206,7 +213,7 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   // the end re-reads the last one (never used)
   vec ring[AZ_PD][AZ_RT][AZ_VL];
   auto issue = [&](int64_t j, int c, int g, int slot) {
-    const int64_t r0 = j * AZ_BR + 32 * w;
+    const int64_t r0 = j * AZ_BR + RW * w;
     const int col0 = c * CW + g * GW + EPL * (lane >> 4);
 #pragma unroll
     for (int rt = 0; rt < AZ_RT; ++rt) {
@@ -290,7 +297,7 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
       // this workgroup's part of the row block is complete: y out (added
       // atomically into a block cut by a range boundary), accumulators cleared
       const bool cut = fc >= FR && (jb * nchunk < F0 || (jb + 1) * nchunk > F0 + FT);
-      const int64_t r0 = jb * AZ_BR + 32 * w;
+      const int64_t r0 = jb * AZ_BR + RW * w;
 #pragma unroll
       for (int rt = 0; rt < AZ_RT; ++rt)
 #pragma unroll
@@ -360,7 +367,7 @@ template <int KT, int AV>
 constexpr int at_pd() { return AV == 1 ? (KT >= 4 ? 4 : 6) : (KT >= 4 ? 4 : 8); }
 
 template <typename T, int KT, bool VEC, int AV>
-__global__ void __launch_bounds__(AT_NT, AV == 1 ? 2 : 1)
+__global__ void __launch_bounds__(AT_NT, AV == 1 && KT <= 4 ? 2 : 1)
 k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Q, int k, int64_t rows_per,
          T* __restrict__ slab) {
   using M = Mf<T>;
@@ -711,6 +718,33 @@ __global__ void __launch_bounds__(256) k_ts_gram64m(const double* __restrict__ X
 __host__ __device__ constexpr int gw_pa(int p) { int a = 0; while (p >= 8 - a) { p -= 8 - a; ++a; } return a; }
 __host__ __device__ constexpr int gw_pb(int p) { int a = 0; while (p >= 8 - a) { p -= 8 - a; ++a; } return a + p; }
 
+// the nine MFMAs of wave W on one 4-row step, pair indices folded at compile
+// time (constexpr locals: in an unrolled loop the pair functions were left as
+// run-time scalar loops with a dynamic register index before every MFMA)
+template <int W, int E>
+__device__ __forceinline__ void gw_mma(f64x4 (&acc)[9], const double (&xv)[8]) {
+  if constexpr (E < 9) {
+    constexpr int a = gw_pa(W + 4 * E), b = gw_pb(W + 4 * E);
+    acc[E] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[a], xv[b], acc[E], 0, 0, 0);
+    gw_mma<W, E + 1>(acc, xv);
+  }
+}
+template <int W, int E>
+__device__ __forceinline__ void gw_store(const f64x4 (&acc)[9], double* sb, int k, int lane, int r16) {
+  if constexpr (E < 9) {
+    constexpr int a = gw_pa(W + 4 * E), b = gw_pb(W + 4 * E);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * a + Mf<double>::drow(lane, r), j = 16 * b + r16;
+      if (i < k && j < k) {
+        sb[(int64_t)i * k + j] = acc[E][r];
+        if (a != b) sb[(int64_t)j * k + i] = acc[E][r];
+      }
+    }
+    gw_store<W, E + 1>(acc, sb, k, lane, r16);
+  }
+}
+
 template <typename T, int W>
 __device__ __forceinline__ void gram_w_body(const T* __restrict__ X, int64_t rows, int k, int64_t ldx,
                                             double* __restrict__ slab) {
@@ -721,38 +755,45 @@ __device__ __forceinline__ void gram_w_body(const T* __restrict__ X, int64_t row
   for (int e = 0; e < NP; ++e) acc[e] = f64x4{};
   const int64_t nq = (rows + 3) >> 2;
   const int64_t q0 = nq * blockIdx.x / gridDim.x, q1 = nq * (blockIdx.x + 1) / gridDim.x;
-  for (int64_t q = q0; q < q1; q += U) {
-    double xv[U][KT];
+  // software-pipelined: the next U steps' loads are in flight while this U's
+  // MFMAs run (a load-then-compute loop waited out the memory latency every
+  // iteration: 2.5 ms for a 1e6 x 128 f32 Gram)
+  // unconditional loads from clamped addresses, zeroed by a select after the
+  // load: a conditional load became an exec-masked branch with a vmcnt(0)
+  auto load = [&](int64_t q, double (&xv)[U][KT]) {
+    T raw[U][KT];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = 4 * (q + u) + kg;
+      const T* src = X + (row < rows ? row : rows - 1) * ldx;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int c = 16 * t + r16;
+        raw[u][t] = src[c < k ? c : k - 1];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = 4 * (q + u) + kg;
       const bool rok = q + u < q1 && row < rows;
-      const T* src = X + (rok ? row : 0) * ldx;
 #pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const int c = 16 * t + r16;
-        xv[u][t] = (rok && c < k) ? (double)src[c] : 0.0;
-      }
+      for (int t = 0; t < KT; ++t) xv[u][t] = (rok && 16 * t + r16 < k) ? (double)raw[u][t] : 0.0;
     }
+  };
+  auto mma = [&](const double (&xv)[U][KT]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int e = 0; e < NP; ++e)
-        acc[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[u][gw_pa(W + 4 * e)], xv[u][gw_pb(W + 4 * e)], acc[e], 0, 0, 0);
+    for (int u = 0; u < U; ++u) gw_mma<W, 0>(acc, xv[u]);
+  };
+  double xa[U][KT], xb[U][KT];
+  if (q0 < q1) load(q0, xa);
+  for (int64_t q = q0; q < q1; q += 2 * U) {
+    if (q + U < q1) load(q + U, xb);
+    mma(xa);
+    if (q + U >= q1) break;
+    if (q + 2 * U < q1) load(q + 2 * U, xa);
+    mma(xb);
   }
-  double* sb = slab + (int64_t)blockIdx.x * k * k;
-#pragma unroll
-  for (int e = 0; e < NP; ++e) {
-    const int a = gw_pa(W + 4 * e), b = gw_pb(W + 4 * e);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 16 * a + Mf<double>::drow(lane, r), j = 16 * b + r16;
-      if (i < k && j < k) {
-        sb[(int64_t)i * k + j] = acc[e][r];
-        if (a != b) sb[(int64_t)j * k + i] = acc[e][r];
-      }
-    }
-  }
+  gw_store<W, 0>(acc, slab + (int64_t)blockIdx.x * k * k, k, lane, r16);
 }
 
 template <typename T>
@@ -841,26 +882,31 @@ int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
   const int nchunk = (n + CW - 1) / CW;
   // g <= nrb: every stream-K range spans at least one whole row block
-  const int64_t g = nrb < 2 * (int64_t)ncu() ? nrb : 2 * (int64_t)ncu();
+  const int64_t res = (KT > 4 ? 1 : 2) * (int64_t)ncu();   // resident workgroups
+  const int64_t g = nrb < res ? nrb : res;
   if (g > 1 && g_az_split) {
     k_az_zero_cut<T><<<(unsigned)(g - 1), 256, 0, s>>>(Y, m, k, ldy, nrb, nchunk, (int)g);
     SL_LAUNCH_CHECK();
   }
   if (vec_ok(A, lda, n)) {
     SL_LDS_ATTR((k_ts_az<T, KT, true>), LDS);
-    k_ts_az<T, KT, true><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
+    k_ts_az<T, KT, true><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
   } else {
     SL_LDS_ATTR((k_ts_az<T, KT, false>), LDS);
-    k_ts_az<T, KT, false><<<(unsigned)g, AZ_NT, LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
+    k_ts_az<T, KT, false><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
   }
   SL_LAUNCH_CHECK();
   return SL_OK;
 }
 
+// vectors per wave and row: the knob for k <= 64; one (with one 512-thread
+// workgroup per CU, > 128 VGPRs of accumulators) for 64 < k <= 128
+int atq_av(int k) { return k > 64 ? 1 : g_atq_av; }
+
 // row groups of the A^T Q product: ~2 workgroups per CU over all slices
 template <typename T>
-void atq_geometry(int64_t m, int n, int* slices, int* groups, int64_t* rows_per) {
-  const int CS = 8 * g_atq_av * 16 * (16 / (int)sizeof(T));
+void atq_geometry(int64_t m, int n, int k, int* slices, int* groups, int64_t* rows_per) {
+  const int CS = 8 * atq_av(k) * 16 * (16 / (int)sizeof(T));
   *slices = (n + CS - 1) / CS;
   // AV = 2: one 512-thread workgroup per CU is resident (k_ts_atq needs >
   // 128 VGPRs): slices x groups <= 2 x CUs is two full rounds (rounding the
@@ -881,7 +927,10 @@ int launch_atq(const T* A, int64_t m, int n, int64_t lda, const T* Q, int k, T* 
                int64_t rp, hipStream_t s) {
   const dim3 grid((unsigned)slices, (unsigned)groups);
   const bool v = vec_ok(A, lda, n);
-  if (g_atq_av == 1) {
+  if constexpr (KT > 4) {
+    if (v) k_ts_atq<T, KT, true, 1><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+    else k_ts_atq<T, KT, false, 1><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
+  } else if (atq_av(k) == 1) {
     if (v) k_ts_atq<T, KT, true, 1><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
     else k_ts_atq<T, KT, false, 1><<<grid, AT_NT, 0, s>>>(A, m, n, lda, Q, k, rp, slab);
   } else {
@@ -898,7 +947,10 @@ int az_dispatch(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T*
     case 1: return launch_az<T, 1>(A, m, n, lda, Z, k, Y, ldy, s);
     case 2: return launch_az<T, 2>(A, m, n, lda, Z, k, Y, ldy, s);
     case 3: return launch_az<T, 3>(A, m, n, lda, Z, k, Y, ldy, s);
-    default: return launch_az<T, 4>(A, m, n, lda, Z, k, Y, ldy, s);
+    case 4: return launch_az<T, 4>(A, m, n, lda, Z, k, Y, ldy, s);
+    // 64 < k <= 128: six or eight column tiles (seven spilled f32 registers)
+    case 5: case 6: return launch_az<T, 6>(A, m, n, lda, Z, k, Y, ldy, s);
+    default: return launch_az<T, 8>(A, m, n, lda, Z, k, Y, ldy, s);
   }
 }
 
@@ -909,7 +961,9 @@ int atq_dispatch(const T* A, int64_t m, int n, int64_t lda, const T* Q, int k, T
     case 1: return launch_atq<T, 1>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
     case 2: return launch_atq<T, 2>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
     case 3: return launch_atq<T, 3>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
-    default: return launch_atq<T, 4>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+    case 4: return launch_atq<T, 4>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+    case 5: case 6: return launch_atq<T, 6>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
+    default: return launch_atq<T, 8>(A, m, n, lda, Q, k, slab, slices, groups, rp, s);
   }
 }
 
@@ -921,12 +975,12 @@ int gram_grid(int64_t rows) {
 
 }  // namespace
 
-// Y (m x k, row stride ldy) = A (m x n, lda) Z (n x k, row-major); dt SL_F32 / SL_F64, 1 <= k <= 64
+// Y (m x k, row stride ldy) = A (m x n, lda) Z (n x k, row-major); dt SL_F32 / SL_F64, 1 <= k <= 128
 SL_API int sl_ts_az(const void* A, int64_t m, int64_t n, int64_t lda, const void* Z, int k, void* Y, int64_t ldy,
                     int dt, void* stream) {
   if (m <= 0) return SL_OK;
-  if (k < 1 || k > 64 || n < 1 || n > (int64_t)1 << 30 || lda < n || ldy < k || (dt != SL_F32 && dt != SL_F64)) {
-    sl_set_last_error("ts_az: needs 1 <= k <= 64, lda >= n, ldy >= k, f32 / f64");
+  if (k < 1 || k > 128 || n < 1 || n > (int64_t)1 << 30 || lda < n || ldy < k || (dt != SL_F32 && dt != SL_F64)) {
+    sl_set_last_error("ts_az: needs 1 <= k <= 128, lda >= n, ldy >= k, f32 / f64");
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -945,16 +999,16 @@ SL_API void sl_ts_set_az_split(int v) { g_az_split = v ? 1 : 0; }
 SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt) {
   int slices = 0, groups = 0;
   int64_t rp = 0;
-  if (dt == SL_F64) atq_geometry<double>(m, (int)n, &slices, &groups, &rp);
-  else atq_geometry<float>(m, (int)n, &slices, &groups, &rp);
+  if (dt == SL_F64) atq_geometry<double>(m, (int)n, k, &slices, &groups, &rp);
+  else atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp);
   return (int64_t)groups * n * k * (dt == SL_F64 ? 8 : 4) + 256;
 }
 
 // W (n x k f64, row stride ldw) = A^T Q, A m x n (lda), Q m x k (row-major, A's dtype)
 SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const void* Q, int k, double* W, int ldw,
                      void* ws, int dt, void* stream) {
-  if (k < 1 || k > 64 || n < 1 || n > (int64_t)1 << 30 || lda < n || ldw < k || (dt != SL_F32 && dt != SL_F64)) {
-    sl_set_last_error("ts_atq: needs 1 <= k <= 64, lda >= n, ldw >= k, f32 / f64");
+  if (k < 1 || k > 128 || n < 1 || n > (int64_t)1 << 30 || lda < n || ldw < k || (dt != SL_F32 && dt != SL_F64)) {
+    sl_set_last_error("ts_atq: needs 1 <= k <= 128, lda >= n, ldw >= k, f32 / f64");
     return SL_ERR_UNSUPPORTED;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -963,12 +1017,12 @@ SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const voi
   int64_t rp = 0;
   int rc;
   if (dt == SL_F32) {
-    atq_geometry<float>(m, (int)n, &slices, &groups, &rp);
+    atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp);
     rc = atq_dispatch<float>((const float*)A, m, (int)n, lda, (const float*)Q, k, (float*)ws, slices, groups, rp, s);
     if (rc != SL_OK) return rc;
     return sl_slab_reduce_launch_f64((const float*)ws, groups, n * k, k, (int)n, k, W, ldw, s);
   }
-  atq_geometry<double>(m, (int)n, &slices, &groups, &rp);
+  atq_geometry<double>(m, (int)n, k, &slices, &groups, &rp);
   rc = atq_dispatch<double>((const double*)A, m, (int)n, lda, (const double*)Q, k, (double*)ws, slices, groups, rp, s);
   if (rc != SL_OK) return rc;
   return sl_slab_reduce_launch_d2d((const double*)ws, groups, n * k, k, (int)n, k, W, ldw, s);

@@ -36,7 +36,9 @@ def _st():
 
 # (300_007, 200, 24, 4): whole-block rounds then the stream-K tail of k_ts_az
 SHAPES = [(100_003, 1000, 40, 0), (4_097, 1000, 40, 8), (777, 37, 20, 0), (129, 16, 1, 0), (2_500, 530, 64, 3),
-          (20_000, 5000, 40, 0), (64, 2049, 33, 0), (300_007, 200, 24, 4)]
+          (20_000, 5000, 40, 0), (64, 2049, 33, 0), (300_007, 200, 24, 4),
+          # 64 < k <= 128: six / eight column tiles (512-thread az, one vector per wave in atq)
+          (50_001, 1000, 128, 0), (3_001, 530, 65, 3), (20_000, 5000, 96, 0), (7_777, 300, 111, 4)]
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
