@@ -151,6 +151,7 @@ def test_normal_form_lsqr_unpreconditioned_ill_conditioned(dev, cond):
     assert rf <= 1.01 * rc, (rf, rc, cf, cc)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("m,n,k,with_d", [(50000, 1024, 4, True), (50000, 1024, 4, False), (20000, 512, 2, True),
                                           (30000, 304, 1, True), (20003, 1000, 8, False), (4096, 16, 3, True)])
 def test_pass_mfma_matches_fp64(m, n, k, with_d):
