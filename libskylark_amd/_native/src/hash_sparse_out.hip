@@ -38,10 +38,36 @@ k_cwt_rw_sparse(const int64_t* __restrict__ rowptr, const IT* __restrict__ col, 
   for (int j = 0; j < L; ++j) {
     key[j] = 0xFFFFFFFFu;
     v[j] = (OT)0;
-    if (j < n) {
-      const int64_t c = (int64_t)col[p0 + j] + col_offset;
-      key[j] = (uint32_t)h[c];
-      v[j] = (OT)vals[p0 + j] * (OT)hval[c];
+  }
+  if (n > 0) {
+    // every load of the row issued unconditionally (entries past n re-read
+    // entry n - 1) and pinned by an empty asm, then masked: per-entry
+    // conditional loads compiled to exec-masked branches, each with its own
+    // vmcnt(0), so the dependent col -> h / hval gathers ran one at a time
+    int64_t cj[L];
+    VT vj[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int64_t q = p0 + (j < n ? j : n - 1);
+      cj[j] = (int64_t)col[q] + col_offset;
+      vj[j] = vals[q];
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) asm volatile("" : "+v"(cj[j]), "+v"(vj[j]));
+    int64_t hj[L];
+    double hv[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      hj[j] = h[cj[j]];
+      hv[j] = hval[cj[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      asm volatile("" : "+v"(hj[j]), "+v"(hv[j]));
+      if (j < n) {
+        key[j] = (uint32_t)hj[j];
+        v[j] = (OT)vj[j] * (OT)hv[j];
+      }
     }
   }
 #pragma unroll

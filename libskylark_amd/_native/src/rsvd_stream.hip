@@ -611,12 +611,23 @@ __global__ void __launch_bounds__(256) k_ts_xm64m(const double* __restrict__ X, 
       int64_t row = 16 * t + r16;
       row = row < rows ? row : rows - 1;   // clamped (never stored)
       const double* src = X + row * ldx;
+      // unconditional loads from clamped columns, pinned by an empty asm
+      // (else the compiler sinks each into an exec-masked branch with its
+      // own vmcnt(0)), zeroed after
 #pragma unroll
       for (int st = 0; st < KS; ++st) {
         const int c = 8 * st + 2 * kg;
-        xv[u][st] = (st < ks && c < k) ? *(const f64x2*)(src + c) : f64x2{0.0, 0.0};
+        xv[u][st] = *(const f64x2*)(src + (c < k ? c : 0));
       }
     }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int st = 0; st < KS; ++st) {
+        asm volatile("" : "+v"(xv[u][st]));
+        const int c = 8 * st + 2 * kg;
+        if (!(st < ks && c < k)) xv[u][st] = f64x2{0.0, 0.0};
+      }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t t = t0 + u * nw;
@@ -672,11 +683,21 @@ __global__ void __launch_bounds__(256) k_ts_gram64m(const double* __restrict__ X
     for (int u = 0; u < U; ++u) {
       const int64_t row = 4 * (q + u) + kg;
       const bool rok = q + u < q1 && row < rows;
-      const double* src = X + (rok ? row : 0) * ldx;
+      const double* src = X + (row < rows ? row : rows - 1) * ldx;
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         const int c = 16 * t + r16;
-        xv[u][t] = (rok && c < k) ? src[c] : 0.0;
+        xv[u][t] = src[c < k ? c : k - 1];   // unconditional, pinned below (see k_ts_xm64m)
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = 4 * (q + u) + kg;
+      const bool rok = q + u < q1 && row < rows;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        asm volatile("" : "+v"(xv[u][t]));
+        if (!(rok && 16 * t + r16 < k)) xv[u][t] = 0.0;
       }
     }
 #pragma unroll
