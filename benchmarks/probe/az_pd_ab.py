@@ -1,7 +1,9 @@
 """A/B of the Y = A Z product's prefetch depth (rsvd_stream.hip k_ts_az:
 2 A groups in flight per wave with two workgroups per CU, or 4 with one):
 f32 1e6 x 1000 and f64 2e5 x 5000 at k = 40, interleaved, plus the max
-relative difference of the two results."""
+relative difference of the two results.  (The PD = 4 variant and its
+sl_ts_set_az_pd knob were removed after this A/B found no difference:
+profiles/r6/az_prefetch_depth_ab.jsonl.)"""
 import ctypes as C
 import json
 import os
