@@ -133,7 +133,13 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   using acc_t = typename M::acc;
   constexpr int AZ_NT = az_nt<KT>(), AZ_RT = az_rt<KT>(), RW = 16 * AZ_RT;   // RW rows per wave
   constexpr int VW = M::VW, EPL = AZ_VL * VW, GW = 4 * EPL, CW = AZ_NG * GW, KP = 16 * KT;
-  constexpr int ZE = (CW * KP + AZ_NT - 1) / AZ_NT;   // Z elements per thread per chunk
+  // Z of a chunk is loaded as (column vector of VW, k index) pairs: VW
+  // coalesced scalar loads per pair, one 16-B LDS store (scalar stores at the
+  // fragment layout's 32-B stride were 8-way bank conflicts: 9e7 conflict
+  // cycles per f32 k = 40 launch, in front of the chunk barrier)
+  constexpr int CQ = CW / VW;                         // column vectors per chunk
+  constexpr int ZQ = (CQ * KP + AZ_NT - 1) / AZ_NT;   // pairs per thread per chunk
+  constexpr int ZE = ZQ * VW;                          // Z loads per thread per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* zl = (T*)smem;                                    // [2][NG][KT][64][EPL]
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -179,31 +185,38 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   constexpr int RWA = (AZ_PD - 1) * LPG + ZE < 63 ? (AZ_PD - 1) * LPG + ZE : 63;   // g < PD
   constexpr int RWB = (AZ_PD - 1) * LPG < 63 ? (AZ_PD - 1) * LPG : 63;             // g >= PD
   constexpr int ZW = AZ_NG * LPG < 63 ? AZ_NG * LPG : 63;   // loads after a Z chunk's at its LDS store
-  T zr[ZE];
+  T zr[ZQ][VW];
   auto zload = [&](int c) {
 #pragma unroll
-    for (int u = 0; u < ZE; ++u) {
-      const int e = tid + AZ_NT * u;
-      const int cc = e / KP, jj = e - cc * KP;
-      int col = c * CW + cc;
-      col = col < n ? col : n - 1;
-      zr[u] = ld_el(Z + (int64_t)col * k + (jj < k ? jj : k - 1));
+    for (int u = 0; u < ZQ; ++u) {
+      const int qd = tid + AZ_NT * u;
+      const int cq = qd / KP, jj = qd - cq * KP;
+#pragma unroll
+      for (int s = 0; s < VW; ++s) {
+        int col = c * CW + cq * VW + s;
+        col = col < n ? col : n - 1;
+        zr[u][s] = ld_el(Z + (int64_t)col * k + (jj < k ? jj : k - 1));
+      }
     }
   };
   auto zstore = [&](int buf, int c) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ZW) : "memory");
 #pragma unroll
-    for (int u = 0; u < ZE; ++u) asm volatile("" : "+v"(zr[u]));
+    for (int u = 0; u < ZQ; ++u)
+#pragma unroll
+      for (int s = 0; s < VW; ++s) asm volatile("" : "+v"(zr[u][s]));
     T* zb = zl + buf * (AZ_NG * KT * 64 * EPL);
 #pragma unroll
-    for (int u = 0; u < ZE; ++u) {
-      const int e = tid + AZ_NT * u;
-      if (e < CW * KP) {
-        const int cc = e / KP, jj = e - cc * KP;
-        const int q = cc / GW, wq = cc - q * GW, kk = wq / EPL, s = wq - kk * EPL;
+    for (int u = 0; u < ZQ; ++u) {
+      const int qd = tid + AZ_NT * u;
+      if (qd < CQ * KP) {
+        const int cq = qd / KP, jj = qd - cq * KP;
+        const int cc = cq * VW, q = cc / GW, wq = cc - q * GW, kk = wq / EPL, s0 = wq - kk * EPL;
         const int t = jj >> 4, j16 = jj & 15;
-        const bool ok = c * CW + cc < n && jj < k;
-        zb[((q * KT + t) * 64 + kk * 16 + j16) * EPL + s] = ok ? zr[u] : (T)0;
+        vec v;
+#pragma unroll
+        for (int s = 0; s < VW; ++s) v[s] = (c * CW + cc + s < n && jj < k) ? zr[u][s] : (T)0;
+        *(vec*)(zb + ((q * KT + t) * 64 + kk * 16 + j16) * EPL + s0) = v;
       }
     }
   };
