@@ -223,6 +223,7 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
   }
   const int rr = lane >> 4, cq = (lane & 15) * 4;     // read-back: row rr + 4 u, columns cq .. cq + 3
   const int gcol = col0 + wn * 64 + cq;
+  const bool c_al = ((uintptr_t)C & 15) == 0 && (ldc & 3) == 0;   // every f32 row 16-B aligned
 #pragma unroll
   for (int pss = 0; pss < 4; ++pss) {
 #pragma unroll
@@ -257,6 +258,21 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // accumulate (f32 out, 16-B aligned rows): this pass's eight C reads issued
+    // together from clamped addresses and pinned -- read inside the row /
+    // column branches they compiled to one load-and-wait at a time
+    f32x4 cpre[8];
+    if constexpr (ACC && sizeof(OutT) == 4) {
+      if (c_al) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int row = row0 + wm * 128 + pss * 32 + rr + 4 * u;
+          cpre[u] = *(const f32x4*)((const float*)C + (int64_t)(row < M ? row : M - 1) * ldc + (gcol + 3 < N ? gcol : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(cpre[u]));
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int lr = rr + 4 * u;
@@ -267,7 +283,10 @@ k_gemm_nt(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ 
         if (gcol + 3 < N && (((uintptr_t)p) & (4 * sizeof(OutT) - 1)) == 0) {
           if constexpr (sizeof(OutT) == 4) {
             float4 o = v;
-            if (ACC) { const float4 c = *(const float4*)p; o.x += c.x; o.y += c.y; o.z += c.z; o.w += c.w; }
+            if (ACC) {
+              const f32x4 c = c_al ? cpre[u] : *(const f32x4*)p;
+              o.x += c[0]; o.y += c[1]; o.z += c[2]; o.w += c[3];
+            }
             if (ntst) __builtin_nontemporal_store(f32x4{o.x, o.y, o.z, o.w}, (f32x4*)p);
             else *(float4*)p = o;
           } else {

@@ -159,16 +159,22 @@ def test_lsrn_gpu_preconditioner_paths(dev, cond, dt):
     assert res < 1e-4, (res, code)
 
 
-@pytest.mark.parametrize("dim", [0, 1])
+@pytest.mark.parametrize("dim,backend", [(0, "gemm_nt"), (0, "hipblaslt"), (1, None)])
 @pytest.mark.parametrize("block", [0, 1000, 1003])
-def test_dense_sketch_bf16x2_panels(dev, dim, block):
+@pytest.mark.parametrize("M", [333, 512])
+def test_dense_sketch_bf16x2_panels(dev, dim, backend, block, M, monkeypatch):
     """LSRN's internal sketch: bf16-realised S panels times the
-    bf16 hi/lo split of f32 A (sl_split_bf16) in reused buffers; equals
-    S_bf16 @ A to ~2^-16 for one or many panels (block 1003: ragged, the
-    16-B alignment fallback for column slices)."""
+    bf16 hi/lo split of f32 A in reused buffers; equals S_bf16 @ A to ~2^-16
+    for one or many panels (block 1003: ragged).  Columnwise: the NT form
+    (transposed split planes, C2 += P HL^T) on the hand-written NT GEMM's
+    accumulate path (M = 512: 16-B aligned C rows, the preloaded-C
+    epilogue; 333: the per-element path) or on hipBLASLt; rowwise: the NN
+    form (16-B alignment fallback for column slices)."""
     from libskylark_amd.ops import dense_sketch as DS
     from libskylark_amd.sketch import params
-    N, S, M = 4100, 96, 333
+    if backend is not None:
+        monkeypatch.setattr(DS, "LSRN_GEMM", backend)
+    N, S = 4100, 96
     T = sk.sketch.JLT(N, S, context=sk.Context(21))
     A = torch.randn(N, M, device=dev) if dim == 0 else torch.randn(M, N, device=dev)
     old = params.get_blocksize()
