@@ -11,6 +11,7 @@ run features_bf16 python benchmarks/bench_features.py --dtype bf16 || exit 1
 run csr_sketch python benchmarks/csr_sketch_bench.py || exit 1
 run fjlt python benchmarks/bench_fjlt.py || exit 1
 run admm python benchmarks/bench_admm.py || exit 1
+run admm_bf16 python benchmarks/bench_admm.py --cache-dtype bf16 --iters 10 || exit 1
 run krr python benchmarks/bench_krr.py || exit 1
 run krr_cg python benchmarks/krr_cg.py || exit 1
 run lsrn python benchmarks/bench_lsrn.py || exit 1
