@@ -23,11 +23,14 @@
 // ones on sl_ts_xm64 / sl_ts_gram64 / sl_ts_small / sl_tsk_f32_xm /
 // sl_tsk_gram64, the CholeskyQR factors and the core eigensolver on the
 // one-wave kernels of sl_wave_la.hpp (sl_chol_inv_wave, sl_sym_eig_tridiag;
-// Jacobi re-solve when flagged) -- no rocBLAS / rocSOLVER call.  bf16 A (n >
-// 1024) and 64 < k <= 128 keep library GEMMs (rocBLAS); the CholeskyQR
-// factors stay on the register kernels up to k = 128 (two waves per row), the
-// core of 64 < k <= 128 on rocSOLVER syevd.  W, H, G and the core are f64
-// whatever A's precision.
+// Jacobi re-solve when flagged) -- no rocBLAS / rocSOLVER call.  f32 / f64 A
+// with 64 < k <= 128 ("big" plans) run the same products on the same kernels
+// at six / eight column tiles (the m x k by k x k ones -- Q = Y R^{-1}, Z = W
+// R^{-1}, V = W N, U = Q M -- on sl_ts_az with the tall factor as its "A",
+// the Grams on sl_ts_gram_w, the k x k ones on sl_ts_small's tiled form, the
+// CholeskyQR factors on the two-waves-per-row register kernel); only their
+// core eigensolver stays on rocSOLVER syevd.  bf16 A (n > 1024) keeps library
+// GEMMs (rocBLAS).  W, H, G and the core are f64 whatever A's precision.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -323,12 +326,15 @@ int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
     if (!final_pass) return SL_OK;
     return gram(p, p->Qb, p->WG + n * k, s);
   }
+  // Q = Y Ry: big plans on the matrix-core stream kernel (Y as the m x k "A")
   if (p->dt == SL_F64) {
-    rc = slb_gemm(SL_F64, false, false, m, k, k, 1.0, p->Y, k, p->Ri, k, 0.0, p->Qb, k, s);
+    rc = p->big ? sl_ts_az(p->Y, m, k, k, p->Ri, k, p->Qb, k, SL_F64, s)
+                : slb_gemm(SL_F64, false, false, m, k, k, 1.0, p->Y, k, p->Ri, k, 0.0, p->Qb, k, s);
   } else {
     k_cast2d<double, float><<<grid_of((int64_t)k * k), 256, 0, s>>>(p->Ri, k, k, k, (float*)p->Rf, k, nullptr);
     SL_LAUNCH_CHECK();
-    rc = slb_gemm(SL_F32, false, false, m, k, k, 1.0, p->Y, k, p->Rf, k, 0.0, p->Qb, k, s);
+    rc = p->big ? sl_ts_az(p->Y, m, k, k, p->Rf, k, p->Qb, k, SL_F32, s)
+                : slb_gemm(SL_F32, false, false, m, k, k, 1.0, p->Y, k, p->Rf, k, 0.0, p->Qb, k, s);
   }
   if (rc != SL_OK) return rc;
   (void)i;
@@ -390,7 +396,9 @@ int inter(GPlan* p, int i, hipStream_t s) {
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
   if (rc != SL_OK) return rc;
-  rc = slb_gemm(SL_F64, false, false, n, k, k, 1.0, p->WG, k, p->Ri, k, 0.0, p->Zf, k, s);
+  if (p->big && p->dt == SL_F64) return sl_ts_az(p->WG, n, k, k, p->Ri, k, p->Z, k, SL_F64, s);   // Z = W R^{-1}
+  rc = p->big ? sl_ts_az(p->WG, n, k, k, p->Ri, k, p->Zf, k, SL_F64, s)
+              : slb_gemm(SL_F64, false, false, n, k, k, 1.0, p->WG, k, p->Ri, k, 0.0, p->Zf, k, s);
   if (rc != SL_OK) return rc;
   return dispatch_dt(p->dt, [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
@@ -431,10 +439,11 @@ int core(GPlan* p, hipStream_t s) {
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, G, p->Ri, p->st + 8, s);
   if (rc != SL_OK) return rc;
-  rc = p->hand ? sl_ts_small(0, 0, k, k, k, p->H, k, p->Ri, k, p->T1, k, s)
+  const bool own = p->hand || p->big;   // the k x k products on sl_ts_small
+  rc = own ? sl_ts_small(0, 0, k, k, k, p->H, k, p->Ri, k, p->T1, k, s)
                : slb_gemm(SL_F64, false, false, k, k, k, 1.0, p->H, k, p->Ri, k, 0.0, p->T1, k, s);   // T = H Rti
   if (rc != SL_OK) return rc;
-  rc = p->hand ? sl_ts_small(1, 0, k, k, k, p->Ri, k, p->T1, k, p->Cc, k, s)
+  rc = own ? sl_ts_small(1, 0, k, k, k, p->Ri, k, p->T1, k, p->Cc, k, s)
                : slb_gemm(SL_F64, true, false, k, k, k, 1.0, p->Ri, k, p->T1, k, 0.0, p->Cc, k, s);   // C = Rti^T T
   if (rc != SL_OK) return rc;
   if (k <= 64) {
@@ -453,7 +462,7 @@ int core(GPlan* p, hipStream_t s) {
     if (rc != SL_OK) return rc;
   }
   // M = Rti Ub_r (k x r), N = M S^{-1}, s
-  rc = p->hand ? sl_ts_small(0, 0, k, r, k, p->Ri, k, p->eig, r, p->M, r, s)
+  rc = own ? sl_ts_small(0, 0, k, r, k, p->Ri, k, p->eig, r, p->M, r, s)
                : slb_gemm(SL_F64, false, false, k, r, k, 1.0, p->Ri, k, p->eig, r, 0.0, p->M, r, s);
   if (rc != SL_OK) return rc;
   const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
@@ -663,7 +672,8 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
     if (udt == SL_F64) return sl_ts_xm64((const double*)p->Qb, p->m, k, k, p->M, r, U, ldu, SL_F64, s);   // U = Q M
     return sl_tsk_f32_xm((const float*)p->Qb, p->m, k, k, (const float*)p->Md, r, (float*)U, ldu, nullptr, nullptr, s);
   }
-  int rc = slb_gemm(SL_F64, false, false, p->n, r, k, 1.0, p->WG, k, p->N, r, 0.0, p->Vf, r, s);   // V = W N
+  int rc = p->big ? sl_ts_az(p->WG, p->n, k, k, p->N, r, p->Vf, r, SL_F64, s)
+                  : slb_gemm(SL_F64, false, false, p->n, r, k, 1.0, p->WG, k, p->N, r, 0.0, p->Vf, r, s);   // V = W N
   if (rc != SL_OK) return rc;
   rc = dispatch_dt(udt, [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
@@ -674,7 +684,8 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
     return SL_OK;
   });
   if (rc != SL_OK) return rc;
-  return slb_gemm(udt, false, false, p->m, r, k, 1.0, p->Qb, k, p->Md, r, 0.0, U, ldu, s);   // U = Q M
+  if (p->big) return sl_ts_az(p->Qb, p->m, k, k, p->Md, r, U, ldu, udt, s);   // U = Q M
+  return slb_gemm(udt, false, false, p->m, r, k, 1.0, p->Qb, k, p->Md, r, 0.0, U, ldu, s);
 }
 
 // single rank: every segment, then the finish

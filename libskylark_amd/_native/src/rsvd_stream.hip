@@ -848,7 +848,7 @@ __global__ void __launch_bounds__(256) k_ts_small(int ta, int tb, int mr, int nc
                                                   int lda, const double* __restrict__ B, int ldb,
                                                   double* __restrict__ C, int ldc) {
   __shared__ double as[64 * 65], bs[64 * 65];
-  if (mr <= 64 && nc <= 64 && kd <= 64) {
+  {
     // as[i][l] = op(A)[i][l], bs[j][l] = op(B)[l][j] (pitch 65: conflict-free rows)
     for (int e = threadIdx.x; e < mr * kd; e += 256) {
       if (ta) {   // A is kd x mr: as[i][l] = A[l][i]
@@ -875,17 +875,48 @@ __global__ void __launch_bounds__(256) k_ts_small(int ta, int tb, int mr, int nc
       for (int l = 0; l < kd; ++l) s = fma(as[i * 65 + l], bs[j * 65 + l], s);
       C[i * ldc + j] = s;
     }
-    return;
   }
-  for (int e = threadIdx.x; e < mr * nc; e += 256) {
-    const int i = e / nc, j = e - i * nc;
-    double s = 0.0;
-    for (int l = 0; l < kd; ++l) {
-      const double a = ta ? A[l * lda + i] : A[i * lda + l];
-      const double b = tb ? B[j * ldb + l] : B[l * ldb + j];
-      s = fma(a, b, s);
+}
+
+// the same product past 64 (the 64 < k <= 128 core): one 32 x 32 tile of C
+// per workgroup, kd in 32-wide chunks through LDS (coalesced along the
+// contiguous index of each operand), four outputs per thread
+__global__ void __launch_bounds__(256) k_ts_small_tiled(int ta, int tb, int mr, int nc, int kd,
+                                                        const double* __restrict__ A, int lda,
+                                                        const double* __restrict__ B, int ldb,
+                                                        double* __restrict__ C, int ldc) {
+  __shared__ double as[32][33], bs[32][33];   // as[i][l] = op(A)[i0 + i][l0 + l], bs[j][l] = op(B)[l0 + l][j0 + j]
+  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int l0 = 0; l0 < kd; l0 += 32) {
+    for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+      const int hi = e >> 5, lo = e & 31;
+      // op(A): ta -> A is kd x mr (contiguous along i), else mr x kd (along l)
+      const int ai = ta ? lo : hi, al = ta ? hi : lo;
+      const int gi = i0 + ai, gl = l0 + al;
+      as[ai][al] = (gi < mr && gl < kd) ? (ta ? A[(int64_t)gl * lda + gi] : A[(int64_t)gi * lda + gl]) : 0.0;
+      // op(B): tb -> B is nc x kd (contiguous along l), else kd x nc (along j)
+      const int bj = tb ? hi : lo, bl = tb ? lo : hi;
+      const int gj = j0 + bj, gm = l0 + bl;
+      bs[bj][bl] = (gj < nc && gm < kd) ? (tb ? B[(int64_t)gj * ldb + gm] : B[(int64_t)gm * ldb + gj]) : 0.0;
     }
-    C[i * ldc + j] = s;
+    __syncthreads();
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const double bv = bs[tx][l];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = fma(as[ty + 8 * u][l], bv, acc[u]);
+    }
+    __syncthreads();
+  }
+  const int j = j0 + tx;
+  if (j < nc) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + ty + 8 * u;
+      if (i < mr) C[(int64_t)i * ldc + j] = acc[u];
+    }
   }
 }
 
@@ -1135,7 +1166,16 @@ SL_API int sl_ts_gram_w(const void* X, int dt, int64_t rows, int k, int64_t ldx,
 // C (mr x nc, ldc) = op(A) op(B) (row-major f64; ta / tb: transpose), one workgroup
 SL_API int sl_ts_small(int ta, int tb, int mr, int nc, int kd, const double* A, int lda, const double* B, int ldb,
                        double* C, int ldc, void* stream) {
-  k_ts_small<<<1, 256, 0, (hipStream_t)stream>>>(ta, tb, mr, nc, kd, A, lda, B, ldb, C, ldc);
+  if (mr < 1 || nc < 1 || kd < 1) {
+    sl_set_last_error("ts_small: needs positive sizes");
+    return SL_ERR_DIMENSION;
+  }
+  if (mr <= 64 && nc <= 64 && kd <= 64) {
+    k_ts_small<<<1, 256, 0, (hipStream_t)stream>>>(ta, tb, mr, nc, kd, A, lda, B, ldb, C, ldc);
+  } else {
+    const dim3 grid((unsigned)((nc + 31) / 32), (unsigned)((mr + 31) / 32));
+    k_ts_small_tiled<<<grid, 256, 0, (hipStream_t)stream>>>(ta, tb, mr, nc, kd, A, lda, B, ldb, C, ldc);
+  }
   SL_LAUNCH_CHECK();
   return SL_OK;
 }

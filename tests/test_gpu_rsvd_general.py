@@ -2,8 +2,9 @@
 operands of any width, k up to 128, the whole call on the device -- against
 fp64 numpy SVDs of the same operand (reference nla/svd.hpp:222-318, double by
 default).  f32 / f64 with k <= 64 run only hand-written kernels (matrix-core
-products rsvd_stream.hip, one-wave small algebra); bf16 and k > 64 keep
-library GEMMs / rocSOLVER."""
+products rsvd_stream.hip, one-wave small algebra); 64 < k <= 128 the same
+products at six / eight column tiles with the core on rocSOLVER syevd; bf16
+with n > 1024 keeps library GEMMs."""
 import numpy as np
 import pytest
 import torch
@@ -56,13 +57,38 @@ def test_general_engine_vs_numpy(dtype, m, n, rank, q, sketch):
 
 
 def test_general_engine_k_above_64_uses_rocsolver():
-    """k = 2 r = 100 > 64: Cholesky inverse by potrf + trtri, core by syevd."""
+    """k = 2 r = 100 > 64: the products on the hand-written kernels at eight
+    column tiles, the Cholesky inverses on the two-waves-per-row register
+    kernel, the core by rocSOLVER syevd."""
     import libskylark_amd as sk
     A64 = _planted(5000, 800, 60, decay=0.95, noise=1e-9, seed=2)
     A = torch.from_numpy(A64).cuda()
     prm = sk.nla.ApproximateSVDParams(num_iterations=2, sketch="JLT", check=True)
     U, s, V = sk.nla.approximate_svd(A, 50, sk.Context(seed=1), prm)
     _check(A64, U, s, V, 50, 1e-8, 1e-10, 1e-6)
+
+
+def test_general_engine_f32_k_above_64_odd_width():
+    """f32, rank 55 -> k = 110 (seven column tiles padded to eight) on an odd
+    row width (n = 777: the scalar-load paths of the products), against fp64
+    numpy; the library-GEMM form of the same plan (sl_rsvd_gen_set_big(0))
+    agrees to f32 roundoff."""
+    import libskylark_amd as sk
+    from libskylark_amd.ops import _lib
+    A64 = _planted(7000, 777, 64, decay=0.93, noise=1e-7, seed=6)
+    A = torch.from_numpy(A64).to("cuda", torch.float32)
+    A64 = A.double().cpu().numpy()
+    prm = sk.nla.ApproximateSVDParams(num_iterations=1, sketch="JLT", check=True)
+    U, s, V = sk.nla.approximate_svd(A, 55, sk.Context(seed=12), prm)
+    _check(A64, U, s, V, 55, 1e-4, 1e-4, 1e-3)
+    lib = _lib.require()
+    lib.sl_rsvd_gen_set_big(0)
+    try:
+        A2 = A.clone()   # a fresh plan, created with the knob off
+        U2, s2, V2 = sk.nla.approximate_svd(A2, 55, sk.Context(seed=12), prm)
+    finally:
+        lib.sl_rsvd_gen_set_big(1)
+    np.testing.assert_allclose(s.cpu().numpy(), s2.cpu().numpy(), rtol=1e-5, atol=1e-5 * float(s[0]))
 
 
 def test_general_engine_matches_host_path_f64():

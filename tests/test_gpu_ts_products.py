@@ -194,3 +194,23 @@ def test_small(L):
         torch.cuda.synchronize()
         ref = (A.t() if ta else A) @ B
         assert torch.allclose(C_, ref, rtol=1e-13, atol=1e-12)
+
+
+@pytest.mark.parametrize("mr,nc,kd", [(128, 128, 128), (100, 77, 128), (65, 130, 33), (128, 40, 128)])
+def test_small_tiled(L, mr, nc, kd):
+    """op(A) op(B) past 64 (the 64 < k <= 128 core): the 32 x 32-tile form,
+    all four transpose combinations, padded leading dimensions."""
+    dev = torch.device("cuda")
+    for ta in (0, 1):
+        for tb in (0, 1):
+            Ab = torch.randn(*((kd, mr + 3) if ta else (mr, kd + 3)), device=dev, dtype=torch.float64)
+            Bb = torch.randn(*((nc, kd + 5) if tb else (kd, nc + 5)), device=dev, dtype=torch.float64)
+            A = Ab[:, :mr] if ta else Ab[:, :kd]
+            B = Bb[:, :kd] if tb else Bb[:, :nc]
+            C_ = torch.full((mr, nc + 2), 7.0, device=dev, dtype=torch.float64)
+            L.call("sl_ts_small", ta, tb, mr, nc, kd, vp(A.data_ptr()), Ab.stride(0), vp(B.data_ptr()), Bb.stride(0),
+                   vp(C_.data_ptr()), C_.stride(0), _st())
+            torch.cuda.synchronize()
+            ref = (A.t() if ta else A) @ (B.t() if tb else B)
+            assert torch.allclose(C_[:, :nc], ref, rtol=1e-13, atol=1e-12)
+            assert torch.all(C_[:, nc:] == 7.0)
