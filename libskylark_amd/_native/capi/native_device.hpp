@@ -82,6 +82,9 @@ struct Lib {
   int (*comm_unique_id)(void*) = nullptr;
   int (*comm_init)(const void*, int, int, void**) = nullptr;
   int (*comm_destroy)(void*) = nullptr;
+  int (*comm_all_reduce)(void*, const void*, void*, int64_t, int, int, void*) = nullptr;
+  int (*comm_rank_size)(void*, int*, int*) = nullptr;
+  int (*dev_memcpy2d)(void*, int64_t, const void*, int64_t, int64_t, int64_t, int, void*) = nullptr;
   int (*set_device)(int) = nullptr;
   int (*dev_count)(int*) = nullptr;
   int (*dct2_rows)(const int64_t*, int64_t, int64_t, const double*, double, void*, int, int64_t, int, void*) = nullptr;
@@ -166,6 +169,9 @@ inline Lib& lib() {
               bind(L.h, "sl_comm_unique_id_bytes", L.comm_id_bytes, L.err) &&
               bind(L.h, "sl_comm_unique_id", L.comm_unique_id, L.err) &&
               bind(L.h, "sl_comm_init", L.comm_init, L.err) && bind(L.h, "sl_comm_destroy", L.comm_destroy, L.err) &&
+              bind(L.h, "sl_comm_all_reduce", L.comm_all_reduce, L.err) &&
+              bind(L.h, "sl_comm_rank_size", L.comm_rank_size, L.err) &&
+              bind(L.h, "sl_dev_memcpy2d", L.dev_memcpy2d, L.err) &&
               bind(L.h, "sl_dev_set_device", L.set_device, L.err) && bind(L.h, "sl_dev_count", L.dev_count, L.err) &&
               bind(L.h, "sl_dct2_rows", L.dct2_rows, L.err) && bind(L.h, "sl_feature_epilogue", L.feature_epi, L.err) &&
               bind(L.h, "sl_transpose", L.transpose, L.err) && bind(L.h, "sl_csr_to_dense", L.csr_to_dense, L.err) &&
@@ -333,20 +339,25 @@ inline int hash_apply(const HashDev& H, int64_t N, int64_t S, const DevMat& A, c
 
 inline bool rowwise_fits(int64_t N, int dt) { return N * (int64_t)esize(dt) <= 160 * 1024; }
 
-inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim);
+inline int apply_linear(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim, int64_t off);
 
 // dim-1 application through dim 0 on the transposes (rows longer than LDS)
-inline int apply_by_transpose(const slnat::Sketch& s, const DevMat& A, const DevMat& SA) {
+inline int apply_by_transpose(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int64_t off) {
   Lib& L = lib();
   const int dt = A.dtype;
   const size_t es = esize(dt);
   Buf At(A.n * A.m * (int64_t)es), T(s.S * A.m * (int64_t)es);
   if (!At.p || !T.p) return fail(101, "device sketch: allocation failed");
   SLDEV_TRY(L.transpose(A.data, dt, A.m, A.n, A.ld, At.p, A.m, nullptr), "transpose");
-  const int rc = apply_sketch(s, DevMat{At.p, dt, A.n, A.m, A.m}, DevMat{T.p, dt, s.S, A.m, A.m}, 0);
+  const int rc = apply_linear(s, DevMat{At.p, dt, A.n, A.m, A.m}, DevMat{T.p, dt, s.S, A.m, A.m}, 0, off);
   if (rc) return rc;
   return check(L.transpose(T.p, dt, s.S, A.m, A.m, SA.data, SA.ld, nullptr), "transpose");
 }
+
+// sketch kinds whose operator mixes the whole sketched dimension non-linearly
+// or through a structured transform with no column-range form here: their
+// distributed application gathers the operand first
+inline bool needs_whole(const slnat::Sketch& s) { return s.kind == slnat::K_FASTFOOD || s.kind == slnat::K_PPT; }
 
 inline int epilogue_dev(const slnat::Sketch& s, const DevMat& SA, int dim) {
   if (s.epi == slnat::EPI_NONE) return 0;
@@ -358,42 +369,44 @@ inline int epilogue_dev(const slnat::Sketch& s, const DevMat& SA, int dim) {
                "feature epilogue");
 }
 
-// SA = S A (dim 0: A is N x n, SA is S x n) or A S^T (dim 1: A is m x N, SA
-// is m x S), row-major device operands of one dtype (f32 / f64): every
-// sketch type of native_sketch.hpp.
-inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim) {
+// The linear part of the sketch (no feature epilogue, no final sync) on the
+// operator's sketched-dimension range [off, off + cnt), cnt = A's extent along
+// dim: dim 0 SA (S x other) = S[:, off : off + cnt] A, dim 1 SA (other x S) =
+// A S[:, off : off + cnt]^T.  off = 0, cnt = N is the whole application; a
+// distributed operand's shard passes its global offset and the ranks' partial
+// results sum to the whole (needs_whole kinds take off = 0, cnt = N only).
+inline int apply_linear(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim, int64_t off) {
   Lib& L = lib();
-  if (!L.loaded) return fail(106, "device C API: " + L.err);
-  if ((A.dtype != F32 && A.dtype != F64) || SA.dtype != A.dtype)
-    return fail(103, "device sketch: A and SA must both be f32 or both f64");
-  const int64_t sk_in = dim == 0 ? A.m : A.n;   // the sketched dimension (N)
-  const int64_t other = dim == 0 ? A.n : A.m;
-  if (sk_in != s.N || (dim == 0 ? (SA.m != s.S || SA.n != other) : (SA.m != other || SA.n != s.S)))
-    return fail(104, "device sketch: dimension mismatch");
   const int dt = A.dtype;
   const size_t es = esize(dt);
+  const int64_t cnt = dim == 0 ? A.m : A.n;
+  const int64_t other = dim == 0 ? A.n : A.m;
   const int64_t N = s.N, S = s.S;
   void* st = nullptr;
-  if (other == 0) return 0;
   using namespace slnat;
-  if (dim == 1 && (s.kind == K_HASH || s.kind == K_SAMPLE || s.kind == K_PPT) && !rowwise_fits(N, dt))
-    return apply_by_transpose(s, A, SA);
-  // column k0.. of the operator against rows k0.. of A (dim 0) / columns (dim 1)
+  if (off < 0 || off + cnt > N || (needs_whole(s) && (off != 0 || cnt != N)))
+    return fail(104, "device sketch: operator column range");
+  if (other == 0) return 0;
+  if (cnt == 0) return zero(SA) ? 106 : 0;
+  if (dim == 1 && (s.kind == K_HASH || s.kind == K_SAMPLE || s.kind == K_PPT) && !rowwise_fits(cnt, dt))
+    return apply_by_transpose(s, A, SA, off);
+  // operator columns k0.. (global) against rows k0 - off.. of A (dim 0) / columns (dim 1)
   auto acc_panel = [&](const void* P, bool p_rowmajor_sxk, int64_t k0, int64_t kb, double beta) -> int {
     // P: S x kb row-major (ld kb) if p_rowmajor_sxk, else kb x S row-major (ld S)
+    const int64_t a0 = k0 - off;
     if (dim == 0)
       return gemm_rm(dt, !p_rowmajor_sxk, false, S, other, kb, P, p_rowmajor_sxk ? kb : S,
-                     (const char*)A.data + k0 * A.ld * es, A.ld, beta, SA.data, SA.ld);
-    return gemm_rm(dt, false, p_rowmajor_sxk, other, S, kb, (const char*)A.data + k0 * es, A.ld, P,
+                     (const char*)A.data + a0 * A.ld * es, A.ld, beta, SA.data, SA.ld);
+    return gemm_rm(dt, false, p_rowmajor_sxk, other, S, kb, (const char*)A.data + a0 * es, A.ld, P,
                    p_rowmajor_sxk ? kb : S, beta, SA.data, SA.ld);
   };
   if (s.kind == K_DENSE || s.kind == K_QMC) {
-    const int64_t b = std::max<int64_t>(1, std::min<int64_t>(N, (int64_t(1) << 24) / std::max<int64_t>(S, 1)));
+    const int64_t b = std::max<int64_t>(1, std::min<int64_t>(cnt, (int64_t(1) << 24) / std::max<int64_t>(S, 1)));
     Buf P(S * b * (int64_t)es);
     if (!P.p) return fail(101, "device sketch: allocation failed");
     std::vector<double> hp;
-    for (int64_t k0 = 0; k0 < N; k0 += b) {
-      const int64_t kb = std::min(b, N - k0);
+    for (int64_t k0 = off; k0 < off + cnt; k0 += b) {
+      const int64_t kb = std::min(b, off + cnt - k0);
       if (s.kind == K_DENSE) {
         SLDEV_TRY(L.fill_random(P.p, dt, s.dist, s.seed, s.wbase, S, kb, kb, 1, 0, k0, 1, S, s.p0, 0.0, s.scale,
                                 dt == F64 ? 1 : 0, st),
@@ -404,7 +417,7 @@ inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& S
         const int rc = upload_as(P, hp.data(), S * kb, dt);
         if (rc) return rc;
       }
-      const int rc = acc_panel(P.p, s.kind == K_DENSE, k0, kb, k0 == 0 ? 0.0 : 1.0);
+      const int rc = acc_panel(P.p, s.kind == K_DENSE, k0, kb, k0 == off ? 0.0 : 1.0);
       if (rc) return rc;
     }
   } else if (s.kind == K_FJLT) {
@@ -418,9 +431,11 @@ inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& S
       const int64_t nb = std::min(pb, S - j0);
       SLDEV_TRY(L.dct2_rows((const int64_t*)dsamp.p + j0, nb, N, (const double*)dD.p, s.scale, W.p, dt, N, 0, st),
                 "fjlt rows");
-      rc = dim == 0 ? gemm_rm(dt, false, false, nb, other, N, W.p, N, A.data, A.ld, 0.0,
+      // the operator's rows j0.. over all N columns; the shard's range is columns off..
+      const char* Wo = (const char*)W.p + off * (int64_t)es;
+      rc = dim == 0 ? gemm_rm(dt, false, false, nb, other, cnt, Wo, N, A.data, A.ld, 0.0,
                               (char*)SA.data + j0 * SA.ld * es, SA.ld)
-                    : gemm_rm(dt, false, true, other, nb, N, A.data, A.ld, W.p, N, 0.0, (char*)SA.data + j0 * es,
+                    : gemm_rm(dt, false, true, other, nb, cnt, A.data, A.ld, Wo, N, 0.0, (char*)SA.data + j0 * es,
                               SA.ld);
       if (rc) return rc;
     }
@@ -455,24 +470,34 @@ inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& S
     }
   } else if (s.kind == K_HASH || s.kind == K_SAMPLE) {
     if (s.kind == K_HASH) {
-      HashDev H(N, S);
-      const int rc = hash_upload(H, s.idx, s.val, S);
+      HashDev H(cnt, S);
+      const std::vector<int64_t> idx(s.idx.begin() + off, s.idx.begin() + off + cnt);
+      const std::vector<double> val(s.val.begin() + off, s.val.begin() + off + cnt);
+      const int rc = hash_upload(H, idx, val, S);
       if (rc) return rc;
-      if (hash_apply(H, N, S, A, SA, dim, 0)) return 106;
+      if (hash_apply(H, cnt, S, A, SA, dim, 0)) return 106;
     } else {
-      // output i = input samples[i]: the bucket structure of a gather
-      std::vector<int64_t> bptr((size_t)S + 1);
-      for (int64_t i = 0; i <= S; ++i) bptr[(size_t)i] = i;
-      std::vector<double> ones((size_t)std::max(N, S), 1.0);
-      Buf perm(S * 8), dbptr((S + 1) * 8), dones((int64_t)ones.size() * 8);
+      // output i = input samples[i]: the bucket structure of a gather (a
+      // shard's buckets hold the samples inside its range, the rest are empty)
+      std::vector<int64_t> bptr((size_t)S + 1, 0), perm;
+      for (int64_t i = 0; i < S; ++i) {
+        const int64_t j = s.samples[(size_t)i] - off;
+        const bool in = j >= 0 && j < cnt;
+        if (in) perm.push_back(j);
+        bptr[(size_t)i + 1] = bptr[(size_t)i] + (in ? 1 : 0);
+      }
+      if (perm.empty()) return zero(SA) ? 106 : 0;
+      std::vector<double> ones((size_t)std::max(cnt, S), 1.0);
+      Buf dperm((int64_t)perm.size() * 8), dbptr((S + 1) * 8), dones((int64_t)ones.size() * 8);
       int rc;
-      if ((rc = upload(perm, s.samples)) || (rc = upload(dbptr, bptr)) || (rc = upload(dones, ones))) return rc;
+      if ((rc = upload(dperm, perm)) || (rc = upload(dbptr, bptr)) || (rc = upload(dones, ones))) return rc;
+      const Buf& perm_ = dperm;
       if (dim == 0)
-        SLDEV_TRY(L.hash_colwise(A.data, dt, A.ld, A.n, (const int64_t*)perm.p, (const int64_t*)dbptr.p,
+        SLDEV_TRY(L.hash_colwise(A.data, dt, A.ld, A.n, (const int64_t*)perm_.p, (const int64_t*)dbptr.p,
                                  (const double*)dones.p, S, SA.data, dt, SA.ld, 0, 0, st),
                   "gather rows");
       else
-        SLDEV_TRY(L.hash_rowwise(A.data, dt, A.ld, A.m, N, (const int64_t*)perm.p, (const int64_t*)dbptr.p,
+        SLDEV_TRY(L.hash_rowwise(A.data, dt, A.ld, A.m, cnt, (const int64_t*)perm_.p, (const int64_t*)dbptr.p,
                                  (const double*)dones.p, S, SA.data, dt, SA.ld, 0, 0, st),
                   "gather columns");
     }
@@ -518,9 +543,175 @@ inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& S
       if ((rc = gemm_rm(dt, false, false, other, S, K, Pi, K, Sm.p, S, 1.0, SA.data, SA.ld, -1.0))) return rc;
     }
   }
-  const int rc = epilogue_dev(s, SA, dim);
+  return 0;
+}
+
+// SA = S A (dim 0: A is N x n, SA is S x n) or A S^T (dim 1: A is m x N, SA
+// is m x S), row-major device operands of one dtype (f32 / f64): every
+// sketch type of native_sketch.hpp.
+inline int apply_sketch(const slnat::Sketch& s, const DevMat& A, const DevMat& SA, int dim) {
+  Lib& L = lib();
+  if (!L.loaded) return fail(106, "device C API: " + L.err);
+  if ((A.dtype != F32 && A.dtype != F64) || SA.dtype != A.dtype)
+    return fail(103, "device sketch: A and SA must both be f32 or both f64");
+  const int64_t sk_in = dim == 0 ? A.m : A.n;   // the sketched dimension (N)
+  const int64_t other = dim == 0 ? A.n : A.m;
+  if (sk_in != s.N || (dim == 0 ? (SA.m != s.S || SA.n != other) : (SA.m != other || SA.n != s.S)))
+    return fail(104, "device sketch: dimension mismatch");
+  if (other == 0) return 0;
+  int rc = apply_linear(s, A, SA, dim, 0);
   if (rc) return rc;
-  return check(L.dev_sync(st), "sync");
+  if ((rc = epilogue_dev(s, SA, dim))) return rc;
+  return check(L.dev_sync(nullptr), "sync");
+}
+
+// ------------------------------------------ distributed (DistMatrix) operands
+// The reference's DistMatrix type names over a device communicator
+// (sl_device_comm_create, or a caller's all-reduce via sl_comm_from_allreduce;
+// null = one rank): each rank passes its shard of the global m x n matrix in
+// the runtime's layouts (parallel/distmatrix.py -- contiguous balanced blocks):
+//   LY_ROWS  DistMatrix_VC_STAR / _VR_STAR   rows [b, e) of block_of(m)
+//   LY_COLS  DistMatrix_STAR_VC / _STAR_VR   columns [b, e) of block_of(n)
+//   LY_STAR  SharedMatrix ([*,*])            the whole matrix on every rank
+//   LY_ROOT  RootMatrix ([CIRC,CIRC])        the whole matrix on rank 0
+// Only all-reduce is used (the one collective a caller's communicator has).
+enum { LY_STAR = 0, LY_ROWS = 1, LY_COLS = 2, LY_ROOT = 3 };
+
+struct DistMat {
+  void* data;        // this rank's shard, row-major (ld)
+  int dtype;
+  int64_t m, n, ld;  // GLOBAL shape; the shard's shape follows from the layout
+  void* comm;
+};
+
+inline void block_of(int64_t n, int p, int r, int64_t* b, int64_t* e) {
+  const int64_t q = n / p, rem = n % p;
+  *b = r * q + std::min<int64_t>(r, rem);
+  *e = *b + q + (r < rem ? 1 : 0);
+}
+
+inline int comm_rank_size(void* comm, int* rank, int* size) {
+  if (!comm) {
+    *rank = 0;
+    *size = 1;
+    return 0;
+  }
+  return check(lib().comm_rank_size(comm, rank, size), "communicator");
+}
+
+// shard offset (r0, c0) and shape of a global m x n matrix in layout ly
+inline void shard_of(int ly, int64_t m, int64_t n, int rank, int size, int64_t* r0, int64_t* c0, int64_t* lm,
+                     int64_t* ln) {
+  int64_t b = 0, e = 0;
+  *r0 = 0;
+  *c0 = 0;
+  *lm = m;
+  *ln = n;
+  if (ly == LY_ROWS) {
+    block_of(m, size, rank, &b, &e);
+    *r0 = b;
+    *lm = e - b;
+  } else if (ly == LY_COLS) {
+    block_of(n, size, rank, &b, &e);
+    *c0 = b;
+    *ln = e - b;
+  } else if (ly == LY_ROOT && rank != 0) {
+    *lm = 0;
+    *ln = 0;
+  }
+}
+
+// in-place sum over the ranks
+inline int all_reduce(void* comm, int size, void* buf, int64_t count, int dt) {
+  if (!comm || size == 1 || count == 0) return 0;
+  SLDEV_TRY(lib().dev_sync(nullptr), "sync");
+  SLDEV_TRY(lib().comm_all_reduce(comm, buf, buf, count, dt, 0, nullptr), "all-reduce");
+  return check(lib().dev_sync(nullptr), "sync");
+}
+
+// rows x cols block: src at (sr, sc) -> dst at (dr, dc)
+inline int copy_block(const DevMat& src, int64_t sr, int64_t sc, const DevMat& dst, int64_t dr, int64_t dc, int64_t rows,
+                      int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int64_t es = (int64_t)esize(src.dtype);
+  return check(lib().dev_memcpy2d((char*)dst.data + (dr * dst.ld + dc) * es, dst.ld * es,
+                                  (const char*)src.data + (sr * src.ld + sc) * es, src.ld * es, cols * es, rows, 2,
+                                  nullptr),
+               "copy");
+}
+
+// the global matrix on every rank: each shard embedded in zeros, summed
+inline int replicate(const DevMat& local, int64_t r0, int64_t c0, int64_t m, int64_t n, void* comm, int size, Buf& out,
+                     DevMat* whole) {
+  const int dt = local.dtype;
+  if (!out.p && m * n > 0) return fail(101, "device sketch: allocation failed");
+  *whole = DevMat{out.p, dt, m, n, n};
+  if (m * n == 0) return 0;
+  SLDEV_TRY(lib().dev_memset(out.p, 0, m * n * (int64_t)esize(dt), nullptr), "memset");
+  int rc = copy_block(local, 0, 0, *whole, r0, c0, local.m, local.n);
+  if (rc) return rc;
+  return all_reduce(comm, size, out.p, m * n, dt);
+}
+
+// SA = S A (dim 0) or A S^T (dim 1) with A and SA distributed (layouts in_ly /
+// out_ly).  The sketched dimension split over the ranks ([VC,*] columnwise,
+// [*,VC] rowwise): every rank applies its column range of the operator to its
+// shard and the partial sketches are summed (the random features' cosine
+// after the sum); the other dimension split: the shards sketch locally, no
+// communication; Fastfood / PPT gather the operand first.  Reference
+// sketch/*_Elemental.hpp (the [VC,*] / [*,VR] specialisations).
+inline int apply_sketch_dist(const slnat::Sketch& s, int in_ly, const DistMat& A, int out_ly, const DistMat& SA,
+                             int dim) {
+  Lib& L = lib();
+  if (!L.loaded) return fail(106, "device C API: " + L.err);
+  const int dt = A.dtype;
+  if ((dt != F32 && dt != F64) || SA.dtype != dt) return fail(103, "distributed sketch: A and SA f32 or f64 alike");
+  if (A.comm != SA.comm) return fail(109, "distributed sketch: A and SA on different communicators");
+  int rank = 0, size = 1;
+  int rc = comm_rank_size(A.comm, &rank, &size);
+  if (rc) return rc;
+  const int64_t om = dim == 0 ? s.S : A.m, on = dim == 0 ? A.n : s.S;
+  if ((dim == 0 ? A.m : A.n) != s.N || SA.m != om || SA.n != on)
+    return fail(104, "distributed sketch: dimension mismatch");
+  int64_t ar0, ac0, alm, aln, or0, oc0, olm, oln;
+  shard_of(in_ly, A.m, A.n, rank, size, &ar0, &ac0, &alm, &aln);
+  shard_of(out_ly, om, on, rank, size, &or0, &oc0, &olm, &oln);
+  const DevMat Al{A.data, dt, alm, aln, A.ld}, SAl{SA.data, dt, olm, oln, SA.ld};
+  const bool split_sk = (in_ly == LY_ROWS && dim == 0) || (in_ly == LY_COLS && dim == 1);
+  const bool split_other = (in_ly == LY_ROWS && dim == 1) || (in_ly == LY_COLS && dim == 0);
+  if (split_other && out_ly == in_ly) return apply_sketch(s, Al, SAl, dim);   // local rows / columns
+  // else: the whole result T (om x on) on every rank, then this rank's part of it
+  const size_t es = esize(dt);
+  Buf Tb(std::max<int64_t>(1, om * on) * (int64_t)es);
+  if (!Tb.p) return fail(101, "distributed sketch: allocation failed");
+  const DevMat T{Tb.p, dt, om, on, on};
+  if (split_sk && !needs_whole(s)) {
+    rc = apply_linear(s, Al, T, dim, dim == 0 ? ar0 : ac0);   // this shard's range of the operator
+    if (!rc) rc = all_reduce(A.comm, size, T.data, om * on, dt);
+    if (!rc) rc = epilogue_dev(s, T, dim);
+  } else if (split_other) {
+    // the local sketch rows / columns, gathered into T
+    int64_t tr0, tc0, tlm, tln;
+    shard_of(in_ly, om, on, rank, size, &tr0, &tc0, &tlm, &tln);
+    Buf Rb(std::max<int64_t>(1, tlm * tln) * (int64_t)es);
+    const DevMat R{Rb.p, dt, tlm, tln, tln};
+    rc = tlm * tln > 0 ? apply_sketch(s, Al, R, dim) : 0;
+    if (!rc) {
+      SLDEV_TRY(L.dev_memset(T.data, 0, om * on * (int64_t)es, nullptr), "memset");
+      rc = copy_block(R, 0, 0, T, tr0, tc0, tlm, tln);
+    }
+    if (!rc) rc = all_reduce(A.comm, size, T.data, om * on, dt);
+  } else {
+    // [*,*] / [CIRC,CIRC] inputs, or a kind that needs the whole operand
+    DevMat W = Al;
+    Buf Wb(in_ly == LY_STAR ? 0 : std::max<int64_t>(1, A.m * A.n) * (int64_t)es);
+    if (in_ly != LY_STAR) rc = replicate(Al, ar0, ac0, A.m, A.n, A.comm, size, Wb, &W);
+    if (!rc) rc = apply_sketch(s, W, T, dim);
+  }
+  if (rc) return rc;
+  rc = copy_block(T, or0, oc0, SAl, 0, 0, olm, oln);
+  if (rc) return rc;
+  return check(L.dev_sync(nullptr), "sync");
 }
 
 // CSR on the device (rowptr int64, col int32, val f64): rows x cols.

@@ -13,8 +13,15 @@
 //  - sl_kernel_gram on "Matrix" and "DeviceMatrix" operands (the Gram
 //    kernels of libskylark_hip.so, host matrices staged to the GPU);
 //  - sl_readlibsvm into "Matrix" / "SparseMatrix" (libsvm_io.cpp).
-// Everything else (DistMatrix-typed operands, runtime-only kernels, the
-// remaining entry points) goes through the Python/HIP runtime
+//  - DistMatrix-typed operands (device shards over a device communicator:
+//    DistMatrix_VC_STAR / _VR_STAR, DistMatrix_STAR_VC / _STAR_VR,
+//    SharedMatrix, RootMatrix; sl_wrap_raw_dist_device_matrix) in
+//    sl_apply_sketch_transform (every sketch type: the ranks' column ranges
+//    of the operator summed by all-reduce), sl_approximate_svd ([VC,*] A) and
+//    sl_kernel_gram (points split over the ranks) -- no interpreter.  The
+//    2-D [MC,MR] "DistMatrix" has no native path.
+// Everything else (runtime-only kernels, the remaining entry points) goes
+// through the Python/HIP runtime
 // (libskylark_amd + libskylark_hip.so); a natively created sketch or context
 // is handed to it lazily (via its JSON / seed + counter), so the two paths
 // see the same objects and the same random streams (sl_runtime_started()
@@ -65,6 +72,11 @@ struct sl_kernel_t {
 };
 struct sl_raw_device_matrix_t {
   sldev::DevMat d;
+};
+// a DistMatrix-typed operand: this rank's device shard of a global matrix
+// (the layout comes with the type string at each call, as in the reference)
+struct sl_raw_dist_device_matrix_t {
+  sldev::DistMat d;
 };
 struct sl_raw_matrix_t {
   double* data;
@@ -213,6 +225,44 @@ PyObject* py_sketch(sl_sketch_transform_t* S) {
 }
 
 bool is_device(const char* type) { return !strcmp(type, "DeviceMatrix"); }
+
+// layout of a DistMatrix type name (reference capi/matrix_types.cpp); -1: not
+// a distributed type; -2: the 2-D [MC,MR] "DistMatrix", which has no native
+// path (redistribute to [VC,*] / [*,VC] first)
+int dist_layout(const char* type) {
+  if (!strcmp(type, "DistMatrix_VC_STAR") || !strcmp(type, "DistMatrix_VR_STAR")) return sldev::LY_ROWS;
+  if (!strcmp(type, "DistMatrix_STAR_VC") || !strcmp(type, "DistMatrix_STAR_VR")) return sldev::LY_COLS;
+  if (!strcmp(type, "SharedMatrix")) return sldev::LY_STAR;
+  if (!strcmp(type, "RootMatrix")) return sldev::LY_ROOT;
+  if (!strcmp(type, "DistMatrix")) return -2;
+  return -1;
+}
+
+const sldev::DistMat& distmat(void* A) { return ((sl_raw_dist_device_matrix_t*)A)->d; }
+
+// shard of a distributed operand as a local DeviceMatrix view
+sldev::DevMat dist_local(int ly, const sldev::DistMat& d, int rank, int size) {
+  int64_t r0, c0, lm, ln;
+  sldev::shard_of(ly, d.m, d.n, rank, size, &r0, &c0, &lm, &ln);
+  return sldev::DevMat{d.data, d.dtype, lm, ln, d.ld};
+}
+
+// both types distributed (or both not); sets the layouts; error text on a mix
+int dist_pair(const char* fn, const char* a, const char* b, int* la, int* lb) {
+  *la = dist_layout(a);
+  *lb = dist_layout(b);
+  if (*la == -1 && *lb == -1) return 0;
+  if (*la == -2 || *lb == -2) {
+    g_last_error = std::string(fn) + ": 2-D [MC,MR] DistMatrix operands have no native path; use DistMatrix_VC_STAR / "
+                   "DistMatrix_STAR_VC (or the Python runtime's redistribute)";
+    return 103;
+  }
+  if (*la < 0 || *lb < 0) {
+    g_last_error = std::string(fn) + ": mix of distributed and local operand types";
+    return 109;
+  }
+  return 0;
+}
 
 sldev::DevMat& devmat(void* A) { return ((sl_raw_device_matrix_t*)A)->d; }
 
@@ -403,6 +453,59 @@ SL_CAPI int sl_wrap_raw_device_matrix(void* data, int dtype, int m, int n, int64
 SL_CAPI int sl_free_raw_device_matrix_wrap(void* A) {
   delete (sl_raw_device_matrix_t*)A;
   return 0;
+}
+
+// DistMatrix-typed operand: local = this rank's shard (device, row-major, ld)
+// of the global m x n matrix; comm = the device communicator the matrix lives
+// on (sl_device_comm_create, a caller's all-reduce through
+// sl_device_comm_from_allreduce, or null for one rank).  Pass the wrap with
+// the reference's type names: DistMatrix_VC_STAR / _VR_STAR (row blocks),
+// DistMatrix_STAR_VC / _STAR_VR (column blocks), SharedMatrix (replicated),
+// RootMatrix (rank 0); sl_dist_local_shape gives the shard's shape.
+SL_CAPI int sl_wrap_raw_dist_device_matrix(void* local, int dtype, int64_t m, int64_t n, int64_t ld, void* comm,
+                                           void** A) {
+  if (dtype < 0 || dtype > 2 || m < 0 || n < 0 || ld < 0) return 109;
+  *A = new sl_raw_dist_device_matrix_t{sldev::DistMat{local, dtype, m, n, ld, comm}};
+  return 0;
+}
+
+SL_CAPI int sl_free_raw_dist_device_matrix_wrap(void* A) {
+  delete (sl_raw_dist_device_matrix_t*)A;
+  return 0;
+}
+
+// this rank's shard (row / column offset and shape) of a global m x n matrix of the given type
+SL_CAPI int sl_dist_local_shape(char* type, int64_t m, int64_t n, void* comm, int64_t* r0, int64_t* c0, int64_t* lm,
+                                int64_t* ln) {
+  const int ly = dist_layout(type);
+  if (ly < 0) {
+    g_last_error = std::string("sl_dist_local_shape: not a native distributed type: ") + type;
+    return ly == -2 ? 103 : 109;
+  }
+  int rank = 0, size = 1;
+  if (comm) {
+    const int rc = sldev::comm_rank_size(comm, &rank, &size);
+    if (rc) return native_fail(rc);
+  }
+  sldev::shard_of(ly, m, n, rank, size, r0, c0, lm, ln);
+  return 0;
+}
+
+// a callback communicator (the caller's all-reduce, e.g. over MPI): the
+// distributed paths only all-reduce.  fn(send, recv, count, dtype, op, stream, user) -> 0
+SL_CAPI int sl_device_comm_from_allreduce(int rank, int size, void* fn, void* user, void** comm) {
+  sldev::Lib& L = sldev::lib();
+  if (!L.loaded) {
+    g_last_error = "device C API: " + L.err;
+    return 106;
+  }
+  using F = int (*)(int, int, void*, void*, void**);
+  static F f = (F)dlsym(L.h, "sl_comm_from_allreduce");
+  if (!f) {
+    g_last_error = "sl_comm_from_allreduce missing";
+    return 106;
+  }
+  return f(rank, size, fn, user, comm) ? (g_last_error = L.last_error(), 106) : 0;
 }
 
 // device memory helpers for C callers of the DeviceMatrix paths (kind: 0
@@ -691,6 +794,20 @@ SL_CAPI int sl_free_sketch_transform(sl_sketch_transform_t* S) {
 
 SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type, void* A, char* output_type,
                                       void* SA, int dim) {
+  int lin, lout;
+  if (const int e = dist_pair("sl_apply_sketch_transform", input_type, output_type, &lin, &lout)) return e;
+  if (lin >= 0) {
+    if (!S->nat) {
+      g_last_error = "sl_apply_sketch_transform: this sketch type has no device C path";
+      return 103;
+    }
+    if (dim != 0 && dim != 1) {
+      g_last_error = "sl_apply_sketch_transform: dim must be 0 (columnwise) or 1 (rowwise)";
+      return 109;
+    }
+    const int rc = sldev::apply_sketch_dist(*S->nat, lin, distmat(A), lout, distmat(SA), dim);
+    return rc ? native_fail(rc) : 0;
+  }
   if (is_device(input_type) || is_device(output_type)) {
     if (!is_device(input_type) || !is_device(output_type)) {
       g_last_error = "sl_apply_sketch_transform: DeviceMatrix input needs a DeviceMatrix output";
@@ -779,6 +896,34 @@ SL_CAPI int sl_apply_sketch_transform(sl_sketch_transform_t* S, char* input_type
 // --------------------------------------------------------------------- NLA
 SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, char* S_type, void* Sv, char* V_type,
                                void* V, uint16_t k, char* params, sl_context_t* ctxt) {
+  int la, lu;
+  if (const int e = dist_pair("sl_approximate_svd", A_type, U_type, &la, &lu)) return e;
+  if (la >= 0) {
+    // row-distributed A ([VC,*] / [VR,*]): U in A's rows, S and V replicated;
+    // the engine's pass sums all-reduced over A's communicator
+    if (la != sldev::LY_ROWS || lu != sldev::LY_ROWS || dist_layout(S_type) != sldev::LY_STAR ||
+        dist_layout(V_type) != sldev::LY_STAR) {
+      g_last_error = "sl_approximate_svd: distributed A must be DistMatrix_VC_STAR / _VR_STAR with U in the same "
+                     "layout and S, V SharedMatrix";
+      return 103;
+    }
+    const sldev::DistMat &a = distmat(A), &u = distmat(U), &sv = distmat(Sv), &v = distmat(V);
+    if (u.comm != a.comm || sv.comm != a.comm || v.comm != a.comm) {
+      g_last_error = "sl_approximate_svd: operands on different communicators";
+      return 109;
+    }
+    if (u.m != a.m) {
+      g_last_error = "sl_approximate_svd: U must have A's rows";
+      return 104;
+    }
+    int rank = 0, size = 1;
+    int rc = sldev::comm_rank_size(a.comm, &rank, &size);
+    if (rc) return native_fail(rc);
+    rc = sldev::approximate_svd(dist_local(la, a, rank, size), dist_local(lu, u, rank, size),
+                                dist_local(sldev::LY_STAR, sv, rank, size), dist_local(sldev::LY_STAR, v, rank, size),
+                                (int)k, params, ctxt->seed, ctxt->counter, a.comm);
+    return rc ? native_fail(rc) : 0;
+  }
   if (is_device(A_type)) {
     if (!is_device(U_type) || !is_device(S_type) || !is_device(V_type)) {
       g_last_error = "sl_approximate_svd: DeviceMatrix A needs DeviceMatrix U, S, V";
@@ -952,6 +1097,37 @@ SL_CAPI int sl_free_kernel(sl_kernel_t* k) {
 
 SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, void* X, char* Y_type, void* Y,
                            char* K_type, void* K) {
+  int lx, ly;
+  if (const int e = dist_pair("sl_kernel_gram", X_type, Y_type, &lx, &ly)) return e;
+  if (lx >= 0) {
+    // K's rows follow X's points and its columns Y's points: X's points (rows,
+    // dirX != SL_COLUMNS) split as [VC,*] give K's rows as [VC,*]; Y's points
+    // (columns, dirY == SL_COLUMNS) split as [*,VC] give K's columns as [*,VC];
+    // the other operand replicated.  Every rank forms its block, no communication.
+    const int lk = dist_layout(K_type);
+    const bool xr = dirX != 1, yc = dirY == 1;
+    int want = -1;
+    if (lx == sldev::LY_STAR && ly == sldev::LY_STAR) want = sldev::LY_STAR;
+    else if (lx == sldev::LY_ROWS && xr && ly == sldev::LY_STAR) want = sldev::LY_ROWS;
+    else if (lx == sldev::LY_STAR && ly == sldev::LY_COLS && yc) want = sldev::LY_COLS;
+    if (want < 0 || lk != want) {
+      g_last_error = "sl_kernel_gram: distributed operands: X's points as DistMatrix_VC_STAR rows (K the same), or Y's "
+                     "points as DistMatrix_STAR_VC columns (K the same), the other SharedMatrix";
+      return 103;
+    }
+    if (k->nat.type == sldev::K_NONE) {
+      g_last_error = "sl_kernel_gram: this kernel has no device C path";
+      return 103;
+    }
+    const sldev::DistMat &x = distmat(X), &y = distmat(Y), &kk = distmat(K);
+    int rank = 0, size = 1;
+    int rc = sldev::comm_rank_size(x.comm, &rank, &size);
+    if (rc) return native_fail(rc);
+    const sldev::DevMat kl = dist_local(lk, kk, rank, size);
+    if (kl.m == 0 || kl.n == 0) return 0;
+    rc = sldev::kernel_gram(k->nat, dirX, dirY, dist_local(lx, x, rank, size), dist_local(ly, y, rank, size), kl);
+    return rc ? native_fail(rc) : 0;
+  }
   if (is_device(X_type) || is_device(Y_type) || is_device(K_type)) {
     if (!is_device(X_type) || !is_device(Y_type) || !is_device(K_type)) {
       g_last_error = "sl_kernel_gram: mix of DeviceMatrix and host operands";

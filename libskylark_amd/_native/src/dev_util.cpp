@@ -27,6 +27,18 @@ SL_API int sl_dev_memcpy(void* dst, const void* src, int64_t bytes, int kind, vo
   return SL_OK;
 }
 
+// rows x width_bytes block between pitched buffers (pitches in bytes), same kinds
+SL_API int sl_dev_memcpy2d(void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width_bytes,
+                           int64_t rows, int kind, void* stream) {
+  if (rows <= 0 || width_bytes <= 0) return SL_OK;
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                        : hipMemcpyDeviceToDevice;
+  SL_HIP_CHECK(hipMemcpy2DAsync(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width_bytes, (size_t)rows, k,
+                                (hipStream_t)stream));
+  if (kind != 2) SL_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  return SL_OK;
+}
+
 SL_API int sl_dev_memset(void* dst, int value, int64_t bytes, void* stream) {
   if (bytes <= 0) return SL_OK;
   SL_HIP_CHECK(hipMemsetAsync(dst, value, (size_t)bytes, (hipStream_t)stream));

@@ -160,6 +160,14 @@ SL_API int sl_comm_from_allreduce(int rank, int size, SlAllReduceFn fn, void* us
   return SL_OK;
 }
 
+// this rank and the communicator size (null: one rank)
+SL_API int sl_comm_rank_size(void* comm, int* rank, int* size) {
+  SlComm* c = as_comm(comm);
+  *rank = c ? c->rank : 0;
+  *size = c ? c->size : 1;
+  return SL_OK;
+}
+
 SL_API int sl_comm_destroy(void* comm) {
   SlComm* c = as_comm(comm);
   if (!c) return SL_OK;

@@ -920,3 +920,59 @@ def test_host_operands_on_device_interpreter_free(capi, tmp_path):
                                rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(ld("kp", (9, 9)), kp.gram(Bp, dirX="rows", dirY="rows", Y=Bp).numpy(),
                                rtol=1e-9, atol=1e-12)
+
+
+def test_dist_matrix_types_shapes_and_errors(capi):
+    """DistMatrix-typed operands in the C ABI (host-side checks, no device
+    work): the shard geometry of every native layout matches the runtime's
+    DistMatrix (parallel/distmatrix.py balanced blocks) on a 3-rank callback
+    communicator; the 2-D [MC,MR] type is refused (103) and a mix of
+    distributed and local types is an error (109) before any device call."""
+    from libskylark_amd.parallel.distmatrix import DistMatrix
+    from libskylark_amd.parallel.comm import Comm
+    i64, vp = C.c_int64, C.c_void_p
+    capi.sl_dist_local_shape.argtypes = [C.c_char_p, i64, i64, vp] + [C.POINTER(i64)] * 4
+
+    def shape(typ, m, n, comm):
+        v = [i64() for _ in range(4)]
+        rc = capi.sl_dist_local_shape(typ, m, n, comm, *[C.byref(x) for x in v])
+        return rc, [x.value for x in v]
+
+    assert shape(b"DistMatrix_VC_STAR", 10, 4, None) == (0, [0, 0, 10, 4])
+    assert shape(b"DistMatrix", 10, 4, None)[0] == 103
+    assert shape(b"Matrix", 10, 4, None)[0] == 109
+
+    @C.CFUNCTYPE(C.c_int, vp, vp, i64, C.c_int, C.c_int, vp, vp)
+    def never(send, recv, count, dtype, op, stream, user):
+        return 1
+
+    class _FakeComm:   # the runtime's geometry for rank r of 3
+        def __init__(self, r):
+            self.rank, self.size = r, 3
+
+    capi.sl_device_comm_from_allreduce.argtypes = [C.c_int, C.c_int, vp, vp, C.POINTER(vp)]
+    for r in range(3):
+        comm = vp()
+        rc = capi.sl_device_comm_from_allreduce(r, 3, C.cast(never, vp), None, C.byref(comm))
+        if rc == 106:
+            pytest.skip("native HIP library not loadable here")
+        assert rc == 0
+        for typ, layout in ((b"DistMatrix_VC_STAR", "VC_STAR"), (b"DistMatrix_VR_STAR", "VR_STAR"),
+                            (b"DistMatrix_STAR_VC", "STAR_VC"), (b"DistMatrix_STAR_VR", "STAR_VR"),
+                            (b"SharedMatrix", "STAR_STAR"), (b"RootMatrix", "CIRC_CIRC")):
+            d = DistMatrix(torch.empty(0), (10, 7), layout, comm=_FakeComm(r))
+            rb, cb = d.row_blocks(), d.col_blocks()
+            want = [rb[0][0] if rb else 0, cb[0][0] if cb else 0, *d.local_shape()]
+            rc, got = shape(typ, 10, 7, comm)
+            assert rc == 0 and got == want, (typ, r, got, want)
+    # type checks come before any device work
+    ctx, h, a = vp(), vp(), vp()
+    assert capi.sl_create_default_context(3, C.byref(ctx)) == 0
+    assert capi.sl_create_sketch_transform(ctx, b"JLT", 10, 4, C.byref(h)) == 0
+    capi.sl_wrap_raw_dist_device_matrix.argtypes = [vp, C.c_int, i64, i64, i64, vp, C.POINTER(vp)]
+    assert capi.sl_wrap_raw_dist_device_matrix(None, 1, 10, 3, 3, None, C.byref(a)) == 0
+    assert capi.sl_apply_sketch_transform(h, b"DistMatrix", a, b"SharedMatrix", a, 0) == 103
+    assert capi.sl_apply_sketch_transform(h, b"DistMatrix_VC_STAR", a, b"Matrix", a, 0) == 109
+    capi.sl_free_raw_dist_device_matrix_wrap(a)
+    capi.sl_free_sketch_transform(h)
+    capi.sl_free_context(ctx)
