@@ -41,6 +41,7 @@ def planted(m, n, r, dtype, dev, seed=0):
 
 
 BIG = 1
+SPLIT = 1
 NO_REF = False   # --no-ref: skip the f64 reference (kernel traces of the engine alone)
 
 
@@ -87,7 +88,7 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     err = float(((s.double() - s_ref).abs() / s_ref).max())
     err_planted = float(((s.double() - s_true[:rank]).abs() / s_true[:rank]).max())
     k = max(rank, min(n, 2 * rank))
-    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}", "big": BIG,
+    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}", "big": BIG, "bf16_split": SPLIT,
            "engine": type(plan).__name__, "native": getattr(plan, "native", None), "ms": round(ms, 3), "ms_min": round(times[0], 3),
            "pass_traffic_GBps": round(bytes_passes / (ms * 1e-3) / 1e9, 1), "max_rel_err_s": err,
            "max_rel_err_s_vs_planted": err_planted}
@@ -103,6 +104,7 @@ CASES = {
     "f64k128": lambda reps: run(200_000, 5000, 64, 1, torch.float64, reps=reps),   # k = 128
     "f32k128": lambda reps: run(1_000_000, 1000, 64, 1, torch.float32, reps=reps),
     "bf16": lambda reps: run(1_000_000, 1000, 20, 2, torch.bfloat16, reps=reps),  # the fused engine, for comparison
+    "bf16w": lambda reps: run(500_000, 4000, 20, 2, torch.bfloat16, reps=reps),   # n > 1024: the general engine
 }
 
 
@@ -113,14 +115,18 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--big", type=int, default=1, help="0: rocBLAS products past k = 64 (A/B)")
+    ap.add_argument("--bf16-split", type=int, default=1, help="0: bf16 A^T [Q_hi Q_lo] as one product (A/B)")
     a = ap.parse_args()
     import ctypes
     from libskylark_amd.ops import _lib
     _lib.require().sl_rsvd_gen_set_big.argtypes = [ctypes.c_int]
     _lib.require().sl_rsvd_gen_set_big(a.big)
-    global NO_REF, BIG
+    _lib.require().sl_rsvd_gen_set_bf16_split.argtypes = [ctypes.c_int]
+    _lib.require().sl_rsvd_gen_set_bf16_split(a.bf16_split)
+    global NO_REF, BIG, SPLIT
     NO_REF = a.no_ref
     BIG = a.big
+    SPLIT = a.bf16_split
     for c in a.cases.split(","):
         CASES[c](a.reps)
 

@@ -29,8 +29,11 @@
 // R^{-1}, V = W N, U = Q M -- on sl_ts_az with the tall factor as its "A",
 // the Grams on sl_ts_gram_w, the k x k ones on sl_ts_small's tiled form, the
 // CholeskyQR factors on the two-waves-per-row register kernel); only their
-// core eigensolver stays on rocSOLVER syevd.  bf16 A (n > 1024) keeps library
-// GEMMs (rocBLAS).  W, H, G and the core are f64 whatever A's precision.
+// core eigensolver stays on rocSOLVER syevd.  bf16 A (n > 1024) keeps its two
+// products over A on rocBLAS bf16 GEMMs (Y = A Z, and W = A^T [Q_hi Q_lo] as
+// ONE product over the side-by-side split planes, so each pass reads A twice,
+// not three times); every other product of its call is on the hand-written
+// kernels above.  W, H, G and the core are f64 whatever A's precision.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -113,16 +116,19 @@ __global__ void __launch_bounds__(256) k_fjlt_z(uint64_t seed, uint64_t baseD, u
   st_d<T>(Z + t, cos(w * (double)a) * (p == 0 ? c0 : c1) * scale * d);
 }
 
-// bf16 hi / lo planes of an f32 matrix: hi = bf16(y), lo = bf16(y - hi), and
-// y <- hi + lo (exact in f32): the rows the bf16 products actually see
-__global__ void __launch_bounds__(256) k_split_bf16(float* __restrict__ y, int64_t tot, bf16_t* __restrict__ hi,
-                                                   bf16_t* __restrict__ lo) {
+// bf16 hi / lo planes of an f32 m x k matrix side by side in hl (m x 2k):
+// hi = bf16(y) in columns [0, k), lo = bf16(y - hi) in [k, 2k), and y <- hi +
+// lo (exact in f32): the rows the bf16 products actually see
+__global__ void __launch_bounds__(256) k_split_bf16(float* __restrict__ y, int64_t m, int k, bf16_t* __restrict__ hl) {
+  const int64_t tot = m * k;
   for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < tot; t += (int64_t)gridDim.x * 256) {
+    const int64_t i = t / k;
+    const int j = (int)(t - i * k);
     const float v = y[t];
     const bf16_t h = f_to_bf16(v);
     const bf16_t l = f_to_bf16(v - bf16_to_f(h));
-    hi[t] = h;
-    lo[t] = l;
+    hl[i * 2 * k + j] = h;
+    hl[i * 2 * k + k + j] = l;
     y[t] = bf16_to_f(h) + bf16_to_f(l);
   }
 }
@@ -186,6 +192,10 @@ int64_t align256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 // over A for f32 / f64 at any k <= 128 (default), 0 = rocBLAS past k = 64
 int g_gen_big = 1;
 
+// A/B knob (plans created after setting it): bf16 A's A^T [Q_hi Q_lo] as a
+// strided batch of row-chunk products (split K; 1, default) or one product (0)
+int g_bf16_split = 1;
+
 size_t esize(int dt) { return dt == SL_F64 ? 8 : dt == SL_F32 ? 4 : 2; }
 
 struct GPlan {
@@ -194,9 +204,8 @@ struct GPlan {
   char* base = nullptr;
   void* Z = nullptr;       // n x k (dt)
   void* Y = nullptr;       // m x k (dt; f32 when A is bf16)
-  void* Yh = nullptr;      // bf16 A: hi / lo planes of Y (m x k bf16 each)
-  void* Yl = nullptr;
-  void* Wt = nullptr;      // n x k pass output (dt; f32 when A is bf16)
+  void* Yh = nullptr;      // bf16 A: hi / lo planes of Q side by side (m x 2k bf16)
+  void* Wt = nullptr;      // bf16 A: n x 2k f32 pass output (A^T [Q_hi Q_lo])
   void* Qb = nullptr;      // m x k orthonormalised Y (dt; f32 when A is bf16): the basis U is formed from
   void* Rf = nullptr;      // k x k f32 copy of R^{-1} (f32 / bf16 A)
   double* WG = nullptr;    // [W (n x k); G (k x k)] f64
@@ -223,7 +232,7 @@ struct GPlan {
   // k = 64), whatever runs the k x k algebra
   bool big = false;
   void* atqw = nullptr;    // big: A^T Q row-group slabs
-  void* g64w = nullptr;    // hand: f64 Gram slabs
+  void* g64w = nullptr;    // f64 Gram slabs (W^T W; Y^T Y of f64 A)
   // sketch of the call
   int sk = 0;              // 0 none, 1 FJLT, 2 dense
   uint64_t seed = 0, b0 = 0, b1 = 0;
@@ -299,62 +308,94 @@ int apply_z(GPlan* p, const void* A, hipStream_t s) {
   return gram(p, p->Y, p->WG + p->n * p->k, s);
 }
 
+// Qb = Y Ry (Ry = R^{-1} in p->Ri): the hand-written tall-skinny kernels --
+// k <= 64 sl_ts_xm64 (f64) / sl_tsk_f32_xm (f32 Y: f32 and bf16 A), past 64
+// sl_ts_az with Y as its operand (big plans and bf16 A); rocBLAS only for the
+// k > 64 library A/B (g_gen_big = 0)
+int q_from_y(GPlan* p, hipStream_t s) {
+  const int64_t m = p->m;
+  const int k = p->k;
+  if (p->dt == SL_F64) {
+    if (k <= 64) return sl_ts_xm64((const double*)p->Y, m, k, k, p->Ri, k, p->Qb, k, SL_F64, s);
+    if (p->big) return sl_ts_az(p->Y, m, k, k, p->Ri, k, p->Qb, k, SL_F64, s);
+    return slb_gemm(SL_F64, false, false, m, k, k, 1.0, p->Y, k, p->Ri, k, 0.0, p->Qb, k, s);
+  }
+  k_cast2d<double, float><<<grid_of((int64_t)k * k), 256, 0, s>>>(p->Ri, k, k, k, (float*)p->Rf, k, nullptr);
+  SL_LAUNCH_CHECK();
+  if (k <= 64)
+    return sl_tsk_f32_xm((const float*)p->Y, m, k, k, (const float*)p->Rf, k, (float*)p->Qb, k, nullptr, nullptr, s);
+  if (p->big || p->dt == SL_BF16) return sl_ts_az(p->Y, m, k, k, p->Rf, k, p->Qb, k, SL_F32, s);
+  return slb_gemm(SL_F32, false, false, m, k, k, 1.0, p->Y, k, p->Rf, k, 0.0, p->Qb, k, s);
+}
+
+// WG[i][j] (f64, n x k) = sum over the np slabs of Wt[i][j] + Wt[i][k + j]
+// (f32, n x 2k each): the bf16 pass's A^T Q_hi and A^T Q_lo halves (per row
+// chunk), summed in f64
+__global__ void __launch_bounds__(256) k_sum_halves(const float* __restrict__ Wt, int np, int64_t n, int k,
+                                                   double* __restrict__ WG) {
+  const int64_t tot = n * k;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < tot; t += (int64_t)gridDim.x * 256) {
+    const int64_t i = t / k;
+    const int j = (int)(t - i * k);
+    double acc = 0.0;
+    for (int q = 0; q < np; ++q) {
+      const float* w = Wt + (int64_t)q * n * 2 * k + i * 2 * k;
+      acc += (double)w[j] + (double)w[k + j];
+    }
+    WG[t] = acc;
+  }
+}
+
 // second half of pass i: Ry = R^{-1} of the (all-reduced) Y^T Y (pivot
-// dropping / eigen-whitening), Q = Y Ry (orthonormal: the power iteration
-// re-orthonormalises after every application of A, so the condition number
-// never squares -- reference nla/svd.hpp:71-149), W = A^T Q -> WG[0 : n k],
-// and on the final pass G = Q^T Q (~ I: the core's second CholeskyQR step).
-// bf16 A: Q is split into bf16 hi / lo planes, and Q' = hi + lo is kept as
-// the stored basis so W, G and U = Q' M all see the same rows.
+// dropping), Q = Y Ry (orthonormal: the power iteration re-orthonormalises
+// after every application of A, so the condition number never squares --
+// reference nla/svd.hpp:71-149), W = A^T Q -> WG[0 : n k], and on the final
+// pass G = Q^T Q (~ I: the core's second CholeskyQR step).  bf16 A: Q is
+// split into bf16 hi / lo planes side by side (one m x 2k operand, so A is
+// read once for both), and Q' = hi + lo is kept as the stored basis so W, G
+// and U = Q' M all see the same rows.
 int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
   const int64_t m = p->m, n = p->n;
   const int k = p->k;
+  (void)i;
   int rc = chol_inv(p, p->WG + n * k, p->Ri, p->st + 10, s);
   if (rc != SL_OK) return rc;
-  if (p->hand) {
-    // Q = Y Ry, then W = A^T Q straight into WG (row-group slabs summed in f64)
-    if (p->dt == SL_F64) {
-      rc = sl_ts_xm64((const double*)p->Y, m, k, k, p->Ri, k, p->Qb, k, SL_F64, s);
+  if ((rc = q_from_y(p, s)) != SL_OK) return rc;
+  if (p->big) {
+    // W = A^T Q straight into WG (row-group slabs summed in f64)
+    rc = sl_ts_atq(A, m, n, p->lda, p->Qb, k, p->WG, k, p->atqw, p->dt, s);
+  } else if (p->dt == SL_BF16) {
+    k_split_bf16<<<grid_of(m * k), 256, 0, s>>>((float*)p->Qb, m, k, (bf16_t*)p->Yh);
+    SL_LAUNCH_CHECK();
+    const bf16_t* Ab = (const bf16_t*)A;
+    const bf16_t* Q2 = (const bf16_t*)p->Yh;
+    float* out = (float*)p->Wt;
+    int nparts = 1;
+    if (p->np > 0) {
+      // split K: np row chunks in one strided-batched launch (+ the remainder rows)
+      const int64_t tot = n * 2 * k;
+      out = (float*)p->parts;
+      rc = slb_gemm_strided(SL_BF16, true, false, n, 2 * k, p->ch, 1.0, Ab, p->lda, p->ch * p->lda, Q2, 2 * k,
+                            p->ch * 2 * k, 0.0, out, 2 * k, tot, p->np, s);
+      if (rc != SL_OK) return rc;
+      nparts = p->np;
+      const int64_t r0 = p->ch * p->np;
+      if (r0 < m) {
+        rc = slb_gemm(SL_BF16, true, false, n, 2 * k, m - r0, 1.0, Ab + r0 * p->lda, p->lda, Q2 + r0 * 2 * k, 2 * k,
+                      0.0, out + (int64_t)p->np * tot, 2 * k, s);
+        if (rc != SL_OK) return rc;
+        ++nparts;
+      }
     } else {
-      k_cast2d<double, float><<<grid_of((int64_t)k * k), 256, 0, s>>>(p->Ri, k, k, k, (float*)p->Rf, k, nullptr);
-      SL_LAUNCH_CHECK();
-      rc = sl_tsk_f32_xm((const float*)p->Y, m, k, k, (const float*)p->Rf, k, (float*)p->Qb, k, nullptr, nullptr, s);
+      rc = slb_gemm(SL_BF16, true, false, n, 2 * k, m, 1.0, A, p->lda, p->Yh, 2 * k, 0.0, p->Wt, 2 * k, s);
+      if (rc != SL_OK) return rc;
     }
-    if (rc != SL_OK) return rc;
-    rc = sl_ts_atq(A, m, n, p->lda, p->Qb, k, p->WG, k, p->atqw, p->dt, s);
-    if (rc != SL_OK) return rc;
-    if (!final_pass) return SL_OK;
-    return gram(p, p->Qb, p->WG + n * k, s);
-  }
-  // Q = Y Ry: big plans on the matrix-core stream kernel (Y as the m x k "A")
-  if (p->dt == SL_F64) {
-    rc = p->big ? sl_ts_az(p->Y, m, k, k, p->Ri, k, p->Qb, k, SL_F64, s)
-                : slb_gemm(SL_F64, false, false, m, k, k, 1.0, p->Y, k, p->Ri, k, 0.0, p->Qb, k, s);
+    k_sum_halves<<<grid_of(n * k), 256, 0, s>>>(out, nparts, n, k, p->WG);
+    SL_LAUNCH_CHECK();
   } else {
-    k_cast2d<double, float><<<grid_of((int64_t)k * k), 256, 0, s>>>(p->Ri, k, k, k, (float*)p->Rf, k, nullptr);
-    SL_LAUNCH_CHECK();
-    rc = p->big ? sl_ts_az(p->Y, m, k, k, p->Rf, k, p->Qb, k, SL_F32, s)
-                : slb_gemm(SL_F32, false, false, m, k, k, 1.0, p->Y, k, p->Rf, k, 0.0, p->Qb, k, s);
-  }
-  if (rc != SL_OK) return rc;
-  (void)i;
-  if (p->dt == SL_BF16) {
-    k_split_bf16<<<grid_of(m * k), 256, 0, s>>>((float*)p->Qb, m * k, (bf16_t*)p->Yh, (bf16_t*)p->Yl);
-    SL_LAUNCH_CHECK();
-    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yh, k, 0.0, p->Wt, k, s);
-    if (rc != SL_OK) return rc;
-    rc = slb_gemm(SL_BF16, true, false, n, k, m, 1.0, A, p->lda, p->Yl, k, 1.0, p->Wt, k, s);
-    if (rc != SL_OK) return rc;
-    k_cast2d<float, double><<<grid_of(n * k), 256, 0, s>>>((const float*)p->Wt, k, n, k, p->WG, k, nullptr);
-    SL_LAUNCH_CHECK();
-  } else if (p->big) {
-    // 64 < k <= 128, f32 / f64 A: the hand-written A^T Q (row-group slabs summed in f64)
-    rc = sl_ts_atq(A, m, n, p->lda, p->Qb, k, p->WG, k, p->atqw, p->dt, s);
-    if (rc != SL_OK) return rc;
-  } else {
-    // W = A^T Q as np row-chunk products (one strided-batched launch fills the
-    // chip; a single K = m product runs on a handful of workgroups), then one
-    // f64 sum of the partial slabs straight into WG
+    // library A/B (g_gen_big = 0, k > 64): W = A^T Q as np row-chunk products
+    // (one strided-batched launch fills the chip; a single K = m product runs
+    // on a handful of workgroups), then one f64 sum of the partial slabs
     const size_t es = p->dt == SL_F64 ? 8 : 4;
     const int64_t tot = n * k;
     rc = slb_gemm_strided(p->dt, true, false, n, k, p->ch, 1.0, A, p->lda, p->ch * p->lda, p->Qb, k, p->ch * k, 0.0,
@@ -374,31 +415,32 @@ int apply_t(GPlan* p, const void* A, bool final_pass, int i, hipStream_t s) {
       SL_LAUNCH_CHECK();
       return SL_OK;
     });
-    if (rc != SL_OK) return rc;
   }
+  if (rc != SL_OK) return rc;
   if (!final_pass) return SL_OK;
   return gram(p, p->Qb, p->WG + n * k, s);
 }
 
 // the boundary between pass i - 1 and pass i: CholeskyQR of the (all-reduced) W
+// H (k x k) = W^T W of the f64 n x k W: the hand-written matrix-core Grams
+int gram_w64(GPlan* p, const double* W, double* H, hipStream_t s) {
+  const int k = p->k;
+  return k > 64 ? sl_ts_gram_w(W, SL_F64, p->n, k, k, H, k, p->g64w, s) : sl_ts_gram64(W, p->n, k, k, H, k, p->g64w, s);
+}
+
 int inter(GPlan* p, int i, hipStream_t s) {
   const int k = p->k;
   const int64_t n = p->n;
-  if (p->hand) {
-    int rc = sl_ts_gram64(p->WG, n, k, k, p->H, k, p->g64w, s);
-    if (rc != SL_OK) return rc;
-    rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
-    if (rc != SL_OK) return rc;
-    return sl_ts_xm64(p->WG, n, k, k, p->Ri, k, p->Z, k, p->dt, s);   // Z = W R^{-1} in A's dtype
-  }
-  int rc = k > 64 ? sl_ts_gram_w(p->WG, SL_F64, n, k, k, p->H, k, p->g64w, s)
-                  : slb_gemm(SL_F64, true, false, k, k, n, 1.0, p->WG, k, p->WG, k, 0.0, p->H, k, s);
+  int rc = gram_w64(p, p->WG, p->H, s);
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, p->H, p->Ri, p->st + 4 + 2 * (i % 2), s);
   if (rc != SL_OK) return rc;
-  if (p->big && p->dt == SL_F64) return sl_ts_az(p->WG, n, k, k, p->Ri, k, p->Z, k, SL_F64, s);   // Z = W R^{-1}
-  rc = p->big ? sl_ts_az(p->WG, n, k, k, p->Ri, k, p->Zf, k, SL_F64, s)
-              : slb_gemm(SL_F64, false, false, n, k, k, 1.0, p->WG, k, p->Ri, k, 0.0, p->Zf, k, s);
+  // Z = W R^{-1} in A's dtype (bf16: through the f64 Zf)
+  if (k <= 64 && p->dt != SL_BF16) return sl_ts_xm64(p->WG, n, k, k, p->Ri, k, p->Z, k, p->dt, s);
+  if (p->big && p->dt == SL_F64) return sl_ts_az(p->WG, n, k, k, p->Ri, k, p->Z, k, SL_F64, s);
+  rc = k <= 64 ? sl_ts_xm64(p->WG, n, k, k, p->Ri, k, p->Zf, k, SL_F64, s)
+       : p->big || p->dt == SL_BF16 ? sl_ts_az(p->WG, n, k, k, p->Ri, k, p->Zf, k, SL_F64, s)
+                                    : slb_gemm(SL_F64, false, false, n, k, k, 1.0, p->WG, k, p->Ri, k, 0.0, p->Zf, k, s);
   if (rc != SL_OK) return rc;
   return dispatch_dt(p->dt, [&](auto* tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
@@ -433,18 +475,14 @@ int core(GPlan* p, hipStream_t s) {
   const int64_t n = p->n;
   const double* W = p->WG;
   const double* G = p->WG + n * k;
-  int rc = p->hand ? sl_ts_gram64(W, n, k, k, p->H, k, p->g64w, s)
-           : k > 64 ? sl_ts_gram_w(W, SL_F64, n, k, k, p->H, k, p->g64w, s)
-                    : slb_gemm(SL_F64, true, false, k, k, n, 1.0, W, k, W, k, 0.0, p->H, k, s);   // H = W^T W
+  int rc = gram_w64(p, W, p->H, s);   // H = W^T W
   if (rc != SL_OK) return rc;
   rc = chol_inv(p, G, p->Ri, p->st + 8, s);
   if (rc != SL_OK) return rc;
-  const bool own = p->hand || p->big;   // the k x k products on sl_ts_small
-  rc = own ? sl_ts_small(0, 0, k, k, k, p->H, k, p->Ri, k, p->T1, k, s)
-               : slb_gemm(SL_F64, false, false, k, k, k, 1.0, p->H, k, p->Ri, k, 0.0, p->T1, k, s);   // T = H Rti
+  // the k x k products on sl_ts_small (one workgroup to k = 64, 32 x 32 tiles past)
+  rc = sl_ts_small(0, 0, k, k, k, p->H, k, p->Ri, k, p->T1, k, s);   // T = H Rti
   if (rc != SL_OK) return rc;
-  rc = own ? sl_ts_small(1, 0, k, k, k, p->Ri, k, p->T1, k, p->Cc, k, s)
-               : slb_gemm(SL_F64, true, false, k, k, k, 1.0, p->Ri, k, p->T1, k, 0.0, p->Cc, k, s);   // C = Rti^T T
+  rc = sl_ts_small(1, 0, k, k, k, p->Ri, k, p->T1, k, p->Cc, k, s);   // C = Rti^T T
   if (rc != SL_OK) return rc;
   if (k <= 64) {
     SL_HIP_CHECK(hipMemsetAsync(p->st + 1, 0, 8, s));   // st[1] flag, st[2] re-solve no-convergence
@@ -462,8 +500,7 @@ int core(GPlan* p, hipStream_t s) {
     if (rc != SL_OK) return rc;
   }
   // M = Rti Ub_r (k x r), N = M S^{-1}, s
-  rc = own ? sl_ts_small(0, 0, k, r, k, p->Ri, k, p->eig, r, p->M, r, s)
-               : slb_gemm(SL_F64, false, false, k, r, k, 1.0, p->Ri, k, p->eig, r, 0.0, p->M, r, s);
+  rc = sl_ts_small(0, 0, k, r, k, p->Ri, k, p->eig, r, p->M, r, s);
   if (rc != SL_OK) return rc;
   const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
   rc = dispatch_dt(udt, [&](auto* tag) {
@@ -534,9 +571,8 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   int64_t off = 0;
   const int64_t o_z = off;   off = align256(off + n * k * (int64_t)es);
   const int64_t o_y = off;   off = align256(off + m * k * (int64_t)ys);
-  const int64_t o_yh = off;  off = align256(off + (dt == SL_BF16 ? m * k * 2 : 0));
-  const int64_t o_yl = off;  off = align256(off + (dt == SL_BF16 ? m * k * 2 : 0));
-  const int64_t o_w = off;   off = align256(off + n * k * (int64_t)ys);
+  const int64_t o_yh = off;  off = align256(off + (dt == SL_BF16 ? m * 2 * k * 2 : 0));   // bf16: [hi lo] planes
+  const int64_t o_w = off;   off = align256(off + n * (dt == SL_BF16 ? 2 * k : k) * (int64_t)ys);
   const int64_t o_qb = off;  off = align256(off + m * k * (int64_t)ys);
   const int64_t o_rf = off;  off = align256(off + (int64_t)k * k * 4);
   const int64_t o_wg = off;  off = align256(off + (n + k) * k * 8);
@@ -554,14 +590,17 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
   // f32 / f64 A: row-chunk partials of A^T Y (and of Y^T Y), <= 64 MB of slabs
   int np = 0;
   int64_t ch = 0;
-  if (dt != SL_BF16 && !p->big) {
-    const int64_t slab = std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es;
-    np = (int)std::max<int64_t>(1, std::min<int64_t>({128, (int64_t(64) << 20) / slab, m / 512}));
+  // (bf16 A: of A^T [Q_hi Q_lo], n x 2k f32 slabs, when g_bf16_split)
+  const bool bsplit = dt == SL_BF16 && g_bf16_split;
+  const int64_t slab_el = dt == SL_BF16 ? n * 2 * k : std::max<int64_t>(n * k, (int64_t)k * k);
+  const int64_t slab_es = dt == SL_BF16 ? 4 : (int64_t)es;
+  if ((dt != SL_BF16 && !p->big) || bsplit) {
+    np = (int)std::max<int64_t>(1, std::min<int64_t>({128, (int64_t(64) << 20) / (slab_el * slab_es), m / 512}));
     ch = m / np;
   }
-  const int64_t o_pt = off;  off = align256(off + (dt != SL_BF16 && !p->big ? (int64_t)(np + 1) * std::max<int64_t>(n * k, (int64_t)k * k) * (int64_t)es : 0));
+  const int64_t o_pt = off;  off = align256(off + (np ? (int64_t)(np + 1) * slab_el * slab_es : 0));
   const int64_t o_aw = off;  off = align256(off + (p->big ? sl_ts_atq_workspace(m, n, k, dt) : 0));
-  const int64_t o_g6 = off;  off = align256(off + (hand || k > 64 ? sl_ts_gram64_workspace(std::max(m, n), k) : 0));
+  const int64_t o_g6 = off;  off = align256(off + sl_ts_gram64_workspace(std::max(m, n), k));
   const int64_t o_st = off;  off = align256(off + 64 * 4);
   if (hipMalloc((void**)&p->base, (size_t)off) != hipSuccess) {
     delete p;
@@ -569,7 +608,7 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
     return SL_ERR_HIP;
   }
   char* b = p->base;
-  p->Z = b + o_z; p->Y = b + o_y; p->Yh = b + o_yh; p->Yl = b + o_yl; p->Wt = b + o_w;
+  p->Z = b + o_z; p->Y = b + o_y; p->Yh = b + o_yh; p->Wt = b + o_w;
   p->Qb = b + o_qb; p->Rf = b + o_rf;
   p->WG = (double*)(b + o_wg); p->Zf = (double*)(b + o_zf); p->H = (double*)(b + o_h); p->Ri = (double*)(b + o_ri);
   p->T1 = (double*)(b + o_t1); p->Cc = (double*)(b + o_c); p->eig = (double*)(b + o_e); p->M = (double*)(b + o_m);
@@ -590,6 +629,7 @@ SL_API int sl_rsvd_gen_create(int64_t m, int64_t n, int64_t lda, int k, int r, i
 }
 
 SL_API void sl_rsvd_gen_set_big(int v) { g_gen_big = v ? 1 : 0; }
+SL_API void sl_rsvd_gen_set_bf16_split(int v) { g_bf16_split = v ? 1 : 0; }
 
 SL_API int sl_rsvd_gen_destroy(void* plan) {
   GPlan* p = (GPlan*)plan;
@@ -659,7 +699,7 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
   hipStream_t s = (hipStream_t)stream;
   const int k = p->k, r = p->r;
   const int udt = p->dt == SL_BF16 ? SL_F32 : p->dt;
-  if (p->hand) {
+  if (k <= 64) {
     int rc = sl_ts_xm64(p->WG, p->n, k, k, p->N, r, V, r, udt, s);   // V = W N
     if (rc != SL_OK) return rc;
     rc = dispatch_dt(udt, [&](auto* tag) {
@@ -672,7 +712,8 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
     if (udt == SL_F64) return sl_ts_xm64((const double*)p->Qb, p->m, k, k, p->M, r, U, ldu, SL_F64, s);   // U = Q M
     return sl_tsk_f32_xm((const float*)p->Qb, p->m, k, k, (const float*)p->Md, r, (float*)U, ldu, nullptr, nullptr, s);
   }
-  int rc = p->big ? sl_ts_az(p->WG, p->n, k, k, p->N, r, p->Vf, r, SL_F64, s)
+  const bool own = p->big || p->dt == SL_BF16;   // hand-written past k = 64 (all but the library A/B)
+  int rc = own ? sl_ts_az(p->WG, p->n, k, k, p->N, r, p->Vf, r, SL_F64, s)
                   : slb_gemm(SL_F64, false, false, p->n, r, k, 1.0, p->WG, k, p->N, r, 0.0, p->Vf, r, s);   // V = W N
   if (rc != SL_OK) return rc;
   rc = dispatch_dt(udt, [&](auto* tag) {
@@ -684,7 +725,7 @@ SL_API int sl_rsvd_gen_finish(void* plan, void* U, int64_t ldu, void* s_out, voi
     return SL_OK;
   });
   if (rc != SL_OK) return rc;
-  if (p->big) return sl_ts_az(p->Qb, p->m, k, k, p->Md, r, U, ldu, udt, s);   // U = Q M
+  if (own) return sl_ts_az(p->Qb, p->m, k, k, p->Md, r, U, ldu, udt, s);   // U = Q M
   return slb_gemm(udt, false, false, p->m, r, k, 1.0, p->Qb, k, p->Md, r, 0.0, U, ldu, s);
 }
 

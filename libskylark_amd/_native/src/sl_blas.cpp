@@ -40,6 +40,9 @@ struct Blas {
   int (*sgemm_sb)(void*, int, int, int, int, int, const float*, const float*, int, int64_t, const float*, int,
                   int64_t, const float*, float*, int, int64_t, int) = nullptr;
   int (*dtrsv)(void*, int, int, int, int, const double*, int, double*, int) = nullptr;
+  int (*gemm_sb_ex)(void*, int, int, int, int, int, const void*, const void*, int, int, int64_t, const void*, int, int,
+                    int64_t, const void*, const void*, int, int, int64_t, void*, int, int, int64_t, int, int, int, int,
+                    uint32_t) = nullptr;
   void* handle[64] = {};
 };
 
@@ -69,6 +72,7 @@ Blas& blas() {
   B.dgemm_sb = (decltype(B.dgemm_sb))sym(B.rb, "rocblas_dgemm_strided_batched");
   B.sgemm_sb = (decltype(B.sgemm_sb))sym(B.rb, "rocblas_sgemm_strided_batched");
   B.dtrsv = (decltype(B.dtrsv))sym(B.rb, "rocblas_dtrsv");
+  B.gemm_sb_ex = (decltype(B.gemm_sb_ex))dlsym(B.rb, "rocblas_gemm_strided_batched_ex");
   if (B.rs) {
     B.dsyevd = (decltype(B.dsyevd))dlsym(B.rs, "rocsolver_dsyevd");
     B.dtrtri = (decltype(B.dtrtri))dlsym(B.rs, "rocsolver_dtrtri");
@@ -144,7 +148,7 @@ int slb_gemm(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, double a
 
 // batch of row-major products C_b = alpha op(A_b) op(B_b) + beta C_b with
 // element strides sA / sB / sC between the operands of consecutive batches
-// (SL_F32 / SL_F64)
+// (SL_F32 / SL_F64, or SL_BF16: A, B bf16, C f32, f32 accumulation)
 int slb_gemm_strided(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, double alpha, const void* A,
                      int64_t lda, int64_t sA, const void* B, int64_t ldb, int64_t sB, double beta, void* C, int64_t ldc,
                      int64_t sC, int batch, hipStream_t s) {
@@ -154,6 +158,16 @@ int slb_gemm_strided(int dt, bool ta, bool tb, int64_t M, int64_t N, int64_t K, 
   if (rc != SL_OK) return rc;
   Blas& L = blas();
   const int opA = ta ? OP_T : OP_N, opB = tb ? OP_T : OP_N;
+  if (dt == SL_BF16) {
+    if (!L.gemm_sb_ex) {
+      sl_set_last_error("rocblas_gemm_strided_batched_ex not found");
+      return SL_ERR_UNSUPPORTED;
+    }
+    const float al = (float)alpha, be = (float)beta;
+    return rc_of(L.gemm_sb_ex(h, opB, opA, (int)N, (int)M, (int)K, &al, B, DT_BF16, (int)ldb, sB, A, DT_BF16, (int)lda,
+                              sA, &be, C, DT_F32, (int)ldc, sC, C, DT_F32, (int)ldc, sC, batch, DT_F32, 0, 0, 0),
+                 "rocblas_gemm_strided_batched_ex");
+  }
   if (dt == SL_F64) {
     const double al = alpha, be = beta;
     return rc_of(L.dgemm_sb(h, opB, opA, (int)N, (int)M, (int)K, &al, (const double*)B, (int)ldb, sB,
