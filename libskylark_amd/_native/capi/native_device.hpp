@@ -112,6 +112,8 @@ struct Lib {
                   double*, void*) = nullptr;
   int (*blendenpik)(const double*, int64_t, int64_t, int64_t, const double*, int, int64_t, double*, int64_t, uint64_t,
                     uint64_t*, double, int, int*, void*) = nullptr;
+  int (*blendenpik_comm)(const double*, int64_t, int64_t, int64_t, const double*, int, int64_t, double*, int64_t,
+                         int64_t, int64_t, void*, uint64_t, uint64_t*, double, int, int*, void*) = nullptr;
   int (*libsvm_scan)(const char*, int64_t, int, int64_t*, int64_t*, int64_t*, int*) = nullptr;
   int (*libsvm_fill)(const char*, const int64_t*, const int64_t*, int, int64_t, double*, int64_t*, int64_t*,
                      double*) = nullptr;
@@ -185,6 +187,7 @@ inline Lib& lib() {
               bind(L.h, "sl_rsvd_gen_set_z", L.gen_set_z, L.err) && bind(L.h, "sl_rsvd_gen_run", L.gen_run, L.err) &&
               bind(L.h, "sl_rsvd_gen_status", L.gen_status, L.err) &&
               bind(L.h, "sl_nat_sym_rsvd", L.sym_rsvd, L.err) && bind(L.h, "sl_nat_blendenpik", L.blendenpik, L.err) &&
+              bind(L.h, "sl_nat_blendenpik_comm", L.blendenpik_comm, L.err) &&
               bind(L.h, "sl_libsvm_scan", L.libsvm_scan, L.err) && bind(L.h, "sl_libsvm_fill", L.libsvm_fill, L.err);
     if (!ok) return;
     L.rb = dlopen("librocblas.so", RTLD_NOW | RTLD_LOCAL);
@@ -1082,6 +1085,47 @@ inline int faster_least_squares_host(int orientation, const double* A, int64_t m
                          &ctr, tol, iter_lim, &code, nullptr),
             "faster least squares");
   SLDEV_TRY(L.dev_memcpy(X, dX.p, xm * xn * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
+// FasterLeastSquares on DistMatrix operands: A (mg x n) and B (mg x nrhs) as
+// [VC,*] / [VR,*] f64 device shards (row-major), X (n x nrhs) replicated
+// ([*,*]); the same sketch-and-precondition LSQR as the host path with the
+// sketch and A^T u summed over A's communicator (sl_nat_blendenpik_comm).
+inline int faster_least_squares_dist(const DistMat& A, const DistMat& B, const DistMat& X, const char* params,
+                                     uint64_t seed, uint64_t& ctr) {
+  Lib& L = lib();
+  if (!L.loaded) return fail(106, "device C API: " + L.err);
+  if (A.dtype != F64 || B.dtype != F64 || X.dtype != F64) return fail(103, "faster_least_squares: f64 operands");
+  if (B.comm != A.comm || X.comm != A.comm) return fail(109, "faster_least_squares: operands on different communicators");
+  if (B.m != A.m || X.m != A.n || X.n != B.n) return fail(104, "faster_least_squares: dimension mismatch");
+  if (A.m < A.n) return fail(103, "faster_least_squares: distributed A must be overdetermined (m >= n)");
+  double tol = 1e-14, v;
+  int iter_lim = 100;
+  if (params && *params) {
+    if (slnat::get_number(params, "tolerance", v)) tol = v;
+    if (slnat::get_number(params, "iter_lim", v)) iter_lim = (int)v;
+  }
+  int rank = 0, size = 1;
+  int rc = comm_rank_size(A.comm, &rank, &size);
+  if (rc) return rc;
+  int64_t r0, c0, lm, ln;
+  shard_of(LY_ROWS, A.m, A.n, rank, size, &r0, &c0, &lm, &ln);
+  const int64_t n = A.n, nrhs = B.n;
+  // column-major shards: the row-major transposes
+  Buf At(std::max<int64_t>(1, lm * n) * 8), Bt(std::max<int64_t>(1, lm * nrhs) * 8), Xc(n * nrhs * 8);
+  if (!At.p || !Bt.p || !Xc.p) return fail(101, "faster_least_squares: device allocation failed");
+  if (lm > 0) {
+    SLDEV_TRY(L.transpose(A.data, F64, lm, n, A.ld, At.p, lm, nullptr), "transpose");
+    SLDEV_TRY(L.transpose(B.data, F64, lm, nrhs, B.ld, Bt.p, lm, nullptr), "transpose");
+  }
+  int code = 0;
+  SLDEV_TRY(L.blendenpik_comm((const double*)At.p, lm, n, std::max<int64_t>(lm, 1), (const double*)Bt.p, (int)nrhs,
+                              std::max<int64_t>(lm, 1), (double*)Xc.p, n, A.m, r0, A.comm, seed, &ctr, tol, iter_lim,
+                              &code, nullptr),
+            "faster least squares");
+  // X (row-major n x nrhs) = the transpose of the column-major result
+  SLDEV_TRY(L.transpose(Xc.p, F64, nrhs, n, n, X.data, X.ld, nullptr), "transpose");
   return check(L.dev_sync(nullptr), "sync");
 }
 

@@ -17,8 +17,9 @@
 //    DistMatrix_VC_STAR / _VR_STAR, DistMatrix_STAR_VC / _STAR_VR,
 //    SharedMatrix, RootMatrix; sl_wrap_raw_dist_device_matrix) in
 //    sl_apply_sketch_transform (every sketch type: the ranks' column ranges
-//    of the operator summed by all-reduce), sl_approximate_svd ([VC,*] A) and
-//    sl_kernel_gram (points split over the ranks) -- no interpreter.  The
+//    of the operator summed by all-reduce), sl_approximate_svd ([VC,*] A),
+//    sl_faster_least_squares ([VC,*] A and B) and sl_kernel_gram (points
+//    split over the ranks) -- no interpreter.  The
 //    2-D [MC,MR] "DistMatrix" has no native path.
 // Everything else (runtime-only kernels, the remaining entry points) goes
 // through the Python/HIP runtime
@@ -998,6 +999,20 @@ SL_CAPI int sl_approximate_symmetric_svd(char* A_type, void* A, char* S_type, vo
 
 SL_CAPI int sl_faster_least_squares(int orientation, char* A_type, void* A, char* B_type, void* B, char* X_type,
                                     void* X, char* params, sl_context_t* ctxt) {
+  int la, lb;
+  if (const int e = dist_pair("sl_faster_least_squares", A_type, B_type, &la, &lb)) return e;
+  if (la >= 0) {
+    if (orientation != 0 || la != sldev::LY_ROWS || lb != sldev::LY_ROWS || dist_layout(X_type) != sldev::LY_STAR) {
+      g_last_error = "sl_faster_least_squares: distributed operands: orientation NORMAL, A and B DistMatrix_VC_STAR / "
+                     "_VR_STAR, X SharedMatrix";
+      return 103;
+    }
+    uint64_t ctr = ctxt->counter;
+    const int rc = sldev::faster_least_squares_dist(distmat(A), distmat(B), distmat(X), params, ctxt->seed, ctr);
+    if (rc) return native_fail(rc);
+    ctxt->counter = ctr;
+    return 0;
+  }
   if (!strcmp(A_type, "Matrix") && !strcmp(B_type, "Matrix") && !strcmp(X_type, "Matrix") && sldev::device_present()) {
     auto *a = (sl_raw_matrix_t*)A, *b = (sl_raw_matrix_t*)B, *x = (sl_raw_matrix_t*)X;
     uint64_t ctr = ctxt->counter;

@@ -32,6 +32,8 @@ SL_API int sl_symmetrize(const void* A, int dtype, int64_t n, int64_t lda, int l
                          void* stream);
 SL_API int sl_dct2_rows(const int64_t* rows, int64_t S, int64_t N, const double* d, double scale, void* out,
                         int dtype, int64_t ld, int transpose, void* stream);
+SL_API int sl_comm_all_reduce(void* comm, const void* send, void* recv, int64_t count, int dtype, int op,
+                              void* stream);
 
 namespace {
 
@@ -177,15 +179,44 @@ SL_API int sl_nat_sym_rsvd(const double* A, int64_t n, int64_t lda, int lower, i
 
 namespace {
 
+// Row distribution of the least-squares operand: this rank holds rows
+// [r0, r0 + m) of the mg-row A and B; comm (sl_comm_*) sums over the ranks,
+// null = one rank.  Every n-vector / n x n quantity is replicated and, the
+// sums being identical on every rank, bit-equal across ranks.
+struct Dist {
+  void* comm = nullptr;
+  int64_t mg = 0, r0 = 0;
+  double* scal = nullptr;   // device scratch (1 double) for scalar sums
+};
+
+int dsum(const Dist& D, double* dev, int64_t count, hipStream_t s) {
+  if (!D.comm) return SL_OK;
+  return sl_comm_all_reduce(D.comm, dev, dev, count, SL_F64, 0, s);
+}
+
+// 2-norm of a row-distributed vector (m local entries)
+int nrm2_rows(const Dist& D, int64_t m, const double* u, double* out, hipStream_t s) {
+  NAT_TRY(slb_dnrm2((int)m, u, out, s));
+  if (!D.comm) return SL_OK;
+  double sq = (*out) * (*out);
+  SL_HIP_CHECK(hipMemcpyAsync(D.scal, &sq, sizeof(double), hipMemcpyHostToDevice, s));
+  NAT_TRY(dsum(D, D.scal, 1, s));
+  SL_HIP_CHECK(hipMemcpyAsync(&sq, D.scal, sizeof(double), hipMemcpyDeviceToHost, s));
+  SL_HIP_CHECK(hipStreamSynchronize(s));
+  *out = std::sqrt(sq);
+  return SL_OK;
+}
+
 // runtime lsqr (algorithms/krylov.py) for one right-hand side, preconditioned
-// by P = R^{-1} (explicit Rinv when given, else triangular solves with R)
-int lsqr_one(const double* A, int64_t m, int64_t n, int64_t lda, const double* b, double* x, const double* R,
-             const double* Rinv, double tol, int iter_lim, int* code, double* u, double* v, double* w, double* z,
-             double* t, hipStream_t s) {
+// by P = R^{-1} (explicit Rinv when given, else triangular solves with R); A,
+// b, u row-distributed per D (m local rows), x, v, w, z, t replicated
+int lsqr_one(const Dist& D, const double* A, int64_t m, int64_t n, int64_t lda, const double* b, double* x,
+             const double* R, const double* Rinv, double tol, int iter_lim, int* code, double* u, double* v, double* w,
+             double* z, double* t, hipStream_t s) {
   const double eps = 32 * DBL_EPSILON;
   if (tol < eps) tol = eps;
   if (tol >= 1.0) tol = 1 - eps;
-  if (iter_lim < 0) iter_lim = std::max<int64_t>(20, 2 * std::min(m, n));
+  if (iter_lim < 0) iter_lim = std::max<int64_t>(20, 2 * std::min(D.mg, n));
   auto P = [&](double* vec) -> int {   // vec = R^{-1} vec (z = P v)
     if (Rinv) {
       NAT_TRY(slb_dgemv_cm(false, (int)n, (int)n, 1.0, Rinv, (int)n, vec, 0.0, t, s));
@@ -197,10 +228,11 @@ int lsqr_one(const double* A, int64_t m, int64_t n, int64_t lda, const double* b
   SL_HIP_CHECK(hipMemcpyAsync(u, b, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
   SL_HIP_CHECK(hipMemsetAsync(x, 0, sizeof(double) * n, s));
   double beta = 0, alpha = 0;
-  NAT_TRY(slb_dnrm2((int)m, u, &beta, s));
+  NAT_TRY(nrm2_rows(D, m, u, &beta, s));
   k_axpby<<<grid_of(m), 256, 0, s>>>(m, 0.0, u, 1.0 / std::max(beta, DBL_MIN), u);
   // v = P^T A^T u
   NAT_TRY(slb_dgemv_cm(true, (int)m, (int)n, 1.0, A, (int)lda, u, 0.0, t, s));
+  NAT_TRY(dsum(D, t, n, s));
   if (Rinv) {
     NAT_TRY(slb_dgemv_cm(true, (int)n, (int)n, 1.0, Rinv, (int)n, t, 0.0, v, s));
   } else {
@@ -223,10 +255,11 @@ int lsqr_one(const double* A, int64_t m, int64_t n, int64_t lda, const double* b
   *code = -6;
   for (int itn = 0; itn < iter_lim; ++itn) {
     NAT_TRY(slb_dgemv_cm(false, (int)m, (int)n, 1.0, A, (int)lda, z, -alpha, u, s));   // u = A z - alpha u
-    NAT_TRY(slb_dnrm2((int)m, u, &beta, s));
+    NAT_TRY(nrm2_rows(D, m, u, &beta, s));
     k_axpby<<<grid_of(m), 256, 0, s>>>(m, 0.0, u, 1.0 / beta, u);
     nrm_a = std::sqrt(nrm_a * nrm_a + alpha * alpha + beta * beta);
     NAT_TRY(slb_dgemv_cm(true, (int)m, (int)n, 1.0, A, (int)lda, u, 0.0, t, s));        // t = A^T u
+    NAT_TRY(dsum(D, t, n, s));
     if (Rinv) {
       NAT_TRY(slb_dgemv_cm(true, (int)n, (int)n, 1.0, Rinv, (int)n, t, -beta, v, s));   // v = P^T t - beta v
     } else {
@@ -273,57 +306,67 @@ int lsqr_one(const double* A, int64_t m, int64_t n, int64_t lda, const double* b
 
 }  // namespace
 
-// min ||A X - B||: A column-major m x n (lda), B m x nrhs (ldb), X n x nrhs
-// (ldx), device memory.  *ctr: the context counter (advanced by m + 4n per
-// sketch drawn, as the runtime's FJLT draws); *code: the last column's LSQR
-// code (-1 zero rhs, -2 / -3 converged, -4 ill-conditioned, -5 stagnation,
-// -6 iteration limit, -7 exact SVD fallback).
-SL_API int sl_nat_blendenpik(const double* A, int64_t m, int64_t n, int64_t lda, const double* B, int nrhs,
-                             int64_t ldb, double* X, int64_t ldx, uint64_t seed, uint64_t* ctr, double tol,
-                             int iter_lim, int* code, void* stream) {
+// min ||A X - B|| with A and B row-distributed: this rank holds rows [r0, r0
+// + m) of the mg x n A (column-major, lda) and of B (ldb); X (n x nrhs, ldx)
+// comes out the same on every rank.  The FJLT sketch draws the operator over
+// all mg rows (so every rank count gives the one-rank sketch), each rank
+// applies its columns of it and the t x n partial sketches are summed; LSQR
+// sums A^T u and ||u||^2 over the ranks (comm: sl_comm_*, null = one rank).
+SL_API int sl_nat_blendenpik_comm(const double* A, int64_t m, int64_t n, int64_t lda, const double* B, int nrhs,
+                                  int64_t ldb, double* X, int64_t ldx, int64_t mg, int64_t r0, void* comm,
+                                  uint64_t seed, uint64_t* ctr, double tol, int iter_lim, int* code, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (m < 1 || n < 1 || n > m) {
-    sl_set_last_error("blendenpik: needs m >= n >= 1 (an overdetermined system)");
+  if (mg < 1 || n < 1 || n > mg || m < 0 || r0 < 0 || r0 + m > mg) {
+    sl_set_last_error("blendenpik: needs mg >= n >= 1 (an overdetermined system) and a row range inside it");
     return SL_ERR_INVALID;
   }
   if (!slb_solver_available()) {
     sl_set_last_error("blendenpik: rocBLAS / rocSOLVER not available");
     return SL_ERR_UNSUPPORTED;
   }
+  DevBuf scal(sizeof(double));
+  Dist D;
+  D.comm = comm;
+  D.mg = mg;
+  D.r0 = r0;
+  D.scal = scal.d();
   const int64_t t = 4 * n;
-  const double scale = std::sqrt((double)m / (double)t);
-  DevBuf dD(sizeof(double) * m), dsamp(sizeof(int64_t) * t), SA(sizeof(double) * t * n), tau(sizeof(double) * n),
+  const double scale = std::sqrt((double)mg / (double)t);
+  DevBuf dD(sizeof(double) * mg), dsamp(sizeof(int64_t) * t), SA(sizeof(double) * t * n), tau(sizeof(double) * n),
       R(sizeof(double) * n * n), Ri(sizeof(double) * n * n), nrm(sizeof(double) * 2 * n), info(sizeof(int) * 4);
   if (!dD.p || !dsamp.p || !SA.p || !tau.p || !R.p || !Ri.p || !nrm.p || !info.p) {
     sl_set_last_error("blendenpik: device allocation failed");
     return SL_ERR_HIP;
   }
-  const int64_t PB = std::max<int64_t>(1, std::min<int64_t>(t, (int64_t(1) << 25) / m));   // operator rows per panel
-  DevBuf panel(sizeof(double) * PB * m);
+  const int64_t PB = std::max<int64_t>(1, std::min<int64_t>(t, (int64_t(1) << 25) / mg));   // operator rows per panel
+  DevBuf panel(sizeof(double) * PB * mg);
   if (!panel.p) {
     sl_set_last_error("blendenpik: device allocation failed");
     return SL_ERR_HIP;
   }
   bool ok = false;
   double kappa = HUGE_VAL;
-  std::vector<double> hD((size_t)m);
+  std::vector<double> hD((size_t)mg);
   std::vector<int64_t> hs((size_t)t);
   for (int attempt = 0; attempt < 3 && !ok; ++attempt) {
-    // FJLT(m, t) from the stream: m Rademacher signs, then t sample rows
+    // FJLT(mg, t) from the stream: mg Rademacher signs, then t sample rows
     const uint64_t c = *ctr;
-    for (int64_t i = 0; i < m; ++i) hD[(size_t)i] = sl::sample_d(sl::DIST_RADEMACHER, seed, c + (uint64_t)i, 0, 0);
+    for (int64_t i = 0; i < mg; ++i) hD[(size_t)i] = sl::sample_d(sl::DIST_RADEMACHER, seed, c + (uint64_t)i, 0, 0);
     for (int64_t j = 0; j < t; ++j)
-      hs[(size_t)j] = sl::uniform_int(sl::stream_block(seed, c + (uint64_t)(m + j)).x, 0, m - 1);
-    *ctr = c + (uint64_t)(m + t);
-    SL_HIP_CHECK(hipMemcpyAsync(dD.p, hD.data(), sizeof(double) * m, hipMemcpyHostToDevice, s));
+      hs[(size_t)j] = sl::uniform_int(sl::stream_block(seed, c + (uint64_t)(mg + j)).x, 0, mg - 1);
+    *ctr = c + (uint64_t)(mg + t);
+    SL_HIP_CHECK(hipMemcpyAsync(dD.p, hD.data(), sizeof(double) * mg, hipMemcpyHostToDevice, s));
     SL_HIP_CHECK(hipMemcpyAsync(dsamp.p, hs.data(), sizeof(int64_t) * t, hipMemcpyHostToDevice, s));
     // S A (t x n, ld t) = (operator rows) A, panel by panel of operator rows;
-    // a panel is stored m x pb column-major (sl_dct2_rows transpose layout)
-    for (int64_t j0 = 0; j0 < t; j0 += PB) {
+    // a panel is the pb x mg column-major operator block (ld pb), this rank's
+    // columns r0 .. r0 + m of it against its rows of A
+    if (m == 0) SL_HIP_CHECK(hipMemsetAsync(SA.p, 0, sizeof(double) * t * n, s));
+    for (int64_t j0 = 0; j0 < t && m > 0; j0 += PB) {
       const int64_t pb = std::min(PB, t - j0);
-      NAT_TRY(sl_dct2_rows((const int64_t*)dsamp.p + j0, pb, m, dD.d(), scale, panel.p, SL_F64, pb, 1, s));
-      NAT_TRY(gemm_cm(false, false, pb, n, m, panel.d(), pb, A, lda, 0.0, SA.d() + j0, t, s));
+      NAT_TRY(sl_dct2_rows((const int64_t*)dsamp.p + j0, pb, mg, dD.d(), scale, panel.p, SL_F64, pb, 1, s));
+      NAT_TRY(gemm_cm(false, false, pb, n, m, panel.d() + r0 * pb, pb, A, lda, 0.0, SA.d() + j0, t, s));
     }
+    NAT_TRY(dsum(D, SA.d(), t * n, s));
     NAT_TRY(slb_dgeqrf_cm((int)t, (int)n, SA.d(), (int)t, tau.d(), s));
     k_upper<<<grid_of(n * n), 256, 0, s>>>(SA.d(), t, n, R.d());
     SL_LAUNCH_CHECK();
@@ -346,23 +389,32 @@ SL_API int sl_nat_blendenpik(const double* A, int64_t m, int64_t n, int64_t lda,
     ok = std::isfinite(kappa) && kappa < 1e14;
   }
   if (!ok) {
-    // reference: an exact solver when the sketch never yields a usable R
+    // reference: an exact solver when the sketch never yields a usable R (the
+    // whole A and B on every rank: each rank's rows placed in zeros, summed)
     const int64_t r = n;
-    DevBuf Ac(sizeof(double) * m * n), U(sizeof(double) * m * r), VT(sizeof(double) * r * n), sv(sizeof(double) * r),
-        E(sizeof(double) * r), W(sizeof(double) * r * nrhs);
-    if (!Ac.p || !U.p || !VT.p || !sv.p || !E.p || !W.p) {
+    DevBuf Ac(sizeof(double) * mg * n), Bc(sizeof(double) * mg * nrhs), U(sizeof(double) * mg * r),
+        VT(sizeof(double) * r * n), sv(sizeof(double) * r), E(sizeof(double) * r), W(sizeof(double) * r * nrhs);
+    if (!Ac.p || !Bc.p || !U.p || !VT.p || !sv.p || !E.p || !W.p) {
       sl_set_last_error("blendenpik: device allocation failed");
       return SL_ERR_HIP;
     }
-    SL_HIP_CHECK(hipMemcpy2DAsync(Ac.p, sizeof(double) * m, A, sizeof(double) * lda, sizeof(double) * m, n,
-                                  hipMemcpyDeviceToDevice, s));
-    NAT_TRY(slb_dgesvd_cm((int)m, (int)n, Ac.d(), (int)m, sv.d(), U.d(), (int)m, VT.d(), (int)r, E.d(), (int*)info.p,
-                          s));
+    SL_HIP_CHECK(hipMemsetAsync(Ac.p, 0, sizeof(double) * mg * n, s));
+    SL_HIP_CHECK(hipMemsetAsync(Bc.p, 0, sizeof(double) * mg * nrhs, s));
+    if (m > 0) {
+      SL_HIP_CHECK(hipMemcpy2DAsync(Ac.d() + r0, sizeof(double) * mg, A, sizeof(double) * lda, sizeof(double) * m, n,
+                                    hipMemcpyDeviceToDevice, s));
+      SL_HIP_CHECK(hipMemcpy2DAsync(Bc.d() + r0, sizeof(double) * mg, B, sizeof(double) * ldb, sizeof(double) * m, nrhs,
+                                    hipMemcpyDeviceToDevice, s));
+    }
+    NAT_TRY(dsum(D, Ac.d(), mg * n, s));
+    NAT_TRY(dsum(D, Bc.d(), mg * nrhs, s));
+    NAT_TRY(slb_dgesvd_cm((int)mg, (int)n, Ac.d(), (int)mg, sv.d(), U.d(), (int)mg, VT.d(), (int)r, E.d(),
+                          (int*)info.p, s));
     double smax = 0;
     SL_HIP_CHECK(hipMemcpyAsync(&smax, sv.p, sizeof(double), hipMemcpyDeviceToHost, s));
     SL_HIP_CHECK(hipStreamSynchronize(s));
-    const double cut = smax * (double)std::max(m, n) * DBL_EPSILON;
-    NAT_TRY(gemm_cm(true, false, r, nrhs, m, U.d(), m, B, ldb, 0.0, W.d(), r, s));
+    const double cut = smax * (double)std::max(mg, n) * DBL_EPSILON;
+    NAT_TRY(gemm_cm(true, false, r, nrhs, mg, U.d(), mg, Bc.d(), mg, 0.0, W.d(), r, s));
     k_scale_rows<<<grid_of(r * nrhs), 256, 0, s>>>(W.d(), r, nrhs, r, sv.d(), cut);
     SL_LAUNCH_CHECK();
     NAT_TRY(gemm_cm(true, false, n, nrhs, r, VT.d(), r, W.d(), r, 0.0, X, ldx, s));
@@ -370,8 +422,8 @@ SL_API int sl_nat_blendenpik(const double* A, int64_t m, int64_t n, int64_t lda,
     *code = -7;
     return SL_OK;
   }
-  DevBuf u(sizeof(double) * m), v(sizeof(double) * n), w(sizeof(double) * n), z(sizeof(double) * n),
-      tv(sizeof(double) * std::max(m, n));
+  DevBuf u(sizeof(double) * std::max<int64_t>(m, 1)), v(sizeof(double) * n), w(sizeof(double) * n),
+      z(sizeof(double) * n), tv(sizeof(double) * std::max(m, n));
   if (!u.p || !v.p || !w.p || !z.p || !tv.p) {
     sl_set_last_error("blendenpik: device allocation failed");
     return SL_ERR_HIP;
@@ -379,8 +431,20 @@ SL_API int sl_nat_blendenpik(const double* A, int64_t m, int64_t n, int64_t lda,
   // explicit R^{-1} while it stays accurate (error ~ kappa eps), else solves
   const double* Rinv = kappa < 1e7 ? Ri.d() : nullptr;
   for (int j = 0; j < nrhs; ++j)
-    NAT_TRY(lsqr_one(A, m, n, lda, B + (int64_t)j * ldb, X + (int64_t)j * ldx, R.d(), Rinv, tol, iter_lim, code, u.d(),
-                     v.d(), w.d(), z.d(), tv.d(), s));
+    NAT_TRY(lsqr_one(D, A, m, n, lda, B + (int64_t)j * ldb, X + (int64_t)j * ldx, R.d(), Rinv, tol, iter_lim, code,
+                     u.d(), v.d(), w.d(), z.d(), tv.d(), s));
   SL_HIP_CHECK(hipStreamSynchronize(s));
   return SL_OK;
+}
+
+// min ||A X - B||: A column-major m x n (lda), B m x nrhs (ldb), X n x nrhs
+// (ldx), device memory.  *ctr: the context counter (advanced by m + 4n per
+// sketch drawn, as the runtime's FJLT draws); *code: the last column's LSQR
+// code (-1 zero rhs, -2 / -3 converged, -4 ill-conditioned, -5 stagnation,
+// -6 iteration limit, -7 exact SVD fallback).
+SL_API int sl_nat_blendenpik(const double* A, int64_t m, int64_t n, int64_t lda, const double* B, int nrhs,
+                             int64_t ldb, double* X, int64_t ldx, uint64_t seed, uint64_t* ctr, double tol,
+                             int iter_lim, int* code, void* stream) {
+  return sl_nat_blendenpik_comm(A, m, n, lda, B, nrhs, ldb, X, ldx, m, 0, nullptr, seed, ctr, tol, iter_lim, code,
+                                stream);
 }

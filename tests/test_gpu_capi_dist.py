@@ -5,9 +5,12 @@ reference's type names (capi/matrix_types.cpp: DistMatrix_VC_STAR,
 DistMatrix_STAR_VC, SharedMatrix, RootMatrix), the sums going through a
 callback communicator (sl_device_comm_from_allreduce) that all-reduces over
 this test's gloo group -- the same code an RCCL communicator drives across
-GPUs.  Oracle: the single-rank DeviceMatrix call of the same C ABI on the
-whole operand (the reference's distributed == local invariant,
-tests/unit/DenseSketchApplyElementalTest.cpp:52-101)."""
+GPUs.  Covers sketch application (8 layout cases x 7 sketch types),
+randSVD ([VC,*] A), kernel Grams and FasterLeastSquares ([VC,*] A and B).
+Oracle: the single-rank call of the same C ABI on the whole operand
+(DeviceMatrix; host "Matrix" for least squares, plus numpy lstsq) -- the
+reference's distributed == local invariant
+(tests/unit/DenseSketchApplyElementalTest.cpp:52-101)."""
 import pytest
 import torch
 
@@ -176,14 +179,44 @@ def _worker(rank, world):
     assert lib.sl_kernel_gram(2, 1, kh, b"DeviceMatrix", wx, b"DeviceMatrix", wy, b"DeviceMatrix", wk) == 0, err()
     torch.cuda.synchronize()
     kdiff = (Kl[:klm] - Kref[kr0:kr0 + klm]).abs().max().item()
+    # least squares with A and B row-distributed, X replicated, against the
+    # one-rank host-operand call on the same context stream and numpy
+    mL, nL, nr = 3000, 40, 2
+    gA = np.random.RandomState(8)
+    Ah = gA.randn(mL, nL) @ np.diag(np.logspace(0, 3, nL))
+    Bh = Ah @ gA.randn(nL, nr) + 1e-3 * gA.randn(mL, nr)
+    Ad = torch.from_numpy(Ah).to(dev)
+    Bd = torch.from_numpy(Bh).to(dev)
+    _, hA, _ = dwrap("DistMatrix_VC_STAR", Ad, mL, nL)
+    _, hB, _ = dwrap("DistMatrix_VC_STAR", Bd, mL, nr)
+    Xd, hX, _ = dwrap("SharedMatrix", None, nL, nr)
+    lib.sl_faster_least_squares.argtypes = [C.c_int, C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp]
+    c4 = vp()
+    assert lib.sl_create_default_context(55, C.byref(c4)) == 0
+    lsp = b'{"tolerance": 1e-14, "iter_lim": 200}'
+    assert lib.sl_faster_least_squares(0, b"DistMatrix_VC_STAR", hA, b"DistMatrix_VC_STAR", hB, b"SharedMatrix", hX,
+                                       lsp, c4) == 0, err()
+    torch.cuda.synchronize()
+    Af, Bf, Xf = np.asfortranarray(Ah), np.asfortranarray(Bh), np.zeros((nL, nr), order="F")
+    wA, wB, wX = vp(), vp(), vp()
+    lib.sl_wrap_raw_matrix.argtypes = [vp, C.c_int, C.c_int, C.POINTER(vp)]
+    lib.sl_wrap_raw_matrix(Af.ctypes.data, mL, nL, C.byref(wA))
+    lib.sl_wrap_raw_matrix(Bf.ctypes.data, mL, nr, C.byref(wB))
+    lib.sl_wrap_raw_matrix(Xf.ctypes.data, nL, nr, C.byref(wX))
+    c5 = vp()
+    assert lib.sl_create_default_context(55, C.byref(c5)) == 0
+    assert lib.sl_faster_least_squares(0, b"Matrix", wA, b"Matrix", wB, b"Matrix", wX, lsp, c5) == 0, err()
+    Xls = np.linalg.lstsq(Ah, Bh, rcond=None)[0]
+    xd = Xd.cpu().numpy()
+    ls = (np.abs(xd - Xf).max() / np.abs(Xf).max(), np.abs(xd - Xls).max() / np.abs(Xls).max())
     lib.sl_runtime_started.restype = C.c_int
-    return worst, mcmr, svd, kdiff, lib.sl_runtime_started()
+    return worst, mcmr, svd, kdiff, ls, lib.sl_runtime_started()
 
 
 def test_capi_dist_matrix_world2():
     from mp_utils import run_distributed
     res = run_distributed(_worker, 2, timeout=300)
-    for worst, mcmr, svd, kdiff, started in res:
+    for worst, mcmr, svd, kdiff, ls, started in res:
         assert len(worst) >= len(TYPES) * 4
         bad = {k: v for k, v in worst.items() if v > 1e-12}
         assert not bad, bad
@@ -191,4 +224,5 @@ def test_capi_dist_matrix_world2():
         s_rel, v_diff, u_diff = svd
         assert s_rel < 2e-5 and v_diff < 2e-4 and u_diff < 2e-4, svd
         assert kdiff < 1e-13
+        assert ls[0] < 1e-9 and ls[1] < 1e-8, ls   # vs the one-rank call, vs numpy lstsq
         assert started == 0   # no call above started the interpreter-side runtime
