@@ -110,6 +110,8 @@ struct Lib {
   // host-operand NLA drivers (nla_native.hip) and the LIBSVM reader (libsvm_io.cpp)
   int (*sym_rsvd)(const double*, int64_t, int64_t, int, int, int, int, int, uint64_t, uint64_t, double*, int64_t,
                   double*, void*) = nullptr;
+  int (*sym_rsvd_comm)(const double*, int64_t, int64_t, int64_t, int64_t, int, int, int, int, int, uint64_t, uint64_t,
+                       double*, int64_t, double*, void*, void*) = nullptr;
   int (*blendenpik)(const double*, int64_t, int64_t, int64_t, const double*, int, int64_t, double*, int64_t, uint64_t,
                     uint64_t*, double, int, int*, void*) = nullptr;
   int (*blendenpik_comm)(const double*, int64_t, int64_t, int64_t, const double*, int, int64_t, double*, int64_t,
@@ -186,7 +188,8 @@ inline Lib& lib() {
               bind(L.h, "sl_rsvd_gen_set_dense", L.gen_set_dense, L.err) &&
               bind(L.h, "sl_rsvd_gen_set_z", L.gen_set_z, L.err) && bind(L.h, "sl_rsvd_gen_run", L.gen_run, L.err) &&
               bind(L.h, "sl_rsvd_gen_status", L.gen_status, L.err) &&
-              bind(L.h, "sl_nat_sym_rsvd", L.sym_rsvd, L.err) && bind(L.h, "sl_nat_blendenpik", L.blendenpik, L.err) &&
+              bind(L.h, "sl_nat_sym_rsvd", L.sym_rsvd, L.err) &&
+              bind(L.h, "sl_nat_sym_rsvd_comm", L.sym_rsvd_comm, L.err) && bind(L.h, "sl_nat_blendenpik", L.blendenpik, L.err) &&
               bind(L.h, "sl_nat_blendenpik_comm", L.blendenpik_comm, L.err) &&
               bind(L.h, "sl_libsvm_scan", L.libsvm_scan, L.err) && bind(L.h, "sl_libsvm_fill", L.libsvm_fill, L.err);
     if (!ok) return;
@@ -1085,6 +1088,42 @@ inline int faster_least_squares_host(int orientation, const double* A, int64_t m
                          &ctr, tol, iter_lim, &code, nullptr),
             "faster least squares");
   SLDEV_TRY(L.dev_memcpy(X, dX.p, xm * xn * 8, 1, nullptr), "copy");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
+// ApproximateSymmetricSVD of a DistMatrix A ([VC,*] / [VR,*] f64 rows of the
+// symmetric n x n A, lower triangle read as the reference's El::LOWER): S
+// (rank) replicated, V (n x rank) replicated ([*,*]) or in A's rows
+// (sl_nat_sym_rsvd_comm: one n x k all-reduce per application of A).
+inline int approximate_symmetric_svd_dist(const DistMat& A, const DistMat& Sv, int v_ly, const DistMat& V, int rank,
+                                          const char* params, uint64_t seed, uint64_t& ctr) {
+  Lib& L = lib();
+  if (!L.loaded) return fail(106, "device C API: " + L.err);
+  if (A.dtype != F64 || Sv.dtype != F64 || V.dtype != F64) return fail(103, "approximate_symmetric_svd: f64 operands");
+  if (Sv.comm != A.comm || V.comm != A.comm) return fail(109, "approximate_symmetric_svd: operands on different communicators");
+  const int64_t n = A.n;
+  if (A.m != n) return fail(109, "approximate_symmetric_svd: matrix is not square -- symmetric matrix required");
+  if (rank < 1 || rank > n) return fail(109, "approximate_symmetric_svd: incompatible matrix dimensions and rank");
+  if (V.m != n || V.n != rank || Sv.m * Sv.n != rank) return fail(104, "approximate_symmetric_svd: output shapes");
+  const SvdParams p = parse_svd_params(params);
+  const int k = (int)std::max<int64_t>(rank, std::min<int64_t>(n, (int64_t)p.ratio * rank + p.additive));
+  int rnk = 0, size = 1;
+  int rc = comm_rank_size(A.comm, &rnk, &size);
+  if (rc) return rc;
+  int64_t r0, c0, lm, ln;
+  shard_of(LY_ROWS, n, n, rnk, size, &r0, &c0, &lm, &ln);
+  Buf Vc(n * rank * 8), Vr(n * rank * 8);
+  if (!Vc.p || !Vr.p) return fail(101, "approximate_symmetric_svd: device allocation failed");
+  SLDEV_TRY(L.sym_rsvd_comm((const double*)A.data, lm, n, A.ld, r0, 1, k, rank, std::max(0, p.iters),
+                            p.skip_qr ? 1 : 0, seed, ctr, (double*)Vc.p, n, (double*)Sv.data, A.comm, nullptr),
+            "symmetric randSVD");
+  ctr += (uint64_t)(n * k);
+  // V row-major (n x rank) = the transpose of the column-major result, then this rank's part
+  SLDEV_TRY(L.transpose(Vc.p, F64, rank, n, n, Vr.p, rank, nullptr), "transpose");
+  int64_t vr0, vc0, vlm, vln;
+  shard_of(v_ly, n, rank, rnk, size, &vr0, &vc0, &vlm, &vln);
+  rc = copy_block(DevMat{Vr.p, F64, n, rank, rank}, vr0, vc0, DevMat{V.data, F64, vlm, vln, V.ld}, 0, 0, vlm, vln);
+  if (rc) return rc;
   return check(L.dev_sync(nullptr), "sync");
 }
 

@@ -18,8 +18,9 @@
 //    SharedMatrix, RootMatrix; sl_wrap_raw_dist_device_matrix) in
 //    sl_apply_sketch_transform (every sketch type: the ranks' column ranges
 //    of the operator summed by all-reduce), sl_approximate_svd ([VC,*] A),
-//    sl_faster_least_squares ([VC,*] A and B) and sl_kernel_gram (points
-//    split over the ranks) -- no interpreter.  The
+//    sl_approximate_symmetric_svd ([VC,*] A), sl_faster_least_squares
+//    ([VC,*] A and B) and sl_kernel_gram (points split over the ranks) -- no
+//    interpreter.  The
 //    2-D [MC,MR] "DistMatrix" has no native path.
 // Everything else (runtime-only kernels, the remaining entry points) goes
 // through the Python/HIP runtime
@@ -966,6 +967,21 @@ SL_CAPI int sl_approximate_svd(char* A_type, void* A, char* U_type, void* U, cha
 
 SL_CAPI int sl_approximate_symmetric_svd(char* A_type, void* A, char* S_type, void* Sv, char* V_type, void* V,
                                          uint16_t k, char* params, sl_context_t* ctxt) {
+  int la, lv;
+  if (const int e = dist_pair("sl_approximate_symmetric_svd", A_type, V_type, &la, &lv)) return e;
+  if (la >= 0) {
+    if (la != sldev::LY_ROWS || dist_layout(S_type) != sldev::LY_STAR || (lv != sldev::LY_STAR && lv != sldev::LY_ROWS)) {
+      g_last_error = "sl_approximate_symmetric_svd: distributed A must be DistMatrix_VC_STAR / _VR_STAR, S "
+                     "SharedMatrix, V SharedMatrix or A's layout";
+      return 103;
+    }
+    uint64_t ctr = ctxt->counter;
+    const int rc = sldev::approximate_symmetric_svd_dist(distmat(A), distmat(Sv), lv, distmat(V), (int)k, params,
+                                                         ctxt->seed, ctr);
+    if (rc) return native_fail(rc);
+    ctxt->counter = ctr;
+    return 0;
+  }
   if (!strcmp(A_type, "Matrix") && !strcmp(S_type, "Matrix") && !strcmp(V_type, "Matrix") && sldev::device_present()) {
     auto *a = (sl_raw_matrix_t*)A, *sv = (sl_raw_matrix_t*)Sv, *v = (sl_raw_matrix_t*)V;
     if (a->m != a->n) {

@@ -179,6 +179,102 @@ SL_API int sl_nat_sym_rsvd(const double* A, int64_t n, int64_t lda, int lower, i
 
 namespace {
 
+// T (m x n row-major, ld n) = the stored triangle of this rank's rows [r0, r0
+// + m) of a symmetric A (row-major shard R, ld ldr): lower keeps columns j <=
+// r0 + i, upper j >= r0 + i
+__global__ void k_tri_rows(const double* __restrict__ R, int64_t ldr, int64_t m, int64_t n, int64_t r0, int lower,
+                           double* __restrict__ T) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m * n; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / n, j = t - i * n;
+    const bool keep = lower ? j <= r0 + i : j >= r0 + i;
+    T[t] = keep ? R[i * ldr + j] : 0.0;
+  }
+}
+
+// F (n x k col-major) rows r0 .. r0 + m += P (m x k col-major) - diag(T) X rows
+__global__ void k_fold_rows(double* __restrict__ F, int64_t n, int64_t m, int k, int64_t r0,
+                            const double* __restrict__ P, const double* __restrict__ T, const double* __restrict__ X) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m * k; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t % m, c = t / m;
+    const int64_t g = r0 + i;
+    F[g + c * n] += P[i + c * m] - T[i * n + g] * X[g + c * n];
+  }
+}
+
+}  // namespace
+
+// ApproximateSymmetricSVD of a row-distributed symmetric A: this rank holds
+// rows [r0, r0 + m) of the n x n A (row-major shard, ld ldr), only its lower
+// (1) / upper (0) triangle read.  A X = L X + L^T X - D X over the stored
+// triangle L: each rank forms its rows of L X - D X and its partial L^T X,
+// and ONE n x k all-reduce per application of A gives A X on every rank; the
+// orthonormalisation, the k x k Rayleigh-Ritz and V (n x rank, col-major,
+// ldv) / s are replicated.  Same operator stream as sl_nat_sym_rsvd (the
+// same Omega at base), so one rank reproduces the host-operand call.
+SL_API int sl_nat_sym_rsvd_comm(const double* R, int64_t m, int64_t n, int64_t ldr, int64_t r0, int lower, int k,
+                                int rank, int iters, int skip_qr, uint64_t seed, uint64_t base, double* V, int64_t ldv,
+                                double* s_out, void* comm, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n < 1 || k < rank || rank < 1 || k > n || m < 0 || r0 < 0 || r0 + m > n) {
+    sl_set_last_error("sym_rsvd: needs 1 <= rank <= k <= n and a row range inside n");
+    return SL_ERR_INVALID;
+  }
+  if (!slb_solver_available()) {
+    sl_set_last_error("sym_rsvd: rocBLAS / rocSOLVER not available");
+    return SL_ERR_UNSUPPORTED;
+  }
+  DevBuf T(sizeof(double) * std::max<int64_t>(1, m * n)), X(sizeof(double) * n * k), Y(sizeof(double) * n * k),
+      P(sizeof(double) * std::max<int64_t>(1, m * k)), tau(sizeof(double) * k), Bk(sizeof(double) * k * k),
+      w(sizeof(double) * k), E(sizeof(double) * k), T2(sizeof(double) * n * rank), info(sizeof(int) * 4);
+  if (!T.p || !X.p || !Y.p || !P.p || !tau.p || !Bk.p || !w.p || !E.p || !T2.p || !info.p) {
+    sl_set_last_error("sym_rsvd: device allocation failed");
+    return SL_ERR_HIP;
+  }
+  if (m > 0) {
+    k_tri_rows<<<grid_of(m * n), 256, 0, s>>>(R, ldr, m, n, r0, lower, T.d());
+    SL_LAUNCH_CHECK();
+  }
+  // out (n x k col-major, every rank) = A in (n x k col-major, every rank)
+  auto apply = [&](const double* in, double* out) -> int {
+    if (m > 0) {
+      NAT_TRY(gemm_cm(true, false, m, k, n, T.d(), n, in, n, 0.0, P.d(), m, s));        // rows of L X
+      NAT_TRY(gemm_cm(false, false, n, k, m, T.d(), n, in + r0, n, 0.0, out, n, s));     // partial L^T X
+      k_fold_rows<<<grid_of(m * k), 256, 0, s>>>(out, n, m, k, r0, P.d(), T.d(), in);
+      SL_LAUNCH_CHECK();
+    } else {
+      SL_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(double) * n * k, s));
+    }
+    if (!comm) return SL_OK;
+    return sl_comm_all_reduce(comm, out, out, n * k, SL_F64, 0, s);
+  };
+  NAT_TRY(sl_fill_random(X.p, SL_F64, sl::DIST_NORMAL, seed, base, n, k, 1, n, 0, 0, 1, n, 0.0, 0.0, 1.0, 1, s));
+  NAT_TRY(apply(X.d(), Y.d()));                                                          // Y = A Omega
+  for (int it = 0; it < iters; ++it) {
+    if (!skip_qr) NAT_TRY(orth_inplace(Y.d(), n, k, tau.d(), s));
+    NAT_TRY(apply(Y.d(), X.d()));
+    std::swap(X.p, Y.p);
+  }
+  NAT_TRY(orth_inplace(Y.d(), n, k, tau.d(), s));                                        // Q
+  NAT_TRY(apply(Y.d(), X.d()));                                                          // U = A Q
+  NAT_TRY(gemm_cm(true, false, k, k, n, Y.d(), n, X.d(), n, 0.0, Bk.d(), k, s));         // B = Q^T U
+  k_sym_avg<<<grid_of((int64_t)k * k), 256, 0, s>>>(Bk.d(), k);
+  SL_LAUNCH_CHECK();
+  NAT_TRY(slb_dsyevd(k, Bk.d(), k, w.d(), E.d(), (int*)info.p, s));
+  NAT_TRY(gemm_cm(false, false, n, rank, k, Y.d(), n, Bk.d() + (int64_t)(k - rank) * k, k, 0.0, T2.d(), n, s));
+  k_reverse_cols<<<grid_of(n * rank), 256, 0, s>>>(T2.d(), n, rank, V, ldv, w.d(), k, s_out);
+  SL_LAUNCH_CHECK();
+  int hinfo = 0;
+  SL_HIP_CHECK(hipMemcpyAsync(&hinfo, info.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  SL_HIP_CHECK(hipStreamSynchronize(s));
+  if (hinfo != 0) {
+    sl_set_last_error("sym_rsvd: syevd did not converge");
+    return SL_ERR_GENERIC;
+  }
+  return SL_OK;
+}
+
+namespace {
+
 // Row distribution of the least-squares operand: this rank holds rows
 // [r0, r0 + m) of the mg-row A and B; comm (sl_comm_*) sums over the ranks,
 // null = one rank.  Every n-vector / n x n quantity is replicated and, the

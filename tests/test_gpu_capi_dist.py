@@ -6,7 +6,8 @@ DistMatrix_STAR_VC, SharedMatrix, RootMatrix), the sums going through a
 callback communicator (sl_device_comm_from_allreduce) that all-reduces over
 this test's gloo group -- the same code an RCCL communicator drives across
 GPUs.  Covers sketch application (8 layout cases x 7 sketch types),
-randSVD ([VC,*] A), kernel Grams and FasterLeastSquares ([VC,*] A and B).
+randSVD and symmetric randSVD ([VC,*] A), kernel Grams and
+FasterLeastSquares ([VC,*] A and B).
 Oracle: the single-rank call of the same C ABI on the whole operand
 (DeviceMatrix; host "Matrix" for least squares, plus numpy lstsq) -- the
 reference's distributed == local invariant
@@ -209,14 +210,49 @@ def _worker(rank, world):
     Xls = np.linalg.lstsq(Ah, Bh, rcond=None)[0]
     xd = Xd.cpu().numpy()
     ls = (np.abs(xd - Xf).max() / np.abs(Xf).max(), np.abs(xd - Xls).max() / np.abs(Xls).max())
+    # symmetric randSVD of a row-distributed symmetric A (lower triangle read;
+    # garbage above it) vs the one-rank host-operand call on the same stream
+    ns, rs = 400, 6
+    gS = np.random.RandomState(9)
+    Qs = np.linalg.qr(gS.randn(ns, ns))[0]
+    Sym = (Qs * np.concatenate([50.0 * 0.7 ** np.arange(20), 1e-3 * gS.rand(ns - 20)])) @ Qs.T
+    Sym = (Sym + Sym.T) / 2
+    Sg = np.tril(Sym) + np.triu(gS.randn(ns, ns), 1)   # only the lower triangle is valid
+    Sd = torch.from_numpy(Sg).to(dev)
+    _, hS, _ = dwrap("DistMatrix_VC_STAR", Sd, ns, ns)
+    sd, hs_, _ = dwrap("SharedMatrix", None, rs, 1)
+    Vsd, hv, (vr0, _, vlm, _) = dwrap("DistMatrix_VC_STAR", None, ns, rs)
+    lib.sl_approximate_symmetric_svd.argtypes = [C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_uint16,
+                                                 C.c_char_p, vp]
+    c6 = vp()
+    assert lib.sl_create_default_context(66, C.byref(c6)) == 0
+    sprm = b'{"num_iterations": 2}'
+    assert lib.sl_approximate_symmetric_svd(b"DistMatrix_VC_STAR", hS, b"SharedMatrix", hs_, b"DistMatrix_VC_STAR", hv,
+                                            rs, sprm, c6) == 0, err()
+    torch.cuda.synchronize()
+    Sf = np.asfortranarray(Sg)
+    sh, Vh = np.zeros((rs, 1), order="F"), np.zeros((ns, rs), order="F")
+    w1, w2, w3 = vp(), vp(), vp()
+    lib.sl_wrap_raw_matrix(Sf.ctypes.data, ns, ns, C.byref(w1))
+    lib.sl_wrap_raw_matrix(sh.ctypes.data, rs, 1, C.byref(w2))
+    lib.sl_wrap_raw_matrix(Vh.ctypes.data, ns, rs, C.byref(w3))
+    c7 = vp()
+    assert lib.sl_create_default_context(66, C.byref(c7)) == 0
+    assert lib.sl_approximate_symmetric_svd(b"Matrix", w1, b"Matrix", w2, b"Matrix", w3, rs, sprm, c7) == 0, err()
+    s_d = sd.cpu().numpy().ravel()
+    Vl = Vsd[:vlm].cpu().numpy()
+    Vref = Vh[vr0:vr0 + vlm]
+    sgn = np.sign(np.sum(Vl * Vref, axis=0))
+    sym = (np.abs(s_d - sh.ravel()).max() / np.abs(sh).max(), np.abs(Vl * sgn - Vref).max(),
+           np.abs(s_d - np.linalg.eigvalsh(Sym)[::-1][:rs]).max() / 50.0)
     lib.sl_runtime_started.restype = C.c_int
-    return worst, mcmr, svd, kdiff, ls, lib.sl_runtime_started()
+    return worst, mcmr, svd, kdiff, ls, sym, lib.sl_runtime_started()
 
 
 def test_capi_dist_matrix_world2():
     from mp_utils import run_distributed
     res = run_distributed(_worker, 2, timeout=300)
-    for worst, mcmr, svd, kdiff, ls, started in res:
+    for worst, mcmr, svd, kdiff, ls, sym, started in res:
         assert len(worst) >= len(TYPES) * 4
         bad = {k: v for k, v in worst.items() if v > 1e-12}
         assert not bad, bad
@@ -225,4 +261,5 @@ def test_capi_dist_matrix_world2():
         assert s_rel < 2e-5 and v_diff < 2e-4 and u_diff < 2e-4, svd
         assert kdiff < 1e-13
         assert ls[0] < 1e-9 and ls[1] < 1e-8, ls   # vs the one-rank call, vs numpy lstsq
+        assert sym[0] < 1e-10 and sym[1] < 1e-8 and sym[2] < 1e-6, sym
         assert started == 0   # no call above started the interpreter-side runtime
