@@ -104,6 +104,11 @@ class _Data:
 
 
 SPLIT_GRAM_ROWS = 8192   # rows per f32-accumulated chunk of the split Gram
+# row blocks of the split Gram's block-upper-triangle form (1: the full s x s
+# products, the default); env SKH_KRR_GRAM_BLOCKS for A/Bs -- 2 / 4 / 8 blocks
+# cut the flops to 75 / 62 / 56% but ran 0.193 / 0.243 / 0.336 s against 0.190
+# (profiles/r6/krr_gram_blocks_ab.jsonl: the narrower products run far slower)
+SPLIT_GRAM_BLOCKS = int(os.environ.get("SKH_KRR_GRAM_BLOCKS", "1"))
 
 
 def _split3(Zc: torch.Tensor):
@@ -144,13 +149,29 @@ def _gram_split(Z: torch.Tensor, G: torch.Tensor) -> None:
     seg = -(-min(R, n) // 64) * 64
     S = torch.empty(s, 5 * seg, dtype=torch.bfloat16, device=Z.device)
     st = C.c_void_p(_lib.stream_of(Z))
+    # both window products are symmetric: with nb > 1 only the block upper
+    # triangle (row block b against columns b.. of the s x s result) is
+    # formed, (nb + 1) / 2nb of the flops, and mirrored once at the end
+    nb = SPLIT_GRAM_BLOCKS if s % SPLIT_GRAM_BLOCKS == 0 and (s // SPLIT_GRAM_BLOCKS) % 64 == 0 else 1
+    bs = s // nb
+    Gu = torch.zeros_like(G) if nb > 1 else G
     for r0 in range(0, n, R):
         w = min(R, n - r0)
         _lib.call("sl_split3_bf16_t", _lib.ptr(Z[r0:]), w, s, Z.stride(0), _lib.ptr(S), seg, 5 * seg, st)
         A = S[:, seg:3 * seg]
-        Cm = torch.mm(A, A.t(), out_dtype=torch.float32)
-        Cm += torch.mm(S[:, seg:5 * seg], S[:, :4 * seg].t(), out_dtype=torch.float32)
-        G += Cm.double()
+        B1, B2 = S[:, seg:5 * seg], S[:, :4 * seg]
+        if nb == 1:
+            Cm = torch.mm(A, A.t(), out_dtype=torch.float32)
+            Cm += torch.mm(B1, B2.t(), out_dtype=torch.float32)
+            G += Cm.double()
+            continue
+        for b in range(nb):
+            rb, cb = slice(b * bs, (b + 1) * bs), slice(b * bs, s)
+            Cm = torch.mm(A[rb], A[cb].t(), out_dtype=torch.float32)
+            Cm += torch.mm(B1[rb], B2[cb].t(), out_dtype=torch.float32)
+            Gu[rb, cb] += Cm.double()
+    if nb > 1:
+        G += torch.triu(Gu) + torch.triu(Gu, 1).t()
 
 
 def _ridge(Z: torch.Tensor, Y: torch.Tensor, lam: float, data: _Data | None = None) -> torch.Tensor:

@@ -201,14 +201,18 @@ def test_feature_map_precond_f32_apply_matches_f64(dev):
     assert float((A32 - A64).norm() / A64.norm()) < 1e-4
 
 
+@pytest.mark.parametrize("blocks", [1, 4])
 @pytest.mark.parametrize("n,s", [(20000, 512), (9000, 300), (777, 64)])
-def test_krr_split_gram_matches_fp64(dev, n, s, monkeypatch):
+def test_krr_split_gram_matches_fp64(dev, n, s, blocks, monkeypatch):
     """Z^T Z of f32 features from the exact three-plane bf16 split (gemm_nt.hip
     k_split3_t + two NT GEMMs per row chunk, f32 sums per chunk, f64 across)
     against the fp64 product, ragged last chunk included (reference
-    ml/krr.hpp:94-196 forms Z^T Z in the features' precision)."""
+    ml/krr.hpp:94-196 forms Z^T Z in the features' precision); blocks > 1:
+    the block-upper-triangle products mirrored (s = 512 only; the others fall
+    back to the full products)."""
     from libskylark_amd.ml import krr as K
     monkeypatch.setattr(K, "SPLIT_GRAM_ROWS", 4096)
+    monkeypatch.setattr(K, "SPLIT_GRAM_BLOCKS", blocks)
     g = torch.Generator(device=dev).manual_seed(n)
     Z = torch.cos(torch.randn(n, s, generator=g, device=dev) * 3.0) * (2.0 / s) ** 0.5
     G = torch.zeros(s, s, dtype=torch.float64, device=dev)
