@@ -19,8 +19,8 @@
 //    sl_apply_sketch_transform (every sketch type: the ranks' column ranges
 //    of the operator summed by all-reduce), sl_approximate_svd ([VC,*] A),
 //    sl_approximate_symmetric_svd ([VC,*] A), sl_faster_least_squares
-//    ([VC,*] A and B) and sl_kernel_gram (points split over the ranks) -- no
-//    interpreter.  The
+//    ([VC,*] A and B), sl_kernel_gram (points split over the ranks) and
+//    sl_readlibsvm (each rank's examples) -- no interpreter.  The
 //    2-D [MC,MR] "DistMatrix" has no native path.
 // Everything else (runtime-only kernels, the remaining entry points) goes
 // through the Python/HIP runtime
@@ -1202,6 +1202,62 @@ SL_CAPI int sl_kernel_gram(int dirX, int dirY, sl_kernel_t* k, char* X_type, voi
 // ---------------------------------------------------------------------- IO
 SL_CAPI int sl_readlibsvm(char* fname, char* X_type, void* X, char* Y_type, void* Y, int direction, int min_d,
                           int max_n) {
+  int lx, ly;
+  if (const int e = dist_pair("sl_readlibsvm", X_type, Y ? Y_type : X_type, &lx, &ly)) return e;
+  if (lx >= 0) {
+    // DistMatrix X (f64 device shards): examples as rows split [VC,*] (direction
+    // rows: n x d) or as columns split [*,VC] (SL_COLUMNS: d x n); Y (labels,
+    // n x 1 / 1 x n) in the matching layout or replicated.  Every rank parses
+    // the file and uploads its own examples.
+    const bool cols = direction == 1;
+    const int want = cols ? sldev::LY_COLS : sldev::LY_ROWS;
+    if (lx != want || (Y && ly != want && ly != sldev::LY_STAR)) {
+      g_last_error = "sl_readlibsvm: distributed X must be DistMatrix_VC_STAR (examples as rows) or DistMatrix_STAR_VC "
+                     "(SL_COLUMNS), Y in the same layout or SharedMatrix";
+      return 103;
+    }
+    sldev::Libsvm L;
+    int rc = sldev::read_libsvm(fname, min_d, max_n, L);
+    if (rc) return native_fail(rc);
+    const sldev::DistMat& x = distmat(X);
+    const int64_t n = L.rows, d = L.d;
+    if (x.dtype != sldev::F64 || x.m != (cols ? d : n) || x.n != (cols ? n : d)) {
+      g_last_error = "sl_readlibsvm: X wrap has the wrong global shape or dtype (f64)";
+      return 109;
+    }
+    int rank = 0, size = 1;
+    if ((rc = sldev::comm_rank_size(x.comm, &rank, &size))) return native_fail(rc);
+    int64_t r0, c0, lm, ln;
+    sldev::shard_of(lx, x.m, x.n, rank, size, &r0, &c0, &lm, &ln);
+    const int64_t e0 = cols ? c0 : r0, ne = cols ? ln : lm;   // this rank's examples
+    std::vector<double> h((size_t)std::max<int64_t>(1, lm * ln), 0.0);
+    for (int64_t i = e0; i < e0 + ne; ++i)
+      for (int64_t q = L.rowptr[(size_t)i]; q < L.rowptr[(size_t)i + 1]; ++q) {
+        const int64_t j = L.cols[(size_t)q];
+        h[(size_t)(cols ? j * ln + (i - e0) : (i - e0) * ln + j)] += L.vals[(size_t)q];
+      }
+    sldev::Lib& Lb = sldev::lib();
+    if (lm * ln > 0 &&
+        (rc = sldev::check(Lb.dev_memcpy2d(x.data, x.ld * 8, h.data(), ln * 8, ln * 8, lm, 0, nullptr), "copy")))
+      return native_fail(rc);
+    if (Y) {
+      const sldev::DistMat& y = distmat(Y);
+      if (y.dtype != sldev::F64 || y.m != (cols ? 1 : n) || y.n != (cols ? n : 1) || y.comm != x.comm) {
+        g_last_error = "sl_readlibsvm: Y wrap has the wrong global shape, dtype (f64) or communicator";
+        return 109;
+      }
+      int64_t yr0, yc0, ylm, yln;
+      sldev::shard_of(ly, y.m, y.n, rank, size, &yr0, &yc0, &ylm, &yln);
+      const int64_t y0 = cols ? yc0 : yr0, ny = ylm * yln;   // the labels of this shard, in example order
+      if (ny > 0) {
+        // a column of labels is strided by ld, a row contiguous
+        if (cols) rc = sldev::check(Lb.dev_memcpy(y.data, L.labels.data() + y0, ny * 8, 0, nullptr), "copy");
+        else rc = sldev::check(Lb.dev_memcpy2d(y.data, y.ld * 8, L.labels.data() + y0, 8, 8, ny, 0, nullptr), "copy");
+        if (rc) return native_fail(rc);
+      }
+    }
+    return 0;
+  }
   const bool xd = !strcmp(X_type, "Matrix"), xs = !strcmp(X_type, "SparseMatrix");
   if ((xd || xs) && (!Y || !strcmp(Y_type, "Matrix")) && sldev::lib().loaded) {
     // native LIBSVM reader (libsvm_io.cpp): examples are columns (direction

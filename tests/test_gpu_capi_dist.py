@@ -6,8 +6,8 @@ DistMatrix_STAR_VC, SharedMatrix, RootMatrix), the sums going through a
 callback communicator (sl_device_comm_from_allreduce) that all-reduces over
 this test's gloo group -- the same code an RCCL communicator drives across
 GPUs.  Covers sketch application (8 layout cases x 7 sketch types),
-randSVD and symmetric randSVD ([VC,*] A), kernel Grams and
-FasterLeastSquares ([VC,*] A and B).
+randSVD and symmetric randSVD ([VC,*] A), kernel Grams, FasterLeastSquares
+([VC,*] A and B) and the LIBSVM reader ([VC,*] / [*,VC] examples).
 Oracle: the single-rank call of the same C ABI on the whole operand
 (DeviceMatrix; host "Matrix" for least squares, plus numpy lstsq) -- the
 reference's distributed == local invariant
@@ -245,14 +245,43 @@ def _worker(rank, world):
     sgn = np.sign(np.sum(Vl * Vref, axis=0))
     sym = (np.abs(s_d - sh.ravel()).max() / np.abs(sh).max(), np.abs(Vl * sgn - Vref).max(),
            np.abs(s_d - np.linalg.eigvalsh(Sym)[::-1][:rs]).max() / 50.0)
+    # LIBSVM into [VC,*] shards (examples as rows) and [*,VC] (SL_COLUMNS)
+    # against the host-operand read of the same file
+    import os
+    import tempfile
+    gL = np.random.RandomState(10)
+    path = os.path.join(tempfile.gettempdir(), f"sl_dist_{os.getpid()}.libsvm")
+    with open(path, "w") as f:
+        for i in range(37):
+            feats = sorted(gL.choice(12, size=gL.randint(1, 6), replace=False))
+            f.write(f"{i % 3} " + " ".join(f"{j + 1}:{gL.rand():.6f}" for j in feats) + "\n")
+    Xh = np.zeros((37, 12), order="F")
+    Yh = np.zeros((37, 1), order="F")
+    wx1, wy1 = vp(), vp()
+    lib.sl_wrap_raw_matrix(Xh.ctypes.data, 37, 12, C.byref(wx1))
+    lib.sl_wrap_raw_matrix(Yh.ctypes.data, 37, 1, C.byref(wy1))
+    lib.sl_readlibsvm.argtypes = [C.c_char_p, C.c_char_p, vp, C.c_char_p, vp, C.c_int, C.c_int, C.c_int]
+    assert lib.sl_readlibsvm(path.encode(), b"Matrix", wx1, b"Matrix", wy1, 2, 0, -1) == 0, err()
+    io = 0.0
+    for direction, xt, xshape, yt, yshape in ((2, "DistMatrix_VC_STAR", (37, 12), "DistMatrix_VC_STAR", (37, 1)),
+                                              (1, "DistMatrix_STAR_VC", (12, 37), "SharedMatrix", (1, 37))):
+        Xl, hx2, (xr0, xc0, xlm, xln) = dwrap(xt, None, *xshape)
+        Yl, hy2, (yr0, yc0, ylm, yln) = dwrap(yt, None, *yshape)
+        assert lib.sl_readlibsvm(path.encode(), xt.encode(), hx2, yt.encode(), hy2, direction, 0, -1) == 0, err()
+        torch.cuda.synchronize()
+        Xr = Xh if direction == 2 else Xh.T
+        Yr = Yh if direction == 2 else Yh.T
+        io = max(io, np.abs(Xl[:xlm, :xln].cpu().numpy() - Xr[xr0:xr0 + xlm, xc0:xc0 + xln]).max(),
+                 np.abs(Yl[:ylm, :yln].cpu().numpy() - Yr[yr0:yr0 + ylm, yc0:yc0 + yln]).max())
+    os.remove(path)
     lib.sl_runtime_started.restype = C.c_int
-    return worst, mcmr, svd, kdiff, ls, sym, lib.sl_runtime_started()
+    return worst, mcmr, svd, kdiff, ls, sym, io, lib.sl_runtime_started()
 
 
 def test_capi_dist_matrix_world2():
     from mp_utils import run_distributed
     res = run_distributed(_worker, 2, timeout=300)
-    for worst, mcmr, svd, kdiff, ls, sym, started in res:
+    for worst, mcmr, svd, kdiff, ls, sym, io, started in res:
         assert len(worst) >= len(TYPES) * 4
         bad = {k: v for k, v in worst.items() if v > 1e-12}
         assert not bad, bad
@@ -262,4 +291,5 @@ def test_capi_dist_matrix_world2():
         assert kdiff < 1e-13
         assert ls[0] < 1e-9 and ls[1] < 1e-8, ls   # vs the one-rank call, vs numpy lstsq
         assert sym[0] < 1e-10 and sym[1] < 1e-8 and sym[2] < 1e-6, sym
+        assert io == 0.0
         assert started == 0   # no call above started the interpreter-side runtime
