@@ -56,6 +56,12 @@ k_csr_panel(const int64_t* __restrict__ rowptr, const IT* __restrict__ col, cons
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (c[e] >= c1) { v[e] = (T)0; c[e] = c0; done = true; }
+      // every panel load issued unconditionally (clamped column, then zeroed):
+      // `j < S ? pr[j] : 0` compiled to one exec-masked branch per load, each
+      // waiting for its own load (same-box A/B: rowwise 10.5 -> 10.15 ms,
+      // profiles/r6/csr_panel_loads_ab.jsonl; eight nonzeros per step with a
+      // masked tail measured slower, 11.6 ms -- the panel gathers, ~1 KB per
+      // nonzero from the Infinity Cache, are the bound, not load latency)
       T p[4][U];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -63,9 +69,18 @@ k_csr_panel(const int64_t* __restrict__ rowptr, const IT* __restrict__ col, cons
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int j = gl + LPR * u;
-          p[e][u] = j < S ? pr[j] : (T)0;
+          p[e][u] = pr[j < S ? j : 0];
         }
       }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < U; ++u) asm volatile("" : "+v"(p[e][u]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (gl + LPR * u >= S) p[e][u] = (T)0;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -76,11 +91,17 @@ k_csr_panel(const int64_t* __restrict__ rowptr, const IT* __restrict__ col, cons
       if (c >= c1) break;
       const T v = vals[q];
       const T* pr = P + (c - c0) * ldp;
+      T p1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int j = gl + LPR * u;
-        if (j < S) acc[u] += v * pr[j];
+        p1[u] = pr[j < S ? j : 0];
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) asm volatile("" : "+v"(p1[u]));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (gl + LPR * u < S) acc[u] += v * p1[u];
     }
     T* yr = Y + row * ldy;
 #pragma unroll
