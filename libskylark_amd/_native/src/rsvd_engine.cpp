@@ -110,6 +110,18 @@ int pass_nt_code() {
   return c;
 }
 
+// the same policy for the FINAL pass alone (env SL_PASS_NT_FINAL, A/B): its
+// A reads not allocated in the MALL, so the Y it writes may stay there for U = Y M
+int pass_nt_final_code() {
+  static int c = -1;
+  if (c < 0) {
+    const char* e = std::getenv("SL_PASS_NT_FINAL");
+    c = e ? (std::atoi(e) & 7) : -1;
+    if (c < 0) c = 8;   // unset: the all-pass policy
+  }
+  return c == 8 ? pass_nt_code() : c;
+}
+
 // launch a deferred FJLT operator (and, with tab, the pointer-table write)
 int flush_fjlt(Plan* p, hipStream_t s, float** tab = nullptr, float* a = nullptr, float* b = nullptr,
                float* c = nullptr) {
@@ -141,7 +153,8 @@ int seg(Plan* p, const void* A, int i, hipStream_t s, float* V = nullptr, float*
   // odd passes walk the row blocks backwards: each pass starts on the rows
   // the previous one read last, which are still in the MALL
   rc = sl_rsvd_pass(A, p->m, p->n, p->lda, p->Zt, p->k, p->pass_ws, final_pass ? p->Y : nullptr, p->k,
-                    final_pass ? 1 : 0, ((i & 1) ? 256 : 0) | (pass_nt_code() << 9), s);
+                    final_pass ? 1 : 0, ((i & 1) ? 256 : 0) | ((final_pass ? pass_nt_final_code() : pass_nt_code()) << 9),
+                    s);
   if (rc != SL_OK) return rc;
   // the first reduce of the call also clears the status word (no memset node)
   return sl_rsvd_reduce_z(p->pass_ws, p->m, p->n, p->k, p->WG, 1, p->k, final_pass ? p->WG + p->n * p->k : nullptr,
