@@ -107,6 +107,7 @@ struct Lib {
   int (*gen_set_z)(void*, const void*, void*) = nullptr;
   int (*gen_run)(void*, const void*, void*, int64_t, void*, void*, void*) = nullptr;
   int (*gen_status)(void*, int*, void*) = nullptr;
+  int (*gen_run_comm)(void*, const void*, void*, void*, int64_t, void*, void*, void*) = nullptr;
   // host-operand NLA drivers (nla_native.hip) and the LIBSVM reader (libsvm_io.cpp)
   int (*sym_rsvd)(const double*, int64_t, int64_t, int, int, int, int, int, uint64_t, uint64_t, double*, int64_t,
                   double*, void*) = nullptr;
@@ -188,6 +189,7 @@ inline Lib& lib() {
               bind(L.h, "sl_rsvd_gen_set_dense", L.gen_set_dense, L.err) &&
               bind(L.h, "sl_rsvd_gen_set_z", L.gen_set_z, L.err) && bind(L.h, "sl_rsvd_gen_run", L.gen_run, L.err) &&
               bind(L.h, "sl_rsvd_gen_status", L.gen_status, L.err) &&
+              bind(L.h, "sl_rsvd_gen_run_comm", L.gen_run_comm, L.err) &&
               bind(L.h, "sl_nat_sym_rsvd", L.sym_rsvd, L.err) &&
               bind(L.h, "sl_nat_sym_rsvd_comm", L.sym_rsvd_comm, L.err) && bind(L.h, "sl_nat_blendenpik", L.blendenpik, L.err) &&
               bind(L.h, "sl_nat_blendenpik_comm", L.blendenpik_comm, L.err) &&
@@ -862,17 +864,84 @@ inline void drop_rsvd_plan(void* plan) {
 }
 
 // U (m x rank f32), S (rank f32, any 1-column / 1-row shape), V (n x rank f32)
-// of bf16 A (m x n, m >= n).  ctr: the context counter (advanced by the
-// sketch's draws exactly as the runtime advances it).  comm (a NativeComm
+// of bf16 A (m x n, m >= n) on the fused engine (16 <= n <= 1024, k <= 48;
+// otherwise, and for f32 / f64 A, the general engine: approximate_svd_gen).
+// ctr: the context counter (advanced by the sketch's draws exactly as the
+// runtime advances it).  comm (a NativeComm
 // RCCL communicator, sl_device_comm_create): A is this rank's row shard of a
 // row-distributed matrix (every rank the same n), U its rows of the left
 // factor, S and V replicated; the [W; G] pass sums are all-reduced over RCCL
 // between the engine's segments (sl_rsvd_run_comm).
+// f32 / f64 A on the general engine (rsvd_general.hip: hand-written products
+// for k <= 128): U (m x rank), S (rank) and V (n x rank) in A's dtype; comm:
+// A is this rank's row shard, the [W; G] spans all-reduced per segment
+// (sl_rsvd_gen_run_comm).  Same operator streams as the runtime.
+inline int approximate_svd_gen(const DevMat& A, const DevMat& U, const DevMat& Sv, const DevMat& V, int rank,
+                               const char* params, uint64_t seed, uint64_t& ctr, void* comm) {
+  Lib& L = lib();
+  const int dt = A.dtype;
+  const int udt = dt == BF16 ? F32 : dt;
+  if (U.dtype != udt || Sv.dtype != udt || V.dtype != udt)
+    return fail(103, "device approximate_svd: U, S, V in A's dtype (f32 for bf16 A)");
+  const int64_t m = A.m, n = A.n;
+  if (m < n && !comm) return fail(103, "device approximate_svd: needs a tall A (m >= n); pass A^T and swap U / V");
+  if (rank < 1 || rank > n) return fail(109, "device approximate_svd: bad rank");
+  const SvdParams p = parse_svd_params(params);
+  const int k = (int)std::max<int64_t>(rank, std::min<int64_t>(n, (int64_t)p.ratio * rank + p.additive));
+  if (k > 128) return fail(103, "device approximate_svd: the general engine covers k <= 128");
+  if (U.m != m || U.n != rank || V.m != n || V.n != rank || V.ld != rank || Sv.m * Sv.n != rank)
+    return fail(104, "device approximate_svd: output shapes");
+  if (p.sketch != "JLT" && p.sketch != "CT" && p.sketch != "FJLT" && p.sketch != "CWT")
+    return fail(109, "device approximate_svd: sketch must be JLT, CT, FJLT or CWT");
+  const int q = std::max(0, p.iters);
+  void* plan = nullptr;
+  SLDEV_TRY(L.gen_create(m, n, A.ld, k, rank, q, dt, &plan), "rsvd plan");
+  struct Guard {
+    void* p;
+    ~Guard() { lib().gen_destroy(p); }
+  } guard{plan};
+  const uint64_t base = ctr;
+  if (p.sketch == "JLT" || p.sketch == "CT") {
+    const bool jlt = p.sketch == "JLT";
+    SLDEV_TRY(L.gen_set_dense(plan, jlt ? sl::DIST_NORMAL : sl::DIST_CAUCHY, seed, base, 0.0, 0.0,
+                              jlt ? std::sqrt(1.0 / k) : 1.0 / k),
+              "sketch operator");
+    ctr = base + (uint64_t)(n * k);
+  } else if (p.sketch == "FJLT") {
+    SLDEV_TRY(L.gen_set_fjlt(plan, seed, base, base + (uint64_t)n, std::sqrt((double)n / k)), "sketch operator");
+    ctr = base + (uint64_t)(n + k);
+  } else {
+    slnat::Sketch cw;
+    cw.type = "CWT";
+    cw.N = n;
+    cw.S = k;
+    cw.seed = seed;
+    cw.ctr0 = base;
+    ctr = slnat::build(cw);
+    std::vector<double> z((size_t)(n * k), 0.0);   // Z = Omega^T (n x k)
+    for (int64_t j = 0; j < n; ++j) z[(size_t)(j * k + cw.idx[(size_t)j])] = cw.val[(size_t)j];
+    Buf dz(n * k * (int64_t)esize(dt));
+    const int rc = upload_as(dz, z.data(), n * k, dt);
+    if (rc) return rc;
+    SLDEV_TRY(L.gen_set_z(plan, dz.p, nullptr), "sketch operator");
+    SLDEV_TRY(L.dev_sync(nullptr), "sync");
+  }
+  if (comm)
+    SLDEV_TRY(L.gen_run_comm(plan, A.data, comm, U.data, U.ld, Sv.data, V.data, nullptr), "rsvd run (comm)");
+  else
+    SLDEV_TRY(L.gen_run(plan, A.data, U.data, U.ld, Sv.data, V.data, nullptr), "rsvd run");
+  int status = 0;
+  SLDEV_TRY(L.gen_status(plan, &status, nullptr), "rsvd status");
+  if (status & 2) return fail(108, "device approximate_svd: non-finite values in A");
+  return check(L.dev_sync(nullptr), "sync");
+}
+
 inline int approximate_svd(const DevMat& A, const DevMat& U, const DevMat& Sv, const DevMat& V, int rank,
                            const char* params, uint64_t seed, uint64_t& ctr, void* comm = nullptr) {
   Lib& L = lib();
   if (!L.loaded) return fail(106, "device C API: " + L.err);
-  if (A.dtype != BF16) return fail(103, "device approximate_svd: A must be bf16");
+  if (A.dtype == F32 || A.dtype == F64) return approximate_svd_gen(A, U, Sv, V, rank, params, seed, ctr, comm);
+  if (A.dtype != BF16) return fail(103, "device approximate_svd: A must be bf16, f32 or f64");
   if (U.dtype != F32 || Sv.dtype != F32 || V.dtype != F32) return fail(103, "device approximate_svd: U, S, V are f32");
   const int64_t m = A.m, n = A.n;
   if (m < n && !comm) return fail(103, "device approximate_svd: needs a tall A (m >= n); pass A^T and swap U / V");
@@ -881,8 +950,8 @@ inline int approximate_svd(const DevMat& A, const DevMat& U, const DevMat& Sv, c
   const int k = (int)std::max<int64_t>(rank, std::min<int64_t>(n, (int64_t)p.ratio * rank + p.additive));
   if (U.m != m || U.n != rank || V.m != n || V.n != rank || V.ld != rank || Sv.m * Sv.n != rank)
     return fail(104, "device approximate_svd: output shapes");
-  if (n % 8 || n < 16 || n > 1024 || A.ld % 8 || k > 48)
-    return fail(103, "device approximate_svd: engine covers 16 <= n <= 1024, n % 8 == 0, lda % 8 == 0, k <= 48");
+  if (n % 8 || n < 16 || n > 1024 || A.ld % 8 || k > 48)   // beyond the fused engine: the general one
+    return approximate_svd_gen(A, U, Sv, V, rank, params, seed, ctr, comm);
   const int q = std::max(0, p.iters);
   const PlanKey key{A.data, m, n, A.ld, k, rank, q};
   void* plan = nullptr;

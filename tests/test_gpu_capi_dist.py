@@ -6,7 +6,8 @@ DistMatrix_STAR_VC, SharedMatrix, RootMatrix), the sums going through a
 callback communicator (sl_device_comm_from_allreduce) that all-reduces over
 this test's gloo group -- the same code an RCCL communicator drives across
 GPUs.  Covers sketch application (8 layout cases x 7 sketch types),
-randSVD and symmetric randSVD ([VC,*] A), kernel Grams, FasterLeastSquares
+randSVD (bf16 fused engine; f32 / f64 general engine) and symmetric randSVD
+([VC,*] A), kernel Grams, FasterLeastSquares
 ([VC,*] A and B) and the LIBSVM reader ([VC,*] / [*,VC] examples).
 Oracle: the single-rank call of the same C ABI on the whole operand
 (DeviceMatrix; host "Matrix" for least squares, plus numpy lstsq) -- the
@@ -161,6 +162,47 @@ def _worker(rank, world):
     svd = ((sv - s1).abs().max().item() / s1.abs().max().item(), (Vd * sg - Vw).abs().max().item(),
            (Ul * sg - Uw[r0:r0 + lm]).abs().max().item())
 
+    # f32 / f64 A on the general engine through the same entry point: the
+    # row-distributed f32 call vs the one-rank f32 call, and f64 vs numpy
+    gm_, gn_, gr_ = 9000, 300, 8
+    U1_ = torch.linalg.qr(torch.randn(gm_, 16, dtype=torch.float64, device=dev, generator=g))[0]
+    V1_ = torch.linalg.qr(torch.randn(gn_, 16, dtype=torch.float64, device=dev, generator=g))[0]
+    A64_ = (U1_ * (20.0 * 0.75 ** torch.arange(16, device=dev))) @ V1_.t() + 1e-6 * torch.randn(
+        gm_, gn_, dtype=torch.float64, device=dev, generator=g)
+    gen = {}
+    for dtn, tdt, dcode in (("f32", torch.float32, 0), ("f64", torch.float64, 1)):
+        Ag = A64_.to(tdt)
+        r0g, _, lmg, _ = shard("DistMatrix_VC_STAR", gm_, gn_)
+        tens = (Ag[r0g:r0g + lmg].contiguous(), torch.empty(lmg, gr_, dtype=tdt, device=dev),
+                torch.empty(gr_, 1, dtype=tdt, device=dev), torch.empty(gn_, gr_, dtype=tdt, device=dev))
+        hw = []
+        for t_, (gm2, gn2) in zip(tens, ((gm_, gn_), (gm_, gr_), (gr_, 1), (gn_, gr_))):
+            w = vp()
+            assert lib.sl_wrap_raw_dist_device_matrix(t_.data_ptr(), dcode, gm2, gn2, t_.stride(0), comm, C.byref(w)) == 0
+            hw.append(w)
+        cg = vp()
+        assert lib.sl_create_default_context(88, C.byref(cg)) == 0
+        pj = b'{"num_iterations": 2, "sketch": "JLT"}'
+        assert lib.sl_approximate_svd(b"DistMatrix_VC_STAR", hw[0], b"DistMatrix_VC_STAR", hw[1], b"SharedMatrix", hw[2],
+                                      b"SharedMatrix", hw[3], gr_, pj, cg) == 0, err()
+        one = (torch.empty(gm_, gr_, dtype=tdt, device=dev), torch.empty(gr_, 1, dtype=tdt, device=dev),
+               torch.empty(gn_, gr_, dtype=tdt, device=dev))
+        ww = []
+        for t_ in (Ag,) + one:
+            w = vp()
+            lib.sl_wrap_raw_device_matrix(t_.data_ptr(), dcode, t_.shape[0], t_.shape[1], t_.stride(0), C.byref(w))
+            ww.append(w)
+        cg2 = vp()
+        assert lib.sl_create_default_context(88, C.byref(cg2)) == 0
+        assert lib.sl_approximate_svd(b"DeviceMatrix", ww[0], b"DeviceMatrix", ww[1], b"DeviceMatrix", ww[2],
+                                      b"DeviceMatrix", ww[3], gr_, pj, cg2) == 0, err()
+        torch.cuda.synchronize()
+        s_true = torch.linalg.svdvals(A64_)[:gr_]
+        sgn_ = torch.sign((tens[3] * one[2]).sum(0))
+        gen[dtn] = ((tens[2].ravel() - one[1].ravel()).abs().max().item() / one[1].abs().max().item(),
+                    (tens[3] * sgn_ - one[2]).abs().max().item(),
+                    ((one[1].ravel().double() - s_true).abs() / s_true).max().item())
+
     # kernel Gram with X's points (rows) split [VC,*], Y replicated -> K rows [VC,*]
     lib.sl_create_kernel.restype = C.c_int
     kh = vp()
@@ -275,13 +317,13 @@ def _worker(rank, world):
                  np.abs(Yl[:ylm, :yln].cpu().numpy() - Yr[yr0:yr0 + ylm, yc0:yc0 + yln]).max())
     os.remove(path)
     lib.sl_runtime_started.restype = C.c_int
-    return worst, mcmr, svd, kdiff, ls, sym, io, lib.sl_runtime_started()
+    return worst, mcmr, svd, kdiff, ls, sym, io, gen, lib.sl_runtime_started()
 
 
 def test_capi_dist_matrix_world2():
     from mp_utils import run_distributed
     res = run_distributed(_worker, 2, timeout=300)
-    for worst, mcmr, svd, kdiff, ls, sym, io, started in res:
+    for worst, mcmr, svd, kdiff, ls, sym, io, gen, started in res:
         assert len(worst) >= len(TYPES) * 4
         bad = {k: v for k, v in worst.items() if v > 1e-12}
         assert not bad, bad
@@ -292,4 +334,7 @@ def test_capi_dist_matrix_world2():
         assert ls[0] < 1e-9 and ls[1] < 1e-8, ls   # vs the one-rank call, vs numpy lstsq
         assert sym[0] < 1e-10 and sym[1] < 1e-8 and sym[2] < 1e-6, sym
         assert io == 0.0
+        # the general engine: distributed vs one rank (f32 / f64 roundoff), s vs the true values
+        assert gen["f32"][0] < 1e-5 and gen["f32"][1] < 1e-3 and gen["f32"][2] < 1e-4, gen
+        assert gen["f64"][0] < 1e-12 and gen["f64"][1] < 1e-9 and gen["f64"][2] < 1e-9, gen
         assert started == 0   # no call above started the interpreter-side runtime
