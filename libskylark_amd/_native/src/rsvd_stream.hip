@@ -782,7 +782,9 @@ __device__ __forceinline__ void gw_store(const f64x4 (&acc)[9], double* sb, int 
 template <typename T, int W>
 __device__ __forceinline__ void gram_w_body(const T* __restrict__ X, int64_t rows, int k, int64_t ldx,
                                             double* __restrict__ slab) {
-  constexpr int KT = 8, NP = 9, U = 4;
+  // U 4-row steps per load group; f32 X keeps its raw words in the ping-pong
+  // buffers (half the registers of f64), so it prefetches deeper
+  constexpr int KT = 8, NP = 9, U = sizeof(T) == 4 ? 8 : 4;
   const int lane = threadIdx.x & 63, kg = lane >> 4, r16 = lane & 15;
   f64x4 acc[NP];
 #pragma unroll
@@ -791,11 +793,11 @@ __device__ __forceinline__ void gram_w_body(const T* __restrict__ X, int64_t row
   const int64_t q0 = nq * blockIdx.x / gridDim.x, q1 = nq * (blockIdx.x + 1) / gridDim.x;
   // software-pipelined: the next U steps' loads are in flight while this U's
   // MFMAs run (a load-then-compute loop waited out the memory latency every
-  // iteration: 2.5 ms for a 1e6 x 128 f32 Gram)
-  // unconditional loads from clamped addresses, zeroed by a select after the
-  // load: a conditional load became an exec-masked branch with a vmcnt(0)
-  auto load = [&](int64_t q, double (&xv)[U][KT]) {
-    T raw[U][KT];
+  // iteration: 2.5 ms for a 1e6 x 128 f32 Gram).  Unconditional loads from
+  // clamped addresses (a conditional load became an exec-masked branch with a
+  // vmcnt(0)); the widening and the zero-select happen at the MFMA, so nothing
+  // waits on a group's loads before the previous group's MFMAs have issued
+  auto load = [&](int64_t q, T (&raw)[U][KT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = 4 * (q + u) + kg;
@@ -806,26 +808,26 @@ __device__ __forceinline__ void gram_w_body(const T* __restrict__ X, int64_t row
         raw[u][t] = src[c < k ? c : k - 1];
       }
     }
+  };
+  auto mma = [&](int64_t q, const T (&raw)[U][KT]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = 4 * (q + u) + kg;
       const bool rok = q + u < q1 && row < rows;
+      double xv[KT];
 #pragma unroll
-      for (int t = 0; t < KT; ++t) xv[u][t] = (rok && 16 * t + r16 < k) ? (double)raw[u][t] : 0.0;
+      for (int t = 0; t < KT; ++t) xv[t] = (rok && 16 * t + r16 < k) ? (double)raw[u][t] : 0.0;
+      gw_mma<W, 0>(acc, xv);
     }
   };
-  auto mma = [&](const double (&xv)[U][KT]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) gw_mma<W, 0>(acc, xv[u]);
-  };
-  double xa[U][KT], xb[U][KT];
+  T xa[U][KT], xb[U][KT];
   if (q0 < q1) load(q0, xa);
   for (int64_t q = q0; q < q1; q += 2 * U) {
     if (q + U < q1) load(q + U, xb);
-    mma(xa);
+    mma(q, xa);
     if (q + U >= q1) break;
     if (q + 2 * U < q1) load(q + 2 * U, xa);
-    mma(xb);
+    mma(q + U, xb);
   }
   gw_store<W, 0>(acc, slab + (int64_t)blockIdx.x * k * k, k, lane, r16);
 }
