@@ -34,12 +34,35 @@ struct u64x2 { uint64_t x, y; };
 
 SL_HD uint64_t rotl64(uint64_t v, int r) { return (v << r) | (v >> (64 - r)); }
 
+// rotl64 by a constant: on the device two v_alignbit_b32 (a funnel shift of
+// the two 32-bit halves; the generic form compiled to a 64-bit shift, a
+// 32-bit shift and two ORs), the same bits
+template <int R>
+SL_HD uint64_t rotl64c(uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  if constexpr (R == 32) {
+    return ((uint64_t)lo << 32) | hi;
+  } else if constexpr (R < 32) {
+    const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 32 - R);
+    const uint32_t nl = __builtin_amdgcn_alignbit(lo, hi, 32 - R);
+    return ((uint64_t)nh << 32) | nl;
+  } else {   // rotate the swapped halves by R - 32
+    const uint32_t nh = __builtin_amdgcn_alignbit(lo, hi, 64 - R);
+    const uint32_t nl = __builtin_amdgcn_alignbit(hi, lo, 64 - R);
+    return ((uint64_t)nh << 32) | nl;
+  }
+#else
+  return rotl64(v, R);
+#endif
+}
+
 // Threefry-2x64-13.  Rotation constants R_64x2 and key-schedule parity are the
 // published Random123 / Skein values.
 SL_HD u64x2 threefry2x64_13(uint64_t c0, uint64_t c1, uint64_t k0, uint64_t k1) {
   const uint64_t k2 = 0x1BD11BDAA9FC1A22ULL ^ k0 ^ k1;
   uint64_t x0 = c0 + k0, x1 = c1 + k1;
-#define SL_TF_R(r) { x0 += x1; x1 = rotl64(x1, r); x1 ^= x0; }
+#define SL_TF_R(r) { x0 += x1; x1 = rotl64c<r>(x1); x1 ^= x0; }
   SL_TF_R(16) SL_TF_R(42) SL_TF_R(12) SL_TF_R(31)
   x0 += k1; x1 += k2 + 1;
   SL_TF_R(16) SL_TF_R(32) SL_TF_R(24) SL_TF_R(21)
