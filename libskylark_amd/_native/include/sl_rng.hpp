@@ -81,7 +81,18 @@ SL_HD u64x2 stream_block(uint64_t seed, uint64_t idx, uint64_t sub = 0) {
 // -------------------------------------------------------- bit -> uniform
 // Uniforms on the OPEN interval (0,1): never 0 (safe for log), never 1.
 SL_HD double u01_d(uint64_t b) { return ((double)(b >> 11) + 0.5) * 0x1.0p-53; }
-SL_HD float u01_f(uint64_t b) { return ((float)(uint32_t)(b >> 40) + 0.5f) * 0x1.0p-24f; }
+SL_HD float u01_f(uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the 24-bit value through ONE 32-bit convert (the compiler folded the cast
+  // back into its 64-bit -> f32 sequence, five instructions), same value
+  const uint32_t x = (uint32_t)(b >> 32) >> 8;
+  float f;
+  asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(x));
+  return (f + 0.5f) * 0x1.0p-24f;
+#else
+  return ((float)(uint32_t)(b >> 40) + 0.5f) * 0x1.0p-24f;
+#endif
+}
 
 // Unbiased-enough uniform integer in [lo, hi] via 64x64->128 multiply-high
 // (bias < range / 2^64).

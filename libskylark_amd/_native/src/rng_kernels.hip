@@ -71,10 +71,14 @@ __global__ void __launch_bounds__(256) k_fill_normal_lines(T* __restrict__ out, 
     T* p = out + (int64_t)l * ld + f;
     if (f + 8 <= nfast && (((uintptr_t)p) & 15) == 0) {
       if constexpr (sizeof(T) == 2) {
+        // hardware round-to-nearest-even pairs (v_cvt_pk_bf16_f32): the same
+        // bits as f_to_bf16's software RNE for the finite normals here
+        typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+        typedef __attribute__((ext_vector_type(2))) float f32x2_t;
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          w[j] = (uint32_t)Cvt<T>::from_f(v[2 * j]) | ((uint32_t)Cvt<T>::from_f(v[2 * j + 1]) << 16);
+          w[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){v[2 * j], v[2 * j + 1]}, bf16x2_t));
         *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
       } else {
         *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
