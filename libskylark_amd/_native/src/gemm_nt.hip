@@ -378,34 +378,59 @@ k_split_bf16(const float* __restrict__ A, int64_t M, int64_t K, int64_t lda, bf1
 // K-contiguous B operand of a columnwise sketch panel product S_panel X.
 // 64 (k) x 64 (column) tiles through LDS: coalesced row reads of X, one
 // 128-B bf16 row piece per output row and plane.
+// the 64 x 64 f32 tile X[k0 .., c0 ..] (zero outside w x m) into LDS: all 16
+// loads of a thread issued unconditionally from clamped addresses, then
+// zeroed (a `cond ? X[..] : 0` load compiled to one exec-masked branch per
+// load, each waiting for its own)
+__device__ __forceinline__ void load_tile_t(const float* __restrict__ X, int w, int m, int64_t ldx, int c0, int k0,
+                                            float (&tile)[64][65]) {
+  const int t = threadIdx.x;
+  if (w > 0) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = t + 256 * i, k = k0 + (e >> 6), c = c0 + (e & 63);
+      v[i] = X[(int64_t)(k < w ? k : w - 1) * ldx + (c < m ? c : m - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(v[i]));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = t + 256 * i, kk = e >> 6, cc = e & 63;
+      tile[kk][cc] = (k0 + kk < w && c0 + cc < m) ? v[i] : 0.f;
+    }
+  } else {
+    for (int e = t; e < 64 * 64; e += 256) tile[e >> 6][e & 63] = 0.f;
+  }
+  __syncthreads();
+}
+
+// bf16 pair (x0, x1) -> the packed hardware RNE word and the two rounded values
+__device__ __forceinline__ uint32_t rne_pair(float x0, float x1, float* r0, float* r1) {
+  const uint32_t p = hw_bf16x2(x0, x1);
+  *r0 = bf16_to_f((bf16_t)(p & 0xffffu));
+  *r1 = bf16_to_f((bf16_t)(p >> 16));
+  return p;
+}
+
 __global__ void __launch_bounds__(256)
 k_split_t(const float* __restrict__ X, int w, int m, int64_t ldx, bf16_t* __restrict__ Ht, bf16_t* __restrict__ Lt,
           int wpad, int64_t ldt) {
   __shared__ float tile[64][65];
   const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  load_tile_t(X, w, m, ldx, c0, k0, tile);
   const int t = threadIdx.x;
-  for (int e = t; e < 64 * 64; e += 256) {
-    const int kk = e >> 6, cc = e & 63;
-    const int k = k0 + kk, c = c0 + cc;
-    tile[kk][cc] = (k < w && c < m) ? X[(int64_t)k * ldx + c] : 0.f;
-  }
-  __syncthreads();
   const int cc = t >> 2, q = t & 3;
   const int c = c0 + cc;
   if (c >= m || k0 + 16 * q >= wpad) return;
+  // hi = rne(x), lo = rne(x - hi), two elements per hardware conversion
   uint32_t h[8], l[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    uint32_t hh[2], ll[2];
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const float x = tile[16 * q + 2 * u + v][cc];
-      const bf16_t hb = f_to_bf16(x);
-      hh[v] = hb;
-      ll[v] = f_to_bf16(x - bf16_to_f(hb));
-    }
-    h[u] = hh[0] | (hh[1] << 16);
-    l[u] = ll[0] | (ll[1] << 16);
+    const float x0 = tile[16 * q + 2 * u][cc], x1 = tile[16 * q + 2 * u + 1][cc];
+    float h0, h1, d0, d1;
+    h[u] = rne_pair(x0, x1, &h0, &h1);
+    l[u] = rne_pair(x0 - h0, x1 - h1, &d0, &d1);
   }
   uint4* ph = (uint4*)(Ht + (int64_t)c * ldt + k0 + 16 * q);
   uint4* pl = (uint4*)(Lt + (int64_t)c * ldt + k0 + 16 * q);
@@ -425,33 +450,20 @@ __global__ void __launch_bounds__(256)
 k_split3_t(const float* __restrict__ X, int w, int m, int64_t ldx, bf16_t* __restrict__ S, int seg, int64_t lds) {
   __shared__ float tile[64][65];
   const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  load_tile_t(X, w, m, ldx, c0, k0, tile);
   const int t = threadIdx.x;
-  for (int e = t; e < 64 * 64; e += 256) {
-    const int kk = e >> 6, cc = e & 63;
-    const int k = k0 + kk, c = c0 + cc;
-    tile[kk][cc] = (k < w && c < m) ? X[(int64_t)k * ldx + c] : 0.f;
-  }
-  __syncthreads();
   const int cc = t >> 2, q = t & 3;
   const int c = c0 + cc;
   if (c >= m || k0 + 16 * q >= seg) return;
   uint32_t h[8], md[8], l[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    uint32_t hh[2], mm[2], ll[2];
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const float x = tile[16 * q + 2 * u + v][cc];
-      const bf16_t hb = f_to_bf16(x);
-      const float r = x - bf16_to_f(hb);
-      const bf16_t mb = f_to_bf16(r);
-      hh[v] = hb;
-      mm[v] = mb;
-      ll[v] = f_to_bf16(r - bf16_to_f(mb));
-    }
-    h[u] = hh[0] | (hh[1] << 16);
-    md[u] = mm[0] | (mm[1] << 16);
-    l[u] = ll[0] | (ll[1] << 16);
+    const float x0 = tile[16 * q + 2 * u][cc], x1 = tile[16 * q + 2 * u + 1][cc];
+    float h0, h1, m0, m1, d0, d1;
+    h[u] = rne_pair(x0, x1, &h0, &h1);
+    const float r0 = x0 - h0, r1 = x1 - h1;
+    md[u] = rne_pair(r0, r1, &m0, &m1);
+    l[u] = rne_pair(r0 - m0, r1 - m1, &d0, &d1);
   }
   bf16_t* row = S + (int64_t)c * lds + k0 + 16 * q;
   auto put = [&](int sg, const uint32_t* v) {
