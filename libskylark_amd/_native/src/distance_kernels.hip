@@ -48,14 +48,32 @@ k_pairwise(const T* __restrict__ X, const T* __restrict__ Y, T* __restrict__ K, 
 
   for (int64_t k0 = 0; k0 < d; k0 += KC) {
     // stage: 64 rows x 32 k of X and of Y; consecutive threads walk k (coalesced)
+    // every load issued unconditionally from a clamped address, then zeroed:
+    // `cond ? X[..] : 0` compiled to one exec-masked branch per load, each
+    // waiting for its own load
+    constexpr int NE = (TB * KC) / 256;
+    T xl[NE], yl[NE];
 #pragma unroll
-    for (int e = 0; e < (TB * KC) / 256; ++e) {
+    for (int e = 0; e < NE; ++e) {
       const int flat = e * 256 + tid;
       const int kk = flat & (KC - 1), rr = flat / KC;
-      const int64_t gk = k0 + kk;
-      const int64_t gx = r0 + rr, gy = c0 + rr;
-      xs[kk][rr] = (gx < m && gk < d) ? X[gx * ldx + gk * sdx] : T(0);
-      ys[kk][rr] = (gy < n && gk < d) ? Y[gy * ldy + gk * sdy] : T(0);
+      const int64_t gk = k0 + kk < d ? k0 + kk : d - 1;
+      const int64_t gx = r0 + rr < m ? r0 + rr : m - 1, gy = c0 + rr < n ? c0 + rr : n - 1;
+      xl[e] = X[gx * ldx + gk * sdx];
+      yl[e] = Y[gy * ldy + gk * sdy];
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      asm volatile("" : "+v"(xl[e]));
+      asm volatile("" : "+v"(yl[e]));
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int flat = e * 256 + tid;
+      const int kk = flat & (KC - 1), rr = flat / KC;
+      const bool kok = k0 + kk < d;
+      xs[kk][rr] = (kok && r0 + rr < m) ? xl[e] : T(0);
+      ys[kk][rr] = (kok && c0 + rr < n) ? yl[e] : T(0);
     }
     __syncthreads();
     const int kmax = (int)((d - k0) < KC ? (d - k0) : KC);
