@@ -976,3 +976,40 @@ def test_dist_matrix_types_shapes_and_errors(capi):
     capi.sl_free_raw_dist_device_matrix_wrap(a)
     capi.sl_free_sketch_transform(h)
     capi.sl_free_context(ctx)
+
+
+def test_dist_matrix_entry_points_refuse_before_device_work(capi):
+    """Every DistMatrix-aware entry point checks its type strings first: the
+    2-D [MC,MR] "DistMatrix" is refused with 103 and a mix of distributed and
+    local operands with 109, before any device call (so these hold on a host
+    without a GPU)."""
+    vp, i64 = C.c_void_p, C.c_int64
+    capi.sl_wrap_raw_dist_device_matrix.argtypes = [vp, C.c_int, i64, i64, i64, vp, C.POINTER(vp)]
+    d = vp()
+    assert capi.sl_wrap_raw_dist_device_matrix(None, 1, 10, 3, 3, None, C.byref(d)) == 0
+    ctx = vp()
+    assert capi.sl_create_default_context(5, C.byref(ctx)) == 0
+    prm = b'{"num_iterations": 1}'
+    capi.sl_approximate_svd.argtypes = [C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_uint16,
+                                        C.c_char_p, vp]
+    capi.sl_approximate_symmetric_svd.argtypes = [C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_uint16,
+                                                  C.c_char_p, vp]
+    capi.sl_faster_least_squares.argtypes = [C.c_int, C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp]
+    capi.sl_readlibsvm.argtypes = [C.c_char_p, C.c_char_p, vp, C.c_char_p, vp, C.c_int, C.c_int, C.c_int]
+    capi.sl_kernel_gram.argtypes = [C.c_int, C.c_int, vp, C.c_char_p, vp, C.c_char_p, vp, C.c_char_p, vp]
+    for a_t, b_t, want in ((b"DistMatrix", b"DistMatrix", 103), (b"DistMatrix_VC_STAR", b"Matrix", 109)):
+        assert capi.sl_approximate_svd(a_t, d, b_t, d, b"SharedMatrix", d, b"SharedMatrix", d, 2, prm, ctx) == want
+        assert capi.sl_approximate_symmetric_svd(a_t, d, b"SharedMatrix", d, b_t, d, 2, prm, ctx) == want
+        assert capi.sl_faster_least_squares(0, a_t, d, b_t, d, b"SharedMatrix", d, b"{}", ctx) == want
+        assert capi.sl_readlibsvm(b"/nonexistent", a_t, d, b_t, d, 2, 0, -1) == want
+        k = vp()
+        assert capi.sl_create_kernel(b"gaussian", 3, C.byref(k), C.c_double(1.0)) == 0
+        assert capi.sl_kernel_gram(2, 1, k, a_t, d, b_t, d, b"SharedMatrix", d) == want
+        capi.sl_free_kernel(k)
+    # layouts the paths do not take: a column-distributed A for randSVD / least squares
+    assert capi.sl_approximate_svd(b"DistMatrix_STAR_VC", d, b"DistMatrix_STAR_VC", d, b"SharedMatrix", d,
+                                   b"SharedMatrix", d, 2, prm, ctx) == 103
+    assert capi.sl_faster_least_squares(1, b"DistMatrix_VC_STAR", d, b"DistMatrix_VC_STAR", d, b"SharedMatrix", d,
+                                        b"{}", ctx) == 103
+    capi.sl_free_raw_dist_device_matrix_wrap(d)
+    capi.sl_free_context(ctx)
