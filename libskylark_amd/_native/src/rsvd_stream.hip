@@ -11,10 +11,13 @@
 //   sl_ts_gram_w G = X^T X for 64 < k <= 128 (X f32 / f64)
 //   sl_ts_small  C = op(A) op(B), k x k operands, one workgroup (f64)
 //
-// Both big products run in A's own precision on the matrix cores
+// Both big products run at A's own precision on the matrix cores
 // (v_mfma_f32_16x16x4_f32: exact f32 products in a k-ordered fmaf chain;
-// v_mfma_f64_16x16x4_f64) -- the reference's precision, not a split bf16
-// shortcut.  At k = 40 (three 16-column tiles) a pass over a 1e6 x 1000 f32 A
+// v_mfma_f64_16x16x4_f64) -- the reference's precision.  For f32 with k <= 48,
+// Y = A Z uses an exact three-plane bf16 split of A and Z instead (six
+// 16x16x32 bf16 MFMAs per group, f32 accumulation, dropped terms below 2^-24
+// |a| |z|): the same error bound, and the product took 1168 -> 1032 us on a
+// 1e6 x 1000 operand (profiles/r6/az_bf16_split_ab.txt).  At k = 40 (three 16-column tiles) a pass over a 1e6 x 1000 f32 A
 // is 2 x 0.96e11 FLOP, i.e. 0.62 ms per product at the f32 matrix peak against
 // 0.67 ms of HBM for the 4 GB read: the kernels are built so neither the
 // matrix pipe nor the memory system waits on the other (software-pipelined
@@ -38,6 +41,21 @@ namespace {
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) double f64x4;
 typedef __attribute__((ext_vector_type(2))) double f64x2;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+// Exact three-plane bf16 split of f32 values (H = rne(x), M = rne(x - H),
+// L = rne(x - H - M); H + M + L == x for normal f32), two values per
+// hardware conversion; the packed words (element 2u in the low half of u).
+__device__ __forceinline__ uint32_t bf2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((__attribute__((ext_vector_type(2))) float){lo, hi}, b2));
+}
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = bf2(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = bf2(r0, r1);
+  l = bf2(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xffff0000u));
+}
 
 template <typename T>
 struct Mf;
@@ -117,14 +135,20 @@ constexpr int AZ_VL = 2, AZ_NG = 4, AZ_PD = 2, AZ_BR = 128;
 template <int KT> constexpr int az_nt() { return KT > 4 ? 512 : 256; }
 template <int KT> constexpr int az_rt() { return KT > 4 ? 1 : 2; }
 
-template <typename T, int KT>
-constexpr int az_lds() { return 2 * AZ_NG * KT * 64 * 16 * AZ_VL; }
+// BS (f32 only): A and Z enter the matrix cores as exact three-plane bf16
+// splits, six v_mfma_f32_16x16x32_bf16 per 32-column group and tile (H H, H M,
+// M H, M M, H L, L H; the dropped M L / L M / L L terms are below 2^-24 of
+// |a| |z|) instead of eight v_mfma_f32_16x16x4_f32: 96 instead of 256 matrix
+// cycles per group.  Z's B fragments sit in LDS as the three planes (48 B per
+// lane and tile instead of 32).
+template <typename T, int KT, bool BS = false>
+constexpr int az_lds() { return 2 * AZ_NG * KT * 64 * (BS ? 48 : 16 * AZ_VL); }
 
 // whole-block interleaved rounds before the stream-K tail (the tail keeps
 // g .. 2g - 1 blocks; g <= nrb)
 __host__ __device__ inline int64_t az_rounds(int64_t nrb, int64_t g) { return nrb >= 2 * g ? nrb / g - 1 : 0; }
 
-template <typename T, int KT, bool VEC>
+template <typename T, int KT, bool VEC, bool BS>
 __global__ void __launch_bounds__(az_nt<KT>(), KT > 4 ? 1 : 2)
 k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Z, int k, T* __restrict__ Y,
         int64_t ldy, int split) {
@@ -142,6 +166,8 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   constexpr int ZE = ZQ * VW;                          // Z loads per thread per chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* zl = (T*)smem;                                    // [2][NG][KT][64][EPL]
+  static_assert(!BS || (sizeof(T) == 4 && KT <= 4), "bf16 split: f32, k <= 64");
+  constexpr int BUFB = AZ_NG * KT * 64 * 48;           // BS: bytes per Z buffer
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nchunk = (n + CW - 1) / CW;
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
@@ -216,7 +242,18 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
         vec v;
 #pragma unroll
         for (int s = 0; s < VW; ++s) v[s] = (c * CW + cc + s < n && jj < k) ? zr[u][s] : (T)0;
-        *(vec*)(zb + ((q * KT + t) * 64 + kk * 16 + j16) * EPL + s0) = v;
+        if constexpr (BS) {
+          // planes H / M / L of the slot at +0 / +16 / +32 B, elements s0 .. s0 + 3
+          uint32_t h[2], md[2], l[2];
+          split_pair(v[0], v[1], h[0], md[0], l[0]);
+          split_pair(v[2], v[3], h[1], md[1], l[1]);
+          char* p = smem + buf * BUFB + ((q * KT + t) * 64 + kk * 16 + j16) * 48 + 2 * s0;
+          *(uint2*)p = make_uint2(h[0], h[1]);
+          *(uint2*)(p + 16) = make_uint2(md[0], md[1]);
+          *(uint2*)(p + 32) = make_uint2(l[0], l[1]);
+        } else {
+          *(vec*)(zb + ((q * KT + t) * 64 + kk * 16 + j16) * EPL + s0) = v;
+        }
       }
     }
   };
@@ -288,17 +325,48 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
     for (int g = 0; g < AZ_NG; ++g) {
       wait_slot(g);
       const int slot = g % AZ_PD;
+      if constexpr (BS) {
+        // the lane's 8 columns (both 16-B pieces) are the K index of one
+        // 16x16x32 MFMA; the slot's planes hold the same 8 columns of Z
+        const char* zs = smem + buf * BUFB;
+        bf16x8 zp[3][KT];
 #pragma unroll
-      for (int vl = 0; vl < AZ_VL; ++vl) {
-        vec zv[KT];
+        for (int t = 0; t < KT; ++t)
 #pragma unroll
-        for (int t = 0; t < KT; ++t) zv[t] = *(const vec*)(zb + ((g * KT + t) * 64 + lane) * EPL + VW * vl);
+          for (int pl = 0; pl < 3; ++pl) zp[pl][t] = *(const bf16x8*)(zs + ((g * KT + t) * 64 + lane) * 48 + 16 * pl);
 #pragma unroll
-        for (int s = 0; s < VW; ++s)
+        for (int rt = 0; rt < AZ_RT; ++rt) {
+          uint32_t h[4], md[4], l[4];
 #pragma unroll
-          for (int rt = 0; rt < AZ_RT; ++rt)
+          for (int u = 0; u < 4; ++u)
+            split_pair(ring[slot][rt][u >> 1][2 * (u & 1)], ring[slot][rt][u >> 1][2 * (u & 1) + 1], h[u], md[u], l[u]);
+          const bf16x8 ah = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+          const bf16x8 am = __builtin_bit_cast(bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+          const bf16x8 al = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
 #pragma unroll
-            for (int t = 0; t < KT; ++t) acc[rt][t] = M::mfma(ring[slot][rt][vl][s], zv[t][s], acc[rt][t]);
+          for (int t = 0; t < KT; ++t) {
+            acc_t a = acc[rt][t];
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, zp[0][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, zp[2][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, zp[1][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, zp[0][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, zp[1][t], a, 0, 0, 0);
+            acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, zp[0][t], a, 0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int vl = 0; vl < AZ_VL; ++vl) {
+          vec zv[KT];
+#pragma unroll
+          for (int t = 0; t < KT; ++t) zv[t] = *(const vec*)(zb + ((g * KT + t) * 64 + lane) * EPL + VW * vl);
+#pragma unroll
+          for (int s = 0; s < VW; ++s)
+#pragma unroll
+            for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+              for (int t = 0; t < KT; ++t) acc[rt][t] = M::mfma(ring[slot][rt][vl][s], zv[t][s], acc[rt][t]);
+        }
       }
       // refill this slot with group g + PD (of the next flat chunk past the end)
       __builtin_amdgcn_sched_barrier(0);
@@ -941,10 +1009,11 @@ bool vec_ok(const T* A, int64_t lda, int64_t n) {
 }
 
 int g_az_split = 1;
+int g_az_bf16 = 1;   // f32, k <= 48: the exact-split bf16 form of Y = A Z (0: f32 MFMA, A/B)
 
-template <typename T, int KT>
-int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
-  constexpr int LDS = az_lds<T, KT>();
+template <typename T, int KT, bool BS>
+int launch_az_(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
+  constexpr int LDS = az_lds<T, KT, BS>();
   constexpr int CW = AZ_NG * 4 * AZ_VL * Mf<T>::VW;
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
   const int nchunk = (n + CW - 1) / CW;
@@ -956,14 +1025,23 @@ int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y
     SL_LAUNCH_CHECK();
   }
   if (vec_ok(A, lda, n)) {
-    SL_LDS_ATTR((k_ts_az<T, KT, true>), LDS);
-    k_ts_az<T, KT, true><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
+    SL_LDS_ATTR((k_ts_az<T, KT, true, BS>), LDS);
+    k_ts_az<T, KT, true, BS><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
   } else {
-    SL_LDS_ATTR((k_ts_az<T, KT, false>), LDS);
-    k_ts_az<T, KT, false><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
+    SL_LDS_ATTR((k_ts_az<T, KT, false, BS>), LDS);
+    k_ts_az<T, KT, false, BS><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
   }
   SL_LAUNCH_CHECK();
   return SL_OK;
+}
+
+template <typename T, int KT>
+int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
+  // the split form's Z planes (48 B per slot) keep two workgroups per CU in
+  // LDS up to three column tiles
+  if constexpr (sizeof(T) == 4 && KT <= 3)
+    if (g_az_bf16) return launch_az_<T, KT, true>(A, m, n, lda, Z, k, Y, ldy, s);
+  return launch_az_<T, KT, false>(A, m, n, lda, Z, k, Y, ldy, s);
 }
 
 // vectors per wave and row: the knob for k <= 64; one (with one 512-thread
@@ -1061,6 +1139,7 @@ SL_API void sl_ts_set_atq_av(int v) { g_atq_av = v == 1 ? 1 : 2; }
 
 // A/B knob: 1 (default) whole-block rounds + stream-K tail, 0 whole blocks round-robin
 SL_API void sl_ts_set_az_split(int v) { g_az_split = v ? 1 : 0; }
+SL_API void sl_ts_set_az_bf16(int v) { g_az_bf16 = v ? 1 : 0; }
 
 // bytes of slab workspace sl_ts_atq needs
 SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt) {

@@ -1,6 +1,7 @@
 """Hand-written tall-skinny products of the general-precision randSVD engine
 (rsvd_stream.hip) against fp64 torch references of the same ops:
-Y = A Z and W = A^T Q in A's precision (f32 / f64 matrix cores), the f64
+Y = A Z and W = A^T Q in A's precision (f32 / f64 matrix cores; f32 Y = A Z
+with k <= 48 on the exact three-plane bf16 split), the f64
 helpers X M, X^T X and the one-workgroup k x k product.  Ragged shapes cover
 partial row blocks / row quads, n not a multiple of the column group, lda > n
 and an lda that rules out 16-B vector loads (scalar path)."""
@@ -74,6 +75,38 @@ def test_az_and_atq(L, dt, m, n, k, pad):
     assert torch.isfinite(W).all()
     assert ((W - wref).abs() <= 4 * eps * (m ** 0.5 + 4) * wmag + 1e-300).all(), \
         float(((W - wref).abs() / wmag).max())
+
+
+@pytest.mark.parametrize("m,n,k,pad", [sh for sh in SHAPES if sh[2] <= 48])
+def test_az_f32_mfma_form(L, m, n, k, pad):
+    """f32 Y = A Z with k <= 48 on the f32 matrix-core form (the A/B knob
+    sl_ts_set_az_bf16(0); the default exact three-plane bf16 split is what
+    test_az_and_atq checks): the same error bound, and stream-K cut blocks
+    still bit-reproducible."""
+    dev = torch.device("cuda")
+    L.register("sl_ts_set_az_bf16", [i32], None)
+    g = torch.Generator(device=dev).manual_seed(m + n + k + 1)
+    lda = n + pad
+    Afull = torch.randn(m, lda, device=dev, generator=g)
+    A = Afull[:, :n]
+    Z = torch.randn(n, k, device=dev, generator=g)
+    outs = []
+    try:
+        L.require().sl_ts_set_az_bf16(0)
+        for _ in range(2):
+            Y = torch.full((m, k), float("nan"), device=dev)
+            L.call("sl_ts_az", vp(Afull.data_ptr()), m, n, lda, vp(Z.data_ptr()), k, vp(Y.data_ptr()), k, F32, _st())
+            outs.append(Y)
+        torch.cuda.synchronize()
+    finally:
+        L.require().sl_ts_set_az_bf16(1)
+    Y = outs[0]
+    assert torch.isfinite(Y).all() and torch.equal(outs[0], outs[1])
+    Ad = A.double()
+    yref = Ad @ Z.double()
+    ymag = Ad.abs() @ Z.double().abs()
+    assert ((Y.double() - yref).abs() <= 4 * 1.2e-7 * (n ** 0.5 + 4) * ymag).all(), \
+        float(((Y.double() - yref).abs() / ymag).max())
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
