@@ -14,6 +14,9 @@ from libskylark_amd.ops import _lib  # noqa: E402
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_int64
 _lib.register("sl_ts_az", [vp, i64, i64, i64, vp, i32, vp, i64, i32, vp])
 _lib.register("sl_ts_set_az_bf16", [i32], None)
+_lib.register("sl_ts_set_az_align", [i32], None)
+ALIGN = int(os.environ.get("SL_AZ_ALIGN", "1"))   # row-alignment classes on / off (A/B)
+_lib.require().sl_ts_set_az_align(ALIGN)
 dev = torch.device("cuda")
 cases = [(torch.float32, 1_000_000, 1000), (torch.float64, 200_000, 5000)]
 KS = (8, 16, 32, 40, 48, 64)
@@ -40,7 +43,7 @@ for dt, m, n in cases:
                 ts.append(e0.elapsed_time(e1))
             ts = sorted(ts[2:])
             us = 1e3 * ts[len(ts) // 2]
-            print(json.dumps({"dtype": str(dt)[6:], "m": m, "n": n, "k": k, "split": bs, "us": round(us, 1),
+            print(json.dumps({"dtype": str(dt)[6:], "m": m, "n": n, "k": k, "split": bs, "align": ALIGN, "us": round(us, 1),
                               "TBps": round(A.numel() * A.element_size() / us / 1e6, 2)}), flush=True)
     _lib.require().sl_ts_set_az_bf16(1)
     del A

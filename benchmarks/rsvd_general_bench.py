@@ -43,6 +43,7 @@ def planted(m, n, r, dtype, dev, seed=0):
 BIG = 1
 SPLIT = 1
 AZB = None
+AZA = None
 NO_REF = False   # --no-ref: skip the f64 reference (kernel traces of the engine alone)
 
 
@@ -89,7 +90,7 @@ def run(m, n, rank, q, dtype, sketch="FJLT", reps=5):
     err = float(((s.double() - s_ref).abs() / s_ref).max())
     err_planted = float(((s.double() - s_true[:rank]).abs() / s_true[:rank]).max())
     k = max(rank, min(n, 2 * rank))
-    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}", "big": BIG, "bf16_split": SPLIT, "az_bf16": AZB,
+    out = {"case": f"{m}x{n} {str(dtype).split('.')[-1]} rank {rank} (k {k}) q {q} {sketch}", "big": BIG, "bf16_split": SPLIT, "az_bf16": AZB, "az_align": AZA,
            "engine": type(plan).__name__, "native": getattr(plan, "native", None), "ms": round(ms, 3), "ms_min": round(times[0], 3),
            "pass_traffic_GBps": round(bytes_passes / (ms * 1e-3) / 1e9, 1), "max_rel_err_s": err,
            "max_rel_err_s_vs_planted": err_planted}
@@ -117,6 +118,7 @@ def main():
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--big", type=int, default=1, help="0: rocBLAS products past k = 64 (A/B)")
     ap.add_argument("--bf16-split", type=int, default=1, help="0: bf16 A^T [Q_hi Q_lo] as one product (A/B)")
+    ap.add_argument("--az-align", type=int, default=None, help="Y = A Z row-alignment classes on (1) / off (0)")
     ap.add_argument("--az-bf16", type=int, default=None, help="f32 Y = A Z on the exact bf16 split (1) or f32 MFMA (0)")
     a = ap.parse_args()
     import ctypes
@@ -125,11 +127,15 @@ def main():
     _lib.require().sl_rsvd_gen_set_big(a.big)
     _lib.require().sl_rsvd_gen_set_bf16_split.argtypes = [ctypes.c_int]
     _lib.require().sl_rsvd_gen_set_bf16_split(a.bf16_split)
+    if a.az_align is not None:
+        _lib.require().sl_ts_set_az_align.argtypes = [ctypes.c_int]
+        _lib.require().sl_ts_set_az_align(a.az_align)
     if a.az_bf16 is not None:
         _lib.require().sl_ts_set_az_bf16.argtypes = [ctypes.c_int]
         _lib.require().sl_ts_set_az_bf16(a.az_bf16)
-    global NO_REF, BIG, SPLIT, AZB
+    global NO_REF, BIG, SPLIT, AZB, AZA
     AZB = a.az_bf16
+    AZA = a.az_align
     NO_REF = a.no_ref
     BIG = a.big
     SPLIT = a.bf16_split

@@ -13,7 +13,7 @@
 //
 // Both big products run at A's own precision on the matrix cores
 // (v_mfma_f32_16x16x4_f32: exact f32 products in a k-ordered fmaf chain;
-// v_mfma_f64_16x16x4_f64) -- the reference's precision.  For f32 with k <= 48,
+// v_mfma_f64_16x16x4_f64) -- the reference's precision.  For f32 with 16 < k <= 48,
 // Y = A Z uses an exact three-plane bf16 split of A and Z instead (six
 // 16x16x32 bf16 MFMAs per group, f32 accumulation, dropped terms below 2^-24
 // |a| |z|): the same error bound, and the product took 1168 -> 1032 us on a
@@ -151,7 +151,7 @@ __host__ __device__ inline int64_t az_rounds(int64_t nrb, int64_t g) { return nr
 template <typename T, int KT, bool VEC, bool BS>
 __global__ void __launch_bounds__(az_nt<KT>(), KT > 4 ? 1 : 2)
 k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restrict__ Z, int k, T* __restrict__ Y,
-        int64_t ldy, int split) {
+        int64_t ldy, int split, int P, int stepB) {
   using M = Mf<T>;
   using vec = typename M::vec;
   using acc_t = typename M::acc;
@@ -169,7 +169,24 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   static_assert(!BS || (sizeof(T) == 4 && KT <= 4), "bf16 split: f32, k <= 64");
   constexpr int BUFB = AZ_NG * KT * 64 * 48;           // BS: bytes per Z buffer
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nchunk = (n + CW - 1) / CW;
+  // Row-alignment classes.  With P > 1, A's row pitch (stepB = lda * sizeof(T)
+  // mod 128, a multiple of 32) is not a whole number of 128-B lines, so the row
+  // starts cycle through P offsets.  Wave w takes only rows of class
+  // cl = w % P and shifts its column groups back by osh lane groups of 32 B,
+  // so every 128-B piece it loads is one whole cache line.  Loading each
+  // piece straddling two lines capped the f32 1e6 x 1000 product at
+  // ~4.2 TB/s (profiles/r6/az_row_alignment.log).  Z's fragments are read
+  // with the same shift; the lane groups shifted past a group's start take
+  // the previous group's fragments, and past a chunk's start the previous
+  // chunk's, which stays resident in the other LDS buffer.  The columns before
+  // 0 of chunk 0 meet zeroed operands.
+  const int lp = P == 4 ? 2 : P == 2 ? 1 : 0;
+  const int cl = w & (P - 1);
+  const int osh = ((cl * stepB) & 127) >> 5;
+  int rowb[AZ_RT];   // block-relative row of lane & 15 in tile rt; store rows: rowb - P (lane & 15) + P drow
+#pragma unroll
+  for (int rt = 0; rt < AZ_RT; ++rt) rowb[rt] = P * (16 * ((w >> lp) * AZ_RT + rt) + (lane & 15)) + cl;
+  const int nchunk = (n + (P > 1 ? 3 * EPL : 0) + CW - 1) / CW;
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
   const int64_t G = gridDim.x;
   // split 0 (A/B only): whole blocks round-robin, no tail
@@ -262,23 +279,31 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   // clamped to a valid position (their Z rows are zero), a flat chunk past
   // the end re-reads the last one (never used)
   vec ring[AZ_PD][AZ_RT][AZ_VL];
+  // (columns before 0 -- shifted lane groups of chunk 0 -- read the previous
+  // row's tail, or A[0] for row 0; their operands are zeroed at use)
   auto issue = [&](int64_t j, int c, int g, int slot) {
-    const int64_t r0 = j * AZ_BR + RW * w;
-    const int col0 = c * CW + g * GW + EPL * (lane >> 4);
+    const int64_t rb = j * AZ_BR;
+    const int col0 = c * CW + g * GW + EPL * ((lane >> 4) - osh);
 #pragma unroll
     for (int rt = 0; rt < AZ_RT; ++rt) {
-      int64_t row = r0 + 16 * rt + (lane & 15);
+      int64_t row = rb + rowb[rt];
       row = row < m ? row : m - 1;
-      const T* src = A + row * lda;
+      const int64_t base = row * lda;
 #pragma unroll
       for (int vl = 0; vl < AZ_VL; ++vl) {
         const int col = col0 + VW * vl;
         if constexpr (VEC) {
-          ring[slot][rt][vl] = ld16<vec>(src + (col < n ? col : n - VW));
+          int64_t off = base + (col < n ? col : n - VW);
+          off = off < 0 ? 0 : off;
+          ring[slot][rt][vl] = ld16<vec>(A + off);
         } else {
           vec v;
 #pragma unroll
-          for (int e = 0; e < VW; ++e) v[e] = ld_el(src + (col + e < n ? col + e : n - 1));
+          for (int e = 0; e < VW; ++e) {
+            int64_t off = base + (col + e < n ? col + e : n - 1);
+            off = off < 0 ? 0 : off;
+            v[e] = ld_el(A + off);
+          }
           ring[slot][rt][vl] = v;
         }
       }
@@ -313,27 +338,54 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
   zload(c0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   zstore(0, c0);
+  if (P > 1 && c0 > 0 && nchunk > 1) {   // a range starting inside a block: chunk c0 - 1 for the shift
+    zload(c0 - 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    zstore(1, c0 - 1);
+  }
 #pragma unroll
   for (int g = 0; g < AZ_PD; ++g) issue(jb, c, g, g);
   __syncthreads();
 
+  // this lane's Z fragments: lane group (lane >> 4) - osh of the same group,
+  // or (when negative) + 4 of the previous group
+  const int kd = (lane >> 4) - osh;
+  const bool zprev = kd < 0;
+  const int lsrc = ((kd + 4) & 3) * 16 + (lane & 15);
   for (int64_t fc = 0; fc < nfc; ++fc) {
     const int buf = nchunk > 1 ? (int)(fc & 1) : 0;   // one chunk: Z never reloads
     zload(cn);   // always issued: the wait arithmetic counts it
     const T* zb = zl + buf * (AZ_NG * KT * 64 * EPL);
+    // fragment group of this lane for group g: -1 = the previous chunk's last
+    auto zgrp = [&](int g) { return zprev ? g - 1 : g; };
 #pragma unroll
     for (int g = 0; g < AZ_NG; ++g) {
       wait_slot(g);
       const int slot = g % AZ_PD;
+      // chunk 0's shifted lane groups of group 0 sit before column 0
+      const bool zero = g == 0 && zprev && c == 0;
+      if (g == 0 && c == 0 && osh > 0) {
+#pragma unroll
+        for (int rt = 0; rt < AZ_RT; ++rt)
+#pragma unroll
+          for (int vl = 0; vl < AZ_VL; ++vl) ring[slot][rt][vl] = zero ? vec{} : ring[slot][rt][vl];
+      }
+      const int gs = zgrp(g);
+      const int zbuf = gs < 0 ? buf ^ 1 : buf;
+      const int zg = gs < 0 ? AZ_NG - 1 : gs;
       if constexpr (BS) {
         // the lane's 8 columns (both 16-B pieces) are the K index of one
         // 16x16x32 MFMA; the slot's planes hold the same 8 columns of Z
-        const char* zs = smem + buf * BUFB;
+        const char* zs = smem + zbuf * BUFB;
         bf16x8 zp[3][KT];
 #pragma unroll
         for (int t = 0; t < KT; ++t)
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl) zp[pl][t] = *(const bf16x8*)(zs + ((g * KT + t) * 64 + lane) * 48 + 16 * pl);
+          for (int pl = 0; pl < 3; ++pl) {
+            bf16x8 v = *(const bf16x8*)(zs + ((zg * KT + t) * 64 + lsrc) * 48 + 16 * pl);
+            asm volatile("" : "+v"(v));
+            zp[pl][t] = zero ? bf16x8{} : v;
+          }
 #pragma unroll
         for (int rt = 0; rt < AZ_RT; ++rt) {
           uint32_t h[4], md[4], l[4];
@@ -358,8 +410,13 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
 #pragma unroll
         for (int vl = 0; vl < AZ_VL; ++vl) {
           vec zv[KT];
+          const T* zsb = zl + zbuf * (AZ_NG * KT * 64 * EPL);
 #pragma unroll
-          for (int t = 0; t < KT; ++t) zv[t] = *(const vec*)(zb + ((g * KT + t) * 64 + lane) * EPL + VW * vl);
+          for (int t = 0; t < KT; ++t) {
+            vec v = *(const vec*)(zsb + ((zg * KT + t) * 64 + lsrc) * EPL + VW * vl);
+            asm volatile("" : "+v"(v));
+            zv[t] = zero ? vec{} : v;
+          }
 #pragma unroll
           for (int s = 0; s < VW; ++s)
 #pragma unroll
@@ -378,7 +435,7 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
       // this workgroup's part of the row block is complete: y out (added
       // atomically into a block cut by a range boundary), accumulators cleared
       const bool cut = fc >= FR && (jb * nchunk < F0 || (jb + 1) * nchunk > F0 + FT);
-      const int64_t r0 = jb * AZ_BR + RW * w;
+      const int64_t rb = jb * AZ_BR;
 #pragma unroll
       for (int rt = 0; rt < AZ_RT; ++rt)
 #pragma unroll
@@ -386,7 +443,7 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
           const int col = 16 * t + (lane & 15);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int64_t row = r0 + 16 * rt + M::drow(lane, r);
+            const int64_t row = rb + rowb[rt] + P * (M::drow(lane, r) - (lane & 15));
             if (row < m && col < k) {
               if (cut) atomicAdd(Y + row * ldy + col, acc[rt][t][r]);
               else Y[row * ldy + col] = acc[rt][t][r];
@@ -397,6 +454,15 @@ k_ts_az(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __restr
     }
     zstore(buf ^ 1, cn);   // (one chunk: a scratch copy into the unused buffer)
     __syncthreads();
+    if (P > 1 && fc + 1 == FR && cn > 0 && nchunk > 1) {
+      // entering the stream-K range inside a block: its chunk cn - 1 into the
+      // buffer just consumed (the next chunk's "previous"); once per workgroup
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      zload(cn - 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      zstore(buf, cn - 1);
+      __syncthreads();
+    }
     jb = jn;
     c = cn;
     advance(fc + 1, jn, cn);
@@ -1009,14 +1075,25 @@ bool vec_ok(const T* A, int64_t lda, int64_t n) {
 }
 
 int g_az_split = 1;
-int g_az_bf16 = 1;   // f32, k <= 48: the exact-split bf16 form of Y = A Z (0: f32 MFMA, A/B)
+int g_az_align = 1;   // row-alignment classes in Y = A Z (0: A/B)
+int g_az_bf16 = 1;   // f32, 16 < k <= 48: the exact-split bf16 form of Y = A Z (0: f32 MFMA, A/B)
 
 template <typename T, int KT, bool BS>
 int launch_az_(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
   constexpr int LDS = az_lds<T, KT, BS>();
-  constexpr int CW = AZ_NG * 4 * AZ_VL * Mf<T>::VW;
+  constexpr int EPL = AZ_VL * Mf<T>::VW, CW = AZ_NG * 4 * EPL;
+  // row pitch not a whole number of 128-B lines (but of 32-B lane groups),
+  // A line-aligned: the kernel's alignment classes (P = 2 or 4 row offsets)
+  int P = 1, stepB = 0;
+  if (g_az_align && ((uintptr_t)A % 128) == 0) {
+    const int64_t sb = (lda * (int64_t)sizeof(T)) & 127;
+    if (sb != 0 && sb % 32 == 0) {
+      P = sb == 64 ? 2 : 4;
+      stepB = (int)sb;
+    }
+  }
   const int64_t nrb = (m + AZ_BR - 1) / AZ_BR;
-  const int nchunk = (n + CW - 1) / CW;
+  const int nchunk = (n + (P > 1 ? 3 * EPL : 0) + CW - 1) / CW;
   // g <= nrb: every stream-K range spans at least one whole row block
   const int64_t res = (KT > 4 ? 1 : 2) * (int64_t)ncu();   // resident workgroups
   const int64_t g = nrb < res ? nrb : res;
@@ -1026,10 +1103,10 @@ int launch_az_(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* 
   }
   if (vec_ok(A, lda, n)) {
     SL_LDS_ATTR((k_ts_az<T, KT, true, BS>), LDS);
-    k_ts_az<T, KT, true, BS><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
+    k_ts_az<T, KT, true, BS><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split, P, stepB);
   } else {
     SL_LDS_ATTR((k_ts_az<T, KT, false, BS>), LDS);
-    k_ts_az<T, KT, false, BS><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split);
+    k_ts_az<T, KT, false, BS><<<(unsigned)g, az_nt<KT>(), LDS, s>>>(A, m, n, lda, Z, k, Y, ldy, g_az_split, P, stepB);
   }
   SL_LAUNCH_CHECK();
   return SL_OK;
@@ -1038,8 +1115,9 @@ int launch_az_(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* 
 template <typename T, int KT>
 int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y, int64_t ldy, hipStream_t s) {
   // the split form's Z planes (48 B per slot) keep two workgroups per CU in
-  // LDS up to three column tiles
-  if constexpr (sizeof(T) == 4 && KT <= 3)
+  // LDS up to three column tiles; one column tile (k <= 16) streams faster
+  // on the f32 form (720 vs 759 us at k = 16, profiles/r6/az_align_ab.txt)
+  if constexpr (sizeof(T) == 4 && KT >= 2 && KT <= 3)
     if (g_az_bf16) return launch_az_<T, KT, true>(A, m, n, lda, Z, k, Y, ldy, s);
   return launch_az_<T, KT, false>(A, m, n, lda, Z, k, Y, ldy, s);
 }
@@ -1140,6 +1218,7 @@ SL_API void sl_ts_set_atq_av(int v) { g_atq_av = v == 1 ? 1 : 2; }
 // A/B knob: 1 (default) whole-block rounds + stream-K tail, 0 whole blocks round-robin
 SL_API void sl_ts_set_az_split(int v) { g_az_split = v ? 1 : 0; }
 SL_API void sl_ts_set_az_bf16(int v) { g_az_bf16 = v ? 1 : 0; }
+SL_API void sl_ts_set_az_align(int v) { g_az_align = v ? 1 : 0; }
 
 // bytes of slab workspace sl_ts_atq needs
 SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt) {

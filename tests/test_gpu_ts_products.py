@@ -1,7 +1,7 @@
 """Hand-written tall-skinny products of the general-precision randSVD engine
 (rsvd_stream.hip) against fp64 torch references of the same ops:
 Y = A Z and W = A^T Q in A's precision (f32 / f64 matrix cores; f32 Y = A Z
-with k <= 48 on the exact three-plane bf16 split), the f64
+with 16 < k <= 48 on the exact three-plane bf16 split), the f64
 helpers X M, X^T X and the one-workgroup k x k product.  Ragged shapes cover
 partial row blocks / row quads, n not a multiple of the column group, lda > n
 and an lda that rules out 16-B vector loads (scalar path)."""
@@ -77,9 +77,9 @@ def test_az_and_atq(L, dt, m, n, k, pad):
         float(((W - wref).abs() / wmag).max())
 
 
-@pytest.mark.parametrize("m,n,k,pad", [sh for sh in SHAPES if sh[2] <= 48])
+@pytest.mark.parametrize("m,n,k,pad", [sh for sh in SHAPES if 16 < sh[2] <= 48])
 def test_az_f32_mfma_form(L, m, n, k, pad):
-    """f32 Y = A Z with k <= 48 on the f32 matrix-core form (the A/B knob
+    """f32 Y = A Z with 16 < k <= 48 on the f32 matrix-core form (the A/B knob
     sl_ts_set_az_bf16(0); the default exact three-plane bf16 split is what
     test_az_and_atq checks): the same error bound, and stream-K cut blocks
     still bit-reproducible."""
@@ -107,6 +107,45 @@ def test_az_f32_mfma_form(L, m, n, k, pad):
     ymag = Ad.abs() @ Z.double().abs()
     assert ((Y.double() - yref).abs() <= 4 * 1.2e-7 * (n ** 0.5 + 4) * ymag).all(), \
         float(((Y.double() - yref).abs() / ymag).max())
+
+
+@pytest.mark.parametrize("dt,m,n,lda,k", [
+    (torch.float32, 300_007, 1000, 1000, 40),   # 4000-B rows: four alignment classes, stream-K tail
+    (torch.float64, 300_007, 1000, 1000, 40),   # 8000-B rows: two classes
+    (torch.float64, 60_001, 5000, 5000, 20),
+    (torch.float32, 5_000, 100, 104, 24),       # one chunk per row block
+    (torch.float32, 50_001, 1000, 1000, 128),   # eight column tiles, eight waves
+    (torch.float32, 3, 1000, 1000, 16)])         # fewer rows than a tile's classes
+def test_az_alignment_classes(L, dt, m, n, lda, k):
+    """Y = A Z with rows grouped by 128-B alignment class and the column
+    groups shifted to whole cache lines (row pitch not a multiple of 128 B):
+    within the product's error bound, bit-reproducible, and equal in bound to
+    the unshifted form (sl_ts_set_az_align(0))."""
+    dev = torch.device("cuda")
+    L.register("sl_ts_set_az_align", [i32], None)
+    g = torch.Generator(device=dev).manual_seed(m + n + k + 7)
+    Afull = torch.randn(m, lda, device=dev, dtype=dt, generator=g)
+    A = Afull[:, :n]
+    Z = torch.randn(n, k, device=dev, dtype=dt, generator=g)
+    code = F32 if dt == torch.float32 else F64
+    outs = []
+    try:
+        for al in (1, 1, 0):
+            L.require().sl_ts_set_az_align(al)
+            Y = torch.full((m, k), float("nan"), device=dev, dtype=dt)
+            L.call("sl_ts_az", vp(Afull.data_ptr()), m, n, lda, vp(Z.data_ptr()), k, vp(Y.data_ptr()), k, code, _st())
+            outs.append(Y)
+        torch.cuda.synchronize()
+    finally:
+        L.require().sl_ts_set_az_align(1)
+    assert torch.isfinite(outs[0]).all() and torch.equal(outs[0], outs[1])
+    Ad = A.double()
+    yref = Ad @ Z.double()
+    ymag = Ad.abs() @ Z.double().abs()
+    eps = 1.2e-7 if dt == torch.float32 else 2.3e-16
+    for Y in (outs[0], outs[2]):
+        assert ((Y.double() - yref).abs() <= 4 * eps * (n ** 0.5 + 4) * ymag).all(), \
+            float(((Y.double() - yref).abs() / ymag).max())
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
