@@ -6,6 +6,7 @@
 //   sl_ts_az     Y (m x k) = A (m x n) Z (n x k)          one streaming read of A
 //   sl_ts_atq    W (n x k, f64) = A^T Q (Q m x k)         one streaming read of A,
 //                                                         per-row-group slabs + f64 sum
+//                                                         (f32, 16 < k <= 48: k_ts_atq_bs)
 //   sl_ts_xm64   out (rows x k2, f32 / f64) = X (rows x k, f64) M (k x k2, f64)
 //   sl_ts_gram64 G (k x k, f64) = X^T X (X rows x k, f64)
 //   sl_ts_gram_w G = X^T X for 64 < k <= 128 (X f32 / f64)
@@ -633,6 +634,146 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
       }
 }
 
+// ----------------------------------------------- W = A^T Q, f32 on bf16 splits
+// 512-thread workgroups as k_ts_atq; wave w owns 64 columns of the slice (16
+// lanes x 4) and all rows of the row group.  Per 32-row step the lane (kk =
+// l >> 4, nn = l & 15) loads rows r + 8 kk + j (j < 8), columns cbw + 4 nn ..
+// + 3: element e of those 8 rows is the K = 32 A^T operand of W tile e, whose
+// 16 rows are the columns cbw + 4 i + e; the Q operand is Q[r + 8 kk + j][16 t
+// + nn].  Both enter the matrix cores as exact three-plane bf16 splits, six
+// v_mfma_f32_16x16x32_bf16 per tile pair (the split form of k_ts_az), instead
+// of eight v_mfma_f32_16x16x4_f32 per 32 rows: the f32 product at k = 40 was
+// bound by the f32 matrix rate (profiles/r6/atq_bf16_split_ab.txt).
+constexpr int ATB_PD = 2;
+
+template <int KT>
+__global__ void __launch_bounds__(AT_NT, 1)
+k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Q, int k,
+            int64_t rows_per, float* __restrict__ slab) {
+  constexpr int WC = 64, CS = 8 * WC;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kk = lane >> 4, nn = lane & 15;
+  const int64_t rbeg = (int64_t)blockIdx.y * rows_per;
+  int64_t rend = rbeg + rows_per;
+  rend = rend < m ? rend : m;
+  const int cbw = blockIdx.x * CS + w * WC;
+  const int64_t nq = (rend > rbeg && cbw < n) ? (rend - rbeg + 31) / 32 : 0;
+  f32x4 acc[4][KT];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) acc[e][t] = f32x4{};
+  // loads branch-free: rows clamped into the group (their Q operand zeroed at
+  // use from the mask formed at issue), columns clamped into [0, n)
+  f32x4 ra[ATB_PD][8];
+  float rq[ATB_PD][KT][8];
+  int rok[ATB_PD];
+  const int col = cbw + 4 * nn;
+  const int cc = col < n ? col : n - 4;
+  auto issue = [&](int64_t qi, int slot) {
+    const int64_t r0 = rbeg + 32 * qi + 8 * kk;
+    int ok = 0;
+    int64_t rows[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t row = r0 + j;
+      ok |= (row < rend ? 1 : 0) << j;
+      rows[j] = row < rend ? row : rend - 1;
+      ra[slot][j] = ld16<f32x4>(A + rows[j] * lda + cc);
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int kc = 16 * t + nn;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rq[slot][t][j] = ld_el(Q + rows[j] * k + (kc < k ? kc : k - 1));
+    }
+    rok[slot] = ok;
+  };
+  constexpr int LPS = 8 + 8 * KT;
+  constexpr int INFLIGHT = (ATB_PD - 1) * LPS < 63 ? (ATB_PD - 1) * LPS : 63;
+  auto wait_ring = [&](int p) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ra[p][0]) : "n"(INFLIGHT));
+#pragma unroll
+    for (int j = 1; j < 8; ++j) asm volatile("" : "+v"(ra[p][j]));
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(rq[p][t][j]));
+  };
+  if (nq > 0) {
+#pragma unroll
+    for (int p = 0; p < ATB_PD; ++p) issue(p, p);
+    for (int64_t q0 = 0; q0 < nq; q0 += ATB_PD) {
+#pragma unroll
+      for (int p = 0; p < ATB_PD; ++p) {
+        wait_ring(p);
+        bf16x8 qp[3][KT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const bool kin = 16 * t + nn < k;
+          uint32_t h[4], md[4], l[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float v0 = (kin && ((rok[p] >> (2 * u)) & 1)) ? rq[p][t][2 * u] : 0.f;
+            const float v1 = (kin && ((rok[p] >> (2 * u + 1)) & 1)) ? rq[p][t][2 * u + 1] : 0.f;
+            split_pair(v0, v1, h[u], md[u], l[u]);
+          }
+          qp[0][t] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+          qp[1][t] = __builtin_bit_cast(bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+          qp[2][t] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          uint32_t h[4], md[4], l[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) split_pair(ra[p][2 * u][e], ra[p][2 * u + 1][e], h[u], md[u], l[u]);
+          const bf16x8 ah = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+          const bf16x8 am = __builtin_bit_cast(bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+          const bf16x8 al = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+#pragma unroll
+          for (int t = 0; t < KT; ++t) {
+            f32x4 a = acc[e][t];
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, qp[0][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, qp[2][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, qp[1][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, qp[0][t], a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, qp[1][t], a, 0, 0, 0);
+            acc[e][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, qp[0][t], a, 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        issue(q0 + p + ATB_PD, p);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // the clamped refills past the end: landed, and kept live until then
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < ATB_PD; ++p) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ra[p][j]));
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(rq[p][t][j]));
+    }
+  }
+  if (cbw >= n) return;
+  // slab (row group y) [n][k]: tile e row i (D row 4 (l >> 4) + r) is column cbw + 4 i + e
+  float* sb = slab + (int64_t)blockIdx.y * n * k;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int kc = 16 * t + nn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int cw = cbw + 4 * (4 * kk + r) + e;
+        if (cw < n && kc < k) sb[(int64_t)cw * k + kc] = acc[e][t][r];
+      }
+    }
+}
+
 // ------------------------------------------------------- small f64 helpers
 // out (rows x k2, TO, ldo) = X (rows x k, f64, ldx) M (k x k2, f64): 64-row
 // tiles staged in LDS (coalesced), thread (row = t & 63, column group t >> 6)
@@ -1126,10 +1267,14 @@ int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y
 // workgroup per CU, > 128 VGPRs of accumulators) for 64 < k <= 128
 int atq_av(int k) { return k > 64 ? 1 : g_atq_av; }
 
+int g_atq_bf16 = 1;   // f32, 16 < k <= 48: k_ts_atq_bs (0: f32 MFMA, A/B)
+bool atq_bs(int k) { return g_atq_bf16 && k > 16 && k <= 48; }
+
 // row groups of the A^T Q product: ~2 workgroups per CU over all slices
+// (bs: the split-form kernel's 512-column slices)
 template <typename T>
-void atq_geometry(int64_t m, int n, int k, int* slices, int* groups, int64_t* rows_per) {
-  const int CS = 8 * atq_av(k) * 16 * (16 / (int)sizeof(T));
+void atq_geometry(int64_t m, int n, int k, int* slices, int* groups, int64_t* rows_per, bool bs = false) {
+  const int CS = bs ? 512 : 8 * atq_av(k) * 16 * (16 / (int)sizeof(T));
   *slices = (n + CS - 1) / CS;
   // AV = 2: one 512-thread workgroup per CU is resident (k_ts_atq needs >
   // 128 VGPRs): slices x groups <= 2 x CUs is two full rounds (rounding the
@@ -1219,13 +1364,21 @@ SL_API void sl_ts_set_atq_av(int v) { g_atq_av = v == 1 ? 1 : 2; }
 SL_API void sl_ts_set_az_split(int v) { g_az_split = v ? 1 : 0; }
 SL_API void sl_ts_set_az_bf16(int v) { g_az_bf16 = v ? 1 : 0; }
 SL_API void sl_ts_set_az_align(int v) { g_az_align = v ? 1 : 0; }
+SL_API void sl_ts_set_atq_bf16(int v) { g_atq_bf16 = v ? 1 : 0; }
 
 // bytes of slab workspace sl_ts_atq needs
 SL_API int64_t sl_ts_atq_workspace(int64_t m, int64_t n, int k, int dt) {
   int slices = 0, groups = 0;
   int64_t rp = 0;
-  if (dt == SL_F64) atq_geometry<double>(m, (int)n, k, &slices, &groups, &rp);
-  else atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp);
+  if (dt == SL_F64) {
+    atq_geometry<double>(m, (int)n, k, &slices, &groups, &rp);
+  } else {
+    // either f32 kernel may run (the split form needs 16-B loads): the larger
+    atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp);
+    int s2 = 0, g2 = 0;
+    atq_geometry<float>(m, (int)n, k, &s2, &g2, &rp, true);
+    groups = g2 > groups ? g2 : groups;
+  }
   return (int64_t)groups * n * k * (dt == SL_F64 ? 8 : 4) + 256;
 }
 
@@ -1242,8 +1395,17 @@ SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const voi
   int64_t rp = 0;
   int rc;
   if (dt == SL_F32) {
-    atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp);
-    rc = atq_dispatch<float>((const float*)A, m, (int)n, lda, (const float*)Q, k, (float*)ws, slices, groups, rp, s);
+    const bool bs = atq_bs(k) && vec_ok((const float*)A, lda, n);
+    atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp, bs);
+    if (bs) {
+      const dim3 grid((unsigned)slices, (unsigned)groups);
+      if (k > 32) k_ts_atq_bs<3><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      else k_ts_atq_bs<2><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      SL_LAUNCH_CHECK();
+      rc = SL_OK;
+    } else {
+      rc = atq_dispatch<float>((const float*)A, m, (int)n, lda, (const float*)Q, k, (float*)ws, slices, groups, rp, s);
+    }
     if (rc != SL_OK) return rc;
     return sl_slab_reduce_launch_f64((const float*)ws, groups, n * k, k, (int)n, k, W, ldw, s);
   }

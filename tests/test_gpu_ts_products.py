@@ -148,6 +148,37 @@ def test_az_alignment_classes(L, dt, m, n, lda, k):
             float(((Y.double() - yref).abs() / ymag).max())
 
 
+@pytest.mark.parametrize("m,n,k,lda", [(100_003, 1000, 40, 1000), (300_007, 200, 24, 204), (4_097, 1000, 33, 1008)])
+def test_atq_f32_forms(L, m, n, k, lda):
+    """f32 W = A^T Q for 16 < k <= 48 on both forms: the exact three-plane
+    bf16 split (default, k_ts_atq_bs) and the f32 matrix-core kernel
+    (sl_ts_set_atq_bf16(0)), each within the f32 product's error bound."""
+    dev = torch.device("cuda")
+    L.register("sl_ts_set_atq_bf16", [i32], None)
+    g = torch.Generator(device=dev).manual_seed(m + n + k + 3)
+    Afull = torch.randn(m, lda, device=dev, generator=g)
+    A = Afull[:, :n]
+    Q = torch.randn(m, k, device=dev, generator=g)
+    ws = torch.zeros(int(L.require().sl_ts_atq_workspace(m, n, k, F32)), dtype=torch.uint8, device=dev)
+    outs = []
+    try:
+        for bs in (1, 0):
+            L.require().sl_ts_set_atq_bf16(bs)
+            W = torch.full((n, k), float("nan"), device=dev, dtype=torch.float64)
+            L.call("sl_ts_atq", vp(Afull.data_ptr()), m, n, lda, vp(Q.data_ptr()), k, vp(W.data_ptr()), k,
+                   vp(ws.data_ptr()), F32, _st())
+            torch.cuda.synchronize()
+            outs.append(W)
+    finally:
+        L.require().sl_ts_set_atq_bf16(1)
+    Ad = A.double()
+    wref = Ad.t() @ Q.double()
+    wmag = Ad.abs().t() @ Q.double().abs()
+    for W in outs:
+        assert torch.isfinite(W).all()
+        assert ((W - wref).abs() <= 4 * 1.2e-7 * (m ** 0.5 + 4) * wmag).all(), float(((W - wref).abs() / wmag).max())
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 def test_az_stream_k_deterministic(L, dt):
     """Row blocks cut by a stream-K range boundary are summed from two atomic
