@@ -16,6 +16,9 @@ _lib.register("sl_ts_atq", [vp, i64, i64, i64, vp, i32, vp, i32, vp, i32, vp])
 _lib.register("sl_ts_set_atq_bf16", [i32], None)
 BS = int(os.environ.get("SL_ATQ_BF16", "1"))   # split form on / off (A/B)
 _lib.require().sl_ts_set_atq_bf16(BS)
+_lib.register("sl_ts_set_az_align", [i32], None)
+ALIGN = int(os.environ.get("SL_AZ_ALIGN", "1"))   # alignment classes (shared knob with Y = A Z)
+_lib.require().sl_ts_set_az_align(ALIGN)
 dev = torch.device("cuda")
 for dt, m, n, k in ((torch.float32, 1_000_000, 1000, 40), (torch.float32, 1_000_000, 1024, 40),
                     (torch.float32, 250_000, 4000, 40), (torch.float32, 1_000_000, 1000, 16),
@@ -38,7 +41,7 @@ for dt, m, n, k in ((torch.float32, 1_000_000, 1000, 40), (torch.float32, 1_000_
         ts.append(e0.elapsed_time(e1))
     ts = sorted(ts[2:])
     us = 1e3 * ts[len(ts) // 2]
-    print(json.dumps({"dtype": str(dt)[6:], "m": m, "n": n, "k": k, "split": BS, "us": round(us, 1),
+    print(json.dumps({"dtype": str(dt)[6:], "m": m, "n": n, "k": k, "split": BS, "align": ALIGN, "us": round(us, 1),
                       "TBps": round(A.numel() * A.element_size() / us / 1e6, 2)}), flush=True)
     del A, Q, ws
     torch.cuda.empty_cache()

@@ -148,11 +148,13 @@ def test_az_alignment_classes(L, dt, m, n, lda, k):
             float(((Y.double() - yref).abs() / ymag).max())
 
 
-@pytest.mark.parametrize("m,n,k,lda", [(100_003, 1000, 40, 1000), (300_007, 200, 24, 204), (4_097, 1000, 33, 1008)])
+@pytest.mark.parametrize("m,n,k,lda", [(100_003, 1000, 40, 1000), (300_007, 200, 24, 204), (4_097, 1000, 33, 1008),
+                                       (20_011, 1020, 40, 1020), (77, 104, 17, 104), (2, 1000, 48, 1000)])
 def test_atq_f32_forms(L, m, n, k, lda):
     """f32 W = A^T Q for 16 < k <= 48 on both forms: the exact three-plane
-    bf16 split (default, k_ts_atq_bs) and the f32 matrix-core kernel
-    (sl_ts_set_atq_bf16(0)), each within the f32 product's error bound."""
+    bf16 split (default, k_ts_atq_bs; ragged slices, a two-row operand) and
+    the f32 matrix-core kernel (sl_ts_set_atq_bf16(0)), each within the f32
+    product's error bound."""
     dev = torch.device("cuda")
     L.register("sl_ts_set_atq_bf16", [i32], None)
     g = torch.Generator(device=dev).manual_seed(m + n + k + 3)
