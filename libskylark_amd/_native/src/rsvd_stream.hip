@@ -657,7 +657,13 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
   int64_t rend = rbeg + rows_per;
   rend = rend < m ? rend : m;
   const int cbw = blockIdx.x * CS + w * WC;
-  const int64_t nq = (rend > rbeg && cbw < n) ? (rend - rbeg + 31) / 32 : 0;
+  // every wave runs every step (the per-step barrier); waves past n discard
+  const int64_t nq = rend > rbeg ? (rend - rbeg + 31) / 32 : 0;
+  // Q's split is shared: per step each thread splits KT of the 32 x 16 KT Q
+  // elements into the LDS B fragments [buf][plane][tile][lane][row] (the 8
+  // waves all need the same ones; split in every wave, the kernel was
+  // VALU-bound, profiles/r6/atq_pmc.txt)
+  __shared__ __attribute__((aligned(16))) uint16_t qs[2][3][KT][64][8];
   f32x4 acc[4][KT];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
@@ -666,39 +672,37 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
   // loads branch-free: rows clamped into the group (their Q operand zeroed at
   // use from the mask formed at issue), columns clamped into [0, n)
   f32x4 ra[ATB_PD][8];
-  float rq[ATB_PD][KT][8];
+  float rq[ATB_PD][KT];
   int rok[ATB_PD];
   const int col = cbw + 4 * nn;
   const int cc = col < n ? col : n - 4;
   auto issue = [&](int64_t qi, int slot) {
     const int64_t r0 = rbeg + 32 * qi + 8 * kk;
-    int ok = 0;
-    int64_t rows[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int64_t row = r0 + j;
-      ok |= (row < rend ? 1 : 0) << j;
-      rows[j] = row < rend ? row : rend - 1;
-      ra[slot][j] = ld16<f32x4>(A + rows[j] * lda + cc);
+      int64_t row = r0 + j;
+      row = row < rend ? row : rend - 1;
+      ra[slot][j] = ld16<f32x4>(A + row * lda + cc);
     }
+    int ok = 0;
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      const int kc = 16 * t + nn;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) rq[slot][t][j] = ld_el(Q + rows[j] * k + (kc < k ? kc : k - 1));
+    for (int u = 0; u < KT; ++u) {
+      const int e = tid + AT_NT * u, qr = e / (16 * KT), qc = e - qr * (16 * KT);
+      int64_t row = rbeg + 32 * qi + qr;
+      ok |= (row < rend && qc < k ? 1 : 0) << u;
+      row = row < rend ? row : rend - 1;
+      rq[slot][u] = ld_el(Q + row * k + (qc < k ? qc : k - 1));
     }
     rok[slot] = ok;
   };
-  constexpr int LPS = 8 + 8 * KT;
+  constexpr int LPS = 8 + KT;
   constexpr int INFLIGHT = (ATB_PD - 1) * LPS < 63 ? (ATB_PD - 1) * LPS : 63;
   auto wait_ring = [&](int p) {
     asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ra[p][0]) : "n"(INFLIGHT));
 #pragma unroll
     for (int j = 1; j < 8; ++j) asm volatile("" : "+v"(ra[p][j]));
 #pragma unroll
-    for (int t = 0; t < KT; ++t)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(rq[p][t][j]));
+    for (int u = 0; u < KT; ++u) asm volatile("" : "+v"(rq[p][u]));
   };
   if (nq > 0) {
 #pragma unroll
@@ -707,21 +711,24 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
 #pragma unroll
       for (int p = 0; p < ATB_PD; ++p) {
         wait_ring(p);
+        const int b = p & 1;   // LDS buffer of this step (ATB_PD even: steps alternate)
+#pragma unroll
+        for (int u = 0; u < KT; ++u) {
+          const int e = tid + AT_NT * u, qr = e / (16 * KT), qc = e - qr * (16 * KT);
+          const float v = ((rok[p] >> u) & 1) ? rq[p][u] : 0.f;
+          uint32_t h, md, l;
+          split_pair(v, 0.f, h, md, l);
+          uint16_t* d = &qs[b][0][qc >> 4][(qr >> 3) * 16 + (qc & 15)][qr & 7];
+          d[0] = (uint16_t)h;
+          d[KT * 64 * 8] = (uint16_t)md;
+          d[2 * KT * 64 * 8] = (uint16_t)l;
+        }
+        __syncthreads();
         bf16x8 qp[3][KT];
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-          const bool kin = 16 * t + nn < k;
-          uint32_t h[4], md[4], l[4];
+        for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float v0 = (kin && ((rok[p] >> (2 * u)) & 1)) ? rq[p][t][2 * u] : 0.f;
-            const float v1 = (kin && ((rok[p] >> (2 * u + 1)) & 1)) ? rq[p][t][2 * u + 1] : 0.f;
-            split_pair(v0, v1, h[u], md[u], l[u]);
-          }
-          qp[0][t] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-          qp[1][t] = __builtin_bit_cast(bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
-          qp[2][t] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
-        }
+          for (int t = 0; t < KT; ++t) qp[pl][t] = *(const bf16x8*)&qs[b][pl][t][lane][0];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           uint32_t h[4], md[4], l[4];
@@ -753,9 +760,7 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
 #pragma unroll
       for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(ra[p][j]));
 #pragma unroll
-      for (int t = 0; t < KT; ++t)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(rq[p][t][j]));
+      for (int u = 0; u < KT; ++u) asm volatile("" : "+v"(rq[p][u]));
     }
   }
   if (cbw >= n) return;
