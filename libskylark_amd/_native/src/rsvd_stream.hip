@@ -6,7 +6,7 @@
 //   sl_ts_az     Y (m x k) = A (m x n) Z (n x k)          one streaming read of A
 //   sl_ts_atq    W (n x k, f64) = A^T Q (Q m x k)         one streaming read of A,
 //                                                         per-row-group slabs + f64 sum
-//                                                         (f32, 16 < k <= 48: k_ts_atq_bs)
+//                                                         (f32, 16 < k <= 64: k_ts_atq_bs)
 //   sl_ts_xm64   out (rows x k2, f32 / f64) = X (rows x k, f64) M (k x k2, f64)
 //   sl_ts_gram64 G (k x k, f64) = X^T X (X rows x k, f64)
 //   sl_ts_gram_w G = X^T X for 64 < k <= 128 (X f32 / f64)
@@ -1272,8 +1272,8 @@ int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y
 // workgroup per CU, > 128 VGPRs of accumulators) for 64 < k <= 128
 int atq_av(int k) { return k > 64 ? 1 : g_atq_av; }
 
-int g_atq_bf16 = 1;   // f32, 16 < k <= 48: k_ts_atq_bs (0: f32 MFMA, A/B)
-bool atq_bs(int k) { return g_atq_bf16 && k > 16 && k <= 48; }
+int g_atq_bf16 = 1;   // f32, 16 < k <= 64: k_ts_atq_bs (0: f32 MFMA, A/B)
+bool atq_bs(int k) { return g_atq_bf16 && k > 16 && k <= 64; }
 
 // row groups of the A^T Q product: ~2 workgroups per CU over all slices
 // (bs: the split-form kernel's 512-column slices)
@@ -1404,7 +1404,8 @@ SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const voi
     atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp, bs);
     if (bs) {
       const dim3 grid((unsigned)slices, (unsigned)groups);
-      if (k > 32) k_ts_atq_bs<3><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      if (k > 48) k_ts_atq_bs<4><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      else if (k > 32) k_ts_atq_bs<3><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
       else k_ts_atq_bs<2><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
       SL_LAUNCH_CHECK();
       rc = SL_OK;
