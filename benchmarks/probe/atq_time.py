@@ -26,6 +26,8 @@ CASES = ((torch.float32, 1_000_000, 1000, 40), (torch.float32, 1_000_000, 1024, 
                     (torch.float64, 500_000, 1024, 16), (torch.float64, 200_000, 5000, 40))
 if len(sys.argv) > 1 and sys.argv[1] == "one":   # one case (PMC passes)
     CASES = CASES[:1]
+if len(sys.argv) > 1 and sys.argv[1] == "k128":   # 64 < k <= 128
+    CASES = ((torch.float32, 1_000_000, 1000, 128), (torch.float32, 1_000_000, 1000, 96), (torch.float32, 250_000, 4000, 128))
 if len(sys.argv) > 1 and sys.argv[1] == "k64":   # 48 < k <= 64
     CASES = ((torch.float32, 1_000_000, 1000, 64), (torch.float32, 1_000_000, 1000, 56), (torch.float32, 250_000, 4000, 64))
 for dt, m, n, k in CASES:

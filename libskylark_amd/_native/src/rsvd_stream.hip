@@ -6,7 +6,7 @@
 //   sl_ts_az     Y (m x k) = A (m x n) Z (n x k)          one streaming read of A
 //   sl_ts_atq    W (n x k, f64) = A^T Q (Q m x k)         one streaming read of A,
 //                                                         per-row-group slabs + f64 sum
-//                                                         (f32, 16 < k <= 64: k_ts_atq_bs)
+//                                                         (f32, 16 < k <= 128: k_ts_atq_bs)
 //   sl_ts_xm64   out (rows x k2, f32 / f64) = X (rows x k, f64) M (k x k2, f64)
 //   sl_ts_gram64 G (k x k, f64) = X^T X (X rows x k, f64)
 //   sl_ts_gram_w G = X^T X for 64 < k <= 128 (X f32 / f64)
@@ -31,6 +31,8 @@
 // element s of that vector to the s-th MFMA of the group: global loads stay
 // 16-B per lane and 64-256 B contiguous per row, with no transposition.
 #include "sl_common.hpp"
+
+#include <type_traits>
 
 int sl_slab_reduce_launch_f64(const float* slab, int nslab, int64_t slab_stride, int ld_in, int rows, int cols,
                               double* out, int ld_out, hipStream_t s);
@@ -91,6 +93,11 @@ template <typename V>
 __device__ __forceinline__ V ld16(const void* p) {
   V v;
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float2 ld8(const void* p) {
+  float2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
 __device__ __forceinline__ float ld_el(const float* p) {
@@ -646,11 +653,16 @@ k_ts_atq(const T* __restrict__ A, int64_t m, int n, int64_t lda, const T* __rest
 // bound by the f32 matrix rate (profiles/r6/atq_bf16_split_ab.txt).
 constexpr int ATB_PD = 2;
 
-template <int KT>
+// EW = 4 columns per lane and row (k <= 64); EW = 2 for 64 < k <= 128 (six /
+// eight Q tiles: the accumulators of four A tiles would not fit), 32-column
+// windows, 8-B loads.
+template <int KT, int EW = 4>
 __global__ void __launch_bounds__(AT_NT, 1)
 k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const float* __restrict__ Q, int k,
             int64_t rows_per, float* __restrict__ slab) {
-  constexpr int WC = 64, CS = 8 * WC;
+  static_assert(EW == 4 || EW == 2, "EW");
+  using ev = typename std::conditional<EW == 4, f32x4, float2>::type;
+  constexpr int WC = 16 * EW, CS = 8 * WC;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kk = lane >> 4, nn = lane & 15;
   const int64_t rbeg = (int64_t)blockIdx.y * rows_per;
@@ -664,25 +676,26 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
   // waves all need the same ones; split in every wave, the kernel was
   // VALU-bound, profiles/r6/atq_pmc.txt)
   __shared__ __attribute__((aligned(16))) uint16_t qs[2][3][KT][64][8];
-  f32x4 acc[4][KT];
+  f32x4 acc[EW][KT];
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int e = 0; e < EW; ++e)
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[e][t] = f32x4{};
   // loads branch-free: rows clamped into the group (their Q operand zeroed at
   // use from the mask formed at issue), columns clamped into [0, n)
-  f32x4 ra[ATB_PD][8];
+  ev ra[ATB_PD][8];
   float rq[ATB_PD][KT];
   int rok[ATB_PD];
-  const int col = cbw + 4 * nn;
-  const int cc = col < n ? col : n - 4;
+  const int col = cbw + EW * nn;
+  const int cc = col < n ? col : n - EW;
   auto issue = [&](int64_t qi, int slot) {
     const int64_t r0 = rbeg + 32 * qi + 8 * kk;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       int64_t row = r0 + j;
       row = row < rend ? row : rend - 1;
-      ra[slot][j] = ld16<f32x4>(A + row * lda + cc);
+      if constexpr (EW == 4) ra[slot][j] = ld16<f32x4>(A + row * lda + cc);
+      else ra[slot][j] = ld8(A + row * lda + cc);
     }
     int ok = 0;
 #pragma unroll
@@ -724,6 +737,35 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
           d[2 * KT * 64 * 8] = (uint16_t)l;
         }
         __syncthreads();
+        if constexpr (EW == 2) {
+          // A planes of both tiles first, then Q's per tile (the register budget of eight tiles)
+          bf16x8 ap[EW][3];
+#pragma unroll
+          for (int e = 0; e < EW; ++e) {
+            uint32_t h[4], md[4], l[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) split_pair(ra[p][2 * u][e], ra[p][2 * u + 1][e], h[u], md[u], l[u]);
+            ap[e][0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+            ap[e][1] = __builtin_bit_cast(bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+            ap[e][2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+          }
+#pragma unroll
+          for (int t = 0; t < KT; ++t) {
+            bf16x8 qt[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) qt[pl] = *(const bf16x8*)&qs[b][pl][t][lane][0];
+#pragma unroll
+            for (int e = 0; e < EW; ++e) {
+              f32x4 a = acc[e][t];
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[e][2], qt[0], a, 0, 0, 0);
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[e][0], qt[2], a, 0, 0, 0);
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[e][1], qt[1], a, 0, 0, 0);
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[e][1], qt[0], a, 0, 0, 0);
+              a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[e][0], qt[1], a, 0, 0, 0);
+              acc[e][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ap[e][0], qt[0], a, 0, 0, 0);
+            }
+          }
+        } else {
         bf16x8 qp[3][KT];
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
@@ -748,6 +790,7 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
             acc[e][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, qp[0][t], a, 0, 0, 0);
           }
         }
+        }
         __builtin_amdgcn_sched_barrier(0);
         issue(q0 + p + ATB_PD, p);
         __builtin_amdgcn_sched_barrier(0);
@@ -764,16 +807,16 @@ k_ts_atq_bs(const float* __restrict__ A, int64_t m, int n, int64_t lda, const fl
     }
   }
   if (cbw >= n) return;
-  // slab (row group y) [n][k]: tile e row i (D row 4 (l >> 4) + r) is column cbw + 4 i + e
+  // slab (row group y) [n][k]: tile e row i (D row 4 (l >> 4) + r) is column cbw + EW i + e
   float* sb = slab + (int64_t)blockIdx.y * n * k;
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+  for (int e = 0; e < EW; ++e)
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       const int kc = 16 * t + nn;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int cw = cbw + 4 * (4 * kk + r) + e;
+        const int cw = cbw + EW * (4 * kk + r) + e;
         if (cw < n && kc < k) sb[(int64_t)cw * k + kc] = acc[e][t][r];
       }
     }
@@ -1272,14 +1315,15 @@ int launch_az(const T* A, int64_t m, int n, int64_t lda, const T* Z, int k, T* Y
 // workgroup per CU, > 128 VGPRs of accumulators) for 64 < k <= 128
 int atq_av(int k) { return k > 64 ? 1 : g_atq_av; }
 
-int g_atq_bf16 = 1;   // f32, 16 < k <= 64: k_ts_atq_bs (0: f32 MFMA, A/B)
-bool atq_bs(int k) { return g_atq_bf16 && k > 16 && k <= 64; }
+int g_atq_bf16 = 1;   // f32, 16 < k <= 128: k_ts_atq_bs (0: f32 MFMA, A/B)
+bool atq_bs(int k) { return g_atq_bf16 && k > 16; }
+int atq_bs_cs(int k) { return k > 64 ? 256 : 512; }   // slice width of k_ts_atq_bs (EW = 2 / 4)
 
 // row groups of the A^T Q product: ~2 workgroups per CU over all slices
 // (bs: the split-form kernel's 512-column slices)
 template <typename T>
 void atq_geometry(int64_t m, int n, int k, int* slices, int* groups, int64_t* rows_per, bool bs = false) {
-  const int CS = bs ? 512 : 8 * atq_av(k) * 16 * (16 / (int)sizeof(T));
+  const int CS = bs ? atq_bs_cs(k) : 8 * atq_av(k) * 16 * (16 / (int)sizeof(T));
   *slices = (n + CS - 1) / CS;
   // AV = 2: one 512-thread workgroup per CU is resident (k_ts_atq needs >
   // 128 VGPRs): slices x groups <= 2 x CUs is two full rounds (rounding the
@@ -1404,7 +1448,9 @@ SL_API int sl_ts_atq(const void* A, int64_t m, int64_t n, int64_t lda, const voi
     atq_geometry<float>(m, (int)n, k, &slices, &groups, &rp, bs);
     if (bs) {
       const dim3 grid((unsigned)slices, (unsigned)groups);
-      if (k > 48) k_ts_atq_bs<4><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      if (k > 96) k_ts_atq_bs<8, 2><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      else if (k > 64) k_ts_atq_bs<6, 2><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
+      else if (k > 48) k_ts_atq_bs<4><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
       else if (k > 32) k_ts_atq_bs<3><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
       else k_ts_atq_bs<2><<<grid, AT_NT, 0, s>>>((const float*)A, m, (int)n, lda, (const float*)Q, k, rp, (float*)ws);
       SL_LAUNCH_CHECK();

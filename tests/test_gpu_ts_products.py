@@ -150,9 +150,10 @@ def test_az_alignment_classes(L, dt, m, n, lda, k):
 
 @pytest.mark.parametrize("m,n,k,lda", [(100_003, 1000, 40, 1000), (300_007, 200, 24, 204), (4_097, 1000, 33, 1008),
                                        (20_011, 1020, 40, 1020), (77, 104, 17, 104), (2, 1000, 48, 1000),
-                                       (50_001, 1000, 64, 1000), (3_001, 200, 50, 200)])
+                                       (50_001, 1000, 64, 1000), (3_001, 200, 50, 200),
+                                       (50_001, 1000, 128, 1000), (4_001, 300, 80, 304), (999, 104, 111, 104)])
 def test_atq_f32_forms(L, m, n, k, lda):
-    """f32 W = A^T Q for 16 < k <= 64 on both forms: the exact three-plane
+    """f32 W = A^T Q for 16 < k <= 128 on both forms: the exact three-plane
     bf16 split (default, k_ts_atq_bs; ragged slices, a two-row operand) and
     the f32 matrix-core kernel (sl_ts_set_atq_bf16(0)), each within the f32
     product's error bound."""
